@@ -1,0 +1,313 @@
+// Golden-vector generator (run in the build container only; needs node and
+// /root/reference). It builds a throw-away, runtime-instrumented copy of the
+// reference bundle in /tmp (header + glpdebug.js + lib/*.js + hooks + footer,
+// the same concatenation as build.sh:3), runs the reference's own
+// glp_simplex / glp_intopt flows on each instance and writes the inputs and
+// outputs as JSON fixtures next to this script. Nothing from the reference is
+// copied into the repository: only generated numbers are.
+//
+// Hooks added to the throw-away copy:
+//   * a per-pivot trace call in front of change_basis(csa) in the primal and
+//     dual main loops (glpspx01.js:2051, glpspx02.js:1962);
+//   * counters around ios_solve_node (glpios01.js:866) and bfd_factorize
+//     (glpbfd.js:47), rebinding the closure names (SURVEY.md §0).
+//
+// usage: node tests/golden/gen_golden.js [--big]
+'use strict';
+var fs = require('fs');
+var path = require('path');
+
+var REF = process.env.GLPK_REF || '/root/reference';
+var OUT = __dirname;
+var BIG = process.argv.indexOf('--big') >= 0;
+
+function buildBundle() {
+    var lib = path.join(REF, 'lib');
+    var files = fs.readdirSync(lib).filter(function (f) { return /\.js$/.test(f); }).sort();
+    var parts = [fs.readFileSync(path.join(REF, 'header'), 'utf8'),
+                 fs.readFileSync(path.join(REF, 'glpdebug.js'), 'utf8')];
+    files.forEach(function (f) {
+        var src = fs.readFileSync(path.join(lib, f), 'utf8');
+        if (f === 'glpspx01.js')
+            src = src.replace('\n        change_basis(csa);',
+                '\n        if (__trace) __trace(1, csa.it_cnt, csa.phase, csa.p, csa.q, csa.head[csa.m+csa.q], csa.p > 0 ? csa.head[csa.p] : 0, csa.teta);' +
+                '\n        change_basis(csa);');
+        if (f === 'glpspx02.js')
+            src = src.replace('\n        change_basis(csa);',
+                '\n        if (__trace) __trace(2, csa.it_cnt, csa.phase, csa.p, csa.q, csa.head[csa.m+csa.q], csa.head[csa.p], csa.delta);' +
+                '\n        change_basis(csa);');
+        parts.push(src);
+    });
+    parts.push([
+        'var __trace = null;',
+        'exports["__set_trace"] = function(f){ __trace = f; };',
+        'var __cnt = {solve_node: 0, factorize: 0};',
+        'exports["__cnt"] = __cnt;',
+        'ios_solve_node = (function(f){ return function(t){ __cnt.solve_node++; return f(t); }; })(ios_solve_node);',
+        'bfd_factorize = (function(f){ return function(a,b,c,d,e){ __cnt.factorize++; return f(a,b,c,d,e); }; })(bfd_factorize);',
+        ''].join('\n'));
+    parts.push(fs.readFileSync(path.join(REF, 'footer'), 'utf8'));
+    var dst = '/tmp/glpk_golden_bundle.js';
+    fs.writeFileSync(dst, parts.join('\n'));
+    return require(dst);
+}
+
+var glpk = buildBundle();
+glpk.glp_set_print_func(function () {});
+
+// ---- deterministic generators (SURVEY.md §8(d)) --------------------------
+function SplitMix(seed) { this.s = BigInt.asUintN(64, BigInt(seed)); }
+SplitMix.prototype.u = function () {
+    var M = 0xFFFFFFFFFFFFFFFFn;
+    this.s = (this.s + 0x9E3779B97F4A7C15n) & M;
+    var z = this.s;
+    z = ((z ^ (z >> 30n)) * 0xBF58476D1CE4E5B9n) & M;
+    z = ((z ^ (z >> 27n)) * 0x94D049BB133111EBn) & M;
+    z = z ^ (z >> 31n);
+    return Number(z >> 11n) * Math.pow(2, -53);
+};
+
+function newProb() { return glpk.glp_create_prob(); }
+
+function genDense(m, n, seed) {
+    var r = new SplitMix(seed), P = newProb(), i, j;
+    glpk.glp_set_obj_dir(P, glpk.GLP_MAX);
+    glpk.glp_add_rows(P, m); glpk.glp_add_cols(P, n);
+    for (j = 1; j <= n; j++) { glpk.glp_set_obj_coef(P, j, r.u()); glpk.glp_set_col_bnds(P, j, glpk.GLP_LO, 0, 0); }
+    var ne = m * n, ia = new Int32Array(1 + ne), ja = new Int32Array(1 + ne), ar = new Float64Array(1 + ne), k = 0;
+    for (i = 1; i <= m; i++) {
+        glpk.glp_set_row_bnds(P, i, glpk.GLP_UP, 0, 0.25 * n);
+        for (j = 1; j <= n; j++) { k++; ia[k] = i; ja[k] = j; ar[k] = 0.5 + r.u(); }
+    }
+    glpk.glp_load_matrix(P, ne, ia, ja, ar);
+    return P;
+}
+
+function genC2s(m, n, nzc, seed) {
+    var r = new SplitMix(seed), P = newProb(), i, j, t;
+    glpk.glp_set_obj_dir(P, glpk.GLP_MAX);
+    glpk.glp_add_rows(P, m); glpk.glp_add_cols(P, n);
+    for (j = 1; j <= n; j++) { glpk.glp_set_obj_coef(P, j, r.u()); glpk.glp_set_col_bnds(P, j, glpk.GLP_LO, 0, 0); }
+    var ia = [0], ja = [0], ar = [0];
+    for (j = 1; j <= n; j++) {
+        var used = {};
+        for (t = 0; t < nzc; ) {
+            i = 1 + Math.floor(r.u() * m);
+            if (used[i]) continue;
+            used[i] = 1; t++;
+            ia.push(i); ja.push(j); ar.push(0.5 + r.u());
+        }
+    }
+    for (i = 1; i <= m; i++) glpk.glp_set_row_bnds(P, i, glpk.GLP_UP, 0, 1 + 9 * r.u());
+    glpk.glp_load_matrix(P, ia.length - 1, ia, ja, ar);
+    return P;
+}
+
+function genC5s(m, n, seed) {
+    var r = new SplitMix(seed), P = newProb(), i, j;
+    glpk.glp_set_obj_dir(P, glpk.GLP_MAX);
+    glpk.glp_add_rows(P, m); glpk.glp_add_cols(P, n);
+    var w = [], ia = [0], ja = [0], ar = [0];
+    for (i = 1; i <= m; i++) {
+        w[i] = [];
+        var s = 0;
+        for (j = 1; j <= n; j++) { w[i][j] = 1 + Math.floor(1000 * r.u()); s += w[i][j]; ia.push(i); ja.push(j); ar.push(w[i][j]); }
+        glpk.glp_set_row_bnds(P, i, glpk.GLP_UP, 0, Math.floor(s / 2));
+    }
+    for (j = 1; j <= n; j++) {
+        var cs = 0;
+        for (i = 1; i <= m; i++) cs += w[i][j];
+        glpk.glp_set_obj_coef(P, j, Math.floor(cs / m) + 500);
+        glpk.glp_set_col_kind(P, j, glpk.GLP_BV);
+    }
+    glpk.glp_load_matrix(P, ia.length - 1, ia, ja, ar);
+    return P;
+}
+
+// random sparse LP with every bound type on rows and columns; exercises the
+// phase-I/phase-II logic, free and fixed variables, infeasible/unbounded ends.
+// feasible=true builds the bounds around a random point x0 (so the LP has a
+// feasible solution; integer columns get integer x0 and integer bounds).
+function genMix(seed, m, n, dens, withInt, feasible) {
+    var r = new SplitMix(seed), P = newProb(), i, j;
+    glpk.glp_set_obj_dir(P, r.u() < 0.5 ? glpk.GLP_MIN : glpk.GLP_MAX);
+    glpk.glp_add_rows(P, m); glpk.glp_add_cols(P, n);
+    var isint = [], x0 = [];
+    for (j = 1; j <= n; j++) {
+        isint[j] = withInt && r.u() < 0.7;
+        x0[j] = isint[j] ? Math.floor(r.u() * 7) - 3 : Math.round((r.u() * 10 - 5) * 4) / 4;
+    }
+    function bnds(setter, idx, c, integral) {
+        var t = r.u(), a = Math.round((r.u() * 20 - 10) * 4) / 4, w = 1 + Math.round(r.u() * 40) / 4,
+            w2 = 1 + Math.round(r.u() * 40) / 4;
+        if (integral) { w = Math.ceil(w); w2 = Math.ceil(w2); }
+        if (feasible) {
+            if (t < 0.08) setter(P, idx, glpk.GLP_FR, 0, 0);
+            else if (t < 0.38) setter(P, idx, glpk.GLP_LO, c - w, 0);
+            else if (t < 0.58) setter(P, idx, glpk.GLP_UP, 0, c + w);
+            else if (t < 0.95) setter(P, idx, glpk.GLP_DB, c - w, c + w2);
+            else setter(P, idx, glpk.GLP_FX, c, c);
+            return;
+        }
+        if (t < 0.10) setter(P, idx, glpk.GLP_FR, 0, 0);
+        else if (t < 0.45) setter(P, idx, glpk.GLP_LO, a, 0);
+        else if (t < 0.65) setter(P, idx, glpk.GLP_UP, 0, a);
+        else if (t < 0.92) setter(P, idx, glpk.GLP_DB, a, a + w);
+        else setter(P, idx, glpk.GLP_FX, a, a);
+    }
+    for (j = 1; j <= n; j++) {
+        glpk.glp_set_obj_coef(P, j, Math.round((r.u() * 20 - 10) * 8) / 8);
+    }
+    glpk.glp_set_obj_coef(P, 0, Math.round(r.u() * 100) / 4);
+    var ia = [0], ja = [0], ar = [0], rowv = [];
+    for (i = 1; i <= m; i++) {
+        rowv[i] = 0;
+        for (j = 1; j <= n; j++)
+            if (r.u() < dens) {
+                var v = Math.round((r.u() * 18 - 9) * 16) / 16 || 1;
+                ia.push(i); ja.push(j); ar.push(v); rowv[i] += v * x0[j];
+            }
+    }
+    for (i = 1; i <= m; i++) bnds(glpk.glp_set_row_bnds, i, rowv[i], false);
+    for (j = 1; j <= n; j++) bnds(glpk.glp_set_col_bnds, j, x0[j], isint[j]);
+    glpk.glp_load_matrix(P, ia.length - 1, ia, ja, ar);
+    if (withInt) {
+        for (j = 1; j <= n; j++) if (isint[j]) glpk.glp_set_col_kind(P, j, glpk.GLP_IV);
+    }
+    return P;
+}
+
+function readLp(file) {
+    var P = newProb();
+    glpk.glp_read_lp_from_string(P, null, fs.readFileSync(path.join(REF, 'test', file)).toString());
+    return P;
+}
+
+// ---- dump helpers ---------------------------------------------------------
+function dumpProb(P, gen) {
+    var m = P.m, n = P.n, i, j, d = {m: m, n: n, nnz: P.nnz, dir: P.dir, c0: P.col[0] ? 0 : P.c0};
+    d.c0 = P.c0;
+    if (gen) d.gen = gen;
+    var rt = [], rl = [], ru = [], rr = [], rs = [];
+    for (i = 1; i <= m; i++) { var R = P.row[i]; rt.push(R.type); rl.push(R.lb); ru.push(R.ub); rr.push(R.rii); rs.push(R.stat); }
+    var ct = [], cl = [], cu = [], cc = [], cs = [], ck = [], cst = [];
+    for (j = 1; j <= n; j++) { var C = P.col[j]; ct.push(C.type); cl.push(C.lb); cu.push(C.ub); cc.push(C.coef); cs.push(C.sjj); ck.push(C.kind); cst.push(C.stat); }
+    Object.assign(d, {row_type: rt, row_lb: rl, row_ub: ru, row_rii: rr, row_stat: rs,
+                      col_type: ct, col_lb: cl, col_ub: cu, col_coef: cc, col_sjj: cs, col_kind: ck, col_stat: cst});
+    if (!gen) {
+        // A by columns in list order (init_csa, glpspx01.js:96-105)
+        var ptr = [0], ind = [], val = [];
+        for (j = 1; j <= n; j++) {
+            for (var a = P.col[j].ptr; a != null; a = a.c_next) { ind.push(a.row.i); val.push(a.val); }
+            ptr.push(ind.length);
+        }
+        d.A_ptr = ptr; d.A_ind = ind; d.A_val = val;
+    }
+    return d;
+}
+
+function snapshotBasis(P) {
+    var i, j, rs = [], cs = [];
+    for (i = 1; i <= P.m; i++) rs.push(P.row[i].stat);
+    for (j = 1; j <= P.n; j++) cs.push(P.col[j].stat);
+    return {row_stat: rs, col_stat: cs};
+}
+
+function runLp(P, opts, traceCap) {
+    var tr = [];
+    glpk.__set_trace(function (kind, it, phase, p, q, kq, kp, t) {
+        if (tr.length < traceCap) tr.push([it, phase, p, q, kq, kp, t]);
+    });
+    var parm = new glpk.SMCP(opts);
+    var f0 = glpk.__cnt.factorize;
+    var t0 = process.hrtime.bigint();
+    var ret = glpk.glp_simplex(P, parm);
+    var dt = Number(process.hrtime.bigint() - t0) / 1e9;
+    glpk.__set_trace(null);
+    var i, j, out = {opts: opts, ret: ret, pbs_stat: P.pbs_stat, dbs_stat: P.dbs_stat, obj_val: P.obj_val,
+                     it_cnt: P.it_cnt, some: P.some, factorizations: glpk.__cnt.factorize - f0, seconds: dt};
+    var a = snapshotBasis(P);
+    out.row_stat = a.row_stat; out.col_stat = a.col_stat;
+    out.row_prim = []; out.row_dual = []; out.col_prim = []; out.col_dual = [];
+    for (i = 1; i <= P.m; i++) { out.row_prim.push(P.row[i].prim); out.row_dual.push(P.row[i].dual); }
+    for (j = 1; j <= P.n; j++) { out.col_prim.push(P.col[j].prim); out.col_dual.push(P.col[j].dual); }
+    out.trace = tr;
+    return out;
+}
+
+function writeJson(name, obj) {
+    fs.writeFileSync(path.join(OUT, name + '.json'), JSON.stringify(obj));
+    console.log('wrote', name, obj.runs ? obj.runs.map(function (r) { return 'meth' + (r.opts.meth || 1) + ':ret' + r.ret + ':it' + r.it_cnt + ':obj' + r.obj_val + (r.mip_obj !== undefined ? ':mip' + r.mip_obj : ''); }).join(' ') : '');
+}
+
+// LP instance: run primal and dual each on a fresh copy, from the initial basis.
+function lpCase(name, mk, gen, methods, traceCap, extraRuns) {
+    var P0 = mk();
+    var d = dumpProb(P0, gen);
+    d.name = name; d.kind = 'lp'; d.runs = [];
+    (methods || [1, 3]).forEach(function (meth) {
+        var P = mk();
+        d.runs.push(runLp(P, {meth: meth}, traceCap === undefined ? 100000 : traceCap));
+    });
+    (extraRuns || []).forEach(function (opts) {
+        var P = mk();
+        d.runs.push(runLp(P, opts, traceCap === undefined ? 100000 : traceCap));
+    });
+    writeJson('lp_' + name, d);
+}
+
+// MIP instance: root primal glp_simplex then glp_intopt (default IOCP), the
+// flow of SURVEY.md §8(d) C4/C5.
+function mipCase(name, mk, gen) {
+    var P = mk();
+    var d = dumpProb(P, gen);
+    d.name = name; d.kind = 'mip';
+    var root = runLp(P, {}, 0);
+    delete root.trace;
+    var s0 = glpk.__cnt.solve_node, f0 = glpk.__cnt.factorize, it0 = P.it_cnt;
+    var t0 = process.hrtime.bigint();
+    var ret = glpk.glp_intopt(P, new glpk.IOCP({}));
+    var dt = Number(process.hrtime.bigint() - t0) / 1e9;
+    var j, x = [];
+    for (j = 1; j <= P.n; j++) x.push(P.col[j].mipx);
+    var rx = [];
+    for (j = 1; j <= P.m; j++) rx.push(P.row[j].mipx);
+    d.root = root;
+    d.mip = {ret: ret, mip_stat: P.mip_stat, mip_obj: P.mip_obj, col_mipx: x, row_mipx: rx,
+             lp_solves: glpk.__cnt.solve_node - s0, factorizations: glpk.__cnt.factorize - f0,
+             pivots: P.it_cnt - it0, seconds: dt};
+    fs.writeFileSync(path.join(OUT, 'mip_' + name + '.json'), JSON.stringify(d));
+    console.log('wrote mip', name, 'ret', ret, 'obj', P.mip_obj, 'lp', d.mip.lp_solves, 'piv', d.mip.pivots, 'sec', dt.toFixed(2));
+}
+
+// ---- instances ------------------------------------------------------------
+lpCase('test', function () { return readLp('test.lpt'); }, null);
+lpCase('todd', function () { return readLp('todd.lpt'); }, null);
+lpCase('gap', function () { return readLp('gap.lpt'); }, null);
+[[64, 256], [128, 512], [256, 1024]].forEach(function (s) {
+    lpCase('dense_' + s[0] + 'x' + s[1], function () { return genDense(s[0], s[1], 42); },
+           {kind: 'dense', m: s[0], n: s[1], seed: 42}, [1, 3], 100000,
+           s[0] === 256 ? [{meth: 3, it_lim: 100}, {meth: 1, it_lim: 50}] : []);
+});
+for (var sd = 1; sd <= 32; sd++) {
+    var mm = 4 + (sd * 7) % 29, nn = 5 + (sd * 13) % 41;
+    (function (sd, mm, nn) {
+        if (sd <= 12)
+            lpCase('wild' + sd, function () { return genMix(sd, mm, nn, 0.35, false, false); }, null, [1, 2, 3]);
+        else
+            lpCase('mix' + sd, function () { return genMix(sd, mm, nn, 0.35, false, true); }, null, [1, 2, 3]);
+    })(sd, mm, nn);
+}
+mipCase('gap', function () { return readLp('gap.lpt'); }, null);
+mipCase('todd', function () { return readLp('todd.lpt'); }, null);
+mipCase('c5s_12x20', function () { return genC5s(12, 20, 42); }, {kind: 'c5s', m: 12, n: 20, seed: 42});
+for (var ms = 1; ms <= 12; ms++) {
+    (function (ms) {
+        mipCase('mixint' + ms, function () { return genMix(100 + ms, 6 + ms, 8 + 2 * ms, 0.5, true, true); }, null);
+    })(ms);
+}
+if (BIG) {
+    lpCase('c2s', function () { return genC2s(821, 1571, 7, 42); }, {kind: 'c2s', m: 821, n: 1571, nzc: 7, seed: 42}, [3, 1], 0);
+    lpCase('dense_512x2048', function () { return genDense(512, 2048, 42); }, {kind: 'dense', m: 512, n: 2048, seed: 42}, [1, 3], 0);
+    mipCase('c5s_12x30', function () { return genC5s(12, 30, 42); }, {kind: 'c5s', m: 12, n: 30, seed: 42});
+}
