@@ -1,0 +1,1437 @@
+// libglpk_mi355x host side: the C-ABI of include/glpk_mi355x.h.
+//
+// The control flow of spx_primal / spx_dual (glpspx01.js:1705-2056,
+// glpspx02.js:1614-1966) runs here unchanged; the inner "normal pivot" path
+// of each loop is executed on the device in batches (gk_kernels.hip), and
+// the host only resumes at the branch the device stopped on (DState.stop).
+// Problem data, the basis header and the explicit inverse stay resident in
+// HBM across calls; O(m+n) vectors cross PCIe only at phase switches,
+// refactorizations and store_sol.
+#include "gk_internal.h"
+#include "../../include/glpk_mi355x.h"
+
+#include <algorithm>
+#include <chrono>
+#include <cfloat>
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+using namespace gk;
+
+namespace {
+
+thread_local std::string g_err;
+
+void set_err(const char *fmt, ...)
+{
+    char buf[1024];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof buf, fmt, ap);
+    va_end(ap);
+    g_err = buf;
+}
+
+struct AbiError {
+    std::string msg;
+};
+
+#define HIPCHK(x)                                                                            \
+    do {                                                                                     \
+        hipError_t e__ = (x);                                                                \
+        if (e__ != hipSuccess) throw AbiError{std::string("HIP error ") + hipGetErrorString(e__) + " at " #x}; \
+    } while (0)
+
+#define ABI_REQUIRE(c, ...)                                                                  \
+    do {                                                                                     \
+        if (!(c)) {                                                                          \
+            char b__[512];                                                                   \
+            snprintf(b__, sizeof b__, __VA_ARGS__);                                          \
+            throw AbiError{b__};                                                             \
+        }                                                                                    \
+    } while (0)
+
+double now_s()
+{
+    return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+template <typename T>
+struct DBuf {
+    T *p = nullptr;
+    size_t n = 0;
+    void ensure(size_t cnt)
+    {
+        if (cnt <= n && p) return;
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        n = 0;
+        size_t bytes = std::max<size_t>(cnt, 1) * sizeof(T);
+        HIPCHK(hipMalloc((void **)&p, bytes));
+        n = std::max<size_t>(cnt, 1);
+    }
+    void release()
+    {
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        n = 0;
+    }
+};
+
+}  // namespace
+
+struct gk_ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+};
+
+// device copy of the problem (A in scaled form) plus the simplex working set
+struct Engine {
+    int m = 0, n = 0, nnz = 0;
+    int dense = 0, lda = 0;
+    unsigned long long a_version = 0;
+    DBuf<double> A;                         // dense
+    DBuf<int> cptr, cind, rptr, rcol;        // CSC / CSR
+    DBuf<double> cval, rval;
+    // working set
+    DBuf<signed char> type, orig_type, stat, refsp;
+    DBuf<double> lb, ub, coef, orig_lb, orig_ub, obj;
+    DBuf<int> head, bind;
+    DBuf<double> bbar, cbar, gamma, tcol, trow, rho, rowp, u, s, h, wcol, ys, work, r1, r2, partial;
+    DBuf<DState> st;
+    MatDev mat() const
+    {
+        MatDev M{};
+        M.m = m; M.n = n; M.nnz = nnz; M.dense = dense;
+        M.A = A.p; M.lda = lda;
+        M.cptr = cptr.p; M.cind = cind.p; M.cval = cval.p;
+        M.rptr = rptr.p; M.rcol = rcol.p; M.rval = rval.p;
+        int avg = n > 0 ? nnz / n : 0;
+        M.lpc = avg >= 48 ? 64 : (avg >= 6 ? 8 : 1);
+        return M;
+    }
+    ~Engine()
+    {
+        A.release(); cptr.release(); cind.release(); rptr.release(); rcol.release(); cval.release(); rval.release();
+        type.release(); orig_type.release(); stat.release(); refsp.release();
+        lb.release(); ub.release(); coef.release(); orig_lb.release(); orig_ub.release(); obj.release();
+        head.release(); bind.release();
+        bbar.release(); cbar.release(); gamma.release(); tcol.release(); trow.release(); rho.release(); rowp.release();
+        u.release(); s.release(); h.release(); wcol.release(); ys.release(); work.release(); r1.release(); r2.release();
+        partial.release(); st.release();
+    }
+};
+
+struct gk_bfd {
+    gk_ctx *ctx = nullptr;
+    gk_bfcp parm{};
+    int valid = 0;
+    int m = 0, ldb = 0;
+    int upd_cnt = 0;
+    DBuf<double> Binv;
+    // re-inversion scratch
+    DBuf<double> C, X, Y, CinvR, BS, G, vecx, vecy, partial;
+    DBuf<int> idx_i, piv_step, piv, flag;
+    DBuf<int> bptr, brow;                      // basis given as CSC (gk_bfd_factorize*)
+    DBuf<double> bval;
+    Engine *eng = nullptr;
+    gk_spx_stats stats{};
+};
+
+static const size_t PARTIAL_CAP = (size_t)1 << 20;   // >= splits * rows of every gemv (see gemv_plan)
+
+// ---------------------------------------------------------------------------
+// re-inversion of the basis matrix
+// ---------------------------------------------------------------------------
+// Basis columns: slack-like unit columns e_r (+1) and "structural" columns.
+// With S the rows covered by slack columns (positions posS), R the other
+// rows and J the structural positions, C = B[R, J] is k x k and
+//   inv(B)[J, R] = inv(C),  inv(B)[posS(s), s] = 1,  inv(B)[posS, R] = -B[S, J] inv(C).
+struct BasisSplit {
+    int k = 0, ms = 0;
+    std::vector<int> posJ, colJ, rowR, posS, rowS, rowmap;   // rowmap[r-1] = a (R) or -(s+1) (S)
+};
+
+static int reinvert_core(gk_bfd *f, const BasisSplit &bs, const MatDev *Adense, int from_csc, double sign,
+                         const int *csc_ptr, const int *csc_row, const double *csc_val)
+{
+    hipStream_t s = f->ctx->stream;
+    const int m = f->m, k = bs.k, ms = bs.ms;
+    const double t0 = now_s();
+    f->Binv.ensure((size_t)f->ldb * m);
+    // index lists on the device: posJ | colJ | rowR | posS | rowS | rowmap
+    std::vector<int> packed;
+    packed.reserve((size_t)3 * k + 2 * ms + m);
+    packed.insert(packed.end(), bs.posJ.begin(), bs.posJ.end());
+    packed.insert(packed.end(), bs.colJ.begin(), bs.colJ.end());
+    packed.insert(packed.end(), bs.rowR.begin(), bs.rowR.end());
+    packed.insert(packed.end(), bs.posS.begin(), bs.posS.end());
+    packed.insert(packed.end(), bs.rowS.begin(), bs.rowS.end());
+    packed.insert(packed.end(), bs.rowmap.begin(), bs.rowmap.end());
+    f->idx_i.ensure(packed.size() + 1);
+    HIPCHK(hipMemcpyAsync(f->idx_i.p, packed.data(), packed.size() * sizeof(int), hipMemcpyHostToDevice, s));
+    int *d_posJ = f->idx_i.p, *d_colJ = d_posJ + k, *d_rowR = d_colJ + k, *d_posS = d_rowR + k,
+        *d_rowS = d_posS + ms, *d_rowmap = d_rowS + ms;
+    double *result = nullptr;
+    if (k > 0) {
+        f->C.ensure((size_t)k * k);
+        f->X.ensure((size_t)2 * k * k);
+        f->Y.ensure((size_t)2 * k * k);
+        f->CinvR.ensure((size_t)k * k);
+        if (ms > 0) {
+            f->BS.ensure((size_t)ms * k);
+            f->G.ensure((size_t)ms * k);
+        }
+        if (from_csc) {
+            // C and BS from CSC columns (sign applied), selected by colJ
+            fill_d(s, f->X.p, 0.0, (size_t)k * k);
+            if (ms > 0) fill_d(s, f->BS.p, 0.0, (size_t)ms * k);
+            extern void gather_csc_sel(hipStream_t, int, const int *, const int *, const int *, const double *,
+                                       const int *, double *, double *, int, double);
+            gather_csc_sel(s, k, d_colJ, csc_ptr, csc_row, csc_val, d_rowmap, f->X.p, f->BS.p, ms, sign);
+        } else {
+            gather_basis_blocks(s, *Adense, m, k, d_colJ, d_rowR, f->X.p, f->BS.p, ms, d_rowS);
+        }
+        f->piv_step.ensure(k);
+        f->piv.ensure(k);
+        f->flag.ensure(1);
+        gauss_jordan(s, f->X.p, f->Y.p, k, f->piv_step.p, f->piv.p, f->flag.p, 1e-15, &result);
+        int flag = 0;
+        HIPCHK(hipMemcpyAsync(&flag, f->flag.p, sizeof(int), hipMemcpyDeviceToHost, s));
+        HIPCHK(hipStreamSynchronize(s));
+        if (flag) {
+            f->valid = 0;
+            f->stats.reinversions++;
+            f->stats.seconds_reinvert += now_s() - t0;
+            return 1;   // BFD_ESING
+        }
+        extract_inverse_rowmajor(s, result, k, f->piv.p, f->CinvR.p);
+        if (ms > 0) gemm_bs_cinv(s, f->BS.p, ms, k, f->CinvR.p, f->G.p, 1);
+    }
+    assemble_binv(s, f->Binv.p, m, f->ldb, k, ms, d_posJ, d_rowR, d_posS, d_rowS, f->CinvR.p, f->G.p);
+    HIPCHK(hipStreamSynchronize(s));
+    f->valid = 1;
+    f->upd_cnt = 0;
+    f->stats.reinversions++;
+    f->stats.seconds_reinvert += now_s() - t0;
+    return 0;
+}
+
+// split by the basis header of (I | -A): head[1..m] (1-based values)
+static bool split_from_head(int m, const int *head1, BasisSplit &bs)
+{
+    bs = BasisSplit();
+    std::vector<int> srow_pos(m + 1, 0);
+    for (int i = 1; i <= m; i++) {
+        int k = head1[i];
+        if (k <= m) {
+            if (srow_pos[k]) return false;
+            srow_pos[k] = i;
+        } else {
+            bs.posJ.push_back(i);
+            bs.colJ.push_back(k - m);
+        }
+    }
+    bs.rowmap.assign(m, 0);
+    for (int r = 1; r <= m; r++) {
+        if (srow_pos[r]) {
+            bs.rowmap[r - 1] = -(int)(bs.rowS.size() + 1);
+            bs.rowS.push_back(r);
+            bs.posS.push_back(srow_pos[r]);
+        } else {
+            bs.rowmap[r - 1] = (int)bs.rowR.size();
+            bs.rowR.push_back(r);
+        }
+    }
+    bs.k = (int)bs.posJ.size();
+    bs.ms = (int)bs.rowS.size();
+    return bs.k == (int)bs.rowR.size();
+}
+
+// ---------------------------------------------------------------------------
+// device working set
+// ---------------------------------------------------------------------------
+static void engine_alloc(Engine &E, int m, int n)
+{
+    const size_t mn = (size_t)m + n;
+    E.type.ensure(mn); E.orig_type.ensure(mn); E.refsp.ensure(mn); E.stat.ensure(n);
+    E.lb.ensure(mn); E.ub.ensure(mn); E.coef.ensure(mn); E.orig_lb.ensure(mn); E.orig_ub.ensure(mn);
+    E.obj.ensure(n); E.head.ensure(mn); E.bind.ensure(mn);
+    E.bbar.ensure(m); E.cbar.ensure(n); E.gamma.ensure(std::max(m, n));
+    E.tcol.ensure(m); E.trow.ensure(n); E.rho.ensure(m); E.rowp.ensure(m); E.u.ensure(m); E.s.ensure(n);
+    E.h.ensure(m); E.wcol.ensure(n); E.ys.ensure(m); E.work.ensure(std::max(m, n)); E.r1.ensure(m); E.r2.ensure(m);
+    E.partial.ensure(PARTIAL_CAP);
+    E.st.ensure(1);
+}
+
+__global__ void k_densify(const int *cptr, const int *cind, const double *cval, int n, double *A, int lda)
+{
+    const int c = blockIdx.x;
+    if (c >= n) return;
+    for (int t = cptr[c] + threadIdx.x; t < cptr[c + 1]; t += blockDim.x) A[(size_t)c * lda + cind[t]] = cval[t];
+}
+
+// A := rii * a * sjj as init_csa (glpspx01.js:96-105), uploaded once per a_version
+static void engine_upload_matrix(gk_bfd *f, const gk_lp *lp)
+{
+    Engine &E = *f->eng;
+    hipStream_t s = f->ctx->stream;
+    const int m = lp->m, n = lp->n, nnz = lp->nnz;
+    if (lp->a_version != 0 && lp->a_version == E.a_version && E.m == m && E.n == n && E.nnz == nnz) return;
+    E.m = m; E.n = n; E.nnz = nnz;
+    std::vector<int> cptr(n + 1), cind(std::max(nnz, 1));
+    std::vector<double> cval(std::max(nnz, 1));
+    int t = 0;
+    for (int j = 1; j <= n; j++) {
+        cptr[j - 1] = t;
+        for (int p = lp->A_ptr[j]; p < lp->A_ptr[j + 1]; p++) {
+            int i = lp->A_ind[p];
+            ABI_REQUIRE(1 <= i && i <= m, "gk_spx: A_ind[%d] = %d; row number out of range", p, i);
+            cind[t] = i - 1;
+            cval[t] = lp->rii[i] * lp->A_val[p] * lp->sjj[j];
+            t++;
+        }
+    }
+    cptr[n] = t;
+    ABI_REQUIRE(t == nnz, "gk_spx: A_ptr describes %d entries, nnz = %d", t, nnz);
+    E.dense = ((double)nnz >= 0.5 * (double)m * (double)n) ? 1 : 0;
+    E.cptr.ensure(n + 1);
+    E.cind.ensure(std::max(nnz, 1));
+    E.cval.ensure(std::max(nnz, 1));
+    HIPCHK(hipMemcpyAsync(E.cptr.p, cptr.data(), (n + 1) * sizeof(int), hipMemcpyHostToDevice, s));
+    HIPCHK(hipMemcpyAsync(E.cind.p, cind.data(), (size_t)nnz * sizeof(int), hipMemcpyHostToDevice, s));
+    HIPCHK(hipMemcpyAsync(E.cval.p, cval.data(), (size_t)nnz * sizeof(double), hipMemcpyHostToDevice, s));
+    if (E.dense) {
+        E.lda = (m + 7) & ~7;
+        E.A.ensure((size_t)E.lda * n);
+        fill_d(s, E.A.p, 0.0, (size_t)E.lda * n);
+        hipLaunchKernelGGL(k_densify, dim3(n), dim3(256), 0, s, E.cptr.p, E.cind.p, E.cval.p, n, E.A.p, E.lda);
+    } else {
+        // CSR copy (row order of entries does not matter numerically)
+        std::vector<int> rptr(m + 1, 0), rcol(std::max(nnz, 1));
+        std::vector<double> rval(std::max(nnz, 1));
+        for (int q = 0; q < nnz; q++) rptr[cind[q] + 1]++;
+        for (int r = 0; r < m; r++) rptr[r + 1] += rptr[r];
+        std::vector<int> fillp(rptr.begin(), rptr.end() - 1);
+        for (int c = 0; c < n; c++)
+            for (int q = cptr[c]; q < cptr[c + 1]; q++) {
+                int pos = fillp[cind[q]]++;
+                rcol[pos] = c;
+                rval[pos] = cval[q];
+            }
+        E.rptr.ensure(m + 1);
+        E.rcol.ensure(std::max(nnz, 1));
+        E.rval.ensure(std::max(nnz, 1));
+        HIPCHK(hipMemcpyAsync(E.rptr.p, rptr.data(), (m + 1) * sizeof(int), hipMemcpyHostToDevice, s));
+        HIPCHK(hipMemcpyAsync(E.rcol.p, rcol.data(), (size_t)nnz * sizeof(int), hipMemcpyHostToDevice, s));
+        HIPCHK(hipMemcpyAsync(E.rval.p, rval.data(), (size_t)nnz * sizeof(double), hipMemcpyHostToDevice, s));
+    }
+    HIPCHK(hipStreamSynchronize(s));
+    if (E.dense) {   // the dense copy is the only one the passes read
+        E.cind.release(); E.cval.release();
+        E.cind.ensure(1); E.cval.ensure(1);
+    }
+    E.a_version = lp->a_version;
+}
+
+// ---------------------------------------------------------------------------
+// the simplex driver
+// ---------------------------------------------------------------------------
+struct Spx {
+    gk_ctx *ctx;
+    gk_bfd *f;
+    Engine *E;
+    gk_lp *lp;
+    const gk_smcp *parm;
+    int m, n, dual;
+    hipStream_t s;
+    // host mirrors (1-based like the reference csa)
+    std::vector<signed char> type, orig_type, stat;
+    std::vector<double> lb, ub, coef, orig_lb, orig_ub, obj, bbar, cbar, gamma;
+    std::vector<int> head, bind;
+    double zeta = 0.0, tm_beg = 0.0;
+    int phase = 0, it_beg = 0;
+    DState hs{};
+    bool head_stale = false, vec_stale = false;
+
+    SpxDev dev() const
+    {
+        SpxDev d{};
+        d.m = m; d.n = n; d.A = E->mat();
+        d.type = E->type.p; d.orig_type = E->orig_type.p; d.stat = E->stat.p; d.refsp = E->refsp.p;
+        d.lb = E->lb.p; d.ub = E->ub.p; d.coef = E->coef.p; d.orig_lb = E->orig_lb.p; d.orig_ub = E->orig_ub.p;
+        d.obj = E->obj.p; d.head = E->head.p; d.bind = E->bind.p;
+        d.bbar = E->bbar.p; d.cbar = E->cbar.p; d.gamma = E->gamma.p;
+        d.tcol = E->tcol.p; d.trow = E->trow.p; d.rho = E->rho.p; d.rowp = E->rowp.p; d.u = E->u.p; d.s = E->s.p;
+        d.h = E->h.p; d.wcol = E->wcol.p; d.ys = E->ys.p; d.work = E->work.p; d.r1 = E->r1.p; d.r2 = E->r2.p;
+        d.Binv = f->Binv.p; d.ldb = f->ldb;
+        d.partial = E->partial.p; d.partial_cap = PARTIAL_CAP;
+        d.st = E->st.p;
+        return d;
+    }
+
+    template <typename T>
+    void up(DBuf<T> &d, const std::vector<T> &h, size_t cnt)
+    {
+        HIPCHK(hipMemcpyAsync(d.p, h.data() + 1, cnt * sizeof(T), hipMemcpyHostToDevice, s));
+    }
+    template <typename T>
+    void down(std::vector<T> &h, const DBuf<T> &d, size_t cnt)
+    {
+        HIPCHK(hipMemcpyAsync(h.data() + 1, d.p, cnt * sizeof(T), hipMemcpyDeviceToHost, s));
+    }
+    void sync() { HIPCHK(hipStreamSynchronize(s)); f->stats.host_syncs++; }
+
+    // bring the host mirrors of the pivot-updated arrays up to date
+    void pull()
+    {
+        if (!head_stale && !vec_stale) return;
+        down(head, E->head, (size_t)m + n);
+        down(bind, E->bind, (size_t)m + n);
+        down(stat, E->stat, n);
+        down(bbar, E->bbar, m);
+        down(cbar, E->cbar, n);
+        if (!dual) down(coef, E->coef, (size_t)m + n);
+        sync();
+        head_stale = vec_stale = false;
+    }
+    void push_bounds()
+    {
+        up(E->type, type, (size_t)m + n);
+        up(E->lb, lb, (size_t)m + n);
+        up(E->ub, ub, (size_t)m + n);
+        up(E->stat, stat, n);
+    }
+    void push_state()
+    {
+        HIPCHK(hipMemcpyAsync(E->st.p, &hs, sizeof(DState), hipMemcpyHostToDevice, s));
+    }
+    void pull_state()
+    {
+        HIPCHK(hipMemcpyAsync(&hs, E->st.p, sizeof(DState), hipMemcpyDeviceToHost, s));
+        sync();
+    }
+
+    double get_xN(int j) const
+    {
+        int k = head[m + j];
+        switch (stat[j]) {
+        case NL: return lb[k];
+        case NU: return ub[k];
+        case NF: return 0.0;
+        default: return lb[k];
+        }
+    }
+
+    // ---- device computations between batches ------------------------------
+    // eval_cbar (glpspx01.js:565): pi = inv(B') cB refined once, d_j = c_k - N_j' pi
+    void eval_cbar()
+    {
+        SpxDev d = dev();
+        MatDev A = E->mat();
+        double *cB = E->r1.p, *pi = E->u.p, *r = E->r2.p, *dd = E->work.p;
+        cb_vector(s, m, E->head.p, E->coef.p, cB);
+        gemv_t(s, f->Binv.p, m, m, f->ldb, cB, pi, 1.0);
+        colpass(s, A, CP_RESID, 0, m, E->head.p, E->stat.p, E->coef.p, cB, pi, nullptr, r, nullptr, nullptr);
+        gemv_t(s, f->Binv.p, m, m, f->ldb, r, dd, 1.0);
+        vec_axpy(s, pi, dd, 1.0, m);
+        colpass(s, A, CP_CBAR, m, n, E->head.p, E->stat.p, E->coef.p, nullptr, pi, nullptr, E->cbar.p, nullptr, nullptr);
+        (void)d;
+        down(cbar, E->cbar, n);
+        sync();
+    }
+
+    // eval_beta (glpspx01.js:473): h = -N xN; beta = inv(B) h, refined once
+    // (refine_ftran :251: beta += inv(B) (h - B beta))
+    void eval_bbar()
+    {
+        SpxDev d = dev();
+        MatDev A = E->mat();
+        double *w = E->s.p;   // n-sized scratch
+        double *ys = E->r1.p, *wc = E->wcol.p, *h = E->h.p, *beta = E->bbar.p, *t = E->r2.p, *dd = E->work.p;
+        neg_xn_weights(s, d, w);
+        fill_d(s, ys, 0.0, m);
+        fill_d(s, wc, 0.0, n);
+        scatter_pos(s, m, m, n, E->head.p, w, ys, wc);
+        aprod_neg(s, A, wc, ys, h, E->partial.p, PARTIAL_CAP);                  // h = ys - A wc
+        gemv_n(s, f->Binv.p, m, m, f->ldb, h, E->partial.p, PARTIAL_CAP, beta, 1.0, nullptr, 0.0);
+        fill_d(s, ys, 0.0, m);
+        fill_d(s, wc, 0.0, n);
+        scatter_pos(s, m, 0, m, E->head.p, beta, ys, wc);
+        aprod_neg(s, A, wc, ys, t, E->partial.p, PARTIAL_CAP);                  // t = B beta
+        rsub_into(t, h);                                                       // t = h - B beta
+        gemv_n(s, f->Binv.p, m, m, f->ldb, t, E->partial.p, PARTIAL_CAP, dd, 1.0, nullptr, 0.0);
+        vec_axpy(s, beta, dd, 1.0, m);
+        down(bbar, E->bbar, m);
+        sync();
+    }
+
+    void rsub_into(double *y, const double *a);   // y = a - y
+
+    bool reinvert()
+    {
+        pull();
+        BasisSplit bs;
+        if (!split_from_head(m, head.data(), bs)) return false;
+        MatDev A = E->mat();
+        int ret;
+        if (E->dense)
+            ret = reinvert_core(f, bs, &A, 0, 1.0, nullptr, nullptr, nullptr);
+        else
+            ret = reinvert_core_csc(bs);
+        return ret == 0;
+    }
+    int reinvert_core_csc(const BasisSplit &bs);
+
+    // ---- host-side logic on the mirrors -------------------------------------
+    // dual: check_feas (glpspx02.js:1296)
+    int dual_check_feas(double tol_dj)
+    {
+        for (int j = 1; j <= n; j++) {
+            int k = head[m + j];
+            if (cbar[j] < -tol_dj)
+                if (orig_type[k] == LO || orig_type[k] == FR) return 1;
+            if (cbar[j] > +tol_dj)
+                if (orig_type[k] == UP || orig_type[k] == FR) return 1;
+        }
+        return 0;
+    }
+    void set_aux_bnds()                                  // glpspx02.js:1317
+    {
+        for (int k = 1; k <= m + n; k++) {
+            switch (orig_type[k]) {
+            case FR: type[k] = DB; lb[k] = -1e3; ub[k] = +1e3; break;
+            case LO: type[k] = DB; lb[k] = 0.0; ub[k] = +1.0; break;
+            case UP: type[k] = DB; lb[k] = -1.0; ub[k] = 0.0; break;
+            default: type[k] = FX; lb[k] = ub[k] = 0.0; break;
+            }
+        }
+        for (int j = 1; j <= n; j++) {
+            int k = head[m + j];
+            if (type[k] == FX) stat[j] = NS;
+            else if (cbar[j] >= 0.0) stat[j] = NL;
+            else stat[j] = NU;
+        }
+        push_bounds();
+    }
+    void set_orig_bnds()                                 // glpspx02.js:1361
+    {
+        type = orig_type; lb = orig_lb; ub = orig_ub;
+        for (int j = 1; j <= n; j++) {
+            int k = head[m + j];
+            switch (type[k]) {
+            case FR: stat[j] = NF; break;
+            case LO: stat[j] = NL; break;
+            case UP: stat[j] = NU; break;
+            case DB:
+                if (cbar[j] >= +DBL_EPSILON) stat[j] = NL;
+                else if (cbar[j] <= -DBL_EPSILON) stat[j] = NU;
+                else if (std::fabs(lb[k]) <= std::fabs(ub[k])) stat[j] = NL;
+                else stat[j] = NU;
+                break;
+            default: stat[j] = NS; break;
+            }
+        }
+        push_bounds();
+    }
+    int dual_check_stab(double tol_dj)                   // glpspx02.js:1410
+    {
+        for (int j = 1; j <= n; j++) {
+            if (cbar[j] < -tol_dj)
+                if (stat[j] == NL || stat[j] == NF) return 1;
+            if (cbar[j] > +tol_dj)
+                if (stat[j] == NU || stat[j] == NF) return 1;
+        }
+        return 0;
+    }
+    // primal: set_aux_obj / set_orig_obj / check_stab / check_feas (glpspx01.js:1373-1522)
+    int set_aux_obj(double tol_bnd)
+    {
+        int cnt = 0;
+        tol_bnd *= 0.90;
+        for (int k = 1; k <= m + n; k++) coef[k] = 0.0;
+        for (int i = 1; i <= m; i++) {
+            int k = head[i];
+            if (type[k] == LO || type[k] == DB || type[k] == FX) {
+                double eps = tol_bnd * (1.0 + 0.10 * std::fabs(lb[k]));
+                if (bbar[i] < lb[k] - eps) { coef[k] = -1.0; cnt++; }
+            }
+            if (type[k] == UP || type[k] == DB || type[k] == FX) {
+                double eps = tol_bnd * (1.0 + 0.10 * std::fabs(ub[k]));
+                if (bbar[i] > ub[k] + eps) { coef[k] = +1.0; cnt++; }
+            }
+        }
+        up(E->coef, coef, (size_t)m + n);
+        return cnt;
+    }
+    void set_orig_obj()
+    {
+        for (int i = 1; i <= m; i++) coef[i] = 0.0;
+        for (int j = 1; j <= n; j++) coef[m + j] = zeta * obj[j];
+        up(E->coef, coef, (size_t)m + n);
+    }
+    int primal_check_stab(double tol_bnd)
+    {
+        for (int i = 1; i <= m; i++) {
+            int k = head[i];
+            if (phase == 1 && coef[k] < 0.0) {
+                double eps = tol_bnd * (1.0 + 0.10 * std::fabs(lb[k]));
+                if (bbar[i] > lb[k] + eps) return 1;
+            } else if (phase == 1 && coef[k] > 0.0) {
+                double eps = tol_bnd * (1.0 + 0.10 * std::fabs(ub[k]));
+                if (bbar[i] < ub[k] - eps) return 1;
+            } else {
+                if (type[k] == LO || type[k] == DB || type[k] == FX) {
+                    double eps = tol_bnd * (1.0 + 0.10 * std::fabs(lb[k]));
+                    if (bbar[i] < lb[k] - eps) return 1;
+                }
+                if (type[k] == UP || type[k] == DB || type[k] == FX) {
+                    double eps = tol_bnd * (1.0 + 0.10 * std::fabs(ub[k]));
+                    if (bbar[i] > ub[k] + eps) return 1;
+                }
+            }
+        }
+        return 0;
+    }
+    int primal_check_feas(double tol_bnd)
+    {
+        for (int i = 1; i <= m; i++) {
+            int k = head[i];
+            if (coef[k] < 0.0) {
+                double eps = tol_bnd * (1.0 + 0.10 * std::fabs(lb[k]));
+                if (bbar[i] < lb[k] - eps) return 1;
+            } else if (coef[k] > 0.0) {
+                double eps = tol_bnd * (1.0 + 0.10 * std::fabs(ub[k]));
+                if (bbar[i] > ub[k] + eps) return 1;
+            }
+        }
+        return 0;
+    }
+    int primal_chuzc(double tol_dj)                       // glpspx01.js:646
+    {
+        down(gamma, E->gamma, n);
+        sync();
+        int q = 0;
+        double best = 0.0;
+        for (int j = 1; j <= n; j++) {
+            double dj = cbar[j];
+            switch (stat[j]) {
+            case NL: if (dj >= -tol_dj) continue; break;
+            case NU: if (dj <= +tol_dj) continue; break;
+            case NF: if (-tol_dj <= dj && dj <= +tol_dj) continue; break;
+            default: continue;
+            }
+            double temp = (dj * dj) / gamma[j];
+            if (best < temp) { q = j; best = temp; }
+        }
+        return q;
+    }
+    double eval_obj()                                     // glpspx01.js:1524
+    {
+        double sum = obj[0];
+        for (int i = 1; i <= m; i++) {
+            int k = head[i];
+            if (k > m) sum += obj[k - m] * bbar[i];
+        }
+        for (int j = 1; j <= n; j++) {
+            int k = head[m + j];
+            if (k > m) sum += obj[k - m] * get_xN(j);
+        }
+        return sum;
+    }
+    void store_sol(int p_stat, int d_stat, int ray)         // glpspx01.js:1591
+    {
+        pull();
+        lp->valid = 1;
+        f->valid = 1;
+        for (int i = 1; i <= m; i++) lp->head[i] = head[i];
+        lp->pbs_stat = p_stat;
+        lp->dbs_stat = d_stat;
+        lp->obj_val = eval_obj();
+        lp->it_cnt = hs.it_cnt;
+        lp->some = ray;
+        for (int i = 1; i <= m; i++) {
+            int k = head[i];
+            if (k <= m) {
+                lp->row_stat[k] = BS;
+                if (lp->row_bind) lp->row_bind[k] = i;
+                lp->row_prim[k] = bbar[i] / lp->rii[k];
+                lp->row_dual[k] = 0.0;
+            } else {
+                int c = k - m;
+                lp->col_stat[c] = BS;
+                if (lp->col_bind) lp->col_bind[c] = i;
+                lp->col_prim[c] = bbar[i] * lp->sjj[c];
+                lp->col_dual[c] = 0.0;
+            }
+        }
+        for (int j = 1; j <= n; j++) {
+            int k = head[m + j];
+            if (k <= m) {
+                lp->row_stat[k] = stat[j];
+                if (lp->row_bind) lp->row_bind[k] = 0;
+                switch (stat[j]) {
+                case NL: lp->row_prim[k] = lp->row_lb[k]; break;
+                case NU: lp->row_prim[k] = lp->row_ub[k]; break;
+                case NF: lp->row_prim[k] = 0.0; break;
+                default: lp->row_prim[k] = lp->row_lb[k]; break;
+                }
+                lp->row_dual[k] = (cbar[j] * lp->rii[k]) / zeta;
+            } else {
+                int c = k - m;
+                lp->col_stat[c] = stat[j];
+                if (lp->col_bind) lp->col_bind[c] = 0;
+                switch (stat[j]) {
+                case NL: lp->col_prim[c] = lp->col_lb[c]; break;
+                case NU: lp->col_prim[c] = lp->col_ub[c]; break;
+                case NF: lp->col_prim[c] = 0.0; break;
+                default: lp->col_prim[c] = lp->col_lb[c]; break;
+                }
+                lp->col_dual[c] = (cbar[j] / lp->sjj[c]) / zeta;
+            }
+        }
+    }
+    int fail_return()
+    {
+        pull();
+        lp->valid = 0;
+        f->valid = 0;
+        lp->pbs_stat = lp->dbs_stat = 1;   // GLP_UNDEF
+        lp->obj_val = 0.0;
+        lp->it_cnt = hs.it_cnt;
+        lp->some = 0;
+        return 5;                          // GLP_EFAIL
+    }
+
+    void init();
+    int run_dual();
+    int run_primal();
+    int batch(int K, int rigorous);
+};
+
+__global__ void k_rsub_plain(double *y, const double *a, int n)
+{
+    int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) y[i] = a[i] - y[i];
+}
+
+void Spx::rsub_into(double *y, const double *a)
+{
+    hipLaunchKernelGGL(k_rsub_plain, dim3((m + 255) / 256), dim3(256), 0, s, y, a, m);
+}
+
+__global__ void k_gather_csc_sel(int k, const int *colJ, const int *cptr, const int *crow, const double *cval,
+                                 const int *rowmap, double *C, double *BS, int ms, double sign)
+{
+    const int b = blockIdx.x;
+    const int c = colJ[b] - 1;
+    for (int t = cptr[c] + threadIdx.x; t < cptr[c + 1]; t += blockDim.x) {
+        const int r = crow[t];
+        const int a = rowmap[r];
+        const double v = sign * cval[t];
+        if (a >= 0) C[(size_t)a + (size_t)b * k] = v;
+        else BS[(size_t)(-a - 1) + (size_t)b * ms] = v;
+    }
+}
+
+void gather_csc_sel(hipStream_t s, int k, const int *colJ, const int *cptr, const int *crow, const double *cval,
+                    const int *rowmap, double *C, double *BS, int ms, double sign)
+{
+    if (k <= 0) return;
+    hipLaunchKernelGGL(k_gather_csc_sel, dim3(k), dim3(64), 0, s, k, colJ, cptr, crow, cval, rowmap, C, BS, ms, sign);
+}
+
+int Spx::reinvert_core_csc(const BasisSplit &bs)
+{
+    // structural basis columns are -A columns of the device CSC
+    return reinvert_core(f, bs, nullptr, 1, -1.0, E->cptr.p, E->cind.p, E->cval.p);
+}
+
+void Spx::init()
+{
+    const gk_lp *L = lp;
+    m = L->m; n = L->n;
+    s = ctx->stream;
+    const size_t mn = (size_t)m + n + 1;
+    type.assign(mn, 0); orig_type.assign(mn, 0); lb.assign(mn, 0.0); ub.assign(mn, 0.0); coef.assign(mn, 0.0);
+    orig_lb.assign(mn, 0.0); orig_ub.assign(mn, 0.0); obj.assign(n + 1, 0.0);
+    head.assign(mn, 0); bind.assign(mn, 0); stat.assign(n + 1, 0);
+    bbar.assign(m + 1, 0.0); cbar.assign(n + 1, 0.0); gamma.assign(std::max(m, n) + 1, 0.0);
+    // init_csa (glpspx01.js:42-145 / glpspx02.js:89-190)
+    for (int i = 1; i <= m; i++) {
+        type[i] = L->row_type[i];
+        lb[i] = L->row_lb[i] * L->rii[i];
+        ub[i] = L->row_ub[i] * L->rii[i];
+        coef[i] = 0.0;
+    }
+    for (int j = 1; j <= n; j++) {
+        type[m + j] = L->col_type[j];
+        lb[m + j] = L->col_lb[j] / L->sjj[j];
+        ub[m + j] = L->col_ub[j] / L->sjj[j];
+        coef[m + j] = L->col_coef[j] * L->sjj[j];
+    }
+    orig_type = type; orig_lb = lb; orig_ub = ub;
+    obj[0] = L->c0;
+    for (int j = 1; j <= n; j++) obj[j] = coef[m + j];
+    double cmax = 0.0;
+    for (int j = 1; j <= n; j++)
+        if (cmax < std::fabs(obj[j])) cmax = std::fabs(obj[j]);
+    if (cmax == 0.0) cmax = 1.0;
+    ABI_REQUIRE(L->dir == 1 || L->dir == 2, "gk_spx: dir = %d; invalid", L->dir);
+    zeta = (L->dir == 1 ? +1.0 : -1.0) / cmax;
+    if (std::fabs(zeta) < 1.0) zeta *= 1000.0;
+    if (dual)
+        for (int j = 1; j <= n; j++) coef[m + j] *= zeta;
+    for (int i = 1; i <= m; i++) {
+        head[i] = L->head[i];
+        ABI_REQUIRE(1 <= head[i] && head[i] <= m + n, "gk_spx: head[%d] = %d; out of range", i, head[i]);
+    }
+    int k = 0;
+    for (int i = 1; i <= m; i++)
+        if (L->row_stat[i] != BS) {
+            k++;
+            ABI_REQUIRE(k <= n, "gk_spx: too many non-basic variables");
+            head[m + k] = i;
+            stat[k] = L->row_stat[i];
+        }
+    for (int j = 1; j <= n; j++)
+        if (L->col_stat[j] != BS) {
+            k++;
+            ABI_REQUIRE(k <= n, "gk_spx: too many non-basic variables");
+            head[m + k] = m + j;
+            stat[k] = L->col_stat[j];
+        }
+    ABI_REQUIRE(k == n, "gk_spx: basis header inconsistent with statuses (%d non-basic, n = %d)", k, n);
+    for (int kk = 1; kk <= m + n; kk++) bind[head[kk]] = kk;
+    engine_alloc(*E, m, n);
+    up(E->type, type, mn - 1); up(E->orig_type, orig_type, mn - 1);
+    up(E->lb, lb, mn - 1); up(E->ub, ub, mn - 1); up(E->orig_lb, orig_lb, mn - 1); up(E->orig_ub, orig_ub, mn - 1);
+    up(E->coef, coef, mn - 1); up(E->obj, obj, n);
+    up(E->head, head, mn - 1); up(E->bind, bind, mn - 1); up(E->stat, stat, n);
+    hs = DState{};
+    hs.phase = 0;
+    hs.it_cnt = L->it_cnt;
+    hs.zeta = zeta;
+    hs.tol_bnd = parm->tol_bnd; hs.tol_dj = parm->tol_dj; hs.tol_piv = parm->tol_piv;
+    hs.obj_ll = parm->obj_ll; hs.obj_ul = parm->obj_ul;
+    hs.pricing = parm->pricing; hs.rtest = parm->r_test;
+    int lim = f->parm.nfs_max > 0 ? f->parm.nfs_max : 100;
+    // the dense inverse tolerates more product-form updates than the FT
+    // eta file; re-inversion cost grows with k^3, so scale the interval
+    lim = std::max(lim, std::min(1000, m / 4));
+    hs.upd_lim = lim;
+    hs.refct = 0;
+    it_beg = L->it_cnt;
+    tm_beg = now_s();
+    push_state();
+    sync();
+}
+
+int Spx::batch(int K, int rigorous)
+{
+    hs.stop = ST_RUN;
+    hs.iter_left = K;
+    hs.npiv = 0;
+    hs.phase = phase;
+    hs.rigorous = rigorous;
+    push_state();
+    SpxDev d = dev();
+    const int pse = (parm->pricing == PT_PSE);
+    for (int t = 0; t < K; t++) {
+        if (dual) dual_iteration(s, d, pse, rigorous);
+        else primal_iteration(s, d, pse, rigorous);
+    }
+    pull_state();
+    f->stats.batches++;
+    f->stats.pivots += hs.npiv;
+    if (hs.npiv > 0) head_stale = vec_stale = true;
+    // a stop on the budget leaves the top kernel of the next iteration unrun
+    return hs.stop == ST_RUN ? ST_BATCH : hs.stop;
+}
+
+static int batch_size(int m, int n)
+{
+    double work = (double)m * (double)m + 2.0 * (double)m * (double)n;
+    if (work > 5e7) return 8;
+    if (work > 5e6) return 32;
+    return 64;
+}
+
+int Spx::run_dual()
+{
+    const gk_smcp *P = parm;
+    int binv_st = f->valid ? 2 : 0, bbar_st = 0, cbar_st = 0, rigorous = 0;
+    int ret;
+    for (;;) {
+        if (binv_st == 0) {
+            if (!reinvert()) return fail_return();
+            binv_st = 1;
+            bbar_st = cbar_st = 0;
+            hs.upd_cnt = 0; hs.refact_pending = 0;
+        }
+        hs.binv_fresh = (binv_st == 1);
+        if (cbar_st == 0) {
+            pull();
+            eval_cbar();
+            cbar_st = 1;
+            if (phase == 0) {
+                if (dual_check_feas(0.90 * P->tol_dj) != 0) { phase = 1; set_aux_bnds(); }
+                else { phase = 2; set_orig_bnds(); }
+                ABI_REQUIRE(dual_check_stab(P->tol_dj) == 0, "spx_dual: check_stab after phase selection");
+                hs.refct = 0;
+                bbar_st = 0;
+            }
+            if (dual_check_stab(P->tol_dj) != 0) {
+                if (P->meth == 2) {            // GLP_DUALP
+                    store_sol(1, 1, 0);
+                    return 5;
+                }
+                phase = 0;
+                binv_st = 0;
+                rigorous = 5;
+                continue;
+            }
+        }
+        if (phase == 1) {
+            pull();
+            if (dual_check_feas(P->tol_dj) == 0) {
+                phase = 2;
+                if (cbar_st != 1) { eval_cbar(); cbar_st = 1; }
+                set_orig_bnds();
+                hs.refct = 0;
+                bbar_st = 0;
+            }
+        }
+        if (bbar_st == 0) {
+            pull();
+            eval_bbar();
+            if (phase == 2) hs.obj = eval_obj();
+            bbar_st = 1;
+        }
+        hs.cbar_fresh = (cbar_st == 1);
+        if (phase == 2 && zeta < 0.0 && P->obj_ll > -DBL_MAX && hs.obj <= P->obj_ll) {
+            if (bbar_st != 1 || cbar_st != 1) {
+                if (bbar_st != 1) bbar_st = 0;
+                if (cbar_st != 1) cbar_st = 0;
+                continue;
+            }
+            store_sol(3, 2, 0);
+            return 6;                                  // GLP_EOBJLL
+        }
+        if (phase == 2 && zeta > 0.0 && P->obj_ul < +DBL_MAX && hs.obj >= P->obj_ul) {
+            if (bbar_st != 1 || cbar_st != 1) {
+                if (bbar_st != 1) bbar_st = 0;
+                if (cbar_st != 1) cbar_st = 0;
+                continue;
+            }
+            store_sol(3, 2, 0);
+            return 7;                                  // GLP_EOBJUL
+        }
+        {
+            bool it_hit = P->it_lim < 0x7fffffff && hs.it_cnt - it_beg >= P->it_lim;
+            bool tm_hit = !it_hit && P->tm_lim < 0x7fffffff && 1000.0 * (now_s() - tm_beg) >= P->tm_lim;
+            if (it_hit || tm_hit) {
+                if ((phase == 2 && bbar_st != 1) || cbar_st != 1) {
+                    if (phase == 2 && bbar_st != 1) bbar_st = 0;
+                    if (cbar_st != 1) cbar_st = 0;
+                    continue;
+                }
+                int d_stat;
+                if (phase == 1) {
+                    pull();
+                    d_stat = 3;
+                    set_orig_bnds();
+                    eval_bbar();
+                } else
+                    d_stat = 2;
+                store_sol(3, d_stat, 0);
+                return it_hit ? 8 : 9;
+            }
+        }
+        int K = rigorous ? 1 : batch_size(m, n);
+        if (P->it_lim < 0x7fffffff) K = std::max(1, std::min(K, P->it_lim - (hs.it_cnt - it_beg)));
+        int why = batch(K, rigorous);
+        if (hs.npiv > 0) {
+            bbar_st = 2;
+            cbar_st = 2;
+            binv_st = 2;
+            rigorous = hs.rigorous;
+        }
+        switch (why) {
+        case ST_BATCH:
+        case ST_PHASE:
+        case ST_OBJLIM:
+            break;
+        case ST_REFACT:
+            binv_st = 0;
+            break;
+        case ST_P0:
+            if (bbar_st != 1 || cbar_st != 1) {
+                if (bbar_st != 1) bbar_st = 0;
+                if (cbar_st != 1) cbar_st = 0;
+                break;
+            }
+            {
+                int p_stat, d_stat;
+                if (phase == 1) {
+                    pull();
+                    set_orig_bnds();
+                    eval_bbar();
+                    p_stat = 3; d_stat = 4;
+                } else
+                    p_stat = d_stat = 2;
+                store_sol(p_stat, d_stat, 0);
+            }
+            return 0;
+        case ST_Q0:
+            if (bbar_st != 1 || cbar_st != 1 || !rigorous) {
+                if (bbar_st != 1) bbar_st = 0;
+                if (cbar_st != 1) cbar_st = 0;
+                rigorous = 1;
+                break;
+            }
+            if (phase == 1) return fail_return();
+            pull();
+            store_sol(4, 2, head[hs.p]);
+            return 0;
+        case ST_SMALLPIV:
+            rigorous = 5;
+            break;
+        case ST_PIVCHK:
+            if (binv_st != 1) binv_st = 0;
+            rigorous = 5;
+            break;
+        default:
+            throw AbiError{"spx_dual: unexpected device stop code"};
+        }
+        (void)ret;
+    }
+}
+
+int Spx::run_primal()
+{
+    const gk_smcp *P = parm;
+    int binv_st = f->valid ? 2 : 0, bbar_st = 0, cbar_st = 0, rigorous = 0;
+    for (;;) {
+        if (binv_st == 0) {
+            if (!reinvert()) return fail_return();
+            binv_st = 1;
+            bbar_st = cbar_st = 0;
+            hs.upd_cnt = 0; hs.refact_pending = 0;
+        }
+        hs.binv_fresh = (binv_st == 1);
+        if (bbar_st == 0) {
+            pull();
+            eval_bbar();
+            bbar_st = 1;
+            if (phase == 0) {
+                if (set_aux_obj(P->tol_bnd) > 0) phase = 1;
+                else { set_orig_obj(); phase = 2; }
+                ABI_REQUIRE(primal_check_stab(P->tol_bnd) == 0, "spx_primal: check_stab after phase selection");
+                cbar_st = 0;
+            }
+            if (primal_check_stab(P->tol_bnd)) {
+                phase = 0;
+                binv_st = 0;
+                rigorous = 5;
+                continue;
+            }
+        }
+        if (phase == 1) {
+            pull();
+            if (!primal_check_feas(P->tol_bnd)) {
+                phase = 2;
+                set_orig_obj();
+                cbar_st = 0;
+            }
+        }
+        if (cbar_st == 0) {
+            pull();
+            eval_cbar();
+            cbar_st = 1;
+        }
+        hs.cbar_fresh = (cbar_st == 1);
+        {
+            bool it_hit = P->it_lim < 0x7fffffff && hs.it_cnt - it_beg >= P->it_lim;
+            bool tm_hit = !it_hit && P->tm_lim < 0x7fffffff && 1000.0 * (now_s() - tm_beg) >= P->tm_lim;
+            if (it_hit || tm_hit) {
+                if (bbar_st != 1 || (phase == 2 && cbar_st != 1)) {
+                    if (bbar_st != 1) bbar_st = 0;
+                    if (phase == 2 && cbar_st != 1) cbar_st = 0;
+                    continue;
+                }
+                int p_stat;
+                pull();
+                if (phase == 1) {
+                    p_stat = 3;
+                    set_orig_obj();
+                    eval_cbar();
+                } else
+                    p_stat = 2;
+                int q = primal_chuzc(P->tol_dj);
+                store_sol(p_stat, q == 0 ? 2 : 3, 0);
+                return it_hit ? 8 : 9;
+            }
+        }
+        int K = rigorous ? 1 : batch_size(m, n);
+        if (P->it_lim < 0x7fffffff) K = std::max(1, std::min(K, P->it_lim - (hs.it_cnt - it_beg)));
+        int why = batch(K, rigorous);
+        if (hs.npiv > 0) {
+            bbar_st = 2;
+            rigorous = hs.rigorous;
+            // cbar and the factor change only on basis changes; the device keeps
+            // their freshness flags, mirror them here
+            if (!hs.cbar_fresh) cbar_st = 2;
+            if (!hs.binv_fresh) binv_st = 2;
+        }
+        switch (why) {
+        case ST_BATCH:
+        case ST_PHASE:
+            break;
+        case ST_REFACT:
+            binv_st = 0;
+            break;
+        case ST_Q0:
+            if (bbar_st != 1 || cbar_st != 1) {
+                if (bbar_st != 1) bbar_st = 0;
+                if (cbar_st != 1) cbar_st = 0;
+                break;
+            }
+            {
+                int p_stat, d_stat;
+                pull();
+                if (phase == 1) {
+                    p_stat = 4;
+                    set_orig_obj();
+                    eval_cbar();
+                    int q = primal_chuzc(P->tol_dj);
+                    d_stat = (q == 0 ? 2 : 3);
+                } else
+                    p_stat = d_stat = 2;
+                store_sol(p_stat, d_stat, 0);
+            }
+            return 0;
+        case ST_DCHK:
+            if (cbar_st != 1) cbar_st = 0;
+            rigorous = 5;
+            break;
+        case ST_P0:
+            if (bbar_st != 1 || cbar_st != 1 || !rigorous) {
+                if (bbar_st != 1) bbar_st = 0;
+                if (cbar_st != 1) cbar_st = 0;
+                rigorous = 1;
+                break;
+            }
+            if (phase == 1) return fail_return();
+            pull();
+            store_sol(2, 4, head[m + hs.q]);
+            return 0;
+        case ST_SMALLPIV:
+            rigorous = 5;
+            break;
+        case ST_PIVCHK:
+            if (binv_st != 1) binv_st = 0;
+            rigorous = 5;
+            break;
+        default:
+            throw AbiError{"spx_primal: unexpected device stop code"};
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// C-ABI
+// ---------------------------------------------------------------------------
+extern "C" {
+
+int gk_abi_version(void) { return GK_ABI_VERSION; }
+
+const char *gk_last_error(void) { return g_err.c_str(); }
+
+int gk_device_count(void)
+{
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+    return n;
+}
+
+gk_ctx *gk_ctx_create(int device)
+{
+    try {
+        int cnt = 0;
+        HIPCHK(hipGetDeviceCount(&cnt));
+        ABI_REQUIRE(device >= 0 && device < cnt, "gk_ctx_create: device %d of %d", device, cnt);
+        hipDeviceProp_t prop;
+        HIPCHK(hipGetDeviceProperties(&prop, device));
+        ABI_REQUIRE(std::strncmp(prop.gcnArchName, "gfx950", 6) == 0,
+                    "gk_ctx_create: device %d is %s; this build targets gfx950 (MI355X) only", device, prop.gcnArchName);
+        HIPCHK(hipSetDevice(device));
+        gk_ctx *c = new gk_ctx;
+        c->device = device;
+        HIPCHK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+        return c;
+    } catch (const AbiError &e) {
+        g_err = e.msg;
+        return nullptr;
+    }
+}
+
+void gk_ctx_destroy(gk_ctx *ctx)
+{
+    if (!ctx) return;
+    (void)hipSetDevice(ctx->device);
+    if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
+    delete ctx;
+}
+
+gk_bfd *gk_bfd_create(gk_ctx *ctx)
+{
+    if (!ctx) { set_err("gk_bfd_create: null context"); return nullptr; }
+    gk_bfd *f = new gk_bfd;
+    f->ctx = ctx;
+    // glp_get_bfcp defaults (glpapi12.js:111-121)
+    f->parm.type = 1; f->parm.lu_size = 0; f->parm.piv_tol = 0.10; f->parm.piv_lim = 4; f->parm.suhl = 1;
+    f->parm.eps_tol = 1e-15; f->parm.max_gro = 1e10; f->parm.nfs_max = 100; f->parm.upd_tol = 1e-6;
+    f->parm.nrs_max = 100; f->parm.rs_size = 0;
+    return f;
+}
+
+void gk_bfd_destroy(gk_bfd *f)
+{
+    if (!f) return;
+    (void)hipSetDevice(f->ctx->device);
+    delete f->eng;
+    f->Binv.release(); f->C.release(); f->X.release(); f->Y.release(); f->CinvR.release(); f->BS.release();
+    f->G.release(); f->vecx.release(); f->vecy.release(); f->partial.release(); f->idx_i.release();
+    f->piv_step.release(); f->piv.release(); f->flag.release(); f->bptr.release(); f->brow.release(); f->bval.release();
+    delete f;
+}
+
+void gk_bfd_set_parm(gk_bfd *f, const gk_bfcp *parm)
+{
+    if (f && parm) f->parm = *parm;
+}
+
+int gk_bfd_valid(const gk_bfd *f) { return f ? f->valid : 0; }
+
+int gk_bfd_get_count(const gk_bfd *f)
+{
+    if (!f || !f->valid) { set_err("bfd_get_count: factorization is not valid"); return GK_EABI; }
+    return f->upd_cnt;
+}
+
+void gk_bfd_last_stats(const gk_bfd *f, gk_spx_stats *st)
+{
+    if (f && st) *st = f->stats;
+}
+
+static void bfd_prepare(gk_bfd *f, int m)
+{
+    HIPCHK(hipSetDevice(f->ctx->device));
+    if (f->m != m) {
+        f->m = m;
+        f->ldb = (m + 7) & ~7;
+        f->valid = 0;
+    }
+}
+
+int gk_bfd_factorize_csc(gk_bfd *f, int m, const int *ptr, const int *ind, const double *val)
+{
+    try {
+        ABI_REQUIRE(f && m >= 1, "bfd_factorize: m = %d; invalid parameter", m);
+        bfd_prepare(f, m);
+        f->valid = 0;
+        hipStream_t s = f->ctx->stream;
+        // classify unit columns (+1 on a single row) as slack-like
+        BasisSplit bs;
+        std::vector<int> srow_pos(m + 1, 0), cptr(m + 1), crow, colJ_all;
+        std::vector<double> cval;
+        std::vector<char> isslack(m + 1, 0);
+        for (int j = 1; j <= m; j++) {
+            int len = ptr[j + 1] - ptr[j];
+            ABI_REQUIRE(0 <= len && len <= m, "luf_factorize: j = %d; len = %d; invalid column length", j, len);
+            if (len == 1 && val[ptr[j]] == 1.0 && !srow_pos[ind[ptr[j]]]) {
+                int r = ind[ptr[j]];
+                ABI_REQUIRE(1 <= r && r <= m, "luf_factorize: i = %d; j = %d; invalid row index", r, j);
+                srow_pos[r] = j;
+                isslack[j] = 1;
+            }
+        }
+        int t = 0;
+        for (int j = 1; j <= m; j++) {
+            cptr[j - 1] = t;
+            std::vector<char> seen;
+            for (int p = ptr[j]; p < ptr[j + 1]; p++) {
+                int r = ind[p];
+                ABI_REQUIRE(1 <= r && r <= m, "luf_factorize: i = %d; j = %d; invalid row index", r, j);
+                ABI_REQUIRE(val[p] != 0.0, "luf_factorize: i = %d; j = %d; zero element not allowed", r, j);
+                crow.push_back(r - 1);
+                cval.push_back(val[p]);
+                t++;
+            }
+            if (!isslack[j]) { bs.posJ.push_back(j); bs.colJ.push_back(j); }
+        }
+        cptr[m] = t;
+        bs.rowmap.assign(m, 0);
+        for (int r = 1; r <= m; r++) {
+            if (srow_pos[r]) {
+                bs.rowmap[r - 1] = -(int)(bs.rowS.size() + 1);
+                bs.rowS.push_back(r);
+                bs.posS.push_back(srow_pos[r]);
+            } else {
+                bs.rowmap[r - 1] = (int)bs.rowR.size();
+                bs.rowR.push_back(r);
+            }
+        }
+        bs.k = (int)bs.posJ.size();
+        bs.ms = (int)bs.rowS.size();
+        ABI_REQUIRE(bs.k == (int)bs.rowR.size(), "bfd_factorize: basis classification failed");
+        f->bptr.ensure(m + 1);
+        f->brow.ensure(std::max(t, 1));
+        f->bval.ensure(std::max(t, 1));
+        HIPCHK(hipMemcpyAsync(f->bptr.p, cptr.data(), (m + 1) * sizeof(int), hipMemcpyHostToDevice, s));
+        if (t) {
+            HIPCHK(hipMemcpyAsync(f->brow.p, crow.data(), t * sizeof(int), hipMemcpyHostToDevice, s));
+            HIPCHK(hipMemcpyAsync(f->bval.p, cval.data(), t * sizeof(double), hipMemcpyHostToDevice, s));
+        }
+        int ret = reinvert_core(f, bs, nullptr, 1, 1.0, f->bptr.p, f->brow.p, f->bval.p);
+        return ret ? 1 : 0;   // BFD_ESING
+    } catch (const AbiError &e) {
+        g_err = e.msg;
+        return GK_EABI;
+    }
+}
+
+int gk_bfd_factorize(gk_bfd *f, int m, gk_col_fn col, void *info)
+{
+    try {
+        ABI_REQUIRE(f && m >= 1 && col, "bfd_factorize: m = %d; invalid parameter", m);
+        std::vector<int> ptr(m + 2), ind(1), tind(m + 1);
+        std::vector<double> val(1), tval(m + 1);
+        ptr[1] = 1;
+        ind.reserve((size_t)4 * m + 1);
+        val.reserve((size_t)4 * m + 1);
+        for (int j = 1; j <= m; j++) {
+            int len = col(info, j, tind.data(), tval.data());
+            ABI_REQUIRE(0 <= len && len <= m, "luf_factorize: j = %d; len = %d; invalid column length", j, len);
+            for (int t = 1; t <= len; t++) { ind.push_back(tind[t]); val.push_back(tval[t]); }
+            ptr[j + 1] = ptr[j] + len;
+        }
+        return gk_bfd_factorize_csc(f, m, ptr.data(), ind.data(), val.data());
+    } catch (const AbiError &e) {
+        g_err = e.msg;
+        return GK_EABI;
+    }
+}
+
+static void bfd_solve(gk_bfd *f, double *x, int tr)
+{
+    ABI_REQUIRE(f && f->valid, "bfd_%stran: factorization is not valid", tr ? "b" : "f");
+    HIPCHK(hipSetDevice(f->ctx->device));
+    hipStream_t s = f->ctx->stream;
+    const int m = f->m;
+    f->vecx.ensure(m);
+    f->vecy.ensure(m);
+    f->partial.ensure(PARTIAL_CAP);
+    HIPCHK(hipMemcpyAsync(f->vecx.p, x + 1, m * sizeof(double), hipMemcpyHostToDevice, s));
+    if (tr) gemv_t(s, f->Binv.p, m, m, f->ldb, f->vecx.p, f->vecy.p, 1.0);
+    else gemv_n(s, f->Binv.p, m, m, f->ldb, f->vecx.p, f->partial.p, PARTIAL_CAP, f->vecy.p, 1.0, nullptr, 0.0);
+    HIPCHK(hipMemcpyAsync(x + 1, f->vecy.p, m * sizeof(double), hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+}
+
+void gk_bfd_ftran(gk_bfd *f, double *x)
+{
+    try { bfd_solve(f, x, 0); } catch (const AbiError &e) { g_err = e.msg; }
+}
+
+void gk_bfd_btran(gk_bfd *f, double *x)
+{
+    try { bfd_solve(f, x, 1); } catch (const AbiError &e) { g_err = e.msg; }
+}
+
+int gk_bfd_update(gk_bfd *f, int j, int len, const int *ind, int idx, const double *val)
+{
+    try {
+        ABI_REQUIRE(f && f->valid, "bfd_update_it: factorization is not valid");
+        const int m = f->m;
+        ABI_REQUIRE(1 <= j && j <= m, "fhv_update_it: j = %d; column number out of range", j);
+        if (f->upd_cnt >= (f->parm.nfs_max > 0 ? f->parm.nfs_max : 100)) { f->valid = 0; return 4; }  // BFD_ELIMIT
+        HIPCHK(hipSetDevice(f->ctx->device));
+        hipStream_t s = f->ctx->stream;
+        std::vector<double> a(m + 1, 0.0);
+        for (int k = 1; k <= len; k++) {
+            int i = ind[idx + k];
+            ABI_REQUIRE(1 <= i && i <= m, "fhv_update_it: ind[%d] = %d; row number out of range", k, i);
+            ABI_REQUIRE(a[i] == 0.0, "fhv_update_it: ind[%d] = %d; duplicate row index not allowed", k, i);
+            ABI_REQUIRE(val[k] != 0.0, "fhv_update_it: val[%d] = 0; zero element not allowed", k);
+            a[i] = val[k];
+        }
+        f->vecx.ensure(m);
+        f->vecy.ensure(m);
+        f->G.ensure(m);
+        f->partial.ensure(PARTIAL_CAP);
+        HIPCHK(hipMemcpyAsync(f->vecx.p, a.data() + 1, m * sizeof(double), hipMemcpyHostToDevice, s));
+        // t = -inv(B) a (the tcol convention of the rank-1 kernel)
+        gemv_n(s, f->Binv.p, m, m, f->ldb, f->vecx.p, f->partial.p, PARTIAL_CAP, f->vecy.p, -1.0, nullptr, 0.0);
+        std::vector<double> t(m + 1);
+        HIPCHK(hipMemcpyAsync(t.data() + 1, f->vecy.p, m * sizeof(double), hipMemcpyDeviceToHost, s));
+        HIPCHK(hipStreamSynchronize(s));
+        double big = 0.0;
+        for (int i = 1; i <= m; i++) big = std::max(big, std::fabs(t[i]));
+        if (t[j] == 0.0) { f->valid = 0; return 1; }                                  // BFD_ESING
+        if (std::fabs(t[j]) < f->parm.upd_tol * big) { f->valid = 0; return 3; }      // BFD_ECHECK
+        gather_row(s, f->Binv.p, f->ldb, m, j, f->G.p);
+        binv_rank1(s, f->Binv.p, m, f->ldb, f->G.p, f->vecy.p, j);
+        HIPCHK(hipStreamSynchronize(s));
+        f->upd_cnt++;
+        return 0;
+    } catch (const AbiError &e) {
+        g_err = e.msg;
+        return GK_EABI;
+    }
+}
+
+static int spx_entry(gk_ctx *ctx, gk_lp *lp, gk_bfd *f, const gk_smcp *parm, int dual)
+{
+    try {
+        ABI_REQUIRE(ctx && lp && f && parm, "gk_spx: null argument");
+        ABI_REQUIRE(lp->m > 0 && lp->n > 0, "spx: m = %d, n = %d; invalid dimensions", lp->m, lp->n);
+        ABI_REQUIRE(lp->m <= 65535, "spx: m = %d exceeds this build's grid limit 65535", lp->m);
+        HIPCHK(hipSetDevice(ctx->device));
+        f->ctx = ctx;
+        const double t0 = now_s();
+        f->stats = gk_spx_stats{};
+        bfd_prepare(f, lp->m);
+        if (!f->eng) f->eng = new Engine;
+        engine_upload_matrix(f, lp);
+        Spx S;
+        S.ctx = ctx; S.f = f; S.E = f->eng; S.lp = lp; S.parm = parm; S.dual = dual;
+        S.init();
+        lp->valid = 0;
+        int ret = dual ? S.run_dual() : S.run_primal();
+        f->upd_cnt = S.hs.upd_cnt;
+        f->stats.seconds_total = now_s() - t0;
+        return ret;
+    } catch (const AbiError &e) {
+        g_err = e.msg;
+        return GK_EABI;
+    }
+}
+
+int gk_spx_primal(gk_ctx *ctx, gk_lp *lp, gk_bfd *bfd, const gk_smcp *parm) { return spx_entry(ctx, lp, bfd, parm, 0); }
+
+int gk_spx_dual(gk_ctx *ctx, gk_lp *lp, gk_bfd *bfd, const gk_smcp *parm) { return spx_entry(ctx, lp, bfd, parm, 1); }
+
+}  // extern "C"
+
+// placeholder until the native branch-and-bound driver lands (gk_ios.hip)
+extern "C" __attribute__((weak)) int gk_ios_driver(gk_ctx *, gk_mip *, const gk_iocp *)
+{
+    set_err("gk_ios_driver: not available in this build");
+    return GK_EABI;
+}

@@ -1,0 +1,144 @@
+// Internal interfaces of libglpk_mi355x: device state layout, kernel
+// launchers (gk_kernels.hip) and the engine structures (gk_engine.hip).
+//
+// Device layout (all 0-based in HBM; the reference's 1-based variable
+// numbers k = 1..m+n are kept as *values* in head[]):
+//   type/lb/ub/coef[k-1]            working bounds and objective, scaled as init_csa
+//   head[pos-1] = k                 basis header, pos 1..m basic, m+1..m+n non-basic
+//   bind[k-1]   = pos               inverse of head
+//   stat[j-1]                       status of non-basic xN[j]
+//   bbar[i-1], cbar[j-1]            values of basic variables / reduced costs
+//   gamma[]                         steepest-edge weights (m for dual, n for primal)
+//   A                               dense column-major (lda) or CSC + CSR copies
+//   Binv[(i-1) + (r-1)*ldb]         explicit inverse of the basis matrix:
+//                                   row i = basis position, column r = row of (I|-A)
+#pragma once
+#include <hip/hip_runtime.h>
+#include <cstdint>
+#include <cstddef>
+
+namespace gk {
+
+enum : int {  // GLP_* (glpk.js:7-141)
+    FR = 1, LO = 2, UP = 3, DB = 4, FX = 5,
+    BS = 1, NL = 2, NU = 3, NF = 4, NS = 5,
+    PT_STD = 0x11, PT_PSE = 0x22, RT_STD = 0x11, RT_HAR = 0x22,
+};
+
+// why a device batch of pivots stopped (the reference main-loop branch the
+// host resumes at; glpspx02.js:1614-1966, glpspx01.js:1705-2056)
+enum : int {
+    ST_RUN = 0,
+    ST_BATCH = 1,     // iteration budget of the batch used up
+    ST_PHASE = 2,     // phase I reached feasibility: switch to phase II
+    ST_OBJLIM = 3,    // obj_ll / obj_ul reached (dual, phase II)
+    ST_P0 = 4,        // no basic variable chosen (dual: optimal / primal: unbounded ray)
+    ST_Q0 = 5,        // no non-basic variable chosen
+    ST_SMALLPIV = 6,  // pivot below 1e-5 (1 + 0.01 max) and not in rigorous mode
+    ST_PIVCHK = 7,    // tcol[p] and trow[q] disagree
+    ST_DCHK = 8,      // primal: cbar[q] disagrees with re-evaluated d_q
+    ST_REFACT = 9,    // update limit reached: re-invert before the next pivot
+    ST_REFSP = 10,    // PSE reference space must be reset (refct == 0)
+};
+
+struct DState {
+    int stop, p, q, p_stat;
+    int phase, it_cnt, npiv, iter_left;
+    int refct, upd_cnt, upd_lim, rigorous;
+    int binv_fresh, cbar_fresh, pricing, rtest;
+    int refact_pending, pad0, pad1, pad2;
+    double delta, teta, new_dq, cbar_q_new;
+    double gamma_pq, eta_pq, pivot, xnq;
+    double zeta, tol_bnd, tol_dj, tol_piv;
+    double obj_ll, obj_ul, obj, tcol_max;
+    unsigned long long trow_max_bits, tcol_max_bits;
+};
+
+// ---- dense GEMV helpers ---------------------------------------------------
+struct GemvPlan {
+    int rows, cols, ld;
+    int tiles, splits, cols_per_split;
+};
+GemvPlan gemv_plan(int rows, int cols, int ld);
+
+// y = beta*base + alpha * M x  (M col-major rows x cols, zero entries of x skipped)
+void gemv_n(hipStream_t s, const double *M, int rows, int cols, int ld, const double *x,
+            double *partial, size_t partial_cap, double *y, double alpha, const double *base, double beta);
+// y[l] = alpha * M[:,l] . x   for l < cols
+void gemv_t(hipStream_t s, const double *M, int rows, int cols, int ld, const double *x, double *y, double alpha);
+
+// ---- the (I | -A) column passes -------------------------------------------
+struct MatDev {
+    int m, n, nnz;
+    int dense;                    // 1: A dense column-major
+    const double *A; int lda;     // dense
+    const int *cptr, *cind; const double *cval;   // CSC, 0-based rows
+    const int *rptr, *rcol; const double *rval;   // CSR, 0-based cols
+    int lpc;                      // lanes per column for CSC passes (1, 8 or 64)
+};
+
+enum : int { CP_TROW = 0, CP_CBAR = 1, CP_RESID = 2, CP_TROW_S = 3, CP_DOT = 4 };
+// For positions pos = off+1 .. off+cnt: k = head[pos-1], N = column k of (I|-A):
+//   CP_TROW   out1[i] = -(N . x), 0 if stat[i] == NS; atomic max |out1| into *maxbits
+//   CP_CBAR   out1[i] = coef[k-1] - N . x
+//   CP_RESID  out1[i] = h[i] - N . x
+//   CP_TROW_S out1[i] = -(N . x), out2[i] = N . y  (0, 0 if NS)
+//   CP_DOT    out1[i] = N . x
+void colpass(hipStream_t s, const MatDev &A, int mode, int off, int cnt, const int *head, const signed char *stat,
+             const double *coef, const double *h, const double *x, const double *y, double *out1, double *out2,
+             unsigned long long *maxbits);
+
+// y = base - A w  over structural columns (w dense over columns, zeros skipped);
+// used for sums of (I|-A) columns (slack parts are added into base by the caller)
+void aprod_neg(hipStream_t s, const MatDev &A, const double *w, const double *base, double *y,
+               double *partial, size_t partial_cap);
+
+// scatter weights of positions off+1..off+cnt: w[pos] -> slack part ys[k-1] += w,
+// structural part wc[c-1] = w  (ys, wc must be zeroed by the caller)
+void scatter_pos(hipStream_t s, int m, int off, int cnt, const int *head, const double *w, double *ys, double *wc);
+
+// ---- simplex pivot kernels --------------------------------------------------
+struct SpxDev {
+    int m, n;
+    MatDev A;
+    signed char *type, *orig_type, *stat, *refsp;
+    double *lb, *ub, *coef, *orig_lb, *orig_ub, *obj;
+    int *head, *bind;
+    double *bbar, *cbar, *gamma;
+    double *tcol, *trow, *rho, *rowp, *u, *s, *h, *wcol, *ys, *work, *r1, *r2;
+    double *Binv; int ldb;
+    double *partial; size_t partial_cap;
+    DState *st;
+};
+
+void dual_iteration(hipStream_t s, const SpxDev &d, int pse, int rigorous);
+void primal_iteration(hipStream_t s, const SpxDev &d, int pse, int rigorous);
+void launch_reset_refsp(hipStream_t s, const SpxDev &d, int dual);
+
+// ---- factor (explicit inverse) kernels ------------------------------------------
+void binv_rank1(hipStream_t s, double *Binv, int m, int ldb, const double *rho, const double *tcol, int p);
+void fill_d(hipStream_t s, double *x, double v, size_t n);
+void set_identity(hipStream_t s, double *M, int m, int ld);
+// gather dense C = B[R, J] and S-part BS = B[S, J] of the basis into dense buffers
+void gather_basis_blocks(hipStream_t s, const MatDev &A, int m, int k, const int *colsJ, const int *rowR,
+                         double *C, double *BS, int ms, const int *rowS);
+void gather_basis_blocks_csc(hipStream_t s, int m, int k, const int *bptr, const int *bind_rows, const double *bval,
+                             const int *posJ, const int *rowR, const int *rowS, double *C, double *BS, int ms);
+// Gauss-Jordan inversion with partial pivoting of the k x k matrix in X (k x 2k,
+// [C | I] ping-pong in X/Y); returns number of steps completed (k on success)
+int gauss_jordan(hipStream_t s, double *X, double *Y, int k, int *piv_step, int *piv, int *flag, double tiny,
+                 double **result);
+void extract_inverse_rowmajor(hipStream_t s, const double *X, int k, const int *piv, double *CinvR);
+// G (ms x k, col-major) = BS (ms x k col-major) * CinvR (k x k row-major)
+void gemm_bs_cinv(hipStream_t s, const double *BS, int ms, int k, const double *CinvR, double *G, int use_mfma);
+void assemble_binv(hipStream_t s, double *Binv, int m, int ldb, int k, int ms, const int *posJ, const int *rowR,
+                   const int *posS, const int *rowS, const double *CinvR, const double *G);
+
+// basic helpers
+void vec_axpy(hipStream_t s, double *y, const double *x, double a, int n);
+void vec_copy(hipStream_t s, double *y, const double *x, int n);
+void gather_row(hipStream_t s, const double *Binv, int ldb, int m, int p, double *rho);
+void cb_vector(hipStream_t s, int m, const int *head, const double *coef, double *cB);
+void neg_xn_weights(hipStream_t s, const SpxDev &d, double *w);
+
+}  // namespace gk

@@ -1,0 +1,432 @@
+"""Host-side mirror of the reference interface for the hot path, over the C-ABI.
+
+`glp_simplex(P, SMCP(...))` and `glp_factorize(P)` follow glpapi06.js:1-340
+and glpapi12.js:5-100 (parameter checks, the double-bound check, the trivial
+LP for nnz == 0, solve_lp's factorize-then-spx flow, GLP_DUALP's fallback to
+the primal), with spx_primal / spx_dual / bfd_* executed by
+libglpk_mi355x.so on the MI355X.  There is no CPU fallback: if the library
+or a gfx950 device is missing, `Context()` raises.
+
+Arrays crossing the boundary are 1-based like the reference's typed arrays
+(element 0 unused); `Problem` (problems.py) holds them 0-based and this
+module pads them.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+import numpy as np
+
+from .problems import (GLP_BS, GLP_DB, GLP_DUAL, GLP_DUALP, GLP_FEAS, GLP_FX, GLP_LO, GLP_MAX, GLP_MIN,
+                       GLP_NF, GLP_NL, GLP_NOFEAS, GLP_NS, GLP_NU, GLP_PRIMAL, GLP_UNDEF, GLP_UP, GLP_FR,
+                       Problem)
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libglpk_mi355x.so")
+
+GLP_MSG_OFF, GLP_MSG_ERR, GLP_MSG_ON, GLP_MSG_ALL, GLP_MSG_DBG = 0, 1, 2, 3, 4
+GLP_PT_STD, GLP_PT_PSE = 0x11, 0x22
+GLP_RT_STD, GLP_RT_HAR = 0x11, 0x22
+GLP_EBADB, GLP_ESING, GLP_ECOND, GLP_EBOUND, GLP_EFAIL = 1, 2, 3, 4, 5
+INT_MAX = 0x7FFFFFFF
+DBL_MAX = np.finfo(np.float64).max
+GK_EABI = -1
+
+
+class GkError(RuntimeError):
+    """Contract violation reported by the C-ABI (the reference's xerror)."""
+
+
+class Bfcp(C.Structure):
+    _fields_ = [("type", C.c_int), ("lu_size", C.c_int), ("piv_tol", C.c_double), ("piv_lim", C.c_int),
+                ("suhl", C.c_int), ("eps_tol", C.c_double), ("max_gro", C.c_double), ("nfs_max", C.c_int),
+                ("upd_tol", C.c_double), ("nrs_max", C.c_int), ("rs_size", C.c_int)]
+
+
+class Smcp(C.Structure):
+    _fields_ = [("msg_lev", C.c_int), ("meth", C.c_int), ("pricing", C.c_int), ("r_test", C.c_int),
+                ("tol_bnd", C.c_double), ("tol_dj", C.c_double), ("tol_piv", C.c_double),
+                ("obj_ll", C.c_double), ("obj_ul", C.c_double),
+                ("it_lim", C.c_int), ("tm_lim", C.c_int), ("out_frq", C.c_int), ("out_dly", C.c_int),
+                ("presolve", C.c_int)]
+
+
+class Lp(C.Structure):
+    _fields_ = [("m", C.c_int), ("n", C.c_int), ("nnz", C.c_int), ("dir", C.c_int), ("c0", C.c_double),
+                ("row_type", C.c_void_p), ("row_lb", C.c_void_p), ("row_ub", C.c_void_p), ("rii", C.c_void_p),
+                ("col_type", C.c_void_p), ("col_lb", C.c_void_p), ("col_ub", C.c_void_p),
+                ("col_coef", C.c_void_p), ("sjj", C.c_void_p),
+                ("A_ptr", C.c_void_p), ("A_ind", C.c_void_p), ("A_val", C.c_void_p),
+                ("a_version", C.c_ulonglong),
+                ("head", C.c_void_p), ("row_stat", C.c_void_p), ("col_stat", C.c_void_p),
+                ("row_bind", C.c_void_p), ("col_bind", C.c_void_p),
+                ("row_prim", C.c_void_p), ("row_dual", C.c_void_p), ("col_prim", C.c_void_p),
+                ("col_dual", C.c_void_p),
+                ("it_cnt", C.c_int), ("pbs_stat", C.c_int), ("dbs_stat", C.c_int), ("some", C.c_int),
+                ("obj_val", C.c_double), ("valid", C.c_int)]
+
+
+class SpxStats(C.Structure):
+    _fields_ = [("pivots", C.c_longlong), ("reinversions", C.c_longlong), ("batches", C.c_longlong),
+                ("host_syncs", C.c_longlong), ("seconds_total", C.c_double), ("seconds_reinvert", C.c_double)]
+
+
+_lib = None
+
+EXPORTS = ["gk_abi_version", "gk_device_count", "gk_ctx_create", "gk_ctx_destroy", "gk_last_error",
+           "gk_bfd_create", "gk_bfd_destroy", "gk_bfd_set_parm", "gk_bfd_factorize", "gk_bfd_factorize_csc",
+           "gk_bfd_ftran", "gk_bfd_btran", "gk_bfd_update", "gk_bfd_get_count", "gk_bfd_valid",
+           "gk_spx_primal", "gk_spx_dual", "gk_bfd_last_stats", "gk_ios_driver"]
+
+
+def load_library(path: str = LIB_PATH):
+    """Load libglpk_mi355x.so; raises if it is missing (no silent fallback)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(path):
+        raise GkError(f"{path} is missing: build it with __graft_entry__.build()")
+    L = C.CDLL(path)
+    P = C.c_void_p
+    L.gk_abi_version.restype = C.c_int
+    L.gk_device_count.restype = C.c_int
+    L.gk_ctx_create.restype = P
+    L.gk_ctx_create.argtypes = [C.c_int]
+    L.gk_ctx_destroy.argtypes = [P]
+    L.gk_last_error.restype = C.c_char_p
+    L.gk_bfd_create.restype = P
+    L.gk_bfd_create.argtypes = [P]
+    L.gk_bfd_destroy.argtypes = [P]
+    L.gk_bfd_set_parm.argtypes = [P, C.POINTER(Bfcp)]
+    L.gk_bfd_factorize_csc.argtypes = [P, C.c_int, P, P, P]
+    L.gk_bfd_factorize_csc.restype = C.c_int
+    L.gk_bfd_ftran.argtypes = [P, P]
+    L.gk_bfd_btran.argtypes = [P, P]
+    L.gk_bfd_update.argtypes = [P, C.c_int, C.c_int, P, C.c_int, P]
+    L.gk_bfd_update.restype = C.c_int
+    L.gk_bfd_get_count.argtypes = [P]
+    L.gk_bfd_get_count.restype = C.c_int
+    L.gk_bfd_valid.argtypes = [P]
+    L.gk_bfd_valid.restype = C.c_int
+    for name in ("gk_spx_primal", "gk_spx_dual"):
+        f = getattr(L, name)
+        f.argtypes = [P, C.POINTER(Lp), P, C.POINTER(Smcp)]
+        f.restype = C.c_int
+    L.gk_bfd_last_stats.argtypes = [P, C.POINTER(SpxStats)]
+    _lib = L
+    return L
+
+
+def _err(L) -> str:
+    return L.gk_last_error().decode(errors="replace")
+
+
+class Context:
+    """One MI355X device (gk_ctx_create)."""
+
+    def __init__(self, device: int = 0):
+        self.L = load_library()
+        self.h = self.L.gk_ctx_create(device)
+        if not self.h:
+            raise GkError(f"gk_ctx_create({device}) failed: {_err(self.L)}")
+
+    def close(self):
+        if getattr(self, "h", None):
+            self.L.gk_ctx_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        self.close()
+
+
+def SMCP(**options) -> Smcp:
+    """glpapi06.js:359-375, including the `options[x] || default` quirk:
+    any falsy option (0) silently becomes the default."""
+    d = dict(msg_lev=GLP_MSG_ALL, meth=GLP_PRIMAL, pricing=GLP_PT_PSE, r_test=GLP_RT_HAR, tol_bnd=1e-7,
+             tol_dj=1e-7, tol_piv=1e-10, obj_ll=-DBL_MAX, obj_ul=+DBL_MAX, it_lim=INT_MAX, tm_lim=INT_MAX,
+             out_frq=500, out_dly=0, presolve=0)
+    for k, v in options.items():
+        if k not in d:
+            raise KeyError(k)
+        if v:
+            d[k] = v
+    return Smcp(**d)
+
+
+def _pad(a, dtype):
+    out = np.zeros(len(a) + 1, dtype=dtype)
+    out[1:] = a
+    return out
+
+
+class GkProblem:
+    """The reference problem object's hot-path fields, 1-based, plus the
+    device factor handle (lp.bfd) — what glp_simplex / glp_intopt operate on."""
+
+    _version = 0
+
+    def __init__(self, ctx: Context, p: Problem):
+        self.ctx, self.L, self.p = ctx, ctx.L, p
+        m, n = p.m, p.n
+        self.m, self.n = m, n
+        self.row_type = _pad(p.row_type, np.int8)
+        self.row_lb = _pad(p.row_lb, np.float64)
+        self.row_ub = _pad(p.row_ub, np.float64)
+        self.rii = _pad(p.rii, np.float64)
+        self.col_type = _pad(p.col_type, np.int8)
+        self.col_lb = _pad(p.col_lb, np.float64)
+        self.col_ub = _pad(p.col_ub, np.float64)
+        self.col_coef = _pad(p.col_coef, np.float64)
+        self.sjj = _pad(p.sjj, np.float64)
+        self.col_kind = _pad(p.col_kind, np.int8)
+        self.A_ptr = _pad(np.asarray(p.A_ptr, np.int32) + 1, np.int32)      # [1..n+1], 1-based positions
+        self.A_ind = _pad(p.A_ind, np.int32)
+        self.A_val = _pad(p.A_val, np.float64)
+        self.row_stat = _pad(p.row_stat, np.int8)
+        self.col_stat = _pad(p.col_stat, np.int8)
+        self.head = np.zeros(m + 1, np.int32)
+        self.row_bind = np.zeros(m + 1, np.int32)
+        self.col_bind = np.zeros(n + 1, np.int32)
+        self.row_prim = np.zeros(m + 1)
+        self.row_dual = np.zeros(m + 1)
+        self.col_prim = np.zeros(n + 1)
+        self.col_dual = np.zeros(n + 1)
+        self.dir, self.c0, self.nnz = p.dir, p.c0, p.nnz
+        self.it_cnt = 0
+        self.pbs_stat = self.dbs_stat = GLP_UNDEF
+        self.obj_val = 0.0
+        self.some = 0
+        self.valid = 0
+        GkProblem._version += 1
+        self.a_version = GkProblem._version
+        self.bfcp = None
+        self.bfd = self.L.gk_bfd_create(ctx.h)
+        if not self.bfd:
+            raise GkError(_err(self.L))
+
+    def __del__(self):
+        if getattr(self, "bfd", None):
+            self.L.gk_bfd_destroy(self.bfd)
+            self.bfd = None
+
+    def set_bfcp(self, **kw):
+        """glp_set_bfcp (glpapi12.js:133)."""
+        b = Bfcp(type=1, lu_size=0, piv_tol=0.10, piv_lim=4, suhl=1, eps_tol=1e-15, max_gro=1e10,
+                 nfs_max=100, upd_tol=1e-6, nrs_max=100, rs_size=0)
+        for k, v in kw.items():
+            setattr(b, k, v)
+        self.bfcp = b
+        self.L.gk_bfd_set_parm(self.bfd, C.byref(b))
+
+    def touch_matrix(self):
+        """Invalidate the device copy of A (the shim's version counter)."""
+        GkProblem._version += 1
+        self.a_version = GkProblem._version
+
+    # ------------------------------------------------------------------
+    def _lp_struct(self) -> Lp:
+        ptr = lambda a: a.ctypes.data_as(C.c_void_p)
+        lp = Lp()
+        lp.m, lp.n, lp.nnz, lp.dir, lp.c0 = self.m, self.n, self.nnz, self.dir, self.c0
+        lp.row_type, lp.row_lb, lp.row_ub, lp.rii = ptr(self.row_type), ptr(self.row_lb), ptr(self.row_ub), ptr(self.rii)
+        lp.col_type, lp.col_lb, lp.col_ub = ptr(self.col_type), ptr(self.col_lb), ptr(self.col_ub)
+        lp.col_coef, lp.sjj = ptr(self.col_coef), ptr(self.sjj)
+        lp.A_ptr, lp.A_ind, lp.A_val = ptr(self.A_ptr), ptr(self.A_ind), ptr(self.A_val)
+        lp.a_version = self.a_version
+        lp.head, lp.row_stat, lp.col_stat = ptr(self.head), ptr(self.row_stat), ptr(self.col_stat)
+        lp.row_bind, lp.col_bind = ptr(self.row_bind), ptr(self.col_bind)
+        lp.row_prim, lp.row_dual = ptr(self.row_prim), ptr(self.row_dual)
+        lp.col_prim, lp.col_dual = ptr(self.col_prim), ptr(self.col_dual)
+        lp.it_cnt = self.it_cnt
+        return lp
+
+    def _take(self, lp: Lp):
+        self.it_cnt, self.pbs_stat, self.dbs_stat = lp.it_cnt, lp.pbs_stat, lp.dbs_stat
+        self.some, self.obj_val, self.valid = lp.some, lp.obj_val, lp.valid
+
+    def factorize(self) -> int:
+        """glp_factorize (glpapi12.js:5): basis header from statuses, then
+        bfd_factorize with the columns of (I | -R A S) (b_col, :7)."""
+        m, n = self.m, self.n
+        self.valid = 0
+        j = 0
+        self.row_bind[:] = 0
+        self.col_bind[:] = 0
+        for k in range(1, m + n + 1):
+            stat = self.row_stat[k] if k <= m else self.col_stat[k - m]
+            if stat == GLP_BS:
+                j += 1
+                if j > m:
+                    return GLP_EBADB
+                self.head[j] = k
+                if k <= m:
+                    self.row_bind[k] = j
+                else:
+                    self.col_bind[k - m] = j
+        if j < m:
+            return GLP_EBADB
+        if m > 0:
+            ptr = np.zeros(m + 2, np.int32)
+            ind, val = [0], [0.0]
+            ptr[1] = 1
+            for jj in range(1, m + 1):
+                k = self.head[jj]
+                if k <= m:
+                    ind.append(k)
+                    val.append(1.0)
+                else:
+                    c = k - m
+                    lo, hi = self.A_ptr[c], self.A_ptr[c + 1]
+                    rows = self.A_ind[lo:hi]
+                    ind.extend(rows.tolist())
+                    val.extend((-self.rii[rows] * self.A_val[lo:hi] * self.sjj[c]).tolist())
+                ptr[jj + 1] = len(ind)
+            ind = np.asarray(ind, np.int32)
+            val = np.asarray(val, np.float64)
+            ret = self.L.gk_bfd_factorize_csc(self.bfd, m, ptr.ctypes.data_as(C.c_void_p),
+                                              ind.ctypes.data_as(C.c_void_p), val.ctypes.data_as(C.c_void_p))
+            if ret == GK_EABI:
+                raise GkError(_err(self.L))
+            if ret == 1:
+                return GLP_ESING
+            if ret == 2:
+                return GLP_ECOND
+            self.valid = 1
+        return 0
+
+    def ftran(self, x: np.ndarray, tr: bool = False) -> np.ndarray:
+        """glp_ftran / glp_btran (glpapi12.js:198/:222) with the scaling."""
+        m = self.m
+        y = np.zeros(m + 1)
+        y[1:] = x
+        if not tr:
+            y[1:] *= self.rii[1:]
+            self.L.gk_bfd_ftran(self.bfd, y.ctypes.data_as(C.c_void_p))
+            for i in range(1, m + 1):
+                k = self.head[i]
+                y[i] = y[i] / self.rii[k] if k <= m else y[i] * self.sjj[k - m]
+        else:
+            for i in range(1, m + 1):
+                k = self.head[i]
+                y[i] = y[i] / self.rii[k] if k <= m else y[i] * self.sjj[k - m]
+            self.L.gk_bfd_btran(self.bfd, y.ctypes.data_as(C.c_void_p))
+            y[1:] *= self.rii[1:]
+        return y[1:]
+
+    def spx(self, parm: Smcp, dual: bool) -> int:
+        lp = self._lp_struct()
+        fn = self.L.gk_spx_dual if dual else self.L.gk_spx_primal
+        ret = fn(self.ctx.h, C.byref(lp), self.bfd, C.byref(parm))
+        if ret == GK_EABI:
+            raise GkError(_err(self.L))
+        self._take(lp)
+        return ret
+
+    def stats(self) -> SpxStats:
+        st = SpxStats()
+        self.L.gk_bfd_last_stats(self.bfd, C.byref(st))
+        return st
+
+    # ------------------------------------------------------------------
+    def result(self) -> dict:
+        return dict(pbs_stat=self.pbs_stat, dbs_stat=self.dbs_stat, obj_val=self.obj_val, it_cnt=self.it_cnt,
+                    some=self.some, row_stat=self.row_stat[1:].copy(), col_stat=self.col_stat[1:].copy(),
+                    row_prim=self.row_prim[1:].copy(), col_prim=self.col_prim[1:].copy(),
+                    row_dual=self.row_dual[1:].copy(), col_dual=self.col_dual[1:].copy())
+
+
+def _trivial_lp(P: GkProblem, parm: Smcp):
+    """glpapi06.js:149."""
+    P.valid = 0
+    P.pbs_stat = P.dbs_stat = GLP_FEAS
+    P.obj_val = P.c0
+    P.some = 0
+    for i in range(1, P.m + 1):
+        t = P.row_type[i]
+        P.row_stat[i] = GLP_BS
+        P.row_prim[i] = P.row_dual[i] = 0.0
+        if t in (GLP_LO, GLP_DB, GLP_FX) and P.row_lb[i] > +parm.tol_bnd:
+            P.pbs_stat = GLP_NOFEAS
+            if P.some == 0 and parm.meth != GLP_PRIMAL:
+                P.some = i
+        if t in (GLP_UP, GLP_DB, GLP_FX) and P.row_ub[i] < -parm.tol_bnd:
+            P.pbs_stat = GLP_NOFEAS
+            if P.some == 0 and parm.meth != GLP_PRIMAL:
+                P.some = i
+    zeta = 1.0
+    for j in range(1, P.n + 1):
+        zeta = max(zeta, abs(P.col_coef[j]))
+    zeta = (1.0 if P.dir == GLP_MIN else -1.0) / zeta
+    for j in range(1, P.n + 1):
+        t, coef = P.col_type[j], P.col_coef[j]
+        if t == GLP_FR:
+            P.col_stat[j], P.col_prim[j] = GLP_NF, 0.0
+        elif t == GLP_LO:
+            P.col_stat[j], P.col_prim[j] = GLP_NL, P.col_lb[j]
+        elif t == GLP_UP:
+            P.col_stat[j], P.col_prim[j] = GLP_NU, P.col_ub[j]
+        elif t == GLP_DB:
+            if zeta * coef > 0.0 or (zeta * coef == 0.0 and abs(P.col_lb[j]) <= abs(P.col_ub[j])):
+                P.col_stat[j], P.col_prim[j] = GLP_NL, P.col_lb[j]
+            else:
+                P.col_stat[j], P.col_prim[j] = GLP_NU, P.col_ub[j]
+        else:
+            P.col_stat[j], P.col_prim[j] = GLP_NS, P.col_lb[j]
+        P.col_dual[j] = coef
+        P.obj_val += coef * P.col_prim[j]
+        if t in (GLP_FR, GLP_LO) and zeta * coef < -parm.tol_dj:
+            P.dbs_stat = GLP_NOFEAS
+            if P.some == 0 and parm.meth == GLP_PRIMAL:
+                P.some = P.m + j
+        if t in (GLP_FR, GLP_UP) and zeta * coef > +parm.tol_dj:
+            P.dbs_stat = GLP_NOFEAS
+            if P.some == 0 and parm.meth == GLP_PRIMAL:
+                P.some = P.m + j
+
+
+def glp_simplex(P: GkProblem, parm: Smcp | None = None) -> int:
+    """glp_simplex (glpapi06.js:1) with presolve OFF."""
+    if parm is None:
+        parm = SMCP()
+    if parm.msg_lev not in (0, 1, 2, 3, 4):
+        raise GkError(f"glp_simplex: msg_lev = {parm.msg_lev}; invalid parameter")
+    if parm.meth not in (GLP_PRIMAL, GLP_DUALP, GLP_DUAL):
+        raise GkError(f"glp_simplex: meth = {parm.meth}; invalid parameter")
+    if parm.pricing not in (GLP_PT_STD, GLP_PT_PSE):
+        raise GkError(f"glp_simplex: pricing = {parm.pricing}; invalid parameter")
+    if parm.r_test not in (GLP_RT_STD, GLP_RT_HAR):
+        raise GkError(f"glp_simplex: r_test = {parm.r_test}; invalid parameter")
+    for name in ("tol_bnd", "tol_dj", "tol_piv"):
+        v = getattr(parm, name)
+        if not (0.0 < v < 1.0):
+            raise GkError(f"glp_simplex: {name} = {v}; invalid parameter")
+    if parm.it_lim < 0 or parm.tm_lim < 0 or parm.out_frq < 1 or parm.out_dly < 0:
+        raise GkError("glp_simplex: invalid it_lim/tm_lim/out_frq/out_dly")
+    if parm.presolve:
+        raise GkError("glp_simplex: presolve is outside the MI355X core (stays in the JS host)")
+    P.pbs_stat = P.dbs_stat = GLP_UNDEF
+    P.obj_val = 0.0
+    P.some = 0
+    for i in range(1, P.m + 1):
+        if P.row_type[i] == GLP_DB and P.row_lb[i] >= P.row_ub[i]:
+            return GLP_EBOUND
+    for j in range(1, P.n + 1):
+        if P.col_type[j] == GLP_DB and P.col_lb[j] >= P.col_ub[j]:
+            return GLP_EBOUND
+    if P.nnz == 0:
+        _trivial_lp(P, parm)
+        return 0
+    # solve_lp (glpapi06.js:3)
+    if not (P.m == 0 or P.valid):
+        ret = P.factorize()
+        if ret != 0:
+            return ret
+    if parm.meth == GLP_PRIMAL:
+        return P.spx(parm, dual=False)
+    if parm.meth == GLP_DUALP:
+        ret = P.spx(parm, dual=True)
+        if ret == GLP_EFAIL and P.valid:
+            ret = P.spx(parm, dual=False)
+        return ret
+    return P.spx(parm, dual=True)

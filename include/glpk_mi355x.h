@@ -1,0 +1,161 @@
+/*
+ * glpk_mi355x.h — C-ABI of the MI355X-native simplex / branch-and-bound core.
+ *
+ * Drop-in boundary for the reference Cyame/glpk.js (GLPK 4.49 in JS).  The
+ * JS host keeps glpapi*.js / glpcpx.js / glpmpl*.js and rebinds the closure
+ * names of the hot path to these entry points through a thin N-API addon
+ * (js/gk_addon.cc, js/gk_shim.js).
+ *
+ *   entry point            replaces (reference file:line)
+ *   ---------------------  ------------------------------------------------
+ *   gk_spx_primal          spx_primal(lp, parm)            glpspx01.js:1
+ *   gk_spx_dual            spx_dual(lp, parm)              glpspx02.js:1
+ *   gk_bfd_create          bfd_create_it()                 glpbfd.js:10
+ *   gk_bfd_set_parm        bfd_set_parm(bfd, parm)         glpbfd.js:31
+ *   gk_bfd_factorize       bfd_factorize(bfd,m,bh,col,info) glpbfd.js:47
+ *   gk_bfd_factorize_csc   (same, columns passed as CSC instead of a callback)
+ *   gk_bfd_ftran           bfd_ftran(bfd, x)               glpbfd.js:148
+ *   gk_bfd_btran           bfd_btran(bfd, x)               glpbfd.js:159
+ *   gk_bfd_update          bfd_update_it(bfd,j,bh,len,ind,idx,val) glpbfd.js:170
+ *   gk_bfd_get_count       bfd_get_count(bfd)              glpbfd.js:225
+ *   gk_ios_driver          ios_driver(T) with cb_func == null (glpios03.js:1),
+ *                          run from glp_intopt's solve_mip (glpapi09.js:62-79)
+ *
+ * Conventions (identical to the reference's typed arrays): every vector is
+ * 1-based with element 0 unused; auxiliary variable k = 1..m is row k,
+ * structural k = m+1..m+n is column k-m.  Return codes are the reference's
+ * GLP_E* / BFD_E* values.  No entry point throws: on a contract violation
+ * (the reference's xerror/xassert) it returns GK_EABI and gk_last_error()
+ * holds the message; the N-API layer rethrows it as a JS Error.
+ *
+ * Every call is synchronous on the calling thread.  Internally a call may
+ * use several HIP streams on the context's device.  There is no CPU
+ * fallback: if no MI355X (gfx950) device is usable, gk_ctx_create fails and
+ * returns NULL.
+ */
+#ifndef GLPK_MI355X_H
+#define GLPK_MI355X_H
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define GK_ABI_VERSION 1
+#define GK_EABI (-1)          /* contract violation; see gk_last_error() */
+
+typedef struct gk_ctx gk_ctx; /* one HIP device + stream(s)                */
+typedef struct gk_bfd gk_bfd; /* replaces lp.bfd: device-resident factor   */
+
+/* ---- context ------------------------------------------------------------ */
+int         gk_abi_version(void);
+int         gk_device_count(void);
+gk_ctx     *gk_ctx_create(int device);          /* NULL on failure          */
+void        gk_ctx_destroy(gk_ctx *ctx);
+const char *gk_last_error(void);                 /* thread-local message     */
+
+/* ---- basis factorization (glpbfd.js) -------------------------------------
+ * The factor of B is held on the device as an explicit dense inverse,
+ * refreshed by re-inversion after nfs_max product-form updates (the
+ * reference refactorizes after nfs_max Forrest–Tomlin updates,
+ * glpfhv.js:182).  Field meanings follow glp_bfcp (glpapi12.js:108-121). */
+typedef struct {
+    int    type;       /* GLP_BF_FT / GLP_BF_BG / GLP_BF_GR (all served by the same factor) */
+    int    lu_size;
+    double piv_tol;
+    int    piv_lim, suhl;
+    double eps_tol, max_gro;
+    int    nfs_max;    /* updates between re-inversions                      */
+    double upd_tol;
+    int    nrs_max, rs_size;
+} gk_bfcp;
+
+typedef int (*gk_col_fn)(void *info, int j, int *ind, double *val);
+
+gk_bfd *gk_bfd_create(gk_ctx *ctx);
+void    gk_bfd_destroy(gk_bfd *bfd);
+void    gk_bfd_set_parm(gk_bfd *bfd, const gk_bfcp *parm);
+/* 0 | BFD_ESING(1) | BFD_ECOND(2); col(info, j, ind, val) fills column j of B
+ * exactly like b_col/inv_col (glpapi12.js:7, glpspx01.js:147). */
+int     gk_bfd_factorize(gk_bfd *bfd, int m, gk_col_fn col, void *info);
+/* same with B given as CSC: column j occupies [ptr[j], ptr[j+1]) of ind/val
+ * (positions 1-based, ptr[1..m+1]); ind holds 1-based row numbers. */
+int     gk_bfd_factorize_csc(gk_bfd *bfd, int m, const int *ptr, const int *ind, const double *val);
+void    gk_bfd_ftran(gk_bfd *bfd, double *x);            /* x[1..m] := inv(B) x  */
+void    gk_bfd_btran(gk_bfd *bfd, double *x);            /* x[1..m] := inv(B') x */
+/* replace column j of B by (ind[idx+1..idx+len], val[1..len]) — the
+ * reference's (odd but exact) indexing convention of fhv_update_it. */
+int     gk_bfd_update(gk_bfd *bfd, int j, int len, const int *ind, int idx, const double *val);
+int     gk_bfd_get_count(const gk_bfd *bfd);
+int     gk_bfd_valid(const gk_bfd *bfd);
+
+/* ---- simplex (glpspx01.js / glpspx02.js) --------------------------------- */
+typedef struct {                /* glp_smcp, SMCP (glpapi06.js:359-375)       */
+    int    msg_lev, meth, pricing, r_test;
+    double tol_bnd, tol_dj, tol_piv, obj_ll, obj_ul;
+    int    it_lim, tm_lim, out_frq, out_dly, presolve;
+} gk_smcp;
+
+typedef struct {
+    /* problem (read; the fields init_csa reads, glpspx01.js:42-145) */
+    int m, n, nnz, dir;
+    double c0;
+    const signed char *row_type;             /* [1..m] GLP_FR..GLP_FX */
+    const double *row_lb, *row_ub, *rii;     /* [1..m] unscaled bounds, row scale */
+    const signed char *col_type;             /* [1..n] */
+    const double *col_lb, *col_ub, *col_coef, *sjj;   /* [1..n] */
+    const int *A_ptr;                        /* [1..n+1] positions into A_ind/A_val */
+    const int *A_ind;                        /* [1..nnz] 1-based row numbers, list order */
+    const double *A_val;                     /* [1..nnz] unscaled values */
+    unsigned long long a_version;            /* !=0: A/scale unchanged since the last call
+                                                with this version => reuse the device copy */
+    /* basis (read/write) */
+    int *head;                               /* [1..m] basis header (lp.head) */
+    signed char *row_stat, *col_stat;        /* [1..m], [1..n] */
+    /* solution (write; store_sol, glpspx01.js:1591) */
+    int *row_bind, *col_bind;
+    double *row_prim, *row_dual, *col_prim, *col_dual;
+    int it_cnt;                              /* in/out: lp.it_cnt */
+    int pbs_stat, dbs_stat, some;            /* out */
+    double obj_val;                          /* out */
+    int valid;                               /* out: lp.valid */
+} gk_lp;
+
+/* The factor handle must be valid for lp->head (as after glp_factorize);
+ * on return it is valid for the new lp->head (store_sol semantics), or on
+ * GLP_EFAIL left as the reference leaves it. Returns 0 | GLP_EFAIL |
+ * GLP_EOBJLL | GLP_EOBJUL | GLP_EITLIM | GLP_ETMLIM | GK_EABI. */
+int gk_spx_primal(gk_ctx *ctx, gk_lp *lp, gk_bfd *bfd, const gk_smcp *parm);
+int gk_spx_dual(gk_ctx *ctx, gk_lp *lp, gk_bfd *bfd, const gk_smcp *parm);
+
+/* engine counters of the last gk_spx_* call on this handle (for benches) */
+typedef struct {
+    long long pivots, reinversions, batches, host_syncs;
+    double seconds_total, seconds_reinvert;
+} gk_spx_stats;
+void gk_bfd_last_stats(const gk_bfd *bfd, gk_spx_stats *st);
+
+/* ---- branch and bound (glpios03.js, glpapi09.js) ------------------------- */
+typedef struct {                /* glp_iocp, IOCP (glpapi09.js:392-414)       */
+    int    msg_lev, br_tech, bt_tech;
+    double tol_int, tol_obj;
+    int    tm_lim, out_frq, out_dly, pp_tech;
+    double mip_gap;
+    int    presolve;
+} gk_iocp;
+
+typedef struct {
+    gk_lp lp;                                 /* root problem, solved to optimality */
+    const signed char *col_kind;              /* [1..n] GLP_CV / GLP_IV */
+    /* out */
+    int mip_stat;
+    double mip_obj;
+    double *col_mipx, *row_mipx;              /* [1..n], [1..m] */
+    long long lp_solves, nodes_created, pivots;
+} gk_mip;
+
+int gk_ios_driver(gk_ctx *ctx, gk_mip *mip, const gk_iocp *parm);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* GLPK_MI355X_H */

@@ -1,0 +1,133 @@
+"""GPU parity of the HIP simplex path (through the C-ABI) against the
+reference's golden outputs and the oracle.
+
+Bar (north star): objective within 1e-9 relative of the reference, identical
+return codes and solution statuses.  Pivot sequences may differ where the GPU
+reductions break near-ties differently, so iteration counts are only checked
+where they are forced (it_lim runs)."""
+import os
+
+import numpy as np
+import pytest
+
+from conftest import golden_files, load_golden
+from glpk_js_amd import gk, problems
+
+pytestmark = pytest.mark.gpu
+
+LP_CASES = []
+for path in golden_files("lp_"):
+    d = load_golden(path)
+    for r, run in enumerate(d["runs"]):
+        LP_CASES.append(pytest.param(path, r, id=f"{os.path.basename(path)[3:-5]}-{r}-m{run['opts'].get('meth', 1)}"))
+
+
+def check_solution(P: gk.GkProblem, tol=1e-7):
+    """Primal consistency of the stored solution: row activities equal A x,
+    bounds hold within tolerance, objective equals c'x + c0."""
+    p = P.p
+    x = P.col_prim[1:]
+    act = np.zeros(p.m)
+    for j in range(p.n):
+        lo, hi = p.A_ptr[j], p.A_ptr[j + 1]
+        act[p.A_ind[lo:hi] - 1] += p.A_val[lo:hi] * x[j]
+    scale = 1.0 + np.abs(act).max(initial=0.0)
+    assert np.max(np.abs(act - P.row_prim[1:]), initial=0.0) <= 1e-8 * scale
+    obj = p.c0 + float(np.dot(p.col_coef, x))
+    assert abs(obj - P.obj_val) <= 1e-9 * max(1.0, abs(obj))
+
+
+@pytest.mark.parametrize("path,run_index", LP_CASES)
+def test_gpu_lp_matches_reference(gpu_ctx, path, run_index):
+    d = load_golden(path)
+    run = d["runs"][run_index]
+    prob = problems.from_fixture(d)
+    P = gk.GkProblem(gpu_ctx, prob)
+    ret = gk.glp_simplex(P, gk.SMCP(**run["opts"]))
+    assert ret == run["ret"]
+    if run["opts"].get("it_lim"):
+        assert P.it_cnt == run["it_cnt"]
+        check_solution(P)
+        return
+    assert (P.pbs_stat, P.dbs_stat) == (run["pbs_stat"], run["dbs_stat"])
+    if P.pbs_stat == problems.GLP_FEAS and P.dbs_stat == problems.GLP_FEAS:
+        ref = run["obj_val"]
+        assert abs(P.obj_val - ref) <= 1e-9 * max(1.0, abs(ref)), (P.obj_val, ref)
+        check_solution(P)
+
+
+@pytest.mark.parametrize("name", ["lp_gap.json", "lp_dense_64x256.json", "lp_mix14.json", "lp_c2s.json"])
+def test_gpu_bfd_ftran_btran_match_oracle(gpu_ctx, oracle, name):
+    """gk_bfd_factorize + gk_bfd_ftran/btran (glpapi12.js:5/:198/:222) agree
+    with the oracle's LU+FT factor on the optimal basis of the instance."""
+    d = load_golden(os.path.join(os.path.dirname(__file__), "golden", name))
+    run = d["runs"][0]
+    prob = problems.from_fixture(d)
+    prob.row_stat = np.asarray(run["row_stat"], np.int8)
+    prob.col_stat = np.asarray(run["col_stat"], np.int8)
+    P = gk.GkProblem(gpu_ctx, prob)
+    assert P.factorize() == 0
+    o = oracle.OracleProb(prob)
+    assert o.factorize() == 0
+    rng = np.random.default_rng(1)
+    for tr in (False, True):
+        for _ in range(3):
+            b = rng.standard_normal(prob.m)
+            xg = P.ftran(b, tr=tr)
+            xo = o.ftran(b, tr=tr)
+            err = np.max(np.abs(xg - xo)) / (1.0 + np.max(np.abs(xo)))
+            assert err <= 1e-10, err
+
+
+def test_gpu_bfd_update_chain(gpu_ctx, oracle):
+    """gk_bfd_update (bfd_update_it, glpbfd.js:170) over a chain of column
+    replacements stays equal to a fresh factorization."""
+    import ctypes as C
+    prob = problems.gen_dense(48, 96, seed=3)
+    P = gk.GkProblem(gpu_ctx, prob)
+    assert P.factorize() == 0          # all-slack basis
+    L = gk.load_library()
+    m = prob.m
+    Bcols = {i: (np.array([i], np.int32), np.array([1.0])) for i in range(1, m + 1)}
+    rng = np.random.default_rng(5)
+    for t in range(20):
+        j = int(rng.integers(1, m + 1))
+        c = int(rng.integers(0, prob.n))
+        lo, hi = prob.A_ptr[c], prob.A_ptr[c + 1]
+        ind = np.zeros(hi - lo + 1, np.int32); ind[1:] = prob.A_ind[lo:hi]
+        val = np.zeros(hi - lo + 1); val[1:] = -prob.A_val[lo:hi]
+        ret = L.gk_bfd_update(P.bfd, j, hi - lo, ind.ctypes.data_as(C.c_void_p), 0, val.ctypes.data_as(C.c_void_p))
+        assert ret == 0
+        Bcols[j] = (ind[1:].copy(), val[1:].copy())
+    B = np.zeros((m, m))
+    for j, (ind, val) in Bcols.items():
+        B[ind - 1, j - 1] = val
+    b = rng.standard_normal(m)
+    y = np.zeros(m + 1); y[1:] = b
+    L.gk_bfd_ftran(P.bfd, y.ctypes.data_as(C.c_void_p))
+    x = np.linalg.solve(B, b)
+    assert np.max(np.abs(y[1:] - x)) <= 1e-9 * (1 + np.max(np.abs(x)))
+    assert L.gk_bfd_get_count(P.bfd) == 20
+
+
+def test_gpu_dense_1024x4096_dual_matches_reference(gpu_ctx):
+    """C3 proxy full solve; reference objective from SURVEY.md §4 (dual)."""
+    prob = problems.gen_dense(1024, 4096, seed=42)
+    P = gk.GkProblem(gpu_ctx, prob)
+    ret = gk.glp_simplex(P, gk.SMCP(meth=gk.GLP_DUAL))
+    assert ret == 0 and P.pbs_stat == P.dbs_stat == problems.GLP_FEAS
+    ref = 978.22910129338311
+    assert abs(P.obj_val - ref) <= 1e-9 * ref, P.obj_val
+    check_solution(P)
+
+
+def test_gpu_c3_full_size_iteration_limit(gpu_ctx):
+    """C3 at full size (4096 x 16384): 300 dual pivots as the reference's
+    it_lim=300 timing run; properties: EITLIM, exactly 300 pivots, the stored
+    point satisfies A x = row activities, objective = c'x."""
+    prob = problems.gen_dense(4096, 16384, seed=42)
+    P = gk.GkProblem(gpu_ctx, prob)
+    ret = gk.glp_simplex(P, gk.SMCP(meth=gk.GLP_DUAL, it_lim=300))
+    assert ret == gk.GLP_EBOUND + 4     # GLP_EITLIM = 8
+    assert P.it_cnt == 300
+    check_solution(P)

@@ -1,0 +1,54 @@
+"""The oracle (C restatement) against the reference's own outputs.
+
+Fixtures come from tests/golden/gen_golden.js, which runs the reference
+dist/glpk.js flows (glp_read_lp / glp_load_matrix, glp_simplex, glp_intopt)
+in the build container.  The oracle must reproduce them bit for bit: return
+code, statuses, objective, iteration count, every primal and dual value and
+the pivot-by-pivot trace (entering/leaving variable and step)."""
+import os
+
+import numpy as np
+import pytest
+
+from conftest import golden_files, load_golden
+from glpk_js_amd import problems
+
+LP_CASES = []
+for path in golden_files("lp_"):
+    d = load_golden(path)
+    for r, run in enumerate(d["runs"]):
+        LP_CASES.append(pytest.param(path, r, id=f"{os.path.basename(path)[3:-5]}-{r}-m{run['opts'].get('meth', 1)}"))
+
+
+@pytest.mark.parametrize("path,run_index", LP_CASES)
+def test_oracle_lp_bit_exact(oracle, path, run_index):
+    d = load_golden(path)
+    run = d["runs"][run_index]
+    prob = problems.from_fixture(d)
+    o = oracle.OracleProb(prob)
+    trace = []
+    ret = o.simplex(trace=trace, **run["opts"])
+    r = o.result()
+    assert ret == run["ret"]
+    assert (r["pbs_stat"], r["dbs_stat"]) == (run["pbs_stat"], run["dbs_stat"])
+    assert r["it_cnt"] == run["it_cnt"]
+    assert r["obj_val"] == run["obj_val"]           # bit-exact
+    for key in ("row_prim", "row_dual", "col_prim", "col_dual"):
+        np.testing.assert_array_equal(r[key], np.asarray(run[key], dtype=np.float64), err_msg=key)
+    np.testing.assert_array_equal(r["row_stat"], run["row_stat"])
+    np.testing.assert_array_equal(r["col_stat"], run["col_stat"])
+    ref_trace = [tuple(t) for t in run["trace"]]
+    assert [tuple(t) for t in trace[:len(ref_trace)]] == ref_trace
+
+
+def test_generators_match_fixture_statistics():
+    """The numpy splitmix64 generators rebuild the reference's instances:
+    the recorded row/column data of the generated fixtures match."""
+    for name in ("lp_dense_64x256.json", "lp_dense_128x512.json"):
+        d = load_golden(os.path.join(os.path.dirname(__file__), "golden", name))
+        p = problems.from_fixture(d)
+        g = d["gen"]
+        q = problems.gen_dense(g["m"], g["n"], g["seed"])
+        np.testing.assert_array_equal(q.col_coef, np.asarray(d["col_coef"]))
+        np.testing.assert_array_equal(q.row_ub, np.asarray(d["row_ub"]))
+        assert p.nnz == d["nnz"] == q.nnz
