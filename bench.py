@@ -1,0 +1,217 @@
+#!/usr/bin/env python3
+"""Benchmark of the MI355X simplex core on BASELINE.json's HBM-roofline
+configuration: the C3 dense random LP, m=4096, n=16384, fp64, dual simplex.
+
+One *step* = one glp_simplex(SMCP{meth: GLP_DUAL, it_lim: P}) call that
+continues from the basis the previous step left (P = 100 pivots by default),
+i.e. the reference's own it_lim-bounded timing run ("first 300
+pivots"), on inputs already resident in HBM.  `value` is simplex pivots/s of
+the whole job: every rank solves its own replica (seed 42 + rank), so per-GPU
+work is fixed as N grows ("scaling": "weak", replicas only for a single LP).
+
+Usage: python bench.py [--gpus N] [--steps K] [--warmup W]
+(torchrun-launched for N > 1; RANK/LOCAL_RANK/WORLD_SIZE from the env).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+import __graft_entry__  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+
+
+def log(rank, *a):
+    if rank == 0:
+        print(*a, file=sys.stderr, flush=True)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--pivots-per-step", type=int, default=100)
+    ap.add_argument("--m", type=int, default=4096)
+    ap.add_argument("--n", type=int, default=16384)
+    ap.add_argument("--cpu-seconds", type=float, default=20.0, help="bounded CPU-baseline sample (oracle)")
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-extra", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+
+    import torch
+    import torch.distributed as dist
+    if world > 1:
+        dist.init_process_group(backend="nccl" if torch.cuda.is_available() else "gloo")
+    if torch.cuda.is_available():
+        torch.cuda.set_device(local_rank)
+
+    __graft_entry__.build_hip()
+    __graft_entry__.load_package()
+    from glpk_js_amd import gk, problems
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+        if torch.cuda.is_available():
+            torch.cuda.synchronize()
+
+    t_gen = time.time()
+    prob = problems.gen_dense(args.m, args.n, seed=42 + rank)
+    ctx = gk.Context(local_rank)
+    P = gk.GkProblem(ctx, prob)
+    assert P.factorize() == 0
+    parm = gk.SMCP(meth=gk.GLP_DUAL, it_lim=args.pivots_per_step, msg_lev=gk.GLP_MSG_ERR)
+    log(rank, f"[bench] generated C3 {args.m}x{args.n} in {time.time() - t_gen:.1f}s")
+
+    restarts = [0]
+
+    def step():
+        it0 = P.it_cnt
+        ret = gk.glp_simplex(P, parm)
+        if ret not in (0, 8):
+            raise RuntimeError(f"glp_simplex returned {ret}")
+        if ret == 0:                    # optimum reached: restart from the slack basis
+            P.row_stat[1:] = problems.GLP_BS
+            P.col_stat[1:] = problems.GLP_NL
+            P.valid = 0
+            assert P.factorize() == 0
+            restarts[0] += 1
+        return P.it_cnt - it0
+
+    for _ in range(args.warmup):
+        step()
+    barrier()
+    t0 = time.perf_counter()
+    piv = 0
+    for _ in range(args.steps):
+        piv += step()
+    barrier()
+    dt = time.perf_counter() - t0
+    st = P.stats()
+
+    tot_piv, max_dt = piv, dt
+    if world > 1:
+        t = torch.tensor([float(piv)], dtype=torch.float64, device="cuda" if torch.cuda.is_available() else "cpu")
+        dist.all_reduce(t, op=dist.ReduceOp.SUM)
+        tot_piv = int(t.item())
+        t = torch.tensor([dt], dtype=torch.float64, device=t.device)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        max_dt = float(t.item())
+    value = tot_piv / max_dt
+
+    # roofline of the dominant kernel (the pricing pass over A_N), timed live
+    # with HIP events on the engine stream; algorithmic bytes per launch
+    roof = None
+    kern = {}
+    if rank == 0:
+        for which, name in ((0, "pricing_pass_AtN"), (1, "dual_pse_A_w"), (2, "ftran_Binv_x"), (3, "binv_rank1")):
+            ms, b = P.time_kernel(which, reps=10)
+            kern[name] = {"ms": round(ms, 5), "bytes": b, "GBps": round(b / (ms * 1e-3) / 1e9, 1)}
+        ms, b = P.time_kernel(0, reps=20)
+        achieved = b / (ms * 1e-3) / 1e9
+        traffic = None
+        tpath = os.path.join(ROOT, "profiles", "r01_pmc_traffic.json")
+        if os.path.exists(tpath):
+            try:
+                traffic = json.load(open(tpath)).get("k_colpass_dense", {}).get("bytes_per_launch")
+            except Exception:
+                traffic = None
+        roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                "kernel": "k_colpass_dense (trow = -rho' A_N)", "ms_per_launch": round(ms, 5),
+                "bytes_per_launch": b}
+
+    cpu = None
+    extra = {}
+    if rank == 0 and world == 1 and not args.no_cpu:
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import orcpy   # CPU baseline leg only: the bit-faithful C port of the reference
+        base = problems.gen_dense(args.m, args.n, seed=42, keep_dense=False)
+        o = orcpy.OracleProb(base)
+        del base
+        t1 = time.perf_counter()
+        o.simplex(meth=3, tm_lim=int(args.cpu_seconds * 1000))
+        cdt = time.perf_counter() - t1
+        cres = o.result()
+        del o
+        cpu = {"value": round(cres["it_cnt"] / cdt, 3), "unit": "pivots/s", "cores": 1, "kind": "port",
+               "sample": f"oracle (C restatement of glpspx02.js) dual simplex on the same C3 4096x16384 "
+                         f"instance from the slack basis, tm_lim={args.cpu_seconds:.0f}s: "
+                         f"{cres['it_cnt']} pivots in {cdt:.1f}s incl. init_csa; reference node "
+                         f"dist/glpk.js measured 9.4 pivots/s on this config (BASELINE.md)"}
+
+    if rank == 0 and world == 1 and not args.no_extra:
+        del P
+        extra = run_extra(gk, problems, ctx, prob)
+
+    if rank == 0:
+        line = {
+            "metric": "simplex pivots/s (dual, C3 dense 4096x16384 fp64)",
+            "value": round(value, 2),
+            "unit": "pivots/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(1000.0 * max_dt / args.steps, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f64",
+            "data": "synthetic (SURVEY.md §8(d) splitmix64 C3 generator, seed 42+rank)",
+            "config": {"workload": "C3 dense random LP m=4096 n=16384 (BASELINE.json configs[2]); "
+                                   f"step = glp_simplex dual with it_lim={args.pivots_per_step} continuing "
+                                   "from the previous basis",
+                       "m": args.m, "n": args.n, "pivots_per_step": args.pivots_per_step,
+                       "parallelism": f"replicas x{world}"},
+            "roofline": roof,
+            "cpu_baseline": cpu,
+            "engine": {"pivots": int(st.pivots), "reinversions": int(st.reinversions),
+                       "batches": int(st.batches), "host_syncs": int(st.host_syncs),
+                       "restarts": restarts[0], "kernels": kern},
+            "extra": extra,
+        }
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def run_extra(gk, problems, ctx, c3):
+    """Secondary configurations of BASELINE.json on the same GPU (C2s surrogate
+    of configs[1]; C3 timed exactly as BASELINE.md times the reference: first
+    300 dual pivots from the slack basis including setup); for context, not
+    the headline."""
+    out = {}
+    P = gk.GkProblem(ctx, c3)
+    t0 = time.perf_counter()
+    ret = gk.glp_simplex(P, gk.SMCP(meth=gk.GLP_DUAL, it_lim=300, msg_lev=gk.GLP_MSG_ERR))
+    dt = time.perf_counter() - t0
+    out["c3_first300_dual_incl_setup"] = {"ret": ret, "pivots": P.it_cnt, "seconds": round(dt, 4),
+                                          "pivots_per_s": round(P.it_cnt / dt, 1),
+                                          "reference_node_pivots_per_s": 9.4}
+    del P
+    p = problems.gen_c2s()
+    P = gk.GkProblem(ctx, p)
+    t0 = time.perf_counter()
+    ret = gk.glp_simplex(P, gk.SMCP(meth=gk.GLP_DUAL, msg_lev=gk.GLP_MSG_ERR))
+    dt = time.perf_counter() - t0
+    out["c2s_dual_full_solve"] = {"ret": ret, "obj": P.obj_val, "ref_obj": 357.82820943518834,
+                                  "pivots": P.it_cnt, "seconds": round(dt, 4),
+                                  "pivots_per_s": round(P.it_cnt / dt, 1),
+                                  "reference_node_pivots_per_s": 1813}
+    return out
+
+
+if __name__ == "__main__":
+    main()

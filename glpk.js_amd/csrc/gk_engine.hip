@@ -1429,6 +1429,61 @@ int gk_spx_dual(gk_ctx *ctx, gk_lp *lp, gk_bfd *bfd, const gk_smcp *parm) { retu
 
 }  // extern "C"
 
+extern "C" double gk_bfd_time_kernel(gk_bfd *f, int which, int reps, double *bytes)
+{
+    try {
+        ABI_REQUIRE(f && f->eng && f->valid && reps > 0, "gk_bfd_time_kernel: no resident problem");
+        HIPCHK(hipSetDevice(f->ctx->device));
+        Engine &E = *f->eng;
+        hipStream_t s = f->ctx->stream;
+        const int m = E.m, n = E.n;
+        MatDev A = E.mat();
+        double *scratch = nullptr;
+        double b = 0.0;
+        const double vec = 8.0;
+        switch (which) {
+        case 0: b = (A.dense ? 8.0 * m * (double)n : 12.0 * E.nnz) + vec * (m + 2.0 * n) + 4.0 * (m + n) + n; break;
+        case 1: b = (A.dense ? 8.0 * m * (double)n : 12.0 * E.nnz) + vec * (n + 2.0 * m); break;
+        case 2: b = 8.0 * m * (double)m + vec * 2.0 * m; break;
+        case 3: b = 16.0 * m * (double)m + vec * 2.0 * m; break;
+        default: ABI_REQUIRE(false, "gk_bfd_time_kernel: which = %d", which);
+        }
+        if (which == 3) {
+            HIPCHK(hipMalloc((void **)&scratch, (size_t)f->ldb * m * sizeof(double)));
+            HIPCHK(hipMemcpyAsync(scratch, f->Binv.p, (size_t)f->ldb * m * sizeof(double), hipMemcpyDeviceToDevice, s));
+            fill_d(s, E.tcol.p, 1.0, m);
+        }
+        hipEvent_t e0, e1;
+        HIPCHK(hipEventCreate(&e0));
+        HIPCHK(hipEventCreate(&e1));
+        auto launch = [&]() {
+            switch (which) {
+            case 0: colpass(s, A, CP_TROW, m, n, E.head.p, E.stat.p, E.coef.p, nullptr, E.rho.p, nullptr, E.trow.p,
+                            nullptr, nullptr); break;
+            case 1: aprod_neg(s, A, E.wcol.p, E.ys.p, E.work.p, E.partial.p, PARTIAL_CAP); break;
+            case 2: gemv_n(s, f->Binv.p, m, m, f->ldb, E.h.p, E.partial.p, PARTIAL_CAP, E.tcol.p, 1.0, nullptr, 0.0); break;
+            case 3: binv_rank1(s, scratch, m, f->ldb, E.rowp.p, E.tcol.p, 1); break;
+            }
+        };
+        launch();                               // warm
+        if (which == 1 || which == 2) fill_d(s, which == 1 ? E.wcol.p : E.h.p, 1.0, which == 1 ? n : m);
+        HIPCHK(hipEventRecord(e0, s));
+        for (int r = 0; r < reps; r++) launch();
+        HIPCHK(hipEventRecord(e1, s));
+        HIPCHK(hipEventSynchronize(e1));
+        float ms = 0.f;
+        HIPCHK(hipEventElapsedTime(&ms, e0, e1));
+        (void)hipEventDestroy(e0);
+        (void)hipEventDestroy(e1);
+        if (scratch) (void)hipFree(scratch);
+        if (bytes) *bytes = b;
+        return (double)ms / reps;
+    } catch (const AbiError &err) {
+        g_err = err.msg;
+        return -1.0;
+    }
+}
+
 // placeholder until the native branch-and-bound driver lands (gk_ios.hip)
 extern "C" __attribute__((weak)) int gk_ios_driver(gk_ctx *, gk_mip *, const gk_iocp *)
 {

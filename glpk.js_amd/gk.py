@@ -114,6 +114,8 @@ def load_library(path: str = LIB_PATH):
         f.argtypes = [P, C.POINTER(Lp), P, C.POINTER(Smcp)]
         f.restype = C.c_int
     L.gk_bfd_last_stats.argtypes = [P, C.POINTER(SpxStats)]
+    L.gk_bfd_time_kernel.argtypes = [P, C.c_int, C.c_int, C.POINTER(C.c_double)]
+    L.gk_bfd_time_kernel.restype = C.c_double
     _lib = L
     return L
 
@@ -322,6 +324,15 @@ class GkProblem:
             raise GkError(_err(self.L))
         self._take(lp)
         return ret
+
+    def time_kernel(self, which: int, reps: int = 10):
+        """(ms per launch, algorithmic bytes per launch) of one engine kernel,
+        timed with HIP events on the engine stream (gk_bfd_time_kernel)."""
+        b = C.c_double(0.0)
+        ms = self.L.gk_bfd_time_kernel(self.bfd, which, reps, C.byref(b))
+        if ms < 0:
+            raise GkError(_err(self.L))
+        return ms, b.value
 
     def stats(self) -> SpxStats:
         st = SpxStats()

@@ -134,6 +134,17 @@ typedef struct {
 } gk_spx_stats;
 void gk_bfd_last_stats(const gk_bfd *bfd, gk_spx_stats *st);
 
+/* measurement hook for bench.py (not part of the reference interface):
+ * launch one engine kernel `reps` times on the problem left resident by the
+ * last gk_spx_* call, bracketed by two HIP events on the engine's stream,
+ * and return the average milliseconds per launch (or < 0 on error).
+ *   which 0: pricing pass trow = -rho' N over the non-basic columns
+ *         1: A w product of the dual steepest-edge update
+ *         2: inv(B) x product (FTRAN)
+ *         3: rank-1 update of inv(B) (on a scratch copy)
+ * *bytes receives the algorithmic bytes one launch must move. */
+double gk_bfd_time_kernel(gk_bfd *bfd, int which, int reps, double *bytes);
+
 /* ---- branch and bound (glpios03.js, glpapi09.js) ------------------------- */
 typedef struct {                /* glp_iocp, IOCP (glpapi09.js:392-414)       */
     int    msg_lev, br_tech, bt_tech;

@@ -90,9 +90,10 @@ def test_gpu_bfd_update_chain(gpu_ctx, oracle):
     m = prob.m
     Bcols = {i: (np.array([i], np.int32), np.array([1.0])) for i in range(1, m + 1)}
     rng = np.random.default_rng(5)
+    pos = rng.permutation(m)[:20] + 1              # distinct positions and columns:
+    cols = rng.permutation(prob.n)[:20]            # a repeated column would make B singular
     for t in range(20):
-        j = int(rng.integers(1, m + 1))
-        c = int(rng.integers(0, prob.n))
+        j, c = int(pos[t]), int(cols[t])
         lo, hi = prob.A_ptr[c], prob.A_ptr[c + 1]
         ind = np.zeros(hi - lo + 1, np.int32); ind[1:] = prob.A_ind[lo:hi]
         val = np.zeros(hi - lo + 1); val[1:] = -prob.A_val[lo:hi]
