@@ -1,0 +1,200 @@
+// Device-side helpers shared by the kernel translation units (wave64
+// reductions, deterministic candidate selection, small accessors).
+#pragma once
+#include "gk_internal.h"
+#include <cfloat>
+
+namespace gk {
+#define GATE(st, need_p)                                                   \
+    if ((st) != nullptr) {                                                 \
+        if ((st)->stop) return;                                            \
+        if ((need_p) && (st)->p <= 0) return;                              \
+    }
+
+constexpr int WG = 1024;       // single-workgroup control kernels
+constexpr double DBL_EPS = 2.220446049250313e-16;   // glpapi.js:7
+
+__device__ __forceinline__ double wsum(double v)
+{
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+    return v;
+}
+
+__device__ __forceinline__ double wmax(double v)
+{
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v = fmax(v, __shfl_xor(v, o));
+    return v;
+}
+
+// block-wide reductions for blockDim.x <= 1024 (16 waves)
+static __device__ double block_sum(double v, double *sh)
+{
+    int lane = threadIdx.x & 63, w = threadIdx.x >> 6, nw = (blockDim.x + 63) >> 6;
+    v = wsum(v);
+    __syncthreads();
+    if (lane == 0) sh[w] = v;
+    __syncthreads();
+    double r = 0.0;
+    if (w == 0) {
+        r = lane < nw ? sh[lane] : 0.0;
+        r = wsum(r);
+        if (lane == 0) sh[0] = r;
+    }
+    __syncthreads();
+    r = sh[0];
+    __syncthreads();
+    return r;
+}
+
+static __device__ double block_max(double v, double *sh)
+{
+    int lane = threadIdx.x & 63, w = threadIdx.x >> 6, nw = (blockDim.x + 63) >> 6;
+    v = wmax(v);
+    __syncthreads();
+    if (lane == 0) sh[w] = v;
+    __syncthreads();
+    double r = 0.0;
+    if (w == 0) {
+        r = lane < nw ? sh[lane] : 0.0;
+        r = wmax(r);
+        if (lane == 0) sh[0] = r;
+    }
+    __syncthreads();
+    r = sh[0];
+    __syncthreads();
+    return r;
+}
+
+static __device__ int block_or(int v, int *sh)
+{
+    __syncthreads();
+    if (threadIdx.x == 0) sh[0] = 0;
+    __syncthreads();
+    if (v) sh[0] = 1;
+    __syncthreads();
+    int r = sh[0];
+    __syncthreads();
+    return r;
+}
+
+// candidate of an index-choosing scan: key1 (primary), key2 (secondary), idx
+struct Cand {
+    double k1, k2;
+    int idx, aux;
+};
+
+// mode 0: max k1, tie lowest idx                   (chuzr dual / chuzc primal)
+// mode 1: min k1, then max k2, tie lowest idx       (Harris pass 1)
+// mode 2: max k2, tie lowest idx                    (Harris pass 2)
+template <int MODE>
+__device__ __forceinline__ bool better(const Cand &a, const Cand &b)
+{
+    if (a.idx == 0) return false;
+    if (b.idx == 0) return true;
+    if (MODE == 0) {
+        if (a.k1 != b.k1) return a.k1 > b.k1;
+    } else if (MODE == 1) {
+        if (a.k1 != b.k1) return a.k1 < b.k1;
+        if (a.k2 != b.k2) return a.k2 > b.k2;
+    } else {
+        if (a.k2 != b.k2) return a.k2 > b.k2;
+    }
+    return a.idx < b.idx;
+}
+
+template <int MODE>
+static __device__ Cand block_best(Cand c, Cand *sh)
+{
+    int lane = threadIdx.x & 63, w = threadIdx.x >> 6, nw = (blockDim.x + 63) >> 6;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        Cand d;
+        d.k1 = __shfl_xor(c.k1, o);
+        d.k2 = __shfl_xor(c.k2, o);
+        d.idx = __shfl_xor(c.idx, o);
+        d.aux = __shfl_xor(c.aux, o);
+        if (better<MODE>(d, c)) c = d;
+    }
+    __syncthreads();
+    if (lane == 0) sh[w] = c;
+    __syncthreads();
+    if (w == 0) {
+        Cand r;
+        if (lane < nw) r = sh[lane];
+        else { r.k1 = 0; r.k2 = 0; r.idx = 0; r.aux = 0; }
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) {
+            Cand d;
+            d.k1 = __shfl_xor(r.k1, o);
+            d.k2 = __shfl_xor(r.k2, o);
+            d.idx = __shfl_xor(r.idx, o);
+            d.aux = __shfl_xor(r.aux, o);
+            if (better<MODE>(d, r)) r = d;
+        }
+        if (lane == 0) sh[0] = r;
+    }
+    __syncthreads();
+    Cand r = sh[0];
+    __syncthreads();
+    return r;
+}
+
+__device__ __forceinline__ unsigned long long dbits(double v) { return (unsigned long long)__double_as_longlong(v); }
+
+__device__ __forceinline__ double get_xN(const signed char *stat, const double *lb, const double *ub, int k, int j)
+{
+    // glpspx01.js:442
+    switch (stat[j - 1]) {
+    case NL: return lb[k - 1];
+    case NU: return ub[k - 1];
+    case NF: return 0.0;
+    default: return lb[k - 1];
+    }
+}
+
+// reset_refsp (glpspx01.js:586 / glpspx02.js:497)
+static __device__ void reset_refsp_dev(const SpxDev &d, int dual)
+{
+    const int m = d.m, n = d.n;
+    for (int k = threadIdx.x; k < m + n; k += blockDim.x) d.refsp[k] = 0;
+    __syncthreads();
+    if (dual) {
+        for (int i = threadIdx.x; i < m; i += blockDim.x) {
+            d.refsp[d.head[i] - 1] = 1;
+            d.gamma[i] = 1.0;
+        }
+    } else {
+        for (int j = threadIdx.x; j < n; j += blockDim.x) {
+            d.refsp[d.head[m + j] - 1] = 1;
+            d.gamma[j] = 1.0;
+        }
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) d.st->refct = 1000;
+    __syncthreads();
+}
+
+// h = -N[q] (eval_tcol, glpspx01.js:702-719); runs inside a single workgroup
+static __device__ void build_hq(const SpxDev &d, int q)
+{
+    const int m = d.m;
+    const int k = d.head[m + q - 1];
+    for (int i = threadIdx.x; i < m; i += blockDim.x) d.h[i] = 0.0;
+    __syncthreads();
+    if (k <= m) {
+        if (threadIdx.x == 0) d.h[k - 1] = -1.0;
+    } else {
+        const int c = k - m - 1;
+        if (d.A.dense) {
+            const double *col = d.A.A + (size_t)c * d.A.lda;
+            for (int i = threadIdx.x; i < m; i += blockDim.x) d.h[i] = col[i];
+        } else {
+            for (int t = d.A.cptr[c] + threadIdx.x; t < d.A.cptr[c + 1]; t += blockDim.x) d.h[d.A.cind[t]] = d.A.cval[t];
+        }
+    }
+    __syncthreads();
+}
+
+}  // namespace gk

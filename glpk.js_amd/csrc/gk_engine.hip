@@ -94,7 +94,8 @@ struct Engine {
     int m = 0, n = 0, nnz = 0;
     int dense = 0, lda = 0;
     unsigned long long a_version = 0;
-    DBuf<double> A;                         // dense
+    DBuf<double> A, AT;                     // dense column-major and row-major
+    int ldt = 0;
     DBuf<int> cptr, cind, rptr, rcol;        // CSC / CSR
     DBuf<double> cval, rval;
     // working set
@@ -103,6 +104,8 @@ struct Engine {
     DBuf<int> head, bind;
     DBuf<double> bbar, cbar, gamma, tcol, trow, rho, rowp, u, s, h, wcol, ys, work, r1, r2, partial;
     DBuf<DState> st;
+    DBuf<int> rlist, rpos, rho_idx;
+    DBuf<double> rho_val, gpart;
     MatDev mat() const
     {
         MatDev M{};
@@ -110,13 +113,15 @@ struct Engine {
         M.A = A.p; M.lda = lda;
         M.cptr = cptr.p; M.cind = cind.p; M.cval = cval.p;
         M.rptr = rptr.p; M.rcol = rcol.p; M.rval = rval.p;
+        M.AT = dense ? AT.p : nullptr; M.ldt = ldt;
         int avg = n > 0 ? nnz / n : 0;
         M.lpc = avg >= 48 ? 64 : (avg >= 6 ? 8 : 1);
         return M;
     }
     ~Engine()
     {
-        A.release(); cptr.release(); cind.release(); rptr.release(); rcol.release(); cval.release(); rval.release();
+        A.release(); AT.release(); rlist.release(); rpos.release(); rho_idx.release(); rho_val.release();
+        gpart.release(); cptr.release(); cind.release(); rptr.release(); rcol.release(); cval.release(); rval.release();
         type.release(); orig_type.release(); stat.release(); refsp.release();
         lb.release(); ub.release(); coef.release(); orig_lb.release(); orig_ub.release(); obj.release();
         head.release(); bind.release();
@@ -132,6 +137,7 @@ struct gk_bfd {
     int valid = 0;
     int m = 0, ldb = 0;
     int upd_cnt = 0;
+    int ext_upd = 0;                           // updated through gk_bfd_update since the last re-inversion
     DBuf<double> Binv;
     // re-inversion scratch
     DBuf<double> C, X, Y, CinvR, BS, G, vecx, vecy, partial;
@@ -142,7 +148,7 @@ struct gk_bfd {
     gk_spx_stats stats{};
 };
 
-static const size_t PARTIAL_CAP = (size_t)1 << 20;   // >= splits * rows of every gemv (see gemv_plan)
+static const size_t PARTIAL_CAP = (size_t)1 << 22;   // >= splits * rows of every gemv (see gemv_plan, dual_plan)
 
 // ---------------------------------------------------------------------------
 // re-inversion of the basis matrix
@@ -216,6 +222,7 @@ static int reinvert_core(gk_bfd *f, const BasisSplit &bs, const MatDev *Adense, 
     HIPCHK(hipStreamSynchronize(s));
     f->valid = 1;
     f->upd_cnt = 0;
+    f->ext_upd = 0;
     f->stats.reinversions++;
     f->stats.seconds_reinvert += now_s() - t0;
     return 0;
@@ -266,6 +273,8 @@ static void engine_alloc(Engine &E, int m, int n)
     E.h.ensure(m); E.wcol.ensure(n); E.ys.ensure(m); E.work.ensure(std::max(m, n)); E.r1.ensure(m); E.r2.ensure(m);
     E.partial.ensure(PARTIAL_CAP);
     E.st.ensure(1);
+    E.rlist.ensure(m); E.rpos.ensure(m); E.rho_idx.ensure((size_t)m + 1); E.rho_val.ensure((size_t)m + 1);
+    E.gpart.ensure((size_t)(std::max(m, n) + 255) / 256 + 1);
 }
 
 __global__ void k_densify(const int *cptr, const int *cind, const double *cval, int n, double *A, int lda)
@@ -310,6 +319,9 @@ static void engine_upload_matrix(gk_bfd *f, const gk_lp *lp)
         E.A.ensure((size_t)E.lda * n);
         fill_d(s, E.A.p, 0.0, (size_t)E.lda * n);
         hipLaunchKernelGGL(k_densify, dim3(n), dim3(256), 0, s, E.cptr.p, E.cind.p, E.cval.p, n, E.A.p, E.lda);
+        E.ldt = (n + 7) & ~7;
+        E.AT.ensure((size_t)E.ldt * m);
+        transpose_dense(s, E.A.p, m, n, E.lda, E.AT.p, E.ldt);
     } else {
         // CSR copy (row order of entries does not matter numerically)
         std::vector<int> rptr(m + 1, 0), rcol(std::max(nnz, 1));
@@ -371,6 +383,8 @@ struct Spx {
         d.Binv = f->Binv.p; d.ldb = f->ldb;
         d.partial = E->partial.p; d.partial_cap = PARTIAL_CAP;
         d.st = E->st.p;
+        d.rlist = E->rlist.p; d.rpos = E->rpos.p; d.rho_idx = E->rho_idx.p; d.rho_val = E->rho_val.p;
+        d.gpart = E->gpart.p;
         return d;
     }
 
@@ -812,7 +826,21 @@ void Spx::init()
     up(E->lb, lb, mn - 1); up(E->ub, ub, mn - 1); up(E->orig_lb, orig_lb, mn - 1); up(E->orig_ub, orig_ub, mn - 1);
     up(E->coef, coef, mn - 1); up(E->obj, obj, n);
     up(E->head, head, mn - 1); up(E->bind, bind, mn - 1); up(E->stat, stat, n);
-    hs = DState{};
+    // dense columns of inv(B): the non-basic slacks
+    {
+        std::vector<int> rl, rp(m, -1);
+        for (int c = 1; c <= m; c++)
+            if (bind[c] > m) {
+                rp[c - 1] = (int)rl.size();
+                rl.push_back(c - 1);
+            }
+        if (!rl.empty()) HIPCHK(hipMemcpyAsync(E->rlist.p, rl.data(), rl.size() * sizeof(int), hipMemcpyHostToDevice, s));
+        HIPCHK(hipMemcpyAsync(E->rpos.p, rp.data(), (size_t)m * sizeof(int), hipMemcpyHostToDevice, s));
+        hs = DState{};
+        hs.nr = (int)rl.size();
+        sync();
+    }
+    if (f->ext_upd) f->valid = 0;    // unit columns may be inexact after external updates
     hs.phase = 0;
     hs.it_cnt = L->it_cnt;
     hs.zeta = zeta;
@@ -841,13 +869,16 @@ int Spx::batch(int K, int rigorous)
     push_state();
     SpxDev d = dev();
     const int pse = (parm->pricing == PT_PSE);
-    for (int t = 0; t < K; t++) {
-        if (dual) dual_iteration(s, d, pse, rigorous);
-        else primal_iteration(s, d, pse, rigorous);
+    if (dual) {
+        const DualPlan pl = dual_plan(d, hs.nr + K + 1, pse, rigorous);
+        for (int t = 0; t < K; t++) dual_iteration2(s, d, pl);
+    } else {
+        for (int t = 0; t < K; t++) primal_iteration(s, d, pse, rigorous);
     }
     pull_state();
     f->stats.batches++;
     f->stats.pivots += hs.npiv;
+    f->stats.bytes_pivots = hs.bytes;
     if (hs.npiv > 0) head_stale = vec_stale = true;
     // a stop on the budget leaves the top kernel of the next iteration unrun
     return hs.stop == ST_RUN ? ST_BATCH : hs.stop;
@@ -1389,6 +1420,7 @@ int gk_bfd_update(gk_bfd *f, int j, int len, const int *ind, int idx, const doub
         binv_rank1(s, f->Binv.p, m, f->ldb, f->G.p, f->vecy.p, j);
         HIPCHK(hipStreamSynchronize(s));
         f->upd_cnt++;
+        f->ext_upd = 1;
         return 0;
     } catch (const AbiError &e) {
         g_err = e.msg;
@@ -1441,8 +1473,19 @@ extern "C" double gk_bfd_time_kernel(gk_bfd *f, int which, int reps, double *byt
         double *scratch = nullptr;
         double b = 0.0;
         const double vec = 8.0;
+        DState hst{};
+        HIPCHK(hipMemcpyAsync(&hst, E.st.p, sizeof(DState), hipMemcpyDeviceToHost, s));
+        HIPCHK(hipStreamSynchronize(s));
+        SpxDev d{};
+        d.m = m; d.n = n; d.A = A; d.st = E.st.p; d.rho_idx = E.rho_idx.p; d.rho_val = E.rho_val.p;
+        d.partial = E.partial.p; d.partial_cap = PARTIAL_CAP;
+        const DualPlan pl = dual_plan(d, hst.ns, 0, 0);
+        const bool rows = (which == 0 && pl.rowpath && hst.ns > 0);
         switch (which) {
-        case 0: b = (A.dense ? 8.0 * m * (double)n : 12.0 * E.nnz) + vec * (m + 2.0 * n) + 4.0 * (m + n) + n; break;
+        case 0:
+            b = rows ? 8.0 * (double)hst.ns * n + 12.0 * hst.ns
+                     : (A.dense ? 8.0 * m * (double)n : 12.0 * E.nnz) + vec * (m + 2.0 * n) + 4.0 * (m + n) + n;
+            break;
         case 1: b = (A.dense ? 8.0 * m * (double)n : 12.0 * E.nnz) + vec * (n + 2.0 * m); break;
         case 2: b = 8.0 * m * (double)m + vec * 2.0 * m; break;
         case 3: b = 16.0 * m * (double)m + vec * 2.0 * m; break;
@@ -1458,8 +1501,11 @@ extern "C" double gk_bfd_time_kernel(gk_bfd *f, int which, int reps, double *byt
         HIPCHK(hipEventCreate(&e1));
         auto launch = [&]() {
             switch (which) {
-            case 0: colpass(s, A, CP_TROW, m, n, E.head.p, E.stat.p, E.coef.p, nullptr, E.rho.p, nullptr, E.trow.p,
-                            nullptr, nullptr); break;
+            case 0:
+                if (rows) launch_trow_rows(s, d, pl, hst.ns);
+                else colpass(s, A, CP_TROW, m, n, E.head.p, E.stat.p, E.coef.p, nullptr, E.rho.p, nullptr, E.trow.p,
+                             nullptr, nullptr);
+                break;
             case 1: aprod_neg(s, A, E.wcol.p, E.ys.p, E.work.p, E.partial.p, PARTIAL_CAP); break;
             case 2: gemv_n(s, f->Binv.p, m, m, f->ldb, E.h.p, E.partial.p, PARTIAL_CAP, E.tcol.p, 1.0, nullptr, 0.0); break;
             case 3: binv_rank1(s, scratch, m, f->ldb, E.rowp.p, E.tcol.p, 1); break;

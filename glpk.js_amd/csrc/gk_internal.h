@@ -46,11 +46,13 @@ struct DState {
     int phase, it_cnt, npiv, iter_left;
     int refct, upd_cnt, upd_lim, rigorous;
     int binv_fresh, cbar_fresh, pricing, rtest;
-    int refact_pending, pad0, pad1, pad2;
+    int refact_pending, nr, ns, nw;        // nr: dense columns of inv(B); ns: support of rho; nw: nonzeros of A w
+    int ce, pad0, pad1, pad2;               // ce: column of inv(B) that becomes the unit vector e_p (-1: none)
     double delta, teta, new_dq, cbar_q_new;
     double gamma_pq, eta_pq, pivot, xnq;
     double zeta, tol_bnd, tol_dj, tol_piv;
     double obj_ll, obj_ul, obj, tcol_max;
+    double cbar_q_old, bytes;               // bytes: algorithmic HBM bytes of the pivots so far
     unsigned long long trow_max_bits, tcol_max_bits;
 };
 
@@ -74,6 +76,7 @@ struct MatDev {
     const double *A; int lda;     // dense
     const int *cptr, *cind; const double *cval;   // CSC, 0-based rows
     const int *rptr, *rcol; const double *rval;   // CSR, 0-based cols
+    const double *AT; int ldt;    // dense: row-major copy (AT[r*ldt + c] = A[r, c]) for row-wise pivot rows
     int lpc;                      // lanes per column for CSC passes (1, 8 or 64)
 };
 
@@ -109,9 +112,27 @@ struct SpxDev {
     double *Binv; int ldb;
     double *partial; size_t partial_cap;
     DState *st;
+    // columns of inv(B) that are not unit vectors: inv(B) e_c = e_{bind[c]} for every
+    // basic slack c, so only the nr columns rlist[0..nr) (the non-basic slacks) are dense
+    int *rlist, *rpos;
+    int *rho_idx; double *rho_val;          // rho in compact form, ns entries
+    double *gpart;                           // per-block partial sums of the pivot-row pass
 };
 
-void dual_iteration(hipStream_t s, const SpxDev &d, int pse, int rigorous);
+// launch geometry of one device batch, fixed on the host from nr at batch start
+struct DualPlan {
+    int pse, rigorous;
+    int rowpath;                  // 1: pivot row by rows of AT over the support of rho
+    int tsplits;                  // row path: splits over the support of rho
+    int fsplits;                  // FTRAN over the dense columns of inv(B): splits
+    int uchunks;                  // rank-1 update: column chunks
+};
+DualPlan dual_plan(const SpxDev &d, int nr_max, int pse, int rigorous);
+void dual_iteration2(hipStream_t s, const SpxDev &d, const DualPlan &pl);
+void transpose_dense(hipStream_t s, const double *A, int m, int n, int lda, double *AT, int ldt);
+// timing hook: the row-path pivot-row kernel alone (returns algorithmic bytes)
+double launch_trow_rows(hipStream_t s, const SpxDev &d, const DualPlan &pl, int ns);
+
 void primal_iteration(hipStream_t s, const SpxDev &d, int pse, int rigorous);
 void launch_reset_refsp(hipStream_t s, const SpxDev &d, int dual);
 

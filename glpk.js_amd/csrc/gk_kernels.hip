@@ -8,150 +8,13 @@
 // Reductions that choose an index reproduce the reference's first-hit scans
 // (strict comparisons, glpspx01.js:681, glpspx02.js:617/:865/:921) with a
 // lowest-index tie-break; sums are fixed-order (deterministic run to run).
-#include "gk_internal.h"
+#include "gk_device.h"
 #include <cfloat>
 #include <cstdio>
 #include <algorithm>
 
 namespace gk {
 
-#define GATE(st, need_p)                                                   \
-    if ((st) != nullptr) {                                                 \
-        if ((st)->stop) return;                                            \
-        if ((need_p) && (st)->p <= 0) return;                              \
-    }
-
-static constexpr int WG = 1024;       // single-workgroup control kernels
-static constexpr double DBL_EPS = 2.220446049250313e-16;   // glpapi.js:7
-
-__device__ __forceinline__ double wsum(double v)
-{
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
-    return v;
-}
-
-__device__ __forceinline__ double wmax(double v)
-{
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v = fmax(v, __shfl_xor(v, o));
-    return v;
-}
-
-// block-wide reductions for blockDim.x <= 1024 (16 waves)
-__device__ double block_sum(double v, double *sh)
-{
-    int lane = threadIdx.x & 63, w = threadIdx.x >> 6, nw = (blockDim.x + 63) >> 6;
-    v = wsum(v);
-    __syncthreads();
-    if (lane == 0) sh[w] = v;
-    __syncthreads();
-    double r = 0.0;
-    if (w == 0) {
-        r = lane < nw ? sh[lane] : 0.0;
-        r = wsum(r);
-        if (lane == 0) sh[0] = r;
-    }
-    __syncthreads();
-    r = sh[0];
-    __syncthreads();
-    return r;
-}
-
-__device__ double block_max(double v, double *sh)
-{
-    int lane = threadIdx.x & 63, w = threadIdx.x >> 6, nw = (blockDim.x + 63) >> 6;
-    v = wmax(v);
-    __syncthreads();
-    if (lane == 0) sh[w] = v;
-    __syncthreads();
-    double r = 0.0;
-    if (w == 0) {
-        r = lane < nw ? sh[lane] : 0.0;
-        r = wmax(r);
-        if (lane == 0) sh[0] = r;
-    }
-    __syncthreads();
-    r = sh[0];
-    __syncthreads();
-    return r;
-}
-
-__device__ int block_or(int v, int *sh)
-{
-    __syncthreads();
-    if (threadIdx.x == 0) sh[0] = 0;
-    __syncthreads();
-    if (v) sh[0] = 1;
-    __syncthreads();
-    int r = sh[0];
-    __syncthreads();
-    return r;
-}
-
-// candidate of an index-choosing scan: key1 (primary), key2 (secondary), idx
-struct Cand {
-    double k1, k2;
-    int idx, aux;
-};
-
-// mode 0: max k1, tie lowest idx                   (chuzr dual / chuzc primal)
-// mode 1: min k1, then max k2, tie lowest idx       (Harris pass 1)
-// mode 2: max k2, tie lowest idx                    (Harris pass 2)
-template <int MODE>
-__device__ __forceinline__ bool better(const Cand &a, const Cand &b)
-{
-    if (a.idx == 0) return false;
-    if (b.idx == 0) return true;
-    if (MODE == 0) {
-        if (a.k1 != b.k1) return a.k1 > b.k1;
-    } else if (MODE == 1) {
-        if (a.k1 != b.k1) return a.k1 < b.k1;
-        if (a.k2 != b.k2) return a.k2 > b.k2;
-    } else {
-        if (a.k2 != b.k2) return a.k2 > b.k2;
-    }
-    return a.idx < b.idx;
-}
-
-template <int MODE>
-__device__ Cand block_best(Cand c, Cand *sh)
-{
-    int lane = threadIdx.x & 63, w = threadIdx.x >> 6, nw = (blockDim.x + 63) >> 6;
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-        Cand d;
-        d.k1 = __shfl_xor(c.k1, o);
-        d.k2 = __shfl_xor(c.k2, o);
-        d.idx = __shfl_xor(c.idx, o);
-        d.aux = __shfl_xor(c.aux, o);
-        if (better<MODE>(d, c)) c = d;
-    }
-    __syncthreads();
-    if (lane == 0) sh[w] = c;
-    __syncthreads();
-    if (w == 0) {
-        Cand r;
-        if (lane < nw) r = sh[lane];
-        else { r.k1 = 0; r.k2 = 0; r.idx = 0; r.aux = 0; }
-#pragma unroll
-        for (int o = 32; o > 0; o >>= 1) {
-            Cand d;
-            d.k1 = __shfl_xor(r.k1, o);
-            d.k2 = __shfl_xor(r.k2, o);
-            d.idx = __shfl_xor(r.idx, o);
-            d.aux = __shfl_xor(r.aux, o);
-            if (better<MODE>(d, r)) r = d;
-        }
-        if (lane == 0) sh[0] = r;
-    }
-    __syncthreads();
-    Cand r = sh[0];
-    __syncthreads();
-    return r;
-}
-
-__device__ __forceinline__ unsigned long long dbits(double v) { return (unsigned long long)__double_as_longlong(v); }
 
 // =====================================================================
 // dense GEMV, y = beta*base + alpha * M x (zero x entries skipped)
@@ -215,19 +78,32 @@ __global__ void __launch_bounds__(256) k_gemv_n_part(const double *__restrict__ 
     }
 }
 
-__global__ void __launch_bounds__(256) k_gemv_reduce(const double *__restrict__ part, int rows, int splits,
+// y[r] = beta*base[r] + alpha * sum_s part[s][r]: 64 rows per block, the 8
+// waves take splits w, w+8, ... and combine in LDS in a fixed order
+__global__ void __launch_bounds__(512) k_gemv_reduce(const double *__restrict__ part, int rows, int splits,
                                                        double *__restrict__ y, double alpha,
                                                        const double *__restrict__ base, double beta,
                                                        const DState *st, int need_p)
 {
     GATE(st, need_p);
-    const int r = blockIdx.x * 256 + threadIdx.x;
-    if (r >= rows) return;
+    __shared__ double sh[8][64];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int r = blockIdx.x * 64 + lane;
     double acc = 0.0;
-    for (int s = 0; s < splits; ++s) acc += part[(size_t)s * rows + r];
-    double v = alpha * acc;
-    if (base) v = beta * base[r] + v;
-    y[r] = v;
+    if (r < rows) {
+#pragma unroll 4
+        for (int s = w; s < splits; s += 8) acc += part[(size_t)s * rows + r];
+    }
+    sh[w][lane] = acc;
+    __syncthreads();
+    if (w == 0 && r < rows) {
+        double v = sh[0][lane];
+#pragma unroll
+        for (int k = 1; k < 8; ++k) v += sh[k][lane];
+        v *= alpha;
+        if (base) v = beta * base[r] + v;
+        y[r] = v;
+    }
 }
 
 static void gemv_n_gated(hipStream_t s, const double *M, int rows, int cols, int ld, const double *x,
@@ -247,7 +123,7 @@ static void gemv_n_gated(hipStream_t s, const double *M, int rows, int cols, int
     } else {
         p.splits = 0;
     }
-    hipLaunchKernelGGL(k_gemv_reduce, dim3((rows + 255) / 256), dim3(256), 0, s, partial, rows, p.splits, y, alpha,
+    hipLaunchKernelGGL(k_gemv_reduce, dim3((rows + 63) / 64), dim3(512), 0, s, partial, rows, p.splits, y, alpha,
                        base, beta, st, need_p);
 }
 
@@ -299,17 +175,17 @@ void gemv_t(hipStream_t s, const double *M, int rows, int cols, int ld, const do
 // (eval_trow1 glpspx02.js:655, eval_cost glpspx01.js:531, error_btran
 // glpspx01.js:265, update_gamma's N'[j] u glpspx01.js:1231-1241)
 // =====================================================================
-__device__ __forceinline__ void colpass_emit(int mode, int i, int k, int m, const signed char *stat,
-                                             const double *coef, const double *h, double d1, double d2,
-                                             double *out1, double *out2, unsigned long long *maxbits)
+// returns |out1[i]| for CP_TROW (folded into one atomic max per block)
+__device__ __forceinline__ double colpass_emit(int mode, int i, int k, int m, const signed char *stat,
+                                               const double *coef, const double *h, double d1, double d2,
+                                               double *out1, double *out2)
 {
     // d1 = N . x, d2 = N . y
     switch (mode) {
     case CP_TROW: {
         double v = (stat && stat[i] == NS) ? 0.0 : -d1;
         out1[i] = v;
-        if (maxbits && v != 0.0) atomicMax(maxbits, dbits(fabs(v)));
-        break;
+        return fabs(v);
     }
     case CP_CBAR: out1[i] = coef[k - 1] - d1; break;
     case CP_RESID: out1[i] = h[i] - d1; break;
@@ -321,6 +197,14 @@ __device__ __forceinline__ void colpass_emit(int mode, int i, int k, int m, cons
     }
     default: out1[i] = d1; break;
     }
+    return 0.0;
+}
+
+__device__ __forceinline__ void block_atomic_max(double v, unsigned long long *maxbits)
+{
+    __shared__ double shm[16];
+    const double b = block_max(v, shm);
+    if (threadIdx.x == 0 && b > 0.0) atomicMax(maxbits, dbits(b));
 }
 
 template <int TWO>
@@ -335,6 +219,7 @@ __global__ void __launch_bounds__(256) k_colpass_dense(int mode, int m, int off,
     const int lane = threadIdx.x & 63;
     const int wv = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
     const int nw = (gridDim.x * blockDim.x) >> 6;
+    double vmax = 0.0;
     for (int i = wv; i < cnt; i += nw) {
         const int k = head[off + i];
         double d1 = 0.0, d2 = 0.0;
@@ -360,8 +245,9 @@ __global__ void __launch_bounds__(256) k_colpass_dense(int mode, int m, int off,
             d1 = -wsum(a1);
             if (TWO) d2 = -wsum(a2);
         }
-        if (lane == 0) colpass_emit(mode, i, k, m, stat, coef, h, d1, d2, out1, out2, maxbits);
+        if (lane == 0) vmax = fmax(vmax, colpass_emit(mode, i, k, m, stat, coef, h, d1, d2, out1, out2));
     }
+    if (maxbits) block_atomic_max(vmax, maxbits);
 }
 
 // CSC columns with LPC lanes per column (LPC = 1, 8 or 64)
@@ -379,6 +265,7 @@ __global__ void __launch_bounds__(256) k_colpass_csc(int mode, int m, int off, i
     const int grp = (blockIdx.x * blockDim.x + threadIdx.x) / LPC;
     const int ngrp = (gridDim.x * blockDim.x) / LPC;
     const int nit = (cnt + ngrp - 1) / ngrp;      // uniform trip count (shuffles need all lanes)
+    double vmax = 0.0;
     for (int it = 0; it < nit; ++it) {
         const int i = grp + it * ngrp;
         const bool act = i < cnt;
@@ -410,11 +297,12 @@ __global__ void __launch_bounds__(256) k_colpass_csc(int mode, int m, int off, i
             }
             if (structural) { d1 = s1; d2 = s2; }
         }
-        if (act && sub == 0) colpass_emit(mode, i, k, m, stat, coef, h, d1, d2, out1, out2, maxbits);
+        if (act && sub == 0) vmax = fmax(vmax, colpass_emit(mode, i, k, m, stat, coef, h, d1, d2, out1, out2));
     }
+    if (maxbits) block_atomic_max(vmax, maxbits);
 }
 
-static void colpass_gated(hipStream_t s, const MatDev &A, int mode, int off, int cnt, const int *head,
+void colpass_gated(hipStream_t s, const MatDev &A, int mode, int off, int cnt, const int *head,
                           const signed char *stat, const double *coef, const double *h, const double *x,
                           const double *y, double *out1, double *out2, unsigned long long *maxbits,
                           const DState *st, int need_p)
@@ -466,7 +354,7 @@ __global__ void __launch_bounds__(256) k_csr_neg(int m, const int *__restrict__ 
     y[r] = (base ? base[r] : 0.0) - acc;
 }
 
-static void aprod_neg_gated(hipStream_t s, const MatDev &A, const double *w, const double *base, double *y,
+void aprod_neg_gated(hipStream_t s, const MatDev &A, const double *w, const double *base, double *y,
                             double *partial, size_t cap, const DState *st, int need_p)
 {
     if (A.dense)
@@ -566,16 +454,6 @@ void cb_vector(hipStream_t s, int m, const int *head, const double *coef, double
     hipLaunchKernelGGL(k_cb, dim3((m + 255) / 256), dim3(256), 0, s, m, head, coef, cB);
 }
 
-__device__ __forceinline__ double get_xN(const signed char *stat, const double *lb, const double *ub, int k, int j)
-{
-    // glpspx01.js:442
-    switch (stat[j - 1]) {
-    case NL: return lb[k - 1];
-    case NU: return ub[k - 1];
-    case NF: return 0.0;
-    default: return lb[k - 1];
-    }
-}
 
 // w[j] = -xN[j] for the non-basic positions (eval_beta, glpspx01.js:483-505)
 __global__ void k_neg_xn(int m, int n, const int *head, const signed char *stat, const double *lb, const double *ub,
@@ -592,27 +470,6 @@ void neg_xn_weights(hipStream_t s, const SpxDev &d, double *w)
     hipLaunchKernelGGL(k_neg_xn, dim3((d.n + 255) / 256), dim3(256), 0, s, d.m, d.n, d.head, d.stat, d.lb, d.ub, w);
 }
 
-// reset_refsp (glpspx01.js:586 / glpspx02.js:497)
-__device__ void reset_refsp_dev(const SpxDev &d, int dual)
-{
-    const int m = d.m, n = d.n;
-    for (int k = threadIdx.x; k < m + n; k += blockDim.x) d.refsp[k] = 0;
-    __syncthreads();
-    if (dual) {
-        for (int i = threadIdx.x; i < m; i += blockDim.x) {
-            d.refsp[d.head[i] - 1] = 1;
-            d.gamma[i] = 1.0;
-        }
-    } else {
-        for (int j = threadIdx.x; j < n; j += blockDim.x) {
-            d.refsp[d.head[m + j] - 1] = 1;
-            d.gamma[j] = 1.0;
-        }
-    }
-    __syncthreads();
-    if (threadIdx.x == 0) d.st->refct = 1000;
-    __syncthreads();
-}
 
 __global__ void __launch_bounds__(WG) k_reset_refsp(SpxDev d, int dual) { reset_refsp_dev(d, dual); }
 
@@ -621,290 +478,6 @@ void launch_reset_refsp(hipStream_t s, const SpxDev &d, int dual)
     hipLaunchKernelGGL(k_reset_refsp, dim3(1), dim3(WG), 0, s, d, dual);
 }
 
-// h = -N[q] (eval_tcol, glpspx01.js:702-719); runs inside a single workgroup
-__device__ void build_hq(const SpxDev &d, int q)
-{
-    const int m = d.m;
-    const int k = d.head[m + q - 1];
-    for (int i = threadIdx.x; i < m; i += blockDim.x) d.h[i] = 0.0;
-    __syncthreads();
-    if (k <= m) {
-        if (threadIdx.x == 0) d.h[k - 1] = -1.0;
-    } else {
-        const int c = k - m - 1;
-        if (d.A.dense) {
-            const double *col = d.A.A + (size_t)c * d.A.lda;
-            for (int i = threadIdx.x; i < m; i += blockDim.x) d.h[i] = col[i];
-        } else {
-            for (int t = d.A.cptr[c] + threadIdx.x; t < d.A.cptr[c + 1]; t += blockDim.x) d.h[d.A.cind[t]] = d.A.cval[t];
-        }
-    }
-    __syncthreads();
-}
-
-// =====================================================================
-// dual simplex pivot (glpspx02.js main loop :1614-1966)
-// =====================================================================
-__global__ void __launch_bounds__(WG) k_dual_top(SpxDev d)
-{
-    __shared__ double shd[16];
-    __shared__ int shi[2];
-    __shared__ Cand shc[16];
-    DState *st = d.st;
-    if (st->stop) return;
-    const int m = d.m, n = d.n;
-    if (st->iter_left <= 0 || st->refact_pending) {
-        __syncthreads();
-        if (threadIdx.x == 0) st->stop = st->refact_pending ? ST_REFACT : ST_BATCH;
-        return;
-    }
-    if (st->pricing == PT_PSE && st->refct == 0) reset_refsp_dev(d, 1);
-    // phase I: dual feasibility reached? (check_feas, :1296)
-    if (st->phase == 1) {
-        const double tol = st->tol_dj;
-        int bad = 0;
-        for (int j = threadIdx.x; j < n && !bad; j += blockDim.x) {
-            const int k = d.head[m + j];
-            const double cb = d.cbar[j];
-            const int ot = d.orig_type[k - 1];
-            if (cb < -tol && (ot == LO || ot == FR)) bad = 1;
-            if (cb > +tol && (ot == UP || ot == FR)) bad = 1;
-        }
-        if (!block_or(bad, shi)) {
-            if (threadIdx.x == 0) st->stop = ST_PHASE;
-            return;
-        }
-    } else {
-        // objective limits (:1729-1760)
-        const double z = st->zeta, obj = st->obj;
-        bool hit = (z < 0.0 && st->obj_ll > -DBL_MAX && obj <= st->obj_ll) ||
-                   (z > 0.0 && st->obj_ul < +DBL_MAX && obj >= st->obj_ul);
-        if (hit) {
-            __syncthreads();
-            if (threadIdx.x == 0) st->stop = ST_OBJLIM;
-            return;
-        }
-    }
-    // chuzr (:572): p = argmax r_i^2 / gamma_i over bound violations
-    const double tol_bnd = st->tol_bnd;
-    Cand c; c.k1 = 0.0; c.k2 = 0.0; c.idx = 0; c.aux = 0;
-    for (int i = threadIdx.x; i < m; i += blockDim.x) {
-        const int k = d.head[i];
-        const int t = d.type[k - 1];
-        const double bb = d.bbar[i];
-        double ri = 0.0;
-        if (t == LO || t == DB || t == FX) {
-            const double eps = tol_bnd * (1.0 + 0.10 * fabs(d.lb[k - 1]));
-            if (bb < d.lb[k - 1] - eps) ri = d.lb[k - 1] - bb;
-        }
-        if (t == UP || t == DB || t == FX) {
-            const double eps = tol_bnd * (1.0 + 0.10 * fabs(d.ub[k - 1]));
-            if (bb > d.ub[k - 1] + eps) ri = d.ub[k - 1] - bb;
-        }
-        if (ri == 0.0) continue;
-        double g = d.gamma[i];
-        if (g < DBL_EPS) g = DBL_EPS;
-        const double temp = (ri * ri) / g;
-        Cand e; e.k1 = temp; e.k2 = ri; e.idx = i + 1; e.aux = 0;
-        if (temp > 0.0 && better<0>(e, c)) c = e;
-    }
-    Cand best = block_best<0>(c, shc);
-    if (best.idx == 0) {
-        if (threadIdx.x == 0) { st->p = 0; st->stop = ST_P0; }
-        return;
-    }
-    const int p = best.idx;
-    // rho = row p of inv(B) (eval_rho, :627: B' rho = e_p)
-    for (int l = threadIdx.x; l < m; l += blockDim.x) {
-        const double v = d.Binv[(size_t)(p - 1) + (size_t)l * d.ldb];
-        d.rho[l] = v;
-        d.rowp[l] = v;
-    }
-    if (threadIdx.x == 0) {
-        st->p = p;
-        st->delta = best.k2;
-        st->trow_max_bits = 0ull;
-    }
-    (void)shd;
-}
-
-__global__ void __launch_bounds__(WG) k_dual_chuzc(SpxDev d)
-{
-    __shared__ Cand shc[16];
-    __shared__ double shd[16];
-    DState *st = d.st;
-    if (st->stop) return;
-    const int m = d.m, n = d.n;
-    const double big = __longlong_as_double((long long)st->trow_max_bits);
-    const double eps = st->tol_bnd * (1.0 + 0.01 * big);     // sort_trow with tol_bnd (:1851)
-    const double delta = st->delta;
-    const double s = (delta > 0.0 ? +1.0 : -1.0);
-    const double rtol = (st->rtest == RT_HAR) ? 0.30 * st->tol_dj : 0.0;
-    // pass 1 (:820-869)
-    Cand c; c.k1 = DBL_MAX; c.k2 = 0.0; c.idx = 0; c.aux = 0;
-    for (int j = threadIdx.x; j < n; j += blockDim.x) {
-        const double tr = d.trow[j];
-        if (tr == 0.0 || fabs(tr) < eps) continue;
-        const double alfa = s * tr;
-        const int sj = d.stat[j];
-        double t;
-        if (alfa > 0.0) {
-            if (sj == NL || sj == NF) t = (d.cbar[j] + rtol) / alfa; else continue;
-        } else {
-            if (sj == NU || sj == NF) t = (d.cbar[j] - rtol) / alfa; else continue;
-        }
-        if (t < 0.0) t = 0.0;
-        Cand e; e.k1 = t; e.k2 = fabs(alfa); e.idx = j + 1; e.aux = 0;
-        if (better<1>(e, c)) c = e;
-    }
-    Cand b1 = block_best<1>(c, shc);
-    int q = b1.idx;
-    double teta = (q ? b1.k1 : DBL_MAX);
-    if (!(rtol == 0.0 || q == 0 || teta == 0.0)) {
-        const double tmax = teta;
-        Cand c2; c2.k1 = 0.0; c2.k2 = 0.0; c2.idx = 0; c2.aux = 0;
-        for (int j = threadIdx.x; j < n; j += blockDim.x) {
-            const double tr = d.trow[j];
-            if (tr == 0.0 || fabs(tr) < eps) continue;
-            const double alfa = s * tr;
-            const int sj = d.stat[j];
-            double t;
-            if (alfa > 0.0) {
-                if (sj == NL || sj == NF) t = d.cbar[j] / alfa; else continue;
-            } else {
-                if (sj == NU || sj == NF) t = d.cbar[j] / alfa; else continue;
-            }
-            if (t < 0.0) t = 0.0;
-            if (!(t <= tmax)) continue;
-            Cand e; e.k1 = t; e.k2 = fabs(alfa); e.idx = j + 1; e.aux = 0;
-            if (better<2>(e, c2)) c2 = e;
-        }
-        Cand b2 = block_best<2>(c2, shc);
-        q = b2.idx;
-        teta = b2.k1;
-    }
-    if (q == 0) {
-        if (threadIdx.x == 0) { st->q = 0; st->stop = ST_Q0; }
-        return;
-    }
-    const double piv = d.trow[q - 1];
-    if (fabs(piv) < 1e-5 * (1.0 + 0.01 * big) && !st->rigorous) {
-        __syncthreads();
-        if (threadIdx.x == 0) { st->q = q; st->stop = ST_SMALLPIV; }
-        return;
-    }
-    // gamma_p for the dual steepest-edge update (update_gamma, :1103-1132)
-    if (st->pricing == PT_PSE) {
-        double acc = 0.0;
-        for (int j = threadIdx.x; j < n; j += blockDim.x) {
-            const double t = d.trow[j];
-            if (t != 0.0 && d.refsp[d.head[m + j] - 1]) acc += t * t;
-        }
-        acc = block_sum(acc, shd);
-        if (threadIdx.x == 0) {
-            const double eta = d.refsp[d.head[st->p - 1] - 1] ? 1.0 : 0.0;
-            st->eta_pq = eta;
-            st->gamma_pq = eta + acc;
-        }
-    }
-    build_hq(d, q);
-    if (threadIdx.x == 0) {
-        st->q = q;
-        st->new_dq = s * teta;
-    }
-}
-
-__global__ void k_dual_pivot(SpxDev d)
-{
-    DState *st = d.st;
-    if (st->stop || threadIdx.x != 0) return;
-    const int m = d.m, p = st->p, q = st->q;
-    const double piv1 = d.tcol[p - 1], piv2 = d.trow[q - 1];
-    if (fabs(piv1 - piv2) > 1e-8 * (1.0 + fabs(piv1)) || !((piv1 > 0.0 && piv2 > 0.0) || (piv1 < 0.0 && piv2 < 0.0))) {
-        if (!st->binv_fresh || !st->rigorous) { st->stop = ST_PIVCHK; return; }
-        d.tcol[p - 1] = piv2;
-    }
-    const double tp = d.tcol[p - 1];
-    const double delta = st->delta;
-    st->teta = delta / tp;
-    const int kq = d.head[m + q - 1];
-    st->xnq = get_xN(d.stat, d.lb, d.ub, kq, q);
-    if (st->phase == 2) st->obj += (d.cbar[q - 1] / st->zeta) * (delta / tp);
-    st->pivot = tp;
-}
-
-// update_bbar (:1042), update_cbar (:1020) and the PSE weight vectors
-__global__ void __launch_bounds__(256) k_dual_update(SpxDev d)
-{
-    DState *st = d.st;
-    if (st->stop) return;
-    const int m = d.m, n = d.n, p = st->p, q = st->q;
-    const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    const double teta = st->teta, new_dq = st->new_dq;
-    if (i < m) {
-        if (i == p - 1) d.bbar[i] = st->xnq + teta;
-        else if (teta != 0.0) d.bbar[i] += d.tcol[i] * teta;
-    }
-    if (i < n) {
-        if (i == q - 1) d.cbar[i] = new_dq;
-        else if (new_dq != 0.0) d.cbar[i] -= d.trow[i] * new_dq;
-    }
-    if (st->pricing == PT_PSE) {
-        // u := sum over refsp non-basics of N[j] trow[j]; slack part in ys, columns in wcol
-        if (i < n) {
-            const int pos = d.bind[m + i];
-            d.wcol[i] = (pos > m && d.refsp[m + i]) ? d.trow[pos - m - 1] : 0.0;
-        }
-        if (i < m) {
-            const int pos = d.bind[i];
-            d.ys[i] = (pos > m && d.refsp[i]) ? d.trow[pos - m - 1] : 0.0;
-        }
-    }
-}
-
-// update_gamma (:1075) after u := inv(B) u
-__global__ void __launch_bounds__(256) k_dual_gamma(SpxDev d)
-{
-    DState *st = d.st;
-    if (st->stop || st->pricing != PT_PSE) return;
-    const int m = d.m, p = st->p, q = st->q;
-    const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= m) return;
-    const double pivot = d.tcol[p - 1];
-    const double gamma_p = st->gamma_pq, eta_p = st->eta_pq;
-    const double ti = d.tcol[i];
-    const int k = d.head[i];
-    const int kq = d.head[m + q - 1];
-    double g = d.gamma[i];
-    if (i == p - 1) {
-        if (d.type[kq - 1] == FR) g = 1.0;
-        else {
-            g = gamma_p / (pivot * pivot);
-            if (g < DBL_EPS) g = DBL_EPS;
-        }
-    } else if (ti != 0.0 && d.type[k - 1] != FR) {
-        const double t = ti / pivot;
-        const double t1 = g + t * t * gamma_p + 2.0 * t * d.u[i];
-        const double t2 = (d.refsp[k - 1] ? 1.0 : 0.0) + eta_p * t * t;
-        g = (t1 >= t2 ? t1 : t2);
-        if (g < DBL_EPS) g = DBL_EPS;
-    }
-    const int kp = d.head[p - 1];
-    if (d.type[kp - 1] == FX && d.refsp[kp - 1] && ti != 0.0) {
-        double t = 0.0;
-        bool apply = true;
-        if (i == p - 1) {
-            if (d.type[kq - 1] == FR) apply = false; else t = 1.0 / pivot;
-        } else {
-            if (d.type[k - 1] == FR) apply = false; else t = ti / pivot;
-        }
-        if (apply) {
-            g -= t * t;
-            if (g < DBL_EPS) g = DBL_EPS;
-        }
-    }
-    d.gamma[i] = g;
-}
 
 // =====================================================================
 // rank-1 update of inv(B) plus the end-of-pivot bookkeeping
@@ -965,9 +538,15 @@ __global__ void __launch_bounds__(256) k_binv_update(SpxDev d, int dual)
         const double f0 = (r == p - 1) ? 1.0 / tp : d.tcol[r] / tp;
         const double f1 = two ? ((r + 1 == p - 1) ? 1.0 / tp : d.tcol[r + 1] / tp) : 0.0;
         const bool z0 = (r == p - 1), z1 = (r + 1 == p - 1);
+        const int ce = st->ce;
         for (int c = c0; c < c1; ++c) {
             const double rl = d.rowp[c];
             double *ptr = d.Binv + (size_t)c * d.ldb + r;
+            if (c == ce) {            // an entering slack's column is exactly e_p
+                ptr[0] = z0 ? 1.0 : 0.0;
+                if (two) ptr[1] = z1 ? 1.0 : 0.0;
+                continue;
+            }
             if (two) {
                 double2 v = *(double2 *)ptr;
                 v.x = (z0 ? 0.0 : v.x) - f0 * rl;
@@ -1049,7 +628,7 @@ __global__ void k_gscatter(int m, int off, int cnt, const int *__restrict__ head
 static inline dim3 g1(int n) { return dim3((std::max(n, 1) + 255) / 256); }
 
 // refine_tcol (glpspx01.js:732 / glpspx02.js:979): tcol += inv(B) (h - B tcol)
-static void refine_tcol_dev(hipStream_t s, const SpxDev &d, int need_p)
+void refine_tcol_dev(hipStream_t s, const SpxDev &d, int need_p)
 {
     const int m = d.m, n = d.n;
     hipLaunchKernelGGL(k_gfill, g1(m), dim3(256), 0, s, d.r1, 0.0, m, d.st, need_p);
@@ -1062,37 +641,13 @@ static void refine_tcol_dev(hipStream_t s, const SpxDev &d, int need_p)
 }
 
 // refine_rho (glpspx01.js:1044 / glpspx02.js:641): rho += inv(B') (e_p - B' rho)
-static void refine_rho_dev(hipStream_t s, const SpxDev &d)
+void refine_rho_dev(hipStream_t s, const SpxDev &d)
 {
     const int m = d.m;
     hipLaunchKernelGGL(k_unit_p, g1(m), dim3(256), 0, s, d.r2, m, d.st);
     colpass_gated(s, d.A, CP_RESID, 0, m, d.head, d.stat, d.coef, d.r2, d.rho, nullptr, d.r1, nullptr, nullptr, d.st, 1);
     gemv_t_gated(s, d.Binv, m, m, d.ldb, d.r1, d.r2, 1.0, d.st, 1);
     hipLaunchKernelGGL(k_axpy, g1(m), dim3(256), 0, s, d.rho, d.r2, 1.0, m, d.st, 1);
-}
-
-void dual_iteration(hipStream_t s, const SpxDev &d, int pse, int rigorous)
-{
-    const int m = d.m, n = d.n;
-    hipLaunchKernelGGL(k_dual_top, dim3(1), dim3(WG), 0, s, d);
-    if (rigorous) refine_rho_dev(s, d);
-    // trow[j] = -rho . N[j] over the non-basic columns (eval_trow1, :655)
-    colpass_gated(s, d.A, CP_TROW, m, n, d.head, d.stat, d.coef, nullptr, d.rho, nullptr, d.trow, nullptr,
-                  &d.st->trow_max_bits, d.st, 0);
-    hipLaunchKernelGGL(k_dual_chuzc, dim3(1), dim3(WG), 0, s, d);
-    // tcol = inv(B) h, h = -N[q] (eval_tcol, :937)
-    gemv_n_gated(s, d.Binv, m, m, d.ldb, d.h, d.partial, d.partial_cap, d.tcol, 1.0, nullptr, 0.0, d.st, 0);
-    if (rigorous) refine_tcol_dev(s, d, 0);
-    hipLaunchKernelGGL(k_dual_pivot, dim3(1), dim3(64), 0, s, d);
-    int g = (std::max(m, n) + 255) / 256;
-    hipLaunchKernelGGL(k_dual_update, dim3(g), dim3(256), 0, s, d);
-    if (pse) {
-        // u = inv(B) (ys - A wcol)  (update_gamma, :1103-1134)
-        aprod_neg_gated(s, d.A, d.wcol, d.ys, d.work, d.partial, d.partial_cap, d.st, 0);
-        gemv_n_gated(s, d.Binv, m, m, d.ldb, d.work, d.partial, d.partial_cap, d.u, 1.0, nullptr, 0.0, d.st, 0);
-        hipLaunchKernelGGL(k_dual_gamma, dim3((m + 255) / 256), dim3(256), 0, s, d);
-    }
-    hipLaunchKernelGGL(k_binv_update, binv_grid(m), dim3(256), 0, s, d, 1);
 }
 
 // =====================================================================
@@ -1319,6 +874,7 @@ __global__ void k_primal_pivot(SpxDev d)
     }
     const int kq = d.head[m + q - 1];
     st->xnq = get_xN(d.stat, d.lb, d.ub, kq, q);
+    st->ce = (kq <= m) ? kq - 1 : -1;
     if (p > 0) {
         const double pivot = d.trow[q - 1];
         const double new_dq = d.cbar[q - 1] / pivot;

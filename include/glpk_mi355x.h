@@ -131,6 +131,7 @@ int gk_spx_dual(gk_ctx *ctx, gk_lp *lp, gk_bfd *bfd, const gk_smcp *parm);
 typedef struct {
     long long pivots, reinversions, batches, host_syncs;
     double seconds_total, seconds_reinvert;
+    double bytes_pivots;        /* algorithmic HBM bytes the pivots had to move */
 } gk_spx_stats;
 void gk_bfd_last_stats(const gk_bfd *bfd, gk_spx_stats *st);
 
@@ -138,7 +139,9 @@ void gk_bfd_last_stats(const gk_bfd *bfd, gk_spx_stats *st);
  * launch one engine kernel `reps` times on the problem left resident by the
  * last gk_spx_* call, bracketed by two HIP events on the engine's stream,
  * and return the average milliseconds per launch (or < 0 on error).
- *   which 0: pricing pass trow = -rho' N over the non-basic columns
+ *   which 0: pivot-row pass trow = -rho' N as the engine runs it at the
+ *            current basis (rows of A in the support of rho when that is
+ *            at most m/2 rows and A is dense, else the column pass)
  *         1: A w product of the dual steepest-edge update
  *         2: inv(B) x product (FTRAN)
  *         3: rank-1 update of inv(B) (on a scratch copy)
