@@ -13,32 +13,105 @@
 // copy AT), reading 8 * ns * n bytes instead of 8 * m * n.  With the basis
 // growing from the slack basis, nr is the number of basic structurals.
 //
-// Kernel sequence of one pivot (each gated on st->stop):
-//   k_dual_top      1 WG   chuzr (:572), rho, reference-space reset
-//   k_lgemv_part    grid   trow partials over rows of AT     (eval_trow :655-791)
-//   k_trow_finish   grid   trow, max|trow|, PSE vectors, gamma_p partials
-//   k_dual_chuzc    1 WG   Harris ratio test (:820-950), gamma_p, h = -N[q]
-//   [PSE] A w       grid   (update_gamma :1103-1134)
-//   k_lgemv_part    grid   tcol = inv(B) h, u = inv(B)(ys - A w)  (eval_tcol :937)
-//   k_lgemv_reduce  grid
-//   k_dual_commit   grid   pivot check (:1913), update_bbar/cbar/gamma, rank-1 update of inv(B)
-//   k_dual_finish   1 WG   change_basis (:1954-1964), list of dense columns, counters
+// A pivot is seven kernels, each gated on st->stop; the decisions that need
+// the whole of a vector are prepared as per-block candidates by the kernel
+// that produces the vector, so that no kernel rescans m or n entries in one
+// workgroup:
+//   k_dual_top     1 WG  change_basis of the previous pivot (:1954-1964),
+//                        reference-space reset (:497), phase-I / limit checks,
+//                        chuzr (:572) from the candidates of k_dual_commit,
+//                        rho = row p of inv(B) (eval_rho :627)
+//   k_lgemv_part   grid  trow partials over the rows of AT      (eval_trow :655-791)
+//   k_trow_finish  grid  trow, max|trow|, PSE vectors, gamma_p partials,
+//                        Harris pass-1 candidates per block     (:820-869)
+//   k_dual_ratio   grid  pass-1 choice, pass-2 candidates (:870-950); A w over
+//                        the reference-space columns            (update_gamma :1103-1134)
+//   k_dual_ftran   grid  pass-2 choice, h = -N[q], tcol = inv(B) h and
+//                        u = inv(B)(ys - A w) over the dense columns (eval_tcol :937)
+//   k_dual_ftran_reduce
+//   k_dual_commit  grid  pivot check (:1913-1933), update_bbar/cbar/gamma
+//                        (:1020-1134), rank-1 update of inv(B); chuzr candidates
+//                        and the phase-I check of the next iteration
 #include "gk_device.h"
 #include <algorithm>
 
 namespace gk {
 
+static inline int cdiv(int a, int b) { return (a + b - 1) / b; }
+__device__ __forceinline__ int gv_of(int m, int n) { return (max(m, n) + 255) / 256; }
+__device__ __forceinline__ Cand *cand_chuzr(const SpxDev &d) { return (Cand *)d.cand; }
+__device__ __forceinline__ Cand *cand_pass1(const SpxDev &d) { return (Cand *)d.cand + gv_of(d.m, d.n); }
+__device__ __forceinline__ Cand *cand_pass2(const SpxDev &d) { return (Cand *)d.cand + 2 * gv_of(d.m, d.n); }
+__device__ __forceinline__ Cand no_cand(double k1)
+{
+    Cand c; c.k1 = k1; c.k2 = 0.0; c.idx = 0; c.aux = 0;
+    return c;
+}
+
 // ---------------------------------------------------------------------------
-// list GEMV partials:
-//   part[(s*NRHS + k)*rows + r] = sum over t in chunk s of M[col_t*ld + r] * x_k(t)
-// col_t = list[t]; XBYT: x_1(t) = x1[t] (compact values), else x_k(t) = xk[col_t].
-// 512 rows per block (2 per lane, 16-byte loads); chunk s = blockIdx.y.
+// list GEMV of one 512-row tile over list entries [t0, t1):
+//   o[k*rows + r] = sum_t M[list[t]*ld + r] * x_k(t, list[t])
+// r + 1 < ld always (ld is a multiple of 8 and r even), so the 16-byte load
+// stays inside the allocation even for the last odd row.
 // ---------------------------------------------------------------------------
-template <int NRHS, int XBYT>
+template <int NRHS, typename XF>
+__device__ __forceinline__ void lgemv_tile(const double *__restrict__ M, size_t ld, int rows,
+                                           const int *__restrict__ list, int t0, int t1, int r, XF xf,
+                                           double *__restrict__ o)
+{
+    if (r >= rows) return;
+    double a0 = 0.0, a1 = 0.0, b0 = 0.0, b1 = 0.0;
+    int t = t0;
+    for (; t + 4 <= t1; t += 4) {
+        int c[4];
+        double xa[4], xb[4];
+        bool any = false;
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            c[u] = list[t + u];
+            xf(t + u, c[u], xa[u], xb[u]);
+            any = any || xa[u] != 0.0 || xb[u] != 0.0;
+        }
+        if (!any) continue;
+        double2 v[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) v[u] = *(const double2 *)(M + (size_t)c[u] * ld + r);
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            a0 += v[u].x * xa[u];
+            a1 += v[u].y * xa[u];
+            if (NRHS == 2) {
+                b0 += v[u].x * xb[u];
+                b1 += v[u].y * xb[u];
+            }
+        }
+    }
+    for (; t < t1; ++t) {
+        const int c = list[t];
+        double xa, xb;
+        xf(t, c, xa, xb);
+        if (xa == 0.0 && xb == 0.0) continue;
+        const double2 v = *(const double2 *)(M + (size_t)c * ld + r);
+        a0 += v.x * xa;
+        a1 += v.y * xa;
+        if (NRHS == 2) {
+            b0 += v.x * xb;
+            b1 += v.y * xb;
+        }
+    }
+    o[r] = a0;
+    if (r + 1 < rows) o[r + 1] = a1;
+    if (NRHS == 2) {
+        o[rows + r] = b0;
+        if (r + 1 < rows) o[rows + r + 1] = b1;
+    }
+}
+
+// trow partials: part[s*n + c] = sum over the support of rho in chunk s of rho_i A[i, c]
 __global__ void __launch_bounds__(256) k_lgemv_part(const double *__restrict__ M, size_t ld, int rows,
                                                       const int *__restrict__ list, const int *cntp,
-                                                      const double *__restrict__ x1, const double *__restrict__ x2,
-                                                      double *__restrict__ part, const DState *st)
+                                                      const double *__restrict__ xv, double *__restrict__ part,
+                                                      const DState *st)
 {
     if (st && st->stop) return;
     const int cnt = *cntp;
@@ -46,131 +119,266 @@ __global__ void __launch_bounds__(256) k_lgemv_part(const double *__restrict__ M
     const int lps = (cnt + splits - 1) / splits;
     const int t0 = blockIdx.y * lps, t1 = min(cnt, t0 + lps);
     const int r = (blockIdx.x * 256 + threadIdx.x) * 2;
-    double a0 = 0.0, a1 = 0.0, b0 = 0.0, b1 = 0.0;
-    if (r < rows) {
-        // r + 1 < ld always (ld is a multiple of 8 and r is even), so the
-        // 16-byte load stays inside the allocation even for the last odd row
-        int t = t0;
-        for (; t + 4 <= t1; t += 4) {
-            int c[4];
-            double xa[4], xb[4];
-            bool any = false;
-#pragma unroll
-            for (int u = 0; u < 4; ++u) {
-                c[u] = list[t + u];
-                xa[u] = XBYT ? x1[t + u] : x1[c[u]];
-                xb[u] = (NRHS == 2) ? x2[c[u]] : 0.0;
-                any = any || xa[u] != 0.0 || xb[u] != 0.0;
-            }
-            if (!any) continue;
-            double2 v[4];
-#pragma unroll
-            for (int u = 0; u < 4; ++u) v[u] = *(const double2 *)(M + (size_t)c[u] * ld + r);
-#pragma unroll
-            for (int u = 0; u < 4; ++u) {
-                a0 += v[u].x * xa[u];
-                a1 += v[u].y * xa[u];
-                if (NRHS == 2) {
-                    b0 += v[u].x * xb[u];
-                    b1 += v[u].y * xb[u];
-                }
-            }
-        }
-        for (; t < t1; ++t) {
-            const int c = list[t];
-            const double xa = XBYT ? x1[t] : x1[c];
-            const double xb = (NRHS == 2) ? x2[c] : 0.0;
-            if (xa == 0.0 && xb == 0.0) continue;
-            const double2 v = *(const double2 *)(M + (size_t)c * ld + r);
-            a0 += v.x * xa;
-            a1 += v.y * xa;
-            if (NRHS == 2) {
-                b0 += v.x * xb;
-                b1 += v.y * xb;
-            }
-        }
-        double *o = part + (size_t)blockIdx.y * NRHS * rows + r;
-        o[0] = a0;
-        if (r + 1 < rows) o[1] = a1;
-        if (NRHS == 2) {
-            o[rows] = b0;
-            if (r + 1 < rows) o[rows + 1] = b1;
-        }
-    }
+    lgemv_tile<1>(M, ld, rows, list, t0, t1, r,
+                  [&](int t, int, double &xa, double &xb) { xa = xv[t]; xb = 0.0; },
+                  part + (size_t)blockIdx.y * rows);
 }
 
-// tcol[i] = sum_s part + (unit column of a basic slack at position i) h,
-// u[i] likewise with w — inv(B) x = sum over the dense columns + x[head[i]]
-// for basic slack head[i].  64 rows per block, 8 waves over the splits,
-// combined in a fixed order.
-template <int NRHS>
-__global__ void __launch_bounds__(512) k_lgemv_reduce(const double *__restrict__ part, int m, int splits,
-                                                        const int *__restrict__ head,
-                                                        const double *__restrict__ x1, const double *__restrict__ x2,
-                                                        double *__restrict__ y1, double *__restrict__ y2,
-                                                        const DState *st)
+// ---------------------------------------------------------------------------
+// the Harris ratio test pieces (glpspx02.js:820-950)
+// ---------------------------------------------------------------------------
+struct RatioCtx {
+    double eps, s, rtol;
+};
+
+__device__ __forceinline__ RatioCtx ratio_ctx(const DState *st, double big)
 {
-    if (st && st->stop) return;
-    __shared__ double sh[NRHS][8][64];
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    const int r = blockIdx.x * 64 + lane;
-    double a = 0.0, b = 0.0;
-    if (r < m) {
-#pragma unroll 4
-        for (int s = w; s < splits; s += 8) {
-            a += part[(size_t)s * NRHS * m + r];
-            if (NRHS == 2) b += part[(size_t)s * NRHS * m + m + r];
+    RatioCtx x;
+    x.eps = st->tol_bnd * (1.0 + 0.01 * big);     // sort_trow with tol_bnd (:1851)
+    x.s = (st->delta > 0.0 ? +1.0 : -1.0);
+    x.rtol = (st->rtest == RT_HAR) ? 0.30 * st->tol_dj : 0.0;
+    return x;
+}
+
+__device__ __forceinline__ double trow_big(const DState *st)
+{
+    return __longlong_as_double((long long)st->trow_max_bits);
+}
+
+__device__ __forceinline__ bool pass1_cand(const RatioCtx &x, double tr, double cb, int sj, int j, Cand &e)
+{
+    if (tr == 0.0 || fabs(tr) < x.eps) return false;
+    const double alfa = x.s * tr;
+    double t;
+    if (alfa > 0.0) {
+        if (sj == NL || sj == NF) t = (cb + x.rtol) / alfa; else return false;
+    } else {
+        if (sj == NU || sj == NF) t = (cb - x.rtol) / alfa; else return false;
+    }
+    if (t < 0.0) t = 0.0;
+    e.k1 = t; e.k2 = fabs(alfa); e.idx = j + 1; e.aux = 0;
+    return true;
+}
+
+__device__ __forceinline__ bool pass2_cand(const RatioCtx &x, double tr, double cb, int sj, int j, double tmax, Cand &e)
+{
+    if (tr == 0.0 || fabs(tr) < x.eps) return false;
+    const double alfa = x.s * tr;
+    double t;
+    if (alfa > 0.0) {
+        if (sj == NL || sj == NF) t = cb / alfa; else return false;
+    } else {
+        if (sj == NU || sj == NF) t = cb / alfa; else return false;
+    }
+    if (t < 0.0) t = 0.0;
+    if (!(t <= tmax)) return false;
+    e.k1 = t; e.k2 = fabs(alfa); e.idx = j + 1; e.aux = 0;
+    return true;
+}
+
+// pass-1 candidate of the non-basic variable(s) handled by thread slot idx
+// of k_trow_finish (structural column idx and slack row idx)
+__device__ __forceinline__ Cand pass1_slot(const SpxDev &d, const RatioCtx &x, int idx)
+{
+    const int m = d.m, n = d.n;
+    Cand best = no_cand(DBL_MAX);
+    if (idx < n) {
+        const int pos = d.bind[m + idx];
+        if (pos > m) {
+            const int j = pos - m - 1;
+            Cand e;
+            if (pass1_cand(x, d.trow[j], d.cbar[j], d.stat[j], j, e) && better<1>(e, best)) best = e;
         }
     }
-    sh[0][w][lane] = a;
-    if (NRHS == 2) sh[NRHS - 1][w][lane] = b;
+    if (idx < m) {
+        const int pos = d.bind[idx];
+        if (pos > m) {
+            const int j = pos - m - 1;
+            Cand e;
+            if (pass1_cand(x, d.trow[j], d.cbar[j], d.stat[j], j, e) && better<1>(e, best)) best = e;
+        }
+    }
+    return best;
+}
+
+// ---------------------------------------------------------------------------
+// change_basis (glpspx02.js:1954-1964) of the committed pivot, plus the lists
+// of dense inv(B) columns and of reference-space non-basic structurals.
+// Called by a whole block (>= 4 threads); four threads do independent parts.
+// ---------------------------------------------------------------------------
+__device__ void dual_finish_block(const SpxDev &d, int rowpath, double bytes_fixed)
+{
+    DState *st = d.st;
+    const int pend = st->pend;
+    const int role = threadIdx.x;
+    const int m = d.m, n = d.n;
+    int p = 0, q = 0, kp = 0, kq = 0, nr0 = 0, nwl0 = 0, ns = 0, tkp = 0, refkp = 0, wq = -1, rq = -1;
+    if (pend && role < 4) {
+        p = st->p; q = st->q;
+        kp = d.head[p - 1];
+        kq = d.head[m + q - 1];
+        nr0 = st->nr; nwl0 = st->nwl; ns = st->ns;
+        tkp = d.type[kp - 1];
+        refkp = d.refsp[kp - 1];
+        if (kq > m) wq = d.wpos[kq - m - 1];
+        if (kq <= m) rq = d.rpos[kq - 1];
+    }
     __syncthreads();
-    if (w == 0 && r < m) {
-        double va = sh[0][0][lane], vb = (NRHS == 2) ? sh[NRHS - 1][0][lane] : 0.0;
-#pragma unroll
-        for (int k = 1; k < 8; ++k) {
-            va += sh[0][k][lane];
-            if (NRHS == 2) vb += sh[NRHS - 1][k][lane];
+    if (pend && role == 0) {
+        d.head[p - 1] = kq;
+        d.head[m + q - 1] = kp;
+        d.bind[kq - 1] = p;
+        d.bind[kp - 1] = m + q;
+        if (tkp == FX) d.stat[q - 1] = NS;
+        else if (st->delta > 0.0) d.stat[q - 1] = NL;
+        else d.stat[q - 1] = NU;
+    } else if (pend && role == 1) {
+        int nr = nr0;
+        if (kq <= m) {           // entering slack: its column is now e_p
+            const int last = d.rlist[nr - 1];
+            d.rlist[rq] = last;
+            d.rpos[last] = rq;
+            d.rpos[kq - 1] = -1;
+            nr--;
         }
-        const int kh = head[r];
-        if (kh <= m) {
-            va += x1[kh - 1];
-            if (NRHS == 2) vb += x2[kh - 1];
+        if (kp <= m) {           // leaving slack: its column became dense
+            d.rlist[nr] = kp - 1;
+            d.rpos[kp - 1] = nr;
+            nr++;
         }
-        y1[r] = va;
-        if (NRHS == 2) y2[r] = vb;
+        st->nr = nr;
+    } else if (pend && role == 2 && st->pricing == PT_PSE) {
+        if (tkp == FX && refkp) {
+            d.refsp[kp - 1] = 0;
+            refkp = 0;
+        }
+        int nwl = nwl0;
+        if (wq >= 0) {
+            const int last = d.wlist[nwl - 1];
+            d.wlist[wq] = last;
+            d.wpos[last] = wq;
+            d.wpos[kq - m - 1] = -1;
+            nwl--;
+        }
+        if (kp > m && refkp) {
+            d.wlist[nwl] = kp - m - 1;
+            d.wpos[kp - m - 1] = nwl;
+            nwl++;
+        }
+        st->nwl = nwl;
+        if (st->refct > 0) st->refct--;
+    } else if (pend && role == 3) {
+        if (st->phase == 2) st->obj += (st->cbar_q_old / st->zeta) * (st->delta / st->pivot);
+        st->upd_cnt++;
+        st->binv_fresh = 0;
+        st->cbar_fresh = 0;
+        if (st->upd_cnt >= st->upd_lim) st->refact_pending = 1;
+        st->it_cnt++;
+        st->npiv++;
+        st->iter_left--;
+        if (st->rigorous > 0) st->rigorous--;
+        st->pend = 0;
+        // algorithmic HBM bytes of this pivot: the pivot row (rows of A in the
+        // support of rho, or all of A), A w over the reference-space columns,
+        // inv(B) once for both right-hand sides, read + write of the updated
+        // columns, and the O(m + n) vectors
+        const double rowb = rowpath ? 8.0 * (double)ns * n : 8.0 * (double)m * n;
+        st->bytes += rowb + 8.0 * (double)m * nwl0 + 8.0 * (double)m * (nr0 + 1) +
+                     16.0 * (double)m * (nr0 + (kp <= m ? 1 : 0)) + bytes_fixed;
+    }
+    __syncthreads();
+}
+
+__global__ void k_dual_finish(SpxDev d, int rowpath, double bytes_fixed)
+{
+    dual_finish_block(d, rowpath, bytes_fixed);
+}
+
+// chuzr candidate of basic position i (glpspx02.js:572-626)
+__device__ __forceinline__ Cand chuzr_cand_v(int i, int t, double lb, double ub, double bb, double g, double tol_bnd)
+{
+    double ri = 0.0;
+    if (t == LO || t == DB || t == FX) {
+        const double eps = tol_bnd * (1.0 + 0.10 * fabs(lb));
+        if (bb < lb - eps) ri = lb - bb;
+    }
+    if (t == UP || t == DB || t == FX) {
+        const double eps = tol_bnd * (1.0 + 0.10 * fabs(ub));
+        if (bb > ub + eps) ri = ub - bb;
+    }
+    Cand e = no_cand(0.0);
+    if (ri == 0.0) return e;
+    if (g < DBL_EPS) g = DBL_EPS;
+    const double temp = (ri * ri) / g;
+    if (temp > 0.0) { e.k1 = temp; e.k2 = ri; e.idx = i + 1; }
+    return e;
+}
+
+// check_feas (glpspx02.js:1296): dual infeasibility of non-basic j
+__device__ __forceinline__ int dual_bad(const SpxDev &d, int k, double cb, double tol)
+{
+    const int ot = d.orig_type[k - 1];
+    if (cb < -tol && (ot == LO || ot == FR)) return 1;
+    if (cb > +tol && (ot == UP || ot == FR)) return 1;
+    return 0;
+}
+
+// batch start: chuzr candidates and the phase-I check of the current state
+__global__ void __launch_bounds__(256) k_dual_prep(SpxDev d)
+{
+    __shared__ Cand shc[16];
+    DState *st = d.st;
+    const int m = d.m, n = d.n;
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    const bool reset = (st->pricing == PT_PSE && st->refct == 0);
+    if ((int)blockIdx.x * 256 < m) {
+        Cand c = no_cand(0.0);
+        if (i < m) {
+            const int k = d.head[i];
+            c = chuzr_cand_v(i, d.type[k - 1], d.lb[k - 1], d.ub[k - 1], d.bbar[i], reset ? 1.0 : d.gamma[i],
+                             st->tol_bnd);
+        }
+        const Cand b = block_best<0>(c, shc);
+        if (threadIdx.x == 0) cand_chuzr(d)[blockIdx.x] = b;
+    }
+    if (st->phase == 1) {
+        const int bad = (i < n) ? dual_bad(d, d.head[m + i], d.cbar[i], st->tol_dj) : 0;
+        if (__syncthreads_or(bad) && threadIdx.x == 0) atomicOr(&st->dinf, 1);
     }
 }
 
 // ---------------------------------------------------------------------------
-// k_dual_top: phase/limit checks, chuzr (glpspx02.js:572) and rho = row p of
-// inv(B) (eval_rho :627) from the dense columns plus the unit entry
+// k_dual_top
 // ---------------------------------------------------------------------------
-__global__ void __launch_bounds__(WG) k_dual_top(SpxDev d)
+__global__ void __launch_bounds__(WG) k_dual_top(SpxDev d, int rowpath, double bytes_fixed)
 {
-    __shared__ int shi[2];
     __shared__ Cand shc[16];
     DState *st = d.st;
     if (st->stop) return;
     const int m = d.m, n = d.n;
+    // the next pivot's chuzr candidates are already final: load them while
+    // the previous pivot's change_basis is applied
+    const int gm = (m + 255) / 256;
+    Cand c = no_cand(0.0);
+    for (int b = threadIdx.x; b < gm; b += blockDim.x) {
+        const Cand e = cand_chuzr(d)[b];
+        if (better<0>(e, c)) c = e;
+    }
+    dual_finish_block(d, rowpath, bytes_fixed);
     if (st->iter_left <= 0 || st->refact_pending) {
         __syncthreads();
         if (threadIdx.x == 0) st->stop = st->refact_pending ? ST_REFACT : ST_BATCH;
         return;
     }
-    if (st->pricing == PT_PSE && st->refct == 0) reset_refsp_dev(d, 1);
+    if (st->pricing == PT_PSE && st->refct == 0) {
+        reset_refsp_dev(d, 1);             // refsp := basic variables, gamma := 1
+        for (int l = threadIdx.x; l < n; l += blockDim.x) d.wpos[l] = -1;
+        if (threadIdx.x == 0) st->nwl = 0;
+        __syncthreads();
+    }
     if (st->phase == 1) {
-        // check_feas (:1296)
-        const double tol = st->tol_dj;
-        int bad = 0;
-        for (int j = threadIdx.x; j < n && !bad; j += blockDim.x) {
-            const int k = d.head[m + j];
-            const double cb = d.cbar[j];
-            const int ot = d.orig_type[k - 1];
-            if (cb < -tol && (ot == LO || ot == FR)) bad = 1;
-            if (cb > +tol && (ot == UP || ot == FR)) bad = 1;
-        }
-        if (!block_or(bad, shi)) {
+        if (!st->dinf) {
+            __syncthreads();
             if (threadIdx.x == 0) st->stop = ST_PHASE;
             return;
         }
@@ -185,29 +393,7 @@ __global__ void __launch_bounds__(WG) k_dual_top(SpxDev d)
             return;
         }
     }
-    // chuzr: p = argmax r_i^2 / gamma_i over bound violations
-    const double tol_bnd = st->tol_bnd;
-    Cand c; c.k1 = 0.0; c.k2 = 0.0; c.idx = 0; c.aux = 0;
-    for (int i = threadIdx.x; i < m; i += blockDim.x) {
-        const int k = d.head[i];
-        const int t = d.type[k - 1];
-        const double bb = d.bbar[i];
-        double ri = 0.0;
-        if (t == LO || t == DB || t == FX) {
-            const double eps = tol_bnd * (1.0 + 0.10 * fabs(d.lb[k - 1]));
-            if (bb < d.lb[k - 1] - eps) ri = d.lb[k - 1] - bb;
-        }
-        if (t == UP || t == DB || t == FX) {
-            const double eps = tol_bnd * (1.0 + 0.10 * fabs(d.ub[k - 1]));
-            if (bb > d.ub[k - 1] + eps) ri = d.ub[k - 1] - bb;
-        }
-        if (ri == 0.0) continue;
-        double g = d.gamma[i];
-        if (g < DBL_EPS) g = DBL_EPS;
-        const double temp = (ri * ri) / g;
-        Cand e; e.k1 = temp; e.k2 = ri; e.idx = i + 1; e.aux = 0;
-        if (temp > 0.0 && better<0>(e, c)) c = e;
-    }
+    // chuzr from the per-block candidates
     const Cand best = block_best<0>(c, shc);
     if (best.idx == 0) {
         if (threadIdx.x == 0) { st->p = 0; st->stop = ST_P0; }
@@ -242,7 +428,7 @@ __global__ void __launch_bounds__(WG) k_dual_top(SpxDev d)
         st->delta = best.k2;
         st->trow_max_bits = 0ull;
         st->ns = ns;
-        st->nw = 0;
+        st->dinf = 0;
     }
 }
 
@@ -251,214 +437,311 @@ __global__ void __launch_bounds__(WG) k_dual_top(SpxDev d)
 // FROM_PART: trow from the row-path partials (structurals) and -rho (slacks);
 // else trow was written by the column pass.  Also the PSE vectors of
 // update_gamma (:1103-1134): wcol[c] / ys[c] = trow of a non-basic variable of
-// the reference space, and per-block sums of those trow^2 (gamma_p).
+// the reference space, per-block sums of those trow^2 (gamma_p), and the
+// block's Harris pass-1 candidate under the block-local significance
+// tolerance (k_dual_ratio re-checks it against the global one).
 // ---------------------------------------------------------------------------
 template <int FROM_PART>
 __global__ void __launch_bounds__(256) k_trow_finish(SpxDev d, const double *__restrict__ part, int splits, int pse)
 {
     __shared__ double shd[16];
-    __shared__ double shm[16];
+    __shared__ Cand shc[16];
     DState *st = d.st;
     if (st->stop) return;
     const int m = d.m, n = d.n;
     const int idx = blockIdx.x * blockDim.x + threadIdx.x;
-    double vmax = 0.0, gsum = 0.0, nwc = 0.0;
-    if (idx < n) {
-        const int c = idx;
-        const int pos = d.bind[m + c];
-        double tv = 0.0;
-        if (pos > m) {
-            const int j = pos - m - 1;
-            if (FROM_PART) {
-                double acc = 0.0;
+    // all gathers first (bind -> stat/cbar/refsp/partials), reductions after
+    const int pos1 = (idx < n) ? d.bind[m + idx] : 0;
+    const int pos2 = (idx < m) ? d.bind[idx] : 0;
+    const int j1 = (pos1 > m) ? pos1 - m - 1 : -1;
+    const int j2 = (pos2 > m) ? pos2 - m - 1 : -1;
+    int s1 = 0, s2 = 0;
+    double cb1 = 0.0, cb2 = 0.0, tv1 = 0.0, tv2 = 0.0;
+    bool ref1 = false, ref2 = false;
+    if (j1 >= 0) {
+        s1 = d.stat[j1];
+        cb1 = d.cbar[j1];
+        if (FROM_PART) {
+            double acc = 0.0;
 #pragma unroll 8
-                for (int s = 0; s < splits; ++s) acc += part[(size_t)s * n + c];
-                tv = (d.stat[j] == NS) ? 0.0 : acc;
-                d.trow[j] = tv;
-            } else
-                tv = d.trow[j];
-            vmax = fabs(tv);
-        }
-        if (pse) {
-            const bool ref = pos > m && d.refsp[m + c];
-            const double w = ref ? tv : 0.0;
-            d.wcol[c] = w;
-            gsum += w * w;
-            nwc += (w != 0.0) ? 1.0 : 0.0;
-        }
+            for (int s = 0; s < splits; ++s) acc += part[(size_t)s * n + idx];
+            tv1 = acc;
+        } else
+            tv1 = d.trow[j1];
+        if (pse) ref1 = d.refsp[m + idx] != 0;
     }
-    if (idx < m) {
-        const int c = idx;
-        const int pos = d.bind[c];
-        double tv = 0.0;
-        if (pos > m) {
-            const int j = pos - m - 1;
-            if (FROM_PART) {
-                tv = (d.stat[j] == NS) ? 0.0 : -d.rho[c];
-                d.trow[j] = tv;
-            } else
-                tv = d.trow[j];
-            vmax = fmax(vmax, fabs(tv));
-        }
-        if (pse) {
-            const double w = (pos > m && d.refsp[c]) ? tv : 0.0;
-            d.ys[c] = w;
-            gsum += w * w;
-        }
+    if (j2 >= 0) {
+        s2 = d.stat[j2];
+        cb2 = d.cbar[j2];
+        tv2 = FROM_PART ? -d.rho[idx] : d.trow[j2];
+        if (pse) ref2 = d.refsp[idx] != 0;
     }
     if (FROM_PART) {
-        const double b = block_max(vmax, shm);
-        if (threadIdx.x == 0 && b > 0.0) atomicMax(&st->trow_max_bits, dbits(b));
+        if (s1 == NS) tv1 = 0.0;
+        if (s2 == NS) tv2 = 0.0;
+        if (j1 >= 0) d.trow[j1] = tv1;
+        if (j2 >= 0) d.trow[j2] = tv2;
     }
+    double gsum = 0.0;
+    if (pse) {
+        const double w1 = ref1 ? tv1 : 0.0, w2 = ref2 ? tv2 : 0.0;
+        if (idx < n) d.wcol[idx] = w1;
+        if (idx < m) d.ys[idx] = w2;
+        gsum = w1 * w1 + w2 * w2;
+    }
+    const double bmax = block_max(fmax(fabs(tv1), fabs(tv2)), shd);
+    if (FROM_PART && threadIdx.x == 0 && bmax > 0.0) atomicMax(&st->trow_max_bits, dbits(bmax));
     if (pse) {
         const double g = block_sum(gsum, shd);
-        const double k = block_sum(nwc, shd);
-        if (threadIdx.x == 0) {
-            d.gpart[blockIdx.x] = g;
-            if (k > 0.0) atomicAdd(&st->nw, (int)k);
+        if (threadIdx.x == 0) d.gpart[blockIdx.x] = g;
+    }
+    // pass-1 candidate with eps_b = tol_bnd (1 + 0.01 max_b) <= eps
+    const RatioCtx x = ratio_ctx(st, bmax);
+    Cand c = no_cand(DBL_MAX);
+    Cand e;
+    if (j1 >= 0 && pass1_cand(x, tv1, cb1, s1, j1, e) && better<1>(e, c)) c = e;
+    if (j2 >= 0 && pass1_cand(x, tv2, cb2, s2, j2, e) && better<1>(e, c)) c = e;
+    const Cand b = block_best<1>(c, shc);
+    if (threadIdx.x == 0) cand_pass1(d)[blockIdx.x] = b;
+}
+
+// ---------------------------------------------------------------------------
+// k_dual_ratio: blocks [0, gn) — pass-1 choice from the block candidates
+// (a block whose candidate fails the global significance tolerance is
+// rescanned), then the pass-2 candidates of positions [256 b, 256 b + 256);
+// blocks [gn, ...) — partials of A w over the reference-space columns.
+// ---------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) k_dual_ratio(SpxDev d, int gn, int tiles_m, int aw)
+{
+    __shared__ Cand shc[16];
+    __shared__ int shf[2];
+    DState *st = d.st;
+    if (st->stop) return;
+    const int m = d.m, n = d.n;
+    if ((int)blockIdx.x >= gn) {
+        const int b = blockIdx.x - gn;
+        const int tile = b % tiles_m, split = b / tiles_m, splits = (gridDim.x - gn) / tiles_m;
+        const int cnt = st->nwl;
+        const int lps = (cnt + splits - 1) / splits;
+        const int t0 = split * lps, t1 = min(cnt, t0 + lps);
+        const int r = (tile * 256 + threadIdx.x) * 2;
+        const double *wc = d.wcol;
+        lgemv_tile<1>(d.A.A, (size_t)d.A.lda, m, d.wlist, t0, t1, r,
+                      [&](int, int c, double &xa, double &xb) { xa = wc[c]; xb = 0.0; },
+                      d.awpart + (size_t)split * m);
+        return;
+    }
+    const RatioCtx x = ratio_ctx(st, trow_big(st));
+    const int gv = gv_of(m, n);
+    const int j = blockIdx.x * blockDim.x + threadIdx.x;
+    const double trj = (j < n) ? d.trow[j] : 0.0;
+    const double cbj = (j < n) ? d.cbar[j] : 0.0;
+    const int sj = (j < n) ? d.stat[j] : 0;
+    Cand c = no_cand(DBL_MAX);
+    int fail = 0;
+    for (int b = threadIdx.x; b < gv; b += blockDim.x) {
+        const Cand e = cand_pass1(d)[b];
+        if (e.idx != 0 && e.k2 < x.eps) fail = 1;
+        else if (better<1>(e, c)) c = e;
+    }
+    if (__syncthreads_or(fail)) {
+        // rare: rescan the blocks whose candidate is not significant
+        for (int b = 0; b < gv; ++b) {
+            const Cand e = cand_pass1(d)[b];
+            if (!(e.idx != 0 && e.k2 < x.eps)) continue;
+            const Cand f = pass1_slot(d, x, b * 256 + threadIdx.x);
+            if (better<1>(f, c)) c = f;
         }
     }
+    const Cand b1 = block_best<1>(c, shc);
+    const int q1 = b1.idx;
+    const double teta1 = q1 ? b1.k1 : DBL_MAX;
+    const int need2 = !(x.rtol == 0.0 || q1 == 0 || teta1 == 0.0);
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        st->q1 = q1;
+        st->teta1 = teta1;
+        st->need2 = need2;
+    }
+    (void)shf;
+    (void)aw;
+    if (!need2) return;
+    Cand c2 = no_cand(0.0);
+    if (j < n) {
+        Cand e;
+        if (pass2_cand(x, trj, cbj, sj, j, teta1, e)) c2 = e;
+    }
+    const Cand b2 = block_best<2>(c2, shc);
+    if (threadIdx.x == 0) cand_pass2(d)[blockIdx.x] = b2;
+}
+
+// the entering choice q (pass 2 if needed), its checks and the st fields;
+// every block of the calling grid evaluates it identically.  Returns q, or 0
+// when the iteration stops.
+__device__ int dual_pick(const SpxDev &d, Cand *shc, double *shd, int pse, int gn)
+{
+    DState *st = d.st;
+    int q;
+    double teta;
+    if (st->need2) {
+        Cand c = no_cand(0.0);
+        for (int b = threadIdx.x; b < gn; b += blockDim.x) {
+            const Cand e = cand_pass2(d)[b];
+            if (better<2>(e, c)) c = e;
+        }
+        const Cand b2 = block_best<2>(c, shc);
+        q = b2.idx;
+        teta = b2.k1;
+    } else {
+        q = st->q1;
+        teta = st->teta1;
+    }
+    const bool lead = (blockIdx.x == 0 && blockIdx.y == 0);
+    if (q == 0) {
+        __syncthreads();
+        if (lead && threadIdx.x == 0) { st->q = 0; st->stop = ST_Q0; }
+        return 0;
+    }
+    const double big = trow_big(st);
+    const double piv = d.trow[q - 1];
+    if (fabs(piv) < 1e-5 * (1.0 + 0.01 * big) && !st->rigorous) {
+        __syncthreads();
+        if (lead && threadIdx.x == 0) { st->q = q; st->stop = ST_SMALLPIV; }
+        return 0;
+    }
+    if (lead) {
+        if (pse) {
+            // gamma_p (update_gamma :1103-1132) from the per-block sums, fixed order
+            const int gv = gv_of(d.m, d.n);
+            double g = 0.0;
+            for (int b = threadIdx.x; b < gv; b += blockDim.x) g += d.gpart[b];
+            g = block_sum(g, shd);
+            if (threadIdx.x == 0) {
+                const double eta = d.refsp[d.head[st->p - 1] - 1] ? 1.0 : 0.0;
+                st->eta_pq = eta;
+                st->gamma_pq = eta + g;
+            }
+        }
+        if (threadIdx.x == 0) {
+            st->q = q;
+            st->new_dq = (st->delta > 0.0 ? +1.0 : -1.0) * teta;
+            st->cbar_q_old = d.cbar[q - 1];
+        }
+    }
+    return q;
+}
+
+// sparse A / rigorous mode: the pick and h = -N[q] in one workgroup
+__global__ void __launch_bounds__(1024) k_dual_pick(SpxDev d, int pse, int gn)
+{
+    __shared__ Cand shc[16];
+    __shared__ double shd[16];
+    if (d.st->stop) return;
+    const int q = dual_pick(d, shc, shd, pse, gn);
+    if (q) build_hq(d, q);
+}
+
+// work_c = ys_c - (A w)_c from the partials, fixed order
+__device__ __forceinline__ double aw_value(const SpxDev &d, int c, int awsplits)
+{
+    double acc = 0.0;
+    for (int s = 0; s < awsplits; ++s) acc += d.awpart[(size_t)s * d.m + c];
+    return d.ys[c] - acc;
 }
 
 // ---------------------------------------------------------------------------
-// k_dual_chuzc: Harris two-pass ratio test over the pivot row (glpspx02.js
-// :820-950, significance filter with tol_bnd as sort_trow :1851), gamma_p
-// (update_gamma :1103-1132), h = -N[q] (eval_tcol :937).  One workgroup; for
-// n <= 16 * 1024 the row is held in registers across both passes.
+// k_dual_ftran: tcol = inv(B) h, u = inv(B) work over the dense columns.
+// FUSED (dense A): the pick runs here and h_c = A[c, q] is read from A.
+// AW: work from the A w partials (dense A), else from d.work.
 // ---------------------------------------------------------------------------
-struct RatioCtx {
-    double eps, s, rtol;
-};
-
-__device__ __forceinline__ bool pass1_cand(const RatioCtx &x, double tr, double cb, int sj, int j, Cand &e)
-{
-    if (tr == 0.0 || fabs(tr) < x.eps) return false;
-    const double alfa = x.s * tr;
-    double t;
-    if (alfa > 0.0) {
-        if (sj == NL || sj == NF) t = (cb + x.rtol) / alfa; else return false;
-    } else {
-        if (sj == NU || sj == NF) t = (cb - x.rtol) / alfa; else return false;
-    }
-    if (t < 0.0) t = 0.0;
-    e.k1 = t; e.k2 = fabs(alfa); e.idx = j + 1; e.aux = 0;
-    return true;
-}
-
-__device__ __forceinline__ bool pass2_cand(const RatioCtx &x, double tr, double cb, int sj, int j, double tmax, Cand &e)
-{
-    if (tr == 0.0 || fabs(tr) < x.eps) return false;
-    const double alfa = x.s * tr;
-    double t;
-    if (alfa > 0.0) {
-        if (sj == NL || sj == NF) t = cb / alfa; else return false;
-    } else {
-        if (sj == NU || sj == NF) t = cb / alfa; else return false;
-    }
-    if (t < 0.0) t = 0.0;
-    if (!(t <= tmax)) return false;
-    e.k1 = t; e.k2 = fabs(alfa); e.idx = j + 1; e.aux = 0;
-    return true;
-}
-
-constexpr int CHUZC_REG = 16;
-
-__global__ void __launch_bounds__(WG) k_dual_chuzc(SpxDev d, int pse, int gblocks)
+template <int NRHS, int FUSED, int AW>
+__global__ void __launch_bounds__(256) k_dual_ftran(SpxDev d, int tiles, int gn, int awsplits)
 {
     __shared__ Cand shc[16];
     __shared__ double shd[16];
     DState *st = d.st;
     if (st->stop) return;
-    const int n = d.n;
-    const double big = __longlong_as_double((long long)st->trow_max_bits);
-    RatioCtx x;
-    x.eps = st->tol_bnd * (1.0 + 0.01 * big);
-    const double delta = st->delta;
-    x.s = (delta > 0.0 ? +1.0 : -1.0);
-    x.rtol = (st->rtest == RT_HAR) ? 0.30 * st->tol_dj : 0.0;
-    const bool reg = n <= CHUZC_REG * WG;
-    double trv[CHUZC_REG], cbv[CHUZC_REG];
-    int sjv[CHUZC_REG];
-    Cand c; c.k1 = DBL_MAX; c.k2 = 0.0; c.idx = 0; c.aux = 0;
-    if (reg) {
+    const int m = d.m;
+    int q;
+    if (FUSED) {
+        q = dual_pick(d, shc, shd, NRHS == 2, gn);
+        if (!q) return;
+    } else
+        q = st->q;
+    const int kq = d.head[m + q - 1];
+    const double *hcol = (kq > m) ? d.A.A + (size_t)(kq - m - 1) * d.A.lda : nullptr;
+    const int b = blockIdx.x;
+    const int tile = b % tiles, split = b / tiles, splits = gridDim.x / tiles;
+    const int cnt = st->nr;
+    const int lps = (cnt + splits - 1) / splits;
+    const int t0 = split * lps, t1 = min(cnt, t0 + lps);
+    const int r = (tile * 256 + threadIdx.x) * 2;
+    const double *h = d.h, *work = d.work;
+    lgemv_tile<NRHS>(d.Binv, (size_t)d.ldb, m, d.rlist, t0, t1, r,
+                     [&](int, int c, double &xa, double &xb) {
+                         if (FUSED) xa = hcol ? hcol[c] : (c == kq - 1 ? -1.0 : 0.0);
+                         else xa = h[c];
+                         if (NRHS == 2) xb = AW ? aw_value(d, c, awsplits) : work[c];
+                         else xb = 0.0;
+                     },
+                     d.partial + (size_t)split * NRHS * m);
+}
+
+// tcol[i] / u[i] = sum of the partials + the unit column of a basic slack
+// at position i; 64 rows per block, 8 waves over the splits in fixed order
+template <int NRHS, int FUSED, int AW>
+__global__ void __launch_bounds__(512) k_dual_ftran_reduce(SpxDev d, int splits, int awsplits)
+{
+    __shared__ double sh[NRHS][8][64];
+    DState *st = d.st;
+    if (st->stop) return;
+    const int m = d.m;
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int r = blockIdx.x * 64 + lane;
+    const double *part = d.partial;
+    double a = 0.0, b = 0.0;
+    if (r < m) {
+#pragma unroll 4
+        for (int s = w; s < splits; s += 8) {
+            a += part[(size_t)s * NRHS * m + r];
+            if (NRHS == 2) b += part[(size_t)s * NRHS * m + m + r];
+        }
+    }
+    sh[0][w][lane] = a;
+    if (NRHS == 2) sh[NRHS - 1][w][lane] = b;
+    __syncthreads();
+    if (w != 0 || r >= m) return;
+    double va = sh[0][0][lane], vb = (NRHS == 2) ? sh[NRHS - 1][0][lane] : 0.0;
 #pragma unroll
-        for (int r = 0; r < CHUZC_REG; ++r) {
-            const int j = threadIdx.x + r * WG;
-            trv[r] = (j < n) ? d.trow[j] : 0.0;
-            cbv[r] = (j < n) ? d.cbar[j] : 0.0;
-            sjv[r] = (j < n) ? d.stat[j] : 0;
-        }
-#pragma unroll
-        for (int r = 0; r < CHUZC_REG; ++r) {
-            Cand e;
-            if (pass1_cand(x, trv[r], cbv[r], sjv[r], threadIdx.x + r * WG, e) && better<1>(e, c)) c = e;
-        }
-    } else {
-        for (int j = threadIdx.x; j < n; j += WG) {
-            Cand e;
-            if (pass1_cand(x, d.trow[j], d.cbar[j], d.stat[j], j, e) && better<1>(e, c)) c = e;
-        }
+    for (int k = 1; k < 8; ++k) {
+        va += sh[0][k][lane];
+        if (NRHS == 2) vb += sh[NRHS - 1][k][lane];
     }
-    const Cand b1 = block_best<1>(c, shc);
-    int q = b1.idx;
-    double teta = (q ? b1.k1 : DBL_MAX);
-    if (!(x.rtol == 0.0 || q == 0 || teta == 0.0)) {
-        const double tmax = teta;
-        Cand c2; c2.k1 = 0.0; c2.k2 = 0.0; c2.idx = 0; c2.aux = 0;
-        if (reg) {
-#pragma unroll
-            for (int r = 0; r < CHUZC_REG; ++r) {
-                Cand e;
-                if (pass2_cand(x, trv[r], cbv[r], sjv[r], threadIdx.x + r * WG, tmax, e) && better<2>(e, c2)) c2 = e;
-            }
-        } else {
-            for (int j = threadIdx.x; j < n; j += WG) {
-                Cand e;
-                if (pass2_cand(x, d.trow[j], d.cbar[j], d.stat[j], j, tmax, e) && better<2>(e, c2)) c2 = e;
-            }
-        }
-        const Cand b2 = block_best<2>(c2, shc);
-        q = b2.idx;
-        teta = b2.k1;
+    const int kh = d.head[r];
+    if (kh <= m) {
+        const int c = kh - 1;
+        if (FUSED) {
+            const int kq = d.head[m + st->q - 1];
+            va += (kq > m) ? d.A.A[(size_t)(kq - m - 1) * d.A.lda + c] : (c == kq - 1 ? -1.0 : 0.0);
+        } else
+            va += d.h[c];
+        if (NRHS == 2) vb += AW ? aw_value(d, c, awsplits) : d.work[c];
     }
-    if (q == 0) {
-        if (threadIdx.x == 0) { st->q = 0; st->stop = ST_Q0; }
-        return;
-    }
-    const double piv = d.trow[q - 1];
-    if (fabs(piv) < 1e-5 * (1.0 + 0.01 * big) && !st->rigorous) {
-        __syncthreads();
-        if (threadIdx.x == 0) { st->q = q; st->stop = ST_SMALLPIV; }
-        return;
-    }
-    if (pse) {
-        double g = 0.0;
-        for (int b = threadIdx.x; b < gblocks; b += WG) g += d.gpart[b];
-        g = block_sum(g, shd);
-        if (threadIdx.x == 0) {
-            const double eta = d.refsp[d.head[st->p - 1] - 1] ? 1.0 : 0.0;
-            st->eta_pq = eta;
-            st->gamma_pq = eta + g;
-        }
-    }
-    build_hq(d, q);
-    if (threadIdx.x == 0) {
-        st->q = q;
-        st->new_dq = x.s * teta;
-        st->cbar_q_old = d.cbar[q - 1];
-    }
+    d.tcol[r] = va;
+    if (NRHS == 2) d.u[r] = vb;
 }
 
 // ---------------------------------------------------------------------------
 // k_dual_commit: pivot check (:1913-1933), update_bbar (:1042), update_cbar
-// (:1020), update_gamma (:1075-1134) in the first `nvb` blocks; the rank-1
-// update of the dense columns of inv(B) in the others (product form of the
-// basis change: row p := rho / alpha_p, row i -= alpha_i / alpha_p rho).
-// A slack leaving the basis turns its unit column dense (virtual list entry
-// nr, rho = 1); a slack entering turns its column into exactly e_p.
+// (:1020), update_gamma (:1075-1134) in the first `nvb` blocks, together with
+// the chuzr candidates and the phase-I check of the next iteration; the
+// rank-1 update of the dense columns of inv(B) in the others (row p :=
+// rho / alpha_p, row i -= alpha_i / alpha_p rho).  A slack leaving the basis
+// turns its unit column dense (virtual list entry nr, rho = 1); a slack
+// entering turns its column into exactly e_p.
 // ---------------------------------------------------------------------------
 __global__ void __launch_bounds__(256) k_dual_commit(SpxDev d, int pse, int nvb, int tiles)
 {
+    __shared__ Cand shc[16];
     DState *st = d.st;
     if (st->stop) return;
     const int m = d.m, n = d.n, p = st->p, q = st->q;
@@ -472,44 +755,61 @@ __global__ void __launch_bounds__(256) k_dual_commit(SpxDev d, int pse, int nvb,
     const double tp = bad ? piv2 : piv1;
     const double delta = st->delta;
     const int kq = d.head[m + q - 1];
+    const int kp = d.head[p - 1];
     if ((int)blockIdx.x < nvb) {
         const int i = blockIdx.x * blockDim.x + threadIdx.x;
+        // gathers first: the row / column operands and what the next
+        // iteration's chuzr and check_feas read
+        const bool in_m = i < m, in_n = i < n;
+        const int kold = in_m ? d.head[i] : 1;
+        const int knew = (i == p - 1) ? kq : kold;
+        double bb = in_m ? d.bbar[i] : 0.0;
+        const double ti = in_m ? d.tcol[i] : 0.0;
+        double g = in_m ? d.gamma[i] : 0.0;
+        const double ui = (pse && in_m) ? d.u[i] : 0.0;
+        const int tkold = in_m ? d.type[kold - 1] : 0;
+        const bool refk = (pse && in_m) ? d.refsp[kold - 1] != 0 : false;
+        const int tknew = in_m ? d.type[knew - 1] : 0;
+        const double lbn = in_m ? d.lb[knew - 1] : 0.0, ubn = in_m ? d.ub[knew - 1] : 0.0;
+        double cb = in_n ? d.cbar[i] : 0.0;
+        const double tri = in_n ? d.trow[i] : 0.0;
+        const int kn = in_n ? ((i == q - 1) ? kp : d.head[m + i]) : 1;
+        const int ot = (st->phase == 1 && in_n) ? d.orig_type[kn - 1] : 0;
         const double teta = delta / tp;
         const double new_dq = st->new_dq;
-        if (i < m) {
-            if (i == p - 1) d.bbar[i] = get_xN(d.stat, d.lb, d.ub, kq, q) + teta;
-            else if (teta != 0.0) d.bbar[i] += d.tcol[i] * teta;
+        if (in_m) {
+            if (i == p - 1) bb = get_xN(d.stat, d.lb, d.ub, kq, q) + teta;
+            else if (teta != 0.0) bb += ti * teta;
+            d.bbar[i] = bb;
         }
-        if (i < n) {
-            if (i == q - 1) d.cbar[i] = new_dq;
-            else if (new_dq != 0.0) d.cbar[i] -= d.trow[i] * new_dq;
+        if (in_n) {
+            if (i == q - 1) cb = new_dq;
+            else if (new_dq != 0.0) cb -= tri * new_dq;
+            d.cbar[i] = cb;
         }
-        if (pse && i < m) {
+        if (pse && in_m) {
             const double gamma_p = st->gamma_pq, eta_p = st->eta_pq;
-            const double ti = d.tcol[i];
-            const int k = d.head[i];
-            double g = d.gamma[i];
+            const int tkq = d.type[kq - 1];
             if (i == p - 1) {
-                if (d.type[kq - 1] == FR) g = 1.0;
+                if (tkq == FR) g = 1.0;
                 else {
                     g = gamma_p / (tp * tp);
                     if (g < DBL_EPS) g = DBL_EPS;
                 }
-            } else if (ti != 0.0 && d.type[k - 1] != FR) {
+            } else if (ti != 0.0 && tkold != FR) {
                 const double t = ti / tp;
-                const double t1 = g + t * t * gamma_p + 2.0 * t * d.u[i];
-                const double t2 = (d.refsp[k - 1] ? 1.0 : 0.0) + eta_p * t * t;
+                const double t1 = g + t * t * gamma_p + 2.0 * t * ui;
+                const double t2 = (refk ? 1.0 : 0.0) + eta_p * t * t;
                 g = (t1 >= t2 ? t1 : t2);
                 if (g < DBL_EPS) g = DBL_EPS;
             }
-            const int kp = d.head[p - 1];
             if (d.type[kp - 1] == FX && d.refsp[kp - 1] && ti != 0.0) {
                 double t = 0.0;
                 bool apply = true;
                 if (i == p - 1) {
-                    if (d.type[kq - 1] == FR) apply = false; else t = 1.0 / tp;
+                    if (tkq == FR) apply = false; else t = 1.0 / tp;
                 } else {
-                    if (d.type[k - 1] == FR) apply = false; else t = ti / tp;
+                    if (tkold == FR) apply = false; else t = ti / tp;
                 }
                 if (apply) {
                     g -= t * t;
@@ -518,16 +818,32 @@ __global__ void __launch_bounds__(256) k_dual_commit(SpxDev d, int pse, int nvb,
             }
             d.gamma[i] = g;
         }
+        // next iteration: chuzr candidates (gamma := 1 if the reference space
+        // is reset before it) and check_feas (:1296) on the updated state
+        if ((int)blockIdx.x * 256 < m) {
+            Cand c = no_cand(0.0);
+            if (in_m) {
+                const bool reset = (pse && st->refct == 1);
+                c = chuzr_cand_v(i, tknew, lbn, ubn, bb, reset ? 1.0 : g, st->tol_bnd);
+            }
+            const Cand b = block_best<0>(c, shc);
+            if (threadIdx.x == 0) cand_chuzr(d)[blockIdx.x] = b;
+        }
+        if (st->phase == 1) {
+            const double tol = st->tol_dj;
+            const int badj = in_n && ((cb < -tol && (ot == LO || ot == FR)) || (cb > +tol && (ot == UP || ot == FR)));
+            if (__syncthreads_or(badj) && threadIdx.x == 0) atomicOr(&st->dinf, 1);
+        }
         if (blockIdx.x == 0 && threadIdx.x == 0) {
             st->teta = teta;
             st->pivot = tp;
+            st->pend = 1;
         }
         return;
     }
     // rank-1 update over the dense columns
     const int b = blockIdx.x - nvb;
     const int tile = b % tiles, chunk = b / tiles, chunks = (gridDim.x - nvb) / tiles;
-    const int kp = d.head[p - 1];
     const int nr = st->nr;
     const int cnt = nr + (kp <= m ? 1 : 0);
     const int ce = (kq <= m) ? kq - 1 : -1;
@@ -557,62 +873,10 @@ __global__ void __launch_bounds__(256) k_dual_commit(SpxDev d, int pse, int nvb,
     }
 }
 
-// change_basis (glpspx02.js:1954-1964) and the list of dense columns
-__global__ void k_dual_finish(SpxDev d, int rowpath, double bytes_fixed)
-{
-    DState *st = d.st;
-    if (st->stop || threadIdx.x != 0) return;
-    const int m = d.m, n = d.n, p = st->p, q = st->q;
-    const int kp = d.head[p - 1];
-    const int kq = d.head[m + q - 1];
-    const int nr0 = st->nr, ns = st->ns, nw = st->nw;
-    if (st->phase == 2) st->obj += (st->cbar_q_old / st->zeta) * (st->delta / st->pivot);
-    if (st->pricing == PT_PSE && d.type[kp - 1] == FX && d.refsp[kp - 1]) d.refsp[kp - 1] = 0;
-    d.head[p - 1] = kq;
-    d.head[m + q - 1] = kp;
-    d.bind[kq - 1] = p;
-    d.bind[kp - 1] = m + q;
-    if (d.type[kp - 1] == FX) d.stat[q - 1] = NS;
-    else if (st->delta > 0.0) d.stat[q - 1] = NL;
-    else d.stat[q - 1] = NU;
-    int nr = nr0;
-    if (kq <= m) {               // entering slack: its column is now e_p
-        const int c = kq - 1, t = d.rpos[c], last = d.rlist[nr - 1];
-        d.rlist[t] = last;
-        d.rpos[last] = t;
-        d.rpos[c] = -1;
-        nr--;
-    }
-    if (kp <= m) {               // leaving slack: its column became dense
-        const int c = kp - 1;
-        d.rlist[nr] = c;
-        d.rpos[c] = nr;
-        nr++;
-    }
-    st->nr = nr;
-    if (st->pricing == PT_PSE && st->refct > 0) st->refct--;
-    st->upd_cnt++;
-    st->binv_fresh = 0;
-    st->cbar_fresh = 0;
-    if (st->upd_cnt >= st->upd_lim) st->refact_pending = 1;
-    st->it_cnt++;
-    st->npiv++;
-    st->iter_left--;
-    if (st->rigorous > 0) st->rigorous--;
-    // algorithmic HBM bytes of this pivot: the pivot row (rows of A in the
-    // support of rho, or all of A), A w, inv(B) once for both right-hand
-    // sides, read + write of the updated columns, and the O(m + n) vectors
-    const double rowb = rowpath ? 8.0 * (double)ns * n : 8.0 * (double)m * n;
-    st->bytes += rowb + 8.0 * (double)m * nw + 8.0 * (double)m * (nr0 + 1) +
-                 16.0 * (double)m * (nr0 + (kp <= m ? 1 : 0)) + bytes_fixed;
-}
-
 // ---------------------------------------------------------------------------
 // host side
 // ---------------------------------------------------------------------------
-static inline int cdiv(int a, int b) { return (a + b - 1) / b; }
-
-DualPlan dual_plan(const SpxDev &d, int nr_max, int pse, int rigorous)
+DualPlan dual_plan(const SpxDev &d, int nr_max, int nwl_max, int pse, int rigorous)
 {
     const int m = d.m, n = d.n;
     DualPlan pl{};
@@ -621,6 +885,7 @@ DualPlan dual_plan(const SpxDev &d, int nr_max, int pse, int rigorous)
     nr_max = std::min(std::max(nr_max, 0), m);
     const int ns_max = std::min(m, nr_max + 1);
     pl.rowpath = (d.A.dense && d.A.AT && !rigorous && 2 * ns_max <= m) ? 1 : 0;
+    pl.fused = (d.A.dense && !rigorous) ? 1 : 0;
     const int tiles_t = cdiv(n, 512), tiles_f = cdiv(m, 512);
     pl.tsplits = std::max(1, std::min(2048 / tiles_t, cdiv(ns_max, 8)));
     pl.tsplits = std::max(1, std::min<int>(pl.tsplits, (int)(d.partial_cap / std::max(n, 1))));
@@ -628,6 +893,8 @@ DualPlan dual_plan(const SpxDev &d, int nr_max, int pse, int rigorous)
     pl.fsplits = std::max(1, std::min(2048 / tiles_f, cdiv(std::max(nr_max, 1), 8)));
     pl.fsplits = std::max(1, std::min<int>(pl.fsplits, (int)(d.partial_cap / ((size_t)nrhs * m))));
     pl.uchunks = std::max(1, std::min(2048 / tiles_f, cdiv(nr_max + 1, 4)));
+    pl.awsplits = std::max(1, std::min(cdiv(std::max(nwl_max, 1), 32), 64));
+    pl.awsplits = std::max(1, std::min<int>(pl.awsplits, (int)(d.awpart_cap / std::max(m, 1))));
     return pl;
 }
 
@@ -643,47 +910,69 @@ void aprod_neg_gated(hipStream_t s, const MatDev &A, const double *w, const doub
 double launch_trow_rows(hipStream_t s, const SpxDev &d, const DualPlan &pl, int ns)
 {
     const int n = d.n;
-    hipLaunchKernelGGL((k_lgemv_part<1, 1>), dim3(cdiv(n, 512), pl.tsplits), dim3(256), 0, s, d.A.AT, (size_t)d.A.ldt,
-                       n, d.rho_idx, &d.st->ns, d.rho_val, (const double *)nullptr, d.partial, (const DState *)nullptr);
-    return 8.0 * (double)ns * n + 8.0 * (double)pl.tsplits * n + 12.0 * ns;
+    hipLaunchKernelGGL(k_lgemv_part, dim3(cdiv(n, 512), pl.tsplits), dim3(256), 0, s, d.A.AT, (size_t)d.A.ldt, n,
+                       d.rho_idx, &d.st->ns, d.rho_val, d.partial, (const DState *)nullptr);
+    return 8.0 * (double)ns * n + 12.0 * ns;
+}
+
+static double bytes_fixed(const SpxDev &d) { return 96.0 * ((double)d.m + d.n); }
+
+void dual_batch_begin(hipStream_t s, const SpxDev &d, const DualPlan &pl)
+{
+    (void)pl;
+    hipLaunchKernelGGL(k_dual_prep, dim3(cdiv(std::max(d.m, d.n), 256)), dim3(256), 0, s, d);
+}
+
+void dual_batch_end(hipStream_t s, const SpxDev &d, const DualPlan &pl)
+{
+    hipLaunchKernelGGL(k_dual_finish, dim3(1), dim3(64), 0, s, d, pl.rowpath, bytes_fixed(d));
+}
+
+template <int NRHS, int FUSED, int AW>
+static void launch_ftran(hipStream_t s, const SpxDev &d, const DualPlan &pl, int gn)
+{
+    const int tiles_f = cdiv(d.m, 512);
+    hipLaunchKernelGGL((k_dual_ftran<NRHS, FUSED, AW>), dim3(tiles_f * pl.fsplits), dim3(256), 0, s, d, tiles_f, gn,
+                       pl.awsplits);
+    hipLaunchKernelGGL((k_dual_ftran_reduce<NRHS, FUSED, AW>), dim3(cdiv(d.m, 64)), dim3(512), 0, s, d, pl.fsplits,
+                       pl.awsplits);
 }
 
 void dual_iteration2(hipStream_t s, const SpxDev &d, const DualPlan &pl)
 {
     const int m = d.m, n = d.n;
-    const int gblocks = cdiv(std::max(m, n), 256);
-    hipLaunchKernelGGL(k_dual_top, dim3(1), dim3(WG), 0, s, d);
+    const int gv = cdiv(std::max(m, n), 256), gn = cdiv(n, 256), tiles_m = cdiv(m, 512);
+    const double bf = bytes_fixed(d);
+    hipLaunchKernelGGL(k_dual_top, dim3(1), dim3(WG), 0, s, d, pl.rowpath, bf);
     if (pl.rigorous) refine_rho_dev(s, d);
     if (pl.rowpath) {
-        hipLaunchKernelGGL((k_lgemv_part<1, 1>), dim3(cdiv(n, 512), pl.tsplits), dim3(256), 0, s, d.A.AT,
-                           (size_t)d.A.ldt, n, d.rho_idx, &d.st->ns, d.rho_val, (const double *)nullptr, d.partial,
-                           (const DState *)d.st);
-        hipLaunchKernelGGL(k_trow_finish<1>, dim3(gblocks), dim3(256), 0, s, d, d.partial, pl.tsplits, pl.pse);
+        hipLaunchKernelGGL(k_lgemv_part, dim3(cdiv(n, 512), pl.tsplits), dim3(256), 0, s, d.A.AT, (size_t)d.A.ldt, n,
+                           d.rho_idx, &d.st->ns, d.rho_val, d.partial, (const DState *)d.st);
+        hipLaunchKernelGGL(k_trow_finish<1>, dim3(gv), dim3(256), 0, s, d, d.partial, pl.tsplits, pl.pse);
     } else {
         colpass_gated(s, d.A, CP_TROW, m, n, d.head, d.stat, d.coef, nullptr, d.rho, nullptr, d.trow, nullptr,
                       &d.st->trow_max_bits, d.st, 0);
-        if (pl.pse)
-            hipLaunchKernelGGL(k_trow_finish<0>, dim3(gblocks), dim3(256), 0, s, d, (const double *)nullptr, 0, 1);
+        hipLaunchKernelGGL(k_trow_finish<0>, dim3(gv), dim3(256), 0, s, d, (const double *)nullptr, 0, pl.pse);
     }
-    hipLaunchKernelGGL(k_dual_chuzc, dim3(1), dim3(WG), 0, s, d, pl.pse, gblocks);
-    const int tiles_f = cdiv(m, 512);
-    if (pl.pse) {
-        aprod_neg_gated(s, d.A, d.wcol, d.ys, d.work, d.partial, d.partial_cap, d.st, 0);   // work = ys - A w
-        hipLaunchKernelGGL((k_lgemv_part<2, 0>), dim3(tiles_f, pl.fsplits), dim3(256), 0, s, d.Binv, (size_t)d.ldb, m,
-                           d.rlist, &d.st->nr, d.h, d.work, d.partial, (const DState *)d.st);
-        hipLaunchKernelGGL(k_lgemv_reduce<2>, dim3(cdiv(m, 64)), dim3(512), 0, s, d.partial, m, pl.fsplits, d.head,
-                           d.h, d.work, d.tcol, d.u, (const DState *)d.st);
+    const int aw = (pl.pse && d.A.dense) ? 1 : 0;
+    hipLaunchKernelGGL(k_dual_ratio, dim3(gn + (aw ? tiles_m * pl.awsplits : 0)), dim3(256), 0, s, d, gn, tiles_m, aw);
+    if (pl.fused) {
+        if (pl.pse) launch_ftran<2, 1, 1>(s, d, pl, gn);
+        else launch_ftran<1, 1, 0>(s, d, pl, gn);
     } else {
-        hipLaunchKernelGGL((k_lgemv_part<1, 0>), dim3(tiles_f, pl.fsplits), dim3(256), 0, s, d.Binv, (size_t)d.ldb, m,
-                           d.rlist, &d.st->nr, d.h, (const double *)nullptr, d.partial, (const DState *)d.st);
-        hipLaunchKernelGGL(k_lgemv_reduce<1>, dim3(cdiv(m, 64)), dim3(512), 0, s, d.partial, m, pl.fsplits, d.head,
-                           d.h, (const double *)nullptr, d.tcol, (double *)nullptr, (const DState *)d.st);
+        hipLaunchKernelGGL(k_dual_pick, dim3(1), dim3(1024), 0, s, d, pl.pse, gn);
+        if (pl.pse) {
+            if (aw) launch_ftran<2, 0, 1>(s, d, pl, gn);
+            else {
+                aprod_neg_gated(s, d.A, d.wcol, d.ys, d.work, d.partial, d.partial_cap, d.st, 0);   // work = ys - A w
+                launch_ftran<2, 0, 0>(s, d, pl, gn);
+            }
+        } else
+            launch_ftran<1, 0, 0>(s, d, pl, gn);
+        if (pl.rigorous) refine_tcol_dev(s, d, 0);
     }
-    if (pl.rigorous) refine_tcol_dev(s, d, 0);
-    const int nvb = gblocks;
-    hipLaunchKernelGGL(k_dual_commit, dim3(nvb + tiles_f * pl.uchunks), dim3(256), 0, s, d, pl.pse, nvb, tiles_f);
-    const double bytes_fixed = 96.0 * ((double)m + n);
-    hipLaunchKernelGGL(k_dual_finish, dim3(1), dim3(64), 0, s, d, pl.rowpath, bytes_fixed);
+    const int nvb = gv;
+    hipLaunchKernelGGL(k_dual_commit, dim3(nvb + tiles_m * pl.uchunks), dim3(256), 0, s, d, pl.pse, nvb, tiles_m);
 }
 
 // AT[r*ldt + c] = A[c*lda + r], 64 x 64 tiles through LDS

@@ -104,8 +104,9 @@ struct Engine {
     DBuf<int> head, bind;
     DBuf<double> bbar, cbar, gamma, tcol, trow, rho, rowp, u, s, h, wcol, ys, work, r1, r2, partial;
     DBuf<DState> st;
-    DBuf<int> rlist, rpos, rho_idx;
-    DBuf<double> rho_val, gpart;
+    DState *st_host = nullptr;              // pinned staging copy of st (hipHostMalloc)
+    DBuf<int> rlist, rpos, rho_idx, wlist, wpos;
+    DBuf<double> rho_val, gpart, cand, awpart;
     MatDev mat() const
     {
         MatDev M{};
@@ -121,13 +122,14 @@ struct Engine {
     ~Engine()
     {
         A.release(); AT.release(); rlist.release(); rpos.release(); rho_idx.release(); rho_val.release();
-        gpart.release(); cptr.release(); cind.release(); rptr.release(); rcol.release(); cval.release(); rval.release();
+        gpart.release(); wlist.release(); wpos.release(); cand.release(); awpart.release(); cptr.release(); cind.release(); rptr.release(); rcol.release(); cval.release(); rval.release();
         type.release(); orig_type.release(); stat.release(); refsp.release();
         lb.release(); ub.release(); coef.release(); orig_lb.release(); orig_ub.release(); obj.release();
         head.release(); bind.release();
         bbar.release(); cbar.release(); gamma.release(); tcol.release(); trow.release(); rho.release(); rowp.release();
         u.release(); s.release(); h.release(); wcol.release(); ys.release(); work.release(); r1.release(); r2.release();
         partial.release(); st.release();
+        if (st_host) (void)hipHostFree(st_host);
     }
 };
 
@@ -149,6 +151,7 @@ struct gk_bfd {
 };
 
 static const size_t PARTIAL_CAP = (size_t)1 << 22;   // >= splits * rows of every gemv (see gemv_plan, dual_plan)
+static const int AW_SPLITS = 64;                      // splits of A w over the reference-space columns
 
 // ---------------------------------------------------------------------------
 // re-inversion of the basis matrix
@@ -273,8 +276,13 @@ static void engine_alloc(Engine &E, int m, int n)
     E.h.ensure(m); E.wcol.ensure(n); E.ys.ensure(m); E.work.ensure(std::max(m, n)); E.r1.ensure(m); E.r2.ensure(m);
     E.partial.ensure(PARTIAL_CAP);
     E.st.ensure(1);
+    if (!E.st_host) HIPCHK(hipHostMalloc((void **)&E.st_host, sizeof(DState), hipHostMallocDefault));
     E.rlist.ensure(m); E.rpos.ensure(m); E.rho_idx.ensure((size_t)m + 1); E.rho_val.ensure((size_t)m + 1);
-    E.gpart.ensure((size_t)(std::max(m, n) + 255) / 256 + 1);
+    const size_t gv = (size_t)(std::max(m, n) + 255) / 256 + 1;
+    E.gpart.ensure(gv);
+    E.cand.ensure(3 * 3 * gv);                   // 3 candidate arrays of gv 24-byte entries
+    E.wlist.ensure(n); E.wpos.ensure(n);
+    E.awpart.ensure((size_t)AW_SPLITS * m);
 }
 
 __global__ void k_densify(const int *cptr, const int *cind, const double *cval, int n, double *A, int lda)
@@ -368,6 +376,7 @@ struct Spx {
     double zeta = 0.0, tm_beg = 0.0;
     int phase = 0, it_beg = 0;
     DState hs{};
+    int kbatch = 8;
     bool head_stale = false, vec_stale = false;
 
     SpxDev dev() const
@@ -385,6 +394,8 @@ struct Spx {
         d.st = E->st.p;
         d.rlist = E->rlist.p; d.rpos = E->rpos.p; d.rho_idx = E->rho_idx.p; d.rho_val = E->rho_val.p;
         d.gpart = E->gpart.p;
+        d.wlist = E->wlist.p; d.wpos = E->wpos.p; d.cand = E->cand.p;
+        d.awpart = E->awpart.p; d.awpart_cap = (size_t)AW_SPLITS * m;
         return d;
     }
 
@@ -422,12 +433,14 @@ struct Spx {
     }
     void push_state()
     {
-        HIPCHK(hipMemcpyAsync(E->st.p, &hs, sizeof(DState), hipMemcpyHostToDevice, s));
+        *E->st_host = hs;
+        HIPCHK(hipMemcpyAsync(E->st.p, E->st_host, sizeof(DState), hipMemcpyHostToDevice, s));
     }
     void pull_state()
     {
-        HIPCHK(hipMemcpyAsync(&hs, E->st.p, sizeof(DState), hipMemcpyDeviceToHost, s));
+        HIPCHK(hipMemcpyAsync(E->st_host, E->st.p, sizeof(DState), hipMemcpyDeviceToHost, s));
         sync();
+        hs = *E->st_host;
     }
 
     double get_xN(int j) const
@@ -836,8 +849,11 @@ void Spx::init()
             }
         if (!rl.empty()) HIPCHK(hipMemcpyAsync(E->rlist.p, rl.data(), rl.size() * sizeof(int), hipMemcpyHostToDevice, s));
         HIPCHK(hipMemcpyAsync(E->rpos.p, rp.data(), (size_t)m * sizeof(int), hipMemcpyHostToDevice, s));
+        std::vector<int> wp(n, -1);   // reference space empty until the first reset (refct = 0)
+        HIPCHK(hipMemcpyAsync(E->wpos.p, wp.data(), (size_t)n * sizeof(int), hipMemcpyHostToDevice, s));
         hs = DState{};
         hs.nr = (int)rl.size();
+        hs.nwl = 0;
         sync();
     }
     if (f->ext_upd) f->valid = 0;    // unit columns may be inexact after external updates
@@ -866,12 +882,16 @@ int Spx::batch(int K, int rigorous)
     hs.npiv = 0;
     hs.phase = phase;
     hs.rigorous = rigorous;
+    hs.dinf = 0;
+    hs.pend = 0;
     push_state();
     SpxDev d = dev();
     const int pse = (parm->pricing == PT_PSE);
     if (dual) {
-        const DualPlan pl = dual_plan(d, hs.nr + K + 1, pse, rigorous);
+        const DualPlan pl = dual_plan(d, hs.nr + K + 1, std::min(n, hs.nwl + K + 1), pse, rigorous);
+        dual_batch_begin(s, d, pl);
         for (int t = 0; t < K; t++) dual_iteration2(s, d, pl);
+        dual_batch_end(s, d, pl);
     } else {
         for (int t = 0; t < K; t++) primal_iteration(s, d, pse, rigorous);
     }
@@ -884,13 +904,9 @@ int Spx::batch(int K, int rigorous)
     return hs.stop == ST_RUN ? ST_BATCH : hs.stop;
 }
 
-static int batch_size(int m, int n)
-{
-    double work = (double)m * (double)m + 2.0 * (double)m * (double)n;
-    if (work > 5e7) return 8;
-    if (work > 5e6) return 32;
-    return 64;
-}
+// pivots per device batch: doubled while batches end on their budget, back
+// to the minimum after any other stop (a stop drains the rest of the batch)
+static int next_batch(int k, int why) { return why == ST_BATCH ? std::min(2 * k, 64) : 8; }
 
 int Spx::run_dual()
 {
@@ -983,9 +999,10 @@ int Spx::run_dual()
                 return it_hit ? 8 : 9;
             }
         }
-        int K = rigorous ? 1 : batch_size(m, n);
+        int K = rigorous ? 1 : kbatch;
         if (P->it_lim < 0x7fffffff) K = std::max(1, std::min(K, P->it_lim - (hs.it_cnt - it_beg)));
         int why = batch(K, rigorous);
+        kbatch = next_batch(kbatch, why);
         if (hs.npiv > 0) {
             bbar_st = 2;
             cbar_st = 2;
@@ -1108,9 +1125,10 @@ int Spx::run_primal()
                 return it_hit ? 8 : 9;
             }
         }
-        int K = rigorous ? 1 : batch_size(m, n);
+        int K = rigorous ? 1 : kbatch;
         if (P->it_lim < 0x7fffffff) K = std::max(1, std::min(K, P->it_lim - (hs.it_cnt - it_beg)));
         int why = batch(K, rigorous);
+        kbatch = next_batch(kbatch, why);
         if (hs.npiv > 0) {
             bbar_st = 2;
             rigorous = hs.rigorous;
@@ -1479,7 +1497,7 @@ extern "C" double gk_bfd_time_kernel(gk_bfd *f, int which, int reps, double *byt
         SpxDev d{};
         d.m = m; d.n = n; d.A = A; d.st = E.st.p; d.rho_idx = E.rho_idx.p; d.rho_val = E.rho_val.p;
         d.partial = E.partial.p; d.partial_cap = PARTIAL_CAP;
-        const DualPlan pl = dual_plan(d, hst.ns, 0, 0);
+        const DualPlan pl = dual_plan(d, hst.ns, 0, 0, 0);
         const bool rows = (which == 0 && pl.rowpath && hst.ns > 0);
         switch (which) {
         case 0:

@@ -47,12 +47,15 @@ struct DState {
     int refct, upd_cnt, upd_lim, rigorous;
     int binv_fresh, cbar_fresh, pricing, rtest;
     int refact_pending, nr, ns, nw;        // nr: dense columns of inv(B); ns: support of rho; nw: nonzeros of A w
-    int ce, pad0, pad1, pad2;               // ce: column of inv(B) that becomes the unit vector e_p (-1: none)
+    int ce, pend, dinf, nwl;                // ce: column of inv(B) that becomes e_p (-1: none); pend: change_basis
+                                            // pending; dinf: phase-I dual infeasibility seen; nwl: entries of wlist
+    int need2, q1, pad0, pad1;              // Harris pass 2 needed; pass-1 choice
     double delta, teta, new_dq, cbar_q_new;
     double gamma_pq, eta_pq, pivot, xnq;
     double zeta, tol_bnd, tol_dj, tol_piv;
     double obj_ll, obj_ul, obj, tcol_max;
     double cbar_q_old, bytes;               // bytes: algorithmic HBM bytes of the pivots so far
+    double teta1, pad_d;
     unsigned long long trow_max_bits, tcol_max_bits;
 };
 
@@ -117,17 +120,27 @@ struct SpxDev {
     int *rlist, *rpos;
     int *rho_idx; double *rho_val;          // rho in compact form, ns entries
     double *gpart;                           // per-block partial sums of the pivot-row pass
+    // structural columns in the PSE reference space that are non-basic (the
+    // columns A w of update_gamma runs over), maintained like rlist
+    int *wlist, *wpos;
+    double *cand;                            // per-block candidates: chuzr | pass 1 | pass 2
+    double *awpart;                          // partial sums of A w
+    size_t awpart_cap;
 };
 
 // launch geometry of one device batch, fixed on the host from nr at batch start
 struct DualPlan {
     int pse, rigorous;
     int rowpath;                  // 1: pivot row by rows of AT over the support of rho
+    int fused;                    // 1: dense A — h and A w read inside the FTRAN kernels
     int tsplits;                  // row path: splits over the support of rho
     int fsplits;                  // FTRAN over the dense columns of inv(B): splits
     int uchunks;                  // rank-1 update: column chunks
+    int awsplits;                 // A w over wlist: splits
 };
-DualPlan dual_plan(const SpxDev &d, int nr_max, int pse, int rigorous);
+void dual_batch_begin(hipStream_t s, const SpxDev &d, const DualPlan &pl);
+void dual_batch_end(hipStream_t s, const SpxDev &d, const DualPlan &pl);
+DualPlan dual_plan(const SpxDev &d, int nr_max, int nwl_max, int pse, int rigorous);
 void dual_iteration2(hipStream_t s, const SpxDev &d, const DualPlan &pl);
 void transpose_dense(hipStream_t s, const double *A, int m, int n, int lda, double *AT, int ldt);
 // timing hook: the row-path pivot-row kernel alone (returns algorithmic bytes)
