@@ -89,6 +89,16 @@ struct gk_ctx {
     hipStream_t stream = nullptr;
 };
 
+// a captured device batch of dual pivots: replayed while the device
+// pointers, the launch plan and the batch length are unchanged
+struct GraphEntry {
+    SpxDev d;
+    DualPlan pl;
+    int K = 0;
+    hipGraphExec_t exec = nullptr;
+    unsigned long long last = 0;
+};
+
 // device copy of the problem (A in scaled form) plus the simplex working set
 struct Engine {
     int m = 0, n = 0, nnz = 0;
@@ -107,6 +117,8 @@ struct Engine {
     DState *st_host = nullptr;              // pinned staging copy of st (hipHostMalloc)
     DBuf<int> rlist, rpos, rho_idx, wlist, wpos;
     DBuf<double> rho_val, gpart, cand, awpart;
+    std::vector<GraphEntry> graphs;
+    unsigned long long graph_clock = 0;
     MatDev mat() const
     {
         MatDev M{};
@@ -130,6 +142,8 @@ struct Engine {
         u.release(); s.release(); h.release(); wcol.release(); ys.release(); work.release(); r1.release(); r2.release();
         partial.release(); st.release();
         if (st_host) (void)hipHostFree(st_host);
+        for (auto &g : graphs)
+            if (g.exec) (void)hipGraphExecDestroy(g.exec);
     }
 };
 
@@ -377,11 +391,13 @@ struct Spx {
     int phase = 0, it_beg = 0;
     DState hs{};
     int kbatch = 8;
+    bool dinf_known = false;
     bool head_stale = false, vec_stale = false;
 
     SpxDev dev() const
     {
-        SpxDev d{};
+        SpxDev d;
+        std::memset(&d, 0, sizeof(d));      // compared bytewise by the graph cache
         d.m = m; d.n = n; d.A = E->mat();
         d.type = E->type.p; d.orig_type = E->orig_type.p; d.stat = E->stat.p; d.refsp = E->refsp.p;
         d.lb = E->lb.p; d.ub = E->ub.p; d.coef = E->coef.p; d.orig_lb = E->orig_lb.p; d.orig_ub = E->orig_ub.p;
@@ -735,6 +751,7 @@ struct Spx {
     }
 
     void init();
+    void run_graph(const SpxDev &d, const DualPlan &pl, int K);
     int run_dual();
     int run_primal();
     int batch(int K, int rigorous);
@@ -888,10 +905,18 @@ int Spx::batch(int K, int rigorous)
     SpxDev d = dev();
     const int pse = (parm->pricing == PT_PSE);
     if (dual) {
-        const DualPlan pl = dual_plan(d, hs.nr + K + 1, std::min(n, hs.nwl + K + 1), pse, rigorous);
-        dual_batch_begin(s, d, pl);
-        for (int t = 0; t < K; t++) dual_iteration2(s, d, pl);
-        dual_batch_end(s, d, pl);
+        // plans are bucketed so that a handful of captured graphs serve a solve
+        auto bucket = [](int x, int cap) {
+            int g = std::max(64, x / 8);
+            return std::min(cap, (x + g - 1) / g * g);
+        };
+        const DualPlan pl = dual_plan(d, bucket(hs.nr + K + 1, m), bucket(hs.nwl + K + 1, n), pse, rigorous);
+        if (!rigorous && K >= 4) run_graph(d, pl, K);
+        else {
+            dual_batch_begin(s, d, pl);
+            for (int t = 0; t < K; t++) dual_iteration2(s, d, pl);
+            dual_batch_end(s, d, pl);
+        }
     } else {
         for (int t = 0; t < K; t++) primal_iteration(s, d, pse, rigorous);
     }
@@ -902,6 +927,41 @@ int Spx::batch(int K, int rigorous)
     if (hs.npiv > 0) head_stale = vec_stale = true;
     // a stop on the budget leaves the top kernel of the next iteration unrun
     return hs.stop == ST_RUN ? ST_BATCH : hs.stop;
+}
+
+void Spx::run_graph(const SpxDev &d, const DualPlan &pl, int K)
+{
+    Engine &En = *E;
+    GraphEntry *hit = nullptr;
+    for (auto &g : En.graphs)
+        if (g.K == K && std::memcmp(&g.pl, &pl, sizeof(pl)) == 0 && std::memcmp(&g.d, &d, sizeof(d)) == 0) {
+            hit = &g;
+            break;
+        }
+    if (!hit) {
+        hipGraph_t graph = nullptr;
+        HIPCHK(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
+        dual_batch_begin(s, d, pl);
+        for (int t = 0; t < K; t++) dual_iteration2(s, d, pl);
+        dual_batch_end(s, d, pl);
+        HIPCHK(hipStreamEndCapture(s, &graph));
+        hipGraphExec_t exec = nullptr;
+        HIPCHK(hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0));
+        (void)hipGraphDestroy(graph);
+        if (En.graphs.size() >= 24) {          // evict the least recently used
+            auto lru = std::min_element(En.graphs.begin(), En.graphs.end(),
+                                        [](const GraphEntry &a, const GraphEntry &b) { return a.last < b.last; });
+            (void)hipGraphExecDestroy(lru->exec);
+            En.graphs.erase(lru);
+        }
+        GraphEntry g;
+        g.d = d; g.pl = pl; g.K = K; g.exec = exec;
+        En.graphs.push_back(g);
+        hit = &En.graphs.back();
+        f->stats.graphs_built++;
+    }
+    hit->last = ++En.graph_clock;
+    HIPCHK(hipGraphLaunch(hit->exec, s));
 }
 
 // pivots per device batch: doubled while batches end on their budget, back
@@ -922,6 +982,7 @@ int Spx::run_dual()
         }
         hs.binv_fresh = (binv_st == 1);
         if (cbar_st == 0) {
+            dinf_known = false;
             pull();
             eval_cbar();
             cbar_st = 1;
@@ -944,8 +1005,16 @@ int Spx::run_dual()
             }
         }
         if (phase == 1) {
-            pull();
-            if (dual_check_feas(P->tol_dj) == 0) {
+            // check_feas: the last pivot's commit evaluated it on the device
+            // when the batch ran to its budget
+            int infeas;
+            if (dinf_known) infeas = hs.dinf;
+            else {
+                pull();
+                infeas = dual_check_feas(P->tol_dj);
+            }
+            if (infeas == 0) {
+                pull();
                 phase = 2;
                 if (cbar_st != 1) { eval_cbar(); cbar_st = 1; }
                 set_orig_bnds();
@@ -1003,6 +1072,7 @@ int Spx::run_dual()
         if (P->it_lim < 0x7fffffff) K = std::max(1, std::min(K, P->it_lim - (hs.it_cnt - it_beg)));
         int why = batch(K, rigorous);
         kbatch = next_batch(kbatch, why);
+        dinf_known = (why == ST_BATCH && hs.npiv > 0);
         if (hs.npiv > 0) {
             bbar_st = 2;
             cbar_st = 2;

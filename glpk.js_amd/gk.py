@@ -70,7 +70,7 @@ class Lp(C.Structure):
 class SpxStats(C.Structure):
     _fields_ = [("pivots", C.c_longlong), ("reinversions", C.c_longlong), ("batches", C.c_longlong),
                 ("host_syncs", C.c_longlong), ("seconds_total", C.c_double), ("seconds_reinvert", C.c_double),
-                ("bytes_pivots", C.c_double)]
+                ("bytes_pivots", C.c_double), ("graphs_built", C.c_longlong)]
 
 
 _lib = None

@@ -132,6 +132,7 @@ typedef struct {
     long long pivots, reinversions, batches, host_syncs;
     double seconds_total, seconds_reinvert;
     double bytes_pivots;        /* algorithmic HBM bytes the pivots had to move */
+    long long graphs_built;     /* device batches captured as HIP graphs */
 } gk_spx_stats;
 void gk_bfd_last_stats(const gk_bfd *bfd, gk_spx_stats *st);
 
