@@ -95,8 +95,14 @@ def main():
     barrier()
     t0 = time.perf_counter()
     piv = 0
+    split = {"init": 0.0, "eval": 0.0, "batches": 0.0, "total": 0.0}
     for _ in range(args.steps):
         piv += step()
+        s_ = P.stats()
+        split["init"] += s_.seconds_init
+        split["eval"] += s_.seconds_eval
+        split["batches"] += s_.seconds_batches
+        split["total"] += s_.seconds_total
     barrier()
     dt = time.perf_counter() - t0
     st = P.stats()
@@ -125,12 +131,13 @@ def main():
         tpath = os.path.join(ROOT, "profiles", "r01_pmc_traffic.json")
         if os.path.exists(tpath):
             try:
-                traffic = json.load(open(tpath)).get("k_colpass_dense", {}).get("bytes_per_launch")
+                traffic = json.load(open(tpath))["kernels"].get("k_lgemv_part", {}).get("bytes_per_launch")
             except Exception:
                 traffic = None
         roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                "kernel": "k_colpass_dense (trow = -rho' A_N)", "ms_per_launch": round(ms, 5),
+                "kernel": "k_lgemv_part (pivot row trow = rho' A over the rows of A in the support of rho)",
+                "ms_per_launch": round(ms, 5),
                 "bytes_per_launch": b}
 
     cpu = None
@@ -177,7 +184,10 @@ def main():
                        "parallelism": f"replicas x{world}"},
             "roofline": roof,
             "cpu_baseline": cpu,
-            "engine": {"pivots": int(st.pivots), "reinversions": int(st.reinversions),
+            "engine": {"ms_split_per_step": {k: round(1000.0 * v / args.steps, 3) for k, v in split.items()},
+                       "bytes_per_pivot_last_step": round(st.bytes_pivots / max(1, st.pivots)),
+                       "graphs_built_last_step": int(st.graphs_built),
+                       "pivots": int(st.pivots), "reinversions": int(st.reinversions),
                        "batches": int(st.batches), "host_syncs": int(st.host_syncs),
                        "restarts": restarts[0], "kernels": kern},
             "extra": extra,

@@ -400,17 +400,16 @@ __global__ void __launch_bounds__(WG) k_dual_top(SpxDev d, int rowpath, double b
         return;
     }
     const int p = best.idx;
-    for (int l = threadIdx.x; l < m; l += blockDim.x) {
-        d.rho[l] = 0.0;
-        d.rowp[l] = 0.0;
+    // rho in compact form; the dense copy only for the column pass
+    if (!rowpath) {
+        for (int l = threadIdx.x; l < m; l += blockDim.x) d.rho[l] = 0.0;
+        __syncthreads();
     }
-    __syncthreads();
     const int nr = st->nr;
     for (int t = threadIdx.x; t < nr; t += blockDim.x) {
         const int cc = d.rlist[t];
         const double v = d.Binv[(size_t)(p - 1) + (size_t)cc * d.ldb];
-        d.rho[cc] = v;
-        d.rowp[cc] = v;
+        if (!rowpath) d.rho[cc] = v;
         d.rho_idx[t] = cc;
         d.rho_val[t] = v;
     }
@@ -418,8 +417,7 @@ __global__ void __launch_bounds__(WG) k_dual_top(SpxDev d, int rowpath, double b
         const int kp = d.head[p - 1];
         int ns = nr;
         if (kp <= m) {   // the basic slack at position p: unit column of inv(B)
-            d.rho[kp - 1] = 1.0;
-            d.rowp[kp - 1] = 1.0;
+            if (!rowpath) d.rho[kp - 1] = 1.0;
             d.rho_idx[nr] = kp - 1;
             d.rho_val[nr] = 1.0;
             ns++;
@@ -453,6 +451,7 @@ __global__ void __launch_bounds__(256) k_trow_finish(SpxDev d, const double *__r
     // all gathers first (bind -> stat/cbar/refsp/partials), reductions after
     const int pos1 = (idx < n) ? d.bind[m + idx] : 0;
     const int pos2 = (idx < m) ? d.bind[idx] : 0;
+    const int rp2 = (FROM_PART && idx < m) ? d.rpos[idx] : -1;   // a non-basic slack is a dense column of inv(B)
     const int j1 = (pos1 > m) ? pos1 - m - 1 : -1;
     const int j2 = (pos2 > m) ? pos2 - m - 1 : -1;
     int s1 = 0, s2 = 0;
@@ -473,7 +472,7 @@ __global__ void __launch_bounds__(256) k_trow_finish(SpxDev d, const double *__r
     if (j2 >= 0) {
         s2 = d.stat[j2];
         cb2 = d.cbar[j2];
-        tv2 = FROM_PART ? -d.rho[idx] : d.trow[j2];
+        tv2 = FROM_PART ? -d.rho_val[rp2] : d.trow[j2];
         if (pse) ref2 = d.refsp[idx] != 0;
     }
     if (FROM_PART) {

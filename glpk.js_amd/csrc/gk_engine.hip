@@ -119,6 +119,7 @@ struct Engine {
     DBuf<double> rho_val, gpart, cand, awpart;
     std::vector<GraphEntry> graphs;
     unsigned long long graph_clock = 0;
+    int kbatch = 8;                           // batch length carried across calls
     MatDev mat() const
     {
         MatDev M{};
@@ -390,7 +391,6 @@ struct Spx {
     double zeta = 0.0, tm_beg = 0.0;
     int phase = 0, it_beg = 0;
     DState hs{};
-    int kbatch = 8;
     bool dinf_known = false;
     bool head_stale = false, vec_stale = false;
 
@@ -474,6 +474,8 @@ struct Spx {
     // eval_cbar (glpspx01.js:565): pi = inv(B') cB refined once, d_j = c_k - N_j' pi
     void eval_cbar()
     {
+        const double t0 = now_s();
+        struct T { gk_bfd *f; double t0; ~T() { f->stats.seconds_eval += now_s() - t0; } } tt{f, t0};
         SpxDev d = dev();
         MatDev A = E->mat();
         double *cB = E->r1.p, *pi = E->u.p, *r = E->r2.p, *dd = E->work.p;
@@ -492,6 +494,8 @@ struct Spx {
     // (refine_ftran :251: beta += inv(B) (h - B beta))
     void eval_bbar()
     {
+        const double t0 = now_s();
+        struct T { gk_bfd *f; double t0; ~T() { f->stats.seconds_eval += now_s() - t0; } } tt{f, t0};
         SpxDev d = dev();
         MatDev A = E->mat();
         double *w = E->s.p;   // n-sized scratch
@@ -797,6 +801,8 @@ int Spx::reinvert_core_csc(const BasisSplit &bs)
 
 void Spx::init()
 {
+    const double t0 = now_s();
+    struct T { gk_bfd *f; double t0; ~T() { f->stats.seconds_init += now_s() - t0; } } tt{f, t0};
     const gk_lp *L = lp;
     m = L->m; n = L->n;
     s = ctx->stream;
@@ -894,6 +900,8 @@ void Spx::init()
 
 int Spx::batch(int K, int rigorous)
 {
+    const double t0 = now_s();
+    struct T { gk_bfd *f; double t0; ~T() { f->stats.seconds_batches += now_s() - t0; } } tt{f, t0};
     hs.stop = ST_RUN;
     hs.iter_left = K;
     hs.npiv = 0;
@@ -1068,10 +1076,10 @@ int Spx::run_dual()
                 return it_hit ? 8 : 9;
             }
         }
-        int K = rigorous ? 1 : kbatch;
+        int K = rigorous ? 1 : E->kbatch;
         if (P->it_lim < 0x7fffffff) K = std::max(1, std::min(K, P->it_lim - (hs.it_cnt - it_beg)));
         int why = batch(K, rigorous);
-        kbatch = next_batch(kbatch, why);
+        E->kbatch = next_batch(E->kbatch, why);
         dinf_known = (why == ST_BATCH && hs.npiv > 0);
         if (hs.npiv > 0) {
             bbar_st = 2;
@@ -1195,10 +1203,10 @@ int Spx::run_primal()
                 return it_hit ? 8 : 9;
             }
         }
-        int K = rigorous ? 1 : kbatch;
+        int K = rigorous ? 1 : E->kbatch;
         if (P->it_lim < 0x7fffffff) K = std::max(1, std::min(K, P->it_lim - (hs.it_cnt - it_beg)));
         int why = batch(K, rigorous);
-        kbatch = next_batch(kbatch, why);
+        E->kbatch = next_batch(E->kbatch, why);
         if (hs.npiv > 0) {
             bbar_st = 2;
             rigorous = hs.rigorous;

@@ -70,7 +70,8 @@ class Lp(C.Structure):
 class SpxStats(C.Structure):
     _fields_ = [("pivots", C.c_longlong), ("reinversions", C.c_longlong), ("batches", C.c_longlong),
                 ("host_syncs", C.c_longlong), ("seconds_total", C.c_double), ("seconds_reinvert", C.c_double),
-                ("bytes_pivots", C.c_double), ("graphs_built", C.c_longlong)]
+                ("bytes_pivots", C.c_double), ("graphs_built", C.c_longlong),
+                ("seconds_init", C.c_double), ("seconds_eval", C.c_double), ("seconds_batches", C.c_double)]
 
 
 _lib = None
@@ -420,12 +421,9 @@ def glp_simplex(P: GkProblem, parm: Smcp | None = None) -> int:
     P.pbs_stat = P.dbs_stat = GLP_UNDEF
     P.obj_val = 0.0
     P.some = 0
-    for i in range(1, P.m + 1):
-        if P.row_type[i] == GLP_DB and P.row_lb[i] >= P.row_ub[i]:
-            return GLP_EBOUND
-    for j in range(1, P.n + 1):
-        if P.col_type[j] == GLP_DB and P.col_lb[j] >= P.col_ub[j]:
-            return GLP_EBOUND
+    if np.any((P.row_type[1:] == GLP_DB) & (P.row_lb[1:] >= P.row_ub[1:])) or \
+            np.any((P.col_type[1:] == GLP_DB) & (P.col_lb[1:] >= P.col_ub[1:])):
+        return GLP_EBOUND
     if P.nnz == 0:
         _trivial_lp(P, parm)
         return 0

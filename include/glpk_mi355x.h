@@ -133,6 +133,7 @@ typedef struct {
     double seconds_total, seconds_reinvert;
     double bytes_pivots;        /* algorithmic HBM bytes the pivots had to move */
     long long graphs_built;     /* device batches captured as HIP graphs */
+    double seconds_init, seconds_eval, seconds_batches;   /* host wall time split */
 } gk_spx_stats;
 void gk_bfd_last_stats(const gk_bfd *bfd, gk_spx_stats *st);
 
