@@ -107,13 +107,16 @@ __device__ __forceinline__ void lgemv_tile(const double *__restrict__ M, size_t 
     }
 }
 
-// trow partials: part[s*n + c] = sum over the support of rho in chunk s of rho_i A[i, c]
+// trow partials: part[s*n + c] = sum over the support of rho in chunk s of rho_i A[i, c].
+// With st, block (0,0) stamps the device wall clock at entry and every block
+// at exit (tslots), so the kernel's span is measured inside captured graphs.
 __global__ void __launch_bounds__(256) k_lgemv_part(const double *__restrict__ M, size_t ld, int rows,
                                                       const int *__restrict__ list, const int *cntp,
                                                       const double *__restrict__ xv, double *__restrict__ part,
-                                                      const DState *st)
+                                                      DState *st, unsigned long long *tslots)
 {
     if (st && st->stop) return;
+    if (st && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) st->tk_start = wall_clock64();
     const int cnt = *cntp;
     const int splits = gridDim.y;
     const int lps = (cnt + splits - 1) / splits;
@@ -122,6 +125,10 @@ __global__ void __launch_bounds__(256) k_lgemv_part(const double *__restrict__ M
     lgemv_tile<1>(M, ld, rows, list, t0, t1, r,
                   [&](int t, int, double &xa, double &xb) { xa = xv[t]; xb = 0.0; },
                   part + (size_t)blockIdx.y * rows);
+    if (tslots) {
+        __syncthreads();
+        if (threadIdx.x == 0) tslots[blockIdx.y * gridDim.x + blockIdx.x] = wall_clock64();
+    }
 }
 
 // ---------------------------------------------------------------------------
@@ -283,6 +290,13 @@ __device__ void dual_finish_block(const SpxDev &d, int rowpath, double bytes_fix
         // inv(B) once for both right-hand sides, read + write of the updated
         // columns, and the O(m + n) vectors
         const double rowb = rowpath ? 8.0 * (double)ns * n : 8.0 * (double)m * n;
+        if (rowpath && st->tk_end > st->tk_start) {
+            st->bytes_trow += rowb;
+            st->trow_ticks += (double)(st->tk_end - st->tk_start);
+            st->trow_ticks_b += (double)(st->tk_next - st->tk_start);
+            st->trow_n += 1.0;
+        }
+        st->tk_end = 0;
         st->bytes += rowb + 8.0 * (double)m * nwl0 + 8.0 * (double)m * (nr0 + 1) +
                      16.0 * (double)m * (nr0 + (kp <= m ? 1 : 0)) + bytes_fixed;
     }
@@ -440,7 +454,8 @@ __global__ void __launch_bounds__(WG) k_dual_top(SpxDev d, int rowpath, double b
 // tolerance (k_dual_ratio re-checks it against the global one).
 // ---------------------------------------------------------------------------
 template <int FROM_PART>
-__global__ void __launch_bounds__(256) k_trow_finish(SpxDev d, const double *__restrict__ part, int splits, int pse)
+__global__ void __launch_bounds__(256) k_trow_finish(SpxDev d, const double *__restrict__ part, int splits, int pse,
+                                                       int nslots)
 {
     __shared__ double shd[16];
     __shared__ Cand shc[16];
@@ -448,6 +463,18 @@ __global__ void __launch_bounds__(256) k_trow_finish(SpxDev d, const double *__r
     if (st->stop) return;
     const int m = d.m, n = d.n;
     const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+    if (FROM_PART) {
+        if (blockIdx.x == 0 && threadIdx.x == 0) st->tk_next = wall_clock64();
+        // end of the pivot-row kernel: latest block stamp
+        unsigned long long e = 0;
+        for (int t = idx; t < nslots; t += gridDim.x * blockDim.x) e = max(e, d.tslots[t]);
+        __shared__ unsigned long long she;
+        if (threadIdx.x == 0) she = 0;
+        __syncthreads();
+        if (e) atomicMax(&she, e);
+        __syncthreads();
+        if (threadIdx.x == 0 && she) atomicMax(&st->tk_end, she);
+    }
     // all gathers first (bind -> stat/cbar/refsp/partials), reductions after
     const int pos1 = (idx < n) ? d.bind[m + idx] : 0;
     const int pos2 = (idx < m) ? d.bind[idx] : 0;
@@ -910,7 +937,7 @@ double launch_trow_rows(hipStream_t s, const SpxDev &d, const DualPlan &pl, int 
 {
     const int n = d.n;
     hipLaunchKernelGGL(k_lgemv_part, dim3(cdiv(n, 512), pl.tsplits), dim3(256), 0, s, d.A.AT, (size_t)d.A.ldt, n,
-                       d.rho_idx, &d.st->ns, d.rho_val, d.partial, (const DState *)nullptr);
+                       d.rho_idx, &d.st->ns, d.rho_val, d.partial, (DState *)nullptr, (unsigned long long *)nullptr);
     return 8.0 * (double)ns * n + 12.0 * ns;
 }
 
@@ -937,7 +964,7 @@ static void launch_ftran(hipStream_t s, const SpxDev &d, const DualPlan &pl, int
                        pl.awsplits);
 }
 
-void dual_iteration2(hipStream_t s, const SpxDev &d, const DualPlan &pl)
+void dual_iteration2(hipStream_t s, const SpxDev &d, const DualPlan &pl, hipEvent_t ev0, hipEvent_t ev1)
 {
     const int m = d.m, n = d.n;
     const int gv = cdiv(std::max(m, n), 256), gn = cdiv(n, 256), tiles_m = cdiv(m, 512);
@@ -945,13 +972,18 @@ void dual_iteration2(hipStream_t s, const SpxDev &d, const DualPlan &pl)
     hipLaunchKernelGGL(k_dual_top, dim3(1), dim3(WG), 0, s, d, pl.rowpath, bf);
     if (pl.rigorous) refine_rho_dev(s, d);
     if (pl.rowpath) {
+        if (ev0) (void)hipEventRecord(ev0, s);
         hipLaunchKernelGGL(k_lgemv_part, dim3(cdiv(n, 512), pl.tsplits), dim3(256), 0, s, d.A.AT, (size_t)d.A.ldt, n,
-                           d.rho_idx, &d.st->ns, d.rho_val, d.partial, (const DState *)d.st);
-        hipLaunchKernelGGL(k_trow_finish<1>, dim3(gv), dim3(256), 0, s, d, d.partial, pl.tsplits, pl.pse);
+                           d.rho_idx, &d.st->ns, d.rho_val, d.partial, d.st, d.tslots);
+        if (ev1) (void)hipEventRecord(ev1, s);
+        hipLaunchKernelGGL(k_trow_finish<1>, dim3(gv), dim3(256), 0, s, d, d.partial, pl.tsplits, pl.pse,
+                           cdiv(n, 512) * pl.tsplits);
     } else {
+        if (ev0) (void)hipEventRecord(ev0, s);
         colpass_gated(s, d.A, CP_TROW, m, n, d.head, d.stat, d.coef, nullptr, d.rho, nullptr, d.trow, nullptr,
                       &d.st->trow_max_bits, d.st, 0);
-        hipLaunchKernelGGL(k_trow_finish<0>, dim3(gv), dim3(256), 0, s, d, (const double *)nullptr, 0, pl.pse);
+        if (ev1) (void)hipEventRecord(ev1, s);
+        hipLaunchKernelGGL(k_trow_finish<0>, dim3(gv), dim3(256), 0, s, d, (const double *)nullptr, 0, pl.pse, 0);
     }
     const int aw = (pl.pse && d.A.dense) ? 1 : 0;
     hipLaunchKernelGGL(k_dual_ratio, dim3(gn + (aw ? tiles_m * pl.awsplits : 0)), dim3(256), 0, s, d, gn, tiles_m, aw);

@@ -87,6 +87,7 @@ struct DBuf {
 struct gk_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
+    int wall_khz = 100000;              // device wall clock (wall_clock64) rate
 };
 
 // a captured device batch of dual pivots: replayed while the device
@@ -117,9 +118,12 @@ struct Engine {
     DState *st_host = nullptr;              // pinned staging copy of st (hipHostMalloc)
     DBuf<int> rlist, rpos, rho_idx, wlist, wpos;
     DBuf<double> rho_val, gpart, cand, awpart;
+    DBuf<unsigned long long> tslots;
     std::vector<GraphEntry> graphs;
     unsigned long long graph_clock = 0;
     int kbatch = 8;                           // batch length carried across calls
+    int prof = 0;                             // gk_bfd_profile: events around the pivot-row kernel
+    std::vector<hipEvent_t> ev;               // 2 per pivot of the longest batch
     MatDev mat() const
     {
         MatDev M{};
@@ -135,7 +139,7 @@ struct Engine {
     ~Engine()
     {
         A.release(); AT.release(); rlist.release(); rpos.release(); rho_idx.release(); rho_val.release();
-        gpart.release(); wlist.release(); wpos.release(); cand.release(); awpart.release(); cptr.release(); cind.release(); rptr.release(); rcol.release(); cval.release(); rval.release();
+        gpart.release(); tslots.release(); wlist.release(); wpos.release(); cand.release(); awpart.release(); cptr.release(); cind.release(); rptr.release(); rcol.release(); cval.release(); rval.release();
         type.release(); orig_type.release(); stat.release(); refsp.release();
         lb.release(); ub.release(); coef.release(); orig_lb.release(); orig_ub.release(); obj.release();
         head.release(); bind.release();
@@ -145,6 +149,7 @@ struct Engine {
         if (st_host) (void)hipHostFree(st_host);
         for (auto &g : graphs)
             if (g.exec) (void)hipGraphExecDestroy(g.exec);
+        for (auto e : ev) (void)hipEventDestroy(e);
     }
 };
 
@@ -155,6 +160,7 @@ struct gk_bfd {
     int m = 0, ldb = 0;
     int upd_cnt = 0;
     int ext_upd = 0;                           // updated through gk_bfd_update since the last re-inversion
+    int prof = 0;                              // gk_bfd_profile
     DBuf<double> Binv;
     // re-inversion scratch
     DBuf<double> C, X, Y, CinvR, BS, G, vecx, vecy, partial;
@@ -298,6 +304,7 @@ static void engine_alloc(Engine &E, int m, int n)
     E.cand.ensure(3 * 3 * gv);                   // 3 candidate arrays of gv 24-byte entries
     E.wlist.ensure(n); E.wpos.ensure(n);
     E.awpart.ensure((size_t)AW_SPLITS * m);
+    E.tslots.ensure((size_t)((n + 511) / 512) * 2048 + 1);
 }
 
 __global__ void k_densify(const int *cptr, const int *cind, const double *cval, int n, double *A, int lda)
@@ -412,6 +419,7 @@ struct Spx {
         d.gpart = E->gpart.p;
         d.wlist = E->wlist.p; d.wpos = E->wpos.p; d.cand = E->cand.p;
         d.awpart = E->awpart.p; d.awpart_cap = (size_t)AW_SPLITS * m;
+        d.tslots = E->tslots.p;
         return d;
     }
 
@@ -756,6 +764,16 @@ struct Spx {
 
     void init();
     void run_graph(const SpxDev &d, const DualPlan &pl, int K);
+    void prof_events(int K)
+    {
+        while ((int)E->ev.size() < 2 * K) {
+            hipEvent_t e;
+            HIPCHK(hipEventCreate(&e));
+            E->ev.push_back(e);
+        }
+    }
+    hipEvent_t ev0(int t) const { return E->prof ? E->ev[2 * t] : nullptr; }
+    hipEvent_t ev1(int t) const { return E->prof ? E->ev[2 * t + 1] : nullptr; }
     int run_dual();
     int run_primal();
     int batch(int K, int rigorous);
@@ -919,10 +937,13 @@ int Spx::batch(int K, int rigorous)
             return std::min(cap, (x + g - 1) / g * g);
         };
         const DualPlan pl = dual_plan(d, bucket(hs.nr + K + 1, m), bucket(hs.nwl + K + 1, n), pse, rigorous);
-        if (!rigorous && K >= 4) run_graph(d, pl, K);
+        // profiling launches eagerly: event-record nodes inside captured
+        // graphs are not timed by every HIP runtime this library may bind to
+        if (E->prof) prof_events(K);
+        if (!rigorous && K >= 4 && !E->prof) run_graph(d, pl, K);
         else {
             dual_batch_begin(s, d, pl);
-            for (int t = 0; t < K; t++) dual_iteration2(s, d, pl);
+            for (int t = 0; t < K; t++) dual_iteration2(s, d, pl, ev0(t), ev1(t));
             dual_batch_end(s, d, pl);
         }
     } else {
@@ -932,6 +953,24 @@ int Spx::batch(int K, int rigorous)
     f->stats.batches++;
     f->stats.pivots += hs.npiv;
     f->stats.bytes_pivots = hs.bytes;
+    f->stats.trow_bytes = hs.bytes_trow;
+    f->stats.trow_dev_ms = hs.trow_ticks / (double)ctx->wall_khz;
+    f->stats.trow_dev_ms_b = hs.trow_ticks_b / (double)ctx->wall_khz;
+    f->stats.trow_dev_launches = (long long)hs.trow_n;
+    if (dual && E->prof) {
+        for (int t = 0; t < hs.npiv; t++) {
+            float ms = 0.f;
+            hipError_t e = hipEventElapsedTime(&ms, E->ev[2 * t], E->ev[2 * t + 1]);
+            if (e != hipSuccess)
+                throw AbiError{std::string("event timing: ") + hipGetErrorName(e) + " t=" + std::to_string(t) +
+                               " K=" + std::to_string(K) + " npiv=" + std::to_string(hs.npiv) +
+                               " graph=" + std::to_string(!rigorous && K >= 4) + " nev=" + std::to_string(E->ev.size()) +
+                               " q0=" + hipGetErrorName(hipEventQuery(E->ev[2 * t])) +
+                               " q1=" + hipGetErrorName(hipEventQuery(E->ev[2 * t + 1]))};
+            f->stats.trow_ms += ms;
+            f->stats.trow_launches++;
+        }
+    }
     if (hs.npiv > 0) head_stale = vec_stale = true;
     // a stop on the budget leaves the top kernel of the next iteration unrun
     return hs.stop == ST_RUN ? ST_BATCH : hs.stop;
@@ -942,7 +981,8 @@ void Spx::run_graph(const SpxDev &d, const DualPlan &pl, int K)
     Engine &En = *E;
     GraphEntry *hit = nullptr;
     for (auto &g : En.graphs)
-        if (g.K == K && std::memcmp(&g.pl, &pl, sizeof(pl)) == 0 && std::memcmp(&g.d, &d, sizeof(d)) == 0) {
+        if (g.K == K && std::memcmp(&g.pl, &pl, sizeof(pl)) == 0 &&
+            std::memcmp(&g.d, &d, sizeof(d)) == 0) {
             hit = &g;
             break;
         }
@@ -1300,6 +1340,9 @@ gk_ctx *gk_ctx_create(int device)
         gk_ctx *c = new gk_ctx;
         c->device = device;
         HIPCHK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+        int khz = 0;
+        if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, device) == hipSuccess && khz > 0)
+            c->wall_khz = khz;
         return c;
     } catch (const AbiError &e) {
         g_err = e.msg;
@@ -1354,6 +1397,11 @@ int gk_bfd_get_count(const gk_bfd *f)
 void gk_bfd_last_stats(const gk_bfd *f, gk_spx_stats *st)
 {
     if (f && st) *st = f->stats;
+}
+
+void gk_bfd_profile(gk_bfd *f, int enable)
+{
+    if (f) f->prof = enable ? 1 : 0;
 }
 
 static void bfd_prepare(gk_bfd *f, int m)
@@ -1536,6 +1584,7 @@ static int spx_entry(gk_ctx *ctx, gk_lp *lp, gk_bfd *f, const gk_smcp *parm, int
         f->stats = gk_spx_stats{};
         bfd_prepare(f, lp->m);
         if (!f->eng) f->eng = new Engine;
+        f->eng->prof = f->prof;
         engine_upload_matrix(f, lp);
         Spx S;
         S.ctx = ctx; S.f = f; S.E = f->eng; S.lp = lp; S.parm = parm; S.dual = dual;

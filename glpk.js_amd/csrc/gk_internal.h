@@ -55,7 +55,11 @@ struct DState {
     double zeta, tol_bnd, tol_dj, tol_piv;
     double obj_ll, obj_ul, obj, tcol_max;
     double cbar_q_old, bytes;               // bytes: algorithmic HBM bytes of the pivots so far
-    double teta1, pad_d;
+    double teta1, bytes_trow;               // bytes_trow: algorithmic bytes of the pivot-row kernels
+    unsigned long long tk_start, tk_end;    // device wall clock around the last pivot-row kernel
+    unsigned long long tk_next, tk_pad;     // entry of the kernel after it
+    double trow_ticks, trow_n;              // accumulated execution span of the pivot-row kernels (row path)
+    double trow_ticks_b, trow_pad;          // same, entry to the next kernel's entry (dispatch included)
     unsigned long long trow_max_bits, tcol_max_bits;
 };
 
@@ -126,6 +130,7 @@ struct SpxDev {
     double *cand;                            // per-block candidates: chuzr | pass 1 | pass 2
     double *awpart;                          // partial sums of A w
     size_t awpart_cap;
+    unsigned long long *tslots;              // per-block end stamps of the pivot-row kernel
 };
 
 // launch geometry of one device batch, fixed on the host from nr at batch start
@@ -141,7 +146,9 @@ struct DualPlan {
 void dual_batch_begin(hipStream_t s, const SpxDev &d, const DualPlan &pl);
 void dual_batch_end(hipStream_t s, const SpxDev &d, const DualPlan &pl);
 DualPlan dual_plan(const SpxDev &d, int nr_max, int nwl_max, int pse, int rigorous);
-void dual_iteration2(hipStream_t s, const SpxDev &d, const DualPlan &pl);
+// ev0/ev1 (optional, eager launches only): events recorded around the pivot-row kernel
+void dual_iteration2(hipStream_t s, const SpxDev &d, const DualPlan &pl, hipEvent_t ev0 = nullptr,
+                     hipEvent_t ev1 = nullptr);
 void transpose_dense(hipStream_t s, const double *A, int m, int n, int lda, double *AT, int ldt);
 // timing hook: the row-path pivot-row kernel alone (returns algorithmic bytes)
 double launch_trow_rows(hipStream_t s, const SpxDev &d, const DualPlan &pl, int ns);

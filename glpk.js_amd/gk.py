@@ -71,7 +71,9 @@ class SpxStats(C.Structure):
     _fields_ = [("pivots", C.c_longlong), ("reinversions", C.c_longlong), ("batches", C.c_longlong),
                 ("host_syncs", C.c_longlong), ("seconds_total", C.c_double), ("seconds_reinvert", C.c_double),
                 ("bytes_pivots", C.c_double), ("graphs_built", C.c_longlong),
-                ("seconds_init", C.c_double), ("seconds_eval", C.c_double), ("seconds_batches", C.c_double)]
+                ("seconds_init", C.c_double), ("seconds_eval", C.c_double), ("seconds_batches", C.c_double),
+                ("trow_ms", C.c_double), ("trow_launches", C.c_longlong), ("trow_bytes", C.c_double),
+                ("trow_dev_ms", C.c_double), ("trow_dev_launches", C.c_longlong), ("trow_dev_ms_b", C.c_double)]
 
 
 _lib = None
@@ -79,7 +81,7 @@ _lib = None
 EXPORTS = ["gk_abi_version", "gk_device_count", "gk_ctx_create", "gk_ctx_destroy", "gk_last_error",
            "gk_bfd_create", "gk_bfd_destroy", "gk_bfd_set_parm", "gk_bfd_factorize", "gk_bfd_factorize_csc",
            "gk_bfd_ftran", "gk_bfd_btran", "gk_bfd_update", "gk_bfd_get_count", "gk_bfd_valid",
-           "gk_spx_primal", "gk_spx_dual", "gk_bfd_last_stats", "gk_ios_driver"]
+           "gk_spx_primal", "gk_spx_dual", "gk_bfd_last_stats", "gk_bfd_profile", "gk_ios_driver"]
 
 
 def load_library(path: str = LIB_PATH):
@@ -116,6 +118,8 @@ def load_library(path: str = LIB_PATH):
         f.argtypes = [P, C.POINTER(Lp), P, C.POINTER(Smcp)]
         f.restype = C.c_int
     L.gk_bfd_last_stats.argtypes = [P, C.POINTER(SpxStats)]
+    L.gk_bfd_profile.argtypes = [P, C.c_int]
+    L.gk_bfd_profile.restype = None
     L.gk_bfd_time_kernel.argtypes = [P, C.c_int, C.c_int, C.POINTER(C.c_double)]
     L.gk_bfd_time_kernel.restype = C.c_double
     _lib = L
@@ -335,6 +339,10 @@ class GkProblem:
         if ms < 0:
             raise GkError(_err(self.L))
         return ms, b.value
+
+    def profile(self, enable: bool = True):
+        """Record HIP events around the pivot-row kernel of every dual pivot."""
+        self.L.gk_bfd_profile(self.bfd, 1 if enable else 0)
 
     def stats(self) -> SpxStats:
         st = SpxStats()

@@ -134,8 +134,16 @@ typedef struct {
     double bytes_pivots;        /* algorithmic HBM bytes the pivots had to move */
     long long graphs_built;     /* device batches captured as HIP graphs */
     double seconds_init, seconds_eval, seconds_batches;   /* host wall time split */
+    double trow_ms;             /* with gk_bfd_profile: HIP-event time of the pivot-row kernels */
+    long long trow_launches;
+    double trow_bytes;          /* algorithmic bytes of those kernels (all pivots of the call) */
+    double trow_dev_ms;         /* device wall-clock execution span of the row-path pivot-row kernels */
+    long long trow_dev_launches;
+    double trow_dev_ms_b;       /* same, from their entry to the next kernel's entry (dispatch included) */
 } gk_spx_stats;
 void gk_bfd_last_stats(const gk_bfd *bfd, gk_spx_stats *st);
+/* record HIP events around the pivot-row kernel of every dual pivot (benches) */
+void gk_bfd_profile(gk_bfd *bfd, int enable);
 
 /* measurement hook for bench.py (not part of the reference interface):
  * launch one engine kernel `reps` times on the problem left resident by the
