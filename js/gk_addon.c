@@ -1,0 +1,372 @@
+/*
+ * gk_addon.c — N-API binding of the MI355X simplex core (include/glpk_mi355x.h)
+ * for the JavaScript host (Cyame/glpk.js).  Every function is a thin,
+ * synchronous marshal of typed arrays to one C-ABI call; a GK_EABI return is
+ * rethrown as a JS Error carrying gk_last_error() (the reference's xerror
+ * text).  See js/gk_core.js for the JS side and INTEGRATION.md for wiring.
+ *
+ *   create(device)                 -> ctx       gk_ctx_create
+ *   deviceCount(), abiVersion(), lastError()
+ *   bfdCreate(ctx)                 -> bfd       gk_bfd_create (finalizer: gk_bfd_destroy)
+ *   bfdSetParm(bfd, parm)                       gk_bfd_set_parm      (glpbfd.js:31)
+ *   bfdFactorizeCsc(bfd, m, ptr, ind, val) -> int  gk_bfd_factorize_csc (glpbfd.js:47)
+ *   bfdFtran(bfd, x), bfdBtran(bfd, x)          gk_bfd_ftran/btran   (glpbfd.js:148/159)
+ *   bfdUpdate(bfd, j, len, ind, idx, val) -> int gk_bfd_update       (glpbfd.js:170)
+ *   bfdGetCount(bfd), bfdValid(bfd)             (glpbfd.js:225)
+ *   spx(ctx, bfd, lp, smcp, dual)  -> int       gk_spx_primal/dual (glpspx01.js:1 / glpspx02.js:1)
+ *   stats(bfd)                     -> object    gk_bfd_last_stats
+ */
+#define NAPI_VERSION 6
+#include <node_api.h>
+#include <stdio.h>
+#include <string.h>
+#include <stdlib.h>
+#include "../include/glpk_mi355x.h"
+
+#define CHECK(call)                                                                 \
+    do {                                                                            \
+        if ((call) != napi_ok) {                                                    \
+            napi_throw_error(env, NULL, "gk_addon: N-API call failed: " #call);     \
+            return NULL;                                                            \
+        }                                                                           \
+    } while (0)
+
+static napi_value throw_gk(napi_env env, const char *what)
+{
+    char msg[1024];
+    snprintf(msg, sizeof msg, "%s: %s", what, gk_last_error());
+    napi_throw_error(env, NULL, msg);
+    return NULL;
+}
+
+static napi_value mk_int(napi_env env, long long v)
+{
+    napi_value r;
+    napi_create_double(env, (double)v, &r);
+    return r;
+}
+
+static int get_args(napi_env env, napi_callback_info info, size_t want, napi_value *argv)
+{
+    size_t argc = want;
+    if (napi_get_cb_info(env, info, &argc, argv, NULL, NULL) != napi_ok || argc < want) {
+        napi_throw_type_error(env, NULL, "gk_addon: wrong number of arguments");
+        return 0;
+    }
+    return 1;
+}
+
+static void *get_ext(napi_env env, napi_value v)
+{
+    void *p = NULL;
+    if (napi_get_value_external(env, v, &p) != napi_ok) return NULL;
+    return p;
+}
+
+/* typed array data pointer (any element type); NULL for null/undefined */
+static void *ta(napi_env env, napi_value v)
+{
+    napi_valuetype t;
+    napi_typeof(env, v, &t);
+    if (t == napi_null || t == napi_undefined) return NULL;
+    bool is = false;
+    napi_is_typedarray(env, v, &is);
+    if (!is) return NULL;
+    napi_typedarray_type type;
+    size_t len, off;
+    void *data;
+    napi_value ab;
+    if (napi_get_typedarray_info(env, v, &type, &len, &data, &ab, &off) != napi_ok) return NULL;
+    return data;
+}
+
+static napi_value prop(napi_env env, napi_value obj, const char *name)
+{
+    napi_value v;
+    if (napi_get_named_property(env, obj, name, &v) != napi_ok) return NULL;
+    return v;
+}
+
+static double dprop(napi_env env, napi_value obj, const char *name, double def)
+{
+    napi_value v = prop(env, obj, name);
+    double d;
+    if (!v || napi_get_value_double(env, v, &d) != napi_ok) return def;
+    return d;
+}
+
+static void *tprop(napi_env env, napi_value obj, const char *name)
+{
+    napi_value v = prop(env, obj, name);
+    return v ? ta(env, v) : NULL;
+}
+
+static void set_num(napi_env env, napi_value obj, const char *name, double v)
+{
+    napi_value x;
+    napi_create_double(env, v, &x);
+    napi_set_named_property(env, obj, name, x);
+}
+
+/* ---------------------------------------------------------------- context */
+static void ctx_fin(napi_env env, void *data, void *hint)
+{
+    (void)env; (void)hint;
+    gk_ctx_destroy((gk_ctx *)data);
+}
+
+static napi_value js_create(napi_env env, napi_callback_info info)
+{
+    napi_value argv[1];
+    if (!get_args(env, info, 1, argv)) return NULL;
+    int dev = 0;
+    CHECK(napi_get_value_int32(env, argv[0], &dev));
+    gk_ctx *c = gk_ctx_create(dev);
+    if (!c) {
+        char what[64];
+        snprintf(what, sizeof what, "gk_ctx_create(%d)", dev);
+        return throw_gk(env, what);
+    }
+    napi_value r;
+    CHECK(napi_create_external(env, c, ctx_fin, NULL, &r));
+    return r;
+}
+
+static napi_value js_device_count(napi_env env, napi_callback_info info)
+{
+    (void)info;
+    return mk_int(env, gk_device_count());
+}
+
+static napi_value js_abi_version(napi_env env, napi_callback_info info)
+{
+    (void)info;
+    return mk_int(env, gk_abi_version());
+}
+
+static napi_value js_last_error(napi_env env, napi_callback_info info)
+{
+    (void)info;
+    napi_value r;
+    napi_create_string_utf8(env, gk_last_error(), NAPI_AUTO_LENGTH, &r);
+    return r;
+}
+
+/* -------------------------------------------------------------------- bfd */
+static void bfd_fin(napi_env env, void *data, void *hint)
+{
+    (void)env; (void)hint;
+    gk_bfd_destroy((gk_bfd *)data);
+}
+
+static napi_value js_bfd_create(napi_env env, napi_callback_info info)
+{
+    napi_value argv[1];
+    if (!get_args(env, info, 1, argv)) return NULL;
+    gk_ctx *c = (gk_ctx *)get_ext(env, argv[0]);
+    gk_bfd *b = gk_bfd_create(c);
+    if (!b) return throw_gk(env, "bfd_create_it");
+    napi_value r;
+    CHECK(napi_create_external(env, b, bfd_fin, NULL, &r));
+    return r;
+}
+
+static napi_value js_bfd_set_parm(napi_env env, napi_callback_info info)
+{
+    napi_value argv[2];
+    if (!get_args(env, info, 2, argv)) return NULL;
+    gk_bfd *b = (gk_bfd *)get_ext(env, argv[0]);
+    gk_bfcp p;
+    p.type = (int)dprop(env, argv[1], "type", 1);
+    p.lu_size = (int)dprop(env, argv[1], "lu_size", 0);
+    p.piv_tol = dprop(env, argv[1], "piv_tol", 0.10);
+    p.piv_lim = (int)dprop(env, argv[1], "piv_lim", 4);
+    p.suhl = (int)dprop(env, argv[1], "suhl", 1);
+    p.eps_tol = dprop(env, argv[1], "eps_tol", 1e-15);
+    p.max_gro = dprop(env, argv[1], "max_gro", 1e10);
+    p.nfs_max = (int)dprop(env, argv[1], "nfs_max", 100);
+    p.upd_tol = dprop(env, argv[1], "upd_tol", 1e-6);
+    p.nrs_max = (int)dprop(env, argv[1], "nrs_max", 100);
+    p.rs_size = (int)dprop(env, argv[1], "rs_size", 0);
+    gk_bfd_set_parm(b, &p);
+    return NULL;
+}
+
+static napi_value js_bfd_factorize_csc(napi_env env, napi_callback_info info)
+{
+    napi_value argv[5];
+    if (!get_args(env, info, 5, argv)) return NULL;
+    gk_bfd *b = (gk_bfd *)get_ext(env, argv[0]);
+    int m = 0;
+    CHECK(napi_get_value_int32(env, argv[1], &m));
+    const int *ptr = (const int *)ta(env, argv[2]);
+    const int *ind = (const int *)ta(env, argv[3]);
+    const double *val = (const double *)ta(env, argv[4]);
+    if (!ptr || !ind || !val) {
+        napi_throw_type_error(env, NULL, "bfdFactorizeCsc: ptr/ind must be Int32Array, val Float64Array");
+        return NULL;
+    }
+    int ret = gk_bfd_factorize_csc(b, m, ptr, ind, val);
+    if (ret == GK_EABI) return throw_gk(env, "bfd_factorize");
+    return mk_int(env, ret);
+}
+
+static napi_value solve(napi_env env, napi_callback_info info, int tr)
+{
+    napi_value argv[2];
+    if (!get_args(env, info, 2, argv)) return NULL;
+    gk_bfd *b = (gk_bfd *)get_ext(env, argv[0]);
+    double *x = (double *)ta(env, argv[1]);
+    if (!x) {
+        napi_throw_type_error(env, NULL, "bfd_ftran/btran: x must be a Float64Array");
+        return NULL;
+    }
+    if (!gk_bfd_valid(b)) {
+        napi_throw_error(env, NULL, tr ? "bfd_btran: factorization is not valid" : "bfd_ftran: factorization is not valid");
+        return NULL;
+    }
+    if (tr) gk_bfd_btran(b, x);
+    else gk_bfd_ftran(b, x);
+    return NULL;
+}
+
+static napi_value js_bfd_ftran(napi_env env, napi_callback_info info) { return solve(env, info, 0); }
+static napi_value js_bfd_btran(napi_env env, napi_callback_info info) { return solve(env, info, 1); }
+
+static napi_value js_bfd_update(napi_env env, napi_callback_info info)
+{
+    napi_value argv[6];
+    if (!get_args(env, info, 6, argv)) return NULL;
+    gk_bfd *b = (gk_bfd *)get_ext(env, argv[0]);
+    int j, len, idx;
+    CHECK(napi_get_value_int32(env, argv[1], &j));
+    CHECK(napi_get_value_int32(env, argv[2], &len));
+    CHECK(napi_get_value_int32(env, argv[4], &idx));
+    const int *ind = (const int *)ta(env, argv[3]);
+    const double *val = (const double *)ta(env, argv[5]);
+    int ret = gk_bfd_update(b, j, len, ind, idx, val);
+    if (ret == GK_EABI) return throw_gk(env, "bfd_update_it");
+    return mk_int(env, ret);
+}
+
+static napi_value js_bfd_get_count(napi_env env, napi_callback_info info)
+{
+    napi_value argv[1];
+    if (!get_args(env, info, 1, argv)) return NULL;
+    int r = gk_bfd_get_count((gk_bfd *)get_ext(env, argv[0]));
+    if (r == GK_EABI) return throw_gk(env, "bfd_get_count");
+    return mk_int(env, r);
+}
+
+static napi_value js_bfd_valid(napi_env env, napi_callback_info info)
+{
+    napi_value argv[1];
+    if (!get_args(env, info, 1, argv)) return NULL;
+    return mk_int(env, gk_bfd_valid((gk_bfd *)get_ext(env, argv[0])));
+}
+
+/* -------------------------------------------------------------------- spx */
+static napi_value js_spx(napi_env env, napi_callback_info info)
+{
+    napi_value argv[5];
+    if (!get_args(env, info, 5, argv)) return NULL;
+    gk_ctx *c = (gk_ctx *)get_ext(env, argv[0]);
+    gk_bfd *b = (gk_bfd *)get_ext(env, argv[1]);
+    napi_value L = argv[2], S = argv[3];
+    bool dual = false;
+    CHECK(napi_get_value_bool(env, argv[4], &dual));
+    gk_lp lp;
+    memset(&lp, 0, sizeof lp);
+    lp.m = (int)dprop(env, L, "m", 0);
+    lp.n = (int)dprop(env, L, "n", 0);
+    lp.nnz = (int)dprop(env, L, "nnz", 0);
+    lp.dir = (int)dprop(env, L, "dir", 1);
+    lp.c0 = dprop(env, L, "c0", 0.0);
+    lp.row_type = (const signed char *)tprop(env, L, "row_type");
+    lp.row_lb = (const double *)tprop(env, L, "row_lb");
+    lp.row_ub = (const double *)tprop(env, L, "row_ub");
+    lp.rii = (const double *)tprop(env, L, "rii");
+    lp.col_type = (const signed char *)tprop(env, L, "col_type");
+    lp.col_lb = (const double *)tprop(env, L, "col_lb");
+    lp.col_ub = (const double *)tprop(env, L, "col_ub");
+    lp.col_coef = (const double *)tprop(env, L, "col_coef");
+    lp.sjj = (const double *)tprop(env, L, "sjj");
+    lp.A_ptr = (const int *)tprop(env, L, "A_ptr");
+    lp.A_ind = (const int *)tprop(env, L, "A_ind");
+    lp.A_val = (const double *)tprop(env, L, "A_val");
+    lp.a_version = (unsigned long long)dprop(env, L, "a_version", 0);
+    lp.head = (int *)tprop(env, L, "head");
+    lp.row_stat = (signed char *)tprop(env, L, "row_stat");
+    lp.col_stat = (signed char *)tprop(env, L, "col_stat");
+    lp.row_bind = (int *)tprop(env, L, "row_bind");
+    lp.col_bind = (int *)tprop(env, L, "col_bind");
+    lp.row_prim = (double *)tprop(env, L, "row_prim");
+    lp.row_dual = (double *)tprop(env, L, "row_dual");
+    lp.col_prim = (double *)tprop(env, L, "col_prim");
+    lp.col_dual = (double *)tprop(env, L, "col_dual");
+    lp.it_cnt = (int)dprop(env, L, "it_cnt", 0);
+    if (!lp.row_type || !lp.row_lb || !lp.row_ub || !lp.rii || !lp.col_type || !lp.col_lb || !lp.col_ub ||
+        !lp.col_coef || !lp.sjj || !lp.A_ptr || !lp.A_ind || !lp.A_val || !lp.head || !lp.row_stat ||
+        !lp.col_stat || !lp.row_prim || !lp.row_dual || !lp.col_prim || !lp.col_dual) {
+        napi_throw_type_error(env, NULL, "spx: lp arrays missing or not typed arrays");
+        return NULL;
+    }
+    gk_smcp p;
+    p.msg_lev = (int)dprop(env, S, "msg_lev", 3);
+    p.meth = (int)dprop(env, S, "meth", 1);
+    p.pricing = (int)dprop(env, S, "pricing", 0x22);
+    p.r_test = (int)dprop(env, S, "r_test", 0x22);
+    p.tol_bnd = dprop(env, S, "tol_bnd", 1e-7);
+    p.tol_dj = dprop(env, S, "tol_dj", 1e-7);
+    p.tol_piv = dprop(env, S, "tol_piv", 1e-10);
+    p.obj_ll = dprop(env, S, "obj_ll", -1.7976931348623157e308);
+    p.obj_ul = dprop(env, S, "obj_ul", +1.7976931348623157e308);
+    p.it_lim = (int)dprop(env, S, "it_lim", 2147483647.0);
+    p.tm_lim = (int)dprop(env, S, "tm_lim", 2147483647.0);
+    p.out_frq = (int)dprop(env, S, "out_frq", 500);
+    p.out_dly = (int)dprop(env, S, "out_dly", 0);
+    p.presolve = (int)dprop(env, S, "presolve", 0);
+    int ret = dual ? gk_spx_dual(c, &lp, b, &p) : gk_spx_primal(c, &lp, b, &p);
+    if (ret == GK_EABI) return throw_gk(env, dual ? "spx_dual" : "spx_primal");
+    set_num(env, L, "it_cnt", lp.it_cnt);
+    set_num(env, L, "pbs_stat", lp.pbs_stat);
+    set_num(env, L, "dbs_stat", lp.dbs_stat);
+    set_num(env, L, "some", lp.some);
+    set_num(env, L, "obj_val", lp.obj_val);
+    set_num(env, L, "valid", lp.valid);
+    return mk_int(env, ret);
+}
+
+static napi_value js_stats(napi_env env, napi_callback_info info)
+{
+    napi_value argv[1];
+    if (!get_args(env, info, 1, argv)) return NULL;
+    gk_spx_stats st;
+    memset(&st, 0, sizeof st);
+    gk_bfd_last_stats((gk_bfd *)get_ext(env, argv[0]), &st);
+    napi_value o;
+    CHECK(napi_create_object(env, &o));
+    set_num(env, o, "pivots", (double)st.pivots);
+    set_num(env, o, "reinversions", (double)st.reinversions);
+    set_num(env, o, "batches", (double)st.batches);
+    set_num(env, o, "seconds_total", st.seconds_total);
+    set_num(env, o, "bytes_pivots", st.bytes_pivots);
+    return o;
+}
+
+#define FN(name, f) { name, NULL, f, NULL, NULL, NULL, napi_enumerable, NULL }
+
+static napi_value init(napi_env env, napi_value exports)
+{
+    napi_property_descriptor d[] = {
+        FN("create", js_create), FN("deviceCount", js_device_count), FN("abiVersion", js_abi_version),
+        FN("lastError", js_last_error), FN("bfdCreate", js_bfd_create), FN("bfdSetParm", js_bfd_set_parm),
+        FN("bfdFactorizeCsc", js_bfd_factorize_csc), FN("bfdFtran", js_bfd_ftran), FN("bfdBtran", js_bfd_btran),
+        FN("bfdUpdate", js_bfd_update), FN("bfdGetCount", js_bfd_get_count), FN("bfdValid", js_bfd_valid),
+        FN("spx", js_spx), FN("stats", js_stats),
+    };
+    napi_define_properties(env, exports, sizeof d / sizeof d[0], d);
+    return exports;
+}
+
+NAPI_MODULE(NODE_GYP_MODULE_NAME, init)

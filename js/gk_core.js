@@ -1,0 +1,168 @@
+// gk_core.js — JS side of the drop-in boundary (Node.js, CommonJS).
+//
+// Marshals the reference's problem object (`lp`, glpapi01.js) into the flat,
+// 1-based typed arrays of gk_lp (include/glpk_mi355x.h) — exactly the fields
+// init_csa reads (glpspx01.js:42-145 / glpspx02.js:89-190) — calls the native
+// core through the N-API addon (js/gk_addon.c), and writes back what
+// store_sol writes (glpspx01.js:1591-1681 / glpspx02.js:1499-1590).
+//
+// There is no CPU fallback: without a gfx950 device the first call throws
+// the native error text.
+'use strict';
+var path = require('path');
+
+var addon = require(path.join(__dirname, 'build', 'gk_addon.node'));
+
+var GLP_BS = 1, GLP_UNDEF = 1, GLP_EFAIL = 0x05;
+var ctx = null;
+var version = 0;
+
+function context() {
+    if (ctx === null) ctx = addon.create(parseInt(process.env.GK_DEVICE || '0', 10));
+    return ctx;
+}
+
+function nextVersion() { return ++version; }
+
+// ---- lp.bfd (glpbfd.js) ------------------------------------------------------
+function bfdCreate() {
+    // the JS object the reference keeps in lp.bfd; the native factor is owned
+    // by the addon external (freed by its finalizer)
+    return {gk: addon.bfdCreate(context()), valid: 0, m: 0};
+}
+
+function bfdSetParm(bfd, parm) { addon.bfdSetParm(bfd.gk, parm); }
+
+// bfd_factorize(bfd, m, bh, col, info) (glpbfd.js:47): the columns come from
+// the reference's own callback col(info, j, ind, val) (b_col, glpapi12.js:7)
+function bfdFactorize(bfd, m, bh, col, info) {
+    var ptr = new Int32Array(m + 2), tind = new Int32Array(m + 1), tval = new Float64Array(m + 1);
+    var ind = [0], val = [0];
+    ptr[1] = 1;
+    for (var j = 1; j <= m; j++) {
+        var len = col(info, j, tind, tval);
+        for (var t = 1; t <= len; t++) { ind.push(tind[t]); val.push(tval[t]); }
+        ptr[j + 1] = ptr[j] + len;
+    }
+    var ret = addon.bfdFactorizeCsc(bfd.gk, m, ptr, Int32Array.from(ind), Float64Array.from(val));
+    bfd.valid = ret === 0 ? 1 : 0;
+    bfd.m = m;
+    return ret;
+}
+
+function solve(bfd, x, tr) {
+    var y = (x instanceof Float64Array) ? x : Float64Array.from(x);
+    if (tr) addon.bfdBtran(bfd.gk, y); else addon.bfdFtran(bfd.gk, y);
+    if (y !== x) for (var i = 1; i <= bfd.m; i++) x[i] = y[i];
+}
+function bfdFtran(bfd, x) { solve(bfd, x, 0); }
+function bfdBtran(bfd, x) { solve(bfd, x, 1); }
+
+function bfdUpdate(bfd, j, bh, len, ind, idx, val) {
+    var ret = addon.bfdUpdate(bfd.gk, j, len, Int32Array.from(ind), idx, Float64Array.from(val));
+    if (ret !== 0) bfd.valid = 0;
+    return ret;
+}
+function bfdGetCount(bfd) { return addon.bfdGetCount(bfd.gk); }
+
+// ---- spx_primal / spx_dual ---------------------------------------------------
+function arrays(lp) {
+    var m = lp.m, n = lp.n, g = lp.__gk;
+    if (!g || g.m !== m || g.n !== n) {
+        g = lp.__gk = {
+            m: m, n: n,
+            row_type: new Int8Array(m + 1), row_lb: new Float64Array(m + 1), row_ub: new Float64Array(m + 1),
+            rii: new Float64Array(m + 1), row_stat: new Int8Array(m + 1), row_bind: new Int32Array(m + 1),
+            row_prim: new Float64Array(m + 1), row_dual: new Float64Array(m + 1),
+            col_type: new Int8Array(n + 1), col_lb: new Float64Array(n + 1), col_ub: new Float64Array(n + 1),
+            col_coef: new Float64Array(n + 1), sjj: new Float64Array(n + 1), col_stat: new Int8Array(n + 1),
+            col_bind: new Int32Array(n + 1), col_prim: new Float64Array(n + 1), col_dual: new Float64Array(n + 1),
+            head: new Int32Array(m + 1), a_version: 0
+        };
+    }
+    return g;
+}
+
+// A by columns in list order (init_csa glpspx01.js:96-108), unscaled; the
+// device scales rii * a * sjj in the same order.  Re-walked only when a
+// matrix/scale mutator ran since the last call (lp.__gk_version).
+function marshalMatrix(lp, g) {
+    if (lp.__gk_version === undefined) lp.__gk_version = nextVersion();
+    if (g.a_version === lp.__gk_version && g.nnz === lp.nnz) return;
+    var n = lp.n, nnz = lp.nnz;
+    var ptr = new Int32Array(n + 2), ind = new Int32Array(nnz + 1), val = new Float64Array(nnz + 1);
+    var loc = 1;
+    for (var j = 1; j <= n; j++) {
+        ptr[j] = loc;
+        for (var aij = lp.col[j].ptr; aij !== null; aij = aij.c_next) {
+            ind[loc] = aij.row.i;
+            val[loc] = aij.val;
+            loc++;
+        }
+    }
+    ptr[n + 1] = loc;
+    if (loc !== nnz + 1) throw new Error('assert');
+    g.A_ptr = ptr; g.A_ind = ind; g.A_val = val; g.nnz = nnz;
+    g.a_version = lp.__gk_version;
+}
+
+function spx(lp, parm, dual) {
+    var m = lp.m, n = lp.n, i, j, row, col;
+    var g = arrays(lp);
+    for (i = 1; i <= m; i++) {
+        row = lp.row[i];
+        g.row_type[i] = row.type; g.row_lb[i] = row.lb; g.row_ub[i] = row.ub;
+        g.rii[i] = row.rii; g.row_stat[i] = row.stat;
+    }
+    for (j = 1; j <= n; j++) {
+        col = lp.col[j];
+        g.col_type[j] = col.type; g.col_lb[j] = col.lb; g.col_ub[j] = col.ub;
+        g.col_coef[j] = col.coef; g.sjj[j] = col.sjj; g.col_stat[j] = col.stat;
+    }
+    for (i = 1; i <= m; i++) g.head[i] = lp.head[i];
+    marshalMatrix(lp, g);
+    var L = {
+        m: m, n: n, nnz: lp.nnz, dir: lp.dir, c0: lp.c0, a_version: g.a_version, it_cnt: lp.it_cnt,
+        row_type: g.row_type, row_lb: g.row_lb, row_ub: g.row_ub, rii: g.rii,
+        col_type: g.col_type, col_lb: g.col_lb, col_ub: g.col_ub, col_coef: g.col_coef, sjj: g.sjj,
+        A_ptr: g.A_ptr, A_ind: g.A_ind, A_val: g.A_val, head: g.head,
+        row_stat: g.row_stat, col_stat: g.col_stat, row_bind: g.row_bind, col_bind: g.col_bind,
+        row_prim: g.row_prim, row_dual: g.row_dual, col_prim: g.col_prim, col_dual: g.col_dual
+    };
+    // init_csa asserts lp.valid and takes lp.bfd (glpspx01.js:129-132)
+    if (!lp.valid || lp.bfd === null) throw new Error('assert');
+    var ret = addon.spx(context(), lp.bfd.gk, L, parm, dual);
+    lp.valid = L.valid;
+    lp.bfd.valid = L.valid;
+    lp.pbs_stat = L.pbs_stat;
+    lp.dbs_stat = L.dbs_stat;
+    lp.obj_val = L.obj_val;
+    lp.it_cnt = L.it_cnt;
+    lp.some = L.some;
+    if (L.valid) {
+        // store_sol
+        for (i = 1; i <= m; i++) lp.head[i] = g.head[i];
+        for (i = 1; i <= m; i++) {
+            row = lp.row[i];
+            row.stat = g.row_stat[i]; row.bind = g.row_bind[i];
+            row.prim = g.row_prim[i]; row.dual = g.row_dual[i];
+        }
+        for (j = 1; j <= n; j++) {
+            col = lp.col[j];
+            col.stat = g.col_stat[j]; col.bind = g.col_bind[j];
+            col.prim = g.col_prim[j]; col.dual = g.col_dual[j];
+        }
+    } else if (ret === GLP_EFAIL) {
+        lp.pbs_stat = lp.dbs_stat = GLP_UNDEF;
+        lp.obj_val = 0.0;
+        lp.some = 0;
+    }
+    return ret;
+}
+
+module.exports = {
+    addon: addon, context: context, nextVersion: nextVersion,
+    bfdCreate: bfdCreate, bfdSetParm: bfdSetParm, bfdFactorize: bfdFactorize,
+    bfdFtran: bfdFtran, bfdBtran: bfdBtran, bfdUpdate: bfdUpdate, bfdGetCount: bfdGetCount,
+    spx: spx, GLP_BS: GLP_BS
+};

@@ -1,0 +1,43 @@
+// gk_shim.js — concatenated into the reference bundle after lib/*.js (see
+// js/load_glpk.js).  The bundle is one closure, so assigning to its function
+// names rebinds every internal caller:
+//   solve_lp (glpapi06.js:27-37)          -> spx_primal / spx_dual
+//   glp_factorize / glp_ftran / glp_btran -> bfd_* (glpapi12.js:75-105, 211, 240)
+// Matrix and scale mutators bump lp.__gk_version so the device copy of A is
+// re-uploaded only when A or the scaling changed (SURVEY.md §8(b).1).
+var __gk = require(__gk_core_path);
+
+spx_primal = function (lp, parm) { return __gk.spx(lp, parm, false); };
+spx_dual = function (lp, parm) { return __gk.spx(lp, parm, true); };
+bfd_create_it = function () { return __gk.bfdCreate(); };
+bfd_set_parm = function (bfd, parm) { __gk.bfdSetParm(bfd, parm); };
+bfd_factorize = function (bfd, m, bh, col, info) { return __gk.bfdFactorize(bfd, m, bh, col, info); };
+bfd_ftran = function (bfd, x) { __gk.bfdFtran(bfd, x); };
+bfd_btran = function (bfd, x) { __gk.bfdBtran(bfd, x); };
+bfd_update_it = function (bfd, j, bh, len, ind, idx, val) { return __gk.bfdUpdate(bfd, j, bh, len, ind, idx, val); };
+bfd_get_count = function (bfd) { return __gk.bfdGetCount(bfd); };
+
+(function () {
+    function versioned(f) {
+        return function (lp) {
+            var r = f.apply(this, arguments);
+            lp.__gk_version = __gk.nextVersion();
+            return r;
+        };
+    }
+    glp_set_mat_row = exports["glp_set_mat_row"] = versioned(glp_set_mat_row);
+    glp_set_mat_col = exports["glp_set_mat_col"] = versioned(glp_set_mat_col);
+    glp_load_matrix = exports["glp_load_matrix"] = versioned(glp_load_matrix);
+    glp_add_rows = exports["glp_add_rows"] = versioned(glp_add_rows);
+    glp_add_cols = exports["glp_add_cols"] = versioned(glp_add_cols);
+    glp_del_rows = exports["glp_del_rows"] = versioned(glp_del_rows);
+    glp_del_cols = exports["glp_del_cols"] = versioned(glp_del_cols);
+    glp_set_rii = exports["glp_set_rii"] = versioned(glp_set_rii);
+    glp_set_sjj = exports["glp_set_sjj"] = versioned(glp_set_sjj);
+    glp_scale_prob = exports["glp_scale_prob"] = versioned(glp_scale_prob);
+    glp_unscale_prob = exports["glp_unscale_prob"] = versioned(glp_unscale_prob);
+    glp_sort_matrix = exports["glp_sort_matrix"] = versioned(glp_sort_matrix);
+    glp_erase_prob = exports["glp_erase_prob"] = versioned(glp_erase_prob);
+    glp_copy_prob = exports["glp_copy_prob"] = versioned(glp_copy_prob);
+})();
+exports["__gk_core"] = __gk;

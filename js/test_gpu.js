@@ -1,0 +1,115 @@
+// GPU parity of the JS boundary (runs on the MI355X box: node + the addon,
+// no reference code there).  For every explicit LP fixture in tests/golden it
+// builds a problem object with the reference's field layout (glpapi01.js:
+// lp.row[i] / lp.col[j] records, column lists of aij elements), runs the
+// solve_lp flow of glp_simplex (glpapi06.js:3-37) — glp_factorize through
+// bfd_factorize with the reference's b_col column callback, then spx_* —
+// through js/gk_core.js, and compares with the reference's recorded result.
+'use strict';
+var assert = require('assert');
+var fs = require('fs');
+var path = require('path');
+var core = require(path.join(__dirname, 'gk_core.js'));
+
+var GLP_BS = 1, GLP_PRIMAL = 1, GLP_DUALP = 2, GLP_DUAL = 3, GLP_EFAIL = 5;
+var DBL_MAX = Number.MAX_VALUE, INT_MAX = 0x7FFFFFFF;
+
+function smcp(o) {  // SMCP with the reference's `||` defaults (glpapi06.js:359-375)
+    o = o || {};
+    return {msg_lev: o.msg_lev || 3, meth: o.meth || GLP_PRIMAL, pricing: o.pricing || 0x22,
+            r_test: o.r_test || 0x22, tol_bnd: o.tol_bnd || 1e-7, tol_dj: o.tol_dj || 1e-7,
+            tol_piv: o.tol_piv || 1e-10, obj_ll: o.obj_ll || -DBL_MAX, obj_ul: o.obj_ul || +DBL_MAX,
+            it_lim: o.it_lim || INT_MAX, tm_lim: o.tm_lim || INT_MAX, out_frq: o.out_frq || 500,
+            out_dly: o.out_dly || 0, presolve: 0};
+}
+
+function buildLp(fx) {
+    var lp = {m: fx.m, n: fx.n, nnz: fx.nnz, dir: fx.dir, c0: fx.c0, row: [null], col: [null],
+              head: new Int32Array(fx.m + 1), valid: 0, bfd: null, it_cnt: 0};
+    for (var i = 1; i <= fx.m; i++)
+        lp.row.push({i: i, type: fx.row_type[i - 1], lb: fx.row_lb[i - 1], ub: fx.row_ub[i - 1],
+                     rii: fx.row_rii[i - 1], stat: fx.row_stat[i - 1], bind: 0, prim: 0, dual: 0});
+    for (var j = 1; j <= fx.n; j++) {
+        var col = {j: j, type: fx.col_type[j - 1], lb: fx.col_lb[j - 1], ub: fx.col_ub[j - 1],
+                   coef: fx.col_coef[j - 1], sjj: fx.col_sjj[j - 1], stat: fx.col_stat[j - 1],
+                   bind: 0, prim: 0, dual: 0, ptr: null};
+        var last = null;
+        for (var t = fx.A_ptr[j - 1]; t < fx.A_ptr[j]; t++) {
+            var aij = {row: lp.row[fx.A_ind[t]], col: col, val: fx.A_val[t], c_next: null};
+            if (last === null) col.ptr = aij; else last.c_next = aij;
+            last = aij;
+        }
+        lp.col.push(col);
+    }
+    return lp;
+}
+
+// glp_factorize (glpapi12.js:5-94) with b_col (:7-31)
+function factorize(lp) {
+    var m = lp.m, n = lp.n, j = 0;
+    lp.valid = 0;
+    for (var k = 1; k <= m + n; k++) {
+        var rec = k <= m ? lp.row[k] : lp.col[k - m];
+        rec.bind = 0;
+        if (rec.stat === GLP_BS) {
+            j++;
+            if (j > m) return 0x02;               // GLP_EBADB
+            lp.head[j] = k;
+            rec.bind = j;
+        }
+    }
+    if (j < m) return 0x02;
+    if (lp.bfd === null) lp.bfd = core.bfdCreate();
+    function bCol(lp, jj, ind, val) {
+        var kk = lp.head[jj];
+        if (kk <= m) { ind[1] = kk; val[1] = 1.0; return 1; }
+        var len = 0;
+        for (var aij = lp.col[kk - m].ptr; aij !== null; aij = aij.c_next) {
+            len++;
+            ind[len] = aij.row.i;
+            val[len] = -aij.row.rii * aij.val * aij.col.sjj;
+        }
+        return len;
+    }
+    var ret = core.bfdFactorize(lp.bfd, m, lp.head, bCol, lp);
+    if (ret === 1) return 0x03;                   // GLP_ESING
+    if (ret === 2) return 0x04;                   // GLP_ECOND
+    lp.valid = 1;
+    return 0;
+}
+
+function simplex(lp, parm) {   // solve_lp (glpapi06.js:3-37)
+    if (!lp.valid) {
+        var r = factorize(lp);
+        if (r) return r;
+    }
+    if (parm.meth === GLP_PRIMAL) return core.spx(lp, parm, false);
+    if (parm.meth === GLP_DUALP) {
+        var ret = core.spx(lp, parm, true);
+        if (ret === GLP_EFAIL && lp.valid) ret = core.spx(lp, parm, false);
+        return ret;
+    }
+    return core.spx(lp, parm, true);
+}
+
+var dir = path.join(__dirname, '..', 'tests', 'golden');
+var files = fs.readdirSync(dir).filter(function (f) { return /^lp_.*\.json$/.test(f); }).sort();
+var ncase = 0;
+files.forEach(function (f) {
+    var fx = JSON.parse(fs.readFileSync(path.join(dir, f), 'utf8'));
+    if (fx.gen || fx.row_type === undefined) return;          // generated instances: Python tests
+    fx.runs.forEach(function (run, r) {
+        var lp = buildLp(fx);
+        var ret = simplex(lp, smcp(run.opts));
+        var tag = f + '#' + r;
+        assert.strictEqual(ret, run.ret, tag + ' ret');
+        assert.strictEqual(lp.pbs_stat, run.pbs_stat, tag + ' pbs_stat');
+        assert.strictEqual(lp.dbs_stat, run.dbs_stat, tag + ' dbs_stat');
+        var scale = Math.max(1.0, Math.abs(run.obj_val));
+        assert.ok(Math.abs(lp.obj_val - run.obj_val) <= 1e-9 * scale, tag + ' obj ' + lp.obj_val + ' vs ' + run.obj_val);
+        if (run.opts && run.opts.it_lim) assert.strictEqual(lp.it_cnt, run.it_cnt, tag + ' it_cnt');
+        ncase++;
+    });
+});
+assert.ok(ncase > 50, 'too few cases: ' + ncase);
+console.log('ok js gpu parity: ' + ncase + ' runs');

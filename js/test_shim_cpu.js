@@ -1,0 +1,45 @@
+// CPU-side checks of the JS boundary (no GPU here): the addon loads and
+// exports the binding, the reference bundle loads with the shim, the hot-path
+// names are rebound, and a solve fails loudly (no fallback to the JS simplex).
+'use strict';
+var assert = require('assert');
+var path = require('path');
+var core = require(path.join(__dirname, 'gk_core.js'));
+
+var names = ['create', 'deviceCount', 'abiVersion', 'lastError', 'bfdCreate', 'bfdSetParm', 'bfdFactorizeCsc',
+             'bfdFtran', 'bfdBtran', 'bfdUpdate', 'bfdGetCount', 'bfdValid', 'spx', 'stats'];
+names.forEach(function (k) { assert.strictEqual(typeof core.addon[k], 'function', k); });
+assert.strictEqual(core.addon.abiVersion(), 1);
+
+var ref = process.env.GLPK_REF || '/root/reference';
+var fs = require('fs');
+if (!fs.existsSync(path.join(ref, 'lib'))) {
+    console.log('ok addon (reference tree absent: shim test skipped)');
+    process.exit(0);
+}
+var glpk = require(path.join(__dirname, 'load_glpk.js'))(ref);
+assert.ok(glpk.__gk_core, 'shim not concatenated');
+glpk.glp_set_print_func(function () {});
+var lp = glpk.glp_create_prob();
+glpk.glp_set_obj_dir(lp, glpk.GLP_MAX);
+glpk.glp_add_rows(lp, 1);
+glpk.glp_set_row_bnds(lp, 1, glpk.GLP_UP, 0, 4);
+glpk.glp_add_cols(lp, 2);
+glpk.glp_set_col_bnds(lp, 1, glpk.GLP_LO, 0, 0);
+glpk.glp_set_col_bnds(lp, 2, glpk.GLP_LO, 0, 0);
+glpk.glp_set_obj_coef(lp, 1, 1);
+glpk.glp_set_obj_coef(lp, 2, 2);
+glpk.glp_load_matrix(lp, 2, [0, 1, 1], [0, 1, 2], [0, 1, 1]);
+assert.ok(lp.__gk_version > 0, 'glp_load_matrix not versioned');
+var threw = null;
+try {
+    glpk.glp_simplex(lp, new glpk.SMCP({presolve: glpk.GLP_OFF}));
+} catch (e) { threw = e; }
+if (core.addon.deviceCount() === 0) {
+    assert.ok(threw && /gk_ctx_create|device/.test(threw.message), 'expected a loud device error, got ' + threw);
+    console.log('ok shim (no device: ' + threw.message + ')');
+} else {
+    assert.ok(!threw, String(threw));
+    assert.strictEqual(glpk.glp_get_obj_val(lp), 8);
+    console.log('ok shim (device solve: obj ' + glpk.glp_get_obj_val(lp) + ')');
+}
