@@ -1675,9 +1675,17 @@ extern "C" double gk_bfd_time_kernel(gk_bfd *f, int which, int reps, double *byt
     }
 }
 
-// placeholder until the native branch-and-bound driver lands (gk_ios.hip)
-extern "C" __attribute__((weak)) int gk_ios_driver(gk_ctx *, gk_mip *, const gk_iocp *)
+// accessors for the other translation units (gk_mip.hip)
+int gk_ctx_device(gk_ctx *c) { return c->device; }
+hipStream_t gk_ctx_stream(gk_ctx *c) { return c->stream; }
+namespace gk {
+void set_err(const char *fmt, ...)
 {
-    set_err("gk_ios_driver: not available in this build");
-    return GK_EABI;
+    char buf[1024];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof buf, fmt, ap);
+    va_end(ap);
+    g_err = buf;
 }
+}  // namespace gk

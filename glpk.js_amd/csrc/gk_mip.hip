@@ -1,0 +1,824 @@
+// Branch and bound on the MI355X: batched node LPs.
+//
+// Replaces ios_driver (glpios03.js:1) for cb_func == null.  The reference
+// solves one node LP at a time with glp_simplex (ios_solve_node,
+// glpios01.js:866) and walks the tree depth-first/best-local-bound.  Node LPs
+// of B&B are tiny (gap 20x75, mas76 12x151) and one at a time they cannot
+// occupy a GPU; here the open nodes are solved in BATCHES, one workgroup per
+// node LP, with the whole simplex tableau of the node in LDS:
+//
+//   T = inv(B) [I | -A]   (m x (m+n), fp64, LDS),  x_B = -T_N x_N,
+//   d = c - c_B' T        (reduced costs, internal minimisation form)
+//
+// Each workgroup builds inv(B) for its node's basis by Gauss-Jordan on
+// [B | I | -A] (the parent's optimal basis: a warm start, dual feasible after
+// the branching bound change), runs the bounded dual simplex to optimality,
+// infeasibility or the incumbent cutoff, and returns the solution, its basis
+// and the branching choice of the Driebeck-Tomlin heuristic (branch_drtom,
+// glpios09.js:84) evaluated on its own tableau rows (the reference does this
+// through glp_eval_tab_row / glp_dual_rtest, glpapi12.js:401/:687).
+//
+// The host driver (gk_ios_driver below) keeps the open nodes in a best-bound
+// priority queue, prunes with the incumbent (ios_is_hopeful, glpios01.js:789)
+// and the rounded bound (ios_round_bound, :730), and launches batches of up
+// to 1024 nodes.  Objective and incumbent match the reference (objective
+// parity); the order in which nodes are evaluated — and hence node counts —
+// differs from the reference's sequential walk (SURVEY.md §8(a) design note).
+#include "gk_device.h"
+#include "../../include/glpk_mi355x.h"
+#include <algorithm>
+#include <cfloat>
+#include <chrono>
+#include <cmath>
+#include <cstring>
+#include <queue>
+#include <string>
+#include <vector>
+
+namespace gk {
+
+void set_err(const char *fmt, ...);
+
+enum : int { NODE_OPT = 0, NODE_INFEAS = 1, NODE_CUTOFF = 2, NODE_FAIL = 3 };
+
+struct NodeProb {
+    int m, n, ld;                 // ld = m + n (row length of T)
+    const double *A;              // dense col-major m x n (unscaled)
+    const double *c;              // internal minimisation costs, [m+n] (0 for rows)
+    const signed char *isint;     // [n]
+    double tol_int;
+};
+
+struct NodeIO {
+    const double *lb, *ub;        // [nb][m+n]
+    const signed char *stat_in;   // [nb][m+n]  GLP_BS / NL / NU / NF / NS
+    const double *cutoff;         // [nb]  stop once the dual objective reaches it
+    int *status, *pivots, *jj, *next;
+    double *obj, *x, *dz;         // obj[nb], x[nb][m+n], dz[nb][2]
+    signed char *stat_out;        // [nb][m+n]
+    int it_lim;
+};
+
+// ---- small block helpers (blockDim.x = 256) --------------------------------
+// argmax of key (ties: lowest idx); idx < 0 = none
+__device__ int block_argmax(double key, int idx, double *shk, int *shi)
+{
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        const double k2 = __shfl_xor(key, o);
+        const int i2 = __shfl_xor(idx, o);
+        if (i2 >= 0 && (idx < 0 || k2 > key || (k2 == key && i2 < idx))) { key = k2; idx = i2; }
+    }
+    __syncthreads();
+    if (lane == 0) { shk[w] = key; shi[w] = idx; }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        for (int v = 1; v < (int)(blockDim.x >> 6); ++v)
+            if (shi[v] >= 0 && (shi[0] < 0 || shk[v] > shk[0] || (shk[v] == shk[0] && shi[v] < shi[0]))) {
+                shk[0] = shk[v];
+                shi[0] = shi[v];
+            }
+    }
+    __syncthreads();
+    const int r = shi[0];
+    __syncthreads();
+    return r;
+}
+
+// dual ratio test choice: min ratio, then max |alfa|, then lowest idx
+__device__ int block_ratio(double t, double a, int idx, double *shk, double *sha, int *shi)
+{
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        const double t2 = __shfl_xor(t, o), a2 = __shfl_xor(a, o);
+        const int i2 = __shfl_xor(idx, o);
+        if (i2 >= 0 && (idx < 0 || t2 < t || (t2 == t && (a2 > a || (a2 == a && i2 < idx))))) {
+            t = t2; a = a2; idx = i2;
+        }
+    }
+    __syncthreads();
+    if (lane == 0) { shk[w] = t; sha[w] = a; shi[w] = idx; }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        for (int v = 1; v < (int)(blockDim.x >> 6); ++v) {
+            if (shi[v] < 0) continue;
+            if (shi[0] < 0 || shk[v] < shk[0] || (shk[v] == shk[0] && (sha[v] > sha[0] || (sha[v] == sha[0] && shi[v] < shi[0])))) {
+                shk[0] = shk[v]; sha[0] = sha[v]; shi[0] = shi[v];
+            }
+        }
+    }
+    __syncthreads();
+    const int r = shi[0];
+    __syncthreads();
+    return r;
+}
+
+__device__ double block_sum256(double v, double *sh)
+{
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    v = wsum(v);
+    __syncthreads();
+    if (lane == 0) sh[w] = v;
+    __syncthreads();
+    double r = 0.0;
+    for (int k = 0; k < (int)(blockDim.x >> 6); ++k) r += sh[k];
+    __syncthreads();
+    return r;
+}
+
+__device__ __forceinline__ double nb_value(int st, double lb, double ub)
+{
+    switch (st) {
+    case NL: return lb;
+    case NU: return ub;
+    case NF: return 0.0;
+    default: return lb;   // NS
+    }
+}
+
+// ---------------------------------------------------------------------------
+// one workgroup = one node LP
+// LDS: M[m][2m+n] during the inversion, then T[m][m+n]; lb, ub, x, d [m+n];
+// head[m], stat[m+n]
+// ---------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) k_node_lp(NodeProb P, NodeIO io)
+{
+    extern __shared__ double lds[];
+    __shared__ double shk[4], sha[4];
+    __shared__ int shi[4];
+    __shared__ int sh_flag;
+    const int m = P.m, n = P.n, N = m + n, b = blockIdx.x;
+    const int W = 2 * m + n;                 // width of [B | I | -A]
+    double *M = lds;                          // m * W
+    double *lb = M + (size_t)m * W, *ub = lb + N, *x = ub + N, *d = x + N;
+    int *head = (int *)(d + N);
+    signed char *stat = (signed char *)(head + m);
+    const double *glb = io.lb + (size_t)b * N, *gub = io.ub + (size_t)b * N;
+    const signed char *gst = io.stat_in + (size_t)b * N;
+    for (int k = threadIdx.x; k < N; k += blockDim.x) {
+        lb[k] = glb[k];
+        ub[k] = gub[k];
+        stat[k] = gst[k];
+    }
+    __syncthreads();
+    // basis header in variable order (glp_factorize's head, glpapi12.js:44-67)
+    if (threadIdx.x == 0) {
+        int j = 0;
+        for (int k = 0; k < N && j <= m; ++k)
+            if (stat[k] == BS) {
+                if (j < m) head[j] = k;
+                j++;
+            }
+        sh_flag = (j == m) ? 0 : 1;
+    }
+    __syncthreads();
+    if (sh_flag) {
+        if (threadIdx.x == 0) { io.status[b] = NODE_FAIL; io.pivots[b] = 0; }
+        return;
+    }
+    // M = [B | I | -A]: column k of (I | -A) is e_k (k < m) or -A[:, k-m]
+    for (int e = threadIdx.x; e < m * W; e += blockDim.x) {
+        const int i = e / W, c = e % W;
+        double v;
+        if (c < m) {
+            const int k = head[c];
+            v = (k < m) ? (i == k ? 1.0 : 0.0) : -P.A[(size_t)(k - m) * m + i];
+        } else if (c < 2 * m) {
+            v = (i == c - m) ? 1.0 : 0.0;
+        } else {
+            v = -P.A[(size_t)(c - 2 * m) * m + i];
+        }
+        M[(size_t)i * W + c] = v;
+    }
+    __syncthreads();
+    // Gauss-Jordan with partial pivoting on the left m x m block
+    for (int k = 0; k < m; ++k) {
+        double key = -1.0;
+        int idx = -1;
+        for (int i = k + threadIdx.x; i < m; i += blockDim.x) {
+            const double v = fabs(M[(size_t)i * W + k]);
+            if (idx < 0 || v > key) { key = v; idx = i; }
+        }
+        const int piv = block_argmax(key, idx, shk, shi);
+        if (piv < 0 || fabs(M[(size_t)piv * W + k]) < 1e-12) {
+            if (threadIdx.x == 0) { io.status[b] = NODE_FAIL; io.pivots[b] = 0; }
+            return;
+        }
+        if (piv != k)
+            for (int c = threadIdx.x; c < W; c += blockDim.x) {
+                const double t = M[(size_t)k * W + c];
+                M[(size_t)k * W + c] = M[(size_t)piv * W + c];
+                M[(size_t)piv * W + c] = t;
+            }
+        __syncthreads();
+        const double inv = 1.0 / M[(size_t)k * W + k];
+        for (int c = threadIdx.x; c < W; c += blockDim.x) M[(size_t)k * W + c] *= inv;
+        __syncthreads();
+        for (int e = threadIdx.x; e < m * W; e += blockDim.x) {
+            const int i = e / W, c = e % W;
+            if (i == k) continue;
+            const double f = M[(size_t)i * W + k];
+            if (f != 0.0) M[(size_t)i * W + c] -= f * M[(size_t)k * W + c];
+        }
+        __syncthreads();
+    }
+    // T[i][j] = M[i][m + j]  (row length W kept; T(i, j) = M[i*W + m + j])
+#define T_(i, j) M[(size_t)(i) * W + m + (j)]
+    // x_N and x_B = -T_N x_N
+    for (int k = threadIdx.x; k < N; k += blockDim.x) x[k] = (stat[k] == BS) ? 0.0 : nb_value(stat[k], lb[k], ub[k]);
+    __syncthreads();
+    for (int i = threadIdx.x; i < m; i += blockDim.x) {
+        double s = 0.0;
+        for (int k = 0; k < N; ++k)
+            if (stat[k] != BS && x[k] != 0.0) s += T_(i, k) * x[k];
+        x[head[i]] = -s;
+    }
+    // d = c - c_B' T
+    __syncthreads();
+    for (int k = threadIdx.x; k < N; k += blockDim.x) {
+        if (stat[k] == BS) { d[k] = 0.0; continue; }
+        double s = P.c[k];
+        for (int i = 0; i < m; ++i) {
+            const double cb = P.c[head[i]];
+            if (cb != 0.0) s -= cb * T_(i, k);
+        }
+        d[k] = s;
+    }
+    __syncthreads();
+    // ---- bounded dual simplex ------------------------------------------
+    const double tol_p = 1e-7, tol_piv = 1e-9;
+    const double cutoff = io.cutoff[b];
+    int it = 0, status = NODE_OPT;
+    for (;;) {
+        // objective (dual objective of the current dual feasible basis)
+        double zs = 0.0;
+        for (int k = threadIdx.x; k < N; k += blockDim.x) zs += P.c[k] * x[k];
+        const double z = block_sum256(zs, shk);
+        if (z >= cutoff) { status = NODE_CUTOFF; break; }
+        // chuzr: largest bound violation
+        double key = 0.0;
+        int idx = -1;
+        for (int i = threadIdx.x; i < m; i += blockDim.x) {
+            const int k = head[i];
+            const double v = x[k];
+            double r = 0.0;
+            if (v < lb[k] - tol_p * (1.0 + fabs(lb[k]))) r = lb[k] - v;
+            else if (v > ub[k] + tol_p * (1.0 + fabs(ub[k]))) r = v - ub[k];
+            if (r > 0.0 && (idx < 0 || r > key)) { key = r; idx = i; }
+        }
+        const int p = block_argmax(key, idx, shk, shi);
+        if (p < 0) break;                                  // primal feasible: optimal
+        if (it >= io.it_lim) { status = NODE_FAIL; break; }
+        const int kp = head[p];
+        const bool to_lb = x[kp] < lb[kp];
+        // ratio test on row p: x_p = -sum T[p,j] x_j
+        double rmax = 0.0;
+        for (int k = threadIdx.x; k < N; k += blockDim.x)
+            if (stat[k] != BS) rmax = fmax(rmax, fabs(T_(p, k)));
+        {
+            __syncthreads();
+            const double r = wmax(rmax);
+            if ((threadIdx.x & 63) == 0) shk[threadIdx.x >> 6] = r;
+            __syncthreads();
+            rmax = fmax(fmax(shk[0], shk[1]), fmax(shk[2], shk[3]));
+            __syncthreads();
+        }
+        const double eps = tol_piv * (1.0 + rmax);
+        double bt = 0.0, ba = 0.0;
+        int bq = -1;
+        for (int k = threadIdx.x; k < N; k += blockDim.x) {
+            const int st = stat[k];
+            if (st == BS || st == NS) continue;
+            const double a = T_(p, k);
+            if (fabs(a) < eps) continue;
+            // x_p changes by -a per unit increase of x_k
+            bool ok;
+            if (to_lb) ok = (st == NL && a < 0.0) || (st == NU && a > 0.0) || (st == NF);
+            else ok = (st == NL && a > 0.0) || (st == NU && a < 0.0) || (st == NF);
+            if (!ok) continue;
+            // the step that keeps d dual feasible: d_k - (d_q / a_pq) a_k
+            double t = (st == NF) ? fabs(d[k]) / fabs(a) : (to_lb ? -d[k] / a : d[k] / a);
+            if (t < 0.0) t = 0.0;
+            if (bq < 0 || t < bt || (t == bt && fabs(a) > ba)) { bt = t; ba = fabs(a); bq = k; }
+        }
+        const int q = block_ratio(bt, ba, bq, shk, sha, shi);
+        if (q < 0) { status = NODE_INFEAS; break; }        // dual unbounded
+        // pivot (p, q)
+        const double apq = T_(p, q);
+        const double bound = to_lb ? lb[kp] : ub[kp];
+        const double tq = (x[kp] - bound) / apq;         // step of x_q
+        const double dq = d[q] / apq;
+        __syncthreads();
+        // x update
+        for (int i = threadIdx.x; i < m; i += blockDim.x) {
+            if (i == p) continue;
+            const double a = T_(i, q);
+            if (a != 0.0) x[head[i]] -= a * tq;
+        }
+        // reduced costs: d_k -= dq * T[p,k]
+        for (int k = threadIdx.x; k < N; k += blockDim.x) {
+            if (k == q) continue;
+            const double a = T_(p, k);
+            if (a != 0.0) d[k] -= dq * a;
+        }
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            x[q] += tq;
+            x[kp] = bound;
+            d[q] = 0.0;
+            d[kp] = -dq;
+            stat[kp] = to_lb ? (lb[kp] == ub[kp] ? NS : NL) : (lb[kp] == ub[kp] ? NS : NU);
+            stat[q] = BS;
+            head[p] = q;
+        }
+        // T update: row p /= apq; row i -= T[i,q] row p
+        __syncthreads();
+        for (int k = threadIdx.x; k < N; k += blockDim.x) T_(p, k) /= apq;
+        __syncthreads();
+        for (int e = threadIdx.x; e < m * N; e += blockDim.x) {
+            const int i = e / N, k = e % N;
+            if (i == p) continue;
+            const double f = T_(i, q);
+            if (f != 0.0 && k != q) T_(i, k) -= f * T_(p, k);
+        }
+        __syncthreads();
+        for (int i = threadIdx.x; i < m; i += blockDim.x)
+            if (i != p) T_(i, q) = 0.0;
+        __syncthreads();
+        it++;
+    }
+    __syncthreads();
+    double zs = 0.0;
+    for (int k = threadIdx.x; k < N; k += blockDim.x) zs += P.c[k] * x[k];
+    const double z = block_sum256(zs, shk);
+    // outputs
+    double *gx = io.x + (size_t)b * N;
+    signed char *gso = io.stat_out + (size_t)b * N;
+    for (int k = threadIdx.x; k < N; k += blockDim.x) {
+        gx[k] = x[k];
+        gso[k] = stat[k];
+    }
+    if (status != NODE_OPT) {
+        if (threadIdx.x == 0) {
+            io.status[b] = status;
+            io.obj[b] = z;
+            io.pivots[b] = it;
+            io.jj[b] = 0;
+        }
+        return;
+    }
+    // ---- branch_drtom (glpios09.js:84) on the node's own tableau rows ----
+    // columns in order; x_j basic and fractional; the dual ratio test of
+    // glp_dual_rtest (glpapi12.js:687) on the row x_j = sum alfa_k x_k,
+    // alfa_k = -T[i,k]; delta z = d_k * delta x_k with Tomlin's rounding
+    __shared__ int sh_jj, sh_next, sh_brk;
+    __shared__ double sh_degrad, sh_dn, sh_up;
+    if (threadIdx.x == 0) { sh_jj = 0; sh_next = 0; sh_degrad = -1.0; sh_dn = 0.0; sh_up = 0.0; sh_brk = 0; }
+    __syncthreads();
+    int any_frac = 0;
+    // visit the basic structural columns in increasing j
+    for (int j = 0; j < n; ++j) {
+        const int k = m + j;
+        if (stat[k] != BS || !P.isint[j]) continue;
+        const double xv = x[k];
+        if (fabs(xv - floor(xv + 0.5)) <= P.tol_int) continue;
+        any_frac = 1;
+        int row = -1;
+        for (int i = 0; i < m; ++i)
+            if (head[i] == k) { row = i; break; }
+        double dz[2];
+        for (int kase = 0; kase < 2; ++kase) {
+            const double dir = kase == 0 ? -1.0 : +1.0;
+            double bt = 0.0, ba = 0.0;
+            int bq = -1;
+            for (int kk = threadIdx.x; kk < N; kk += blockDim.x) {
+                const int st = stat[kk];
+                if (st == BS || st == NS) continue;
+                const double alfa = dir * (-T_(row, kk));
+                double t;
+                if (st == NL) {
+                    if (alfa < +1e-9) continue;
+                    t = d[kk] / alfa;
+                } else if (st == NU) {
+                    if (alfa > -1e-9) continue;
+                    t = d[kk] / alfa;
+                } else {
+                    if (-1e-9 < alfa && alfa < +1e-9) continue;
+                    t = 0.0;
+                }
+                if (t < 0.0) t = 0.0;
+                if (bq < 0 || t < bt || (t == bt && fabs(alfa) > ba)) { bt = t; ba = fabs(alfa); bq = kk; }
+            }
+            const int kq = block_ratio(bt, ba, bq, shk, sha, shi);
+            if (kq < 0) dz[kase] = DBL_MAX;
+            else {
+                const double alfa = -T_(row, kq);
+                const double delta_j = (kase == 0 ? floor(xv) : ceil(xv)) - xv;
+                double delta_k = delta_j / alfa;
+                if (kq >= m && P.isint[kq - m] && fabs(delta_k - floor(delta_k + 0.5)) > 1e-3)
+                    delta_k = delta_k > 0.0 ? ceil(delta_k) : floor(delta_k);
+                double dk = d[kq];
+                const int st = stat[kq];
+                if ((st == NL && dk < 0.0) || (st == NU && dk > 0.0) || st == NF) dk = 0.0;
+                dz[kase] = fabs(dk * delta_k);
+            }
+        }
+        if (threadIdx.x == 0) {
+            if (sh_degrad < dz[0] || sh_degrad < dz[1]) {
+                sh_jj = j + 1;
+                sh_dn = dz[0];
+                sh_up = dz[1];
+                if (dz[0] < dz[1]) { sh_next = -1; sh_degrad = dz[1]; }
+                else { sh_next = +1; sh_degrad = dz[0]; }
+                if (sh_degrad == DBL_MAX) sh_brk = 1;
+            }
+        }
+        __syncthreads();
+        if (sh_brk) break;
+    }
+    if (threadIdx.x == 0) {
+        int jj = sh_jj, next = sh_next;
+        double dn = sh_dn, up = sh_up;
+        if (any_frac && sh_degrad < 1e-6 * (1.0 + 0.001 * fabs(z))) {
+            // branch_mostf (glpios09.js:62): value closest to floor + 1/2
+            double most = DBL_MAX;
+            jj = 0;
+            for (int j = 0; j < n; ++j) {
+                const int k = m + j;
+                if (stat[k] != BS || !P.isint[j]) continue;
+                const double beta = x[k];
+                if (fabs(beta - floor(beta + 0.5)) <= P.tol_int) continue;
+                const double temp = floor(beta) + 0.5;
+                if (most > fabs(beta - temp)) {
+                    jj = j + 1;
+                    most = fabs(beta - temp);
+                    next = beta < temp ? -1 : +1;
+                }
+            }
+            dn = 0.0;
+            up = 0.0;
+        }
+        io.status[b] = NODE_OPT;
+        io.obj[b] = z;
+        io.pivots[b] = it;
+        io.jj[b] = any_frac ? jj : 0;
+        io.next[b] = next;
+        io.dz[2 * b] = dn;
+        io.dz[2 * b + 1] = up;
+    }
+#undef T_
+}
+
+size_t node_lp_lds(int m, int n)
+{
+    const size_t N = (size_t)m + n;
+    return sizeof(double) * ((size_t)m * (2 * m + n) + 4 * N) + sizeof(int) * m + N + 16;
+}
+
+void launch_node_lp(hipStream_t s, const NodeProb &P, const NodeIO &io, int nb)
+{
+    const size_t lds = node_lp_lds(P.m, P.n);
+    hipLaunchKernelGGL(k_node_lp, dim3(nb), dim3(256), lds, s, P, io);
+}
+
+// ---------------------------------------------------------------------------
+// host driver
+// ---------------------------------------------------------------------------
+namespace {
+
+template <typename T>
+struct DevArr {
+    T *p = nullptr;
+    size_t n = 0;
+    void ensure(size_t cnt)
+    {
+        if (cnt <= n && p) return;
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        if (hipMalloc((void **)&p, std::max<size_t>(cnt, 1) * sizeof(T)) != hipSuccess) p = nullptr;
+        n = p ? std::max<size_t>(cnt, 1) : 0;
+    }
+    ~DevArr()
+    {
+        if (p) (void)hipFree(p);
+    }
+};
+
+template <typename T>
+struct HostArr {
+    T *p = nullptr;
+    size_t n = 0;
+    void ensure(size_t cnt)
+    {
+        if (cnt <= n && p) return;
+        if (p) (void)hipHostFree(p);
+        p = nullptr;
+        if (hipHostMalloc((void **)&p, std::max<size_t>(cnt, 1) * sizeof(T), hipHostMallocDefault) != hipSuccess)
+            p = nullptr;
+        n = p ? std::max<size_t>(cnt, 1) : 0;
+    }
+    ~HostArr()
+    {
+        if (p) (void)hipHostFree(p);
+    }
+};
+
+struct OpenNode {
+    double bound;                 // local bound, minimisation form
+    long long seq;                // creation order (tie-break: older first)
+    std::vector<double> lb, ub;   // structural bounds
+    std::vector<signed char> stat;   // warm-start basis, [m+n]
+};
+
+struct NodeCmp {
+    bool operator()(const OpenNode *a, const OpenNode *b) const
+    {
+        if (a->bound != b->bound) return a->bound > b->bound;
+        return a->seq > b->seq;
+    }
+};
+
+}  // namespace
+
+struct MipSolver {
+    int m = 0, n = 0, N = 0;
+    double sign = 1.0, c0 = 0.0;
+    std::vector<double> A, c, rlb, rub, clb, cub, coef;
+    std::vector<signed char> isint, fixed_col;
+    DevArr<double> dA, dc, dlb, dub, dcut, dobj, dx, ddz;
+    DevArr<signed char> dint, dsin, dsout;
+    DevArr<int> dstatus, dpiv, djj, dnext;
+    HostArr<double> hlb, hub, hcut, hobj, hx, hdz;
+    HostArr<signed char> hsin, hsout;
+    HostArr<int> hstatus, hpiv, hjj, hnext;
+    // ios_round_bound (glpios01.js:730): objective integrality
+    bool round_ok = false;
+    double round_s = 0.0, round_d = 1.0;
+
+    void alloc_batch(int B)
+    {
+        const size_t NB = (size_t)B * N;
+        dlb.ensure(NB); dub.ensure(NB); dsin.ensure(NB); dsout.ensure(NB); dx.ensure(NB);
+        dcut.ensure(B); dobj.ensure(B); ddz.ensure(2 * (size_t)B);
+        dstatus.ensure(B); dpiv.ensure(B); djj.ensure(B); dnext.ensure(B);
+        hlb.ensure(NB); hub.ensure(NB); hsin.ensure(NB); hsout.ensure(NB); hx.ensure(NB);
+        hcut.ensure(B); hobj.ensure(B); hdz.ensure(2 * (size_t)B);
+        hstatus.ensure(B); hpiv.ensure(B); hjj.ensure(B); hnext.ensure(B);
+    }
+
+    // min-form bound -> rounded min-form bound
+    double round_bound(double z) const
+    {
+        if (!round_ok) return z;
+        // the reference rounds in the original direction; in minimisation
+        // form both cases are "round up" of (bound - s) / d
+        const double s = sign * (round_s - c0), d = round_d;
+        const double h = (z - s) / d;
+        if (h >= std::floor(h) + 0.001) return d * std::ceil(h) + s;
+        return z;
+    }
+};
+
+static void setup_rounding(MipSolver &S, const gk_mip *mip)
+{
+    // ios_round_bound: all objective coefficients of non-fixed columns
+    // integral and on integer columns; s = c0 + sum over fixed columns
+    const gk_lp &L = mip->lp;
+    double s = L.c0;
+    std::vector<long long> cs;
+    for (int j = 1; j <= S.n; j++) {
+        const double cj = L.col_coef[j];
+        if (cj == 0.0) continue;
+        if (L.col_type[j] == 5) {                       // GLP_FX
+            s += cj * L.col_lb[j];
+            continue;
+        }
+        if (mip->col_kind[j] != 2 || cj != std::floor(cj) || std::fabs(cj) > 2147483647.0) return;
+        cs.push_back((long long)std::fabs(cj));
+    }
+    if (cs.empty()) return;
+    long long g = 0;
+    for (long long v : cs) {
+        long long a = g, b = v;
+        while (b) { long long t = a % b; a = b; b = t; }
+        g = a;
+    }
+    if (g <= 0) return;
+    S.round_ok = true;
+    S.round_s = s;
+    S.round_d = (double)g;
+}
+
+}  // namespace gk
+
+using namespace gk;
+
+int gk_ctx_device(gk_ctx *);
+hipStream_t gk_ctx_stream(gk_ctx *);
+
+extern "C" int gk_ios_driver(gk_ctx *ctx, gk_mip *mip, const gk_iocp *parm)
+{
+    if (!ctx || !mip || !parm) { set_err("gk_ios_driver: null argument"); return GK_EABI; }
+    const gk_lp &L = mip->lp;
+    const int m = L.m, n = L.n;
+    if (m < 1 || n < 1) { set_err("gk_ios_driver: m = %d, n = %d; invalid dimensions", m, n); return GK_EABI; }
+    if (L.pbs_stat != 2 || L.dbs_stat != 2) {
+        set_err("gk_ios_driver: optimal basis to initial LP relaxation not provided");
+        return GK_EABI;
+    }
+    const size_t lds = node_lp_lds(m, n);
+    if (lds > 64 * 1024) {
+        set_err("gk_ios_driver: node LP %d x %d needs %zu bytes of LDS; the batched node kernel holds at most 64 KiB",
+                m, n, lds);
+        return GK_EABI;
+    }
+    if (hipSetDevice(gk_ctx_device(ctx)) != hipSuccess) { set_err("gk_ios_driver: hipSetDevice failed"); return GK_EABI; }
+    hipStream_t s = gk_ctx_stream(ctx);
+    const auto t0 = std::chrono::steady_clock::now();
+    MipSolver S;
+    S.m = m; S.n = n; S.N = m + n;
+    S.sign = (L.dir == 1) ? 1.0 : -1.0;                   // GLP_MIN = 1
+    S.c0 = L.c0;
+    const double INF = DBL_MAX;
+    S.rlb.resize(m); S.rub.resize(m); S.clb.resize(n); S.cub.resize(n);
+    auto bnds = [&](int type, double lb, double ub, double &l, double &u) {
+        switch (type) {
+        case 1: l = -INF; u = +INF; break;               // FR
+        case 2: l = lb; u = +INF; break;                 // LO
+        case 3: l = -INF; u = ub; break;                 // UP
+        case 4: l = lb; u = ub; break;                   // DB
+        default: l = lb; u = lb; break;                  // FX
+        }
+    };
+    for (int i = 0; i < m; i++) bnds(L.row_type[i + 1], L.row_lb[i + 1], L.row_ub[i + 1], S.rlb[i], S.rub[i]);
+    for (int j = 0; j < n; j++) bnds(L.col_type[j + 1], L.col_lb[j + 1], L.col_ub[j + 1], S.clb[j], S.cub[j]);
+    S.A.assign((size_t)m * n, 0.0);
+    for (int j = 1; j <= n; j++)
+        for (int t = L.A_ptr[j]; t < L.A_ptr[j + 1]; t++) {
+            const int i = L.A_ind[t];
+            if (i < 1 || i > m) { set_err("gk_ios_driver: A_ind[%d] = %d; out of range", t, i); return GK_EABI; }
+            S.A[(size_t)(j - 1) * m + (i - 1)] += L.A_val[t];
+        }
+    S.c.assign(S.N, 0.0);
+    S.isint.assign(n, 0);
+    for (int j = 0; j < n; j++) {
+        S.c[m + j] = S.sign * L.col_coef[j + 1];
+        S.isint[j] = (mip->col_kind[j + 1] == 2) ? 1 : 0;
+    }
+    setup_rounding(S, mip);
+    // device problem
+    S.dA.ensure(S.A.size()); S.dc.ensure(S.N); S.dint.ensure(n);
+    const int BMAX = 1024;
+    S.alloc_batch(BMAX);
+    if (!S.dA.p || !S.dc.p || !S.dint.p || !S.dlb.p || !S.hlb.p) { set_err("gk_ios_driver: out of memory"); return GK_EABI; }
+    (void)hipMemcpyAsync(S.dA.p, S.A.data(), S.A.size() * sizeof(double), hipMemcpyHostToDevice, s);
+    (void)hipMemcpyAsync(S.dc.p, S.c.data(), S.N * sizeof(double), hipMemcpyHostToDevice, s);
+    (void)hipMemcpyAsync(S.dint.p, S.isint.data(), n, hipMemcpyHostToDevice, s);
+    NodeProb P;
+    P.m = m; P.n = n; P.ld = S.N; P.A = S.dA.p; P.c = S.dc.p; P.isint = S.dint.p; P.tol_int = parm->tol_int;
+    // root node: the optimal basis of the initial LP relaxation
+    std::vector<OpenNode *> store;
+    std::priority_queue<OpenNode *, std::vector<OpenNode *>, NodeCmp> open;
+    long long seq = 0;
+    {
+        OpenNode *r = new OpenNode;
+        r->bound = -INF;
+        r->seq = seq++;
+        r->lb = S.clb;
+        r->ub = S.cub;
+        r->stat.resize(S.N);
+        for (int i = 0; i < m; i++) r->stat[i] = L.row_stat[i + 1];
+        for (int j = 0; j < n; j++) r->stat[m + j] = L.col_stat[j + 1];
+        store.push_back(r);
+        open.push(r);
+    }
+    bool have = false;
+    double best = INF;                                    // incumbent, minimisation form
+    std::vector<double> xbest(S.N, 0.0);
+    long long lp_solves = 0, pivots = 0, created = 1, failed = 0;
+    auto hopeful = [&](double bound) {
+        if (!have) return true;
+        const double eps = parm->tol_obj * (1.0 + std::fabs(S.c0 + S.sign * best));
+        return bound < best - eps;
+    };
+    std::vector<OpenNode *> batch;
+    while (!open.empty()) {
+        if (parm->tm_lim < 0x7fffffff &&
+            std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() * 1000.0 >= parm->tm_lim)
+            break;
+        batch.clear();
+        while (!open.empty() && (int)batch.size() < BMAX) {
+            OpenNode *nd = open.top();
+            open.pop();
+            if (!hopeful(nd->bound)) continue;
+            batch.push_back(nd);
+        }
+        if (batch.empty()) break;
+        const int nb = (int)batch.size();
+        const double cut = have ? best - parm->tol_obj * (1.0 + std::fabs(S.c0 + S.sign * best)) : INF;
+        for (int b = 0; b < nb; b++) {
+            OpenNode *nd = batch[b];
+            double *l = S.hlb.p + (size_t)b * S.N, *u = S.hub.p + (size_t)b * S.N;
+            std::memcpy(l, S.rlb.data(), m * sizeof(double));
+            std::memcpy(u, S.rub.data(), m * sizeof(double));
+            std::memcpy(l + m, nd->lb.data(), n * sizeof(double));
+            std::memcpy(u + m, nd->ub.data(), n * sizeof(double));
+            std::memcpy(S.hsin.p + (size_t)b * S.N, nd->stat.data(), S.N);
+            S.hcut.p[b] = cut;
+        }
+        const size_t NB = (size_t)nb * S.N;
+        (void)hipMemcpyAsync(S.dlb.p, S.hlb.p, NB * sizeof(double), hipMemcpyHostToDevice, s);
+        (void)hipMemcpyAsync(S.dub.p, S.hub.p, NB * sizeof(double), hipMemcpyHostToDevice, s);
+        (void)hipMemcpyAsync(S.dsin.p, S.hsin.p, NB, hipMemcpyHostToDevice, s);
+        (void)hipMemcpyAsync(S.dcut.p, S.hcut.p, nb * sizeof(double), hipMemcpyHostToDevice, s);
+        NodeIO io;
+        io.lb = S.dlb.p; io.ub = S.dub.p; io.stat_in = S.dsin.p; io.cutoff = S.dcut.p;
+        io.status = S.dstatus.p; io.pivots = S.dpiv.p; io.jj = S.djj.p; io.next = S.dnext.p;
+        io.obj = S.dobj.p; io.x = S.dx.p; io.dz = S.ddz.p; io.stat_out = S.dsout.p;
+        io.it_lim = 10000;
+        launch_node_lp(s, P, io, nb);
+        (void)hipMemcpyAsync(S.hstatus.p, S.dstatus.p, nb * sizeof(int), hipMemcpyDeviceToHost, s);
+        (void)hipMemcpyAsync(S.hpiv.p, S.dpiv.p, nb * sizeof(int), hipMemcpyDeviceToHost, s);
+        (void)hipMemcpyAsync(S.hjj.p, S.djj.p, nb * sizeof(int), hipMemcpyDeviceToHost, s);
+        (void)hipMemcpyAsync(S.hnext.p, S.dnext.p, nb * sizeof(int), hipMemcpyDeviceToHost, s);
+        (void)hipMemcpyAsync(S.hobj.p, S.dobj.p, nb * sizeof(double), hipMemcpyDeviceToHost, s);
+        (void)hipMemcpyAsync(S.hdz.p, S.ddz.p, 2 * nb * sizeof(double), hipMemcpyDeviceToHost, s);
+        (void)hipMemcpyAsync(S.hx.p, S.dx.p, NB * sizeof(double), hipMemcpyDeviceToHost, s);
+        (void)hipMemcpyAsync(S.hsout.p, S.dsout.p, NB, hipMemcpyDeviceToHost, s);
+        if (hipStreamSynchronize(s) != hipSuccess) {
+            set_err("gk_ios_driver: node batch failed: %s", hipGetErrorString(hipGetLastError()));
+            for (auto p : store) delete p;
+            return GK_EABI;
+        }
+        for (int b = 0; b < nb; b++) {
+            OpenNode *nd = batch[b];
+            lp_solves++;
+            pivots += S.hpiv.p[b];
+            const int st = S.hstatus.p[b];
+            if (st == NODE_FAIL) { failed++; continue; }
+            if (st != NODE_OPT) continue;                  // infeasible or cut off
+            const double z = S.hobj.p[b];
+            const double bound = S.round_bound(z);
+            if (!hopeful(bound)) continue;
+            const double *x = S.hx.p + (size_t)b * S.N;
+            const int jj = S.hjj.p[b];
+            if (jj == 0) {                                 // integer feasible
+                if (!have || z < best) {
+                    have = true;
+                    best = z;
+                    std::memcpy(xbest.data(), x, S.N * sizeof(double));
+                }
+                continue;
+            }
+            const int j = jj - 1;
+            const double beta = x[m + j];
+            const double dz[2] = {S.hdz.p[2 * b], S.hdz.p[2 * b + 1]};
+            const int first = S.hnext.p[b] < 0 ? 0 : 1;  // preferred child gets the older seq
+            for (int r = 0; r < 2; r++) {
+                const int kase = (r == 0) ? first : 1 - first;
+                if (dz[kase] == DBL_MAX) continue;        // that branch has no feasible point
+                OpenNode *c = new OpenNode;
+                c->bound = S.round_bound(z + dz[kase]);
+                c->seq = seq++;
+                c->lb = nd->lb;
+                c->ub = nd->ub;
+                if (kase == 0) c->ub[j] = std::floor(beta);
+                else c->lb[j] = std::ceil(beta);
+                c->stat.assign(S.hsout.p + (size_t)b * S.N, S.hsout.p + (size_t)(b + 1) * S.N);
+                // a fixed bound pair makes a non-basic column NS
+                if (c->stat[m + j] != BS && c->lb[j] == c->ub[j]) c->stat[m + j] = NS;
+                store.push_back(c);
+                open.push(c);
+                created++;
+            }
+        }
+        // release the evaluated nodes
+        for (auto nd : batch) {
+            nd->lb.clear(); nd->lb.shrink_to_fit();
+            nd->ub.clear(); nd->ub.shrink_to_fit();
+            nd->stat.clear(); nd->stat.shrink_to_fit();
+        }
+    }
+    const bool timed_out = !open.empty();
+    for (auto p : store) delete p;
+    mip->lp_solves = lp_solves;
+    mip->nodes_created = created;
+    mip->pivots = pivots;
+    if (failed) {
+        set_err("gk_ios_driver: %lld node LP(s) could not be solved by the batched kernel", failed);
+        return GK_EABI;
+    }
+    if (have) {
+        mip->mip_stat = timed_out ? 2 : 5;                // GLP_FEAS / GLP_OPT
+        mip->mip_obj = S.c0 + S.sign * best;
+        for (int i = 0; i < m; i++) mip->row_mipx[i + 1] = xbest[i];
+        for (int j = 0; j < n; j++)
+            mip->col_mipx[j + 1] = S.isint[j] ? std::floor(xbest[m + j] + 0.5) : xbest[m + j];
+    } else {
+        mip->mip_stat = timed_out ? 1 : 4;                // GLP_UNDEF / GLP_NOFEAS
+        mip->mip_obj = 0.0;
+    }
+    return timed_out ? 0x09 : 0;                          // GLP_ETMLIM
+}

@@ -67,6 +67,18 @@ class Lp(C.Structure):
                 ("obj_val", C.c_double), ("valid", C.c_int)]
 
 
+class Iocp(C.Structure):
+    _fields_ = [("msg_lev", C.c_int), ("br_tech", C.c_int), ("bt_tech", C.c_int), ("tol_int", C.c_double),
+                ("tol_obj", C.c_double), ("tm_lim", C.c_int), ("out_frq", C.c_int), ("out_dly", C.c_int),
+                ("pp_tech", C.c_int), ("mip_gap", C.c_double), ("presolve", C.c_int)]
+
+
+class Mip(C.Structure):
+    _fields_ = [("lp", Lp), ("col_kind", C.c_void_p), ("mip_stat", C.c_int), ("mip_obj", C.c_double),
+                ("col_mipx", C.c_void_p), ("row_mipx", C.c_void_p), ("lp_solves", C.c_longlong),
+                ("nodes_created", C.c_longlong), ("pivots", C.c_longlong)]
+
+
 class SpxStats(C.Structure):
     _fields_ = [("pivots", C.c_longlong), ("reinversions", C.c_longlong), ("batches", C.c_longlong),
                 ("host_syncs", C.c_longlong), ("seconds_total", C.c_double), ("seconds_reinvert", C.c_double),
@@ -118,6 +130,8 @@ def load_library(path: str = LIB_PATH):
         f.argtypes = [P, C.POINTER(Lp), P, C.POINTER(Smcp)]
         f.restype = C.c_int
     L.gk_bfd_last_stats.argtypes = [P, C.POINTER(SpxStats)]
+    L.gk_ios_driver.argtypes = [P, C.POINTER(Mip), C.POINTER(Iocp)]
+    L.gk_ios_driver.restype = C.c_int
     L.gk_bfd_profile.argtypes = [P, C.c_int]
     L.gk_bfd_profile.restype = None
     L.gk_bfd_time_kernel.argtypes = [P, C.c_int, C.c_int, C.POINTER(C.c_double)]
@@ -206,6 +220,11 @@ class GkProblem:
         self.obj_val = 0.0
         self.some = 0
         self.valid = 0
+        self.mip_stat = GLP_UNDEF
+        self.mip_obj = 0.0
+        self.col_mipx = np.zeros(n + 1)
+        self.row_mipx = np.zeros(m + 1)
+        self.mip_stats = {}
         GkProblem._version += 1
         self.a_version = GkProblem._version
         self.bfcp = None
@@ -448,3 +467,76 @@ def glp_simplex(P: GkProblem, parm: Smcp | None = None) -> int:
             ret = P.spx(parm, dual=False)
         return ret
     return P.spx(parm, dual=True)
+
+
+# ---------------------------------------------------------------------------
+# glp_intopt (glpapi09.js:61-389) with presolve OFF and cb_func == null;
+# ios_driver (glpios03.js:1) runs as gk_ios_driver on the MI355X
+# ---------------------------------------------------------------------------
+GLP_BR_FFV, GLP_BR_LFV, GLP_BR_MFV, GLP_BR_DTH, GLP_BR_PCH = 1, 2, 3, 4, 5
+GLP_BT_DFS, GLP_BT_BFS, GLP_BT_BLB, GLP_BT_BPH = 1, 2, 3, 4
+GLP_PP_NONE, GLP_PP_ROOT, GLP_PP_ALL = 0, 1, 2
+GLP_EROOT, GLP_ENOPFS, GLP_ENODFS, GLP_EMIPGAP = 0x0C, 0x0A, 0x0B, 0x0E
+GLP_CV, GLP_IV = 1, 2
+
+
+def IOCP(**options) -> Iocp:
+    """IOCP (glpapi09.js:392-414), including its `options[x] || default` quirk."""
+    d = dict(msg_lev=GLP_MSG_ALL, br_tech=GLP_BR_DTH, bt_tech=GLP_BT_BLB, tol_int=1e-5, tol_obj=1e-7,
+             tm_lim=INT_MAX, out_frq=5000, out_dly=10000, pp_tech=GLP_PP_ALL, mip_gap=0.0, presolve=0)
+    p = Iocp()
+    for k, v in d.items():
+        setattr(p, k, options.get(k) or v)
+    return p
+
+
+def glp_intopt(P: GkProblem, parm: Iocp | None = None) -> int:
+    """glp_intopt (glpapi09.js:61) -> solve_mip (:62) -> ios_driver."""
+    if parm is None:
+        parm = IOCP()
+    if parm.msg_lev not in (0, 1, 2, 3, 4):
+        raise GkError(f"glp_intopt: msg_lev = {parm.msg_lev}; invalid parameter")
+    if parm.br_tech not in (1, 2, 3, 4, 5):
+        raise GkError(f"glp_intopt: br_tech = {parm.br_tech}; invalid parameter")
+    if parm.bt_tech not in (1, 2, 3, 4):
+        raise GkError(f"glp_intopt: bt_tech = {parm.bt_tech}; invalid parameter")
+    if not (0.0 < parm.tol_int < 1.0):
+        raise GkError(f"glp_intopt: tol_int = {parm.tol_int}; invalid parameter")
+    if not (0.0 < parm.tol_obj < 1.0):
+        raise GkError(f"glp_intopt: tol_obj = {parm.tol_obj}; invalid parameter")
+    if parm.tm_lim < 0 or parm.out_frq < 0 or parm.out_dly < 0:
+        raise GkError("glp_intopt: invalid tm_lim/out_frq/out_dly")
+    if parm.pp_tech not in (0, 1, 2):
+        raise GkError(f"glp_intopt: pp_tech = {parm.pp_tech}; invalid parameter")
+    if parm.mip_gap < 0.0:
+        raise GkError(f"glp_intopt: mip_gap = {parm.mip_gap}; invalid parameter")
+    if parm.presolve:
+        raise GkError("glp_intopt: the MIP presolver stays in the JS host (presolve must be OFF here)")
+    P.mip_stat = GLP_UNDEF
+    P.mip_obj = 0.0
+    if np.any((P.row_type[1:] == GLP_DB) & (P.row_lb[1:] >= P.row_ub[1:])) or \
+            np.any((P.col_type[1:] == GLP_DB) & (P.col_lb[1:] >= P.col_ub[1:])):
+        return GLP_EBOUND
+    iv = P.col_kind[1:] == GLP_IV
+    t = P.col_type[1:]
+    lb, ub = P.col_lb[1:], P.col_ub[1:]
+    if np.any(iv & np.isin(t, (GLP_LO, GLP_DB, GLP_FX)) & (lb != np.floor(lb))) or \
+            np.any(iv & np.isin(t, (GLP_UP, GLP_DB)) & (ub != np.floor(ub))):
+        return GLP_EBOUND
+    # solve_mip: an optimal basis to the LP relaxation must be provided
+    if not (P.valid and P.pbs_stat == GLP_FEAS and P.dbs_stat == GLP_FEAS):
+        return GLP_EROOT
+    mip = Mip()
+    mip.lp = P._lp_struct()
+    mip.lp.pbs_stat, mip.lp.dbs_stat, mip.lp.obj_val = P.pbs_stat, P.dbs_stat, P.obj_val
+    ptr = lambda a: a.ctypes.data_as(C.c_void_p)
+    mip.col_kind = ptr(P.col_kind)
+    mip.col_mipx = ptr(P.col_mipx)
+    mip.row_mipx = ptr(P.row_mipx)
+    ret = P.L.gk_ios_driver(P.ctx.h, C.byref(mip), C.byref(parm))
+    if ret == GK_EABI:
+        raise GkError(_err(P.L))
+    P.mip_stat = mip.mip_stat
+    P.mip_obj = mip.mip_obj
+    P.mip_stats = dict(lp_solves=mip.lp_solves, nodes_created=mip.nodes_created, pivots=mip.pivots)
+    return ret
