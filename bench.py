@@ -258,6 +258,31 @@ def run_extra(gk, problems, ctx, c3):
                                   "pivots": P.it_cnt, "seconds": round(dt, 4),
                                   "pivots_per_s": round(P.it_cnt / dt, 1),
                                   "reference_node_pivots_per_s": 1813}
+    out.update(run_bnb(gk, problems, ctx))
+    return out
+
+
+def run_bnb(gk, problems, ctx):
+    """B&B configs (BASELINE.json configs[3], C5s surrogate of configs[4]):
+    root glp_simplex + glp_intopt on the device; LP-relaxations/s = node LP
+    solves / wall time of glp_intopt."""
+    import json as _json
+    out = {}
+    gold = os.path.join(ROOT, "tests", "golden")
+    for name, ref_lps, ref_s in (("gap", 196, 0.0477), ("c5s_12x30", 70506, 49.7)):
+        d = _json.load(open(os.path.join(gold, "mip_" + name + ".json")))
+        prob = problems.from_fixture(d)
+        P = gk.GkProblem(ctx, prob)
+        assert gk.glp_simplex(P, gk.SMCP(msg_lev=gk.GLP_MSG_ERR)) == 0
+        t0 = time.perf_counter()
+        ret = gk.glp_intopt(P, gk.IOCP(msg_lev=gk.GLP_MSG_ERR))
+        dt = time.perf_counter() - t0
+        lps = P.mip_stats.get("lp_solves", 0)
+        out["bnb_" + name] = {"ret": ret, "mip_obj": P.mip_obj, "ref_mip_obj": d["mip"]["mip_obj"],
+                              "lp_relaxations": lps, "seconds": round(dt, 4),
+                              "lp_relax_per_s": round(lps / dt, 1), "nodes": P.mip_stats.get("nodes_created"),
+                              "reference_lp_relaxations": ref_lps, "reference_seconds": ref_s,
+                              "reference_lp_relax_per_s": round(ref_lps / ref_s, 1)}
     return out
 
 

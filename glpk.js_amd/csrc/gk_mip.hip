@@ -153,7 +153,8 @@ __global__ void __launch_bounds__(256) k_node_lp(NodeProb P, NodeIO io)
     const int W = 2 * m + n;                 // width of [B | I | -A]
     double *M = lds;                          // m * W
     double *lb = M + (size_t)m * W, *ub = lb + N, *x = ub + N, *d = x + N;
-    int *head = (int *)(d + N);
+    double *fcol = d + N;                     // m
+    int *head = (int *)(fcol + m);
     signed char *stat = (signed char *)(head + m);
     const double *glb = io.lb + (size_t)b * N, *gub = io.ub + (size_t)b * N;
     const signed char *gst = io.stat_in + (size_t)b * N;
@@ -215,11 +216,12 @@ __global__ void __launch_bounds__(256) k_node_lp(NodeProb P, NodeIO io)
         __syncthreads();
         const double inv = 1.0 / M[(size_t)k * W + k];
         for (int c = threadIdx.x; c < W; c += blockDim.x) M[(size_t)k * W + c] *= inv;
+        // multipliers of column k, saved before the elimination overwrites it
+        for (int i = threadIdx.x; i < m; i += blockDim.x) fcol[i] = (i == k) ? 0.0 : M[(size_t)i * W + k];
         __syncthreads();
         for (int e = threadIdx.x; e < m * W; e += blockDim.x) {
             const int i = e / W, c = e % W;
-            if (i == k) continue;
-            const double f = M[(size_t)i * W + k];
+            const double f = fcol[i];
             if (f != 0.0) M[(size_t)i * W + c] -= f * M[(size_t)k * W + c];
         }
         __syncthreads();
@@ -248,7 +250,7 @@ __global__ void __launch_bounds__(256) k_node_lp(NodeProb P, NodeIO io)
     }
     __syncthreads();
     // ---- bounded dual simplex ------------------------------------------
-    const double tol_p = 1e-7, tol_piv = 1e-9;
+    const double tol_p = 1e-7, tol_piv = 1e-7;
     const double cutoff = io.cutoff[b];
     int it = 0, status = NODE_OPT;
     for (;;) {
@@ -285,7 +287,7 @@ __global__ void __launch_bounds__(256) k_node_lp(NodeProb P, NodeIO io)
             rmax = fmax(fmax(shk[0], shk[1]), fmax(shk[2], shk[3]));
             __syncthreads();
         }
-        const double eps = tol_piv * (1.0 + rmax);
+        const double eps = tol_piv * (1.0 + 0.01 * rmax);
         double bt = 0.0, ba = 0.0;
         int bq = -1;
         for (int k = threadIdx.x; k < N; k += blockDim.x) {
@@ -388,7 +390,7 @@ __global__ void __launch_bounds__(256) k_node_lp(NodeProb P, NodeIO io)
         int row = -1;
         for (int i = 0; i < m; ++i)
             if (head[i] == k) { row = i; break; }
-        double dz[2];
+        double dz[2], dzb[2];
         for (int kase = 0; kase < 2; ++kase) {
             const double dir = kase == 0 ? -1.0 : +1.0;
             double bt = 0.0, ba = 0.0;
@@ -412,24 +414,26 @@ __global__ void __launch_bounds__(256) k_node_lp(NodeProb P, NodeIO io)
                 if (bq < 0 || t < bt || (t == bt && fabs(alfa) > ba)) { bt = t; ba = fabs(alfa); bq = kk; }
             }
             const int kq = block_ratio(bt, ba, bq, shk, sha, shi);
-            if (kq < 0) dz[kase] = DBL_MAX;
+            if (kq < 0) dz[kase] = dzb[kase] = DBL_MAX;
             else {
                 const double alfa = -T_(row, kq);
                 const double delta_j = (kase == 0 ? floor(xv) : ceil(xv)) - xv;
                 double delta_k = delta_j / alfa;
-                if (kq >= m && P.isint[kq - m] && fabs(delta_k - floor(delta_k + 0.5)) > 1e-3)
-                    delta_k = delta_k > 0.0 ? ceil(delta_k) : floor(delta_k);
                 double dk = d[kq];
                 const int st = stat[kq];
                 if ((st == NL && dk < 0.0) || (st == NU && dk > 0.0) || st == NF) dk = 0.0;
-                dz[kase] = fabs(dk * delta_k);
+                // the objective after this one dual pivot bounds the branch
+                dzb[kase] = fabs(dk * delta_k);
+                if (kq >= m && P.isint[kq - m] && fabs(delta_k - floor(delta_k + 0.5)) > 1e-3)
+                    delta_k = delta_k > 0.0 ? ceil(delta_k) : floor(delta_k);
+                dz[kase] = fabs(dk * delta_k);   // Tomlin's estimate: choice only
             }
         }
         if (threadIdx.x == 0) {
             if (sh_degrad < dz[0] || sh_degrad < dz[1]) {
                 sh_jj = j + 1;
-                sh_dn = dz[0];
-                sh_up = dz[1];
+                sh_dn = dzb[0];
+                sh_up = dzb[1];
                 if (dz[0] < dz[1]) { sh_next = -1; sh_degrad = dz[1]; }
                 else { sh_next = +1; sh_degrad = dz[0]; }
                 if (sh_degrad == DBL_MAX) sh_brk = 1;
@@ -474,7 +478,7 @@ __global__ void __launch_bounds__(256) k_node_lp(NodeProb P, NodeIO io)
 size_t node_lp_lds(int m, int n)
 {
     const size_t N = (size_t)m + n;
-    return sizeof(double) * ((size_t)m * (2 * m + n) + 4 * N) + sizeof(int) * m + N + 16;
+    return sizeof(double) * ((size_t)m * (2 * m + n) + 4 * N + m) + sizeof(int) * m + N + 16;
 }
 
 void launch_node_lp(hipStream_t s, const NodeProb &P, const NodeIO &io, int nb)
@@ -703,12 +707,20 @@ extern "C" int gk_ios_driver(gk_ctx *ctx, gk_mip *mip, const gk_iocp *parm)
         const double eps = parm->tol_obj * (1.0 + std::fabs(S.c0 + S.sign * best));
         return bound < best - eps;
     };
-    std::vector<OpenNode *> batch;
-    while (!open.empty()) {
+    // the preferred child of every branched node of a batch is evaluated in
+    // the next batch (parallel dives, as BLB dives into its chosen child,
+    // glpios12.js); the other children wait in the best-bound queue
+    std::vector<OpenNode *> batch, dive, next_dive;
+    while (!open.empty() || !dive.empty()) {
         if (parm->tm_lim < 0x7fffffff &&
             std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() * 1000.0 >= parm->tm_lim)
             break;
         batch.clear();
+        for (OpenNode *nd : dive) {
+            if ((int)batch.size() < BMAX && hopeful(nd->bound)) batch.push_back(nd);
+            else if (hopeful(nd->bound)) open.push(nd);
+        }
+        dive.clear();
         while (!open.empty() && (int)batch.size() < BMAX) {
             OpenNode *nd = open.top();
             open.pop();
@@ -776,6 +788,7 @@ extern "C" int gk_ios_driver(gk_ctx *ctx, gk_mip *mip, const gk_iocp *parm)
             const double beta = x[m + j];
             const double dz[2] = {S.hdz.p[2 * b], S.hdz.p[2 * b + 1]};
             const int first = S.hnext.p[b] < 0 ? 0 : 1;  // preferred child gets the older seq
+            bool dived = false;
             for (int r = 0; r < 2; r++) {
                 const int kase = (r == 0) ? first : 1 - first;
                 if (dz[kase] == DBL_MAX) continue;        // that branch has no feasible point
@@ -790,10 +803,16 @@ extern "C" int gk_ios_driver(gk_ctx *ctx, gk_mip *mip, const gk_iocp *parm)
                 // a fixed bound pair makes a non-basic column NS
                 if (c->stat[m + j] != BS && c->lb[j] == c->ub[j]) c->stat[m + j] = NS;
                 store.push_back(c);
-                open.push(c);
+                if (!dived) {
+                    next_dive.push_back(c);
+                    dived = true;
+                } else
+                    open.push(c);
                 created++;
             }
         }
+        dive.swap(next_dive);
+        next_dive.clear();
         // release the evaluated nodes
         for (auto nd : batch) {
             nd->lb.clear(); nd->lb.shrink_to_fit();
@@ -801,7 +820,7 @@ extern "C" int gk_ios_driver(gk_ctx *ctx, gk_mip *mip, const gk_iocp *parm)
             nd->stat.clear(); nd->stat.shrink_to_fit();
         }
     }
-    const bool timed_out = !open.empty();
+    const bool timed_out = !open.empty() || !dive.empty();
     for (auto p : store) delete p;
     mip->lp_solves = lp_solves;
     mip->nodes_created = created;
