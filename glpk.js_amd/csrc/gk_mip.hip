@@ -624,7 +624,19 @@ hipStream_t gk_ctx_stream(gk_ctx *);
 
 extern "C" int gk_ios_driver(gk_ctx *ctx, gk_mip *mip, const gk_iocp *parm)
 {
+    return gk_ios_driver_sharded(ctx, mip, parm, nullptr);
+}
+
+extern "C" int gk_ios_driver_sharded(gk_ctx *ctx, gk_mip *mip, const gk_iocp *parm, const gk_ios_shard *shard)
+{
     if (!ctx || !mip || !parm) { set_err("gk_ios_driver: null argument"); return GK_EABI; }
+    const int rank = shard ? shard->rank : 0, size = shard ? shard->size : 1;
+    if (size < 1 || rank < 0 || rank >= size || (size > 1 && !shard->exchange)) {
+        set_err("gk_ios_driver: invalid shard %d of %d", rank, size);
+        return GK_EABI;
+    }
+    const int ramp = (shard && shard->ramp_nodes > 0) ? shard->ramp_nodes : 8;
+    const int sync_every = (shard && shard->sync_every > 0) ? shard->sync_every : 4;
     const gk_lp &L = mip->lp;
     const int m = L.m, n = L.n;
     if (m < 1 || n < 1) { set_err("gk_ios_driver: m = %d, n = %d; invalid dimensions", m, n); return GK_EABI; }
@@ -698,23 +710,64 @@ extern "C" int gk_ios_driver(gk_ctx *ctx, gk_mip *mip, const gk_iocp *parm)
         store.push_back(r);
         open.push(r);
     }
-    bool have = false;
-    double best = INF;                                    // incumbent, minimisation form
+    bool have = false;                                    // incumbent of this rank (with x)
+    double best = INF;                                    // its objective, minimisation form
+    double gbest = INF;                                   // best over all ranks (sharded runs)
     std::vector<double> xbest(S.N, 0.0);
     long long lp_solves = 0, pivots = 0, created = 1, failed = 0;
+    auto bestall = [&]() { return std::min(best, gbest); };
     auto hopeful = [&](double bound) {
-        if (!have) return true;
-        const double eps = parm->tol_obj * (1.0 + std::fabs(S.c0 + S.sign * best));
-        return bound < best - eps;
+        const double b = bestall();
+        if (b == INF) return true;
+        const double eps = parm->tol_obj * (1.0 + std::fabs(S.c0 + S.sign * b));
+        return bound < b - eps;
     };
     // the preferred child of every branched node of a batch is evaluated in
     // the next batch (parallel dives, as BLB dives into its chosen child,
     // glpios12.js); the other children wait in the best-bound queue
     std::vector<OpenNode *> batch, dive, next_dive;
-    while (!open.empty() || !dive.empty()) {
-        if (parm->tm_lim < 0x7fffffff &&
-            std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() * 1000.0 >= parm->tm_lim)
-            break;
+    // sharded runs: every rank evaluates the same first
+    // batches (deterministic, identical on every GPU) until the frontier holds
+    // ramp * size nodes, then keeps the nodes i = rank (mod size) of the
+    // frontier in (bound, creation) order; the incumbent value is exchanged
+    // every sync_every batches (exchange() is collective: an idle rank keeps
+    // calling it until no rank has work left)
+    bool split_done = (size == 1), timed_out = false;
+    int since_sync = 0;
+    for (;;) {
+        bool have_work = !open.empty() || !dive.empty();
+        if (have_work && parm->tm_lim < 0x7fffffff &&
+            std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() * 1000.0 >= parm->tm_lim) {
+            timed_out = true;
+            while (!open.empty()) open.pop();
+            dive.clear();
+            have_work = false;
+        }
+        if (!split_done) {
+            if (!have_work) break;                        // the tree ended during the ramp-up: same on every rank
+            if ((long long)open.size() + (long long)dive.size() >= (long long)ramp * size) {
+                std::vector<OpenNode *> front(dive.begin(), dive.end());
+                while (!open.empty()) { front.push_back(open.top()); open.pop(); }
+                dive.clear();
+                std::sort(front.begin(), front.end(), [](const OpenNode *a, const OpenNode *b) {
+                    return a->bound != b->bound ? a->bound < b->bound : a->seq < b->seq;
+                });
+                for (size_t i = 0; i < front.size(); i++)
+                    if ((int)(i % size) == rank) open.push(front[i]);
+                split_done = true;
+                continue;
+            }
+        }
+        if (split_done && size > 1 && (since_sync >= sync_every || !have_work)) {
+            double b = best;
+            const int active = shard->exchange(shard->info, &b, have_work ? 1 : 0);
+            if (b < gbest) gbest = b;
+            since_sync = 0;
+            if (active == 0) break;
+            if (!have_work) continue;
+        }
+        if (!have_work) break;
+        since_sync++;
         batch.clear();
         for (OpenNode *nd : dive) {
             if ((int)batch.size() < BMAX && hopeful(nd->bound)) batch.push_back(nd);
@@ -729,7 +782,8 @@ extern "C" int gk_ios_driver(gk_ctx *ctx, gk_mip *mip, const gk_iocp *parm)
         }
         if (batch.empty()) break;
         const int nb = (int)batch.size();
-        const double cut = have ? best - parm->tol_obj * (1.0 + std::fabs(S.c0 + S.sign * best)) : INF;
+        const double ball = bestall();
+        const double cut = ball < INF ? ball - parm->tol_obj * (1.0 + std::fabs(S.c0 + S.sign * ball)) : INF;
         for (int b = 0; b < nb; b++) {
             OpenNode *nd = batch[b];
             double *l = S.hlb.p + (size_t)b * S.N, *u = S.hub.p + (size_t)b * S.N;
@@ -820,7 +874,6 @@ extern "C" int gk_ios_driver(gk_ctx *ctx, gk_mip *mip, const gk_iocp *parm)
             nd->stat.clear(); nd->stat.shrink_to_fit();
         }
     }
-    const bool timed_out = !open.empty() || !dive.empty();
     for (auto p : store) delete p;
     mip->lp_solves = lp_solves;
     mip->nodes_created = created;

@@ -79,6 +79,14 @@ class Mip(C.Structure):
                 ("nodes_created", C.c_longlong), ("pivots", C.c_longlong)]
 
 
+_EXCHANGE_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.POINTER(C.c_double), C.c_int)
+
+
+class IosShard(C.Structure):
+    _fields_ = [("rank", C.c_int), ("size", C.c_int), ("ramp_nodes", C.c_int), ("sync_every", C.c_int),
+                ("exchange", _EXCHANGE_FN), ("info", C.c_void_p)]
+
+
 class SpxStats(C.Structure):
     _fields_ = [("pivots", C.c_longlong), ("reinversions", C.c_longlong), ("batches", C.c_longlong),
                 ("host_syncs", C.c_longlong), ("seconds_total", C.c_double), ("seconds_reinvert", C.c_double),
@@ -132,6 +140,8 @@ def load_library(path: str = LIB_PATH):
     L.gk_bfd_last_stats.argtypes = [P, C.POINTER(SpxStats)]
     L.gk_ios_driver.argtypes = [P, C.POINTER(Mip), C.POINTER(Iocp)]
     L.gk_ios_driver.restype = C.c_int
+    L.gk_ios_driver_sharded.argtypes = [P, C.POINTER(Mip), C.POINTER(Iocp), C.POINTER(IosShard)]
+    L.gk_ios_driver_sharded.restype = C.c_int
     L.gk_bfd_profile.argtypes = [P, C.c_int]
     L.gk_bfd_profile.restype = None
     L.gk_bfd_time_kernel.argtypes = [P, C.c_int, C.c_int, C.POINTER(C.c_double)]
@@ -478,6 +488,7 @@ GLP_BT_DFS, GLP_BT_BFS, GLP_BT_BLB, GLP_BT_BPH = 1, 2, 3, 4
 GLP_PP_NONE, GLP_PP_ROOT, GLP_PP_ALL = 0, 1, 2
 GLP_EROOT, GLP_ENOPFS, GLP_ENODFS, GLP_EMIPGAP = 0x0C, 0x0A, 0x0B, 0x0E
 GLP_CV, GLP_IV = 1, 2
+GLP_OPT = 5
 
 
 def IOCP(**options) -> Iocp:
@@ -490,8 +501,12 @@ def IOCP(**options) -> Iocp:
     return p
 
 
-def glp_intopt(P: GkProblem, parm: Iocp | None = None) -> int:
-    """glp_intopt (glpapi09.js:61) -> solve_mip (:62) -> ios_driver."""
+def glp_intopt(P: GkProblem, parm: Iocp | None = None, comm=None) -> int:
+    """glp_intopt (glpapi09.js:61) -> solve_mip (:62) -> ios_driver.
+
+    comm (shard.TorchComm or alike, size > 1): this process explores its share
+    of the tree on its GPU; the incumbent is exchanged through comm and the
+    best one over all ranks is returned on every rank."""
     if parm is None:
         parm = IOCP()
     if parm.msg_lev not in (0, 1, 2, 3, 4):
@@ -533,10 +548,45 @@ def glp_intopt(P: GkProblem, parm: Iocp | None = None) -> int:
     mip.col_kind = ptr(P.col_kind)
     mip.col_mipx = ptr(P.col_mipx)
     mip.row_mipx = ptr(P.row_mipx)
-    ret = P.L.gk_ios_driver(P.ctx.h, C.byref(mip), C.byref(parm))
+    if comm is None or comm.size == 1:
+        ret = P.L.gk_ios_driver(P.ctx.h, C.byref(mip), C.byref(parm))
+        if ret == GK_EABI:
+            raise GkError(_err(P.L))
+        P.mip_stat = mip.mip_stat
+        P.mip_obj = mip.mip_obj
+        P.mip_stats = dict(lp_solves=mip.lp_solves, nodes_created=mip.nodes_created, pivots=mip.pivots)
+        return ret
+    errors = []
+
+    def exchange(_info, best, active):
+        try:
+            b, act = comm.exchange(best[0], active)
+            best[0] = b
+            return act
+        except Exception as e:          # a failing collective must not unwind through C
+            errors.append(e)
+            return 0
+
+    cb = _EXCHANGE_FN(exchange)
+    sh = IosShard(rank=comm.rank, size=comm.size, ramp_nodes=0, sync_every=0, exchange=cb, info=None)
+    ret = P.L.gk_ios_driver_sharded(P.ctx.h, C.byref(mip), C.byref(parm), C.byref(sh))
+    if errors:
+        raise errors[0]
     if ret == GK_EABI:
         raise GkError(_err(P.L))
-    P.mip_stat = mip.mip_stat
-    P.mip_obj = mip.mip_obj
-    P.mip_stats = dict(lp_solves=mip.lp_solves, nodes_created=mip.nodes_created, pivots=mip.pivots)
+    sign = 1.0 if P.dir == GLP_MIN else -1.0
+    have = mip.mip_stat == GLP_OPT
+    local = sign * (mip.mip_obj - P.c0) if have else float("inf")
+    x = np.concatenate([P.row_mipx[1:], P.col_mipx[1:]])
+    win, found, xw, _ = comm.finalize(local, have, x)
+    if found:
+        P.mip_stat = GLP_OPT
+        P.mip_obj = P.c0 + sign * win
+        P.row_mipx[1:] = xw[:P.m]
+        P.col_mipx[1:] = xw[P.m:]
+    else:
+        P.mip_stat = GLP_NOFEAS
+        P.mip_obj = 0.0
+    P.mip_stats = dict(lp_solves=int(comm.total(mip.lp_solves)), nodes_created=int(comm.total(mip.nodes_created)),
+                       pivots=int(comm.total(mip.pivots)), local_lp_solves=mip.lp_solves)
     return ret

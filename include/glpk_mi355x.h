@@ -179,6 +179,25 @@ typedef struct {
 
 int gk_ios_driver(gk_ctx *ctx, gk_mip *mip, const gk_iocp *parm);
 
+/* one GPU's share of a branch-and-bound run over several GPUs (one process
+ * per GPU).  All ranks call gk_ios_driver_sharded on the same problem; they
+ * evaluate the first batches identically, split the frontier round-robin
+ * (node i -> rank i mod size), and exchange the incumbent value through
+ * exchange() every sync_every batches.  exchange() is collective: it receives
+ * this rank's best objective (internal minimisation form; DBL_MAX if none) and
+ * whether it still has open nodes, must return the minimum over ranks in
+ * *best and the number of ranks with work (0 ends the run).  On return each
+ * rank holds its own incumbent (mip_stat GLP_OPT with a solution, else
+ * GLP_NOFEAS); the caller picks the best over ranks. */
+typedef struct {
+    int rank, size;
+    int ramp_nodes;                 /* frontier per rank before the split (0: 8) */
+    int sync_every;                 /* batches between exchanges (0: 4) */
+    int (*exchange)(void *info, double *best, int active);
+    void *info;
+} gk_ios_shard;
+int gk_ios_driver_sharded(gk_ctx *ctx, gk_mip *mip, const gk_iocp *parm, const gk_ios_shard *shard);
+
 #ifdef __cplusplus
 }
 #endif

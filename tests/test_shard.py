@@ -1,0 +1,115 @@
+"""Multi-process branch and bound (glpk.js_amd/shard.py, gk_ios_driver_sharded).
+
+CPU: the exchange / winner-selection collectives with world_size 2 over gloo.
+GPU: two ranks share the box's GPU (gloo for the incumbent exchange) and
+solve MIP fixtures sharded; both must return the reference's objective and
+the same incumbent."""
+import json
+import os
+import socket
+import sys
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _comm_worker(rank, world, port, q):
+    import torch.distributed as dist
+    sys.path.insert(0, ROOT)
+    import __graft_entry__
+    __graft_entry__.load_package()
+    from glpk_js_amd.shard import TorchComm
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    c = TorchComm()
+    out = {}
+    # exchange: min of the bests, any-active indicator
+    out["ex1"] = c.exchange([5.0, 3.0][rank], [1, 0][rank])
+    out["ex2"] = c.exchange([1e300, 7.0][rank], 0)
+    out["total"] = c.total(rank + 1)
+    # finalize: rank 1 has the better objective; its x is broadcast
+    x = np.full(4, float(rank))
+    obj, have, xw, win = c.finalize([10.0, 2.0][rank], True, x)
+    out["fin"] = (obj, have, xw.tolist(), win)
+    # ties go to the lowest rank; no solution anywhere
+    out["tie"] = c.finalize(3.0, True, np.full(2, float(rank)))[2].tolist()
+    out["none"] = c.finalize(0.0, False, np.zeros(1))[1]
+    dist.destroy_process_group()
+    q.put((rank, out))
+
+
+def test_torchcomm_gloo_world2():
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_comm_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    res = dict(q.get(timeout=120) for _ in ps)
+    for p in ps:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for r in range(2):
+        o = res[r]
+        assert o["ex1"] == (3.0, 1)
+        assert o["ex2"] == (7.0, 0)
+        assert o["total"] == 3.0
+        assert o["fin"] == (2.0, True, [1.0] * 4, 1)
+        assert o["tie"] == [0.0, 0.0]
+        assert o["none"] is False
+
+
+def _bnb_worker(rank, world, port, names, q):
+    import torch
+    import torch.distributed as dist
+    sys.path.insert(0, ROOT)
+    import __graft_entry__
+    __graft_entry__.load_package()
+    from glpk_js_amd import gk, problems
+    from glpk_js_amd.shard import TorchComm
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    comm = TorchComm()
+    ctx = gk.Context(0)
+    out = {}
+    for name in names:
+        d = json.load(open(os.path.join(ROOT, "tests", "golden", f"mip_{name}.json")))
+        P = gk.GkProblem(ctx, problems.from_fixture(d))
+        assert gk.glp_simplex(P, gk.SMCP(**d["root"]["opts"])) == 0
+        ret = gk.glp_intopt(P, gk.IOCP(msg_lev=gk.GLP_MSG_OFF), comm=comm)
+        out[name] = (ret, P.mip_stat, P.mip_obj, P.col_mipx[1:].tolist(), P.mip_stats)
+    dist.destroy_process_group()
+    q.put((rank, out))
+
+
+@pytest.mark.gpu
+def test_sharded_bnb_two_ranks_one_gpu():
+    import torch.multiprocessing as mp
+    names = ["c5s_12x20", "mixint8", "mixint11", "gap"]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_bnb_worker, args=(r, 2, port, names, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    res = dict(q.get(timeout=600) for _ in ps)
+    for p in ps:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    for name in names:
+        ref = json.load(open(os.path.join(ROOT, "tests", "golden", f"mip_{name}.json")))["mip"]
+        a, b = res[0][name], res[1][name]
+        assert a[0] == b[0] == ref["ret"]
+        assert a[1] == b[1] == ref["mip_stat"]
+        assert abs(a[2] - ref["mip_obj"]) <= 1e-9 * max(1.0, abs(ref["mip_obj"]))
+        assert a[2] == b[2] and a[3] == b[3], "ranks disagree on the incumbent"
+        print(name, "lp_solves", a[4])
