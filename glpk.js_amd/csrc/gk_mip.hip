@@ -780,7 +780,7 @@ extern "C" int gk_ios_driver_sharded(gk_ctx *ctx, gk_mip *mip, const gk_iocp *pa
             if (!hopeful(nd->bound)) continue;
             batch.push_back(nd);
         }
-        if (batch.empty()) break;
+        if (batch.empty()) continue;                      // everything left was pruned
         const int nb = (int)batch.size();
         const double ball = bestall();
         const double cut = ball < INF ? ball - parm->tol_obj * (1.0 + std::fabs(S.c0 + S.sign * ball)) : INF;
