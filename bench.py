@@ -54,10 +54,13 @@ def main():
     # (one runtime per process)
     import torch
     import torch.distributed as dist
+    ndev = torch.cuda.device_count() if torch.cuda.is_available() else 0
+    device = local_rank % max(1, ndev)          # more ranks than GPUs only in rehearsals
     if world > 1:
-        dist.init_process_group(backend="nccl" if torch.cuda.is_available() else "gloo")
-    if torch.cuda.is_available():
-        torch.cuda.set_device(local_rank)
+        backend = os.environ.get("GK_DIST_BACKEND") or ("nccl" if ndev else "gloo")
+        dist.init_process_group(backend=backend)
+    if ndev:
+        torch.cuda.set_device(device)
 
     __graft_entry__.build_hip()
     __graft_entry__.load_package()
@@ -71,7 +74,7 @@ def main():
 
     t_gen = time.time()
     prob = problems.gen_dense(args.m, args.n, seed=42 + rank)
-    ctx = gk.Context(local_rank)
+    ctx = gk.Context(device)
     P = gk.GkProblem(ctx, prob)
     assert P.factorize() == 0
     parm = gk.SMCP(meth=gk.GLP_DUAL, it_lim=args.pivots_per_step, msg_lev=gk.GLP_MSG_ERR)
@@ -197,9 +200,14 @@ def main():
                          f"{cres['it_cnt']} pivots in {cdt:.1f}s incl. init_csa; reference node "
                          f"dist/glpk.js measured 9.4 pivots/s on this config (BASELINE.md)"}
 
-    if rank == 0 and world == 1 and not args.no_extra:
-        del P
-        extra = run_extra(gk, problems, ctx, prob)
+    if not args.no_extra:
+        if world == 1:
+            del P
+            extra = run_extra(gk, problems, ctx, prob)
+        else:
+            # B&B sharded over all ranks (subtree per GPU, incumbent all-reduce)
+            from glpk_js_amd.shard import TorchComm
+            extra = run_bnb(gk, problems, ctx, names=("c5s_12x30",), comm=TorchComm())
 
     if rank == 0:
         line = {
@@ -262,27 +270,32 @@ def run_extra(gk, problems, ctx, c3):
     return out
 
 
-def run_bnb(gk, problems, ctx):
+def run_bnb(gk, problems, ctx, names=("gap", "c5s_12x30"), comm=None):
     """B&B configs (BASELINE.json configs[3], C5s surrogate of configs[4]):
     root glp_simplex + glp_intopt on the device; LP-relaxations/s = node LP
-    solves / wall time of glp_intopt."""
+    solves (all ranks) / wall time of glp_intopt."""
     import json as _json
     out = {}
     gold = os.path.join(ROOT, "tests", "golden")
-    for name, ref_lps, ref_s in (("gap", 196, 0.0477), ("c5s_12x30", 70506, 49.7)):
+    refs = {"gap": (196, 0.0477), "c5s_12x30": (70506, 49.7)}
+    for name in names:
+        ref_lps, ref_s = refs[name]
         d = _json.load(open(os.path.join(gold, "mip_" + name + ".json")))
         prob = problems.from_fixture(d)
         P = gk.GkProblem(ctx, prob)
         assert gk.glp_simplex(P, gk.SMCP(msg_lev=gk.GLP_MSG_ERR)) == 0
         t0 = time.perf_counter()
-        ret = gk.glp_intopt(P, gk.IOCP(msg_lev=gk.GLP_MSG_ERR))
+        ret = gk.glp_intopt(P, gk.IOCP(msg_lev=gk.GLP_MSG_ERR), comm=comm)
         dt = time.perf_counter() - t0
+        if comm is not None:
+            dt = -comm.exchange(-dt, 0)[0]         # max over ranks
         lps = P.mip_stats.get("lp_solves", 0)
         out["bnb_" + name] = {"ret": ret, "mip_obj": P.mip_obj, "ref_mip_obj": d["mip"]["mip_obj"],
                               "lp_relaxations": lps, "seconds": round(dt, 4),
                               "lp_relax_per_s": round(lps / dt, 1), "nodes": P.mip_stats.get("nodes_created"),
                               "reference_lp_relaxations": ref_lps, "reference_seconds": ref_s,
-                              "reference_lp_relax_per_s": round(ref_lps / ref_s, 1)}
+                              "reference_lp_relax_per_s": round(ref_lps / ref_s, 1),
+                              "ranks": comm.size if comm is not None else 1}
     return out
 
 
