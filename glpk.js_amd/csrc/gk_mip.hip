@@ -215,6 +215,7 @@ __global__ void __launch_bounds__(256) k_node_lp(NodeProb P, NodeIO io)
             }
         __syncthreads();
         const double inv = 1.0 / M[(size_t)k * W + k];
+        __syncthreads();                      // every thread has read the pivot before row k is scaled
         for (int c = threadIdx.x; c < W; c += blockDim.x) M[(size_t)k * W + c] *= inv;
         // multipliers of column k, saved before the elimination overwrites it
         for (int i = threadIdx.x; i < m; i += blockDim.x) fcol[i] = (i == k) ? 0.0 : M[(size_t)i * W + k];
