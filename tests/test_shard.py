@@ -47,18 +47,41 @@ def _comm_worker(rank, world, port, q):
     q.put((rank, out))
 
 
-def test_torchcomm_gloo_world2():
+def _run_ranks(target, world, args, timeout):
+    """Start `world` spawned ranks, collect one result each; a rank that dies
+    or a run that exceeds `timeout` seconds fails the test (the remaining
+    ranks are terminated, by their own PIDs)."""
+    import queue
+    import time
     import torch.multiprocessing as mp
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    ps = [ctx.Process(target=_comm_worker, args=(r, 2, port, q)) for r in range(2)]
+    ps = [ctx.Process(target=target, args=(r, world, port) + tuple(args) + (q,)) for r in range(world)]
     for p in ps:
         p.start()
-    res = dict(q.get(timeout=120) for _ in ps)
+    res, t_end = {}, time.time() + timeout
+    try:
+        while len(res) < world:
+            try:
+                r, out = q.get(timeout=1.0)
+                res[r] = out
+            except queue.Empty:
+                dead = [p.exitcode for p in ps if p.exitcode not in (None, 0)]
+                assert not dead, f"a rank died with exit code {dead}"
+                assert time.time() < t_end, "ranks did not finish in time"
+    finally:
+        for p in ps:
+            p.join(timeout=30)
+            if p.is_alive():
+                p.terminate()
     for p in ps:
-        p.join(timeout=60)
         assert p.exitcode == 0
+    return res
+
+
+def test_torchcomm_gloo_world2():
+    res = _run_ranks(_comm_worker, 2, (), 120)
     for r in range(2):
         o = res[r]
         assert o["ex1"] == (3.0, 1)
@@ -93,18 +116,8 @@ def _bnb_worker(rank, world, port, names, q):
 
 @pytest.mark.gpu
 def test_sharded_bnb_two_ranks_one_gpu():
-    import torch.multiprocessing as mp
     names = ["c5s_12x20", "mixint8", "mixint11", "gap"]
-    ctx = mp.get_context("spawn")
-    q = ctx.Queue()
-    port = _free_port()
-    ps = [ctx.Process(target=_bnb_worker, args=(r, 2, port, names, q)) for r in range(2)]
-    for p in ps:
-        p.start()
-    res = dict(q.get(timeout=600) for _ in ps)
-    for p in ps:
-        p.join(timeout=120)
-        assert p.exitcode == 0
+    res = _run_ranks(_bnb_worker, 2, (names,), 240)
     for name in names:
         ref = json.load(open(os.path.join(ROOT, "tests", "golden", f"mip_{name}.json")))["mip"]
         a, b = res[0][name], res[1][name]
