@@ -203,7 +203,9 @@ __global__ void __launch_bounds__(256) k_node_lp(NodeProb P, NodeIO io)
             if (idx < 0 || v > key) { key = v; idx = i; }
         }
         const int piv = block_argmax(key, idx, shk, shi);
-        if (piv < 0 || fabs(M[(size_t)piv * W + k]) < 1e-12) {
+        const bool singular = piv < 0 || fabs(M[(size_t)piv * W + k]) < 1e-12;
+        __syncthreads();                      // every wave has read M[piv][k] before the swap moves it
+        if (singular) {
             if (threadIdx.x == 0) { io.status[b] = NODE_FAIL; io.pivots[b] = 0; }
             return;
         }
