@@ -26,6 +26,7 @@ sys.path.insert(0, ROOT)
 import __graft_entry__  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+ROOF_KERNEL = "k_trow_rows"
 
 
 def log(rank, *a):
@@ -165,12 +166,13 @@ def main():
         tpath = os.path.join(ROOT, "profiles", "r01_pmc_traffic.json")
         if os.path.exists(tpath):
             try:
-                traffic = json.load(open(tpath))["kernels"].get("k_lgemv_part", {}).get("bytes_per_launch")
+                traffic = json.load(open(tpath))["kernels"].get(ROOF_KERNEL, {}).get("bytes_per_launch")
             except Exception:
                 traffic = None
         roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                "kernel": "k_lgemv_part (pivot row trow = rho' A over the rows of A in the support of rho)",
+                "kernel": ROOF_KERNEL + " (pivot row trow = -rho' N over the rows of A in the support of rho, "
+                                        "fused with the ratio-test candidates)",
                 "ms_per_launch": round(ms, 5), "launches": dev["launches"],
                 "bytes_per_launch": round(b),
                 "timing": "device wall clock (s_memrealtime) over every launch of the timed region, entry to next entry",

@@ -141,6 +141,22 @@ static __device__ Cand block_best(Cand c, Cand *sh)
     return r;
 }
 
+// the same within one wave (no block synchronisation); every lane gets it
+template <int MODE>
+__device__ __forceinline__ Cand wave_best(Cand c)
+{
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        Cand d;
+        d.k1 = __shfl_xor(c.k1, o);
+        d.k2 = __shfl_xor(c.k2, o);
+        d.idx = __shfl_xor(c.idx, o);
+        d.aux = __shfl_xor(c.aux, o);
+        if (better<MODE>(d, c)) c = d;
+    }
+    return c;
+}
+
 __device__ __forceinline__ unsigned long long dbits(double v) { return (unsigned long long)__double_as_longlong(v); }
 
 __device__ __forceinline__ double get_xN(const signed char *stat, const double *lb, const double *ub, int k, int j)

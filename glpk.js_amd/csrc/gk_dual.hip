@@ -40,8 +40,13 @@ namespace gk {
 static inline int cdiv(int a, int b) { return (a + b - 1) / b; }
 __device__ __forceinline__ int gv_of(int m, int n) { return (max(m, n) + 255) / 256; }
 __device__ __forceinline__ Cand *cand_chuzr(const SpxDev &d) { return (Cand *)d.cand; }
+// per-block outputs: chuzr candidates [gv); pass-1 candidates of the pivot-row
+// blocks [4 gv) (64-slot blocks of k_trow_rows, or 256-slot blocks of
+// k_trow_finish); pass-2 candidates [gv).  gpart: gamma_p sums [4 gv), then
+// max |trow| [4 gv) of the same blocks.
 __device__ __forceinline__ Cand *cand_pass1(const SpxDev &d) { return (Cand *)d.cand + gv_of(d.m, d.n); }
-__device__ __forceinline__ Cand *cand_pass2(const SpxDev &d) { return (Cand *)d.cand + 2 * gv_of(d.m, d.n); }
+__device__ __forceinline__ Cand *cand_pass2(const SpxDev &d) { return (Cand *)d.cand + 5 * gv_of(d.m, d.n); }
+__device__ __forceinline__ double *tmax_part(const SpxDev &d) { return d.gpart + 4 * gv_of(d.m, d.n); }
 __device__ __forceinline__ Cand no_cand(double k1)
 {
     Cand c; c.k1 = k1; c.k2 = 0.0; c.idx = 0; c.aux = 0;
@@ -99,6 +104,77 @@ __device__ __forceinline__ void lgemv_tile(const double *__restrict__ M, size_t 
             b1 += v.y * xb;
         }
     }
+    o[r] = a0;
+    if (r + 1 < rows) o[r + 1] = a1;
+    if (NRHS == 2) {
+        o[rows + r] = b0;
+        if (r + 1 < rows) o[rows + r + 1] = b1;
+    }
+}
+
+// the same with the multipliers staged in LDS, 256 list entries at a time:
+// thread k evaluates xf for entry k of the chunk once per block (xf may be a
+// chain of loads), instead of every thread evaluating it for every entry.
+// Called by the whole block (it synchronises); rows beyond `rows` idle.
+template <int NRHS, typename XF>
+__device__ __forceinline__ void lgemv_tile_staged(const double *__restrict__ M, size_t ld, int rows,
+                                                  const int *__restrict__ list, int t0, int t1, int r, XF xf,
+                                                  double *__restrict__ o)
+{
+    __shared__ double sxa[256], sxb[256];
+    __shared__ int sc[256];
+    const bool act = r < rows;
+    double a0 = 0.0, a1 = 0.0, b0 = 0.0, b1 = 0.0;
+    for (int c0 = t0; c0 < t1; c0 += 256) {
+        const int cn = min(256, t1 - c0);
+        __syncthreads();
+        if ((int)threadIdx.x < cn) {
+            const int c = list[c0 + threadIdx.x];
+            double xa, xb;
+            xf(c0 + threadIdx.x, c, xa, xb);
+            sc[threadIdx.x] = c;
+            sxa[threadIdx.x] = xa;
+            sxb[threadIdx.x] = xb;
+        }
+        __syncthreads();
+        if (!act) continue;
+        int k = 0;
+        for (; k + 4 <= cn; k += 4) {
+            double xa[4], xb[4];
+            bool any = false;
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                xa[u] = sxa[k + u];
+                xb[u] = (NRHS == 2) ? sxb[k + u] : 0.0;
+                any = any || xa[u] != 0.0 || xb[u] != 0.0;
+            }
+            if (!any) continue;
+            double2 v[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) v[u] = *(const double2 *)(M + (size_t)sc[k + u] * ld + r);
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                a0 += v[u].x * xa[u];
+                a1 += v[u].y * xa[u];
+                if (NRHS == 2) {
+                    b0 += v[u].x * xb[u];
+                    b1 += v[u].y * xb[u];
+                }
+            }
+        }
+        for (; k < cn; ++k) {
+            const double xa = sxa[k], xb = (NRHS == 2) ? sxb[k] : 0.0;
+            if (xa == 0.0 && xb == 0.0) continue;
+            const double2 v = *(const double2 *)(M + (size_t)sc[k] * ld + r);
+            a0 += v.x * xa;
+            a1 += v.y * xa;
+            if (NRHS == 2) {
+                b0 += v.x * xb;
+                b1 += v.y * xb;
+            }
+        }
+    }
+    if (!act) return;
     o[r] = a0;
     if (r + 1 < rows) o[r + 1] = a1;
     if (NRHS == 2) {
@@ -463,17 +539,18 @@ __global__ void __launch_bounds__(256) k_trow_finish(SpxDev d, const double *__r
     if (st->stop) return;
     const int m = d.m, n = d.n;
     const int idx = blockIdx.x * blockDim.x + threadIdx.x;
-    if (FROM_PART) {
-        if (blockIdx.x == 0 && threadIdx.x == 0) st->tk_next = wall_clock64();
-        // end of the pivot-row kernel: latest block stamp
+    if (FROM_PART && blockIdx.x == 0) {
+        // end of the pivot-row kernel: latest block stamp (one block, plain
+        // store: same-address atomics from every block serialise)
+        if (threadIdx.x == 0) st->tk_next = wall_clock64();
         unsigned long long e = 0;
-        for (int t = idx; t < nslots; t += gridDim.x * blockDim.x) e = max(e, d.tslots[t]);
+        for (int t = threadIdx.x; t < nslots; t += blockDim.x) e = max(e, d.tslots[t]);
         __shared__ unsigned long long she;
         if (threadIdx.x == 0) she = 0;
         __syncthreads();
         if (e) atomicMax(&she, e);
         __syncthreads();
-        if (threadIdx.x == 0 && she) atomicMax(&st->tk_end, she);
+        if (threadIdx.x == 0 && she) st->tk_end = she;
     }
     // all gathers first (bind -> stat/cbar/refsp/partials), reductions after
     const int pos1 = (idx < n) ? d.bind[m + idx] : 0;
@@ -516,7 +593,8 @@ __global__ void __launch_bounds__(256) k_trow_finish(SpxDev d, const double *__r
         gsum = w1 * w1 + w2 * w2;
     }
     const double bmax = block_max(fmax(fabs(tv1), fabs(tv2)), shd);
-    if (FROM_PART && threadIdx.x == 0 && bmax > 0.0) atomicMax(&st->trow_max_bits, dbits(bmax));
+    // per-block max |trow|; k_dual_ratio reduces them into st->trow_max_bits
+    if (FROM_PART && threadIdx.x == 0) tmax_part(d)[blockIdx.x] = bmax;
     if (pse) {
         const double g = block_sum(gsum, shd);
         if (threadIdx.x == 0) d.gpart[blockIdx.x] = g;
@@ -532,15 +610,116 @@ __global__ void __launch_bounds__(256) k_trow_finish(SpxDev d, const double *__r
 }
 
 // ---------------------------------------------------------------------------
+// k_trow_rows (row path, dense A): the pivot row and the work of
+// k_trow_finish in one kernel.  Block b owns the 64 slots [64 b, 64 b + 64)
+// (structural column c and slack row c of each slot).  Its waves split the
+// support of rho (rows t = w, w + nw, ... of AT, 512-byte coalesced segments
+// of the 64 columns), the partial sums meet in LDS in wave order, and wave 0
+// finishes the slots with wave-level reductions: trow, the PSE vectors, the
+// gamma_p partial, max |trow| and the Harris pass-1 candidate of the block.
+// Block 0 stamps the device clock at entry and every block at exit (tslots).
+// ---------------------------------------------------------------------------
+__global__ void __launch_bounds__(1024) k_trow_rows(SpxDev d, int pse)
+{
+    __shared__ double sp[16][64];
+    DState *st = d.st;
+    if (st->stop) return;
+    const int m = d.m, n = d.n;
+    const int lane = threadIdx.x & 63;
+    const int w = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+    const int nw = blockDim.x >> 6;
+    const int idx = blockIdx.x * 64 + lane;
+    if (blockIdx.x == 0 && threadIdx.x == 0) st->tk_start = wall_clock64();
+    // wave 0 gathers its slot operands first; their latency overlaps the rows
+    int pos1 = 0, pos2 = 0, rp2 = -1;
+    if (w == 0) {
+        pos1 = (idx < n) ? d.bind[m + idx] : 0;
+        pos2 = (idx < m) ? d.bind[idx] : 0;
+        rp2 = (idx < m) ? d.rpos[idx] : -1;
+    }
+    const int ns = st->ns;
+    double acc = 0.0;
+    if (idx < n) {
+        const double *__restrict__ col = d.A.AT + idx;
+        const size_t ldt = (size_t)d.A.ldt;
+        const int *__restrict__ ri = d.rho_idx;
+        const double *__restrict__ rv = d.rho_val;
+        int t = w;
+        for (; t + 7 * nw < ns; t += 8 * nw) {
+            int r[8];
+            double v[8], a[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                r[u] = ri[t + u * nw];
+                v[u] = rv[t + u * nw];
+            }
+#pragma unroll
+            for (int u = 0; u < 8; ++u) a[u] = col[(size_t)r[u] * ldt];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) acc += v[u] * a[u];
+        }
+        for (; t < ns; t += nw) acc += rv[t] * col[(size_t)ri[t] * ldt];
+    }
+    sp[w][lane] = acc;
+    __syncthreads();
+    if (w != 0) return;                      // wave 0 only from here: no block barriers
+    double tsum = 0.0;
+    for (int k = 0; k < nw; ++k) tsum += sp[k][lane];
+    const int j1 = (pos1 > m) ? pos1 - m - 1 : -1;
+    const int j2 = (pos2 > m) ? pos2 - m - 1 : -1;
+    int s1 = 0, s2 = 0;
+    double cb1 = 0.0, cb2 = 0.0, tv1 = 0.0, tv2 = 0.0;
+    bool ref1 = false, ref2 = false;
+    if (j1 >= 0) {
+        s1 = d.stat[j1];
+        cb1 = d.cbar[j1];
+        tv1 = tsum;
+        if (pse) ref1 = d.refsp[m + idx] != 0;
+    }
+    if (j2 >= 0) {
+        s2 = d.stat[j2];
+        cb2 = d.cbar[j2];
+        tv2 = -d.rho_val[rp2];               // a non-basic slack is a dense column of inv(B)
+        if (pse) ref2 = d.refsp[idx] != 0;
+    }
+    if (s1 == NS) tv1 = 0.0;
+    if (s2 == NS) tv2 = 0.0;
+    if (j1 >= 0) d.trow[j1] = tv1;
+    if (j2 >= 0) d.trow[j2] = tv2;
+    double gsum = 0.0;
+    if (pse) {
+        const double w1 = ref1 ? tv1 : 0.0, w2 = ref2 ? tv2 : 0.0;
+        if (idx < n) d.wcol[idx] = w1;
+        if (idx < m) d.ys[idx] = w2;
+        gsum = w1 * w1 + w2 * w2;
+    }
+    const double bmax = wmax(fmax(fabs(tv1), fabs(tv2)));
+    const double g = pse ? wsum(gsum) : 0.0;
+    // pass-1 candidate with eps_b = tol_bnd (1 + 0.01 max_b) <= eps
+    const RatioCtx x = ratio_ctx(st, bmax);
+    Cand c = no_cand(DBL_MAX);
+    Cand e;
+    if (j1 >= 0 && pass1_cand(x, tv1, cb1, s1, j1, e) && better<1>(e, c)) c = e;
+    if (j2 >= 0 && pass1_cand(x, tv2, cb2, s2, j2, e) && better<1>(e, c)) c = e;
+    const Cand b = wave_best<1>(c);
+    if (lane == 0) {
+        tmax_part(d)[blockIdx.x] = bmax;
+        if (pse) d.gpart[blockIdx.x] = g;
+        cand_pass1(d)[blockIdx.x] = b;
+        d.tslots[blockIdx.x] = wall_clock64();
+    }
+}
+
+// ---------------------------------------------------------------------------
 // k_dual_ratio: blocks [0, gn) — pass-1 choice from the block candidates
 // (a block whose candidate fails the global significance tolerance is
 // rescanned), then the pass-2 candidates of positions [256 b, 256 b + 256);
 // blocks [gn, ...) — partials of A w over the reference-space columns.
 // ---------------------------------------------------------------------------
-__global__ void __launch_bounds__(256) k_dual_ratio(SpxDev d, int gn, int tiles_m, int aw)
+__global__ void __launch_bounds__(256) k_dual_ratio(SpxDev d, int gn, int tiles_m, int rowpath, int ncb, int slotw)
 {
     __shared__ Cand shc[16];
-    __shared__ int shf[2];
+    __shared__ double shd[16];
     DState *st = d.st;
     if (st->stop) return;
     const int m = d.m, n = d.n;
@@ -557,26 +736,54 @@ __global__ void __launch_bounds__(256) k_dual_ratio(SpxDev d, int gn, int tiles_
                       d.awpart + (size_t)split * m);
         return;
     }
-    const RatioCtx x = ratio_ctx(st, trow_big(st));
-    const int gv = gv_of(m, n);
+    double big;
+    if (rowpath) {
+        // max |trow| from the pivot-row blocks; block 0 publishes it and the
+        // end of the pivot-row kernel (latest block exit stamp)
+        double v = 0.0;
+        unsigned long long e = 0;
+        for (int b = threadIdx.x; b < ncb; b += blockDim.x) {
+            v = fmax(v, tmax_part(d)[b]);
+            if (blockIdx.x == 0) e = max(e, d.tslots[b]);
+        }
+        big = block_max(v, shd);
+        if (blockIdx.x == 0) {
+            __shared__ unsigned long long she;
+            if (threadIdx.x == 0) {
+                she = 0;
+                st->tk_next = wall_clock64();
+            }
+            __syncthreads();
+            if (e) atomicMax(&she, e);
+            __syncthreads();
+            if (threadIdx.x == 0) {
+                st->trow_max_bits = dbits(big);
+                st->tk_end = she;
+            }
+        }
+    } else
+        big = trow_big(st);
+    const RatioCtx x = ratio_ctx(st, big);
     const int j = blockIdx.x * blockDim.x + threadIdx.x;
     const double trj = (j < n) ? d.trow[j] : 0.0;
     const double cbj = (j < n) ? d.cbar[j] : 0.0;
     const int sj = (j < n) ? d.stat[j] : 0;
     Cand c = no_cand(DBL_MAX);
     int fail = 0;
-    for (int b = threadIdx.x; b < gv; b += blockDim.x) {
+    for (int b = threadIdx.x; b < ncb; b += blockDim.x) {
         const Cand e = cand_pass1(d)[b];
         if (e.idx != 0 && e.k2 < x.eps) fail = 1;
         else if (better<1>(e, c)) c = e;
     }
     if (__syncthreads_or(fail)) {
         // rare: rescan the blocks whose candidate is not significant
-        for (int b = 0; b < gv; ++b) {
+        for (int b = 0; b < ncb; ++b) {
             const Cand e = cand_pass1(d)[b];
             if (!(e.idx != 0 && e.k2 < x.eps)) continue;
-            const Cand f = pass1_slot(d, x, b * 256 + threadIdx.x);
-            if (better<1>(f, c)) c = f;
+            if ((int)threadIdx.x < slotw) {
+                const Cand f = pass1_slot(d, x, b * slotw + threadIdx.x);
+                if (better<1>(f, c)) c = f;
+            }
         }
     }
     const Cand b1 = block_best<1>(c, shc);
@@ -588,8 +795,6 @@ __global__ void __launch_bounds__(256) k_dual_ratio(SpxDev d, int gn, int tiles_
         st->teta1 = teta1;
         st->need2 = need2;
     }
-    (void)shf;
-    (void)aw;
     if (!need2) return;
     Cand c2 = no_cand(0.0);
     if (j < n) {
@@ -603,7 +808,7 @@ __global__ void __launch_bounds__(256) k_dual_ratio(SpxDev d, int gn, int tiles_
 // the entering choice q (pass 2 if needed), its checks and the st fields;
 // every block of the calling grid evaluates it identically.  Returns q, or 0
 // when the iteration stops.
-__device__ int dual_pick(const SpxDev &d, Cand *shc, double *shd, int pse, int gn)
+__device__ int dual_pick(const SpxDev &d, Cand *shc, double *shd, int pse, int gn, int ncb)
 {
     DState *st = d.st;
     int q;
@@ -637,9 +842,8 @@ __device__ int dual_pick(const SpxDev &d, Cand *shc, double *shd, int pse, int g
     if (lead) {
         if (pse) {
             // gamma_p (update_gamma :1103-1132) from the per-block sums, fixed order
-            const int gv = gv_of(d.m, d.n);
             double g = 0.0;
-            for (int b = threadIdx.x; b < gv; b += blockDim.x) g += d.gpart[b];
+            for (int b = threadIdx.x; b < ncb; b += blockDim.x) g += d.gpart[b];
             g = block_sum(g, shd);
             if (threadIdx.x == 0) {
                 const double eta = d.refsp[d.head[st->p - 1] - 1] ? 1.0 : 0.0;
@@ -657,12 +861,12 @@ __device__ int dual_pick(const SpxDev &d, Cand *shc, double *shd, int pse, int g
 }
 
 // sparse A / rigorous mode: the pick and h = -N[q] in one workgroup
-__global__ void __launch_bounds__(1024) k_dual_pick(SpxDev d, int pse, int gn)
+__global__ void __launch_bounds__(1024) k_dual_pick(SpxDev d, int pse, int gn, int ncb)
 {
     __shared__ Cand shc[16];
     __shared__ double shd[16];
     if (d.st->stop) return;
-    const int q = dual_pick(d, shc, shd, pse, gn);
+    const int q = dual_pick(d, shc, shd, pse, gn, ncb);
     if (q) build_hq(d, q);
 }
 
@@ -670,6 +874,7 @@ __global__ void __launch_bounds__(1024) k_dual_pick(SpxDev d, int pse, int gn)
 __device__ __forceinline__ double aw_value(const SpxDev &d, int c, int awsplits)
 {
     double acc = 0.0;
+#pragma unroll 8
     for (int s = 0; s < awsplits; ++s) acc += d.awpart[(size_t)s * d.m + c];
     return d.ys[c] - acc;
 }
@@ -680,7 +885,7 @@ __device__ __forceinline__ double aw_value(const SpxDev &d, int c, int awsplits)
 // AW: work from the A w partials (dense A), else from d.work.
 // ---------------------------------------------------------------------------
 template <int NRHS, int FUSED, int AW>
-__global__ void __launch_bounds__(256) k_dual_ftran(SpxDev d, int tiles, int gn, int awsplits)
+__global__ void __launch_bounds__(256) k_dual_ftran(SpxDev d, int tiles, int gn, int awsplits, int ncb)
 {
     __shared__ Cand shc[16];
     __shared__ double shd[16];
@@ -689,7 +894,7 @@ __global__ void __launch_bounds__(256) k_dual_ftran(SpxDev d, int tiles, int gn,
     const int m = d.m;
     int q;
     if (FUSED) {
-        q = dual_pick(d, shc, shd, NRHS == 2, gn);
+        q = dual_pick(d, shc, shd, NRHS == 2, gn, ncb);
         if (!q) return;
     } else
         q = st->q;
@@ -702,7 +907,7 @@ __global__ void __launch_bounds__(256) k_dual_ftran(SpxDev d, int tiles, int gn,
     const int t0 = split * lps, t1 = min(cnt, t0 + lps);
     const int r = (tile * 256 + threadIdx.x) * 2;
     const double *h = d.h, *work = d.work;
-    lgemv_tile<NRHS>(d.Binv, (size_t)d.ldb, m, d.rlist, t0, t1, r,
+    lgemv_tile_staged<NRHS>(d.Binv, (size_t)d.ldb, m, d.rlist, t0, t1, r,
                      [&](int, int c, double &xa, double &xb) {
                          if (FUSED) xa = hcol ? hcol[c] : (c == kq - 1 ? -1.0 : 0.0);
                          else xa = h[c];
@@ -915,6 +1120,7 @@ DualPlan dual_plan(const SpxDev &d, int nr_max, int nwl_max, int pse, int rigoro
     const int tiles_t = cdiv(n, 512), tiles_f = cdiv(m, 512);
     pl.tsplits = std::max(1, std::min(2048 / tiles_t, cdiv(ns_max, 8)));
     pl.tsplits = std::max(1, std::min<int>(pl.tsplits, (int)(d.partial_cap / std::max(n, 1))));
+    pl.twaves = ns_max <= 32 ? 4 : (ns_max <= 128 ? 8 : 16);
     const int nrhs = pse ? 2 : 1;
     pl.fsplits = std::max(1, std::min(2048 / tiles_f, cdiv(std::max(nr_max, 1), 8)));
     pl.fsplits = std::max(1, std::min<int>(pl.fsplits, (int)(d.partial_cap / ((size_t)nrhs * m))));
@@ -955,11 +1161,11 @@ void dual_batch_end(hipStream_t s, const SpxDev &d, const DualPlan &pl)
 }
 
 template <int NRHS, int FUSED, int AW>
-static void launch_ftran(hipStream_t s, const SpxDev &d, const DualPlan &pl, int gn)
+static void launch_ftran(hipStream_t s, const SpxDev &d, const DualPlan &pl, int gn, int ncb)
 {
     const int tiles_f = cdiv(d.m, 512);
     hipLaunchKernelGGL((k_dual_ftran<NRHS, FUSED, AW>), dim3(tiles_f * pl.fsplits), dim3(256), 0, s, d, tiles_f, gn,
-                       pl.awsplits);
+                       pl.awsplits, ncb);
     hipLaunchKernelGGL((k_dual_ftran_reduce<NRHS, FUSED, AW>), dim3(cdiv(d.m, 64)), dim3(512), 0, s, d, pl.fsplits,
                        pl.awsplits);
 }
@@ -971,13 +1177,13 @@ void dual_iteration2(hipStream_t s, const SpxDev &d, const DualPlan &pl, hipEven
     const double bf = bytes_fixed(d);
     hipLaunchKernelGGL(k_dual_top, dim3(1), dim3(WG), 0, s, d, pl.rowpath, bf);
     if (pl.rigorous) refine_rho_dev(s, d);
+    int ncb = gv, slotw = 256;
     if (pl.rowpath) {
+        ncb = cdiv(std::max(m, n), 64);
+        slotw = 64;
         if (ev0) (void)hipEventRecord(ev0, s);
-        hipLaunchKernelGGL(k_lgemv_part, dim3(cdiv(n, 512), pl.tsplits), dim3(256), 0, s, d.A.AT, (size_t)d.A.ldt, n,
-                           d.rho_idx, &d.st->ns, d.rho_val, d.partial, d.st, d.tslots);
+        hipLaunchKernelGGL(k_trow_rows, dim3(ncb), dim3(64 * pl.twaves), 0, s, d, pl.pse);
         if (ev1) (void)hipEventRecord(ev1, s);
-        hipLaunchKernelGGL(k_trow_finish<1>, dim3(gv), dim3(256), 0, s, d, d.partial, pl.tsplits, pl.pse,
-                           cdiv(n, 512) * pl.tsplits);
     } else {
         if (ev0) (void)hipEventRecord(ev0, s);
         colpass_gated(s, d.A, CP_TROW, m, n, d.head, d.stat, d.coef, nullptr, d.rho, nullptr, d.trow, nullptr,
@@ -986,20 +1192,21 @@ void dual_iteration2(hipStream_t s, const SpxDev &d, const DualPlan &pl, hipEven
         hipLaunchKernelGGL(k_trow_finish<0>, dim3(gv), dim3(256), 0, s, d, (const double *)nullptr, 0, pl.pse, 0);
     }
     const int aw = (pl.pse && d.A.dense) ? 1 : 0;
-    hipLaunchKernelGGL(k_dual_ratio, dim3(gn + (aw ? tiles_m * pl.awsplits : 0)), dim3(256), 0, s, d, gn, tiles_m, aw);
+    hipLaunchKernelGGL(k_dual_ratio, dim3(gn + (aw ? tiles_m * pl.awsplits : 0)), dim3(256), 0, s, d, gn, tiles_m,
+                       pl.rowpath, ncb, slotw);
     if (pl.fused) {
-        if (pl.pse) launch_ftran<2, 1, 1>(s, d, pl, gn);
-        else launch_ftran<1, 1, 0>(s, d, pl, gn);
+        if (pl.pse) launch_ftran<2, 1, 1>(s, d, pl, gn, ncb);
+        else launch_ftran<1, 1, 0>(s, d, pl, gn, ncb);
     } else {
-        hipLaunchKernelGGL(k_dual_pick, dim3(1), dim3(1024), 0, s, d, pl.pse, gn);
+        hipLaunchKernelGGL(k_dual_pick, dim3(1), dim3(1024), 0, s, d, pl.pse, gn, ncb);
         if (pl.pse) {
-            if (aw) launch_ftran<2, 0, 1>(s, d, pl, gn);
+            if (aw) launch_ftran<2, 0, 1>(s, d, pl, gn, ncb);
             else {
                 aprod_neg_gated(s, d.A, d.wcol, d.ys, d.work, d.partial, d.partial_cap, d.st, 0);   // work = ys - A w
-                launch_ftran<2, 0, 0>(s, d, pl, gn);
+                launch_ftran<2, 0, 0>(s, d, pl, gn, ncb);
             }
         } else
-            launch_ftran<1, 0, 0>(s, d, pl, gn);
+            launch_ftran<1, 0, 0>(s, d, pl, gn, ncb);
         if (pl.rigorous) refine_tcol_dev(s, d, 0);
     }
     const int nvb = gv;

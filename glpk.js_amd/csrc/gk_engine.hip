@@ -300,11 +300,11 @@ static void engine_alloc(Engine &E, int m, int n)
     if (!E.st_host) HIPCHK(hipHostMalloc((void **)&E.st_host, sizeof(DState), hipHostMallocDefault));
     E.rlist.ensure(m); E.rpos.ensure(m); E.rho_idx.ensure((size_t)m + 1); E.rho_val.ensure((size_t)m + 1);
     const size_t gv = (size_t)(std::max(m, n) + 255) / 256 + 1;
-    E.gpart.ensure(gv);
-    E.cand.ensure(3 * 3 * gv);                   // 3 candidate arrays of gv 24-byte entries
+    E.gpart.ensure(8 * (size_t)gv);              // gamma_p sums, then per-block max |trow| (64-slot blocks)
+    E.cand.ensure(3 * 6 * (size_t)gv);           // candidates (24-byte entries): chuzr gv | pass 1 4 gv | pass 2 gv
     E.wlist.ensure(n); E.wpos.ensure(n);
     E.awpart.ensure((size_t)AW_SPLITS * m);
-    E.tslots.ensure((size_t)((n + 511) / 512) * 2048 + 1);
+    E.tslots.ensure(std::max((size_t)((n + 511) / 512) * 2048, 4 * (size_t)gv) + 1);
 }
 
 __global__ void k_densify(const int *cptr, const int *cind, const double *cval, int n, double *A, int lda)

@@ -138,7 +138,8 @@ struct DualPlan {
     int pse, rigorous;
     int rowpath;                  // 1: pivot row by rows of AT over the support of rho
     int fused;                    // 1: dense A — h and A w read inside the FTRAN kernels
-    int tsplits;                  // row path: splits over the support of rho
+    int tsplits;                  // row path: splits over the support of rho (timing utility)
+    int twaves;                   // row path: waves per 64-column block of k_trow_rows
     int fsplits;                  // FTRAN over the dense columns of inv(B): splits
     int uchunks;                  // rank-1 update: column chunks
     int awsplits;                 // A w over wlist: splits

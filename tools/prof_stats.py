@@ -1,0 +1,46 @@
+#!/usr/bin/env python3
+"""Per-kernel statistics from a rocprofv3 results database (the default
+rocpd SQLite output of `rocprofv3 --kernel-trace --stats -d DIR -o run`).
+
+usage: prof_stats.py DB [--csv OUT] [--grid]
+Prints name, calls, total/avg/min/max ns (as rocprofv3's kernel_stats.csv),
+and with --grid the grid sizes seen per kernel."""
+import argparse
+import csv
+import sqlite3
+import statistics
+import sys
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("db")
+    ap.add_argument("--csv")
+    ap.add_argument("--grid", action="store_true")
+    a = ap.parse_args()
+    c = sqlite3.connect(a.db)
+    rows = c.execute("select name, duration, grid_x, workgroup_x from kernels").fetchall()
+    by = {}
+    for name, dur, gx, wx in rows:
+        e = by.setdefault(name, {"d": [], "grids": set()})
+        e["d"].append(dur)
+        e["grids"].add(gx // max(1, wx))
+    tot = sum(sum(e["d"]) for e in by.values())
+    out = []
+    for name, e in sorted(by.items(), key=lambda kv: -sum(kv[1]["d"])):
+        d = e["d"]
+        out.append([name, len(d), sum(d), sum(d) / len(d), 100.0 * sum(d) / tot, min(d), max(d),
+                    statistics.pstdev(d)])
+    w = csv.writer(open(a.csv, "w", newline="") if a.csv else sys.stdout, quoting=csv.QUOTE_NONNUMERIC)
+    w.writerow(["Name", "Calls", "TotalDurationNs", "AverageNs", "Percentage", "MinNs", "MaxNs", "StdDev"])
+    for r in out:
+        w.writerow(r)
+    if a.csv or a.grid:
+        for name, e in sorted(by.items(), key=lambda kv: -sum(kv[1]["d"])):
+            d = e["d"]
+            g = sorted(e["grids"])
+            print(f"{name[:70]:70s} {len(d):7d} {sum(d)/len(d)/1000:8.2f} us  blocks {g[:6]}{'...' if len(g) > 6 else ''}")
+
+
+if __name__ == "__main__":
+    main()
