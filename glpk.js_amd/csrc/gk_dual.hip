@@ -40,17 +40,43 @@ namespace gk {
 static inline int cdiv(int a, int b) { return (a + b - 1) / b; }
 __device__ __forceinline__ int gv_of(int m, int n) { return (max(m, n) + 255) / 256; }
 __device__ __forceinline__ Cand *cand_chuzr(const SpxDev &d) { return (Cand *)d.cand; }
-// per-block outputs: chuzr candidates [gv); pass-1 candidates of the pivot-row
-// blocks [4 gv) (64-slot blocks of k_trow_rows, or 256-slot blocks of
-// k_trow_finish); pass-2 candidates [gv).  gpart: gamma_p sums [4 gv), then
-// max |trow| [4 gv) of the same blocks.
-__device__ __forceinline__ Cand *cand_pass1(const SpxDev &d) { return (Cand *)d.cand + gv_of(d.m, d.n); }
-__device__ __forceinline__ Cand *cand_pass2(const SpxDev &d) { return (Cand *)d.cand + 5 * gv_of(d.m, d.n); }
-__device__ __forceinline__ double *tmax_part(const SpxDev &d) { return d.gpart + 4 * gv_of(d.m, d.n); }
 __device__ __forceinline__ Cand no_cand(double k1)
 {
     Cand c; c.k1 = k1; c.k2 = 0.0; c.idx = 0; c.aux = 0;
     return c;
+}
+
+// Per-wave outputs, 4 gv entries each, so that no producer needs a block
+// barrier and every consumer wave reduces them on its own: chuzr candidates
+// (one per wave of k_dual_commit / k_dual_prep), pass-1 candidates (one per
+// 64-slot group of the pivot row), pass-2 candidates (one per wave of
+// k_dual_ratio).  gpart: gamma_p sums of the 64-slot groups [4 gv), then
+// their max |trow| [4 gv).
+__device__ __forceinline__ Cand *cand_pass1(const SpxDev &d) { return (Cand *)d.cand + 4 * gv_of(d.m, d.n); }
+__device__ __forceinline__ Cand *cand_pass2(const SpxDev &d) { return (Cand *)d.cand + 8 * gv_of(d.m, d.n); }
+__device__ __forceinline__ double *tmax_part(const SpxDev &d) { return d.gpart + 4 * gv_of(d.m, d.n); }
+
+// the choice over cnt stored candidates, made by one wave (lane-strided scan,
+// then the butterfly): the same result in every wave that calls it
+template <int MODE>
+__device__ __forceinline__ Cand wave_scan(const Cand *a, int cnt)
+{
+    Cand c = no_cand(0.0);
+    for (int b = (int)(threadIdx.x & 63); b < cnt; b += 64) {
+        const Cand e = a[b];
+        if (better<MODE>(e, c)) c = e;
+    }
+    return wave_best<MODE>(c);
+}
+
+__device__ __forceinline__ unsigned long long wmax_u64(unsigned long long v)
+{
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        const unsigned long long u = __shfl_xor(v, o);
+        v = u > v ? u : v;
+    }
+    return v;
 }
 
 // ---------------------------------------------------------------------------
@@ -228,7 +254,8 @@ __device__ __forceinline__ double trow_big(const DState *st)
     return __longlong_as_double((long long)st->trow_max_bits);
 }
 
-__device__ __forceinline__ bool pass1_cand(const RatioCtx &x, double tr, double cb, int sj, int j, Cand &e)
+// candidates carry k2 = |trow_j| and aux = the variable number of xN[j]
+__device__ __forceinline__ bool pass1_cand(const RatioCtx &x, double tr, double cb, int sj, int j, int k, Cand &e)
 {
     if (tr == 0.0 || fabs(tr) < x.eps) return false;
     const double alfa = x.s * tr;
@@ -239,11 +266,12 @@ __device__ __forceinline__ bool pass1_cand(const RatioCtx &x, double tr, double 
         if (sj == NU || sj == NF) t = (cb - x.rtol) / alfa; else return false;
     }
     if (t < 0.0) t = 0.0;
-    e.k1 = t; e.k2 = fabs(alfa); e.idx = j + 1; e.aux = 0;
+    e.k1 = t; e.k2 = fabs(alfa); e.idx = j + 1; e.aux = k;
     return true;
 }
 
-__device__ __forceinline__ bool pass2_cand(const RatioCtx &x, double tr, double cb, int sj, int j, double tmax, Cand &e)
+__device__ __forceinline__ bool pass2_cand(const RatioCtx &x, double tr, double cb, int sj, int j, int k, double tmax,
+                                           Cand &e)
 {
     if (tr == 0.0 || fabs(tr) < x.eps) return false;
     const double alfa = x.s * tr;
@@ -255,12 +283,12 @@ __device__ __forceinline__ bool pass2_cand(const RatioCtx &x, double tr, double 
     }
     if (t < 0.0) t = 0.0;
     if (!(t <= tmax)) return false;
-    e.k1 = t; e.k2 = fabs(alfa); e.idx = j + 1; e.aux = 0;
+    e.k1 = t; e.k2 = fabs(alfa); e.idx = j + 1; e.aux = k;
     return true;
 }
 
-// pass-1 candidate of the non-basic variable(s) handled by thread slot idx
-// of k_trow_finish (structural column idx and slack row idx)
+// pass-1 candidate of the non-basic variable(s) of slot idx (structural
+// column idx and slack row idx)
 __device__ __forceinline__ Cand pass1_slot(const SpxDev &d, const RatioCtx &x, int idx)
 {
     const int m = d.m, n = d.n;
@@ -270,7 +298,7 @@ __device__ __forceinline__ Cand pass1_slot(const SpxDev &d, const RatioCtx &x, i
         if (pos > m) {
             const int j = pos - m - 1;
             Cand e;
-            if (pass1_cand(x, d.trow[j], d.cbar[j], d.stat[j], j, e) && better<1>(e, best)) best = e;
+            if (pass1_cand(x, d.trow[j], d.cbar[j], d.stat[j], j, m + idx + 1, e) && better<1>(e, best)) best = e;
         }
     }
     if (idx < m) {
@@ -278,114 +306,75 @@ __device__ __forceinline__ Cand pass1_slot(const SpxDev &d, const RatioCtx &x, i
         if (pos > m) {
             const int j = pos - m - 1;
             Cand e;
-            if (pass1_cand(x, d.trow[j], d.cbar[j], d.stat[j], j, e) && better<1>(e, best)) best = e;
+            if (pass1_cand(x, d.trow[j], d.cbar[j], d.stat[j], j, idx + 1, e) && better<1>(e, best)) best = e;
         }
     }
     return best;
 }
 
 // ---------------------------------------------------------------------------
-// change_basis (glpspx02.js:1954-1964) of the committed pivot, plus the lists
-// of dense inv(B) columns and of reference-space non-basic structurals.
-// Called by a whole block (>= 4 threads); four threads do independent parts.
+// change_basis (glpspx02.js:1954-1964) of the committed pivot: the header
+// writes and the scalar state.  k_dual_commit already maintained the lists
+// (rlist / wlist) and precomputed kp, kq and the flags, so this part does no
+// dependent loads.  Every thread computes the updated scalars (returned);
+// threads 0-2 write.
 // ---------------------------------------------------------------------------
-__device__ void dual_finish_block(const SpxDev &d, int rowpath, double bytes_fixed)
+struct TopState {
+    int iter_left, refact, refct;
+    double obj;
+};
+
+__device__ TopState dual_finish_block(const SpxDev &d, bool tail_sync)
 {
     DState *st = d.st;
+    const int m = d.m;
     const int pend = st->pend;
-    const int role = threadIdx.x;
-    const int m = d.m, n = d.n;
-    int p = 0, q = 0, kp = 0, kq = 0, nr0 = 0, nwl0 = 0, ns = 0, tkp = 0, refkp = 0, wq = -1, rq = -1;
-    if (pend && role < 4) {
-        p = st->p; q = st->q;
-        kp = d.head[p - 1];
-        kq = d.head[m + q - 1];
-        nr0 = st->nr; nwl0 = st->nwl; ns = st->ns;
-        tkp = d.type[kp - 1];
-        refkp = d.refsp[kp - 1];
-        if (kq > m) wq = d.wpos[kq - m - 1];
-        if (kq <= m) rq = d.rpos[kq - 1];
+    TopState t;
+    t.iter_left = st->iter_left - pend;
+    t.refact = st->refact_pending || (pend && st->upd_cnt + 1 >= st->upd_lim);
+    t.refct = (pend && st->pricing == PT_PSE && st->refct > 0) ? st->refct - 1 : st->refct;
+    t.obj = st->obj;
+    if (pend && st->phase == 2) t.obj += (st->cbar_q_old / st->zeta) * (st->delta / st->pivot);
+    const int p = st->p, q = st->q, kp = st->kp, kq = st->kq;
+    const int fxp = st->fxp, rclr = st->rclr, upd_cnt = st->upd_cnt, it_cnt = st->it_cnt, npiv = st->npiv;
+    const int rig = st->rigorous;
+    const double delta = st->delta;
+    __syncthreads();                          // every wave has read st before it is written
+    if (pend) {
+        if (threadIdx.x == 0) {
+            d.head[p - 1] = kq;
+            d.head[m + q - 1] = kp;
+            d.bind[kq - 1] = p;
+            d.bind[kp - 1] = m + q;
+            d.stat[q - 1] = fxp ? NS : (delta > 0.0 ? NL : NU);
+        } else if (threadIdx.x == 1) {
+            if (rclr) d.refsp[kp - 1] = 0;
+        } else if (threadIdx.x == 2) {
+            st->obj = t.obj;
+            st->upd_cnt = upd_cnt + 1;
+            st->binv_fresh = 0;
+            st->cbar_fresh = 0;
+            st->refact_pending = t.refact;
+            st->it_cnt = it_cnt + 1;
+            st->npiv = npiv + 1;
+            st->iter_left = t.iter_left;
+            if (rig > 0) st->rigorous = rig - 1;
+            st->refct = t.refct;
+            st->pend = 0;
+        }
     }
-    __syncthreads();
-    if (pend && role == 0) {
-        d.head[p - 1] = kq;
-        d.head[m + q - 1] = kp;
-        d.bind[kq - 1] = p;
-        d.bind[kp - 1] = m + q;
-        if (tkp == FX) d.stat[q - 1] = NS;
-        else if (st->delta > 0.0) d.stat[q - 1] = NL;
-        else d.stat[q - 1] = NU;
-    } else if (pend && role == 1) {
-        int nr = nr0;
-        if (kq <= m) {           // entering slack: its column is now e_p
-            const int last = d.rlist[nr - 1];
-            d.rlist[rq] = last;
-            d.rpos[last] = rq;
-            d.rpos[kq - 1] = -1;
-            nr--;
-        }
-        if (kp <= m) {           // leaving slack: its column became dense
-            d.rlist[nr] = kp - 1;
-            d.rpos[kp - 1] = nr;
-            nr++;
-        }
-        st->nr = nr;
-    } else if (pend && role == 2 && st->pricing == PT_PSE) {
-        if (tkp == FX && refkp) {
-            d.refsp[kp - 1] = 0;
-            refkp = 0;
-        }
-        int nwl = nwl0;
-        if (wq >= 0) {
-            const int last = d.wlist[nwl - 1];
-            d.wlist[wq] = last;
-            d.wpos[last] = wq;
-            d.wpos[kq - m - 1] = -1;
-            nwl--;
-        }
-        if (kp > m && refkp) {
-            d.wlist[nwl] = kp - m - 1;
-            d.wpos[kp - m - 1] = nwl;
-            nwl++;
-        }
-        st->nwl = nwl;
-        if (st->refct > 0) st->refct--;
-    } else if (pend && role == 3) {
-        if (st->phase == 2) st->obj += (st->cbar_q_old / st->zeta) * (st->delta / st->pivot);
-        st->upd_cnt++;
-        st->binv_fresh = 0;
-        st->cbar_fresh = 0;
-        if (st->upd_cnt >= st->upd_lim) st->refact_pending = 1;
-        st->it_cnt++;
-        st->npiv++;
-        st->iter_left--;
-        if (st->rigorous > 0) st->rigorous--;
-        st->pend = 0;
-        // algorithmic HBM bytes of this pivot: the pivot row (rows of A in the
-        // support of rho, or all of A), A w over the reference-space columns,
-        // inv(B) once for both right-hand sides, read + write of the updated
-        // columns, and the O(m + n) vectors
-        const double rowb = rowpath ? 8.0 * (double)ns * n : 8.0 * (double)m * n;
-        if (rowpath && st->tk_end > st->tk_start) {
-            st->bytes_trow += rowb;
-            st->trow_ticks += (double)(st->tk_end - st->tk_start);
-            st->trow_ticks_b += (double)(st->tk_next - st->tk_start);
-            st->trow_n += 1.0;
-        }
-        st->tk_end = 0;
-        st->bytes += rowb + 8.0 * (double)m * nwl0 + 8.0 * (double)m * (nr0 + 1) +
-                     16.0 * (double)m * (nr0 + (kp <= m ? 1 : 0)) + bytes_fixed;
-    }
-    __syncthreads();
+    if (tail_sync) __syncthreads();
+    return t;
 }
 
-__global__ void k_dual_finish(SpxDev d, int rowpath, double bytes_fixed)
+__global__ void k_dual_finish(SpxDev d)
 {
-    dual_finish_block(d, rowpath, bytes_fixed);
+    (void)dual_finish_block(d, true);
 }
 
-// chuzr candidate of basic position i (glpspx02.js:572-626)
-__device__ __forceinline__ Cand chuzr_cand_v(int i, int t, double lb, double ub, double bb, double g, double tol_bnd)
+// chuzr candidate of basic position i holding variable k (glpspx02.js:572-626)
+__device__ __forceinline__ Cand chuzr_cand_v(int i, int k, int t, double lb, double ub, double bb, double g,
+                                             double tol_bnd)
 {
     double ri = 0.0;
     if (t == LO || t == DB || t == FX) {
@@ -400,7 +389,7 @@ __device__ __forceinline__ Cand chuzr_cand_v(int i, int t, double lb, double ub,
     if (ri == 0.0) return e;
     if (g < DBL_EPS) g = DBL_EPS;
     const double temp = (ri * ri) / g;
-    if (temp > 0.0) { e.k1 = temp; e.k2 = ri; e.idx = i + 1; }
+    if (temp > 0.0) { e.k1 = temp; e.k2 = ri; e.idx = i + 1; e.aux = k; }
     return e;
 }
 
@@ -416,7 +405,6 @@ __device__ __forceinline__ int dual_bad(const SpxDev &d, int k, double cb, doubl
 // batch start: chuzr candidates and the phase-I check of the current state
 __global__ void __launch_bounds__(256) k_dual_prep(SpxDev d)
 {
-    __shared__ Cand shc[16];
     DState *st = d.st;
     const int m = d.m, n = d.n;
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -425,11 +413,11 @@ __global__ void __launch_bounds__(256) k_dual_prep(SpxDev d)
         Cand c = no_cand(0.0);
         if (i < m) {
             const int k = d.head[i];
-            c = chuzr_cand_v(i, d.type[k - 1], d.lb[k - 1], d.ub[k - 1], d.bbar[i], reset ? 1.0 : d.gamma[i],
+            c = chuzr_cand_v(i, k, d.type[k - 1], d.lb[k - 1], d.ub[k - 1], d.bbar[i], reset ? 1.0 : d.gamma[i],
                              st->tol_bnd);
         }
-        const Cand b = block_best<0>(c, shc);
-        if (threadIdx.x == 0) cand_chuzr(d)[blockIdx.x] = b;
+        const Cand b = wave_best<0>(c);
+        if ((threadIdx.x & 63) == 0) cand_chuzr(d)[blockIdx.x * 4 + (threadIdx.x >> 6)] = b;
     }
     if (st->phase == 1) {
         const int bad = (i < n) ? dual_bad(d, d.head[m + i], d.cbar[i], st->tol_dj) : 0;
@@ -438,29 +426,40 @@ __global__ void __launch_bounds__(256) k_dual_prep(SpxDev d)
 }
 
 // ---------------------------------------------------------------------------
-// k_dual_top
+// k_dual_top (1 WG of 256): change_basis of the previous pivot, stop checks,
+// chuzr, rho = row p of inv(B) in compact form.  The chuzr candidates (with
+// the leaving variable in aux) and the dense-column list are loaded at entry
+// (the list speculatively up to nr_cap); every wave makes the chuzr choice on
+// its own, so the only block barrier is the one inside change_basis and the
+// only dependent load is inv(B)[p, :].
 // ---------------------------------------------------------------------------
-__global__ void __launch_bounds__(WG) k_dual_top(SpxDev d, int rowpath, double bytes_fixed)
+constexpr int TOP_WG = 256;
+
+__global__ void __launch_bounds__(TOP_WG) k_dual_top(SpxDev d, int rowpath, int nr_cap)
 {
-    __shared__ Cand shc[16];
     DState *st = d.st;
     if (st->stop) return;
     const int m = d.m, n = d.n;
-    // the next pivot's chuzr candidates are already final: load them while
-    // the previous pivot's change_basis is applied
-    const int gm = (m + 255) / 256;
+    const int gm = 4 * ((m + 255) / 256);
     Cand c = no_cand(0.0);
-    for (int b = threadIdx.x; b < gm; b += blockDim.x) {
+    for (int b = (int)(threadIdx.x & 63); b < gm; b += 64) {
         const Cand e = cand_chuzr(d)[b];
         if (better<0>(e, c)) c = e;
     }
-    dual_finish_block(d, rowpath, bytes_fixed);
-    if (st->iter_left <= 0 || st->refact_pending) {
-        __syncthreads();
-        if (threadIdx.x == 0) st->stop = st->refact_pending ? ST_REFACT : ST_BATCH;
+    constexpr int RPT = 16;                   // list entries prefetched per thread
+    int cl[RPT];
+#pragma unroll
+    for (int u = 0; u < RPT; ++u) {
+        const int t = threadIdx.x + u * TOP_WG;
+        cl[u] = (t < nr_cap) ? d.rlist[t] : 0;
+    }
+    const TopState ts = dual_finish_block(d, false);
+    if (ts.iter_left <= 0 || ts.refact) {
+        if (threadIdx.x == 0) st->stop = ts.refact ? ST_REFACT : ST_BATCH;
         return;
     }
-    if (st->pricing == PT_PSE && st->refct == 0) {
+    if (st->pricing == PT_PSE && ts.refct == 0) {
+        __syncthreads();                   // the header writes of change_basis are visible
         reset_refsp_dev(d, 1);             // refsp := basic variables, gamma := 1
         for (int l = threadIdx.x; l < n; l += blockDim.x) d.wpos[l] = -1;
         if (threadIdx.x == 0) st->nwl = 0;
@@ -468,43 +467,56 @@ __global__ void __launch_bounds__(WG) k_dual_top(SpxDev d, int rowpath, double b
     }
     if (st->phase == 1) {
         if (!st->dinf) {
-            __syncthreads();
             if (threadIdx.x == 0) st->stop = ST_PHASE;
             return;
         }
     } else {
         // objective limits (:1729-1760)
-        const double z = st->zeta, obj = st->obj;
+        const double z = st->zeta, obj = ts.obj;
         const bool hit = (z < 0.0 && st->obj_ll > -DBL_MAX && obj <= st->obj_ll) ||
                          (z > 0.0 && st->obj_ul < +DBL_MAX && obj >= st->obj_ul);
         if (hit) {
-            __syncthreads();
             if (threadIdx.x == 0) st->stop = ST_OBJLIM;
             return;
         }
     }
-    // chuzr from the per-block candidates
-    const Cand best = block_best<0>(c, shc);
+    // chuzr from the per-wave candidates (the same choice in every wave)
+    const Cand best = wave_best<0>(c);
     if (best.idx == 0) {
         if (threadIdx.x == 0) { st->p = 0; st->stop = ST_P0; }
         return;
     }
-    const int p = best.idx;
-    // rho in compact form; the dense copy only for the column pass
+    const int p = best.idx, kp = best.aux;
     if (!rowpath) {
         for (int l = threadIdx.x; l < m; l += blockDim.x) d.rho[l] = 0.0;
         __syncthreads();
     }
     const int nr = st->nr;
-    for (int t = threadIdx.x; t < nr; t += blockDim.x) {
+    const double *brow = d.Binv + (p - 1);
+    const size_t ldb = (size_t)d.ldb;
+    double v[RPT];
+#pragma unroll
+    for (int u = 0; u < RPT; ++u) {
+        const int t = threadIdx.x + u * TOP_WG;
+        v[u] = (t < nr) ? brow[(size_t)cl[u] * ldb] : 0.0;
+    }
+#pragma unroll
+    for (int u = 0; u < RPT; ++u) {
+        const int t = threadIdx.x + u * TOP_WG;
+        if (t < nr) {
+            if (!rowpath) d.rho[cl[u]] = v[u];
+            d.rho_idx[t] = cl[u];
+            d.rho_val[t] = v[u];
+        }
+    }
+    for (int t = threadIdx.x + RPT * TOP_WG; t < nr; t += blockDim.x) {   // nr > 4096 only
         const int cc = d.rlist[t];
-        const double v = d.Binv[(size_t)(p - 1) + (size_t)cc * d.ldb];
-        if (!rowpath) d.rho[cc] = v;
+        const double vv = brow[(size_t)cc * ldb];
+        if (!rowpath) d.rho[cc] = vv;
         d.rho_idx[t] = cc;
-        d.rho_val[t] = v;
+        d.rho_val[t] = vv;
     }
     if (threadIdx.x == 0) {
-        const int kp = d.head[p - 1];
         int ns = nr;
         if (kp <= m) {   // the basic slack at position p: unit column of inv(B)
             if (!rowpath) d.rho[kp - 1] = 1.0;
@@ -513,6 +525,7 @@ __global__ void __launch_bounds__(WG) k_dual_top(SpxDev d, int rowpath, double b
             ns++;
         }
         st->p = p;
+        st->kp = kp;
         st->delta = best.k2;
         st->trow_max_bits = 0ull;
         st->ns = ns;
@@ -521,41 +534,20 @@ __global__ void __launch_bounds__(WG) k_dual_top(SpxDev d, int rowpath, double b
 }
 
 // ---------------------------------------------------------------------------
-// k_trow_finish: structural column c / slack row c of the pivot row.
-// FROM_PART: trow from the row-path partials (structurals) and -rho (slacks);
-// else trow was written by the column pass.  Also the PSE vectors of
-// update_gamma (:1103-1134): wcol[c] / ys[c] = trow of a non-basic variable of
-// the reference space, per-block sums of those trow^2 (gamma_p), and the
-// block's Harris pass-1 candidate under the block-local significance
-// tolerance (k_dual_ratio re-checks it against the global one).
+// k_trow_finish (column-pass path: sparse A, or rho too dense for the row
+// path): structural column c / slack row c of the pivot row computed by the
+// column pass; the PSE vectors of update_gamma (:1103-1134), per-block sums
+// of those trow^2 (gamma_p), and the block's Harris pass-1 candidate under the
+// block-local significance tolerance (k_dual_ratio re-checks it).
 // ---------------------------------------------------------------------------
-template <int FROM_PART>
-__global__ void __launch_bounds__(256) k_trow_finish(SpxDev d, const double *__restrict__ part, int splits, int pse,
-                                                       int nslots)
+__global__ void __launch_bounds__(256) k_trow_finish(SpxDev d, int pse)
 {
-    __shared__ double shd[16];
-    __shared__ Cand shc[16];
     DState *st = d.st;
     if (st->stop) return;
     const int m = d.m, n = d.n;
     const int idx = blockIdx.x * blockDim.x + threadIdx.x;
-    if (FROM_PART && blockIdx.x == 0) {
-        // end of the pivot-row kernel: latest block stamp (one block, plain
-        // store: same-address atomics from every block serialise)
-        if (threadIdx.x == 0) st->tk_next = wall_clock64();
-        unsigned long long e = 0;
-        for (int t = threadIdx.x; t < nslots; t += blockDim.x) e = max(e, d.tslots[t]);
-        __shared__ unsigned long long she;
-        if (threadIdx.x == 0) she = 0;
-        __syncthreads();
-        if (e) atomicMax(&she, e);
-        __syncthreads();
-        if (threadIdx.x == 0 && she) st->tk_end = she;
-    }
-    // all gathers first (bind -> stat/cbar/refsp/partials), reductions after
     const int pos1 = (idx < n) ? d.bind[m + idx] : 0;
     const int pos2 = (idx < m) ? d.bind[idx] : 0;
-    const int rp2 = (FROM_PART && idx < m) ? d.rpos[idx] : -1;   // a non-basic slack is a dense column of inv(B)
     const int j1 = (pos1 > m) ? pos1 - m - 1 : -1;
     const int j2 = (pos2 > m) ? pos2 - m - 1 : -1;
     int s1 = 0, s2 = 0;
@@ -564,26 +556,14 @@ __global__ void __launch_bounds__(256) k_trow_finish(SpxDev d, const double *__r
     if (j1 >= 0) {
         s1 = d.stat[j1];
         cb1 = d.cbar[j1];
-        if (FROM_PART) {
-            double acc = 0.0;
-#pragma unroll 8
-            for (int s = 0; s < splits; ++s) acc += part[(size_t)s * n + idx];
-            tv1 = acc;
-        } else
-            tv1 = d.trow[j1];
+        tv1 = d.trow[j1];
         if (pse) ref1 = d.refsp[m + idx] != 0;
     }
     if (j2 >= 0) {
         s2 = d.stat[j2];
         cb2 = d.cbar[j2];
-        tv2 = FROM_PART ? -d.rho_val[rp2] : d.trow[j2];
+        tv2 = d.trow[j2];
         if (pse) ref2 = d.refsp[idx] != 0;
-    }
-    if (FROM_PART) {
-        if (s1 == NS) tv1 = 0.0;
-        if (s2 == NS) tv2 = 0.0;
-        if (j1 >= 0) d.trow[j1] = tv1;
-        if (j2 >= 0) d.trow[j2] = tv2;
     }
     double gsum = 0.0;
     if (pse) {
@@ -592,21 +572,22 @@ __global__ void __launch_bounds__(256) k_trow_finish(SpxDev d, const double *__r
         if (idx < m) d.ys[idx] = w2;
         gsum = w1 * w1 + w2 * w2;
     }
-    const double bmax = block_max(fmax(fabs(tv1), fabs(tv2)), shd);
-    // per-block max |trow|; k_dual_ratio reduces them into st->trow_max_bits
-    if (FROM_PART && threadIdx.x == 0) tmax_part(d)[blockIdx.x] = bmax;
-    if (pse) {
-        const double g = block_sum(gsum, shd);
-        if (threadIdx.x == 0) d.gpart[blockIdx.x] = g;
-    }
-    // pass-1 candidate with eps_b = tol_bnd (1 + 0.01 max_b) <= eps
+    // per 64-slot group (one wave): max |trow|, gamma_p partial, pass-1
+    // candidate with eps_g = tol_bnd (1 + 0.01 max_g) <= eps
+    const int grp = blockIdx.x * 4 + (threadIdx.x >> 6);
+    const double bmax = wmax(fmax(fabs(tv1), fabs(tv2)));
+    const double g = pse ? wsum(gsum) : 0.0;
     const RatioCtx x = ratio_ctx(st, bmax);
     Cand c = no_cand(DBL_MAX);
     Cand e;
-    if (j1 >= 0 && pass1_cand(x, tv1, cb1, s1, j1, e) && better<1>(e, c)) c = e;
-    if (j2 >= 0 && pass1_cand(x, tv2, cb2, s2, j2, e) && better<1>(e, c)) c = e;
-    const Cand b = block_best<1>(c, shc);
-    if (threadIdx.x == 0) cand_pass1(d)[blockIdx.x] = b;
+    if (j1 >= 0 && pass1_cand(x, tv1, cb1, s1, j1, m + idx + 1, e) && better<1>(e, c)) c = e;
+    if (j2 >= 0 && pass1_cand(x, tv2, cb2, s2, j2, idx + 1, e) && better<1>(e, c)) c = e;
+    const Cand b = wave_best<1>(c);
+    if ((threadIdx.x & 63) == 0) {
+        if (pse) d.gpart[grp] = g;
+        tmax_part(d)[grp] = bmax;
+        cand_pass1(d)[grp] = b;
+    }
 }
 
 // ---------------------------------------------------------------------------
@@ -614,9 +595,10 @@ __global__ void __launch_bounds__(256) k_trow_finish(SpxDev d, const double *__r
 // k_trow_finish in one kernel.  Block b owns the 64 slots [64 b, 64 b + 64)
 // (structural column c and slack row c of each slot).  Its waves split the
 // support of rho (rows t = w, w + nw, ... of AT, 512-byte coalesced segments
-// of the 64 columns), the partial sums meet in LDS in wave order, and wave 0
-// finishes the slots with wave-level reductions: trow, the PSE vectors, the
-// gamma_p partial, max |trow| and the Harris pass-1 candidate of the block.
+// of the 64 columns; the first group of rho entries is loaded before ns is
+// known), the partial sums meet in LDS in wave order, and wave 0 finishes the
+// slots with wave-level reductions: trow, the PSE vectors, the gamma_p
+// partial, max |trow| and the Harris pass-1 candidate of the block.
 // Block 0 stamps the device clock at entry and every block at exit (tslots).
 // ---------------------------------------------------------------------------
 __global__ void __launch_bounds__(1024) k_trow_rows(SpxDev d, int pse)
@@ -637,17 +619,32 @@ __global__ void __launch_bounds__(1024) k_trow_rows(SpxDev d, int pse)
         pos2 = (idx < m) ? d.bind[idx] : 0;
         rp2 = (idx < m) ? d.rpos[idx] : -1;
     }
+    const int *__restrict__ ri = d.rho_idx;
+    const double *__restrict__ rv = d.rho_val;
+    // first group of rho entries, inside the allocation (m + 1 entries)
+    int r0[8];
+    double v0[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+        const int t = w + u * nw;
+        r0[u] = (t <= m) ? ri[t] : 0;
+        v0[u] = (t <= m) ? rv[t] : 0.0;
+    }
     const int ns = st->ns;
     double acc = 0.0;
     if (idx < n) {
         const double *__restrict__ col = d.A.AT + idx;
         const size_t ldt = (size_t)d.A.ldt;
-        const int *__restrict__ ri = d.rho_idx;
-        const double *__restrict__ rv = d.rho_val;
-        int t = w;
+        double a[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) a[u] = (w + u * nw < ns) ? col[(size_t)r0[u] * ldt] : 0.0;
+#pragma unroll
+        for (int u = 0; u < 8; ++u)
+            if (w + u * nw < ns) acc += v0[u] * a[u];
+        int t = w + 8 * nw;
         for (; t + 7 * nw < ns; t += 8 * nw) {
             int r[8];
-            double v[8], a[8];
+            double v[8];
 #pragma unroll
             for (int u = 0; u < 8; ++u) {
                 r[u] = ri[t + u * nw];
@@ -699,8 +696,8 @@ __global__ void __launch_bounds__(1024) k_trow_rows(SpxDev d, int pse)
     const RatioCtx x = ratio_ctx(st, bmax);
     Cand c = no_cand(DBL_MAX);
     Cand e;
-    if (j1 >= 0 && pass1_cand(x, tv1, cb1, s1, j1, e) && better<1>(e, c)) c = e;
-    if (j2 >= 0 && pass1_cand(x, tv2, cb2, s2, j2, e) && better<1>(e, c)) c = e;
+    if (j1 >= 0 && pass1_cand(x, tv1, cb1, s1, j1, m + idx + 1, e) && better<1>(e, c)) c = e;
+    if (j2 >= 0 && pass1_cand(x, tv2, cb2, s2, j2, idx + 1, e) && better<1>(e, c)) c = e;
     const Cand b = wave_best<1>(c);
     if (lane == 0) {
         tmax_part(d)[blockIdx.x] = bmax;
@@ -711,15 +708,14 @@ __global__ void __launch_bounds__(1024) k_trow_rows(SpxDev d, int pse)
 }
 
 // ---------------------------------------------------------------------------
-// k_dual_ratio: blocks [0, gn) — pass-1 choice from the block candidates
-// (a block whose candidate fails the global significance tolerance is
-// rescanned), then the pass-2 candidates of positions [256 b, 256 b + 256);
-// blocks [gn, ...) — partials of A w over the reference-space columns.
+// k_dual_ratio: blocks [0, gn) — pass-1 choice from the ncb group candidates
+// (a group whose candidate fails the global significance tolerance is
+// rescanned), then the pass-2 candidates of positions [256 b, 256 b + 256),
+// one per wave; blocks [gn, ...) — partials of A w over the reference-space
+// columns.  Every wave makes the pass-1 choice on its own (no block barrier).
 // ---------------------------------------------------------------------------
-__global__ void __launch_bounds__(256) k_dual_ratio(SpxDev d, int gn, int tiles_m, int rowpath, int ncb, int slotw)
+__global__ void __launch_bounds__(256) k_dual_ratio(SpxDev d, int gn, int tiles_m, int rowpath, int ncb)
 {
-    __shared__ Cand shc[16];
-    __shared__ double shd[16];
     DState *st = d.st;
     if (st->stop) return;
     const int m = d.m, n = d.n;
@@ -734,59 +730,85 @@ __global__ void __launch_bounds__(256) k_dual_ratio(SpxDev d, int gn, int tiles_
         lgemv_tile<1>(d.A.A, (size_t)d.A.lda, m, d.wlist, t0, t1, r,
                       [&](int, int c, double &xa, double &xb) { xa = wc[c]; xb = 0.0; },
                       d.awpart + (size_t)split * m);
+        // the last split to arrive at this tile forms work = ys - A w for its
+        // rows, summing the partials in split order (deterministic)
+        __shared__ int last;
+        __threadfence();
+        __syncthreads();
+        if (threadIdx.x == 0) last = (atomicAdd(&d.awcnt[tile], 1) == splits - 1);
+        __syncthreads();
+        if (!last) return;
+        __threadfence();
+        for (int rr = r; rr < min(r + 2, m); ++rr) {
+            double acc = 0.0;
+            for (int sp = 0; sp < splits; ++sp) acc += d.awpart[(size_t)sp * m + rr];
+            d.work[rr] = d.ys[rr] - acc;
+        }
+        if (threadIdx.x == 0) d.awcnt[tile] = 0;
         return;
     }
-    double big;
-    if (rowpath) {
-        // max |trow| from the pivot-row blocks; block 0 publishes it and the
-        // end of the pivot-row kernel (latest block exit stamp)
-        double v = 0.0;
-        unsigned long long e = 0;
-        for (int b = threadIdx.x; b < ncb; b += blockDim.x) {
-            v = fmax(v, tmax_part(d)[b]);
-            if (blockIdx.x == 0) e = max(e, d.tslots[b]);
-        }
-        big = block_max(v, shd);
-        if (blockIdx.x == 0) {
-            __shared__ unsigned long long she;
-            if (threadIdx.x == 0) {
-                she = 0;
-                st->tk_next = wall_clock64();
-            }
-            __syncthreads();
-            if (e) atomicMax(&she, e);
-            __syncthreads();
-            if (threadIdx.x == 0) {
-                st->trow_max_bits = dbits(big);
-                st->tk_end = she;
-            }
-        }
-    } else
-        big = trow_big(st);
-    const RatioCtx x = ratio_ctx(st, big);
+    const int lane = threadIdx.x & 63;
+    const unsigned long long t_entry = (rowpath && blockIdx.x == 0 && threadIdx.x == 0) ? wall_clock64() : 0ull;
     const int j = blockIdx.x * blockDim.x + threadIdx.x;
     const double trj = (j < n) ? d.trow[j] : 0.0;
     const double cbj = (j < n) ? d.cbar[j] : 0.0;
     const int sj = (j < n) ? d.stat[j] : 0;
-    Cand c = no_cand(DBL_MAX);
-    int fail = 0;
-    for (int b = threadIdx.x; b < ncb; b += blockDim.x) {
-        const Cand e = cand_pass1(d)[b];
-        if (e.idx != 0 && e.k2 < x.eps) fail = 1;
-        else if (better<1>(e, c)) c = e;
+    const int kj = (j < n) ? d.head[m + j] : 0;
+    const bool lead = (blockIdx.x == 0 && threadIdx.x < 64);
+    constexpr int CPL = 8;                    // group candidates per lane held in registers
+    Cand cl[CPL];
+    double v = 0.0;
+    unsigned long long e = 0;
+#pragma unroll
+    for (int u = 0; u < CPL; ++u) {
+        const int b = lane + u * 64;
+        cl[u] = (b < ncb) ? cand_pass1(d)[b] : no_cand(DBL_MAX);
+        if (b < ncb) {
+            v = fmax(v, tmax_part(d)[b]);
+            if (rowpath && lead) e = max(e, d.tslots[b]);
+        }
     }
-    if (__syncthreads_or(fail)) {
-        // rare: rescan the blocks whose candidate is not significant
-        for (int b = 0; b < ncb; ++b) {
-            const Cand e = cand_pass1(d)[b];
-            if (!(e.idx != 0 && e.k2 < x.eps)) continue;
-            if ((int)threadIdx.x < slotw) {
-                const Cand f = pass1_slot(d, x, b * slotw + threadIdx.x);
-                if (better<1>(f, c)) c = f;
+    for (int b = lane + CPL * 64; b < ncb; b += 64) {
+        v = fmax(v, tmax_part(d)[b]);
+        if (rowpath && lead) e = max(e, d.tslots[b]);
+    }
+    const double big = wmax(v);
+    if (lead) {
+        // publish max |trow| and the end of the pivot-row kernel (latest
+        // block exit stamp)
+        const unsigned long long ee = wmax_u64(e);
+        if (lane == 0) {
+            st->trow_max_bits = dbits(big);
+            if (rowpath) {
+                st->tk_next = t_entry;
+                st->tk_end = ee;
             }
         }
     }
-    const Cand b1 = block_best<1>(c, shc);
+    const RatioCtx x = ratio_ctx(st, big);
+    Cand c = no_cand(DBL_MAX);
+    int fail = 0;
+#pragma unroll
+    for (int u = 0; u < CPL; ++u) {
+        if (cl[u].idx != 0 && cl[u].k2 < x.eps) fail = 1;
+        else if (better<1>(cl[u], c)) c = cl[u];
+    }
+    for (int b = lane + CPL * 64; b < ncb; b += 64) {
+        const Cand f = cand_pass1(d)[b];
+        if (f.idx != 0 && f.k2 < x.eps) fail = 1;
+        else if (better<1>(f, c)) c = f;
+    }
+    if (__any(fail)) {
+        // rare: rescan the groups whose candidate is not significant (lane =
+        // slot of the 64-slot group)
+        for (int b = 0; b < ncb; ++b) {
+            const Cand f = cand_pass1(d)[b];
+            if (!(f.idx != 0 && f.k2 < x.eps)) continue;
+            const Cand g = pass1_slot(d, x, b * 64 + lane);
+            if (better<1>(g, c)) c = g;
+        }
+    }
+    const Cand b1 = wave_best<1>(c);
     const int q1 = b1.idx;
     const double teta1 = q1 ? b1.k1 : DBL_MAX;
     const int need2 = !(x.rtol == 0.0 || q1 == 0 || teta1 == 0.0);
@@ -794,79 +816,85 @@ __global__ void __launch_bounds__(256) k_dual_ratio(SpxDev d, int gn, int tiles_
         st->q1 = q1;
         st->teta1 = teta1;
         st->need2 = need2;
+        st->kq1 = b1.aux;
+        st->alfa1 = b1.k2;
     }
     if (!need2) return;
     Cand c2 = no_cand(0.0);
     if (j < n) {
-        Cand e;
-        if (pass2_cand(x, trj, cbj, sj, j, teta1, e)) c2 = e;
+        Cand f;
+        if (pass2_cand(x, trj, cbj, sj, j, kj, teta1, f)) c2 = f;
     }
-    const Cand b2 = block_best<2>(c2, shc);
-    if (threadIdx.x == 0) cand_pass2(d)[blockIdx.x] = b2;
+    const Cand b2 = wave_best<2>(c2);
+    if (lane == 0) cand_pass2(d)[blockIdx.x * 4 + (threadIdx.x >> 6)] = b2;
 }
 
 // the entering choice q (pass 2 if needed), its checks and the st fields;
-// every block of the calling grid evaluates it identically.  Returns q, or 0
-// when the iteration stops.
-__device__ int dual_pick(const SpxDev &d, Cand *shc, double *shd, int pse, int gn, int ncb)
+// every wave of the calling grid evaluates it identically (no block
+// barrier).  Returns q (kq through *kq_out), or 0 when the iteration stops.
+// The candidates carry |trow_q| (k2) and the entering variable (aux).
+__device__ int dual_pick(const SpxDev &d, int pse, int gn, int ncb, int *kq_out)
 {
     DState *st = d.st;
-    int q;
-    double teta;
-    if (st->need2) {
-        Cand c = no_cand(0.0);
-        for (int b = threadIdx.x; b < gn; b += blockDim.x) {
-            const Cand e = cand_pass2(d)[b];
-            if (better<2>(e, c)) c = e;
-        }
-        const Cand b2 = block_best<2>(c, shc);
+    const int lane = threadIdx.x & 63;
+    const bool lead = (blockIdx.x == 0 && blockIdx.y == 0);
+    const int need2 = st->need2;
+    Cand c = no_cand(0.0);
+    for (int b = lane; b < 4 * gn; b += 64) {
+        const Cand e = cand_pass2(d)[b];
+        if (better<2>(e, c)) c = e;
+    }
+    // gamma_p (update_gamma :1103-1132) from the group sums, fixed order
+    double g = 0.0;
+    if (lead && pse && threadIdx.x < 64)
+        for (int b = lane; b < ncb; b += 64) g += d.gpart[b];
+    const double big = trow_big(st);
+    int q, kq;
+    double teta, alfa;
+    if (need2) {
+        const Cand b2 = wave_best<2>(c);
         q = b2.idx;
         teta = b2.k1;
+        kq = b2.aux;
+        alfa = b2.k2;
     } else {
         q = st->q1;
         teta = st->teta1;
+        kq = st->kq1;
+        alfa = st->alfa1;
     }
-    const bool lead = (blockIdx.x == 0 && blockIdx.y == 0);
     if (q == 0) {
-        __syncthreads();
         if (lead && threadIdx.x == 0) { st->q = 0; st->stop = ST_Q0; }
         return 0;
     }
-    const double big = trow_big(st);
-    const double piv = d.trow[q - 1];
-    if (fabs(piv) < 1e-5 * (1.0 + 0.01 * big) && !st->rigorous) {
-        __syncthreads();
+    if (alfa < 1e-5 * (1.0 + 0.01 * big) && !st->rigorous) {
         if (lead && threadIdx.x == 0) { st->q = q; st->stop = ST_SMALLPIV; }
         return 0;
     }
-    if (lead) {
-        if (pse) {
-            // gamma_p (update_gamma :1103-1132) from the per-block sums, fixed order
-            double g = 0.0;
-            for (int b = threadIdx.x; b < ncb; b += blockDim.x) g += d.gpart[b];
-            g = block_sum(g, shd);
-            if (threadIdx.x == 0) {
-                const double eta = d.refsp[d.head[st->p - 1] - 1] ? 1.0 : 0.0;
+    if (lead && threadIdx.x < 64) {
+        if (pse) g = wsum(g);
+        if (threadIdx.x == 0) {
+            if (pse) {
+                const double eta = d.refsp[st->kp - 1] ? 1.0 : 0.0;
                 st->eta_pq = eta;
                 st->gamma_pq = eta + g;
             }
-        }
-        if (threadIdx.x == 0) {
             st->q = q;
+            st->kq = kq;
             st->new_dq = (st->delta > 0.0 ? +1.0 : -1.0) * teta;
             st->cbar_q_old = d.cbar[q - 1];
         }
     }
+    *kq_out = kq;
     return q;
 }
 
 // sparse A / rigorous mode: the pick and h = -N[q] in one workgroup
 __global__ void __launch_bounds__(1024) k_dual_pick(SpxDev d, int pse, int gn, int ncb)
 {
-    __shared__ Cand shc[16];
-    __shared__ double shd[16];
     if (d.st->stop) return;
-    const int q = dual_pick(d, shc, shd, pse, gn, ncb);
+    int kq = 0;
+    const int q = dual_pick(d, pse, gn, ncb, &kq);
     if (q) build_hq(d, q);
 }
 
@@ -880,25 +908,25 @@ __device__ __forceinline__ double aw_value(const SpxDev &d, int c, int awsplits)
 }
 
 // ---------------------------------------------------------------------------
-// k_dual_ftran: tcol = inv(B) h, u = inv(B) work over the dense columns.
+// k_dual_ftran (split path, many dense columns): tcol = inv(B) h,
+// u = inv(B) work over the dense columns, partials over fsplits list chunks.
 // FUSED (dense A): the pick runs here and h_c = A[c, q] is read from A.
 // AW: work from the A w partials (dense A), else from d.work.
 // ---------------------------------------------------------------------------
 template <int NRHS, int FUSED, int AW>
 __global__ void __launch_bounds__(256) k_dual_ftran(SpxDev d, int tiles, int gn, int awsplits, int ncb)
 {
-    __shared__ Cand shc[16];
-    __shared__ double shd[16];
     DState *st = d.st;
     if (st->stop) return;
     const int m = d.m;
-    int q;
+    int q, kq = 0;
     if (FUSED) {
-        q = dual_pick(d, shc, shd, NRHS == 2, gn, ncb);
+        q = dual_pick(d, NRHS == 2, gn, ncb, &kq);
         if (!q) return;
-    } else
+    } else {
         q = st->q;
-    const int kq = d.head[m + q - 1];
+        kq = d.head[m + q - 1];
+    }
     const double *hcol = (kq > m) ? d.A.A + (size_t)(kq - m - 1) * d.A.lda : nullptr;
     const int b = blockIdx.x;
     const int tile = b % tiles, split = b / tiles, splits = gridDim.x / tiles;
@@ -908,13 +936,13 @@ __global__ void __launch_bounds__(256) k_dual_ftran(SpxDev d, int tiles, int gn,
     const int r = (tile * 256 + threadIdx.x) * 2;
     const double *h = d.h, *work = d.work;
     lgemv_tile_staged<NRHS>(d.Binv, (size_t)d.ldb, m, d.rlist, t0, t1, r,
-                     [&](int, int c, double &xa, double &xb) {
-                         if (FUSED) xa = hcol ? hcol[c] : (c == kq - 1 ? -1.0 : 0.0);
-                         else xa = h[c];
-                         if (NRHS == 2) xb = AW ? aw_value(d, c, awsplits) : work[c];
-                         else xb = 0.0;
-                     },
-                     d.partial + (size_t)split * NRHS * m);
+                            [&](int, int c, double &xa, double &xb) {
+                                if (FUSED) xa = hcol ? hcol[c] : (c == kq - 1 ? -1.0 : 0.0);
+                                else xa = h[c];
+                                if (NRHS == 2) xb = work[c];   // AW: formed by k_dual_ratio
+                                else xb = 0.0;
+                            },
+                            d.partial + (size_t)split * NRHS * m);
 }
 
 // tcol[i] / u[i] = sum of the partials + the unit column of a basic slack
@@ -951,14 +979,115 @@ __global__ void __launch_bounds__(512) k_dual_ftran_reduce(SpxDev d, int splits,
     if (kh <= m) {
         const int c = kh - 1;
         if (FUSED) {
-            const int kq = d.head[m + st->q - 1];
+            const int kq = st->kq;
             va += (kq > m) ? d.A.A[(size_t)(kq - m - 1) * d.A.lda + c] : (c == kq - 1 ? -1.0 : 0.0);
         } else
             va += d.h[c];
-        if (NRHS == 2) vb += AW ? aw_value(d, c, awsplits) : d.work[c];
+        if (NRHS == 2) vb += d.work[c];
     }
     d.tcol[r] = va;
     if (NRHS == 2) d.u[r] = vb;
+}
+
+// ---------------------------------------------------------------------------
+// k_dual_ftran1 (dense A, nr <= FONE_MAX): the pick, tcol = inv(B) h and
+// u = inv(B)(ys - A w) in ONE kernel.  Block b owns rows [64 b, 64 b + 64);
+// its waves split the dense-column list (entries t = w, w + nw, ...; each
+// wave reads 512-byte segments of the columns).  A wave's entries, and with
+// them the multipliers h_c = A[c, q] and work_c, are wave-uniform.  The list
+// entries, work_c and the first group of inv(B) values are loaded before the
+// pick resolves (they do not depend on q); the wave partials meet in LDS in
+// wave order (the only block barrier).
+// ---------------------------------------------------------------------------
+constexpr int FONE_MAX = 2048;
+
+template <int NRHS>
+__global__ void __launch_bounds__(1024) k_dual_ftran1(SpxDev d, int gn, int awsplits, int ncb, int nr_cap)
+{
+    __shared__ double sp[NRHS][16][64];
+    DState *st = d.st;
+    if (st->stop) return;
+    const int m = d.m;
+    const int lane = threadIdx.x & 63;
+    const int w = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+    const int nw = blockDim.x >> 6;
+    const int r = blockIdx.x * 64 + lane;
+    const bool act = r < m;
+    const size_t ldb = (size_t)d.ldb;
+    const int *__restrict__ rl = d.rlist;
+    const double *__restrict__ Bv = d.Binv;
+    // q-independent loads
+    constexpr int G = 8;
+    int c0[G];
+    double bv[G], wv[G];
+#pragma unroll
+    for (int u = 0; u < G; ++u) {
+        const int t = w + u * nw;
+        c0[u] = (t < nr_cap) ? rl[t] : 0;
+    }
+    const int nr = st->nr;
+#pragma unroll
+    for (int u = 0; u < G; ++u) {
+        const bool ok = w + u * nw < nr;
+        bv[u] = (act && ok) ? Bv[(size_t)c0[u] * ldb + r] : 0.0;
+        wv[u] = (NRHS == 2 && ok) ? d.work[c0[u]] : 0.0;
+    }
+    const int kh = (w == 0 && act) ? d.head[r] : m + 1;
+    double ub = 0.0;
+    if (NRHS == 2 && kh <= m) ub = d.work[kh - 1];
+    int kq = 0;
+    const int q = dual_pick(d, NRHS == 2, gn, ncb, &kq);
+    if (!q) return;
+    const double *hcol = (kq > m) ? d.A.A + (size_t)(kq - m - 1) * d.A.lda : nullptr;
+    auto hval = [&](int c) { return hcol ? hcol[c] : (c == kq - 1 ? -1.0 : 0.0); };
+    double ua = 0.0;
+    if (kh <= m) ua = hval(kh - 1);
+    double a = 0.0, b = 0.0;
+    {
+        double xa[G];
+#pragma unroll
+        for (int u = 0; u < G; ++u) xa[u] = (w + u * nw < nr) ? hval(c0[u]) : 0.0;
+#pragma unroll
+        for (int u = 0; u < G; ++u) {
+            a += bv[u] * xa[u];
+            if (NRHS == 2) b += bv[u] * wv[u];
+        }
+    }
+    int t = w + G * nw;
+    for (; t + 3 * nw < nr; t += 4 * nw) {
+        int c[4];
+        double x[4], xa[4], xb[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) c[u] = rl[t + u * nw];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            x[u] = act ? Bv[(size_t)c[u] * ldb + r] : 0.0;
+            xa[u] = hval(c[u]);
+            xb[u] = (NRHS == 2) ? d.work[c[u]] : 0.0;
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            a += x[u] * xa[u];
+            if (NRHS == 2) b += x[u] * xb[u];
+        }
+    }
+    for (; t < nr; t += nw) {
+        const int c = rl[t];
+        const double x = act ? Bv[(size_t)c * ldb + r] : 0.0;
+        a += x * hval(c);
+        if (NRHS == 2) b += x * d.work[c];
+    }
+    sp[0][w][lane] = a;
+    if (NRHS == 2) sp[NRHS - 1][w][lane] = b;
+    __syncthreads();
+    if (w != 0 || !act) return;
+    double va = 0.0, vb = 0.0;
+    for (int k = 0; k < nw; ++k) {
+        va += sp[0][k][lane];
+        if (NRHS == 2) vb += sp[NRHS - 1][k][lane];
+    }
+    d.tcol[r] = va + ua;
+    if (NRHS == 2) d.u[r] = vb + ub;
 }
 
 // ---------------------------------------------------------------------------
@@ -966,50 +1095,66 @@ __global__ void __launch_bounds__(512) k_dual_ftran_reduce(SpxDev d, int splits,
 // (:1020), update_gamma (:1075-1134) in the first `nvb` blocks, together with
 // the chuzr candidates and the phase-I check of the next iteration; the
 // rank-1 update of the dense columns of inv(B) in the others (row p :=
-// rho / alpha_p, row i -= alpha_i / alpha_p rho).  A slack leaving the basis
-// turns its unit column dense (virtual list entry nr, rho = 1); a slack
-// entering turns its column into exactly e_p.
+// rho / alpha_p, row i -= alpha_i / alpha_p rho) over the compact rho
+// (entries [chunk lpsu, ...) loaded at entry).  A slack leaving the basis
+// turns its unit column dense (the extra rho entry, value 1); a slack
+// entering turns its column into exactly e_p.  Block 0 also maintains the
+// dense-column and reference-space lists for the change of basis and
+// accounts the pivot's algorithmic bytes.
 // ---------------------------------------------------------------------------
-__global__ void __launch_bounds__(256) k_dual_commit(SpxDev d, int pse, int nvb, int tiles)
+__global__ void __launch_bounds__(256) k_dual_commit(SpxDev d, int pse, int nvb, int tiles, int lpsu, int rowpath,
+                                                     double bytes_fixed)
 {
-    __shared__ Cand shc[16];
     DState *st = d.st;
     if (st->stop) return;
-    const int m = d.m, n = d.n, p = st->p, q = st->q;
-    const double piv1 = d.tcol[p - 1], piv2 = d.trow[q - 1];
-    const bool bad = fabs(piv1 - piv2) > 1e-8 * (1.0 + fabs(piv1)) ||
-                     !((piv1 > 0.0 && piv2 > 0.0) || (piv1 < 0.0 && piv2 < 0.0));
-    if (bad && (!st->binv_fresh || !st->rigorous)) {
-        if (blockIdx.x == 0 && threadIdx.x == 0) st->stop = ST_PIVCHK;
-        return;
-    }
-    const double tp = bad ? piv2 : piv1;
-    const double delta = st->delta;
-    const int kq = d.head[m + q - 1];
-    const int kp = d.head[p - 1];
+    const int m = d.m, n = d.n;
+    const int p = st->p, q = st->q, kp = st->kp, kq = st->kq;
     if ((int)blockIdx.x < nvb) {
         const int i = blockIdx.x * blockDim.x + threadIdx.x;
         // gathers first: the row / column operands and what the next
         // iteration's chuzr and check_feas read
         const bool in_m = i < m, in_n = i < n;
         const int kold = in_m ? d.head[i] : 1;
-        const int knew = (i == p - 1) ? kq : kold;
         double bb = in_m ? d.bbar[i] : 0.0;
         const double ti = in_m ? d.tcol[i] : 0.0;
         double g = in_m ? d.gamma[i] : 0.0;
         const double ui = (pse && in_m) ? d.u[i] : 0.0;
+        double cb = in_n ? d.cbar[i] : 0.0;
+        const double tri = in_n ? d.trow[i] : 0.0;
+        const int kn = in_n ? ((i == q - 1) ? kp : d.head[m + i]) : 1;
+        const double piv1 = d.tcol[p - 1], piv2 = d.trow[q - 1];
+        const int tkq = d.type[kq - 1], tkp = d.type[kp - 1];
+        const bool refkp = pse && d.refsp[kp - 1] != 0;
+        const int knew = (i == p - 1) ? kq : kold;
         const int tkold = in_m ? d.type[kold - 1] : 0;
         const bool refk = (pse && in_m) ? d.refsp[kold - 1] != 0 : false;
         const int tknew = in_m ? d.type[knew - 1] : 0;
         const double lbn = in_m ? d.lb[knew - 1] : 0.0, ubn = in_m ? d.ub[knew - 1] : 0.0;
-        double cb = in_n ? d.cbar[i] : 0.0;
-        const double tri = in_n ? d.trow[i] : 0.0;
-        const int kn = in_n ? ((i == q - 1) ? kp : d.head[m + i]) : 1;
         const int ot = (st->phase == 1 && in_n) ? d.orig_type[kn - 1] : 0;
+        const double xq = (i == p - 1) ? get_xN(d.stat, d.lb, d.ub, kq, q) : 0.0;
+        // list maintenance operands (block 0, wave 1)
+        const bool maint = (blockIdx.x == 0 && threadIdx.x == 64);
+        int rq = -1, wq = -1, rlast = 0, wlast = 0, nr0 = 0, nwl0 = 0;
+        if (maint) {
+            nr0 = st->nr;
+            nwl0 = st->nwl;
+            if (kq <= m) rq = d.rpos[kq - 1];
+            if (kq > m) wq = d.wpos[kq - m - 1];
+            rlast = d.rlist[max(nr0 - 1, 0)];
+            if (pse) wlast = d.wlist[max(nwl0 - 1, 0)];
+        }
+        const bool bad = fabs(piv1 - piv2) > 1e-8 * (1.0 + fabs(piv1)) ||
+                         !((piv1 > 0.0 && piv2 > 0.0) || (piv1 < 0.0 && piv2 < 0.0));
+        if (bad && (!st->binv_fresh || !st->rigorous)) {
+            if (blockIdx.x == 0 && threadIdx.x == 0) st->stop = ST_PIVCHK;
+            return;
+        }
+        const double tp = bad ? piv2 : piv1;
+        const double delta = st->delta;
         const double teta = delta / tp;
         const double new_dq = st->new_dq;
         if (in_m) {
-            if (i == p - 1) bb = get_xN(d.stat, d.lb, d.ub, kq, q) + teta;
+            if (i == p - 1) bb = xq + teta;
             else if (teta != 0.0) bb += ti * teta;
             d.bbar[i] = bb;
         }
@@ -1020,7 +1165,6 @@ __global__ void __launch_bounds__(256) k_dual_commit(SpxDev d, int pse, int nvb,
         }
         if (pse && in_m) {
             const double gamma_p = st->gamma_pq, eta_p = st->eta_pq;
-            const int tkq = d.type[kq - 1];
             if (i == p - 1) {
                 if (tkq == FR) g = 1.0;
                 else {
@@ -1034,7 +1178,7 @@ __global__ void __launch_bounds__(256) k_dual_commit(SpxDev d, int pse, int nvb,
                 g = (t1 >= t2 ? t1 : t2);
                 if (g < DBL_EPS) g = DBL_EPS;
             }
-            if (d.type[kp - 1] == FX && d.refsp[kp - 1] && ti != 0.0) {
+            if (tkp == FX && refkp && ti != 0.0) {
                 double t = 0.0;
                 bool apply = true;
                 if (i == p - 1) {
@@ -1055,10 +1199,10 @@ __global__ void __launch_bounds__(256) k_dual_commit(SpxDev d, int pse, int nvb,
             Cand c = no_cand(0.0);
             if (in_m) {
                 const bool reset = (pse && st->refct == 1);
-                c = chuzr_cand_v(i, tknew, lbn, ubn, bb, reset ? 1.0 : g, st->tol_bnd);
+                c = chuzr_cand_v(i, knew, tknew, lbn, ubn, bb, reset ? 1.0 : g, st->tol_bnd);
             }
-            const Cand b = block_best<0>(c, shc);
-            if (threadIdx.x == 0) cand_chuzr(d)[blockIdx.x] = b;
+            const Cand b = wave_best<0>(c);
+            if ((threadIdx.x & 63) == 0) cand_chuzr(d)[blockIdx.x * 4 + (threadIdx.x >> 6)] = b;
         }
         if (st->phase == 1) {
             const double tol = st->tol_dj;
@@ -1069,38 +1213,124 @@ __global__ void __launch_bounds__(256) k_dual_commit(SpxDev d, int pse, int nvb,
             st->teta = teta;
             st->pivot = tp;
             st->pend = 1;
+            st->fxp = (tkp == FX);
+            st->rclr = (tkp == FX && refkp);
+        }
+        if (maint) {
+            // dense columns of inv(B): an entering slack's column is now e_p,
+            // a leaving slack's column became dense
+            int nr = nr0;
+            if (kq <= m) {
+                d.rlist[rq] = rlast;
+                d.rpos[rlast] = rq;
+                d.rpos[kq - 1] = -1;
+                nr--;
+            }
+            if (kp <= m) {
+                d.rlist[nr] = kp - 1;
+                d.rpos[kp - 1] = nr;
+                nr++;
+            }
+            st->nr = nr;
+            if (pse) {
+                // reference-space non-basic structurals (update_gamma's A w)
+                int nwl = nwl0;
+                if (wq >= 0) {
+                    d.wlist[wq] = wlast;
+                    d.wpos[wlast] = wq;
+                    d.wpos[kq - m - 1] = -1;
+                    nwl--;
+                }
+                if (kp > m && refkp && tkp != FX) {
+                    d.wlist[nwl] = kp - m - 1;
+                    d.wpos[kp - m - 1] = nwl;
+                    nwl++;
+                }
+                st->nwl = nwl;
+            }
+            // algorithmic HBM bytes of this pivot: the pivot row (rows of A in
+            // the support of rho, or all of A), A w over the reference-space
+            // columns, inv(B) once for both right-hand sides, read + write of
+            // the updated columns, and the O(m + n) vectors
+            const int ns = st->ns;
+            const double rowb = rowpath ? 8.0 * (double)ns * n : 8.0 * (double)m * n;
+            const unsigned long long tk0 = st->tk_start, tk1 = st->tk_end, tk2 = st->tk_next;
+            if (rowpath && tk1 > tk0) {
+                st->bytes_trow += rowb;
+                st->trow_ticks += (double)(tk1 - tk0);
+                st->trow_ticks_b += (double)(tk2 - tk0);
+                st->trow_n += 1.0;
+            }
+            st->tk_end = 0;
+            st->bytes += rowb + 8.0 * (double)m * nwl0 + 8.0 * (double)m * (nr0 + 1) +
+                         16.0 * (double)m * (nr0 + (kp <= m ? 1 : 0)) + bytes_fixed;
         }
         return;
     }
-    // rank-1 update over the dense columns
+    // rank-1 update over the dense columns (the compact rho: ns entries)
     const int b = blockIdx.x - nvb;
-    const int tile = b % tiles, chunk = b / tiles, chunks = (gridDim.x - nvb) / tiles;
-    const int nr = st->nr;
-    const int cnt = nr + (kp <= m ? 1 : 0);
-    const int ce = (kq <= m) ? kq - 1 : -1;
-    const int lps = (cnt + chunks - 1) / chunks;
-    const int t0 = chunk * lps, t1 = min(cnt, t0 + lps);
+    const int tile = b % tiles, chunk = b / tiles;
+    const int t0 = chunk * lpsu;
     const int r = (tile * 256 + threadIdx.x) * 2;
     if (r >= m) return;
     const bool two = (r + 1 < m);
+    const double tr0 = d.tcol[r], tr1 = two ? d.tcol[r + 1] : 0.0;
+    constexpr int U = 4;
+    int cc[U];
+    double rl[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        const int t = t0 + u;
+        cc[u] = (t <= m && u < lpsu) ? d.rho_idx[t] : 0;
+        rl[u] = (t <= m && u < lpsu) ? d.rho_val[t] : 0.0;
+    }
+    const int ns = st->ns;
+    const int t1 = min(ns, t0 + lpsu);
+    const double piv1 = d.tcol[p - 1], piv2 = d.trow[q - 1];
+    const int ce = (kq <= m) ? kq - 1 : -1;
+    double2 v0[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+        if (t0 + u < t1) v0[u] = *(const double2 *)(d.Binv + (size_t)cc[u] * d.ldb + r);
+    const bool bad = fabs(piv1 - piv2) > 1e-8 * (1.0 + fabs(piv1)) ||
+                     !((piv1 > 0.0 && piv2 > 0.0) || (piv1 < 0.0 && piv2 < 0.0));
+    if (bad && (!st->binv_fresh || !st->rigorous)) return;
+    const double tp = bad ? piv2 : piv1;
     const bool z0 = (r == p - 1), z1 = (r + 1 == p - 1);
-    const double f0 = z0 ? 1.0 / tp : d.tcol[r] / tp;
-    const double f1 = two ? (z1 ? 1.0 / tp : d.tcol[r + 1] / tp) : 0.0;
-    for (int t = t0; t < t1; ++t) {
-        const int c = (t < nr) ? d.rlist[t] : kp - 1;
-        const double rl = (t < nr) ? d.rho_val[t] : 1.0;
+    const double f0 = z0 ? 1.0 / tp : tr0 / tp;
+    const double f1 = two ? (z1 ? 1.0 / tp : tr1 / tp) : 0.0;
+    auto upd = [&](int c, double rv, double2 v) {
         double *ptr = d.Binv + (size_t)c * d.ldb + r;
-        double2 v;
         if (c == ce) {
             v.x = z0 ? 1.0 : 0.0;
             v.y = z1 ? 1.0 : 0.0;
         } else {
-            v = *(double2 *)ptr;
-            v.x = (z0 ? 0.0 : v.x) - f0 * rl;
-            v.y = (z1 ? 0.0 : v.y) - f1 * rl;
+            v.x = (z0 ? 0.0 : v.x) - f0 * rv;
+            v.y = (z1 ? 0.0 : v.y) - f1 * rv;
         }
         if (two) *(double2 *)ptr = v;
         else ptr[0] = v.x;
+    };
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+        if (t0 + u < t1) upd(cc[u], rl[u], v0[u]);
+    for (int t = t0 + U; t < t1; t += U) {
+        int c[U];
+        double rv[U];
+        double2 v[U];
+        const int cnt = min(U, t1 - t);
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+            if (u < cnt) {
+                c[u] = d.rho_idx[t + u];
+                rv[u] = d.rho_val[t + u];
+            }
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+            if (u < cnt) v[u] = *(const double2 *)(d.Binv + (size_t)c[u] * d.ldb + r);
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+            if (u < cnt) upd(c[u], rv[u], v[u]);
     }
 }
 
@@ -1115,6 +1345,8 @@ DualPlan dual_plan(const SpxDev &d, int nr_max, int nwl_max, int pse, int rigoro
     pl.rigorous = rigorous;
     nr_max = std::min(std::max(nr_max, 0), m);
     const int ns_max = std::min(m, nr_max + 1);
+    pl.nr_cap = nr_max;
+    pl.ns_cap = ns_max;
     pl.rowpath = (d.A.dense && d.A.AT && !rigorous && 2 * ns_max <= m) ? 1 : 0;
     pl.fused = (d.A.dense && !rigorous) ? 1 : 0;
     const int tiles_t = cdiv(n, 512), tiles_f = cdiv(m, 512);
@@ -1124,7 +1356,11 @@ DualPlan dual_plan(const SpxDev &d, int nr_max, int nwl_max, int pse, int rigoro
     const int nrhs = pse ? 2 : 1;
     pl.fsplits = std::max(1, std::min(2048 / tiles_f, cdiv(std::max(nr_max, 1), 8)));
     pl.fsplits = std::max(1, std::min<int>(pl.fsplits, (int)(d.partial_cap / ((size_t)nrhs * m))));
-    pl.uchunks = std::max(1, std::min(2048 / tiles_f, cdiv(nr_max + 1, 4)));
+    pl.fone = (pl.fused && nr_max <= FONE_MAX) ? 1 : 0;
+    pl.fwaves = nr_max <= 32 ? 4 : (nr_max <= 128 ? 8 : 16);
+    pl.uchunks = std::max(1, std::min(2048 / tiles_f, cdiv(ns_max, 4)));
+    pl.lpsu = cdiv(ns_max, pl.uchunks);
+    pl.uchunks = cdiv(ns_max, pl.lpsu);
     pl.awsplits = std::max(1, std::min(cdiv(std::max(nwl_max, 1), 32), 64));
     pl.awsplits = std::max(1, std::min<int>(pl.awsplits, (int)(d.awpart_cap / std::max(m, 1))));
     return pl;
@@ -1157,7 +1393,8 @@ void dual_batch_begin(hipStream_t s, const SpxDev &d, const DualPlan &pl)
 
 void dual_batch_end(hipStream_t s, const SpxDev &d, const DualPlan &pl)
 {
-    hipLaunchKernelGGL(k_dual_finish, dim3(1), dim3(64), 0, s, d, pl.rowpath, bytes_fixed(d));
+    (void)pl;
+    hipLaunchKernelGGL(k_dual_finish, dim3(1), dim3(64), 0, s, d);
 }
 
 template <int NRHS, int FUSED, int AW>
@@ -1174,13 +1411,11 @@ void dual_iteration2(hipStream_t s, const SpxDev &d, const DualPlan &pl, hipEven
 {
     const int m = d.m, n = d.n;
     const int gv = cdiv(std::max(m, n), 256), gn = cdiv(n, 256), tiles_m = cdiv(m, 512);
-    const double bf = bytes_fixed(d);
-    hipLaunchKernelGGL(k_dual_top, dim3(1), dim3(WG), 0, s, d, pl.rowpath, bf);
+    hipLaunchKernelGGL(k_dual_top, dim3(1), dim3(TOP_WG), 0, s, d, pl.rowpath, pl.nr_cap);
     if (pl.rigorous) refine_rho_dev(s, d);
-    int ncb = gv, slotw = 256;
+    int ncb = 4 * gv;                                  // 64-slot groups of the pivot row
     if (pl.rowpath) {
         ncb = cdiv(std::max(m, n), 64);
-        slotw = 64;
         if (ev0) (void)hipEventRecord(ev0, s);
         hipLaunchKernelGGL(k_trow_rows, dim3(ncb), dim3(64 * pl.twaves), 0, s, d, pl.pse);
         if (ev1) (void)hipEventRecord(ev1, s);
@@ -1189,14 +1424,23 @@ void dual_iteration2(hipStream_t s, const SpxDev &d, const DualPlan &pl, hipEven
         colpass_gated(s, d.A, CP_TROW, m, n, d.head, d.stat, d.coef, nullptr, d.rho, nullptr, d.trow, nullptr,
                       &d.st->trow_max_bits, d.st, 0);
         if (ev1) (void)hipEventRecord(ev1, s);
-        hipLaunchKernelGGL(k_trow_finish<0>, dim3(gv), dim3(256), 0, s, d, (const double *)nullptr, 0, pl.pse, 0);
+        hipLaunchKernelGGL(k_trow_finish, dim3(gv), dim3(256), 0, s, d, pl.pse);
     }
     const int aw = (pl.pse && d.A.dense) ? 1 : 0;
     hipLaunchKernelGGL(k_dual_ratio, dim3(gn + (aw ? tiles_m * pl.awsplits : 0)), dim3(256), 0, s, d, gn, tiles_m,
-                       pl.rowpath, ncb, slotw);
+                       pl.rowpath, ncb);
     if (pl.fused) {
-        if (pl.pse) launch_ftran<2, 1, 1>(s, d, pl, gn, ncb);
-        else launch_ftran<1, 1, 0>(s, d, pl, gn, ncb);
+        if (pl.fone) {
+            if (pl.pse)
+                hipLaunchKernelGGL(k_dual_ftran1<2>, dim3(cdiv(m, 64)), dim3(64 * pl.fwaves), 0, s, d, gn,
+                                   pl.awsplits, ncb, pl.nr_cap);
+            else
+                hipLaunchKernelGGL(k_dual_ftran1<1>, dim3(cdiv(m, 64)), dim3(64 * pl.fwaves), 0, s, d, gn,
+                                   pl.awsplits, ncb, pl.nr_cap);
+        } else if (pl.pse)
+            launch_ftran<2, 1, 1>(s, d, pl, gn, ncb);
+        else
+            launch_ftran<1, 1, 0>(s, d, pl, gn, ncb);
     } else {
         hipLaunchKernelGGL(k_dual_pick, dim3(1), dim3(1024), 0, s, d, pl.pse, gn, ncb);
         if (pl.pse) {
@@ -1210,7 +1454,8 @@ void dual_iteration2(hipStream_t s, const SpxDev &d, const DualPlan &pl, hipEven
         if (pl.rigorous) refine_tcol_dev(s, d, 0);
     }
     const int nvb = gv;
-    hipLaunchKernelGGL(k_dual_commit, dim3(nvb + tiles_m * pl.uchunks), dim3(256), 0, s, d, pl.pse, nvb, tiles_m);
+    hipLaunchKernelGGL(k_dual_commit, dim3(nvb + tiles_m * pl.uchunks), dim3(256), 0, s, d, pl.pse, nvb, tiles_m,
+                       pl.lpsu, pl.rowpath, bytes_fixed(d));
 }
 
 // AT[r*ldt + c] = A[c*lda + r], 64 x 64 tiles through LDS

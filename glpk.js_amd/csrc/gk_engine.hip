@@ -116,7 +116,7 @@ struct Engine {
     DBuf<double> bbar, cbar, gamma, tcol, trow, rho, rowp, u, s, h, wcol, ys, work, r1, r2, partial;
     DBuf<DState> st;
     DState *st_host = nullptr;              // pinned staging copy of st (hipHostMalloc)
-    DBuf<int> rlist, rpos, rho_idx, wlist, wpos;
+    DBuf<int> rlist, rpos, rho_idx, wlist, wpos, awcnt;
     DBuf<double> rho_val, gpart, cand, awpart;
     DBuf<unsigned long long> tslots;
     std::vector<GraphEntry> graphs;
@@ -139,7 +139,7 @@ struct Engine {
     ~Engine()
     {
         A.release(); AT.release(); rlist.release(); rpos.release(); rho_idx.release(); rho_val.release();
-        gpart.release(); tslots.release(); wlist.release(); wpos.release(); cand.release(); awpart.release(); cptr.release(); cind.release(); rptr.release(); rcol.release(); cval.release(); rval.release();
+        gpart.release(); awcnt.release(); tslots.release(); wlist.release(); wpos.release(); cand.release(); awpart.release(); cptr.release(); cind.release(); rptr.release(); rcol.release(); cval.release(); rval.release();
         type.release(); orig_type.release(); stat.release(); refsp.release();
         lb.release(); ub.release(); coef.release(); orig_lb.release(); orig_ub.release(); obj.release();
         head.release(); bind.release();
@@ -301,9 +301,16 @@ static void engine_alloc(Engine &E, int m, int n)
     E.rlist.ensure(m); E.rpos.ensure(m); E.rho_idx.ensure((size_t)m + 1); E.rho_val.ensure((size_t)m + 1);
     const size_t gv = (size_t)(std::max(m, n) + 255) / 256 + 1;
     E.gpart.ensure(8 * (size_t)gv);              // gamma_p sums, then per-block max |trow| (64-slot blocks)
-    E.cand.ensure(3 * 6 * (size_t)gv);           // candidates (24-byte entries): chuzr gv | pass 1 4 gv | pass 2 gv
+    E.cand.ensure(3 * 12 * (size_t)gv);          // candidates (24-byte entries): chuzr | pass 1 | pass 2, 4 gv each
     E.wlist.ensure(n); E.wpos.ensure(n);
     E.awpart.ensure((size_t)AW_SPLITS * m);
+    {
+        const size_t tiles = (size_t)(m + 511) / 512 + 1;
+        if (E.awcnt.n < tiles || !E.awcnt.p) {
+            E.awcnt.ensure(tiles);
+            HIPCHK(hipMemset(E.awcnt.p, 0, E.awcnt.n * sizeof(int)));   // arrival counters, reset by their users
+        }
+    }
     E.tslots.ensure(std::max((size_t)((n + 511) / 512) * 2048, 4 * (size_t)gv) + 1);
 }
 
@@ -418,7 +425,7 @@ struct Spx {
         d.rlist = E->rlist.p; d.rpos = E->rpos.p; d.rho_idx = E->rho_idx.p; d.rho_val = E->rho_val.p;
         d.gpart = E->gpart.p;
         d.wlist = E->wlist.p; d.wpos = E->wpos.p; d.cand = E->cand.p;
-        d.awpart = E->awpart.p; d.awpart_cap = (size_t)AW_SPLITS * m;
+        d.awpart = E->awpart.p; d.awpart_cap = (size_t)AW_SPLITS * m; d.awcnt = E->awcnt.p;
         d.tslots = E->tslots.p;
         return d;
     }

@@ -61,6 +61,10 @@ struct DState {
     double trow_ticks, trow_n;              // accumulated execution span of the pivot-row kernels (row path)
     double trow_ticks_b, trow_pad;          // same, entry to the next kernel's entry (dispatch included)
     unsigned long long trow_max_bits, tcol_max_bits;
+    int kp, kq, fxp, rclr;                  // dual: leaving / entering variable of the pivot; x_kp fixed;
+                                            // refsp[kp] to clear at change_basis
+    int kq1, pad2, pad3, pad4;              // variable of the pass-1 choice
+    double alfa1, pad5;                     // |trow| of the pass-1 choice
 };
 
 // ---- dense GEMV helpers ---------------------------------------------------
@@ -130,6 +134,7 @@ struct SpxDev {
     double *cand;                            // per-block candidates: chuzr | pass 1 | pass 2
     double *awpart;                          // partial sums of A w
     size_t awpart_cap;
+    int *awcnt;                              // per 512-row tile: arrivals of the A w splits (the last one reduces)
     unsigned long long *tslots;              // per-block end stamps of the pivot-row kernel
 };
 
@@ -143,6 +148,9 @@ struct DualPlan {
     int fsplits;                  // FTRAN over the dense columns of inv(B): splits
     int uchunks;                  // rank-1 update: column chunks
     int awsplits;                 // A w over wlist: splits
+    int nr_cap, ns_cap;           // upper bounds of nr / ns over the batch (speculative list loads)
+    int fone, fwaves;             // 1: FTRAN in one kernel (k_dual_ftran1), fwaves waves per 64-row block
+    int lpsu;                     // rank-1 update: list entries per chunk
 };
 void dual_batch_begin(hipStream_t s, const SpxDev &d, const DualPlan &pl);
 void dual_batch_end(hipStream_t s, const SpxDev &d, const DualPlan &pl);
