@@ -14,19 +14,18 @@ namespace gk {
 constexpr int WG = 1024;       // single-workgroup control kernels
 constexpr double DBL_EPS = 2.220446049250313e-16;   // glpapi.js:7
 
-__device__ __forceinline__ double wsum(double v)
-{
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
-    return v;
-}
+// wave-wide reductions of the device library (DPP sequences, not LDS
+// permutes); all lanes of the wave must be active
+extern "C" __device__ __attribute__((const)) double __ockl_wfred_add_f64(double);
+extern "C" __device__ __attribute__((const)) double __ockl_wfred_max_f64(double);
+extern "C" __device__ __attribute__((const)) unsigned long long __ockl_wfred_min_u64(unsigned long long);
+extern "C" __device__ __attribute__((const)) unsigned long long __ockl_wfred_max_u64(unsigned long long);
+extern "C" __device__ __attribute__((const)) unsigned int __ockl_wfred_min_u32(unsigned int);
 
-__device__ __forceinline__ double wmax(double v)
-{
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v = fmax(v, __shfl_xor(v, o));
-    return v;
-}
+// sum over the wave in a fixed order (deterministic)
+__device__ __forceinline__ double wsum(double v) { return __ockl_wfred_add_f64(v); }
+
+__device__ __forceinline__ double wmax(double v) { return __ockl_wfred_max_f64(v); }
 
 // block-wide reductions for blockDim.x <= 1024 (16 waves)
 static __device__ double block_sum(double v, double *sh)
@@ -78,6 +77,8 @@ static __device__ int block_or(int v, int *sh)
     __syncthreads();
     return r;
 }
+
+__device__ __forceinline__ unsigned long long dbits(double v) { return (unsigned long long)__double_as_longlong(v); }
 
 // candidate of an index-choosing scan: key1 (primary), key2 (secondary), idx
 struct Cand {
@@ -141,23 +142,48 @@ static __device__ Cand block_best(Cand c, Cand *sh)
     return r;
 }
 
-// the same within one wave (no block synchronisation); every lane gets it
+// the same within one wave (no block synchronisation); every lane gets it.
+// The keys are non-negative doubles (ratios, |alfa|, r^2 / gamma), whose
+// bit patterns order like the values once -0 is folded into +0, so the
+// choice is three exact wave reductions (key, secondary key, index) and a
+// ballot for the winning lane; identical to better<MODE> for distinct
+// indices.
 template <int MODE>
 __device__ __forceinline__ Cand wave_best(Cand c)
 {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-        Cand d;
-        d.k1 = __shfl_xor(c.k1, o);
-        d.k2 = __shfl_xor(c.k2, o);
-        d.idx = __shfl_xor(c.idx, o);
-        d.aux = __shfl_xor(c.aux, o);
-        if (better<MODE>(d, c)) c = d;
+    // every reduction is called by every lane (no short-circuit: the
+    // reductions run over the active lanes)
+    const bool valid = c.idx != 0;
+    bool tie;
+    if (MODE == 1) {
+        const unsigned long long k = valid ? dbits(fabs(c.k1)) : ~0ull;
+        const unsigned long long mk = __ockl_wfred_min_u64(k);
+        tie = valid & (k == mk);
+        const unsigned long long k2 = tie ? dbits(fabs(c.k2)) + 1ull : 0ull;
+        const unsigned long long m2 = __ockl_wfred_max_u64(k2);
+        tie = tie & (k2 == m2);
+    } else {
+        const double kk = (MODE == 0) ? c.k1 : c.k2;
+        const unsigned long long k = valid ? dbits(fabs(kk)) + 1ull : 0ull;
+        const unsigned long long mk = __ockl_wfred_max_u64(k);
+        tie = valid & (k == mk);
     }
-    return c;
+    const unsigned int ii = tie ? (unsigned int)c.idx : 0xffffffffu;
+    const unsigned int mi = __ockl_wfred_min_u32(ii);
+    Cand r;
+    if (mi == 0xffffffffu) {
+        r.k1 = 0.0; r.k2 = 0.0; r.idx = 0; r.aux = 0;
+        return r;
+    }
+    const unsigned long long bal = __ballot(tie & ((unsigned int)c.idx == mi));
+    const int src = __builtin_amdgcn_readfirstlane(__ffsll((long long)bal) - 1);
+    r.k1 = __shfl(c.k1, src);
+    r.k2 = __shfl(c.k2, src);
+    r.idx = (int)mi;
+    r.aux = __shfl(c.aux, src);
+    return r;
 }
 
-__device__ __forceinline__ unsigned long long dbits(double v) { return (unsigned long long)__double_as_longlong(v); }
 
 __device__ __forceinline__ double get_xN(const signed char *stat, const double *lb, const double *ub, int k, int j)
 {

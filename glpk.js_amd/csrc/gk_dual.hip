@@ -79,6 +79,30 @@ __device__ __forceinline__ unsigned long long wmax_u64(unsigned long long v)
     return v;
 }
 
+// profiling (gk_bfd_profile(bfd, 2), eager launches): device clock at block
+// entry (thread 0) and the latest wave exit of the block
+struct TraceScope {
+    unsigned long long *p;
+    __device__ __forceinline__ TraceScope(const SpxDev &d, int kid)
+        : p((d.trace && blockIdx.x < (unsigned)TRACE_BLOCKS) ? d.trace + ((size_t)kid * TRACE_BLOCKS + blockIdx.x) * 2
+                                                              : nullptr)
+    {
+        if (p && threadIdx.x == 0) p[0] = wall_clock64();
+    }
+    __device__ __forceinline__ ~TraceScope()
+    {
+        if (p && (threadIdx.x & 63) == 0) atomicMax(p + 1, wall_clock64());
+    }
+};
+
+// phase stamp of wave 0 (profiling only)
+#define TPH(kid, ph)                                                                                              \
+    do {                                                                                                          \
+        if (d.trace && threadIdx.x == 0 && blockIdx.x < (unsigned)TRACE_BLOCKS)                                   \
+            d.trace[(size_t)TRACE_KERNELS * TRACE_BLOCKS * 2 + ((size_t)(kid) * TRACE_BLOCKS + blockIdx.x) * 8 + \
+                    (ph)] = wall_clock64();                                                                       \
+    } while (0)
+
 // ---------------------------------------------------------------------------
 // list GEMV of one 512-row tile over list entries [t0, t1):
 //   o[k*rows + r] = sum_t M[list[t]*ld + r] * x_k(t, list[t])
@@ -240,14 +264,32 @@ struct RatioCtx {
     double eps, s, rtol;
 };
 
-__device__ __forceinline__ RatioCtx ratio_ctx(const DState *st, double big)
+// the scalars of the ratio test, loaded early (with the kernel's first loads)
+struct RatioIn {
+    double tol_bnd, delta, tol_dj;
+    int rtest;
+};
+
+__device__ __forceinline__ RatioIn ratio_in(const DState *st)
+{
+    RatioIn r;
+    r.tol_bnd = st->tol_bnd;
+    r.delta = st->delta;
+    r.tol_dj = st->tol_dj;
+    r.rtest = st->rtest;
+    return r;
+}
+
+__device__ __forceinline__ RatioCtx ratio_ctx(const RatioIn &r, double big)
 {
     RatioCtx x;
-    x.eps = st->tol_bnd * (1.0 + 0.01 * big);     // sort_trow with tol_bnd (:1851)
-    x.s = (st->delta > 0.0 ? +1.0 : -1.0);
-    x.rtol = (st->rtest == RT_HAR) ? 0.30 * st->tol_dj : 0.0;
+    x.eps = r.tol_bnd * (1.0 + 0.01 * big);       // sort_trow with tol_bnd (:1851)
+    x.s = (r.delta > 0.0 ? +1.0 : -1.0);
+    x.rtol = (r.rtest == RT_HAR) ? 0.30 * r.tol_dj : 0.0;
     return x;
 }
+
+__device__ __forceinline__ RatioCtx ratio_ctx(const DState *st, double big) { return ratio_ctx(ratio_in(st), big); }
 
 __device__ __forceinline__ double trow_big(const DState *st)
 {
@@ -324,47 +366,64 @@ struct TopState {
     double obj;
 };
 
-__device__ TopState dual_finish_block(const SpxDev &d, bool tail_sync)
+struct FinishIn {
+    int pend, p, q, kp, kq, fxp, rclr, upd_cnt, it_cnt, npiv, rig;
+    double delta;
+    TopState t;
+};
+
+__device__ __forceinline__ FinishIn finish_load(const SpxDev &d)
+{
+    const DState *st = d.st;
+    FinishIn f;
+    f.pend = st->pend;
+    f.t.iter_left = st->iter_left - f.pend;
+    f.t.refact = st->refact_pending || (f.pend && st->upd_cnt + 1 >= st->upd_lim);
+    f.t.refct = (f.pend && st->pricing == PT_PSE && st->refct > 0) ? st->refct - 1 : st->refct;
+    f.t.obj = st->obj;
+    if (f.pend && st->phase == 2) f.t.obj += (st->cbar_q_old / st->zeta) * (st->delta / st->pivot);
+    f.p = st->p; f.q = st->q; f.kp = st->kp; f.kq = st->kq;
+    f.fxp = st->fxp; f.rclr = st->rclr; f.upd_cnt = st->upd_cnt; f.it_cnt = st->it_cnt; f.npiv = st->npiv;
+    f.rig = st->rigorous;
+    f.delta = st->delta;
+    return f;
+}
+
+__device__ TopState finish_apply(const SpxDev &d, const FinishIn &f, bool tail_sync)
 {
     DState *st = d.st;
     const int m = d.m;
-    const int pend = st->pend;
-    TopState t;
-    t.iter_left = st->iter_left - pend;
-    t.refact = st->refact_pending || (pend && st->upd_cnt + 1 >= st->upd_lim);
-    t.refct = (pend && st->pricing == PT_PSE && st->refct > 0) ? st->refct - 1 : st->refct;
-    t.obj = st->obj;
-    if (pend && st->phase == 2) t.obj += (st->cbar_q_old / st->zeta) * (st->delta / st->pivot);
-    const int p = st->p, q = st->q, kp = st->kp, kq = st->kq;
-    const int fxp = st->fxp, rclr = st->rclr, upd_cnt = st->upd_cnt, it_cnt = st->it_cnt, npiv = st->npiv;
-    const int rig = st->rigorous;
-    const double delta = st->delta;
     __syncthreads();                          // every wave has read st before it is written
-    if (pend) {
+    if (f.pend) {
         if (threadIdx.x == 0) {
-            d.head[p - 1] = kq;
-            d.head[m + q - 1] = kp;
-            d.bind[kq - 1] = p;
-            d.bind[kp - 1] = m + q;
-            d.stat[q - 1] = fxp ? NS : (delta > 0.0 ? NL : NU);
+            d.head[f.p - 1] = f.kq;
+            d.head[m + f.q - 1] = f.kp;
+            d.bind[f.kq - 1] = f.p;
+            d.bind[f.kp - 1] = m + f.q;
+            d.stat[f.q - 1] = f.fxp ? NS : (f.delta > 0.0 ? NL : NU);
         } else if (threadIdx.x == 1) {
-            if (rclr) d.refsp[kp - 1] = 0;
+            if (f.rclr) d.refsp[f.kp - 1] = 0;
         } else if (threadIdx.x == 2) {
-            st->obj = t.obj;
-            st->upd_cnt = upd_cnt + 1;
+            st->obj = f.t.obj;
+            st->upd_cnt = f.upd_cnt + 1;
             st->binv_fresh = 0;
             st->cbar_fresh = 0;
-            st->refact_pending = t.refact;
-            st->it_cnt = it_cnt + 1;
-            st->npiv = npiv + 1;
-            st->iter_left = t.iter_left;
-            if (rig > 0) st->rigorous = rig - 1;
-            st->refct = t.refct;
+            st->refact_pending = f.t.refact;
+            st->it_cnt = f.it_cnt + 1;
+            st->npiv = f.npiv + 1;
+            st->iter_left = f.t.iter_left;
+            if (f.rig > 0) st->rigorous = f.rig - 1;
+            st->refct = f.t.refct;
             st->pend = 0;
         }
     }
     if (tail_sync) __syncthreads();
-    return t;
+    return f.t;
+}
+
+__device__ TopState dual_finish_block(const SpxDev &d, bool tail_sync)
+{
+    return finish_apply(d, finish_load(d), tail_sync);
 }
 
 __global__ void k_dual_finish(SpxDev d)
@@ -437,8 +496,9 @@ constexpr int TOP_WG = 256;
 
 __global__ void __launch_bounds__(TOP_WG) k_dual_top(SpxDev d, int rowpath, int nr_cap)
 {
+    const TraceScope trace_(d, 0);
     DState *st = d.st;
-    if (st->stop) return;
+    const int stop = st->stop;               // tested before the first store
     const int m = d.m, n = d.n;
     const int gm = 4 * ((m + 255) / 256);
     Cand c = no_cand(0.0);
@@ -453,28 +513,32 @@ __global__ void __launch_bounds__(TOP_WG) k_dual_top(SpxDev d, int rowpath, int 
         const int t = threadIdx.x + u * TOP_WG;
         cl[u] = (t < nr_cap) ? d.rlist[t] : 0;
     }
-    const TopState ts = dual_finish_block(d, false);
+    const FinishIn fin = finish_load(d);
+    const int pricing = st->pricing, phase = st->phase, dinf = st->dinf, nr = st->nr;
+    const double zeta = st->zeta, obj_ll = st->obj_ll, obj_ul = st->obj_ul;
+    if (stop) return;
+    const TopState ts = finish_apply(d, fin, false);
     if (ts.iter_left <= 0 || ts.refact) {
         if (threadIdx.x == 0) st->stop = ts.refact ? ST_REFACT : ST_BATCH;
         return;
     }
-    if (st->pricing == PT_PSE && ts.refct == 0) {
+    if (pricing == PT_PSE && ts.refct == 0) {
         __syncthreads();                   // the header writes of change_basis are visible
         reset_refsp_dev(d, 1);             // refsp := basic variables, gamma := 1
         for (int l = threadIdx.x; l < n; l += blockDim.x) d.wpos[l] = -1;
         if (threadIdx.x == 0) st->nwl = 0;
         __syncthreads();
     }
-    if (st->phase == 1) {
-        if (!st->dinf) {
+    if (phase == 1) {
+        if (!dinf) {
             if (threadIdx.x == 0) st->stop = ST_PHASE;
             return;
         }
     } else {
         // objective limits (:1729-1760)
-        const double z = st->zeta, obj = ts.obj;
-        const bool hit = (z < 0.0 && st->obj_ll > -DBL_MAX && obj <= st->obj_ll) ||
-                         (z > 0.0 && st->obj_ul < +DBL_MAX && obj >= st->obj_ul);
+        const double z = zeta, obj = ts.obj;
+        const bool hit = (z < 0.0 && obj_ll > -DBL_MAX && obj <= obj_ll) ||
+                         (z > 0.0 && obj_ul < +DBL_MAX && obj >= obj_ul);
         if (hit) {
             if (threadIdx.x == 0) st->stop = ST_OBJLIM;
             return;
@@ -491,7 +555,6 @@ __global__ void __launch_bounds__(TOP_WG) k_dual_top(SpxDev d, int rowpath, int 
         for (int l = threadIdx.x; l < m; l += blockDim.x) d.rho[l] = 0.0;
         __syncthreads();
     }
-    const int nr = st->nr;
     const double *brow = d.Binv + (p - 1);
     const size_t ldb = (size_t)d.ldb;
     double v[RPT];
@@ -542,6 +605,7 @@ __global__ void __launch_bounds__(TOP_WG) k_dual_top(SpxDev d, int rowpath, int 
 // ---------------------------------------------------------------------------
 __global__ void __launch_bounds__(256) k_trow_finish(SpxDev d, int pse)
 {
+    const TraceScope trace_(d, 5);
     DState *st = d.st;
     if (st->stop) return;
     const int m = d.m, n = d.n;
@@ -603,16 +667,19 @@ __global__ void __launch_bounds__(256) k_trow_finish(SpxDev d, int pse)
 // ---------------------------------------------------------------------------
 __global__ void __launch_bounds__(1024) k_trow_rows(SpxDev d, int pse)
 {
+    const TraceScope trace_(d, 1);
     __shared__ double sp[16][64];
     DState *st = d.st;
-    if (st->stop) return;
     const int m = d.m, n = d.n;
     const int lane = threadIdx.x & 63;
     const int w = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
     const int nw = blockDim.x >> 6;
     const int idx = blockIdx.x * 64 + lane;
-    if (blockIdx.x == 0 && threadIdx.x == 0) st->tk_start = wall_clock64();
-    // wave 0 gathers its slot operands first; their latency overlaps the rows
+    // trip 1: the state, the slot positions (wave 0) and the first group of
+    // rho entries (inside the allocation: m + 1 entries); stop is tested
+    // before the first store, not before the first load
+    const int stop = st->stop, ns = st->ns;
+    const RatioIn rin = ratio_in(st);
     int pos1 = 0, pos2 = 0, rp2 = -1;
     if (w == 0) {
         pos1 = (idx < n) ? d.bind[m + idx] : 0;
@@ -621,7 +688,6 @@ __global__ void __launch_bounds__(1024) k_trow_rows(SpxDev d, int pse)
     }
     const int *__restrict__ ri = d.rho_idx;
     const double *__restrict__ rv = d.rho_val;
-    // first group of rho entries, inside the allocation (m + 1 entries)
     int r0[8];
     double v0[8];
 #pragma unroll
@@ -630,21 +696,42 @@ __global__ void __launch_bounds__(1024) k_trow_rows(SpxDev d, int pse)
         r0[u] = (t <= m) ? ri[t] : 0;
         v0[u] = (t <= m) ? rv[t] : 0.0;
     }
-    const int ns = st->ns;
+    // trip 2: the slot operands (wave 0) and the first rows of AT
+    const int j1 = (pos1 > m) ? pos1 - m - 1 : -1;
+    const int j2 = (pos2 > m) ? pos2 - m - 1 : -1;
+    int s1 = 0, s2 = 0;
+    double cb1 = 0.0, cb2 = 0.0, rho2 = 0.0;
+    bool ref1 = false, ref2 = false;
+    if (j1 >= 0) {
+        s1 = d.stat[j1];
+        cb1 = d.cbar[j1];
+        if (pse) ref1 = d.refsp[m + idx] != 0;
+    }
+    if (j2 >= 0) {
+        s2 = d.stat[j2];
+        cb2 = d.cbar[j2];
+        rho2 = d.rho_val[rp2];
+        if (pse) ref2 = d.refsp[idx] != 0;
+    }
     double acc = 0.0;
-    if (idx < n) {
-        const double *__restrict__ col = d.A.AT + idx;
-        const size_t ldt = (size_t)d.A.ldt;
+    const double *__restrict__ col = d.A.AT + min(idx, n - 1);
+    const size_t ldt = (size_t)d.A.ldt;
+    {
         double a[8];
 #pragma unroll
         for (int u = 0; u < 8; ++u) a[u] = (w + u * nw < ns) ? col[(size_t)r0[u] * ldt] : 0.0;
 #pragma unroll
         for (int u = 0; u < 8; ++u)
             if (w + u * nw < ns) acc += v0[u] * a[u];
+    }
+    if (stop) return;
+    if (blockIdx.x == 0 && threadIdx.x == 0) st->tk_start = wall_clock64();
+    TPH(1, 0);
+    {
         int t = w + 8 * nw;
         for (; t + 7 * nw < ns; t += 8 * nw) {
             int r[8];
-            double v[8];
+            double v[8], a[8];
 #pragma unroll
             for (int u = 0; u < 8; ++u) {
                 r[u] = ri[t + u * nw];
@@ -657,30 +744,18 @@ __global__ void __launch_bounds__(1024) k_trow_rows(SpxDev d, int pse)
         }
         for (; t < ns; t += nw) acc += rv[t] * col[(size_t)ri[t] * ldt];
     }
-    sp[w][lane] = acc;
+    TPH(1, 1);
+    sp[w][lane] = (idx < n) ? acc : 0.0;
     __syncthreads();
+    TPH(1, 2);
     if (w != 0) return;                      // wave 0 only from here: no block barriers
     double tsum = 0.0;
     for (int k = 0; k < nw; ++k) tsum += sp[k][lane];
-    const int j1 = (pos1 > m) ? pos1 - m - 1 : -1;
-    const int j2 = (pos2 > m) ? pos2 - m - 1 : -1;
-    int s1 = 0, s2 = 0;
-    double cb1 = 0.0, cb2 = 0.0, tv1 = 0.0, tv2 = 0.0;
-    bool ref1 = false, ref2 = false;
-    if (j1 >= 0) {
-        s1 = d.stat[j1];
-        cb1 = d.cbar[j1];
-        tv1 = tsum;
-        if (pse) ref1 = d.refsp[m + idx] != 0;
-    }
-    if (j2 >= 0) {
-        s2 = d.stat[j2];
-        cb2 = d.cbar[j2];
-        tv2 = -d.rho_val[rp2];               // a non-basic slack is a dense column of inv(B)
-        if (pse) ref2 = d.refsp[idx] != 0;
-    }
+    double tv1 = (j1 >= 0) ? tsum : 0.0;
+    double tv2 = (j2 >= 0) ? -rho2 : 0.0;    // a non-basic slack is a dense column of inv(B)
     if (s1 == NS) tv1 = 0.0;
     if (s2 == NS) tv2 = 0.0;
+    TPH(1, 3);
     if (j1 >= 0) d.trow[j1] = tv1;
     if (j2 >= 0) d.trow[j2] = tv2;
     double gsum = 0.0;
@@ -693,12 +768,14 @@ __global__ void __launch_bounds__(1024) k_trow_rows(SpxDev d, int pse)
     const double bmax = wmax(fmax(fabs(tv1), fabs(tv2)));
     const double g = pse ? wsum(gsum) : 0.0;
     // pass-1 candidate with eps_b = tol_bnd (1 + 0.01 max_b) <= eps
-    const RatioCtx x = ratio_ctx(st, bmax);
+    const RatioCtx x = ratio_ctx(rin, bmax);
+    TPH(1, 4);
     Cand c = no_cand(DBL_MAX);
     Cand e;
     if (j1 >= 0 && pass1_cand(x, tv1, cb1, s1, j1, m + idx + 1, e) && better<1>(e, c)) c = e;
     if (j2 >= 0 && pass1_cand(x, tv2, cb2, s2, j2, idx + 1, e) && better<1>(e, c)) c = e;
     const Cand b = wave_best<1>(c);
+    TPH(1, 5);
     if (lane == 0) {
         tmax_part(d)[blockIdx.x] = bmax;
         if (pse) d.gpart[blockIdx.x] = g;
@@ -716,13 +793,15 @@ __global__ void __launch_bounds__(1024) k_trow_rows(SpxDev d, int pse)
 // ---------------------------------------------------------------------------
 __global__ void __launch_bounds__(256) k_dual_ratio(SpxDev d, int gn, int tiles_m, int rowpath, int ncb)
 {
+    const TraceScope trace_(d, 2);
     DState *st = d.st;
-    if (st->stop) return;
+    const int stop = st->stop;               // tested before the first store
     const int m = d.m, n = d.n;
     if ((int)blockIdx.x >= gn) {
         const int b = blockIdx.x - gn;
         const int tile = b % tiles_m, split = b / tiles_m, splits = (gridDim.x - gn) / tiles_m;
         const int cnt = st->nwl;
+        if (stop) return;
         const int lps = (cnt + splits - 1) / splits;
         const int t0 = split * lps, t1 = min(cnt, t0 + lps);
         const int r = (tile * 256 + threadIdx.x) * 2;
@@ -749,6 +828,7 @@ __global__ void __launch_bounds__(256) k_dual_ratio(SpxDev d, int gn, int tiles_
     }
     const int lane = threadIdx.x & 63;
     const unsigned long long t_entry = (rowpath && blockIdx.x == 0 && threadIdx.x == 0) ? wall_clock64() : 0ull;
+    const RatioIn rin = ratio_in(st);
     const int j = blockIdx.x * blockDim.x + threadIdx.x;
     const double trj = (j < n) ? d.trow[j] : 0.0;
     const double cbj = (j < n) ? d.cbar[j] : 0.0;
@@ -773,6 +853,8 @@ __global__ void __launch_bounds__(256) k_dual_ratio(SpxDev d, int gn, int tiles_
         if (rowpath && lead) e = max(e, d.tslots[b]);
     }
     const double big = wmax(v);
+    if (stop) return;
+    TPH(2, 0);
     if (lead) {
         // publish max |trow| and the end of the pivot-row kernel (latest
         // block exit stamp)
@@ -785,7 +867,7 @@ __global__ void __launch_bounds__(256) k_dual_ratio(SpxDev d, int gn, int tiles_
             }
         }
     }
-    const RatioCtx x = ratio_ctx(st, big);
+    const RatioCtx x = ratio_ctx(rin, big);
     Cand c = no_cand(DBL_MAX);
     int fail = 0;
 #pragma unroll
@@ -809,6 +891,7 @@ __global__ void __launch_bounds__(256) k_dual_ratio(SpxDev d, int gn, int tiles_
         }
     }
     const Cand b1 = wave_best<1>(c);
+    TPH(2, 1);
     const int q1 = b1.idx;
     const double teta1 = q1 ? b1.k1 : DBL_MAX;
     const int need2 = !(x.rtol == 0.0 || q1 == 0 || teta1 == 0.0);
@@ -826,53 +909,77 @@ __global__ void __launch_bounds__(256) k_dual_ratio(SpxDev d, int gn, int tiles_
         if (pass2_cand(x, trj, cbj, sj, j, kj, teta1, f)) c2 = f;
     }
     const Cand b2 = wave_best<2>(c2);
+    TPH(2, 2);
     if (lane == 0) cand_pass2(d)[blockIdx.x * 4 + (threadIdx.x >> 6)] = b2;
 }
 
 // the entering choice q (pass 2 if needed), its checks and the st fields;
 // every wave of the calling grid evaluates it identically (no block
-// barrier).  Returns q (kq through *kq_out), or 0 when the iteration stops.
-// The candidates carry |trow_q| (k2) and the entering variable (aux).
-__device__ int dual_pick(const SpxDev &d, int pse, int gn, int ncb, int *kq_out)
+// barrier).  pick_load issues every load the choice needs (so a caller can
+// put them in its first trip); pick_resolve returns q (kq through *kq_out),
+// or 0 when the iteration stops.  The candidates carry |trow_q| (k2) and the
+// entering variable (aux).
+struct PickIn {
+    int need2, q1, kq1, rigorous;
+    double teta1, alfa1, big, delta;
+    Cand c;                                   // this lane's best pass-2 candidate
+    double g;                                 // lead wave: this lane's share of gamma_p
+};
+
+__device__ __forceinline__ PickIn pick_load(const SpxDev &d, int pse, int gn, int ncb)
 {
-    DState *st = d.st;
+    const DState *st = d.st;
     const int lane = threadIdx.x & 63;
     const bool lead = (blockIdx.x == 0 && blockIdx.y == 0);
-    const int need2 = st->need2;
-    Cand c = no_cand(0.0);
+    PickIn pi;
+    pi.need2 = st->need2;
+    pi.q1 = st->q1;
+    pi.kq1 = st->kq1;
+    pi.rigorous = st->rigorous;
+    pi.teta1 = st->teta1;
+    pi.alfa1 = st->alfa1;
+    pi.big = trow_big(st);
+    pi.delta = st->delta;
+    pi.c = no_cand(0.0);
     for (int b = lane; b < 4 * gn; b += 64) {
         const Cand e = cand_pass2(d)[b];
-        if (better<2>(e, c)) c = e;
+        if (better<2>(e, pi.c)) pi.c = e;
     }
     // gamma_p (update_gamma :1103-1132) from the group sums, fixed order
-    double g = 0.0;
+    pi.g = 0.0;
     if (lead && pse && threadIdx.x < 64)
-        for (int b = lane; b < ncb; b += 64) g += d.gpart[b];
-    const double big = trow_big(st);
+        for (int b = lane; b < ncb; b += 64) pi.g += d.gpart[b];
+    return pi;
+}
+
+__device__ int pick_resolve(const SpxDev &d, const PickIn &pi, int pse, int *kq_out)
+{
+    DState *st = d.st;
+    const bool lead = (blockIdx.x == 0 && blockIdx.y == 0);
     int q, kq;
     double teta, alfa;
-    if (need2) {
-        const Cand b2 = wave_best<2>(c);
+    if (pi.need2) {
+        const Cand b2 = wave_best<2>(pi.c);
         q = b2.idx;
         teta = b2.k1;
         kq = b2.aux;
         alfa = b2.k2;
     } else {
-        q = st->q1;
-        teta = st->teta1;
-        kq = st->kq1;
-        alfa = st->alfa1;
+        q = pi.q1;
+        teta = pi.teta1;
+        kq = pi.kq1;
+        alfa = pi.alfa1;
     }
     if (q == 0) {
         if (lead && threadIdx.x == 0) { st->q = 0; st->stop = ST_Q0; }
         return 0;
     }
-    if (alfa < 1e-5 * (1.0 + 0.01 * big) && !st->rigorous) {
+    if (alfa < 1e-5 * (1.0 + 0.01 * pi.big) && !pi.rigorous) {
         if (lead && threadIdx.x == 0) { st->q = q; st->stop = ST_SMALLPIV; }
         return 0;
     }
     if (lead && threadIdx.x < 64) {
-        if (pse) g = wsum(g);
+        const double g = pse ? wsum(pi.g) : 0.0;
         if (threadIdx.x == 0) {
             if (pse) {
                 const double eta = d.refsp[st->kp - 1] ? 1.0 : 0.0;
@@ -881,12 +988,18 @@ __device__ int dual_pick(const SpxDev &d, int pse, int gn, int ncb, int *kq_out)
             }
             st->q = q;
             st->kq = kq;
-            st->new_dq = (st->delta > 0.0 ? +1.0 : -1.0) * teta;
+            st->new_dq = (pi.delta > 0.0 ? +1.0 : -1.0) * teta;
             st->cbar_q_old = d.cbar[q - 1];
         }
     }
     *kq_out = kq;
     return q;
+}
+
+__device__ __forceinline__ int dual_pick(const SpxDev &d, int pse, int gn, int ncb, int *kq_out)
+{
+    const PickIn pi = pick_load(d, pse, gn, ncb);
+    return pick_resolve(d, pi, pse, kq_out);
 }
 
 // sparse A / rigorous mode: the pick and h = -N[q] in one workgroup
@@ -916,6 +1029,7 @@ __device__ __forceinline__ double aw_value(const SpxDev &d, int c, int awsplits)
 template <int NRHS, int FUSED, int AW>
 __global__ void __launch_bounds__(256) k_dual_ftran(SpxDev d, int tiles, int gn, int awsplits, int ncb)
 {
+    const TraceScope trace_(d, 6);
     DState *st = d.st;
     if (st->stop) return;
     const int m = d.m;
@@ -950,6 +1064,7 @@ __global__ void __launch_bounds__(256) k_dual_ftran(SpxDev d, int tiles, int gn,
 template <int NRHS, int FUSED, int AW>
 __global__ void __launch_bounds__(512) k_dual_ftran_reduce(SpxDev d, int splits, int awsplits)
 {
+    const TraceScope trace_(d, 7);
     __shared__ double sh[NRHS][8][64];
     DState *st = d.st;
     if (st->stop) return;
@@ -1004,9 +1119,10 @@ constexpr int FONE_MAX = 2048;
 template <int NRHS>
 __global__ void __launch_bounds__(1024) k_dual_ftran1(SpxDev d, int gn, int awsplits, int ncb, int nr_cap)
 {
+    const TraceScope trace_(d, 3);
     __shared__ double sp[NRHS][16][64];
     DState *st = d.st;
-    if (st->stop) return;
+    const int stop = st->stop;               // tested before the pick's stores
     const int m = d.m;
     const int lane = threadIdx.x & 63;
     const int w = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
@@ -1016,7 +1132,9 @@ __global__ void __launch_bounds__(1024) k_dual_ftran1(SpxDev d, int gn, int awsp
     const size_t ldb = (size_t)d.ldb;
     const int *__restrict__ rl = d.rlist;
     const double *__restrict__ Bv = d.Binv;
-    // q-independent loads
+    // trip 1: the pick's inputs, the wave's first list entries, this row's
+    // basic variable
+    const PickIn pin = pick_load(d, NRHS == 2, gn, ncb);
     constexpr int G = 8;
     int c0[G];
     double bv[G], wv[G];
@@ -1026,19 +1144,23 @@ __global__ void __launch_bounds__(1024) k_dual_ftran1(SpxDev d, int gn, int awsp
         c0[u] = (t < nr_cap) ? rl[t] : 0;
     }
     const int nr = st->nr;
+    const int kh = (w == 0 && act) ? d.head[r] : m + 1;
+    // trip 2: q-independent inv(B) values and work_c
 #pragma unroll
     for (int u = 0; u < G; ++u) {
         const bool ok = w + u * nw < nr;
         bv[u] = (act && ok) ? Bv[(size_t)c0[u] * ldb + r] : 0.0;
         wv[u] = (NRHS == 2 && ok) ? d.work[c0[u]] : 0.0;
     }
-    const int kh = (w == 0 && act) ? d.head[r] : m + 1;
     double ub = 0.0;
     if (NRHS == 2 && kh <= m) ub = d.work[kh - 1];
+    if (stop) return;
+    TPH(3, 0);
     int kq = 0;
-    const int q = dual_pick(d, NRHS == 2, gn, ncb, &kq);
+    const int q = pick_resolve(d, pin, NRHS == 2, &kq);
     if (!q) return;
     const double *hcol = (kq > m) ? d.A.A + (size_t)(kq - m - 1) * d.A.lda : nullptr;
+    TPH(3, 1);
     auto hval = [&](int c) { return hcol ? hcol[c] : (c == kq - 1 ? -1.0 : 0.0); };
     double ua = 0.0;
     if (kh <= m) ua = hval(kh - 1);
@@ -1079,7 +1201,9 @@ __global__ void __launch_bounds__(1024) k_dual_ftran1(SpxDev d, int gn, int awsp
     }
     sp[0][w][lane] = a;
     if (NRHS == 2) sp[NRHS - 1][w][lane] = b;
+    TPH(3, 2);
     __syncthreads();
+    TPH(3, 3);
     if (w != 0 || !act) return;
     double va = 0.0, vb = 0.0;
     for (int k = 0; k < nw; ++k) {
@@ -1105,10 +1229,13 @@ __global__ void __launch_bounds__(1024) k_dual_ftran1(SpxDev d, int gn, int awsp
 __global__ void __launch_bounds__(256) k_dual_commit(SpxDev d, int pse, int nvb, int tiles, int lpsu, int rowpath,
                                                      double bytes_fixed)
 {
+    const TraceScope trace_(d, 4);
     DState *st = d.st;
-    if (st->stop) return;
+    // all loads first, stop tested before the first store; the pivot indices
+    // are clamped so that the loads of a stopped iteration stay in bounds
+    const int stop = st->stop;
     const int m = d.m, n = d.n;
-    const int p = st->p, q = st->q, kp = st->kp, kq = st->kq;
+    const int p = max(st->p, 1), q = max(st->q, 1), kp = max(st->kp, 1), kq = max(st->kq, 1);
     if ((int)blockIdx.x < nvb) {
         const int i = blockIdx.x * blockDim.x + threadIdx.x;
         // gathers first: the row / column operands and what the next
@@ -1130,7 +1257,7 @@ __global__ void __launch_bounds__(256) k_dual_commit(SpxDev d, int pse, int nvb,
         const bool refk = (pse && in_m) ? d.refsp[kold - 1] != 0 : false;
         const int tknew = in_m ? d.type[knew - 1] : 0;
         const double lbn = in_m ? d.lb[knew - 1] : 0.0, ubn = in_m ? d.ub[knew - 1] : 0.0;
-        const int ot = (st->phase == 1 && in_n) ? d.orig_type[kn - 1] : 0;
+        const int ot = in_n ? d.orig_type[kn - 1] : 0;
         const double xq = (i == p - 1) ? get_xN(d.stat, d.lb, d.ub, kq, q) : 0.0;
         // list maintenance operands (block 0, wave 1)
         const bool maint = (blockIdx.x == 0 && threadIdx.x == 64);
@@ -1143,16 +1270,19 @@ __global__ void __launch_bounds__(256) k_dual_commit(SpxDev d, int pse, int nvb,
             rlast = d.rlist[max(nr0 - 1, 0)];
             if (pse) wlast = d.wlist[max(nwl0 - 1, 0)];
         }
+        const int binv_fresh = st->binv_fresh, rig = st->rigorous, phase = st->phase, refct = st->refct;
+        const double delta = st->delta, new_dq = st->new_dq, gamma_p = st->gamma_pq, eta_p = st->eta_pq;
+        const double tol_bnd = st->tol_bnd, tol_dj = st->tol_dj;
+        if (stop) return;
         const bool bad = fabs(piv1 - piv2) > 1e-8 * (1.0 + fabs(piv1)) ||
                          !((piv1 > 0.0 && piv2 > 0.0) || (piv1 < 0.0 && piv2 < 0.0));
-        if (bad && (!st->binv_fresh || !st->rigorous)) {
+        if (bad && (!binv_fresh || !rig)) {
             if (blockIdx.x == 0 && threadIdx.x == 0) st->stop = ST_PIVCHK;
             return;
         }
+        TPH(4, 0);
         const double tp = bad ? piv2 : piv1;
-        const double delta = st->delta;
         const double teta = delta / tp;
-        const double new_dq = st->new_dq;
         if (in_m) {
             if (i == p - 1) bb = xq + teta;
             else if (teta != 0.0) bb += ti * teta;
@@ -1164,7 +1294,6 @@ __global__ void __launch_bounds__(256) k_dual_commit(SpxDev d, int pse, int nvb,
             d.cbar[i] = cb;
         }
         if (pse && in_m) {
-            const double gamma_p = st->gamma_pq, eta_p = st->eta_pq;
             if (i == p - 1) {
                 if (tkq == FR) g = 1.0;
                 else {
@@ -1198,14 +1327,15 @@ __global__ void __launch_bounds__(256) k_dual_commit(SpxDev d, int pse, int nvb,
         if ((int)blockIdx.x * 256 < m) {
             Cand c = no_cand(0.0);
             if (in_m) {
-                const bool reset = (pse && st->refct == 1);
-                c = chuzr_cand_v(i, knew, tknew, lbn, ubn, bb, reset ? 1.0 : g, st->tol_bnd);
+                const bool reset = (pse && refct == 1);
+                c = chuzr_cand_v(i, knew, tknew, lbn, ubn, bb, reset ? 1.0 : g, tol_bnd);
             }
             const Cand b = wave_best<0>(c);
             if ((threadIdx.x & 63) == 0) cand_chuzr(d)[blockIdx.x * 4 + (threadIdx.x >> 6)] = b;
+            TPH(4, 1);
         }
-        if (st->phase == 1) {
-            const double tol = st->tol_dj;
+        if (phase == 1) {
+            const double tol = tol_dj;
             const int badj = in_n && ((cb < -tol && (ot == LO || ot == FR)) || (cb > +tol && (ot == UP || ot == FR)));
             if (__syncthreads_or(badj) && threadIdx.x == 0) atomicOr(&st->dinf, 1);
         }
@@ -1285,6 +1415,7 @@ __global__ void __launch_bounds__(256) k_dual_commit(SpxDev d, int pse, int nvb,
         rl[u] = (t <= m && u < lpsu) ? d.rho_val[t] : 0.0;
     }
     const int ns = st->ns;
+    const int binv_fresh = st->binv_fresh, rig = st->rigorous;
     const int t1 = min(ns, t0 + lpsu);
     const double piv1 = d.tcol[p - 1], piv2 = d.trow[q - 1];
     const int ce = (kq <= m) ? kq - 1 : -1;
@@ -1292,9 +1423,10 @@ __global__ void __launch_bounds__(256) k_dual_commit(SpxDev d, int pse, int nvb,
 #pragma unroll
     for (int u = 0; u < U; ++u)
         if (t0 + u < t1) v0[u] = *(const double2 *)(d.Binv + (size_t)cc[u] * d.ldb + r);
+    if (stop) return;
     const bool bad = fabs(piv1 - piv2) > 1e-8 * (1.0 + fabs(piv1)) ||
                      !((piv1 > 0.0 && piv2 > 0.0) || (piv1 < 0.0 && piv2 < 0.0));
-    if (bad && (!st->binv_fresh || !st->rigorous)) return;
+    if (bad && (!binv_fresh || !rig)) return;
     const double tp = bad ? piv2 : piv1;
     const bool z0 = (r == p - 1), z1 = (r + 1 == p - 1);
     const double f0 = z0 ? 1.0 / tp : tr0 / tp;
@@ -1456,6 +1588,97 @@ void dual_iteration2(hipStream_t s, const SpxDev &d, const DualPlan &pl, hipEven
     const int nvb = gv;
     hipLaunchKernelGGL(k_dual_commit, dim3(nvb + tiles_m * pl.uchunks), dim3(256), 0, s, d, pl.pse, nvb, tiles_m,
                        pl.lpsu, pl.rowpath, bytes_fixed(d));
+}
+
+// ---------------------------------------------------------------------------
+// inv(B) x and inv(B)' x on the structure of the inverse (dual path, where
+// rlist is maintained): the nr dense columns plus the exact unit columns of
+// the basic slacks.  Used by eval_beta / eval_pi between batches instead of
+// passes over all m columns.
+// ---------------------------------------------------------------------------
+// y[i] = sum_t inv(B)[i, rlist[t]] x[rlist[t]] + (head[i] <= m ? x[head[i] - 1] : 0);
+// 64 rows per block, its waves split the list, partials meet in wave order
+__global__ void __launch_bounds__(1024) k_binv_list(SpxDev d, int nr, const double *__restrict__ x,
+                                                    double *__restrict__ y)
+{
+    __shared__ double sp[16][64];
+    const int m = d.m;
+    const int lane = threadIdx.x & 63;
+    const int w = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+    const int nw = blockDim.x >> 6;
+    const int r = blockIdx.x * 64 + lane;
+    const bool act = r < m;
+    const size_t ldb = (size_t)d.ldb;
+    double acc = 0.0;
+    int t = w;
+    for (; t + 3 * nw < nr; t += 4 * nw) {
+        int c[4];
+        double xv[4], bv[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            c[u] = d.rlist[t + u * nw];
+            xv[u] = x[c[u]];
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) bv[u] = (act && xv[u] != 0.0) ? d.Binv[(size_t)c[u] * ldb + r] : 0.0;
+#pragma unroll
+        for (int u = 0; u < 4; ++u) acc += bv[u] * xv[u];
+    }
+    for (; t < nr; t += nw) {
+        const int c = d.rlist[t];
+        const double xv = x[c];
+        if (act && xv != 0.0) acc += d.Binv[(size_t)c * ldb + r] * xv;
+    }
+    sp[w][lane] = acc;
+    __syncthreads();
+    if (w != 0 || !act) return;
+    double v = 0.0;
+    for (int k = 0; k < nw; ++k) v += sp[k][lane];
+    const int kh = d.head[r];
+    if (kh <= m) v += x[kh - 1];
+    y[r] = v;
+}
+
+// y[c] = inv(B)[:, c]' x: block t < nr — the dense column rlist[t]; the
+// other blocks — the unit columns of the basic slacks (y[head[i] - 1] = x[i])
+__global__ void __launch_bounds__(256) k_binvt_list(SpxDev d, int nr, const double *__restrict__ x,
+                                                    double *__restrict__ y)
+{
+    __shared__ double sh[4];
+    const int m = d.m;
+    if ((int)blockIdx.x < nr) {
+        const int c = d.rlist[blockIdx.x];
+        const double *col = d.Binv + (size_t)c * d.ldb;
+        double acc = 0.0;
+        int r = threadIdx.x * 2;
+        for (; r + 1 < m; r += 512) {
+            const double2 v = *(const double2 *)(col + r);
+            acc += v.x * x[r];
+            acc += v.y * x[r + 1];
+        }
+        if (r < m) acc += col[r] * x[r];
+        acc = wsum(acc);
+        if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = acc;
+        __syncthreads();
+        if (threadIdx.x == 0) y[c] = ((sh[0] + sh[1]) + sh[2]) + sh[3];
+        return;
+    }
+    const int i = (blockIdx.x - nr) * 256 + threadIdx.x;
+    if (i < m) {
+        const int k = d.head[i];
+        if (k <= m) y[k - 1] = x[i];
+    }
+}
+
+void binv_ftran_list(hipStream_t s, const SpxDev &d, int nr, const double *x, double *y)
+{
+    const int nw = nr <= 32 ? 4 : (nr <= 128 ? 8 : 16);
+    hipLaunchKernelGGL(k_binv_list, dim3(cdiv(d.m, 64)), dim3(64 * nw), 0, s, d, nr, x, y);
+}
+
+void binv_btran_list(hipStream_t s, const SpxDev &d, int nr, const double *x, double *y)
+{
+    hipLaunchKernelGGL(k_binvt_list, dim3(nr + cdiv(d.m, 256)), dim3(256), 0, s, d, nr, x, y);
 }
 
 // AT[r*ldt + c] = A[c*lda + r], 64 x 64 tiles through LDS

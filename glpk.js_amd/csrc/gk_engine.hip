@@ -122,8 +122,9 @@ struct Engine {
     std::vector<GraphEntry> graphs;
     unsigned long long graph_clock = 0;
     int kbatch = 8;                           // batch length carried across calls
-    int prof = 0;                             // gk_bfd_profile: events around the pivot-row kernel
+    int prof = 0;                             // gk_bfd_profile: events around the pivot-row kernel (2: + block trace)
     std::vector<hipEvent_t> ev;               // 2 per pivot of the longest batch
+    DBuf<unsigned long long> trace;           // prof == 2: per-kernel, per-block clock stamps of the last pivot
     MatDev mat() const
     {
         MatDev M{};
@@ -139,7 +140,7 @@ struct Engine {
     ~Engine()
     {
         A.release(); AT.release(); rlist.release(); rpos.release(); rho_idx.release(); rho_val.release();
-        gpart.release(); awcnt.release(); tslots.release(); wlist.release(); wpos.release(); cand.release(); awpart.release(); cptr.release(); cind.release(); rptr.release(); rcol.release(); cval.release(); rval.release();
+        gpart.release(); awcnt.release(); tslots.release(); trace.release(); wlist.release(); wpos.release(); cand.release(); awpart.release(); cptr.release(); cind.release(); rptr.release(); rcol.release(); cval.release(); rval.release();
         type.release(); orig_type.release(); stat.release(); refsp.release();
         lb.release(); ub.release(); coef.release(); orig_lb.release(); orig_ub.release(); obj.release();
         head.release(); bind.release();
@@ -427,6 +428,14 @@ struct Spx {
         d.wlist = E->wlist.p; d.wpos = E->wpos.p; d.cand = E->cand.p;
         d.awpart = E->awpart.p; d.awpart_cap = (size_t)AW_SPLITS * m; d.awcnt = E->awcnt.p;
         d.tslots = E->tslots.p;
+        d.trace = nullptr;
+        if (E->prof == 2) {
+            if (!E->trace.p) {
+                E->trace.ensure(TRACE_LEN);
+                HIPCHK(hipMemset(E->trace.p, 0, E->trace.n * sizeof(unsigned long long)));
+            }
+            d.trace = E->trace.p;
+        }
         return d;
     }
 
@@ -486,6 +495,19 @@ struct Spx {
     }
 
     // ---- device computations between batches ------------------------------
+    // y = inv(B) x / inv(B)' x: over the dense columns only in the dual path
+    // (rlist maintained by the pivot kernels), all m columns otherwise
+    static constexpr int LIST_FTRAN_MAX = 2048;
+    void ftran_(const double *x, double *y)
+    {
+        if (dual && hs.nr <= LIST_FTRAN_MAX) binv_ftran_list(s, dev(), hs.nr, x, y);
+        else gemv_n(s, f->Binv.p, m, m, f->ldb, x, E->partial.p, PARTIAL_CAP, y, 1.0, nullptr, 0.0);
+    }
+    void btran_(const double *x, double *y)
+    {
+        if (dual) binv_btran_list(s, dev(), hs.nr, x, y);
+        else gemv_t(s, f->Binv.p, m, m, f->ldb, x, y, 1.0);
+    }
     // eval_cbar (glpspx01.js:565): pi = inv(B') cB refined once, d_j = c_k - N_j' pi
     void eval_cbar()
     {
@@ -495,9 +517,9 @@ struct Spx {
         MatDev A = E->mat();
         double *cB = E->r1.p, *pi = E->u.p, *r = E->r2.p, *dd = E->work.p;
         cb_vector(s, m, E->head.p, E->coef.p, cB);
-        gemv_t(s, f->Binv.p, m, m, f->ldb, cB, pi, 1.0);
+        btran_(cB, pi);
         colpass(s, A, CP_RESID, 0, m, E->head.p, E->stat.p, E->coef.p, cB, pi, nullptr, r, nullptr, nullptr);
-        gemv_t(s, f->Binv.p, m, m, f->ldb, r, dd, 1.0);
+        btran_(r, dd);
         vec_axpy(s, pi, dd, 1.0, m);
         colpass(s, A, CP_CBAR, m, n, E->head.p, E->stat.p, E->coef.p, nullptr, pi, nullptr, E->cbar.p, nullptr, nullptr);
         (void)d;
@@ -520,13 +542,13 @@ struct Spx {
         fill_d(s, wc, 0.0, n);
         scatter_pos(s, m, m, n, E->head.p, w, ys, wc);
         aprod_neg(s, A, wc, ys, h, E->partial.p, PARTIAL_CAP);                  // h = ys - A wc
-        gemv_n(s, f->Binv.p, m, m, f->ldb, h, E->partial.p, PARTIAL_CAP, beta, 1.0, nullptr, 0.0);
+        ftran_(h, beta);
         fill_d(s, ys, 0.0, m);
         fill_d(s, wc, 0.0, n);
         scatter_pos(s, m, 0, m, E->head.p, beta, ys, wc);
         aprod_neg(s, A, wc, ys, t, E->partial.p, PARTIAL_CAP);                  // t = B beta
         rsub_into(t, h);                                                       // t = h - B beta
-        gemv_n(s, f->Binv.p, m, m, f->ldb, t, E->partial.p, PARTIAL_CAP, dd, 1.0, nullptr, 0.0);
+        ftran_(t, dd);
         vec_axpy(s, beta, dd, 1.0, m);
         down(bbar, E->bbar, m);
         sync();
@@ -1408,7 +1430,15 @@ void gk_bfd_last_stats(const gk_bfd *f, gk_spx_stats *st)
 
 void gk_bfd_profile(gk_bfd *f, int enable)
 {
-    if (f) f->prof = enable ? 1 : 0;
+    if (f) f->prof = enable == 2 ? 2 : (enable ? 1 : 0);
+}
+
+int gk_bfd_trace(gk_bfd *f, unsigned long long *out, size_t cnt)
+{
+    if (!f || !out || !f->eng || !f->eng->trace.p) return 0;
+    const size_t nn = std::min(cnt, f->eng->trace.n);
+    if (hipMemcpy(out, f->eng->trace.p, nn * sizeof(unsigned long long), hipMemcpyDeviceToHost) != hipSuccess) return 0;
+    return (int)nn;
 }
 
 static void bfd_prepare(gk_bfd *f, int m)

@@ -136,7 +136,11 @@ struct SpxDev {
     size_t awpart_cap;
     int *awcnt;                              // per 512-row tile: arrivals of the A w splits (the last one reduces)
     unsigned long long *tslots;              // per-block end stamps of the pivot-row kernel
+    unsigned long long *trace;               // profiling only: per-kernel, per-block entry / exit clock
 };
+constexpr int TRACE_KERNELS = 8, TRACE_BLOCKS = 2048;   // trace[(kid * TRACE_BLOCKS + block) * 2 + {0, 1}]
+constexpr int TRACE_PHASES = 8;   // then phase stamps of wave 0: [TRACE_KERNELS * TRACE_BLOCKS * 2 + (kid * TRACE_BLOCKS + block) * 8 + ph]
+constexpr size_t TRACE_LEN = (size_t)TRACE_KERNELS * TRACE_BLOCKS * (2 + TRACE_PHASES);
 
 // launch geometry of one device batch, fixed on the host from nr at batch start
 struct DualPlan {
@@ -161,6 +165,10 @@ void dual_iteration2(hipStream_t s, const SpxDev &d, const DualPlan &pl, hipEven
 void transpose_dense(hipStream_t s, const double *A, int m, int n, int lda, double *AT, int ldt);
 // timing hook: the row-path pivot-row kernel alone (returns algorithmic bytes)
 double launch_trow_rows(hipStream_t s, const SpxDev &d, const DualPlan &pl, int ns);
+// y = inv(B) x and y = inv(B)' x over the nr dense columns of rlist and the
+// unit columns of the basic slacks (valid while rlist is maintained: dual path)
+void binv_ftran_list(hipStream_t s, const SpxDev &d, int nr, const double *x, double *y);
+void binv_btran_list(hipStream_t s, const SpxDev &d, int nr, const double *x, double *y);
 
 void primal_iteration(hipStream_t s, const SpxDev &d, int pse, int rigorous);
 void launch_reset_refsp(hipStream_t s, const SpxDev &d, int dual);

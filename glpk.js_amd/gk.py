@@ -144,6 +144,8 @@ def load_library(path: str = LIB_PATH):
     L.gk_ios_driver_sharded.restype = C.c_int
     L.gk_bfd_profile.argtypes = [P, C.c_int]
     L.gk_bfd_profile.restype = None
+    L.gk_bfd_trace.argtypes = [P, C.c_void_p, C.c_size_t]
+    L.gk_bfd_trace.restype = C.c_int
     L.gk_bfd_time_kernel.argtypes = [P, C.c_int, C.c_int, C.POINTER(C.c_double)]
     L.gk_bfd_time_kernel.restype = C.c_double
     _lib = L
@@ -369,9 +371,19 @@ class GkProblem:
             raise GkError(_err(self.L))
         return ms, b.value
 
-    def profile(self, enable: bool = True):
-        """Record HIP events around the pivot-row kernel of every dual pivot."""
-        self.L.gk_bfd_profile(self.bfd, 1 if enable else 0)
+    def profile(self, enable=True):
+        """Record HIP events around the pivot-row kernel of every dual pivot
+        (enable == 2: also per-block device clock stamps, see trace())."""
+        self.L.gk_bfd_profile(self.bfd, 2 if enable == 2 else (1 if enable else 0))
+
+    def trace(self) -> np.ndarray:
+        """Per-kernel, per-block [entry, exit] device clock stamps of the last
+        pivot (profile(2)); shape (8 kernels, 2048 blocks, 2).  The phase
+        stamps that follow them are kept in self.trace_raw."""
+        out = np.zeros(8 * 2048 * 10, dtype=np.uint64)
+        self.L.gk_bfd_trace(self.bfd, out.ctypes.data_as(C.c_void_p), out.size)
+        self.trace_raw = out
+        return out[:8 * 2048 * 2].reshape(8, 2048, 2)
 
     def stats(self) -> SpxStats:
         st = SpxStats()

@@ -144,6 +144,12 @@ typedef struct {
 void gk_bfd_last_stats(const gk_bfd *bfd, gk_spx_stats *st);
 /* record HIP events around the pivot-row kernel of every dual pivot (benches) */
 void gk_bfd_profile(gk_bfd *bfd, int enable);
+/* profiling aid (enable == 2 above): copies the per-kernel, per-block device
+ * clock stamps of the last pivot, trace[(kernel * 2048 + block) * 2 + {0 entry,
+ * 1 exit}], kernels 0 top, 1 pivot row, 2 ratio, 3 FTRAN (one kernel), 4 commit,
+ * 5 row finish (column path), 6 FTRAN (split), 7 FTRAN reduce; returns the
+ * number of entries copied (0 when tracing was never enabled) */
+int gk_bfd_trace(gk_bfd *bfd, unsigned long long *out, size_t cnt);
 
 /* measurement hook for bench.py (not part of the reference interface):
  * launch one engine kernel `reps` times on the problem left resident by the

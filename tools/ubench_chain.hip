@@ -53,6 +53,14 @@ __global__ void k_chain8(const int *__restrict__ idx, const double *__restrict__
     out[blockIdx.x * blockDim.x + threadIdx.x] = v;
 }
 
+// producer: rewrites the index table (a permutation step) so that the
+// consumer's loads find fresh data written by another kernel (other XCDs)
+__global__ void k_produce(int *idx, int n, int salt)
+{
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) idx[i] = (int)(((unsigned)i * 2654435761u + (unsigned)salt * 40503u) & (unsigned)(n - 1));
+}
+
 struct V {
     const char *name;
     void (*fn)(const int *, const double *, double *, int);
@@ -103,6 +111,37 @@ int main()
             best = ms < best ? ms : best;
         }
         printf("%-20s %7.2f us/kernel\n", v.name, 1000.0 * best / reps);
+        (void)hipGraphExecDestroy(ge); (void)hipGraphDestroy(g);
+    }
+    // producer / consumer pairs: D dependent trips over data the previous
+    // kernel wrote
+    struct P { const char *name; void (*fn)(const int *, const double *, double *, int); int blocks, threads; };
+    P ps[] = {
+        {"pair D0  96x256", k_chain<0, 0>, 96, 256},
+        {"pair D1  96x256", k_chain<1, 0>, 96, 256},
+        {"pair D2  96x256", k_chain<2, 0>, 96, 256},
+        {"pair D4  96x256", k_chain<4, 0>, 96, 256},
+        {"pair D1   1x256", k_chain<1, 0>, 1, 256},
+        {"pair D4   1x256", k_chain<4, 0>, 1, 256},
+    };
+    for (const P &v : ps) {
+        hipGraph_t g; hipGraphExec_t ge;
+        CHK(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
+        for (int r = 0; r < reps; ++r) {
+            hipLaunchKernelGGL(k_produce, dim3(n / 256), dim3(256), 0, s, idx, n, r);
+            hipLaunchKernelGGL(v.fn, dim3(v.blocks), dim3(v.threads), 0, s, idx, val, out, n);
+        }
+        CHK(hipStreamEndCapture(s, &g));
+        CHK(hipGraphInstantiate(&ge, g, nullptr, nullptr, 0));
+        CHK(hipGraphLaunch(ge, s)); CHK(hipStreamSynchronize(s));
+        hipEvent_t e0, e1; CHK(hipEventCreate(&e0)); CHK(hipEventCreate(&e1));
+        float best = 1e30f;
+        for (int k = 0; k < 3; ++k) {
+            CHK(hipEventRecord(e0, s)); CHK(hipGraphLaunch(ge, s)); CHK(hipEventRecord(e1, s)); CHK(hipEventSynchronize(e1));
+            float ms; CHK(hipEventElapsedTime(&ms, e0, e1));
+            best = ms < best ? ms : best;
+        }
+        printf("%-20s %7.2f us/pair\n", v.name, 1000.0 * best / reps);
         (void)hipGraphExecDestroy(ge); (void)hipGraphDestroy(g);
     }
     return 0;
