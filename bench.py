@@ -26,7 +26,7 @@ sys.path.insert(0, ROOT)
 import __graft_entry__  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
-ROOF_KERNEL = "k_trow_rows"
+ROOF_KERNEL = "k_dual_row"
 
 
 def log(rank, *a):
@@ -171,8 +171,8 @@ def main():
                 traffic = None
         roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                "kernel": ROOF_KERNEL + " (pivot row trow = -rho' N over the rows of A in the support of rho, "
-                                        "fused with the ratio-test candidates)",
+                "kernel": ROOF_KERNEL + " (chuzr, rho = row p of inv(B), pivot row trow = -rho' N over the rows "
+                                        "of A in the support of rho, ratio-test candidates: one kernel)",
                 "ms_per_launch": round(ms, 5), "launches": dev["launches"],
                 "bytes_per_launch": round(b),
                 "timing": "device wall clock (s_memrealtime) over every launch of the timed region, entry to next entry",

@@ -785,6 +785,222 @@ __global__ void __launch_bounds__(1024) k_trow_rows(SpxDev d, int pse)
 }
 
 // ---------------------------------------------------------------------------
+// k_dual_row (row path, dense A): k_dual_top and k_trow_rows in ONE kernel.
+// Every block makes the chuzr choice itself (wave reduction over the
+// commit's per-wave candidates, the leaving variable in aux), reads its rho
+// entries straight from inv(B) (rho_t = inv(B)[p, rlist[t]], plus the unit
+// entry 1 at row kp - 1 when the leaving variable is a slack) and forms its
+// 64 slots of the pivot row.  The pending change of basis of the previous
+// pivot is applied by block 0; the other blocks patch the few entries it
+// changes (bind of kp / kq, stat of q, refsp of kp) where they read them, so
+// the race with block 0's writes is benign (the patch is idempotent).  Block
+// 0 also publishes the compact rho (rho_idx / rho_val, read by the commit),
+// the scalar state and, every 1000 pivots, the reference-space reset.
+// ---------------------------------------------------------------------------
+__global__ void __launch_bounds__(1024) k_dual_row(SpxDev d, int pse, int nr_cap)
+{
+    const TraceScope trace_(d, 1);
+    __shared__ double sp[16][64];
+    DState *st = d.st;
+    const int m = d.m, n = d.n;
+    const int lane = threadIdx.x & 63;
+    const int w = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+    const int nw = blockDim.x >> 6;
+    const int idx = blockIdx.x * 64 + lane;
+    const bool lead = (blockIdx.x == 0);
+    // ---- trip 1: state, chuzr candidates, the wave's list entries, slots
+    const int stop = st->stop;
+    const FinishIn fin = finish_load(d);
+    const int pricing = st->pricing, phase = st->phase, dinf = st->dinf, nr = st->nr;
+    const double zeta = st->zeta, obj_ll = st->obj_ll, obj_ul = st->obj_ul;
+    const RatioIn rin = ratio_in(st);
+    const int gm = 4 * ((m + 255) / 256);
+    Cand cc = no_cand(0.0);
+    for (int b = lane; b < gm; b += 64) {
+        const Cand e = cand_chuzr(d)[b];
+        if (better<0>(e, cc)) cc = e;
+    }
+    int c0[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+        const int t = w + u * nw;
+        c0[u] = (t < nr_cap) ? d.rlist[t] : 0;
+    }
+    int pos1 = 0, pos2 = 0;
+    if (w == 0) {
+        pos1 = (idx < n) ? d.bind[m + idx] : 0;
+        pos2 = (idx < m) ? d.bind[idx] : 0;
+    }
+    if (stop) return;
+    if (lead && threadIdx.x == 0) st->tk_start = wall_clock64();
+    // ---- decisions (identical in every block)
+    const TopState ts = fin.t;
+    int why = ST_RUN;
+    if (ts.iter_left <= 0 || ts.refact) why = ts.refact ? ST_REFACT : ST_BATCH;
+    else if (phase == 1 && !dinf) why = ST_PHASE;
+    else if (phase != 1 && ((zeta < 0.0 && obj_ll > -DBL_MAX && ts.obj <= obj_ll) ||
+                            (zeta > 0.0 && obj_ul < +DBL_MAX && ts.obj >= obj_ul)))
+        why = ST_OBJLIM;
+    const Cand best = wave_best<0>(cc);
+    if (why == ST_RUN && best.idx == 0) why = ST_P0;
+    const bool reset = (why == ST_RUN && pricing == PT_PSE && ts.refct == 0);
+    if (lead) {
+        (void)finish_apply(d, fin, true);
+        if (why != ST_RUN) {
+            if (threadIdx.x == 0) {
+                if (why == ST_P0) st->p = 0;
+                st->stop = why;
+            }
+            return;
+        }
+        if (reset) {
+            reset_refsp_dev(d, 1);            // refsp := basic variables, gamma := 1
+            for (int l = threadIdx.x; l < n; l += blockDim.x) d.wpos[l] = -1;
+            if (threadIdx.x == 0) st->nwl = 0;
+        }
+    }
+    if (why != ST_RUN) return;
+    const int p = best.idx, kp = best.aux;
+    const int ns = nr + (kp <= m ? 1 : 0);
+    // the pending change of basis, as seen by this block
+    auto bind_new = [&](int k1, int v) {
+        if (!fin.pend) return v;
+        if (k1 == fin.kq) return fin.p;
+        if (k1 == fin.kp) return m + fin.q;
+        return v;
+    };
+    // only slots that exist (structural idx < n, slack idx < m) and only in
+    // wave 0, which holds the positions
+    if (w == 0 && idx < n) pos1 = bind_new(m + idx + 1, pos1);
+    if (w == 0 && idx < m) pos2 = bind_new(idx + 1, pos2);
+    const int j1 = (pos1 > m) ? pos1 - m - 1 : -1;
+    const int j2 = (pos2 > m) ? pos2 - m - 1 : -1;
+    // ---- trip 2: rho entries of the wave and their rows of AT; slot operands
+    const double *__restrict__ brow = d.Binv + (p - 1);
+    const size_t ldb = (size_t)d.ldb;
+    const double *__restrict__ col = d.A.AT + min(idx, n - 1);
+    const size_t ldt = (size_t)d.A.ldt;
+    double v0[8], a0[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+        const int t = w + u * nw;
+        int c = c0[u];
+        if (t == nr) c = kp - 1;             // the unit entry (only when kp <= m: t < ns)
+        v0[u] = (t < nr) ? brow[(size_t)c * ldb] : 1.0;
+        a0[u] = (t < ns) ? col[(size_t)c * ldt] : 0.0;
+        c0[u] = c;
+    }
+    const signed char stq = fin.fxp ? NS : (fin.delta > 0.0 ? NL : NU);
+    int s1 = 0, s2 = 0;
+    double cb1 = 0.0, cb2 = 0.0, rho2 = 0.0;
+    bool ref1 = false, ref2 = false;
+    if (j1 >= 0) {
+        s1 = (fin.pend && j1 == fin.q - 1) ? stq : d.stat[j1];
+        cb1 = d.cbar[j1];
+        if (pse && !reset) ref1 = d.refsp[m + idx] != 0 && !(fin.pend && fin.rclr && m + idx + 1 == fin.kp);
+    }
+    if (j2 >= 0) {
+        s2 = (fin.pend && j2 == fin.q - 1) ? stq : d.stat[j2];
+        cb2 = d.cbar[j2];
+        rho2 = brow[(size_t)idx * ldb];      // a non-basic slack: column idx of inv(B) is dense
+        if (pse && !reset) ref2 = d.refsp[idx] != 0 && !(fin.pend && fin.rclr && idx + 1 == fin.kp);
+    }
+    double acc = 0.0;
+#pragma unroll
+    for (int u = 0; u < 8; ++u)
+        if (w + u * nw < ns) acc += v0[u] * a0[u];
+    if (lead && lane == 0) {
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            const int t = w + u * nw;
+            if (t < ns) {
+                d.rho_idx[t] = c0[u];
+                d.rho_val[t] = v0[u];
+            }
+        }
+    }
+    TPH(1, 0);
+    {
+        int t = w + 8 * nw;
+        for (; t < ns; t += 4 * nw) {
+            int c[4];
+            double v[4], a[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const int tt = t + u * nw;
+                c[u] = (tt < nr) ? d.rlist[tt] : kp - 1;
+            }
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const int tt = t + u * nw;
+                v[u] = (tt < nr) ? brow[(size_t)c[u] * ldb] : 1.0;
+                a[u] = (tt < ns) ? col[(size_t)c[u] * ldt] : 0.0;
+            }
+#pragma unroll
+            for (int u = 0; u < 4; ++u)
+                if (t + u * nw < ns) acc += v[u] * a[u];
+            if (lead && lane == 0) {
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    const int tt = t + u * nw;
+                    if (tt < ns) {
+                        d.rho_idx[tt] = c[u];
+                        d.rho_val[tt] = v[u];
+                    }
+                }
+            }
+        }
+    }
+    TPH(1, 1);
+    sp[w][lane] = (idx < n) ? acc : 0.0;
+    __syncthreads();
+    TPH(1, 2);
+    if (w != 0) return;                      // wave 0 only from here: no block barriers
+    if (lead && lane == 0) {
+        st->p = p;
+        st->kp = kp;
+        st->delta = best.k2;
+        st->trow_max_bits = 0ull;
+        st->ns = ns;
+        st->dinf = 0;
+    }
+    double tsum = 0.0;
+    for (int k = 0; k < nw; ++k) tsum += sp[k][lane];
+    double tv1 = (j1 >= 0) ? tsum : 0.0;
+    double tv2 = (j2 >= 0) ? -rho2 : 0.0;
+    if (s1 == NS) tv1 = 0.0;
+    if (s2 == NS) tv2 = 0.0;
+    if (j1 >= 0) d.trow[j1] = tv1;
+    if (j2 >= 0) d.trow[j2] = tv2;
+    double gsum = 0.0;
+    if (pse) {
+        const double w1 = ref1 ? tv1 : 0.0, w2 = ref2 ? tv2 : 0.0;
+        if (idx < n) d.wcol[idx] = w1;
+        if (idx < m) d.ys[idx] = w2;
+        gsum = w1 * w1 + w2 * w2;
+    }
+    const double bmax = wmax(fmax(fabs(tv1), fabs(tv2)));
+    const double g = pse ? wsum(gsum) : 0.0;
+    // pass-1 candidate with eps_b = tol_bnd (1 + 0.01 max_b) <= eps; the
+    // sign of delta is that of the chosen row
+    RatioIn rin2 = rin;
+    rin2.delta = best.k2;
+    const RatioCtx x = ratio_ctx(rin2, bmax);
+    Cand c = no_cand(DBL_MAX);
+    Cand e;
+    if (j1 >= 0 && pass1_cand(x, tv1, cb1, s1, j1, m + idx + 1, e) && better<1>(e, c)) c = e;
+    if (j2 >= 0 && pass1_cand(x, tv2, cb2, s2, j2, idx + 1, e) && better<1>(e, c)) c = e;
+    const Cand b = wave_best<1>(c);
+    TPH(1, 5);
+    if (lane == 0) {
+        tmax_part(d)[blockIdx.x] = bmax;
+        if (pse) d.gpart[blockIdx.x] = g;
+        cand_pass1(d)[blockIdx.x] = b;
+        d.tslots[blockIdx.x] = wall_clock64();
+    }
+}
+
+// ---------------------------------------------------------------------------
 // k_dual_ratio: blocks [0, gn) — pass-1 choice from the ncb group candidates
 // (a group whose candidate fails the global significance tolerance is
 // rescanned), then the pass-2 candidates of positions [256 b, 256 b + 256),
@@ -1543,15 +1759,16 @@ void dual_iteration2(hipStream_t s, const SpxDev &d, const DualPlan &pl, hipEven
 {
     const int m = d.m, n = d.n;
     const int gv = cdiv(std::max(m, n), 256), gn = cdiv(n, 256), tiles_m = cdiv(m, 512);
-    hipLaunchKernelGGL(k_dual_top, dim3(1), dim3(TOP_WG), 0, s, d, pl.rowpath, pl.nr_cap);
-    if (pl.rigorous) refine_rho_dev(s, d);
     int ncb = 4 * gv;                                  // 64-slot groups of the pivot row
     if (pl.rowpath) {
+        // chuzr, rho and the pivot row in one kernel
         ncb = cdiv(std::max(m, n), 64);
         if (ev0) (void)hipEventRecord(ev0, s);
-        hipLaunchKernelGGL(k_trow_rows, dim3(ncb), dim3(64 * pl.twaves), 0, s, d, pl.pse);
+        hipLaunchKernelGGL(k_dual_row, dim3(ncb), dim3(64 * pl.twaves), 0, s, d, pl.pse, pl.nr_cap);
         if (ev1) (void)hipEventRecord(ev1, s);
     } else {
+        hipLaunchKernelGGL(k_dual_top, dim3(1), dim3(TOP_WG), 0, s, d, pl.rowpath, pl.nr_cap);
+        if (pl.rigorous) refine_rho_dev(s, d);
         if (ev0) (void)hipEventRecord(ev0, s);
         colpass_gated(s, d.A, CP_TROW, m, n, d.head, d.stat, d.coef, nullptr, d.rho, nullptr, d.trow, nullptr,
                       &d.st->trow_max_bits, d.st, 0);

@@ -16,7 +16,7 @@ import __graft_entry__  # noqa: E402
 __graft_entry__.load_package()
 from glpk_js_amd import gk, problems  # noqa: E402
 
-NAMES = ["top", "trow_rows", "ratio", "ftran1", "commit", "trow_finish", "ftran_split", "ftran_reduce"]
+NAMES = ["top", "row", "ratio", "ftran1", "commit", "trow_finish", "ftran_split", "ftran_reduce"]
 
 
 def main():
