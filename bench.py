@@ -98,6 +98,7 @@ def main():
 
     for _ in range(args.warmup):
         step()
+    ctx.mark(1)                         # timed region starts (kernel-trace window)
     barrier()
     t0 = time.perf_counter()
     piv = 0
@@ -116,6 +117,7 @@ def main():
         dev["bytes"] += s_.trow_bytes
     barrier()
     dt = time.perf_counter() - t0
+    ctx.mark(2)                         # timed region ends
     st = P.stats()
 
     # cross-check pass: the same number of steps again with HIP events
@@ -162,13 +164,20 @@ def main():
         b = dev["bytes"] / nl
         achieved = b / (ms * 1e-3) / 1e9 if ms > 0 else 0.0
         ne = max(1, trow["launches"])
-        traffic = None
+        # committed profiles of the same command (tools/profile_round.sh):
+        # HBM bytes per launch from the --pmc passes and rocprofv3's own
+        # average duration, both over the timed region only (k_gk_mark window)
+        traffic = rocprof_ms = None
         tpath = os.path.join(ROOT, "profiles", "r01_pmc_traffic.json")
-        if os.path.exists(tpath):
-            try:
-                traffic = json.load(open(tpath))["kernels"].get(ROOF_KERNEL, {}).get("bytes_per_launch")
-            except Exception:
-                traffic = None
+        spath = os.path.join(ROOT, "profiles", "r01_kernel_stats_timed.json")
+        try:
+            traffic = json.load(open(tpath))["kernels"].get(ROOF_KERNEL, {}).get("bytes_per_launch")
+        except Exception:
+            traffic = None
+        try:
+            rocprof_ms = json.load(open(spath))[ROOF_KERNEL]["avg_ns"] / 1e6
+        except Exception:
+            rocprof_ms = None
         roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                 "kernel": ROOF_KERNEL + " (chuzr, rho = row p of inv(B), pivot row trow = -rho' N over the rows "
@@ -181,7 +190,11 @@ def main():
                 "hip_events_cross_check": {"ms_per_launch": round(trow["ms"] / ne, 5), "launches": trow["launches"],
                                            "bytes_per_launch": round(trow["bytes"] / ne),
                                            "note": "second pass, eager launches, interval includes launch gap"},
-                "traffic_source": "profiles/r01_pmc_traffic.json (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes)"}
+                "traffic_source": "profiles/r01_pmc_traffic.json (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes, "
+                                  "timed region only)",
+                "rocprof_ms_per_launch": round(rocprof_ms, 5) if rocprof_ms else None,
+                "rocprof_source": "profiles/r01_kernel_stats_timed.json (rocprofv3 --kernel-trace of this command, "
+                                  "timed region; includes the profiler's per-dispatch overhead, DESIGN.md §5)"}
 
     cpu = None
     extra = {}

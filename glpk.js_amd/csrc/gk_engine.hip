@@ -116,6 +116,8 @@ struct Engine {
     DBuf<double> bbar, cbar, gamma, tcol, trow, rho, rowp, u, s, h, wcol, ys, work, r1, r2, partial;
     DBuf<DState> st;
     DState *st_host = nullptr;              // pinned staging copy of st (hipHostMalloc)
+    char *pin = nullptr;                     // pinned staging of the per-call host <-> device copies
+    size_t pin_cap = 0;
     DBuf<int> rlist, rpos, rho_idx, wlist, wpos, awcnt;
     DBuf<double> rho_val, gpart, cand, awpart;
     DBuf<unsigned long long> tslots;
@@ -148,6 +150,7 @@ struct Engine {
         u.release(); s.release(); h.release(); wcol.release(); ys.release(); work.release(); r1.release(); r2.release();
         partial.release(); st.release();
         if (st_host) (void)hipHostFree(st_host);
+        if (pin) (void)hipHostFree(pin);
         for (auto &g : graphs)
             if (g.exec) (void)hipGraphExecDestroy(g.exec);
         for (auto e : ev) (void)hipEventDestroy(e);
@@ -299,6 +302,16 @@ static void engine_alloc(Engine &E, int m, int n)
     E.partial.ensure(PARTIAL_CAP);
     E.st.ensure(1);
     if (!E.st_host) HIPCHK(hipHostMalloc((void **)&E.st_host, sizeof(DState), hipHostMallocDefault));
+    {
+        const size_t need = std::max<size_t>((size_t)8 << 20, (size_t)32 * ((size_t)m + n + 1) * sizeof(double));
+        if (E.pin_cap < need) {
+            if (E.pin) (void)hipHostFree(E.pin);
+            E.pin = nullptr;
+            E.pin_cap = 0;
+            HIPCHK(hipHostMalloc((void **)&E.pin, need, hipHostMallocDefault));
+            E.pin_cap = need;
+        }
+    }
     E.rlist.ensure(m); E.rpos.ensure(m); E.rho_idx.ensure((size_t)m + 1); E.rho_val.ensure((size_t)m + 1);
     const size_t gv = (size_t)(std::max(m, n) + 255) / 256 + 1;
     E.gpart.ensure(8 * (size_t)gv);              // gamma_p sums, then per-block max |trow| (64-slot blocks)
@@ -442,14 +455,55 @@ struct Spx {
     template <typename T>
     void up(DBuf<T> &d, const std::vector<T> &h, size_t cnt)
     {
-        HIPCHK(hipMemcpyAsync(d.p, h.data() + 1, cnt * sizeof(T), hipMemcpyHostToDevice, s));
+        // through the pinned staging buffer: the host data is taken now, the
+        // copy itself is asynchronous
+        const size_t bytes = cnt * sizeof(T);
+        char *stage = pin_take(bytes);
+        if (!stage) {
+            HIPCHK(hipMemcpyAsync(d.p, h.data() + 1, bytes, hipMemcpyHostToDevice, s));
+            return;
+        }
+        std::memcpy(stage, h.data() + 1, bytes);
+        HIPCHK(hipMemcpyAsync(d.p, stage, bytes, hipMemcpyHostToDevice, s));
     }
     template <typename T>
     void down(std::vector<T> &h, const DBuf<T> &d, size_t cnt)
     {
-        HIPCHK(hipMemcpyAsync(h.data() + 1, d.p, cnt * sizeof(T), hipMemcpyDeviceToHost, s));
+        // into the pinned staging buffer; the host vector is filled by the
+        // sync() that every download is followed by
+        const size_t bytes = cnt * sizeof(T);
+        char *stage = pin_take(bytes);
+        if (!stage) {
+            HIPCHK(hipMemcpyAsync(h.data() + 1, d.p, bytes, hipMemcpyDeviceToHost, s));
+            return;
+        }
+        HIPCHK(hipMemcpyAsync(stage, d.p, bytes, hipMemcpyDeviceToHost, s));
+        pending.push_back(Pending{(void *)(h.data() + 1), stage, bytes});
     }
-    void sync() { HIPCHK(hipStreamSynchronize(s)); f->stats.host_syncs++; }
+    struct Pending {
+        void *dst;
+        const char *src;
+        size_t bytes;
+    };
+    std::vector<Pending> pending;
+    size_t pin_off = 0;
+    char *pin_take(size_t bytes)
+    {
+        const size_t need = (bytes + 255) & ~(size_t)255;
+        if (need > E->pin_cap) return nullptr;
+        if (pin_off + need > E->pin_cap) sync();
+        char *p = E->pin + pin_off;
+        pin_off += need;
+        return p;
+    }
+    void sync()
+    {
+        HIPCHK(hipStreamSynchronize(s));
+        f->stats.host_syncs++;
+        for (const Pending &q : pending) std::memcpy(q.dst, q.src, q.bytes);
+        pending.clear();
+        pin_off = 0;
+    }
 
     // bring the host mirrors of the pivot-updated arrays up to date
     void pull()
@@ -1713,6 +1767,18 @@ extern "C" double gk_bfd_time_kernel(gk_bfd *f, int which, int reps, double *byt
 }
 
 // accessors for the other translation units (gk_mip.hip)
+__global__ void k_gk_mark(int tag, int *sink)
+{
+    if (tag < 0 && sink) sink[0] = tag;      // never taken: the launch itself is the marker
+}
+
+int gk_ctx_mark(gk_ctx *c, int tag)
+{
+    if (!c) return GK_EABI;
+    hipLaunchKernelGGL(k_gk_mark, dim3(1), dim3(64), 0, c->stream, tag, (int *)nullptr);
+    return hipGetLastError() == hipSuccess ? 0 : GK_EABI;
+}
+
 int gk_ctx_device(gk_ctx *c) { return c->device; }
 hipStream_t gk_ctx_stream(gk_ctx *c) { return c->stream; }
 namespace gk {

@@ -38,40 +38,61 @@ __global__ void __launch_bounds__(256) k_gemv_n_part(const double *__restrict__ 
                                                        double *__restrict__ part, const DState *st, int need_p)
 {
     GATE(st, need_p);
+    // the split's multipliers are read once per block, 256 at a time, and
+    // the non-zero ones compacted in LDS (ballot + wave prefix), so the
+    // column loop touches only columns with x_c != 0, in column order
+    __shared__ double sxv[256];
+    __shared__ int scol[256];
+    __shared__ int swcnt[4];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int r = (blockIdx.x * 256 + threadIdx.x) * 2;
     const int c0 = blockIdx.y * cps;
     const int c1 = min(cols, c0 + cps);
+    const bool act = r < rows, two = (r + 1 < rows);
     double a0 = 0.0, a1 = 0.0;
-    if (r < rows) {
-        const bool two = (r + 1 < rows);
-        int c = c0;
-        for (; c + 4 <= c1; c += 4) {
-            const double x0 = x[c], x1 = x[c + 1], x2 = x[c + 2], x3 = x[c + 3];
-            if (x0 == 0.0 && x1 == 0.0 && x2 == 0.0 && x3 == 0.0) continue;
-            const double *p0 = M + (size_t)c * ld + r;
-            if (two) {
-                double2 v0 = *(const double2 *)(p0);
-                double2 v1 = *(const double2 *)(p0 + ld);
-                double2 v2 = *(const double2 *)(p0 + 2 * (size_t)ld);
-                double2 v3 = *(const double2 *)(p0 + 3 * (size_t)ld);
-                a0 += v0.x * x0; a1 += v0.y * x0;
-                a0 += v1.x * x1; a1 += v1.y * x1;
-                a0 += v2.x * x2; a1 += v2.y * x2;
-                a0 += v3.x * x3; a1 += v3.y * x3;
-            } else {
-                a0 += p0[0] * x0; a0 += p0[ld] * x1; a0 += p0[2 * (size_t)ld] * x2; a0 += p0[3 * (size_t)ld] * x3;
+    for (int cb = c0; cb < c1; cb += 256) {
+        const int c = cb + threadIdx.x;
+        const double xv = (c < c1) ? x[c] : 0.0;
+        const bool nz = xv != 0.0;
+        const unsigned long long bal = __ballot(nz);
+        const int below = __popcll(bal & ((1ull << lane) - 1ull));
+        if (lane == 0) swcnt[w] = __popcll(bal);
+        __syncthreads();
+        int off = 0, tot = 0;
+        for (int k = 0; k < 4; ++k) {
+            if (k < w) off += swcnt[k];
+            tot += swcnt[k];
+        }
+        if (nz) {
+            sxv[off + below] = xv;
+            scol[off + below] = c;
+        }
+        __syncthreads();
+        if (act) {
+            int k = 0;
+            for (; k + 4 <= tot; k += 4) {
+                double2 v[4];
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    const double *p0 = M + (size_t)scol[k + u] * ld + r;
+                    v[u] = two ? *(const double2 *)p0 : make_double2(p0[0], 0.0);
+                }
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    a0 += v[u].x * sxv[k + u];
+                    a1 += v[u].y * sxv[k + u];
+                }
+            }
+            for (; k < tot; ++k) {
+                const double *p0 = M + (size_t)scol[k] * ld + r;
+                const double2 v = two ? *(const double2 *)p0 : make_double2(p0[0], 0.0);
+                a0 += v.x * sxv[k];
+                a1 += v.y * sxv[k];
             }
         }
-        for (; c < c1; ++c) {
-            const double xv = x[c];
-            if (xv == 0.0) continue;
-            const double *p0 = M + (size_t)c * ld + r;
-            if (two) {
-                double2 v = *(const double2 *)p0;
-                a0 += v.x * xv; a1 += v.y * xv;
-            } else
-                a0 += p0[0] * xv;
-        }
+        __syncthreads();
+    }
+    if (act) {
         double *out = part + (size_t)blockIdx.y * rows + r;
         out[0] = a0;
         if (two) out[1] = a1;

@@ -144,6 +144,8 @@ def load_library(path: str = LIB_PATH):
     L.gk_ios_driver_sharded.restype = C.c_int
     L.gk_bfd_profile.argtypes = [P, C.c_int]
     L.gk_bfd_profile.restype = None
+    L.gk_ctx_mark.argtypes = [P, C.c_int]
+    L.gk_ctx_mark.restype = C.c_int
     L.gk_bfd_trace.argtypes = [P, C.c_void_p, C.c_size_t]
     L.gk_bfd_trace.restype = C.c_int
     L.gk_bfd_time_kernel.argtypes = [P, C.c_int, C.c_int, C.POINTER(C.c_double)]
@@ -164,6 +166,10 @@ class Context:
         self.h = self.L.gk_ctx_create(device)
         if not self.h:
             raise GkError(f"gk_ctx_create({device}) failed: {_err(self.L)}")
+
+    def mark(self, tag: int):
+        """Enqueue the marker kernel k_gk_mark (windows a kernel trace)."""
+        self.L.gk_ctx_mark(self.h, int(tag))
 
     def close(self):
         if getattr(self, "h", None):

@@ -17,11 +17,18 @@ def main():
     ap.add_argument("db")
     ap.add_argument("--csv")
     ap.add_argument("--grid", action="store_true")
+    ap.add_argument("--marked", action="store_true",
+                    help="only the kernels between the first two k_gk_mark launches (bench.py's timed region)")
+    ap.add_argument("--json", help="write {kernel: {calls, avg_ns}} of the selection")
     a = ap.parse_args()
     c = sqlite3.connect(a.db)
-    rows = c.execute("select name, duration, grid_x, workgroup_x from kernels").fetchall()
+    rows = c.execute("select name, duration, grid_x, workgroup_x, start from kernels order by start").fetchall()
+    if a.marked:
+        marks = [r[4] for r in rows if r[0].startswith("k_gk_mark")]
+        assert len(marks) >= 2, "no k_gk_mark window in the trace"
+        rows = [r for r in rows if marks[0] < r[4] < marks[1]]
     by = {}
-    for name, dur, gx, wx in rows:
+    for name, dur, gx, wx, _ in rows:
         e = by.setdefault(name, {"d": [], "grids": set()})
         e["d"].append(dur)
         e["grids"].add(gx // max(1, wx))
@@ -31,6 +38,10 @@ def main():
         d = e["d"]
         out.append([name, len(d), sum(d), sum(d) / len(d), 100.0 * sum(d) / tot, min(d), max(d),
                     statistics.pstdev(d)])
+    if a.json:
+        import json
+        short = lambda nm: nm.split("(")[0].replace("void ", "").replace("gk::", "")
+        json.dump({short(r[0]): {"calls": r[1], "avg_ns": round(r[3], 1)} for r in out}, open(a.json, "w"), indent=1)
     w = csv.writer(open(a.csv, "w", newline="") if a.csv else sys.stdout, quoting=csv.QUOTE_NONNUMERIC)
     w.writerow(["Name", "Calls", "TotalDurationNs", "AverageNs", "Percentage", "MinNs", "MaxNs", "StdDev"])
     for r in out:
