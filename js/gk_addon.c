@@ -266,15 +266,9 @@ static napi_value js_bfd_valid(napi_env env, napi_callback_info info)
 }
 
 /* -------------------------------------------------------------------- spx */
-static napi_value js_spx(napi_env env, napi_callback_info info)
+/* the gk_lp arrays of the marshalled problem object L (js/gk_core.js) */
+static int fill_lp(napi_env env, napi_value L, gk_lp *out)
 {
-    napi_value argv[5];
-    if (!get_args(env, info, 5, argv)) return NULL;
-    gk_ctx *c = (gk_ctx *)get_ext(env, argv[0]);
-    gk_bfd *b = (gk_bfd *)get_ext(env, argv[1]);
-    napi_value L = argv[2], S = argv[3];
-    bool dual = false;
-    CHECK(napi_get_value_bool(env, argv[4], &dual));
     gk_lp lp;
     memset(&lp, 0, sizeof lp);
     lp.m = (int)dprop(env, L, "m", 0);
@@ -308,9 +302,24 @@ static napi_value js_spx(napi_env env, napi_callback_info info)
     if (!lp.row_type || !lp.row_lb || !lp.row_ub || !lp.rii || !lp.col_type || !lp.col_lb || !lp.col_ub ||
         !lp.col_coef || !lp.sjj || !lp.A_ptr || !lp.A_ind || !lp.A_val || !lp.head || !lp.row_stat ||
         !lp.col_stat || !lp.row_prim || !lp.row_dual || !lp.col_prim || !lp.col_dual) {
-        napi_throw_type_error(env, NULL, "spx: lp arrays missing or not typed arrays");
-        return NULL;
+        napi_throw_type_error(env, NULL, "gk_addon: lp arrays missing or not typed arrays");
+        return 0;
     }
+    *out = lp;
+    return 1;
+}
+
+static napi_value js_spx(napi_env env, napi_callback_info info)
+{
+    napi_value argv[5];
+    if (!get_args(env, info, 5, argv)) return NULL;
+    gk_ctx *c = (gk_ctx *)get_ext(env, argv[0]);
+    gk_bfd *b = (gk_bfd *)get_ext(env, argv[1]);
+    napi_value L = argv[2], S = argv[3];
+    bool dual = false;
+    CHECK(napi_get_value_bool(env, argv[4], &dual));
+    gk_lp lp;
+    if (!fill_lp(env, L, &lp)) return NULL;
     gk_smcp p;
     p.msg_lev = (int)dprop(env, S, "msg_lev", 3);
     p.meth = (int)dprop(env, S, "meth", 1);
@@ -334,6 +343,50 @@ static napi_value js_spx(napi_env env, napi_callback_info info)
     set_num(env, L, "some", lp.some);
     set_num(env, L, "obj_val", lp.obj_val);
     set_num(env, L, "valid", lp.valid);
+    return mk_int(env, ret);
+}
+
+/* -------------------------------------------------------------- ios_driver */
+/* ios(ctx, L, iocp): L = the marshalled root problem (solved to optimality,
+ * pbs_stat/dbs_stat/obj_val set) plus col_kind (Int8Array [1..n]) and the
+ * outputs row_mipx / col_mipx (Float64Array); sets L.mip_stat, L.mip_obj,
+ * L.lp_solves; returns the ios_driver code (0 or GLP_ETMLIM) */
+static napi_value js_ios(napi_env env, napi_callback_info info)
+{
+    napi_value argv[3];
+    if (!get_args(env, info, 3, argv)) return NULL;
+    gk_ctx *c = (gk_ctx *)get_ext(env, argv[0]);
+    napi_value L = argv[1], I = argv[2];
+    gk_mip mip;
+    memset(&mip, 0, sizeof mip);
+    if (!fill_lp(env, L, &mip.lp)) return NULL;
+    mip.lp.pbs_stat = (int)dprop(env, L, "pbs_stat", 0);
+    mip.lp.dbs_stat = (int)dprop(env, L, "dbs_stat", 0);
+    mip.lp.obj_val = dprop(env, L, "obj_val", 0.0);
+    mip.col_kind = (const signed char *)tprop(env, L, "col_kind");
+    mip.row_mipx = (double *)tprop(env, L, "row_mipx");
+    mip.col_mipx = (double *)tprop(env, L, "col_mipx");
+    if (!mip.col_kind || !mip.row_mipx || !mip.col_mipx) {
+        napi_throw_type_error(env, NULL, "ios: col_kind / row_mipx / col_mipx missing or not typed arrays");
+        return NULL;
+    }
+    gk_iocp p;
+    p.msg_lev = (int)dprop(env, I, "msg_lev", 3);
+    p.br_tech = (int)dprop(env, I, "br_tech", 4);
+    p.bt_tech = (int)dprop(env, I, "bt_tech", 4);
+    p.tol_int = dprop(env, I, "tol_int", 1e-5);
+    p.tol_obj = dprop(env, I, "tol_obj", 1e-7);
+    p.tm_lim = (int)dprop(env, I, "tm_lim", 2147483647.0);
+    p.out_frq = (int)dprop(env, I, "out_frq", 5000);
+    p.out_dly = (int)dprop(env, I, "out_dly", 10000);
+    p.pp_tech = (int)dprop(env, I, "pp_tech", 2);
+    p.mip_gap = dprop(env, I, "mip_gap", 0.0);
+    p.presolve = (int)dprop(env, I, "presolve", 0);
+    int ret = gk_ios_driver(c, &mip, &p);
+    if (ret == GK_EABI) return throw_gk(env, "ios_driver");
+    set_num(env, L, "mip_stat", mip.mip_stat);
+    set_num(env, L, "mip_obj", mip.mip_obj);
+    set_num(env, L, "lp_solves", (double)mip.lp_solves);
     return mk_int(env, ret);
 }
 
@@ -363,7 +416,7 @@ static napi_value init(napi_env env, napi_value exports)
         FN("lastError", js_last_error), FN("bfdCreate", js_bfd_create), FN("bfdSetParm", js_bfd_set_parm),
         FN("bfdFactorizeCsc", js_bfd_factorize_csc), FN("bfdFtran", js_bfd_ftran), FN("bfdBtran", js_bfd_btran),
         FN("bfdUpdate", js_bfd_update), FN("bfdGetCount", js_bfd_get_count), FN("bfdValid", js_bfd_valid),
-        FN("spx", js_spx), FN("stats", js_stats),
+        FN("spx", js_spx), FN("ios", js_ios), FN("stats", js_stats),
     };
     napi_define_properties(env, exports, sizeof d / sizeof d[0], d);
     return exports;

@@ -106,9 +106,9 @@ function marshalMatrix(lp, g) {
     g.a_version = lp.__gk_version;
 }
 
-function spx(lp, parm, dual) {
+// the init_csa inputs of lp into the marshalled object L
+function marshal(lp, g) {
     var m = lp.m, n = lp.n, i, j, row, col;
-    var g = arrays(lp);
     for (i = 1; i <= m; i++) {
         row = lp.row[i];
         g.row_type[i] = row.type; g.row_lb[i] = row.lb; g.row_ub[i] = row.ub;
@@ -121,7 +121,7 @@ function spx(lp, parm, dual) {
     }
     for (i = 1; i <= m; i++) g.head[i] = lp.head[i];
     marshalMatrix(lp, g);
-    var L = {
+    return {
         m: m, n: n, nnz: lp.nnz, dir: lp.dir, c0: lp.c0, a_version: g.a_version, it_cnt: lp.it_cnt,
         row_type: g.row_type, row_lb: g.row_lb, row_ub: g.row_ub, rii: g.rii,
         col_type: g.col_type, col_lb: g.col_lb, col_ub: g.col_ub, col_coef: g.col_coef, sjj: g.sjj,
@@ -129,6 +129,12 @@ function spx(lp, parm, dual) {
         row_stat: g.row_stat, col_stat: g.col_stat, row_bind: g.row_bind, col_bind: g.col_bind,
         row_prim: g.row_prim, row_dual: g.row_dual, col_prim: g.col_prim, col_dual: g.col_dual
     };
+}
+
+function spx(lp, parm, dual) {
+    var m = lp.m, n = lp.n, i, j, row, col;
+    var g = arrays(lp);
+    var L = marshal(lp, g);
     // init_csa asserts lp.valid and takes lp.bfd (glpspx01.js:129-132)
     if (!lp.valid || lp.bfd === null) throw new Error('assert');
     var ret = addon.spx(context(), lp.bfd.gk, L, parm, dual);
@@ -160,9 +166,51 @@ function spx(lp, parm, dual) {
     return ret;
 }
 
+// ---- ios_driver (glpios03.js:1) ---------------------------------------------
+var GLP_IV = 2, GLP_FEAS = 2, GLP_OPT = 5;
+
+// the requests the native driver serves: no callbacks (glpios03.js:533-897),
+// no MIP-gap stop, no cut generators / feasibility pump (they stay in JS),
+// and node LPs whose tableau fits the node kernel's LDS (gk_mip.hip)
+function nativeIos(T) {
+    var P = T.mip, parm = T.parm, m = P.m, n = P.n;
+    if (parm.cb_func != null) return false;
+    if (parm.mip_gap > 0.0) return false;
+    if (parm.gmi_cuts || parm.mir_cuts || parm.cov_cuts || parm.clq_cuts || parm.fp_heur) return false;
+    var lds = 8 * (m * (2 * m + n) + 4 * (m + n) + m) + 4 * m + (m + n) + 16;
+    return lds <= 65536;
+}
+
+// T = the tree of ios_create_tree: T.mip is the problem (its LP relaxation
+// solved to optimality by glp_intopt's caller), T.parm the IOCP.  Writes what
+// the reference's driver writes into the problem on an integer solution
+// (record_solution, glpios03.js:113-135): mip_stat = GLP_FEAS, mip_obj, mipx;
+// solve_mip then turns FEAS into OPT (glpapi09.js:82-92).
+function iosDriver(T) {
+    var P = T.mip, m = P.m, n = P.n, i, j;
+    var g = arrays(P);
+    var L = marshal(P, g);
+    if (!g.col_kind || g.col_kind.length !== n + 1) {
+        g.col_kind = new Int8Array(n + 1);
+        g.row_mipx = new Float64Array(m + 1);
+        g.col_mipx = new Float64Array(n + 1);
+    }
+    for (j = 1; j <= n; j++) g.col_kind[j] = P.col[j].kind;
+    L.col_kind = g.col_kind; L.row_mipx = g.row_mipx; L.col_mipx = g.col_mipx;
+    L.pbs_stat = P.pbs_stat; L.dbs_stat = P.dbs_stat; L.obj_val = P.obj_val;
+    var ret = addon.ios(context(), L, T.parm);
+    if (L.mip_stat === GLP_OPT || (ret !== 0 && L.mip_stat === GLP_FEAS)) {
+        P.mip_stat = GLP_FEAS;
+        P.mip_obj = L.mip_obj;
+        for (i = 1; i <= m; i++) P.row[i].mipx = g.row_mipx[i];
+        for (j = 1; j <= n; j++) P.col[j].mipx = g.col_mipx[j];
+    }
+    return ret;
+}
+
 module.exports = {
     addon: addon, context: context, nextVersion: nextVersion,
     bfdCreate: bfdCreate, bfdSetParm: bfdSetParm, bfdFactorize: bfdFactorize,
     bfdFtran: bfdFtran, bfdBtran: bfdBtran, bfdUpdate: bfdUpdate, bfdGetCount: bfdGetCount,
-    spx: spx, GLP_BS: GLP_BS
+    spx: spx, iosDriver: iosDriver, nativeIos: nativeIos, GLP_BS: GLP_BS
 };

@@ -16,6 +16,10 @@ bfd_ftran = function (bfd, x) { __gk.bfdFtran(bfd, x); };
 bfd_btran = function (bfd, x) { __gk.bfdBtran(bfd, x); };
 bfd_update_it = function (bfd, j, bh, len, ind, idx, val) { return __gk.bfdUpdate(bfd, j, bh, len, ind, idx, val); };
 bfd_get_count = function (bfd) { return __gk.bfdGetCount(bfd); };
+// ios_driver (glpios03.js:1, called by solve_mip glpapi09.js:79): the native
+// batched B&B when the request is one it serves, else the reference's driver
+var __gk_js_ios_driver = ios_driver;
+ios_driver = function (T) { return __gk.nativeIos(T) ? __gk.iosDriver(T) : __gk_js_ios_driver(T); };
 
 (function () {
     function versioned(f) {
@@ -41,3 +45,4 @@ bfd_get_count = function (bfd) { return __gk.bfdGetCount(bfd); };
     glp_copy_prob = exports["glp_copy_prob"] = versioned(glp_copy_prob);
 })();
 exports["__gk_core"] = __gk;
+exports["__gk_ios_driver"] = ios_driver;

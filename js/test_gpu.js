@@ -112,4 +112,47 @@ files.forEach(function (f) {
     });
 });
 assert.ok(ncase > 50, 'too few cases: ' + ncase);
-console.log('ok js gpu parity: ' + ncase + ' runs');
+
+// MIP fixtures: root LP through solve_lp as above, then the native driver
+// through gk_core.iosDriver with the tree object ios_driver receives
+// (T.mip = the problem, T.parm = IOCP with the reference's defaults,
+// glpapi09.js:392-414); solve_mip's FEAS -> OPT / NOFEAS (glpapi09.js:82-92)
+function iocp() {
+    return {msg_lev: 3, br_tech: 4, bt_tech: 4, tol_int: 1e-5, tol_obj: 1e-7, tm_lim: INT_MAX, out_frq: 5000,
+            out_dly: 10000, cb_func: null, cb_info: null, cb_size: 0, pp_tech: 2, mip_gap: 0.0, mir_cuts: 0,
+            gmi_cuts: 0, cov_cuts: 0, clq_cuts: 0, presolve: 0, binarize: 0, fp_heur: 0};
+}
+var nmip = 0;
+fs.readdirSync(dir).filter(function (f) { return /^mip_.*\.json$/.test(f) && !/12x30/.test(f); }).sort()
+    .forEach(function (f) {
+        var fx = JSON.parse(fs.readFileSync(path.join(dir, f), 'utf8'));
+        if (fx.gen || fx.A_ptr === undefined) return;              // generated instances: Python tests
+        var lp = buildLp(fx);
+        for (var j = 1; j <= fx.n; j++) lp.col[j].kind = fx.col_kind[j - 1];
+        var ret = simplex(lp, smcp(fx.root.opts));
+        assert.strictEqual(ret, fx.root.ret, f + ' root ret');
+        if (lp.pbs_stat !== 2 || lp.dbs_stat !== 2) return;       // glp_intopt would return GLP_EROOT
+        lp.mip_stat = 1; lp.mip_obj = 0.0;
+        for (var i = 1; i <= fx.m; i++) lp.row[i].mipx = 0.0;
+        for (j = 1; j <= fx.n; j++) lp.col[j].mipx = 0.0;
+        var T = {mip: lp, parm: iocp()};
+        assert.ok(core.nativeIos(T), f + ' not served natively');
+        ret = core.iosDriver(T);
+        if (ret === 0) lp.mip_stat = (lp.mip_stat === 2) ? 5 : 4;
+        assert.strictEqual(ret, fx.mip.ret, f + ' ret');
+        assert.strictEqual(lp.mip_stat, fx.mip.mip_stat, f + ' mip_stat');
+        if (lp.mip_stat === 5) {
+            var sc = Math.max(1.0, Math.abs(fx.mip.mip_obj));
+            assert.ok(Math.abs(lp.mip_obj - fx.mip.mip_obj) <= 1e-9 * sc, f + ' mip_obj ' + lp.mip_obj);
+            var obj = fx.c0;
+            for (j = 1; j <= fx.n; j++) {
+                var x = lp.col[j].mipx;
+                if (fx.col_kind[j - 1] === 2) assert.strictEqual(x, Math.floor(x), f + ' integrality');
+                obj += fx.col_coef[j - 1] * x;
+            }
+            assert.ok(Math.abs(obj - lp.mip_obj) <= 1e-7 * sc, f + ' objective of mipx');
+        }
+        nmip++;
+    });
+assert.ok(nmip >= 10, 'too few MIP cases: ' + nmip);
+console.log('ok js gpu parity: ' + ncase + ' runs, ' + nmip + ' MIPs');

@@ -7,7 +7,7 @@ var path = require('path');
 var core = require(path.join(__dirname, 'gk_core.js'));
 
 var names = ['create', 'deviceCount', 'abiVersion', 'lastError', 'bfdCreate', 'bfdSetParm', 'bfdFactorizeCsc',
-             'bfdFtran', 'bfdBtran', 'bfdUpdate', 'bfdGetCount', 'bfdValid', 'spx', 'stats'];
+             'bfdFtran', 'bfdBtran', 'bfdUpdate', 'bfdGetCount', 'bfdValid', 'spx', 'ios', 'stats'];
 names.forEach(function (k) { assert.strictEqual(typeof core.addon[k], 'function', k); });
 assert.strictEqual(core.addon.abiVersion(), 1);
 
@@ -19,6 +19,13 @@ if (!fs.existsSync(path.join(ref, 'lib'))) {
 }
 var glpk = require(path.join(__dirname, 'load_glpk.js'))(ref);
 assert.ok(glpk.__gk_core, 'shim not concatenated');
+assert.ok(/nativeIos/.test(String(glpk.__gk_ios_driver)), 'ios_driver not rebound');
+// requests the native driver does not serve go to the reference's driver
+assert.strictEqual(core.nativeIos({mip: {m: 2, n: 3}, parm: {cb_func: function () {}}}), false);
+assert.strictEqual(core.nativeIos({mip: {m: 2, n: 3}, parm: {cb_func: null, mip_gap: 0.01}}), false);
+assert.strictEqual(core.nativeIos({mip: {m: 2, n: 3}, parm: {cb_func: null, mip_gap: 0, gmi_cuts: 1}}), false);
+assert.strictEqual(core.nativeIos({mip: {m: 2, n: 3}, parm: {cb_func: null, mip_gap: 0}}), true);
+assert.strictEqual(core.nativeIos({mip: {m: 80, n: 200}, parm: {cb_func: null, mip_gap: 0}}), false);
 glpk.glp_set_print_func(function () {});
 var lp = glpk.glp_create_prob();
 glpk.glp_set_obj_dir(lp, glpk.GLP_MAX);
