@@ -214,7 +214,7 @@ static int reinvert_core(gk_bfd *f, const BasisSplit &bs, const MatDev *Adense, 
     if (k > 0) {
         f->C.ensure((size_t)k * k);
         f->X.ensure((size_t)2 * k * k);
-        f->Y.ensure((size_t)2 * k * k);
+        f->Y.ensure(std::max((size_t)2 * k * k, gj_blocked_scratch(k)));
         f->CinvR.ensure((size_t)k * k);
         if (ms > 0) {
             f->BS.ensure((size_t)ms * k);
@@ -233,7 +233,9 @@ static int reinvert_core(gk_bfd *f, const BasisSplit &bs, const MatDev *Adense, 
         f->piv_step.ensure(k);
         f->piv.ensure(k);
         f->flag.ensure(1);
-        gauss_jordan(s, f->X.p, f->Y.p, k, f->piv_step.p, f->piv.p, f->flag.p, 1e-15, &result);
+        const bool blocked = k <= gj_blocked_max();
+        if (blocked) gauss_jordan_blocked(s, f->X.p, f->Y.p, k, f->piv_step.p, f->piv.p, f->flag.p, 1e-15);
+        else gauss_jordan(s, f->X.p, f->Y.p, k, f->piv_step.p, f->piv.p, f->flag.p, 1e-15, &result);
         int flag = 0;
         HIPCHK(hipMemcpyAsync(&flag, f->flag.p, sizeof(int), hipMemcpyDeviceToHost, s));
         HIPCHK(hipStreamSynchronize(s));
@@ -243,7 +245,8 @@ static int reinvert_core(gk_bfd *f, const BasisSplit &bs, const MatDev *Adense, 
             f->stats.seconds_reinvert += now_s() - t0;
             return 1;   // BFD_ESING
         }
-        extract_inverse_rowmajor(s, result, k, f->piv.p, f->CinvR.p);
+        if (blocked) extract_inverse_blocked(s, f->X.p, k, f->piv.p, f->piv_step.p, f->CinvR.p);
+        else extract_inverse_rowmajor(s, result, k, f->piv.p, f->CinvR.p);
         if (ms > 0) gemm_bs_cinv(s, f->BS.p, ms, k, f->CinvR.p, f->G.p, 1);
     }
     assemble_binv(s, f->Binv.p, m, f->ldb, k, ms, d_posJ, d_rowR, d_posS, d_rowS, f->CinvR.p, f->G.p);

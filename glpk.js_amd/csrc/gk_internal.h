@@ -187,6 +187,13 @@ void gather_basis_blocks_csc(hipStream_t s, int m, int k, const int *bptr, const
 int gauss_jordan(hipStream_t s, double *X, double *Y, int k, int *piv_step, int *piv, int *flag, double tiny,
                  double **result);
 void extract_inverse_rowmajor(hipStream_t s, const double *X, int k, const int *piv, double *CinvR);
+// blocked Gauss-Jordan (gk_reinvert.hip): C column-major in X, inverted in place
+int gj_blocked_max();
+size_t gj_blocked_scratch(int k);
+void gauss_jordan_blocked(hipStream_t s, double *X, double *scratch, int k, int *piv_step, int *piv, int *flag,
+                          double tiny);
+void extract_inverse_blocked(hipStream_t s, const double *M, int k, const int *piv, const int *piv_step,
+                             double *CinvR);
 // G (ms x k, col-major) = BS (ms x k col-major) * CinvR (k x k row-major)
 void gemm_bs_cinv(hipStream_t s, const double *BS, int ms, int k, const double *CinvR, double *G, int use_mfma);
 void assemble_binv(hipStream_t s, double *Binv, int m, int ldb, int k, int ms, const int *posJ, const int *rowR,

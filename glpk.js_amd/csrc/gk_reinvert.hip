@@ -1,0 +1,252 @@
+// Blocked Gauss–Jordan inversion of the structural block C of the basis
+// (re-inversion, the device counterpart of bfd_factorize → luf_factorize,
+// glpbfd.js:74-103 / glpluf.js:461-812; the reference factorizes B = F·H·V,
+// the device keeps inv(B) explicitly).
+//
+// C (k x k) arrives column-major, i.e. M := C' row-major (M[r * k + c]).
+// In-place Gauss–Jordan with partial pivoting on M (rows chosen implicitly,
+// never swapped): step t picks the unpivoted row rs with the largest
+// |M[rs, t]| (lowest row on ties), and slot t then holds column rs of the
+// right half of [M | I], so that at the end
+//   inv(M)[b, a] = M[piv[b], piv_step[a]]   (piv_step = inverse of piv).
+//
+// Blocking (panel of B columns [t0, t0 + b)): one workgroup runs the b steps
+// on the panel, k rows held in registers (RPT rows per thread), and leaves
+// Q = the transformed panel and R = its pivot rows.  The b steps act on any
+// other column x as  x <- x + (Q - E_R) x_R  (every step reads x only at its
+// pivot row), so the rest of M takes one rank-b update — an MFMA GEMM
+// (v_mfma_f64_16x16x4_f64) — after the pivot rows X_R are copied aside.
+// 2 launches per panel instead of one launch per column.
+#include "gk_device.h"
+
+namespace gk {
+
+constexpr int GJ_NONE = 0x7fffffff;
+
+template <int NT, int RPT, int B>
+__global__ void __launch_bounds__(NT) k_gjb_panel(double *__restrict__ M, double *__restrict__ Qm,
+                                                  double *__restrict__ XR, int k, int t0, int *__restrict__ piv_step,
+                                                  int *__restrict__ piv, int *__restrict__ flag, double tiny)
+{
+    __shared__ Cand shc[NT / 64];
+    __shared__ double frs[B];
+    __shared__ int rsl[B];
+    if (*flag) return;
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int b = min(B, k - t0);
+    double x[RPT][B];
+    bool live[RPT];                      // row owned, and not pivoted yet
+#pragma unroll
+    for (int j = 0; j < RPT; ++j) {
+        const int r = tid + j * NT;
+        live[j] = r < k && piv_step[r] == GJ_NONE;
+        const double *row = M + (size_t)r * k + t0;
+#pragma unroll
+        for (int c = 0; c < B; ++c) x[j][c] = (r < k && c < b) ? row[c] : 0.0;
+    }
+    bool dead = false;                   // singular (uniform over the block)
+#pragma unroll
+    for (int i = 0; i < B; ++i) {
+        if (i >= b || dead) continue;
+        // pivot row: largest |M[r, t]| over the unpivoted rows, lowest row on ties
+        Cand c; c.k1 = 0.0; c.k2 = 0.0; c.idx = 0; c.aux = 0;
+#pragma unroll
+        for (int j = 0; j < RPT; ++j) {
+            const double v = fabs(x[j][i]);
+            if (live[j] && v > 0.0 && (c.idx == 0 || v > c.k1)) {   // rows ascend with j
+                c.k1 = v;
+                c.idx = tid + j * NT + 1;
+            }
+        }
+        c = wave_best<0>(c);
+        if (lane == 0) shc[w] = c;
+        __syncthreads();
+        Cand e;
+        if (lane < NT / 64) e = shc[lane];
+        else { e.k1 = 0.0; e.k2 = 0.0; e.idx = 0; e.aux = 0; }
+        const Cand best = wave_best<0>(e);
+        if (best.idx == 0 || best.k1 <= tiny) {
+            if (tid == 0) *flag = 1 + t0 + i;
+            dead = true;
+            continue;
+        }
+        const int rs = best.idx - 1;
+        // the elementary step, in k_gj_step's arithmetic: fr = x[rs] / pv,
+        // y = x - colt * fr; the new slot i is the right-half column e_rs
+        // (fr = 1 / pv).  The owner of row rs publishes fr.
+        if (tid == rs % NT) {
+            const int jo = rs / NT;
+#pragma unroll
+            for (int j = 0; j < RPT; ++j)
+                if (j == jo) {
+                    const double pv = x[j][i];
+#pragma unroll
+                    for (int cc = 0; cc < B; ++cc) frs[cc] = (cc == i) ? 1.0 / pv : x[j][cc] / pv;
+                }
+        }
+        if (tid == 0) {
+            rsl[i] = rs;
+            piv[t0 + i] = rs;
+            piv_step[rs] = t0 + i;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int j = 0; j < RPT; ++j) {
+            const int r = tid + j * NT;
+            if (r == rs) {
+#pragma unroll
+                for (int cc = 0; cc < B; ++cc) x[j][cc] = frs[cc];
+                live[j] = false;
+            } else {
+                const double colt = x[j][i];
+#pragma unroll
+                for (int cc = 0; cc < B; ++cc) x[j][cc] = ((cc == i) ? 0.0 : x[j][cc]) - colt * frs[cc];
+            }
+        }
+    }
+    if (dead) return;
+    // the panel back in place, Q - E_R for the update
+#pragma unroll
+    for (int j = 0; j < RPT; ++j) {
+        const int r = tid + j * NT;
+        if (r >= k) continue;
+        double *row = M + (size_t)r * k + t0;
+        double *q = Qm + (size_t)r * B;
+#pragma unroll
+        for (int c = 0; c < B; ++c) {
+            if (c < b) row[c] = x[j][c];
+            q[c] = (c < b) ? x[j][c] - (r == rsl[c] ? 1.0 : 0.0) : 0.0;
+        }
+    }
+    // X_R = the pivot rows of the other columns, as they were before the panel
+    // (rows of M, contiguous); zero rows pad the last panel
+    for (int e = tid; e < B * k; e += NT) {
+        const int kk = e / k, c = e - kk * k;
+        XR[e] = (kk < b && (c < t0 || c >= t0 + b)) ? M[(size_t)rsl[kk] * k + c] : 0.0;
+    }
+}
+
+// M[r, c] += sum_kk Q[r, kk] XR[kk, c] for the columns outside the panel.
+// One block = 64 x 64 outputs, four waves of 32 x 32 (2 x 2 MFMA tiles).
+// Fragments of v_mfma_f64_16x16x4_f64 per lane l: A[i = l & 15][kk = l >> 4],
+// B[kk = l >> 4][j = l & 15], D[(l >> 4) + 4 r][l & 15].
+typedef double gj_double4 __attribute__((ext_vector_type(4)));
+
+template <int B>
+__global__ void __launch_bounds__(256) k_gjb_update(double *__restrict__ M, const double *__restrict__ Qm,
+                                                    const double *__restrict__ XR, int k, int t0,
+                                                    const int *__restrict__ flag)
+{
+    if (*flag) return;
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int li = lane & 15, lk = lane >> 4;
+    const int row0 = blockIdx.y * 64 + (w & 1) * 32;
+    const int col0 = blockIdx.x * 64 + (w >> 1) * 32;
+    const int b = min(B, k - t0);
+    gj_double4 acc[2][2];
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+        for (int bb = 0; bb < 2; ++bb)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int gr = row0 + a * 16 + lk + 4 * r, gc = col0 + bb * 16 + li;
+                acc[a][bb][r] = (gr < k && gc < k) ? M[(size_t)gr * k + gc] : 0.0;
+            }
+#pragma unroll
+    for (int kk = 0; kk < B; kk += 4) {
+        const int gk = kk + lk;
+        double av[2], bv[2];
+#pragma unroll
+        for (int a = 0; a < 2; ++a) {
+            const int gr = row0 + a * 16 + li;
+            av[a] = gr < k ? Qm[(size_t)gr * B + gk] : 0.0;
+        }
+#pragma unroll
+        for (int bb = 0; bb < 2; ++bb) {
+            const int gc = col0 + bb * 16 + li;
+            bv[bb] = gc < k ? XR[(size_t)gk * k + gc] : 0.0;
+        }
+#pragma unroll
+        for (int a = 0; a < 2; ++a)
+#pragma unroll
+            for (int bb = 0; bb < 2; ++bb)
+                acc[a][bb] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[a], bv[bb], acc[a][bb], 0, 0, 0);
+    }
+    (void)b;
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+        for (int bb = 0; bb < 2; ++bb)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int gr = row0 + a * 16 + lk + 4 * r, gc = col0 + bb * 16 + li;
+                if (gr < k && gc < k && (gc < t0 || gc >= t0 + b)) M[(size_t)gr * k + gc] = acc[a][bb][r];
+            }
+}
+
+template <int NT, int RPT, int B>
+static void gjb_run(hipStream_t s, double *M, double *Qm, double *XR, int k, int *piv_step, int *piv, int *flag,
+                    double tiny)
+{
+    const dim3 g((k + 63) / 64, (k + 63) / 64);
+    for (int t0 = 0; t0 < k; t0 += B) {
+        hipLaunchKernelGGL((k_gjb_panel<NT, RPT, B>), dim3(1), dim3(NT), 0, s, M, Qm, XR, k, t0, piv_step, piv, flag,
+                           tiny);
+        if (k > B)
+            hipLaunchKernelGGL((k_gjb_update<B>), g, dim3(256), 0, s, M, Qm, XR, k, t0, flag);
+    }
+}
+
+__global__ void k_gjb_init(int *piv_step, int k, int *flag)
+{
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < k; i += gridDim.x * blockDim.x) piv_step[i] = GJ_NONE;
+    if (blockIdx.x == 0 && threadIdx.x == 0) *flag = 0;
+}
+
+int gj_blocked_max() { return 8192; }
+
+size_t gj_blocked_scratch(int k)
+{
+    // Q (k x 32) and X_R (32 x k)
+    return (size_t)64 * k;
+}
+
+// inverse of C (k x k, column-major in X) by the blocked scheme above; X is
+// overwritten, scratch needs gj_blocked_scratch(k) doubles; BFD_ESING is
+// reported through *flag (1 + step)
+void gauss_jordan_blocked(hipStream_t s, double *X, double *scratch, int k, int *piv_step, int *piv, int *flag,
+                          double tiny)
+{
+    if (k <= 0) return;
+    hipLaunchKernelGGL(k_gjb_init, dim3(std::min((k + 255) / 256, 64)), dim3(256), 0, s, piv_step, k, flag);
+    double *Qm = scratch, *XR = scratch + (size_t)32 * k;
+    // registers: RPT * B doubles of the panel per thread (1 / 2 / 4 waves per SIMD)
+    if (k <= 256) gjb_run<256, 1, 16>(s, X, Qm, XR, k, piv_step, piv, flag, tiny);
+    else if (k <= 512) gjb_run<256, 2, 16>(s, X, Qm, XR, k, piv_step, piv, flag, tiny);
+    else if (k <= 1024) gjb_run<512, 2, 16>(s, X, Qm, XR, k, piv_step, piv, flag, tiny);
+    else if (k <= 2048) gjb_run<1024, 2, 16>(s, X, Qm, XR, k, piv_step, piv, flag, tiny);
+    else if (k <= 4096) gjb_run<1024, 4, 8>(s, X, Qm, XR, k, piv_step, piv, flag, tiny);
+    else gjb_run<1024, 8, 4>(s, X, Qm, XR, k, piv_step, piv, flag, tiny);
+}
+
+// CinvR (row-major inv(C)): with M = C' inverted in place,
+// inv(C)[a, b] = inv(M)[b, a] = M[piv[b], piv_step[a]]
+__global__ void k_gjb_extract(const double *__restrict__ M, int k, const int *__restrict__ piv,
+                              const int *__restrict__ piv_step, double *__restrict__ CinvR)
+{
+    const int a = blockIdx.y;
+    const size_t col = (size_t)piv_step[a];
+    for (int b = blockIdx.x * blockDim.x + threadIdx.x; b < k; b += gridDim.x * blockDim.x)
+        CinvR[(size_t)a * k + b] = M[(size_t)piv[b] * k + col];
+}
+
+void extract_inverse_blocked(hipStream_t s, const double *M, int k, const int *piv, const int *piv_step,
+                             double *CinvR)
+{
+    if (k <= 0) return;
+    dim3 g(std::max(1, std::min((k + 255) / 256, 16)), k);
+    hipLaunchKernelGGL(k_gjb_extract, g, dim3(256), 0, s, M, k, piv, piv_step, CinvR);
+}
+
+}  // namespace gk

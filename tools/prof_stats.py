@@ -19,14 +19,17 @@ def main():
     ap.add_argument("--grid", action="store_true")
     ap.add_argument("--marked", action="store_true",
                     help="only the kernels between the first two k_gk_mark launches (bench.py's timed region)")
+    ap.add_argument("--window", type=int, default=0,
+                    help="with --marked: the i-th pair of k_gk_mark launches (0-based)")
     ap.add_argument("--json", help="write {kernel: {calls, avg_ns}} of the selection")
     a = ap.parse_args()
     c = sqlite3.connect(a.db)
     rows = c.execute("select name, duration, grid_x, workgroup_x, start from kernels order by start").fetchall()
     if a.marked:
         marks = [r[4] for r in rows if r[0].startswith("k_gk_mark")]
-        assert len(marks) >= 2, "no k_gk_mark window in the trace"
-        rows = [r for r in rows if marks[0] < r[4] < marks[1]]
+        w = 2 * a.window
+        assert len(marks) >= w + 2, "no such k_gk_mark window in the trace"
+        rows = [r for r in rows if marks[w] < r[4] < marks[w + 1]]
     by = {}
     for name, dur, gx, wx, _ in rows:
         e = by.setdefault(name, {"d": [], "grids": set()})
