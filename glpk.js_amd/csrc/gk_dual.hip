@@ -1001,6 +1001,172 @@ __global__ void __launch_bounds__(1024) k_dual_row(SpxDev d, int pse, int nr_cap
 }
 
 // ---------------------------------------------------------------------------
+// k_dual_col (column path, sparse A): k_dual_top, the CSC column pass and
+// k_trow_finish in ONE kernel — the sparse counterpart of k_dual_row.  Every
+// wave owns 64 slots (structural column c and slack row c of each slot) and
+// is one 64-slot group of the candidates.  The CSC entries of the slot's
+// column are loaded before the pivot decision (they do not depend on it);
+// after the chuzr choice (made in every wave from the commit's candidates)
+// rho_i is read straight from row p of inv(B) — the unit columns of the
+// basic slacks are stored exactly — so trow_c = sum_t cval[t] rho_cind[t]
+// (eval_trow glpspx02.js:655-791, -rho' N_j) takes two dependent trips
+// whatever the column length up to CU entries.  Block 0 applies the pending
+// change of basis and publishes the compact rho (rho_idx / rho_val, read by
+// the commit) and the scalar state; the other blocks patch what it changes,
+// as in k_dual_row.
+// ---------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) k_dual_col(SpxDev d, int pse)
+{
+    const TraceScope trace_(d, 1);
+    DState *st = d.st;
+    const int m = d.m, n = d.n;
+    const int lane = threadIdx.x & 63;
+    const int grp = blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int idx = grp * 64 + lane;
+    const bool lead = (blockIdx.x == 0);
+    // ---- trip 1: state, chuzr candidates, slot positions, CSC entries
+    const int stop = st->stop;
+    const FinishIn fin = finish_load(d);
+    const int pricing = st->pricing, phase = st->phase, dinf = st->dinf, nr = st->nr;
+    const double zeta = st->zeta, obj_ll = st->obj_ll, obj_ul = st->obj_ul;
+    const RatioIn rin = ratio_in(st);
+    const int gm = 4 * ((m + 255) / 256);
+    Cand cc = no_cand(0.0);
+    for (int b = lane; b < gm; b += 64) {
+        const Cand e = cand_chuzr(d)[b];
+        if (better<0>(e, cc)) cc = e;
+    }
+    int pos1 = (idx < n) ? d.bind[m + idx] : 0;
+    int pos2 = (idx < m) ? d.bind[idx] : 0;
+    constexpr int CU = 8;                    // CSC entries per column loaded ahead
+    int beg = 0, end = 0;
+    if (idx < n) {
+        beg = d.A.cptr[idx];
+        end = d.A.cptr[idx + 1];
+    }
+    int ci[CU];
+    double cv[CU];
+#pragma unroll
+    for (int u = 0; u < CU; ++u) {
+        const bool ok = beg + u < end;
+        ci[u] = ok ? d.A.cind[beg + u] : 0;
+        cv[u] = ok ? d.A.cval[beg + u] : 0.0;
+    }
+    if (stop) return;
+    if (lead && threadIdx.x == 0) st->tk_start = wall_clock64();
+    // ---- decisions (identical in every wave)
+    const TopState ts = fin.t;
+    int why = ST_RUN;
+    if (ts.iter_left <= 0 || ts.refact) why = ts.refact ? ST_REFACT : ST_BATCH;
+    else if (phase == 1 && !dinf) why = ST_PHASE;
+    else if (phase != 1 && ((zeta < 0.0 && obj_ll > -DBL_MAX && ts.obj <= obj_ll) ||
+                            (zeta > 0.0 && obj_ul < +DBL_MAX && ts.obj >= obj_ul)))
+        why = ST_OBJLIM;
+    const Cand best = wave_best<0>(cc);
+    if (why == ST_RUN && best.idx == 0) why = ST_P0;
+    const bool reset = (why == ST_RUN && pricing == PT_PSE && ts.refct == 0);
+    if (lead) {
+        (void)finish_apply(d, fin, true);
+        if (why != ST_RUN) {
+            if (threadIdx.x == 0) {
+                if (why == ST_P0) st->p = 0;
+                st->stop = why;
+            }
+            return;
+        }
+        if (reset) {
+            reset_refsp_dev(d, 1);            // refsp := basic variables, gamma := 1
+            for (int l = threadIdx.x; l < n; l += blockDim.x) d.wpos[l] = -1;
+            if (threadIdx.x == 0) st->nwl = 0;
+        }
+    }
+    if (why != ST_RUN) return;
+    const int p = best.idx, kp = best.aux;
+    const int ns = nr + (kp <= m ? 1 : 0);
+    auto bind_new = [&](int k1, int v) {
+        if (!fin.pend) return v;
+        if (k1 == fin.kq) return fin.p;
+        if (k1 == fin.kp) return m + fin.q;
+        return v;
+    };
+    if (idx < n) pos1 = bind_new(m + idx + 1, pos1);
+    if (idx < m) pos2 = bind_new(idx + 1, pos2);
+    const int j1 = (pos1 > m) ? pos1 - m - 1 : -1;
+    const int j2 = (pos2 > m) ? pos2 - m - 1 : -1;
+    // ---- trip 2: rho at the column's rows, the slot operands
+    const double *__restrict__ brow = d.Binv + (p - 1);
+    const size_t ldb = (size_t)d.ldb;
+    double rv[CU];
+#pragma unroll
+    for (int u = 0; u < CU; ++u) rv[u] = (j1 >= 0 && beg + u < end) ? brow[(size_t)ci[u] * ldb] : 0.0;
+    const signed char stq = fin.fxp ? NS : (fin.delta > 0.0 ? NL : NU);
+    int s1 = 0, s2 = 0;
+    double cb1 = 0.0, cb2 = 0.0, rho2 = 0.0;
+    bool ref1 = false, ref2 = false;
+    if (j1 >= 0) {
+        s1 = (fin.pend && j1 == fin.q - 1) ? stq : d.stat[j1];
+        cb1 = d.cbar[j1];
+        if (pse && !reset) ref1 = d.refsp[m + idx] != 0 && !(fin.pend && fin.rclr && m + idx + 1 == fin.kp);
+    }
+    if (j2 >= 0) {
+        s2 = (fin.pend && j2 == fin.q - 1) ? stq : d.stat[j2];
+        cb2 = d.cbar[j2];
+        rho2 = brow[(size_t)idx * ldb];      // a non-basic slack: column idx of inv(B) is dense
+        if (pse && !reset) ref2 = d.refsp[idx] != 0 && !(fin.pend && fin.rclr && idx + 1 == fin.kp);
+    }
+    double acc = 0.0;
+#pragma unroll
+    for (int u = 0; u < CU; ++u) acc += cv[u] * rv[u];
+    if (j1 >= 0)
+        for (int t = beg + CU; t < end; ++t) acc += d.A.cval[t] * brow[(size_t)d.A.cind[t] * ldb];
+    if (lead) {
+        // the compact rho for the rank-1 update of the commit
+        for (int t = threadIdx.x; t < ns; t += blockDim.x) {
+            const int c = (t < nr) ? d.rlist[t] : kp - 1;
+            d.rho_idx[t] = c;
+            d.rho_val[t] = (t < nr) ? brow[(size_t)c * ldb] : 1.0;
+        }
+        if (threadIdx.x == 0) {
+            st->p = p;
+            st->kp = kp;
+            st->delta = best.k2;
+            st->trow_max_bits = 0ull;
+            st->ns = ns;
+            st->dinf = 0;
+        }
+    }
+    double tv1 = (j1 >= 0) ? acc : 0.0;
+    double tv2 = (j2 >= 0) ? -rho2 : 0.0;
+    if (s1 == NS) tv1 = 0.0;
+    if (s2 == NS) tv2 = 0.0;
+    if (j1 >= 0) d.trow[j1] = tv1;
+    if (j2 >= 0) d.trow[j2] = tv2;
+    double gsum = 0.0;
+    if (pse) {
+        const double w1 = ref1 ? tv1 : 0.0, w2 = ref2 ? tv2 : 0.0;
+        if (idx < n) d.wcol[idx] = w1;
+        if (idx < m) d.ys[idx] = w2;
+        gsum = w1 * w1 + w2 * w2;
+    }
+    const double bmax = wmax(fmax(fabs(tv1), fabs(tv2)));
+    const double g = pse ? wsum(gsum) : 0.0;
+    RatioIn rin2 = rin;
+    rin2.delta = best.k2;
+    const RatioCtx x = ratio_ctx(rin2, bmax);
+    Cand c = no_cand(DBL_MAX);
+    Cand e;
+    if (j1 >= 0 && pass1_cand(x, tv1, cb1, s1, j1, m + idx + 1, e) && better<1>(e, c)) c = e;
+    if (j2 >= 0 && pass1_cand(x, tv2, cb2, s2, j2, idx + 1, e) && better<1>(e, c)) c = e;
+    const Cand b = wave_best<1>(c);
+    if (lane == 0) {
+        tmax_part(d)[grp] = bmax;
+        if (pse) d.gpart[grp] = g;
+        cand_pass1(d)[grp] = b;
+        d.tslots[grp] = wall_clock64();
+    }
+}
+
+// ---------------------------------------------------------------------------
 // k_dual_ratio: blocks [0, gn) — pass-1 choice from the ncb group candidates
 // (a group whose candidate fails the global significance tolerance is
 // rescanned), then the pass-2 candidates of positions [256 b, 256 b + 256),
@@ -1013,6 +1179,33 @@ __global__ void __launch_bounds__(256) k_dual_ratio(SpxDev d, int gn, int tiles_
     DState *st = d.st;
     const int stop = st->stop;               // tested before the first store
     const int m = d.m, n = d.n;
+    if ((int)blockIdx.x >= gn && !d.A.dense) {
+        // sparse A: work = ys - A w, one row per thread over its CSR entries
+        // (update_gamma :1103-1134; entries loaded ahead, fixed order)
+        const int r = (blockIdx.x - gn) * 256 + threadIdx.x;
+        if (r >= m) return;
+        const int beg = d.A.rptr[r], end = d.A.rptr[r + 1];
+        constexpr int RU = 16;
+        int cc[RU];
+        double av[RU];
+#pragma unroll
+        for (int u = 0; u < RU; ++u) {
+            const bool ok = beg + u < end;
+            cc[u] = ok ? d.A.rcol[beg + u] : 0;
+            av[u] = ok ? d.A.rval[beg + u] : 0.0;
+        }
+        const double ysr = d.ys[r];
+        if (stop) return;
+        double wv[RU];
+#pragma unroll
+        for (int u = 0; u < RU; ++u) wv[u] = (beg + u < end) ? d.wcol[cc[u]] : 0.0;
+        double acc = 0.0;
+#pragma unroll
+        for (int u = 0; u < RU; ++u) acc += av[u] * wv[u];
+        for (int t = beg + RU; t < end; ++t) acc += d.A.rval[t] * d.wcol[d.A.rcol[t]];
+        d.work[r] = ysr - acc;
+        return;
+    }
     if ((int)blockIdx.x >= gn) {
         const int b = blockIdx.x - gn;
         const int tile = b % tiles_m, split = b / tiles_m, splits = (gridDim.x - gn) / tiles_m;
@@ -1332,7 +1525,7 @@ __global__ void __launch_bounds__(512) k_dual_ftran_reduce(SpxDev d, int splits,
 // ---------------------------------------------------------------------------
 constexpr int FONE_MAX = 2048;
 
-template <int NRHS>
+template <int NRHS, int SP>
 __global__ void __launch_bounds__(1024) k_dual_ftran1(SpxDev d, int gn, int awsplits, int ncb, int nr_cap)
 {
     const TraceScope trace_(d, 3);
@@ -1375,45 +1568,60 @@ __global__ void __launch_bounds__(1024) k_dual_ftran1(SpxDev d, int gn, int awsp
     int kq = 0;
     const int q = pick_resolve(d, pin, NRHS == 2, &kq);
     if (!q) return;
-    const double *hcol = (kq > m) ? d.A.A + (size_t)(kq - m - 1) * d.A.lda : nullptr;
+    const double *hcol = (!SP && kq > m) ? d.A.A + (size_t)(kq - m - 1) * d.A.lda : nullptr;
     TPH(3, 1);
     auto hval = [&](int c) { return hcol ? hcol[c] : (c == kq - 1 ? -1.0 : 0.0); };
     double ua = 0.0;
-    if (kh <= m) ua = hval(kh - 1);
+    if (!SP && kh <= m) ua = hval(kh - 1);
     double a = 0.0, b = 0.0;
+    if (SP) {
+        // sparse h = -N[q]: tcol = inv(B) h over the entries of column q,
+        // the waves splitting them; the columns of inv(B) are read whole
+        // (unit columns included), so no unit part is added
+        if (kq > m) {
+            const int cq = kq - m - 1;
+            const int beg = d.A.cptr[cq], end = d.A.cptr[cq + 1];
+            for (int t = beg + w; t < end; t += nw)
+                a += d.A.cval[t] * (act ? Bv[(size_t)d.A.cind[t] * ldb + r] : 0.0);
+        } else if (w == 0) {
+            a = act ? -Bv[(size_t)(kq - 1) * ldb + r] : 0.0;
+        }
+    }
     {
         double xa[G];
 #pragma unroll
-        for (int u = 0; u < G; ++u) xa[u] = (w + u * nw < nr) ? hval(c0[u]) : 0.0;
+        for (int u = 0; u < G; ++u) xa[u] = (!SP && w + u * nw < nr) ? hval(c0[u]) : 0.0;
 #pragma unroll
         for (int u = 0; u < G; ++u) {
-            a += bv[u] * xa[u];
+            if (!SP) a += bv[u] * xa[u];
             if (NRHS == 2) b += bv[u] * wv[u];
         }
     }
-    int t = w + G * nw;
-    for (; t + 3 * nw < nr; t += 4 * nw) {
-        int c[4];
-        double x[4], xa[4], xb[4];
+    if (!SP || NRHS == 2) {
+        int t = w + G * nw;
+        for (; t + 3 * nw < nr; t += 4 * nw) {
+            int c[4];
+            double x[4], xa[4], xb[4];
 #pragma unroll
-        for (int u = 0; u < 4; ++u) c[u] = rl[t + u * nw];
+            for (int u = 0; u < 4; ++u) c[u] = rl[t + u * nw];
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
-            x[u] = act ? Bv[(size_t)c[u] * ldb + r] : 0.0;
-            xa[u] = hval(c[u]);
-            xb[u] = (NRHS == 2) ? d.work[c[u]] : 0.0;
+            for (int u = 0; u < 4; ++u) {
+                x[u] = act ? Bv[(size_t)c[u] * ldb + r] : 0.0;
+                xa[u] = SP ? 0.0 : hval(c[u]);
+                xb[u] = (NRHS == 2) ? d.work[c[u]] : 0.0;
+            }
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                if (!SP) a += x[u] * xa[u];
+                if (NRHS == 2) b += x[u] * xb[u];
+            }
         }
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-            a += x[u] * xa[u];
-            if (NRHS == 2) b += x[u] * xb[u];
+        for (; t < nr; t += nw) {
+            const int c = rl[t];
+            const double x = act ? Bv[(size_t)c * ldb + r] : 0.0;
+            if (!SP) a += x * hval(c);
+            if (NRHS == 2) b += x * d.work[c];
         }
-    }
-    for (; t < nr; t += nw) {
-        const int c = rl[t];
-        const double x = act ? Bv[(size_t)c * ldb + r] : 0.0;
-        a += x * hval(c);
-        if (NRHS == 2) b += x * d.work[c];
     }
     sp[0][w][lane] = a;
     if (NRHS == 2) sp[NRHS - 1][w][lane] = b;
@@ -1599,7 +1807,8 @@ __global__ void __launch_bounds__(256) k_dual_commit(SpxDev d, int pse, int nvb,
             // columns, inv(B) once for both right-hand sides, read + write of
             // the updated columns, and the O(m + n) vectors
             const int ns = st->ns;
-            const double rowb = rowpath ? 8.0 * (double)ns * n : 8.0 * (double)m * n;
+            const double rowb = rowpath == 1 ? 8.0 * (double)ns * n
+                                : rowpath == 2 ? 12.0 * (double)d.A.nnz : 8.0 * (double)m * n;
             const unsigned long long tk0 = st->tk_start, tk1 = st->tk_end, tk2 = st->tk_next;
             if (rowpath && tk1 > tk0) {
                 st->bytes_trow += rowb;
@@ -1709,6 +1918,7 @@ DualPlan dual_plan(const SpxDev &d, int nr_max, int nwl_max, int pse, int rigoro
     pl.uchunks = std::max(1, std::min(2048 / tiles_f, cdiv(ns_max, 4)));
     pl.lpsu = cdiv(ns_max, pl.uchunks);
     pl.uchunks = cdiv(ns_max, pl.lpsu);
+    pl.colpath = (!d.A.dense && !rigorous && nr_max <= FONE_MAX) ? 1 : 0;
     pl.awsplits = std::max(1, std::min(cdiv(std::max(nwl_max, 1), 32), 64));
     pl.awsplits = std::max(1, std::min<int>(pl.awsplits, (int)(d.awpart_cap / std::max(m, 1))));
     return pl;
@@ -1760,6 +1970,23 @@ void dual_iteration2(hipStream_t s, const SpxDev &d, const DualPlan &pl, hipEven
     const int m = d.m, n = d.n;
     const int gv = cdiv(std::max(m, n), 256), gn = cdiv(n, 256), tiles_m = cdiv(m, 512);
     int ncb = 4 * gv;                                  // 64-slot groups of the pivot row
+    if (pl.colpath) {
+        // sparse A: four kernels, as the dense row path
+        if (ev0) (void)hipEventRecord(ev0, s);
+        hipLaunchKernelGGL(k_dual_col, dim3(gv), dim3(256), 0, s, d, pl.pse);
+        if (ev1) (void)hipEventRecord(ev1, s);
+        hipLaunchKernelGGL(k_dual_ratio, dim3(gn + (pl.pse ? cdiv(m, 256) : 0)), dim3(256), 0, s, d, gn, tiles_m, 2,
+                           ncb);
+        if (pl.pse)
+            hipLaunchKernelGGL((k_dual_ftran1<2, 1>), dim3(cdiv(m, 64)), dim3(64 * pl.fwaves), 0, s, d, gn,
+                               pl.awsplits, ncb, pl.nr_cap);
+        else
+            hipLaunchKernelGGL((k_dual_ftran1<1, 1>), dim3(cdiv(m, 64)), dim3(64 * pl.fwaves), 0, s, d, gn,
+                               pl.awsplits, ncb, pl.nr_cap);
+        hipLaunchKernelGGL(k_dual_commit, dim3(gv + tiles_m * pl.uchunks), dim3(256), 0, s, d, pl.pse, gv, tiles_m,
+                           pl.lpsu, 2, bytes_fixed(d));
+        return;
+    }
     if (pl.rowpath) {
         // chuzr, rho and the pivot row in one kernel
         ncb = cdiv(std::max(m, n), 64);
@@ -1781,10 +2008,10 @@ void dual_iteration2(hipStream_t s, const SpxDev &d, const DualPlan &pl, hipEven
     if (pl.fused) {
         if (pl.fone) {
             if (pl.pse)
-                hipLaunchKernelGGL(k_dual_ftran1<2>, dim3(cdiv(m, 64)), dim3(64 * pl.fwaves), 0, s, d, gn,
+                hipLaunchKernelGGL((k_dual_ftran1<2, 0>), dim3(cdiv(m, 64)), dim3(64 * pl.fwaves), 0, s, d, gn,
                                    pl.awsplits, ncb, pl.nr_cap);
             else
-                hipLaunchKernelGGL(k_dual_ftran1<1>, dim3(cdiv(m, 64)), dim3(64 * pl.fwaves), 0, s, d, gn,
+                hipLaunchKernelGGL((k_dual_ftran1<1, 0>), dim3(cdiv(m, 64)), dim3(64 * pl.fwaves), 0, s, d, gn,
                                    pl.awsplits, ncb, pl.nr_cap);
         } else if (pl.pse)
             launch_ftran<2, 1, 1>(s, d, pl, gn, ncb);

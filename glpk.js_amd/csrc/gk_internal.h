@@ -155,6 +155,7 @@ struct DualPlan {
     int nr_cap, ns_cap;           // upper bounds of nr / ns over the batch (speculative list loads)
     int fone, fwaves;             // 1: FTRAN in one kernel (k_dual_ftran1), fwaves waves per 64-row block
     int lpsu;                     // rank-1 update: list entries per chunk
+    int colpath;                  // 1: sparse A — k_dual_col, CSR A w in k_dual_ratio, sparse k_dual_ftran1
 };
 void dual_batch_begin(hipStream_t s, const SpxDev &d, const DualPlan &pl);
 void dual_batch_end(hipStream_t s, const SpxDev &d, const DualPlan &pl);
