@@ -239,4 +239,75 @@ static __device__ void build_hq(const SpxDev &d, int q)
     __syncthreads();
 }
 
+// ---------------------------------------------------------------------------
+// per-wave candidate buffers and profiling stamps shared by the pivot
+// pipelines (gk_dual.hip, gk_primal.hip)
+// ---------------------------------------------------------------------------
+static inline int cdiv(int a, int b) { return (a + b - 1) / b; }
+__device__ __forceinline__ int gv_of(int m, int n) { return (max(m, n) + 255) / 256; }
+__device__ __forceinline__ Cand *cand_chuzr(const SpxDev &d) { return (Cand *)d.cand; }
+__device__ __forceinline__ Cand no_cand(double k1)
+{
+    Cand c; c.k1 = k1; c.k2 = 0.0; c.idx = 0; c.aux = 0;
+    return c;
+}
+
+// Per-wave outputs, 4 gv entries each, so that no producer needs a block
+// barrier and every consumer wave reduces them on its own: chuzr candidates
+// (one per wave of k_dual_commit / k_dual_prep), pass-1 candidates (one per
+// 64-slot group of the pivot row), pass-2 candidates (one per wave of
+// k_dual_ratio).  gpart: gamma_p sums of the 64-slot groups [4 gv), then
+// their max |trow| [4 gv).
+__device__ __forceinline__ Cand *cand_pass1(const SpxDev &d) { return (Cand *)d.cand + 4 * gv_of(d.m, d.n); }
+__device__ __forceinline__ Cand *cand_pass2(const SpxDev &d) { return (Cand *)d.cand + 8 * gv_of(d.m, d.n); }
+__device__ __forceinline__ double *tmax_part(const SpxDev &d) { return d.gpart + 4 * gv_of(d.m, d.n); }
+
+// the choice over cnt stored candidates, made by one wave (lane-strided scan,
+// then the butterfly): the same result in every wave that calls it
+template <int MODE>
+__device__ __forceinline__ Cand wave_scan(const Cand *a, int cnt)
+{
+    Cand c = no_cand(0.0);
+    for (int b = (int)(threadIdx.x & 63); b < cnt; b += 64) {
+        const Cand e = a[b];
+        if (better<MODE>(e, c)) c = e;
+    }
+    return wave_best<MODE>(c);
+}
+
+__device__ __forceinline__ unsigned long long wmax_u64(unsigned long long v)
+{
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        const unsigned long long u = __shfl_xor(v, o);
+        v = u > v ? u : v;
+    }
+    return v;
+}
+
+// profiling (gk_bfd_profile(bfd, 2), eager launches): device clock at block
+// entry (thread 0) and the latest wave exit of the block
+struct TraceScope {
+    unsigned long long *p;
+    __device__ __forceinline__ TraceScope(const SpxDev &d, int kid)
+        : p((d.trace && blockIdx.x < (unsigned)TRACE_BLOCKS) ? d.trace + ((size_t)kid * TRACE_BLOCKS + blockIdx.x) * 2
+                                                              : nullptr)
+    {
+        if (p && threadIdx.x == 0) p[0] = wall_clock64();
+    }
+    __device__ __forceinline__ ~TraceScope()
+    {
+        if (p && (threadIdx.x & 63) == 0) atomicMax(p + 1, wall_clock64());
+    }
+};
+
+// phase stamp of wave 0 (profiling only)
+#define TPH(kid, ph)                                                                                              \
+    do {                                                                                                          \
+        if (d.trace && threadIdx.x == 0 && blockIdx.x < (unsigned)TRACE_BLOCKS)                                   \
+            d.trace[(size_t)TRACE_KERNELS * TRACE_BLOCKS * 2 + ((size_t)(kid) * TRACE_BLOCKS + blockIdx.x) * 8 + \
+                    (ph)] = wall_clock64();                                                                       \
+    } while (0)
+
+
 }  // namespace gk

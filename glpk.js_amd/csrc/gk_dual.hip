@@ -37,72 +37,6 @@
 
 namespace gk {
 
-static inline int cdiv(int a, int b) { return (a + b - 1) / b; }
-__device__ __forceinline__ int gv_of(int m, int n) { return (max(m, n) + 255) / 256; }
-__device__ __forceinline__ Cand *cand_chuzr(const SpxDev &d) { return (Cand *)d.cand; }
-__device__ __forceinline__ Cand no_cand(double k1)
-{
-    Cand c; c.k1 = k1; c.k2 = 0.0; c.idx = 0; c.aux = 0;
-    return c;
-}
-
-// Per-wave outputs, 4 gv entries each, so that no producer needs a block
-// barrier and every consumer wave reduces them on its own: chuzr candidates
-// (one per wave of k_dual_commit / k_dual_prep), pass-1 candidates (one per
-// 64-slot group of the pivot row), pass-2 candidates (one per wave of
-// k_dual_ratio).  gpart: gamma_p sums of the 64-slot groups [4 gv), then
-// their max |trow| [4 gv).
-__device__ __forceinline__ Cand *cand_pass1(const SpxDev &d) { return (Cand *)d.cand + 4 * gv_of(d.m, d.n); }
-__device__ __forceinline__ Cand *cand_pass2(const SpxDev &d) { return (Cand *)d.cand + 8 * gv_of(d.m, d.n); }
-__device__ __forceinline__ double *tmax_part(const SpxDev &d) { return d.gpart + 4 * gv_of(d.m, d.n); }
-
-// the choice over cnt stored candidates, made by one wave (lane-strided scan,
-// then the butterfly): the same result in every wave that calls it
-template <int MODE>
-__device__ __forceinline__ Cand wave_scan(const Cand *a, int cnt)
-{
-    Cand c = no_cand(0.0);
-    for (int b = (int)(threadIdx.x & 63); b < cnt; b += 64) {
-        const Cand e = a[b];
-        if (better<MODE>(e, c)) c = e;
-    }
-    return wave_best<MODE>(c);
-}
-
-__device__ __forceinline__ unsigned long long wmax_u64(unsigned long long v)
-{
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-        const unsigned long long u = __shfl_xor(v, o);
-        v = u > v ? u : v;
-    }
-    return v;
-}
-
-// profiling (gk_bfd_profile(bfd, 2), eager launches): device clock at block
-// entry (thread 0) and the latest wave exit of the block
-struct TraceScope {
-    unsigned long long *p;
-    __device__ __forceinline__ TraceScope(const SpxDev &d, int kid)
-        : p((d.trace && blockIdx.x < (unsigned)TRACE_BLOCKS) ? d.trace + ((size_t)kid * TRACE_BLOCKS + blockIdx.x) * 2
-                                                              : nullptr)
-    {
-        if (p && threadIdx.x == 0) p[0] = wall_clock64();
-    }
-    __device__ __forceinline__ ~TraceScope()
-    {
-        if (p && (threadIdx.x & 63) == 0) atomicMax(p + 1, wall_clock64());
-    }
-};
-
-// phase stamp of wave 0 (profiling only)
-#define TPH(kid, ph)                                                                                              \
-    do {                                                                                                          \
-        if (d.trace && threadIdx.x == 0 && blockIdx.x < (unsigned)TRACE_BLOCKS)                                   \
-            d.trace[(size_t)TRACE_KERNELS * TRACE_BLOCKS * 2 + ((size_t)(kid) * TRACE_BLOCKS + blockIdx.x) * 8 + \
-                    (ph)] = wall_clock64();                                                                       \
-    } while (0)
-
 // ---------------------------------------------------------------------------
 // list GEMV of one 512-row tile over list entries [t0, t1):
 //   o[k*rows + r] = sum_t M[list[t]*ld + r] * x_k(t, list[t])
@@ -1015,7 +949,7 @@ __global__ void __launch_bounds__(1024) k_dual_row(SpxDev d, int pse, int nr_cap
 // the commit) and the scalar state; the other blocks patch what it changes,
 // as in k_dual_row.
 // ---------------------------------------------------------------------------
-__global__ void __launch_bounds__(256) k_dual_col(SpxDev d, int pse)
+__global__ void __launch_bounds__(256) k_dual_col(SpxDev d, int pse, int nr_cap)
 {
     const TraceScope trace_(d, 1);
     DState *st = d.st;
@@ -1051,6 +985,15 @@ __global__ void __launch_bounds__(256) k_dual_col(SpxDev d, int pse)
         const bool ok = beg + u < end;
         ci[u] = ok ? d.A.cind[beg + u] : 0;
         cv[u] = ok ? d.A.cval[beg + u] : 0.0;
+    }
+    // the dense-column list entries this thread publishes rho for
+    constexpr int PU = 4;
+    const int tpub = blockIdx.x * blockDim.x + threadIdx.x, npub = gridDim.x * blockDim.x;
+    int cpub[PU];
+#pragma unroll
+    for (int u = 0; u < PU; ++u) {
+        const int t = tpub + u * npub;
+        cpub[u] = (t < nr_cap) ? d.rlist[t] : 0;
     }
     if (stop) return;
     if (lead && threadIdx.x == 0) st->tk_start = wall_clock64();
@@ -1119,13 +1062,31 @@ __global__ void __launch_bounds__(256) k_dual_col(SpxDev d, int pse)
     for (int u = 0; u < CU; ++u) acc += cv[u] * rv[u];
     if (j1 >= 0)
         for (int t = beg + CU; t < end; ++t) acc += d.A.cval[t] * brow[(size_t)d.A.cind[t] * ldb];
-    if (lead) {
-        // the compact rho for the rank-1 update of the commit
-        for (int t = threadIdx.x; t < ns; t += blockDim.x) {
+    {
+        // the compact rho for the rank-1 update of the commit, spread over
+        // the grid (list entries loaded at entry)
+        double vpub[PU];
+#pragma unroll
+        for (int u = 0; u < PU; ++u) {
+            const int t = tpub + u * npub;
+            if (t == nr) cpub[u] = kp - 1;
+            vpub[u] = (t < nr) ? brow[(size_t)cpub[u] * ldb] : 1.0;
+        }
+#pragma unroll
+        for (int u = 0; u < PU; ++u) {
+            const int t = tpub + u * npub;
+            if (t < ns) {
+                d.rho_idx[t] = cpub[u];
+                d.rho_val[t] = vpub[u];
+            }
+        }
+        for (int t = tpub + PU * npub; t < ns; t += npub) {
             const int c = (t < nr) ? d.rlist[t] : kp - 1;
             d.rho_idx[t] = c;
             d.rho_val[t] = (t < nr) ? brow[(size_t)c * ldb] : 1.0;
         }
+    }
+    if (lead) {
         if (threadIdx.x == 0) {
             st->p = p;
             st->kp = kp;
@@ -1525,7 +1486,7 @@ __global__ void __launch_bounds__(512) k_dual_ftran_reduce(SpxDev d, int splits,
 // ---------------------------------------------------------------------------
 constexpr int FONE_MAX = 2048;
 
-template <int NRHS, int SP>
+template <int NRHS, int SP, int RPB>
 __global__ void __launch_bounds__(1024) k_dual_ftran1(SpxDev d, int gn, int awsplits, int ncb, int nr_cap)
 {
     const TraceScope trace_(d, 3);
@@ -1536,7 +1497,10 @@ __global__ void __launch_bounds__(1024) k_dual_ftran1(SpxDev d, int gn, int awsp
     const int lane = threadIdx.x & 63;
     const int w = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
     const int nw = blockDim.x >> 6;
-    const int r = blockIdx.x * 64 + lane;
+    constexpr int SL = 64 / RPB;             // list slices per wave (RPB rows per block)
+    const int sl = lane / RPB;
+    const int r = blockIdx.x * RPB + (lane % RPB);
+    const int gs = w * SL + sl, NSL = nw * SL;
     const bool act = r < m;
     const size_t ldb = (size_t)d.ldb;
     const int *__restrict__ rl = d.rlist;
@@ -1549,15 +1513,15 @@ __global__ void __launch_bounds__(1024) k_dual_ftran1(SpxDev d, int gn, int awsp
     double bv[G], wv[G];
 #pragma unroll
     for (int u = 0; u < G; ++u) {
-        const int t = w + u * nw;
+        const int t = gs + u * NSL;
         c0[u] = (t < nr_cap) ? rl[t] : 0;
     }
     const int nr = st->nr;
-    const int kh = (w == 0 && act) ? d.head[r] : m + 1;
+    const int kh = (w == 0 && sl == 0 && act) ? d.head[r] : m + 1;
     // trip 2: q-independent inv(B) values and work_c
 #pragma unroll
     for (int u = 0; u < G; ++u) {
-        const bool ok = w + u * nw < nr;
+        const bool ok = gs + u * NSL < nr;
         bv[u] = (act && ok) ? Bv[(size_t)c0[u] * ldb + r] : 0.0;
         wv[u] = (NRHS == 2 && ok) ? d.work[c0[u]] : 0.0;
     }
@@ -1581,16 +1545,16 @@ __global__ void __launch_bounds__(1024) k_dual_ftran1(SpxDev d, int gn, int awsp
         if (kq > m) {
             const int cq = kq - m - 1;
             const int beg = d.A.cptr[cq], end = d.A.cptr[cq + 1];
-            for (int t = beg + w; t < end; t += nw)
+            for (int t = beg + gs; t < end; t += NSL)
                 a += d.A.cval[t] * (act ? Bv[(size_t)d.A.cind[t] * ldb + r] : 0.0);
-        } else if (w == 0) {
+        } else if (gs == 0) {
             a = act ? -Bv[(size_t)(kq - 1) * ldb + r] : 0.0;
         }
     }
     {
         double xa[G];
 #pragma unroll
-        for (int u = 0; u < G; ++u) xa[u] = (!SP && w + u * nw < nr) ? hval(c0[u]) : 0.0;
+        for (int u = 0; u < G; ++u) xa[u] = (!SP && gs + u * NSL < nr) ? hval(c0[u]) : 0.0;
 #pragma unroll
         for (int u = 0; u < G; ++u) {
             if (!SP) a += bv[u] * xa[u];
@@ -1598,12 +1562,12 @@ __global__ void __launch_bounds__(1024) k_dual_ftran1(SpxDev d, int gn, int awsp
         }
     }
     if (!SP || NRHS == 2) {
-        int t = w + G * nw;
-        for (; t + 3 * nw < nr; t += 4 * nw) {
+        int t = gs + G * NSL;
+        for (; t + 3 * NSL < nr; t += 4 * NSL) {
             int c[4];
             double x[4], xa[4], xb[4];
 #pragma unroll
-            for (int u = 0; u < 4; ++u) c[u] = rl[t + u * nw];
+            for (int u = 0; u < 4; ++u) c[u] = rl[t + u * NSL];
 #pragma unroll
             for (int u = 0; u < 4; ++u) {
                 x[u] = act ? Bv[(size_t)c[u] * ldb + r] : 0.0;
@@ -1616,7 +1580,7 @@ __global__ void __launch_bounds__(1024) k_dual_ftran1(SpxDev d, int gn, int awsp
                 if (NRHS == 2) b += x[u] * xb[u];
             }
         }
-        for (; t < nr; t += nw) {
+        for (; t < nr; t += NSL) {
             const int c = rl[t];
             const double x = act ? Bv[(size_t)c * ldb + r] : 0.0;
             if (!SP) a += x * hval(c);
@@ -1628,12 +1592,14 @@ __global__ void __launch_bounds__(1024) k_dual_ftran1(SpxDev d, int gn, int awsp
     TPH(3, 2);
     __syncthreads();
     TPH(3, 3);
-    if (w != 0 || !act) return;
+    if (w != 0 || sl != 0 || !act) return;
     double va = 0.0, vb = 0.0;
-    for (int k = 0; k < nw; ++k) {
-        va += sp[0][k][lane];
-        if (NRHS == 2) vb += sp[NRHS - 1][k][lane];
-    }
+    for (int k = 0; k < nw; ++k)
+#pragma unroll
+        for (int z = 0; z < SL; ++z) {
+            va += sp[0][k][lane + z * RPB];
+            if (NRHS == 2) vb += sp[NRHS - 1][k][lane + z * RPB];
+        }
     d.tcol[r] = va + ua;
     if (NRHS == 2) d.u[r] = vb + ub;
 }
@@ -1973,15 +1939,17 @@ void dual_iteration2(hipStream_t s, const SpxDev &d, const DualPlan &pl, hipEven
     if (pl.colpath) {
         // sparse A: four kernels, as the dense row path
         if (ev0) (void)hipEventRecord(ev0, s);
-        hipLaunchKernelGGL(k_dual_col, dim3(gv), dim3(256), 0, s, d, pl.pse);
+        hipLaunchKernelGGL(k_dual_col, dim3(gv), dim3(256), 0, s, d, pl.pse, pl.nr_cap);
         if (ev1) (void)hipEventRecord(ev1, s);
         hipLaunchKernelGGL(k_dual_ratio, dim3(gn + (pl.pse ? cdiv(m, 256) : 0)), dim3(256), 0, s, d, gn, tiles_m, 2,
                            ncb);
+        // 16 rows per block (4 list slices per wave): 4x the blocks of the
+        // dense layout for the small m of sparse problems
         if (pl.pse)
-            hipLaunchKernelGGL((k_dual_ftran1<2, 1>), dim3(cdiv(m, 64)), dim3(64 * pl.fwaves), 0, s, d, gn,
+            hipLaunchKernelGGL((k_dual_ftran1<2, 1, 16>), dim3(cdiv(m, 16)), dim3(64 * pl.fwaves), 0, s, d, gn,
                                pl.awsplits, ncb, pl.nr_cap);
         else
-            hipLaunchKernelGGL((k_dual_ftran1<1, 1>), dim3(cdiv(m, 64)), dim3(64 * pl.fwaves), 0, s, d, gn,
+            hipLaunchKernelGGL((k_dual_ftran1<1, 1, 16>), dim3(cdiv(m, 16)), dim3(64 * pl.fwaves), 0, s, d, gn,
                                pl.awsplits, ncb, pl.nr_cap);
         hipLaunchKernelGGL(k_dual_commit, dim3(gv + tiles_m * pl.uchunks), dim3(256), 0, s, d, pl.pse, gv, tiles_m,
                            pl.lpsu, 2, bytes_fixed(d));
@@ -2008,10 +1976,10 @@ void dual_iteration2(hipStream_t s, const SpxDev &d, const DualPlan &pl, hipEven
     if (pl.fused) {
         if (pl.fone) {
             if (pl.pse)
-                hipLaunchKernelGGL((k_dual_ftran1<2, 0>), dim3(cdiv(m, 64)), dim3(64 * pl.fwaves), 0, s, d, gn,
+                hipLaunchKernelGGL((k_dual_ftran1<2, 0, 64>), dim3(cdiv(m, 64)), dim3(64 * pl.fwaves), 0, s, d, gn,
                                    pl.awsplits, ncb, pl.nr_cap);
             else
-                hipLaunchKernelGGL((k_dual_ftran1<1, 0>), dim3(cdiv(m, 64)), dim3(64 * pl.fwaves), 0, s, d, gn,
+                hipLaunchKernelGGL((k_dual_ftran1<1, 0, 64>), dim3(cdiv(m, 64)), dim3(64 * pl.fwaves), 0, s, d, gn,
                                    pl.awsplits, ncb, pl.nr_cap);
         } else if (pl.pse)
             launch_ftran<2, 1, 1>(s, d, pl, gn, ncb);

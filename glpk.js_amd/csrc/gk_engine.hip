@@ -96,6 +96,7 @@ struct GraphEntry {
     SpxDev d;
     DualPlan pl;
     int K = 0;
+    int kind = 0;                               // 0: dual, 1: primal
     hipGraphExec_t exec = nullptr;
     unsigned long long last = 0;
 };
@@ -234,7 +235,7 @@ static int reinvert_core(gk_bfd *f, const BasisSplit &bs, const MatDev *Adense, 
         f->piv.ensure(k);
         f->flag.ensure(1);
         const bool blocked = k <= gj_blocked_max();
-        if (blocked) gauss_jordan_blocked(s, f->X.p, f->Y.p, k, f->piv_step.p, f->piv.p, f->flag.p, 1e-15);
+        if (blocked) result = gauss_jordan_blocked(s, f->X.p, f->Y.p, k, f->piv_step.p, f->piv.p, f->flag.p, 1e-15);
         else gauss_jordan(s, f->X.p, f->Y.p, k, f->piv_step.p, f->piv.p, f->flag.p, 1e-15, &result);
         int flag = 0;
         HIPCHK(hipMemcpyAsync(&flag, f->flag.p, sizeof(int), hipMemcpyDeviceToHost, s));
@@ -245,7 +246,7 @@ static int reinvert_core(gk_bfd *f, const BasisSplit &bs, const MatDev *Adense, 
             f->stats.seconds_reinvert += now_s() - t0;
             return 1;   // BFD_ESING
         }
-        if (blocked) extract_inverse_blocked(s, f->X.p, k, f->piv.p, f->piv_step.p, f->CinvR.p);
+        if (blocked) extract_inverse_blocked(s, result, k, f->piv.p, f->piv_step.p, f->CinvR.p);
         else extract_inverse_rowmajor(s, result, k, f->piv.p, f->CinvR.p);
         if (ms > 0) gemm_bs_cinv(s, f->BS.p, ms, k, f->CinvR.p, f->G.p, 1);
     }
@@ -317,8 +318,12 @@ static void engine_alloc(Engine &E, int m, int n)
     }
     E.rlist.ensure(m); E.rpos.ensure(m); E.rho_idx.ensure((size_t)m + 1); E.rho_val.ensure((size_t)m + 1);
     const size_t gv = (size_t)(std::max(m, n) + 255) / 256 + 1;
-    E.gpart.ensure(8 * (size_t)gv);              // gamma_p sums, then per-block max |trow| (64-slot blocks)
-    E.cand.ensure(3 * 12 * (size_t)gv);          // candidates (24-byte entries): chuzr | pass 1 | pass 2, 4 gv each
+    // dual: gamma_p sums, then per-block max |trow| (64-slot blocks), 4 gv
+    // each; primal: max |tcol|, d_q sums, gamma_q sums of the row groups, 16 gv each
+    E.gpart.ensure(56 * (size_t)gv);
+    // candidates (24-byte entries): chuzr | pass 1 | pass 2, 4 gv each, then
+    // the primal pass-1 candidates of the row groups, 16 gv
+    E.cand.ensure(3 * 28 * (size_t)gv);
     E.wlist.ensure(n); E.wpos.ensure(n);
     E.awpart.ensure((size_t)AW_SPLITS * m);
     {
@@ -849,7 +854,9 @@ struct Spx {
     }
 
     void init();
-    void run_graph(const SpxDev &d, const DualPlan &pl, int K);
+    void run_graph(const SpxDev &d, const DualPlan &pl, int K, int kind = 0);
+    bool lists_stale = false;                   // rlist / rpos / nr to rebuild from the header
+    void rebuild_lists();
     void prof_events(int K)
     {
         while ((int)E->ev.size() < 2 * K) {
@@ -1032,8 +1039,24 @@ int Spx::batch(int K, int rigorous)
             for (int t = 0; t < K; t++) dual_iteration2(s, d, pl, ev0(t), ev1(t));
             dual_batch_end(s, d, pl);
         }
+    } else if (!rigorous && primal_fast_ok(d)) {
+        if (lists_stale) {
+            rebuild_lists();
+            d = dev();
+        }
+        auto bucket = [](int x, int cap) {
+            int g = std::max(64, x / 8);
+            return std::min(cap, (x + g - 1) / g * g);
+        };
+        const DualPlan pl = primal_plan(d, bucket(hs.nr + K + 1, m), pse);
+        if (K >= 4) run_graph(d, pl, K, 1);
+        else {
+            primal_batch_begin(s, d);
+            for (int t = 0; t < K; t++) primal_iteration2(s, d, pl);
+        }
     } else {
         for (int t = 0; t < K; t++) primal_iteration(s, d, pse, rigorous);
+        lists_stale = true;                   // the single-workgroup kernels do not maintain rlist
     }
     pull_state();
     f->stats.batches++;
@@ -1062,12 +1085,31 @@ int Spx::batch(int K, int rigorous)
     return hs.stop == ST_RUN ? ST_BATCH : hs.stop;
 }
 
-void Spx::run_graph(const SpxDev &d, const DualPlan &pl, int K)
+// rlist / rpos (the dense columns of inv(B): the non-basic slacks) from the
+// header, after batches of the single-workgroup primal kernels
+void Spx::rebuild_lists()
+{
+    pull();
+    std::vector<int> rl, rp(m, -1);
+    for (int c = 1; c <= m; c++)
+        if (bind[c] > m) {
+            rp[c - 1] = (int)rl.size();
+            rl.push_back(c - 1);
+        }
+    if (!rl.empty()) HIPCHK(hipMemcpyAsync(E->rlist.p, rl.data(), rl.size() * sizeof(int), hipMemcpyHostToDevice, s));
+    HIPCHK(hipMemcpyAsync(E->rpos.p, rp.data(), (size_t)m * sizeof(int), hipMemcpyHostToDevice, s));
+    hs.nr = (int)rl.size();
+    push_state();
+    sync();
+    lists_stale = false;
+}
+
+void Spx::run_graph(const SpxDev &d, const DualPlan &pl, int K, int kind)
 {
     Engine &En = *E;
     GraphEntry *hit = nullptr;
     for (auto &g : En.graphs)
-        if (g.K == K && std::memcmp(&g.pl, &pl, sizeof(pl)) == 0 &&
+        if (g.K == K && g.kind == kind && std::memcmp(&g.pl, &pl, sizeof(pl)) == 0 &&
             std::memcmp(&g.d, &d, sizeof(d)) == 0) {
             hit = &g;
             break;
@@ -1075,9 +1117,14 @@ void Spx::run_graph(const SpxDev &d, const DualPlan &pl, int K)
     if (!hit) {
         hipGraph_t graph = nullptr;
         HIPCHK(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
-        dual_batch_begin(s, d, pl);
-        for (int t = 0; t < K; t++) dual_iteration2(s, d, pl);
-        dual_batch_end(s, d, pl);
+        if (kind == 0) {
+            dual_batch_begin(s, d, pl);
+            for (int t = 0; t < K; t++) dual_iteration2(s, d, pl);
+            dual_batch_end(s, d, pl);
+        } else {
+            primal_batch_begin(s, d);
+            for (int t = 0; t < K; t++) primal_iteration2(s, d, pl);
+        }
         HIPCHK(hipStreamEndCapture(s, &graph));
         hipGraphExec_t exec = nullptr;
         HIPCHK(hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0));
@@ -1089,7 +1136,7 @@ void Spx::run_graph(const SpxDev &d, const DualPlan &pl, int K)
             En.graphs.erase(lru);
         }
         GraphEntry g;
-        g.d = d; g.pl = pl; g.K = K; g.exec = exec;
+        g.d = d; g.pl = pl; g.K = K; g.kind = kind; g.exec = exec;
         En.graphs.push_back(g);
         hit = &En.graphs.back();
         f->stats.graphs_built++;

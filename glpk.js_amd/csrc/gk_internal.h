@@ -164,6 +164,11 @@ DualPlan dual_plan(const SpxDev &d, int nr_max, int nwl_max, int pse, int rigoro
 void dual_iteration2(hipStream_t s, const SpxDev &d, const DualPlan &pl, hipEvent_t ev0 = nullptr,
                      hipEvent_t ev1 = nullptr);
 void transpose_dense(hipStream_t s, const double *A, int m, int n, int lda, double *AT, int ldt);
+// primal pivot pipeline (gk_primal.hip); the plan reuses DualPlan's fields
+DualPlan primal_plan(const SpxDev &d, int nr_max, int pse);
+bool primal_fast_ok(const SpxDev &d);
+void primal_batch_begin(hipStream_t s, const SpxDev &d);
+void primal_iteration2(hipStream_t s, const SpxDev &d, const DualPlan &pl);
 // timing hook: the row-path pivot-row kernel alone (returns algorithmic bytes)
 double launch_trow_rows(hipStream_t s, const SpxDev &d, const DualPlan &pl, int ns);
 // y = inv(B) x and y = inv(B)' x over the nr dense columns of rlist and the
@@ -188,11 +193,12 @@ void gather_basis_blocks_csc(hipStream_t s, int m, int k, const int *bptr, const
 int gauss_jordan(hipStream_t s, double *X, double *Y, int k, int *piv_step, int *piv, int *flag, double tiny,
                  double **result);
 void extract_inverse_rowmajor(hipStream_t s, const double *X, int k, const int *piv, double *CinvR);
-// blocked Gauss-Jordan (gk_reinvert.hip): C column-major in X, inverted in place
+// blocked Gauss-Jordan (gk_reinvert.hip): C column-major in X (2 k^2 doubles),
+// returns the buffer holding the inverted M = C' (see gk_reinvert.hip)
 int gj_blocked_max();
 size_t gj_blocked_scratch(int k);
-void gauss_jordan_blocked(hipStream_t s, double *X, double *scratch, int k, int *piv_step, int *piv, int *flag,
-                          double tiny);
+double *gauss_jordan_blocked(hipStream_t s, double *X, double *scratch, int k, int *piv_step, int *piv, int *flag,
+                             double tiny);
 void extract_inverse_blocked(hipStream_t s, const double *M, int k, const int *piv, const int *piv_step,
                              double *CinvR);
 // G (ms x k, col-major) = BS (ms x k col-major) * CinvR (k x k row-major)

@@ -15,8 +15,10 @@
 // Q = the transformed panel and R = its pivot rows.  The b steps act on any
 // other column x as  x <- x + (Q - E_R) x_R  (every step reads x only at its
 // pivot row), so the rest of M takes one rank-b update — an MFMA GEMM
-// (v_mfma_f64_16x16x4_f64) — after the pivot rows X_R are copied aside.
-// 2 launches per panel instead of one launch per column.
+// (v_mfma_f64_16x16x4_f64).  M is double-buffered: the panel kernel and the
+// update read M and write M2 (panel columns / the others), so the update
+// reads X_R = M[R, :] in place with no race.  2 launches per panel instead
+// of one launch per column.
 #include "gk_device.h"
 
 namespace gk {
@@ -24,8 +26,8 @@ namespace gk {
 constexpr int GJ_NONE = 0x7fffffff;
 
 template <int NT, int RPT, int B>
-__global__ void __launch_bounds__(NT) k_gjb_panel(double *__restrict__ M, double *__restrict__ Qm,
-                                                  double *__restrict__ XR, int k, int t0, int *__restrict__ piv_step,
+__global__ void __launch_bounds__(NT) k_gjb_panel(const double *__restrict__ M, double *__restrict__ M2,
+                                                  double *__restrict__ Qm, int k, int t0, int *__restrict__ piv_step,
                                                   int *__restrict__ piv, int *__restrict__ flag, double tiny)
 {
     __shared__ Cand shc[NT / 64];
@@ -71,7 +73,7 @@ __global__ void __launch_bounds__(NT) k_gjb_panel(double *__restrict__ M, double
             continue;
         }
         const int rs = best.idx - 1;
-        // the elementary step, in k_gj_step's arithmetic: fr = x[rs] / pv,
+        // the elementary step: fr = x[rs] / pv (as x[rs] * (1 / pv)),
         // y = x - colt * fr; the new slot i is the right-half column e_rs
         // (fr = 1 / pv).  The owner of row rs publishes fr.
         if (tid == rs % NT) {
@@ -79,16 +81,13 @@ __global__ void __launch_bounds__(NT) k_gjb_panel(double *__restrict__ M, double
 #pragma unroll
             for (int j = 0; j < RPT; ++j)
                 if (j == jo) {
-                    const double pv = x[j][i];
+                    const double ipv = 1.0 / x[j][i];
 #pragma unroll
-                    for (int cc = 0; cc < B; ++cc) frs[cc] = (cc == i) ? 1.0 / pv : x[j][cc] / pv;
+                    for (int cc = 0; cc < B; ++cc) frs[cc] = (cc == i) ? ipv : x[j][cc] * ipv;
                 }
         }
-        if (tid == 0) {
-            rsl[i] = rs;
-            piv[t0 + i] = rs;
-            piv_step[rs] = t0 + i;
-        }
+        if (tid == 0) rsl[i] = rs;     // global writes after the loop: a barrier
+                                       // would otherwise wait for the stores
         __syncthreads();
 #pragma unroll
         for (int j = 0; j < RPT; ++j) {
@@ -105,12 +104,16 @@ __global__ void __launch_bounds__(NT) k_gjb_panel(double *__restrict__ M, double
         }
     }
     if (dead) return;
-    // the panel back in place, Q - E_R for the update
+    if (tid < b) {
+        piv[t0 + tid] = rsl[tid];
+        piv_step[rsl[tid]] = t0 + tid;
+    }
+    // the panel into M2, Q - E_R for the update
 #pragma unroll
     for (int j = 0; j < RPT; ++j) {
         const int r = tid + j * NT;
         if (r >= k) continue;
-        double *row = M + (size_t)r * k + t0;
+        double *row = M2 + (size_t)r * k + t0;
         double *q = Qm + (size_t)r * B;
 #pragma unroll
         for (int c = 0; c < B; ++c) {
@@ -118,24 +121,19 @@ __global__ void __launch_bounds__(NT) k_gjb_panel(double *__restrict__ M, double
             q[c] = (c < b) ? x[j][c] - (r == rsl[c] ? 1.0 : 0.0) : 0.0;
         }
     }
-    // X_R = the pivot rows of the other columns, as they were before the panel
-    // (rows of M, contiguous); zero rows pad the last panel
-    for (int e = tid; e < B * k; e += NT) {
-        const int kk = e / k, c = e - kk * k;
-        XR[e] = (kk < b && (c < t0 || c >= t0 + b)) ? M[(size_t)rsl[kk] * k + c] : 0.0;
-    }
 }
 
-// M[r, c] += sum_kk Q[r, kk] XR[kk, c] for the columns outside the panel.
+// M2[r, c] = M[r, c] + sum_kk Q[r, kk] M[R[kk], c] for the columns outside
+// the panel (R = piv[t0 ..]).
 // One block = 64 x 64 outputs, four waves of 32 x 32 (2 x 2 MFMA tiles).
 // Fragments of v_mfma_f64_16x16x4_f64 per lane l: A[i = l & 15][kk = l >> 4],
 // B[kk = l >> 4][j = l & 15], D[(l >> 4) + 4 r][l & 15].
 typedef double gj_double4 __attribute__((ext_vector_type(4)));
 
 template <int B>
-__global__ void __launch_bounds__(256) k_gjb_update(double *__restrict__ M, const double *__restrict__ Qm,
-                                                    const double *__restrict__ XR, int k, int t0,
-                                                    const int *__restrict__ flag)
+__global__ void __launch_bounds__(256) k_gjb_update(const double *__restrict__ M, double *__restrict__ M2,
+                                                    const double *__restrict__ Qm, const int *__restrict__ rsl,
+                                                    int k, int t0, const int *__restrict__ flag)
 {
     if (*flag) return;
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -162,10 +160,11 @@ __global__ void __launch_bounds__(256) k_gjb_update(double *__restrict__ M, cons
             const int gr = row0 + a * 16 + li;
             av[a] = gr < k ? Qm[(size_t)gr * B + gk] : 0.0;
         }
+        const int rk = gk < b ? rsl[gk] : -1;
 #pragma unroll
         for (int bb = 0; bb < 2; ++bb) {
             const int gc = col0 + bb * 16 + li;
-            bv[bb] = gc < k ? XR[(size_t)gk * k + gc] : 0.0;
+            bv[bb] = (gc < k && rk >= 0) ? M[(size_t)rk * k + gc] : 0.0;
         }
 #pragma unroll
         for (int a = 0; a < 2; ++a)
@@ -173,7 +172,6 @@ __global__ void __launch_bounds__(256) k_gjb_update(double *__restrict__ M, cons
             for (int bb = 0; bb < 2; ++bb)
                 acc[a][bb] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[a], bv[bb], acc[a][bb], 0, 0, 0);
     }
-    (void)b;
 #pragma unroll
     for (int a = 0; a < 2; ++a)
 #pragma unroll
@@ -181,21 +179,23 @@ __global__ void __launch_bounds__(256) k_gjb_update(double *__restrict__ M, cons
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
                 const int gr = row0 + a * 16 + lk + 4 * r, gc = col0 + bb * 16 + li;
-                if (gr < k && gc < k && (gc < t0 || gc >= t0 + b)) M[(size_t)gr * k + gc] = acc[a][bb][r];
+                if (gr < k && gc < k && (gc < t0 || gc >= t0 + b)) M2[(size_t)gr * k + gc] = acc[a][bb][r];
             }
 }
 
 template <int NT, int RPT, int B>
-static void gjb_run(hipStream_t s, double *M, double *Qm, double *XR, int k, int *piv_step, int *piv, int *flag,
-                    double tiny)
+static double *gjb_run(hipStream_t s, double *M, double *M2, double *Qm, int k, int *piv_step, int *piv, int *flag,
+                       double tiny)
 {
     const dim3 g((k + 63) / 64, (k + 63) / 64);
     for (int t0 = 0; t0 < k; t0 += B) {
-        hipLaunchKernelGGL((k_gjb_panel<NT, RPT, B>), dim3(1), dim3(NT), 0, s, M, Qm, XR, k, t0, piv_step, piv, flag,
+        hipLaunchKernelGGL((k_gjb_panel<NT, RPT, B>), dim3(1), dim3(NT), 0, s, M, M2, Qm, k, t0, piv_step, piv, flag,
                            tiny);
         if (k > B)
-            hipLaunchKernelGGL((k_gjb_update<B>), g, dim3(256), 0, s, M, Qm, XR, k, t0, flag);
+            hipLaunchKernelGGL((k_gjb_update<B>), g, dim3(256), 0, s, M, M2, Qm, piv + t0, k, t0, flag);
+        std::swap(M, M2);
     }
+    return M;
 }
 
 __global__ void k_gjb_init(int *piv_step, int k, int *flag)
@@ -208,26 +208,26 @@ int gj_blocked_max() { return 8192; }
 
 size_t gj_blocked_scratch(int k)
 {
-    // Q (k x 32) and X_R (32 x k)
-    return (size_t)64 * k;
+    return (size_t)32 * k;                 // Q (k x B, B <= 32)
 }
 
-// inverse of C (k x k, column-major in X) by the blocked scheme above; X is
-// overwritten, scratch needs gj_blocked_scratch(k) doubles; BFD_ESING is
-// reported through *flag (1 + step)
-void gauss_jordan_blocked(hipStream_t s, double *X, double *scratch, int k, int *piv_step, int *piv, int *flag,
-                          double tiny)
+// inverse of C (k x k, column-major in X[0, k^2)) by the blocked scheme
+// above; X must hold 2 k^2 doubles (the second buffer of M), scratch
+// gj_blocked_scratch(k); returns the buffer holding the result.  BFD_ESING
+// is reported through *flag (1 + step).
+double *gauss_jordan_blocked(hipStream_t s, double *X, double *scratch, int k, int *piv_step, int *piv, int *flag,
+                             double tiny)
 {
-    if (k <= 0) return;
+    if (k <= 0) return X;
     hipLaunchKernelGGL(k_gjb_init, dim3(std::min((k + 255) / 256, 64)), dim3(256), 0, s, piv_step, k, flag);
-    double *Qm = scratch, *XR = scratch + (size_t)32 * k;
+    double *M2 = X + (size_t)k * k, *Qm = scratch;
     // registers: RPT * B doubles of the panel per thread (1 / 2 / 4 waves per SIMD)
-    if (k <= 256) gjb_run<256, 1, 16>(s, X, Qm, XR, k, piv_step, piv, flag, tiny);
-    else if (k <= 512) gjb_run<256, 2, 16>(s, X, Qm, XR, k, piv_step, piv, flag, tiny);
-    else if (k <= 1024) gjb_run<512, 2, 16>(s, X, Qm, XR, k, piv_step, piv, flag, tiny);
-    else if (k <= 2048) gjb_run<1024, 2, 16>(s, X, Qm, XR, k, piv_step, piv, flag, tiny);
-    else if (k <= 4096) gjb_run<1024, 4, 8>(s, X, Qm, XR, k, piv_step, piv, flag, tiny);
-    else gjb_run<1024, 8, 4>(s, X, Qm, XR, k, piv_step, piv, flag, tiny);
+    if (k <= 256) return gjb_run<256, 1, 16>(s, X, M2, Qm, k, piv_step, piv, flag, tiny);
+    if (k <= 512) return gjb_run<256, 2, 16>(s, X, M2, Qm, k, piv_step, piv, flag, tiny);
+    if (k <= 1024) return gjb_run<512, 2, 16>(s, X, M2, Qm, k, piv_step, piv, flag, tiny);
+    if (k <= 2048) return gjb_run<1024, 2, 16>(s, X, M2, Qm, k, piv_step, piv, flag, tiny);
+    if (k <= 4096) return gjb_run<1024, 4, 8>(s, X, M2, Qm, k, piv_step, piv, flag, tiny);
+    return gjb_run<1024, 8, 4>(s, X, M2, Qm, k, piv_step, piv, flag, tiny);
 }
 
 // CinvR (row-major inv(C)): with M = C' inverted in place,
