@@ -57,6 +57,8 @@ struct NodeIO {
     double *obj, *x, *dz;         // obj[nb], x[nb][m+n], dz[nb][2]
     signed char *stat_out;        // [nb][m+n]
     int it_lim;
+    double *scratch;              // GLOBAL kernel: per-node work area (node_lp_lds(m, n) bytes each)
+    size_t scratch_stride;        // in doubles
 };
 
 // ---- small block helpers (blockDim.x = 256) --------------------------------
@@ -141,11 +143,14 @@ __device__ __forceinline__ double nb_value(int st, double lb, double ub)
 // ---------------------------------------------------------------------------
 // one workgroup = one node LP
 // LDS: M[m][2m+n] during the inversion, then T[m][m+n]; lb, ub, x, d [m+n];
-// head[m], stat[m+n]
+// head[m], stat[m+n].  GLOBAL = 1: the same work area in a per-node slice of
+// HBM (node LPs beyond 64 KiB of LDS; L2 serves the workgroup's sweeps).
 // ---------------------------------------------------------------------------
+template <int GLOBAL>
 __global__ void __launch_bounds__(256) k_node_lp(NodeProb P, NodeIO io)
 {
-    extern __shared__ double lds[];
+    extern __shared__ double lds_[];
+    double *lds = GLOBAL ? io.scratch + (size_t)blockIdx.x * io.scratch_stride : lds_;
     __shared__ double shk[4], sha[4];
     __shared__ int shi[4];
     __shared__ int sh_flag;
@@ -484,10 +489,13 @@ size_t node_lp_lds(int m, int n)
     return sizeof(double) * ((size_t)m * (2 * m + n) + 4 * N + m) + sizeof(int) * m + N + 16;
 }
 
+constexpr size_t NODE_LDS_MAX = 64 * 1024;
+
 void launch_node_lp(hipStream_t s, const NodeProb &P, const NodeIO &io, int nb)
 {
     const size_t lds = node_lp_lds(P.m, P.n);
-    hipLaunchKernelGGL(k_node_lp, dim3(nb), dim3(256), lds, s, P, io);
+    if (lds <= NODE_LDS_MAX) hipLaunchKernelGGL(k_node_lp<0>, dim3(nb), dim3(256), lds, s, P, io);
+    else hipLaunchKernelGGL(k_node_lp<1>, dim3(nb), dim3(256), 0, s, P, io);
 }
 
 // ---------------------------------------------------------------------------
@@ -554,7 +562,7 @@ struct MipSolver {
     double sign = 1.0, c0 = 0.0;
     std::vector<double> A, c, rlb, rub, clb, cub, coef;
     std::vector<signed char> isint, fixed_col;
-    DevArr<double> dA, dc, dlb, dub, dcut, dobj, dx, ddz;
+    DevArr<double> dA, dc, dlb, dub, dcut, dobj, dx, ddz, dscratch;
     DevArr<signed char> dint, dsin, dsout;
     DevArr<int> dstatus, dpiv, djj, dnext;
     HostArr<double> hlb, hub, hcut, hobj, hx, hdz;
@@ -647,10 +655,12 @@ extern "C" int gk_ios_driver_sharded(gk_ctx *ctx, gk_mip *mip, const gk_iocp *pa
         set_err("gk_ios_driver: optimal basis to initial LP relaxation not provided");
         return GK_EABI;
     }
+    // node LPs up to 64 KiB keep their tableau in LDS; larger ones work in a
+    // per-node slice of HBM, batches sized to at most 8 GiB of work area
     const size_t lds = node_lp_lds(m, n);
-    if (lds > 64 * 1024) {
-        set_err("gk_ios_driver: node LP %d x %d needs %zu bytes of LDS; the batched node kernel holds at most 64 KiB",
-                m, n, lds);
+    const size_t SCRATCH_MAX = (size_t)8 << 30;
+    if (lds > SCRATCH_MAX) {
+        set_err("gk_ios_driver: node LP %d x %d needs %zu bytes of work area; at most %zu", m, n, lds, SCRATCH_MAX);
         return GK_EABI;
     }
     if (hipSetDevice(gk_ctx_device(ctx)) != hipSuccess) { set_err("gk_ios_driver: hipSetDevice failed"); return GK_EABI; }
@@ -689,8 +699,13 @@ extern "C" int gk_ios_driver_sharded(gk_ctx *ctx, gk_mip *mip, const gk_iocp *pa
     setup_rounding(S, mip);
     // device problem
     S.dA.ensure(S.A.size()); S.dc.ensure(S.N); S.dint.ensure(n);
-    const int BMAX = 1024;
+    const int BMAX = (lds <= NODE_LDS_MAX) ? 1024 : (int)std::max<size_t>(1, std::min<size_t>(1024, SCRATCH_MAX / lds));
     S.alloc_batch(BMAX);
+    const size_t stride = (lds + 255) / 256 * 32;          // doubles, 256-byte aligned slices
+    if (lds > NODE_LDS_MAX) {
+        S.dscratch.ensure(stride * BMAX);
+        if (!S.dscratch.p) { set_err("gk_ios_driver: out of memory (node work area)"); return GK_EABI; }
+    }
     if (!S.dA.p || !S.dc.p || !S.dint.p || !S.dlb.p || !S.hlb.p) { set_err("gk_ios_driver: out of memory"); return GK_EABI; }
     (void)hipMemcpyAsync(S.dA.p, S.A.data(), S.A.size() * sizeof(double), hipMemcpyHostToDevice, s);
     (void)hipMemcpyAsync(S.dc.p, S.c.data(), S.N * sizeof(double), hipMemcpyHostToDevice, s);
@@ -807,6 +822,8 @@ extern "C" int gk_ios_driver_sharded(gk_ctx *ctx, gk_mip *mip, const gk_iocp *pa
         io.status = S.dstatus.p; io.pivots = S.dpiv.p; io.jj = S.djj.p; io.next = S.dnext.p;
         io.obj = S.dobj.p; io.x = S.dx.p; io.dz = S.ddz.p; io.stat_out = S.dsout.p;
         io.it_lim = 10000;
+        io.scratch = S.dscratch.p;
+        io.scratch_stride = stride;
         launch_node_lp(s, P, io, nb);
         (void)hipMemcpyAsync(S.hstatus.p, S.dstatus.p, nb * sizeof(int), hipMemcpyDeviceToHost, s);
         (void)hipMemcpyAsync(S.hpiv.p, S.dpiv.p, nb * sizeof(int), hipMemcpyDeviceToHost, s);

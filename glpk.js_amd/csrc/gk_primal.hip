@@ -670,16 +670,17 @@ __global__ void __launch_bounds__(1024) k_primal_row(SpxDev d, int pse, int nr_c
     // s = -A[:, idx]' u over all rows (the second pass of update_gamma)
     double sa = 0.0;
     if (pse) {
+        // 8 rows in flight per wave: the pass is bound by the loads in flight
         int t = w;
-        for (; t + 3 * nw < m; t += 4 * nw) {
-            double uu[4], aa[4];
+        for (; t + 7 * nw < m; t += 8 * nw) {
+            double uu[8], aa[8];
 #pragma unroll
-            for (int u = 0; u < 4; ++u) {
+            for (int u = 0; u < 8; ++u) {
                 uu[u] = d.u[t + u * nw];
                 aa[u] = col[(size_t)(t + u * nw) * ldt];
             }
 #pragma unroll
-            for (int u = 0; u < 4; ++u) sa += uu[u] * aa[u];
+            for (int u = 0; u < 8; ++u) sa += uu[u] * aa[u];
         }
         for (; t < m; t += nw) sa += d.u[t] * col[(size_t)t * ldt];
     }

@@ -25,7 +25,10 @@ assert.strictEqual(core.nativeIos({mip: {m: 2, n: 3}, parm: {cb_func: function (
 assert.strictEqual(core.nativeIos({mip: {m: 2, n: 3}, parm: {cb_func: null, mip_gap: 0.01}}), false);
 assert.strictEqual(core.nativeIos({mip: {m: 2, n: 3}, parm: {cb_func: null, mip_gap: 0, gmi_cuts: 1}}), false);
 assert.strictEqual(core.nativeIos({mip: {m: 2, n: 3}, parm: {cb_func: null, mip_gap: 0}}), true);
-assert.strictEqual(core.nativeIos({mip: {m: 80, n: 200}, parm: {cb_func: null, mip_gap: 0}}), false);
+// node LPs beyond 64 KiB of LDS run natively too (HBM work area); only a
+// work area beyond 8 GiB per node stays with the reference's driver
+assert.strictEqual(core.nativeIos({mip: {m: 80, n: 200}, parm: {cb_func: null, mip_gap: 0}}), true);
+assert.strictEqual(core.nativeIos({mip: {m: 30000, n: 40000}, parm: {cb_func: null, mip_gap: 0}}), false);
 glpk.glp_set_print_func(function () {});
 var lp = glpk.glp_create_prob();
 glpk.glp_set_obj_dir(lp, glpk.GLP_MAX);

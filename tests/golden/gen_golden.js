@@ -12,7 +12,7 @@
 //   * counters around ios_solve_node (glpios01.js:866) and bfd_factorize
 //     (glpbfd.js:47), rebinding the closure names (SURVEY.md §0).
 //
-// usage: node tests/golden/gen_golden.js [--big]
+// usage: node tests/golden/gen_golden.js [--big] [--only PREFIX]
 'use strict';
 var fs = require('fs');
 var path = require('path');
@@ -20,6 +20,7 @@ var path = require('path');
 var REF = process.env.GLPK_REF || '/root/reference';
 var OUT = __dirname;
 var BIG = process.argv.indexOf('--big') >= 0;
+var ONLY = process.argv.indexOf('--only') >= 0 ? process.argv[process.argv.indexOf('--only') + 1] : null;
 
 function buildBundle() {
     var lib = path.join(REF, 'lib');
@@ -128,19 +129,20 @@ function genC5s(m, n, seed) {
 // phase-I/phase-II logic, free and fixed variables, infeasible/unbounded ends.
 // feasible=true builds the bounds around a random point x0 (so the LP has a
 // feasible solution; integer columns get integer x0 and integer bounds).
-function genMix(seed, m, n, dens, withInt, feasible) {
+function genMix(seed, m, n, dens, withInt, feasible, colsBounded) {
     var r = new SplitMix(seed), P = newProb(), i, j;
     glpk.glp_set_obj_dir(P, r.u() < 0.5 ? glpk.GLP_MIN : glpk.GLP_MAX);
     glpk.glp_add_rows(P, m); glpk.glp_add_cols(P, n);
     var isint = [], x0 = [];
     for (j = 1; j <= n; j++) {
-        isint[j] = withInt && r.u() < 0.7;
+        isint[j] = withInt && r.u() < (typeof withInt === 'number' ? withInt : 0.7);
         x0[j] = isint[j] ? Math.floor(r.u() * 7) - 3 : Math.round((r.u() * 10 - 5) * 4) / 4;
     }
-    function bnds(setter, idx, c, integral) {
+    function bnds(setter, idx, c, integral, boxed) {
         var t = r.u(), a = Math.round((r.u() * 20 - 10) * 4) / 4, w = 1 + Math.round(r.u() * 40) / 4,
             w2 = 1 + Math.round(r.u() * 40) / 4;
         if (integral) { w = Math.ceil(w); w2 = Math.ceil(w2); }
+        if (boxed) { setter(P, idx, glpk.GLP_DB, c - w, c + w2); return; }
         if (feasible) {
             if (t < 0.08) setter(P, idx, glpk.GLP_FR, 0, 0);
             else if (t < 0.38) setter(P, idx, glpk.GLP_LO, c - w, 0);
@@ -169,7 +171,7 @@ function genMix(seed, m, n, dens, withInt, feasible) {
             }
     }
     for (i = 1; i <= m; i++) bnds(glpk.glp_set_row_bnds, i, rowv[i], false);
-    for (j = 1; j <= n; j++) bnds(glpk.glp_set_col_bnds, j, x0[j], isint[j]);
+    for (j = 1; j <= n; j++) bnds(glpk.glp_set_col_bnds, j, x0[j], isint[j], !!colsBounded);
     glpk.glp_load_matrix(P, ia.length - 1, ia, ja, ar);
     if (withInt) {
         for (j = 1; j <= n; j++) if (isint[j]) glpk.glp_set_col_kind(P, j, glpk.GLP_IV);
@@ -242,6 +244,7 @@ function writeJson(name, obj) {
 
 // LP instance: run primal and dual each on a fresh copy, from the initial basis.
 function lpCase(name, mk, gen, methods, traceCap, extraRuns) {
+    if (ONLY && name.indexOf(ONLY) !== 0) return;
     var P0 = mk();
     var d = dumpProb(P0, gen);
     d.name = name; d.kind = 'lp'; d.runs = [];
@@ -259,6 +262,7 @@ function lpCase(name, mk, gen, methods, traceCap, extraRuns) {
 // MIP instance: root primal glp_simplex then glp_intopt (default IOCP), the
 // flow of SURVEY.md §8(d) C4/C5.
 function mipCase(name, mk, gen) {
+    if (ONLY && name.indexOf(ONLY) !== 0) return;
     var P = mk();
     var d = dumpProb(P, gen);
     d.name = name; d.kind = 'mip';
@@ -306,6 +310,10 @@ for (var ms = 1; ms <= 12; ms++) {
         mipCase('mixint' + ms, function () { return genMix(100 + ms, 6 + ms, 8 + 2 * ms, 0.5, true, true); }, null);
     })(ms);
 }
+// node LPs beyond the node kernel's 64 KiB of LDS (gk_mip.hip, HBM work area)
+[[50, 80, 0.15], [60, 90, 0.15], [70, 100, 0.1], [48, 90, 0.35]].forEach(function (s, k) {
+    mipCase('mixbig' + (k + 1), function () { return genMix(300 + k, s[0], s[1], 0.15, s[2], true, true); }, null);
+});
 if (BIG) {
     lpCase('c2s', function () { return genC2s(821, 1571, 7, 42); }, {kind: 'c2s', m: 821, n: 1571, nzc: 7, seed: 42}, [3, 1], 0);
     lpCase('dense_512x2048', function () { return genDense(512, 2048, 42); }, {kind: 'dense', m: 512, n: 2048, seed: 42}, [1, 3], 0);
