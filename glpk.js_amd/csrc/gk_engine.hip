@@ -324,7 +324,8 @@ static void engine_alloc(Engine &E, int m, int n)
     // candidates (24-byte entries): chuzr | pass 1 | pass 2, 4 gv each, then
     // the primal pass-1 candidates of the row groups, 16 gv
     E.cand.ensure(3 * 28 * (size_t)gv);
-    E.wlist.ensure(n); E.wpos.ensure(n);
+    // dual: reference-space non-basic structurals (n); primal: basic slacks in the reference space (m)
+    E.wlist.ensure(std::max(m, n)); E.wpos.ensure(std::max(m, n));
     E.awpart.ensure((size_t)AW_SPLITS * m);
     {
         const size_t tiles = (size_t)(m + 511) / 512 + 1;
@@ -983,8 +984,8 @@ void Spx::init()
             }
         if (!rl.empty()) HIPCHK(hipMemcpyAsync(E->rlist.p, rl.data(), rl.size() * sizeof(int), hipMemcpyHostToDevice, s));
         HIPCHK(hipMemcpyAsync(E->rpos.p, rp.data(), (size_t)m * sizeof(int), hipMemcpyHostToDevice, s));
-        std::vector<int> wp(n, -1);   // reference space empty until the first reset (refct = 0)
-        HIPCHK(hipMemcpyAsync(E->wpos.p, wp.data(), (size_t)n * sizeof(int), hipMemcpyHostToDevice, s));
+        std::vector<int> wp(std::max(m, n), -1);   // reference space empty until the first reset (refct = 0)
+        HIPCHK(hipMemcpyAsync(E->wpos.p, wp.data(), wp.size() * sizeof(int), hipMemcpyHostToDevice, s));
         hs = DState{};
         hs.nr = (int)rl.size();
         hs.nwl = 0;
@@ -1099,6 +1100,20 @@ void Spx::rebuild_lists()
     if (!rl.empty()) HIPCHK(hipMemcpyAsync(E->rlist.p, rl.data(), rl.size() * sizeof(int), hipMemcpyHostToDevice, s));
     HIPCHK(hipMemcpyAsync(E->rpos.p, rp.data(), (size_t)m * sizeof(int), hipMemcpyHostToDevice, s));
     hs.nr = (int)rl.size();
+    // the basic slacks in the PSE reference space (the support of u = inv(B)' v
+    // beyond the dense columns, gk_primal.hip)
+    std::vector<signed char> ref((size_t)m + n);
+    HIPCHK(hipMemcpyAsync(ref.data(), E->refsp.p, (size_t)m + n, hipMemcpyDeviceToHost, s));
+    sync();
+    std::vector<int> sl, sp(std::max(m, n), -1);
+    for (int c = 1; c <= m; c++)
+        if (bind[c] <= m && ref[c - 1]) {
+            sp[c - 1] = (int)sl.size();
+            sl.push_back(c - 1);
+        }
+    if (!sl.empty()) HIPCHK(hipMemcpyAsync(E->wlist.p, sl.data(), sl.size() * sizeof(int), hipMemcpyHostToDevice, s));
+    HIPCHK(hipMemcpyAsync(E->wpos.p, sp.data(), sp.size() * sizeof(int), hipMemcpyHostToDevice, s));
+    hs.nwl = (int)sl.size();
     push_state();
     sync();
     lists_stale = false;

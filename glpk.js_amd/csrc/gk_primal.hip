@@ -228,7 +228,11 @@ __global__ void __launch_bounds__(1024) k_primal_ftran(SpxDev d, int pse, int nr
             return;
         }
         if (reset) {
-            reset_refsp_dev(d, 0);            // refsp := non-basic variables, gamma := 1
+            // the basic slacks in the reference space: none after the reset
+            const int nsl = st->nwl;
+            for (int l = threadIdx.x; l < nsl; l += blockDim.x) d.wpos[d.wlist[l]] = -1;
+            reset_refsp_dev(d, 0);            // refsp := non-basic variables, gamma := 1 (syncs)
+            if (threadIdx.x == 0) st->nwl = 0;
         }
     }
     if (why != ST_RUN) return;
@@ -667,22 +671,36 @@ __global__ void __launch_bounds__(1024) k_primal_row(SpxDev d, int pse, int nr_c
             }
         }
     }
-    // s = -A[:, idx]' u over all rows (the second pass of update_gamma)
+    // s = -A[:, idx]' u (the second pass of update_gamma): u = inv(B)' v with
+    // v = tcol on the basic variables of the reference space is zero outside
+    // the dense columns of inv(B) and the basic slacks of the reference space
+    // (a basic slack c has u_c = v[bind[c]]), so the pass runs over the rows
+    // of AT in rlist and slist only
     double sa = 0.0;
     if (pse) {
-        // 8 rows in flight per wave: the pass is bound by the loads in flight
+        const int nsl = st->nwl;
+        const int nu = nr + nsl;
         int t = w;
-        for (; t + 7 * nw < m; t += 8 * nw) {
-            double uu[8], aa[8];
+        for (; t + 3 * nw < nu; t += 4 * nw) {
+            int c[4];
+            double uu[4], aa[4];
 #pragma unroll
-            for (int u = 0; u < 8; ++u) {
-                uu[u] = d.u[t + u * nw];
-                aa[u] = col[(size_t)(t + u * nw) * ldt];
+            for (int u = 0; u < 4; ++u) {
+                const int tt = t + u * nw;
+                c[u] = (tt < nr) ? d.rlist[tt] : d.wlist[tt - nr];
             }
 #pragma unroll
-            for (int u = 0; u < 8; ++u) sa += uu[u] * aa[u];
+            for (int u = 0; u < 4; ++u) {
+                uu[u] = d.u[c[u]];
+                aa[u] = col[(size_t)c[u] * ldt];
+            }
+#pragma unroll
+            for (int u = 0; u < 4; ++u) sa += uu[u] * aa[u];
         }
-        for (; t < m; t += nw) sa += d.u[t] * col[(size_t)t * ldt];
+        for (; t < nu; t += nw) {
+            const int c = (t < nr) ? d.rlist[t] : d.wlist[t - nr];
+            sa += d.u[c] * col[(size_t)c * ldt];
+        }
     }
     sp[0][w][lane] = (idx < n) ? acc : 0.0;
     sp[1][w][lane] = (idx < n) ? sa : 0.0;
@@ -844,11 +862,18 @@ __global__ void __launch_bounds__(256) k_primal_commit(SpxDev d, int pse, int nv
         const double lbn = in_m ? d.lb[knew - 1] : 0.0, ubn = in_m ? d.ub[knew - 1] : 0.0;
         const double cfn = in_m ? d.coef[knew - 1] : 0.0;
         const bool maint = (blockIdx.x == 0 && threadIdx.x == 64);
-        int rq = -1, rlast = 0, nr0 = 0;
+        int rq = -1, rlast = 0, nr0 = 0, sp = -1, slast = 0, nsl0 = 0;
+        bool refkq = false;
         if (maint) {
             nr0 = st->nr;
+            nsl0 = st->nwl;
             if (kq <= m) rq = d.rpos[kq - 1];
             rlast = d.rlist[max(nr0 - 1, 0)];
+            if (pse) {
+                if (kp <= m) sp = d.wpos[kp - 1];
+                slast = d.wlist[max(nsl0 - 1, 0)];
+                refkq = kq <= m && d.refsp[kq - 1] != 0;
+            }
         }
         if (stop) return;
         double pivot = 0.0, new_dq = 0.0, cq_new = 0.0;
@@ -951,12 +976,30 @@ __global__ void __launch_bounds__(256) k_primal_commit(SpxDev d, int pse, int nv
                 nr++;
             }
             st->nr = nr;
+            if (pse) {
+                // basic slacks in the reference space: a slack leaving drops
+                // out, a slack of the reference space entering joins
+                int nsl = nsl0;
+                if (sp >= 0) {
+                    d.wlist[sp] = slast;
+                    d.wpos[slast] = sp;
+                    d.wpos[kp - 1] = -1;
+                    nsl--;
+                }
+                if (refkq) {
+                    d.wlist[nsl] = kq - 1;
+                    d.wpos[kq - 1] = nsl;
+                    nsl++;
+                }
+                st->nwl = nsl;
+            }
             // algorithmic bytes: the pivot row (rows of AT in the support of
-            // rho, or the CSC), s = N' u (all of A with PSE), inv(B) for the
-            // FTRAN and the PSE BTRAN, the rank-1 update and the vectors
+            // rho, or the CSC), s = N' u (rows of AT in the support of u, or
+            // the CSC), inv(B) for the FTRAN and the PSE BTRAN, the rank-1
+            // update and the vectors
             const int ns = st->ns;
             const double rowb = rowmode == 1 ? 8.0 * (double)ns * n : 12.0 * (double)d.A.nnz;
-            const double sb = pse ? (rowmode == 1 ? 8.0 * (double)m * n : 12.0 * (double)d.A.nnz) : 0.0;
+            const double sb = pse ? (rowmode == 1 ? 8.0 * (double)(nr0 + nsl0) * n : 12.0 * (double)d.A.nnz) : 0.0;
             st->bytes += rowb + sb + 8.0 * (double)m * (nr0 + 1) * (pse ? 2.0 : 1.0) +
                          16.0 * (double)m * (nr0 + (kp <= m ? 1 : 0)) + bytes_fixed;
         }
