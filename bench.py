@@ -272,15 +272,32 @@ def run_extra(gk, problems, ctx, c3):
                                           "pivots_per_s": round(P.it_cnt / dt, 1),
                                           "reference_node_pivots_per_s": 9.4}
     del P
-    p = problems.gen_c2s()
-    P = gk.GkProblem(ctx, p)
+    # the primal (glp_simplex's default method) on the same instance, timed
+    # like the headline: it_lim=100 steps continuing from the previous basis
+    P = gk.GkProblem(ctx, c3)
+    parm = gk.SMCP(meth=gk.GLP_PRIMAL, it_lim=100, msg_lev=gk.GLP_MSG_ERR)
+    gk.glp_simplex(P, parm)
     t0 = time.perf_counter()
-    ret = gk.glp_simplex(P, gk.SMCP(meth=gk.GLP_DUAL, msg_lev=gk.GLP_MSG_ERR))
+    it0 = P.it_cnt
+    for _ in range(5):
+        ret = gk.glp_simplex(P, parm)
     dt = time.perf_counter() - t0
-    out["c2s_dual_full_solve"] = {"ret": ret, "obj": P.obj_val, "ref_obj": 357.82820943518834,
-                                  "pivots": P.it_cnt, "seconds": round(dt, 4),
-                                  "pivots_per_s": round(P.it_cnt / dt, 1),
-                                  "reference_node_pivots_per_s": 1813}
+    out["c3_primal_steps"] = {"ret": ret, "pivots": P.it_cnt - it0, "seconds": round(dt, 4),
+                              "pivots_per_s": round((P.it_cnt - it0) / dt, 1),
+                              "window": "pivots 100-600 from the slack basis, 5 steps of it_lim=100",
+                              "reference_node_pivots_per_s": 4.0}
+    del P
+    for meth, name, ref_rate in ((gk.GLP_DUAL, "dual", 1813), (gk.GLP_PRIMAL, "primal", 1833)):
+        p = problems.gen_c2s()
+        P = gk.GkProblem(ctx, p)
+        t0 = time.perf_counter()
+        ret = gk.glp_simplex(P, gk.SMCP(meth=meth, msg_lev=gk.GLP_MSG_ERR))
+        dt = time.perf_counter() - t0
+        out["c2s_" + name + "_full_solve"] = {"ret": ret, "obj": P.obj_val, "ref_obj": 357.82820943518834,
+                                              "pivots": P.it_cnt, "seconds": round(dt, 4),
+                                              "pivots_per_s": round(P.it_cnt / dt, 1),
+                                              "reference_node_pivots_per_s": ref_rate}
+        del P
     out.update(run_bnb(gk, problems, ctx))
     return out
 
