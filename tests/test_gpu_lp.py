@@ -132,3 +132,20 @@ def test_gpu_c3_full_size_iteration_limit(gpu_ctx):
     assert ret == gk.GLP_EBOUND + 4     # GLP_EITLIM = 8
     assert P.it_cnt == 300
     check_solution(P)
+
+
+def test_gpu_dense_2048x8192_full_dual_kkt(gpu_ctx):
+    """A full dual solve of the dense generator at 2048 x 8192 (tens of
+    thousands of pivots, re-inversions at k up to 2048); the returned basis
+    is certified optimal by KKT (tests/kkt.py: feasibility, reduced costs,
+    complementary slackness, zero duality gap within 1e-9)."""
+    from kkt import dense_kkt
+    prob = problems.gen_dense(2048, 8192, seed=42)
+    P = gk.GkProblem(gpu_ctx, prob)
+    ret = gk.glp_simplex(P, gk.SMCP(meth=gk.GLP_DUAL))
+    assert ret == 0 and P.pbs_stat == P.dbs_stat == problems.GLP_FEAS
+    dense_kkt(P, prob)
+    gold = os.path.join(os.path.dirname(__file__), "golden", "dense_full_2048x8192.json")
+    if os.path.exists(gold):                       # the oracle's full solve, when it has finished
+        ref = load_golden(gold)["obj_val"]
+        assert abs(P.obj_val - ref) <= 1e-9 * abs(ref), (P.obj_val, ref)
