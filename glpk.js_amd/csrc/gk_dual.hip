@@ -34,6 +34,7 @@
 //                        and the phase-I check of the next iteration
 #include "gk_device.h"
 #include <algorithm>
+#include <cstdlib>
 
 namespace gk {
 
@@ -517,6 +518,86 @@ __global__ void __launch_bounds__(TOP_WG) k_dual_top(SpxDev d, int rowpath, int 
         int ns = nr;
         if (kp <= m) {   // the basic slack at position p: unit column of inv(B)
             if (!rowpath) d.rho[kp - 1] = 1.0;
+            d.rho_idx[nr] = kp - 1;
+            d.rho_val[nr] = 1.0;
+            ns++;
+        }
+        st->p = p;
+        st->kp = kp;
+        st->delta = best.k2;
+        st->trow_max_bits = 0ull;
+        st->ns = ns;
+        st->dinf = 0;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// k_dual_top_grid (column-pass path, dense A, nr large): k_dual_top spread
+// over the grid.  Every block makes the chuzr choice itself; block 0 applies
+// the pending change of basis, the stop tests and the reference-space reset.
+// The dense rho is written by rows (rho_i = inv(B)[p, i] for a dense column
+// i, else 1 at the leaving slack, else 0: the unit columns are exact), the
+// compact rho by list position; 256 rows / list entries per thread block.
+// ---------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) k_dual_top_grid(SpxDev d)
+{
+    const TraceScope trace_(d, 0);
+    DState *st = d.st;
+    const int m = d.m, n = d.n;
+    const int lane = threadIdx.x & 63;
+    const bool lead = (blockIdx.x == 0);
+    const int stop = st->stop;
+    const FinishIn fin = finish_load(d);
+    const int pricing = st->pricing, phase = st->phase, dinf = st->dinf, nr = st->nr;
+    const double zeta = st->zeta, obj_ll = st->obj_ll, obj_ul = st->obj_ul;
+    const int gm = 4 * ((m + 255) / 256);
+    Cand cc = no_cand(0.0);
+    for (int b = lane; b < gm; b += 64) {
+        const Cand e = cand_chuzr(d)[b];
+        if (better<0>(e, cc)) cc = e;
+    }
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    const int rp = (i < m) ? d.rpos[i] : -1;
+    const int cl = (i < nr) ? d.rlist[i] : 0;
+    if (stop) return;
+    const TopState ts = fin.t;
+    int why = ST_RUN;
+    if (ts.iter_left <= 0 || ts.refact) why = ts.refact ? ST_REFACT : ST_BATCH;
+    else if (phase == 1 && !dinf) why = ST_PHASE;
+    else if (phase != 1 && ((zeta < 0.0 && obj_ll > -DBL_MAX && ts.obj <= obj_ll) ||
+                            (zeta > 0.0 && obj_ul < +DBL_MAX && ts.obj >= obj_ul)))
+        why = ST_OBJLIM;
+    const Cand best = wave_best<0>(cc);
+    if (why == ST_RUN && best.idx == 0) why = ST_P0;
+    if (lead) {
+        (void)finish_apply(d, fin, true);
+        if (why != ST_RUN) {
+            if (threadIdx.x == 0) {
+                if (why == ST_P0) st->p = 0;
+                st->stop = why;
+            }
+            return;
+        }
+        if (pricing == PT_PSE && ts.refct == 0) {
+            reset_refsp_dev(d, 1);            // refsp := basic variables, gamma := 1
+            for (int l = threadIdx.x; l < n; l += blockDim.x) d.wpos[l] = -1;
+            if (threadIdx.x == 0) st->nwl = 0;
+        }
+    }
+    if (why != ST_RUN) return;
+    const int p = best.idx, kp = best.aux;
+    const double *brow = d.Binv + (p - 1);
+    const size_t ldb = (size_t)d.ldb;
+    const double vr = (i < m && rp >= 0) ? brow[(size_t)i * ldb] : 0.0;
+    const double vl = (i < nr) ? brow[(size_t)cl * ldb] : 0.0;
+    if (i < m) d.rho[i] = (rp >= 0) ? vr : (i == kp - 1 ? 1.0 : 0.0);
+    if (i < nr) {
+        d.rho_idx[i] = cl;
+        d.rho_val[i] = vl;
+    }
+    if (lead && threadIdx.x == 0) {
+        int ns = nr;
+        if (kp <= m) {
             d.rho_idx[nr] = kp - 1;
             d.rho_val[nr] = 1.0;
             ns++;
@@ -1870,7 +1951,13 @@ DualPlan dual_plan(const SpxDev &d, int nr_max, int nwl_max, int pse, int rigoro
     const int ns_max = std::min(m, nr_max + 1);
     pl.nr_cap = nr_max;
     pl.ns_cap = ns_max;
-    pl.rowpath = (d.A.dense && d.A.AT && !rigorous && 2 * ns_max <= m) ? 1 : 0;
+    // the row path reads 8 ns n bytes of AT, the column pass all of A plus a
+    // dense rho; GK_ROWPATH_FRAC (experiments) moves the switch point ns / m
+    static const double row_frac = [] {
+        const char *e = std::getenv("GK_ROWPATH_FRAC");
+        return e ? std::atof(e) : 0.5;
+    }();
+    pl.rowpath = (d.A.dense && d.A.AT && !rigorous && ns_max <= row_frac * m) ? 1 : 0;
     pl.fused = (d.A.dense && !rigorous) ? 1 : 0;
     const int tiles_t = cdiv(n, 512), tiles_f = cdiv(m, 512);
     pl.tsplits = std::max(1, std::min(2048 / tiles_t, cdiv(ns_max, 8)));
@@ -1962,7 +2049,10 @@ void dual_iteration2(hipStream_t s, const SpxDev &d, const DualPlan &pl, hipEven
         hipLaunchKernelGGL(k_dual_row, dim3(ncb), dim3(64 * pl.twaves), 0, s, d, pl.pse, pl.nr_cap);
         if (ev1) (void)hipEventRecord(ev1, s);
     } else {
-        hipLaunchKernelGGL(k_dual_top, dim3(1), dim3(TOP_WG), 0, s, d, pl.rowpath, pl.nr_cap);
+        if (!pl.rigorous && d.A.dense && m >= 1024)
+            hipLaunchKernelGGL(k_dual_top_grid, dim3(cdiv(m, 256)), dim3(256), 0, s, d);
+        else
+            hipLaunchKernelGGL(k_dual_top, dim3(1), dim3(TOP_WG), 0, s, d, pl.rowpath, pl.nr_cap);
         if (pl.rigorous) refine_rho_dev(s, d);
         if (ev0) (void)hipEventRecord(ev0, s);
         colpass_gated(s, d.A, CP_TROW, m, n, d.head, d.stat, d.coef, nullptr, d.rho, nullptr, d.trow, nullptr,

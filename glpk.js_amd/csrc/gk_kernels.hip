@@ -253,6 +253,23 @@ __global__ void __launch_bounds__(256) k_colpass_dense(int mode, int m, int off,
             const double *col = A + (size_t)(k - m - 1) * lda;
             double a1 = 0.0, a2 = 0.0;
             int r = lane * 2;
+            // 4 segments of the column in flight per lane (the pass is bound
+            // by the bytes in flight); the same order of accumulation
+            for (; r + 3 * 128 + 1 < m; r += 4 * 128) {
+                double2 v[4], xv[4], yv[4];
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    v[u] = *(const double2 *)(col + r + 128 * u);
+                    xv[u] = *(const double2 *)(x + r + 128 * u);
+                    if (TWO) yv[u] = *(const double2 *)(y + r + 128 * u);
+                }
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    a1 += v[u].x * xv[u].x;
+                    a1 += v[u].y * xv[u].y;
+                    if (TWO) { a2 += v[u].x * yv[u].x; a2 += v[u].y * yv[u].y; }
+                }
+            }
             for (; r + 1 < m; r += 128) {
                 double2 v = *(const double2 *)(col + r);
                 a1 += v.x * x[r];
