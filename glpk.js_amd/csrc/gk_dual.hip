@@ -2178,6 +2178,69 @@ void binv_ftran_list(hipStream_t s, const SpxDev &d, int nr, const double *x, do
     hipLaunchKernelGGL(k_binv_list, dim3(cdiv(d.m, 64)), dim3(64 * nw), 0, s, d, nr, x, y);
 }
 
+// ---------------------------------------------------------------------------
+// eval_pi's residual and eval_cbar (glpspx02.js:426-495) by rows of AT, for
+// the dual with dense A: pi = inv(B)' cB vanishes outside the dense columns of
+// inv(B) (a basic slack c has pi_c = cB[bind[c]] = 0: row costs are 0), so
+// N_k' pi runs over the nr rows of AT in rlist instead of all m rows of A.
+// Block b owns the 64 variable slots [64 b, 64 b + 64) (structural column c
+// and slack row c); waves split the list rows, partial sums meet in LDS.
+//   CP_CBAR:  out[j] = coef[k] - N_k' pi for the non-basic position j of k
+//   CP_RESID: out[i] = h[i]   - N_k' pi for the basic position i of k
+// ---------------------------------------------------------------------------
+__global__ void __launch_bounds__(1024) k_rowpass_pi(SpxDev d, int mode, int nr, const double *__restrict__ pi,
+                                                     const double *__restrict__ h, double *__restrict__ out)
+{
+    __shared__ double sp[16][64];
+    const int m = d.m, n = d.n;
+    const int lane = threadIdx.x & 63;
+    const int w = threadIdx.x >> 6, nw = blockDim.x >> 6;
+    const int idx = blockIdx.x * 64 + lane;
+    const double *__restrict__ col = d.A.AT + min(idx, n - 1);
+    const size_t ldt = (size_t)d.A.ldt;
+    double acc = 0.0;
+    int t = w;
+    for (; t + 3 * nw < nr; t += 4 * nw) {
+        int c[4];
+        double v[4], a[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) c[u] = d.rlist[t + u * nw];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            v[u] = pi[c[u]];
+            a[u] = col[(size_t)c[u] * ldt];
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) acc += v[u] * a[u];
+    }
+    for (; t < nr; t += nw) {
+        const int c = d.rlist[t];
+        acc += pi[c] * col[(size_t)c * ldt];
+    }
+    sp[w][lane] = acc;
+    __syncthreads();
+    if (w != 0) return;
+    double dot = 0.0;
+    for (int k = 0; k < nw; ++k) dot += sp[k][lane];
+    if (idx < n) {
+        const int pos = d.bind[m + idx];
+        if (mode == CP_CBAR && pos > m) out[pos - m - 1] = d.coef[m + idx] + dot;
+        if (mode == CP_RESID && pos <= m) out[pos - 1] = h[pos - 1] + dot;
+    }
+    if (idx < m) {
+        const int pos = d.bind[idx];
+        if (mode == CP_CBAR && pos > m) out[pos - m - 1] = d.coef[idx] - pi[idx];
+        if (mode == CP_RESID && pos <= m) out[pos - 1] = h[pos - 1] - pi[idx];
+    }
+}
+
+void rowpass_pi(hipStream_t s, const SpxDev &d, int mode, int nr, const double *pi, const double *h, double *out)
+{
+    const int nw = nr <= 64 ? 4 : (nr <= 256 ? 8 : 16);
+    hipLaunchKernelGGL(k_rowpass_pi, dim3(cdiv(std::max(d.m, d.n), 64)), dim3(64 * nw), 0, s, d, mode, nr, pi, h,
+                       out);
+}
+
 void binv_btran_list(hipStream_t s, const SpxDev &d, int nr, const double *x, double *y)
 {
     hipLaunchKernelGGL(k_binvt_list, dim3(nr + cdiv(d.m, 256)), dim3(256), 0, s, d, nr, x, y);

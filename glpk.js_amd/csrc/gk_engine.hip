@@ -581,10 +581,15 @@ struct Spx {
         double *cB = E->r1.p, *pi = E->u.p, *r = E->r2.p, *dd = E->work.p;
         cb_vector(s, m, E->head.p, E->coef.p, cB);
         btran_(cB, pi);
-        colpass(s, A, CP_RESID, 0, m, E->head.p, E->stat.p, E->coef.p, cB, pi, nullptr, r, nullptr, nullptr);
+        // dual, dense A: pi lives on the dense columns of inv(B) (row costs
+        // are 0), so the passes run over those rows of AT
+        const bool rows = dual && E->dense && A.AT && hs.nr <= LIST_FTRAN_MAX && 2 * hs.nr <= m;
+        if (rows) rowpass_pi(s, d, CP_RESID, hs.nr, pi, cB, r);
+        else colpass(s, A, CP_RESID, 0, m, E->head.p, E->stat.p, E->coef.p, cB, pi, nullptr, r, nullptr, nullptr);
         btran_(r, dd);
         vec_axpy(s, pi, dd, 1.0, m);
-        colpass(s, A, CP_CBAR, m, n, E->head.p, E->stat.p, E->coef.p, nullptr, pi, nullptr, E->cbar.p, nullptr, nullptr);
+        if (rows) rowpass_pi(s, d, CP_CBAR, hs.nr, pi, nullptr, E->cbar.p);
+        else colpass(s, A, CP_CBAR, m, n, E->head.p, E->stat.p, E->coef.p, nullptr, pi, nullptr, E->cbar.p, nullptr, nullptr);
         (void)d;
         down(cbar, E->cbar, n);
         sync();
@@ -1265,7 +1270,11 @@ int Spx::run_dual()
             }
         }
         int K = rigorous ? 1 : E->kbatch;
-        if (P->it_lim < 0x7fffffff) K = std::max(1, std::min(K, P->it_lim - (hs.it_cnt - it_beg)));
+        if (P->it_lim < 0x7fffffff) {
+            // an iteration budget of up to two full batches runs as one
+            const int rem = P->it_lim - (hs.it_cnt - it_beg);
+            K = (!rigorous && K >= 64 && rem <= 128) ? rem : std::max(1, std::min(K, rem));
+        }
         int why = batch(K, rigorous);
         E->kbatch = next_batch(E->kbatch, why);
         dinf_known = (why == ST_BATCH && hs.npiv > 0);
@@ -1392,7 +1401,11 @@ int Spx::run_primal()
             }
         }
         int K = rigorous ? 1 : E->kbatch;
-        if (P->it_lim < 0x7fffffff) K = std::max(1, std::min(K, P->it_lim - (hs.it_cnt - it_beg)));
+        if (P->it_lim < 0x7fffffff) {
+            // an iteration budget of up to two full batches runs as one
+            const int rem = P->it_lim - (hs.it_cnt - it_beg);
+            K = (!rigorous && K >= 64 && rem <= 128) ? rem : std::max(1, std::min(K, rem));
+        }
         int why = batch(K, rigorous);
         E->kbatch = next_batch(E->kbatch, why);
         if (hs.npiv > 0) {

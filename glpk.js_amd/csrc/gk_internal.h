@@ -169,6 +169,8 @@ DualPlan primal_plan(const SpxDev &d, int nr_max, int pse);
 bool primal_fast_ok(const SpxDev &d);
 void primal_batch_begin(hipStream_t s, const SpxDev &d);
 void primal_iteration2(hipStream_t s, const SpxDev &d, const DualPlan &pl);
+// dual, dense A: CP_CBAR / CP_RESID of eval_cbar over the rows of AT in rlist
+void rowpass_pi(hipStream_t s, const SpxDev &d, int mode, int nr, const double *pi, const double *h, double *out);
 // timing hook: the row-path pivot-row kernel alone (returns algorithmic bytes)
 double launch_trow_rows(hipStream_t s, const SpxDev &d, const DualPlan &pl, int ns);
 // y = inv(B) x and y = inv(B)' x over the nr dense columns of rlist and the
