@@ -1008,6 +1008,11 @@ void Spx::init()
     // eta file; re-inversion cost grows with k^3, so scale the interval
     lim = std::max(lim, std::min(1000, m / 4));
     hs.upd_lim = lim;
+    // the product-form updates of the factor persist across calls, as the
+    // reference's FT eta count does in lp.bfd (glpfhv.js:182): a run of short
+    // it_lim calls re-inverts on the same schedule as one long call
+    hs.upd_cnt = f->valid ? std::min(f->upd_cnt, lim) : 0;
+    hs.refact_pending = (f->valid && hs.upd_cnt >= lim) ? 1 : 0;
     hs.refct = 0;
     it_beg = L->it_cnt;
     tm_beg = now_s();
@@ -1169,6 +1174,18 @@ void Spx::run_graph(const SpxDev &d, const DualPlan &pl, int K, int kind)
 // to the minimum after any other stop (a stop drains the rest of the batch)
 static int next_batch(int k, int why) { return why == ST_BATCH ? std::min(2 * k, 64) : 8; }
 
+// a batch that would run past the update limit stops inside its graph and
+// drains the rest as gated no-op launches: end it at the re-inversion point
+// instead, in power-of-two steps (their graphs are cached) down to 8
+static int align_to_refactor(int K, int left)
+{
+    if (left <= 0 || left >= K) return K;
+    if (left < 8) return left;
+    int p = 8;
+    while (2 * p <= left) p *= 2;
+    return p;
+}
+
 int Spx::run_dual()
 {
     const gk_smcp *P = parm;
@@ -1269,12 +1286,19 @@ int Spx::run_dual()
                 return it_hit ? 8 : 9;
             }
         }
+        if (hs.refact_pending && binv_st != 0) {
+            // the update limit was reached at the end of the last batch:
+            // re-invert before launching (a batch would stop at its first pivot)
+            binv_st = 0;
+            continue;
+        }
         int K = rigorous ? 1 : E->kbatch;
         if (P->it_lim < 0x7fffffff) {
             // an iteration budget of up to two full batches runs as one
             const int rem = P->it_lim - (hs.it_cnt - it_beg);
             K = (!rigorous && K >= 64 && rem <= 128) ? rem : std::max(1, std::min(K, rem));
         }
+        K = align_to_refactor(K, hs.upd_lim - hs.upd_cnt);
         int why = batch(K, rigorous);
         E->kbatch = next_batch(E->kbatch, why);
         dinf_known = (why == ST_BATCH && hs.npiv > 0);
@@ -1400,12 +1424,19 @@ int Spx::run_primal()
                 return it_hit ? 8 : 9;
             }
         }
+        if (hs.refact_pending && binv_st != 0) {
+            // the update limit was reached at the end of the last batch:
+            // re-invert before launching (a batch would stop at its first pivot)
+            binv_st = 0;
+            continue;
+        }
         int K = rigorous ? 1 : E->kbatch;
         if (P->it_lim < 0x7fffffff) {
             // an iteration budget of up to two full batches runs as one
             const int rem = P->it_lim - (hs.it_cnt - it_beg);
             K = (!rigorous && K >= 64 && rem <= 128) ? rem : std::max(1, std::min(K, rem));
         }
+        K = align_to_refactor(K, hs.upd_lim - hs.upd_cnt);
         int why = batch(K, rigorous);
         E->kbatch = next_batch(E->kbatch, why);
         if (hs.npiv > 0) {
