@@ -20,29 +20,38 @@
 // reads X_R = M[R, :] in place with no race.  2 launches per panel instead
 // of one launch per column.
 #include "gk_device.h"
+#include <cstdlib>
 
 namespace gk {
 
 constexpr int GJ_NONE = 0x7fffffff;
 
+// The panel: columns [c0, c0 + b) of a row-major buffer with row stride ld
+// (M itself, or the outer panel P of the two-level scheme), b = min(B,
+// ncols - c0); global step numbers start at tg0.  With xr_cols > 0 the pivot
+// rows of the buffer's first xr_cols columns are copied to xr before the
+// panel is written back (the inner update's X_R).
 template <int NT, int RPT, int B>
-__global__ void __launch_bounds__(NT) k_gjb_panel(const double *__restrict__ M, double *__restrict__ M2,
-                                                  double *__restrict__ Qm, int k, int t0, int *__restrict__ piv_step,
-                                                  int *__restrict__ piv, int *__restrict__ flag, double tiny)
+__global__ void __launch_bounds__(NT) k_gjb_panel(const double *__restrict__ M, double *__restrict__ M2, int ld,
+                                                  int c0, int ncols, double *__restrict__ Qm, int k, int tg0,
+                                                  int *__restrict__ piv_step, int *__restrict__ piv,
+                                                  int *__restrict__ flag, double tiny, double *__restrict__ xr,
+                                                  int xr_cols)
 {
     __shared__ Cand shc[NT / 64];
     __shared__ double frs[B];
     __shared__ int rsl[B];
     if (*flag) return;
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-    const int b = min(B, k - t0);
+    const int b = min(B, ncols - c0);
+    const int t0 = tg0;
     double x[RPT][B];
     bool live[RPT];                      // row owned, and not pivoted yet
 #pragma unroll
     for (int j = 0; j < RPT; ++j) {
         const int r = tid + j * NT;
         live[j] = r < k && piv_step[r] == GJ_NONE;
-        const double *row = M + (size_t)r * k + t0;
+        const double *row = M + (size_t)r * ld + c0;
 #pragma unroll
         for (int c = 0; c < B; ++c) x[j][c] = (r < k && c < b) ? row[c] : 0.0;
     }
@@ -108,12 +117,19 @@ __global__ void __launch_bounds__(NT) k_gjb_panel(const double *__restrict__ M, 
         piv[t0 + tid] = rsl[tid];
         piv_step[rsl[tid]] = t0 + tid;
     }
+    if (xr_cols > 0) {
+        for (int e = tid; e < B * xr_cols; e += NT) {
+            const int kk = e / xr_cols, c = e - kk * xr_cols;
+            xr[e] = (kk < b) ? M[(size_t)rsl[kk] * ld + c] : 0.0;
+        }
+        __syncthreads();                 // read before the panel is written back (in place)
+    }
     // the panel into M2, Q - E_R for the update
 #pragma unroll
     for (int j = 0; j < RPT; ++j) {
         const int r = tid + j * NT;
         if (r >= k) continue;
-        double *row = M2 + (size_t)r * k + t0;
+        double *row = M2 + (size_t)r * ld + c0;
         double *q = Qm + (size_t)r * B;
 #pragma unroll
         for (int c = 0; c < B; ++c) {
@@ -130,10 +146,11 @@ __global__ void __launch_bounds__(NT) k_gjb_panel(const double *__restrict__ M, 
 // B[kk = l >> 4][j = l & 15], D[(l >> 4) + 4 r][l & 15].
 typedef double gj_double4 __attribute__((ext_vector_type(4)));
 
-template <int B>
+template <int B, int SUBE>
 __global__ void __launch_bounds__(256) k_gjb_update(const double *__restrict__ M, double *__restrict__ M2,
-                                                    const double *__restrict__ Qm, const int *__restrict__ rsl,
-                                                    int k, int t0, const int *__restrict__ flag)
+                                                    const double *__restrict__ Qm, int ldq,
+                                                    const int *__restrict__ rsl, int k, int t0,
+                                                    const int *__restrict__ flag)
 {
     if (*flag) return;
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -151,16 +168,18 @@ __global__ void __launch_bounds__(256) k_gjb_update(const double *__restrict__ M
                 const int gr = row0 + a * 16 + lk + 4 * r, gc = col0 + bb * 16 + li;
                 acc[a][bb][r] = (gr < k && gc < k) ? M[(size_t)gr * k + gc] : 0.0;
             }
-#pragma unroll
+#pragma unroll 4
     for (int kk = 0; kk < B; kk += 4) {
         const int gk = kk + lk;
+        const int rk = gk < b ? rsl[gk] : -1;
         double av[2], bv[2];
 #pragma unroll
         for (int a = 0; a < 2; ++a) {
             const int gr = row0 + a * 16 + li;
-            av[a] = gr < k ? Qm[(size_t)gr * B + gk] : 0.0;
+            double q = (gr < k && gk < b) ? Qm[(size_t)gr * ldq + gk] : 0.0;
+            if (SUBE && gr == rk) q -= 1.0;          // Q - E_R
+            av[a] = q;
         }
-        const int rk = gk < b ? rsl[gk] : -1;
 #pragma unroll
         for (int bb = 0; bb < 2; ++bb) {
             const int gc = col0 + bb * 16 + li;
@@ -183,16 +202,75 @@ __global__ void __launch_bounds__(256) k_gjb_update(const double *__restrict__ M
             }
 }
 
+// ---------------------------------------------------------------------------
+// two-level scheme (large k, narrow register panels): an outer panel of
+// BO = 64 columns is copied to P (k x 64), factored by inner panels of B
+// columns, each followed by a rank-B update of the other columns of P only
+// (k_gjb_inner); the rest of M then takes one rank-64 update with
+// Q = P - E_R (k_gjb_update<64, 1>): the same arithmetic as the one-level
+// scheme regrouped, M streamed k / 64 times instead of k / B.
+// ---------------------------------------------------------------------------
+constexpr int GJ_BO = 64;
+
+__global__ void __launch_bounds__(256) k_gjb_copy(const double *__restrict__ src, int lds, int cs,
+                                                  double *__restrict__ dst, int ldd, int cd, int k, int bo,
+                                                  const int *__restrict__ flag)
+{
+    if (*flag) return;
+    const int r = blockIdx.x * 4 + (threadIdx.x >> 6), c = threadIdx.x & 63;
+    if (r < k && c < bo) dst[(size_t)r * ldd + cd + c] = src[(size_t)r * lds + cs + c];
+}
+
+// P[r, j] += sum_kk (Q - E_R)[r, kk] X_R[kk, j] for j outside the inner panel [i0, i0 + b)
+template <int B>
+__global__ void __launch_bounds__(256) k_gjb_inner(double *__restrict__ P, int bo, int i0, const double *__restrict__ Qm,
+                                                   const double *__restrict__ xr, int k, const int *__restrict__ flag)
+{
+    __shared__ double sx[B * GJ_BO];
+    if (*flag) return;
+    for (int e = threadIdx.x; e < B * bo; e += 256) sx[(e / bo) * GJ_BO + e % bo] = xr[e];
+    __syncthreads();
+    const int r = blockIdx.x * 4 + (threadIdx.x >> 6), j = threadIdx.x & 63;
+    if (r >= k || j >= bo || (j >= i0 && j < i0 + B)) return;
+    double acc = P[(size_t)r * GJ_BO + j];
+    const double *q = Qm + (size_t)r * B;
+#pragma unroll
+    for (int kk = 0; kk < B; ++kk) acc += q[kk] * sx[kk * GJ_BO + j];
+    P[(size_t)r * GJ_BO + j] = acc;
+}
+
 template <int NT, int RPT, int B>
 static double *gjb_run(hipStream_t s, double *M, double *M2, double *Qm, int k, int *piv_step, int *piv, int *flag,
                        double tiny)
 {
     const dim3 g((k + 63) / 64, (k + 63) / 64);
     for (int t0 = 0; t0 < k; t0 += B) {
-        hipLaunchKernelGGL((k_gjb_panel<NT, RPT, B>), dim3(1), dim3(NT), 0, s, M, M2, Qm, k, t0, piv_step, piv, flag,
-                           tiny);
+        hipLaunchKernelGGL((k_gjb_panel<NT, RPT, B>), dim3(1), dim3(NT), 0, s, M, M2, k, t0, k, Qm, k, t0, piv_step,
+                           piv, flag, tiny, (double *)nullptr, 0);
         if (k > B)
-            hipLaunchKernelGGL((k_gjb_update<B>), g, dim3(256), 0, s, M, M2, Qm, piv + t0, k, t0, flag);
+            hipLaunchKernelGGL((k_gjb_update<B, 0>), g, dim3(256), 0, s, M, M2, Qm, B, piv + t0, k, t0, flag);
+        std::swap(M, M2);
+    }
+    return M;
+}
+
+template <int NT, int RPT, int B>
+static double *gjb_run2(hipStream_t s, double *M, double *M2, double *P, double *Qm, double *xr, int k,
+                        int *piv_step, int *piv, int *flag, double tiny)
+{
+    const dim3 g((k + 63) / 64, (k + 63) / 64);
+    const dim3 gr((k + 3) / 4);
+    for (int T0 = 0; T0 < k; T0 += GJ_BO) {
+        const int bo = std::min(GJ_BO, k - T0);
+        hipLaunchKernelGGL(k_gjb_copy, gr, dim3(256), 0, s, M, k, T0, P, GJ_BO, 0, k, bo, flag);
+        for (int i0 = 0; i0 < bo; i0 += B) {
+            hipLaunchKernelGGL((k_gjb_panel<NT, RPT, B>), dim3(1), dim3(NT), 0, s, P, P, GJ_BO, i0, bo, Qm, k,
+                               T0 + i0, piv_step, piv, flag, tiny, xr, bo);
+            if (bo > B) hipLaunchKernelGGL((k_gjb_inner<B>), gr, dim3(256), 0, s, P, bo, i0, Qm, xr, k, flag);
+        }
+        if (k > bo)
+            hipLaunchKernelGGL((k_gjb_update<GJ_BO, 1>), g, dim3(256), 0, s, M, M2, P, GJ_BO, piv + T0, k, T0, flag);
+        hipLaunchKernelGGL(k_gjb_copy, gr, dim3(256), 0, s, P, GJ_BO, 0, M2, k, T0, k, bo, flag);
         std::swap(M, M2);
     }
     return M;
@@ -208,7 +286,8 @@ int gj_blocked_max() { return 8192; }
 
 size_t gj_blocked_scratch(int k)
 {
-    return (size_t)32 * k;                 // Q (k x B, B <= 32)
+    // Q (k x B, B <= 32), the outer panel P (k x 64), X_R (32 x 64)
+    return (size_t)32 * k + (size_t)GJ_BO * k + 32 * GJ_BO;
 }
 
 // inverse of C (k x k, column-major in X[0, k^2)) by the blocked scheme
@@ -220,14 +299,15 @@ double *gauss_jordan_blocked(hipStream_t s, double *X, double *scratch, int k, i
 {
     if (k <= 0) return X;
     hipLaunchKernelGGL(k_gjb_init, dim3(std::min((k + 255) / 256, 64)), dim3(256), 0, s, piv_step, k, flag);
-    double *M2 = X + (size_t)k * k, *Qm = scratch;
-    // registers: RPT * B doubles of the panel per thread (1 / 2 / 4 waves per SIMD)
+    double *M2 = X + (size_t)k * k, *Qm = scratch, *P = scratch + (size_t)32 * k, *xr = P + (size_t)GJ_BO * k;
+    // registers: RPT * B doubles of the panel per thread (1 / 2 / 4 waves per
+    // SIMD); beyond 1024 the two-level scheme streams M once per 64 columns
     if (k <= 256) return gjb_run<256, 1, 16>(s, X, M2, Qm, k, piv_step, piv, flag, tiny);
     if (k <= 512) return gjb_run<256, 2, 16>(s, X, M2, Qm, k, piv_step, piv, flag, tiny);
     if (k <= 1024) return gjb_run<512, 2, 16>(s, X, M2, Qm, k, piv_step, piv, flag, tiny);
-    if (k <= 2048) return gjb_run<1024, 2, 16>(s, X, M2, Qm, k, piv_step, piv, flag, tiny);
-    if (k <= 4096) return gjb_run<1024, 4, 8>(s, X, M2, Qm, k, piv_step, piv, flag, tiny);
-    return gjb_run<1024, 8, 4>(s, X, M2, Qm, k, piv_step, piv, flag, tiny);
+    if (k <= 2048) return gjb_run2<1024, 2, 16>(s, X, M2, P, Qm, xr, k, piv_step, piv, flag, tiny);
+    if (k <= 4096) return gjb_run2<1024, 4, 8>(s, X, M2, P, Qm, xr, k, piv_step, piv, flag, tiny);
+    return gjb_run2<1024, 8, 4>(s, X, M2, P, Qm, xr, k, piv_step, piv, flag, tiny);
 }
 
 // CinvR (row-major inv(C)): with M = C' inverted in place,
