@@ -540,18 +540,57 @@ struct HostArr {
     }
 };
 
-struct OpenNode {
+// an open node: its bound and creation order in the queue, its structural
+// bounds and warm-start basis in a slot of the node pool
+struct NodeRec {
     double bound;                 // local bound, minimisation form
     long long seq;                // creation order (tie-break: older first)
-    std::vector<double> lb, ub;   // structural bounds
-    std::vector<signed char> stat;   // warm-start basis, [m+n]
+    int slot;
 };
 
 struct NodeCmp {
-    bool operator()(const OpenNode *a, const OpenNode *b) const
+    bool operator()(const NodeRec &a, const NodeRec &b) const
     {
-        if (a->bound != b->bound) return a->bound > b->bound;
-        return a->seq > b->seq;
+        if (a.bound != b.bound) return a.bound > b.bound;
+        return a.seq > b.seq;
+    }
+};
+
+// slots of 2 n doubles (lb | ub of the structurals) and m + n statuses,
+// recycled through a free list (no per-node heap allocation)
+struct NodePool {
+    int n = 0, N = 0;
+    std::vector<double> bnd;
+    std::vector<signed char> st;
+    std::vector<int> freel;
+    int alloc()
+    {
+        if (!freel.empty()) {
+            const int sl = freel.back();
+            freel.pop_back();
+            return sl;
+        }
+        const int sl = (int)(st.size() / (size_t)N);
+        bnd.resize(bnd.size() + 2 * (size_t)n);
+        st.resize(st.size() + (size_t)N);
+        return sl;
+    }
+    void release(int sl) { freel.push_back(sl); }
+    double *lb(int sl) { return bnd.data() + (size_t)sl * 2 * n; }
+    double *ub(int sl) { return bnd.data() + (size_t)sl * 2 * n + n; }
+    signed char *stat(int sl) { return st.data() + (size_t)sl * N; }
+};
+
+// one batch in flight: packed inputs / outputs (one copy each way)
+struct BatchBuf {
+    DevArr<char> din, dout;
+    HostArr<char> hin, hout;
+    hipEvent_t done = nullptr;
+    std::vector<NodeRec> nodes;
+    int nb = 0;
+    ~BatchBuf()
+    {
+        if (done) (void)hipEventDestroy(done);
     }
 };
 
@@ -562,26 +601,30 @@ struct MipSolver {
     double sign = 1.0, c0 = 0.0;
     std::vector<double> A, c, rlb, rub, clb, cub, coef;
     std::vector<signed char> isint, fixed_col;
-    DevArr<double> dA, dc, dlb, dub, dcut, dobj, dx, ddz, dscratch;
-    DevArr<signed char> dint, dsin, dsout;
-    DevArr<int> dstatus, dpiv, djj, dnext;
-    HostArr<double> hlb, hub, hcut, hobj, hx, hdz;
-    HostArr<signed char> hsin, hsout;
-    HostArr<int> hstatus, hpiv, hjj, hnext;
+    DevArr<double> dA, dc, dscratch;
+    DevArr<signed char> dint;
+    BatchBuf bufs[2];
+    NodePool pool;
+    int bmax = 0;
+    size_t in_bytes(int nb) const { return (size_t)nb * (2 * (size_t)N + 1) * sizeof(double) + (size_t)nb * N; }
+    size_t out_bytes(int nb) const
+    {
+        return (size_t)nb * (3 + (size_t)N) * sizeof(double) + 4 * (size_t)nb * sizeof(int) + (size_t)nb * N;
+    }
+    bool alloc_batch(int B)
+    {
+        bmax = B;
+        for (auto &bf : bufs) {
+            bf.din.ensure(in_bytes(B) + 64); bf.dout.ensure(out_bytes(B) + 64);
+            bf.hin.ensure(in_bytes(B) + 64); bf.hout.ensure(out_bytes(B) + 64);
+            if (!bf.done && hipEventCreateWithFlags(&bf.done, hipEventDisableTiming) != hipSuccess) return false;
+            if (!bf.din.p || !bf.dout.p || !bf.hin.p || !bf.hout.p) return false;
+        }
+        return true;
+    }
     // ios_round_bound (glpios01.js:730): objective integrality
     bool round_ok = false;
     double round_s = 0.0, round_d = 1.0;
-
-    void alloc_batch(int B)
-    {
-        const size_t NB = (size_t)B * N;
-        dlb.ensure(NB); dub.ensure(NB); dsin.ensure(NB); dsout.ensure(NB); dx.ensure(NB);
-        dcut.ensure(B); dobj.ensure(B); ddz.ensure(2 * (size_t)B);
-        dstatus.ensure(B); dpiv.ensure(B); djj.ensure(B); dnext.ensure(B);
-        hlb.ensure(NB); hub.ensure(NB); hsin.ensure(NB); hsout.ensure(NB); hx.ensure(NB);
-        hcut.ensure(B); hobj.ensure(B); hdz.ensure(2 * (size_t)B);
-        hstatus.ensure(B); hpiv.ensure(B); hjj.ensure(B); hnext.ensure(B);
-    }
 
     // min-form bound -> rounded min-form bound
     double round_bound(double z) const
@@ -700,33 +743,33 @@ extern "C" int gk_ios_driver_sharded(gk_ctx *ctx, gk_mip *mip, const gk_iocp *pa
     // device problem
     S.dA.ensure(S.A.size()); S.dc.ensure(S.N); S.dint.ensure(n);
     const int BMAX = (lds <= NODE_LDS_MAX) ? 1024 : (int)std::max<size_t>(1, std::min<size_t>(1024, SCRATCH_MAX / lds));
-    S.alloc_batch(BMAX);
     const size_t stride = (lds + 255) / 256 * 32;          // doubles, 256-byte aligned slices
     if (lds > NODE_LDS_MAX) {
         S.dscratch.ensure(stride * BMAX);
         if (!S.dscratch.p) { set_err("gk_ios_driver: out of memory (node work area)"); return GK_EABI; }
     }
-    if (!S.dA.p || !S.dc.p || !S.dint.p || !S.dlb.p || !S.hlb.p) { set_err("gk_ios_driver: out of memory"); return GK_EABI; }
+    if (!S.alloc_batch(BMAX) || !S.dA.p || !S.dc.p || !S.dint.p) {
+        set_err("gk_ios_driver: out of memory");
+        return GK_EABI;
+    }
     (void)hipMemcpyAsync(S.dA.p, S.A.data(), S.A.size() * sizeof(double), hipMemcpyHostToDevice, s);
     (void)hipMemcpyAsync(S.dc.p, S.c.data(), S.N * sizeof(double), hipMemcpyHostToDevice, s);
     (void)hipMemcpyAsync(S.dint.p, S.isint.data(), n, hipMemcpyHostToDevice, s);
     NodeProb P;
     P.m = m; P.n = n; P.ld = S.N; P.A = S.dA.p; P.c = S.dc.p; P.isint = S.dint.p; P.tol_int = parm->tol_int;
+    NodePool &pool = S.pool;
+    pool.n = n; pool.N = S.N;
     // root node: the optimal basis of the initial LP relaxation
-    std::vector<OpenNode *> store;
-    std::priority_queue<OpenNode *, std::vector<OpenNode *>, NodeCmp> open;
+    std::priority_queue<NodeRec, std::vector<NodeRec>, NodeCmp> open;
     long long seq = 0;
     {
-        OpenNode *r = new OpenNode;
-        r->bound = -INF;
-        r->seq = seq++;
-        r->lb = S.clb;
-        r->ub = S.cub;
-        r->stat.resize(S.N);
-        for (int i = 0; i < m; i++) r->stat[i] = L.row_stat[i + 1];
-        for (int j = 0; j < n; j++) r->stat[m + j] = L.col_stat[j + 1];
-        store.push_back(r);
-        open.push(r);
+        const int sl = pool.alloc();
+        std::memcpy(pool.lb(sl), S.clb.data(), n * sizeof(double));
+        std::memcpy(pool.ub(sl), S.cub.data(), n * sizeof(double));
+        signed char *st = pool.stat(sl);
+        for (int i = 0; i < m; i++) st[i] = L.row_stat[i + 1];
+        for (int j = 0; j < n; j++) st[m + j] = L.col_stat[j + 1];
+        open.push(NodeRec{-INF, seq++, sl});
     }
     bool have = false;                                    // incumbent of this rank (with x)
     double best = INF;                                    // its objective, minimisation form
@@ -741,9 +784,112 @@ extern "C" int gk_ios_driver_sharded(gk_ctx *ctx, gk_mip *mip, const gk_iocp *pa
         return bound < b - eps;
     };
     // the preferred child of every branched node of a batch is evaluated in
-    // the next batch (parallel dives, as BLB dives into its chosen child,
-    // glpios12.js); the other children wait in the best-bound queue
-    std::vector<OpenNode *> batch, dive, next_dive;
+    // the next batch assembled (parallel dives, as BLB dives into its chosen
+    // child, glpios12.js); the other children wait in the best-bound queue
+    std::vector<NodeRec> dive, next_dive;
+    // single GPU: two batches in flight — the host assembles and launches
+    // batch k + 1 before it processes the results of batch k (more
+    // speculative nodes, the GPU never waits for the host)
+    const int depth = (size == 1) ? 2 : 1;
+    int inflight[2] = {0, 0}, cur = 0;
+    bool fail_sync = false;
+    auto launch = [&](BatchBuf &bf) {
+        const int nb = (int)bf.nodes.size();
+        bf.nb = nb;
+        const double ball = bestall();
+        const double cut = ball < INF ? ball - parm->tol_obj * (1.0 + std::fabs(S.c0 + S.sign * ball)) : INF;
+        const size_t NB = (size_t)nb * S.N;
+        double *hl = (double *)bf.hin.p, *hu = hl + NB, *hc = hu + NB;
+        signed char *hs = (signed char *)(hc + nb);
+        for (int b = 0; b < nb; b++) {
+            const int sl = bf.nodes[b].slot;
+            double *l = hl + (size_t)b * S.N, *u = hu + (size_t)b * S.N;
+            std::memcpy(l, S.rlb.data(), m * sizeof(double));
+            std::memcpy(u, S.rub.data(), m * sizeof(double));
+            std::memcpy(l + m, pool.lb(sl), n * sizeof(double));
+            std::memcpy(u + m, pool.ub(sl), n * sizeof(double));
+            std::memcpy(hs + (size_t)b * S.N, pool.stat(sl), S.N);
+            hc[b] = cut;
+        }
+        (void)hipMemcpyAsync(bf.din.p, bf.hin.p, S.in_bytes(nb), hipMemcpyHostToDevice, s);
+        double *dl = (double *)bf.din.p, *du = dl + NB, *dc = du + NB;
+        double *dobj = (double *)bf.dout.p, *ddz = dobj + nb, *dx = ddz + 2 * (size_t)nb;
+        int *dstat = (int *)(dx + NB), *dpiv = dstat + nb, *djj = dpiv + nb, *dnext = djj + nb;
+        NodeIO io;
+        io.lb = dl; io.ub = du; io.stat_in = (const signed char *)(dc + nb); io.cutoff = dc;
+        io.status = dstat; io.pivots = dpiv; io.jj = djj; io.next = dnext;
+        io.obj = dobj; io.x = dx; io.dz = ddz; io.stat_out = (signed char *)(dnext + nb);
+        io.it_lim = 10000;
+        io.scratch = S.dscratch.p;
+        io.scratch_stride = stride;
+        launch_node_lp(s, P, io, nb);
+        (void)hipMemcpyAsync(bf.hout.p, bf.dout.p, S.out_bytes(nb), hipMemcpyDeviceToHost, s);
+        (void)hipEventRecord(bf.done, s);
+    };
+    auto process = [&](BatchBuf &bf) {
+        if (hipEventSynchronize(bf.done) != hipSuccess) { fail_sync = true; return; }
+        const int nb = bf.nb;
+        const size_t NB = (size_t)nb * S.N;
+        const double *hobj = (const double *)bf.hout.p, *hdz = hobj + nb, *hx = hdz + 2 * (size_t)nb;
+        const int *hstat = (const int *)(hx + NB), *hpiv = hstat + nb, *hjj = hpiv + nb, *hnext = hjj + nb;
+        const signed char *hso = (const signed char *)(hnext + nb);
+        for (int b = 0; b < nb; b++) {
+            const NodeRec nd = bf.nodes[b];
+            lp_solves++;
+            pivots += hpiv[b];
+            const int st = hstat[b];
+            if (st == NODE_FAIL) { failed++; continue; }
+            if (st != NODE_OPT) continue;                  // infeasible or cut off
+            const double z = hobj[b];
+            const double bound = S.round_bound(z);
+            if (!hopeful(bound)) continue;
+            const double *x = hx + (size_t)b * S.N;
+            const int jj = hjj[b];
+            if (jj == 0) {                                 // integer feasible
+                if (!have || z < best) {
+                    have = true;
+                    best = z;
+                    std::memcpy(xbest.data(), x, S.N * sizeof(double));
+                }
+                continue;
+            }
+            const int j = jj - 1;
+            const double beta = x[m + j];
+            const double dz[2] = {hdz[2 * b], hdz[2 * b + 1]};
+            const int first = hnext[b] < 0 ? 0 : 1;      // preferred child gets the older seq
+            bool dived = false;
+            for (int r = 0; r < 2; r++) {
+                const int kase = (r == 0) ? first : 1 - first;
+                if (dz[kase] == DBL_MAX) continue;        // that branch has no feasible point
+                const int sl = pool.alloc();
+                std::memcpy(pool.lb(sl), pool.lb(nd.slot), n * sizeof(double));
+                std::memcpy(pool.ub(sl), pool.ub(nd.slot), n * sizeof(double));
+                if (kase == 0) pool.ub(sl)[j] = std::floor(beta);
+                else pool.lb(sl)[j] = std::ceil(beta);
+                signed char *cs = pool.stat(sl);
+                std::memcpy(cs, hso + (size_t)b * S.N, S.N);
+                // a fixed bound pair makes a non-basic column NS
+                if (cs[m + j] != BS && pool.lb(sl)[j] == pool.ub(sl)[j]) cs[m + j] = NS;
+                const NodeRec c{S.round_bound(z + dz[kase]), seq++, sl};
+                if (!dived) {
+                    next_dive.push_back(c);
+                    dived = true;
+                } else
+                    open.push(c);
+                created++;
+            }
+        }
+        for (const NodeRec &nd : bf.nodes) pool.release(nd.slot);
+        bf.nodes.clear();
+        for (const NodeRec &c : next_dive) dive.push_back(c);
+        next_dive.clear();
+    };
+    auto drain = [&]() {
+        for (int k = 0; k < 2; k++) {
+            const int sb = (cur + k) & 1;
+            if (inflight[sb]) { process(S.bufs[sb]); inflight[sb] = 0; }
+        }
+    };
     // sharded runs: every rank evaluates the same first
     // batches (deterministic, identical on every GPU) until the frontier holds
     // ramp * size nodes, then keeps the nodes i = rank (mod size) of the
@@ -753,25 +899,31 @@ extern "C" int gk_ios_driver_sharded(gk_ctx *ctx, gk_mip *mip, const gk_iocp *pa
     bool split_done = (size == 1), timed_out = false;
     int since_sync = 0;
     for (;;) {
-        bool have_work = !open.empty() || !dive.empty();
+        if (fail_sync) break;
+        const bool any_inflight = inflight[0] || inflight[1];
+        bool have_work = !open.empty() || !dive.empty() || any_inflight;
         if (have_work && parm->tm_lim < 0x7fffffff &&
             std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() * 1000.0 >= parm->tm_lim) {
             timed_out = true;
-            while (!open.empty()) open.pop();
+            drain();
+            while (!open.empty()) { pool.release(open.top().slot); open.pop(); }
+            for (const NodeRec &d : dive) pool.release(d.slot);
             dive.clear();
             have_work = false;
         }
         if (!split_done) {
             if (!have_work) break;                        // the tree ended during the ramp-up: same on every rank
             if ((long long)open.size() + (long long)dive.size() >= (long long)ramp * size) {
-                std::vector<OpenNode *> front(dive.begin(), dive.end());
+                std::vector<NodeRec> front(dive.begin(), dive.end());
                 while (!open.empty()) { front.push_back(open.top()); open.pop(); }
                 dive.clear();
-                std::sort(front.begin(), front.end(), [](const OpenNode *a, const OpenNode *b) {
-                    return a->bound != b->bound ? a->bound < b->bound : a->seq < b->seq;
+                std::sort(front.begin(), front.end(), [](const NodeRec &a, const NodeRec &b) {
+                    return a.bound != b.bound ? a.bound < b.bound : a.seq < b.seq;
                 });
-                for (size_t i = 0; i < front.size(); i++)
+                for (size_t i = 0; i < front.size(); i++) {
                     if ((int)(i % size) == rank) open.push(front[i]);
+                    else pool.release(front[i].slot);
+                }
                 split_done = true;
                 continue;
             }
@@ -786,115 +938,45 @@ extern "C" int gk_ios_driver_sharded(gk_ctx *ctx, gk_mip *mip, const gk_iocp *pa
         }
         if (!have_work) break;
         since_sync++;
-        batch.clear();
-        for (OpenNode *nd : dive) {
-            if ((int)batch.size() < BMAX && hopeful(nd->bound)) batch.push_back(nd);
-            else if (hopeful(nd->bound)) open.push(nd);
+        // assemble the next batch into the free buffer set
+        BatchBuf &bf = S.bufs[cur];
+        if (inflight[cur]) { process(bf); inflight[cur] = 0; }
+        bf.nodes.clear();
+        {
+            std::vector<NodeRec> keep;
+            for (const NodeRec &nd : dive) {
+                if (!hopeful(nd.bound)) { pool.release(nd.slot); continue; }
+                if ((int)bf.nodes.size() < BMAX) bf.nodes.push_back(nd);
+                else open.push(nd);
+            }
+            dive.clear();
         }
-        dive.clear();
-        while (!open.empty() && (int)batch.size() < BMAX) {
-            OpenNode *nd = open.top();
+        while (!open.empty() && (int)bf.nodes.size() < BMAX) {
+            const NodeRec nd = open.top();
             open.pop();
-            if (!hopeful(nd->bound)) continue;
-            batch.push_back(nd);
+            if (!hopeful(nd.bound)) { pool.release(nd.slot); continue; }
+            bf.nodes.push_back(nd);
         }
-        if (batch.empty()) continue;                      // everything left was pruned
-        const int nb = (int)batch.size();
-        const double ball = bestall();
-        const double cut = ball < INF ? ball - parm->tol_obj * (1.0 + std::fabs(S.c0 + S.sign * ball)) : INF;
-        for (int b = 0; b < nb; b++) {
-            OpenNode *nd = batch[b];
-            double *l = S.hlb.p + (size_t)b * S.N, *u = S.hub.p + (size_t)b * S.N;
-            std::memcpy(l, S.rlb.data(), m * sizeof(double));
-            std::memcpy(u, S.rub.data(), m * sizeof(double));
-            std::memcpy(l + m, nd->lb.data(), n * sizeof(double));
-            std::memcpy(u + m, nd->ub.data(), n * sizeof(double));
-            std::memcpy(S.hsin.p + (size_t)b * S.N, nd->stat.data(), S.N);
-            S.hcut.p[b] = cut;
+        if (!bf.nodes.empty()) {
+            launch(bf);
+            inflight[cur] = 1;
         }
-        const size_t NB = (size_t)nb * S.N;
-        (void)hipMemcpyAsync(S.dlb.p, S.hlb.p, NB * sizeof(double), hipMemcpyHostToDevice, s);
-        (void)hipMemcpyAsync(S.dub.p, S.hub.p, NB * sizeof(double), hipMemcpyHostToDevice, s);
-        (void)hipMemcpyAsync(S.dsin.p, S.hsin.p, NB, hipMemcpyHostToDevice, s);
-        (void)hipMemcpyAsync(S.dcut.p, S.hcut.p, nb * sizeof(double), hipMemcpyHostToDevice, s);
-        NodeIO io;
-        io.lb = S.dlb.p; io.ub = S.dub.p; io.stat_in = S.dsin.p; io.cutoff = S.dcut.p;
-        io.status = S.dstatus.p; io.pivots = S.dpiv.p; io.jj = S.djj.p; io.next = S.dnext.p;
-        io.obj = S.dobj.p; io.x = S.dx.p; io.dz = S.ddz.p; io.stat_out = S.dsout.p;
-        io.it_lim = 10000;
-        io.scratch = S.dscratch.p;
-        io.scratch_stride = stride;
-        launch_node_lp(s, P, io, nb);
-        (void)hipMemcpyAsync(S.hstatus.p, S.dstatus.p, nb * sizeof(int), hipMemcpyDeviceToHost, s);
-        (void)hipMemcpyAsync(S.hpiv.p, S.dpiv.p, nb * sizeof(int), hipMemcpyDeviceToHost, s);
-        (void)hipMemcpyAsync(S.hjj.p, S.djj.p, nb * sizeof(int), hipMemcpyDeviceToHost, s);
-        (void)hipMemcpyAsync(S.hnext.p, S.dnext.p, nb * sizeof(int), hipMemcpyDeviceToHost, s);
-        (void)hipMemcpyAsync(S.hobj.p, S.dobj.p, nb * sizeof(double), hipMemcpyDeviceToHost, s);
-        (void)hipMemcpyAsync(S.hdz.p, S.ddz.p, 2 * nb * sizeof(double), hipMemcpyDeviceToHost, s);
-        (void)hipMemcpyAsync(S.hx.p, S.dx.p, NB * sizeof(double), hipMemcpyDeviceToHost, s);
-        (void)hipMemcpyAsync(S.hsout.p, S.dsout.p, NB, hipMemcpyDeviceToHost, s);
-        if (hipStreamSynchronize(s) != hipSuccess) {
-            set_err("gk_ios_driver: node batch failed: %s", hipGetErrorString(hipGetLastError()));
-            for (auto p : store) delete p;
-            return GK_EABI;
+        const int prev = cur ^ 1;
+        if (depth == 1 || bf.nodes.empty()) {
+            // no pipelining (sharded runs), or nothing new to launch: finish
+            // what is in flight, oldest first
+            if (inflight[prev]) { process(S.bufs[prev]); inflight[prev] = 0; }
+            if (depth == 1 && inflight[cur]) { process(bf); inflight[cur] = 0; }
+        } else if (inflight[prev]) {
+            process(S.bufs[prev]);
+            inflight[prev] = 0;
         }
-        for (int b = 0; b < nb; b++) {
-            OpenNode *nd = batch[b];
-            lp_solves++;
-            pivots += S.hpiv.p[b];
-            const int st = S.hstatus.p[b];
-            if (st == NODE_FAIL) { failed++; continue; }
-            if (st != NODE_OPT) continue;                  // infeasible or cut off
-            const double z = S.hobj.p[b];
-            const double bound = S.round_bound(z);
-            if (!hopeful(bound)) continue;
-            const double *x = S.hx.p + (size_t)b * S.N;
-            const int jj = S.hjj.p[b];
-            if (jj == 0) {                                 // integer feasible
-                if (!have || z < best) {
-                    have = true;
-                    best = z;
-                    std::memcpy(xbest.data(), x, S.N * sizeof(double));
-                }
-                continue;
-            }
-            const int j = jj - 1;
-            const double beta = x[m + j];
-            const double dz[2] = {S.hdz.p[2 * b], S.hdz.p[2 * b + 1]};
-            const int first = S.hnext.p[b] < 0 ? 0 : 1;  // preferred child gets the older seq
-            bool dived = false;
-            for (int r = 0; r < 2; r++) {
-                const int kase = (r == 0) ? first : 1 - first;
-                if (dz[kase] == DBL_MAX) continue;        // that branch has no feasible point
-                OpenNode *c = new OpenNode;
-                c->bound = S.round_bound(z + dz[kase]);
-                c->seq = seq++;
-                c->lb = nd->lb;
-                c->ub = nd->ub;
-                if (kase == 0) c->ub[j] = std::floor(beta);
-                else c->lb[j] = std::ceil(beta);
-                c->stat.assign(S.hsout.p + (size_t)b * S.N, S.hsout.p + (size_t)(b + 1) * S.N);
-                // a fixed bound pair makes a non-basic column NS
-                if (c->stat[m + j] != BS && c->lb[j] == c->ub[j]) c->stat[m + j] = NS;
-                store.push_back(c);
-                if (!dived) {
-                    next_dive.push_back(c);
-                    dived = true;
-                } else
-                    open.push(c);
-                created++;
-            }
-        }
-        dive.swap(next_dive);
-        next_dive.clear();
-        // release the evaluated nodes
-        for (auto nd : batch) {
-            nd->lb.clear(); nd->lb.shrink_to_fit();
-            nd->ub.clear(); nd->ub.shrink_to_fit();
-            nd->stat.clear(); nd->stat.shrink_to_fit();
-        }
+        cur ^= 1;
     }
-    for (auto p : store) delete p;
+    if (fail_sync) {
+        set_err("gk_ios_driver: node batch failed: %s", hipGetErrorString(hipGetLastError()));
+        return GK_EABI;
+    }
     mip->lp_solves = lp_solves;
     mip->nodes_created = created;
     mip->pivots = pivots;
