@@ -121,6 +121,7 @@ struct Engine {
     size_t pin_cap = 0;
     DBuf<int> rlist, rpos, rho_idx, wlist, wpos, awcnt;
     DBuf<double> rho_val, gpart, cand, awpart;
+    DBuf<char> upstage;                         // device side of the coalesced uploads
     DBuf<unsigned long long> tslots;
     std::vector<GraphEntry> graphs;
     unsigned long long graph_clock = 0;
@@ -465,7 +466,8 @@ struct Spx {
     void up(DBuf<T> &d, const std::vector<T> &h, size_t cnt)
     {
         // through the pinned staging buffer: the host data is taken now, the
-        // copy itself is asynchronous
+        // copy itself is asynchronous (or, between begin_up and flush_up, one
+        // copy of the whole staged region plus a device-side scatter)
         const size_t bytes = cnt * sizeof(T);
         char *stage = pin_take(bytes);
         if (!stage) {
@@ -473,7 +475,43 @@ struct Spx {
             return;
         }
         std::memcpy(stage, h.data() + 1, bytes);
+        if (coalesce) {
+            segs.push_back(UpSeg{(size_t)(stage - E->pin) - coal_beg, (void *)d.p, bytes});
+            return;
+        }
         HIPCHK(hipMemcpyAsync(d.p, stage, bytes, hipMemcpyHostToDevice, s));
+    }
+    bool coalesce = false;
+    size_t coal_beg = 0;
+    std::vector<UpSeg> segs;
+    void begin_up()
+    {
+        // start from an empty staging buffer (it holds 32 (m + n + 1)
+        // doubles, more than init's uploads: no sync inside the region)
+        if (pin_off) sync();
+        coalesce = true;
+        coal_beg = pin_off;
+        segs.clear();
+    }
+    void flush_up()
+    {
+        coalesce = false;
+        if (segs.empty()) return;
+        // the segment table behind the data, then one copy and one kernel
+        char *tab = pin_take(segs.size() * sizeof(UpSeg));
+        if (!tab) {
+            for (const UpSeg &g : segs)
+                HIPCHK(hipMemcpyAsync(g.dst, E->pin + coal_beg + g.off, g.bytes, hipMemcpyHostToDevice, s));
+            segs.clear();
+            return;
+        }
+        std::memcpy(tab, segs.data(), segs.size() * sizeof(UpSeg));
+        const size_t total = pin_off - coal_beg;
+        E->upstage.ensure(E->pin_cap);
+        HIPCHK(hipMemcpyAsync(E->upstage.p, E->pin + coal_beg, total, hipMemcpyHostToDevice, s));
+        scatter_segments(s, E->upstage.p, (const UpSeg *)(E->upstage.p + (tab - (E->pin + coal_beg))),
+                         (int)segs.size());
+        segs.clear();
     }
     template <typename T>
     void down(std::vector<T> &h, const DBuf<T> &d, size_t cnt)
@@ -975,10 +1013,12 @@ void Spx::init()
     ABI_REQUIRE(k == n, "gk_spx: basis header inconsistent with statuses (%d non-basic, n = %d)", k, n);
     for (int kk = 1; kk <= m + n; kk++) bind[head[kk]] = kk;
     engine_alloc(*E, m, n);
+    begin_up();
     up(E->type, type, mn - 1); up(E->orig_type, orig_type, mn - 1);
     up(E->lb, lb, mn - 1); up(E->ub, ub, mn - 1); up(E->orig_lb, orig_lb, mn - 1); up(E->orig_ub, orig_ub, mn - 1);
     up(E->coef, coef, mn - 1); up(E->obj, obj, n);
     up(E->head, head, mn - 1); up(E->bind, bind, mn - 1); up(E->stat, stat, n);
+    flush_up();
     // dense columns of inv(B): the non-basic slacks
     {
         std::vector<int> rl, rp(m, -1);

@@ -169,6 +169,13 @@ DualPlan primal_plan(const SpxDev &d, int nr_max, int pse);
 bool primal_fast_ok(const SpxDev &d);
 void primal_batch_begin(hipStream_t s, const SpxDev &d);
 void primal_iteration2(hipStream_t s, const SpxDev &d, const DualPlan &pl);
+// coalesced host->device uploads: segment g of a staged region goes to g.dst
+struct UpSeg {
+    size_t off;
+    void *dst;
+    size_t bytes;
+};
+void scatter_segments(hipStream_t s, const char *src, const UpSeg *segs, int nseg);
 // dual, dense A: CP_CBAR / CP_RESID of eval_cbar over the rows of AT in rlist
 void rowpass_pi(hipStream_t s, const SpxDev &d, int mode, int nr, const double *pi, const double *h, double *out);
 // timing hook: the row-path pivot-row kernel alone (returns algorithmic bytes)
