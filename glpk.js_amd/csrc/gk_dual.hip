@@ -2179,17 +2179,19 @@ void binv_ftran_list(hipStream_t s, const SpxDev &d, int nr, const double *x, do
 }
 
 // ---------------------------------------------------------------------------
-// eval_pi's residual and eval_cbar (glpspx02.js:426-495) by rows of AT, for
-// the dual with dense A: pi = inv(B)' cB vanishes outside the dense columns of
-// inv(B) (a basic slack c has pi_c = cB[bind[c]] = 0: row costs are 0), so
-// N_k' pi runs over the nr rows of AT in rlist instead of all m rows of A.
+// eval_pi's residual and eval_cbar (glpspx02.js:426-495, glpspx01.js:514-584)
+// by rows of AT, dense A: pi = inv(B)' cB vanishes outside the dense columns
+// of inv(B) and the basic slacks c with a nonzero cost (pi_c = cB[bind[c]]:
+// none in the dual, the primal's phase-I costs), so N_k' pi runs over those
+// rows of AT (rlist, then `extra`) instead of all m rows of A.
 // Block b owns the 64 variable slots [64 b, 64 b + 64) (structural column c
 // and slack row c); waves split the list rows, partial sums meet in LDS.
 //   CP_CBAR:  out[j] = coef[k] - N_k' pi for the non-basic position j of k
 //   CP_RESID: out[i] = h[i]   - N_k' pi for the basic position i of k
 // ---------------------------------------------------------------------------
 __global__ void __launch_bounds__(1024) k_rowpass_pi(SpxDev d, int mode, int nr, const double *__restrict__ pi,
-                                                     const double *__restrict__ h, double *__restrict__ out)
+                                                     const double *__restrict__ h, double *__restrict__ out,
+                                                     const int *__restrict__ extra, int nextra)
 {
     __shared__ double sp[16][64];
     const int m = d.m, n = d.n;
@@ -2217,6 +2219,10 @@ __global__ void __launch_bounds__(1024) k_rowpass_pi(SpxDev d, int mode, int nr,
         const int c = d.rlist[t];
         acc += pi[c] * col[(size_t)c * ldt];
     }
+    for (t = w; t < nextra; t += nw) {        // basic slacks with a cost (primal phase I)
+        const int c = extra[t];
+        acc += pi[c] * col[(size_t)c * ldt];
+    }
     sp[w][lane] = acc;
     __syncthreads();
     if (w != 0) return;
@@ -2234,11 +2240,12 @@ __global__ void __launch_bounds__(1024) k_rowpass_pi(SpxDev d, int mode, int nr,
     }
 }
 
-void rowpass_pi(hipStream_t s, const SpxDev &d, int mode, int nr, const double *pi, const double *h, double *out)
+void rowpass_pi(hipStream_t s, const SpxDev &d, int mode, int nr, const double *pi, const double *h, double *out,
+                const int *extra, int nextra)
 {
-    const int nw = nr <= 64 ? 4 : (nr <= 256 ? 8 : 16);
+    const int nw = nr + nextra <= 64 ? 4 : (nr + nextra <= 256 ? 8 : 16);
     hipLaunchKernelGGL(k_rowpass_pi, dim3(cdiv(std::max(d.m, d.n), 64)), dim3(64 * nw), 0, s, d, mode, nr, pi, h,
-                       out);
+                       out, extra, nextra);
 }
 
 void binv_btran_list(hipStream_t s, const SpxDev &d, int nr, const double *x, double *y)

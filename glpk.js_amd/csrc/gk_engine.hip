@@ -122,6 +122,7 @@ struct Engine {
     DBuf<int> rlist, rpos, rho_idx, wlist, wpos, awcnt;
     DBuf<double> rho_val, gpart, cand, awpart;
     DBuf<char> upstage;                         // device side of the coalesced uploads
+    DBuf<int> xlist;                            // eval_cbar: basic slacks with a nonzero cost (primal phase I)
     DBuf<unsigned long long> tslots;
     std::vector<GraphEntry> graphs;
     unsigned long long graph_clock = 0;
@@ -599,14 +600,17 @@ struct Spx {
     // y = inv(B) x / inv(B)' x: over the dense columns only in the dual path
     // (rlist maintained by the pivot kernels), all m columns otherwise
     static constexpr int LIST_FTRAN_MAX = 2048;
+    // rlist is exact in the dual always, in the primal unless a batch of the
+    // single-workgroup (rigorous) kernels ran since the last rebuild
+    bool lists_ok() const { return dual || !lists_stale; }
     void ftran_(const double *x, double *y)
     {
-        if (dual && hs.nr <= LIST_FTRAN_MAX) binv_ftran_list(s, dev(), hs.nr, x, y);
+        if (lists_ok() && hs.nr <= LIST_FTRAN_MAX) binv_ftran_list(s, dev(), hs.nr, x, y);
         else gemv_n(s, f->Binv.p, m, m, f->ldb, x, E->partial.p, PARTIAL_CAP, y, 1.0, nullptr, 0.0);
     }
     void btran_(const double *x, double *y)
     {
-        if (dual) binv_btran_list(s, dev(), hs.nr, x, y);
+        if (lists_ok()) binv_btran_list(s, dev(), hs.nr, x, y);
         else gemv_t(s, f->Binv.p, m, m, f->ldb, x, y, 1.0);
     }
     // eval_cbar (glpspx01.js:565): pi = inv(B') cB refined once, d_j = c_k - N_j' pi
@@ -619,14 +623,28 @@ struct Spx {
         double *cB = E->r1.p, *pi = E->u.p, *r = E->r2.p, *dd = E->work.p;
         cb_vector(s, m, E->head.p, E->coef.p, cB);
         btran_(cB, pi);
-        // dual, dense A: pi lives on the dense columns of inv(B) (row costs
-        // are 0), so the passes run over those rows of AT
-        const bool rows = dual && E->dense && A.AT && hs.nr <= LIST_FTRAN_MAX && 2 * hs.nr <= m;
-        if (rows) rowpass_pi(s, d, CP_RESID, hs.nr, pi, cB, r);
+        // dense A: pi = inv(B)' cB lives on the dense columns of inv(B) and
+        // the basic slacks with a nonzero cost (the primal's phase-I costs;
+        // none in the dual), so the passes run over those rows of AT
+        std::vector<int> extra;
+        if (!dual && E->dense && A.AT && lists_ok()) {
+            pull();
+            for (int i = 1; i <= m; i++)
+                if (head[i] <= m && coef[head[i]] != 0.0) extra.push_back(head[i] - 1);
+        }
+        const bool rows = E->dense && A.AT && lists_ok() && hs.nr <= LIST_FTRAN_MAX &&
+                          2 * (hs.nr + (int)extra.size()) <= m;
+        if (rows && !extra.empty()) {
+            E->xlist.ensure(extra.size());
+            HIPCHK(hipMemcpyAsync(E->xlist.p, extra.data(), extra.size() * sizeof(int), hipMemcpyHostToDevice, s));
+            sync();
+        }
+        const int nx = rows ? (int)extra.size() : 0;
+        if (rows) rowpass_pi(s, d, CP_RESID, hs.nr, pi, cB, r, E->xlist.p, nx);
         else colpass(s, A, CP_RESID, 0, m, E->head.p, E->stat.p, E->coef.p, cB, pi, nullptr, r, nullptr, nullptr);
         btran_(r, dd);
         vec_axpy(s, pi, dd, 1.0, m);
-        if (rows) rowpass_pi(s, d, CP_CBAR, hs.nr, pi, nullptr, E->cbar.p);
+        if (rows) rowpass_pi(s, d, CP_CBAR, hs.nr, pi, nullptr, E->cbar.p, E->xlist.p, nx);
         else colpass(s, A, CP_CBAR, m, n, E->head.p, E->stat.p, E->coef.p, nullptr, pi, nullptr, E->cbar.p, nullptr, nullptr);
         (void)d;
         down(cbar, E->cbar, n);

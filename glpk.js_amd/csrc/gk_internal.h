@@ -177,7 +177,8 @@ struct UpSeg {
 };
 void scatter_segments(hipStream_t s, const char *src, const UpSeg *segs, int nseg);
 // dual, dense A: CP_CBAR / CP_RESID of eval_cbar over the rows of AT in rlist
-void rowpass_pi(hipStream_t s, const SpxDev &d, int mode, int nr, const double *pi, const double *h, double *out);
+void rowpass_pi(hipStream_t s, const SpxDev &d, int mode, int nr, const double *pi, const double *h, double *out,
+                const int *extra, int nextra);
 // timing hook: the row-path pivot-row kernel alone (returns algorithmic bytes)
 double launch_trow_rows(hipStream_t s, const SpxDev &d, const DualPlan &pl, int ns);
 // y = inv(B) x and y = inv(B)' x over the nr dense columns of rlist and the
