@@ -245,3 +245,351 @@ def from_fixture(d: dict) -> Problem:
 def load_fixture(path: str) -> dict:
     with open(path) as f:
         return json.load(f)
+
+
+# ---------------------------------------------------------------------------
+# CPLEX LP format reader (glp_read_lp, glpcpx.js:10-753): the problem as the
+# reference builds it — columns in order of first appearance, column lists
+# sorted by row (glp_sort_matrix), bounds stored as glp_set_col_bnds stores
+# them, zero coefficients dropped, binaries as integer columns with 0-1 bounds
+# ---------------------------------------------------------------------------
+_LP_CHARSET = "!\"#$%&()/,.;?@_`'{}|~"
+_LP_KEYWORDS = {"minimize": "min", "minimum": "min", "min": "min", "maximize": "max", "maximum": "max",
+                "max": "max", "st": "st", "s.t.": "st", "st.": "st", "bounds": "bounds", "bound": "bounds",
+                "general": "gen", "generals": "gen", "gen": "gen", "integer": "int", "integers": "int",
+                "int": "int", "binary": "bin", "binaries": "bin", "bin": "bin", "end": "end"}
+
+
+class LpFormatError(ValueError):
+    pass
+
+
+def _lp_tokens(text: str):
+    """Tokens (kind, image, value, next_char, line) with glp_read_lp's rules:
+    keywords only at the start of a line, '\\' comments, '<', '<=', '=<', ..."""
+    s = text if text.endswith("\n") else text + "\n"
+    i, line, at_line_start = 0, 1, True
+    out = []
+    N = len(s)
+
+    def isname(ch):
+        return ch.isalnum() or ch in _LP_CHARSET
+
+    while True:
+        while i < N and s[i] != "\n" and s[i].isspace():
+            i += 1
+        if i >= N:
+            out.append(("eof", "", 0.0, "", line))
+            return out
+        ch = s[i]
+        if ch == "\n":
+            i += 1
+            line += 1
+            at_line_start = True
+            continue
+        if ch == "\\":
+            while i < N and s[i] != "\n":
+                i += 1
+            continue
+        start_of_line = at_line_start
+        at_line_start = False
+        if ch.isalpha() or (ch != "." and ch in _LP_CHARSET):
+            j = i
+            while j < N and isname(s[j]):
+                j += 1
+            img = s[i:j]
+            kind = "name"
+            if start_of_line:
+                low = img.lower()
+                if low in ("subject", "such"):
+                    k = j
+                    if k < N and s[k] == " ":
+                        k2 = k + 1
+                        want = "to" if low == "subject" else "that"
+                        if s[k2:k2 + len(want)].lower() == want and not (k2 + len(want) < N and s[k2 + len(want)].isalpha()):
+                            kind, img, j = "st", s[i:k2 + len(want)], k2 + len(want)
+                elif low in _LP_KEYWORDS:
+                    kind = _LP_KEYWORDS[low]
+            i = j
+            out.append((kind, img, 0.0, _lp_peek(s, i), line))
+            continue
+        if ch.isdigit() or ch == ".":
+            j = i
+            while j < N and s[j].isdigit():
+                j += 1
+            if j < N and s[j] == ".":
+                j += 1
+                if j - i == 1 and not (j < N and s[j].isdigit()):
+                    raise LpFormatError(f"{line}: invalid use of decimal point")
+                while j < N and s[j].isdigit():
+                    j += 1
+            if j < N and s[j] in "eE":
+                j += 1
+                if j < N and s[j] in "+-":
+                    j += 1
+                if not (j < N and s[j].isdigit()):
+                    raise LpFormatError(f"{line}: numeric constant `{s[i:j]}' incomplete")
+                while j < N and s[j].isdigit():
+                    j += 1
+            img = s[i:j]
+            i = j
+            out.append(("num", img, float(img), _lp_peek(s, i), line))
+            continue
+        if ch in "+-:":
+            i += 1
+            out.append(({"+": "plus", "-": "minus", ":": "colon"}[ch], ch, 0.0, _lp_peek(s, i), line))
+            continue
+        if ch in "<>=":
+            j = i + 1
+            kind = {"<": "le", ">": "ge", "=": "eq"}[ch]
+            if ch in "<>" and j < N and s[j] == "=":
+                j += 1
+            elif ch == "=" and j < N and s[j] in "<>":
+                kind = "le" if s[j] == "<" else "ge"
+                j += 1
+            img = s[i:j]
+            i = j
+            out.append((kind, img, 0.0, _lp_peek(s, i), line))
+            continue
+        raise LpFormatError(f"{line}: character `{ch}' not recognized")
+
+
+def _lp_peek(s: str, i: int) -> str:
+    """the next significant character after a token (blanks skipped), as
+    glp_read_lp sees csa.c after scan_token"""
+    while i < len(s) and s[i] != "\n" and s[i].isspace():
+        i += 1
+    return s[i] if i < len(s) else ""
+
+
+def read_lp(text: str) -> Problem:
+    """glp_read_lp (glpcpx.js:10) on the text of a CPLEX LP file."""
+    toks = _lp_tokens(text)
+    pos = 0
+    cols: dict[str, int] = {}
+    col_names: list[str] = []
+    lbs: list[float] = []
+    ubs: list[float] = []
+    obj: dict[int, float] = {}
+    isint: set[int] = set()
+    rows: list[tuple[list[int], list[float], int, float]] = []
+    BIG = 1.7976931348623157e308
+
+    def tok():
+        return toks[pos]
+
+    def nxt():
+        nonlocal pos
+        pos += 1
+
+    def err(msg):
+        raise LpFormatError(f"{tok()[4]}: {msg}")
+
+    def find_col(name):
+        if name not in cols:
+            cols[name] = len(col_names)
+            col_names.append(name)
+            lbs.append(+BIG)
+            ubs.append(-BIG)
+        return cols[name]
+
+    def linear_form():
+        ind, val, used = [], [], set()
+        while True:
+            s = 1.0
+            if tok()[0] in ("plus", "minus"):
+                s = 1.0 if tok()[0] == "plus" else -1.0
+                nxt()
+            coef = 1.0
+            if tok()[0] == "num":
+                coef = tok()[2]
+                nxt()
+            if tok()[0] != "name":
+                err("missing variable name")
+            j = find_col(tok()[1])
+            if j in used:
+                err(f"multiple use of variable `{tok()[1]}' not allowed")
+            used.add(j)
+            ind.append(j)
+            val.append(s * coef)
+            nxt()
+            if tok()[0] in ("plus", "minus"):
+                continue
+            keep = [(a, v) for a, v in zip(ind, val) if v != 0.0]
+            return [a for a, _ in keep], [v for _, v in keep]
+
+    # objective
+    if tok()[0] not in ("min", "max"):
+        err("`minimize' or `maximize' keyword missing")
+    direction = GLP_MIN if tok()[0] == "min" else GLP_MAX
+    nxt()
+    if tok()[0] == "name" and tok()[3] == ":":
+        nxt()
+        nxt()
+    ind, val = linear_form()
+    for a, v in zip(ind, val):
+        obj[a] = v
+    # constraints
+    if tok()[0] != "st":
+        err("constraints section missing")
+    nxt()
+    while True:
+        if tok()[0] == "name" and tok()[3] == ":":
+            nxt()
+            nxt()
+        ind, val = linear_form()
+        kind = tok()[0]
+        if kind == "le":
+            rtype = GLP_UP
+        elif kind == "ge":
+            rtype = GLP_LO
+        elif kind == "eq":
+            rtype = GLP_FX
+        else:
+            err("missing constraint sense")
+        nxt()
+        s = 1.0
+        if tok()[0] in ("plus", "minus"):
+            s = 1.0 if tok()[0] == "plus" else -1.0
+            nxt()
+        if tok()[0] != "num":
+            err("missing right-hand side")
+        rows.append((ind, val, rtype, s * tok()[2]))
+        if tok()[3] not in ("\n", ""):
+            err("invalid symbol(s) beyond right-hand side")
+        nxt()
+        if tok()[0] in ("plus", "minus", "num", "name"):
+            continue
+        break
+    # bounds
+    if tok()[0] == "bounds":
+        nxt()
+        while tok()[0] in ("plus", "minus", "num", "name"):
+            lb_flag, lb = False, 0.0
+            if tok()[0] in ("plus", "minus"):
+                s = 1.0 if tok()[0] == "plus" else -1.0
+                nxt()
+                lb_flag = True
+                if tok()[0] == "num":
+                    lb = s * tok()[2]
+                    nxt()
+                elif tok()[1].lower() in ("infinity", "inf"):
+                    if s > 0:
+                        err("invalid use of `+inf' as lower bound")
+                    lb = -BIG
+                    nxt()
+                else:
+                    err("missing lower bound")
+            elif tok()[0] == "num":
+                lb_flag, lb = True, tok()[2]
+                nxt()
+            if lb_flag:
+                if tok()[0] != "le":
+                    err("missing `<', `<=', or `=<' after lower bound")
+                nxt()
+            if tok()[0] != "name":
+                err("missing variable name")
+            j = find_col(tok()[1])
+            if lb_flag:
+                lbs[j] = lb
+            nxt()
+            k = tok()[0]
+            if k in ("le", "ge", "eq"):
+                if k != "le" and lb_flag:
+                    err("invalid bound definition")
+                nxt()
+                s = 1.0
+                signed = tok()[0] in ("plus", "minus")
+                if signed:
+                    s = 1.0 if tok()[0] == "plus" else -1.0
+                    nxt()
+                if tok()[0] == "num":
+                    v = s * tok()[2]
+                    if k == "le":
+                        ubs[j] = v
+                    elif k == "ge":
+                        lbs[j] = v
+                    else:
+                        lbs[j] = ubs[j] = v
+                    nxt()
+                elif signed and k == "le" and tok()[1].lower() in ("infinity", "inf"):
+                    if s < 0:
+                        err("invalid use of `-inf' as upper bound")
+                    ubs[j] = +BIG
+                    nxt()
+                elif signed and k == "ge" and (tok()[1].lower() == "infinity" or tok()[1].lower() != "inf"):
+                    # as the reference: any token but `inf' reads as infinity
+                    # after `>= -' (glpcpx.js:543, `the_same(...) == 0')
+                    if s > 0:
+                        err("invalid use of `+inf' as lower bound")
+                    lbs[j] = -BIG
+                    nxt()
+                elif k == "le":
+                    err("missing upper bound")
+                elif k == "ge":
+                    err("missing lower bound")
+                else:
+                    err("missing fixed value")
+            elif tok()[0] == "name" and tok()[1].lower() == "free":
+                if lb_flag:
+                    err("invalid bound definition")
+                lbs[j], ubs[j] = -BIG, +BIG
+                nxt()
+            elif not lb_flag:
+                err("invalid bound definition")
+    # general / integer / binary
+    while tok()[0] in ("gen", "int", "bin"):
+        binary = tok()[0] == "bin"
+        nxt()
+        while tok()[0] == "name":
+            j = find_col(tok()[1])
+            isint.add(j)
+            if binary:
+                lbs[j], ubs[j] = 0.0, 1.0
+            nxt()
+    if tok()[0] == "end":
+        nxt()
+    elif tok()[0] != "eof":
+        err(f"symbol {tok()[1]} in wrong position")
+    if tok()[0] != "eof":
+        err("extra symbol(s) detected beyond `end'")
+    # columns: bounds as glp_set_col_bnds stores them, statuses of non-basic columns
+    n, m = len(col_names), len(rows)
+    ctype, clb, cub, cstat = [], [], [], []
+    for j in range(n):
+        lb = 0.0 if lbs[j] == +BIG else lbs[j]
+        ub = +BIG if ubs[j] == -BIG else ubs[j]
+        if lb == -BIG and ub == +BIG:
+            t, l, u, st = GLP_FR, 0.0, 0.0, GLP_NF
+        elif ub == +BIG:
+            t, l, u, st = GLP_LO, lb, 0.0, GLP_NL
+        elif lb == -BIG:
+            t, l, u, st = GLP_UP, 0.0, ub, GLP_NU
+        elif lb != ub:
+            t, l, u, st = GLP_DB, lb, ub, GLP_NL
+        else:
+            t, l, u, st = GLP_FX, lb, ub, GLP_NS
+        ctype.append(t); clb.append(l); cub.append(u); cstat.append(st)
+    rtype, rlb, rub = [], [], []
+    for (_, _, t, rhs) in rows:
+        rtype.append(t)
+        rlb.append(0.0 if t == GLP_UP else rhs)
+        rub.append(0.0 if t == GLP_LO else rhs)
+    # column lists sorted by row (glp_sort_matrix)
+    entries = [[] for _ in range(n)]
+    for i, (ind, val, _, _) in enumerate(rows):
+        for a, v in zip(ind, val):
+            entries[a].append((i + 1, v))
+    A_ptr = np.zeros(n + 1, np.int32)
+    A_ind, A_val = [], []
+    for j in range(n):
+        for i, v in sorted(entries[j]):
+            A_ind.append(i)
+            A_val.append(v)
+        A_ptr[j + 1] = len(A_ind)
+    return Problem(m=m, n=n, dir=direction, c0=0.0,
+                   row_type=_i8(rtype), row_lb=_f8(rlb), row_ub=_f8(rub), rii=np.ones(m),
+                   row_stat=_i8(np.full(m, GLP_BS)), col_type=_i8(ctype), col_lb=_f8(clb), col_ub=_f8(cub),
+                   col_coef=_f8([obj.get(j, 0.0) for j in range(n)]), sjj=np.ones(n), col_stat=_i8(cstat),
+                   col_kind=_i8([GLP_IV if j in isint else GLP_CV for j in range(n)]), A_ptr=A_ptr,
+                   A_ind=_i4(A_ind), A_val=_f8(A_val), name="")

@@ -310,6 +310,39 @@ for (var ms = 1; ms <= 12; ms++) {
         mipCase('mixint' + ms, function () { return genMix(100 + ms, 6 + ms, 8 + 2 * ms, 0.5, true, true); }, null);
     })(ms);
 }
+// glp_read_lp on CPLEX LP texts exercising every section and bound form
+// (the Python reader problems.read_lp is pinned on these problem dumps; the
+// texts travel in the fixture, the error cases record the reference's message)
+function readCase(name, text) {
+    if (ONLY && ('lpread_' + name).indexOf(ONLY) !== 0) return;
+    var P = newProb(), d;
+    try {
+        glpk.glp_read_lp_from_string(P, null, text);
+        d = dumpProb(P, null);
+    } catch (e) {
+        d = {error: String(e.message)};
+    }
+    d.text = text;
+    fs.writeFileSync(path.join(OUT, 'lpread_' + name + '.json'), JSON.stringify(d));
+    console.log('wrote lpread', name, d.error || (d.m + 'x' + d.n));
+}
+readCase('sections', [
+    '\\ every bound form', 'Minimize', ' cost: 3 x + 2.5e-1 y - z + 0 w + 1e1 v', 'Subject To',
+    ' c1: x + y + z >= 2', ' c2: - x + 3 y <= -1.5', ' 2 z - w = 4', ' c4: v + x - 0 y >= -3', 'Bounds',
+    ' x <= 10', ' -5 <= y <= 5', ' z free', ' w >= -infinity', ' 0 <= v <= 0', ' q = 2', ' -inf <= r <= 7',
+    ' s >= 1', 'Generals', ' y', 'Binaries', ' b', 'End', ''].join('\n'));
+readCase('keywords', [
+    'maximize', ' obj: x1 + x2 + x3', 'such that', ' x1 + x2 <= 4', ' r2: x2 + x3 <= 3',
+    ' x1 + x3 =< 5', ' x3 => 0.5', 'bound', ' x1 <= 3', 'int', ' x2', 'end', ''].join('\n'));
+readCase('st_dot', ['MIN', ' a + b', 'S.T.', ' a - b >= -2', ' a + 2 b <= 6', 'END', ''].join('\n'));
+// the reference accepts any name but `inf' after `>= -' (glpcpx.js:543)
+readCase('ge_quirk', ['Minimize', ' x + y', 'Subject To', ' x + y >= 1', 'Bounds', ' x >= -foo', 'End', ''].join('\n'));
+readCase('err_geinf', ['Minimize', ' x + y', 'Subject To', ' x + y >= 1', 'Bounds', ' x >= -inf', 'End', ''].join('\n'));
+readCase('err_noobj', ['Subject To', ' x + y <= 1', 'End', ''].join('\n'));
+readCase('err_nost', ['Minimize', ' x + y', 'Bounds', ' x <= 1', 'End', ''].join('\n'));
+readCase('err_dupvar', ['Minimize', ' x + x', 'Subject To', ' x <= 1', 'End', ''].join('\n'));
+readCase('err_norhs', ['Minimize', ' x', 'Subject To', ' x <= y', 'End', ''].join('\n'));
+
 // node LPs beyond the node kernel's 64 KiB of LDS (gk_mip.hip, HBM work area)
 [[50, 80, 0.15], [60, 90, 0.15], [70, 100, 0.1], [48, 90, 0.35]].forEach(function (s, k) {
     mipCase('mixbig' + (k + 1), function () { return genMix(300 + k, s[0], s[1], 0.15, s[2], true, true); }, null);
