@@ -593,3 +593,255 @@ def read_lp(text: str) -> Problem:
                    col_coef=_f8([obj.get(j, 0.0) for j in range(n)]), sjj=np.ones(n), col_stat=_i8(cstat),
                    col_kind=_i8([GLP_IV if j in isint else GLP_CV for j in range(n)]), A_ptr=A_ptr,
                    A_ind=_i4(A_ind), A_val=_f8(A_val), name="")
+
+
+# ---------------------------------------------------------------------------
+# MPS reader (fixed or free format; SURVEY.md §8(f): the configs' netlib
+# 25fv47 and MIPLIB mas76 are MPS files, which the reference cannot read).
+# Conventions of GLPK's glp_read_mps (glpmps.c, GLPK 4.49): rows in ROWS
+# order (the first N row is the objective, other N rows are dropped), columns
+# in COLUMNS order, RHS on the objective row = minus the constant term, RANGES
+# per row type, BOUNDS types UP/LO/FX/FR/MI/PL/BV/LI/UI (UP with a negative
+# value and no lower bound makes the lower bound -inf), integer columns from
+# MARKER INTORG / INTEND keep the default bounds [0, +inf); column lists
+# sorted by row.  Parity is by content: the same LP written in CPLEX LP form
+# reads to the same problem (tests/test_readers.py).
+# ---------------------------------------------------------------------------
+class MpsFormatError(ValueError):
+    pass
+
+
+def read_mps(text: str, free: bool = True) -> Problem:
+    BIG = 1.7976931348623157e308
+    section = None
+    rows: dict[str, int] = {}
+    row_names: list[str] = []
+    row_kind: list[str] = []
+    obj_name = None
+    cols: dict[str, int] = {}
+    col_int: list[bool] = []
+    entries: list[list[tuple[int, float]]] = []
+    coef: list[float] = []
+    rhs: dict[int, float] = {}
+    rng: dict[int, float] = {}
+    lbs: list[float] = []
+    ubs: list[float] = []
+    seen_lb: list[bool] = []
+    seen_ub: list[bool] = []
+    c0 = 0.0
+    in_int = False
+    direction = GLP_MIN
+
+    def fields(line: str) -> list[str]:
+        if free:
+            return line.split()
+        # fixed MPS: columns 2-3, 5-12, 15-22, 25-36, 40-47, 50-61
+        spans = ((1, 3), (4, 12), (14, 22), (24, 36), (39, 47), (49, 61))
+        out = [line[a:b].strip() for a, b in spans]
+        while out and out[-1] == "":
+            out.pop()
+        if out and out[0] == "" and section not in ("ROWS", "BOUNDS"):
+            out.pop(0)          # the blank type field of COLUMNS/RHS/RANGES
+        return out
+
+    for ln, raw in enumerate(text.splitlines(), 1):
+        if not raw.strip() or raw.startswith("*"):
+            continue
+        if not raw[0].isspace():
+            head = raw.split()
+            section = head[0].upper()
+            if section == "OBJSENSE" and len(head) > 1:
+                direction = GLP_MAX if head[1].upper().startswith("MAX") else GLP_MIN
+            if section == "ENDATA":
+                break
+            continue
+        f = fields(raw)
+        if section == "OBJSENSE":
+            direction = GLP_MAX if f[0].upper().startswith("MAX") else GLP_MIN
+        elif section == "ROWS":
+            kind, name = f[0].upper(), f[1]
+            if kind == "N":
+                if obj_name is None:
+                    obj_name = name
+                continue
+            if kind not in ("L", "G", "E"):
+                raise MpsFormatError(f"{ln}: row type `{kind}' not recognized")
+            rows[name] = len(row_names)
+            row_names.append(name)
+            row_kind.append(kind)
+        elif section == "COLUMNS":
+            if len(f) >= 3 and f[1].upper() == "'MARKER'":
+                tag = f[-1].upper()
+                in_int = tag == "'INTORG'"
+                continue
+            name = f[0]
+            if name not in cols:
+                cols[name] = len(entries)
+                entries.append([])
+                coef.append(0.0)
+                col_int.append(in_int)
+                lbs.append(0.0); ubs.append(+BIG); seen_lb.append(False); seen_ub.append(False)
+            j = cols[name]
+            for k in range(1, len(f) - 1, 2):
+                rname, v = f[k], float(f[k + 1])
+                if rname == obj_name:
+                    coef[j] = v
+                elif rname in rows:
+                    if v != 0.0:
+                        entries[j].append((rows[rname] + 1, v))
+                else:
+                    raise MpsFormatError(f"{ln}: row `{rname}' not found")
+        elif section in ("RHS", "RANGES"):
+            start = 1 if len(f) % 2 == 1 else 0
+            for k in range(start, len(f) - 1, 2):
+                rname, v = f[k], float(f[k + 1])
+                if rname == obj_name and section == "RHS":
+                    c0 = -v
+                elif rname in rows:
+                    (rhs if section == "RHS" else rng)[rows[rname]] = v
+                else:
+                    raise MpsFormatError(f"{ln}: row `{rname}' not found")
+        elif section == "BOUNDS":
+            kind = f[0].upper()
+            name = f[2] if len(f) >= 3 else f[1]
+            v = float(f[3]) if len(f) >= 4 else 0.0
+            if name not in cols:
+                raise MpsFormatError(f"{ln}: column `{name}' not found")
+            j = cols[name]
+            if kind == "UP":
+                ubs[j] = v
+                if v < 0.0 and not seen_lb[j]:
+                    lbs[j] = -BIG
+                seen_ub[j] = True
+            elif kind in ("LO", "LI"):
+                lbs[j] = v
+                seen_lb[j] = True
+                if kind == "LI":
+                    col_int[j] = True
+            elif kind == "UI":
+                ubs[j] = v
+                col_int[j] = True
+                seen_ub[j] = True
+            elif kind == "FX":
+                lbs[j] = ubs[j] = v
+                seen_lb[j] = seen_ub[j] = True
+            elif kind == "FR":
+                lbs[j], ubs[j] = -BIG, +BIG
+            elif kind == "MI":
+                lbs[j] = -BIG
+            elif kind == "PL":
+                ubs[j] = +BIG
+            elif kind == "BV":
+                lbs[j], ubs[j] = 0.0, 1.0
+                col_int[j] = True
+            else:
+                raise MpsFormatError(f"{ln}: bound type `{kind}' not recognized")
+        elif section in ("NAME",):
+            continue
+        else:
+            raise MpsFormatError(f"{ln}: data line outside a known section")
+    m, n = len(row_names), len(entries)
+    rtype, rlb, rub = [], [], []
+    for i in range(m):
+        b = rhs.get(i, 0.0)
+        kind = row_kind[i]
+        if i in rng:
+            r = rng[i]
+            if kind == "E":
+                lo, hi = (b, b + abs(r)) if r >= 0.0 else (b - abs(r), b)
+            elif kind == "L":
+                lo, hi = b - abs(r), b
+            else:
+                lo, hi = b, b + abs(r)
+            t = GLP_FX if lo == hi else GLP_DB
+        elif kind == "L":
+            t, lo, hi = GLP_UP, 0.0, b
+        elif kind == "G":
+            t, lo, hi = GLP_LO, b, 0.0
+        else:
+            t, lo, hi = GLP_FX, b, b
+        rtype.append(t); rlb.append(lo); rub.append(hi)
+    ctype, clb, cub, cstat = [], [], [], []
+    for j in range(n):
+        lb, ub = lbs[j], ubs[j]
+        if lb == -BIG and ub == +BIG:
+            t, l, u, st = GLP_FR, 0.0, 0.0, GLP_NF
+        elif ub == +BIG:
+            t, l, u, st = GLP_LO, lb, 0.0, GLP_NL
+        elif lb == -BIG:
+            t, l, u, st = GLP_UP, 0.0, ub, GLP_NU
+        elif lb != ub:
+            t, l, u, st = GLP_DB, lb, ub, GLP_NL
+        else:
+            t, l, u, st = GLP_FX, lb, ub, GLP_NS
+        ctype.append(t); clb.append(l); cub.append(u); cstat.append(st)
+    A_ptr = np.zeros(n + 1, np.int32)
+    A_ind, A_val = [], []
+    for j in range(n):
+        for i, v in sorted(entries[j]):
+            A_ind.append(i)
+            A_val.append(v)
+        A_ptr[j + 1] = len(A_ind)
+    return Problem(m=m, n=n, dir=direction, c0=c0,
+                   row_type=_i8(rtype), row_lb=_f8(rlb), row_ub=_f8(rub), rii=np.ones(m),
+                   row_stat=_i8(np.full(m, GLP_BS)), col_type=_i8(ctype), col_lb=_f8(clb), col_ub=_f8(cub),
+                   col_coef=_f8(coef), sjj=np.ones(n), col_stat=_i8(cstat),
+                   col_kind=_i8([GLP_IV if t else GLP_CV for t in col_int]), A_ptr=A_ptr,
+                   A_ind=_i4(A_ind), A_val=_f8(A_val), name="")
+
+
+def write_mps(p: Problem) -> str:
+    """Free MPS text of a Problem (the inverse of read_mps, unscaled data)."""
+    def _num(v) -> str:
+        return repr(float(v))
+
+    out = ["NAME " + (p.name or "problem")]
+    if p.dir == GLP_MAX:
+        out += ["OBJSENSE", "    MAX"]
+    out += ["ROWS", " N obj"]
+    kind = {GLP_UP: "L", GLP_LO: "G", GLP_FX: "E", GLP_DB: "L", GLP_FR: "N"}
+    for i in range(p.m):
+        if p.row_type[i] == GLP_FR:
+            raise ValueError("free rows are not written")
+        out.append(f" {kind[int(p.row_type[i])]} r{i + 1}")
+    out.append("COLUMNS")
+    in_int = False
+    for j in range(p.n):
+        isint = p.col_kind[j] == GLP_IV
+        if isint != in_int:
+            out.append("    MARKER 'MARKER' " + ("'INTORG'" if isint else "'INTEND'"))
+            in_int = isint
+        if p.col_coef[j] != 0.0:
+            out.append(f"    c{j + 1} obj {_num(p.col_coef[j])}")
+        for t in range(p.A_ptr[j], p.A_ptr[j + 1]):
+            out.append(f"    c{j + 1} r{p.A_ind[t]} {_num(p.A_val[t])}")
+    if in_int:
+        out.append("    MARKER 'MARKER' 'INTEND'")
+    out.append("RHS")
+    if p.c0 != 0.0:
+        out.append(f"    RHS obj {_num(-p.c0)}")
+    for i in range(p.m):
+        t = int(p.row_type[i])
+        b = p.row_ub[i] if t in (GLP_UP, GLP_DB) else p.row_lb[i]
+        if b != 0.0:
+            out.append(f"    RHS r{i + 1} {_num(b)}")
+    rng = [f"    RNG r{i + 1} {_num(p.row_ub[i] - p.row_lb[i])}" for i in range(p.m) if p.row_type[i] == GLP_DB]
+    if rng:
+        out += ["RANGES"] + rng
+    out.append("BOUNDS")
+    for j in range(p.n):
+        t, lb, ub = int(p.col_type[j]), p.col_lb[j], p.col_ub[j]
+        c = f"c{j + 1}"
+        if t == GLP_FR:
+            out.append(f" FR BND {c}")
+        elif t == GLP_LO:
+            if lb != 0.0:
+                out.append(f" LO BND {c} {_num(lb)}")
+        elif t == GLP_UP:
+            out += [f" MI BND {c}", f" UP BND {c} {_num(ub)}"]
+        elif t == GLP_DB:
+            out += [f" LO BND {c} {_num(lb)}", f" UP BND {c} {_num(ub)}"]
+        else:
+            out.append(f" FX BND {c} {_num(lb)}")
+    out.append("ENDATA")
+    return "\n".join(out) + "\n"
