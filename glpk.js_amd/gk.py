@@ -101,7 +101,8 @@ _lib = None
 EXPORTS = ["gk_abi_version", "gk_device_count", "gk_ctx_create", "gk_ctx_destroy", "gk_last_error",
            "gk_bfd_create", "gk_bfd_destroy", "gk_bfd_set_parm", "gk_bfd_factorize", "gk_bfd_factorize_csc",
            "gk_bfd_ftran", "gk_bfd_btran", "gk_bfd_update", "gk_bfd_get_count", "gk_bfd_valid",
-           "gk_spx_primal", "gk_spx_dual", "gk_bfd_last_stats", "gk_bfd_profile", "gk_ios_driver"]
+           "gk_spx_primal", "gk_spx_dual", "gk_bfd_last_stats", "gk_bfd_profile", "gk_ios_driver",
+           "gk_scale_prob", "gk_scale_prob_timed"]
 
 
 def load_library(path: str = LIB_PATH):
@@ -150,6 +151,10 @@ def load_library(path: str = LIB_PATH):
     L.gk_bfd_trace.restype = C.c_int
     L.gk_bfd_time_kernel.argtypes = [P, C.c_int, C.c_int, C.POINTER(C.c_double)]
     L.gk_bfd_time_kernel.restype = C.c_double
+    L.gk_scale_prob.argtypes = [P, C.c_int, C.c_int, P, P, P, C.c_int, P, P, P]
+    L.gk_scale_prob.restype = C.c_int
+    L.gk_scale_prob_timed.argtypes = [P, C.c_int, C.c_int, P, P, P, C.c_int, P, P, P, P, P]
+    L.gk_scale_prob_timed.restype = C.c_int
     _lib = L
     return L
 
@@ -608,3 +613,126 @@ def glp_intopt(P: GkProblem, parm: Iocp | None = None, comm=None) -> int:
     P.mip_stats = dict(lp_solves=int(comm.total(mip.lp_solves)), nodes_created=int(comm.total(mip.nodes_created)),
                        pivots=int(comm.total(mip.pivots)), local_lp_solves=mip.lp_solves)
     return ret
+
+
+# ---------------------------------------------------------------------------
+# glp_scale_prob (glpscl.js:1-225) — the factors come from the device
+# (gk_scale_prob, gk_scale.hip); the host validates the flags, prints the
+# reference's report lines and stores the factors like glp_set_rii /
+# glp_set_sjj (glpapi04.js:1-28).
+# ---------------------------------------------------------------------------
+GLP_SF_GM, GLP_SF_EQ, GLP_SF_2N, GLP_SF_SKIP, GLP_SF_AUTO = 0x01, 0x10, 0x20, 0x40, 0x80
+
+_print_func = None
+
+
+def glp_set_print_func(f) -> None:
+    """The reference's glp_set_print_func: every xprintf line goes to f (None:
+    stdout)."""
+    global _print_func
+    _print_func = f
+
+
+def _xprintf(s: str) -> None:
+    if _print_func is not None:
+        _print_func(s)
+    else:
+        print(s)
+
+
+def _js_num(x: float) -> str:
+    """A double as JavaScript's Number.prototype.toString prints it (the
+    shortest round-trip digits, JS's choice between plain and exponent form)."""
+    x = float(x)
+    if x != x:
+        return "NaN"
+    if x in (float("inf"), float("-inf")):
+        return "Infinity" if x > 0 else "-Infinity"
+    if x == 0.0:
+        return "0"
+    sign = "-" if x < 0 else ""
+    r = repr(abs(x))
+    mant, _, exp = r.partition("e")
+    e10 = int(exp) if exp else 0
+    ip, _, fp = mant.partition(".")
+    if fp == "0":
+        fp = ""
+    digits = (ip + fp).lstrip("0")
+    lead_zeros = len(ip + fp) - len((ip + fp).lstrip("0"))
+    nexp = len(ip) + e10 - lead_zeros          # value = 0.digits * 10^nexp
+    digits = digits.rstrip("0")
+    k = len(digits)
+    if k <= nexp <= 21:
+        out = digits + "0" * (nexp - k)
+    elif 0 < nexp <= 21:
+        out = digits[:nexp] + "." + digits[nexp:]
+    elif -6 < nexp <= 0:
+        out = "0." + "0" * (-nexp) + digits
+    else:
+        e = nexp - 1
+        out = digits[0] + ("." + digits[1:] if k > 1 else "") + "e" + ("+" if e > 0 else "-") + str(abs(e))
+    return sign + out
+
+
+class ScaleError(ValueError):
+    """glp_scale_prob's xerror."""
+
+
+def glp_scale_prob(P: GkProblem, flags: int) -> dict:
+    """glp_scale_prob(lp, flags) (glpscl.js:215-225): the factors on the
+    device, the report lines through the print function; returns the stage
+    numbers {stage: (min, max, ratio)}."""
+    flags = int(flags)
+    if flags & ~(GLP_SF_GM | GLP_SF_EQ | GLP_SF_2N | GLP_SF_SKIP | GLP_SF_AUTO):
+        raise ScaleError(f"glp_scale_prob: flags = {flags}; invalid scaling options")
+    m, n = P.m, P.n
+    ptr = np.ascontiguousarray(np.asarray(P.p.A_ptr, np.int32))
+    ind = np.ascontiguousarray(np.asarray(P.p.A_ind, np.int32))
+    val = np.ascontiguousarray(np.asarray(P.p.A_val, np.float64))
+    rii, sjj, rep = np.ones(max(m, 1)), np.ones(max(n, 1)), np.zeros(13)
+    f = lambda a: a.ctypes.data_as(C.c_void_p)  # noqa: E731
+    ret = P.L.gk_scale_prob(P.ctx.h, m, n, f(ptr), f(ind), f(val), flags, f(rii), f(sjj), f(rep))
+    if ret == 1:
+        raise ScaleError(f"glp_scale_prob: flags = {flags}; invalid scaling options")
+    if ret != 0:
+        raise GkError(_err(P.L))
+    bits = int(rep[12])
+    _xprintf("Scaling...")
+    stages = {}
+
+    def line(tag, k):
+        mn, mx, ratio = rep[3 * k: 3 * k + 3]
+        stages[tag.strip()] = (mn, mx, ratio)
+        _xprintf(f"{tag}: min|aij| = {_js_num(mn)}  max|aij| = {_js_num(mx)}  ratio = {_js_num(ratio)}")
+
+    line(" A", 0)
+    if bits & 1:
+        _xprintf("Problem data seem to be well scaled")
+    if not bits & 16:
+        if bits & 2:
+            line("GM", 1)
+        if bits & 4:
+            line("EQ", 2)
+        if bits & 8:
+            line("2N", 3)
+    # glp_set_rii / glp_set_sjj: a change of a factor invalidates the basis
+    # factorization when it touches a basic column (glpapi04.js:6-13, :23-26)
+    old_r, old_s = P.rii[1:m + 1].copy(), P.sjj[1:n + 1].copy()
+    new_r, new_s = rii[:m], sjj[:n]
+    if P.valid:
+        ch_r = (old_r != 1.0) | (new_r != 1.0)
+        ch_s = (old_s != 1.0) | (new_s != 1.0)
+        basic_c = np.asarray(P.col_stat[1:n + 1]) == GLP_BS
+        if np.any(ch_s & basic_c):
+            P.valid = 0
+        elif np.any(ch_r):
+            cols = np.repeat(np.arange(n), np.diff(ptr))
+            rows = ind - 1
+            if np.any(ch_r[rows] & basic_c[cols]):
+                P.valid = 0
+    P.rii[1:m + 1] = new_r
+    P.sjj[1:n + 1] = new_s
+    P.p.rii = new_r.copy()
+    P.p.sjj = new_s.copy()
+    P.touch_matrix()                              # the device copy of A is scaled: re-upload
+    return stages

@@ -207,6 +207,22 @@ typedef struct {
 } gk_ios_shard;
 int gk_ios_driver_sharded(gk_ctx *ctx, gk_mip *mip, const gk_iocp *parm, const gk_ios_shard *shard);
 
+/* glp_scale_prob (glpscl.js:1-225) on the device: the
+ * row and column scale factors of A (CSC: ptr[0..n] 0-based offsets, ind[]
+ * 1-based row numbers, val[]) after glp_unscale_prob and the flags'
+ * geometric-mean / equilibration / power-of-two steps, bit-identical to the
+ * reference.  rii[m], sjj[n] receive the factors; report[13] receives
+ * (min|aij|, max|aij|, ratio) after the stages A, GM, EQ, 2N (the numbers
+ * the reference prints) and report[12] the stage bits (1 well scaled, 2 GM,
+ * 4 EQ, 8 2N, 16 skipped as well scaled).  Returns 0, 1 for invalid flags
+ * (the reference's xerror "invalid scaling options"), or GK_EABI. */
+int gk_scale_prob(gk_ctx *ctx, int m, int n, const int *ptr, const int *ind, const double *val, int flags,
+                  double *rii, double *sjj, double *report);
+/* the same, also returning the device time of the sweeps (ms, HIP events)
+ * and their algorithmic bytes (bench.py) */
+int gk_scale_prob_timed(gk_ctx *ctx, int m, int n, const int *ptr, const int *ind, const double *val, int flags,
+                        double *rii, double *sjj, double *report, double *sweep_ms, double *sweep_bytes);
+
 #ifdef __cplusplus
 }
 #endif

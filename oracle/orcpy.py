@@ -73,6 +73,8 @@ def lib():
         L.orc_prob_ftran.argtypes = [P, f8p, C.c_int]
         L.orc_prob_set_bfcp.argtypes = [P, C.c_int, C.c_int, C.c_int]
         L.orc_last_error.restype = C.c_char_p
+        L.orc_scale_prob.argtypes = [C.c_int, C.c_int, i4p, i4p, f8p, C.c_int, f8p, f8p, f8p]
+        L.orc_scale_prob.restype = C.c_int
         if hasattr(L, "orc_prob_intopt"):
             L.orc_prob_intopt.argtypes = [P, C.POINTER(IocpFlat), C.POINTER(IosStats)]
             L.orc_prob_intopt.restype = C.c_int
@@ -148,3 +150,12 @@ class OracleProb:
         out = {k: getattr(r, k) for k, _ in ResultFlat._fields_}
         out.update(a)
         return out
+
+
+def scale_prob(m: int, n: int, A_ptr, A_ind, A_val, flags: int):
+    """glp_scale_prob restated (oracle/scale.c): (ret, rii[m], sjj[n],
+    report[13]) for the CSC matrix (0-based offsets, 1-based rows)."""
+    rii, sjj, rep = np.ones(max(m, 1)), np.ones(max(n, 1)), np.zeros(13)
+    ret = lib().orc_scale_prob(m, n, np.ascontiguousarray(A_ptr, np.int32), np.ascontiguousarray(A_ind, np.int32),
+                               np.ascontiguousarray(A_val, np.float64), int(flags), rii, sjj, rep)
+    return ret, rii[:m], sjj[:n], rep

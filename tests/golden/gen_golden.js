@@ -352,3 +352,62 @@ if (BIG) {
     lpCase('dense_512x2048', function () { return genDense(512, 2048, 42); }, {kind: 'dense', m: 512, n: 2048, seed: 42}, [1, 3], 0);
     mipCase('c5s_12x30', function () { return genC5s(12, 30, 42); }, {kind: 'c5s', m: 12, n: 30, seed: 42});
 }
+
+// ---- glp_scale_prob (glpscl.js:1): scale factors and printed lines ---------
+// badly scaled sparse matrix with an empty row and an empty column
+function genBadScale(seed, m, n, dens) {
+    var r = new SplitMix(seed), P = newProb(), i, j;
+    glpk.glp_add_rows(P, m); glpk.glp_add_cols(P, n);
+    var ia = [0], ja = [0], ar = [0];
+    for (i = 1; i <= m; i++) {
+        if (i === 3) continue;
+        for (j = 1; j <= n; j++) {
+            if (j === 5 || r.u() >= dens) continue;
+            var k = Math.floor(r.u() * 11) - 5;
+            ia.push(i); ja.push(j); ar.push((r.u() < 0.5 ? -1 : 1) * Math.pow(10, k) * (1 + r.u()));
+        }
+    }
+    glpk.glp_load_matrix(P, ia.length - 1, ia, ja, ar);
+    return P;
+}
+function genWellScaled(seed, m, n) {
+    var r = new SplitMix(seed), P = newProb(), i, j;
+    glpk.glp_add_rows(P, m); glpk.glp_add_cols(P, n);
+    var ia = [0], ja = [0], ar = [0];
+    for (i = 1; i <= m; i++)
+        for (j = 1; j <= n; j++)
+            if (r.u() < 0.3) { ia.push(i); ja.push(j); ar.push(0.5 + 1.5 * r.u()); }
+    glpk.glp_load_matrix(P, ia.length - 1, ia, ja, ar);
+    return P;
+}
+var SCALE_FLAGS = [0, 0x01, 0x10, 0x20, 0x11, 0x31, 0x71, 0x80, 0x40, 0x21, 0x200];
+function scaleCase(name, mk) {
+    if (ONLY && ('scale_' + name).indexOf(ONLY) !== 0) return;
+    var d = dumpProb(mk(), null);
+    d.name = name; d.kind = 'scale'; d.runs = [];
+    SCALE_FLAGS.forEach(function (flags) {
+        var P = mk(), lines = [], run = {flags: flags};
+        glpk.glp_set_print_func(function (s) { lines.push(s); });
+        try {
+            glpk.glp_scale_prob(P, flags);
+            var i, j;
+            run.rii = []; run.sjj = [];
+            for (i = 1; i <= P.m; i++) run.rii.push(P.row[i].rii);
+            for (j = 1; j <= P.n; j++) run.sjj.push(P.col[j].sjj);
+        } catch (e) {
+            run.error = String(e.message);
+        }
+        glpk.glp_set_print_func(function () {});
+        run.lines = lines;
+        d.runs.push(run);
+    });
+    fs.writeFileSync(path.join(OUT, 'scale_' + name + '.json'), JSON.stringify(d));
+    console.log('wrote scale', name, d.m + 'x' + d.n);
+}
+scaleCase('test', function () { return readLp('test.lpt'); });
+scaleCase('todd', function () { return readLp('todd.lpt'); });
+scaleCase('gap', function () { return readLp('gap.lpt'); });
+scaleCase('bad', function () { return genBadScale(77, 40, 60, 0.2); });
+scaleCase('well', function () { return genWellScaled(78, 20, 30); });
+scaleCase('dense_64x256', function () { return genDense(64, 256, 42); });
+scaleCase('c2s', function () { return genC2s(821, 1571, 7, 42); });
