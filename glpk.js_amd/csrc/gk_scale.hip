@@ -6,7 +6,7 @@
 // min / max over a row or a column of |a_ij| * (r_i * s_j), a product or
 // quotient of two of them, or a square root — all exactly rounded and, for
 // min / max, independent of the order of the entries — so the device result
-// is the reference's bit for bit (tests/test_gpu_scale.py against the
+// is the reference's bit for bit (tests/test_scale.py against the
 // reference's own factors, tests/golden/scale_*.json).
 //
 // Layout: A arrives by columns (the boundary's CSC); the row sweeps need it
@@ -78,28 +78,42 @@ __global__ void __launch_bounds__(256) k_scl_sweep(int lines, const int *__restr
     const int beg = ptr[line], end = ptr[line + 1];
     const double o = own[line];
     double lo = DBL_MAX * 2.0, hi = 0.0;
-    int t = beg + lane;
-    for (; t + 192 < end; t += 256) {
-        double v[4];
-        int c[4];
+    // software-pipelined: the next group's values and indices load while
+    // this group's gathers of the other factor are in flight
+    constexpr int U = 8;
+    if (end > beg) {
+        const int last = end - 1;
+        double v[U];
+        int c[U];
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
-            v[u] = val[t + 64 * u];
-            c[u] = idx[t + 64 * u];
+        for (int u = 0; u < U; ++u) {
+            const int tt = min(beg + lane + 64 * u, last);
+            v[u] = val[tt];
+            c[u] = idx[tt];
         }
+        for (int t = beg + lane; t - lane < end; t += 64 * U) {
+            double g[U], v2[U];
+            int c2[U];
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
-            const int k = ROWS ? c[u] : c[u] - 1;       // rows hold 0-based columns, A 1-based rows
-            const double temp = ROWS ? fabs(v[u]) * (o * other[k]) : fabs(v[u]) * (other[k] * o);
-            lo = fmin(lo, temp);
-            hi = fmax(hi, temp);
+            for (int u = 0; u < U; ++u) g[u] = other[ROWS ? c[u] : c[u] - 1];
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const int tt = min(t + 64 * (U + u), last);
+                v2[u] = val[tt];
+                c2[u] = idx[tt];
+            }
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                // rows: |a| (r_i s_j); columns: |a| (r_i s_j) with own = s_j
+                const double temp = ROWS ? fabs(v[u]) * (o * g[u]) : fabs(v[u]) * (g[u] * o);
+                if (t + 64 * u < end) {
+                    lo = fmin(lo, temp);
+                    hi = fmax(hi, temp);
+                }
+                v[u] = v2[u];
+                c[u] = c2[u];
+            }
         }
-    }
-    for (; t < end; t += 64) {
-        const int k = ROWS ? idx[t] : idx[t] - 1;
-        const double temp = ROWS ? fabs(val[t]) * (o * other[k]) : fabs(val[t]) * (other[k] * o);
-        lo = fmin(lo, temp);
-        hi = fmax(hi, temp);
     }
     lo = wmin_d(lo);
     hi = wmax_d(hi);

@@ -407,6 +407,29 @@ static napi_value js_stats(napi_env env, napi_callback_info info)
     return o;
 }
 
+/* scale(ctx, m, n, ptr, ind, val, flags, rii, sjj, report) -> 0 | 1 (bad flags) */
+static napi_value js_scale(napi_env env, napi_callback_info info)
+{
+    napi_value argv[10];
+    if (!get_args(env, info, 10, argv)) return NULL;
+    gk_ctx *c = (gk_ctx *)get_ext(env, argv[0]);
+    int m = 0, n = 0, flags = 0;
+    CHECK(napi_get_value_int32(env, argv[1], &m));
+    CHECK(napi_get_value_int32(env, argv[2], &n));
+    CHECK(napi_get_value_int32(env, argv[6], &flags));
+    const int *ptr = (const int *)ta(env, argv[3]);
+    const int *ind = (const int *)ta(env, argv[4]);
+    const double *val = (const double *)ta(env, argv[5]);
+    double *rii = (double *)ta(env, argv[7]), *sjj = (double *)ta(env, argv[8]), *rep = (double *)ta(env, argv[9]);
+    if (!c || !ptr || !ind || !val || !rii || !sjj || !rep) {
+        napi_throw_type_error(env, NULL, "scale: ptr/ind Int32Array, val/rii/sjj/report Float64Array");
+        return NULL;
+    }
+    int ret = gk_scale_prob(c, m, n, ptr, ind, val, flags, rii, sjj, rep);
+    if (ret == GK_EABI) return throw_gk(env, "scale_prob");
+    return mk_int(env, ret);
+}
+
 #define FN(name, f) { name, NULL, f, NULL, NULL, NULL, napi_enumerable, NULL }
 
 static napi_value init(napi_env env, napi_value exports)
@@ -416,7 +439,7 @@ static napi_value init(napi_env env, napi_value exports)
         FN("lastError", js_last_error), FN("bfdCreate", js_bfd_create), FN("bfdSetParm", js_bfd_set_parm),
         FN("bfdFactorizeCsc", js_bfd_factorize_csc), FN("bfdFtran", js_bfd_ftran), FN("bfdBtran", js_bfd_btran),
         FN("bfdUpdate", js_bfd_update), FN("bfdGetCount", js_bfd_get_count), FN("bfdValid", js_bfd_valid),
-        FN("spx", js_spx), FN("ios", js_ios), FN("stats", js_stats),
+        FN("spx", js_spx), FN("ios", js_ios), FN("stats", js_stats), FN("scale", js_scale),
     };
     napi_define_properties(env, exports, sizeof d / sizeof d[0], d);
     return exports;

@@ -215,3 +215,18 @@ module.exports = {
     bfdFtran: bfdFtran, bfdBtran: bfdBtran, bfdUpdate: bfdUpdate, bfdGetCount: bfdGetCount,
     spx: spx, iosDriver: iosDriver, nativeIos: nativeIos, GLP_BS: GLP_BS
 };
+
+// ---- glp_scale_prob (glpscl.js:1) -------------------------------------------
+// A by columns in list order (the row numbers of the aij elements), the
+// factors and the report numbers from the device (gk_scale_prob)
+function scaleProb(lp, flags) {
+    var m = lp.m, n = lp.n, ptr = new Int32Array(n + 1), ind = [], val = [];
+    for (var j = 1; j <= n; j++) {
+        for (var a = lp.col[j].ptr; a != null; a = a.c_next) { ind.push(a.row.i); val.push(a.val); }
+        ptr[j] = ind.length;
+    }
+    var rii = new Float64Array(Math.max(m, 1)), sjj = new Float64Array(Math.max(n, 1)), rep = new Float64Array(13);
+    var ret = addon.scale(context(), m, n, ptr, Int32Array.from(ind), Float64Array.from(val), flags | 0, rii, sjj, rep);
+    return {ret: ret, rii: rii, sjj: sjj, report: rep};
+}
+module.exports.scaleProb = scaleProb;

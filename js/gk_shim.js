@@ -21,6 +21,30 @@ bfd_get_count = function (bfd) { return __gk.bfdGetCount(bfd); };
 var __gk_js_ios_driver = ios_driver;
 ios_driver = function (T) { return __gk.nativeIos(T) ? __gk.iosDriver(T) : __gk_js_ios_driver(T); };
 
+// glp_scale_prob (glpscl.js:215-225): the factors from the device, the
+// reference's report lines through its own xprintf, the factors stored
+// through its own glp_unscale_prob / glp_set_rii / glp_set_sjj (which keep
+// the basis-invalidation rules of glpapi04.js:1-28)
+glp_scale_prob = exports["glp_scale_prob"] = function (lp, flags) {
+    if (flags & ~(GLP_SF_GM | GLP_SF_EQ | GLP_SF_2N | GLP_SF_SKIP | GLP_SF_AUTO))
+        xerror("glp_scale_prob: flags = " + flags + "; invalid scaling options");
+    var r = __gk.scaleProb(lp, flags), rep = r.report, bits = rep[12], i, j;
+    function line(tag, k) {
+        xprintf(tag + ": min|aij| = " + rep[3 * k] + "  max|aij| = " + rep[3 * k + 1] + "  ratio = " + rep[3 * k + 2] + "");
+    }
+    xprintf("Scaling...");
+    glp_unscale_prob(lp);
+    line(" A", 0);
+    if (bits & 1) xprintf("Problem data seem to be well scaled");
+    if (!(bits & 16)) {
+        if (bits & 2) line("GM", 1);
+        if (bits & 4) line("EQ", 2);
+        if (bits & 8) line("2N", 3);
+    }
+    for (i = 1; i <= lp.m; i++) glp_set_rii(lp, i, r.rii[i - 1]);
+    for (j = 1; j <= lp.n; j++) glp_set_sjj(lp, j, r.sjj[j - 1]);
+};
+
 (function () {
     function versioned(f) {
         return function (lp) {

@@ -155,4 +155,24 @@ fs.readdirSync(dir).filter(function (f) { return /^mip_.*\.json$/.test(f) && !/1
         nmip++;
     });
 assert.ok(nmip >= 10, 'too few MIP cases: ' + nmip);
-console.log('ok js gpu parity: ' + ncase + ' runs, ' + nmip + ' MIPs');
+
+// glp_scale_prob through the addon: the factors the reference computed
+// (tests/golden/scale_*.json), bit for bit, and its report numbers as JS
+// prints them (the shim's report lines are built from these)
+var nscale = 0;
+fs.readdirSync(dir).filter(function (f) { return /^scale_.*\.json$/.test(f); }).sort().forEach(function (f) {
+    var fx = JSON.parse(fs.readFileSync(path.join(dir, f)));
+    var lp = buildLp(fx);
+    fx.runs.forEach(function (r) {
+        if (r.error) return;
+        var out = core.scaleProb(lp, r.flags);
+        assert.strictEqual(out.ret, 0, f + ' ret');
+        for (var i = 0; i < fx.m; i++) assert.strictEqual(out.rii[i], r.rii[i], f + ' rii ' + i + ' flags ' + r.flags);
+        for (var j = 0; j < fx.n; j++) assert.strictEqual(out.sjj[j], r.sjj[j], f + ' sjj ' + j + ' flags ' + r.flags);
+        var a = out.report;
+        assert.strictEqual(r.lines[1], ' A: min|aij| = ' + a[0] + '  max|aij| = ' + a[1] + '  ratio = ' + a[2], f + ' A line');
+        nscale++;
+    });
+});
+assert.ok(nscale >= 60, 'too few scaling runs: ' + nscale);
+console.log('ok js gpu parity: ' + ncase + ' runs, ' + nmip + ' MIPs, ' + nscale + ' scalings');
