@@ -88,8 +88,8 @@ __global__ void __launch_bounds__(256) k_scl_sweep(int lines, const int *__restr
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             const int tt = min(beg + lane + 64 * u, last);
-            v[u] = val[tt];
-            c[u] = idx[tt];
+            v[u] = __builtin_nontemporal_load(val + tt);      // streamed once per sweep
+            c[u] = __builtin_nontemporal_load(idx + tt);
         }
         for (int t = beg + lane; t - lane < end; t += 64 * U) {
             double g[U], v2[U];
@@ -99,8 +99,8 @@ __global__ void __launch_bounds__(256) k_scl_sweep(int lines, const int *__restr
 #pragma unroll
             for (int u = 0; u < U; ++u) {
                 const int tt = min(t + 64 * (U + u), last);
-                v2[u] = val[tt];
-                c2[u] = idx[tt];
+                v2[u] = __builtin_nontemporal_load(val + tt);
+                c2[u] = __builtin_nontemporal_load(idx + tt);
             }
 #pragma unroll
             for (int u = 0; u < U; ++u) {
