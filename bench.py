@@ -309,9 +309,10 @@ def run_extra(gk, problems, ctx, c3):
 
 def run_scale(gk, ctx, p, flags=0x31):
     """glp_scale_prob(GM | EQ | 2N) on C3 (gk_scale.hip):
-    the device sweeps' rate with A resident (each sweep streams the 12-byte
-    entries of A once, by rows or by columns), and the whole call including
-    the upload of A and the row copy."""
+    the device time of the scaling work with A resident (every sweep, each
+    streaming the 12-byte entries of A once by rows or by columns, plus the
+    row copy when one is built) against the sweeps' algorithmic bytes, and
+    the whole call including the upload of A."""
     import ctypes as C
     import numpy as np
     ptr = np.ascontiguousarray(np.asarray(p.A_ptr, np.int32))
@@ -321,6 +322,8 @@ def run_scale(gk, ctx, p, flags=0x31):
     ms, by = C.c_double(0.0), C.c_double(0.0)
     f = lambda a: a.ctypes.data_as(C.c_void_p)  # noqa: E731
     L = gk.load_library()
+    L.gk_scale_prob_timed(ctx.h, p.m, p.n, f(ptr), f(ind), f(val), flags, f(rii), f(sjj), f(rep),   # warm-up
+                          C.byref(ms), C.byref(by))
     t0 = time.perf_counter()
     ret = L.gk_scale_prob_timed(ctx.h, p.m, p.n, f(ptr), f(ind), f(val), flags, f(rii), f(sjj), f(rep),
                                 C.byref(ms), C.byref(by))
@@ -328,7 +331,7 @@ def run_scale(gk, ctx, p, flags=0x31):
     gbps = by.value / (ms.value * 1e-3) / 1e9 if ms.value > 0 else 0.0
     return {"ret": ret, "flags": flags, "nnz": int(ptr[-1]), "sweeps_ms": round(ms.value, 3),
             "sweep_bytes": by.value, "sweeps_GBps": round(gbps, 1), "frac_of_hbm_peak": round(gbps / 8000.0, 4),
-            "seconds_incl_upload_and_row_copy": round(dt, 4),
+            "seconds_incl_upload": round(dt, 4),
             "report": {"A": list(rep[0:3]), "GM": list(rep[3:6]), "EQ": list(rep[6:9]), "2N": list(rep[9:12])}}
 
 

@@ -23,6 +23,8 @@
 #include "../../include/glpk_mi355x.h"
 #include <cfloat>
 #include <cmath>
+#include <cstdlib>
+#include <algorithm>
 #include <vector>
 
 namespace gk {
@@ -67,12 +69,12 @@ __device__ __forceinline__ double wmax_d(double v)
 //   SC_EQ    own /= max               (eq_scaling, glpscl.js:82-96)
 // `own` is r (rows) or s (columns); `other` is indexed by the entry's index.
 template <int ROWS>
-__global__ void __launch_bounds__(256) k_scl_sweep(int lines, const int *__restrict__ ptr,
+__global__ void __launch_bounds__(1024) k_scl_sweep(int lines, const int *__restrict__ ptr,
                                                    const int *__restrict__ idx, const double *__restrict__ val,
                                                    double *__restrict__ own, const double *__restrict__ other,
                                                    int mode, unsigned long long *acc)
 {
-    const int line = blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int line = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
     if (line >= lines) return;                          // wave-uniform
     const int beg = ptr[line], end = ptr[line + 1];
@@ -196,6 +198,114 @@ __global__ void __launch_bounds__(256) k_scl_scatter(int n, const int *__restric
     }
 }
 
+// Row statistics without a row copy (m <= ROWPART_MAX): block b takes a
+// contiguous range of columns and keeps per-row min / max of its entries in
+// LDS (bit patterns of non-negative doubles, ds_min_u64 / ds_max_u64); the
+// block's m pairs go to partials[b], and k_scl_rowfin reduces them per row.
+constexpr int ROWPART_MAX = 8192;
+constexpr int ROWPART_TILES = 256;
+
+__global__ void __launch_bounds__(1024) k_scl_rowpart(int n, int m, int cols_per_block, const int *__restrict__ cptr,
+                                                     const int *__restrict__ ind, const double *__restrict__ val,
+                                                     const double *__restrict__ r, const double *__restrict__ sj,
+                                                     unsigned long long *__restrict__ plo,
+                                                     unsigned long long *__restrict__ phi)
+{
+    extern __shared__ unsigned long long lds[];
+    unsigned long long *lo = lds, *hi = lds + m;
+    const unsigned long long INF = (unsigned long long)__double_as_longlong(DBL_MAX * 2.0);
+    for (int i = threadIdx.x; i < m; i += blockDim.x) {
+        lo[i] = INF;
+        hi[i] = 0ull;
+    }
+    __syncthreads();
+    const int j0 = blockIdx.x * cols_per_block, j1 = min(n, j0 + cols_per_block);
+    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, nw = blockDim.x >> 6;
+    for (int j = j0 + w; j < j1; j += nw) {
+        const int beg = cptr[j], end = cptr[j + 1];
+        const double o = sj[j];
+        constexpr int U = 8;
+        for (int t0 = beg; t0 < end; t0 += 64 * U) {
+            double v[U], g[U];
+            int c[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const int tt = min(t0 + lane + 64 * u, end - 1);
+                v[u] = __builtin_nontemporal_load(val + tt);
+                c[u] = __builtin_nontemporal_load(ind + tt) - 1;
+            }
+#pragma unroll
+            for (int u = 0; u < U; ++u) g[u] = r[c[u]];
+#pragma unroll
+            for (int u = 0; u < U; ++u)
+                if (t0 + lane + 64 * u < end) {
+                    const double temp = fabs(v[u]) * (g[u] * o);        // |a| (r_i s_j)
+                    const unsigned long long b = (unsigned long long)__double_as_longlong(temp);
+                    atomicMin(&lo[c[u]], b);        // (a read-compare first measured slower)
+                    atomicMax(&hi[c[u]], b);
+                }
+        }
+    }
+    __syncthreads();
+    unsigned long long *ql = plo + (size_t)blockIdx.x * m, *qh = phi + (size_t)blockIdx.x * m;
+    for (int i = threadIdx.x; i < m; i += blockDim.x) {
+        ql[i] = lo[i];
+        qh[i] = hi[i];
+    }
+}
+
+// per row: min / max over the tiles' partials (an empty row: 1, 1), then the
+// epilogue of k_scl_sweep<1>.  64 rows per block (lanes), the 16 waves split
+// the tiles (8 loads in flight each) and meet in LDS.
+__global__ void __launch_bounds__(1024) k_scl_rowfin(int m, int tiles, const unsigned long long *__restrict__ plo,
+                                                     const unsigned long long *__restrict__ phi,
+                                                     double *__restrict__ r, int mode, unsigned long long *acc)
+{
+    __shared__ unsigned long long sl[16][64], sh[16][64];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, nw = blockDim.x >> 6;
+    const int i = blockIdx.x * 64 + lane;
+    const int ii = min(i, m - 1);
+    const unsigned long long INF = (unsigned long long)__double_as_longlong(DBL_MAX * 2.0);
+    unsigned long long a = INF, b = 0ull;
+    for (int t0 = w; t0 < tiles; t0 += 8 * nw) {
+        unsigned long long x[8], y[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            const int t = min(t0 + u * nw, tiles - 1);
+            x[u] = plo[(size_t)t * m + ii];
+            y[u] = phi[(size_t)t * m + ii];
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            a = x[u] < a ? x[u] : a;                  // repeated tiles (clamped) change nothing
+            b = y[u] > b ? y[u] : b;
+        }
+    }
+    sl[w][lane] = a;
+    sh[w][lane] = b;
+    __syncthreads();
+    if (w != 0) return;
+    for (int k = 1; k < nw; ++k) {
+        a = sl[k][lane] < a ? sl[k][lane] : a;
+        b = sh[k][lane] > b ? sh[k][lane] : b;
+    }
+    double lo = __longlong_as_double((long long)a), hi = __longlong_as_double((long long)b);
+    if (a == INF) lo = hi = 1.0;                      // no entries
+    if (mode == SC_STAT) {
+        double l = i < m ? lo : DBL_MAX * 2.0, h = i < m ? hi : 0.0, q = i < m ? hi / lo : 0.0;
+        l = wmin_d(l);
+        h = wmax_d(h);
+        q = wmax_d(q);
+        if (lane == 0) {
+            atomicMin(&acc[0], (unsigned long long)__double_as_longlong(l));
+            atomicMax(&acc[1], (unsigned long long)__double_as_longlong(h));
+            atomicMax(&acc[2], (unsigned long long)__double_as_longlong(q));
+        }
+    } else if (i < m) {
+        r[i] = (mode == SC_GM) ? r[i] / sqrt(lo * hi) : r[i] / hi;
+    }
+}
+
 template <class T>
 struct DevBuf {
     T *p = nullptr;
@@ -227,10 +337,20 @@ int scale_prob_dev(hipStream_t s, int m, int n, const int *ptr, const int *ind, 
     SCHK(d_cptr.alloc(n + 1));
     SCHK(d_ind.alloc(nnz));
     SCHK(d_val.alloc(nnz));
-    SCHK(d_rptr.alloc(m + 1));
-    SCHK(d_fill.alloc(m + 1));
-    SCHK(d_rcol.alloc(nnz));
-    SCHK(d_rval.alloc(nnz));
+    // rows by LDS partials when m fits, else a row copy of A
+    const bool part = m > 0 && m <= ROWPART_MAX && n > 0 && std::getenv("GK_SCALE_ROWCOPY") == nullptr;
+    const int tiles = part ? std::min(ROWPART_TILES, n) : 0;
+    const int cpb = part ? cdiv(n, tiles) : 0;
+    DevBuf<unsigned long long> d_plo, d_phi;
+    if (part) {
+        SCHK(d_plo.alloc((size_t)tiles * m));
+        SCHK(d_phi.alloc((size_t)tiles * m));
+    } else {
+        SCHK(d_rptr.alloc(m + 1));
+        SCHK(d_fill.alloc(m + 1));
+        SCHK(d_rcol.alloc(nnz));
+        SCHK(d_rval.alloc(nnz));
+    }
     SCHK(d_r.alloc(m));
     SCHK(d_s.alloc(n));
     SCHK(d_acc.alloc(4));
@@ -239,37 +359,60 @@ int scale_prob_dev(hipStream_t s, int m, int n, const int *ptr, const int *ind, 
         SCHK(hipMemcpyAsync(d_ind.p, ind, sizeof(int) * nnz, hipMemcpyHostToDevice, s));
         SCHK(hipMemcpyAsync(d_val.p, val, sizeof(double) * nnz, hipMemcpyHostToDevice, s));
     }
-    // the row copy
-    SCHK(hipMemsetAsync(d_fill.p, 0, sizeof(int) * (m + 1), s));
-    if (nnz) hipLaunchKernelGGL(k_scl_count, dim3((unsigned)((nnz + 255) / 256)), dim3(256), 0, s, d_ind.p, nnz, d_fill.p);
-    if (m) hipLaunchKernelGGL(k_scl_scan, dim3(1), dim3(1024), 0, s, d_fill.p, m, d_rptr.p);
-    SCHK(hipMemcpyAsync(d_fill.p, d_rptr.p, sizeof(int) * (m + 1), hipMemcpyDeviceToDevice, s));
-    if (n) hipLaunchKernelGGL(k_scl_scatter, dim3(cdiv(n, 4)), dim3(256), 0, s, n, d_cptr.p, d_ind.p, d_val.p, d_fill.p,
-                              d_rcol.p, d_rval.p);
+    hipEvent_t b0, b1;
+    SCHK(hipEventCreate(&b0));
+    SCHK(hipEventCreate(&b1));
+    SCHK(hipEventRecord(b0, s));
+    if (!part) {
+        // the row copy
+        SCHK(hipMemsetAsync(d_fill.p, 0, sizeof(int) * (m + 1), s));
+        if (nnz)
+            hipLaunchKernelGGL(k_scl_count, dim3((unsigned)((nnz + 255) / 256)), dim3(256), 0, s, d_ind.p, nnz, d_fill.p);
+        if (m) hipLaunchKernelGGL(k_scl_scan, dim3(1), dim3(1024), 0, s, d_fill.p, m, d_rptr.p);
+        SCHK(hipMemcpyAsync(d_fill.p, d_rptr.p, sizeof(int) * (m + 1), hipMemcpyDeviceToDevice, s));
+        if (n)
+            hipLaunchKernelGGL(k_scl_scatter, dim3(cdiv(n, 4)), dim3(256), 0, s, n, d_cptr.p, d_ind.p, d_val.p,
+                               d_fill.p, d_rcol.p, d_rval.p);
+    }
     // glp_unscale_prob
     if (m) hipLaunchKernelGGL(k_scl_fill1, dim3(cdiv(m, 256)), dim3(256), 0, s, d_r.p, m);
     if (n) hipLaunchKernelGGL(k_scl_fill1, dim3(cdiv(n, 256)), dim3(256), 0, s, d_s.p, n);
     SCHK(hipGetLastError());
+    SCHK(hipEventRecord(b1, s));
+    SCHK(hipEventSynchronize(b1));
+    float build_ms = 0.f;
+    (void)hipEventElapsedTime(&build_ms, b0, b1);
+    (void)hipEventDestroy(b0);
+    (void)hipEventDestroy(b1);
 
     hipEvent_t e0, e1;
     SCHK(hipEventCreate(&e0));
     SCHK(hipEventCreate(&e1));
-    double ms_total = 0.0, bytes_total = 0.0;
+    // device time of the scaling work: the row copy (when built) plus every
+    // sweep (the host's stage decisions between sweeps are not counted)
+    double ms_total = build_ms, bytes_total = 0.0;
     auto sweep = [&](bool rows, int mode) -> hipError_t {
         if (rows ? m == 0 : n == 0) return hipSuccess;
         hipError_t e = hipEventRecord(e0, s);
         if (e != hipSuccess) return e;
-        if (rows)
-            hipLaunchKernelGGL(k_scl_sweep<1>, dim3(cdiv(m, 4)), dim3(256), 0, s, m, d_rptr.p, d_rcol.p, d_rval.p, d_r.p,
+        if (rows && part) {
+            hipLaunchKernelGGL(k_scl_rowpart, dim3(tiles), dim3(1024), (size_t)16 * m, s, n, m, cpb, d_cptr.p, d_ind.p,
+                               d_val.p, d_r.p, d_s.p, d_plo.p, d_phi.p);
+            hipLaunchKernelGGL(k_scl_rowfin, dim3(cdiv(m, 64)), dim3(1024), 0, s, m, tiles, d_plo.p, d_phi.p, d_r.p,
+                               mode, d_acc.p);
+        } else if (rows)
+            hipLaunchKernelGGL(k_scl_sweep<1>, dim3(cdiv(m, 16)), dim3(1024), 0, s, m, d_rptr.p, d_rcol.p, d_rval.p, d_r.p,
                                d_s.p, mode, d_acc.p);
         else
-            hipLaunchKernelGGL(k_scl_sweep<0>, dim3(cdiv(n, 4)), dim3(256), 0, s, n, d_cptr.p, d_ind.p, d_val.p, d_s.p,
+            hipLaunchKernelGGL(k_scl_sweep<0>, dim3(cdiv(n, 16)), dim3(1024), 0, s, n, d_cptr.p, d_ind.p, d_val.p, d_s.p,
                                d_r.p, mode, d_acc.p);
         if ((e = hipEventRecord(e1, s)) != hipSuccess) return e;
         if ((e = hipEventSynchronize(e1)) != hipSuccess) return e;
         float ms = 0.f;
         (void)hipEventElapsedTime(&ms, e0, e1);
         ms_total += ms;
+        // algorithmic: the 12-byte entries once, the line's own factor (read,
+        // and written by GM / EQ), its pointers
         bytes_total += 12.0 * (double)nnz + 8.0 * (rows ? m : n) * (mode == SC_STAT ? 1 : 2) + 4.0 * ((rows ? m : n) + 1);
         return hipGetLastError();
     };

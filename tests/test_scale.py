@@ -91,13 +91,13 @@ def test_gpu_scale_matches_reference(gpu_ctx, path, flags):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("seed", [1, 2, 3])
-def test_gpu_scale_matches_oracle_large(gpu_ctx, seed):
-    """larger random badly scaled matrices (20k rows, empty rows and columns,
-    magnitudes 1e-6 .. 1e6) against the oracle, every flag combination the
-    reference uses"""
+@pytest.mark.parametrize("seed,m", [(1, 20000), (2, 20000), (3, 6000), (4, 8192)])
+def test_gpu_scale_matches_oracle_large(gpu_ctx, seed, m):
+    """larger random badly scaled matrices (empty rows and columns, magnitudes
+    1e-6 .. 1e6) against the oracle, every flag combination the reference
+    uses; m <= 8192 takes the LDS row-partials path, 20k rows the row copy"""
     rng = np.random.default_rng(seed)
-    m, n, nnz = 20000, 30000, 300000
+    n, nnz = 30000, 300000
     rows = rng.integers(1, m + 1, nnz)
     rows[rows == 7] = 8                                   # an empty row
     cols = np.sort(rng.integers(0, n, nnz))
