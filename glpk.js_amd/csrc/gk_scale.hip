@@ -209,7 +209,7 @@ __global__ void __launch_bounds__(1024) k_scl_rowpart(int n, int m, int cols_per
                                                      const int *__restrict__ ind, const double *__restrict__ val,
                                                      const double *__restrict__ r, const double *__restrict__ sj,
                                                      unsigned long long *__restrict__ plo,
-                                                     unsigned long long *__restrict__ phi)
+                                                     unsigned long long *__restrict__ phi, unsigned long long *colacc)
 {
     extern __shared__ unsigned long long lds[];
     unsigned long long *lo = lds, *hi = lds + m;
@@ -224,6 +224,7 @@ __global__ void __launch_bounds__(1024) k_scl_rowpart(int n, int m, int cols_per
     for (int j = j0 + w; j < j1; j += nw) {
         const int beg = cptr[j], end = cptr[j + 1];
         const double o = sj[j];
+        double clo = DBL_MAX * 2.0, chi = 0.0;          // the column's own min / max (colacc)
         constexpr int U = 8;
         for (int t0 = beg; t0 < end; t0 += 64 * U) {
             double v[U], g[U];
@@ -243,7 +244,17 @@ __global__ void __launch_bounds__(1024) k_scl_rowpart(int n, int m, int cols_per
                     const unsigned long long b = (unsigned long long)__double_as_longlong(temp);
                     atomicMin(&lo[c[u]], b);        // (a read-compare first measured slower)
                     atomicMax(&hi[c[u]], b);
+                    clo = fmin(clo, temp);
+                    chi = fmax(chi, temp);
                 }
+        }
+        // column statistics of the same pass (k_scl_sweep<0>'s SC_STAT epilogue:
+        // the same |a| (r_i s_j) products, an empty column counts as 1, 1)
+        if (colacc) {
+            clo = wmin_d(clo);
+            chi = wmax_d(chi);
+            if (end == beg) clo = chi = 1.0;
+            if (lane == 0) atomicMax(colacc, (unsigned long long)__double_as_longlong(chi / clo));
         }
     }
     __syncthreads();
@@ -391,13 +402,15 @@ int scale_prob_dev(hipStream_t s, int m, int n, const int *ptr, const int *ind, 
     // device time of the scaling work: the row copy (when built) plus every
     // sweep (the host's stage decisions between sweeps are not counted)
     double ms_total = build_ms, bytes_total = 0.0;
-    auto sweep = [&](bool rows, int mode) -> hipError_t {
+    // colstat: a row statistics pass by partials also forms the column ratio
+    // (acc 3) from the same entries, so stats(true) streams A once
+    auto sweep = [&](bool rows, int mode, bool colstat = false) -> hipError_t {
         if (rows ? m == 0 : n == 0) return hipSuccess;
         hipError_t e = hipEventRecord(e0, s);
         if (e != hipSuccess) return e;
         if (rows && part) {
             hipLaunchKernelGGL(k_scl_rowpart, dim3(tiles), dim3(1024), (size_t)16 * m, s, n, m, cpb, d_cptr.p, d_ind.p,
-                               d_val.p, d_r.p, d_s.p, d_plo.p, d_phi.p);
+                               d_val.p, d_r.p, d_s.p, d_plo.p, d_phi.p, colstat ? d_acc.p + 3 : nullptr);
             hipLaunchKernelGGL(k_scl_rowfin, dim3(cdiv(m, 64)), dim3(1024), 0, s, m, tiles, d_plo.p, d_phi.p, d_r.p,
                                mode, d_acc.p);
         } else if (rows)
@@ -414,13 +427,15 @@ int scale_prob_dev(hipStream_t s, int m, int n, const int *ptr, const int *ind, 
         // algorithmic: the 12-byte entries once, the line's own factor (read,
         // and written by GM / EQ), its pointers
         bytes_total += 12.0 * (double)nnz + 8.0 * (rows ? m : n) * (mode == SC_STAT ? 1 : 2) + 4.0 * ((rows ? m : n) + 1);
+        if (colstat) bytes_total += 8.0 * n + 4.0 * (n + 1);   // the column factors and pointers
         return hipGetLastError();
     };
     // statistics with the current factors: (mat min, mat max, row ratio, col ratio)
     auto stats = [&](bool cols, double *q) -> int {
         hipLaunchKernelGGL(k_scl_acc_init, dim3(1), dim3(64), 0, s, d_acc.p);
-        SCHK(sweep(true, SC_STAT));
-        if (cols) SCHK(sweep(false, SC_STAT));
+        const bool fused = cols && part;
+        SCHK(sweep(true, SC_STAT, fused));
+        if (cols && !fused) SCHK(sweep(false, SC_STAT));
         unsigned long long a[4];
         SCHK(hipMemcpyAsync(a, d_acc.p, sizeof a, hipMemcpyDeviceToHost, s));
         SCHK(hipStreamSynchronize(s));
