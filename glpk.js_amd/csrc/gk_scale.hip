@@ -205,6 +205,7 @@ __global__ void __launch_bounds__(256) k_scl_scatter(int n, const int *__restric
 constexpr int ROWPART_MAX = 8192;
 constexpr int ROWPART_TILES = 256;
 
+template <bool COLSTAT>
 __global__ void __launch_bounds__(1024) k_scl_rowpart(int n, int m, int cols_per_block, const int *__restrict__ cptr,
                                                      const int *__restrict__ ind, const double *__restrict__ val,
                                                      const double *__restrict__ r, const double *__restrict__ sj,
@@ -244,13 +245,15 @@ __global__ void __launch_bounds__(1024) k_scl_rowpart(int n, int m, int cols_per
                     const unsigned long long b = (unsigned long long)__double_as_longlong(temp);
                     atomicMin(&lo[c[u]], b);        // (a read-compare first measured slower)
                     atomicMax(&hi[c[u]], b);
-                    clo = fmin(clo, temp);
-                    chi = fmax(chi, temp);
+                    if (COLSTAT) {
+                        clo = fmin(clo, temp);
+                        chi = fmax(chi, temp);
+                    }
                 }
         }
         // column statistics of the same pass (k_scl_sweep<0>'s SC_STAT epilogue:
         // the same |a| (r_i s_j) products, an empty column counts as 1, 1)
-        if (colacc) {
+        if (COLSTAT) {
             clo = wmin_d(clo);
             chi = wmax_d(chi);
             if (end == beg) clo = chi = 1.0;
@@ -409,8 +412,12 @@ int scale_prob_dev(hipStream_t s, int m, int n, const int *ptr, const int *ind, 
         hipError_t e = hipEventRecord(e0, s);
         if (e != hipSuccess) return e;
         if (rows && part) {
-            hipLaunchKernelGGL(k_scl_rowpart, dim3(tiles), dim3(1024), (size_t)16 * m, s, n, m, cpb, d_cptr.p, d_ind.p,
-                               d_val.p, d_r.p, d_s.p, d_plo.p, d_phi.p, colstat ? d_acc.p + 3 : nullptr);
+            if (colstat)
+                hipLaunchKernelGGL(k_scl_rowpart<true>, dim3(tiles), dim3(1024), (size_t)16 * m, s, n, m, cpb, d_cptr.p,
+                                   d_ind.p, d_val.p, d_r.p, d_s.p, d_plo.p, d_phi.p, d_acc.p + 3);
+            else
+                hipLaunchKernelGGL(k_scl_rowpart<false>, dim3(tiles), dim3(1024), (size_t)16 * m, s, n, m, cpb, d_cptr.p,
+                                   d_ind.p, d_val.p, d_r.p, d_s.p, d_plo.p, d_phi.p, nullptr);
             hipLaunchKernelGGL(k_scl_rowfin, dim3(cdiv(m, 64)), dim3(1024), 0, s, m, tiles, d_plo.p, d_phi.p, d_r.p,
                                mode, d_acc.p);
         } else if (rows)
