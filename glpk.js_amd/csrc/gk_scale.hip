@@ -222,6 +222,8 @@ __global__ void __launch_bounds__(1024) k_scl_rowpart(int n, int m, int cols_per
     __syncthreads();
     const int j0 = blockIdx.x * cols_per_block, j1 = min(n, j0 + cols_per_block);
     const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, nw = blockDim.x >> 6;
+    __shared__ unsigned long long wr[16];             // per-wave max column ratio
+    double cmax = 0.0;
     for (int j = j0 + w; j < j1; j += nw) {
         const int beg = cptr[j], end = cptr[j + 1];
         const double o = sj[j];
@@ -257,10 +259,17 @@ __global__ void __launch_bounds__(1024) k_scl_rowpart(int n, int m, int cols_per
             clo = wmin_d(clo);
             chi = wmax_d(chi);
             if (end == beg) clo = chi = 1.0;
-            if (lane == 0) atomicMax(colacc, (unsigned long long)__double_as_longlong(chi / clo));
+            cmax = fmax(cmax, chi / clo);
         }
     }
+    if (COLSTAT && lane == 0) wr[w] = (unsigned long long)__double_as_longlong(cmax);
     __syncthreads();
+    // one atomic per workgroup (one per column serialised on a single L2 line)
+    if (COLSTAT && threadIdx.x == 0) {
+        unsigned long long b = 0ull;
+        for (int k = 0; k < nw; ++k) b = wr[k] > b ? wr[k] : b;
+        atomicMax(colacc, b);
+    }
     unsigned long long *ql = plo + (size_t)blockIdx.x * m, *qh = phi + (size_t)blockIdx.x * m;
     for (int i = threadIdx.x; i < m; i += blockDim.x) {
         ql[i] = lo[i];
