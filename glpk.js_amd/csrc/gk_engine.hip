@@ -1631,9 +1631,29 @@ void gk_bfd_destroy(gk_bfd *f)
     delete f;
 }
 
-void gk_bfd_set_parm(gk_bfd *f, const gk_bfcp *parm)
+// the checks of glp_set_bfcp (glpapi12.js:133-166), messages included (the
+// rs_size message prints nrs_max there too); type FT / BG / GR all select the
+// explicit-inverse factor, the fields of the sparse LU (piv_tol, piv_lim,
+// suhl, lu_size, eps_tol, max_gro, nrs_max, rs_size) are kept but steer
+// nothing; nfs_max and upd_tol act (re-inversion interval, update check)
+int gk_bfd_set_parm(gk_bfd *f, const gk_bfcp *parm)
 {
-    if (f && parm) f->parm = *parm;
+    if (!f || !parm) { set_err("gk_bfd_set_parm: null argument"); return GK_EABI; }
+    const gk_bfcp &b = *parm;
+    if (!(b.type == 1 || b.type == 2 || b.type == 3)) { set_err("glp_set_bfcp: type = %d; invalid parameter", b.type); return GK_EABI; }
+    if (b.lu_size < 0) { set_err("glp_set_bfcp: lu_size = %d; invalid parameter", b.lu_size); return GK_EABI; }
+    if (!(0.0 < b.piv_tol && b.piv_tol < 1.0)) { set_err("glp_set_bfcp: piv_tol = %.17g; invalid parameter", b.piv_tol); return GK_EABI; }
+    if (b.piv_lim < 1) { set_err("glp_set_bfcp: piv_lim = %d; invalid parameter", b.piv_lim); return GK_EABI; }
+    if (!(b.suhl == 1 || b.suhl == 0)) { set_err("glp_set_bfcp: suhl = %d; invalid parameter", b.suhl); return GK_EABI; }
+    if (!(0.0 <= b.eps_tol && b.eps_tol <= 1e-6)) { set_err("glp_set_bfcp: eps_tol = %.17g; invalid parameter", b.eps_tol); return GK_EABI; }
+    if (b.max_gro < 1.0) { set_err("glp_set_bfcp: max_gro = %.17g; invalid parameter", b.max_gro); return GK_EABI; }
+    if (!(1 <= b.nfs_max && b.nfs_max <= 32767)) { set_err("glp_set_bfcp: nfs_max = %d; invalid parameter", b.nfs_max); return GK_EABI; }
+    if (!(0.0 < b.upd_tol && b.upd_tol < 1.0)) { set_err("glp_set_bfcp: upd_tol = %.17g; invalid parameter", b.upd_tol); return GK_EABI; }
+    if (!(1 <= b.nrs_max && b.nrs_max <= 32767)) { set_err("glp_set_bfcp: nrs_max = %d; invalid parameter", b.nrs_max); return GK_EABI; }
+    if (b.rs_size < 0) { set_err("glp_set_bfcp: rs_size = %d; invalid parameter", b.nrs_max); return GK_EABI; }
+    f->parm = b;
+    if (f->parm.rs_size == 0) f->parm.rs_size = 20 * f->parm.nrs_max;
+    return 0;
 }
 
 int gk_bfd_valid(const gk_bfd *f) { return f ? f->valid : 0; }
@@ -1863,6 +1883,19 @@ int gk_spx_primal(gk_ctx *ctx, gk_lp *lp, gk_bfd *bfd, const gk_smcp *parm) { re
 int gk_spx_dual(gk_ctx *ctx, gk_lp *lp, gk_bfd *bfd, const gk_smcp *parm) { return spx_entry(ctx, lp, bfd, parm, 1); }
 
 }  // extern "C"
+
+namespace gk {
+// gk_mip.hip's fallback for a node LP the batched kernel could not finish:
+// glp_simplex with meth = GLP_DUALP (solve_lp, glpapi06.js:27-37) on a fresh
+// factorization of lp->head
+int gk_spx_node(gk_ctx *ctx, gk_lp *lp, gk_bfd *bfd, const gk_smcp *parm)
+{
+    if (bfd) bfd->valid = 0;
+    int ret = spx_entry(ctx, lp, bfd, parm, 1);
+    if (ret == 5 && lp->valid) ret = spx_entry(ctx, lp, bfd, parm, 0);
+    return ret;
+}
+}  // namespace gk
 
 extern "C" double gk_bfd_time_kernel(gk_bfd *f, int which, int reps, double *bytes)
 {

@@ -30,6 +30,7 @@
 #include <cfloat>
 #include <chrono>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <queue>
 #include <string>
@@ -39,7 +40,12 @@ namespace gk {
 
 void set_err(const char *fmt, ...);
 
-enum : int { NODE_OPT = 0, NODE_INFEAS = 1, NODE_CUTOFF = 2, NODE_FAIL = 3 };
+// node LP outcomes (status[]): OPT / INFEAS (dual unbounded) / CUTOFF (dual
+// objective reached the incumbent) are final; FAIL (singular basis or a
+// status the kernel cannot warm-start from) and ITLIM (iteration limit; the
+// dual objective is still a valid bound) send a node to the engine fallback;
+// PPINF: ios_preprocess_node proved the node infeasible (no LP solved)
+enum : int { NODE_OPT = 0, NODE_INFEAS = 1, NODE_CUTOFF = 2, NODE_FAIL = 3, NODE_ITLIM = 4, NODE_PPINF = 5 };
 
 struct NodeProb {
     int m, n, ld;                 // ld = m + n (row length of T)
@@ -47,16 +53,20 @@ struct NodeProb {
     const double *c;              // internal minimisation costs, [m+n] (0 for rows)
     const signed char *isint;     // [n]
     double tol_int;
+    int dth;                      // 1: choose the branching column by branch_drtom
 };
 
 struct NodeIO {
     const double *lb, *ub;        // [nb][m+n]
     const signed char *stat_in;   // [nb][m+n]  GLP_BS / NL / NU / NF / NS
     const double *cutoff;         // [nb]  stop once the dual objective reaches it
+    const int *it_lim;            // [nb]  dual simplex iteration limit of the node
+    const int *pp_pass;           // [nb]  ios_preprocess_node passes (0: none)
+    double obj_bound;             // preprocessing: objective row bound (minimisation form, DBL_MAX: none)
     int *status, *pivots, *jj, *next;
-    double *obj, *x, *dz;         // obj[nb], x[nb][m+n], dz[nb][2]
+    double *obj, *x, *dzb, *bnd;  // obj[nb], x[nb][m+n], dzb[nb][2n] (dn, up degradation
+                                  // bounds of every fractional column), bnd[nb][2n] (final column bounds)
     signed char *stat_out;        // [nb][m+n]
-    int it_lim;
     double *scratch;              // GLOBAL kernel: per-node work area (node_lp_lds(m, n) bytes each)
     size_t scratch_stride;        // in doubles
 };
@@ -141,10 +151,162 @@ __device__ __forceinline__ double nb_value(int st, double lb, double ub)
 }
 
 // ---------------------------------------------------------------------------
+// ios_preprocess_node (glpios02.js:1, called per node at glpios03.js:643-656):
+// bound propagation over the rows of the node and the objective row under
+// the incumbent.  The reference walks a LIFO list of rows, each row seeing
+// the bounds tightened by the previous one; here a pass is two parallel
+// phases over the whole node — one wave per row forms the row's activity
+// bounds (prepare_row_info :2, check_row_bounds :137: infeasibility and
+// redundant row bounds), then one thread per column intersects the implied
+// bounds of all its rows (col_implied_bounds :74, check_col_bounds :177 with
+// integer rounding) — repeated while some column changed efficiently
+// (check_efficiency :245), at most max_pass times.  Every tightening is one
+// the reference's rules derive, so the node's feasible set is unchanged.
+// ri[6 i + {0..5}] = f_min, f_max, j_min, j_max, L, U of row i (row 0: the
+// objective, sum c_j x_j <= incumbent in minimisation form).
+// Returns 1 when the node is infeasible.  Called by the whole block.
+// ---------------------------------------------------------------------------
+__device__ int node_preprocess(const NodeProb &P, double objU, double *lb, double *ub, signed char *stat,
+                               signed char *chg, double *ri, int max_pass)
+{
+    const int m = P.m, n = P.n;
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, nw = blockDim.x >> 6;
+    for (int i = threadIdx.x; i <= m; i += blockDim.x) {
+        ri[6 * i + 4] = (i == 0) ? -DBL_MAX : lb[i - 1];
+        ri[6 * i + 5] = (i == 0) ? objU : ub[i - 1];
+    }
+    __syncthreads();
+    for (int pass = 0; pass < max_pass; ++pass) {
+        // ---- rows: activity bounds, infeasibility, redundant row bounds
+        int bad = 0;
+        for (int i = w; i <= m; i += nw) {
+            double L = ri[6 * i + 4], U = ri[6 * i + 5];
+            if (L == -DBL_MAX && U == DBL_MAX) continue;           // free row (wave-uniform)
+            double smin = 0.0, smax = 0.0, cmin = 0.0, cmax = 0.0, jmin = 0.0, jmax = 0.0;
+            for (int j = lane; j < n; j += 64) {
+                const double a = (i == 0) ? P.c[m + j] : P.A[(size_t)j * m + (i - 1)];
+                if (a == 0.0) continue;
+                const double l = lb[m + j], u = ub[m + j];
+                const double lo = a > 0.0 ? l : u, hi = a > 0.0 ? u : l;
+                if ((a > 0.0 && l == -DBL_MAX) || (a < 0.0 && u == DBL_MAX)) { cmin += 1.0; jmin = j + 1; }
+                else smin += a * lo;
+                if ((a > 0.0 && u == DBL_MAX) || (a < 0.0 && l == -DBL_MAX)) { cmax += 1.0; jmax = j + 1; }
+                else smax += a * hi;
+            }
+            smin = wsum(smin); smax = wsum(smax);
+            cmin = wsum(cmin); cmax = wsum(cmax);
+            jmin = wmax(jmin); jmax = wmax(jmax);
+            // prepare_row_info: one unbounded term -> the sum of the others and
+            // its column; two or more -> infinite
+            const double fmin = cmin >= 2.0 ? -DBL_MAX : smin, fmax = cmax >= 2.0 ? DBL_MAX : smax;
+            const int jn = cmin == 1.0 ? (int)jmin : 0, jx = cmax == 1.0 ? (int)jmax : 0;
+            const double LL = jn == 0 ? fmin : -DBL_MAX, UU = jx == 0 ? fmax : DBL_MAX;
+            if (L != -DBL_MAX && UU < L - 1e-3 * (1.0 + fabs(L))) bad = 1;
+            if (U != DBL_MAX && LL > U + 1e-3 * (1.0 + fabs(U))) bad = 1;
+            if (L != -DBL_MAX && LL > L - 1e-12 * (1.0 + fabs(L))) L = -DBL_MAX;
+            if (U != DBL_MAX && UU < U + 1e-12 * (1.0 + fabs(U))) U = DBL_MAX;
+            if (lane == 0) {
+                ri[6 * i + 0] = fmin; ri[6 * i + 1] = fmax;
+                ri[6 * i + 2] = jn; ri[6 * i + 3] = jx;
+                ri[6 * i + 4] = L; ri[6 * i + 5] = U;
+            }
+        }
+        if (__syncthreads_or(bad)) return 1;
+        // ---- columns: implied bounds of every row the column is in
+        int eff = 0;
+        for (int j = threadIdx.x; j < n; j += blockDim.x) {
+            const double l0 = lb[m + j], u0 = ub[m + j];
+            const bool flag = P.isint[j] != 0;
+            double lj = l0, uj = u0;
+            for (int i = 0; i <= m && !bad; ++i) {
+                const double L = ri[6 * i + 4], U = ri[6 * i + 5];
+                if (L == -DBL_MAX && U == DBL_MAX) continue;
+                const double a = (i == 0) ? P.c[m + j] : P.A[(size_t)j * m + (i - 1)];
+                if (a == 0.0) continue;
+                const double fmin = ri[6 * i + 0], fmax = ri[6 * i + 1];
+                const int jn = (int)ri[6 * i + 2], jx = (int)ri[6 * i + 3];
+                double ilb, iub, ll, uu;
+                if (L == -DBL_MAX || fmax == DBL_MAX) ilb = -DBL_MAX;
+                else if (jx == 0) ilb = L - (fmax - a * (a > 0.0 ? u0 : l0));
+                else if (jx == j + 1) ilb = L - fmax;
+                else ilb = -DBL_MAX;
+                if (U == DBL_MAX || fmin == -DBL_MAX) iub = DBL_MAX;
+                else if (jn == 0) iub = U - (fmin - a * (a > 0.0 ? l0 : u0));
+                else if (jn == j + 1) iub = U - fmin;
+                else iub = DBL_MAX;
+                if (fabs(a) < 1e-6) { ll = -DBL_MAX; uu = DBL_MAX; }
+                else if (a > 0.0) {
+                    ll = ilb == -DBL_MAX ? -DBL_MAX : ilb / a;
+                    uu = iub == DBL_MAX ? DBL_MAX : iub / a;
+                } else {
+                    ll = iub == DBL_MAX ? -DBL_MAX : iub / a;
+                    uu = ilb == -DBL_MAX ? DBL_MAX : ilb / a;
+                }
+                if (flag) {
+                    if (ll != -DBL_MAX) ll = (ll - floor(ll) < 1e-3 ? floor(ll) : ceil(ll));
+                    if (uu != DBL_MAX) uu = (ceil(uu) - uu < 1e-3 ? ceil(uu) : floor(uu));
+                }
+                const double lp = lj, up = uj;
+                if (lj != -DBL_MAX && uu < lj - 1e-3 * (1.0 + fabs(lj))) { bad = 1; break; }
+                if (uj != DBL_MAX && ll > uj + 1e-3 * (1.0 + fabs(uj))) { bad = 1; break; }
+                if (ll != -DBL_MAX && lj < ll - 1e-3 * (1.0 + fabs(ll))) lj = ll;
+                if (uu != DBL_MAX && uj > uu + 1e-3 * (1.0 + fabs(uu))) uj = uu;
+                if (!(lj == -DBL_MAX || uj == DBL_MAX)) {
+                    const double t1 = fabs(lj), t2 = fabs(uj);
+                    if (lj > uj - 1e-10 * (1.0 + (t1 <= t2 ? t1 : t2))) {
+                        if (lj == lp) uj = lj;
+                        else if (uj == up) lj = uj;
+                        else if (t1 <= t2) uj = lj;
+                        else lj = uj;
+                    }
+                }
+            }
+            // check_efficiency (:245)
+            if (l0 < lj) {
+                if (flag || l0 == -DBL_MAX) eff = 1;
+                else {
+                    const double r = (u0 == DBL_MAX) ? 1.0 + fabs(l0) : 1.0 + (u0 - l0);
+                    if (lj - l0 >= 0.25 * r) eff = 1;
+                }
+            }
+            if (u0 > uj) {
+                if (flag || u0 == DBL_MAX) eff = 1;
+                else {
+                    const double r = (l0 == -DBL_MAX) ? 1.0 + fabs(u0) : 1.0 + (u0 - l0);
+                    if (u0 - uj >= 0.25 * r) eff = 1;
+                }
+            }
+            lb[m + j] = lj;
+            ub[m + j] = uj;
+        }
+        if (__syncthreads_or(bad)) return 1;
+        if (!__syncthreads_or(eff)) break;
+    }
+    // relaxed bounds of the basic rows (non-active: dual feasibility kept);
+    // statuses of non-basic columns whose type changed (glp_set_col_bnds):
+    // fixed -> NS, a free column that gained a bound is re-chosen once the
+    // reduced costs are known (chg)
+    for (int i = threadIdx.x; i < m; i += blockDim.x)
+        if (stat[i] == BS) {
+            lb[i] = ri[6 * (i + 1) + 4];
+            ub[i] = ri[6 * (i + 1) + 5];
+        }
+    for (int j = threadIdx.x; j < n; j += blockDim.x) {
+        const int k = m + j;
+        if (stat[k] == BS) continue;
+        if (lb[k] == ub[k]) stat[k] = NS;
+        else if (stat[k] == NF && (lb[k] != -DBL_MAX || ub[k] != DBL_MAX)) chg[j] = 1;
+    }
+    __syncthreads();
+    return 0;
+}
+
+// ---------------------------------------------------------------------------
 // one workgroup = one node LP
 // LDS: M[m][2m+n] during the inversion, then T[m][m+n]; lb, ub, x, d [m+n];
-// head[m], stat[m+n].  GLOBAL = 1: the same work area in a per-node slice of
-// HBM (node LPs beyond 64 KiB of LDS; L2 serves the workgroup's sweeps).
+// fcol[m]; preprocessing row info [6 (m+1)]; head[m], stat[m+n], chg[n].
+// GLOBAL = 1: the same work area in a per-node slice of HBM (node LPs beyond
+// 64 KiB of LDS; L2 serves the workgroup's sweeps).
 // ---------------------------------------------------------------------------
 template <int GLOBAL>
 __global__ void __launch_bounds__(256) k_node_lp(NodeProb P, NodeIO io)
@@ -159,16 +321,37 @@ __global__ void __launch_bounds__(256) k_node_lp(NodeProb P, NodeIO io)
     double *M = lds;                          // m * W
     double *lb = M + (size_t)m * W, *ub = lb + N, *x = ub + N, *d = x + N;
     double *fcol = d + N;                     // m
-    int *head = (int *)(fcol + m);
+    double *rinfo = fcol + m;                 // 6 (m + 1)
+    int *head = (int *)(rinfo + 6 * (m + 1));
     signed char *stat = (signed char *)(head + m);
+    signed char *chg = stat + N;              // n
     const double *glb = io.lb + (size_t)b * N, *gub = io.ub + (size_t)b * N;
     const signed char *gst = io.stat_in + (size_t)b * N;
+    double *gbnd = io.bnd + (size_t)b * 2 * n, *gdz = io.dzb + (size_t)b * 2 * n;
     for (int k = threadIdx.x; k < N; k += blockDim.x) {
         lb[k] = glb[k];
         ub[k] = gub[k];
         stat[k] = gst[k];
     }
+    for (int j = threadIdx.x; j < n; j += blockDim.x) {
+        chg[j] = 0;
+        gdz[2 * j] = 0.0;
+        gdz[2 * j + 1] = 0.0;
+    }
     __syncthreads();
+    auto put_bounds = [&]() {
+        for (int j = threadIdx.x; j < n; j += blockDim.x) {
+            gbnd[2 * j] = lb[m + j];
+            gbnd[2 * j + 1] = ub[m + j];
+        }
+    };
+    const int max_pass = io.pp_pass[b];
+    if (max_pass > 0 && node_preprocess(P, io.obj_bound, lb, ub, stat, chg, rinfo, max_pass)) {
+        put_bounds();
+        if (threadIdx.x == 0) { io.status[b] = NODE_PPINF; io.pivots[b] = 0; io.jj[b] = 0; io.obj[b] = 0.0; }
+        return;
+    }
+    put_bounds();
     // basis header in variable order (glp_factorize's head, glpapi12.js:44-67)
     if (threadIdx.x == 0) {
         int j = 0;
@@ -181,7 +364,7 @@ __global__ void __launch_bounds__(256) k_node_lp(NodeProb P, NodeIO io)
     }
     __syncthreads();
     if (sh_flag) {
-        if (threadIdx.x == 0) { io.status[b] = NODE_FAIL; io.pivots[b] = 0; }
+        if (threadIdx.x == 0) { io.status[b] = NODE_FAIL; io.pivots[b] = 0; io.jj[b] = 0; }
         return;
     }
     // M = [B | I | -A]: column k of (I | -A) is e_k (k < m) or -A[:, k-m]
@@ -211,7 +394,7 @@ __global__ void __launch_bounds__(256) k_node_lp(NodeProb P, NodeIO io)
         const bool singular = piv < 0 || fabs(M[(size_t)piv * W + k]) < 1e-12;
         __syncthreads();                      // every wave has read M[piv][k] before the swap moves it
         if (singular) {
-            if (threadIdx.x == 0) { io.status[b] = NODE_FAIL; io.pivots[b] = 0; }
+            if (threadIdx.x == 0) { io.status[b] = NODE_FAIL; io.pivots[b] = 0; io.jj[b] = 0; }
             return;
         }
         if (piv != k)
@@ -236,17 +419,7 @@ __global__ void __launch_bounds__(256) k_node_lp(NodeProb P, NodeIO io)
     }
     // T[i][j] = M[i][m + j]  (row length W kept; T(i, j) = M[i*W + m + j])
 #define T_(i, j) M[(size_t)(i) * W + m + (j)]
-    // x_N and x_B = -T_N x_N
-    for (int k = threadIdx.x; k < N; k += blockDim.x) x[k] = (stat[k] == BS) ? 0.0 : nb_value(stat[k], lb[k], ub[k]);
-    __syncthreads();
-    for (int i = threadIdx.x; i < m; i += blockDim.x) {
-        double s = 0.0;
-        for (int k = 0; k < N; ++k)
-            if (stat[k] != BS && x[k] != 0.0) s += T_(i, k) * x[k];
-        x[head[i]] = -s;
-    }
     // d = c - c_B' T
-    __syncthreads();
     for (int k = threadIdx.x; k < N; k += blockDim.x) {
         if (stat[k] == BS) { d[k] = 0.0; continue; }
         double s = P.c[k];
@@ -257,9 +430,37 @@ __global__ void __launch_bounds__(256) k_node_lp(NodeProb P, NodeIO io)
         d[k] = s;
     }
     __syncthreads();
+    // a free column that gained a bound in preprocessing: the bound its
+    // reduced cost allows (a warm start must stay dual feasible)
+    {
+        int bad = 0;
+        for (int j = threadIdx.x; j < n; j += blockDim.x) {
+            if (!chg[j]) continue;
+            const int k = m + j;
+            const bool hl = lb[k] != -DBL_MAX, hu = ub[k] != DBL_MAX;
+            if (hl && hu) stat[k] = d[k] >= 0.0 ? NL : NU;
+            else if (hl) { stat[k] = NL; if (d[k] < -1e-9) bad = 1; }
+            else { stat[k] = NU; if (d[k] > 1e-9) bad = 1; }
+        }
+        if (__syncthreads_or(bad)) {
+            if (threadIdx.x == 0) { io.status[b] = NODE_FAIL; io.pivots[b] = 0; io.jj[b] = 0; }
+            return;
+        }
+    }
+    // x_N and x_B = -T_N x_N
+    for (int k = threadIdx.x; k < N; k += blockDim.x) x[k] = (stat[k] == BS) ? 0.0 : nb_value(stat[k], lb[k], ub[k]);
+    __syncthreads();
+    for (int i = threadIdx.x; i < m; i += blockDim.x) {
+        double s = 0.0;
+        for (int k = 0; k < N; ++k)
+            if (stat[k] != BS && x[k] != 0.0) s += T_(i, k) * x[k];
+        x[head[i]] = -s;
+    }
+    __syncthreads();
     // ---- bounded dual simplex ------------------------------------------
     const double tol_p = 1e-7, tol_piv = 1e-7;
     const double cutoff = io.cutoff[b];
+    const int it_lim = io.it_lim[b];
     int it = 0, status = NODE_OPT;
     for (;;) {
         // objective (dual objective of the current dual feasible basis)
@@ -280,7 +481,7 @@ __global__ void __launch_bounds__(256) k_node_lp(NodeProb P, NodeIO io)
         }
         const int p = block_argmax(key, idx, shk, shi);
         if (p < 0) break;                                  // primal feasible: optimal
-        if (it >= io.it_lim) { status = NODE_FAIL; break; }
+        if (it >= it_lim) { status = NODE_ITLIM; break; }
         const int kp = head[p];
         const bool to_lb = x[kp] < lb[kp];
         // ratio test on row p: x_p = -sum T[p,j] x_j
@@ -379,13 +580,17 @@ __global__ void __launch_bounds__(256) k_node_lp(NodeProb P, NodeIO io)
         }
         return;
     }
-    // ---- branch_drtom (glpios09.js:84) on the node's own tableau rows ----
+    // ---- ios_eval_degrad (glpios03.js:188) for every fractional column and
+    // branch_drtom (glpios09.js:84) on the node's own tableau rows ---------
     // columns in order; x_j basic and fractional; the dual ratio test of
     // glp_dual_rtest (glpapi12.js:687) on the row x_j = sum alfa_k x_k,
-    // alfa_k = -T[i,k]; delta z = d_k * delta x_k with Tomlin's rounding
+    // alfa_k = -T[i,k]; delta z = d_k * delta x_k.  dzb (the one-pivot dual
+    // bound of each branch, DBL_MAX: the branch has no feasible point) goes
+    // to the host for whichever column the branching rule picks; with DTH
+    // the choice uses Tomlin's rounding of delta x_k on integer columns
     __shared__ int sh_jj, sh_next, sh_brk;
-    __shared__ double sh_degrad, sh_dn, sh_up;
-    if (threadIdx.x == 0) { sh_jj = 0; sh_next = 0; sh_degrad = -1.0; sh_dn = 0.0; sh_up = 0.0; sh_brk = 0; }
+    __shared__ double sh_degrad;
+    if (threadIdx.x == 0) { sh_jj = 0; sh_next = 0; sh_degrad = -1.0; sh_brk = 0; }
     __syncthreads();
     int any_frac = 0;
     // visit the basic structural columns in increasing j
@@ -438,10 +643,10 @@ __global__ void __launch_bounds__(256) k_node_lp(NodeProb P, NodeIO io)
             }
         }
         if (threadIdx.x == 0) {
-            if (sh_degrad < dz[0] || sh_degrad < dz[1]) {
+            gdz[2 * j] = dzb[0];
+            gdz[2 * j + 1] = dzb[1];
+            if (P.dth && (sh_degrad < dz[0] || sh_degrad < dz[1])) {
                 sh_jj = j + 1;
-                sh_dn = dzb[0];
-                sh_up = dzb[1];
                 if (dz[0] < dz[1]) { sh_next = -1; sh_degrad = dz[1]; }
                 else { sh_next = +1; sh_degrad = dz[0]; }
                 if (sh_degrad == DBL_MAX) sh_brk = 1;
@@ -452,8 +657,14 @@ __global__ void __launch_bounds__(256) k_node_lp(NodeProb P, NodeIO io)
     }
     if (threadIdx.x == 0) {
         int jj = sh_jj, next = sh_next;
-        double dn = sh_dn, up = sh_up;
-        if (any_frac && sh_degrad < 1e-6 * (1.0 + 0.001 * fabs(z))) {
+        if (!P.dth) {
+            // the host applies the branching rule; report the first candidate
+            jj = 0;
+            for (int j = 0; j < n && !jj; ++j) {
+                const int k = m + j;
+                if (stat[k] == BS && P.isint[j] && fabs(x[k] - floor(x[k] + 0.5)) > P.tol_int) jj = j + 1;
+            }
+        } else if (any_frac && sh_degrad < 1e-6 * (1.0 + 0.001 * fabs(z))) {
             // branch_mostf (glpios09.js:62): value closest to floor + 1/2
             double most = DBL_MAX;
             jj = 0;
@@ -469,16 +680,12 @@ __global__ void __launch_bounds__(256) k_node_lp(NodeProb P, NodeIO io)
                     next = beta < temp ? -1 : +1;
                 }
             }
-            dn = 0.0;
-            up = 0.0;
         }
         io.status[b] = NODE_OPT;
         io.obj[b] = z;
         io.pivots[b] = it;
         io.jj[b] = any_frac ? jj : 0;
         io.next[b] = next;
-        io.dz[2 * b] = dn;
-        io.dz[2 * b + 1] = up;
     }
 #undef T_
 }
@@ -486,7 +693,7 @@ __global__ void __launch_bounds__(256) k_node_lp(NodeProb P, NodeIO io)
 size_t node_lp_lds(int m, int n)
 {
     const size_t N = (size_t)m + n;
-    return sizeof(double) * ((size_t)m * (2 * m + n) + 4 * N + m) + sizeof(int) * m + N + 16;
+    return sizeof(double) * ((size_t)m * (2 * m + n) + 4 * N + m + 6 * ((size_t)m + 1)) + sizeof(int) * m + N + n + 16;
 }
 
 constexpr size_t NODE_LDS_MAX = 64 * 1024;
@@ -540,28 +747,42 @@ struct HostArr {
     }
 };
 
-// an open node: its bound and creation order in the queue, its structural
-// bounds and warm-start basis in a slot of the node pool
+// what a node knows about its parent (the reference keeps it in node.up and
+// in the branching fields of the parent: glpios01.js, glpios03.js:141)
+struct NodeMeta {
+    int level = 0;
+    int br_var = -1;              // column the parent branched on (0-based); -1: root
+    double br_val = 0.0;          // its value in the parent's LP solution (ios_pcost_update)
+    double up_lpobj = 0.0;        // the parent's LP objective (minimisation form)
+    double up_bound = 0.0;        // the parent's local bound (best projection)
+    double up_ii = 0.0;           // the parent's sum of integer infeasibilities
+};
+
+// an open node: its local bound, the selection keys of the backtracking
+// technique (smaller first), creation order and its slot in the node pool
 struct NodeRec {
-    double bound;                 // local bound, minimisation form
-    long long seq;                // creation order (tie-break: older first)
+    double bound;
+    double key, key2;
+    long long seq;
     int slot;
 };
 
-struct NodeCmp {
+struct NodeWorse {                // heap order: a is selected after b
     bool operator()(const NodeRec &a, const NodeRec &b) const
     {
-        if (a.bound != b.bound) return a.bound > b.bound;
+        if (a.key != b.key) return a.key > b.key;
+        if (a.key2 != b.key2) return a.key2 > b.key2;
         return a.seq > b.seq;
     }
 };
 
-// slots of 2 n doubles (lb | ub of the structurals) and m + n statuses,
-// recycled through a free list (no per-node heap allocation)
+// slots of 2 n doubles (lb | ub of the structurals), m + n statuses and the
+// parent information, recycled through a free list
 struct NodePool {
     int n = 0, N = 0;
     std::vector<double> bnd;
     std::vector<signed char> st;
+    std::vector<NodeMeta> meta;
     std::vector<int> freel;
     int alloc()
     {
@@ -570,9 +791,10 @@ struct NodePool {
             freel.pop_back();
             return sl;
         }
-        const int sl = (int)(st.size() / (size_t)N);
+        const int sl = (int)meta.size();
         bnd.resize(bnd.size() + 2 * (size_t)n);
         st.resize(st.size() + (size_t)N);
+        meta.emplace_back();
         return sl;
     }
     void release(int sl) { freel.push_back(sl); }
@@ -581,12 +803,32 @@ struct NodePool {
     signed char *stat(int sl) { return st.data() + (size_t)sl * N; }
 };
 
-// one batch in flight: packed inputs / outputs (one copy each way)
+// one batch entry: a node LP, or a pseudocost probe (a node with one
+// column fixed, 30 dual pivots: eval_degrad, glpios09.js:337)
+struct Entry {
+    int kind;                     // 0 node, 1 probe
+    NodeRec nd;
+    int pid, j, dir;              // probe: parked node, column, 0 down / 1 up
+};
+
+// packed batch buffers (one copy each way): byte offsets for nb entries
+struct Layout {
+    size_t lb, ub, cut, itl, pp, st, in_end;
+    size_t obj, dz, x, bnd, stat, piv, jj, next, sto, out_end;
+    Layout(size_t N, size_t n, size_t nb)
+    {
+        lb = 0; ub = lb + 8 * nb * N; cut = ub + 8 * nb * N; itl = cut + 8 * nb; pp = itl + 4 * nb;
+        st = pp + 4 * nb; in_end = st + nb * N;
+        obj = 0; dz = obj + 8 * nb; x = dz + 16 * nb * n; bnd = x + 8 * nb * N; stat = bnd + 16 * nb * n;
+        piv = stat + 4 * nb; jj = piv + 4 * nb; next = jj + 4 * nb; sto = next + 4 * nb; out_end = sto + nb * N;
+    }
+};
+
 struct BatchBuf {
     DevArr<char> din, dout;
     HostArr<char> hin, hout;
     hipEvent_t done = nullptr;
-    std::vector<NodeRec> nodes;
+    std::vector<Entry> ents;
     int nb = 0;
     ~BatchBuf()
     {
@@ -594,26 +836,76 @@ struct BatchBuf {
     }
 };
 
+// a node whose branching column waits for pseudocost probes (PCH)
+struct Parked {
+    NodeRec nd;
+    NodeMeta meta;
+    double z = 0.0, bound = 0.0, ii = 0.0;
+    std::vector<double> x, bnd;
+    std::vector<double> dzb;             // the kernel's one-pivot branch bounds (ios_eval_degrad)
+    std::vector<double> probe;           // probe[2 j + dir]: degradation from the probe LP
+    std::vector<signed char> so;
+    std::vector<int> cand;
+    int pending = 0;
+};
+
 }  // namespace
 
+// ---------------------------------------------------------------------------
+// one glp_intopt search (ios_driver, glpios03.js:1) on one GPU
+// ---------------------------------------------------------------------------
 struct MipSolver {
+    gk_ctx *ctx = nullptr;
+    hipStream_t s = nullptr;
+    gk_mip *mip = nullptr;
+    const gk_iocp *parm = nullptr;
     int m = 0, n = 0, N = 0;
     double sign = 1.0, c0 = 0.0;
-    std::vector<double> A, c, rlb, rub, clb, cub, coef;
-    std::vector<signed char> isint, fixed_col;
+    std::vector<double> A, c, rlb, rub, clb, cub;
+    std::vector<signed char> isint;
     DevArr<double> dA, dc, dscratch;
     DevArr<signed char> dint;
     BatchBuf bufs[2];
     NodePool pool;
-    int bmax = 0;
-    size_t in_bytes(int nb) const { return (size_t)nb * (2 * (size_t)N + 1) * sizeof(double) + (size_t)nb * N; }
-    size_t out_bytes(int nb) const
+    NodeProb P{};
+    int BMAX = 0;
+    size_t stride = 0;
+    int node_it_lim = 10000;
+    // search state
+    std::vector<NodeRec> open;                // heap (NodeWorse)
+    std::vector<NodeRec> dive, next_dive;     // preferred children (T.child): evaluated in the next batch
+    long long seq = 0;
+    bool have = false;                        // incumbent of this rank (with x)
+    double best = DBL_MAX, gbest = DBL_MAX;   // minimisation form; gbest: best over all ranks
+    std::vector<double> xbest;
+    long long lp_solves = 0, pivots = 0, created = 1, fallbacks = 0, probes = 0, pp_fathomed = 0;
+    int err = 0;                              // GLP_EFAIL: a node LP could not be solved at all
+    bool root_seen = false;
+    double root_bound = 0.0, root_ii = 0.0;   // best projection (glpios12.js:19)
+    // pseudocosts (ios_pcost_init, glpios09.js:272)
+    bool pcost_on = false;
+    std::vector<int> dn_cnt, up_cnt;
+    std::vector<double> dn_sum, up_sum;
+    std::vector<Parked> parked;
+    std::vector<int> parked_free;
+    std::vector<Entry> probeq;
+    // engine fallback (ios_solve_node with glp_simplex, glpios01.js:866)
+    gk_bfd *fb = nullptr;
+    unsigned long long fb_version = 0;
+    // ios_round_bound (glpios01.js:730): objective integrality
+    bool round_ok = false;
+    double round_s = 0.0, round_d = 1.0;
+
+    ~MipSolver()
     {
-        return (size_t)nb * (3 + (size_t)N) * sizeof(double) + 4 * (size_t)nb * sizeof(int) + (size_t)nb * N;
+        if (fb) gk_bfd_destroy(fb);
     }
+
+    size_t in_bytes(int nb) const { return Layout(N, n, nb).in_end; }
+    size_t out_bytes(int nb) const { return Layout(N, n, nb).out_end; }
     bool alloc_batch(int B)
     {
-        bmax = B;
+        BMAX = B;
         for (auto &bf : bufs) {
             bf.din.ensure(in_bytes(B) + 64); bf.dout.ensure(out_bytes(B) + 64);
             bf.hin.ensure(in_bytes(B) + 64); bf.hout.ensure(out_bytes(B) + 64);
@@ -622,22 +914,394 @@ struct MipSolver {
         }
         return true;
     }
-    // ios_round_bound (glpios01.js:730): objective integrality
-    bool round_ok = false;
-    double round_s = 0.0, round_d = 1.0;
 
     // min-form bound -> rounded min-form bound
     double round_bound(double z) const
     {
-        if (!round_ok) return z;
+        if (!round_ok || z == DBL_MAX || z == -DBL_MAX) return z;
         // the reference rounds in the original direction; in minimisation
         // form both cases are "round up" of (bound - s) / d
-        const double s = sign * (round_s - c0), d = round_d;
-        const double h = (z - s) / d;
-        if (h >= std::floor(h) + 0.001) return d * std::ceil(h) + s;
+        const double s0 = sign * (round_s - c0), d = round_d;
+        const double h = (z - s0) / d;
+        if (h >= std::floor(h) + 0.001) return d * std::ceil(h) + s0;
         return z;
     }
+    double bestall() const { return std::min(best, gbest); }
+    // ios_is_hopeful (glpios01.js:789)
+    bool hopeful(double bound) const
+    {
+        const double b = bestall();
+        if (b == DBL_MAX) return true;
+        const double eps = parm->tol_obj * (1.0 + std::fabs(c0 + sign * b));
+        return bound < b - eps;
+    }
+
+    // ---- node selection (ios_choose_node, glpios12.js:2) -----------------
+    void set_keys(NodeRec &r) const
+    {
+        const NodeMeta &mt = pool.meta[r.slot];
+        r.key2 = 0.0;
+        switch (parm->bt_tech) {
+        case 1: r.key = -(double)r.seq; break;                      // DFS: the newest node (T.tail)
+        case 2: r.key = (double)r.seq; break;                       // BFS: the oldest node (T.head)
+        case 4:                                                     // BPH
+            if (bestall() == DBL_MAX || !root_seen || root_ii <= 0.0) r.key = mt.up_ii;   // most_feas
+            else r.key = mt.up_bound + (bestall() - root_bound) / root_ii * mt.up_ii;  // best_proj
+            break;
+        default:                                                    // BLB: best local bound,
+            r.key = r.bound;                                        // then the parent's ii_sum
+            r.key2 = mt.up_ii;
+            break;
+        }
+    }
+    void push_open(NodeRec r)
+    {
+        set_keys(r);
+        open.push_back(r);
+        std::push_heap(open.begin(), open.end(), NodeWorse());
+    }
+    NodeRec pop_open()
+    {
+        std::pop_heap(open.begin(), open.end(), NodeWorse());
+        NodeRec r = open.back();
+        open.pop_back();
+        return r;
+    }
+    // the best projection keys depend on the incumbent
+    void rekey()
+    {
+        if (parm->bt_tech != 4) return;
+        for (NodeRec &r : open) set_keys(r);
+        std::make_heap(open.begin(), open.end(), NodeWorse());
+    }
+    void new_incumbent(double z, const double *x)
+    {
+        const double before = bestall();
+        have = true;
+        best = z;
+        std::memcpy(xbest.data(), x, N * sizeof(double));
+        if (bestall() != before) rekey();
+    }
+    void set_gbest(double b)
+    {
+        if (b < gbest) {
+            gbest = b;
+            rekey();
+        }
+    }
+
+    // check_integrality (glpios03.js:55): fractional integer columns and the
+    // sum of integer infeasibilities, on the node's own (possibly tightened)
+    // column bounds
+    int integrality(const double *x, const signed char *so, const double *bl, const double *bu,
+                    std::vector<int> &cand, double &ii_sum) const
+    {
+        cand.clear();
+        ii_sum = 0.0;
+        const double tol = parm->tol_int;
+        for (int j = 0; j < n; j++) {
+            if (!isint[j] || so[m + j] != BS) continue;
+            const double v = x[m + j], l = bl[j], u = bu[j];
+            if (l != -DBL_MAX) {
+                if (l - tol <= v && v <= l + tol) continue;
+                if (v < l) continue;
+            }
+            if (u != DBL_MAX) {
+                if (u - tol <= v && v <= u + tol) continue;
+                if (v > u) continue;
+            }
+            const double r = std::floor(v + 0.5);
+            if (r - tol <= v && v <= r + tol) continue;
+            cand.push_back(j);
+            const double t1 = v - std::floor(v), t2 = std::ceil(v) - v;
+            ii_sum += (t1 <= t2 ? t1 : t2);
+        }
+        return (int)cand.size();
+    }
+
+    // branch_first / branch_last / branch_mostf (glpios09.js:28-82); next:
+    // -1 down, +1 up
+    static int next_of(double beta) { return (beta - std::floor(beta) < std::ceil(beta) - beta) ? -1 : +1; }
+    int choose_simple(int tech, const std::vector<int> &cand, const double *x, int &next) const
+    {
+        if (tech == 1 || tech == 2) {
+            const int j = tech == 1 ? cand.front() : cand.back();
+            next = next_of(x[m + j]);
+            return j;
+        }
+        int jj = -1;
+        double most = DBL_MAX;
+        for (int j : cand) {
+            const double beta = x[m + j], temp = std::floor(beta) + 0.5;
+            if (most > std::fabs(beta - temp)) {
+                jj = j;
+                most = std::fabs(beta - temp);
+                next = beta < temp ? -1 : +1;
+            }
+        }
+        return jj;
+    }
+
+    // ios_pcost_branch (glpios09.js:336) over pseudocosts that are all
+    // initialised (probe[] holds the probes of this node, DBL_MAX: that
+    // branch has no feasible point); returns the column, next through *next
+    int choose_pcost(const std::vector<int> &cand, const double *x, const double *probe, int &next)
+    {
+        int jjj = -1;
+        double dmax = -1.0;
+        for (int j : cand) {
+            const double beta = x[m + j];
+            double psi;
+            if (dn_cnt[j] == 0) {
+                const double dg = probe[2 * j];
+                if (dg == DBL_MAX) { next = -1; return j; }
+                dn_cnt[j] = 1;
+                dn_sum[j] = dg / (beta - std::floor(beta));
+            }
+            psi = dn_sum[j] / dn_cnt[j];
+            const double d1 = psi * (beta - std::floor(beta));
+            if (up_cnt[j] == 0) {
+                const double dg = probe[2 * j + 1];
+                if (dg == DBL_MAX) { next = +1; return j; }
+                up_cnt[j] = 1;
+                up_sum[j] = dg / (std::ceil(beta) - beta);
+            }
+            psi = up_sum[j] / up_cnt[j];
+            const double d2 = psi * (std::ceil(beta) - beta);
+            const double d = d1 > d2 ? d1 : d2;
+            if (dmax < d) {
+                dmax = d;
+                jjj = j;
+                next = d1 <= d2 ? -1 : +1;
+            }
+        }
+        if (dmax == 0.0) return choose_simple(3, cand, x, next);
+        return jjj;
+    }
+
+    // branch_on (glpios03.js:141): the two children, the preferred one
+    // (T.child) first into the next batch
+    void branch(const NodeRec &nd, const NodeMeta &mt, double z, double bound, double ii, const double *x,
+                const signed char *so, const double *bl, const double *bu, int j, int next, double dn, double up)
+    {
+        const double beta = x[m + j];
+        const double dz[2] = {dn, up};
+        const int first = next < 0 ? 0 : 1;
+        bool dived = false;
+        for (int r = 0; r < 2; r++) {
+            const int kase = (r == 0) ? first : 1 - first;
+            if (dz[kase] == DBL_MAX) continue;        // that branch has no feasible point
+            const double cb = std::max(bound, round_bound(z + dz[kase]));
+            if (!hopeful(cb)) continue;
+            const int sl = pool.alloc();
+            std::memcpy(pool.lb(sl), bl, n * sizeof(double));
+            std::memcpy(pool.ub(sl), bu, n * sizeof(double));
+            if (kase == 0) pool.ub(sl)[j] = std::floor(beta);
+            else pool.lb(sl)[j] = std::ceil(beta);
+            signed char *cs = pool.stat(sl);
+            std::memcpy(cs, so, N);
+            for (int q = 0; q < n; q++) {             // statuses follow the column types (glp_set_col_bnds)
+                if (cs[m + q] == BS) continue;
+                const double l = pool.lb(sl)[q], u = pool.ub(sl)[q];
+                if (l == u) cs[m + q] = NS;
+                else if (cs[m + q] == NS) cs[m + q] = (l != -DBL_MAX) ? NL : (u != DBL_MAX ? NU : NF);
+            }
+            NodeMeta &cm = pool.meta[sl];
+            cm.level = mt.level + 1;
+            cm.br_var = j;
+            cm.br_val = beta;
+            cm.up_lpobj = z;
+            cm.up_bound = bound;
+            cm.up_ii = ii;
+            NodeRec c{cb, 0.0, 0.0, seq++, sl};
+            set_keys(c);
+            if (!dived) {
+                next_dive.push_back(c);
+                dived = true;
+            } else
+                push_open(c);
+            created++;
+        }
+    }
+
+    // the result of one node LP (kernel or fallback): incumbent, pruning,
+    // branching (ios_driver's "analyze" part, glpios03.js:670-905)
+    // returns true when the node is parked (its pool slot stays in use)
+    bool node_done(const NodeRec &nd, double z, const double *x, const signed char *so, const double *bl,
+                   const double *bu, const double *dzb, int kjj, int knext, bool tableau)
+    {
+        const NodeMeta mt = pool.meta[nd.slot];
+        // ios_pcost_update (glpios09.js:288)
+        if (pcost_on && mt.br_var >= 0) {
+            const double dx = x[m + mt.br_var] - mt.br_val;
+            if (dx != 0.0) {
+                const double psi = std::fabs((z - mt.up_lpobj) / dx);
+                if (dx < 0.0) { dn_cnt[mt.br_var]++; dn_sum[mt.br_var] += psi; }
+                else { up_cnt[mt.br_var]++; up_sum[mt.br_var] += psi; }
+            }
+        }
+        const double bound = std::max(nd.bound, round_bound(z));
+        if (!hopeful(bound)) return false;
+        std::vector<int> cand;
+        double ii = 0.0;
+        if (integrality(x, so, bl, bu, cand, ii) == 0) {
+            if (!have || z < best) new_incumbent(z, x);
+            return false;
+        }
+        if (mt.level == 0 && !root_seen) {
+            root_seen = true;
+            root_bound = bound;
+            root_ii = ii;
+        }
+        int j = -1, next = 0;
+        switch (parm->br_tech) {
+        case 1: case 2: case 3:
+            j = choose_simple(parm->br_tech, cand, x, next);
+            break;
+        case 5:
+            if (!tableau) { j = choose_simple(3, cand, x, next); break; }
+            if (!pcost_on) {
+                pcost_on = true;
+                dn_cnt.assign(n, 0); up_cnt.assign(n, 0); dn_sum.assign(n, 0.0); up_sum.assign(n, 0.0);
+            }
+            {
+                // probes for the pseudocosts still missing (eval_psi :397),
+                // solved in the next batches; the node waits parked
+                std::vector<std::pair<int, int>> need;
+                for (int q : cand) {
+                    if (dn_cnt[q] == 0) need.emplace_back(q, 0);
+                    if (up_cnt[q] == 0) need.emplace_back(q, 1);
+                }
+                if (!need.empty()) {
+                    int pid;
+                    if (!parked_free.empty()) { pid = parked_free.back(); parked_free.pop_back(); }
+                    else { pid = (int)parked.size(); parked.emplace_back(); }
+                    Parked &pk = parked[pid];
+                    pk.nd = nd; pk.meta = mt; pk.z = z; pk.bound = bound; pk.ii = ii;
+                    pk.x.assign(x, x + N);
+                    pk.so.assign(so, so + N);
+                    pk.bnd.resize(2 * (size_t)n);
+                    std::memcpy(pk.bnd.data(), bl, n * sizeof(double));
+                    std::memcpy(pk.bnd.data() + n, bu, n * sizeof(double));
+                    pk.dzb.assign(dzb, dzb + 2 * (size_t)n);
+                    pk.probe.assign(2 * (size_t)n, 0.0);
+                    pk.cand = cand;
+                    pk.pending = (int)need.size();
+                    for (auto &pr : need) {
+                        Entry e{};
+                        e.kind = 1; e.nd = nd; e.pid = pid; e.j = pr.first; e.dir = pr.second;
+                        probeq.push_back(e);
+                    }
+                    return true;                      // the slot stays alive while parked
+                }
+                j = choose_pcost(cand, x, nullptr, next);
+            }
+            break;
+        default:                                      // DTH: the kernel's choice on the tableau
+            if (kjj > 0 && std::find(cand.begin(), cand.end(), kjj - 1) != cand.end()) { j = kjj - 1; next = knext; }
+            else j = choose_simple(3, cand, x, next);
+            break;
+        }
+        const double dn = tableau ? dzb[2 * j] : 0.0, up = tableau ? dzb[2 * j + 1] : 0.0;
+        branch(nd, mt, z, bound, ii, x, so, bl, bu, j, next, dn, up);
+        return false;
+    }
+
+    void parked_done(int pid)
+    {
+        Parked &pk = parked[pid];
+        int next = 0;
+        const int j = choose_pcost(pk.cand, pk.x.data(), pk.probe.data(), next);
+        const double *bl = pk.bnd.data(), *bu = pk.bnd.data() + n;
+        const double dn = pk.dzb[2 * j], up = pk.dzb[2 * j + 1];
+        branch(pk.nd, pk.meta, pk.z, pk.bound, pk.ii, pk.x.data(), pk.so.data(), bl, bu, j, next, dn, up);
+        parked_free.push_back(pid);
+    }
+
+    // ios_solve_node with the full engine (glp_simplex, meth = GLP_DUALP,
+    // the incumbent as objective limit): a node LP the batched kernel could
+    // not finish.  Returns 0 solved (OPT: *opt = true), 0 fathomed, or
+    // GLP_EFAIL.
+    int fallback(const NodeRec &nd, const double *bl, const double *bu, std::vector<double> &x,
+                 std::vector<signed char> &so, double &z, bool &opt);
 };
+
+int gk_spx_node(gk_ctx *ctx, gk_lp *lp, gk_bfd *bfd, const gk_smcp *parm);
+
+int MipSolver::fallback(const NodeRec &nd, const double *bl, const double *bu, std::vector<double> &x,
+                        std::vector<signed char> &so, double &z, bool &opt)
+{
+    const gk_lp &R = mip->lp;
+    opt = false;
+    fallbacks++;
+    if (!fb) {
+        fb = gk_bfd_create(ctx);
+        if (!fb) return 5;
+        static unsigned long long ver = 0;
+        fb_version = (1ull << 62) | ++ver;        // A uploaded once per search
+    }
+    std::vector<signed char> ctype(n + 1), rstat(m + 1), cstat(n + 1);
+    std::vector<double> clo(n + 1, 0.0), cup(n + 1, 0.0);
+    std::vector<int> head(m + 1), rbind(m + 1), cbind(n + 1);
+    std::vector<double> rprim(m + 1), rdual(m + 1), cprim(n + 1), cdual(n + 1);
+    for (int j = 0; j < n; j++) {
+        const double l = bl[j], u = bu[j];
+        ctype[j + 1] = (l == -DBL_MAX && u == DBL_MAX) ? 1 : (u == DBL_MAX ? 2 : (l == -DBL_MAX ? 3 : (l != u ? 4 : 5)));
+        clo[j + 1] = l == -DBL_MAX ? 0.0 : l;
+        cup[j + 1] = u == DBL_MAX ? 0.0 : u;
+    }
+    gk_smcp sp{};
+    sp.msg_lev = 1; sp.meth = 2; sp.pricing = 0x22; sp.r_test = 0x22;     // GLP_MSG_ERR, GLP_DUALP, PSE, Harris
+    sp.tol_bnd = 1e-7; sp.tol_dj = 1e-7; sp.tol_piv = 1e-10;
+    sp.obj_ll = -DBL_MAX; sp.obj_ul = DBL_MAX;
+    if (bestall() != DBL_MAX) {
+        const double mo = c0 + sign * bestall();
+        if (sign > 0) sp.obj_ul = mo; else sp.obj_ll = mo;
+    }
+    sp.it_lim = 0x7fffffff; sp.tm_lim = 0x7fffffff; sp.out_frq = 500; sp.out_dly = 0;
+    for (int attempt = 0; attempt < 2; attempt++) {
+        const signed char *st0 = pool.stat(nd.slot);
+        for (int i = 0; i < m; i++) rstat[i + 1] = attempt == 0 ? st0[i] : (signed char)BS;
+        for (int j = 0; j < n; j++) {
+            signed char v = attempt == 0 ? st0[m + j] : (signed char)NL;
+            if (v != BS) {                            // statuses consistent with the node's column types
+                const int t = ctype[j + 1];
+                if (t == 5) v = NS;
+                else if (t == 1) v = NF;
+                else if (t == 2) v = NL;
+                else if (t == 3) v = NU;
+                else if (v != NL && v != NU) v = NL;
+            }
+            cstat[j + 1] = v;
+        }
+        int k = 0;
+        for (int i = 1; i <= m; i++) if (rstat[i] == BS && k < m) head[++k] = i;
+        for (int j = 1; j <= n; j++) if (cstat[j] == BS && k < m) head[++k] = m + j;
+        if (k != m) continue;
+        gk_lp L{};
+        L.m = m; L.n = n; L.nnz = R.nnz; L.dir = R.dir; L.c0 = R.c0;
+        L.row_type = R.row_type; L.row_lb = R.row_lb; L.row_ub = R.row_ub; L.rii = R.rii;
+        L.col_type = ctype.data(); L.col_lb = clo.data(); L.col_ub = cup.data(); L.col_coef = R.col_coef; L.sjj = R.sjj;
+        L.A_ptr = R.A_ptr; L.A_ind = R.A_ind; L.A_val = R.A_val; L.a_version = fb_version;
+        L.head = head.data(); L.row_stat = rstat.data(); L.col_stat = cstat.data();
+        L.row_bind = rbind.data(); L.col_bind = cbind.data();
+        L.row_prim = rprim.data(); L.row_dual = rdual.data(); L.col_prim = cprim.data(); L.col_dual = cdual.data();
+        const int ret = gk_spx_node(ctx, &L, fb, &sp);
+        if (ret == 6 || ret == 7) return 0;           // GLP_EOBJLL / EOBJUL: no better than the incumbent
+        if (ret != 0) continue;
+        if (L.dbs_stat != 2) break;                   // no dual feasible solution: the reference fails here
+        if (L.pbs_stat != 2) return 0;                // infeasible, or no better than the incumbent
+        x.assign(N, 0.0);
+        so.assign(N, 0);
+        for (int i = 0; i < m; i++) { x[i] = rprim[i + 1]; so[i] = rstat[i + 1]; }
+        for (int j = 0; j < n; j++) { x[m + j] = cprim[j + 1]; so[m + j] = cstat[j + 1]; }
+        z = sign * (L.obj_val - c0);
+        pivots += L.it_cnt;
+        opt = true;
+        return 0;
+    }
+    return 5;                                         // GLP_EFAIL (ios_driver, glpios03.js:669-673)
+}
 
 static void setup_rounding(MipSolver &S, const gk_mip *mip)
 {
@@ -669,6 +1333,111 @@ static void setup_rounding(MipSolver &S, const gk_mip *mip)
     S.round_d = (double)g;
 }
 
+// ---------------------------------------------------------------------------
+// open-node exchange between ranks: at every sync epoch
+// the ranks all-gather {incumbent, best open bound, open nodes, active};
+// every rank derives the same plan from it — idle ranks paired with the
+// ranks holding the most open nodes, each donor handing over up to half of
+// its queue (at most XFER_MAX nodes, best first) — and the node descriptors
+// (bounds, warm-start basis, parent information) travel in one more
+// all-gather of fixed-size blocks.
+// ---------------------------------------------------------------------------
+struct ShardMsg {
+    double best, bound;
+    long long open;
+    int active, pad;
+};
+constexpr int XFER_MAX = 32;
+
+static size_t desc_bytes(int n, int N)
+{
+    return (((size_t)6 * 8 + 2 * 4 + 16 * (size_t)n + (size_t)N) + 7) & ~(size_t)7;
+}
+
+static void put_desc(MipSolver &S, const NodeRec &r, char *p)
+{
+    const NodeMeta &mt = S.pool.meta[r.slot];
+    double *d = (double *)p;
+    d[0] = r.bound; d[1] = mt.br_val; d[2] = mt.up_lpobj; d[3] = mt.up_bound; d[4] = mt.up_ii; d[5] = 0.0;
+    int *iv = (int *)(d + 6);
+    iv[0] = mt.level; iv[1] = mt.br_var;
+    double *bl = (double *)(iv + 2);
+    std::memcpy(bl, S.pool.lb(r.slot), S.n * sizeof(double));
+    std::memcpy(bl + S.n, S.pool.ub(r.slot), S.n * sizeof(double));
+    std::memcpy((char *)(bl + 2 * S.n), S.pool.stat(r.slot), S.N);
+}
+
+static void get_desc(MipSolver &S, const char *p)
+{
+    const double *d = (const double *)p;
+    const int sl = S.pool.alloc();
+    NodeMeta &mt = S.pool.meta[sl];
+    mt.br_val = d[1]; mt.up_lpobj = d[2]; mt.up_bound = d[3]; mt.up_ii = d[4];
+    const int *iv = (const int *)(d + 6);
+    mt.level = iv[0]; mt.br_var = iv[1];
+    const double *bl = (const double *)(iv + 2);
+    std::memcpy(S.pool.lb(sl), bl, S.n * sizeof(double));
+    std::memcpy(S.pool.ub(sl), bl + S.n, S.n * sizeof(double));
+    std::memcpy(S.pool.stat(sl), (const char *)(bl + 2 * S.n), S.N);
+    S.push_open(NodeRec{d[0], 0.0, 0.0, S.seq++, sl});
+}
+
+// one sync epoch; returns the number of ranks with work (0 ends the run) or
+// -1 when a collective failed
+static int shard_epoch(MipSolver &S, const gk_ios_shard *sh, bool have_work, long long &moved)
+{
+    const int size = sh->size, rank = sh->rank;
+    ShardMsg me{};
+    me.best = S.best;
+    me.bound = DBL_MAX;
+    for (const NodeRec &r : S.open) me.bound = std::min(me.bound, r.bound);
+    for (const NodeRec &r : S.dive) me.bound = std::min(me.bound, r.bound);
+    me.open = (long long)S.open.size();
+    me.active = have_work ? 1 : 0;
+    std::vector<ShardMsg> all(size);
+    if (sh->allgather(sh->info, &me, sizeof me, all.data()) != 0) return -1;
+    int nact = 0;
+    double gb = DBL_MAX;
+    for (const ShardMsg &x : all) {
+        nact += x.active;
+        gb = std::min(gb, x.best);
+    }
+    S.set_gbest(gb);
+    if (nact == 0) return 0;
+    // the plan (identical on every rank)
+    std::vector<int> idle, donors;
+    for (int r = 0; r < size; r++) {
+        if (!all[r].active && all[r].open == 0) idle.push_back(r);
+        else if (all[r].open >= 2) donors.push_back(r);
+    }
+    std::stable_sort(donors.begin(), donors.end(), [&](int a, int b) { return all[a].open > all[b].open; });
+    const int pairs = (int)std::min(idle.size(), donors.size());
+    if (pairs == 0) return nact;
+    const size_t db = desc_bytes(S.n, S.N), blk = 16 + XFER_MAX * db;
+    std::vector<char> send(blk, 0), recv(blk * size);
+    int *hdr = (int *)send.data();
+    hdr[0] = 0; hdr[1] = -1;
+    for (int k = 0; k < pairs; k++) {
+        if (donors[k] != rank) continue;
+        const int give = (int)std::min<long long>(XFER_MAX, all[rank].open / 2);
+        hdr[1] = idle[k];
+        for (int g = 0; g < give && !S.open.empty(); g++) {
+            const NodeRec r = S.pop_open();
+            put_desc(S, r, send.data() + 16 + g * db);
+            S.pool.release(r.slot);
+            hdr[0]++;
+        }
+    }
+    if (sh->allgather(sh->info, send.data(), blk, recv.data()) != 0) return -1;
+    for (int r = 0; r < size; r++) {
+        const int *h = (const int *)(recv.data() + r * blk);
+        if (h[1] != rank) continue;
+        for (int g = 0; g < h[0]; g++) get_desc(S, recv.data() + r * blk + 16 + g * db);
+        moved += h[0];
+    }
+    return nact + pairs;                  // receivers have work now
+}
+
 }  // namespace gk
 
 using namespace gk;
@@ -685,11 +1454,17 @@ extern "C" int gk_ios_driver_sharded(gk_ctx *ctx, gk_mip *mip, const gk_iocp *pa
 {
     if (!ctx || !mip || !parm) { set_err("gk_ios_driver: null argument"); return GK_EABI; }
     const int rank = shard ? shard->rank : 0, size = shard ? shard->size : 1;
-    if (size < 1 || rank < 0 || rank >= size || (size > 1 && !shard->exchange)) {
+    if (size < 1 || rank < 0 || rank >= size || (size > 1 && !shard->exchange && !shard->allgather)) {
         set_err("gk_ios_driver: invalid shard %d of %d", rank, size);
         return GK_EABI;
     }
-    const int ramp = (shard && shard->ramp_nodes > 0) ? shard->ramp_nodes : 8;
+    // glp_intopt's parameter checks (glpapi09.js:240-262)
+    if (parm->br_tech < 1 || parm->br_tech > 5) { set_err("glp_intopt: br_tech = %d; invalid parameter", parm->br_tech); return GK_EABI; }
+    if (parm->bt_tech < 1 || parm->bt_tech > 4) { set_err("glp_intopt: bt_tech = %d; invalid parameter", parm->bt_tech); return GK_EABI; }
+    if (parm->pp_tech < 0 || parm->pp_tech > 2) { set_err("glp_intopt: pp_tech = %d; invalid parameter", parm->pp_tech); return GK_EABI; }
+    // ramp_nodes < 0: split the root alone (rank 0 starts with all the work;
+    // exercises the open-node exchange)
+    const int ramp = (shard && shard->ramp_nodes < 0) ? 0 : ((shard && shard->ramp_nodes > 0) ? shard->ramp_nodes : 8);
     const int sync_every = (shard && shard->sync_every > 0) ? shard->sync_every : 4;
     const gk_lp &L = mip->lp;
     const int m = L.m, n = L.n;
@@ -710,9 +1485,15 @@ extern "C" int gk_ios_driver_sharded(gk_ctx *ctx, gk_mip *mip, const gk_iocp *pa
     hipStream_t s = gk_ctx_stream(ctx);
     const auto t0 = std::chrono::steady_clock::now();
     MipSolver S;
+    S.ctx = ctx; S.s = s; S.mip = mip; S.parm = parm;
     S.m = m; S.n = n; S.N = m + n;
     S.sign = (L.dir == 1) ? 1.0 : -1.0;                   // GLP_MIN = 1
     S.c0 = L.c0;
+    S.xbest.assign(S.N, 0.0);
+    if (const char *e = std::getenv("GK_TEST_NODE_IT_LIM")) {   // test knob: force node LPs onto the fallback
+        const int v = std::atoi(e);
+        if (v >= 0) S.node_it_lim = v;
+    }
     const double INF = DBL_MAX;
     S.rlb.resize(m); S.rub.resize(m); S.clb.resize(n); S.cub.resize(n);
     auto bnds = [&](int type, double lb, double ub, double &l, double &u) {
@@ -743,9 +1524,9 @@ extern "C" int gk_ios_driver_sharded(gk_ctx *ctx, gk_mip *mip, const gk_iocp *pa
     // device problem
     S.dA.ensure(S.A.size()); S.dc.ensure(S.N); S.dint.ensure(n);
     const int BMAX = (lds <= NODE_LDS_MAX) ? 1024 : (int)std::max<size_t>(1, std::min<size_t>(1024, SCRATCH_MAX / lds));
-    const size_t stride = (lds + 255) / 256 * 32;          // doubles, 256-byte aligned slices
+    S.stride = (lds + 255) / 256 * 32;                    // doubles, 256-byte aligned slices
     if (lds > NODE_LDS_MAX) {
-        S.dscratch.ensure(stride * BMAX);
+        S.dscratch.ensure(S.stride * BMAX);
         if (!S.dscratch.p) { set_err("gk_ios_driver: out of memory (node work area)"); return GK_EABI; }
     }
     if (!S.alloc_batch(BMAX) || !S.dA.p || !S.dc.p || !S.dint.p) {
@@ -755,13 +1536,12 @@ extern "C" int gk_ios_driver_sharded(gk_ctx *ctx, gk_mip *mip, const gk_iocp *pa
     (void)hipMemcpyAsync(S.dA.p, S.A.data(), S.A.size() * sizeof(double), hipMemcpyHostToDevice, s);
     (void)hipMemcpyAsync(S.dc.p, S.c.data(), S.N * sizeof(double), hipMemcpyHostToDevice, s);
     (void)hipMemcpyAsync(S.dint.p, S.isint.data(), n, hipMemcpyHostToDevice, s);
-    NodeProb P;
+    NodeProb &P = S.P;
     P.m = m; P.n = n; P.ld = S.N; P.A = S.dA.p; P.c = S.dc.p; P.isint = S.dint.p; P.tol_int = parm->tol_int;
+    P.dth = (parm->br_tech == 4) ? 1 : 0;
     NodePool &pool = S.pool;
     pool.n = n; pool.N = S.N;
     // root node: the optimal basis of the initial LP relaxation
-    std::priority_queue<NodeRec, std::vector<NodeRec>, NodeCmp> open;
-    long long seq = 0;
     {
         const int sl = pool.alloc();
         std::memcpy(pool.lb(sl), S.clb.data(), n * sizeof(double));
@@ -769,120 +1549,127 @@ extern "C" int gk_ios_driver_sharded(gk_ctx *ctx, gk_mip *mip, const gk_iocp *pa
         signed char *st = pool.stat(sl);
         for (int i = 0; i < m; i++) st[i] = L.row_stat[i + 1];
         for (int j = 0; j < n; j++) st[m + j] = L.col_stat[j + 1];
-        open.push(NodeRec{-INF, seq++, sl});
+        pool.meta[sl] = NodeMeta{};
+        S.push_open(NodeRec{-INF, 0.0, 0.0, S.seq++, sl});
     }
-    bool have = false;                                    // incumbent of this rank (with x)
-    double best = INF;                                    // its objective, minimisation form
-    double gbest = INF;                                   // best over all ranks (sharded runs)
-    std::vector<double> xbest(S.N, 0.0);
-    long long lp_solves = 0, pivots = 0, created = 1, failed = 0;
-    auto bestall = [&]() { return std::min(best, gbest); };
-    auto hopeful = [&](double bound) {
-        const double b = bestall();
-        if (b == INF) return true;
-        const double eps = parm->tol_obj * (1.0 + std::fabs(S.c0 + S.sign * b));
-        return bound < b - eps;
+    // ios_preprocess_node passes of a node (glpios03.js:643-656)
+    auto pp_passes = [&](int level) {
+        if (parm->pp_tech == 2) return level == 0 ? 100 : 10;
+        if (parm->pp_tech == 1) return level == 0 ? 100 : 0;
+        return 0;
     };
-    // the preferred child of every branched node of a batch is evaluated in
-    // the next batch assembled (parallel dives, as BLB dives into its chosen
-    // child, glpios12.js); the other children wait in the best-bound queue
-    std::vector<NodeRec> dive, next_dive;
     // single GPU: two batches in flight — the host assembles and launches
     // batch k + 1 before it processes the results of batch k (more
     // speculative nodes, the GPU never waits for the host)
     const int depth = (size == 1) ? 2 : 1;
     int inflight[2] = {0, 0}, cur = 0;
     bool fail_sync = false;
+    long long moved = 0;
     auto launch = [&](BatchBuf &bf) {
-        const int nb = (int)bf.nodes.size();
+        const int nb = (int)bf.ents.size();
         bf.nb = nb;
-        const double ball = bestall();
+        const double ball = S.bestall();
         const double cut = ball < INF ? ball - parm->tol_obj * (1.0 + std::fabs(S.c0 + S.sign * ball)) : INF;
-        const size_t NB = (size_t)nb * S.N;
-        double *hl = (double *)bf.hin.p, *hu = hl + NB, *hc = hu + NB;
-        signed char *hs = (signed char *)(hc + nb);
+        const Layout Y(S.N, n, nb);
+        char *h = bf.hin.p;
+        double *hl = (double *)(h + Y.lb), *hu = (double *)(h + Y.ub), *hc = (double *)(h + Y.cut);
+        int *hit = (int *)(h + Y.itl), *hpp = (int *)(h + Y.pp);
+        signed char *hs = (signed char *)(h + Y.st);
         for (int b = 0; b < nb; b++) {
-            const int sl = bf.nodes[b].slot;
+            const Entry &e = bf.ents[b];
             double *l = hl + (size_t)b * S.N, *u = hu + (size_t)b * S.N;
             std::memcpy(l, S.rlb.data(), m * sizeof(double));
             std::memcpy(u, S.rub.data(), m * sizeof(double));
-            std::memcpy(l + m, pool.lb(sl), n * sizeof(double));
-            std::memcpy(u + m, pool.ub(sl), n * sizeof(double));
-            std::memcpy(hs + (size_t)b * S.N, pool.stat(sl), S.N);
-            hc[b] = cut;
+            if (e.kind == 0) {
+                const int sl = e.nd.slot;
+                std::memcpy(l + m, pool.lb(sl), n * sizeof(double));
+                std::memcpy(u + m, pool.ub(sl), n * sizeof(double));
+                std::memcpy(hs + (size_t)b * S.N, pool.stat(sl), S.N);
+                hc[b] = cut;
+                hit[b] = S.node_it_lim;
+                hpp[b] = pp_passes(pool.meta[sl].level);
+            } else {
+                // eval_degrad (glpios09.js:337): x_j fixed at floor / ceil,
+                // 30 dual pivots from the node's optimal basis
+                const Parked &pk = S.parked[e.pid];
+                std::memcpy(l + m, pk.bnd.data(), n * sizeof(double));
+                std::memcpy(u + m, pk.bnd.data() + n, n * sizeof(double));
+                const double beta = pk.x[m + e.j], v = e.dir == 0 ? std::floor(beta) : std::ceil(beta);
+                l[m + e.j] = u[m + e.j] = v;
+                std::memcpy(hs + (size_t)b * S.N, pk.so.data(), S.N);
+                hc[b] = INF;
+                hit[b] = 30;
+                hpp[b] = 0;
+            }
         }
-        (void)hipMemcpyAsync(bf.din.p, bf.hin.p, S.in_bytes(nb), hipMemcpyHostToDevice, s);
-        double *dl = (double *)bf.din.p, *du = dl + NB, *dc = du + NB;
-        double *dobj = (double *)bf.dout.p, *ddz = dobj + nb, *dx = ddz + 2 * (size_t)nb;
-        int *dstat = (int *)(dx + NB), *dpiv = dstat + nb, *djj = dpiv + nb, *dnext = djj + nb;
+        (void)hipMemcpyAsync(bf.din.p, bf.hin.p, Y.in_end, hipMemcpyHostToDevice, s);
+        char *din = bf.din.p, *dout = bf.dout.p;
         NodeIO io;
-        io.lb = dl; io.ub = du; io.stat_in = (const signed char *)(dc + nb); io.cutoff = dc;
-        io.status = dstat; io.pivots = dpiv; io.jj = djj; io.next = dnext;
-        io.obj = dobj; io.x = dx; io.dz = ddz; io.stat_out = (signed char *)(dnext + nb);
-        io.it_lim = 10000;
+        io.lb = (const double *)(din + Y.lb); io.ub = (const double *)(din + Y.ub);
+        io.cutoff = (const double *)(din + Y.cut); io.it_lim = (const int *)(din + Y.itl);
+        io.pp_pass = (const int *)(din + Y.pp); io.stat_in = (const signed char *)(din + Y.st);
+        io.obj_bound = ball;
+        io.obj = (double *)(dout + Y.obj); io.dzb = (double *)(dout + Y.dz); io.x = (double *)(dout + Y.x);
+        io.bnd = (double *)(dout + Y.bnd); io.status = (int *)(dout + Y.stat); io.pivots = (int *)(dout + Y.piv);
+        io.jj = (int *)(dout + Y.jj); io.next = (int *)(dout + Y.next); io.stat_out = (signed char *)(dout + Y.sto);
         io.scratch = S.dscratch.p;
-        io.scratch_stride = stride;
+        io.scratch_stride = S.stride;
         launch_node_lp(s, P, io, nb);
-        (void)hipMemcpyAsync(bf.hout.p, bf.dout.p, S.out_bytes(nb), hipMemcpyDeviceToHost, s);
+        (void)hipMemcpyAsync(bf.hout.p, bf.dout.p, Y.out_end, hipMemcpyDeviceToHost, s);
         (void)hipEventRecord(bf.done, s);
     };
     auto process = [&](BatchBuf &bf) {
         if (hipEventSynchronize(bf.done) != hipSuccess) { fail_sync = true; return; }
         const int nb = bf.nb;
-        const size_t NB = (size_t)nb * S.N;
-        const double *hobj = (const double *)bf.hout.p, *hdz = hobj + nb, *hx = hdz + 2 * (size_t)nb;
-        const int *hstat = (const int *)(hx + NB), *hpiv = hstat + nb, *hjj = hpiv + nb, *hnext = hjj + nb;
-        const signed char *hso = (const signed char *)(hnext + nb);
+        const Layout Y(S.N, n, nb);
+        const char *h = bf.hout.p;
+        const double *hobj = (const double *)(h + Y.obj), *hdz = (const double *)(h + Y.dz);
+        const double *hx = (const double *)(h + Y.x), *hb = (const double *)(h + Y.bnd);
+        const int *hstat = (const int *)(h + Y.stat), *hpiv = (const int *)(h + Y.piv);
+        const int *hjj = (const int *)(h + Y.jj), *hnext = (const int *)(h + Y.next);
+        const signed char *hso = (const signed char *)(h + Y.sto);
+        std::vector<double> fx, fbl(n), fbu(n);
+        std::vector<signed char> fso;
+        const std::vector<double> zeros(2 * (size_t)n, 0.0);
         for (int b = 0; b < nb; b++) {
-            const NodeRec nd = bf.nodes[b];
-            lp_solves++;
-            pivots += hpiv[b];
+            const Entry &e = bf.ents[b];
             const int st = hstat[b];
-            if (st == NODE_FAIL) { failed++; continue; }
-            if (st != NODE_OPT) continue;                  // infeasible or cut off
-            const double z = hobj[b];
-            const double bound = S.round_bound(z);
-            if (!hopeful(bound)) continue;
-            const double *x = hx + (size_t)b * S.N;
-            const int jj = hjj[b];
-            if (jj == 0) {                                 // integer feasible
-                if (!have || z < best) {
-                    have = true;
-                    best = z;
-                    std::memcpy(xbest.data(), x, S.N * sizeof(double));
-                }
+            const double *x = hx + (size_t)b * S.N, *bb = hb + (size_t)b * 2 * n;
+            S.pivots += hpiv[b];
+            if (e.kind == 1) {
+                // the probe's degradation (eval_degrad :337-392)
+                S.probes++;
+                Parked &pk = S.parked[e.pid];
+                double dg;
+                if (st == NODE_INFEAS) dg = DBL_MAX;
+                else if (st == NODE_OPT || st == NODE_ITLIM) {
+                    dg = hobj[b] - pk.z;
+                    if (dg < 1e-6 * (1.0 + 0.001 * std::fabs(S.c0 + S.sign * pk.z))) dg = 0.0;
+                } else dg = 0.0;                   // the simplex failed
+                pk.probe[2 * e.j + e.dir] = dg;
+                if (--pk.pending == 0) S.parked_done(e.pid);
                 continue;
             }
-            const int j = jj - 1;
-            const double beta = x[m + j];
-            const double dz[2] = {hdz[2 * b], hdz[2 * b + 1]};
-            const int first = hnext[b] < 0 ? 0 : 1;      // preferred child gets the older seq
-            bool dived = false;
-            for (int r = 0; r < 2; r++) {
-                const int kase = (r == 0) ? first : 1 - first;
-                if (dz[kase] == DBL_MAX) continue;        // that branch has no feasible point
-                const int sl = pool.alloc();
-                std::memcpy(pool.lb(sl), pool.lb(nd.slot), n * sizeof(double));
-                std::memcpy(pool.ub(sl), pool.ub(nd.slot), n * sizeof(double));
-                if (kase == 0) pool.ub(sl)[j] = std::floor(beta);
-                else pool.lb(sl)[j] = std::ceil(beta);
-                signed char *cs = pool.stat(sl);
-                std::memcpy(cs, hso + (size_t)b * S.N, S.N);
-                // a fixed bound pair makes a non-basic column NS
-                if (cs[m + j] != BS && pool.lb(sl)[j] == pool.ub(sl)[j]) cs[m + j] = NS;
-                const NodeRec c{S.round_bound(z + dz[kase]), seq++, sl};
-                if (!dived) {
-                    next_dive.push_back(c);
-                    dived = true;
-                } else
-                    open.push(c);
-                created++;
+            const NodeRec &nd = e.nd;
+            if (st == NODE_PPINF) S.pp_fathomed++;
+            else S.lp_solves++;
+            for (int j = 0; j < n; j++) { fbl[j] = bb[2 * j]; fbu[j] = bb[2 * j + 1]; }
+            if (st == NODE_OPT) {
+                S.node_done(nd, hobj[b], x, hso + (size_t)b * S.N, fbl.data(), fbu.data(), hdz + (size_t)b * 2 * n,
+                            hjj[b], hnext[b], true);
+            } else if ((st == NODE_FAIL || st == NODE_ITLIM) && !S.err) {
+                double z = 0.0;
+                bool opt = false;
+                const int ret = S.fallback(nd, fbl.data(), fbu.data(), fx, fso, z, opt);
+                if (ret) S.err = ret;
+                else if (opt)
+                    S.node_done(nd, z, fx.data(), fso.data(), fbl.data(), fbu.data(), zeros.data(), 0, 0, false);
             }
+            pool.release(nd.slot);
         }
-        for (const NodeRec &nd : bf.nodes) pool.release(nd.slot);
-        bf.nodes.clear();
-        for (const NodeRec &c : next_dive) dive.push_back(c);
-        next_dive.clear();
+        bf.ents.clear();
+        for (const NodeRec &c : S.next_dive) S.dive.push_back(c);
+        S.next_dive.clear();
     };
     auto drain = [&]() {
         for (int k = 0; k < 2; k++) {
@@ -890,38 +1677,46 @@ extern "C" int gk_ios_driver_sharded(gk_ctx *ctx, gk_mip *mip, const gk_iocp *pa
             if (inflight[sb]) { process(S.bufs[sb]); inflight[sb] = 0; }
         }
     };
+    auto release_all = [&]() {
+        for (const NodeRec &r : S.open) pool.release(r.slot);
+        S.open.clear();
+        for (const NodeRec &d : S.dive) pool.release(d.slot);
+        S.dive.clear();
+        S.probeq.clear();
+    };
     // sharded runs: every rank evaluates the same first
     // batches (deterministic, identical on every GPU) until the frontier holds
     // ramp * size nodes, then keeps the nodes i = rank (mod size) of the
-    // frontier in (bound, creation) order; the incumbent value is exchanged
-    // every sync_every batches (exchange() is collective: an idle rank keeps
-    // calling it until no rank has work left)
+    // frontier in (bound, creation) order; at every sync_every batches the
+    // ranks exchange the incumbent and, with an all-gather, hand open nodes
+    // to idle ranks (the collective is called by idle ranks too, until no
+    // rank has work left)
     bool split_done = (size == 1), timed_out = false;
     int since_sync = 0;
     for (;;) {
-        if (fail_sync) break;
+        if (fail_sync || S.err) break;
         const bool any_inflight = inflight[0] || inflight[1];
-        bool have_work = !open.empty() || !dive.empty() || any_inflight;
+        bool have_work = !S.open.empty() || !S.dive.empty() || !S.probeq.empty() || any_inflight;
         if (have_work && parm->tm_lim < 0x7fffffff &&
             std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() * 1000.0 >= parm->tm_lim) {
             timed_out = true;
             drain();
-            while (!open.empty()) { pool.release(open.top().slot); open.pop(); }
-            for (const NodeRec &d : dive) pool.release(d.slot);
-            dive.clear();
+            release_all();
             have_work = false;
         }
         if (!split_done) {
             if (!have_work) break;                        // the tree ended during the ramp-up: same on every rank
-            if ((long long)open.size() + (long long)dive.size() >= (long long)ramp * size) {
-                std::vector<NodeRec> front(dive.begin(), dive.end());
-                while (!open.empty()) { front.push_back(open.top()); open.pop(); }
-                dive.clear();
+            if (S.probeq.empty() && !any_inflight &&
+                (long long)S.open.size() + (long long)S.dive.size() >= (long long)ramp * size) {
+                std::vector<NodeRec> front(S.dive.begin(), S.dive.end());
+                for (const NodeRec &r : S.open) front.push_back(r);
+                S.open.clear();
+                S.dive.clear();
                 std::sort(front.begin(), front.end(), [](const NodeRec &a, const NodeRec &b) {
                     return a.bound != b.bound ? a.bound < b.bound : a.seq < b.seq;
                 });
                 for (size_t i = 0; i < front.size(); i++) {
-                    if ((int)(i % size) == rank) open.push(front[i]);
+                    if ((int)(i % size) == rank) S.push_open(front[i]);
                     else pool.release(front[i].slot);
                 }
                 split_done = true;
@@ -929,40 +1724,56 @@ extern "C" int gk_ios_driver_sharded(gk_ctx *ctx, gk_mip *mip, const gk_iocp *pa
             }
         }
         if (split_done && size > 1 && (since_sync >= sync_every || !have_work)) {
-            double b = best;
-            const int active = shard->exchange(shard->info, &b, have_work ? 1 : 0);
-            if (b < gbest) gbest = b;
             since_sync = 0;
-            if (active == 0) break;
-            if (!have_work) continue;
+            if (shard->allgather) {
+                if (!have_work) drain();
+                const int act = shard_epoch(S, shard, have_work, moved);
+                if (act < 0) { set_err("gk_ios_driver: shard all-gather failed"); return GK_EABI; }
+                if (act == 0) break;
+                have_work = !S.open.empty() || !S.dive.empty() || !S.probeq.empty() || inflight[0] || inflight[1];
+                if (!have_work) continue;
+            } else {
+                double bx = S.best;
+                const int active = shard->exchange(shard->info, &bx, have_work ? 1 : 0);
+                S.set_gbest(bx);
+                if (active == 0) break;
+                if (!have_work) continue;
+            }
         }
         if (!have_work) break;
         since_sync++;
-        // assemble the next batch into the free buffer set
+        // assemble the next batch into the free buffer set: pseudocost
+        // probes first (they unblock parked nodes), then the preferred
+        // children, then the open nodes in the order of bt_tech
         BatchBuf &bf = S.bufs[cur];
         if (inflight[cur]) { process(bf); inflight[cur] = 0; }
-        bf.nodes.clear();
+        if (S.err) break;
+        bf.ents.clear();
+        {
+            size_t k = 0;
+            for (; k < S.probeq.size() && (int)bf.ents.size() < S.BMAX; k++) bf.ents.push_back(S.probeq[k]);
+            S.probeq.erase(S.probeq.begin(), S.probeq.begin() + k);
+        }
         {
             std::vector<NodeRec> keep;
-            for (const NodeRec &nd : dive) {
-                if (!hopeful(nd.bound)) { pool.release(nd.slot); continue; }
-                if ((int)bf.nodes.size() < BMAX) bf.nodes.push_back(nd);
-                else open.push(nd);
+            for (const NodeRec &nd : S.dive) {
+                if (!S.hopeful(nd.bound)) { pool.release(nd.slot); continue; }
+                if ((int)bf.ents.size() < S.BMAX) bf.ents.push_back(Entry{0, nd, 0, 0, 0});
+                else S.push_open(nd);
             }
-            dive.clear();
+            S.dive.clear();
         }
-        while (!open.empty() && (int)bf.nodes.size() < BMAX) {
-            const NodeRec nd = open.top();
-            open.pop();
-            if (!hopeful(nd.bound)) { pool.release(nd.slot); continue; }
-            bf.nodes.push_back(nd);
+        while (!S.open.empty() && (int)bf.ents.size() < S.BMAX) {
+            const NodeRec nd = S.pop_open();
+            if (!S.hopeful(nd.bound)) { pool.release(nd.slot); continue; }
+            bf.ents.push_back(Entry{0, nd, 0, 0, 0});
         }
-        if (!bf.nodes.empty()) {
+        if (!bf.ents.empty()) {
             launch(bf);
             inflight[cur] = 1;
         }
         const int prev = cur ^ 1;
-        if (depth == 1 || bf.nodes.empty()) {
+        if (depth == 1 || bf.ents.empty()) {
             // no pipelining (sharded runs), or nothing new to launch: finish
             // what is in flight, oldest first
             if (inflight[prev]) { process(S.bufs[prev]); inflight[prev] = 0; }
@@ -977,22 +1788,27 @@ extern "C" int gk_ios_driver_sharded(gk_ctx *ctx, gk_mip *mip, const gk_iocp *pa
         set_err("gk_ios_driver: node batch failed: %s", hipGetErrorString(hipGetLastError()));
         return GK_EABI;
     }
-    mip->lp_solves = lp_solves;
-    mip->nodes_created = created;
-    mip->pivots = pivots;
-    if (failed) {
-        set_err("gk_ios_driver: %lld node LP(s) could not be solved by the batched kernel", failed);
-        return GK_EABI;
+    if (S.err) {                                          // the reference's "unable to solve current LP relaxation"
+        drain();
+        release_all();
     }
-    if (have) {
-        mip->mip_stat = timed_out ? 2 : 5;                // GLP_FEAS / GLP_OPT
-        mip->mip_obj = S.c0 + S.sign * best;
-        for (int i = 0; i < m; i++) mip->row_mipx[i + 1] = xbest[i];
+    mip->lp_solves = S.lp_solves;
+    mip->nodes_created = S.created;
+    mip->pivots = S.pivots;
+    mip->node_fallbacks = S.fallbacks;
+    mip->probe_lps = S.probes;
+    mip->pp_fathomed = S.pp_fathomed;
+    mip->nodes_moved = moved;
+    if (S.have) {
+        mip->mip_stat = (timed_out || S.err) ? 2 : 5;     // GLP_FEAS / GLP_OPT
+        mip->mip_obj = S.c0 + S.sign * S.best;
+        for (int i = 0; i < m; i++) mip->row_mipx[i + 1] = S.xbest[i];
         for (int j = 0; j < n; j++)
-            mip->col_mipx[j + 1] = S.isint[j] ? std::floor(xbest[m + j] + 0.5) : xbest[m + j];
+            mip->col_mipx[j + 1] = S.isint[j] ? std::floor(S.xbest[m + j] + 0.5) : S.xbest[m + j];
     } else {
-        mip->mip_stat = timed_out ? 1 : 4;                // GLP_UNDEF / GLP_NOFEAS
+        mip->mip_stat = (timed_out || S.err) ? 1 : 4;     // GLP_UNDEF / GLP_NOFEAS
         mip->mip_obj = 0.0;
     }
+    if (S.err) return S.err;                              // GLP_EFAIL
     return timed_out ? 0x09 : 0;                          // GLP_ETMLIM
 }

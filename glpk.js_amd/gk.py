@@ -76,15 +76,17 @@ class Iocp(C.Structure):
 class Mip(C.Structure):
     _fields_ = [("lp", Lp), ("col_kind", C.c_void_p), ("mip_stat", C.c_int), ("mip_obj", C.c_double),
                 ("col_mipx", C.c_void_p), ("row_mipx", C.c_void_p), ("lp_solves", C.c_longlong),
-                ("nodes_created", C.c_longlong), ("pivots", C.c_longlong)]
+                ("nodes_created", C.c_longlong), ("pivots", C.c_longlong), ("node_fallbacks", C.c_longlong),
+                ("probe_lps", C.c_longlong), ("pp_fathomed", C.c_longlong), ("nodes_moved", C.c_longlong)]
 
 
 _EXCHANGE_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.POINTER(C.c_double), C.c_int)
+_ALLGATHER_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_void_p, C.c_size_t, C.c_void_p)
 
 
 class IosShard(C.Structure):
     _fields_ = [("rank", C.c_int), ("size", C.c_int), ("ramp_nodes", C.c_int), ("sync_every", C.c_int),
-                ("exchange", _EXCHANGE_FN), ("info", C.c_void_p)]
+                ("exchange", _EXCHANGE_FN), ("info", C.c_void_p), ("allgather", _ALLGATHER_FN)]
 
 
 class SpxStats(C.Structure):
@@ -124,6 +126,7 @@ def load_library(path: str = LIB_PATH):
     L.gk_bfd_create.argtypes = [P]
     L.gk_bfd_destroy.argtypes = [P]
     L.gk_bfd_set_parm.argtypes = [P, C.POINTER(Bfcp)]
+    L.gk_bfd_set_parm.restype = C.c_int
     L.gk_bfd_factorize_csc.argtypes = [P, C.c_int, P, P, P]
     L.gk_bfd_factorize_csc.restype = C.c_int
     L.gk_bfd_ftran.argtypes = [P, P]
@@ -266,8 +269,9 @@ class GkProblem:
                  nfs_max=100, upd_tol=1e-6, nrs_max=100, rs_size=0)
         for k, v in kw.items():
             setattr(b, k, v)
+        if self.L.gk_bfd_set_parm(self.bfd, C.byref(b)) != 0:
+            raise GkError(_err(self.L))
         self.bfcp = b
-        self.L.gk_bfd_set_parm(self.bfd, C.byref(b))
 
     def touch_matrix(self):
         """Invalidate the device copy of A (the shim's version counter)."""
@@ -524,12 +528,15 @@ def IOCP(**options) -> Iocp:
     return p
 
 
-def glp_intopt(P: GkProblem, parm: Iocp | None = None, comm=None) -> int:
+def glp_intopt(P: GkProblem, parm: Iocp | None = None, comm=None, ramp_nodes: int = 0) -> int:
     """glp_intopt (glpapi09.js:61) -> solve_mip (:62) -> ios_driver.
 
     comm (shard.TorchComm or alike, size > 1): this process explores its share
-    of the tree on its GPU; the incumbent is exchanged through comm and the
-    best one over all ranks is returned on every rank."""
+    of the tree on its GPU; the incumbent and open nodes are exchanged through
+    comm (an all-gather per sync epoch) and the best incumbent over all ranks
+    is returned on every rank.  ramp_nodes: frontier per rank before the
+    split (0: the driver's default; < 0: split the root alone, so that rank 0
+    starts with all the work — a test of the open-node exchange)."""
     if parm is None:
         parm = IOCP()
     if parm.msg_lev not in (0, 1, 2, 3, 4):
@@ -577,7 +584,7 @@ def glp_intopt(P: GkProblem, parm: Iocp | None = None, comm=None) -> int:
             raise GkError(_err(P.L))
         P.mip_stat = mip.mip_stat
         P.mip_obj = mip.mip_obj
-        P.mip_stats = dict(lp_solves=mip.lp_solves, nodes_created=mip.nodes_created, pivots=mip.pivots)
+        P.mip_stats = _mip_stats(mip)
         return ret
     errors = []
 
@@ -590,8 +597,18 @@ def glp_intopt(P: GkProblem, parm: Iocp | None = None, comm=None) -> int:
             errors.append(e)
             return 0
 
+    def allgather(_info, send, nbytes, recv):
+        try:
+            comm.allgather_bytes(send, nbytes, recv)
+            return 0
+        except Exception as e:
+            errors.append(e)
+            return 1
+
     cb = _EXCHANGE_FN(exchange)
-    sh = IosShard(rank=comm.rank, size=comm.size, ramp_nodes=0, sync_every=0, exchange=cb, info=None)
+    ag = _ALLGATHER_FN(allgather) if hasattr(comm, "allgather_bytes") else _ALLGATHER_FN()
+    sh = IosShard(rank=comm.rank, size=comm.size, ramp_nodes=int(ramp_nodes), sync_every=0, exchange=cb, info=None,
+                  allgather=ag)
     ret = P.L.gk_ios_driver_sharded(P.ctx.h, C.byref(mip), C.byref(parm), C.byref(sh))
     if errors:
         raise errors[0]
@@ -611,8 +628,15 @@ def glp_intopt(P: GkProblem, parm: Iocp | None = None, comm=None) -> int:
         P.mip_stat = GLP_NOFEAS
         P.mip_obj = 0.0
     P.mip_stats = dict(lp_solves=int(comm.total(mip.lp_solves)), nodes_created=int(comm.total(mip.nodes_created)),
-                       pivots=int(comm.total(mip.pivots)), local_lp_solves=mip.lp_solves)
+                       pivots=int(comm.total(mip.pivots)), local_lp_solves=mip.lp_solves,
+                       node_fallbacks=int(comm.total(mip.node_fallbacks)), probe_lps=int(comm.total(mip.probe_lps)),
+                       pp_fathomed=int(comm.total(mip.pp_fathomed)), local_nodes_moved=mip.nodes_moved)
     return ret
+
+
+def _mip_stats(mip) -> dict:
+    return dict(lp_solves=mip.lp_solves, nodes_created=mip.nodes_created, pivots=mip.pivots,
+                node_fallbacks=mip.node_fallbacks, probe_lps=mip.probe_lps, pp_fathomed=mip.pp_fathomed)
 
 
 # ---------------------------------------------------------------------------

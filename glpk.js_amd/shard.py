@@ -1,12 +1,15 @@
 """Multi-GPU branch and bound: one process per GPU.
 
 Every rank runs gk_ios_driver_sharded on the same problem: identical
-ramp-up batches, then a round-robin split of the frontier.  The only
-exchange is the incumbent: `TorchComm.exchange` is the collective the native
-driver calls every few batches (one all-reduce MIN of [best, -active], i.e.
-the best objective and whether any rank still has open nodes), and
-`TorchComm.finalize` picks the winning incumbent (lowest objective, lowest
-rank on ties) and broadcasts it.  The backend is whatever process group is
+ramp-up batches, then a round-robin split of the frontier.  Every few
+batches the native driver calls `TorchComm.allgather_bytes`, an all-gather
+of a fixed-size byte block per rank: first {incumbent, best open bound, open
+nodes, active} of every rank, then — when some rank is idle and another
+holds open nodes — the node descriptors (bounds, warm-start basis, parent
+information) the donors hand to the idle ranks (gk_mip.hip, shard_epoch).
+`TorchComm.exchange` (all-reduce MIN of [best, -active]) is the older,
+incumbent-only protocol; `TorchComm.finalize` picks the winning incumbent
+(lowest objective, lowest rank on ties) and broadcasts it.  The backend is whatever process group is
 initialised: "nccl" (RCCL over xGMI) on MI355X nodes, "gloo" for CPU tests.
 """
 from __future__ import annotations
@@ -31,6 +34,20 @@ class TorchComm:
         self.dist.all_reduce(t, op=self.dist.ReduceOp.MIN, group=self.group)
         v = t.cpu().tolist()
         return v[0], int(-v[1])
+
+    def allgather_bytes(self, send_ptr: int, nbytes: int, recv_ptr: int) -> None:
+        """All-gather of nbytes from every rank (the C driver's buffers, raw
+        addresses) into recv (size * nbytes, rank order)."""
+        import ctypes
+        torch, dist = self.torch, self.dist
+        buf = np.empty(nbytes, dtype=np.uint8)
+        ctypes.memmove(buf.ctypes.data, send_ptr, nbytes)
+        t = torch.from_numpy(buf).to(self.device)
+        outs = [torch.empty_like(t) for _ in range(self.size)]
+        dist.all_gather(outs, t, group=self.group)
+        for r, o in enumerate(outs):
+            a = np.ascontiguousarray(o.cpu().numpy())
+            ctypes.memmove(recv_ptr + r * nbytes, a.ctypes.data, nbytes)
 
     def total(self, v: float) -> float:
         t = self.torch.tensor([float(v)], dtype=self.torch.float64, device=self.device)

@@ -40,7 +40,8 @@
 extern "C" {
 #endif
 
-#define GK_ABI_VERSION 1
+#define GK_ABI_VERSION 2
+#include <stddef.h>
 #define GK_EABI (-1)          /* contract violation; see gk_last_error() */
 
 typedef struct gk_ctx gk_ctx; /* one HIP device + stream(s)                */
@@ -62,7 +63,11 @@ const char *gk_last_error(void);                 /* thread-local message     */
  * reference refactorizes after nfs_max Forrest–Tomlin updates,
  * glpfhv.js:182).  Field meanings follow glp_bfcp (glpapi12.js:108-121). */
 typedef struct {
-    int    type;       /* GLP_BF_FT / GLP_BF_BG / GLP_BF_GR (all served by the same factor) */
+    int    type;       /* GLP_BF_FT (1) / GLP_BF_BG (2) / GLP_BF_GR (3): all three are served
+                          by the same explicit-inverse factor (the update is exact product
+                          form, so the Bartels-Golub / Givens variants coincide with it);
+                          any other value: gk_bfd_set_parm fails with the reference's
+                          "glp_set_bfcp: type = %d; invalid parameter" */
     int    lu_size;
     double piv_tol;
     int    piv_lim, suhl;
@@ -76,7 +81,7 @@ typedef int (*gk_col_fn)(void *info, int j, int *ind, double *val);
 
 gk_bfd *gk_bfd_create(gk_ctx *ctx);
 void    gk_bfd_destroy(gk_bfd *bfd);
-void    gk_bfd_set_parm(gk_bfd *bfd, const gk_bfcp *parm);
+int     gk_bfd_set_parm(gk_bfd *bfd, const gk_bfcp *parm);   /* 0 | GK_EABI (invalid field) */
 /* 0 | BFD_ESING(1) | BFD_ECOND(2); col(info, j, ind, val) fills column j of B
  * exactly like b_col/inv_col (glpapi12.js:7, glpspx01.js:147). */
 int     gk_bfd_factorize(gk_bfd *bfd, int m, gk_col_fn col, void *info);
@@ -92,6 +97,10 @@ int     gk_bfd_get_count(const gk_bfd *bfd);
 int     gk_bfd_valid(const gk_bfd *bfd);
 
 /* ---- simplex (glpspx01.js / glpspx02.js) --------------------------------- */
+/* Limits of the explicit-inverse factor: m <= 65535 rows (grid limits of
+ * the pivot kernels), and inv(B) is dense: 8 m^2 bytes of HBM per factor
+ * (34 GB at m = 65535; 128 MiB at m = 4096).  gk_spx_* return GK_EABI with
+ * a message beyond that; the JS shim then keeps the reference's own solver. */
 typedef struct {                /* glp_smcp, SMCP (glpapi06.js:359-375)       */
     int    msg_lev, meth, pricing, r_test;
     double tol_bnd, tol_dj, tol_piv, obj_ll, obj_ul;
@@ -167,7 +176,15 @@ int gk_bfd_trace(gk_bfd *bfd, unsigned long long *out, size_t cnt);
  * *bytes receives the algorithmic bytes one launch must move. */
 double gk_bfd_time_kernel(gk_bfd *bfd, int which, int reps, double *bytes);
 
-/* ---- branch and bound (glpios03.js, glpapi09.js) ------------------------- */
+/* ---- branch and bound (glpios03.js, glpapi09.js) -------------------------
+ * gk_ios_driver serves glp_intopt with cb_func == null, presolve off and no
+ * cut generators.  Every br_tech (FFV, LFV, MFV, DTH, PCH; glpios09.js:1) and
+ * bt_tech (DFS, BFS, BLB, BPH; glpios12.js:2) is native; pp_tech NONE / ROOT
+ * / ALL runs ios_preprocess_node (glpios02.js:1) inside the node kernel.
+ * Node LPs are solved in batches, one workgroup per node; a node the batched
+ * kernel cannot finish is re-solved by the full engine (ios_solve_node's
+ * glp_simplex, GLP_DUALP); GLP_EFAIL (5) only when that fails too, as the
+ * reference's ios_driver (glpios03.js:669-673). */
 typedef struct {                /* glp_iocp, IOCP (glpapi09.js:392-414)       */
     int    msg_lev, br_tech, bt_tech;
     double tol_int, tol_obj;
@@ -184,6 +201,11 @@ typedef struct {
     double mip_obj;
     double *col_mipx, *row_mipx;              /* [1..n], [1..m] */
     long long lp_solves, nodes_created, pivots;
+    long long node_fallbacks;   /* node LPs re-solved by the full engine (gk_spx_*) after the
+                                   batched kernel gave up (iteration limit, singular basis) */
+    long long probe_lps;        /* PCH pseudocost probes (eval_degrad, glpios09.js:337) */
+    long long pp_fathomed;      /* nodes fathomed by ios_preprocess_node (no LP solved) */
+    long long nodes_moved;      /* sharded runs: open nodes received from other ranks */
 } gk_mip;
 
 int gk_ios_driver(gk_ctx *ctx, gk_mip *mip, const gk_iocp *parm);
@@ -204,6 +226,12 @@ typedef struct {
     int sync_every;                 /* batches between exchanges (0: 4) */
     int (*exchange)(void *info, double *best, int active);
     void *info;
+    /* optional (preferred when set): all-gather of `bytes` bytes from every
+     * rank into recv (size * bytes, rank order); returns 0 on success.  With
+     * it every sync epoch exchanges {incumbent, best bound, open nodes,
+     * active} and hands open nodes (bounds + warm-start basis) from the ranks
+     * with the most to idle ranks; exchange is then unused */
+    int (*allgather)(void *info, const void *send, size_t bytes, void *recv);
 } gk_ios_shard;
 int gk_ios_driver_sharded(gk_ctx *ctx, gk_mip *mip, const gk_iocp *parm, const gk_ios_shard *shard);
 

@@ -188,7 +188,7 @@ static napi_value js_bfd_set_parm(napi_env env, napi_callback_info info)
     p.upd_tol = dprop(env, argv[1], "upd_tol", 1e-6);
     p.nrs_max = (int)dprop(env, argv[1], "nrs_max", 100);
     p.rs_size = (int)dprop(env, argv[1], "rs_size", 0);
-    gk_bfd_set_parm(b, &p);
+    if (gk_bfd_set_parm(b, &p) != 0) napi_throw_error(env, NULL, gk_last_error());
     return NULL;
 }
 

@@ -9,7 +9,7 @@ var core = require(path.join(__dirname, 'gk_core.js'));
 var names = ['create', 'deviceCount', 'abiVersion', 'lastError', 'bfdCreate', 'bfdSetParm', 'bfdFactorizeCsc',
              'bfdFtran', 'bfdBtran', 'bfdUpdate', 'bfdGetCount', 'bfdValid', 'spx', 'ios', 'stats'];
 names.forEach(function (k) { assert.strictEqual(typeof core.addon[k], 'function', k); });
-assert.strictEqual(core.addon.abiVersion(), 1);
+assert.strictEqual(core.addon.abiVersion(), 2);
 
 var ref = process.env.GLPK_REF || '/root/reference';
 var fs = require('fs');

@@ -284,6 +284,33 @@ function mipCase(name, mk, gen) {
     console.log('wrote mip', name, 'ret', ret, 'obj', P.mip_obj, 'lp', d.mip.lp_solves, 'piv', d.mip.pivots, 'sec', dt.toFixed(2));
 }
 
+// MIP instance under several IOCP option sets (branching rule br_tech,
+// node selection bt_tech, preprocessing pp_tech; glpios09.js:1,
+// glpios12.js:2, glpios03.js:643-656): one root solve per run, the
+// reference's objective, incumbent and node-LP count for each.
+function mipOptsCase(name, mk, optsList) {
+    if (ONLY && ('mipopt_' + name).indexOf(ONLY) !== 0) return;
+    var d = dumpProb(mk(), null);
+    d.name = name; d.kind = 'mipopt'; d.runs = [];
+    optsList.forEach(function (opts) {
+        var P = mk();
+        var root = runLp(P, {}, 0);
+        var s0 = glpk.__cnt.solve_node, it0 = P.it_cnt;
+        var t0 = process.hrtime.bigint();
+        var ret = glpk.glp_intopt(P, new glpk.IOCP(opts));
+        var dt = Number(process.hrtime.bigint() - t0) / 1e9;
+        var j, x = [];
+        for (j = 1; j <= P.n; j++) x.push(P.col[j].mipx);
+        d.runs.push({opts: opts, root_ret: root.ret, ret: ret, mip_stat: P.mip_stat, mip_obj: P.mip_obj, col_mipx: x,
+                     lp_solves: glpk.__cnt.solve_node - s0, pivots: P.it_cnt - it0, seconds: dt});
+    });
+    fs.writeFileSync(path.join(OUT, 'mipopt_' + name + '.json'), JSON.stringify(d));
+    console.log('wrote mipopt', name, d.runs.map(function (r) {
+        return JSON.stringify(r.opts) + ':ret' + r.ret + ':mip' + r.mip_obj + ':lp' + r.lp_solves; }).join(' '));
+}
+var MIP_OPTS = [{br_tech: 1}, {br_tech: 2}, {br_tech: 3}, {br_tech: 5}, {bt_tech: 1}, {bt_tech: 2}, {bt_tech: 4},
+                {br_tech: 3, bt_tech: 1}, {br_tech: 5, bt_tech: 4}, {pp_tech: 1}, {br_tech: 1, bt_tech: 2, pp_tech: 1}];
+
 // ---- instances ------------------------------------------------------------
 lpCase('test', function () { return readLp('test.lpt'); }, null);
 lpCase('todd', function () { return readLp('todd.lpt'); }, null);
@@ -310,6 +337,10 @@ for (var ms = 1; ms <= 12; ms++) {
         mipCase('mixint' + ms, function () { return genMix(100 + ms, 6 + ms, 8 + 2 * ms, 0.5, true, true); }, null);
     })(ms);
 }
+mipOptsCase('gap', function () { return readLp('gap.lpt'); }, MIP_OPTS);
+mipOptsCase('c5s_12x20', function () { return genC5s(12, 20, 42); }, MIP_OPTS);
+mipOptsCase('mixint4', function () { return genMix(104, 10, 16, 0.5, true, true); }, MIP_OPTS);
+mipOptsCase('mixint9', function () { return genMix(109, 15, 26, 0.5, true, true); }, MIP_OPTS);
 // glp_read_lp on CPLEX LP texts exercising every section and bound form
 // (the Python reader problems.read_lp is pinned on these problem dumps; the
 // texts travel in the fixture, the error cases record the reference's message)

@@ -36,6 +36,12 @@ def _comm_worker(rank, world, port, q):
     out["ex1"] = c.exchange([5.0, 3.0][rank], [1, 0][rank])
     out["ex2"] = c.exchange([1e300, 7.0][rank], 0)
     out["total"] = c.total(rank + 1)
+    # allgather_bytes: fixed-size byte blocks in rank order (the C driver's
+    # open-node exchange), through raw addresses
+    send = np.frombuffer(bytes([rank + 1] * 5), dtype=np.uint8).copy()
+    recv = np.zeros(10, dtype=np.uint8)
+    c.allgather_bytes(send.ctypes.data, 5, recv.ctypes.data)
+    out["ag"] = recv.tolist()
     # finalize: rank 1 has the better objective; its x is broadcast
     x = np.full(4, float(rank))
     obj, have, xw, win = c.finalize([10.0, 2.0][rank], True, x)
@@ -87,12 +93,13 @@ def test_torchcomm_gloo_world2():
         assert o["ex1"] == (3.0, 1)
         assert o["ex2"] == (7.0, 0)
         assert o["total"] == 3.0
+        assert o["ag"] == [1] * 5 + [2] * 5
         assert o["fin"] == (2.0, True, [1.0] * 4, 1)
         assert o["tie"] == [0.0, 0.0]
         assert o["none"] is False
 
 
-def _bnb_worker(rank, world, port, names, q):
+def _bnb_worker(rank, world, port, names, q, ramp=0):
     import torch
     import torch.distributed as dist
     sys.path.insert(0, ROOT)
@@ -108,7 +115,7 @@ def _bnb_worker(rank, world, port, names, q):
         d = json.load(open(os.path.join(ROOT, "tests", "golden", f"mip_{name}.json")))
         P = gk.GkProblem(ctx, problems.from_fixture(d))
         assert gk.glp_simplex(P, gk.SMCP(**d["root"]["opts"])) == 0
-        ret = gk.glp_intopt(P, gk.IOCP(msg_lev=gk.GLP_MSG_OFF), comm=comm)
+        ret = gk.glp_intopt(P, gk.IOCP(msg_lev=gk.GLP_MSG_OFF), comm=comm, ramp_nodes=ramp)
         out[name] = (ret, P.mip_stat, P.mip_obj, P.col_mipx[1:].tolist(), P.mip_stats)
     dist.destroy_process_group()
     q.put((rank, out))
@@ -126,3 +133,25 @@ def test_sharded_bnb_two_ranks_one_gpu():
         assert abs(a[2] - ref["mip_obj"]) <= 1e-9 * max(1.0, abs(ref["mip_obj"]))
         assert a[2] == b[2] and a[3] == b[3], "ranks disagree on the incumbent"
         print(name, "lp_solves", a[4])
+
+
+def _bnb_worker_root_split(rank, world, port, names, q):
+    _bnb_worker(rank, world, port, names, q, ramp=-1)
+
+
+@pytest.mark.gpu
+def test_sharded_bnb_open_node_exchange():
+    """Rank 1 starts with nothing (the root alone is split, to rank 0); the
+    open-node exchange must hand it work: both ranks solve node LPs, rank 1
+    receives nodes, and the result is the reference's (C5s 12x30: 15039)."""
+    names = ["c5s_12x30", "gap"]
+    res = _run_ranks(_bnb_worker_root_split, 2, (names,), 240)
+    for name in names:
+        ref = json.load(open(os.path.join(ROOT, "tests", "golden", f"mip_{name}.json")))["mip"]
+        a, b = res[0][name], res[1][name]
+        assert a[0] == b[0] == ref["ret"]
+        assert abs(a[2] - ref["mip_obj"]) <= 1e-9 * max(1.0, abs(ref["mip_obj"]))
+        assert a[2] == b[2] and a[3] == b[3], "ranks disagree on the incumbent"
+        assert a[4]["local_lp_solves"] > 0 and b[4]["local_lp_solves"] > 0, (a[4], b[4])
+        assert b[4]["local_nodes_moved"] > 0, b[4]
+        print(name, "rank0", a[4], "rank1", b[4])
