@@ -27,6 +27,42 @@ import __graft_entry__  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 ROOF_KERNEL = "k_dual_row"
+ROUND = "r02"
+# the C port (oracle/) against the reference itself, both on one core of the
+# build container on C3 from the slack basis: the port 285.8 pivots/s over a
+# 20 s window (6,874 pivots, init_csa included), the reference node 9.4
+# pivots/s over its first 300 pivots; later pivots cost more, so
+# the ratio on the same window is larger still
+PORT_OVER_NODE = 30.4
+
+
+def load_profile(args):
+    """rocprofv3 numbers of this exact command from profiles/ (written by
+    tools/profile_round.sh with the command it profiled); {} when the
+    committed profile is of a different command."""
+    out = {}
+    meta_p = os.path.join(ROOT, "profiles", f"{ROUND}_profile_meta.json")
+    try:
+        meta = json.load(open(meta_p))
+    except Exception:
+        return out
+    want = {"steps": args.steps, "warmup": args.warmup, "pivots_per_step": args.pivots_per_step,
+            "m": args.m, "n": args.n}
+    if any(meta.get("args", {}).get(k) != v for k, v in want.items()):
+        return out
+    out["source"] = f"profiles/{ROUND}_kernel_stats_timed.json, profiles/{ROUND}_pmc_traffic.json " \
+                    f"(command: {meta.get('cmd')}; head {meta.get('head')})"
+    try:
+        out["rocprof_ms"] = round(json.load(open(os.path.join(ROOT, "profiles", f"{ROUND}_kernel_stats_timed.json")))
+                                  [ROOF_KERNEL]["avg_ns"] / 1e6, 5)
+    except Exception:
+        pass
+    try:
+        out["traffic"] = json.load(open(os.path.join(ROOT, "profiles", f"{ROUND}_pmc_traffic.json")))[
+            "kernels"][ROOF_KERNEL]["bytes_per_launch"]
+    except Exception:
+        pass
+    return out
 
 
 def log(rank, *a):
@@ -38,7 +74,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--pivots-per-step", type=int, default=100)
     ap.add_argument("--m", type=int, default=4096)
     ap.add_argument("--n", type=int, default=16384)
@@ -104,7 +140,7 @@ def main():
     piv = 0
     split = {"init": 0.0, "eval": 0.0, "batches": 0.0, "reinvert": 0.0, "total": 0.0}
     reinv = 0
-    dev = {"ms": 0.0, "ms_b": 0.0, "launches": 0, "bytes": 0.0}
+    dev = {"ms": 0.0, "ms_b": 0.0, "launches": 0, "bytes": 0.0, "ms_r": 0.0, "launches_r": 0, "bytes_pivots": 0.0}
     for _ in range(args.steps):
         piv += step()
         s_ = P.stats()
@@ -118,6 +154,9 @@ def main():
         dev["ms_b"] += s_.trow_dev_ms_b
         dev["launches"] += s_.trow_dev_launches
         dev["bytes"] += s_.trow_bytes
+        dev["ms_r"] += s_.trow_dev_ms_r
+        dev["launches_r"] += s_.trow_dev_launches_r
+        dev["bytes_pivots"] += s_.bytes_pivots
     barrier()
     dt = time.perf_counter() - t0
     ctx.mark(2)                         # timed region ends
@@ -148,9 +187,14 @@ def main():
         max_dt = float(t.item())
     value = tot_piv / max_dt
 
-    # roofline of the dominant kernel (the pivot-row pass), timed live with
-    # HIP events on the engine stream around every launch of the timed
-    # region; algorithmic bytes per launch = 8 * |supp rho| * n
+    # roofline of the dominant kernel, k_dual_row (chuzr, rho, the pivot row
+    # over the rows of AT in the support of rho, Harris pass-1 candidates),
+    # timed live over every launch of the timed region with the device wall
+    # clock (s_memrealtime, stamped inside the captured graphs): from the last
+    # block exit of the kernel before it to its own last block exit — the
+    # bracket of a profiler's per-dispatch record (rocprofv3 --kernel-trace
+    # start/end).  Algorithmic bytes per launch = 8 * |supp rho| * n
+    # (DESIGN.md §4), accumulated on the device for the same launches.
     roof = None
     kern = {}
     if rank == 0:
@@ -158,46 +202,42 @@ def main():
                             (3, "binv_rank1_dense")):
             ms_k, b_k = P.time_kernel(which, reps=10)
             kern[name] = {"ms": round(ms_k, 5), "bytes": b_k, "GBps": round(b_k / (ms_k * 1e-3) / 1e9, 1)}
-        # primary: device wall clock over every pivot-row launch of the timed
-        # region, from the kernel's entry to the entry of the next kernel on
-        # the stream (the dispatch boundary included, as rocprofv3 counts a
-        # back-to-back dispatch); exec_ms_per_launch: entry to last block exit
         nl = max(1, dev["launches"])
-        ms = dev["ms_b"] / nl
         b = dev["bytes"] / nl
+        nr_ = max(1, dev["launches_r"])
+        ms = dev["ms_r"] / nr_
         achieved = b / (ms * 1e-3) / 1e9 if ms > 0 else 0.0
         ne = max(1, trow["launches"])
-        # committed profiles of the same command (tools/profile_round.sh):
-        # HBM bytes per launch from the --pmc passes and rocprofv3's own
-        # average duration, both over the timed region only (k_gk_mark window)
-        traffic = rocprof_ms = None
-        tpath = os.path.join(ROOT, "profiles", "r01_pmc_traffic.json")
-        spath = os.path.join(ROOT, "profiles", "r01_kernel_stats_timed.json")
-        try:
-            traffic = json.load(open(tpath))["kernels"].get(ROOF_KERNEL, {}).get("bytes_per_launch")
-        except Exception:
-            traffic = None
-        try:
-            rocprof_ms = json.load(open(spath))[ROOF_KERNEL]["avg_ns"] / 1e6
-        except Exception:
-            rocprof_ms = None
+        # the committed profiles of this same command (tools/profile_round.sh
+        # writes profiles/<round>_profile_meta.json with the command it
+        # profiled): rocprofv3's average duration of the kernel over the timed
+        # region, and HBM bytes per launch from the --pmc FETCH_SIZE /
+        # WRITE_SIZE passes; used only when the profiled command matches
+        prof = load_profile(args)
+        step_bytes = dev["bytes_pivots"]
+        step_gbps = step_bytes / max_dt / 1e9 if max_dt > 0 else 0.0
         roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                "frac": round(achieved / HBM_PEAK_GBS, 4),
+                "traffic": prof.get("traffic"),
+                "traffic_over_algorithmic": round(prof["traffic"] / b, 3) if prof.get("traffic") else None,
                 "kernel": ROOF_KERNEL + " (chuzr, rho = row p of inv(B), pivot row trow = -rho' N over the rows "
                                         "of A in the support of rho, ratio-test candidates: one kernel)",
-                "ms_per_launch": round(ms, 5), "launches": dev["launches"],
+                "ms_per_launch": round(ms, 5), "launches": dev["launches_r"],
                 "bytes_per_launch": round(b),
-                "timing": "device wall clock (s_memrealtime) over every launch of the timed region, entry to next entry",
+                "timing": "device wall clock over every launch of the timed region: last block exit of the kernel "
+                          "before it to its own last block exit (a profiler's per-dispatch bracket)",
+                "entry_to_next_entry_ms": round(dev["ms_b"] / nl, 5),
                 "exec_ms_per_launch": round(dev["ms"] / nl, 5),
-                "exec_GBps": round(b / (dev["ms"] / nl * 1e-3) / 1e9, 1) if dev["ms"] > 0 else None,
+                "rocprof_ms_per_launch": prof.get("rocprof_ms"),
+                "rocprof_frac": round(b / (prof["rocprof_ms"] * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
+                if prof.get("rocprof_ms") else None,
+                "profile_source": prof.get("source"),
                 "hip_events_cross_check": {"ms_per_launch": round(trow["ms"] / ne, 5), "launches": trow["launches"],
                                            "bytes_per_launch": round(trow["bytes"] / ne),
                                            "note": "second pass, eager launches, interval includes launch gap"},
-                "traffic_source": "profiles/r01_pmc_traffic.json (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes, "
-                                  "timed region only)",
-                "rocprof_ms_per_launch": round(rocprof_ms, 5) if rocprof_ms else None,
-                "rocprof_source": "profiles/r01_kernel_stats_timed.json (rocprofv3 --kernel-trace of this command, "
-                                  "timed region; includes the profiler's per-dispatch overhead, DESIGN.md §5)"}
+                # the whole pivot (all kernels) against the same peak
+                "step_achieved": round(step_gbps, 1), "step_frac": round(step_gbps / HBM_PEAK_GBS, 4),
+                "step_bytes_per_pivot": round(step_bytes / max(1, piv))}
 
     cpu = None
     extra = {}
@@ -216,7 +256,11 @@ def main():
                "sample": f"oracle (C restatement of glpspx02.js) dual simplex on the same C3 4096x16384 "
                          f"instance from the slack basis, tm_lim={args.cpu_seconds:.0f}s: "
                          f"{cres['it_cnt']} pivots in {cdt:.1f}s incl. init_csa; reference node "
-                         f"dist/glpk.js measured 9.4 pivots/s on this config (BASELINE.md)"}
+                         f"dist/glpk.js measured 9.4 pivots/s on this config (BASELINE.md)",
+               # the port is not a proxy for the reference's speed: both timed
+               # in the build container on the same instance
+               "port_over_reference_node": PORT_OVER_NODE,
+               "reference_node_pivots_per_s": 9.4}
 
     if not args.no_extra:
         if world == 1:
@@ -389,11 +433,19 @@ def run_bnb(gk, problems, ctx, names=("gap", "c5s_12x30"), comm=None):
         if comm is not None:
             dt = -comm.exchange(-dt, 0)[0]         # max over ranks
         lps = P.mip_stats.get("lp_solves", 0)
+        # LP-relax/s counts every node LP the batched search solves, including
+        # the speculative ones a sequential walk would have pruned: read it
+        # with the time to the optimum and the node-LP counts beside it
         out["bnb_" + name] = {"ret": ret, "mip_obj": P.mip_obj, "ref_mip_obj": d["mip"]["mip_obj"],
-                              "lp_relaxations": lps, "seconds": round(dt, 4),
-                              "lp_relax_per_s": round(lps / dt, 1), "nodes": P.mip_stats.get("nodes_created"),
-                              "reference_lp_relaxations": ref_lps, "reference_seconds": ref_s,
+                              "time_to_optimal_s": round(dt, 4), "reference_time_to_optimal_s": ref_s,
+                              "time_speedup": round(ref_s / dt, 1) if dt > 0 else None,
+                              "node_lps": lps, "reference_node_lps": ref_lps,
+                              "node_lps_over_reference": round(lps / ref_lps, 2),
+                              "lp_relax_per_s": round(lps / dt, 1),
                               "reference_lp_relax_per_s": round(ref_lps / ref_s, 1),
+                              "nodes": P.mip_stats.get("nodes_created"),
+                              "pp_fathomed": P.mip_stats.get("pp_fathomed"),
+                              "node_fallbacks": P.mip_stats.get("node_fallbacks"),
                               "ranks": comm.size if comm is not None else 1}
     return out
 

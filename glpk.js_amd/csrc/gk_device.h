@@ -301,6 +301,17 @@ struct TraceScope {
     }
 };
 
+// exit stamp of a block (the latest wave exit; atomicMax over the waves —
+// the stamps only grow, so the slot needs no reset between pivots)
+struct ExitStamp {
+    unsigned long long *p;
+    __device__ __forceinline__ ExitStamp(unsigned long long *slots, unsigned b) : p(slots ? slots + b : nullptr) {}
+    __device__ __forceinline__ ~ExitStamp()
+    {
+        if (p && (threadIdx.x & 63) == 0) atomicMax(p, wall_clock64());
+    }
+};
+
 // phase stamp of wave 0 (profiling only)
 #define TPH(kid, ph)                                                                                              \
     do {                                                                                                          \

@@ -396,12 +396,15 @@ __device__ __forceinline__ int dual_bad(const SpxDev &d, int k, double cb, doubl
     return 0;
 }
 
-// batch start: chuzr candidates and the phase-I check of the current state
-__global__ void __launch_bounds__(256) k_dual_prep(SpxDev d)
+// batch start: chuzr candidates (one per 64 rows) and the phase-I check of
+// the current state; the candidate slots [4 ceil(m / 256), gm) of a finer
+// layout (k_dual_update: one per 16 rows) are cleared
+__global__ void __launch_bounds__(256) k_dual_prep(SpxDev d, int gm)
 {
     DState *st = d.st;
     const int m = d.m, n = d.n;
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    for (int s = 4 * ((m + 255) / 256) + i; s < gm; s += gridDim.x * blockDim.x) cand_chuzr(d)[s] = no_cand(0.0);
     const bool reset = (st->pricing == PT_PSE && st->refct == 0);
     if ((int)blockIdx.x * 256 < m) {
         Cand c = no_cand(0.0);
@@ -812,7 +815,7 @@ __global__ void __launch_bounds__(1024) k_trow_rows(SpxDev d, int pse)
 // 0 also publishes the compact rho (rho_idx / rho_val, read by the commit),
 // the scalar state and, every 1000 pivots, the reference-space reset.
 // ---------------------------------------------------------------------------
-__global__ void __launch_bounds__(1024) k_dual_row(SpxDev d, int pse, int nr_cap)
+__global__ void __launch_bounds__(1024) k_dual_row(SpxDev d, int pse, int nr_cap, int gm)
 {
     const TraceScope trace_(d, 1);
     __shared__ double sp[16][64];
@@ -829,7 +832,6 @@ __global__ void __launch_bounds__(1024) k_dual_row(SpxDev d, int pse, int nr_cap
     const int pricing = st->pricing, phase = st->phase, dinf = st->dinf, nr = st->nr;
     const double zeta = st->zeta, obj_ll = st->obj_ll, obj_ul = st->obj_ul;
     const RatioIn rin = ratio_in(st);
-    const int gm = 4 * ((m + 255) / 256);
     Cand cc = no_cand(0.0);
     for (int b = lane; b < gm; b += 64) {
         const Cand e = cand_chuzr(d)[b];
@@ -1030,7 +1032,7 @@ __global__ void __launch_bounds__(1024) k_dual_row(SpxDev d, int pse, int nr_cap
 // the commit) and the scalar state; the other blocks patch what it changes,
 // as in k_dual_row.
 // ---------------------------------------------------------------------------
-__global__ void __launch_bounds__(256) k_dual_col(SpxDev d, int pse, int nr_cap)
+__global__ void __launch_bounds__(256) k_dual_col(SpxDev d, int pse, int nr_cap, int gm)
 {
     const TraceScope trace_(d, 1);
     DState *st = d.st;
@@ -1045,7 +1047,6 @@ __global__ void __launch_bounds__(256) k_dual_col(SpxDev d, int pse, int nr_cap)
     const int pricing = st->pricing, phase = st->phase, dinf = st->dinf, nr = st->nr;
     const double zeta = st->zeta, obj_ll = st->obj_ll, obj_ul = st->obj_ul;
     const RatioIn rin = ratio_in(st);
-    const int gm = 4 * ((m + 255) / 256);
     Cand cc = no_cand(0.0);
     for (int b = lane; b < gm; b += 64) {
         const Cand e = cand_chuzr(d)[b];
@@ -1215,12 +1216,51 @@ __global__ void __launch_bounds__(256) k_dual_col(SpxDev d, int pse, int nr_cap)
 // one per wave; blocks [gn, ...) — partials of A w over the reference-space
 // columns.  Every wave makes the pass-1 choice on its own (no block barrier).
 // ---------------------------------------------------------------------------
-__global__ void __launch_bounds__(256) k_dual_ratio(SpxDev d, int gn, int tiles_m, int rowpath, int ncb)
+__global__ void __launch_bounds__(256) k_dual_ratio(SpxDev d, int gn, int tiles_m, int rowpath, int ncb, int nwl_cap,
+                                                    int nprev)
 {
     const TraceScope trace_(d, 2);
     DState *st = d.st;
     const int stop = st->stop;               // tested before the first store
     const int m = d.m, n = d.n;
+    if ((int)blockIdx.x >= gn && d.A.dense && nwl_cap > 0) {
+        // work = ys - A w in one pass (nwl <= nwl_cap): 64 rows per block,
+        // lane = row, the 4 waves split wlist (entries loaded ahead up to the
+        // cap, before nwl is known), partials combined in wave order
+        __shared__ double sw[4][64];
+        const int lane = threadIdx.x & 63, w4 = threadIdx.x >> 6;
+        const int r = (blockIdx.x - gn) * 64 + lane;
+        constexpr int WU = 16;
+        int cl[WU];
+#pragma unroll
+        for (int u = 0; u < WU; ++u) {
+            const int t = w4 + 4 * u;
+            cl[u] = (t < nwl_cap) ? d.wlist[t] : 0;
+        }
+        const int cnt = st->nwl;
+        const double ysr = (r < m) ? d.ys[r] : 0.0;
+        if (stop) return;
+        const double *__restrict__ A = d.A.A;
+        const size_t lda = (size_t)d.A.lda;
+        double wv[WU], av[WU];
+#pragma unroll
+        for (int u = 0; u < WU; ++u) {
+            const bool ok = w4 + 4 * u < cnt;
+            wv[u] = ok ? d.wcol[cl[u]] : 0.0;
+            av[u] = (ok && r < m) ? A[(size_t)cl[u] * lda + r] : 0.0;
+        }
+        double acc = 0.0;
+#pragma unroll
+        for (int u = 0; u < WU; ++u) acc += av[u] * wv[u];
+        for (int t = w4 + 4 * WU; t < cnt; t += 4) {
+            const int c = d.wlist[t];
+            acc += (r < m ? A[(size_t)c * lda + r] : 0.0) * d.wcol[c];
+        }
+        sw[w4][lane] = acc;
+        __syncthreads();
+        if (w4 == 0 && r < m) d.work[r] = ysr - (((sw[0][lane] + sw[1][lane]) + sw[2][lane]) + sw[3][lane]);
+        return;
+    }
     if ((int)blockIdx.x >= gn && !d.A.dense) {
         // sparse A: work = ys - A w, one row per thread over its CSR entries
         // (update_gamma :1103-1134; entries loaded ahead, fixed order)
@@ -1303,18 +1343,22 @@ __global__ void __launch_bounds__(256) k_dual_ratio(SpxDev d, int gn, int tiles_
         v = fmax(v, tmax_part(d)[b]);
         if (rowpath && lead) e = max(e, d.tslots[b]);
     }
+    unsigned long long xp = 0;
+    if (rowpath && lead)
+        for (int b = lane; b < nprev; b += 64) xp = max(xp, d.xslots[b]);
     const double big = wmax(v);
     if (stop) return;
     TPH(2, 0);
     if (lead) {
         // publish max |trow| and the end of the pivot-row kernel (latest
-        // block exit stamp)
-        const unsigned long long ee = wmax_u64(e);
+        // block exit stamp), and the last exit of the kernel before it
+        const unsigned long long ee = wmax_u64(e), xx = wmax_u64(xp);
         if (lane == 0) {
             st->trow_max_bits = dbits(big);
             if (rowpath) {
                 st->tk_next = t_entry;
                 st->tk_end = ee;
+                st->tk_prev = xx;
             }
         }
     }
@@ -1701,6 +1745,7 @@ __global__ void __launch_bounds__(256) k_dual_commit(SpxDev d, int pse, int nvb,
                                                      double bytes_fixed)
 {
     const TraceScope trace_(d, 4);
+    const ExitStamp xs_(d.xslots, blockIdx.x);
     DState *st = d.st;
     // all loads first, stop tested before the first store; the pivot indices
     // are clamped so that the loads of a stopped iteration stay in bounds
@@ -1856,12 +1901,18 @@ __global__ void __launch_bounds__(256) k_dual_commit(SpxDev d, int pse, int nvb,
             const int ns = st->ns;
             const double rowb = rowpath == 1 ? 8.0 * (double)ns * n
                                 : rowpath == 2 ? 12.0 * (double)d.A.nnz : 8.0 * (double)m * n;
-            const unsigned long long tk0 = st->tk_start, tk1 = st->tk_end, tk2 = st->tk_next;
+            const unsigned long long tk0 = st->tk_start, tk1 = st->tk_end, tk2 = st->tk_next, tkp = st->tk_prev;
             if (rowpath && tk1 > tk0) {
                 st->bytes_trow += rowb;
                 st->trow_ticks += (double)(tk1 - tk0);
                 st->trow_ticks_b += (double)(tk2 - tk0);
                 st->trow_n += 1.0;
+                // from the last exit of the kernel before it (the previous
+                // pivot's commit / update; not the first pivot of a batch)
+                if (tkp < tk0 && tk0 - tkp < 20000ull) {
+                    st->trow_ticks_r += (double)(tk1 - tkp);
+                    st->trow_nr += 1.0;
+                }
             }
             st->tk_end = 0;
             st->bytes += rowb + 8.0 * (double)m * nwl0 + 8.0 * (double)m * (nr0 + 1) +
@@ -1939,6 +1990,385 @@ __global__ void __launch_bounds__(256) k_dual_commit(SpxDev d, int pse, int nvb,
 }
 
 // ---------------------------------------------------------------------------
+// k_dual_update (nr + 1 <= GM * 4 * waves): k_dual_ftran1 and k_dual_commit
+// in ONE kernel.  Block b owns the UPD_RPB = 16 rows [16 b, 16 b + 16); its
+// lanes are (list slice, row) pairs, its waves split the compact rho
+// (rho_idx[t] = rlist[t] for t < nr, then the unit entry of a leaving slack).
+// A thread loads its GM entries of inv(B)[r, rho_idx[t]] once, into
+// registers, and uses them twice:
+//   eval_tcol / update_gamma's FTRAN (glpspx02.js:937, :1103-1134):
+//     tcol_r = sum_{t < nr} inv(B)[r, c_t] h_c (+ h at a basic slack's row),
+//     u_r    = sum_{t < nr} inv(B)[r, c_t] work_c (+ the same unit part);
+//   then, once tcol_r is combined in LDS, the product-form update of those
+//     same entries: row r -= tcol_r / alpha_p rho (row p := rho / alpha_p).
+// alpha_p = tcol[p] = rho' h is formed by every block the same way (one
+// wave over the compact rho, fixed order), so no block waits for the block
+// that owns row p.  Everything else is k_dual_commit's per-row and per-column
+// work (update_bbar / update_cbar / update_gamma :1020-1134, the next chuzr
+// candidates — one per block — and the phase-I check), each block for its
+// 16 rows and an n / grid slice of the columns; the pick (pass 2) runs in
+// every wave as in k_dual_ftran1.  One kernel boundary and one read of the
+// active columns of inv(B) less per pivot than ftran1 + commit.
+// ---------------------------------------------------------------------------
+// rows per block of k_dual_update: 32 (GM = 8 entries per thread) or 16
+// (GM = 4); GK_UPD_RPB selects (experiments)
+static int upd_rpb()
+{
+    static const int v = [] {
+        const char *e = std::getenv("GK_UPD_RPB");
+        return (e && std::atoi(e) == 16) ? 16 : 32;
+    }();
+    return v;
+}
+
+struct PickOut {
+    int q, kq;
+    double teta, alfa;
+};
+
+// pick_resolve's choice without its state writes (every block of the caller
+// needs the same values)
+__device__ __forceinline__ PickOut pick_choose(const PickIn &pi)
+{
+    PickOut o;
+    if (pi.need2) {
+        const Cand b2 = wave_best<2>(pi.c);
+        o.q = b2.idx; o.teta = b2.k1; o.kq = b2.aux; o.alfa = b2.k2;
+    } else {
+        o.q = pi.q1; o.teta = pi.teta1; o.kq = pi.kq1; o.alfa = pi.alfa1;
+    }
+    return o;
+}
+
+template <int NRHS, int SP, int GM, int RPB>
+__global__ void __launch_bounds__(1024) k_dual_update(SpxDev d, int gn, int ncb, int nr_cap, int rowpath,
+                                                      double bytes_fixed)
+{
+    const TraceScope trace_(d, 3);
+    const ExitStamp xs_(d.xslots, blockIdx.x);
+    constexpr int SL = 64 / RPB;
+    __shared__ double sp[NRHS][16][64];
+    __shared__ double srow[NRHS][RPB];
+    __shared__ double salp[16 * SL];
+    __shared__ double salpha;
+    DState *st = d.st;
+    const int m = d.m, n = d.n;
+    const int lane = threadIdx.x & 63;
+    const int w = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+    const int nw = blockDim.x >> 6;
+    const int wa = nw - 1;                          // the wave that forms alpha_p
+    const int sl = lane / RPB, rl = lane % RPB;
+    const int r = blockIdx.x * RPB + rl;
+    const int gs = w * SL + sl, NSL = nw * SL;
+    const bool act = r < m;
+    const bool rowlane = (w == 0 && sl == 0 && act);
+    const size_t ldb = (size_t)d.ldb;
+    const double *__restrict__ Bv = d.Binv;
+    // ---- trip 1: everything independent of the entering choice
+    const int stop = st->stop;
+    PickIn pin = pick_load(d, NRHS == 2, gn, ncb);
+    pin.g = 0.0;                                    // gamma_p in every block, fixed order
+    if (NRHS == 2 && w == 0)
+        for (int b = lane; b < ncb; b += 64) pin.g += d.gpart[b];
+    const int nr = st->nr, ns = st->ns, p = max(st->p, 1), kp = max(st->kp, 1);
+    const double delta = st->delta;
+    const int binv_fresh = st->binv_fresh, rig = st->rigorous, phase = st->phase, refct = st->refct;
+    const double tol_bnd = st->tol_bnd, tol_dj = st->tol_dj;
+    int c0[GM];
+    double rv[GM];
+#pragma unroll
+    for (int u = 0; u < GM; ++u) {
+        const int t = gs + u * NSL;
+        c0[u] = (t <= nr_cap) ? d.rho_idx[t] : 0;
+        rv[u] = (t <= nr_cap) ? d.rho_val[t] : 0.0;
+    }
+    // the block's rows
+    const int kold = rowlane ? d.head[r] : 1;
+    double bb = rowlane ? d.bbar[r] : 0.0;
+    double g = (NRHS == 2 && rowlane) ? d.gamma[r] : 0.0;
+    const int tkp = d.type[kp - 1];
+    const bool refkp = NRHS == 2 && d.refsp[kp - 1] != 0;
+    // the block's columns (update_cbar, check_feas)
+    const int JPB = (n + gridDim.x - 1) / gridDim.x;
+    const int j = blockIdx.x * JPB + (int)threadIdx.x;
+    const bool colth = (int)threadIdx.x < JPB && j < n;
+    double cb = colth ? d.cbar[j] : 0.0;
+    const double tri = colth ? d.trow[j] : 0.0;
+    const int hkj = colth ? d.head[m + j] : 1;
+    // list maintenance operands (block 0, one thread of the last wave)
+    const bool maint = (blockIdx.x == 0 && w == wa && lane == 0);
+    int nr0 = 0, nwl0 = 0, rlast = 0, wlast = 0;
+    if (maint) {
+        nr0 = nr;
+        nwl0 = st->nwl;
+        rlast = d.rlist[max(nr0 - 1, 0)];
+        if (NRHS == 2) wlast = d.wlist[max(nwl0 - 1, 0)];
+    }
+    if (stop) return;
+    TPH(3, 0);
+    const double gsum = (NRHS == 2 && w == 0) ? wsum(pin.g) : 0.0;
+    // ---- the entering choice (every wave)
+    const PickOut pk = pick_choose(pin);
+    const int q = pk.q, kq = pk.kq;
+    const bool lead = blockIdx.x == 0 && threadIdx.x == 0;
+    if (q == 0) {
+        if (lead) { st->q = 0; st->stop = ST_Q0; }
+        return;
+    }
+    if (pk.alfa < 1e-5 * (1.0 + 0.01 * pin.big) && !pin.rigorous) {
+        if (lead) { st->q = q; st->stop = ST_SMALLPIV; }
+        return;
+    }
+    const double new_dq = (delta > 0.0 ? +1.0 : -1.0) * pk.teta;
+    // ---- trip 2: inv(B) entries, the multipliers, the choice's operands
+    const double *hcol = (!SP && kq > m) ? d.A.A + (size_t)(kq - m - 1) * d.A.lda : nullptr;
+    auto hval = [&](int c) { return hcol ? hcol[c] : (c == kq - 1 ? -1.0 : 0.0); };
+    double bv[GM];
+#pragma unroll
+    for (int u = 0; u < GM; ++u) {
+        const int t = gs + u * NSL;
+        bv[u] = (act && t < ns) ? Bv[(size_t)c0[u] * ldb + r] : 0.0;
+    }
+    double a = 0.0, b = 0.0, al = 0.0;
+    {
+        double xa[GM], xb[GM];
+#pragma unroll
+        for (int u = 0; u < GM; ++u) {
+            const int t = gs + u * NSL;
+            xa[u] = (!SP && t < ns) ? hval(c0[u]) : 0.0;
+            xb[u] = (NRHS == 2 && t < nr) ? d.work[c0[u]] : 0.0;
+        }
+#pragma unroll
+        for (int u = 0; u < GM; ++u) {
+            // alpha_p = rho' h over the slice's entries (the unit entry t = nr
+            // included); the FTRAN over t < nr only (unit columns per row)
+            if (!SP) {
+                al += rv[u] * xa[u];
+                if (gs + u * NSL < nr) a += bv[u] * xa[u];
+            }
+            if (NRHS == 2) b += bv[u] * xb[u];
+        }
+    }
+    double ua = 0.0, ub = 0.0;                      // unit columns of a basic slack at this row
+    if (rowlane && kold <= m) {
+        if (!SP) ua = hval(kold - 1);
+        if (NRHS == 2) ub = d.work[kold - 1];
+    }
+    if (SP) {
+        // sparse h = -N[q]: tcol = inv(B) h over the entries of column q, the
+        // columns of inv(B) read whole (unit columns included: no unit part)
+        if (kq > m) {
+            const int cq = kq - m - 1;
+            const int beg = d.A.cptr[cq], end = d.A.cptr[cq + 1];
+            for (int t = beg + gs; t < end; t += NSL)
+                a += d.A.cval[t] * (act ? Bv[(size_t)d.A.cind[t] * ldb + r] : 0.0);
+        } else if (gs == 0) {
+            a = act ? -Bv[(size_t)(kq - 1) * ldb + r] : 0.0;
+        }
+    }
+    // alpha_p: dense — the slices' partial sums of rho' h (lanes of row 0
+    // of each slice), combined in slice order below; sparse — row p of inv(B)
+    // times the CSC column, one wave
+    if (!SP && rl == 0) salp[gs] = al;
+    if (SP && w == wa) {
+        double s = 0.0;
+        if (kq > m) {
+            const int cq = kq - m - 1;
+            const int beg = d.A.cptr[cq], end = d.A.cptr[cq + 1];
+            for (int t = beg + lane; t < end; t += 64) s += d.A.cval[t] * Bv[(size_t)d.A.cind[t] * ldb + (p - 1)];
+        } else if (lane == 0) {
+            s = -Bv[(size_t)(kq - 1) * ldb + (p - 1)];
+        }
+        s = wsum(s);
+        if (lane == 0) salpha = s;
+    }
+    // operands of the row updates that depend on the choice
+    const int knew = (r == p - 1) ? kq : kold;
+    const int tkold = rowlane ? d.type[kold - 1] : 0;
+    const bool refk = (NRHS == 2 && rowlane) ? d.refsp[kold - 1] != 0 : false;
+    const int tknew = rowlane ? d.type[knew - 1] : 0;
+    const double lbn = rowlane ? d.lb[knew - 1] : 0.0, ubn = rowlane ? d.ub[knew - 1] : 0.0;
+    const double xq = (rowlane && r == p - 1) ? get_xN(d.stat, d.lb, d.ub, kq, q) : 0.0;
+    const int tkq = d.type[kq - 1];
+    const double piv2 = d.trow[q - 1];
+    const int kn = colth ? ((j == q - 1) ? kp : hkj) : 1;
+    const int ot = colth ? d.orig_type[kn - 1] : 0;
+    int rq = -1, wq = -1;
+    if (maint) {
+        if (kq <= m) rq = d.rpos[kq - 1];
+        if (NRHS == 2 && kq > m) wq = d.wpos[kq - m - 1];
+    }
+    sp[0][w][lane] = a;
+    if (NRHS == 2) sp[NRHS - 1][w][lane] = b;
+    TPH(3, 2);
+    __syncthreads();
+    if (w == 0 && sl == 0) {
+        double sa = 0.0, sb = 0.0;
+        for (int k = 0; k < nw; ++k)
+#pragma unroll
+            for (int z = 0; z < SL; ++z) {
+                sa += sp[0][k][rl + z * RPB];
+                if (NRHS == 2) sb += sp[NRHS - 1][k][rl + z * RPB];
+            }
+        srow[0][rl] = sa + ua;
+        if (NRHS == 2) srow[NRHS - 1][rl] = sb + ub;
+        if (!SP && rl == 0) {
+            double s = 0.0;
+            for (int k = 0; k < NSL; ++k) s += salp[k];
+            salpha = s;
+        }
+    }
+    __syncthreads();
+    TPH(3, 3);
+    const double piv1 = salpha;
+    const bool bad = fabs(piv1 - piv2) > 1e-8 * (1.0 + fabs(piv1)) ||
+                     !((piv1 > 0.0 && piv2 > 0.0) || (piv1 < 0.0 && piv2 < 0.0));
+    if (bad && (!binv_fresh || !rig)) {
+        if (lead) { st->q = q; st->kq = kq; st->stop = ST_PIVCHK; }
+        return;
+    }
+    const double tp = bad ? piv2 : piv1;
+    const double teta = delta / tp;
+    const double ti = srow[0][rl];
+    const double ui = (NRHS == 2) ? srow[NRHS - 1][rl] : 0.0;
+    // ---- product-form update of the entries held in registers
+    {
+        const bool z = (r == p - 1);
+        const double f = z ? 1.0 / tp : ti / tp;
+        const int ce = (kq <= m) ? kq - 1 : -1;
+#pragma unroll
+        for (int u = 0; u < GM; ++u) {
+            const int t = gs + u * NSL;
+            if (!act || t >= ns) continue;
+            const int c = c0[u];
+            double v = bv[u];
+            if (c == ce) v = z ? 1.0 : 0.0;
+            else v = (z ? 0.0 : v) - f * rv[u];
+            d.Binv[(size_t)c * ldb + r] = v;
+        }
+    }
+    // ---- rows: update_bbar / update_gamma, the next chuzr candidates
+    if (w == 0) {
+        Cand cnd = no_cand(0.0);
+        if (rowlane) {
+            d.tcol[r] = ti;
+            if (r == p - 1) bb = xq + teta;
+            else if (teta != 0.0) bb += ti * teta;
+            d.bbar[r] = bb;
+            if (NRHS == 2) {
+                const double eta_p = refkp ? 1.0 : 0.0;
+                const double gamma_p = eta_p + gsum;
+                if (r == p - 1) {
+                    if (tkq == FR) g = 1.0;
+                    else {
+                        g = gamma_p / (tp * tp);
+                        if (g < DBL_EPS) g = DBL_EPS;
+                    }
+                } else if (ti != 0.0 && tkold != FR) {
+                    const double t = ti / tp;
+                    const double t1 = g + t * t * gamma_p + 2.0 * t * ui;
+                    const double t2 = (refk ? 1.0 : 0.0) + eta_p * t * t;
+                    g = (t1 >= t2 ? t1 : t2);
+                    if (g < DBL_EPS) g = DBL_EPS;
+                }
+                if (tkp == FX && refkp && ti != 0.0) {
+                    double t = 0.0;
+                    bool apply = true;
+                    if (r == p - 1) {
+                        if (tkq == FR) apply = false; else t = 1.0 / tp;
+                    } else {
+                        if (tkold == FR) apply = false; else t = ti / tp;
+                    }
+                    if (apply) {
+                        g -= t * t;
+                        if (g < DBL_EPS) g = DBL_EPS;
+                    }
+                }
+                d.gamma[r] = g;
+            }
+            const bool reset = (NRHS == 2 && refct == 1);
+            cnd = chuzr_cand_v(r, knew, tknew, lbn, ubn, bb, reset ? 1.0 : g, tol_bnd);
+        }
+        const Cand best = wave_best<0>(cnd);
+        if (lane == 0) cand_chuzr(d)[blockIdx.x] = best;
+    }
+    // ---- columns: update_cbar (:1020), check_feas of phase I (:1296)
+    int badj = 0;
+    if (colth) {
+        const double cb_old = cb;
+        if (j == q - 1) {
+            cb = new_dq;
+            st->cbar_q_old = cb_old;
+        } else if (new_dq != 0.0)
+            cb -= tri * new_dq;
+        d.cbar[j] = cb;
+        badj = phase == 1 && ((cb < -tol_dj && (ot == LO || ot == FR)) || (cb > +tol_dj && (ot == UP || ot == FR)));
+    }
+    if (phase == 1 && __syncthreads_or(badj) && threadIdx.x == 0) atomicOr(&st->dinf, 1);
+    if (lead) {
+        st->q = q;
+        st->kq = kq;
+        st->new_dq = new_dq;
+        st->teta = teta;
+        st->pivot = tp;
+        st->pend = 1;
+        st->fxp = (tkp == FX);
+        st->rclr = (tkp == FX && refkp);
+    }
+    if (maint) {
+        // dense columns of inv(B): an entering slack's column is now e_p,
+        // a leaving slack's column became dense
+        int nrn = nr0;
+        if (kq <= m) {
+            d.rlist[rq] = rlast;
+            d.rpos[rlast] = rq;
+            d.rpos[kq - 1] = -1;
+            nrn--;
+        }
+        if (kp <= m) {
+            d.rlist[nrn] = kp - 1;
+            d.rpos[kp - 1] = nrn;
+            nrn++;
+        }
+        st->nr = nrn;
+        if (NRHS == 2) {
+            int nwl = nwl0;
+            if (wq >= 0) {
+                d.wlist[wq] = wlast;
+                d.wpos[wlast] = wq;
+                d.wpos[kq - m - 1] = -1;
+                nwl--;
+            }
+            if (kp > m && refkp && tkp != FX) {
+                d.wlist[nwl] = kp - m - 1;
+                d.wpos[kp - m - 1] = nwl;
+                nwl++;
+            }
+            st->nwl = nwl;
+        }
+        // algorithmic HBM bytes of this pivot: the pivot row,
+        // A w, and inv(B) read once and written once over the support of rho
+        const double rowb = rowpath == 1 ? 8.0 * (double)ns * n
+                            : rowpath == 2 ? 12.0 * (double)d.A.nnz : 8.0 * (double)m * n;
+        const unsigned long long tk0 = st->tk_start, tk1 = st->tk_end, tk2 = st->tk_next, tkp = st->tk_prev;
+        if (rowpath && tk1 > tk0) {
+            st->bytes_trow += rowb;
+            st->trow_ticks += (double)(tk1 - tk0);
+            st->trow_ticks_b += (double)(tk2 - tk0);
+            st->trow_n += 1.0;
+            // from the last exit of the kernel before it (the previous
+            // pivot's commit / update; not the first pivot of a batch)
+            if (tkp < tk0 && tk0 - tkp < 20000ull) {
+                st->trow_ticks_r += (double)(tk1 - tkp);
+                st->trow_nr += 1.0;
+            }
+        }
+        st->tk_end = 0;
+        st->bytes += rowb + 8.0 * (double)m * nwl0 + 16.0 * (double)m * ns + bytes_fixed;
+    }
+}
+
+// ---------------------------------------------------------------------------
 // host side
 // ---------------------------------------------------------------------------
 DualPlan dual_plan(const SpxDev &d, int nr_max, int nwl_max, int pse, int rigorous)
@@ -1974,6 +2404,28 @@ DualPlan dual_plan(const SpxDev &d, int nr_max, int nwl_max, int pse, int rigoro
     pl.colpath = (!d.A.dense && !rigorous && nr_max <= FONE_MAX) ? 1 : 0;
     pl.awsplits = std::max(1, std::min(cdiv(std::max(nwl_max, 1), 32), 64));
     pl.awsplits = std::max(1, std::min<int>(pl.awsplits, (int)(d.awpart_cap / std::max(m, 1))));
+    // FTRAN + commit in one kernel while the active columns of inv(B) fit the
+    // registers of a 16-row block (4 entries per thread — 124 VGPRs at 1024
+    // threads; 8 would spill —, 4 list slices per wave, up to 16 waves: at
+    // most 256 entries); GK_DUAL_UPDATE=0 keeps the two-kernel path
+    static const int upd_on = [] {
+        const char *e = std::getenv("GK_DUAL_UPDATE");
+        return e ? std::atoi(e) : 1;
+    }();
+    pl.gm = 4 * cdiv(m, 256);
+    const int need = ns_max + 1;
+    const int rpb = upd_rpb(), sl = 64 / rpb;
+    const int rows_blocks = cdiv(m, rpb);
+    if (upd_on && !rigorous && (pl.rowpath || pl.colpath) && (pl.fone || pl.colpath) && need <= 4 * 4 * 16 &&
+        n <= rows_blocks * 1024) {
+        pl.ugm = rpb == 32 ? 8 : 4;
+        pl.uwaves = std::min(16, std::max(1, cdiv(need, pl.ugm * sl)));
+        // every thread of the block also covers a column slot of update_cbar
+        while (pl.uwaves < 16 && cdiv(n, rows_blocks) > 64 * pl.uwaves) pl.uwaves++;
+        pl.fupd = 1;
+        pl.gm = rows_blocks;
+    }
+    pl.awone = (pse && d.A.dense && nwl_max <= 512) ? std::max(nwl_max, 1) : 0;
     return pl;
 }
 
@@ -1998,8 +2450,27 @@ static double bytes_fixed(const SpxDev &d) { return 96.0 * ((double)d.m + d.n); 
 
 void dual_batch_begin(hipStream_t s, const SpxDev &d, const DualPlan &pl)
 {
-    (void)pl;
-    hipLaunchKernelGGL(k_dual_prep, dim3(cdiv(std::max(d.m, d.n), 256)), dim3(256), 0, s, d);
+    hipLaunchKernelGGL(k_dual_prep, dim3(cdiv(std::max(d.m, d.n), 256)), dim3(256), 0, s, d,
+                       std::max(pl.gm, 4 * cdiv(d.m, 256)));
+}
+
+// blocks of the kernel that ends a pivot (their exit stamps: xslots)
+static int prev_blocks(const SpxDev &d, const DualPlan &pl)
+{
+    if (pl.fupd) return cdiv(d.m, pl.ugm == 8 ? 32 : 16);
+    return cdiv(std::max(d.m, d.n), 256) + cdiv(d.m, 512) * pl.uchunks;
+}
+
+template <int NRHS, int SP>
+static void launch_update(hipStream_t s, const SpxDev &d, const DualPlan &pl, int gn, int ncb, int rowpath)
+{
+    const dim3 grid(cdiv(d.m, pl.ugm == 8 ? 32 : 16)), block(64 * pl.uwaves);
+    if (pl.ugm == 8)
+        hipLaunchKernelGGL((k_dual_update<NRHS, SP, 8, 32>), grid, block, 0, s, d, gn, ncb, pl.nr_cap, rowpath,
+                           bytes_fixed(d));
+    else
+        hipLaunchKernelGGL((k_dual_update<NRHS, SP, 4, 16>), grid, block, 0, s, d, gn, ncb, pl.nr_cap, rowpath,
+                           bytes_fixed(d));
 }
 
 void dual_batch_end(hipStream_t s, const SpxDev &d, const DualPlan &pl)
@@ -2026,10 +2497,15 @@ void dual_iteration2(hipStream_t s, const SpxDev &d, const DualPlan &pl, hipEven
     if (pl.colpath) {
         // sparse A: four kernels, as the dense row path
         if (ev0) (void)hipEventRecord(ev0, s);
-        hipLaunchKernelGGL(k_dual_col, dim3(gv), dim3(256), 0, s, d, pl.pse, pl.nr_cap);
+        hipLaunchKernelGGL(k_dual_col, dim3(gv), dim3(256), 0, s, d, pl.pse, pl.nr_cap, pl.gm);
         if (ev1) (void)hipEventRecord(ev1, s);
         hipLaunchKernelGGL(k_dual_ratio, dim3(gn + (pl.pse ? cdiv(m, 256) : 0)), dim3(256), 0, s, d, gn, tiles_m, 2,
-                           ncb);
+                           ncb, 0, prev_blocks(d, pl));
+        if (pl.fupd) {
+            if (pl.pse) launch_update<2, 1>(s, d, pl, gn, ncb, 2);
+            else launch_update<1, 1>(s, d, pl, gn, ncb, 2);
+            return;
+        }
         // 16 rows per block (4 list slices per wave): 4x the blocks of the
         // dense layout for the small m of sparse problems
         if (pl.pse)
@@ -2046,7 +2522,7 @@ void dual_iteration2(hipStream_t s, const SpxDev &d, const DualPlan &pl, hipEven
         // chuzr, rho and the pivot row in one kernel
         ncb = cdiv(std::max(m, n), 64);
         if (ev0) (void)hipEventRecord(ev0, s);
-        hipLaunchKernelGGL(k_dual_row, dim3(ncb), dim3(64 * pl.twaves), 0, s, d, pl.pse, pl.nr_cap);
+        hipLaunchKernelGGL(k_dual_row, dim3(ncb), dim3(64 * pl.twaves), 0, s, d, pl.pse, pl.nr_cap, pl.gm);
         if (ev1) (void)hipEventRecord(ev1, s);
     } else {
         if (!pl.rigorous && d.A.dense && m >= 1024)
@@ -2061,8 +2537,14 @@ void dual_iteration2(hipStream_t s, const SpxDev &d, const DualPlan &pl, hipEven
         hipLaunchKernelGGL(k_trow_finish, dim3(gv), dim3(256), 0, s, d, pl.pse);
     }
     const int aw = (pl.pse && d.A.dense) ? 1 : 0;
-    hipLaunchKernelGGL(k_dual_ratio, dim3(gn + (aw ? tiles_m * pl.awsplits : 0)), dim3(256), 0, s, d, gn, tiles_m,
-                       pl.rowpath, ncb);
+    const int awone = (aw && pl.fused) ? pl.awone : 0;
+    hipLaunchKernelGGL(k_dual_ratio, dim3(gn + (aw ? (awone ? cdiv(m, 64) : tiles_m * pl.awsplits) : 0)), dim3(256), 0,
+                       s, d, gn, tiles_m, pl.rowpath, ncb, awone, prev_blocks(d, pl));
+    if (pl.fupd) {
+        if (pl.pse) launch_update<2, 0>(s, d, pl, gn, ncb, pl.rowpath);
+        else launch_update<1, 0>(s, d, pl, gn, ncb, pl.rowpath);
+        return;
+    }
     if (pl.fused) {
         if (pl.fone) {
             if (pl.pse)

@@ -123,7 +123,7 @@ struct Engine {
     DBuf<double> rho_val, gpart, cand, awpart;
     DBuf<char> upstage;                         // device side of the coalesced uploads
     DBuf<int> xlist;                            // eval_cbar: basic slacks with a nonzero cost (primal phase I)
-    DBuf<unsigned long long> tslots;
+    DBuf<unsigned long long> tslots, xslots;
     std::vector<GraphEntry> graphs;
     unsigned long long graph_clock = 0;
     int kbatch = 8;                           // batch length carried across calls
@@ -145,7 +145,7 @@ struct Engine {
     ~Engine()
     {
         A.release(); AT.release(); rlist.release(); rpos.release(); rho_idx.release(); rho_val.release();
-        gpart.release(); awcnt.release(); tslots.release(); trace.release(); wlist.release(); wpos.release(); cand.release(); awpart.release(); cptr.release(); cind.release(); rptr.release(); rcol.release(); cval.release(); rval.release();
+        gpart.release(); awcnt.release(); tslots.release(); xslots.release(); trace.release(); wlist.release(); wpos.release(); cand.release(); awpart.release(); cptr.release(); cind.release(); rptr.release(); rcol.release(); cval.release(); rval.release();
         type.release(); orig_type.release(); stat.release(); refsp.release();
         lb.release(); ub.release(); coef.release(); orig_lb.release(); orig_ub.release(); obj.release();
         head.release(); bind.release();
@@ -337,6 +337,13 @@ static void engine_alloc(Engine &E, int m, int n)
         }
     }
     E.tslots.ensure(std::max((size_t)((n + 511) / 512) * 2048, 4 * (size_t)gv) + 1);
+    {
+        const size_t nx = (size_t)(m + 15) / 16 + gv + (size_t)((m + 511) / 512) * 2048 + 1;
+        if (E.xslots.n < nx || !E.xslots.p) {
+            E.xslots.ensure(nx);
+            HIPCHK(hipMemset(E.xslots.p, 0, E.xslots.n * sizeof(unsigned long long)));
+        }
+    }
 }
 
 __global__ void k_densify(const int *cptr, const int *cind, const double *cval, int n, double *A, int lda)
@@ -452,6 +459,7 @@ struct Spx {
         d.wlist = E->wlist.p; d.wpos = E->wpos.p; d.cand = E->cand.p;
         d.awpart = E->awpart.p; d.awpart_cap = (size_t)AW_SPLITS * m; d.awcnt = E->awcnt.p;
         d.tslots = E->tslots.p;
+        d.xslots = E->xslots.p;
         d.trace = nullptr;
         if (E->prof == 2) {
             if (!E->trace.p) {
@@ -1135,6 +1143,8 @@ int Spx::batch(int K, int rigorous)
     f->stats.trow_dev_ms = hs.trow_ticks / (double)ctx->wall_khz;
     f->stats.trow_dev_ms_b = hs.trow_ticks_b / (double)ctx->wall_khz;
     f->stats.trow_dev_launches = (long long)hs.trow_n;
+    f->stats.trow_dev_ms_r = hs.trow_ticks_r / (double)ctx->wall_khz;
+    f->stats.trow_dev_launches_r = (long long)hs.trow_nr;
     if (dual && E->prof) {
         for (int t = 0; t < hs.npiv; t++) {
             float ms = 0.f;

@@ -65,6 +65,9 @@ struct DState {
                                             // refsp[kp] to clear at change_basis
     int kq1, pad2, pad3, pad4;              // variable of the pass-1 choice
     double alfa1, pad5;                     // |trow| of the pass-1 choice
+    unsigned long long tk_prev, tk_pad2;    // last block exit of the kernel before the pivot-row kernel
+    double trow_ticks_r, trow_nr;           // pivot-row kernels, previous kernel's last exit to their last
+                                            // exit (the bracket of a profiler's per-dispatch record)
 };
 
 // ---- dense GEMV helpers ---------------------------------------------------
@@ -136,6 +139,7 @@ struct SpxDev {
     size_t awpart_cap;
     int *awcnt;                              // per 512-row tile: arrivals of the A w splits (the last one reduces)
     unsigned long long *tslots;              // per-block end stamps of the pivot-row kernel
+    unsigned long long *xslots;              // per-block exit stamps of the commit / update kernel
     unsigned long long *trace;               // profiling only: per-kernel, per-block entry / exit clock
 };
 constexpr int TRACE_KERNELS = 8, TRACE_BLOCKS = 2048;   // trace[(kid * TRACE_BLOCKS + block) * 2 + {0, 1}]
@@ -156,6 +160,10 @@ struct DualPlan {
     int fone, fwaves;             // 1: FTRAN in one kernel (k_dual_ftran1), fwaves waves per 64-row block
     int lpsu;                     // rank-1 update: list entries per chunk
     int colpath;                  // 1: sparse A — k_dual_col, CSR A w in k_dual_ratio, sparse k_dual_ftran1
+    int fupd;                     // 1: FTRAN + commit in one kernel (k_dual_update)
+    int ugm, uwaves;              // k_dual_update: inv(B) entries per thread, waves per block
+    int gm;                       // chuzr candidate slots (4 per 256 rows, or one per 16 rows with fupd)
+    int awone;                    // dense A w in one pass over 64-row tiles: the cap of nwl (0: split path)
 };
 void dual_batch_begin(hipStream_t s, const SpxDev &d, const DualPlan &pl);
 void dual_batch_end(hipStream_t s, const SpxDev &d, const DualPlan &pl);

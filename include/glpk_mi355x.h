@@ -152,6 +152,9 @@ typedef struct {
     double trow_dev_ms;         /* device wall-clock execution span of the row-path pivot-row kernels */
     long long trow_dev_launches;
     double trow_dev_ms_b;       /* same, from their entry to the next kernel's entry (dispatch included) */
+    double trow_dev_ms_r;       /* same, from the last block exit of the kernel before them to their
+                                   own last block exit (a profiler's per-dispatch bracket) */
+    long long trow_dev_launches_r;
 } gk_spx_stats;
 void gk_bfd_last_stats(const gk_bfd *bfd, gk_spx_stats *st);
 /* record HIP events around the pivot-row kernel of every dual pivot (benches) */
