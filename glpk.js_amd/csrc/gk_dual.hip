@@ -307,20 +307,27 @@ struct FinishIn {
     TopState t;
 };
 
+// every field is loaded unconditionally before any of them is tested (a
+// short-circuit test between two loads makes the compiler issue the second
+// only after the first returned: one memory round trip per test)
 __device__ __forceinline__ FinishIn finish_load(const SpxDev &d)
 {
     const DState *st = d.st;
     FinishIn f;
-    f.pend = st->pend;
-    f.t.iter_left = st->iter_left - f.pend;
-    f.t.refact = st->refact_pending || (f.pend && st->upd_cnt + 1 >= st->upd_lim);
-    f.t.refct = (f.pend && st->pricing == PT_PSE && st->refct > 0) ? st->refct - 1 : st->refct;
-    f.t.obj = st->obj;
-    if (f.pend && st->phase == 2) f.t.obj += (st->cbar_q_old / st->zeta) * (st->delta / st->pivot);
+    const int pend = st->pend, iter_left = st->iter_left, rpend = st->refact_pending, upd_cnt = st->upd_cnt,
+              upd_lim = st->upd_lim, pricing = st->pricing, refct = st->refct, phase = st->phase;
+    const double obj = st->obj, cqo = st->cbar_q_old, zeta = st->zeta, delta = st->delta, pivot = st->pivot;
     f.p = st->p; f.q = st->q; f.kp = st->kp; f.kq = st->kq;
-    f.fxp = st->fxp; f.rclr = st->rclr; f.upd_cnt = st->upd_cnt; f.it_cnt = st->it_cnt; f.npiv = st->npiv;
+    f.fxp = st->fxp; f.rclr = st->rclr; f.it_cnt = st->it_cnt; f.npiv = st->npiv;
     f.rig = st->rigorous;
-    f.delta = st->delta;
+    f.pend = pend;
+    f.upd_cnt = upd_cnt;
+    f.delta = delta;
+    f.t.iter_left = iter_left - pend;
+    f.t.refact = (rpend != 0) | ((pend != 0) & (upd_cnt + 1 >= upd_lim));
+    f.t.refct = ((pend != 0) & (pricing == PT_PSE) & (refct > 0)) ? refct - 1 : refct;
+    const double dobj = (cqo / zeta) * (delta / pivot);
+    f.t.obj = ((pend != 0) & (phase == 2)) ? obj + dobj : obj;
     return f;
 }
 
@@ -825,29 +832,37 @@ __global__ void __launch_bounds__(1024) k_dual_row(SpxDev d, int pse, int nr_cap
     const int w = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
     const int nw = blockDim.x >> 6;
     const int idx = blockIdx.x * 64 + lane;
-    const bool lead = (blockIdx.x == 0);
+    // the block that applies the pending change of basis, publishes rho and the
+    // scalar state: the last one (no slack slots when n > m, so the lightest)
+    const bool lead = (blockIdx.x == gridDim.x - 1);
     // ---- trip 1: state, chuzr candidates, the wave's list entries, slots
     const int stop = st->stop;
     const FinishIn fin = finish_load(d);
     const int pricing = st->pricing, phase = st->phase, dinf = st->dinf, nr = st->nr;
     const double zeta = st->zeta, obj_ll = st->obj_ll, obj_ul = st->obj_ul;
     const RatioIn rin = ratio_in(st);
+    // unconditional loads at clamped indices, selected afterwards: no load
+    // waits for another (see finish_load)
+    Cand ce[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) ce[u] = cand_chuzr(d)[min(lane + 64 * u, gm - 1)];
+    int c0[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) c0[u] = d.rlist[min(w + u * nw, m - 1)];
+    int pos1 = d.bind[m + min(idx, n - 1)];
+    int pos2 = d.bind[min(idx, m - 1)];
     Cand cc = no_cand(0.0);
-    for (int b = lane; b < gm; b += 64) {
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+        if (lane + 64 * u < gm && better<0>(ce[u], cc)) cc = ce[u];
+    for (int b = lane + 256; b < gm; b += 64) {
         const Cand e = cand_chuzr(d)[b];
         if (better<0>(e, cc)) cc = e;
     }
-    int c0[8];
 #pragma unroll
-    for (int u = 0; u < 8; ++u) {
-        const int t = w + u * nw;
-        c0[u] = (t < nr_cap) ? d.rlist[t] : 0;
-    }
-    int pos1 = 0, pos2 = 0;
-    if (w == 0) {
-        pos1 = (idx < n) ? d.bind[m + idx] : 0;
-        pos2 = (idx < m) ? d.bind[idx] : 0;
-    }
+    for (int u = 0; u < 8; ++u) c0[u] = (w + u * nw < nr_cap) ? c0[u] : 0;
+    if (w != 0 || idx >= n) pos1 = 0;
+    if (w != 0 || idx >= m) pos2 = 0;
     if (stop) return;
     if (lead && threadIdx.x == 0) st->tk_start = wall_clock64();
     // ---- decisions (identical in every block)
@@ -903,24 +918,36 @@ __global__ void __launch_bounds__(1024) k_dual_row(SpxDev d, int pse, int nr_cap
         const int t = w + u * nw;
         int c = c0[u];
         if (t == nr) c = kp - 1;             // the unit entry (only when kp <= m: t < ns)
-        v0[u] = (t < nr) ? brow[(size_t)c * ldb] : 1.0;
-        a0[u] = (t < ns) ? col[(size_t)c * ldt] : 0.0;
+        // list entries past nr are stale (or never written): clamp the
+        // address, the value is not used
+        const int ca = min(max(c, 0), m - 1);
+        const double bv = brow[(size_t)ca * ldb], av = col[(size_t)ca * ldt];
+        v0[u] = (t < nr) ? bv : 1.0;
+        a0[u] = (t < ns) ? av : 0.0;
         c0[u] = c;
     }
     const signed char stq = fin.fxp ? NS : (fin.delta > 0.0 ? NL : NU);
     int s1 = 0, s2 = 0;
     double cb1 = 0.0, cb2 = 0.0, rho2 = 0.0;
     bool ref1 = false, ref2 = false;
-    if (j1 >= 0) {
-        s1 = (fin.pend && j1 == fin.q - 1) ? stq : d.stat[j1];
-        cb1 = d.cbar[j1];
-        if (pse && !reset) ref1 = d.refsp[m + idx] != 0 && !(fin.pend && fin.rclr && m + idx + 1 == fin.kp);
-    }
-    if (j2 >= 0) {
-        s2 = (fin.pend && j2 == fin.q - 1) ? stq : d.stat[j2];
-        cb2 = d.cbar[j2];
-        rho2 = brow[(size_t)idx * ldb];      // a non-basic slack: column idx of inv(B) is dense
-        if (pse && !reset) ref2 = d.refsp[idx] != 0 && !(fin.pend && fin.rclr && idx + 1 == fin.kp);
+    if (w == 0) {
+        // the slot operands, loaded at clamped indices with the trip-2 loads
+        const int j1c = max(j1, 0), j2c = max(j2, 0);
+        const int l1 = d.stat[j1c], l2 = d.stat[j2c];
+        const double c1 = d.cbar[j1c], c2 = d.cbar[j2c];
+        const double r2 = brow[(size_t)min(idx, m - 1) * ldb];   // a non-basic slack: column idx of inv(B) is dense
+        const int f1 = d.refsp[m + min(idx, n - 1)], f2 = d.refsp[min(idx, m - 1)];
+        if (j1 >= 0) {
+            s1 = (fin.pend && j1 == fin.q - 1) ? stq : l1;
+            cb1 = c1;
+            if (pse && !reset) ref1 = f1 != 0 && !(fin.pend && fin.rclr && m + idx + 1 == fin.kp);
+        }
+        if (j2 >= 0) {
+            s2 = (fin.pend && j2 == fin.q - 1) ? stq : l2;
+            cb2 = c2;
+            rho2 = r2;
+            if (pse && !reset) ref2 = f2 != 0 && !(fin.pend && fin.rclr && idx + 1 == fin.kp);
+        }
     }
     double acc = 0.0;
 #pragma unroll
@@ -1230,24 +1257,30 @@ __global__ void __launch_bounds__(256) k_dual_ratio(SpxDev d, int gn, int tiles_
         __shared__ double sw[4][64];
         const int lane = threadIdx.x & 63, w4 = threadIdx.x >> 6;
         const int r = (blockIdx.x - gn) * 64 + lane;
+        const int rc = min(r, m - 1);
         constexpr int WU = 16;
+        // unconditional loads at clamped indices (no load waits for another)
         int cl[WU];
 #pragma unroll
-        for (int u = 0; u < WU; ++u) {
-            const int t = w4 + 4 * u;
-            cl[u] = (t < nwl_cap) ? d.wlist[t] : 0;
-        }
+        for (int u = 0; u < WU; ++u) cl[u] = d.wlist[min(w4 + 4 * u, n - 1)];
         const int cnt = st->nwl;
-        const double ysr = (r < m) ? d.ys[r] : 0.0;
+        const double ysr = d.ys[rc];
         if (stop) return;
         const double *__restrict__ A = d.A.A;
         const size_t lda = (size_t)d.A.lda;
         double wv[WU], av[WU];
 #pragma unroll
         for (int u = 0; u < WU; ++u) {
-            const bool ok = w4 + 4 * u < cnt;
-            wv[u] = ok ? d.wcol[cl[u]] : 0.0;
-            av[u] = (ok && r < m) ? A[(size_t)cl[u] * lda + r] : 0.0;
+            // entries past nwl are stale (or never written): clamped address
+            const int c = (w4 + 4 * u < nwl_cap) ? min(max(cl[u], 0), n - 1) : 0;
+            wv[u] = d.wcol[c];
+            av[u] = A[(size_t)c * lda + rc];
+        }
+#pragma unroll
+        for (int u = 0; u < WU; ++u) {
+            const bool ok = w4 + 4 * u < cnt && r < m;
+            wv[u] = ok ? wv[u] : 0.0;
+            av[u] = ok ? av[u] : 0.0;
         }
         double acc = 0.0;
 #pragma unroll
@@ -1321,31 +1354,43 @@ __global__ void __launch_bounds__(256) k_dual_ratio(SpxDev d, int gn, int tiles_
     const unsigned long long t_entry = (rowpath && blockIdx.x == 0 && threadIdx.x == 0) ? wall_clock64() : 0ull;
     const RatioIn rin = ratio_in(st);
     const int j = blockIdx.x * blockDim.x + threadIdx.x;
-    const double trj = (j < n) ? d.trow[j] : 0.0;
-    const double cbj = (j < n) ? d.cbar[j] : 0.0;
-    const int sj = (j < n) ? d.stat[j] : 0;
-    const int kj = (j < n) ? d.head[m + j] : 0;
+    const int jc = min(j, n - 1);
+    // unconditional loads at clamped indices, selected afterwards (no load
+    // waits for another)
+    double trj = d.trow[jc], cbj = d.cbar[jc];
+    int sj = d.stat[jc], kj = d.head[m + jc];
     const bool lead = (blockIdx.x == 0 && threadIdx.x < 64);
     constexpr int CPL = 8;                    // group candidates per lane held in registers
     Cand cl[CPL];
-    double v = 0.0;
-    unsigned long long e = 0;
+    double tv[CPL];
 #pragma unroll
     for (int u = 0; u < CPL; ++u) {
-        const int b = lane + u * 64;
-        cl[u] = (b < ncb) ? cand_pass1(d)[b] : no_cand(DBL_MAX);
-        if (b < ncb) {
-            v = fmax(v, tmax_part(d)[b]);
-            if (rowpath && lead) e = max(e, d.tslots[b]);
-        }
+        const int b = min(lane + u * 64, ncb - 1);
+        cl[u] = cand_pass1(d)[b];
+        tv[u] = tmax_part(d)[b];
     }
-    for (int b = lane + CPL * 64; b < ncb; b += 64) {
-        v = fmax(v, tmax_part(d)[b]);
-        if (rowpath && lead) e = max(e, d.tslots[b]);
+    unsigned long long e = 0, xp = 0;
+    if (rowpath && lead) {
+        unsigned long long te[CPL], tx[4];
+#pragma unroll
+        for (int u = 0; u < CPL; ++u) te[u] = d.tslots[min(lane + u * 64, ncb - 1)];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) tx[u] = d.xslots[min(lane + u * 64, max(nprev - 1, 0))];
+#pragma unroll
+        for (int u = 0; u < CPL; ++u) e = max(e, te[u]);
+#pragma unroll
+        for (int u = 0; u < 4; ++u) xp = max(xp, tx[u]);
+        for (int b = lane + CPL * 64; b < ncb; b += 64) e = max(e, d.tslots[b]);
+        for (int b = lane + 4 * 64; b < nprev; b += 64) xp = max(xp, d.xslots[b]);
     }
-    unsigned long long xp = 0;
-    if (rowpath && lead)
-        for (int b = lane; b < nprev; b += 64) xp = max(xp, d.xslots[b]);
+    if (j >= n) { trj = 0.0; cbj = 0.0; sj = 0; kj = 0; }
+    double v = 0.0;
+#pragma unroll
+    for (int u = 0; u < CPL; ++u) {
+        if (lane + u * 64 >= ncb) cl[u] = no_cand(DBL_MAX);
+        else v = fmax(v, tv[u]);
+    }
+    for (int b = lane + CPL * 64; b < ncb; b += 64) v = fmax(v, tmax_part(d)[b]);
     const double big = wmax(v);
     if (stop) return;
     TPH(2, 0);
@@ -2010,13 +2055,15 @@ __global__ void __launch_bounds__(256) k_dual_commit(SpxDev d, int pse, int nvb,
 // every wave as in k_dual_ftran1.  One kernel boundary and one read of the
 // active columns of inv(B) less per pivot than ftran1 + commit.
 // ---------------------------------------------------------------------------
-// rows per block of k_dual_update: 32 (GM = 8 entries per thread) or 16
-// (GM = 4); GK_UPD_RPB selects (experiments)
+// rows per block of k_dual_update: 16 (GM = 4 entries per thread) or 32
+// (GM = 8: spills to scratch at 1024 threads and 128 VGPRs — 68 bytes per
+// thread, 2.3x the algorithmic write traffic in the PMC counts);
+// GK_UPD_RPB=32 selects it (experiments)
 static int upd_rpb()
 {
     static const int v = [] {
         const char *e = std::getenv("GK_UPD_RPB");
-        return (e && std::atoi(e) == 16) ? 16 : 32;
+        return (e && std::atoi(e) == 32) ? 32 : 16;
     }();
     return v;
 }
@@ -2040,6 +2087,83 @@ __device__ __forceinline__ PickOut pick_choose(const PickIn &pi)
     return o;
 }
 
+// the books of a committed pivot (k_dual_update's block 0, its last wave):
+// the dense-column list of inv(B) — an entering slack's column is now e_p, a
+// leaving slack's column became dense —, the reference-space list of
+// update_gamma's A w, and the algorithmic bytes and device-clock spans of the
+// pivot.  Its operands are loaded with the kernel's second
+// trip and parked in LDS (holding them in registers to the end of the kernel
+// spills), so the bookkeeping at the end is stores only.
+struct Books {
+    int nwl0, rlast, wlast, rq, wq;
+    unsigned long long tk0, tk1, tk2, tkp;
+    double ab, abt, att, attb, atn, attr, atnr;
+};
+
+template <int NRHS>
+__device__ __forceinline__ void books_load(const SpxDev &d, Books &b, int nr, int kqc)
+{
+    const DState *st = d.st;
+    const int m = d.m, n = d.n;
+    const int nwl0 = (NRHS == 2) ? st->nwl : 0;
+    const int rlast = d.rlist[max(nr - 1, 0)];
+    const int wlast = (NRHS == 2) ? d.wlist[max(nwl0 - 1, 0)] : 0;
+    const int rq = d.rpos[min(kqc, m) - 1];
+    const int wq = (NRHS == 2) ? d.wpos[min(max(kqc - m, 1), n) - 1] : -1;
+    const unsigned long long tk0 = st->tk_start, tk1 = st->tk_end, tk2 = st->tk_next, tkp = st->tk_prev;
+    const double ab = st->bytes, abt = st->bytes_trow, att = st->trow_ticks, attb = st->trow_ticks_b;
+    const double atn = st->trow_n, attr = st->trow_ticks_r, atnr = st->trow_nr;
+    b.nwl0 = nwl0; b.rlast = rlast; b.wlast = wlast; b.rq = rq; b.wq = wq;
+    b.tk0 = tk0; b.tk1 = tk1; b.tk2 = tk2; b.tkp = tkp;
+    b.ab = ab; b.abt = abt; b.att = att; b.attb = attb; b.atn = atn; b.attr = attr; b.atnr = atnr;
+}
+
+template <int NRHS>
+__device__ __forceinline__ void books_store(const SpxDev &d, const Books &b, int kp, int kq, int tkp, bool refkp,
+                                            int nr, int ns, int rowpath, double bytes_fixed)
+{
+    // straight-line code (selects and stores to a spare slot past the end of
+    // each list instead of branches): this runs in one wave per pivot, and
+    // each branch of it costs an instruction fetch on the critical path
+    DState *st = d.st;
+    const int m = d.m, n = d.n;
+    const int ds = m, dw = max(m, n);                     // spare slots of rlist / rpos and wlist / wpos
+    const bool ent = kq <= m, lv = kp <= m;
+    d.rlist[ent ? b.rq : ds] = b.rlast;
+    d.rpos[ent ? b.rlast : ds] = b.rq;
+    d.rpos[ent ? kq - 1 : ds] = -1;
+    const int nr1 = nr - (ent ? 1 : 0);
+    d.rlist[lv ? nr1 : ds] = kp - 1;
+    d.rpos[lv ? kp - 1 : ds] = nr1;
+    st->nr = nr1 + (lv ? 1 : 0);
+    if (NRHS == 2) {
+        const bool wout = kq > m && b.wq >= 0, win = kp > m && refkp && tkp != FX;
+        d.wlist[wout ? b.wq : dw] = b.wlast;
+        d.wpos[wout ? b.wlast : dw] = b.wq;
+        d.wpos[wout ? kq - m - 1 : dw] = -1;
+        const int nw1 = b.nwl0 - (wout ? 1 : 0);
+        d.wlist[win ? nw1 : dw] = kp - m - 1;
+        d.wpos[win ? kp - m - 1 : dw] = nw1;
+        st->nwl = nw1 + (win ? 1 : 0);
+    }
+    // the pivot row, A w, and inv(B) read once and written once over the
+    // support of rho; the device-clock spans of the pivot-row kernel, from
+    // its entry and from the last exit of the kernel before it (the previous
+    // pivot's commit / update; not the first pivot of a batch)
+    const double rowb = rowpath == 1 ? 8.0 * (double)ns * n
+                        : rowpath == 2 ? 12.0 * (double)d.A.nnz : 8.0 * (double)m * n;
+    const bool tm = rowpath && b.tk1 > b.tk0;
+    const bool tr = tm && b.tkp < b.tk0 && b.tk0 - b.tkp < 20000ull;
+    st->bytes_trow = tm ? b.abt + rowb : b.abt;
+    st->trow_ticks = tm ? b.att + (double)(b.tk1 - b.tk0) : b.att;
+    st->trow_ticks_b = tm ? b.attb + (double)(b.tk2 - b.tk0) : b.attb;
+    st->trow_n = tm ? b.atn + 1.0 : b.atn;
+    st->trow_ticks_r = tr ? b.attr + (double)(b.tk1 - b.tkp) : b.attr;
+    st->trow_nr = tr ? b.atnr + 1.0 : b.atnr;
+    st->tk_end = 0;
+    st->bytes = b.ab + (rowb + 8.0 * (double)m * b.nwl0 + 16.0 * (double)m * ns + bytes_fixed);
+}
+
 template <int NRHS, int SP, int GM, int RPB>
 __global__ void __launch_bounds__(1024) k_dual_update(SpxDev d, int gn, int ncb, int nr_cap, int rowpath,
                                                       double bytes_fixed)
@@ -2051,6 +2175,7 @@ __global__ void __launch_bounds__(1024) k_dual_update(SpxDev d, int gn, int ncb,
     __shared__ double srow[NRHS][RPB];
     __shared__ double salp[16 * SL];
     __shared__ double salpha;
+    __shared__ Books sbk;
     DState *st = d.st;
     const int m = d.m, n = d.n;
     const int lane = threadIdx.x & 63;
@@ -2058,18 +2183,30 @@ __global__ void __launch_bounds__(1024) k_dual_update(SpxDev d, int gn, int ncb,
     const int nw = blockDim.x >> 6;
     const int wa = nw - 1;                          // the wave that forms alpha_p
     const int sl = lane / RPB, rl = lane % RPB;
+    // block 0 keeps the books (list maintenance, the scalar state and the
+    // byte / clock accounting of the pivot), in its last wave
+    const bool bk = blockIdx.x == 0;
     const int r = blockIdx.x * RPB + rl;
     const int gs = w * SL + sl, NSL = nw * SL;
     const bool act = r < m;
     const bool rowlane = (w == 0 && sl == 0 && act);
     const size_t ldb = (size_t)d.ldb;
     const double *__restrict__ Bv = d.Binv;
-    // ---- trip 1: everything independent of the entering choice
+    // ---- trip 1: everything independent of the entering choice.  Every
+    // load is unconditional at a clamped index and selected afterwards, so
+    // the trip is one batch of loads (a load guarded by a test of another
+    // load's value waits for it: one memory round trip per guard)
     const int stop = st->stop;
-    PickIn pin = pick_load(d, NRHS == 2, gn, ncb);
-    pin.g = 0.0;                                    // gamma_p in every block, fixed order
-    if (NRHS == 2 && w == 0)
-        for (int b = lane; b < ncb; b += 64) pin.g += d.gpart[b];
+    PickIn pin;
+    pin.need2 = st->need2; pin.q1 = st->q1; pin.kq1 = st->kq1; pin.rigorous = st->rigorous;
+    pin.teta1 = st->teta1; pin.alfa1 = st->alfa1; pin.big = trow_big(st); pin.delta = st->delta;
+    const int np2 = 4 * gn;
+    Cand c2l[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) c2l[u] = cand_pass2(d)[min(lane + 64 * u, np2 - 1)];
+    double gp[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) gp[u] = (NRHS == 2) ? d.gpart[min(lane + 64 * u, ncb - 1)] : 0.0;
     const int nr = st->nr, ns = st->ns, p = max(st->p, 1), kp = max(st->kp, 1);
     const double delta = st->delta;
     const int binv_fresh = st->binv_fresh, rig = st->rigorous, phase = st->phase, refct = st->refct;
@@ -2078,39 +2215,86 @@ __global__ void __launch_bounds__(1024) k_dual_update(SpxDev d, int gn, int ncb,
     double rv[GM];
 #pragma unroll
     for (int u = 0; u < GM; ++u) {
-        const int t = gs + u * NSL;
-        c0[u] = (t <= nr_cap) ? d.rho_idx[t] : 0;
-        rv[u] = (t <= nr_cap) ? d.rho_val[t] : 0.0;
+        const int t = min(gs + u * NSL, m);
+        c0[u] = d.rho_idx[t];
+        rv[u] = d.rho_val[t];
     }
     // the block's rows
-    const int kold = rowlane ? d.head[r] : 1;
-    double bb = rowlane ? d.bbar[r] : 0.0;
-    double g = (NRHS == 2 && rowlane) ? d.gamma[r] : 0.0;
-    const int tkp = d.type[kp - 1];
-    const bool refkp = NRHS == 2 && d.refsp[kp - 1] != 0;
+    const int rc = min(r, m - 1);
+    const int kold_l = d.head[rc];
+    double bb = d.bbar[rc];
+    double g = (NRHS == 2) ? d.gamma[rc] : 0.0;
     // the block's columns (update_cbar, check_feas)
     const int JPB = (n + gridDim.x - 1) / gridDim.x;
     const int j = blockIdx.x * JPB + (int)threadIdx.x;
     const bool colth = (int)threadIdx.x < JPB && j < n;
-    double cb = colth ? d.cbar[j] : 0.0;
-    const double tri = colth ? d.trow[j] : 0.0;
-    const int hkj = colth ? d.head[m + j] : 1;
-    // list maintenance operands (block 0, one thread of the last wave)
-    const bool maint = (blockIdx.x == 0 && w == wa && lane == 0);
-    int nr0 = 0, nwl0 = 0, rlast = 0, wlast = 0;
-    if (maint) {
-        nr0 = nr;
-        nwl0 = st->nwl;
-        rlast = d.rlist[max(nr0 - 1, 0)];
-        if (NRHS == 2) wlast = d.wlist[max(nwl0 - 1, 0)];
+    const int jc = min(j, n - 1);
+    double cb = d.cbar[jc];
+    double tri = d.trow[jc];
+    int hkj = d.head[m + jc];
+    // ---- the selections of trip 1
+    pin.c = no_cand(0.0);
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+        if (lane + 64 * u < np2 && better<2>(c2l[u], pin.c)) pin.c = c2l[u];
+    for (int b = lane + 256; b < np2; b += 64) {
+        const Cand e = cand_pass2(d)[b];
+        if (better<2>(e, pin.c)) pin.c = e;
     }
-    if (stop) return;
+    pin.g = 0.0;                                    // gamma_p in every block, fixed order
+    if (NRHS == 2 && w == 0) {
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+            if (lane + 64 * u < ncb) pin.g += gp[u];
+        for (int b = lane + 256; b < ncb; b += 64) pin.g += d.gpart[b];
+    }
+#pragma unroll
+    for (int u = 0; u < GM; ++u)
+        if (gs + u * NSL > nr_cap) { c0[u] = 0; rv[u] = 0.0; }
+    const int kold = rowlane ? kold_l : 1;
+    if (!rowlane) { bb = 0.0; g = 0.0; }
+    if (!colth) { cb = 0.0; tri = 0.0; hkj = 1; }
     TPH(3, 0);
     const double gsum = (NRHS == 2 && w == 0) ? wsum(pin.g) : 0.0;
     // ---- the entering choice (every wave)
     const PickOut pk = pick_choose(pin);
     const int q = pk.q, kq = pk.kq;
-    const bool lead = blockIdx.x == 0 && threadIdx.x == 0;
+    const int qc = min(max(q, 1), n), kqc = min(max(kq, 1), m + n);
+    // ---- trip 2: inv(B) entries, the multipliers, the choice's operands
+    // (issued before the stop tests; addresses clamped)
+    const bool hdense = !SP && kqc > m;
+    const double *__restrict__ hcolv = d.A.A + (size_t)(hdense ? kqc - m - 1 : 0) * d.A.lda;
+    double bv[GM], xa[GM], xb[GM];
+#pragma unroll
+    for (int u = 0; u < GM; ++u) {
+        const int ca = min(max(c0[u], 0), m - 1);
+        bv[u] = Bv[(size_t)ca * ldb + rc];
+        xa[u] = SP ? 0.0 : hcolv[ca];
+        xb[u] = (NRHS == 2) ? d.work[ca] : 0.0;
+    }
+    const int kou = min(max(kold - 1, 0), m - 1);          // a basic slack's row (kold <= m)
+    const double ua_l = SP ? 0.0 : hcolv[kou];
+    const double ub_l = (NRHS == 2) ? d.work[kou] : 0.0;
+    const int tkp = d.type[kp - 1];
+    const bool refkp = NRHS == 2 && d.refsp[kp - 1] != 0;
+    const int knew = (r == p - 1) ? kqc : kold;
+    const int tkold_l = d.type[kold - 1];
+    const int refk_l = (NRHS == 2) ? d.refsp[kold - 1] : 0;
+    const int tknew_l = d.type[knew - 1];
+    const double lbn_l = d.lb[knew - 1], ubn_l = d.ub[knew - 1];
+    const int stq_l = d.stat[qc - 1];
+    const double lbq = d.lb[kqc - 1], ubq = d.ub[kqc - 1];
+    const int tkq = d.type[kqc - 1];
+    const double piv2 = d.trow[qc - 1];
+    const int kn = colth ? ((j == q - 1) ? kp : hkj) : 1;
+    const int ot_l = d.orig_type[kn - 1];
+    if (bk && w == wa) {
+        Books b;
+        books_load<NRHS>(d, b, nr, kqc);
+        if (lane == 0) sbk = b;
+    }
+    if (stop) return;
+    const bool lead = bk && threadIdx.x == 0;
     if (q == 0) {
         if (lead) { st->q = 0; st->stop = ST_Q0; }
         return;
@@ -2120,39 +2304,27 @@ __global__ void __launch_bounds__(1024) k_dual_update(SpxDev d, int gn, int ncb,
         return;
     }
     const double new_dq = (delta > 0.0 ? +1.0 : -1.0) * pk.teta;
-    // ---- trip 2: inv(B) entries, the multipliers, the choice's operands
-    const double *hcol = (!SP && kq > m) ? d.A.A + (size_t)(kq - m - 1) * d.A.lda : nullptr;
-    auto hval = [&](int c) { return hcol ? hcol[c] : (c == kq - 1 ? -1.0 : 0.0); };
-    double bv[GM];
+    // h = -N[q]: a structural's column of A, or -e at a slack's row
+    auto hsel = [&](int c, double v) { return hdense ? v : (c == kq - 1 ? -1.0 : 0.0); };
+    double a = 0.0, b = 0.0, al = 0.0;
 #pragma unroll
     for (int u = 0; u < GM; ++u) {
+        // alpha_p = rho' h over the slice's entries (the unit entry t = nr
+        // included); the FTRAN over t < nr only (unit columns per row)
         const int t = gs + u * NSL;
-        bv[u] = (act && t < ns) ? Bv[(size_t)c0[u] * ldb + r] : 0.0;
-    }
-    double a = 0.0, b = 0.0, al = 0.0;
-    {
-        double xa[GM], xb[GM];
-#pragma unroll
-        for (int u = 0; u < GM; ++u) {
-            const int t = gs + u * NSL;
-            xa[u] = (!SP && t < ns) ? hval(c0[u]) : 0.0;
-            xb[u] = (NRHS == 2 && t < nr) ? d.work[c0[u]] : 0.0;
+        const double h = (!SP && t < ns) ? hsel(c0[u], xa[u]) : 0.0;
+        const double bvu = (act && t < ns) ? bv[u] : 0.0;
+        bv[u] = bvu;
+        if (!SP) {
+            al += rv[u] * h;
+            if (t < nr) a += bvu * h;
         }
-#pragma unroll
-        for (int u = 0; u < GM; ++u) {
-            // alpha_p = rho' h over the slice's entries (the unit entry t = nr
-            // included); the FTRAN over t < nr only (unit columns per row)
-            if (!SP) {
-                al += rv[u] * xa[u];
-                if (gs + u * NSL < nr) a += bv[u] * xa[u];
-            }
-            if (NRHS == 2) b += bv[u] * xb[u];
-        }
+        if (NRHS == 2 && t < nr) b += bvu * xb[u];
     }
     double ua = 0.0, ub = 0.0;                      // unit columns of a basic slack at this row
     if (rowlane && kold <= m) {
-        if (!SP) ua = hval(kold - 1);
-        if (NRHS == 2) ub = d.work[kold - 1];
+        if (!SP) ua = hsel(kold - 1, ua_l);
+        if (NRHS == 2) ub = ub_l;
     }
     if (SP) {
         // sparse h = -N[q]: tcol = inv(B) h over the entries of column q, the
@@ -2183,21 +2355,14 @@ __global__ void __launch_bounds__(1024) k_dual_update(SpxDev d, int gn, int ncb,
         if (lane == 0) salpha = s;
     }
     // operands of the row updates that depend on the choice
-    const int knew = (r == p - 1) ? kq : kold;
-    const int tkold = rowlane ? d.type[kold - 1] : 0;
-    const bool refk = (NRHS == 2 && rowlane) ? d.refsp[kold - 1] != 0 : false;
-    const int tknew = rowlane ? d.type[knew - 1] : 0;
-    const double lbn = rowlane ? d.lb[knew - 1] : 0.0, ubn = rowlane ? d.ub[knew - 1] : 0.0;
-    const double xq = (rowlane && r == p - 1) ? get_xN(d.stat, d.lb, d.ub, kq, q) : 0.0;
-    const int tkq = d.type[kq - 1];
-    const double piv2 = d.trow[q - 1];
-    const int kn = colth ? ((j == q - 1) ? kp : hkj) : 1;
-    const int ot = colth ? d.orig_type[kn - 1] : 0;
-    int rq = -1, wq = -1;
-    if (maint) {
-        if (kq <= m) rq = d.rpos[kq - 1];
-        if (NRHS == 2 && kq > m) wq = d.wpos[kq - m - 1];
-    }
+    const int tkold = rowlane ? tkold_l : 0;
+    const bool refk = (NRHS == 2 && rowlane) ? refk_l != 0 : false;
+    const int tknew = rowlane ? tknew_l : 0;
+    const double lbn = rowlane ? lbn_l : 0.0, ubn = rowlane ? ubn_l : 0.0;
+    // get_xN (glpspx01.js:442) of the entering variable
+    const double xq_v = (stq_l == NU) ? ubq : (stq_l == NF ? 0.0 : lbq);
+    const double xq = (rowlane && r == p - 1) ? xq_v : 0.0;
+    const int ot = colth ? ot_l : 0;
     sp[0][w][lane] = a;
     if (NRHS == 2) sp[NRHS - 1][w][lane] = b;
     TPH(3, 2);
@@ -2247,6 +2412,7 @@ __global__ void __launch_bounds__(1024) k_dual_update(SpxDev d, int gn, int ncb,
             d.Binv[(size_t)c * ldb + r] = v;
         }
     }
+    TPH(3, 4);
     // ---- rows: update_bbar / update_gamma, the next chuzr candidates
     if (w == 0) {
         Cand cnd = no_cand(0.0);
@@ -2292,6 +2458,7 @@ __global__ void __launch_bounds__(1024) k_dual_update(SpxDev d, int gn, int ncb,
         const Cand best = wave_best<0>(cnd);
         if (lane == 0) cand_chuzr(d)[blockIdx.x] = best;
     }
+    TPH(3, 5);
     // ---- columns: update_cbar (:1020), check_feas of phase I (:1296)
     int badj = 0;
     if (colth) {
@@ -2304,6 +2471,7 @@ __global__ void __launch_bounds__(1024) k_dual_update(SpxDev d, int gn, int ncb,
         d.cbar[j] = cb;
         badj = phase == 1 && ((cb < -tol_dj && (ot == LO || ot == FR)) || (cb > +tol_dj && (ot == UP || ot == FR)));
     }
+    TPH(3, 6);
     if (phase == 1 && __syncthreads_or(badj) && threadIdx.x == 0) atomicOr(&st->dinf, 1);
     if (lead) {
         st->q = q;
@@ -2315,57 +2483,10 @@ __global__ void __launch_bounds__(1024) k_dual_update(SpxDev d, int gn, int ncb,
         st->fxp = (tkp == FX);
         st->rclr = (tkp == FX && refkp);
     }
-    if (maint) {
-        // dense columns of inv(B): an entering slack's column is now e_p,
-        // a leaving slack's column became dense
-        int nrn = nr0;
-        if (kq <= m) {
-            d.rlist[rq] = rlast;
-            d.rpos[rlast] = rq;
-            d.rpos[kq - 1] = -1;
-            nrn--;
-        }
-        if (kp <= m) {
-            d.rlist[nrn] = kp - 1;
-            d.rpos[kp - 1] = nrn;
-            nrn++;
-        }
-        st->nr = nrn;
-        if (NRHS == 2) {
-            int nwl = nwl0;
-            if (wq >= 0) {
-                d.wlist[wq] = wlast;
-                d.wpos[wlast] = wq;
-                d.wpos[kq - m - 1] = -1;
-                nwl--;
-            }
-            if (kp > m && refkp && tkp != FX) {
-                d.wlist[nwl] = kp - m - 1;
-                d.wpos[kp - m - 1] = nwl;
-                nwl++;
-            }
-            st->nwl = nwl;
-        }
-        // algorithmic HBM bytes of this pivot: the pivot row,
-        // A w, and inv(B) read once and written once over the support of rho
-        const double rowb = rowpath == 1 ? 8.0 * (double)ns * n
-                            : rowpath == 2 ? 12.0 * (double)d.A.nnz : 8.0 * (double)m * n;
-        const unsigned long long tk0 = st->tk_start, tk1 = st->tk_end, tk2 = st->tk_next, tkp = st->tk_prev;
-        if (rowpath && tk1 > tk0) {
-            st->bytes_trow += rowb;
-            st->trow_ticks += (double)(tk1 - tk0);
-            st->trow_ticks_b += (double)(tk2 - tk0);
-            st->trow_n += 1.0;
-            // from the last exit of the kernel before it (the previous
-            // pivot's commit / update; not the first pivot of a batch)
-            if (tkp < tk0 && tk0 - tkp < 20000ull) {
-                st->trow_ticks_r += (double)(tk1 - tkp);
-                st->trow_nr += 1.0;
-            }
-        }
-        st->tk_end = 0;
-        st->bytes += rowb + 8.0 * (double)m * nwl0 + 16.0 * (double)m * ns + bytes_fixed;
+    if (bk && w == wa && lane == 0) {
+        books_store<NRHS>(d, sbk, kp, kq, tkp, refkp, nr, ns, rowpath, bytes_fixed);
     }
+    TPH(3, 7);
 }
 
 // ---------------------------------------------------------------------------
@@ -2392,7 +2513,7 @@ DualPlan dual_plan(const SpxDev &d, int nr_max, int nwl_max, int pse, int rigoro
     const int tiles_t = cdiv(n, 512), tiles_f = cdiv(m, 512);
     pl.tsplits = std::max(1, std::min(2048 / tiles_t, cdiv(ns_max, 8)));
     pl.tsplits = std::max(1, std::min<int>(pl.tsplits, (int)(d.partial_cap / std::max(n, 1))));
-    pl.twaves = ns_max <= 32 ? 4 : (ns_max <= 128 ? 8 : 16);
+    pl.twaves = ns_max <= 32 ? 4 : (ns_max <= 64 ? 8 : 16);    // 8 list entries per wave in trip 2
     const int nrhs = pse ? 2 : 1;
     pl.fsplits = std::max(1, std::min(2048 / tiles_f, cdiv(std::max(nr_max, 1), 8)));
     pl.fsplits = std::max(1, std::min<int>(pl.fsplits, (int)(d.partial_cap / ((size_t)nrhs * m))));

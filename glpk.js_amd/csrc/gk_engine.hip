@@ -18,6 +18,7 @@
 #include <cstdio>
 #include <cstring>
 #include <string>
+#include <type_traits>
 #include <vector>
 
 using namespace gk;
@@ -64,21 +65,31 @@ template <typename T>
 struct DBuf {
     T *p = nullptr;
     size_t n = 0;
+    bool own = true;                      // false: a view into an arena (Engine::arena)
     void ensure(size_t cnt)
     {
         if (cnt <= n && p) return;
-        if (p) (void)hipFree(p);
+        if (p && own) (void)hipFree(p);
         p = nullptr;
         n = 0;
+        own = true;
         size_t bytes = std::max<size_t>(cnt, 1) * sizeof(T);
         HIPCHK(hipMalloc((void **)&p, bytes));
         n = std::max<size_t>(cnt, 1);
     }
+    void view(T *q, size_t cnt)
+    {
+        if (p && own) (void)hipFree(p);
+        p = q;
+        n = cnt;
+        own = false;
+    }
     void release()
     {
-        if (p) (void)hipFree(p);
+        if (p && own) (void)hipFree(p);
         p = nullptr;
         n = 0;
+        own = true;
     }
 };
 
@@ -130,6 +141,14 @@ struct Engine {
     int prof = 0;                             // gk_bfd_profile: events around the pivot-row kernel (2: + block trace)
     std::vector<hipEvent_t> ev;               // 2 per pivot of the longest batch
     DBuf<unsigned long long> trace;           // prof == 2: per-kernel, per-block clock stamps of the last pivot
+    // one allocation for the whole O(m + n) working set (the vectors, lists,
+    // candidates and the state): a pivot kernel touches tens of these arrays,
+    // and one allocation keeps them on a few large pages — as separate
+    // allocations each first touch from a CU was a translation miss (the
+    // bookkeeping wave of k_dual_update spent 2 us on ten stores)
+    char *arena = nullptr;
+    size_t arena_cap = 0;
+    int arena_m = -1, arena_n = -1;
     MatDev mat() const
     {
         MatDev M{};
@@ -152,6 +171,7 @@ struct Engine {
         bbar.release(); cbar.release(); gamma.release(); tcol.release(); trow.release(); rho.release(); rowp.release();
         u.release(); s.release(); h.release(); wcol.release(); ys.release(); work.release(); r1.release(); r2.release();
         partial.release(); st.release();
+        if (arena) (void)hipFree(arena);
         if (st_host) (void)hipHostFree(st_host);
         if (pin) (void)hipHostFree(pin);
         for (auto &g : graphs)
@@ -299,14 +319,62 @@ static bool split_from_head(int m, const int *head1, BasisSplit &bs)
 static void engine_alloc(Engine &E, int m, int n)
 {
     const size_t mn = (size_t)m + n;
-    E.type.ensure(mn); E.orig_type.ensure(mn); E.refsp.ensure(mn); E.stat.ensure(n);
-    E.lb.ensure(mn); E.ub.ensure(mn); E.coef.ensure(mn); E.orig_lb.ensure(mn); E.orig_ub.ensure(mn);
-    E.obj.ensure(n); E.head.ensure(mn); E.bind.ensure(mn);
-    E.bbar.ensure(m); E.cbar.ensure(n); E.gamma.ensure(std::max(m, n));
-    E.tcol.ensure(m); E.trow.ensure(n); E.rho.ensure(m); E.rowp.ensure(m); E.u.ensure(m); E.s.ensure(n);
-    E.h.ensure(m); E.wcol.ensure(n); E.ys.ensure(m); E.work.ensure(std::max(m, n)); E.r1.ensure(m); E.r2.ensure(m);
+    const size_t gv = (size_t)(std::max(m, n) + 255) / 256 + 1;
+    if (E.arena_m != m || E.arena_n != n) {
+        // the working set as views into one arena (256-byte aligned slices)
+        size_t off = 0;
+        char *base = nullptr;
+        auto place = [&](auto &b, size_t cnt) {
+            using T = typename std::remove_pointer<decltype(b.p)>::type;
+            cnt = std::max<size_t>(cnt, 1);
+            if (base) b.view((T *)(base + off), cnt);
+            off += (cnt * sizeof(T) + 255) & ~(size_t)255;
+        };
+        auto layout = [&]() {
+            off = 0;
+            place(E.st, 1);
+            place(E.type, mn); place(E.orig_type, mn); place(E.refsp, mn); place(E.stat, n);
+            place(E.lb, mn); place(E.ub, mn); place(E.coef, mn); place(E.orig_lb, mn); place(E.orig_ub, mn);
+            place(E.obj, n); place(E.head, mn); place(E.bind, mn);
+            place(E.bbar, m); place(E.cbar, n); place(E.gamma, std::max(m, n));
+            place(E.tcol, m); place(E.trow, n); place(E.rho, m); place(E.rowp, m); place(E.u, m); place(E.s, n);
+            place(E.h, m); place(E.wcol, n); place(E.ys, m); place(E.work, std::max(m, n)); place(E.r1, m);
+            place(E.r2, m);
+            // + a spare slot each (branch-free list updates, books_store)
+            place(E.rlist, (size_t)m + 1); place(E.rpos, (size_t)m + 1);
+            place(E.rho_idx, (size_t)m + 1); place(E.rho_val, (size_t)m + 1);
+            // dual: gamma_p sums, then per-block max |trow| (64-slot blocks), 4
+            // gv each; primal: max |tcol|, d_q sums, gamma_q sums of the row
+            // groups, 16 gv each
+            place(E.gpart, 56 * gv);
+            // candidates (24-byte entries): chuzr | pass 1 | pass 2, 4 gv each,
+            // then the primal pass-1 candidates of the row groups, 16 gv
+            place(E.cand, 3 * 28 * gv);
+            // dual: reference-space non-basic structurals (n); primal: basic
+            // slacks in the reference space (m)
+            place(E.wlist, (size_t)std::max(m, n) + 1); place(E.wpos, (size_t)std::max(m, n) + 1);
+            place(E.awcnt, (size_t)(m + 511) / 512 + 1);
+            place(E.tslots, std::max((size_t)((n + 511) / 512) * 2048, 4 * gv) + 1);
+            place(E.xslots, (size_t)(m + 15) / 16 + gv + (size_t)((m + 511) / 512) * 2048 + 1);
+        };
+        layout();
+        if (E.arena_cap < off) {
+            if (E.arena) (void)hipFree(E.arena);
+            E.arena = nullptr;
+            E.arena_cap = 0;
+            HIPCHK(hipMalloc((void **)&E.arena, off));
+            E.arena_cap = off;
+        }
+        base = E.arena;
+        layout();
+        // arrival counters (reset by their users) and exit stamps start at 0
+        HIPCHK(hipMemset(E.awcnt.p, 0, E.awcnt.n * sizeof(int)));
+        HIPCHK(hipMemset(E.xslots.p, 0, E.xslots.n * sizeof(unsigned long long)));
+        E.arena_m = m;
+        E.arena_n = n;
+    }
     E.partial.ensure(PARTIAL_CAP);
-    E.st.ensure(1);
+    E.awpart.ensure((size_t)AW_SPLITS * m);
     if (!E.st_host) HIPCHK(hipHostMalloc((void **)&E.st_host, sizeof(DState), hipHostMallocDefault));
     {
         const size_t need = std::max<size_t>((size_t)8 << 20, (size_t)32 * ((size_t)m + n + 1) * sizeof(double));
@@ -316,32 +384,6 @@ static void engine_alloc(Engine &E, int m, int n)
             E.pin_cap = 0;
             HIPCHK(hipHostMalloc((void **)&E.pin, need, hipHostMallocDefault));
             E.pin_cap = need;
-        }
-    }
-    E.rlist.ensure(m); E.rpos.ensure(m); E.rho_idx.ensure((size_t)m + 1); E.rho_val.ensure((size_t)m + 1);
-    const size_t gv = (size_t)(std::max(m, n) + 255) / 256 + 1;
-    // dual: gamma_p sums, then per-block max |trow| (64-slot blocks), 4 gv
-    // each; primal: max |tcol|, d_q sums, gamma_q sums of the row groups, 16 gv each
-    E.gpart.ensure(56 * (size_t)gv);
-    // candidates (24-byte entries): chuzr | pass 1 | pass 2, 4 gv each, then
-    // the primal pass-1 candidates of the row groups, 16 gv
-    E.cand.ensure(3 * 28 * (size_t)gv);
-    // dual: reference-space non-basic structurals (n); primal: basic slacks in the reference space (m)
-    E.wlist.ensure(std::max(m, n)); E.wpos.ensure(std::max(m, n));
-    E.awpart.ensure((size_t)AW_SPLITS * m);
-    {
-        const size_t tiles = (size_t)(m + 511) / 512 + 1;
-        if (E.awcnt.n < tiles || !E.awcnt.p) {
-            E.awcnt.ensure(tiles);
-            HIPCHK(hipMemset(E.awcnt.p, 0, E.awcnt.n * sizeof(int)));   // arrival counters, reset by their users
-        }
-    }
-    E.tslots.ensure(std::max((size_t)((n + 511) / 512) * 2048, 4 * (size_t)gv) + 1);
-    {
-        const size_t nx = (size_t)(m + 15) / 16 + gv + (size_t)((m + 511) / 512) * 2048 + 1;
-        if (E.xslots.n < nx || !E.xslots.p) {
-            E.xslots.ensure(nx);
-            HIPCHK(hipMemset(E.xslots.p, 0, E.xslots.n * sizeof(unsigned long long)));
         }
     }
 }

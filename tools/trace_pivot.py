@@ -31,6 +31,8 @@ def main():
     khz = 100000.0
     acc = {}
     ph = {}
+    slow = {}
+    ph0 = {}
     reps = 20
     for _ in range(reps):
         gk.glp_simplex(P, gk.SMCP(meth=gk.GLP_DUAL, it_lim=60, msg_lev=gk.GLP_MSG_ERR))
@@ -56,6 +58,10 @@ def main():
             if rel.any():
                 cnt = np.maximum((rel > 0).sum(axis=0), 1)
                 ph.setdefault(name, []).append(rel.sum(axis=0) / cnt)
+                ph0.setdefault(name, []).append(rel[0])
+            sl = slow.setdefault(name, np.zeros((2, len(e))))
+            sl[0, sel] += (x[sel] - t0) / reps
+            sl[1, sel] += (e[sel] - t0) / reps
             a = acc.setdefault(name, [])
             a.append(((ev.min() - t_ref), ev.max() - ev.min(), xv.max() - ev.min(), np.mean(xv - ev),
                       np.max(xv - ev), valid.sum()))
@@ -64,8 +70,14 @@ def main():
         if name in ph and ph[name]:
             a = np.array(ph[name], dtype=float).mean(axis=0)
             print(f"  {name:14s} " + " ".join(f"{v/100:6.2f}" for v in a if v > 0))
+            a0 = np.array(ph0[name], dtype=float).mean(axis=0)
+            print(f"  {name + ' b0':14s} " + " ".join(f"{v/100:6.2f}" for v in a0))
     print(f"C3 {m}x{n}, last pivot of {reps} calls of 60 pivots after {warm} (times in us; device clock 100 MHz)")
     print(f"{'kernel':14s} {'start':>8s} {'ramp':>7s} {'span':>7s} {'blk avg':>8s} {'blk max':>8s} {'blocks':>7s}")
+    print("latest-finishing blocks (exit and entry after block 0's entry, us, mean over calls):")
+    for name, sl in slow.items():
+        o = np.argsort(-sl[0])[:6]
+        print(f"  {name:14s} " + " ".join(f"b{b}:{sl[0, b]/100:.2f}(in {sl[1, b]/100:.2f})" for b in o))
     for name, a in acc.items():
         a = np.array(a, dtype=float)
         mu = a.mean(axis=0)
