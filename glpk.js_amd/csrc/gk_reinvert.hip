@@ -21,6 +21,7 @@
 // of one launch per column.
 #include "gk_device.h"
 #include <cstdlib>
+#include <cstdio>
 
 namespace gk {
 
@@ -146,7 +147,7 @@ __global__ void __launch_bounds__(NT) k_gjb_panel(const double *__restrict__ M, 
 // B[kk = l >> 4][j = l & 15], D[(l >> 4) + 4 r][l & 15].
 typedef double gj_double4 __attribute__((ext_vector_type(4)));
 
-template <int B, int SUBE>
+template <int B, int SUBE, int QCM = 0>
 __global__ void __launch_bounds__(256) k_gjb_update(const double *__restrict__ M, double *__restrict__ M2,
                                                     const double *__restrict__ Qm, int ldq,
                                                     const int *__restrict__ rsl, int k, int t0,
@@ -176,7 +177,8 @@ __global__ void __launch_bounds__(256) k_gjb_update(const double *__restrict__ M
 #pragma unroll
         for (int a = 0; a < 2; ++a) {
             const int gr = row0 + a * 16 + li;
-            double q = (gr < k && gk < b) ? Qm[(size_t)gr * ldq + gk] : 0.0;
+            // Q row-major (ldq >= B) or, QCM, column-major (ldq = k)
+            double q = (gr < k && gk < b) ? (QCM ? Qm[(size_t)gk * ldq + gr] : Qm[(size_t)gr * ldq + gk]) : 0.0;
             if (SUBE && gr == rk) q -= 1.0;          // Q - E_R
             av[a] = q;
         }
@@ -276,6 +278,244 @@ static double *gjb_run2(hipStream_t s, double *M, double *M2, double *P, double 
     return M;
 }
 
+// ---------------------------------------------------------------------------
+// two-level scheme with a column-major outer panel (k > 256): P[c * k + r],
+// so every panel load / store and the inner updates are coalesced over rows
+// (the row-major panel read 64 scattered lines per wave instruction: one
+// workgroup spent 67 us per 8-column panel at k = 4096, 34 ms per
+// re-inversion).  Q = the transformed inner panel minus E_R, column-major
+// (Q[c * k + r]); X_R = the pivot rows of P's bo columns (B x bo).
+// ---------------------------------------------------------------------------
+template <int NT, int RPT, int B>
+__global__ void __launch_bounds__(NT) k_gjc_panel(double *__restrict__ P, int k, int c0, int bo,
+                                                  double *__restrict__ Qm, int tg0, int *__restrict__ piv_step,
+                                                  int *__restrict__ piv, int *__restrict__ flag, double tiny,
+                                                  double *__restrict__ xr)
+{
+    constexpr int NW = NT / 64;
+    // per step and wave: the wave's best candidate and its row's B values,
+    // double-buffered by step parity (one barrier per step)
+    __shared__ Cand shc[2][NW];
+    __shared__ double shr[2][NW][B];
+    __shared__ int rsl[B];
+    if (*flag) return;
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int b = min(B, bo - c0);
+    double x[RPT][B];
+    bool live[RPT];                      // row owned, and not pivoted yet
+#pragma unroll
+    for (int j = 0; j < RPT; ++j) {
+        const int r = tid + j * NT;
+        const int rc = min(r, k - 1);
+        live[j] = r < k && piv_step[rc] == GJ_NONE;
+#pragma unroll
+        for (int c = 0; c < B; ++c) x[j][c] = (r < k && c < b) ? P[(size_t)(c0 + c) * k + rc] : 0.0;
+    }
+    // B steps, the active column always in slot 0: after a step the columns
+    // rotate left by one (the transformed pivot column goes to slot B - 1),
+    // so after B steps every column is back in its slot (static register
+    // indices, the step body a loop).  A step: every wave reduces its rows'
+    // candidates and publishes the best one with that row's B values; after
+    // the barrier every wave picks the winner among the NW published ones
+    // (largest |x|, lowest row on ties) and forms fr = x[rs] / pv itself.
+#pragma unroll 1
+    for (int i = 0; i < B; ++i) {
+        const int par = i & 1;
+        if (i >= b) {
+            // inactive step (narrow last panel): rotate only
+#pragma unroll
+            for (int j = 0; j < RPT; ++j) {
+                const double t0 = x[j][0];
+#pragma unroll
+                for (int cc = 1; cc < B; ++cc) x[j][cc - 1] = x[j][cc];
+                x[j][B - 1] = t0;
+            }
+            continue;
+        }
+        Cand c; c.k1 = 0.0; c.k2 = 0.0; c.idx = 0; c.aux = 0;
+        int jb = 0;
+#pragma unroll
+        for (int j = 0; j < RPT; ++j) {
+            const double v = fabs(x[j][0]);
+            if (live[j] && v > 0.0 && (c.idx == 0 || v > c.k1)) {   // rows ascend with j
+                c.k1 = v;
+                c.idx = tid + j * NT + 1;
+                jb = j;
+            }
+        }
+        const Cand wb = wave_best<0>(c);
+        // the winning lane's row values (lane = (idx - 1) % 64 within this wave)
+        const int src = wb.idx ? ((wb.idx - 1) & 63) : 0;
+        double rowv[B];
+#pragma unroll
+        for (int cc = 0; cc < B; ++cc) {
+            double mine = 0.0;
+#pragma unroll
+            for (int j = 0; j < RPT; ++j)
+                if (j == jb) mine = x[j][cc];
+            rowv[cc] = __shfl(mine, src);
+        }
+        if (lane == 0) {
+            shc[par][w] = wb;
+#pragma unroll
+            for (int cc = 0; cc < B; ++cc) shr[par][w][cc] = rowv[cc];
+        }
+        __syncthreads();
+        Cand e;
+        if (lane < NW) e = shc[par][lane];
+        else { e.k1 = 0.0; e.k2 = 0.0; e.idx = 0; e.aux = 0; }
+        const Cand best = wave_best<0>(e);
+        if (best.idx == 0 || best.k1 <= tiny) {
+            if (tid == 0) *flag = 1 + tg0 + i;
+            return;                      // uniform: every thread saw the same best
+        }
+        const int rs = best.idx - 1;
+        const int ws = (rs % NT) >> 6;   // the wave that published it
+        if (tid == 0) rsl[i] = rs;
+        const double ipv = 1.0 / shr[par][ws][0];
+        // the update, rotating left in place: slot 0 (the step's column)
+        // goes to slot B - 1; the pivot row is overwritten afterwards by its
+        // owner (no per-element select)
+        double fr[B];
+        fr[0] = ipv;
+#pragma unroll
+        for (int cc = 1; cc < B; ++cc) fr[cc] = shr[par][ws][cc] * ipv;
+#pragma unroll
+        for (int j = 0; j < RPT; ++j) {
+            const double colt = x[j][0];
+#pragma unroll
+            for (int cc = 1; cc < B; ++cc) x[j][cc - 1] = x[j][cc] - colt * fr[cc];
+            x[j][B - 1] = -colt * fr[0];
+        }
+        if ((rs % NT) == tid) {
+            const int jo = rs / NT;
+#pragma unroll
+            for (int j = 0; j < RPT; ++j)
+                if (j == jo) {
+#pragma unroll
+                    for (int cc = 1; cc < B; ++cc) x[j][cc - 1] = fr[cc];
+                    x[j][B - 1] = fr[0];
+                    live[j] = false;
+                }
+        }
+    }
+    __syncthreads();                     // rsl complete
+    if (tid < b) {
+        piv[tg0 + tid] = rsl[tid];
+        piv_step[rsl[tid]] = tg0 + tid;
+    }
+    // X_R of the columns outside this panel (unchanged by it; a panel column
+    // read here races with the write-back below and is never used)
+    for (int e = tid; e < B * bo; e += NT) {
+        const int kk = e / bo, c = e - kk * bo;
+        xr[e] = (kk < b) ? P[(size_t)c * k + rsl[kk]] : 0.0;
+    }
+    // the panel back into P, Q - E_R for the updates
+#pragma unroll
+    for (int j = 0; j < RPT; ++j) {
+        const int r = tid + j * NT;
+        if (r >= k) continue;
+#pragma unroll
+        for (int c = 0; c < B; ++c) {
+            if (c < b) P[(size_t)(c0 + c) * k + r] = x[j][c];
+            Qm[(size_t)c * k + r] = (c < b) ? x[j][c] - (r == rsl[c] ? 1.0 : 0.0) : 0.0;
+        }
+    }
+}
+
+// P[j, r] += sum_kk Q[kk, r] X_R[kk, j] for the columns j < bo outside the
+// inner panel [i0, i0 + B); one row per thread
+template <int B>
+__global__ void __launch_bounds__(256) k_gjc_inner(double *__restrict__ P, int bo, int i0,
+                                                   const double *__restrict__ Qm, const double *__restrict__ xr, int k,
+                                                   const int *__restrict__ flag)
+{
+    __shared__ double sx[B * GJ_BO];
+    if (*flag) return;
+    for (int e = threadIdx.x; e < B * bo; e += 256) sx[e] = xr[e];
+    const int r = blockIdx.x * 256 + threadIdx.x;
+    const int rc = min(r, k - 1);
+    double q[B];
+#pragma unroll
+    for (int kk = 0; kk < B; ++kk) q[kk] = Qm[(size_t)kk * k + rc];
+    __syncthreads();
+    // 8 columns per thread (blockIdx.y), their loads issued together: one
+    // memory round trip per thread
+    {
+        const int j0 = blockIdx.y * 8;
+        double a[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) a[u] = (j0 + u < bo) ? P[(size_t)(j0 + u) * k + rc] : 0.0;
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            const int j = j0 + u;
+            double acc = a[u];
+#pragma unroll
+            for (int kk = 0; kk < B; ++kk) acc += q[kk] * sx[kk * bo + min(j, bo - 1)];
+            if (r < k && j < bo && !(j >= i0 && j < i0 + B)) P[(size_t)j * k + r] = acc;
+        }
+    }
+}
+
+// the outer panel between M (row-major k x k, columns [T0, T0 + bo)) and P
+// (column-major k x bo): 64 x 64 tiles transposed through LDS
+template <int IN>
+__global__ void __launch_bounds__(256) k_gjc_copy(const double *__restrict__ src, double *__restrict__ dst, int k,
+                                                  int T0, int bo, const int *__restrict__ flag)
+{
+    __shared__ double t[64][65];
+    if (*flag) return;
+    const int r0 = blockIdx.x * 64;
+    const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+    if (IN) {
+        // read rows of M (coalesced over columns), write columns of P
+        for (int y = ty; y < 64; y += 4) {
+            const int r = r0 + y;
+            t[y][tx] = (r < k && tx < bo) ? src[(size_t)r * k + T0 + tx] : 0.0;
+        }
+        __syncthreads();
+        for (int c = ty; c < bo; c += 4) {
+            const int r = r0 + tx;
+            if (r < k) dst[(size_t)c * k + r] = t[tx][c];
+        }
+    } else {
+        // read columns of P (coalesced over rows), write rows of M
+        for (int c = ty; c < 64; c += 4) {
+            const int r = r0 + tx;
+            t[tx][c] = (r < k && c < bo) ? src[(size_t)c * k + r] : 0.0;
+        }
+        __syncthreads();
+        for (int y = ty; y < 64; y += 4) {
+            const int r = r0 + y;
+            if (r < k && tx < bo) dst[(size_t)r * k + T0 + tx] = t[y][tx];
+        }
+    }
+}
+
+template <int NT, int RPT, int B>
+static double *gjc_run(hipStream_t s, double *M, double *M2, double *P, double *Qm, double *xr, int k,
+                       int *piv_step, int *piv, int *flag, double tiny)
+{
+    const dim3 g((k + 63) / 64, (k + 63) / 64);
+    const dim3 gt((k + 63) / 64), gr((k + 255) / 256);
+    for (int T0 = 0; T0 < k; T0 += GJ_BO) {
+        const int bo = std::min(GJ_BO, k - T0);
+        hipLaunchKernelGGL(k_gjc_copy<1>, gt, dim3(256), 0, s, M, P, k, T0, bo, flag);
+        for (int i0 = 0; i0 < bo; i0 += B) {
+            hipLaunchKernelGGL((k_gjc_panel<NT, RPT, B>), dim3(1), dim3(NT), 0, s, P, k, i0, bo, Qm, T0 + i0,
+                               piv_step, piv, flag, tiny, xr);
+            if (bo > B)
+                hipLaunchKernelGGL((k_gjc_inner<B>), dim3(gr.x, (bo + 7) / 8), dim3(256), 0, s, P, bo, i0, Qm, xr, k,
+                                   flag);
+        }
+        if (k > bo)
+            hipLaunchKernelGGL((k_gjb_update<GJ_BO, 1, 1>), g, dim3(256), 0, s, M, M2, P, k, piv + T0, k, T0, flag);
+        hipLaunchKernelGGL(k_gjc_copy<0>, gt, dim3(256), 0, s, P, M2, k, T0, bo, flag);
+        std::swap(M, M2);
+    }
+    return M;
+}
+
 __global__ void k_gjb_init(int *piv_step, int k, int *flag)
 {
     for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < k; i += gridDim.x * blockDim.x) piv_step[i] = GJ_NONE;
@@ -302,12 +542,22 @@ double *gauss_jordan_blocked(hipStream_t s, double *X, double *scratch, int k, i
     double *M2 = X + (size_t)k * k, *Qm = scratch, *P = scratch + (size_t)32 * k, *xr = P + (size_t)GJ_BO * k;
     // registers: RPT * B doubles of the panel per thread (1 / 2 / 4 waves per
     // SIMD); beyond 1024 the two-level scheme streams M once per 64 columns
+    static const int rowmajor = [] {
+        const char *e = std::getenv("GK_GJ_ROWMAJOR");   // the row-major two-level panels (experiments)
+        return e ? std::atoi(e) : 0;
+    }();
     if (k <= 256) return gjb_run<256, 1, 16>(s, X, M2, Qm, k, piv_step, piv, flag, tiny);
-    if (k <= 512) return gjb_run<256, 2, 16>(s, X, M2, Qm, k, piv_step, piv, flag, tiny);
-    if (k <= 1024) return gjb_run<512, 2, 16>(s, X, M2, Qm, k, piv_step, piv, flag, tiny);
-    if (k <= 2048) return gjb_run2<1024, 2, 16>(s, X, M2, P, Qm, xr, k, piv_step, piv, flag, tiny);
-    if (k <= 4096) return gjb_run2<1024, 4, 8>(s, X, M2, P, Qm, xr, k, piv_step, piv, flag, tiny);
-    return gjb_run2<1024, 8, 4>(s, X, M2, P, Qm, xr, k, piv_step, piv, flag, tiny);
+    if (rowmajor) {
+        if (k <= 512) return gjb_run<256, 2, 16>(s, X, M2, Qm, k, piv_step, piv, flag, tiny);
+        if (k <= 1024) return gjb_run<512, 2, 16>(s, X, M2, Qm, k, piv_step, piv, flag, tiny);
+        if (k <= 2048) return gjb_run2<1024, 2, 16>(s, X, M2, P, Qm, xr, k, piv_step, piv, flag, tiny);
+        if (k <= 4096) return gjb_run2<1024, 4, 8>(s, X, M2, P, Qm, xr, k, piv_step, piv, flag, tiny);
+        return gjb_run2<1024, 8, 4>(s, X, M2, P, Qm, xr, k, piv_step, piv, flag, tiny);
+    }
+    if (k <= 1024) return gjc_run<1024, 1, 16>(s, X, M2, P, Qm, xr, k, piv_step, piv, flag, tiny);
+    if (k <= 2048) return gjc_run<1024, 2, 16>(s, X, M2, P, Qm, xr, k, piv_step, piv, flag, tiny);
+    if (k <= 4096) return gjc_run<1024, 4, 8>(s, X, M2, P, Qm, xr, k, piv_step, piv, flag, tiny);
+    return gjc_run<1024, 8, 4>(s, X, M2, P, Qm, xr, k, piv_step, piv, flag, tiny);
 }
 
 // CinvR (row-major inv(C)): with M = C' inverted in place,
