@@ -105,7 +105,7 @@ EXPORTS = ["gk_abi_version", "gk_device_count", "gk_ctx_create", "gk_ctx_destroy
            "gk_bfd_create", "gk_bfd_destroy", "gk_bfd_set_parm", "gk_bfd_factorize", "gk_bfd_factorize_csc",
            "gk_bfd_ftran", "gk_bfd_btran", "gk_bfd_update", "gk_bfd_get_count", "gk_bfd_valid",
            "gk_spx_primal", "gk_spx_dual", "gk_bfd_last_stats", "gk_bfd_profile", "gk_ios_driver",
-           "gk_scale_prob", "gk_scale_prob_timed"]
+           "gk_scale_prob", "gk_scale_prob_timed", "gk_adv_basis"]
 
 
 def load_library(path: str = LIB_PATH):
@@ -159,6 +159,8 @@ def load_library(path: str = LIB_PATH):
     L.gk_scale_prob.restype = C.c_int
     L.gk_scale_prob_timed.argtypes = [P, C.c_int, C.c_int, P, P, P, C.c_int, P, P, P, P, P]
     L.gk_scale_prob_timed.restype = C.c_int
+    L.gk_adv_basis.argtypes = [P]
+    L.gk_adv_basis.restype = C.c_int
     _lib = L
     return L
 
@@ -761,3 +763,47 @@ def glp_scale_prob(P: GkProblem, flags: int) -> dict:
     P.p.sjj = new_s.copy()
     P.touch_matrix()                              # the device copy of A is scaled: re-upload
     return stages
+
+
+# ---------------------------------------------------------------------------
+# glp_adv_basis (glpini01.js:1): the triangular starting basis (gk_adv_basis,
+# host code in the library; no device needed)
+# ---------------------------------------------------------------------------
+def adv_basis_statuses(p, L=None):
+    """gk_adv_basis on a problems.Problem: (size of the triangular part,
+    row_stat[m], col_stat[n]) as the reference's adv_basis sets them."""
+    L = L or load_library()
+    m, n = p.m, p.n
+    keep = dict(row_type=_pad(p.row_type, np.int8), row_lb=_pad(p.row_lb, np.float64),
+                row_ub=_pad(p.row_ub, np.float64), col_type=_pad(p.col_type, np.int8),
+                col_lb=_pad(p.col_lb, np.float64), col_ub=_pad(p.col_ub, np.float64),
+                A_ptr=_pad(np.asarray(p.A_ptr, np.int32) + 1, np.int32), A_ind=_pad(p.A_ind, np.int32),
+                row_stat=np.zeros(m + 1, np.int8), col_stat=np.zeros(n + 1, np.int8))
+    f = lambda a: a.ctypes.data_as(C.c_void_p)  # noqa: E731
+    lp = Lp()
+    lp.m, lp.n, lp.nnz = m, n, p.nnz
+    for k, v in keep.items():
+        setattr(lp, k, f(v))
+    ret = L.gk_adv_basis(C.byref(lp))
+    if ret < 0:
+        raise GkError(_err(L))
+    return ret, keep["row_stat"][1:].copy(), keep["col_stat"][1:].copy()
+
+
+def glp_adv_basis(P: "GkProblem", flags: int = 0, msg_lev: int = 3) -> int:
+    """glp_adv_basis(lp, flags) (glpini01.js:356-362) on the Python host:
+    the statuses of the triangular basis into P (the basis factorization is
+    then invalid, as glp_set_row_stat / glp_set_col_stat leave it)."""
+    if flags != 0:
+        raise GkError(f"glp_adv_basis: flags = {flags}; invalid flags")
+    if P.m == 0 or P.n == 0:
+        size, rs, cs = adv_basis_statuses(P.p, P.L)
+    else:
+        _xprintf("Constructing initial basis...")
+        size, rs, cs = adv_basis_statuses(P.p, P.L)
+        if msg_lev >= 3:
+            _xprintf(f"Size of triangular part = {size}")
+    P.row_stat[1:P.m + 1] = rs
+    P.col_stat[1:P.n + 1] = cs
+    P.valid = 0
+    return size

@@ -40,7 +40,7 @@
 extern "C" {
 #endif
 
-#define GK_ABI_VERSION 2
+#define GK_ABI_VERSION 3
 #include <stddef.h>
 #define GK_EABI (-1)          /* contract violation; see gk_last_error() */
 
@@ -253,6 +253,17 @@ int gk_scale_prob(gk_ctx *ctx, int m, int n, const int *ptr, const int *ind, con
  * and their algorithmic bytes (bench.py) */
 int gk_scale_prob_timed(gk_ctx *ctx, int m, int n, const int *ptr, const int *ind, const double *val, int flags,
                         double *rii, double *sjj, double *report, double *sweep_ms, double *sweep_bytes);
+
+/* ---- advanced initial basis (glpini01.js) ---------------------------------
+ * Replaces adv_basis (glpini01.js:268-354, called by glp_adv_basis(lp, 0)):
+ * the basis of the maximal lower triangular part of (I | -A) found by triang
+ * (:2-212), columns of fixed variables removed, completed with auxiliary
+ * variables; non-basic statuses by type (double-bounded: the bound of
+ * smaller magnitude).  Reads m, n, row/col type and bounds, A_ptr / A_ind
+ * (list order) of lp; writes lp->row_stat[1..m], lp->col_stat[1..n].  With
+ * m == 0 or n == 0 it is glp_std_basis (glpapi05.js:49).  Host code (no
+ * context, no device).  Returns the size of the triangular part, or GK_EABI. */
+int gk_adv_basis(gk_lp *lp);
 
 #ifdef __cplusplus
 }

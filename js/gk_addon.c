@@ -430,6 +430,38 @@ static napi_value js_scale(napi_env env, napi_callback_info info)
     return mk_int(env, ret);
 }
 
+/* advBasis(m, n, row_type, row_lb, row_ub, col_type, col_lb, col_ub, ptr, ind,
+ *           row_stat, col_stat) -> size of the triangular part; types and
+ * statuses Int8Array [1..], bounds Float64Array [1..], ptr / ind Int32Array
+ * (1-based positions, list order).  Host code: no context. */
+static napi_value js_adv_basis(napi_env env, napi_callback_info info)
+{
+    napi_value argv[12];
+    if (!get_args(env, info, 12, argv)) return NULL;
+    gk_lp L;
+    memset(&L, 0, sizeof L);
+    CHECK(napi_get_value_int32(env, argv[0], &L.m));
+    CHECK(napi_get_value_int32(env, argv[1], &L.n));
+    L.row_type = (const signed char *)ta(env, argv[2]);
+    L.row_lb = (const double *)ta(env, argv[3]);
+    L.row_ub = (const double *)ta(env, argv[4]);
+    L.col_type = (const signed char *)ta(env, argv[5]);
+    L.col_lb = (const double *)ta(env, argv[6]);
+    L.col_ub = (const double *)ta(env, argv[7]);
+    L.A_ptr = (const int *)ta(env, argv[8]);
+    L.A_ind = (const int *)ta(env, argv[9]);
+    L.row_stat = (signed char *)ta(env, argv[10]);
+    L.col_stat = (signed char *)ta(env, argv[11]);
+    if (!L.row_type || !L.row_lb || !L.row_ub || !L.col_type || !L.col_lb || !L.col_ub || !L.A_ptr || !L.A_ind ||
+        !L.row_stat || !L.col_stat) {
+        napi_throw_type_error(env, NULL, "advBasis: typed arrays expected");
+        return NULL;
+    }
+    int ret = gk_adv_basis(&L);
+    if (ret == GK_EABI) return throw_gk(env, "adv_basis");
+    return mk_int(env, ret);
+}
+
 #define FN(name, f) { name, NULL, f, NULL, NULL, NULL, napi_enumerable, NULL }
 
 static napi_value init(napi_env env, napi_value exports)
@@ -440,6 +472,7 @@ static napi_value init(napi_env env, napi_value exports)
         FN("bfdFactorizeCsc", js_bfd_factorize_csc), FN("bfdFtran", js_bfd_ftran), FN("bfdBtran", js_bfd_btran),
         FN("bfdUpdate", js_bfd_update), FN("bfdGetCount", js_bfd_get_count), FN("bfdValid", js_bfd_valid),
         FN("spx", js_spx), FN("ios", js_ios), FN("stats", js_stats), FN("scale", js_scale),
+        FN("advBasis", js_adv_basis),
     };
     napi_define_properties(env, exports, sizeof d / sizeof d[0], d);
     return exports;

@@ -230,3 +230,17 @@ function scaleProb(lp, flags) {
     return {ret: ret, rii: rii, sjj: sjj, report: rep};
 }
 module.exports.scaleProb = scaleProb;
+
+// ---- glp_adv_basis (glpini01.js:1) -------------------------------------------
+// the statuses of the triangular starting basis (gk_adv_basis, host code)
+function advBasis(lp) {
+    var m = lp.m, n = lp.n, i, j, g = arrays(lp);
+    for (i = 1; i <= m; i++) { var R = lp.row[i]; g.row_type[i] = R.type; g.row_lb[i] = R.lb; g.row_ub[i] = R.ub; }
+    for (j = 1; j <= n; j++) { var Cj = lp.col[j]; g.col_type[j] = Cj.type; g.col_lb[j] = Cj.lb; g.col_ub[j] = Cj.ub; }
+    marshalMatrix(lp, g);
+    var rs = new Int8Array(m + 1), cs = new Int8Array(n + 1);
+    var size = addon.advBasis(m, n, g.row_type, g.row_lb, g.row_ub, g.col_type, g.col_lb, g.col_ub,
+                              g.A_ptr, g.A_ind, rs, cs);
+    return {size: size, row_stat: rs, col_stat: cs};
+}
+module.exports.advBasis = advBasis;

@@ -45,6 +45,25 @@ glp_scale_prob = exports["glp_scale_prob"] = function (lp, flags) {
     for (j = 1; j <= lp.n; j++) glp_set_sjj(lp, j, r.sjj[j - 1]);
 };
 
+// glp_adv_basis (glpini01.js:356-362): the triangular basis from the native
+// library (gk_adv_basis); the reference's lines through its own xprintf, the
+// statuses (GLP_*) through its own glp_set_row_stat / glp_set_col_stat, which
+// lpx_set_row_stat / lpx_set_col_stat forward to (glplpx01.js:233-240)
+glp_adv_basis = exports["glp_adv_basis"] = function (lp, flags) {
+    if (flags != 0)
+        xerror("glp_adv_basis: flags = " + flags + "; invalid flags");
+    if (lp.m == 0 || lp.n == 0) {
+        glp_std_basis(lp);
+        return;
+    }
+    xprintf("Constructing initial basis...");
+    var r = __gk.advBasis(lp), i, j;
+    if (lpx_get_int_parm(lp, LPX_K_MSGLEV) >= 3)
+        xprintf("Size of triangular part = " + r.size + "");
+    for (i = 1; i <= lp.m; i++) glp_set_row_stat(lp, i, r.row_stat[i]);
+    for (j = 1; j <= lp.n; j++) glp_set_col_stat(lp, j, r.col_stat[j]);
+};
+
 (function () {
     function versioned(f) {
         return function (lp) {

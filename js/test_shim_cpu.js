@@ -9,7 +9,7 @@ var core = require(path.join(__dirname, 'gk_core.js'));
 var names = ['create', 'deviceCount', 'abiVersion', 'lastError', 'bfdCreate', 'bfdSetParm', 'bfdFactorizeCsc',
              'bfdFtran', 'bfdBtran', 'bfdUpdate', 'bfdGetCount', 'bfdValid', 'spx', 'ios', 'stats'];
 names.forEach(function (k) { assert.strictEqual(typeof core.addon[k], 'function', k); });
-assert.strictEqual(core.addon.abiVersion(), 2);
+assert.strictEqual(core.addon.abiVersion(), 3);
 
 var ref = process.env.GLPK_REF || '/root/reference';
 var fs = require('fs');
@@ -30,6 +30,51 @@ assert.strictEqual(core.nativeIos({mip: {m: 2, n: 3}, parm: {cb_func: null, mip_
 assert.strictEqual(core.nativeIos({mip: {m: 80, n: 200}, parm: {cb_func: null, mip_gap: 0}}), true);
 assert.strictEqual(core.nativeIos({mip: {m: 30000, n: 40000}, parm: {cb_func: null, mip_gap: 0}}), false);
 glpk.glp_set_print_func(function () {});
+// glp_adv_basis through the shim (host code in the library, no device): the
+// reference's statuses and printed lines on its fixtures (tests/golden/adv_*)
+(function () {
+    var gdir = path.join(__dirname, '..', 'tests', 'golden');
+    var files = fs.readdirSync(gdir).filter(function (f) { return /^adv_.*\.json$/.test(f); }).sort();
+    assert.ok(files.length > 0, 'no adv_* fixtures');
+    files.forEach(function (f) {
+        var d = JSON.parse(fs.readFileSync(path.join(gdir, f), 'utf8'));
+        var P = glpk.glp_create_prob(), i, j, k;
+        if (d.m) glpk.glp_add_rows(P, d.m);
+        if (d.n) glpk.glp_add_cols(P, d.n);
+        for (i = 1; i <= d.m; i++) glpk.glp_set_row_bnds(P, i, d.row_type[i - 1], d.row_lb[i - 1], d.row_ub[i - 1]);
+        for (j = 1; j <= d.n; j++) glpk.glp_set_col_bnds(P, j, d.col_type[j - 1], d.col_lb[j - 1], d.col_ub[j - 1]);
+        // glp_load_matrix leaves the column lists in descending row order
+        // (glpapi01.js:512-528), glp_sort_matrix in ascending order (the
+        // order glp_read_lp leaves): the recorded problems have one or the other
+        var ia = [0], ja = [0], ar = [0];
+        for (j = 1; j <= d.n; j++)
+            for (k = d.A_ptr[j - 1]; k < d.A_ptr[j]; k++) { ia.push(d.A_ind[k]); ja.push(j); ar.push(d.A_val[k]); }
+        if (ia.length > 1) glpk.glp_load_matrix(P, ia.length - 1, ia, ja, ar);
+        var same = function () {
+            for (j = 1; j <= d.n; j++) {
+                var l = [];
+                for (var a = P.col[j].ptr; a != null; a = a.c_next) l.push(a.row.i);
+                if (JSON.stringify(l) !== JSON.stringify(d.A_ind.slice(d.A_ptr[j - 1], d.A_ptr[j]))) return false;
+            }
+            return true;
+        };
+        if (!same()) glpk.glp_sort_matrix(P);
+        assert.ok(same(), f + ': column list order not reproduced');
+        var lines = [];
+        glpk.glp_set_print_func(function (s) { lines.push(s); });
+        glpk.glp_adv_basis(P, 0);
+        glpk.glp_set_print_func(function () {});
+        assert.deepStrictEqual(lines, d.adv.lines, f + ': printed lines');
+        for (i = 1; i <= d.m; i++) assert.strictEqual(P.row[i].stat, d.adv.row_stat[i - 1], f + ': row ' + i);
+        for (j = 1; j <= d.n; j++) assert.strictEqual(P.col[j].stat, d.adv.col_stat[j - 1], f + ': col ' + j);
+        if (d.adv.flags_error) {
+            var err = null;
+            try { glpk.glp_adv_basis(P, 1); } catch (e) { err = String(e.message); }
+            assert.strictEqual(err, d.adv.flags_error, f + ': flags error');
+        }
+    });
+    console.log('ok adv basis (' + files.length + ' reference fixtures)');
+})();
 var lp = glpk.glp_create_prob();
 glpk.glp_set_obj_dir(lp, glpk.GLP_MAX);
 glpk.glp_add_rows(lp, 1);

@@ -46,6 +46,7 @@ function buildBundle() {
         'exports["__cnt"] = __cnt;',
         'ios_solve_node = (function(f){ return function(t){ __cnt.solve_node++; return f(t); }; })(ios_solve_node);',
         'bfd_factorize = (function(f){ return function(a,b,c,d,e){ __cnt.factorize++; return f(a,b,c,d,e); }; })(bfd_factorize);',
+        'exports["__glp_adv_basis"] = glp_adv_basis;',
         ''].join('\n'));
     parts.push(fs.readFileSync(path.join(REF, 'footer'), 'utf8'));
     var dst = '/tmp/glpk_golden_bundle.js';
@@ -442,3 +443,40 @@ scaleCase('bad', function () { return genBadScale(77, 40, 60, 0.2); });
 scaleCase('well', function () { return genWellScaled(78, 20, 30); });
 scaleCase('dense_64x256', function () { return genDense(64, 256, 42); });
 scaleCase('c2s', function () { return genC2s(821, 1571, 7, 42); });
+
+// ---- glp_adv_basis (glpini01.js:1): the triangular starting basis ----------
+// statuses and printed lines, the bad-flags error, and both simplex methods
+// run from that basis
+function advCase(name, mk) {
+    if (ONLY && ('adv_' + name).indexOf(ONLY) !== 0) return;
+    var P = mk(), d = dumpProb(P, null), lines = [];
+    d.name = name; d.kind = 'adv';
+    glpk.glp_set_print_func(function (s) { lines.push(s); });
+    glpk.__glp_adv_basis(P, 0);
+    glpk.glp_set_print_func(function () {});
+    var b = snapshotBasis(P);
+    d.adv = {row_stat: b.row_stat, col_stat: b.col_stat, lines: lines};
+    try { glpk.__glp_adv_basis(mk(), 1); } catch (e) { d.adv.flags_error = String(e.message); }
+    d.runs = [];
+    [1, 3].forEach(function (meth) {
+        var Q = mk();
+        glpk.__glp_adv_basis(Q, 0);
+        d.runs.push(runLp(Q, {meth: meth}, 0));
+    });
+    fs.writeFileSync(path.join(OUT, 'adv_' + name + '.json'), JSON.stringify(d));
+    console.log('wrote adv', name, d.m + 'x' + d.n, d.adv.lines.join(' | '),
+                d.runs.map(function (r) { return 'meth' + r.opts.meth + ':ret' + r.ret + ':it' + r.it_cnt + ':obj' + r.obj_val; }).join(' '));
+}
+advCase('test', function () { return readLp('test.lpt'); });
+advCase('todd', function () { return readLp('todd.lpt'); });
+advCase('gap', function () { return readLp('gap.lpt'); });
+advCase('dense_64x256', function () { return genDense(64, 256, 42); });
+advCase('c2s', function () { return genC2s(821, 1571, 7, 42); });
+[13, 14, 15, 16, 17, 18].forEach(function (sd) {
+    advCase('mix' + sd, function () { return genMix(sd, 8 + sd, 10 + 2 * sd, 0.35, false, true); });
+});
+[1, 2, 3].forEach(function (sd) {
+    advCase('wild' + sd, function () { return genMix(sd, 6 + 2 * sd, 9 + 3 * sd, 0.35, false, false); });
+});
+advCase('mixbig1', function () { return genMix(300, 50, 80, 0.15, false, true, false); });
+advCase('nocols', function () { var P = newProb(); glpk.glp_add_rows(P, 3); return P; });
