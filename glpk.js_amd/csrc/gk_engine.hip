@@ -196,6 +196,8 @@ struct gk_bfd {
     DBuf<double> bval;
     Engine *eng = nullptr;
     gk_spx_stats stats{};
+    gk_report_fn rpt = nullptr;                // progress / termination reports (gk_bfd_set_report)
+    void *rpt_ud = nullptr;
 };
 
 static const size_t PARTIAL_CAP = (size_t)1 << 22;   // >= splits * rows of every gemv (see gemv_plan, dual_plan)
@@ -734,14 +736,72 @@ struct Spx {
     {
         pull();
         BasisSplit bs;
-        if (!split_from_head(m, head.data(), bs)) return false;
+        if (!split_from_head(m, head.data(), bs)) {
+            fact_ret = 1;                       // BFD_ESING
+            return false;
+        }
         MatDev A = E->mat();
         int ret;
         if (E->dense)
             ret = reinvert_core(f, bs, &A, 0, 1.0, nullptr, nullptr, nullptr);
         else
             ret = reinvert_core_csc(bs);
+        fact_ret = ret;
         return ret == 0;
+    }
+    int fact_ret = 0;
+
+    // ---- the reference's terminal output (display, glpspx01.js:1550-1589 /
+    // glpspx02.js:1452-1497, and the xprintf lines of the main loops), as
+    // structured reports: the host formats them with its own number
+    // printing (the reference prints doubles with JavaScript's conversion)
+    int it_dpy = -1;
+    void report_msg(int code, int lev, int aux = 0)
+    {
+        if (f->rpt && parm->msg_lev >= lev) f->rpt(f->rpt_ud, GK_RPT_MSG, code, hs.it_cnt, phase, 0.0, 0.0, aux);
+    }
+    void display(int spec)
+    {
+        const gk_smcp *P = parm;
+        if (!f->rpt || P->msg_lev < 2) return;             // GLP_MSG_ON
+        if (P->out_dly > 0 && 1000.0 * (now_s() - tm_beg) < P->out_dly) return;
+        if (hs.it_cnt == it_dpy) return;
+        if (!spec && hs.it_cnt % std::max(P->out_frq, 1) != 0) return;
+        pull();
+        double sum = 0.0;
+        int cnt = 0;
+        if (dual) {
+            // the sum of dual infeasibilities (phase I: of the working costs)
+            if (phase == 1) {
+                for (int i = 1; i <= m; i++) sum -= coef[head[i]] * bbar[i];
+                for (int j = 1; j <= n; j++) sum -= coef[head[m + j]] * get_xN(j);
+            } else {
+                for (int j = 1; j <= n; j++) {
+                    if (cbar[j] < 0.0 && (stat[j] == NL || stat[j] == NF)) sum -= cbar[j];
+                    if (cbar[j] > 0.0 && (stat[j] == NU || stat[j] == NF)) sum += cbar[j];
+                }
+            }
+            for (int i = 1; i <= m; i++)
+                if (orig_type[head[i]] == FX) cnt++;
+        } else {
+            // the sum of primal infeasibilities of the basic variables
+            for (int i = 1; i <= m; i++) {
+                const int k = head[i];
+                if ((type[k] == LO || type[k] == DB || type[k] == FX) && bbar[i] < lb[k]) sum += lb[k] - bbar[i];
+                if ((type[k] == UP || type[k] == DB || type[k] == FX) && bbar[i] > ub[k]) sum += bbar[i] - ub[k];
+                if (type[k] == FX) cnt++;
+            }
+        }
+        const double ob = (dual && phase == 1) ? 0.0 : eval_obj();
+        f->rpt(f->rpt_ud, GK_RPT_PROGRESS, dual ? 2 : 1, hs.it_cnt, phase, ob, sum, cnt);
+        it_dpy = hs.it_cnt;
+    }
+    // pivots of the next batch: up to the next progress line
+    int align_to_display(int K) const
+    {
+        if (!f->rpt || parm->msg_lev < 2) return K;
+        const int fr = std::max(parm->out_frq, 1);
+        return std::max(1, std::min(K, fr - hs.it_cnt % fr));
     }
     int reinvert_core_csc(const BasisSplit &bs);
 
@@ -1303,7 +1363,10 @@ int Spx::run_dual()
     int ret;
     for (;;) {
         if (binv_st == 0) {
-            if (!reinvert()) return fail_return();
+            if (!reinvert()) {
+                report_msg(GK_MSG_FACTERR, 1, fact_ret);     // GLP_MSG_ERR
+                return fail_return();
+            }
             binv_st = 1;
             bbar_st = cbar_st = 0;
             hs.upd_cnt = 0; hs.refact_pending = 0;
@@ -1322,6 +1385,7 @@ int Spx::run_dual()
                 bbar_st = 0;
             }
             if (dual_check_stab(P->tol_dj) != 0) {
+                report_msg(GK_MSG_INSTAB, 1, 2);
                 if (P->meth == 2) {            // GLP_DUALP
                     store_sol(1, 1, 0);
                     return 5;
@@ -1343,6 +1407,7 @@ int Spx::run_dual()
             }
             if (infeas == 0) {
                 pull();
+                display(1);
                 phase = 2;
                 if (cbar_st != 1) { eval_cbar(); cbar_st = 1; }
                 set_orig_bnds();
@@ -1363,6 +1428,8 @@ int Spx::run_dual()
                 if (cbar_st != 1) cbar_st = 0;
                 continue;
             }
+            display(1);
+            report_msg(GK_MSG_OBJLL, 3);
             store_sol(3, 2, 0);
             return 6;                                  // GLP_EOBJLL
         }
@@ -1372,6 +1439,8 @@ int Spx::run_dual()
                 if (cbar_st != 1) cbar_st = 0;
                 continue;
             }
+            display(1);
+            report_msg(GK_MSG_OBJUL, 3);
             store_sol(3, 2, 0);
             return 7;                                  // GLP_EOBJUL
         }
@@ -1384,6 +1453,8 @@ int Spx::run_dual()
                     if (cbar_st != 1) cbar_st = 0;
                     continue;
                 }
+                display(1);
+                report_msg(it_hit ? GK_MSG_ITLIM : GK_MSG_TMLIM, 3);
                 int d_stat;
                 if (phase == 1) {
                     pull();
@@ -1402,6 +1473,7 @@ int Spx::run_dual()
             binv_st = 0;
             continue;
         }
+        display(0);
         int K = rigorous ? 1 : E->kbatch;
         if (P->it_lim < 0x7fffffff) {
             // an iteration budget of up to two full batches runs as one
@@ -1409,6 +1481,7 @@ int Spx::run_dual()
             K = (!rigorous && K >= 64 && rem <= 128) ? rem : std::max(1, std::min(K, rem));
         }
         K = align_to_refactor(K, hs.upd_lim - hs.upd_cnt);
+        K = align_to_display(K);
         int why = batch(K, rigorous);
         E->kbatch = next_batch(E->kbatch, why);
         dinf_known = (why == ST_BATCH && hs.npiv > 0);
@@ -1433,6 +1506,8 @@ int Spx::run_dual()
                 break;
             }
             {
+                display(1);
+                report_msg(phase == 1 ? GK_MSG_NODFS : GK_MSG_OPTIMAL, 3);
                 int p_stat, d_stat;
                 if (phase == 1) {
                     pull();
@@ -1451,7 +1526,12 @@ int Spx::run_dual()
                 rigorous = 1;
                 break;
             }
-            if (phase == 1) return fail_return();
+            display(1);
+            if (phase == 1) {
+                report_msg(GK_MSG_NOCHOICE, 1);
+                return fail_return();
+            }
+            report_msg(GK_MSG_NOPFS, 3);
             pull();
             store_sol(4, 2, head[hs.p]);
             return 0;
@@ -1475,7 +1555,10 @@ int Spx::run_primal()
     int binv_st = f->valid ? 2 : 0, bbar_st = 0, cbar_st = 0, rigorous = 0;
     for (;;) {
         if (binv_st == 0) {
-            if (!reinvert()) return fail_return();
+            if (!reinvert()) {
+                report_msg(GK_MSG_FACTERR, 1, fact_ret);     // GLP_MSG_ERR
+                return fail_return();
+            }
             binv_st = 1;
             bbar_st = cbar_st = 0;
             hs.upd_cnt = 0; hs.refact_pending = 0;
@@ -1490,8 +1573,10 @@ int Spx::run_primal()
                 else { set_orig_obj(); phase = 2; }
                 ABI_REQUIRE(primal_check_stab(P->tol_bnd) == 0, "spx_primal: check_stab after phase selection");
                 cbar_st = 0;
+                display(1);
             }
             if (primal_check_stab(P->tol_bnd)) {
+                report_msg(GK_MSG_INSTAB, 1, 1);
                 phase = 0;
                 binv_st = 0;
                 rigorous = 5;
@@ -1504,6 +1589,7 @@ int Spx::run_primal()
                 phase = 2;
                 set_orig_obj();
                 cbar_st = 0;
+                display(1);
             }
         }
         if (cbar_st == 0) {
@@ -1521,6 +1607,8 @@ int Spx::run_primal()
                     if (phase == 2 && cbar_st != 1) cbar_st = 0;
                     continue;
                 }
+                display(1);
+                report_msg(it_hit ? GK_MSG_ITLIM : GK_MSG_TMLIM, 3);
                 int p_stat;
                 pull();
                 if (phase == 1) {
@@ -1540,6 +1628,7 @@ int Spx::run_primal()
             binv_st = 0;
             continue;
         }
+        display(0);
         int K = rigorous ? 1 : E->kbatch;
         if (P->it_lim < 0x7fffffff) {
             // an iteration budget of up to two full batches runs as one
@@ -1547,6 +1636,7 @@ int Spx::run_primal()
             K = (!rigorous && K >= 64 && rem <= 128) ? rem : std::max(1, std::min(K, rem));
         }
         K = align_to_refactor(K, hs.upd_lim - hs.upd_cnt);
+        K = align_to_display(K);
         int why = batch(K, rigorous);
         E->kbatch = next_batch(E->kbatch, why);
         if (hs.npiv > 0) {
@@ -1571,6 +1661,8 @@ int Spx::run_primal()
                 break;
             }
             {
+                display(1);
+                report_msg(phase == 1 ? GK_MSG_NOPFS : GK_MSG_OPTIMAL, 3);
                 int p_stat, d_stat;
                 pull();
                 if (phase == 1) {
@@ -1595,7 +1687,12 @@ int Spx::run_primal()
                 rigorous = 1;
                 break;
             }
-            if (phase == 1) return fail_return();
+            display(1);
+            if (phase == 1) {
+                report_msg(GK_MSG_NOCHOICE, 1);
+                return fail_return();
+            }
+            report_msg(GK_MSG_UNBND, 3);
             pull();
             store_sol(2, 4, head[m + hs.q]);
             return 0;
@@ -1709,6 +1806,13 @@ int gk_bfd_set_parm(gk_bfd *f, const gk_bfcp *parm)
 }
 
 int gk_bfd_valid(const gk_bfd *f) { return f ? f->valid : 0; }
+
+void gk_bfd_set_report(gk_bfd *f, gk_report_fn fn, void *ud)
+{
+    if (!f) return;
+    f->rpt = fn;
+    f->rpt_ud = ud;
+}
 
 int gk_bfd_get_count(const gk_bfd *f)
 {

@@ -26,6 +26,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "libglpk_mi355x.so")
 
 GLP_MSG_OFF, GLP_MSG_ERR, GLP_MSG_ON, GLP_MSG_ALL, GLP_MSG_DBG = 0, 1, 2, 3, 4
+GLP_VERSION = "4.49"                         # glp_version (glpapi.js:76, glpk.js:3-4)
 GLP_PT_STD, GLP_PT_PSE = 0x11, 0x22
 GLP_RT_STD, GLP_RT_HAR = 0x11, 0x22
 GLP_EBADB, GLP_ESING, GLP_ECOND, GLP_EBOUND, GLP_EFAIL = 1, 2, 3, 4, 5
@@ -105,7 +106,11 @@ EXPORTS = ["gk_abi_version", "gk_device_count", "gk_ctx_create", "gk_ctx_destroy
            "gk_bfd_create", "gk_bfd_destroy", "gk_bfd_set_parm", "gk_bfd_factorize", "gk_bfd_factorize_csc",
            "gk_bfd_ftran", "gk_bfd_btran", "gk_bfd_update", "gk_bfd_get_count", "gk_bfd_valid",
            "gk_spx_primal", "gk_spx_dual", "gk_bfd_last_stats", "gk_bfd_profile", "gk_ios_driver",
-           "gk_scale_prob", "gk_scale_prob_timed", "gk_adv_basis"]
+           "gk_scale_prob", "gk_scale_prob_timed", "gk_adv_basis", "gk_bfd_set_report"]
+
+# gk_report_fn (glpk_mi355x.h): one progress line or termination message of
+# a gk_spx_* call, in the order the reference prints them
+REPORT_FN = C.CFUNCTYPE(None, C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_double, C.c_double, C.c_int)
 
 
 def load_library(path: str = LIB_PATH):
@@ -161,6 +166,8 @@ def load_library(path: str = LIB_PATH):
     L.gk_scale_prob_timed.restype = C.c_int
     L.gk_adv_basis.argtypes = [P]
     L.gk_adv_basis.restype = C.c_int
+    L.gk_bfd_set_report.argtypes = [P, REPORT_FN, P]
+    L.gk_bfd_set_report.restype = None
     _lib = L
     return L
 
@@ -374,7 +381,18 @@ class GkProblem:
     def spx(self, parm: Smcp, dual: bool) -> int:
         lp = self._lp_struct()
         fn = self.L.gk_spx_dual if dual else self.L.gk_spx_primal
-        ret = fn(self.ctx.h, C.byref(lp), self.bfd, C.byref(parm))
+        reports = []
+        cb = REPORT_FN(lambda ud, *r: reports.append(r))
+        self.L.gk_bfd_set_report(self.bfd, cb, None)
+        try:
+            ret = fn(self.ctx.h, C.byref(lp), self.bfd, C.byref(parm))
+        finally:
+            self.L.gk_bfd_set_report(self.bfd, REPORT_FN(), None)
+        # the display lines and messages (glpspx01.js:1587, glpspx02.js:1493),
+        # printed in order after the solve
+        for r in reports:
+            for line in report_lines(*r):
+                _xprintf(line)
         if ret == GK_EABI:
             raise GkError(_err(self.L))
         self._take(lp)
@@ -422,6 +440,7 @@ def _trivial_lp(P: GkProblem, parm: Smcp):
     P.pbs_stat = P.dbs_stat = GLP_FEAS
     P.obj_val = P.c0
     P.some = 0
+    p_infeas = d_infeas = 0.0
     for i in range(1, P.m + 1):
         t = P.row_type[i]
         P.row_stat[i] = GLP_BS
@@ -430,10 +449,14 @@ def _trivial_lp(P: GkProblem, parm: Smcp):
             P.pbs_stat = GLP_NOFEAS
             if P.some == 0 and parm.meth != GLP_PRIMAL:
                 P.some = i
+        if t in (GLP_LO, GLP_DB, GLP_FX):
+            p_infeas = max(p_infeas, P.row_lb[i])
         if t in (GLP_UP, GLP_DB, GLP_FX) and P.row_ub[i] < -parm.tol_bnd:
             P.pbs_stat = GLP_NOFEAS
             if P.some == 0 and parm.meth != GLP_PRIMAL:
                 P.some = i
+        if t in (GLP_UP, GLP_DB, GLP_FX):
+            p_infeas = max(p_infeas, -P.row_ub[i])
     zeta = 1.0
     for j in range(1, P.n + 1):
         zeta = max(zeta, abs(P.col_coef[j]))
@@ -459,10 +482,27 @@ def _trivial_lp(P: GkProblem, parm: Smcp):
             P.dbs_stat = GLP_NOFEAS
             if P.some == 0 and parm.meth == GLP_PRIMAL:
                 P.some = P.m + j
+        if t in (GLP_FR, GLP_LO):
+            d_infeas = max(d_infeas, -zeta * coef)
         if t in (GLP_FR, GLP_UP) and zeta * coef > +parm.tol_dj:
             P.dbs_stat = GLP_NOFEAS
             if P.some == 0 and parm.meth == GLP_PRIMAL:
                 P.some = P.m + j
+        if t in (GLP_FR, GLP_UP):
+            d_infeas = max(d_infeas, zeta * coef)
+    # the simulated solver output (glpapi06.js:244-256)
+    if parm.msg_lev >= GLP_MSG_ON and parm.out_dly == 0:
+        inf = p_infeas if parm.meth == GLP_PRIMAL else d_infeas
+        _xprintf(f"~{P.it_cnt}: obj = {_js_num(P.obj_val)}  infeas = {_js_num(inf)}")
+    if parm.msg_lev >= GLP_MSG_ALL and parm.out_dly == 0:
+        if P.pbs_stat == GLP_FEAS and P.dbs_stat == GLP_FEAS:
+            _xprintf("OPTIMAL SOLUTION FOUND")
+        elif P.pbs_stat == GLP_NOFEAS:
+            _xprintf("PROBLEM HAS NO FEASIBLE SOLUTION")
+        elif parm.meth == GLP_PRIMAL:
+            _xprintf("PROBLEM HAS UNBOUNDED SOLUTION")
+        else:
+            _xprintf("PROBLEM HAS NO DUAL FEASIBLE SOLUTION")
 
 
 def glp_simplex(P: GkProblem, parm: Smcp | None = None) -> int:
@@ -488,9 +528,17 @@ def glp_simplex(P: GkProblem, parm: Smcp | None = None) -> int:
     P.pbs_stat = P.dbs_stat = GLP_UNDEF
     P.obj_val = 0.0
     P.some = 0
-    if np.any((P.row_type[1:] == GLP_DB) & (P.row_lb[1:] >= P.row_ub[1:])) or \
-            np.any((P.col_type[1:] == GLP_DB) & (P.col_lb[1:] >= P.col_ub[1:])):
-        return GLP_EBOUND
+    for what, typ, lb, ub in (("row", P.row_type, P.row_lb, P.row_ub), ("column", P.col_type, P.col_lb, P.col_ub)):
+        bad = np.nonzero((typ[1:] == GLP_DB) & (lb[1:] >= ub[1:]))[0]
+        if bad.size:
+            k = int(bad[0]) + 1
+            if parm.msg_lev >= GLP_MSG_ERR:
+                _xprintf(f"glp_simplex: {what} {k}: lb = {_js_num(lb[k])}, ub = {_js_num(ub[k])}; incorrect bounds")
+            return GLP_EBOUND
+    if parm.msg_lev >= GLP_MSG_ALL:
+        _xprintf(f"GLPK Simplex Optimizer, v{GLP_VERSION}")
+        _xprintf(f"{P.m} row{'' if P.m == 1 else 's'}, {P.n} column{'' if P.n == 1 else 's'}, "
+                 f"{P.nnz} non-zero{'' if P.nnz == 1 else 's'}")
     if P.nnz == 0:
         _trivial_lp(P, parm)
         return 0
@@ -498,6 +546,10 @@ def glp_simplex(P: GkProblem, parm: Smcp | None = None) -> int:
     if not (P.m == 0 or P.valid):
         ret = P.factorize()
         if ret != 0:
+            if parm.msg_lev >= GLP_MSG_ERR:
+                _xprintf({GLP_EBADB: "glp_simplex: initial basis is invalid",
+                          GLP_ESING: "glp_simplex: initial basis is singular",
+                          GLP_ECOND: "glp_simplex: initial basis is ill-conditioned"}[ret])
             return ret
     if parm.meth == GLP_PRIMAL:
         return P.spx(parm, dual=False)
@@ -665,6 +717,33 @@ def _xprintf(s: str) -> None:
         _print_func(s)
     else:
         print(s)
+
+
+_REPORT_MSG = {1: "OPTIMAL SOLUTION FOUND", 2: "PROBLEM HAS NO DUAL FEASIBLE SOLUTION",
+               3: "PROBLEM HAS NO FEASIBLE SOLUTION", 4: "PROBLEM HAS UNBOUNDED SOLUTION",
+               5: "ITERATION LIMIT EXCEEDED; SEARCH TERMINATED", 6: "TIME LIMIT EXCEEDED; SEARCH TERMINATED",
+               7: "OBJECTIVE LOWER LIMIT REACHED; SEARCH TERMINATED",
+               8: "OBJECTIVE UPPER LIMIT REACHED; SEARCH TERMINATED",
+               10: "Error: unable to choose basic variable on phase I"}
+
+
+def report_lines(kind, code, it, phase, obj, inf, aux) -> list:
+    """The lines the reference prints for one gk_report_fn record: the display
+    lines of glpspx01.js:1587 (primal) and glpspx02.js:1493-1495 (dual), the
+    termination messages of glpspx01.js:1815-1886 / glpspx02.js:1668-1886."""
+    if kind == 1:
+        if code == 1:
+            return [f"{' ' if phase == 1 else '*'}{it}: obj = {_js_num(obj)}  infeas = {_js_num(inf)} ({aux})"]
+        if phase == 1:
+            return [f" {it}:  infeas = {_js_num(inf)} ({aux})"]
+        return [f"|{it}: obj = {_js_num(obj)}  infeas = {_js_num(inf)} ({aux})"]
+    if code == 9:
+        return [f"Warning: numerical instability ({'primal' if aux == 1 else 'dual'} simplex, "
+                f"phase {'I' if phase == 1 else 'II'})"]
+    if code == 11:
+        return [f"Error: unable to factorize the basis matrix ({aux})",
+                "Sorry, basis recovery procedure not implemented yet"]
+    return [_REPORT_MSG[code]] if code in _REPORT_MSG else []
 
 
 def _js_num(x: float) -> str:

@@ -139,6 +139,39 @@ typedef struct {
 int gk_spx_primal(gk_ctx *ctx, gk_lp *lp, gk_bfd *bfd, const gk_smcp *parm);
 int gk_spx_dual(gk_ctx *ctx, gk_lp *lp, gk_bfd *bfd, const gk_smcp *parm);
 
+/* The reference's terminal output of the simplex (display, glpspx01.js:
+ * 1550-1589 / glpspx02.js:1452-1497, and the messages of the main loops),
+ * reported instead of printed: the host formats each line with its own
+ * number printing (the reference's are JavaScript conversions of doubles),
+ * in call order, on the calling thread, during the gk_spx_* call.  Reports
+ * follow parm->msg_lev and out_frq / out_dly as the reference's do (a device
+ * batch ends at every multiple of out_frq when progress lines are on).
+ *   kind GK_RPT_PROGRESS: code 1 primal / 2 dual, it_cnt, phase, obj (primal;
+ *     dual phase II), infeas (the sum of primal / dual infeasibilities), aux =
+ *     the number of basic fixed variables:
+ *       primal  (phase 1 ? ' ' : '*') it ": obj = " obj "  infeas = " inf " (" aux ")"
+ *       dual I  " " it ":  infeas = " inf " (" aux ")"
+ *       dual II "|" it ": obj = " obj "  infeas = " inf " (" aux ")"
+ *   kind GK_RPT_MSG: code GK_MSG_*, phase, aux (GK_MSG_INSTAB: 1 primal /
+ *     2 dual; GK_MSG_FACTERR: the factorization's return code) */
+#define GK_RPT_PROGRESS 1
+#define GK_RPT_MSG 2
+#define GK_MSG_OPTIMAL 1    /* "OPTIMAL SOLUTION FOUND" */
+#define GK_MSG_NODFS 2      /* "PROBLEM HAS NO DUAL FEASIBLE SOLUTION" */
+#define GK_MSG_NOPFS 3      /* "PROBLEM HAS NO FEASIBLE SOLUTION" */
+#define GK_MSG_UNBND 4      /* "PROBLEM HAS UNBOUNDED SOLUTION" */
+#define GK_MSG_ITLIM 5      /* "ITERATION LIMIT EXCEEDED; SEARCH TERMINATED" */
+#define GK_MSG_TMLIM 6      /* "TIME LIMIT EXCEEDED; SEARCH TERMINATED" */
+#define GK_MSG_OBJLL 7      /* "OBJECTIVE LOWER LIMIT REACHED; SEARCH TERMINATED" */
+#define GK_MSG_OBJUL 8      /* "OBJECTIVE UPPER LIMIT REACHED; SEARCH TERMINATED" */
+#define GK_MSG_INSTAB 9     /* "Warning: numerical instability (primal|dual simplex, phase I|II)" */
+#define GK_MSG_NOCHOICE 10  /* "Error: unable to choose basic variable on phase I" */
+#define GK_MSG_FACTERR 11   /* "Error: unable to factorize the basis matrix (aux)",
+                               "Sorry, basis recovery procedure not implemented yet" */
+typedef void (*gk_report_fn)(void *ud, int kind, int code, int it_cnt, int phase, double obj, double infeas,
+                             int aux);
+void gk_bfd_set_report(gk_bfd *bfd, gk_report_fn fn, void *ud);
+
 /* engine counters of the last gk_spx_* call on this handle (for benches) */
 typedef struct {
     long long pivots, reinversions, batches, host_syncs;

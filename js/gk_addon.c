@@ -309,6 +309,31 @@ static int fill_lp(napi_env env, napi_value L, gk_lp *out)
     return 1;
 }
 
+/* the reports of one gk_spx_* call (gk_bfd_set_report), handed to JS as
+ * L.reports = [[kind, code, it_cnt, phase, obj, infeas, aux], ...] */
+typedef struct {
+    int kind, code, it_cnt, phase, aux;
+    double obj, infeas;
+} rpt_rec;
+typedef struct {
+    rpt_rec *v;
+    size_t n, cap;
+} rpt_buf;
+
+static void rpt_collect(void *ud, int kind, int code, int it_cnt, int phase, double obj, double infeas, int aux)
+{
+    rpt_buf *b = (rpt_buf *)ud;
+    if (b->n == b->cap) {
+        size_t cap = b->cap ? 2 * b->cap : 64;
+        rpt_rec *v = (rpt_rec *)realloc(b->v, cap * sizeof(rpt_rec));
+        if (!v) return;
+        b->v = v;
+        b->cap = cap;
+    }
+    rpt_rec r = {kind, code, it_cnt, phase, aux, obj, infeas};
+    b->v[b->n++] = r;
+}
+
 static napi_value js_spx(napi_env env, napi_callback_info info)
 {
     napi_value argv[5];
@@ -335,7 +360,27 @@ static napi_value js_spx(napi_env env, napi_callback_info info)
     p.out_frq = (int)dprop(env, S, "out_frq", 500);
     p.out_dly = (int)dprop(env, S, "out_dly", 0);
     p.presolve = (int)dprop(env, S, "presolve", 0);
+    rpt_buf rb = {NULL, 0, 0};
+    gk_bfd_set_report(b, rpt_collect, &rb);
     int ret = dual ? gk_spx_dual(c, &lp, b, &p) : gk_spx_primal(c, &lp, b, &p);
+    gk_bfd_set_report(b, NULL, NULL);
+    {
+        napi_value arr;
+        CHECK(napi_create_array_with_length(env, rb.n, &arr));
+        for (size_t k = 0; k < rb.n; k++) {
+            const rpt_rec *r = &rb.v[k];
+            const double f[7] = {r->kind, r->code, r->it_cnt, r->phase, r->obj, r->infeas, r->aux};
+            napi_value e, x;
+            CHECK(napi_create_array_with_length(env, 7, &e));
+            for (uint32_t t = 0; t < 7; t++) {
+                CHECK(napi_create_double(env, f[t], &x));
+                CHECK(napi_set_element(env, e, t, x));
+            }
+            CHECK(napi_set_element(env, arr, (uint32_t)k, e));
+        }
+        CHECK(napi_set_named_property(env, L, "reports", arr));
+        free(rb.v);
+    }
     if (ret == GK_EABI) return throw_gk(env, dual ? "spx_dual" : "spx_primal");
     set_num(env, L, "it_cnt", lp.it_cnt);
     set_num(env, L, "pbs_stat", lp.pbs_stat);

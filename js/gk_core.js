@@ -131,13 +131,42 @@ function marshal(lp, g) {
     };
 }
 
-function spx(lp, parm, dual) {
+// the simplex's terminal output (gk_bfd_set_report) as the reference prints
+// it (display, glpspx01.js:1587 / glpspx02.js:1492-1495, and the main loops'
+// xprintf lines): one report -> its lines
+var MSG = {1: 'OPTIMAL SOLUTION FOUND', 2: 'PROBLEM HAS NO DUAL FEASIBLE SOLUTION',
+           3: 'PROBLEM HAS NO FEASIBLE SOLUTION', 4: 'PROBLEM HAS UNBOUNDED SOLUTION',
+           5: 'ITERATION LIMIT EXCEEDED; SEARCH TERMINATED', 6: 'TIME LIMIT EXCEEDED; SEARCH TERMINATED',
+           7: 'OBJECTIVE LOWER LIMIT REACHED; SEARCH TERMINATED', 8: 'OBJECTIVE UPPER LIMIT REACHED; SEARCH TERMINATED',
+           10: 'Error: unable to choose basic variable on phase I'};
+function reportLines(r) {
+    var kind = r[0], code = r[1], it = r[2], phase = r[3], obj = r[4], inf = r[5], aux = r[6];
+    if (kind === 1) {
+        if (code === 1) return [(phase == 1 ? ' ' : '*') + it + ": obj = " + obj + "  infeas = " + inf + " (" + aux + ")"];
+        if (phase == 1) return [" " + it + ":  infeas = " + inf + " (" + aux + ")"];
+        return ["|" + it + ": obj = " + obj + "  infeas = " + inf + " (" + aux + ")"];
+    }
+    if (code === 9)
+        return ["Warning: numerical instability (" + (aux == 1 ? "primal" : "dual") + " simplex, phase " +
+                (phase == 1 ? "I" : "II") + ")"];
+    if (code === 11)
+        return ["Error: unable to factorize the basis matrix (" + aux + ")",
+                "Sorry, basis recovery procedure not implemented yet"];
+    return MSG[code] ? [MSG[code]] : [];
+}
+module.exports.reportLines = reportLines;
+
+// print: the reference's xprintf (the shim passes it), called in order for
+// every line the solve produced
+function spx(lp, parm, dual, print) {
     var m = lp.m, n = lp.n, i, j, row, col;
     var g = arrays(lp);
     var L = marshal(lp, g);
     // init_csa asserts lp.valid and takes lp.bfd (glpspx01.js:129-132)
     if (!lp.valid || lp.bfd === null) throw new Error('assert');
     var ret = addon.spx(context(), lp.bfd.gk, L, parm, dual);
+    if (print && L.reports)
+        L.reports.forEach(function (r) { reportLines(r).forEach(function (s) { print(s); }); });
     lp.valid = L.valid;
     lp.bfd.valid = L.valid;
     lp.pbs_stat = L.pbs_stat;

@@ -7,8 +7,8 @@
 // re-uploaded only when A or the scaling changed (SURVEY.md §8(b).1).
 var __gk = require(__gk_core_path);
 
-spx_primal = function (lp, parm) { return __gk.spx(lp, parm, false); };
-spx_dual = function (lp, parm) { return __gk.spx(lp, parm, true); };
+spx_primal = function (lp, parm) { return __gk.spx(lp, parm, false, xprintf); };
+spx_dual = function (lp, parm) { return __gk.spx(lp, parm, true, xprintf); };
 bfd_create_it = function () { return __gk.bfdCreate(); };
 bfd_set_parm = function (bfd, parm) { __gk.bfdSetParm(bfd, parm); };
 bfd_factorize = function (bfd, m, bh, col, info) { return __gk.bfdFactorize(bfd, m, bh, col, info); };

@@ -78,30 +78,53 @@ function factorize(lp) {
     return 0;
 }
 
-function simplex(lp, parm) {   // solve_lp (glpapi06.js:3-37)
+function simplex(lp, parm, print) {   // solve_lp (glpapi06.js:3-37)
     if (!lp.valid) {
         var r = factorize(lp);
         if (r) return r;
     }
-    if (parm.meth === GLP_PRIMAL) return core.spx(lp, parm, false);
+    if (parm.meth === GLP_PRIMAL) return core.spx(lp, parm, false, print);
     if (parm.meth === GLP_DUALP) {
-        var ret = core.spx(lp, parm, true);
-        if (ret === GLP_EFAIL && lp.valid) ret = core.spx(lp, parm, false);
+        var ret = core.spx(lp, parm, true, print);
+        if (ret === GLP_EFAIL && lp.valid) ret = core.spx(lp, parm, false, print);
         return ret;
     }
-    return core.spx(lp, parm, true);
+    return core.spx(lp, parm, true, print);
+}
+
+// the display lines and messages the engine reported against the
+// reference's (tests/golden lp_* runs[].lines, minus glp_simplex's own header
+// lines): same text, numbers within 1e-7 relative
+var NUM = /-?(?:\d+\.?\d*(?:e[+-]?\d+)?|Infinity)/g;
+function linesClose(ours, ref) {
+    if (ours.length !== ref.length) return false;
+    for (var i = 0; i < ours.length; i++) {
+        if (ours[i].replace(NUM, '#') !== ref[i].replace(NUM, '#')) return false;
+        var a = ours[i].match(NUM) || [], b = ref[i].match(NUM) || [];
+        for (var k = 0; k < a.length; k++) {
+            var x = Number(a[k]), y = Number(b[k]);
+            if (!(Math.abs(x - y) <= 1e-7 * Math.max(1, Math.abs(y)))) return false;
+        }
+    }
+    return true;
 }
 
 var dir = path.join(__dirname, '..', 'tests', 'golden');
 var files = fs.readdirSync(dir).filter(function (f) { return /^lp_.*\.json$/.test(f); }).sort();
-var ncase = 0;
+var ncase = 0, nlines = 0;
 files.forEach(function (f) {
     var fx = JSON.parse(fs.readFileSync(path.join(dir, f), 'utf8'));
     if (fx.gen || fx.row_type === undefined) return;          // generated instances: Python tests
     fx.runs.forEach(function (run, r) {
-        var lp = buildLp(fx);
-        var ret = simplex(lp, smcp(run.opts));
+        var lp = buildLp(fx), lines = [];
+        var ret = simplex(lp, smcp(run.opts), function (s) { lines.push(s); });
         var tag = f + '#' + r;
+        if (run.lines && !run.lines.some(function (s) { return s[0] === '~'; })) {
+            var ref = run.lines.slice(2);
+            if (lp.it_cnt === run.it_cnt) assert.ok(linesClose(lines, ref), tag + ' lines ' + JSON.stringify([lines, ref]));
+            else assert.strictEqual(lines[lines.length - 1], ref[ref.length - 1], tag + ' last line');
+            nlines++;
+        }
         assert.strictEqual(ret, run.ret, tag + ' ret');
         assert.strictEqual(lp.pbs_stat, run.pbs_stat, tag + ' pbs_stat');
         assert.strictEqual(lp.dbs_stat, run.dbs_stat, tag + ' dbs_stat');
@@ -112,6 +135,7 @@ files.forEach(function (f) {
     });
 });
 assert.ok(ncase > 50, 'too few cases: ' + ncase);
+assert.ok(nlines > 50, 'too few line checks: ' + nlines);
 
 // MIP fixtures: root LP through solve_lp as above, then the native driver
 // through gk_core.iosDriver with the tree object ios_driver receives

@@ -223,9 +223,12 @@ function runLp(P, opts, traceCap) {
     });
     var parm = new glpk.SMCP(opts);
     var f0 = glpk.__cnt.factorize;
+    var lines = [];
+    glpk.glp_set_print_func(function (s) { lines.push(s); });
     var t0 = process.hrtime.bigint();
     var ret = glpk.glp_simplex(P, parm);
     var dt = Number(process.hrtime.bigint() - t0) / 1e9;
+    glpk.glp_set_print_func(function () {});
     glpk.__set_trace(null);
     var i, j, out = {opts: opts, ret: ret, pbs_stat: P.pbs_stat, dbs_stat: P.dbs_stat, obj_val: P.obj_val,
                      it_cnt: P.it_cnt, some: P.some, factorizations: glpk.__cnt.factorize - f0, seconds: dt};
@@ -235,6 +238,7 @@ function runLp(P, opts, traceCap) {
     for (i = 1; i <= P.m; i++) { out.row_prim.push(P.row[i].prim); out.row_dual.push(P.row[i].dual); }
     for (j = 1; j <= P.n; j++) { out.col_prim.push(P.col[j].prim); out.col_dual.push(P.col[j].dual); }
     out.trace = tr;
+    out.lines = lines;
     return out;
 }
 
