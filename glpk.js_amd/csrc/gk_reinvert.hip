@@ -287,20 +287,20 @@ static double *gjb_run2(hipStream_t s, double *M, double *M2, double *P, double 
 // (Q[c * k + r]); X_R = the pivot rows of P's bo columns (B x bo).
 // ---------------------------------------------------------------------------
 template <int NT, int RPT, int B>
-__global__ void __launch_bounds__(NT) k_gjc_panel(double *__restrict__ P, int k, int c0, int bo,
-                                                  double *__restrict__ Qm, int tg0, int *__restrict__ piv_step,
-                                                  int *__restrict__ piv, int *__restrict__ flag, double tiny,
-                                                  double *__restrict__ xr)
+__global__ void __launch_bounds__(NT) k_gjc_panel(double *__restrict__ P, int k, int c0, int bo, int tg0,
+                                                  int *__restrict__ piv_step, int *__restrict__ piv,
+                                                  int *__restrict__ flag, double tiny, double *__restrict__ xr)
 {
     constexpr int NW = NT / 64;
-    // per step and wave: the wave's best candidate and its row's B values,
+    // per step and wave: the wave's best key and its row's B values,
     // double-buffered by step parity (one barrier per step)
-    __shared__ Cand shc[2][NW];
+    __shared__ unsigned long long shk[2][NW];
     __shared__ double shr[2][NW][B];
     __shared__ int rsl[B];
-    if (*flag) return;
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const int b = min(B, bo - c0);
+    // the panel loads go out before the singularity flag of an earlier panel
+    // is read (a load tested before the others costs a memory round trip)
     double x[RPT][B];
     bool live[RPT];                      // row owned, and not pivoted yet
 #pragma unroll
@@ -311,13 +311,21 @@ __global__ void __launch_bounds__(NT) k_gjc_panel(double *__restrict__ P, int k,
 #pragma unroll
         for (int c = 0; c < B; ++c) x[j][c] = (r < k && c < b) ? P[(size_t)(c0 + c) * k + rc] : 0.0;
     }
+    if (*flag) return;
     // B steps, the active column always in slot 0: after a step the columns
     // rotate left by one (the transformed pivot column goes to slot B - 1),
     // so after B steps every column is back in its slot (static register
-    // indices, the step body a loop).  A step: every wave reduces its rows'
-    // candidates and publishes the best one with that row's B values; after
-    // the barrier every wave picks the winner among the NW published ones
-    // (largest |x|, lowest row on ties) and forms fr = x[rs] / pv itself.
+    // indices, the step body a loop).  The candidate of a row is one 64-bit
+    // key: the bits of |x| with the low 13 mantissa bits replaced by
+    // 8191 - row (k <= 8192), so one unsigned max picks the largest |x| and
+    // the lowest row among values equal to 2^-39 relative — partial pivoting
+    // up to a tie margin far below any pivot tolerance.  A step: every wave
+    // reduces its keys (DPP), its winning lane stores its row's B values in
+    // LDS; after the barrier every wave scans the NW keys and forms the
+    // multipliers itself.  Per-step cost is instruction issue (every wave
+    // repeats the choice), so the panel runs 8 waves, not 16 (tools/
+    // ubench_gjpanel.hip: 1.7 us per step at 8 waves x 8 rows against 2.6 us
+    // for 16 waves x 4 rows with shuffled row values).
 #pragma unroll 1
     for (int i = 0; i < B; ++i) {
         const int par = i & 1;
@@ -332,47 +340,40 @@ __global__ void __launch_bounds__(NT) k_gjc_panel(double *__restrict__ P, int k,
             }
             continue;
         }
-        Cand c; c.k1 = 0.0; c.k2 = 0.0; c.idx = 0; c.aux = 0;
+        unsigned long long key = 0;
         int jb = 0;
 #pragma unroll
         for (int j = 0; j < RPT; ++j) {
             const double v = fabs(x[j][0]);
-            if (live[j] && v > 0.0 && (c.idx == 0 || v > c.k1)) {   // rows ascend with j
-                c.k1 = v;
-                c.idx = tid + j * NT + 1;
-                jb = j;
+            const unsigned long long kk =
+                (live[j] && v > 0.0) ? ((dbits(v) & ~0x1fffull) | (unsigned long long)(0x1fff - (tid + j * NT))) : 0ull;
+            if (kk > key) { key = kk; jb = j; }
+        }
+        const unsigned long long wk = __ockl_wfred_max_u64(key);
+        const bool win = wk != 0 && key == wk;           // unique: the key holds the row
+#pragma unroll
+        for (int j = 0; j < RPT; ++j)
+            if (win && j == jb) {
+#pragma unroll
+                for (int cc = 0; cc < B; ++cc) shr[par][w][cc] = x[j][cc];
             }
-        }
-        const Cand wb = wave_best<0>(c);
-        // the winning lane's row values (lane = (idx - 1) % 64 within this wave)
-        const int src = wb.idx ? ((wb.idx - 1) & 63) : 0;
-        double rowv[B];
-#pragma unroll
-        for (int cc = 0; cc < B; ++cc) {
-            double mine = 0.0;
-#pragma unroll
-            for (int j = 0; j < RPT; ++j)
-                if (j == jb) mine = x[j][cc];
-            rowv[cc] = __shfl(mine, src);
-        }
-        if (lane == 0) {
-            shc[par][w] = wb;
-#pragma unroll
-            for (int cc = 0; cc < B; ++cc) shr[par][w][cc] = rowv[cc];
-        }
+        if (lane == 0) shk[par][w] = wk;
         __syncthreads();
-        Cand e;
-        if (lane < NW) e = shc[par][lane];
-        else { e.k1 = 0.0; e.k2 = 0.0; e.idx = 0; e.aux = 0; }
-        const Cand best = wave_best<0>(e);
-        if (best.idx == 0 || best.k1 <= tiny) {
-            if (tid == 0) *flag = 1 + tg0 + i;
-            return;                      // uniform: every thread saw the same best
+        unsigned long long bk = 0;
+        int ws = 0;
+#pragma unroll
+        for (int q = 0; q < NW; ++q) {
+            const unsigned long long e = shk[par][q];
+            if (e > bk) { bk = e; ws = q; }
         }
-        const int rs = best.idx - 1;
-        const int ws = (rs % NT) >> 6;   // the wave that published it
+        const double pv = shr[par][ws][0];
+        if (bk == 0 || fabs(pv) <= tiny) {
+            if (tid == 0) *flag = 1 + tg0 + i;
+            return;                      // uniform: every thread saw the same keys
+        }
+        const int rs = 0x1fff - (int)(bk & 0x1fff);
         if (tid == 0) rsl[i] = rs;
-        const double ipv = 1.0 / shr[par][ws][0];
+        const double ipv = 1.0 / pv;
         // the update, rotating left in place: slot 0 (the step's column)
         // goes to slot B - 1; the pivot row is overwritten afterwards by its
         // owner (no per-element select)
@@ -410,16 +411,14 @@ __global__ void __launch_bounds__(NT) k_gjc_panel(double *__restrict__ P, int k,
         const int kk = e / bo, c = e - kk * bo;
         xr[e] = (kk < b) ? P[(size_t)c * k + rsl[kk]] : 0.0;
     }
-    // the panel back into P, Q - E_R for the updates
+    // the panel back into P (k_gjc_inner forms Q = panel - E_R from it)
 #pragma unroll
     for (int j = 0; j < RPT; ++j) {
         const int r = tid + j * NT;
         if (r >= k) continue;
 #pragma unroll
-        for (int c = 0; c < B; ++c) {
+        for (int c = 0; c < B; ++c)
             if (c < b) P[(size_t)(c0 + c) * k + r] = x[j][c];
-            Qm[(size_t)c * k + r] = (c < b) ? x[j][c] - (r == rsl[c] ? 1.0 : 0.0) : 0.0;
-        }
     }
 }
 
@@ -427,7 +426,7 @@ __global__ void __launch_bounds__(NT) k_gjc_panel(double *__restrict__ P, int k,
 // inner panel [i0, i0 + B); one row per thread
 template <int B>
 __global__ void __launch_bounds__(256) k_gjc_inner(double *__restrict__ P, int bo, int i0,
-                                                   const double *__restrict__ Qm, const double *__restrict__ xr, int k,
+                                                   const int *__restrict__ pivp, const double *__restrict__ xr, int k,
                                                    const int *__restrict__ flag)
 {
     __shared__ double sx[B * GJ_BO];
@@ -435,9 +434,16 @@ __global__ void __launch_bounds__(256) k_gjc_inner(double *__restrict__ P, int b
     for (int e = threadIdx.x; e < B * bo; e += 256) sx[e] = xr[e];
     const int r = blockIdx.x * 256 + threadIdx.x;
     const int rc = min(r, k - 1);
+    const int bi = min(B, bo - i0);
+    // Q = the transformed panel columns minus E_R (the unit at the step's
+    // pivot row); a column past the panel's width contributes nothing
     double q[B];
 #pragma unroll
-    for (int kk = 0; kk < B; ++kk) q[kk] = Qm[(size_t)kk * k + rc];
+    for (int kk = 0; kk < B; ++kk) {
+        const double pk = P[(size_t)(i0 + min(kk, bi - 1)) * k + rc];
+        const int rp = pivp[min(kk, bi - 1)];
+        q[kk] = kk < bi ? pk - (rc == rp ? 1.0 : 0.0) : 0.0;
+    }
     __syncthreads();
     // 8 columns per thread (blockIdx.y), their loads issued together: one
     // memory round trip per thread
@@ -502,11 +508,11 @@ static double *gjc_run(hipStream_t s, double *M, double *M2, double *P, double *
         const int bo = std::min(GJ_BO, k - T0);
         hipLaunchKernelGGL(k_gjc_copy<1>, gt, dim3(256), 0, s, M, P, k, T0, bo, flag);
         for (int i0 = 0; i0 < bo; i0 += B) {
-            hipLaunchKernelGGL((k_gjc_panel<NT, RPT, B>), dim3(1), dim3(NT), 0, s, P, k, i0, bo, Qm, T0 + i0,
-                               piv_step, piv, flag, tiny, xr);
+            hipLaunchKernelGGL((k_gjc_panel<NT, RPT, B>), dim3(1), dim3(NT), 0, s, P, k, i0, bo, T0 + i0, piv_step,
+                               piv, flag, tiny, xr);
             if (bo > B)
-                hipLaunchKernelGGL((k_gjc_inner<B>), dim3(gr.x, (bo + 7) / 8), dim3(256), 0, s, P, bo, i0, Qm, xr, k,
-                                   flag);
+                hipLaunchKernelGGL((k_gjc_inner<B>), dim3(gr.x, (bo + 7) / 8), dim3(256), 0, s, P, bo, i0,
+                                   piv + T0 + i0, xr, k, flag);
         }
         if (k > bo)
             hipLaunchKernelGGL((k_gjb_update<GJ_BO, 1, 1>), g, dim3(256), 0, s, M, M2, P, k, piv + T0, k, T0, flag);
@@ -554,9 +560,9 @@ double *gauss_jordan_blocked(hipStream_t s, double *X, double *scratch, int k, i
         if (k <= 4096) return gjb_run2<1024, 4, 8>(s, X, M2, P, Qm, xr, k, piv_step, piv, flag, tiny);
         return gjb_run2<1024, 8, 4>(s, X, M2, P, Qm, xr, k, piv_step, piv, flag, tiny);
     }
-    if (k <= 1024) return gjc_run<1024, 1, 16>(s, X, M2, P, Qm, xr, k, piv_step, piv, flag, tiny);
-    if (k <= 2048) return gjc_run<1024, 2, 16>(s, X, M2, P, Qm, xr, k, piv_step, piv, flag, tiny);
-    if (k <= 4096) return gjc_run<1024, 4, 8>(s, X, M2, P, Qm, xr, k, piv_step, piv, flag, tiny);
+    if (k <= 1024) return gjc_run<512, 2, 16>(s, X, M2, P, Qm, xr, k, piv_step, piv, flag, tiny);
+    if (k <= 2048) return gjc_run<512, 4, 16>(s, X, M2, P, Qm, xr, k, piv_step, piv, flag, tiny);
+    if (k <= 4096) return gjc_run<512, 8, 8>(s, X, M2, P, Qm, xr, k, piv_step, piv, flag, tiny);
     return gjc_run<1024, 8, 4>(s, X, M2, P, Qm, xr, k, piv_step, piv, flag, tiny);
 }
 
