@@ -102,6 +102,9 @@ def main():
     __graft_entry__.build_hip()
     __graft_entry__.load_package()
     from glpk_js_amd import gk, problems
+    # the solver's printed lines (glp_simplex's xprintf) go to stderr: stdout
+    # carries the one JSON line
+    gk.glp_set_print_func(lambda s: print(s, file=sys.stderr))
 
     def barrier():
         if world > 1:
