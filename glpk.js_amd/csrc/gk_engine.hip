@@ -2053,6 +2053,63 @@ int gk_spx_node(gk_ctx *ctx, gk_lp *lp, gk_bfd *bfd, const gk_smcp *parm)
 }
 }  // namespace gk
 
+extern "C" int gk_bfd_eval_tab_rows(gk_bfd *f, gk_lp *lp, int nk, const int *k, double *alfa, int flags)
+{
+    try {
+        ABI_REQUIRE(f && lp && (nk == 0 || (k && alfa)), "glp_eval_tab_row: null argument");
+        ABI_REQUIRE(lp->m > 0 && lp->n > 0 && nk >= 0, "glp_eval_tab_row: m = %d, n = %d, nk = %d", lp->m, lp->n, nk);
+        ABI_REQUIRE(f->valid && f->m == lp->m, "glp_eval_tab_row: basis factorization does not exist");
+        if (nk == 0) return 0;
+        HIPCHK(hipSetDevice(f->ctx->device));
+        const int m = lp->m, n = lp->n;
+        // basis positions (glp_get_row_bind / glp_get_col_bind) and the SB
+        // entry of each requested row
+        std::vector<int> bind(m + n + 1, 0), pos(nk);
+        for (int i = 1; i <= m; i++) {
+            ABI_REQUIRE(1 <= lp->head[i] && lp->head[i] <= m + n, "glp_eval_tab_row: head[%d] out of range", i);
+            bind[lp->head[i]] = i;
+        }
+        std::vector<double> rs(nk), cs(n), aux(m);
+        for (int t = 0; t < nk; t++) {
+            const int kk = k[t];
+            ABI_REQUIRE(1 <= kk && kk <= m + n, "glp_eval_tab_row: k = %d; variable number out of range", kk);
+            ABI_REQUIRE(bind[kk] != 0, "glp_eval_tab_row: k = %d; variable must be basic", kk);
+            pos[t] = bind[kk] - 1;
+            rs[t] = kk <= m ? 1.0 / lp->rii[kk] : lp->sjj[kk - m];
+        }
+        for (int j = 1; j <= n; j++) cs[j - 1] = lp->col_stat[j] == BS ? 0.0 : 1.0 / lp->sjj[j];
+        for (int i = 1; i <= m; i++) aux[i - 1] = lp->row_stat[i] == BS ? 0.0 : -lp->rii[i];
+        if (!f->eng) f->eng = new Engine;
+        engine_upload_matrix(f, lp);
+        hipStream_t s = f->ctx->stream;
+        const size_t ldo = (size_t)m + n;
+        DBuf<double> G, sc, out;
+        DBuf<int> dpos;
+        struct Rel {
+            DBuf<double> &a, &b, &c;
+            DBuf<int> &d;
+            ~Rel() { a.release(); b.release(); c.release(); d.release(); }
+        } rel{G, sc, out, dpos};
+        G.ensure((size_t)nk * m);
+        sc.ensure((size_t)nk + n + m);
+        out.ensure((size_t)nk * ldo);
+        dpos.ensure(nk);
+        HIPCHK(hipMemcpyAsync(dpos.p, pos.data(), nk * sizeof(int), hipMemcpyHostToDevice, s));
+        HIPCHK(hipMemcpyAsync(sc.p, rs.data(), nk * sizeof(double), hipMemcpyHostToDevice, s));
+        HIPCHK(hipMemcpyAsync(sc.p + nk, cs.data(), n * sizeof(double), hipMemcpyHostToDevice, s));
+        HIPCHK(hipMemcpyAsync(sc.p + nk + n, aux.data(), m * sizeof(double), hipMemcpyHostToDevice, s));
+        tab_rows(s, f->Binv.p, f->ldb, f->eng->mat(), nk, dpos.p, G.p, sc.p + nk + n, sc.p + nk, sc.p, out.p,
+                 (flags & 1) ? 0 : 1);
+        HIPCHK(hipGetLastError());
+        HIPCHK(hipMemcpyAsync(alfa, out.p, (size_t)nk * ldo * sizeof(double), hipMemcpyDeviceToHost, s));
+        HIPCHK(hipStreamSynchronize(s));
+        return 0;
+    } catch (const AbiError &e) {
+        g_err = e.msg;
+        return GK_EABI;
+    }
+}
+
 extern "C" double gk_bfd_time_kernel(gk_bfd *f, int which, int reps, double *bytes)
 {
     try {

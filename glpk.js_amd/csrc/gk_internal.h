@@ -107,6 +107,9 @@ void colpass(hipStream_t s, const MatDev &A, int mode, int off, int cnt, const i
 
 // y = base - A w  over structural columns (w dense over columns, zeros skipped);
 // used for sums of (I|-A) columns (slack parts are added into base by the caller)
+// glp_eval_tab_row for a batch (gk_tabrow.hip): out[t * (m + n) + k - 1]
+void tab_rows(hipStream_t s, const double *Binv, int ldb, const MatDev &A, int nk, const int *pos, double *G,
+              const double *aux, const double *cs, const double *rs, double *out, int use_mfma);
 void aprod_neg(hipStream_t s, const MatDev &A, const double *w, const double *base, double *y,
                double *partial, size_t partial_cap);
 

@@ -106,7 +106,8 @@ EXPORTS = ["gk_abi_version", "gk_device_count", "gk_ctx_create", "gk_ctx_destroy
            "gk_bfd_create", "gk_bfd_destroy", "gk_bfd_set_parm", "gk_bfd_factorize", "gk_bfd_factorize_csc",
            "gk_bfd_ftran", "gk_bfd_btran", "gk_bfd_update", "gk_bfd_get_count", "gk_bfd_valid",
            "gk_spx_primal", "gk_spx_dual", "gk_bfd_last_stats", "gk_bfd_profile", "gk_ios_driver",
-           "gk_scale_prob", "gk_scale_prob_timed", "gk_adv_basis", "gk_bfd_set_report"]
+           "gk_scale_prob", "gk_scale_prob_timed", "gk_adv_basis", "gk_bfd_set_report",
+           "gk_bfd_eval_tab_rows"]
 
 # gk_report_fn (glpk_mi355x.h): one progress line or termination message of
 # a gk_spx_* call, in the order the reference prints them
@@ -168,6 +169,8 @@ def load_library(path: str = LIB_PATH):
     L.gk_adv_basis.restype = C.c_int
     L.gk_bfd_set_report.argtypes = [P, REPORT_FN, P]
     L.gk_bfd_set_report.restype = None
+    L.gk_bfd_eval_tab_rows.argtypes = [P, P, C.c_int, P, P, C.c_int]
+    L.gk_bfd_eval_tab_rows.restype = C.c_int
     _lib = L
     return L
 
@@ -398,6 +401,23 @@ class GkProblem:
         self._take(lp)
         return ret
 
+    def eval_tab_rows(self, ks, per_row: bool = False) -> np.ndarray:
+        """Rows of the simplex tableau of the basic variables ks (1..m+n) on
+        the current factor, one GEMM for the batch (gk_bfd_eval_tab_rows;
+        per_row: the CSC path): a (len(ks), m + n) array, column k - 1 =
+        alfa of variable k (0 for basic variables), glp_eval_tab_row's
+        values (glpapi12.js:401)."""
+        ks = np.ascontiguousarray(ks, dtype=np.int32)
+        out = np.zeros((len(ks), self.m + self.n))
+        if len(ks) == 0:
+            return out
+        lp = self._lp_struct()
+        ret = self.L.gk_bfd_eval_tab_rows(self.bfd, C.byref(lp), len(ks), ks.ctypes.data_as(C.c_void_p),
+                                          out.ctypes.data_as(C.c_void_p), 1 if per_row else 0)
+        if ret != 0:
+            raise GkError(_err(self.L))
+        return out
+
     def time_kernel(self, which: int, reps: int = 10):
         """(ms per launch, algorithmic bytes per launch) of one engine kernel,
         timed with HIP events on the engine stream (gk_bfd_time_kernel)."""
@@ -503,6 +523,18 @@ def _trivial_lp(P: GkProblem, parm: Smcp):
             _xprintf("PROBLEM HAS UNBOUNDED SOLUTION")
         else:
             _xprintf("PROBLEM HAS NO DUAL FEASIBLE SOLUTION")
+
+
+def glp_eval_tab_row(P: GkProblem, k: int):
+    """glp_eval_tab_row (glpapi12.js:401): the non-zeros of the tableau row of
+    basic variable k as (ind, val) lists, variables in ascending order."""
+    if not (P.m == 0 or P.valid):
+        raise GkError("glp_eval_tab_row: basis factorization does not exist")
+    if not (1 <= k <= P.m + P.n):
+        raise GkError(f"glp_eval_tab_row: k = {k}; variable number out of range")
+    row = P.eval_tab_rows([k])[0]
+    ind = np.nonzero(row)[0]
+    return (ind + 1).tolist(), row[ind].tolist()
 
 
 def glp_simplex(P: GkProblem, parm: Smcp | None = None) -> int:

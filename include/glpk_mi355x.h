@@ -212,6 +212,18 @@ int gk_bfd_trace(gk_bfd *bfd, unsigned long long *out, size_t cnt);
  * *bytes receives the algorithmic bytes one launch must move. */
 double gk_bfd_time_kernel(gk_bfd *bfd, int which, int reps, double *bytes);
 
+/* ---- tableau rows (glp_eval_tab_row, glpapi12.js:401) --------------------
+ * Rows of the simplex tableau of the basic variables k[0..nk) (1..m+n, each
+ * basic in lp->head) on the current factor of bfd, all in one pass:
+ *   alfa[t * (m + n) + j - 1] = alfa_{k_t, j} for every non-basic variable j
+ * (rho' A_j for a structural, -rho_j for an auxiliary, rho = glp_btran(e_i),
+ * the problem's scaling applied as glp_btran does), 0 for basic j.  The
+ * reference returns the non-zeros as (ind, val) lists; the host compacts.
+ * On dense A the batch is one GEMM on the matrix cores; flags & 1 forces the
+ * per-row CSC path.  A is taken from lp (uploaded when lp->a_version is new).
+ * 0 | GK_EABI (no valid factor, k out of range or non-basic). */
+int gk_bfd_eval_tab_rows(gk_bfd *bfd, gk_lp *lp, int nk, const int *k, double *alfa, int flags);
+
 /* ---- branch and bound (glpios03.js, glpapi09.js) -------------------------
  * gk_ios_driver serves glp_intopt with cb_func == null, presolve off and no
  * cut generators.  Every br_tech (FFV, LFV, MFV, DTH, PCH; glpios09.js:1) and

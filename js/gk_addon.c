@@ -80,6 +80,20 @@ static void *ta(napi_env env, napi_value v)
     return data;
 }
 
+/* the same with its element count */
+static void *ta_len(napi_env env, napi_value v, size_t *len)
+{
+    bool is = false;
+    *len = 0;
+    if (napi_is_typedarray(env, v, &is) != napi_ok || !is) return NULL;
+    napi_typedarray_type type;
+    size_t off;
+    void *data;
+    napi_value ab;
+    if (napi_get_typedarray_info(env, v, &type, len, &data, &ab, &off) != napi_ok) return NULL;
+    return data;
+}
+
 static napi_value prop(napi_env env, napi_value obj, const char *name)
 {
     napi_value v;
@@ -507,6 +521,28 @@ static napi_value js_adv_basis(napi_env env, napi_callback_info info)
     return mk_int(env, ret);
 }
 
+// evalTabRows(bfd, L, ks Int32Array, out Float64Array (nk * (m + n)), flags):
+// gk_bfd_eval_tab_rows (glp_eval_tab_row for a batch, glpapi12.js:401)
+static napi_value js_eval_tab_rows(napi_env env, napi_callback_info info)
+{
+    napi_value argv[5];
+    if (!get_args(env, info, 5, argv)) return NULL;
+    gk_bfd *b = (gk_bfd *)get_ext(env, argv[0]);
+    gk_lp lp;
+    if (!fill_lp(env, argv[1], &lp)) return NULL;
+    size_t nk = 0, nout = 0;
+    const int *ks = (const int *)ta_len(env, argv[2], &nk);
+    double *out = (double *)ta_len(env, argv[3], &nout);
+    int flags = 0;
+    CHECK(napi_get_value_int32(env, argv[4], &flags));
+    if (!ks || !out || nout < nk * (size_t)(lp.m + lp.n)) {
+        napi_throw_type_error(env, NULL, "evalTabRows: Int32Array ks and Float64Array nk * (m + n) expected");
+        return NULL;
+    }
+    if (gk_bfd_eval_tab_rows(b, &lp, (int)nk, ks, out, flags) == GK_EABI) return throw_gk(env, "eval_tab_rows");
+    return mk_int(env, 0);
+}
+
 #define FN(name, f) { name, NULL, f, NULL, NULL, NULL, napi_enumerable, NULL }
 
 static napi_value init(napi_env env, napi_value exports)
@@ -517,7 +553,7 @@ static napi_value init(napi_env env, napi_value exports)
         FN("bfdFactorizeCsc", js_bfd_factorize_csc), FN("bfdFtran", js_bfd_ftran), FN("bfdBtran", js_bfd_btran),
         FN("bfdUpdate", js_bfd_update), FN("bfdGetCount", js_bfd_get_count), FN("bfdValid", js_bfd_valid),
         FN("spx", js_spx), FN("ios", js_ios), FN("stats", js_stats), FN("scale", js_scale),
-        FN("advBasis", js_adv_basis),
+        FN("advBasis", js_adv_basis), FN("evalTabRows", js_eval_tab_rows),
     };
     napi_define_properties(env, exports, sizeof d / sizeof d[0], d);
     return exports;

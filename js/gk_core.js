@@ -273,3 +273,18 @@ function advBasis(lp) {
     return {size: size, row_stat: rs, col_stat: cs};
 }
 module.exports.advBasis = advBasis;
+
+// glp_eval_tab_row (glpapi12.js:401) for a batch of basic variables ks on
+// the current factor: one Float64Array row of m + n entries per k (index
+// j - 1 = alfa of variable j, 0 for basic variables), one device GEMM for
+// the batch (gk_bfd_eval_tab_rows; perRow: the per-row device path)
+function evalTabRows(lp, ks, perRow) {
+    if (!(lp.m == 0 || lp.valid) || lp.bfd === null) throw new Error('glp_eval_tab_row: basis factorization does not exist');
+    var g = arrays(lp), L = marshal(lp, g), w = lp.m + lp.n;
+    var out = new Float64Array(ks.length * w);
+    addon.evalTabRows(lp.bfd.gk, L, Int32Array.from(ks), out, perRow ? 1 : 0);
+    var rows = [];
+    for (var t = 0; t < ks.length; t++) rows.push(out.subarray(t * w, (t + 1) * w));
+    return rows;
+}
+module.exports.evalTabRows = evalTabRows;

@@ -7,7 +7,8 @@ var path = require('path');
 var core = require(path.join(__dirname, 'gk_core.js'));
 
 var names = ['create', 'deviceCount', 'abiVersion', 'lastError', 'bfdCreate', 'bfdSetParm', 'bfdFactorizeCsc',
-             'bfdFtran', 'bfdBtran', 'bfdUpdate', 'bfdGetCount', 'bfdValid', 'spx', 'ios', 'stats'];
+             'bfdFtran', 'bfdBtran', 'bfdUpdate', 'bfdGetCount', 'bfdValid', 'spx', 'ios', 'stats', 'advBasis',
+             'evalTabRows'];
 names.forEach(function (k) { assert.strictEqual(typeof core.addon[k], 'function', k); });
 assert.strictEqual(core.addon.abiVersion(), 3);
 

@@ -484,3 +484,33 @@ advCase('c2s', function () { return genC2s(821, 1571, 7, 42); });
 });
 advCase('mixbig1', function () { return genMix(300, 50, 80, 0.15, false, true, false); });
 advCase('nocols', function () { var P = newProb(); glpk.glp_add_rows(P, 3); return P; });
+
+// ---- glp_eval_tab_row (glpapi12.js:401) on optimal bases -------------------
+// the problem (after scaling, when asked: rii / sjj in the dump), the basis
+// glp_simplex left, and the tableau row of every basic variable (up to 48)
+function tabCase(name, mk, scale) {
+    if (ONLY && ('tab_' + name).indexOf(ONLY) !== 0) return;
+    var P = mk();
+    if (scale) glpk.glp_scale_prob(P, scale);
+    var ret = glpk.glp_simplex(P, new glpk.SMCP({meth: glpk.GLP_DUAL, presolve: glpk.GLP_OFF}));
+    var d = dumpProb(P, null);
+    d.name = name; d.kind = 'tab'; d.simplex_ret = ret;
+    var b = snapshotBasis(P), rows = [], k;
+    d.row_stat = b.row_stat; d.col_stat = b.col_stat;
+    for (k = 1; k <= P.m + P.n && rows.length < 48; k++) {
+        var st = k <= P.m ? P.row[k].stat : P.col[k - P.m].stat;
+        if (st !== glpk.GLP_BS) continue;
+        var ind = new Int32Array(1 + P.n), val = new Float64Array(1 + P.n);
+        var len = glpk.glp_eval_tab_row(P, k, ind, val);
+        rows.push({k: k, ind: Array.from(ind.slice(1, len + 1)), val: Array.from(val.slice(1, len + 1))});
+    }
+    d.tab_rows = rows;
+    fs.writeFileSync(path.join(OUT, 'tab_' + name + '.json'), JSON.stringify(d));
+    console.log('wrote tab', name, d.m + 'x' + d.n, 'ret', ret, rows.length, 'rows');
+}
+tabCase('test', function () { return readLp('test.lpt'); }, 0);
+tabCase('gap', function () { return readLp('gap.lpt'); }, 0);
+tabCase('dense_64x256', function () { return genDense(64, 256, 42); }, 0);
+tabCase('dense_64x256_scaled', function () { return genDense(64, 256, 42); }, glpk.GLP_SF_GM | glpk.GLP_SF_EQ | glpk.GLP_SF_2N);
+tabCase('mix14_scaled', function () { return genMix(14, 22, 38, 0.35, false, true); }, glpk.GLP_SF_GM | glpk.GLP_SF_EQ);
+tabCase('c2s_scaled', function () { return genC2s(821, 1571, 7, 42); }, glpk.GLP_SF_GM | glpk.GLP_SF_EQ);
