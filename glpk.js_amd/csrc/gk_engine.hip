@@ -99,7 +99,19 @@ struct gk_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
     int wall_khz = 100000;              // device wall clock (wall_clock64) rate
+    // the owner's reference plus one per factor handle: a host whose
+    // finalizers run in any order (N-API at exit, Python's GC) may destroy
+    // the context before its factors, which still need it
+    int refs = 1;
 };
+
+static void ctx_unref(gk_ctx *ctx)
+{
+    if (--ctx->refs > 0) return;
+    (void)hipSetDevice(ctx->device);
+    if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
+    delete ctx;
+}
 
 // a captured device batch of dual pivots: replayed while the device
 // pointers, the launch plan and the batch length are unchanged
@@ -1752,9 +1764,7 @@ gk_ctx *gk_ctx_create(int device)
 void gk_ctx_destroy(gk_ctx *ctx)
 {
     if (!ctx) return;
-    (void)hipSetDevice(ctx->device);
-    if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
-    delete ctx;
+    ctx_unref(ctx);
 }
 
 gk_bfd *gk_bfd_create(gk_ctx *ctx)
@@ -1762,6 +1772,7 @@ gk_bfd *gk_bfd_create(gk_ctx *ctx)
     if (!ctx) { set_err("gk_bfd_create: null context"); return nullptr; }
     gk_bfd *f = new gk_bfd;
     f->ctx = ctx;
+    ctx->refs++;
     // glp_get_bfcp defaults (glpapi12.js:111-121)
     f->parm.type = 1; f->parm.lu_size = 0; f->parm.piv_tol = 0.10; f->parm.piv_lim = 4; f->parm.suhl = 1;
     f->parm.eps_tol = 1e-15; f->parm.max_gro = 1e10; f->parm.nfs_max = 100; f->parm.upd_tol = 1e-6;
@@ -1777,7 +1788,9 @@ void gk_bfd_destroy(gk_bfd *f)
     f->Binv.release(); f->C.release(); f->X.release(); f->Y.release(); f->CinvR.release(); f->BS.release();
     f->G.release(); f->vecx.release(); f->vecy.release(); f->partial.release(); f->idx_i.release();
     f->piv_step.release(); f->piv.release(); f->flag.release(); f->bptr.release(); f->brow.release(); f->bval.release();
+    gk_ctx *ctx = f->ctx;
     delete f;
+    ctx_unref(ctx);
 }
 
 // the checks of glp_set_bfcp (glpapi12.js:133-166), messages included (the
@@ -2013,7 +2026,11 @@ static int spx_entry(gk_ctx *ctx, gk_lp *lp, gk_bfd *f, const gk_smcp *parm, int
         ABI_REQUIRE(lp->m > 0 && lp->n > 0, "spx: m = %d, n = %d; invalid dimensions", lp->m, lp->n);
         ABI_REQUIRE(lp->m <= 65535, "spx: m = %d exceeds this build's grid limit 65535", lp->m);
         HIPCHK(hipSetDevice(ctx->device));
-        f->ctx = ctx;
+        if (f->ctx != ctx) {                  // the factor moves to the caller's context
+            ctx->refs++;
+            ctx_unref(f->ctx);
+            f->ctx = ctx;
+        }
         const double t0 = now_s();
         f->stats = gk_spx_stats{};
         bfd_prepare(f, lp->m);

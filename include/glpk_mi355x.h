@@ -51,7 +51,7 @@ typedef struct gk_bfd gk_bfd; /* replaces lp.bfd: device-resident factor   */
 int         gk_abi_version(void);
 int         gk_device_count(void);
 gk_ctx     *gk_ctx_create(int device);          /* NULL on failure          */
-void        gk_ctx_destroy(gk_ctx *ctx);
+void        gk_ctx_destroy(gk_ctx *ctx);       /* factors made on it keep it alive until they are destroyed */
 /* profiling aid: enqueue an empty kernel (k_gk_mark) on the context stream,
  * so that a kernel trace can be windowed on a region of the host program */
 int         gk_ctx_mark(gk_ctx *ctx, int tag);
