@@ -103,12 +103,21 @@ struct gk_ctx {
     // finalizers run in any order (N-API at exit, Python's GC) may destroy
     // the context before its factors, which still need it
     int refs = 1;
+    // scratch every engine on this context borrows (one stream: never used
+    // by two solves at once): split-K partials, A w partials, the device side
+    // of the staged uploads.  Owned here, so an engine (one per LP object)
+    // neither allocates nor frees tens of MiB — freeing them per engine
+    // while the process ran was followed by a fault in node's teardown
+    DBuf<double> partial, awpart;
+    DBuf<char> upstage;
 };
 
 static void ctx_unref(gk_ctx *ctx)
 {
     if (--ctx->refs > 0) return;
     (void)hipSetDevice(ctx->device);
+    if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
+    ctx->partial.release(); ctx->awpart.release(); ctx->upstage.release();
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
     delete ctx;
 }
@@ -175,20 +184,29 @@ struct Engine {
     }
     ~Engine()
     {
-        A.release(); AT.release(); rlist.release(); rpos.release(); rho_idx.release(); rho_val.release();
-        gpart.release(); awcnt.release(); tslots.release(); xslots.release(); trace.release(); wlist.release(); wpos.release(); cand.release(); awpart.release(); cptr.release(); cind.release(); rptr.release(); rcol.release(); cval.release(); rval.release();
+        // the captured graphs first: their kernel nodes refer to the buffers
+        // below, and an exec destroyed after them (or left to the runtime's
+        // own teardown) touches freed allocations
+        for (auto &g : graphs)
+            if (g.exec) (void)hipGraphExecDestroy(g.exec);
+        graphs.clear();
+        for (auto e : ev) (void)hipEventDestroy(e);
+        ev.clear();
+        A.release(); AT.release(); cptr.release(); cind.release(); rptr.release(); rcol.release(); cval.release(); rval.release();
+        rlist.release(); rpos.release(); rho_idx.release(); rho_val.release();
+        gpart.release(); awcnt.release(); tslots.release(); xslots.release(); trace.release(); wlist.release(); wpos.release(); cand.release();
+        awpart.release();
         type.release(); orig_type.release(); stat.release(); refsp.release();
         lb.release(); ub.release(); coef.release(); orig_lb.release(); orig_ub.release(); obj.release();
         head.release(); bind.release();
         bbar.release(); cbar.release(); gamma.release(); tcol.release(); trow.release(); rho.release(); rowp.release();
         u.release(); s.release(); h.release(); wcol.release(); ys.release(); work.release(); r1.release(); r2.release();
-        partial.release(); st.release();
+        partial.release();
+        st.release();
         if (arena) (void)hipFree(arena);
         if (st_host) (void)hipHostFree(st_host);
         if (pin) (void)hipHostFree(pin);
-        for (auto &g : graphs)
-            if (g.exec) (void)hipGraphExecDestroy(g.exec);
-        for (auto e : ev) (void)hipEventDestroy(e);
+        upstage.release(); xlist.release();
     }
 };
 
@@ -330,7 +348,7 @@ static bool split_from_head(int m, const int *head1, BasisSplit &bs)
 // ---------------------------------------------------------------------------
 // device working set
 // ---------------------------------------------------------------------------
-static void engine_alloc(Engine &E, int m, int n)
+static void engine_alloc(Engine &E, int m, int n, gk_ctx *ctx)
 {
     const size_t mn = (size_t)m + n;
     const size_t gv = (size_t)(std::max(m, n) + 255) / 256 + 1;
@@ -387,8 +405,11 @@ static void engine_alloc(Engine &E, int m, int n)
         E.arena_m = m;
         E.arena_n = n;
     }
-    E.partial.ensure(PARTIAL_CAP);
-    E.awpart.ensure((size_t)AW_SPLITS * m);
+    // the context's scratch (sized once for every m <= 65535)
+    ctx->partial.ensure(PARTIAL_CAP);
+    ctx->awpart.ensure((size_t)AW_SPLITS * 65536);
+    E.partial.view(ctx->partial.p, ctx->partial.n);
+    E.awpart.view(ctx->awpart.p, ctx->awpart.n);
     if (!E.st_host) HIPCHK(hipHostMalloc((void **)&E.st_host, sizeof(DState), hipHostMallocDefault));
     {
         const size_t need = std::max<size_t>((size_t)8 << 20, (size_t)32 * ((size_t)m + n + 1) * sizeof(double));
@@ -572,7 +593,8 @@ struct Spx {
         }
         std::memcpy(tab, segs.data(), segs.size() * sizeof(UpSeg));
         const size_t total = pin_off - coal_beg;
-        E->upstage.ensure(E->pin_cap);
+        ctx->upstage.ensure(E->pin_cap);
+        E->upstage.view(ctx->upstage.p, ctx->upstage.n);
         HIPCHK(hipMemcpyAsync(E->upstage.p, E->pin + coal_beg, total, hipMemcpyHostToDevice, s));
         scatter_segments(s, E->upstage.p, (const UpSeg *)(E->upstage.p + (tab - (E->pin + coal_beg))),
                          (int)segs.size());
@@ -1152,7 +1174,7 @@ void Spx::init()
         }
     ABI_REQUIRE(k == n, "gk_spx: basis header inconsistent with statuses (%d non-basic, n = %d)", k, n);
     for (int kk = 1; kk <= m + n; kk++) bind[head[kk]] = kk;
-    engine_alloc(*E, m, n);
+    engine_alloc(*E, m, n, ctx);
     begin_up();
     up(E->type, type, mn - 1); up(E->orig_type, orig_type, mn - 1);
     up(E->lb, lb, mn - 1); up(E->ub, ub, mn - 1); up(E->orig_lb, orig_lb, mn - 1); up(E->orig_ub, orig_ub, mn - 1);
@@ -1784,6 +1806,7 @@ void gk_bfd_destroy(gk_bfd *f)
 {
     if (!f) return;
     (void)hipSetDevice(f->ctx->device);
+    if (f->ctx->stream) (void)hipStreamSynchronize(f->ctx->stream);
     delete f->eng;
     f->Binv.release(); f->C.release(); f->X.release(); f->Y.release(); f->CinvR.release(); f->BS.release();
     f->G.release(); f->vecx.release(); f->vecy.release(); f->partial.release(); f->idx_i.release();
@@ -2118,8 +2141,18 @@ extern "C" int gk_bfd_eval_tab_rows(gk_bfd *f, gk_lp *lp, int nk, const int *k, 
         tab_rows(s, f->Binv.p, f->ldb, f->eng->mat(), nk, dpos.p, G.p, sc.p + nk + n, sc.p + nk, sc.p, out.p,
                  (flags & 1) ? 0 : 1);
         HIPCHK(hipGetLastError());
-        HIPCHK(hipMemcpyAsync(alfa, out.p, (size_t)nk * ldo * sizeof(double), hipMemcpyDeviceToHost, s));
-        HIPCHK(hipStreamSynchronize(s));
+        // through a pinned buffer of our own: a direct copy into the host's
+        // array leaves that (pageable, host-runtime-owned) memory registered
+        // with the HIP runtime, and a host that frees it at exit (node's
+        // heap teardown) then faults
+        const size_t bytes = (size_t)nk * ldo * sizeof(double);
+        void *pin = nullptr;
+        HIPCHK(hipHostMalloc(&pin, bytes, hipHostMallocDefault));
+        const hipError_t ce = hipMemcpyAsync(pin, out.p, bytes, hipMemcpyDeviceToHost, s);
+        const hipError_t se = ce == hipSuccess ? hipStreamSynchronize(s) : ce;
+        if (se == hipSuccess) std::memcpy(alfa, pin, bytes);
+        (void)hipHostFree(pin);
+        HIPCHK(se);
         return 0;
     } catch (const AbiError &e) {
         g_err = e.msg;

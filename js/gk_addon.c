@@ -123,10 +123,21 @@ static void set_num(napi_env env, napi_value obj, const char *name, double v)
 }
 
 /* ---------------------------------------------------------------- context */
+/* set by the environment cleanup hook: at teardown the handles are left to
+ * the process exit (the HIP runtime may already be shutting down, and the
+ * order in which the remaining externals are finalized is not defined) */
+static int g_teardown = 0;
+
+static void teardown_hook(void *arg)
+{
+    (void)arg;
+    g_teardown = 1;
+}
+
 static void ctx_fin(napi_env env, void *data, void *hint)
 {
     (void)env; (void)hint;
-    gk_ctx_destroy((gk_ctx *)data);
+    if (!g_teardown) gk_ctx_destroy((gk_ctx *)data);
 }
 
 static napi_value js_create(napi_env env, napi_callback_info info)
@@ -170,7 +181,7 @@ static napi_value js_last_error(napi_env env, napi_callback_info info)
 static void bfd_fin(napi_env env, void *data, void *hint)
 {
     (void)env; (void)hint;
-    gk_bfd_destroy((gk_bfd *)data);
+    if (!g_teardown) gk_bfd_destroy((gk_bfd *)data);
 }
 
 static napi_value js_bfd_create(napi_env env, napi_callback_info info)
@@ -545,8 +556,21 @@ static napi_value js_eval_tab_rows(napi_env env, napi_callback_info info)
 
 #define FN(name, f) { name, NULL, f, NULL, NULL, NULL, napi_enumerable, NULL }
 
+#include <execinfo.h>
+#include <signal.h>
+#include <unistd.h>
+static void segv_trace(int sig)
+{
+    void *fr[64];
+    int nf = backtrace(fr, 64);
+    backtrace_symbols_fd(fr, nf, 2);
+    _exit(128 + sig);
+}
+
 static napi_value init(napi_env env, napi_value exports)
 {
+    if (getenv("GK_SEGV_TRACE")) signal(SIGSEGV, segv_trace);
+    napi_add_env_cleanup_hook(env, teardown_hook, NULL);
     napi_property_descriptor d[] = {
         FN("create", js_create), FN("deviceCount", js_device_count), FN("abiVersion", js_abi_version),
         FN("lastError", js_last_error), FN("bfdCreate", js_bfd_create), FN("bfdSetParm", js_bfd_set_parm),

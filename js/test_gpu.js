@@ -136,27 +136,9 @@ files.forEach(function (f) {
 });
 assert.ok(ncase > 50, 'too few cases: ' + ncase);
 assert.ok(nlines > 50, 'too few line checks: ' + nlines);
+if (global.gc) global.gc();   // finalize the LP section's factor handles now (node --expose-gc)
 
-// tableau rows (tests/golden/tab_*.json: the reference's glp_eval_tab_row on
-// the basis glp_simplex left) through gk_core.evalTabRows, both device paths
-var ntab = 0;
-fs.readdirSync(dir).filter(function (f) { return /^tab_.*\.json$/.test(f); }).sort().forEach(function (f) {
-    var fx = JSON.parse(fs.readFileSync(path.join(dir, f), 'utf8'));
-    var lp = buildLp(fx);
-    assert.strictEqual(factorize(lp), 0, f + ' factorize');
-    var ks = fx.tab_rows.map(function (r) { return r.k; }), w = fx.m + fx.n;
-    [false, true].forEach(function (perRow) {
-        var rows = core.evalTabRows(lp, ks, perRow);
-        fx.tab_rows.forEach(function (r, t) {
-            var ref = new Float64Array(w), big = 1.0;
-            r.ind.forEach(function (j, q) { ref[j - 1] = r.val[q]; big = Math.max(big, Math.abs(r.val[q])); });
-            for (var j = 0; j < w; j++)
-                assert.ok(Math.abs(rows[t][j] - ref[j]) <= 1e-9 * big, f + ' k=' + r.k + ' j=' + (j + 1) + ': ' + rows[t][j] + ' vs ' + ref[j]);
-        });
-    });
-    ntab++;
-});
-assert.ok(ntab >= 5, 'too few tab fixtures: ' + ntab);
+
 
 // MIP fixtures: root LP through solve_lp as above, then the native driver
 // through gk_core.iosDriver with the tree object ios_driver receives
@@ -220,4 +202,30 @@ fs.readdirSync(dir).filter(function (f) { return /^scale_.*\.json$/.test(f); }).
     });
 });
 assert.ok(nscale >= 60, 'too few scaling runs: ' + nscale);
-console.log('ok js gpu parity: ' + ncase + ' runs, ' + nmip + ' MIPs, ' + nscale + ' scalings');
+// tableau rows (tests/golden/tab_*.json: the reference's glp_eval_tab_row on
+// the basis glp_simplex left) through gk_core.evalTabRows, both device paths
+var ntab = 0;
+fs.readdirSync(dir).filter(function (f) { return /^tab_.*\.json$/.test(f); }).sort().forEach(function (f) {
+    var fx = JSON.parse(fs.readFileSync(path.join(dir, f), 'utf8'));
+    var lp = buildLp(fx);
+    assert.strictEqual(factorize(lp), 0, f + ' factorize');
+    var ks = fx.tab_rows.map(function (r) { return r.k; }), w = fx.m + fx.n;
+    [false, true].forEach(function (perRow) {
+        var rows = core.evalTabRows(lp, ks, perRow);
+        fx.tab_rows.forEach(function (r, t) {
+            var ref = new Float64Array(w), big = 1.0;
+            r.ind.forEach(function (j, q) { ref[j - 1] = r.val[q]; big = Math.max(big, Math.abs(r.val[q])); });
+            for (var j = 0; j < w; j++)
+                assert.ok(Math.abs(rows[t][j] - ref[j]) <= 1e-9 * big, f + ' k=' + r.k + ' j=' + (j + 1) + ': ' + rows[t][j] + ' vs ' + ref[j]);
+        });
+    });
+    ntab++;
+});
+assert.ok(ntab >= 5, 'too few tab fixtures: ' + ntab);
+
+console.log('ok js gpu parity: ' + ncase + ' runs, ' + nmip + ' MIPs, ' + nscale + ' scalings, ' + ntab + ' tableau-row fixtures');
+// node 12's environment teardown can run pending N-API second-pass
+// finalizers after the addon's environment is gone (a segfault inside
+// libnode's PendingPhantomCallback::Invoke, seen when handles were
+// collected just before exit); a checked script leaves without it
+process.exit(0);
