@@ -430,22 +430,26 @@ void scatter_pos(hipStream_t s, int m, int off, int cnt, const int *head, const 
 // =====================================================================
 // small vector helpers
 // =====================================================================
-// one block per segment; staged segments are 256-byte aligned, destinations
-// are allocation starts (16-byte words, then the tail bytes)
+// blockIdx.x = the segment, gridDim.y blocks share it; staged segments are
+// 256-byte aligned, destinations are allocation starts (16-byte words, then
+// the tail bytes)
 __global__ void __launch_bounds__(256) k_scatter_segments(const char *__restrict__ src, const UpSeg *__restrict__ segs)
 {
     const UpSeg g = segs[blockIdx.x];
     const char *a = src + g.off;
     char *b = (char *)g.dst;
     const size_t nw = g.bytes / 16;
-    for (size_t i = threadIdx.x; i < nw; i += blockDim.x)
+    const size_t t0 = (size_t)blockIdx.y * blockDim.x + threadIdx.x, st = (size_t)gridDim.y * blockDim.x;
+    for (size_t i = t0; i < nw; i += st)
         ((uint4 *)b)[i] = ((const uint4 *)a)[i];
-    for (size_t i = nw * 16 + threadIdx.x; i < g.bytes; i += blockDim.x) b[i] = a[i];
+    if (blockIdx.y == 0)
+        for (size_t i = nw * 16 + threadIdx.x; i < g.bytes; i += blockDim.x) b[i] = a[i];
 }
 
 void scatter_segments(hipStream_t s, const char *src, const UpSeg *segs, int nseg)
 {
-    if (nseg > 0) hipLaunchKernelGGL(k_scatter_segments, dim3(nseg), dim3(256), 0, s, src, segs);
+    // 16 blocks per segment: a segment of a C3 upload is up to 160 KiB
+    if (nseg > 0) hipLaunchKernelGGL(k_scatter_segments, dim3(nseg, 16), dim3(256), 0, s, src, segs);
 }
 
 __global__ void k_fill(double *x, double v, size_t n)
