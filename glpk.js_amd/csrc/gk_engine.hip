@@ -538,7 +538,7 @@ struct Spx {
         d.tslots = E->tslots.p;
         d.xslots = E->xslots.p;
         d.trace = nullptr;
-        if (E->prof == 2) {
+        if (E->prof >= 2) {
             if (!E->trace.p) {
                 E->trace.ensure(TRACE_LEN);
                 HIPCHK(hipMemset(E->trace.p, 0, E->trace.n * sizeof(unsigned long long)));
@@ -1071,8 +1071,8 @@ struct Spx {
             E->ev.push_back(e);
         }
     }
-    hipEvent_t ev0(int t) const { return E->prof ? E->ev[2 * t] : nullptr; }
-    hipEvent_t ev1(int t) const { return E->prof ? E->ev[2 * t + 1] : nullptr; }
+    hipEvent_t ev0(int t) const { return (E->prof == 1 || E->prof == 2) ? E->ev[2 * t] : nullptr; }
+    hipEvent_t ev1(int t) const { return (E->prof == 1 || E->prof == 2) ? E->ev[2 * t + 1] : nullptr; }
     int run_dual();
     int run_primal();
     int batch(int K, int rigorous);
@@ -1245,8 +1245,11 @@ int Spx::batch(int K, int rigorous)
         const DualPlan pl = dual_plan(d, bucket(hs.nr + K + 1, m), bucket(hs.nwl + K + 1, n), pse, rigorous);
         // profiling launches eagerly: event-record nodes inside captured
         // graphs are not timed by every HIP runtime this library may bind to
-        if (E->prof) prof_events(K);
-        if (!rigorous && K >= 4 && !E->prof) run_graph(d, pl, K);
+        // prof 1/2 launch eagerly (events around the pivot-row kernel); prof 3
+        // keeps the graphs and records only the per-block clock stamps
+        const int evp = E->prof == 1 || E->prof == 2;
+        if (evp) prof_events(K);
+        if (!rigorous && K >= 4 && !evp) run_graph(d, pl, K);
         else {
             dual_batch_begin(s, d, pl);
             for (int t = 0; t < K; t++) dual_iteration2(s, d, pl, ev0(t), ev1(t));
@@ -1281,7 +1284,7 @@ int Spx::batch(int K, int rigorous)
     f->stats.trow_dev_launches = (long long)hs.trow_n;
     f->stats.trow_dev_ms_r = hs.trow_ticks_r / (double)ctx->wall_khz;
     f->stats.trow_dev_launches_r = (long long)hs.trow_nr;
-    if (dual && E->prof) {
+    if (dual && (E->prof == 1 || E->prof == 2)) {
         for (int t = 0; t < hs.npiv; t++) {
             float ms = 0.f;
             hipError_t e = hipEventElapsedTime(&ms, E->ev[2 * t], E->ev[2 * t + 1]);
@@ -1863,7 +1866,7 @@ void gk_bfd_last_stats(const gk_bfd *f, gk_spx_stats *st)
 
 void gk_bfd_profile(gk_bfd *f, int enable)
 {
-    if (f) f->prof = enable == 2 ? 2 : (enable ? 1 : 0);
+    if (f) f->prof = (enable == 2 || enable == 3) ? enable : (enable ? 1 : 0);
 }
 
 int gk_bfd_trace(gk_bfd *f, unsigned long long *out, size_t cnt)

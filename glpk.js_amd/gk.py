@@ -429,8 +429,9 @@ class GkProblem:
 
     def profile(self, enable=True):
         """Record HIP events around the pivot-row kernel of every dual pivot
-        (enable == 2: also per-block device clock stamps, see trace())."""
-        self.L.gk_bfd_profile(self.bfd, 2 if enable == 2 else (1 if enable else 0))
+        (enable == 2: also per-block device clock stamps, see trace(); 3:
+        the stamps only, inside the replayed graphs)."""
+        self.L.gk_bfd_profile(self.bfd, enable if enable in (2, 3) else (1 if enable else 0))
 
     def trace(self) -> np.ndarray:
         """Per-kernel, per-block [entry, exit] device clock stamps of the last

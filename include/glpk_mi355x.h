@@ -191,7 +191,7 @@ typedef struct {
 } gk_spx_stats;
 void gk_bfd_last_stats(const gk_bfd *bfd, gk_spx_stats *st);
 /* record HIP events around the pivot-row kernel of every dual pivot (benches) */
-void gk_bfd_profile(gk_bfd *bfd, int enable);
+void gk_bfd_profile(gk_bfd *bfd, int enable);   /* 1: events, eager; 2: + block clock stamps; 3: stamps only, graphs kept */
 /* profiling aid (enable == 2 above): copies the per-kernel, per-block device
  * clock stamps of the last pivot, trace[(kernel * 2048 + block) * 2 + {0 entry,
  * 1 exit}], kernels 0 top, 1 pivot row, 2 ratio, 3 FTRAN (one kernel), 4 commit,

@@ -27,7 +27,8 @@ def main():
     P = gk.GkProblem(ctx, problems.gen_dense(m, n, seed=42))
     assert P.factorize() == 0
     gk.glp_simplex(P, gk.SMCP(meth=gk.GLP_DUAL, it_lim=warm, msg_lev=gk.GLP_MSG_ERR))
-    P.profile(2)
+    # GK_TRACE_GRAPH=1: stamps inside the replayed graphs (gk_bfd_profile 3)
+    P.profile(3 if os.environ.get("GK_TRACE_GRAPH") else 2)
     khz = 100000.0
     acc = {}
     ph = {}
