@@ -289,8 +289,26 @@ static int reinvert_core(gk_bfd *f, const BasisSplit &bs, const MatDev *Adense, 
         f->piv.ensure(k);
         f->flag.ensure(1);
         const bool blocked = k <= gj_blocked_max();
+        // GK_GJ_TIME=1 (tools/prof_reinvert.py): device span of the
+        // Gauss–Jordan inversion by events on s, printed to stderr
+        static const bool gj_time = std::getenv("GK_GJ_TIME") != nullptr;
+        hipEvent_t gj_ev[2] = {nullptr, nullptr};
+        if (gj_time) {
+            HIPCHK(hipEventCreate(&gj_ev[0]));
+            HIPCHK(hipEventCreate(&gj_ev[1]));
+            HIPCHK(hipEventRecord(gj_ev[0], s));
+        }
         if (blocked) result = gauss_jordan_blocked(s, f->X.p, f->Y.p, k, f->piv_step.p, f->piv.p, f->flag.p, 1e-15);
         else gauss_jordan(s, f->X.p, f->Y.p, k, f->piv_step.p, f->piv.p, f->flag.p, 1e-15, &result);
+        if (gj_time) {
+            float ms = 0.f;
+            HIPCHK(hipEventRecord(gj_ev[1], s));
+            HIPCHK(hipEventSynchronize(gj_ev[1]));
+            HIPCHK(hipEventElapsedTime(&ms, gj_ev[0], gj_ev[1]));
+            fprintf(stderr, "gauss-jordan k=%d: %.3f ms (device, events)\n", k, ms);
+            (void)hipEventDestroy(gj_ev[0]);
+            (void)hipEventDestroy(gj_ev[1]);
+        }
         int flag = 0;
         HIPCHK(hipMemcpyAsync(&flag, f->flag.p, sizeof(int), hipMemcpyDeviceToHost, s));
         HIPCHK(hipStreamSynchronize(s));

@@ -21,6 +21,10 @@
 // of one launch per column.
 #include "gk_device.h"
 #include <cstdlib>
+#include <climits>
+#include <map>
+#include <vector>
+#include <hip/hip_ext.h>
 #include <cstdio>
 
 namespace gk {
@@ -151,13 +155,17 @@ template <int B, int SUBE, int QCM = 0>
 __global__ void __launch_bounds__(256) k_gjb_update(const double *__restrict__ M, double *__restrict__ M2,
                                                     const double *__restrict__ Qm, int ldq,
                                                     const int *__restrict__ rsl, int k, int t0,
-                                                    const int *__restrict__ flag)
+                                                    const int *__restrict__ flag, int cb0, int gap_at, int gap)
 {
     if (*flag) return;
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int li = lane & 15, lk = lane >> 4;
+    // column tile: cb0 + blockIdx.x, tiles from gap_at on shifted by gap
+    // (the look-ahead schedule updates a column range in two launches)
+    int cb = cb0 + (int)blockIdx.x;
+    if (cb >= gap_at) cb += gap;
     const int row0 = blockIdx.y * 64 + (w & 1) * 32;
-    const int col0 = blockIdx.x * 64 + (w >> 1) * 32;
+    const int col0 = cb * 64 + (w >> 1) * 32;
     const int b = min(B, k - t0);
     gj_double4 acc[2][2];
 #pragma unroll
@@ -250,7 +258,7 @@ static double *gjb_run(hipStream_t s, double *M, double *M2, double *Qm, int k, 
         hipLaunchKernelGGL((k_gjb_panel<NT, RPT, B>), dim3(1), dim3(NT), 0, s, M, M2, k, t0, k, Qm, k, t0, piv_step,
                            piv, flag, tiny, (double *)nullptr, 0);
         if (k > B)
-            hipLaunchKernelGGL((k_gjb_update<B, 0>), g, dim3(256), 0, s, M, M2, Qm, B, piv + t0, k, t0, flag);
+            hipLaunchKernelGGL((k_gjb_update<B, 0>), g, dim3(256), 0, s, M, M2, Qm, B, piv + t0, k, t0, flag, 0, INT_MAX, 0);
         std::swap(M, M2);
     }
     return M;
@@ -271,7 +279,7 @@ static double *gjb_run2(hipStream_t s, double *M, double *M2, double *P, double 
             if (bo > B) hipLaunchKernelGGL((k_gjb_inner<B>), gr, dim3(256), 0, s, P, bo, i0, Qm, xr, k, flag);
         }
         if (k > bo)
-            hipLaunchKernelGGL((k_gjb_update<GJ_BO, 1>), g, dim3(256), 0, s, M, M2, P, GJ_BO, piv + T0, k, T0, flag);
+            hipLaunchKernelGGL((k_gjb_update<GJ_BO, 1>), g, dim3(256), 0, s, M, M2, P, GJ_BO, piv + T0, k, T0, flag, 0, INT_MAX, 0);
         hipLaunchKernelGGL(k_gjb_copy, gr, dim3(256), 0, s, P, GJ_BO, 0, M2, k, T0, k, bo, flag);
         std::swap(M, M2);
     }
@@ -515,10 +523,135 @@ static double *gjc_run(hipStream_t s, double *M, double *M2, double *P, double *
                                    piv + T0 + i0, xr, k, flag);
         }
         if (k > bo)
-            hipLaunchKernelGGL((k_gjb_update<GJ_BO, 1, 1>), g, dim3(256), 0, s, M, M2, P, k, piv + T0, k, T0, flag);
+            hipLaunchKernelGGL((k_gjb_update<GJ_BO, 1, 1>), g, dim3(256), 0, s, M, M2, P, k, piv + T0, k, T0, flag, 0, INT_MAX, 0);
         hipLaunchKernelGGL(k_gjc_copy<0>, gt, dim3(256), 0, s, P, M2, k, T0, bo, flag);
         std::swap(M, M2);
     }
+    return M;
+}
+
+// The same arithmetic with look-ahead: the one-workgroup panels are the
+// critical path, so outer panel T0's rank-64 update is split.  The next
+// outer panel's 64 columns are updated first, on s, and copied into the
+// other P buffer; the rest of M (every other column, all rows) and the
+// write-back of P run on a side stream under the next panel's Gauss–Jordan
+// steps.  Every element sees the same operations in the same order as in
+// gjc_run, so the inverse is bit-identical.  Hazards: outer panel T0 + 64's
+// own next-columns update reads columns written by T0's rest update and
+// writes the buffer that update reads, and its copy-in overwrites the P that
+// T0's write-back reads, so s waits for the side stream's event of T0 before
+// them.
+struct GjSide {
+    hipStream_t crit = nullptr, side = nullptr;
+    hipEvent_t ev_in = nullptr, ev_main = nullptr, ev_side = nullptr;
+};
+
+// the critical-path stream (the panels, on GK_GJ_CRIT_CUS compute units,
+// default 64) and the side stream (the other CUs), disjoint CU masks so the
+// big updates do not share a CU with the one-workgroup panel; three events;
+// created once per device and thread, nullptr when the runtime refuses them
+// (the single-stream schedule then runs)
+static GjSide *gj_side()
+{
+    static thread_local std::map<int, GjSide> per_dev;
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return nullptr;
+    GjSide &g = per_dev[dev];
+    if (g.side) return &g;
+    static const int crit_cus = [] {
+        const char *e = std::getenv("GK_GJ_CRIT_CUS");
+        return e ? std::atoi(e) : 64;
+    }();
+    int ncu = 0;
+    if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return nullptr;
+    bool ok;
+    if (crit_cus > 0 && crit_cus < ncu) {
+        const int words = (ncu + 31) / 32;
+        std::vector<uint32_t> mc(words, 0u), ms(words, 0u);
+        for (int c = 0; c < ncu; ++c) (c < crit_cus ? mc : ms)[c / 32] |= 1u << (c % 32);
+        ok = hipExtStreamCreateWithCUMask(&g.crit, words, mc.data()) == hipSuccess &&
+             hipExtStreamCreateWithCUMask(&g.side, words, ms.data()) == hipSuccess;
+    } else {
+        ok = hipStreamCreateWithFlags(&g.crit, hipStreamNonBlocking) == hipSuccess &&
+             hipStreamCreateWithFlags(&g.side, hipStreamNonBlocking) == hipSuccess;
+    }
+    ok = ok && hipEventCreateWithFlags(&g.ev_in, hipEventDisableTiming) == hipSuccess &&
+         hipEventCreateWithFlags(&g.ev_main, hipEventDisableTiming) == hipSuccess &&
+         hipEventCreateWithFlags(&g.ev_side, hipEventDisableTiming) == hipSuccess;
+    if (!ok) {
+        fprintf(stderr, "gk re-inversion: look-ahead streams unavailable, single stream\n");
+        g = GjSide{};
+        return nullptr;
+    }
+    return &g;
+}
+
+// event record / wait on valid handles; a failure is reported, never ignored
+#define GJCHK(x)                                                                              \
+    do {                                                                                      \
+        hipError_t e__ = (x);                                                                 \
+        if (e__ != hipSuccess) {                                                              \
+            fprintf(stderr, "gk re-inversion: %s failed: %s\n", #x, hipGetErrorString(e__));   \
+            abort();                                                                          \
+        }                                                                                     \
+    } while (0)
+
+template <int NT, int RPT, int B>
+static double *gjc_run_la(hipStream_t s, double *M, double *M2, double *P0, double *P1, double *xr, int k,
+                          int *piv_step, int *piv, int *flag, double tiny)
+{
+    GjSide &gs = *gj_side();
+    const hipStream_t s_in = s;
+    GJCHK(hipEventRecord(gs.ev_in, s_in));
+    s = gs.crit;
+    GJCHK(hipStreamWaitEvent(s, gs.ev_in, 0));
+    const int nb = (k + 63) / 64;                       // column (and row) tiles
+    const dim3 gt(nb), gr((k + 255) / 256);
+    double *P[2] = {P0, P1};
+    int cur = 0;
+    bool side_busy = false;
+    hipLaunchKernelGGL(k_gjc_copy<1>, gt, dim3(256), 0, s, M, P[cur], k, 0, std::min(GJ_BO, k), flag);
+    for (int T0 = 0; T0 < k; T0 += GJ_BO) {
+        const int bo = std::min(GJ_BO, k - T0);
+        double *Pc = P[cur];
+        for (int i0 = 0; i0 < bo; i0 += B) {
+            hipLaunchKernelGGL((k_gjc_panel<NT, RPT, B>), dim3(1), dim3(NT), 0, s, Pc, k, i0, bo, T0 + i0, piv_step,
+                               piv, flag, tiny, xr);
+            if (bo > B)
+                hipLaunchKernelGGL((k_gjc_inner<B>), dim3(gr.x, (bo + 7) / 8), dim3(256), 0, s, Pc, bo, i0,
+                                   piv + T0 + i0, xr, k, flag);
+        }
+        const int tb = T0 / 64;                         // this panel's tile
+        if (side_busy) GJCHK(hipStreamWaitEvent(s, gs.ev_side, 0));
+        side_busy = false;
+        if (T0 + GJ_BO < k) {
+            // the next panel's columns first, then its copy into the other P
+            hipLaunchKernelGGL((k_gjb_update<GJ_BO, 1, 1>), dim3(1, nb), dim3(256), 0, s, M, M2, Pc, k, piv + T0, k,
+                               T0, flag, tb + 1, INT_MAX, 0);
+            hipLaunchKernelGGL(k_gjc_copy<1>, gt, dim3(256), 0, s, M2, P[cur ^ 1], k, T0 + GJ_BO,
+                               std::min(GJ_BO, k - T0 - GJ_BO), flag);
+            // the rest on the side stream: tiles [0, tb) and [tb + 2, nb)
+            GJCHK(hipEventRecord(gs.ev_main, s));
+            GJCHK(hipStreamWaitEvent(gs.side, gs.ev_main, 0));
+            if (nb - 2 > 0)
+                hipLaunchKernelGGL((k_gjb_update<GJ_BO, 1, 1>), dim3(nb - 2, nb), dim3(256), 0, gs.side, M, M2, Pc, k,
+                                   piv + T0, k, T0, flag, 0, tb, 2);
+            hipLaunchKernelGGL(k_gjc_copy<0>, gt, dim3(256), 0, gs.side, Pc, M2, k, T0, bo, flag);
+            GJCHK(hipEventRecord(gs.ev_side, gs.side));
+            side_busy = true;
+        } else {
+            // last panel: the other tiles (all before it) and the write-back on s
+            if (tb > 0)
+                hipLaunchKernelGGL((k_gjb_update<GJ_BO, 1, 1>), dim3(tb, nb), dim3(256), 0, s, M, M2, Pc, k, piv + T0,
+                                   k, T0, flag, 0, INT_MAX, 0);
+            hipLaunchKernelGGL(k_gjc_copy<0>, gt, dim3(256), 0, s, Pc, M2, k, T0, bo, flag);
+        }
+        std::swap(M, M2);
+        cur ^= 1;
+    }
+    if (side_busy) GJCHK(hipStreamWaitEvent(s_in, gs.ev_side, 0));
+    GJCHK(hipEventRecord(gs.ev_main, s));
+    GJCHK(hipStreamWaitEvent(s_in, gs.ev_main, 0));
     return M;
 }
 
@@ -532,8 +665,9 @@ int gj_blocked_max() { return 8192; }
 
 size_t gj_blocked_scratch(int k)
 {
-    // Q (k x B, B <= 32), the outer panel P (k x 64), X_R (32 x 64)
-    return (size_t)32 * k + (size_t)GJ_BO * k + 32 * GJ_BO;
+    // Q (k x B, B <= 32), the outer panel P (k x 64), X_R (32 x 64), the
+    // look-ahead's second outer panel (k x 64)
+    return (size_t)32 * k + (size_t)GJ_BO * k + 32 * GJ_BO + (size_t)GJ_BO * k;
 }
 
 // inverse of C (k x k, column-major in X[0, k^2)) by the blocked scheme
@@ -559,6 +693,21 @@ double *gauss_jordan_blocked(hipStream_t s, double *X, double *scratch, int k, i
         if (k <= 2048) return gjb_run2<1024, 2, 16>(s, X, M2, P, Qm, xr, k, piv_step, piv, flag, tiny);
         if (k <= 4096) return gjb_run2<1024, 4, 8>(s, X, M2, P, Qm, xr, k, piv_step, piv, flag, tiny);
         return gjb_run2<1024, 8, 4>(s, X, M2, P, Qm, xr, k, piv_step, piv, flag, tiny);
+    }
+    // look-ahead (k = 4096: 21.3 -> 19.8 ms; k = 2048: no gain, the panels
+    // slow down by what the hidden updates save), opt-in: GK_GJ_LOOKAHEAD=1
+    // for k > 2048, 2 for every k.  Off by default: a process holding the
+    // CU-masked streams crashed in its exit handlers under rocprofv3.
+    static const int lookahead = [] {
+        const char *e = std::getenv("GK_GJ_LOOKAHEAD");
+        return e ? std::atoi(e) : 0;
+    }();
+    double *P1 = xr + 32 * GJ_BO;
+    if ((lookahead > 1 || (lookahead == 1 && k > 2048)) && gj_side()) {
+        if (k <= 1024) return gjc_run_la<512, 2, 16>(s, X, M2, P, P1, xr, k, piv_step, piv, flag, tiny);
+        if (k <= 2048) return gjc_run_la<512, 4, 16>(s, X, M2, P, P1, xr, k, piv_step, piv, flag, tiny);
+        if (k <= 4096) return gjc_run_la<512, 8, 8>(s, X, M2, P, P1, xr, k, piv_step, piv, flag, tiny);
+        return gjc_run_la<1024, 8, 4>(s, X, M2, P, P1, xr, k, piv_step, piv, flag, tiny);
     }
     if (k <= 1024) return gjc_run<512, 2, 16>(s, X, M2, P, Qm, xr, k, piv_step, piv, flag, tiny);
     if (k <= 2048) return gjc_run<512, 4, 16>(s, X, M2, P, Qm, xr, k, piv_step, piv, flag, tiny);

@@ -56,6 +56,32 @@ def test_gpu_lp_matches_reference(gpu_ctx, path, run_index):
         check_solution(P)
 
 
+IT_LIM_CASES = [c for c in LP_CASES if load_golden(c.values[0])["runs"][c.values[1]]["opts"].get("it_lim")]
+
+
+@pytest.mark.parametrize("path,run_index", IT_LIM_CASES)
+def test_gpu_lp_it_lim_state_matches_reference(gpu_ctx, path, run_index):
+    """A run stopped by it_lim (glpspx01.js / glpspx02.js: ITERATION LIMIT
+    EXCEEDED) leaves the reference's intermediate state: the same statuses,
+    the same basis after it_lim pivots, and the same (non-optimal) objective
+    and primal values.  The reference's pivot trace pins the pivots; a GPU
+    run that followed them must reproduce this state exactly."""
+    d = load_golden(path)
+    run = d["runs"][run_index]
+    prob = problems.from_fixture(d)
+    P = gk.GkProblem(gpu_ctx, prob)
+    ret = gk.glp_simplex(P, gk.SMCP(**run["opts"]))
+    assert ret == run["ret"] and P.it_cnt == run["it_cnt"]
+    assert (P.pbs_stat, P.dbs_stat) == (run["pbs_stat"], run["dbs_stat"])
+    assert list(P.row_stat[1:]) == list(run["row_stat"])
+    assert list(P.col_stat[1:]) == list(run["col_stat"])
+    ref = run["obj_val"]
+    assert abs(P.obj_val - ref) <= 1e-9 * max(1.0, abs(ref)), (P.obj_val, ref)
+    for got, want in ((P.row_prim[1:], run["row_prim"]), (P.col_prim[1:], run["col_prim"])):
+        want = np.asarray(want, np.float64)
+        assert np.max(np.abs(np.asarray(got) - want), initial=0.0) <= 1e-9 * (1.0 + np.abs(want).max(initial=0.0))
+
+
 @pytest.mark.parametrize("name", ["lp_gap.json", "lp_dense_64x256.json", "lp_mix14.json", "lp_c2s.json"])
 def test_gpu_bfd_ftran_btran_match_oracle(gpu_ctx, oracle, name):
     """gk_bfd_factorize + gk_bfd_ftran/btran (glpapi12.js:5/:198/:222) agree
