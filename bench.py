@@ -65,6 +65,13 @@ def load_profile(args):
     return out
 
 
+LEG = {"name": "setup"}
+
+
+def leg(name):
+    LEG["name"] = name
+
+
 def log(rank, *a):
     if rank == 0:
         print(*a, file=sys.stderr, flush=True)
@@ -104,7 +111,10 @@ def main():
     from glpk_js_amd import gk, problems
     # the solver's printed lines (glp_simplex's xprintf) go to stderr: stdout
     # carries the one JSON line
-    gk.glp_set_print_func(lambda s: print(s, file=sys.stderr))
+    # (a warning is tagged with the bench leg and the iteration count at the
+    # start of the call that printed it, so that it can be traced)
+    gk.glp_set_print_func(lambda s: print(s + (f"  [{LEG['name']}]" if s.startswith(("Warning", "Error")) else ""),
+                                          file=sys.stderr))
 
     def barrier():
         if world > 1:
@@ -122,8 +132,9 @@ def main():
 
     restarts = [0]
 
-    def step():
+    def step(tag="headline"):
         it0 = P.it_cnt
+        leg(f"{tag} step from it_cnt={it0}")
         ret = gk.glp_simplex(P, parm)
         if ret not in (0, 8):
             raise RuntimeError(f"glp_simplex returned {ret}")
@@ -173,7 +184,7 @@ def main():
     if rank == 0:
         P.profile(True)
         for _ in range(args.steps):
-            step()
+            step("events cross-check")
             s_ = P.stats()
             trow["ms"] += s_.trow_ms
             trow["launches"] += s_.trow_launches
@@ -315,6 +326,7 @@ def run_extra(gk, problems, ctx, c3):
     the headline."""
     out = {}
     P = gk.GkProblem(ctx, c3)
+    leg("c3_first300_dual")
     t0 = time.perf_counter()
     ret = gk.glp_simplex(P, gk.SMCP(meth=gk.GLP_DUAL, it_lim=300, msg_lev=gk.GLP_MSG_ERR))
     dt = time.perf_counter() - t0
@@ -326,6 +338,7 @@ def run_extra(gk, problems, ctx, c3):
     # like the headline: it_lim=100 steps continuing from the previous basis
     P = gk.GkProblem(ctx, c3)
     parm = gk.SMCP(meth=gk.GLP_PRIMAL, it_lim=100, msg_lev=gk.GLP_MSG_ERR)
+    leg("c3_primal_steps")
     gk.glp_simplex(P, parm)
     t0 = time.perf_counter()
     it0 = P.it_cnt
@@ -340,6 +353,7 @@ def run_extra(gk, problems, ctx, c3):
     for meth, name, ref_rate in ((gk.GLP_DUAL, "dual", 1813), (gk.GLP_PRIMAL, "primal", 1833)):
         p = problems.gen_c2s()
         P = gk.GkProblem(ctx, p)
+        leg("c2s_" + name)
         t0 = time.perf_counter()
         ret = gk.glp_simplex(P, gk.SMCP(meth=meth, msg_lev=gk.GLP_MSG_ERR))
         dt = time.perf_counter() - t0
@@ -393,6 +407,7 @@ def run_mid(gk, problems, ctx, c3, start=100000, steps=10):
     adv = gk.SMCP(meth=gk.GLP_DUAL, it_lim=2000, msg_lev=gk.GLP_MSG_ERR)
     t0 = time.perf_counter()
     while P.it_cnt < start:
+        leg(f"c3_mid advance from it_cnt={P.it_cnt}")
         if gk.glp_simplex(P, adv) != 8:
             return {"error": "solve ended before the window"}
     t_adv = time.perf_counter() - t0
@@ -403,6 +418,7 @@ def run_mid(gk, problems, ctx, c3, start=100000, steps=10):
     piv, byts = 0, 0.0
     for _ in range(steps):
         it0 = P.it_cnt
+        leg(f"c3_mid window from it_cnt={it0}")
         gk.glp_simplex(P, parm)
         piv += P.it_cnt - it0
         byts += P.stats().bytes_pivots
@@ -429,6 +445,7 @@ def run_bnb(gk, problems, ctx, names=("gap", "c5s_12x30"), comm=None):
         d = _json.load(open(os.path.join(gold, "mip_" + name + ".json")))
         prob = problems.from_fixture(d)
         P = gk.GkProblem(ctx, prob)
+        leg("bnb_" + name)
         assert gk.glp_simplex(P, gk.SMCP(msg_lev=gk.GLP_MSG_ERR)) == 0
         t0 = time.perf_counter()
         ret = gk.glp_intopt(P, gk.IOCP(msg_lev=gk.GLP_MSG_ERR), comm=comm)

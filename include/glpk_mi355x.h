@@ -4,7 +4,7 @@
  * Drop-in boundary for the reference Cyame/glpk.js (GLPK 4.49 in JS).  The
  * JS host keeps glpapi*.js / glpcpx.js / glpmpl*.js and rebinds the closure
  * names of the hot path to these entry points through a thin N-API addon
- * (js/gk_addon.cc, js/gk_shim.js).
+ * (js/gk_addon.c, js/gk_shim.js).
  *
  *   entry point            replaces (reference file:line)
  *   ---------------------  ------------------------------------------------

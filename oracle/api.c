@@ -18,6 +18,14 @@ jmp_buf *orc_err_jmp = NULL;
 char orc_err_msg[512];
 orc_trace_fn orc_trace = NULL;
 void *orc_trace_ctx = NULL;
+long orc_instab_events = 0;
+int orc_instab_last_it = -1;
+
+long orc_instab_count(int *last_it)
+{
+    if (last_it) *last_it = orc_instab_last_it;
+    return orc_instab_events;
+}
 
 void orc_fail(const char *fmt, ...)
 {

@@ -184,6 +184,9 @@ typedef struct {
  * hooks in tests/golden/gen_golden.js */
 typedef void (*orc_trace_fn)(void *ctx, int kind, int it, int phase, int p, int q, int kq, int kp, double t);
 extern orc_trace_fn orc_trace; extern void *orc_trace_ctx;
+/* "Warning: numerical instability" events (check_stab failures) since load */
+extern long orc_instab_events; extern int orc_instab_last_it;
+long orc_instab_count(int *last_it);
 
 /* glpapi06.js / glpapi12.js */
 void orc_smcp_default(orc_smcp *parm);

@@ -75,6 +75,8 @@ def lib():
         L.orc_last_error.restype = C.c_char_p
         L.orc_scale_prob.argtypes = [C.c_int, C.c_int, i4p, i4p, f8p, C.c_int, f8p, f8p, f8p]
         L.orc_scale_prob.restype = C.c_int
+        L.orc_instab_count.restype = C.c_long
+        L.orc_instab_count.argtypes = [C.POINTER(C.c_int)]
         if hasattr(L, "orc_prob_intopt"):
             L.orc_prob_intopt.argtypes = [P, C.POINTER(IocpFlat), C.POINTER(IosStats)]
             L.orc_prob_intopt.restype = C.c_int
@@ -150,6 +152,13 @@ class OracleProb:
         out = {k: getattr(r, k) for k, _ in ResultFlat._fields_}
         out.update(a)
         return out
+
+
+def instab_count():
+    """(number of "numerical instability" restarts so far, it_cnt of the last)"""
+    it = C.c_int(-1)
+    n = lib().orc_instab_count(C.byref(it))
+    return n, it.value
 
 
 def scale_prob(m: int, n: int, A_ptr, A_ind, A_val, flags: int):

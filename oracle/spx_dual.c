@@ -815,6 +815,7 @@ int spx_dual(orc_prob *lp, const orc_smcp *parm)                     /* :1, loop
                 bbar_st = 0;
             }
             if (check_stab(csa, parm->tol_dj) != 0) {
+                orc_instab_events++; orc_instab_last_it = csa->it_cnt;
                 if (parm->meth == GLP_DUALP) {
                     store_sol(csa, lp, GLP_UNDEF, GLP_UNDEF, 0);
                     ret = GLP_EFAIL;

@@ -866,6 +866,7 @@ int spx_primal(orc_prob *lp, const orc_smcp *parm)                 /* :1, loop :
                 cbar_st = 0;
             }
             if (check_stab(csa, parm->tol_bnd)) {
+                orc_instab_events++; orc_instab_last_it = csa->it_cnt;
                 csa->phase = 0;
                 binv_st = 0;
                 rigorous = 5;

@@ -13,6 +13,10 @@
 //     (glpbfd.js:47), rebinding the closure names (SURVEY.md §0).
 //
 // usage: node tests/golden/gen_golden.js [--big] [--only PREFIX]
+//        node --max-old-space-size=12000 tests/golden/gen_golden.js --c3
+//          (C3 4096x16384 at full size only: the reference's state after its
+//           first 300 dual pivots, one it_lim=300 call and three it_lim=100
+//           calls; about 10 minutes and a 7 GB heap)
 'use strict';
 var fs = require('fs');
 var path = require('path');
@@ -20,6 +24,7 @@ var path = require('path');
 var REF = process.env.GLPK_REF || '/root/reference';
 var OUT = __dirname;
 var BIG = process.argv.indexOf('--big') >= 0;
+var C3 = process.argv.indexOf('--c3') >= 0;
 var ONLY = process.argv.indexOf('--only') >= 0 ? process.argv[process.argv.indexOf('--only') + 1] : null;
 
 function buildBundle() {
@@ -315,6 +320,42 @@ function mipOptsCase(name, mk, optsList) {
 }
 var MIP_OPTS = [{br_tech: 1}, {br_tech: 2}, {br_tech: 3}, {br_tech: 5}, {bt_tech: 1}, {bt_tech: 2}, {bt_tech: 4},
                 {br_tech: 3, bt_tech: 1}, {br_tech: 5, bt_tech: 4}, {pp_tech: 1}, {br_tech: 1, bt_tech: 2, pp_tech: 1}];
+
+// ---- C3 at full size (BASELINE.json configs[2]): the headline instance -----
+// The reference's own timing run (BASELINE.md: first 300 dual pivots) as
+// glp_simplex(SMCP{meth: GLP_DUAL, it_lim}) from the slack basis, once with
+// it_lim = 300 and once as three it_lim = 100 calls continuing from the basis
+// the previous call left (the bench's step definition: the factor and its
+// update count persist in lp.bfd across calls).  Recorded: the pivot trace,
+// statuses, objective, primal and dual values after the last call.  Gzipped
+// (20k-entry vectors); A is not stored (the generator is exact, §8(d)).
+function c3Case() {
+    var zlib = require('zlib');
+    var m = 4096, n = 16384, seed = 42;
+    var d = {name: 'c3_itlim', kind: 'lp', gen: {kind: 'dense', m: m, n: n, seed: seed}, runs: []};
+    [[300, 1], [100, 3]].forEach(function (c) {
+        var t0 = Date.now();
+        var P = genDense(m, n, seed);
+        console.log('C3 built in', (Date.now() - t0) / 1000, 's');
+        var calls = [], trace = [], lines = [], last = null;
+        for (var k = 0; k < c[1]; k++) {
+            last = runLp(P, {meth: glpk.GLP_DUAL, it_lim: c[0]}, 1000000);
+            calls.push({ret: last.ret, it_cnt: last.it_cnt, obj_val: last.obj_val, factorizations: last.factorizations,
+                        seconds: last.seconds});
+            trace = trace.concat(last.trace);
+            lines = lines.concat(last.lines);
+            console.log('C3 call', k, 'ret', last.ret, 'it', last.it_cnt, 'obj', last.obj_val, last.seconds.toFixed(1), 's');
+        }
+        last.trace = trace; last.lines = lines; last.calls = calls;
+        last.opts = {meth: glpk.GLP_DUAL, it_lim: c[0]}; last.ncalls = c[1];
+        d.runs.push(last);
+        P = null;
+        if (global.gc) global.gc();
+    });
+    fs.writeFileSync(path.join(OUT, 'c3_itlim.json.gz'), zlib.gzipSync(JSON.stringify(d)));
+    console.log('wrote c3_itlim.json.gz');
+}
+if (C3) { c3Case(); process.exit(0); }
 
 // ---- instances ------------------------------------------------------------
 lpCase('test', function () { return readLp('test.lpt'); }, null);

@@ -176,3 +176,66 @@ def test_gpu_dense_2048x8192_full_dual_kkt(gpu_ctx):
     gold = os.path.join(os.path.dirname(__file__), "golden", "dense_full_2048x8192.json")
     ref = load_golden(gold)                        # the oracle's full solve (2.4 h on one core)
     assert abs(P.obj_val - ref["obj_val"]) <= 1e-9 * abs(ref["obj_val"]), (P.obj_val, ref)
+
+
+def _gz(name):
+    import gzip
+    import json
+    with gzip.open(os.path.join(os.path.dirname(__file__), "golden", name), "rt") as f:
+        return json.load(f)
+
+
+def _assert_state(P, want, tol=1e-9):
+    """statuses equal; objective, primal and dual values within tol (relative
+    to the vector's largest magnitude)"""
+    assert (P.pbs_stat, P.dbs_stat) == (want["pbs_stat"], want["dbs_stat"])
+    rs = np.asarray(P.row_stat[1:]) != np.asarray(want["row_stat"])
+    cs = np.asarray(P.col_stat[1:]) != np.asarray(want["col_stat"])
+    assert not rs.any() and not cs.any(), (f"{int(rs.sum())} row / {int(cs.sum())} column statuses differ; first "
+                                           f"rows {np.nonzero(rs)[0][:5] + 1}, cols {np.nonzero(cs)[0][:5] + 1}")
+    ref = want["obj_val"]
+    assert abs(P.obj_val - ref) <= tol * max(1.0, abs(ref)), (P.obj_val, ref)
+    for key in ("row_prim", "col_prim", "row_dual", "col_dual"):
+        got, w = np.asarray(getattr(P, key)[1:]), np.asarray(want[key], np.float64)
+        err = np.max(np.abs(got - w), initial=0.0)
+        assert err <= tol * (1.0 + np.abs(w).max(initial=0.0)), (key, err)
+
+
+@pytest.mark.parametrize("run_index", [0, 1], ids=["1x300", "3x100"])
+def test_gpu_c3_full_size_state_matches_reference(gpu_ctx, run_index):
+    """The headline instance at full size (C3 4096 x 16384, seed 42) against
+    the reference itself: its 300-pivot timing run as one
+    it_lim=300 call and as three it_lim=100 calls continuing from the basis
+    the previous call left (the bench's step).  After 300 pivots the GPU holds
+    the reference's basis (every row and column status), and its objective,
+    primal and dual values agree to 1e-9 (tests/golden/c3_itlim.json.gz,
+    gen_golden.js --c3)."""
+    d = _gz("c3_itlim.json.gz")
+    g, run = d["gen"], d["runs"][run_index]
+    prob = problems.gen_dense(g["m"], g["n"], seed=g["seed"])
+    P = gk.GkProblem(gpu_ctx, prob)
+    for call in run["calls"]:
+        ret = gk.glp_simplex(P, gk.SMCP(**run["opts"]))
+        assert ret == call["ret"] and P.it_cnt == call["it_cnt"]
+        assert abs(P.obj_val - call["obj_val"]) <= 1e-9 * max(1.0, abs(call["obj_val"])), (P.it_cnt, P.obj_val)
+    _assert_state(P, run)
+    check_solution(P)
+
+
+def test_gpu_c3_bench_window_matches_oracle(gpu_ctx):
+    """The bench's whole window on C3 (warm-up + timed steps: 25 calls of
+    it_lim=100 from the slack basis, pivots 1-2500) against the oracle carried
+    along the same calls (tests/golden/c3_oracle_window.json.gz; the oracle is
+    bit-exact with the reference over the first 300 pivots,
+    test_oracle_c3_full_size_matches_reference).  After every call the
+    objective matches; at pivots 300 and 2500 the whole state does."""
+    w = _gz("c3_oracle_window.json.gz")
+    g = w["gen"]
+    prob = problems.gen_dense(g["m"], g["n"], seed=g["seed"])
+    P = gk.GkProblem(gpu_ctx, prob)
+    states = {s["call"]: s for s in w["states"]}
+    for k, want_ret in enumerate(w["rets"], start=1):
+        ret = gk.glp_simplex(P, gk.SMCP(**w["opts"]))
+        assert ret == want_ret and P.it_cnt == 100 * k
+        if k in states:
+            _assert_state(P, states[k])

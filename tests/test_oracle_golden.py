@@ -52,3 +52,43 @@ def test_generators_match_fixture_statistics():
         np.testing.assert_array_equal(q.col_coef, np.asarray(d["col_coef"]))
         np.testing.assert_array_equal(q.row_ub, np.asarray(d["row_ub"]))
         assert p.nnz == d["nnz"] == q.nnz
+
+
+def _gz(name):
+    import gzip
+    import json
+    with gzip.open(os.path.join(os.path.dirname(__file__), "golden", name), "rt") as f:
+        return json.load(f)
+
+
+def test_oracle_c3_full_size_matches_reference(oracle):
+    """C3 at full size (4096 x 16384, BASELINE.json configs[2]): the oracle
+    repeats the reference's own 300-pivot timing run bit for bit
+    (tests/golden/c3_itlim.json.gz, gen_golden.js --c3), as one it_lim=300
+    call and as three it_lim=100 calls continuing from the basis the previous
+    call left (the bench's step) — pivot trace, statuses, objective, primal
+    and dual values.  This pins tests/golden/c3_oracle_window.json.gz (the
+    oracle carried on to pivot 2500, gen_c3_oracle.py) to the reference."""
+    d = _gz("c3_itlim.json.gz")
+    g = d["gen"]
+    prob = problems.gen_dense(g["m"], g["n"], seed=g["seed"], keep_dense=False)
+    for run in d["runs"]:
+        o = oracle.OracleProb(prob)
+        trace = []
+        for call in run["calls"]:
+            ret = o.simplex(trace=trace, **run["opts"])
+            assert ret == call["ret"]
+            r = o.result()
+            assert r["it_cnt"] == call["it_cnt"] and r["obj_val"] == call["obj_val"]
+        assert [tuple(t) for t in trace] == [tuple(t) for t in run["trace"]]
+        for key in ("row_prim", "row_dual", "col_prim", "col_dual"):
+            np.testing.assert_array_equal(r[key], np.asarray(run[key], dtype=np.float64), err_msg=key)
+        np.testing.assert_array_equal(r["row_stat"], run["row_stat"])
+        np.testing.assert_array_equal(r["col_stat"], run["col_stat"])
+        del o
+    # the committed oracle window starts with the reference's 3 x 100 run
+    w = _gz("c3_oracle_window.json.gz")
+    s300 = w["states"][0]
+    ref = d["runs"][1]
+    assert s300["it_cnt"] == 300 and s300["obj_val"] == ref["obj_val"]
+    assert [tuple(t) for t in s300["trace"]] == [tuple(t) for t in ref["trace"]]
