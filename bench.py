@@ -154,6 +154,7 @@ def main():
     piv = 0
     split = {"init": 0.0, "eval": 0.0, "batches": 0.0, "reinvert": 0.0, "total": 0.0}
     reinv = 0
+    resident, skipped = 0, 0
     dev = {"ms": 0.0, "ms_b": 0.0, "launches": 0, "bytes": 0.0, "ms_r": 0.0, "launches_r": 0, "bytes_pivots": 0.0}
     for _ in range(args.steps):
         piv += step()
@@ -164,6 +165,8 @@ def main():
         split["reinvert"] += s_.seconds_reinvert
         split["total"] += s_.seconds_total
         reinv += s_.reinversions
+        resident += s_.resident
+        skipped += s_.evals_skipped
         dev["ms"] += s_.trow_dev_ms
         dev["ms_b"] += s_.trow_dev_ms_b
         dev["launches"] += s_.trow_dev_launches
@@ -311,7 +314,8 @@ def main():
                        "graphs_built_last_step": int(st.graphs_built),
                        "pivots": int(st.pivots), "reinversions_timed_region": reinv,
                        "batches": int(st.batches), "host_syncs": int(st.host_syncs),
-                       "restarts": restarts[0], "kernels": kern},
+                       "restarts": restarts[0], "resident_calls": resident, "evals_skipped": skipped,
+                       "kernels": kern},
             "extra": extra,
         }
         print(json.dumps(line), flush=True)

@@ -170,6 +170,22 @@ struct Engine {
     char *arena = nullptr;
     size_t arena_cap = 0;
     int arena_m = -1, arena_n = -1;
+    // the working set a gk_spx_* call left on the device (host mirrors of it),
+    // so that the next call on the same problem — a run of it_lim-bounded
+    // calls, or glp_simplex after glp_simplex — does not upload it again and
+    // does not repeat an evaluation whose result is already resident
+    // (Spx::resident_match); ok is cleared by every call and set again by a
+    // normal return
+    struct Resident {
+        bool ok = false;
+        int dual = -1, m = 0, n = 0, nr = 0;
+        unsigned long long a_version = 0, fact_ver = 0;
+        double zeta = 0.0;
+        std::vector<signed char> type, orig_type, stat;
+        std::vector<double> lb, ub, coef, orig_lb, orig_ub, obj, bbar, cbar;
+        std::vector<int> head, bind;
+        bool cbar_ok = false, bbar_ok = false;
+    } res;
     MatDev mat() const
     {
         MatDev M{};
@@ -216,6 +232,11 @@ struct gk_bfd {
     int valid = 0;
     int m = 0, ldb = 0;
     int upd_cnt = 0;
+    // product-form updates between re-inversions chosen by the engine (nfs_max
+    // left at its default): adapted to the reduced-cost / primal drift measured
+    // at every re-inversion (Spx::drift_adapt); 0 = not set yet
+    int upd_lim_adapt = 0;
+    unsigned long long fact_ver = 0;           // bumped whenever inv(B) is rebuilt or updated outside a solve
     int ext_upd = 0;                           // updated through gk_bfd_update since the last re-inversion
     int prof = 0;                              // gk_bfd_profile
     DBuf<double> Binv;
@@ -313,6 +334,7 @@ static int reinvert_core(gk_bfd *f, const BasisSplit &bs, const MatDev *Adense, 
         HIPCHK(hipMemcpyAsync(&flag, f->flag.p, sizeof(int), hipMemcpyDeviceToHost, s));
         HIPCHK(hipStreamSynchronize(s));
         if (flag) {
+            f->fact_ver++;
             f->valid = 0;
             f->stats.reinversions++;
             f->stats.seconds_reinvert += now_s() - t0;
@@ -324,6 +346,7 @@ static int reinvert_core(gk_bfd *f, const BasisSplit &bs, const MatDev *Adense, 
     }
     assemble_binv(s, f->Binv.p, m, f->ldb, k, ms, d_posJ, d_rowR, d_posS, d_rowS, f->CinvR.p, f->G.p);
     HIPCHK(hipStreamSynchronize(s));
+    f->fact_ver++;
     f->valid = 1;
     f->upd_cnt = 0;
     f->ext_upd = 0;
@@ -534,6 +557,12 @@ struct Spx {
     DState hs{};
     bool dinf_known = false;
     bool head_stale = false, vec_stale = false;
+    // the device's cbar / bbar equal a fresh eval_cbar / eval_bbar of the
+    // current device state (basis, costs, bounds, factor and list order):
+    // the evaluation is deterministic, so repeating it is skipped.  Cleared
+    // by pivots, re-inversion, list rebuilds, and cost / bound changes.
+    bool cbar_ok = false, bbar_ok = false;
+    int evals_skipped = 0;
 
     SpxDev dev() const
     {
@@ -672,6 +701,7 @@ struct Spx {
     }
     void push_bounds()
     {
+        bbar_ok = false;
         up(E->type, type, (size_t)m + n);
         up(E->lb, lb, (size_t)m + n);
         up(E->ub, ub, (size_t)m + n);
@@ -720,6 +750,7 @@ struct Spx {
     // eval_cbar (glpspx01.js:565): pi = inv(B') cB refined once, d_j = c_k - N_j' pi
     void eval_cbar()
     {
+        if (cbar_ok) { evals_skipped++; return; }
         const double t0 = now_s();
         struct T { gk_bfd *f; double t0; ~T() { f->stats.seconds_eval += now_s() - t0; } } tt{f, t0};
         SpxDev d = dev();
@@ -753,12 +784,14 @@ struct Spx {
         (void)d;
         down(cbar, E->cbar, n);
         sync();
+        cbar_ok = true;
     }
 
     // eval_beta (glpspx01.js:473): h = -N xN; beta = inv(B) h, refined once
     // (refine_ftran :251: beta += inv(B) (h - B beta))
     void eval_bbar()
     {
+        if (bbar_ok) { evals_skipped++; return; }
         const double t0 = now_s();
         struct T { gk_bfd *f; double t0; ~T() { f->stats.seconds_eval += now_s() - t0; } } tt{f, t0};
         SpxDev d = dev();
@@ -780,6 +813,7 @@ struct Spx {
         vec_axpy(s, beta, dd, 1.0, m);
         down(bbar, E->bbar, m);
         sync();
+        bbar_ok = true;
     }
 
     void rsub_into(double *y, const double *a);   // y = a - y
@@ -787,6 +821,7 @@ struct Spx {
     bool reinvert()
     {
         pull();
+        cbar_ok = bbar_ok = false;
         BasisSplit bs;
         if (!split_from_head(m, head.data(), bs)) {
             fact_ret = 1;                       // BFD_ESING
@@ -921,6 +956,7 @@ struct Spx {
     // primal: set_aux_obj / set_orig_obj / check_stab / check_feas (glpspx01.js:1373-1522)
     int set_aux_obj(double tol_bnd)
     {
+        cbar_ok = false;
         int cnt = 0;
         tol_bnd *= 0.90;
         for (int k = 1; k <= m + n; k++) coef[k] = 0.0;
@@ -940,6 +976,7 @@ struct Spx {
     }
     void set_orig_obj()
     {
+        cbar_ok = false;
         for (int i = 1; i <= m; i++) coef[i] = 0.0;
         for (int j = 1; j <= n; j++) coef[m + j] = zeta * obj[j];
         up(E->coef, coef, (size_t)m + n);
@@ -1077,6 +1114,45 @@ struct Spx {
         return 5;                          // GLP_EFAIL
     }
 
+    // ---- re-inversion interval from the measured drift --------------------
+    // At a re-inversion the host holds the incrementally updated values
+    // (dual: cbar, primal: bbar); the fresh evaluation right after it gives
+    // the drift D = max |updated - fresh| the chain accumulated.  The
+    // reference's stability checks fail at tol_dj (check_stab, glpspx02.js:
+    // 1410) / tol_bnd (glpspx01.js:1429) while Harris' pass 1 already relaxes
+    // by 0.3 of it; the chain is halved once D > tol / 20 and doubled again
+    // (up to the cap) while D < tol / 200.
+    int upd_cap = 0, upd_floor = 0;
+    bool sched_refact = false;                  // the batch stopped on the update limit
+    bool drift_armed = false;
+    int drift_upd = 0;
+    std::vector<double> drift_ref;
+    void drift_arm(const std::vector<double> &v, int st)
+    {
+        drift_armed = (st == 2 && hs.upd_cnt > 0 && upd_cap > upd_floor);
+        if (!drift_armed) return;
+        drift_ref = v;
+        drift_upd = hs.upd_cnt;
+    }
+    void drift_adapt(const std::vector<double> &fresh, int cnt, double tol)
+    {
+        if (!drift_armed) return;
+        drift_armed = false;
+        double D = 0.0;
+        for (int j = 1; j <= cnt; j++) D = std::max(D, std::fabs(fresh[j] - drift_ref[j]));
+        int lim = f->upd_lim_adapt > 0 ? f->upd_lim_adapt : upd_cap;
+        if (D > 0.05 * tol) lim = std::max(upd_floor, std::min(lim, drift_upd) / 2);
+        else if (D < 0.005 * tol && drift_upd >= lim) lim = std::min(upd_cap, 2 * lim);
+        static const bool log = std::getenv("GK_DRIFT_LOG") != nullptr;
+        if (log)
+            fprintf(stderr, "[gk drift] %s it %d: %d updates, drift %.3e (tol %.1e) -> interval %d\n",
+                    dual ? "dual" : "primal", hs.it_cnt, drift_upd, D, tol, lim);
+        f->upd_lim_adapt = lim;
+        hs.upd_lim = lim;
+    }
+
+    bool resident_match() const;
+    void save_resident();
     void init();
     void run_graph(const SpxDev &d, const DualPlan &pl, int K, int kind = 0);
     bool lists_stale = false;                   // rlist / rpos / nr to rebuild from the header
@@ -1132,6 +1208,47 @@ int Spx::reinvert_core_csc(const BasisSplit &bs)
 {
     // structural basis columns are -A columns of the device CSC
     return reinvert_core(f, bs, nullptr, 1, -1.0, E->cptr.p, E->cind.p, E->cval.p);
+}
+
+bool Spx::resident_match() const
+{
+    const Engine::Resident &R = E->res;
+    if (!R.ok || R.dual != dual || R.m != m || R.n != n) return false;
+    if (lp->a_version == 0 || lp->a_version != R.a_version) return false;
+    if (!f->valid || f->ext_upd || R.fact_ver != f->fact_ver || lists_stale) return false;
+    if (std::memcmp(&R.zeta, &zeta, sizeof zeta) != 0) return false;
+    auto same = [](const auto &a, const auto &b) {
+        return a.size() == b.size() && std::memcmp(a.data(), b.data(), a.size() * sizeof(a[0])) == 0;
+    };
+    if (!same(type, R.type) || !same(orig_type, R.orig_type) || !same(lb, R.lb) || !same(ub, R.ub) ||
+        !same(orig_lb, R.orig_lb) || !same(orig_ub, R.orig_ub) || !same(coef, R.coef) || !same(obj, R.obj))
+        return false;
+    for (int i = 1; i <= m; i++)
+        if (head[i] != R.head[i]) return false;
+    for (int j = 1; j <= n; j++) {
+        const int jo = R.bind[head[m + j]] - m;
+        if (jo < 1 || jo > n || stat[j] != R.stat[jo]) return false;
+    }
+    return true;
+}
+
+// after a normal return: the host mirrors (current after store_sol's pull)
+// become the resident record of what the device holds
+void Spx::save_resident()
+{
+    Engine::Resident &R = E->res;
+    R.ok = !head_stale && !vec_stale && !lists_stale && f->valid;
+    if (!R.ok) return;
+    R.dual = dual; R.m = m; R.n = n; R.nr = hs.nr;
+    R.a_version = lp->a_version;
+    R.fact_ver = f->fact_ver;
+    R.zeta = zeta;
+    R.type.swap(type); R.orig_type.swap(orig_type); R.stat.swap(stat);
+    R.lb.swap(lb); R.ub.swap(ub); R.coef.swap(coef); R.orig_lb.swap(orig_lb); R.orig_ub.swap(orig_ub);
+    R.obj.swap(obj); R.bbar.swap(bbar); R.cbar.swap(cbar);
+    R.head.swap(head); R.bind.swap(bind);
+    R.cbar_ok = cbar_ok;
+    R.bbar_ok = bbar_ok;
 }
 
 void Spx::init()
@@ -1193,14 +1310,39 @@ void Spx::init()
     ABI_REQUIRE(k == n, "gk_spx: basis header inconsistent with statuses (%d non-basic, n = %d)", k, n);
     for (int kk = 1; kk <= m + n; kk++) bind[head[kk]] = kk;
     engine_alloc(*E, m, n, ctx);
+    if (f->ext_upd) f->valid = 0;    // unit columns may be inexact after external updates
+    // the working set the last call left on the device, when it is this one
+    const bool keep = resident_match();
+    Engine::Resident &R = E->res;
+    R.ok = false;
     begin_up();
-    up(E->type, type, mn - 1); up(E->orig_type, orig_type, mn - 1);
-    up(E->lb, lb, mn - 1); up(E->ub, ub, mn - 1); up(E->orig_lb, orig_lb, mn - 1); up(E->orig_ub, orig_ub, mn - 1);
-    up(E->coef, coef, mn - 1); up(E->obj, obj, n);
+    if (!keep) {
+        up(E->type, type, mn - 1); up(E->orig_type, orig_type, mn - 1);
+        up(E->lb, lb, mn - 1); up(E->ub, ub, mn - 1); up(E->orig_lb, orig_lb, mn - 1); up(E->orig_ub, orig_ub, mn - 1);
+        up(E->coef, coef, mn - 1); up(E->obj, obj, n);
+    } else {
+        // the non-basic variables are numbered as init_csa numbers them
+        // (rows, then columns); the resident reduced costs follow them
+        cbar.assign(n + 1, 0.0);
+        for (int j = 1; j <= n; j++) cbar[j] = R.cbar[R.bind[head[m + j]] - m];
+        bbar = R.bbar;
+        up(E->cbar, cbar, n);
+    }
     up(E->head, head, mn - 1); up(E->bind, bind, mn - 1); up(E->stat, stat, n);
     flush_up();
-    // dense columns of inv(B): the non-basic slacks
-    {
+    if (keep) {
+        // the dense-column list of inv(B) stays as the pivots left it (its
+        // order is the order of the sums over it); the PSE reference space
+        // starts empty, as below
+        HIPCHK(hipMemsetAsync(E->wpos.p, 0xFF, (size_t)std::max(m, n) * sizeof(int), s));
+        hs = DState{};
+        hs.nr = R.nr;
+        hs.nwl = 0;
+        cbar_ok = R.cbar_ok;
+        bbar_ok = R.bbar_ok;
+        f->stats.resident = 1;
+    } else {
+        // dense columns of inv(B): the non-basic slacks
         std::vector<int> rl, rp(m, -1);
         for (int c = 1; c <= m; c++)
             if (bind[c] > m) {
@@ -1216,17 +1358,29 @@ void Spx::init()
         hs.nwl = 0;
         sync();
     }
-    if (f->ext_upd) f->valid = 0;    // unit columns may be inexact after external updates
     hs.phase = 0;
     hs.it_cnt = L->it_cnt;
     hs.zeta = zeta;
     hs.tol_bnd = parm->tol_bnd; hs.tol_dj = parm->tol_dj; hs.tol_piv = parm->tol_piv;
     hs.obj_ll = parm->obj_ll; hs.obj_ul = parm->obj_ul;
     hs.pricing = parm->pricing; hs.rtest = parm->r_test;
-    int lim = f->parm.nfs_max > 0 ? f->parm.nfs_max : 100;
-    // the dense inverse tolerates more product-form updates than the FT
-    // eta file; re-inversion cost grows with k^3, so scale the interval
-    lim = std::max(lim, std::min(1000, m / 4));
+    // the re-inversion interval.  The reference refactorizes after nfs_max
+    // Forrest-Tomlin updates (glpfhv.js:182-187, default 100).  An explicit
+    // nfs_max (any value but the default) is honoured exactly.  With the
+    // default the engine may lengthen the product-form chain of the dense
+    // inverse up to min(1000, m/4) — re-inversion grows with k^3 — as long as
+    // the drift of the updated values against a fresh evaluation, measured at
+    // every re-inversion, stays far below the tolerances the reference's own
+    // checks use (drift_adapt); a chain whose drift grows is shortened
+    const int nfs = f->parm.nfs_max > 0 ? f->parm.nfs_max : 100;
+    int lim = nfs;
+    if (nfs == 100) {
+        upd_cap = std::max(nfs, std::min(1000, m / 4));
+        if (f->upd_lim_adapt <= 0) f->upd_lim_adapt = upd_cap;
+        lim = std::min(std::max(f->upd_lim_adapt, nfs), upd_cap);
+    } else
+        upd_cap = nfs;
+    upd_floor = nfs;
     hs.upd_lim = lim;
     // the product-form updates of the factor persist across calls, as the
     // reference's FT eta count does in lp.bfd (glpfhv.js:182): a run of short
@@ -1316,7 +1470,10 @@ int Spx::batch(int K, int rigorous)
             f->stats.trow_launches++;
         }
     }
-    if (hs.npiv > 0) head_stale = vec_stale = true;
+    if (hs.npiv > 0) {
+        head_stale = vec_stale = true;
+        cbar_ok = bbar_ok = false;
+    }
     // a stop on the budget leaves the top kernel of the next iteration unrun
     return hs.stop == ST_RUN ? ST_BATCH : hs.stop;
 }
@@ -1326,6 +1483,7 @@ int Spx::batch(int K, int rigorous)
 void Spx::rebuild_lists()
 {
     pull();
+    cbar_ok = bbar_ok = false;                  // the list order sets the order of the sums
     std::vector<int> rl, rp(m, -1);
     for (int c = 1; c <= m; c++)
         if (bind[c] > m) {
@@ -1418,6 +1576,9 @@ int Spx::run_dual()
     int ret;
     for (;;) {
         if (binv_st == 0) {
+            pull();
+            drift_arm(cbar, sched_refact ? cbar_st : 0);
+            sched_refact = false;
             if (!reinvert()) {
                 report_msg(GK_MSG_FACTERR, 1, fact_ret);     // GLP_MSG_ERR
                 return fail_return();
@@ -1431,6 +1592,7 @@ int Spx::run_dual()
             dinf_known = false;
             pull();
             eval_cbar();
+            drift_adapt(cbar, n, P->tol_dj);
             cbar_st = 1;
             if (phase == 0) {
                 if (dual_check_feas(0.90 * P->tol_dj) != 0) { phase = 1; set_aux_bnds(); }
@@ -1553,6 +1715,7 @@ int Spx::run_dual()
             break;
         case ST_REFACT:
             binv_st = 0;
+            sched_refact = true;
             break;
         case ST_P0:
             if (bbar_st != 1 || cbar_st != 1) {
@@ -1610,6 +1773,9 @@ int Spx::run_primal()
     int binv_st = f->valid ? 2 : 0, bbar_st = 0, cbar_st = 0, rigorous = 0;
     for (;;) {
         if (binv_st == 0) {
+            pull();
+            drift_arm(bbar, sched_refact ? bbar_st : 0);
+            sched_refact = false;
             if (!reinvert()) {
                 report_msg(GK_MSG_FACTERR, 1, fact_ret);     // GLP_MSG_ERR
                 return fail_return();
@@ -1622,6 +1788,7 @@ int Spx::run_primal()
         if (bbar_st == 0) {
             pull();
             eval_bbar();
+            drift_adapt(bbar, m, P->tol_bnd);
             bbar_st = 1;
             if (phase == 0) {
                 if (set_aux_obj(P->tol_bnd) > 0) phase = 1;
@@ -1708,6 +1875,7 @@ int Spx::run_primal()
             break;
         case ST_REFACT:
             binv_st = 0;
+            sched_refact = true;
             break;
         case ST_Q0:
             if (bbar_st != 1 || cbar_st != 1) {
@@ -2055,6 +2223,7 @@ int gk_bfd_update(gk_bfd *f, int j, int len, const int *ind, int idx, const doub
         binv_rank1(s, f->Binv.p, m, f->ldb, f->G.p, f->vecy.p, j);
         HIPCHK(hipStreamSynchronize(s));
         f->upd_cnt++;
+        f->fact_ver++;
         f->ext_upd = 1;
         return 0;
     } catch (const AbiError &e) {
@@ -2087,6 +2256,8 @@ static int spx_entry(gk_ctx *ctx, gk_lp *lp, gk_bfd *f, const gk_smcp *parm, int
         lp->valid = 0;
         int ret = dual ? S.run_dual() : S.run_primal();
         f->upd_cnt = S.hs.upd_cnt;
+        f->stats.evals_skipped = S.evals_skipped;
+        if (ret == 0 || (ret >= 6 && ret <= 9)) S.save_resident();
         f->stats.seconds_total = now_s() - t0;
         return ret;
     } catch (const AbiError &e) {

@@ -97,7 +97,8 @@ class SpxStats(C.Structure):
                 ("seconds_init", C.c_double), ("seconds_eval", C.c_double), ("seconds_batches", C.c_double),
                 ("trow_ms", C.c_double), ("trow_launches", C.c_longlong), ("trow_bytes", C.c_double),
                 ("trow_dev_ms", C.c_double), ("trow_dev_launches", C.c_longlong), ("trow_dev_ms_b", C.c_double),
-                ("trow_dev_ms_r", C.c_double), ("trow_dev_launches_r", C.c_longlong)]
+                ("trow_dev_ms_r", C.c_double), ("trow_dev_launches_r", C.c_longlong),
+                ("resident", C.c_int), ("evals_skipped", C.c_int)]
 
 
 _lib = None

@@ -188,6 +188,8 @@ typedef struct {
     double trow_dev_ms_r;       /* same, from the last block exit of the kernel before them to their
                                    own last block exit (a profiler's per-dispatch bracket) */
     long long trow_dev_launches_r;
+    int resident;               /* 1: the call found its working set resident (no re-upload) */
+    int evals_skipped;          /* eval_cbar / eval_bbar calls whose result was already resident */
 } gk_spx_stats;
 void gk_bfd_last_stats(const gk_bfd *bfd, gk_spx_stats *st);
 /* record HIP events around the pivot-row kernel of every dual pivot (benches) */
