@@ -26,8 +26,9 @@ sys.path.insert(0, ROOT)
 import __graft_entry__  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
-ROOF_KERNEL = "k_dual_row"
-ROUND = "r02"
+ROOF_KERNEL = "k_dual_update"
+ROW_KERNEL = "k_dual_row"
+ROUND = "r03"
 # the C port (oracle/) against the reference itself, both on one core of the
 # build container on C3 from the slack basis: the port 285.8 pivots/s over a
 # 20 s window (6,874 pivots, init_csa included), the reference node 9.4
@@ -52,16 +53,19 @@ def load_profile(args):
         return out
     out["source"] = f"profiles/{ROUND}_kernel_stats_timed.json, profiles/{ROUND}_pmc_traffic.json " \
                     f"(command: {meta.get('cmd')}; head {meta.get('head')})"
-    try:
-        out["rocprof_ms"] = round(json.load(open(os.path.join(ROOT, "profiles", f"{ROUND}_kernel_stats_timed.json")))
-                                  [ROOF_KERNEL]["avg_ns"] / 1e6, 5)
-    except Exception:
-        pass
-    try:
-        out["traffic"] = json.load(open(os.path.join(ROOT, "profiles", f"{ROUND}_pmc_traffic.json")))[
-            "kernels"][ROOF_KERNEL]["bytes_per_launch"]
-    except Exception:
-        pass
+    for kern in (ROOF_KERNEL, ROW_KERNEL):
+        try:
+            stats = json.load(open(os.path.join(ROOT, "profiles", f"{ROUND}_kernel_stats_timed.json")))
+            key = next(k for k in stats if k.startswith(kern))
+            out.setdefault(kern, {})["rocprof_ms"] = round(stats[key]["avg_ns"] / 1e6, 5)
+        except Exception:
+            pass
+        try:
+            tr = json.load(open(os.path.join(ROOT, "profiles", f"{ROUND}_pmc_traffic.json")))["kernels"]
+            key = next(k for k in tr if k.startswith(kern))
+            out.setdefault(kern, {})["traffic"] = tr[key]["bytes_per_launch"]
+        except Exception:
+            pass
     return out
 
 
@@ -148,6 +152,17 @@ def main():
 
     for _ in range(args.warmup):
         step()
+    # the basis the timed region starts from: the roofline and cross-check
+    # passes below replay the same window of pivots from it
+    saved = (P.row_stat.copy(), P.col_stat.copy(), P.it_cnt)
+
+    def rewind():
+        P.row_stat[:] = saved[0]
+        P.col_stat[:] = saved[1]
+        P.it_cnt = saved[2]
+        P.valid = 0
+        assert P.factorize() == 0
+
     ctx.mark(1)                         # timed region starts (kernel-trace window)
     barrier()
     t0 = time.perf_counter()
@@ -155,7 +170,6 @@ def main():
     split = {"init": 0.0, "eval": 0.0, "batches": 0.0, "reinvert": 0.0, "total": 0.0}
     reinv = 0
     resident, skipped = 0, 0
-    dev = {"ms": 0.0, "ms_b": 0.0, "launches": 0, "bytes": 0.0, "ms_r": 0.0, "launches_r": 0, "bytes_pivots": 0.0}
     for _ in range(args.steps):
         piv += step()
         s_ = P.stats()
@@ -167,17 +181,34 @@ def main():
         reinv += s_.reinversions
         resident += s_.resident
         skipped += s_.evals_skipped
-        dev["ms"] += s_.trow_dev_ms
-        dev["ms_b"] += s_.trow_dev_ms_b
-        dev["launches"] += s_.trow_dev_launches
-        dev["bytes"] += s_.trow_bytes
-        dev["ms_r"] += s_.trow_dev_ms_r
-        dev["launches_r"] += s_.trow_dev_launches_r
-        dev["bytes_pivots"] += s_.bytes_pivots
     barrier()
     dt = time.perf_counter() - t0
     ctx.mark(2)                         # timed region ends
     st = P.stats()
+
+    # roofline pass: the same steps again (continuing), with the pivot
+    # kernels' device-clock stamps and byte accounting on (gk_bfd_profile(4):
+    # stores and a reduction on every pivot's critical path, so never inside
+    # the timed region), graphs kept as in the timed region
+    dev = {"ms": 0.0, "ms_b": 0.0, "launches": 0, "bytes": 0.0, "ms_r": 0.0, "launches_r": 0, "bytes_pivots": 0.0,
+           "upd_ms": 0.0, "upd_launches": 0, "upd_bytes": 0.0, "pivots": 0}
+    if rank == 0:
+        rewind()
+        P.profile(4)
+        for _ in range(args.steps):
+            dev["pivots"] += step("roofline pass")
+            s_ = P.stats()
+            dev["ms"] += s_.trow_dev_ms
+            dev["ms_b"] += s_.trow_dev_ms_b
+            dev["launches"] += s_.trow_dev_launches
+            dev["bytes"] += s_.trow_bytes
+            dev["ms_r"] += s_.trow_dev_ms_r
+            dev["launches_r"] += s_.trow_dev_launches_r
+            dev["bytes_pivots"] += s_.bytes_pivots
+            dev["upd_ms"] += s_.upd_dev_ms
+            dev["upd_launches"] += s_.upd_dev_launches
+            dev["upd_bytes"] += s_.upd_bytes
+        P.profile(0)
 
     # cross-check pass: the same number of steps again with HIP events
     # recorded on the engine stream around every pivot-row kernel (eager
@@ -185,6 +216,7 @@ def main():
     # captured graphs); the event interval includes the launch gap
     trow = {"ms": 0.0, "launches": 0, "bytes": 0.0}
     if rank == 0:
+        rewind()
         P.profile(True)
         for _ in range(args.steps):
             step("events cross-check")
@@ -204,14 +236,19 @@ def main():
         max_dt = float(t.item())
     value = tot_piv / max_dt
 
-    # roofline of the dominant kernel, k_dual_row (chuzr, rho, the pivot row
-    # over the rows of AT in the support of rho, Harris pass-1 candidates),
-    # timed live over every launch of the timed region with the device wall
-    # clock (s_memrealtime, stamped inside the captured graphs): from the last
-    # block exit of the kernel before it to its own last block exit — the
-    # bracket of a profiler's per-dispatch record (rocprofv3 --kernel-trace
-    # start/end).  Algorithmic bytes per launch = 8 * |supp rho| * n
-    # (DESIGN.md §4), accumulated on the device for the same launches.
+    # roofline of the dominant kernel, k_dual_update (pass-2 choice, FTRAN
+    # of the entering column and the PSE vector over the dense columns of
+    # inv(B), the product-form update of those entries, update_bbar / cbar /
+    # gamma and the next chuzr candidates: 31% of the pivot's kernel time),
+    # and beside it k_dual_row (chuzr, rho, the pivot row over the rows of AT
+    # in the support of rho), both timed live in the roofline pass with the
+    # device wall clock (s_memrealtime, stamped inside the captured graphs):
+    # k_dual_update from its block 0's entry to its last block exit;
+    # k_dual_row from the last block exit of the kernel before it to its own
+    # last block exit (a profiler's per-dispatch bracket).  Algorithmic bytes
+    # per launch are accumulated on the device for the same launches
+    # (16 m ns + 64 m + 29 n for k_dual_update, 8 ns n for
+    # k_dual_row).
     roof = None
     kern = {}
     if rank == 0:
@@ -220,9 +257,13 @@ def main():
             ms_k, b_k = P.time_kernel(which, reps=10)
             kern[name] = {"ms": round(ms_k, 5), "bytes": b_k, "GBps": round(b_k / (ms_k * 1e-3) / 1e9, 1)}
         nl = max(1, dev["launches"])
-        b = dev["bytes"] / nl
+        b_row = dev["bytes"] / nl
         nr_ = max(1, dev["launches_r"])
-        ms = dev["ms_r"] / nr_
+        ms_row = dev["ms_r"] / nr_
+        ach_row = b_row / (ms_row * 1e-3) / 1e9 if ms_row > 0 else 0.0
+        nu = max(1, dev["upd_launches"])
+        b = dev["upd_bytes"] / max(1, dev["pivots"])
+        ms = dev["upd_ms"] / nu
         achieved = b / (ms * 1e-3) / 1e9 if ms > 0 else 0.0
         ne = max(1, trow["launches"])
         # the committed profiles of this same command (tools/profile_round.sh
@@ -231,30 +272,44 @@ def main():
         # region, and HBM bytes per launch from the --pmc FETCH_SIZE /
         # WRITE_SIZE passes; used only when the profiled command matches
         prof = load_profile(args)
-        step_bytes = dev["bytes_pivots"]
-        step_gbps = step_bytes / max_dt / 1e9 if max_dt > 0 else 0.0
+        pu, pr = prof.get(ROOF_KERNEL, {}), prof.get(ROW_KERNEL, {})
+        # the whole pivot (all kernels): the roofline pass's algorithmic bytes
+        # per pivot times the timed region's pivots over its time
+        step_bpp = dev["bytes_pivots"] / max(1, dev["pivots"])
+        step_gbps = step_bpp * piv / max_dt / 1e9 if max_dt > 0 else 0.0
         roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4),
-                "traffic": prof.get("traffic"),
-                "traffic_over_algorithmic": round(prof["traffic"] / b, 3) if prof.get("traffic") else None,
-                "kernel": ROOF_KERNEL + " (chuzr, rho = row p of inv(B), pivot row trow = -rho' N over the rows "
-                                        "of A in the support of rho, ratio-test candidates: one kernel)",
-                "ms_per_launch": round(ms, 5), "launches": dev["launches_r"],
+                "traffic": pu.get("traffic"),
+                "traffic_over_algorithmic": round(pu["traffic"] / b, 3) if pu.get("traffic") else None,
+                "kernel": ROOF_KERNEL + " (pass-2 choice, FTRAN of the entering column and the PSE vector over the "
+                                        "dense columns of inv(B), their product-form update, update_bbar/cbar/gamma, "
+                                        "next chuzr candidates: one kernel)",
+                "ms_per_launch": round(ms, 5), "launches": dev["upd_launches"],
                 "bytes_per_launch": round(b),
-                "timing": "device wall clock over every launch of the timed region: last block exit of the kernel "
-                          "before it to its own last block exit (a profiler's per-dispatch bracket)",
-                "entry_to_next_entry_ms": round(dev["ms_b"] / nl, 5),
-                "exec_ms_per_launch": round(dev["ms"] / nl, 5),
-                "rocprof_ms_per_launch": prof.get("rocprof_ms"),
-                "rocprof_frac": round(b / (prof["rocprof_ms"] * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
-                if prof.get("rocprof_ms") else None,
+                "timing": "device wall clock over every launch of the roofline pass (the timed region's steps "
+                          "repeated with kernel stamps on): block 0 entry to the last block exit",
+                "rocprof_ms_per_launch": pu.get("rocprof_ms"),
+                "rocprof_frac": round(b / (pu["rocprof_ms"] * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
+                if pu.get("rocprof_ms") else None,
                 "profile_source": prof.get("source"),
-                "hip_events_cross_check": {"ms_per_launch": round(trow["ms"] / ne, 5), "launches": trow["launches"],
+                "pivot_row_kernel": {
+                    "kernel": ROW_KERNEL + " (chuzr, rho = row p of inv(B), pivot row trow = -rho' N over the rows of "
+                                           "A in the support of rho, ratio-test candidates)",
+                    "achieved": round(ach_row, 1), "frac": round(ach_row / HBM_PEAK_GBS, 4),
+                    "ms_per_launch": round(ms_row, 5), "launches": dev["launches_r"],
+                    "bytes_per_launch": round(b_row), "traffic": pr.get("traffic"),
+                    "traffic_over_algorithmic": round(pr["traffic"] / b_row, 3) if pr.get("traffic") else None,
+                    "rocprof_ms_per_launch": pr.get("rocprof_ms"),
+                    "timing": "last block exit of the kernel before it to its own last block exit",
+                    "entry_to_next_entry_ms": round(dev["ms_b"] / nl, 5),
+                    "exec_ms_per_launch": round(dev["ms"] / nl, 5)},
+                "hip_events_cross_check": {"kernel": ROW_KERNEL, "ms_per_launch": round(trow["ms"] / ne, 5),
+                                           "launches": trow["launches"],
                                            "bytes_per_launch": round(trow["bytes"] / ne),
-                                           "note": "second pass, eager launches, interval includes launch gap"},
-                # the whole pivot (all kernels) against the same peak
+                                           "note": "third pass, eager launches, HIP events on the engine stream "
+                                                   "around the kernel; the interval includes the launch gap"},
                 "step_achieved": round(step_gbps, 1), "step_frac": round(step_gbps / HBM_PEAK_GBS, 4),
-                "step_bytes_per_pivot": round(step_bytes / max(1, piv))}
+                "step_bytes_per_pivot": round(step_bpp)}
 
     cpu = None
     extra = {}
@@ -310,7 +365,7 @@ def main():
             "roofline": roof,
             "cpu_baseline": cpu,
             "engine": {"ms_split_per_step": {k: round(1000.0 * v / args.steps, 3) for k, v in split.items()},
-                       "bytes_per_pivot_last_step": round(st.bytes_pivots / max(1, st.pivots)),
+                       "bytes_per_pivot_roofline_pass": round(dev["bytes_pivots"] / max(1, dev["pivots"])),
                        "graphs_built_last_step": int(st.graphs_built),
                        "pivots": int(st.pivots), "reinversions_timed_region": reinv,
                        "batches": int(st.batches), "host_syncs": int(st.host_syncs),
@@ -417,6 +472,7 @@ def run_mid(gk, problems, ctx, c3, start=100000, steps=10):
     t_adv = time.perf_counter() - t0
     parm = gk.SMCP(meth=gk.GLP_DUAL, it_lim=100, msg_lev=gk.GLP_MSG_ERR)
     gk.glp_simplex(P, parm)
+    P.profile(4)                        # byte accounting on (the window's algorithmic bytes)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     piv, byts = 0, 0.0

@@ -750,7 +750,7 @@ __global__ void __launch_bounds__(1024) k_trow_rows(SpxDev d, int pse)
             if (w + u * nw < ns) acc += v0[u] * a[u];
     }
     if (stop) return;
-    if (blockIdx.x == 0 && threadIdx.x == 0) st->tk_start = wall_clock64();
+    if (d.tslots && blockIdx.x == 0 && threadIdx.x == 0) st->tk_start = wall_clock64();
     TPH(1, 0);
     {
         int t = w + 8 * nw;
@@ -805,7 +805,7 @@ __global__ void __launch_bounds__(1024) k_trow_rows(SpxDev d, int pse)
         tmax_part(d)[blockIdx.x] = bmax;
         if (pse) d.gpart[blockIdx.x] = g;
         cand_pass1(d)[blockIdx.x] = b;
-        d.tslots[blockIdx.x] = wall_clock64();
+        if (d.tslots) d.tslots[blockIdx.x] = wall_clock64();
     }
 }
 
@@ -864,7 +864,7 @@ __global__ void __launch_bounds__(1024) k_dual_row(SpxDev d, int pse, int nr_cap
     if (w != 0 || idx >= n) pos1 = 0;
     if (w != 0 || idx >= m) pos2 = 0;
     if (stop) return;
-    if (lead && threadIdx.x == 0) st->tk_start = wall_clock64();
+    if (d.tslots && lead && threadIdx.x == 0) st->tk_start = wall_clock64();
     // ---- decisions (identical in every block)
     const TopState ts = fin.t;
     int why = ST_RUN;
@@ -1040,7 +1040,7 @@ __global__ void __launch_bounds__(1024) k_dual_row(SpxDev d, int pse, int nr_cap
         tmax_part(d)[blockIdx.x] = bmax;
         if (pse) d.gpart[blockIdx.x] = g;
         cand_pass1(d)[blockIdx.x] = b;
-        d.tslots[blockIdx.x] = wall_clock64();
+        if (d.tslots) d.tslots[blockIdx.x] = wall_clock64();
     }
 }
 
@@ -1105,7 +1105,7 @@ __global__ void __launch_bounds__(256) k_dual_col(SpxDev d, int pse, int nr_cap,
         cpub[u] = (t < nr_cap) ? d.rlist[t] : 0;
     }
     if (stop) return;
-    if (lead && threadIdx.x == 0) st->tk_start = wall_clock64();
+    if (d.tslots && lead && threadIdx.x == 0) st->tk_start = wall_clock64();
     // ---- decisions (identical in every wave)
     const TopState ts = fin.t;
     int why = ST_RUN;
@@ -1232,7 +1232,7 @@ __global__ void __launch_bounds__(256) k_dual_col(SpxDev d, int pse, int nr_cap,
         tmax_part(d)[grp] = bmax;
         if (pse) d.gpart[grp] = g;
         cand_pass1(d)[grp] = b;
-        d.tslots[grp] = wall_clock64();
+        if (d.tslots) d.tslots[grp] = wall_clock64();
     }
 }
 
@@ -1351,7 +1351,11 @@ __global__ void __launch_bounds__(256) k_dual_ratio(SpxDev d, int gn, int tiles_
         return;
     }
     const int lane = threadIdx.x & 63;
-    const unsigned long long t_entry = (rowpath && blockIdx.x == 0 && threadIdx.x == 0) ? wall_clock64() : 0ull;
+    // roofline stamps (benches only: d.tslots set): the span of the pivot-row
+    // kernel and of the previous pivot's k_dual_update, reduced from the
+    // per-block exit stamps by block 0's first wave
+    const bool stamps = d.tslots != nullptr;
+    const unsigned long long t_entry = (stamps && rowpath && blockIdx.x == 0 && threadIdx.x == 0) ? wall_clock64() : 0ull;
     const RatioIn rin = ratio_in(st);
     const int j = blockIdx.x * blockDim.x + threadIdx.x;
     const int jc = min(j, n - 1);
@@ -1369,8 +1373,12 @@ __global__ void __launch_bounds__(256) k_dual_ratio(SpxDev d, int gn, int tiles_
         cl[u] = cand_pass1(d)[b];
         tv[u] = tmax_part(d)[b];
     }
-    unsigned long long e = 0, xp = 0;
-    if (rowpath && lead) {
+    unsigned long long e = 0, xp = 0, u0 = 0;
+    double uticks = 0.0, un = 0.0;
+    if (stamps && rowpath && lead) {
+        u0 = st->tk_upd0;
+        uticks = st->upd_ticks;
+        un = st->upd_n;
         unsigned long long te[CPL], tx[4];
 #pragma unroll
         for (int u = 0; u < CPL; ++u) te[u] = d.tslots[min(lane + u * 64, ncb - 1)];
@@ -1397,13 +1405,20 @@ __global__ void __launch_bounds__(256) k_dual_ratio(SpxDev d, int gn, int tiles_
     if (lead) {
         // publish max |trow| and the end of the pivot-row kernel (latest
         // block exit stamp), and the last exit of the kernel before it
-        const unsigned long long ee = wmax_u64(e), xx = wmax_u64(xp);
+        const unsigned long long ee = stamps ? wmax_u64(e) : 0ull, xx = stamps ? wmax_u64(xp) : 0ull;
         if (lane == 0) {
             st->trow_max_bits = dbits(big);
-            if (rowpath) {
+            if (stamps && rowpath) {
                 st->tk_next = t_entry;
                 st->tk_end = ee;
                 st->tk_prev = xx;
+                // the previous pivot's k_dual_update: entry of its block 0 to
+                // its last block exit (not across a batch boundary)
+                if (u0 != 0ull && xx > u0 && xx - u0 < 20000ull) {
+                    st->upd_ticks = uticks + (double)(xx - u0);
+                    st->upd_n = un + 1.0;
+                }
+                st->tk_upd0 = 0ull;
             }
         }
     }
@@ -1833,7 +1848,7 @@ __global__ void __launch_bounds__(256) k_dual_commit(SpxDev d, int pse, int nvb,
         }
         const int binv_fresh = st->binv_fresh, rig = st->rigorous, phase = st->phase, refct = st->refct;
         const double delta = st->delta, new_dq = st->new_dq, gamma_p = st->gamma_pq, eta_p = st->eta_pq;
-        const double tol_bnd = st->tol_bnd, tol_dj = st->tol_dj;
+        const double tol_bnd = st->tol_bnd, tol_dj = st->tol_dj, upd_tol = st->upd_tol;
         if (stop) return;
         const bool bad = fabs(piv1 - piv2) > 1e-8 * (1.0 + fabs(piv1)) ||
                          !((piv1 > 0.0 && piv2 > 0.0) || (piv1 < 0.0 && piv2 < 0.0));
@@ -1894,6 +1909,12 @@ __global__ void __launch_bounds__(256) k_dual_commit(SpxDev d, int pse, int nvb,
             const Cand b = wave_best<0>(c);
             if ((threadIdx.x & 63) == 0) cand_chuzr(d)[blockIdx.x * 4 + (threadIdx.x >> 6)] = b;
             TPH(4, 1);
+            // growth check of the product-form update (see k_dual_update)
+            const bool grow = in_m && i != p - 1 && fabs(ti) * upd_tol > fabs(tp);
+            if (__any(grow) && (threadIdx.x & 63) == 0) {
+                atomicOr(&st->refact_pending, 1);
+                atomicAdd(&st->echk, 1);
+            }
         }
         if (phase == 1) {
             const double tol = tol_dj;
@@ -1947,7 +1968,7 @@ __global__ void __launch_bounds__(256) k_dual_commit(SpxDev d, int pse, int nvb,
             const double rowb = rowpath == 1 ? 8.0 * (double)ns * n
                                 : rowpath == 2 ? 12.0 * (double)d.A.nnz : 8.0 * (double)m * n;
             const unsigned long long tk0 = st->tk_start, tk1 = st->tk_end, tk2 = st->tk_next, tkp = st->tk_prev;
-            if (rowpath && tk1 > tk0) {
+            if (d.tslots && rowpath && tk1 > tk0) {
                 st->bytes_trow += rowb;
                 st->trow_ticks += (double)(tk1 - tk0);
                 st->trow_ticks_b += (double)(tk2 - tk0);
@@ -2097,7 +2118,7 @@ __device__ __forceinline__ PickOut pick_choose(const PickIn &pi)
 struct Books {
     int nwl0, rlast, wlast, rq, wq;
     unsigned long long tk0, tk1, tk2, tkp;
-    double ab, abt, att, attb, atn, attr, atnr;
+    double ab, abt, att, attb, atn, attr, atnr, abu;
 };
 
 template <int NRHS>
@@ -2110,12 +2131,12 @@ __device__ __forceinline__ void books_load(const SpxDev &d, Books &b, int nr, in
     const int wlast = (NRHS == 2) ? d.wlist[max(nwl0 - 1, 0)] : 0;
     const int rq = d.rpos[min(kqc, m) - 1];
     const int wq = (NRHS == 2) ? d.wpos[min(max(kqc - m, 1), n) - 1] : -1;
-    const unsigned long long tk0 = st->tk_start, tk1 = st->tk_end, tk2 = st->tk_next, tkp = st->tk_prev;
-    const double ab = st->bytes, abt = st->bytes_trow, att = st->trow_ticks, attb = st->trow_ticks_b;
-    const double atn = st->trow_n, attr = st->trow_ticks_r, atnr = st->trow_nr;
     b.nwl0 = nwl0; b.rlast = rlast; b.wlast = wlast; b.rq = rq; b.wq = wq;
-    b.tk0 = tk0; b.tk1 = tk1; b.tk2 = tk2; b.tkp = tkp;
-    b.ab = ab; b.abt = abt; b.att = att; b.attb = attb; b.atn = atn; b.attr = attr; b.atnr = atnr;
+    if (d.tslots) {                           // byte / clock accounting: benches only
+        b.tk0 = st->tk_start; b.tk1 = st->tk_end; b.tk2 = st->tk_next; b.tkp = st->tk_prev;
+        b.ab = st->bytes; b.abt = st->bytes_trow; b.att = st->trow_ticks; b.attb = st->trow_ticks_b;
+        b.atn = st->trow_n; b.attr = st->trow_ticks_r; b.atnr = st->trow_nr; b.abu = st->bytes_upd;
+    }
 }
 
 template <int NRHS>
@@ -2146,10 +2167,15 @@ __device__ __forceinline__ void books_store(const SpxDev &d, const Books &b, int
         d.wpos[win ? kp - m - 1 : dw] = nw1;
         st->nwl = nw1 + (win ? 1 : 0);
     }
-    // the pivot row, A w, and inv(B) read once and written once over the
-    // support of rho; the device-clock spans of the pivot-row kernel, from
-    // its entry and from the last exit of the kernel before it (the previous
-    // pivot's commit / update; not the first pivot of a batch)
+    if (!d.tslots) return;
+    // (benches) the pivot row, A w, and inv(B) read once and written once
+    // over the support of rho; the device-clock spans of the pivot-row
+    // kernel, from its entry and from the last exit of the kernel before it
+    // (the previous pivot's commit / update; not the first pivot of a batch);
+    // k_dual_update's own algorithmic bytes: the touched entries of inv(B)
+    // read and written (16 m ns), h = -N[q] and the PSE work vector, the
+    // O(m) row vectors (head, bbar, gamma, tcol, type, bounds) and the O(n)
+    // column vectors (cbar read + write, trow, head, orig_type)
     const double rowb = rowpath == 1 ? 8.0 * (double)ns * n
                         : rowpath == 2 ? 12.0 * (double)d.A.nnz : 8.0 * (double)m * n;
     const bool tm = rowpath && b.tk1 > b.tk0;
@@ -2162,6 +2188,7 @@ __device__ __forceinline__ void books_store(const SpxDev &d, const Books &b, int
     st->trow_nr = tr ? b.atnr + 1.0 : b.atnr;
     st->tk_end = 0;
     st->bytes = b.ab + (rowb + 8.0 * (double)m * b.nwl0 + 16.0 * (double)m * ns + bytes_fixed);
+    st->bytes_upd = b.abu + (16.0 * (double)m * ns + 16.0 * (double)m + 48.0 * (double)m + 29.0 * (double)n);
 }
 
 template <int NRHS, int SP, int GM, int RPB>
@@ -2170,6 +2197,7 @@ __global__ void __launch_bounds__(1024) k_dual_update(SpxDev d, int gn, int ncb,
 {
     const TraceScope trace_(d, 3);
     const ExitStamp xs_(d.xslots, blockIdx.x);
+    if (d.tslots && blockIdx.x == 0 && threadIdx.x == 0) d.st->tk_upd0 = wall_clock64();
     constexpr int SL = 64 / RPB;
     __shared__ double sp[NRHS][16][64];
     __shared__ double srow[NRHS][RPB];
@@ -2210,7 +2238,7 @@ __global__ void __launch_bounds__(1024) k_dual_update(SpxDev d, int gn, int ncb,
     const int nr = st->nr, ns = st->ns, p = max(st->p, 1), kp = max(st->kp, 1);
     const double delta = st->delta;
     const int binv_fresh = st->binv_fresh, rig = st->rigorous, phase = st->phase, refct = st->refct;
-    const double tol_bnd = st->tol_bnd, tol_dj = st->tol_dj;
+    const double tol_bnd = st->tol_bnd, tol_dj = st->tol_dj, upd_tol = st->upd_tol;
     int c0[GM];
     double rv[GM];
 #pragma unroll
@@ -2457,6 +2485,17 @@ __global__ void __launch_bounds__(1024) k_dual_update(SpxDev d, int gn, int ncb,
         }
         const Cand best = wave_best<0>(cnd);
         if (lane == 0) cand_chuzr(d)[blockIdx.x] = best;
+        // growth of the product-form update: row i of the new inverse gains
+        // tcol_i / alpha_p times row p, so a pivot with |alpha_p| < upd_tol
+        // |tcol_i| amplifies the inverse's error by more than 1 / upd_tol —
+        // the explicit inverse's counterpart of the Forrest-Tomlin check
+        // |u_k2k2| < upd_tol max |u| (glpfhv.js:436-442): re-invert before
+        // the next pivot (refact_pending ends the batch there)
+        const bool grow = rowlane && r != p - 1 && fabs(ti) * upd_tol > fabs(tp);
+        if (__any(grow) && lane == 0) {
+            atomicOr(&st->refact_pending, 1);
+            atomicAdd(&st->echk, 1);
+        }
     }
     TPH(3, 5);
     // ---- columns: update_cbar (:1020), check_feas of phase I (:1296)

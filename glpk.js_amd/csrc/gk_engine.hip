@@ -186,6 +186,14 @@ struct Engine {
         std::vector<int> head, bind;
         bool cbar_ok = false, bbar_ok = false;
     } res;
+    // host mirror vectors of the last call, kept for their capacity: a call
+    // assigns into them instead of allocating (and page-faulting) ~20 arrays
+    // of m + n entries each time
+    struct Spare {
+        std::vector<signed char> type, orig_type, stat;
+        std::vector<double> lb, ub, coef, orig_lb, orig_ub, obj, bbar, cbar, gamma;
+        std::vector<int> head, bind;
+    } spare;
     MatDev mat() const
     {
         MatDev M{};
@@ -406,10 +414,13 @@ static void engine_alloc(Engine &E, int m, int n, gk_ctx *ctx)
         auto layout = [&]() {
             off = 0;
             place(E.st, 1);
-            place(E.type, mn); place(E.orig_type, mn); place(E.refsp, mn); place(E.stat, n);
-            place(E.lb, mn); place(E.ub, mn); place(E.coef, mn); place(E.orig_lb, mn); place(E.orig_ub, mn);
-            place(E.obj, n); place(E.head, mn); place(E.bind, mn);
-            place(E.bbar, m); place(E.cbar, n); place(E.gamma, std::max(m, n));
+            place(E.type, mn); place(E.orig_type, mn); place(E.refsp, mn);
+            place(E.lb, mn); place(E.ub, mn); place(E.orig_lb, mn); place(E.orig_ub, mn);
+            place(E.obj, n);
+            // what pull() brings back, contiguous: one copy
+            place(E.head, mn); place(E.bind, mn); place(E.stat, n); place(E.bbar, m); place(E.cbar, n);
+            place(E.coef, mn);
+            place(E.gamma, std::max(m, n));
             place(E.tcol, m); place(E.trow, n); place(E.rho, m); place(E.rowp, m); place(E.u, m); place(E.s, n);
             place(E.h, m); place(E.wcol, n); place(E.ys, m); place(E.work, std::max(m, n)); place(E.r1, m);
             place(E.r2, m);
@@ -582,10 +593,13 @@ struct Spx {
         d.gpart = E->gpart.p;
         d.wlist = E->wlist.p; d.wpos = E->wpos.p; d.cand = E->cand.p;
         d.awpart = E->awpart.p; d.awpart_cap = (size_t)AW_SPLITS * m; d.awcnt = E->awcnt.p;
-        d.tslots = E->tslots.p;
-        d.xslots = E->xslots.p;
+        // the roofline stamps (per-block exit clocks, kernel spans, algorithmic
+        // bytes) cost stores and a reduction on the critical path of every
+        // pivot: they run only while a profiling mode is on (gk_bfd_profile)
+        d.tslots = E->prof ? E->tslots.p : nullptr;
+        d.xslots = E->prof ? E->xslots.p : nullptr;
         d.trace = nullptr;
-        if (E->prof >= 2) {
+        if (E->prof == 2 || E->prof == 3) {
             if (!E->trace.p) {
                 E->trace.ensure(TRACE_LEN);
                 HIPCHK(hipMemset(E->trace.p, 0, E->trace.n * sizeof(unsigned long long)));
@@ -690,12 +704,30 @@ struct Spx {
     void pull()
     {
         if (!head_stale && !vec_stale) return;
-        down(head, E->head, (size_t)m + n);
-        down(bind, E->bind, (size_t)m + n);
-        down(stat, E->stat, n);
-        down(bbar, E->bbar, m);
-        down(cbar, E->cbar, n);
-        if (!dual) down(coef, E->coef, (size_t)m + n);
+        // head | bind | stat | bbar | cbar (| coef) lie contiguous in the
+        // arena (engine_alloc): one copy into the pinned staging buffer
+        const char *lo = (const char *)E->head.p;
+        const char *hi = dual ? (const char *)(E->cbar.p + n) : (const char *)(E->coef.p + m + n);
+        char *stage = pin_take((size_t)(hi - lo));
+        if (!stage) {
+            down(head, E->head, (size_t)m + n);
+            down(bind, E->bind, (size_t)m + n);
+            down(stat, E->stat, n);
+            down(bbar, E->bbar, m);
+            down(cbar, E->cbar, n);
+            if (!dual) down(coef, E->coef, (size_t)m + n);
+        } else {
+            HIPCHK(hipMemcpyAsync(stage, lo, (size_t)(hi - lo), hipMemcpyDeviceToHost, s));
+            auto take = [&](void *dst, const void *src, size_t bytes) {
+                pending.push_back(Pending{dst, stage + ((const char *)src - lo), bytes});
+            };
+            take(head.data() + 1, E->head.p, ((size_t)m + n) * sizeof(int));
+            take(bind.data() + 1, E->bind.p, ((size_t)m + n) * sizeof(int));
+            take(stat.data() + 1, E->stat.p, (size_t)n);
+            take(bbar.data() + 1, E->bbar.p, (size_t)m * sizeof(double));
+            take(cbar.data() + 1, E->cbar.p, (size_t)n * sizeof(double));
+            if (!dual) take(coef.data() + 1, E->coef.p, ((size_t)m + n) * sizeof(double));
+        }
         sync();
         head_stale = vec_stale = false;
     }
@@ -798,15 +830,11 @@ struct Spx {
         MatDev A = E->mat();
         double *w = E->s.p;   // n-sized scratch
         double *ys = E->r1.p, *wc = E->wcol.p, *h = E->h.p, *beta = E->bbar.p, *t = E->r2.p, *dd = E->work.p;
-        neg_xn_weights(s, d, w);
-        fill_d(s, ys, 0.0, m);
-        fill_d(s, wc, 0.0, n);
-        scatter_pos(s, m, m, n, E->head.p, w, ys, wc);
+        (void)w;
+        split_pos(s, d, 0, nullptr, ys, wc);
         aprod_neg(s, A, wc, ys, h, E->partial.p, PARTIAL_CAP);                  // h = ys - A wc
         ftran_(h, beta);
-        fill_d(s, ys, 0.0, m);
-        fill_d(s, wc, 0.0, n);
-        scatter_pos(s, m, 0, m, E->head.p, beta, ys, wc);
+        split_pos(s, d, 1, beta, ys, wc);
         aprod_neg(s, A, wc, ys, t, E->partial.p, PARTIAL_CAP);                  // t = B beta
         rsub_into(t, h);                                                       // t = h - B beta
         ftran_(t, dd);
@@ -1123,13 +1151,14 @@ struct Spx {
     // by 0.3 of it; the chain is halved once D > tol / 20 and doubled again
     // (up to the cap) while D < tol / 200.
     int upd_cap = 0, upd_floor = 0;
-    bool sched_refact = false;                  // the batch stopped on the update limit
     bool drift_armed = false;
     int drift_upd = 0;
     std::vector<double> drift_ref;
     void drift_arm(const std::vector<double> &v, int st)
     {
-        drift_armed = (st == 2 && hs.upd_cnt > 0 && upd_cap > upd_floor);
+        // only a re-inversion the update limit scheduled measures the chain
+        // (not one after a failed pivot check or a growth check)
+        drift_armed = (st == 2 && hs.upd_cnt > 0 && hs.upd_cnt >= hs.upd_lim && upd_cap > upd_floor);
         if (!drift_armed) return;
         drift_ref = v;
         drift_upd = hs.upd_cnt;
@@ -1145,14 +1174,23 @@ struct Spx {
         else if (D < 0.005 * tol && drift_upd >= lim) lim = std::min(upd_cap, 2 * lim);
         static const bool log = std::getenv("GK_DRIFT_LOG") != nullptr;
         if (log)
-            fprintf(stderr, "[gk drift] %s it %d: %d updates, drift %.3e (tol %.1e) -> interval %d\n",
-                    dual ? "dual" : "primal", hs.it_cnt, drift_upd, D, tol, lim);
+            fprintf(stderr, "[gk drift] %s it %d: %d updates, drift %.3e (tol %.1e) -> interval %d (growth checks %d)\n",
+                    dual ? "dual" : "primal", hs.it_cnt, drift_upd, D, tol, lim, hs.echk);
         f->upd_lim_adapt = lim;
         hs.upd_lim = lim;
     }
 
     bool resident_match() const;
     void save_resident();
+    // move the host mirrors to / from the engine's spare set
+    void swap_spare()
+    {
+        Engine::Spare &q = E->spare;
+        type.swap(q.type); orig_type.swap(q.orig_type); stat.swap(q.stat);
+        lb.swap(q.lb); ub.swap(q.ub); coef.swap(q.coef); orig_lb.swap(q.orig_lb); orig_ub.swap(q.orig_ub);
+        obj.swap(q.obj); bbar.swap(q.bbar); cbar.swap(q.cbar); gamma.swap(q.gamma);
+        head.swap(q.head); bind.swap(q.bind);
+    }
     void init();
     void run_graph(const SpxDev &d, const DualPlan &pl, int K, int kind = 0);
     bool lists_stale = false;                   // rlist / rpos / nr to rebuild from the header
@@ -1259,6 +1297,7 @@ void Spx::init()
     m = L->m; n = L->n;
     s = ctx->stream;
     const size_t mn = (size_t)m + n + 1;
+    swap_spare();
     type.assign(mn, 0); orig_type.assign(mn, 0); lb.assign(mn, 0.0); ub.assign(mn, 0.0); coef.assign(mn, 0.0);
     orig_lb.assign(mn, 0.0); orig_ub.assign(mn, 0.0); obj.assign(n + 1, 0.0);
     head.assign(mn, 0); bind.assign(mn, 0); stat.assign(n + 1, 0);
@@ -1382,6 +1421,7 @@ void Spx::init()
         upd_cap = nfs;
     upd_floor = nfs;
     hs.upd_lim = lim;
+    hs.upd_tol = f->parm.upd_tol > 0.0 ? f->parm.upd_tol : 1e-6;
     // the product-form updates of the factor persist across calls, as the
     // reference's FT eta count does in lp.bfd (glpfhv.js:182): a run of short
     // it_lim calls re-inverts on the same schedule as one long call
@@ -1456,6 +1496,9 @@ int Spx::batch(int K, int rigorous)
     f->stats.trow_dev_launches = (long long)hs.trow_n;
     f->stats.trow_dev_ms_r = hs.trow_ticks_r / (double)ctx->wall_khz;
     f->stats.trow_dev_launches_r = (long long)hs.trow_nr;
+    f->stats.upd_dev_ms = hs.upd_ticks / (double)ctx->wall_khz;
+    f->stats.upd_dev_launches = (long long)hs.upd_n;
+    f->stats.upd_bytes = hs.bytes_upd;
     if (dual && (E->prof == 1 || E->prof == 2)) {
         for (int t = 0; t < hs.npiv; t++) {
             float ms = 0.f;
@@ -1577,8 +1620,7 @@ int Spx::run_dual()
     for (;;) {
         if (binv_st == 0) {
             pull();
-            drift_arm(cbar, sched_refact ? cbar_st : 0);
-            sched_refact = false;
+            drift_arm(cbar, cbar_st);
             if (!reinvert()) {
                 report_msg(GK_MSG_FACTERR, 1, fact_ret);     // GLP_MSG_ERR
                 return fail_return();
@@ -1715,7 +1757,6 @@ int Spx::run_dual()
             break;
         case ST_REFACT:
             binv_st = 0;
-            sched_refact = true;
             break;
         case ST_P0:
             if (bbar_st != 1 || cbar_st != 1) {
@@ -1774,8 +1815,7 @@ int Spx::run_primal()
     for (;;) {
         if (binv_st == 0) {
             pull();
-            drift_arm(bbar, sched_refact ? bbar_st : 0);
-            sched_refact = false;
+            drift_arm(bbar, bbar_st);
             if (!reinvert()) {
                 report_msg(GK_MSG_FACTERR, 1, fact_ret);     // GLP_MSG_ERR
                 return fail_return();
@@ -1875,7 +1915,6 @@ int Spx::run_primal()
             break;
         case ST_REFACT:
             binv_st = 0;
-            sched_refact = true;
             break;
         case ST_Q0:
             if (bbar_st != 1 || cbar_st != 1) {
@@ -2052,7 +2091,7 @@ void gk_bfd_last_stats(const gk_bfd *f, gk_spx_stats *st)
 
 void gk_bfd_profile(gk_bfd *f, int enable)
 {
-    if (f) f->prof = (enable == 2 || enable == 3) ? enable : (enable ? 1 : 0);
+    if (f) f->prof = (enable >= 2 && enable <= 4) ? enable : (enable ? 1 : 0);
 }
 
 int gk_bfd_trace(gk_bfd *f, unsigned long long *out, size_t cnt)
@@ -2258,6 +2297,7 @@ static int spx_entry(gk_ctx *ctx, gk_lp *lp, gk_bfd *f, const gk_smcp *parm, int
         f->upd_cnt = S.hs.upd_cnt;
         f->stats.evals_skipped = S.evals_skipped;
         if (ret == 0 || (ret >= 6 && ret <= 9)) S.save_resident();
+        S.swap_spare();
         f->stats.seconds_total = now_s() - t0;
         return ret;
     } catch (const AbiError &e) {

@@ -63,11 +63,14 @@ struct DState {
     unsigned long long trow_max_bits, tcol_max_bits;
     int kp, kq, fxp, rclr;                  // dual: leaving / entering variable of the pivot; x_kp fixed;
                                             // refsp[kp] to clear at change_basis
-    int kq1, pad2, pad3, pad4;              // variable of the pass-1 choice
+    int kq1, echk, pad3, pad4;              // variable of the pass-1 choice; echk: growth re-inversions requested
     double alfa1, pad5;                     // |trow| of the pass-1 choice
     unsigned long long tk_prev, tk_pad2;    // last block exit of the kernel before the pivot-row kernel
     double trow_ticks_r, trow_nr;           // pivot-row kernels, previous kernel's last exit to their last
                                             // exit (the bracket of a profiler's per-dispatch record)
+    unsigned long long tk_upd0, tk_pad3;    // entry of the last k_dual_update (block 0)
+    double upd_ticks, upd_n;                // k_dual_update spans (entry of block 0 to the last block exit)
+    double bytes_upd, upd_tol;              // algorithmic bytes of the k_dual_update launches; bfcp upd_tol
 };
 
 // ---- dense GEMV helpers ---------------------------------------------------
@@ -233,5 +236,7 @@ void vec_copy(hipStream_t s, double *y, const double *x, int n);
 void gather_row(hipStream_t s, const double *Binv, int ldb, int m, int p, double *rho);
 void cb_vector(hipStream_t s, int m, const int *head, const double *coef, double *cB);
 void neg_xn_weights(hipStream_t s, const SpxDev &d, double *w);
+// eval_beta's right-hand sides by variable: mode 0 -N xN, mode 1 B beta (see gk_kernels.hip)
+void split_pos(hipStream_t s, const SpxDev &d, int mode, const double *beta, double *ys, double *wc);
 
 }  // namespace gk

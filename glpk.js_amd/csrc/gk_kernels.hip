@@ -525,6 +525,35 @@ __global__ void k_neg_xn(int m, int n, const int *head, const signed char *stat,
     w[j] = -get_xN(stat, lb, ub, k, j + 1);
 }
 
+// eval_beta's two right-hand sides split into the slack part ys[m] and the
+// structural weights wc[n] in one gather over the variables (instead of two
+// fills and a scatter over the positions): variable k at position pos =
+// bind[k] contributes
+//   mode 0 (h = -N xN):  -xN(pos - m) when pos > m, else 0
+//   mode 1 (B beta):      beta[pos - 1] when pos <= m, else 0
+__global__ void k_split_pos(int m, int n, int mode, const int *__restrict__ bind, const signed char *__restrict__ stat,
+                            const double *__restrict__ lb, const double *__restrict__ ub,
+                            const double *__restrict__ beta, double *__restrict__ ys, double *__restrict__ wc)
+{
+    const int k = blockIdx.x * blockDim.x + threadIdx.x;          // variable k + 1
+    if (k >= m + n) return;
+    const int pos = bind[k];
+    double v = 0.0;
+    if (mode == 0) {
+        if (pos > m) v = -get_xN(stat, lb, ub, k + 1, pos - m);
+    } else if (pos <= m)
+        v = beta[pos - 1];
+    if (k < m) ys[k] = v;
+    else wc[k - m] = v;
+}
+
+void split_pos(hipStream_t s, const SpxDev &d, int mode, const double *beta, double *ys, double *wc)
+{
+    const int N = d.m + d.n;
+    hipLaunchKernelGGL(k_split_pos, dim3((N + 255) / 256), dim3(256), 0, s, d.m, d.n, mode, d.bind, d.stat, d.lb, d.ub,
+                       beta, ys, wc);
+}
+
 void neg_xn_weights(hipStream_t s, const SpxDev &d, double *w)
 {
     hipLaunchKernelGGL(k_neg_xn, dim3((d.n + 255) / 256), dim3(256), 0, s, d.m, d.n, d.head, d.stat, d.lb, d.ub, w);

@@ -1565,7 +1565,17 @@ extern "C" int gk_ios_driver_sharded(gk_ctx *ctx, gk_mip *mip, const gk_iocp *pa
     int inflight[2] = {0, 0}, cur = 0;
     bool fail_sync = false;
     long long moved = 0;
+    // GK_BNB_LOG=1: where the search's wall time goes (stderr)
+    static const bool bnb_log = std::getenv("GK_BNB_LOG") != nullptr;
+    double t_launch = 0.0, t_wait = 0.0, t_proc = 0.0;
+    long long n_batches = 0, n_ents = 0;
+    auto secs = [](std::chrono::steady_clock::time_point a) {
+        return std::chrono::duration<double>(std::chrono::steady_clock::now() - a).count();
+    };
     auto launch = [&](BatchBuf &bf) {
+        const auto tl0 = std::chrono::steady_clock::now();
+        n_batches++;
+        n_ents += (long long)bf.ents.size();
         const int nb = (int)bf.ents.size();
         bf.nb = nb;
         const double ball = S.bestall();
@@ -1617,9 +1627,15 @@ extern "C" int gk_ios_driver_sharded(gk_ctx *ctx, gk_mip *mip, const gk_iocp *pa
         launch_node_lp(s, P, io, nb);
         (void)hipMemcpyAsync(bf.hout.p, bf.dout.p, Y.out_end, hipMemcpyDeviceToHost, s);
         (void)hipEventRecord(bf.done, s);
+        t_launch += secs(tl0);
     };
     auto process = [&](BatchBuf &bf) {
+        const auto tw0 = std::chrono::steady_clock::now();
         if (hipEventSynchronize(bf.done) != hipSuccess) { fail_sync = true; return; }
+        t_wait += secs(tw0);
+        const auto tp0 = std::chrono::steady_clock::now();
+        struct Acc { double &t; std::chrono::steady_clock::time_point a; ~Acc() {
+            t += std::chrono::duration<double>(std::chrono::steady_clock::now() - a).count(); } } acc_{t_proc, tp0};
         const int nb = bf.nb;
         const Layout Y(S.N, n, nb);
         const char *h = bf.hout.p;
@@ -1792,6 +1808,11 @@ extern "C" int gk_ios_driver_sharded(gk_ctx *ctx, gk_mip *mip, const gk_iocp *pa
         drain();
         release_all();
     }
+    if (bnb_log)
+        fprintf(stderr, "[gk bnb] %.3f ms: %lld batches, %lld entries (%.1f per batch); host launch %.3f ms, "
+                        "wait %.3f ms, process %.3f ms; lp %lld, pp-fathomed %lld, created %lld\n",
+                1e3 * secs(t0), n_batches, n_ents, n_batches ? (double)n_ents / n_batches : 0.0, 1e3 * t_launch,
+                1e3 * t_wait, 1e3 * t_proc, S.lp_solves, S.pp_fathomed, S.created);
     mip->lp_solves = S.lp_solves;
     mip->nodes_created = S.created;
     mip->pivots = S.pivots;

@@ -98,6 +98,7 @@ class SpxStats(C.Structure):
                 ("trow_ms", C.c_double), ("trow_launches", C.c_longlong), ("trow_bytes", C.c_double),
                 ("trow_dev_ms", C.c_double), ("trow_dev_launches", C.c_longlong), ("trow_dev_ms_b", C.c_double),
                 ("trow_dev_ms_r", C.c_double), ("trow_dev_launches_r", C.c_longlong),
+                ("upd_dev_ms", C.c_double), ("upd_dev_launches", C.c_longlong), ("upd_bytes", C.c_double),
                 ("resident", C.c_int), ("evals_skipped", C.c_int)]
 
 
@@ -431,8 +432,9 @@ class GkProblem:
     def profile(self, enable=True):
         """Record HIP events around the pivot-row kernel of every dual pivot
         (enable == 2: also per-block device clock stamps, see trace(); 3:
-        the stamps only, inside the replayed graphs)."""
-        self.L.gk_bfd_profile(self.bfd, enable if enable in (2, 3) else (1 if enable else 0))
+        the stamps only, inside the replayed graphs; 4: kernel spans and
+        algorithmic bytes only, graphs kept — the bench's roofline pass)."""
+        self.L.gk_bfd_profile(self.bfd, enable if enable in (2, 3, 4) else (1 if enable else 0))
 
     def trace(self) -> np.ndarray:
         """Per-kernel, per-block [entry, exit] device clock stamps of the last

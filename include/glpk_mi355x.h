@@ -188,12 +188,20 @@ typedef struct {
     double trow_dev_ms_r;       /* same, from the last block exit of the kernel before them to their
                                    own last block exit (a profiler's per-dispatch bracket) */
     long long trow_dev_launches_r;
+    double upd_dev_ms;          /* (profiling) device span of the k_dual_update launches: entry of
+                                   block 0 to the last block exit, summed */
+    long long upd_dev_launches;
+    double upd_bytes;           /* (profiling) algorithmic bytes of every k_dual_update launch */
     int resident;               /* 1: the call found its working set resident (no re-upload) */
     int evals_skipped;          /* eval_cbar / eval_bbar calls whose result was already resident */
 } gk_spx_stats;
 void gk_bfd_last_stats(const gk_bfd *bfd, gk_spx_stats *st);
 /* record HIP events around the pivot-row kernel of every dual pivot (benches) */
-void gk_bfd_profile(gk_bfd *bfd, int enable);   /* 1: events, eager; 2: + block clock stamps; 3: stamps only, graphs kept */
+/* 1: events, eager; 2: + block clock stamps; 3: block stamps only, graphs
+ * kept; 4: kernel-span stamps and byte accounting only, graphs kept.  With 0
+ * (the default) the pivot kernels keep no clocks and no byte counts: the
+ * trow_* / upd_* / bytes_pivots statistics are filled only in modes 1-4 */
+void gk_bfd_profile(gk_bfd *bfd, int enable);
 /* profiling aid (enable == 2 above): copies the per-kernel, per-block device
  * clock stamps of the last pivot, trace[(kernel * 2048 + block) * 2 + {0 entry,
  * 1 exit}], kernels 0 top, 1 pivot row, 2 ratio, 3 FTRAN (one kernel), 4 commit,

@@ -12,7 +12,7 @@
 # matches its own arguments.  Raw traces stay in /tmp on the box; every GPU
 # step has its own time limit and the script stops at the first failure.
 set -e
-R=${1:-r02}
+R=${1:-r03}
 OUT=gpurun_out/$R
 mkdir -p $OUT
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
