@@ -339,9 +339,13 @@ def main():
             del P
             extra = run_extra(gk, problems, ctx, prob)
         else:
-            # B&B sharded over all ranks (subtree per GPU, incumbent all-reduce)
-            from glpk_js_amd.shard import TorchComm
-            extra = run_bnb(gk, problems, ctx, names=("c5s_12x30",), comm=TorchComm())
+            # B&B sharded over all ranks (subtree per GPU) through the
+            # library's own collective (gk_comm: RCCL over xGMI between the
+            # ranks' devices), every epoch's exchange inside the C driver
+            port = int(os.environ.get("MASTER_PORT", "29500")) + 7
+            comm = gk.Comm(ctx, rank, world, f"{os.environ.get('MASTER_ADDR', '127.0.0.1')}:{port}")
+            extra = run_bnb(gk, problems, ctx, names=("c5s_12x30",), comm=comm)
+            extra["bnb_comm_backend"] = {1: "tcp", 2: "rccl"}.get(comm.backend, comm.backend)
 
     if rank == 0:
         line = {
@@ -511,8 +515,12 @@ def run_bnb(gk, problems, ctx, names=("gap", "c5s_12x30"), comm=None):
         ret = gk.glp_intopt(P, gk.IOCP(msg_lev=gk.GLP_MSG_ERR), comm=comm)
         dt = time.perf_counter() - t0
         if comm is not None:
-            dt = -comm.exchange(-dt, 0)[0]         # max over ranks
+            import struct
+            dt = max(struct.unpack("d", blk)[0] for blk in comm.allgather(struct.pack("d", dt)))   # max over ranks
         lps = P.mip_stats.get("lp_solves", 0)
+        if comm is not None:
+            import struct
+            lps = sum(struct.unpack("q", blk)[0] for blk in comm.allgather(struct.pack("q", int(lps))))  # all ranks
         # LP-relax/s counts every node LP the batched search solves, including
         # the speculative ones a sequential walk would have pruned: read it
         # with the time to the optimum and the node-LP counts beside it

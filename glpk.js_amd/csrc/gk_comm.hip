@@ -1,0 +1,374 @@
+// Collective for the sharded branch and bound, inside the
+// library: one process per GPU, every rank holding a gk_comm.
+//
+// The only collective the B&B needs is an all-gather of a fixed-size byte
+// block per sync epoch ({incumbent, best bound, open nodes, active} and the
+// node descriptors handed from busy to idle ranks, gk_mip.hip shard_epoch),
+// plus one at the end that agrees on the winning incumbent.  Two transports:
+//   RCCL (ncclAllGather over xGMI) when every rank drives its own device —
+//     the 8-GPU node; the unique id travels over the bootstrap connection;
+//   TCP through rank 0 (127.0.0.1 / a host address) otherwise — ranks that
+//     share a device (RCCL refuses duplicate GPUs), CPU-only tests.
+// The bootstrap is always the TCP star: rank 0 listens on addr ("host:port"),
+// the others connect and announce their rank.  RCCL is loaded with dlopen
+// (RTLD_LOCAL): the process may already carry another RCCL build (torch's).
+#include "../../include/glpk_mi355x.h"
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <arpa/inet.h>
+#include <dlfcn.h>
+#include <netdb.h>
+#include <netinet/in.h>
+#include <netinet/tcp.h>
+#include <sys/socket.h>
+#include <sys/time.h>
+#include <unistd.h>
+
+#include <algorithm>
+#include <cerrno>
+#include <cfloat>
+#include <chrono>
+#include <cstring>
+#include <string>
+#include <thread>
+#include <vector>
+
+namespace gk {
+void set_err(const char *fmt, ...);
+}
+int gk_ctx_device(gk_ctx *);
+
+namespace {
+
+struct Rccl {
+    void *lib = nullptr;
+    decltype(&ncclGetUniqueId) get_id = nullptr;
+    decltype(&ncclCommInitRank) init = nullptr;
+    decltype(&ncclAllGather) allgather = nullptr;
+    decltype(&ncclCommDestroy) destroy = nullptr;
+    bool load()
+    {
+        if (lib) return true;
+        for (const char *name : {"librccl.so.1", "librccl.so", "/opt/rocm/lib/librccl.so.1"}) {
+            lib = dlopen(name, RTLD_NOW | RTLD_LOCAL);
+            if (lib) break;
+        }
+        if (!lib) return false;
+        get_id = (decltype(get_id))dlsym(lib, "ncclGetUniqueId");
+        init = (decltype(init))dlsym(lib, "ncclCommInitRank");
+        allgather = (decltype(allgather))dlsym(lib, "ncclAllGather");
+        destroy = (decltype(destroy))dlsym(lib, "ncclCommDestroy");
+        return get_id && init && allgather && destroy;
+    }
+};
+
+bool send_all(int fd, const void *p, size_t n)
+{
+    const char *c = (const char *)p;
+    while (n) {
+        const ssize_t k = ::send(fd, c, n, MSG_NOSIGNAL);
+        if (k < 0 && errno == EINTR) continue;
+        if (k <= 0) return false;
+        c += k;
+        n -= (size_t)k;
+    }
+    return true;
+}
+
+bool recv_all(int fd, void *p, size_t n)
+{
+    char *c = (char *)p;
+    while (n) {
+        const ssize_t k = ::recv(fd, c, n, 0);
+        if (k < 0 && errno == EINTR) continue;
+        if (k <= 0) return false;
+        c += k;
+        n -= (size_t)k;
+    }
+    return true;
+}
+
+void nodelay(int fd)
+{
+    int one = 1;
+    (void)setsockopt(fd, IPPROTO_TCP, TCP_NODELAY, &one, sizeof one);
+}
+
+}  // namespace
+
+struct gk_comm {
+    int rank = 0, size = 1, backend = GK_COMM_TCP;
+    int ramp_nodes = 0, sync_every = 0;  // gk_comm_set_option: the sharded driver's ramp-up and epoch length
+    int device = -1;
+    std::vector<int> fds;                 // rank 0: fds[r] for r >= 1; others: fds[0] = the link to rank 0
+    // RCCL
+    Rccl rccl;
+    ncclComm_t nc = nullptr;
+    hipStream_t stream = nullptr;
+    char *dbuf = nullptr;                 // device staging: send block | gathered blocks
+    size_t dcap = 0;
+    ~gk_comm()
+    {
+        if (nc && rccl.destroy) (void)rccl.destroy(nc);
+        if (dbuf) (void)hipFree(dbuf);
+        if (stream) (void)hipStreamDestroy(stream);
+        for (int fd : fds)
+            if (fd >= 0) ::close(fd);
+    }
+    // the TCP all-gather through rank 0 (also the bootstrap)
+    bool tcp_allgather(const void *send, size_t bytes, void *recv)
+    {
+        char *out = (char *)recv;
+        if (rank == 0) {
+            std::memcpy(out, send, bytes);
+            for (int r = 1; r < size; r++)
+                if (!recv_all(fds[r], out + (size_t)r * bytes, bytes)) return false;
+            for (int r = 1; r < size; r++)
+                if (!send_all(fds[r], out, (size_t)size * bytes)) return false;
+            return true;
+        }
+        return send_all(fds[0], send, bytes) && recv_all(fds[0], out, (size_t)size * bytes);
+    }
+};
+
+static bool split_addr(const char *addr, std::string &host, int &port)
+{
+    std::string a = addr ? addr : "";
+    const size_t c = a.rfind(':');
+    if (c == std::string::npos) return false;
+    host = a.substr(0, c);
+    if (host.empty()) host = "127.0.0.1";
+    port = std::atoi(a.c_str() + c + 1);
+    return port > 0 && port < 65536;
+}
+
+extern "C" gk_comm *gk_comm_create(gk_ctx *ctx, int rank, int size, const char *addr, int backend)
+{
+    using gk::set_err;
+    if (size < 1 || rank < 0 || rank >= size) { set_err("gk_comm_create: rank %d of %d", rank, size); return nullptr; }
+    if (backend != GK_COMM_AUTO && backend != GK_COMM_TCP && backend != GK_COMM_RCCL) {
+        set_err("gk_comm_create: backend = %d; invalid", backend);
+        return nullptr;
+    }
+    gk_comm *c = new gk_comm;
+    c->rank = rank;
+    c->size = size;
+    c->device = ctx ? gk_ctx_device(ctx) : -1;
+    if (size > 1) {
+        std::string host;
+        int port = 0;
+        if (!split_addr(addr, host, port)) {
+            set_err("gk_comm_create: address \"%s\"; expected host:port", addr ? addr : "");
+            delete c;
+            return nullptr;
+        }
+        addrinfo hints{}, *ai = nullptr;
+        hints.ai_family = AF_INET;
+        hints.ai_socktype = SOCK_STREAM;
+        if (getaddrinfo(host.c_str(), std::to_string(port).c_str(), &hints, &ai) != 0 || !ai) {
+            set_err("gk_comm_create: cannot resolve %s", host.c_str());
+            delete c;
+            return nullptr;
+        }
+        const auto deadline = std::chrono::steady_clock::now() + std::chrono::seconds(120);
+        bool ok = true;
+        if (rank == 0) {
+            c->fds.assign(size, -1);
+            const int ls = ::socket(AF_INET, SOCK_STREAM, 0);
+            int one = 1;
+            (void)setsockopt(ls, SOL_SOCKET, SO_REUSEADDR, &one, sizeof one);
+            timeval tv{120, 0};                   // accept() gives up after 2 minutes
+            (void)setsockopt(ls, SOL_SOCKET, SO_RCVTIMEO, &tv, sizeof tv);
+            ok = ls >= 0 && ::bind(ls, ai->ai_addr, ai->ai_addrlen) == 0 && ::listen(ls, size) == 0;
+            for (int k = 1; ok && k < size; k++) {
+                const int fd = ::accept(ls, nullptr, nullptr);
+                int r = -1;
+                ok = fd >= 0 && recv_all(fd, &r, sizeof r) && r >= 1 && r < size && c->fds[r] < 0;
+                if (ok) {
+                    nodelay(fd);
+                    c->fds[r] = fd;
+                } else if (fd >= 0)
+                    ::close(fd);
+            }
+            if (ls >= 0) ::close(ls);
+            if (!ok) set_err("gk_comm_create: rank 0 could not accept the other ranks on %s:%d (%s)", host.c_str(),
+                             port, std::strerror(errno));
+        } else {
+            int fd = -1;
+            for (;;) {
+                fd = ::socket(AF_INET, SOCK_STREAM, 0);
+                if (fd >= 0 && ::connect(fd, ai->ai_addr, ai->ai_addrlen) == 0) break;
+                if (fd >= 0) ::close(fd);
+                fd = -1;
+                if (std::chrono::steady_clock::now() > deadline) break;
+                std::this_thread::sleep_for(std::chrono::milliseconds(20));
+            }
+            ok = fd >= 0 && send_all(fd, &rank, sizeof rank);
+            if (ok) {
+                nodelay(fd);
+                c->fds.assign(1, fd);
+            } else {
+                if (fd >= 0) ::close(fd);
+                set_err("gk_comm_create: rank %d could not reach rank 0 at %s:%d", rank, host.c_str(), port);
+            }
+        }
+        freeaddrinfo(ai);
+        if (!ok) {
+            delete c;
+            return nullptr;
+        }
+    }
+    // RCCL when every rank has a device of its own (auto) or when asked
+    c->backend = GK_COMM_TCP;
+    if (size > 1 && backend != GK_COMM_TCP) {
+        std::vector<int> devs(size);
+        int mine[2] = {c->device, 0};
+        // host identity: ranks on different hosts may use the same ordinal
+        char hn[64] = {0};
+        (void)gethostname(hn, sizeof hn - 1);
+        for (const char *p = hn; *p; ++p) mine[1] = mine[1] * 31 + *p;
+        std::vector<int> all(2 * size);
+        if (!c->tcp_allgather(mine, sizeof mine, all.data())) {
+            set_err("gk_comm_create: bootstrap exchange failed");
+            delete c;
+            return nullptr;
+        }
+        bool distinct = true;
+        for (int r = 0; r < size; r++)
+            for (int q = r + 1; q < size; q++)
+                if (all[2 * r] < 0 || (all[2 * r] == all[2 * q] && all[2 * r + 1] == all[2 * q + 1])) distinct = false;
+        const bool want = backend == GK_COMM_RCCL || distinct;
+        if (want && !distinct) {
+            set_err("gk_comm_create: RCCL needs one device per rank");
+            delete c;
+            return nullptr;
+        }
+        if (want) {
+            int have = c->rccl.load() ? 1 : 0;
+            std::vector<int> hv(size);
+            if (!c->tcp_allgather(&have, sizeof have, hv.data())) { delete c; return nullptr; }
+            const bool every = std::all_of(hv.begin(), hv.end(), [](int v) { return v == 1; });
+            if (!every && backend == GK_COMM_RCCL) {
+                set_err("gk_comm_create: librccl could not be loaded on every rank");
+                delete c;
+                return nullptr;
+            }
+            if (every) {
+                ncclUniqueId id;
+                std::memset(&id, 0, sizeof id);
+                if (rank == 0 && c->rccl.get_id(&id) != ncclSuccess) std::memset(&id, 0, sizeof id);
+                std::vector<ncclUniqueId> ids(size);
+                if (!c->tcp_allgather(&id, sizeof id, ids.data())) { delete c; return nullptr; }
+                if (hipSetDevice(c->device) != hipSuccess ||
+                    hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
+                    c->rccl.init(&c->nc, size, ids[0], rank) != ncclSuccess) {
+                    set_err("gk_comm_create: ncclCommInitRank failed on rank %d", rank);
+                    delete c;
+                    return nullptr;
+                }
+                c->backend = GK_COMM_RCCL;
+            }
+        }
+    }
+    return c;
+}
+
+extern "C" void gk_comm_destroy(gk_comm *c) { delete c; }
+
+extern "C" int gk_comm_backend(const gk_comm *c) { return c ? c->backend : -1; }
+
+extern "C" int gk_comm_allgather(void *comm, const void *send, size_t bytes, void *recv)
+{
+    gk_comm *c = (gk_comm *)comm;
+    if (!c || (!send && bytes) || (!recv && bytes)) return 1;
+    if (c->size == 1) {
+        std::memcpy(recv, send, bytes);
+        return 0;
+    }
+    if (c->backend == GK_COMM_TCP) return c->tcp_allgather(send, bytes, recv) ? 0 : 1;
+    // RCCL: ncclAllGather on device buffers (xGMI), host blocks in and out
+    const size_t need = bytes * (size_t)(c->size + 1);
+    if (c->dcap < need) {
+        if (c->dbuf) (void)hipFree(c->dbuf);
+        c->dbuf = nullptr;
+        c->dcap = 0;
+        if (hipMalloc((void **)&c->dbuf, need) != hipSuccess) return 1;
+        c->dcap = need;
+    }
+    if (hipSetDevice(c->device) != hipSuccess) return 1;
+    char *dsend = c->dbuf, *drecv = c->dbuf + bytes;
+    if (hipMemcpyAsync(dsend, send, bytes, hipMemcpyHostToDevice, c->stream) != hipSuccess) return 1;
+    if (c->rccl.allgather(dsend, drecv, bytes, ncclChar, c->nc, c->stream) != ncclSuccess) return 1;
+    if (hipMemcpyAsync(recv, drecv, bytes * c->size, hipMemcpyDeviceToHost, c->stream) != hipSuccess) return 1;
+    return hipStreamSynchronize(c->stream) == hipSuccess ? 0 : 1;
+}
+
+extern "C" int gk_comm_rank(const gk_comm *c) { return c ? c->rank : -1; }
+
+extern "C" int gk_comm_set_option(gk_comm *c, int opt, int value)
+{
+    if (!c) return GK_EABI;
+    if (opt == GK_COMM_OPT_RAMP) c->ramp_nodes = value;
+    else if (opt == GK_COMM_OPT_SYNC) c->sync_every = value;
+    else { gk::set_err("gk_comm_set_option: opt = %d; invalid", opt); return GK_EABI; }
+    return 0;
+}
+extern "C" int gk_comm_size(const gk_comm *c) { return c ? c->size : -1; }
+
+// glp_intopt over every rank of comm: the sharded search
+// (gk_ios_driver_sharded with this library's all-gather), then one more
+// all-gather that agrees on the winning incumbent — the best objective,
+// the lowest rank on ties — so every rank returns the same solution
+extern "C" int gk_ios_driver_comm(gk_ctx *ctx, gk_mip *mip, const gk_iocp *parm, gk_comm *comm)
+{
+    using gk::set_err;
+    if (!comm) { set_err("gk_ios_driver_comm: null communicator"); return GK_EABI; }
+    if (comm->size == 1) return gk_ios_driver(ctx, mip, parm);
+    gk_ios_shard sh{};
+    sh.rank = comm->rank;
+    sh.size = comm->size;
+    sh.ramp_nodes = comm->ramp_nodes;
+    sh.sync_every = comm->sync_every;
+    sh.exchange = nullptr;
+    sh.info = comm;
+    sh.allgather = gk_comm_allgather;
+    const int ret = gk_ios_driver_sharded(ctx, mip, parm, &sh);
+    if (ret == GK_EABI) return ret;
+    const int m = mip->lp.m, n = mip->lp.n;
+    const size_t blk = 4 * sizeof(double) + ((size_t)m + n) * sizeof(double);
+    std::vector<char> me(blk, 0), all(blk * comm->size);
+    double *h = (double *)me.data();
+    const bool have = mip->mip_stat == 5 || mip->mip_stat == 2;      // GLP_OPT / GLP_FEAS
+    h[0] = have ? 1.0 : 0.0;
+    h[1] = have ? mip->mip_obj : 0.0;
+    h[2] = (double)ret;
+    h[3] = (double)mip->mip_stat;
+    for (int i = 0; i < m; i++) h[4 + i] = mip->row_mipx[i + 1];
+    for (int j = 0; j < n; j++) h[4 + m + j] = mip->col_mipx[j + 1];
+    if (gk_comm_allgather(comm, me.data(), blk, all.data()) != 0) {
+        set_err("gk_ios_driver_comm: final all-gather failed");
+        return GK_EABI;
+    }
+    const double sign = (mip->lp.dir == 1) ? 1.0 : -1.0;               // GLP_MIN
+    int win = -1, worst_ret = 0;
+    bool any_partial = false;
+    for (int r = 0; r < comm->size; r++) {
+        const double *g = (const double *)(all.data() + (size_t)r * blk);
+        if ((int)g[2] != 0) worst_ret = (int)g[2];
+        if ((int)g[3] == 2 || (int)g[3] == 1) any_partial = true;   // stopped before proving optimality
+        if (g[0] != 1.0) continue;
+        if (win < 0 || sign * g[1] < sign * ((const double *)(all.data() + (size_t)win * blk))[1]) win = r;
+    }
+    if (win >= 0) {
+        const double *g = (const double *)(all.data() + (size_t)win * blk);
+        mip->mip_obj = g[1];
+        for (int i = 0; i < m; i++) mip->row_mipx[i + 1] = g[4 + i];
+        for (int j = 0; j < n; j++) mip->col_mipx[j + 1] = g[4 + m + j];
+        mip->mip_stat = (worst_ret == 0 && !any_partial) ? 5 : 2;
+    } else {
+        mip->mip_obj = 0.0;
+        mip->mip_stat = (worst_ret == 0 && !any_partial) ? 4 : 1;
+    }
+    return worst_ret;
+}

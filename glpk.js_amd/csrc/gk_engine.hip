@@ -110,6 +110,15 @@ struct gk_ctx {
     // while the process ran was followed by a fault in node's teardown
     DBuf<double> partial, awpart;
     DBuf<char> upstage;
+    // the branch-and-bound driver's buffers, kept across searches (gk_mip.hip)
+    void *mip_cache = nullptr;
+    void (*mip_cache_free)(void *) = nullptr;
+    // the look-ahead streams of large re-inversions (gk_reinvert.hip)
+    GjSide *gj = nullptr;
+    bool gj_tried = false;
+    // the branch-and-bound driver's progress lines (gk_ios_set_report)
+    gk_report_fn ios_rpt = nullptr;
+    void *ios_rpt_ud = nullptr;
 };
 
 static void ctx_unref(gk_ctx *ctx)
@@ -118,6 +127,10 @@ static void ctx_unref(gk_ctx *ctx)
     (void)hipSetDevice(ctx->device);
     if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
     ctx->partial.release(); ctx->awpart.release(); ctx->upstage.release();
+    if (ctx->gj) gj_side_destroy(ctx->gj);
+    ctx->gj = nullptr;
+    if (ctx->mip_cache && ctx->mip_cache_free) ctx->mip_cache_free(ctx->mip_cache);
+    ctx->mip_cache = nullptr;
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
     delete ctx;
 }
@@ -327,7 +340,16 @@ static int reinvert_core(gk_bfd *f, const BasisSplit &bs, const MatDev *Adense, 
             HIPCHK(hipEventCreate(&gj_ev[1]));
             HIPCHK(hipEventRecord(gj_ev[0], s));
         }
-        if (blocked) result = gauss_jordan_blocked(s, f->X.p, f->Y.p, k, f->piv_step.p, f->piv.p, f->flag.p, 1e-15);
+        GjSide *side = nullptr;
+        if (blocked && gj_lookahead(k)) {
+            if (!f->ctx->gj && !f->ctx->gj_tried) {
+                f->ctx->gj_tried = true;
+                f->ctx->gj = gj_side_create(f->ctx->device);
+            }
+            side = f->ctx->gj;
+        }
+        if (blocked)
+            result = gauss_jordan_blocked(s, f->X.p, f->Y.p, k, f->piv_step.p, f->piv.p, f->flag.p, 1e-15, side);
         else gauss_jordan(s, f->X.p, f->Y.p, k, f->piv_step.p, f->piv.p, f->flag.p, 1e-15, &result);
         if (gj_time) {
             float ms = 0.f;
@@ -2475,6 +2497,24 @@ int gk_ctx_mark(gk_ctx *c, int tag)
 }
 
 int gk_ctx_device(gk_ctx *c) { return c->device; }
+void mip_cache_free_hook(void *p);
+void **gk_ctx_mip_cache(gk_ctx *c, void (**freer)(void *))
+{
+    c->mip_cache_free = mip_cache_free_hook;
+    *freer = mip_cache_free_hook;
+    return &c->mip_cache;
+}
+void gk_ios_set_report(gk_ctx *c, gk_report_fn fn, void *ud)
+{
+    if (!c) return;
+    c->ios_rpt = fn;
+    c->ios_rpt_ud = ud;
+}
+void gk_ctx_ios_report(gk_ctx *c, gk_report_fn *fn, void **ud)
+{
+    *fn = c ? c->ios_rpt : nullptr;
+    *ud = c ? c->ios_rpt_ud : nullptr;
+}
 hipStream_t gk_ctx_stream(gk_ctx *c) { return c->stream; }
 namespace gk {
 void set_err(const char *fmt, ...)

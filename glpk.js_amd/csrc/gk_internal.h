@@ -221,8 +221,16 @@ void extract_inverse_rowmajor(hipStream_t s, const double *X, int k, const int *
 // returns the buffer holding the inverted M = C' (see gk_reinvert.hip)
 int gj_blocked_max();
 size_t gj_blocked_scratch(int k);
+// look-ahead side streams of the blocked inversion (owned by a gk_ctx)
+struct GjSide {
+    hipStream_t crit = nullptr, side = nullptr;
+    hipEvent_t ev_in = nullptr, ev_main = nullptr, ev_side = nullptr;
+};
+GjSide *gj_side_create(int device);
+void gj_side_destroy(GjSide *g);
+bool gj_lookahead(int k);
 double *gauss_jordan_blocked(hipStream_t s, double *X, double *scratch, int k, int *piv_step, int *piv, int *flag,
-                             double tiny);
+                             double tiny, GjSide *side = nullptr);
 void extract_inverse_blocked(hipStream_t s, const double *M, int k, const int *piv, const int *piv_step,
                              double *CinvR);
 // G (ms x k, col-major) = BS (ms x k col-major) * CinvR (k x k row-major)

@@ -580,6 +580,28 @@ __global__ void __launch_bounds__(256) k_node_lp(NodeProb P, NodeIO io)
         }
         return;
     }
+    // ---- fix_by_red_cost (glpios03.js:307, called at :801 once an incumbent
+    // exists): a non-basic integer column whose reduced cost alone lifts the
+    // node's objective to the incumbent is fixed on its current bound (the
+    // LP solution does not change; the children inherit the fixing through
+    // the node's final bounds, and the branching below skips it as NS)
+    if (io.obj_bound < DBL_MAX) {
+        const double best = io.obj_bound;
+        for (int j = threadIdx.x; j < n; j += blockDim.x) {
+            const int k = m + j;
+            if (!P.isint[j]) continue;
+            double dj = d[k];
+            if (stat[k] == NL) {
+                if (dj < 0.0) dj = 0.0;
+                if (z + dj >= best) { ub[k] = lb[k]; stat[k] = NS; }
+            } else if (stat[k] == NU) {
+                if (dj > 0.0) dj = 0.0;
+                if (z - dj >= best) { lb[k] = ub[k]; stat[k] = NS; }
+            }
+        }
+        __syncthreads();
+        put_bounds();
+    }
     // ---- ios_eval_degrad (glpios03.js:188) for every fractional column and
     // branch_drtom (glpios09.js:84) on the node's own tableau rows ---------
     // columns in order; x_j basic and fractional; the dual ratio test of
@@ -849,7 +871,22 @@ struct Parked {
     int pending = 0;
 };
 
+// the device and pinned host buffers of the driver, kept by the context
+// from one glp_intopt to the next (allocating them — hipHostMalloc of the
+// packed batch buffers above all — cost a search of gap several
+// milliseconds when it was done per call); the arrays only grow
+struct MipCache {
+    BatchBuf bufs[2];
+    DevArr<double> dA, dc, dscratch;
+    DevArr<signed char> dint;
+};
+
 }  // namespace
+
+}  // namespace gk
+void **gk_ctx_mip_cache(gk_ctx *c, void (**freer)(void *));
+void mip_cache_free_hook(void *p) { delete (gk::MipCache *)p; }
+namespace gk {
 
 // ---------------------------------------------------------------------------
 // one glp_intopt search (ios_driver, glpios03.js:1) on one GPU
@@ -863,9 +900,8 @@ struct MipSolver {
     double sign = 1.0, c0 = 0.0;
     std::vector<double> A, c, rlb, rub, clb, cub;
     std::vector<signed char> isint;
-    DevArr<double> dA, dc, dscratch;
-    DevArr<signed char> dint;
-    BatchBuf bufs[2];
+    MipCache *cache = nullptr;
+    BatchBuf *bufs = nullptr;
     NodePool pool;
     NodeProb P{};
     int BMAX = 0;
@@ -906,7 +942,8 @@ struct MipSolver {
     bool alloc_batch(int B)
     {
         BMAX = B;
-        for (auto &bf : bufs) {
+        for (int q = 0; q < 2; q++) {
+            BatchBuf &bf = bufs[q];
             bf.din.ensure(in_bytes(B) + 64); bf.dout.ensure(out_bytes(B) + 64);
             bf.hin.ensure(in_bytes(B) + 64); bf.hout.ensure(out_bytes(B) + 64);
             if (!bf.done && hipEventCreateWithFlags(&bf.done, hipEventDisableTiming) != hipSuccess) return false;
@@ -974,10 +1011,13 @@ struct MipSolver {
         for (NodeRec &r : open) set_keys(r);
         std::make_heap(open.begin(), open.end(), NodeWorse());
     }
+    int bingos = 0;                           // new incumbents not yet reported
+    std::vector<int> cand_buf;                // node_done's fractional columns
     void new_incumbent(double z, const double *x)
     {
         const double before = bestall();
         have = true;
+        bingos++;
         best = z;
         std::memcpy(xbest.data(), x, N * sizeof(double));
         if (bestall() != before) rekey();
@@ -1142,7 +1182,7 @@ struct MipSolver {
         }
         const double bound = std::max(nd.bound, round_bound(z));
         if (!hopeful(bound)) return false;
-        std::vector<int> cand;
+        std::vector<int> &cand = cand_buf;           // reused: no allocation per node
         double ii = 0.0;
         if (integrality(x, so, bl, bu, cand, ii) == 0) {
             if (!have || z < best) new_incumbent(z, x);
@@ -1444,6 +1484,7 @@ using namespace gk;
 
 int gk_ctx_device(gk_ctx *);
 hipStream_t gk_ctx_stream(gk_ctx *);
+void gk_ctx_ios_report(gk_ctx *c, gk_report_fn *fn, void **ud);
 
 extern "C" int gk_ios_driver(gk_ctx *ctx, gk_mip *mip, const gk_iocp *parm)
 {
@@ -1522,22 +1563,32 @@ extern "C" int gk_ios_driver_sharded(gk_ctx *ctx, gk_mip *mip, const gk_iocp *pa
     }
     setup_rounding(S, mip);
     // device problem
-    S.dA.ensure(S.A.size()); S.dc.ensure(S.N); S.dint.ensure(n);
+    {
+        void (*freer)(void *) = nullptr;
+        void **slot = gk_ctx_mip_cache(ctx, &freer);
+        if (!*slot) *slot = new MipCache;
+        (void)freer;
+        S.cache = (MipCache *)*slot;
+        S.bufs = S.cache->bufs;
+        // the previous search may have left events in use: nothing of it is in flight
+    }
+    MipCache &Cc = *S.cache;
+    Cc.dA.ensure(S.A.size()); Cc.dc.ensure(S.N); Cc.dint.ensure(n);
     const int BMAX = (lds <= NODE_LDS_MAX) ? 1024 : (int)std::max<size_t>(1, std::min<size_t>(1024, SCRATCH_MAX / lds));
     S.stride = (lds + 255) / 256 * 32;                    // doubles, 256-byte aligned slices
     if (lds > NODE_LDS_MAX) {
-        S.dscratch.ensure(S.stride * BMAX);
-        if (!S.dscratch.p) { set_err("gk_ios_driver: out of memory (node work area)"); return GK_EABI; }
+        Cc.dscratch.ensure(S.stride * BMAX);
+        if (!Cc.dscratch.p) { set_err("gk_ios_driver: out of memory (node work area)"); return GK_EABI; }
     }
-    if (!S.alloc_batch(BMAX) || !S.dA.p || !S.dc.p || !S.dint.p) {
+    if (!S.alloc_batch(BMAX) || !Cc.dA.p || !Cc.dc.p || !Cc.dint.p) {
         set_err("gk_ios_driver: out of memory");
         return GK_EABI;
     }
-    (void)hipMemcpyAsync(S.dA.p, S.A.data(), S.A.size() * sizeof(double), hipMemcpyHostToDevice, s);
-    (void)hipMemcpyAsync(S.dc.p, S.c.data(), S.N * sizeof(double), hipMemcpyHostToDevice, s);
-    (void)hipMemcpyAsync(S.dint.p, S.isint.data(), n, hipMemcpyHostToDevice, s);
+    (void)hipMemcpyAsync(Cc.dA.p, S.A.data(), S.A.size() * sizeof(double), hipMemcpyHostToDevice, s);
+    (void)hipMemcpyAsync(Cc.dc.p, S.c.data(), S.N * sizeof(double), hipMemcpyHostToDevice, s);
+    (void)hipMemcpyAsync(Cc.dint.p, S.isint.data(), n, hipMemcpyHostToDevice, s);
     NodeProb &P = S.P;
-    P.m = m; P.n = n; P.ld = S.N; P.A = S.dA.p; P.c = S.dc.p; P.isint = S.dint.p; P.tol_int = parm->tol_int;
+    P.m = m; P.n = n; P.ld = S.N; P.A = Cc.dA.p; P.c = Cc.dc.p; P.isint = Cc.dint.p; P.tol_int = parm->tol_int;
     P.dth = (parm->br_tech == 4) ? 1 : 0;
     NodePool &pool = S.pool;
     pool.n = n; pool.N = S.N;
@@ -1567,7 +1618,7 @@ extern "C" int gk_ios_driver_sharded(gk_ctx *ctx, gk_mip *mip, const gk_iocp *pa
     long long moved = 0;
     // GK_BNB_LOG=1: where the search's wall time goes (stderr)
     static const bool bnb_log = std::getenv("GK_BNB_LOG") != nullptr;
-    double t_launch = 0.0, t_wait = 0.0, t_proc = 0.0;
+    double t_launch = 0.0, t_wait = 0.0, t_proc = 0.0, t_nd = 0.0;
     long long n_batches = 0, n_ents = 0;
     auto secs = [](std::chrono::steady_clock::time_point a) {
         return std::chrono::duration<double>(std::chrono::steady_clock::now() - a).count();
@@ -1622,7 +1673,7 @@ extern "C" int gk_ios_driver_sharded(gk_ctx *ctx, gk_mip *mip, const gk_iocp *pa
         io.obj = (double *)(dout + Y.obj); io.dzb = (double *)(dout + Y.dz); io.x = (double *)(dout + Y.x);
         io.bnd = (double *)(dout + Y.bnd); io.status = (int *)(dout + Y.stat); io.pivots = (int *)(dout + Y.piv);
         io.jj = (int *)(dout + Y.jj); io.next = (int *)(dout + Y.next); io.stat_out = (signed char *)(dout + Y.sto);
-        io.scratch = S.dscratch.p;
+        io.scratch = Cc.dscratch.p;
         io.scratch_stride = S.stride;
         launch_node_lp(s, P, io, nb);
         (void)hipMemcpyAsync(bf.hout.p, bf.dout.p, Y.out_end, hipMemcpyDeviceToHost, s);
@@ -1671,8 +1722,10 @@ extern "C" int gk_ios_driver_sharded(gk_ctx *ctx, gk_mip *mip, const gk_iocp *pa
             else S.lp_solves++;
             for (int j = 0; j < n; j++) { fbl[j] = bb[2 * j]; fbu[j] = bb[2 * j + 1]; }
             if (st == NODE_OPT) {
+                const auto tn0 = bnb_log ? std::chrono::steady_clock::now() : std::chrono::steady_clock::time_point{};
                 S.node_done(nd, hobj[b], x, hso + (size_t)b * S.N, fbl.data(), fbu.data(), hdz + (size_t)b * 2 * n,
                             hjj[b], hnext[b], true);
+                if (bnb_log) t_nd += secs(tn0);
             } else if ((st == NODE_FAIL || st == NODE_ITLIM) && !S.err) {
                 double z = 0.0;
                 bool opt = false;
@@ -1707,10 +1760,70 @@ extern "C" int gk_ios_driver_sharded(gk_ctx *ctx, gk_mip *mip, const gk_iocp *pa
     // ranks exchange the incumbent and, with an all-gather, hand open nodes
     // to idle ranks (the collective is called by idle ranks too, until no
     // rank has work left)
-    bool split_done = (size == 1), timed_out = false;
+    bool split_done = (size == 1), timed_out = false, gap_hit = false;
     int since_sync = 0;
+    // show_progress (glpios03.js:2-48) through the context's report hook, and
+    // the relative gap of ios_relative_gap (glpios01.js:842): both need the
+    // best local bound over the active subproblems (open, preferred children,
+    // in flight, parked for pseudocost probes)
+    gk_report_fn rfn = nullptr;
+    void *rud = nullptr;
+    gk_ctx_ios_report(ctx, &rfn, &rud);
+    const bool rpt_on = rfn && parm->msg_lev >= 2;                          // GLP_MSG_ON
+    auto active = [&](double &bnd) {
+        long long a = 0;
+        bnd = INF;
+        auto take = [&](const NodeRec &r) { a++; bnd = std::min(bnd, r.bound); };
+        for (const NodeRec &r : S.open) take(r);
+        for (const NodeRec &r : S.dive) take(r);
+        for (const NodeRec &r : S.next_dive) take(r);
+        for (int k = 0; k < 2; k++)
+            if (inflight[k])
+                for (const Entry &e : S.bufs[k].ents)
+                    if (e.kind == 0) take(e.nd);
+        for (size_t p = 0; p < S.parked.size(); p++)
+            if (std::find(S.parked_free.begin(), S.parked_free.end(), (int)p) == S.parked_free.end())
+                take(S.parked[p].nd);
+        return a;
+    };
+    auto tm_lag = std::chrono::steady_clock::time_point{};
+    bool lag_set = false;
+    auto report = [&](int bingo) {
+        double bnd;
+        const long long a = active(bnd);
+        const int code = (bingo ? 1 : 0) | (S.have ? 2 : 0) | (a == 0 ? 4 : 0);
+        const double obj = S.have ? S.c0 + S.sign * S.best : 0.0;
+        // -DBL_MAX (the root's bound) prints as -inf / +inf by direction
+        const double ob = (bnd == -INF) ? -S.sign * DBL_MAX : (bnd == INF ? S.sign * DBL_MAX : S.c0 + S.sign * bnd);
+        rfn(rud, GK_RPT_MIP, code, (int)(L.it_cnt + S.pivots), (int)std::min<long long>(a, 0x7fffffff), obj, ob,
+            (int)std::min<long long>(S.created - a, 0x7fffffff));
+        tm_lag = std::chrono::steady_clock::now();
+        lag_set = true;
+    };
+    auto rel_gap = [&]() {
+        if (!S.have) return DBL_MAX;
+        double bnd;
+        if (active(bnd) == 0) return 0.0;
+        const double bm = S.c0 + S.sign * S.best, bb = S.c0 + S.sign * bnd;
+        return std::fabs(bm - bb) / (std::fabs(bm) + DBL_EPSILON);
+    };
     for (;;) {
         if (fail_sync || S.err) break;
+        if (rpt_on) {
+            if (S.bingos) { S.bingos = 0; report(1); }
+            // every out_frq milliseconds (glpios03.js:603-607; the first line at the root)
+            if (!lag_set || (double)(parm->out_frq - 1) <=
+                                1000.0 * std::chrono::duration<double>(std::chrono::steady_clock::now() - tm_lag).count())
+                report(0);
+        }
+        // the relative mip gap (glpios03.js:613-620)
+        if (parm->mip_gap > 0.0 && S.have && rel_gap() <= parm->mip_gap) {
+            gap_hit = true;
+            drain();
+            if (rpt_on && S.bingos) { S.bingos = 0; report(1); }
+            release_all();
+            break;
+        }
         const bool any_inflight = inflight[0] || inflight[1];
         bool have_work = !S.open.empty() || !S.dive.empty() || !S.probeq.empty() || any_inflight;
         if (have_work && parm->tm_lim < 0x7fffffff &&
@@ -1808,11 +1921,15 @@ extern "C" int gk_ios_driver_sharded(gk_ctx *ctx, gk_mip *mip, const gk_iocp *pa
         drain();
         release_all();
     }
+    if (rpt_on) {
+        if (S.bingos) { S.bingos = 0; report(1); }
+        report(0);                                        // glpios03.js:941-943
+    }
     if (bnb_log)
         fprintf(stderr, "[gk bnb] %.3f ms: %lld batches, %lld entries (%.1f per batch); host launch %.3f ms, "
-                        "wait %.3f ms, process %.3f ms; lp %lld, pp-fathomed %lld, created %lld\n",
+                        "wait %.3f ms, process %.3f ms (node_done %.3f); open %zu; lp %lld, pp-fathomed %lld, created %lld\n",
                 1e3 * secs(t0), n_batches, n_ents, n_batches ? (double)n_ents / n_batches : 0.0, 1e3 * t_launch,
-                1e3 * t_wait, 1e3 * t_proc, S.lp_solves, S.pp_fathomed, S.created);
+                1e3 * t_wait, 1e3 * t_proc, 1e3 * t_nd, S.open.size(), S.lp_solves, S.pp_fathomed, S.created);
     mip->lp_solves = S.lp_solves;
     mip->nodes_created = S.created;
     mip->pivots = S.pivots;
@@ -1821,7 +1938,7 @@ extern "C" int gk_ios_driver_sharded(gk_ctx *ctx, gk_mip *mip, const gk_iocp *pa
     mip->pp_fathomed = S.pp_fathomed;
     mip->nodes_moved = moved;
     if (S.have) {
-        mip->mip_stat = (timed_out || S.err) ? 2 : 5;     // GLP_FEAS / GLP_OPT
+        mip->mip_stat = (timed_out || S.err || gap_hit) ? 2 : 5;     // GLP_FEAS / GLP_OPT
         mip->mip_obj = S.c0 + S.sign * S.best;
         for (int i = 0; i < m; i++) mip->row_mipx[i + 1] = S.xbest[i];
         for (int j = 0; j < n; j++)
@@ -1831,5 +1948,6 @@ extern "C" int gk_ios_driver_sharded(gk_ctx *ctx, gk_mip *mip, const gk_iocp *pa
         mip->mip_obj = 0.0;
     }
     if (S.err) return S.err;                              // GLP_EFAIL
+    if (gap_hit) return 0x0E;                             // GLP_EMIPGAP
     return timed_out ? 0x09 : 0;                          // GLP_ETMLIM
 }

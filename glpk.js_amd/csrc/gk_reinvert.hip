@@ -23,6 +23,8 @@
 #include <cstdlib>
 #include <climits>
 #include <map>
+#include <algorithm>
+#include <mutex>
 #include <vector>
 #include <hip/hip_ext.h>
 #include <cstdio>
@@ -541,49 +543,89 @@ static double *gjc_run(hipStream_t s, double *M, double *M2, double *P, double *
 // writes the buffer that update reads, and its copy-in overwrites the P that
 // T0's write-back reads, so s waits for the side stream's event of T0 before
 // them.
-struct GjSide {
-    hipStream_t crit = nullptr, side = nullptr;
-    hipEvent_t ev_in = nullptr, ev_main = nullptr, ev_side = nullptr;
-};
-
 // the critical-path stream (the panels, on GK_GJ_CRIT_CUS compute units,
 // default 64) and the side stream (the other CUs), disjoint CU masks so the
-// big updates do not share a CU with the one-workgroup panel; three events;
-// created once per device and thread, nullptr when the runtime refuses them
-// (the single-stream schedule then runs)
-static GjSide *gj_side()
+// big updates do not share a CU with the one-workgroup panel; three events.
+// Owned by the context that re-inverts (gk_ctx, created on its first
+// look-ahead re-inversion, destroyed with it) and, until then, recorded in
+// a registry that an atexit handler drains: the handles are never left to
+// the runtime's own teardown (a process that left CU-masked streams alive
+// died in its exit handlers under rocprofv3).
+static std::mutex g_side_mu;
+static std::vector<GjSide *> *g_sides = nullptr;     // live handles (never freed itself: outlives exit)
+
+static void gj_side_release(GjSide *g)
 {
-    static thread_local std::map<int, GjSide> per_dev;
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess) return nullptr;
-    GjSide &g = per_dev[dev];
-    if (g.side) return &g;
+    if (g->crit) (void)hipStreamSynchronize(g->crit);
+    if (g->side) (void)hipStreamSynchronize(g->side);
+    if (g->ev_in) (void)hipEventDestroy(g->ev_in);
+    if (g->ev_main) (void)hipEventDestroy(g->ev_main);
+    if (g->ev_side) (void)hipEventDestroy(g->ev_side);
+    if (g->crit) (void)hipStreamDestroy(g->crit);
+    if (g->side) (void)hipStreamDestroy(g->side);
+    *g = GjSide{};
+}
+
+static void gj_side_atexit()
+{
+    std::lock_guard<std::mutex> lk(g_side_mu);
+    if (!g_sides) return;
+    for (GjSide *g : *g_sides) {
+        gj_side_release(g);
+        delete g;
+    }
+    g_sides->clear();
+}
+
+GjSide *gj_side_create(int dev)
+{
     static const int crit_cus = [] {
         const char *e = std::getenv("GK_GJ_CRIT_CUS");
         return e ? std::atoi(e) : 64;
     }();
     int ncu = 0;
-    if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return nullptr;
+    if (hipSetDevice(dev) != hipSuccess ||
+        hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+        return nullptr;
+    GjSide *g = new GjSide;
     bool ok;
     if (crit_cus > 0 && crit_cus < ncu) {
         const int words = (ncu + 31) / 32;
         std::vector<uint32_t> mc(words, 0u), ms(words, 0u);
         for (int c = 0; c < ncu; ++c) (c < crit_cus ? mc : ms)[c / 32] |= 1u << (c % 32);
-        ok = hipExtStreamCreateWithCUMask(&g.crit, words, mc.data()) == hipSuccess &&
-             hipExtStreamCreateWithCUMask(&g.side, words, ms.data()) == hipSuccess;
+        ok = hipExtStreamCreateWithCUMask(&g->crit, words, mc.data()) == hipSuccess &&
+             hipExtStreamCreateWithCUMask(&g->side, words, ms.data()) == hipSuccess;
     } else {
-        ok = hipStreamCreateWithFlags(&g.crit, hipStreamNonBlocking) == hipSuccess &&
-             hipStreamCreateWithFlags(&g.side, hipStreamNonBlocking) == hipSuccess;
+        ok = hipStreamCreateWithFlags(&g->crit, hipStreamNonBlocking) == hipSuccess &&
+             hipStreamCreateWithFlags(&g->side, hipStreamNonBlocking) == hipSuccess;
     }
-    ok = ok && hipEventCreateWithFlags(&g.ev_in, hipEventDisableTiming) == hipSuccess &&
-         hipEventCreateWithFlags(&g.ev_main, hipEventDisableTiming) == hipSuccess &&
-         hipEventCreateWithFlags(&g.ev_side, hipEventDisableTiming) == hipSuccess;
+    ok = ok && hipEventCreateWithFlags(&g->ev_in, hipEventDisableTiming) == hipSuccess &&
+         hipEventCreateWithFlags(&g->ev_main, hipEventDisableTiming) == hipSuccess &&
+         hipEventCreateWithFlags(&g->ev_side, hipEventDisableTiming) == hipSuccess;
     if (!ok) {
         fprintf(stderr, "gk re-inversion: look-ahead streams unavailable, single stream\n");
-        g = GjSide{};
+        gj_side_release(g);
+        delete g;
         return nullptr;
     }
-    return &g;
+    std::lock_guard<std::mutex> lk(g_side_mu);
+    if (!g_sides) {
+        g_sides = new std::vector<GjSide *>;
+        std::atexit(gj_side_atexit);
+    }
+    g_sides->push_back(g);
+    return g;
+}
+
+void gj_side_destroy(GjSide *g)
+{
+    if (!g) return;
+    {
+        std::lock_guard<std::mutex> lk(g_side_mu);
+        if (g_sides) g_sides->erase(std::remove(g_sides->begin(), g_sides->end(), g), g_sides->end());
+    }
+    gj_side_release(g);
+    delete g;
 }
 
 // event record / wait on valid handles; a failure is reported, never ignored
@@ -597,10 +639,9 @@ static GjSide *gj_side()
     } while (0)
 
 template <int NT, int RPT, int B>
-static double *gjc_run_la(hipStream_t s, double *M, double *M2, double *P0, double *P1, double *xr, int k,
-                          int *piv_step, int *piv, int *flag, double tiny)
+static double *gjc_run_la(GjSide &gs, hipStream_t s, double *M, double *M2, double *P0, double *P1, double *xr,
+                          int k, int *piv_step, int *piv, int *flag, double tiny)
 {
-    GjSide &gs = *gj_side();
     const hipStream_t s_in = s;
     GJCHK(hipEventRecord(gs.ev_in, s_in));
     s = gs.crit;
@@ -663,6 +704,17 @@ __global__ void k_gjb_init(int *piv_step, int k, int *flag)
 
 int gj_blocked_max() { return 8192; }
 
+// whether a re-inversion of order k runs the look-ahead schedule:
+// GK_GJ_LOOKAHEAD=0 never, 2 every k, default (1) k > 2048
+bool gj_lookahead(int k)
+{
+    static const int la = [] {
+        const char *e = std::getenv("GK_GJ_LOOKAHEAD");
+        return e ? std::atoi(e) : 1;
+    }();
+    return la > 1 || (la == 1 && k > 2048);
+}
+
 size_t gj_blocked_scratch(int k)
 {
     // Q (k x B, B <= 32), the outer panel P (k x 64), X_R (32 x 64), the
@@ -675,7 +727,7 @@ size_t gj_blocked_scratch(int k)
 // gj_blocked_scratch(k); returns the buffer holding the result.  BFD_ESING
 // is reported through *flag (1 + step).
 double *gauss_jordan_blocked(hipStream_t s, double *X, double *scratch, int k, int *piv_step, int *piv, int *flag,
-                             double tiny)
+                             double tiny, GjSide *side)
 {
     if (k <= 0) return X;
     hipLaunchKernelGGL(k_gjb_init, dim3(std::min((k + 255) / 256, 64)), dim3(256), 0, s, piv_step, k, flag);
@@ -694,20 +746,15 @@ double *gauss_jordan_blocked(hipStream_t s, double *X, double *scratch, int k, i
         if (k <= 4096) return gjb_run2<1024, 4, 8>(s, X, M2, P, Qm, xr, k, piv_step, piv, flag, tiny);
         return gjb_run2<1024, 8, 4>(s, X, M2, P, Qm, xr, k, piv_step, piv, flag, tiny);
     }
-    // look-ahead (k = 4096: 21.3 -> 19.8 ms; k = 2048: no gain, the panels
-    // slow down by what the hidden updates save), opt-in: GK_GJ_LOOKAHEAD=1
-    // for k > 2048, 2 for every k.  Off by default: a process holding the
-    // CU-masked streams crashed in its exit handlers under rocprofv3.
-    static const int lookahead = [] {
-        const char *e = std::getenv("GK_GJ_LOOKAHEAD");
-        return e ? std::atoi(e) : 0;
-    }();
+    // look-ahead when the caller passes the side streams (gj_lookahead:
+    // k > 2048 by default; k = 4096: 21.3 -> 19.8 ms; k = 2048: no gain, the
+    // panels slow down by what the hidden updates save)
     double *P1 = xr + 32 * GJ_BO;
-    if ((lookahead > 1 || (lookahead == 1 && k > 2048)) && gj_side()) {
-        if (k <= 1024) return gjc_run_la<512, 2, 16>(s, X, M2, P, P1, xr, k, piv_step, piv, flag, tiny);
-        if (k <= 2048) return gjc_run_la<512, 4, 16>(s, X, M2, P, P1, xr, k, piv_step, piv, flag, tiny);
-        if (k <= 4096) return gjc_run_la<512, 8, 8>(s, X, M2, P, P1, xr, k, piv_step, piv, flag, tiny);
-        return gjc_run_la<1024, 8, 4>(s, X, M2, P, P1, xr, k, piv_step, piv, flag, tiny);
+    if (side) {
+        if (k <= 1024) return gjc_run_la<512, 2, 16>(*side, s, X, M2, P, P1, xr, k, piv_step, piv, flag, tiny);
+        if (k <= 2048) return gjc_run_la<512, 4, 16>(*side, s, X, M2, P, P1, xr, k, piv_step, piv, flag, tiny);
+        if (k <= 4096) return gjc_run_la<512, 8, 8>(*side, s, X, M2, P, P1, xr, k, piv_step, piv, flag, tiny);
+        return gjc_run_la<1024, 8, 4>(*side, s, X, M2, P, P1, xr, k, piv_step, piv, flag, tiny);
     }
     if (k <= 1024) return gjc_run<512, 2, 16>(s, X, M2, P, Qm, xr, k, piv_step, piv, flag, tiny);
     if (k <= 2048) return gjc_run<512, 4, 16>(s, X, M2, P, Qm, xr, k, piv_step, piv, flag, tiny);

@@ -20,7 +20,7 @@ import numpy as np
 
 from .problems import (GLP_BS, GLP_DB, GLP_DUAL, GLP_DUALP, GLP_FEAS, GLP_FX, GLP_LO, GLP_MAX, GLP_MIN,
                        GLP_NF, GLP_NL, GLP_NOFEAS, GLP_NS, GLP_NU, GLP_PRIMAL, GLP_UNDEF, GLP_UP, GLP_FR,
-                       Problem)
+                       GLP_ETMLIM, Problem)
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "libglpk_mi355x.so")
@@ -109,7 +109,9 @@ EXPORTS = ["gk_abi_version", "gk_device_count", "gk_ctx_create", "gk_ctx_destroy
            "gk_bfd_ftran", "gk_bfd_btran", "gk_bfd_update", "gk_bfd_get_count", "gk_bfd_valid",
            "gk_spx_primal", "gk_spx_dual", "gk_bfd_last_stats", "gk_bfd_profile", "gk_ios_driver",
            "gk_scale_prob", "gk_scale_prob_timed", "gk_adv_basis", "gk_bfd_set_report",
-           "gk_bfd_eval_tab_rows"]
+           "gk_bfd_eval_tab_rows", "gk_ios_set_report", "gk_ios_driver_sharded", "gk_comm_create",
+           "gk_comm_destroy", "gk_comm_backend", "gk_comm_rank", "gk_comm_size", "gk_comm_allgather",
+           "gk_ios_driver_comm", "gk_comm_set_option"]
 
 # gk_report_fn (glpk_mi355x.h): one progress line or termination message of
 # a gk_spx_* call, in the order the reference prints them
@@ -151,6 +153,16 @@ def load_library(path: str = LIB_PATH):
         f.argtypes = [P, C.POINTER(Lp), P, C.POINTER(Smcp)]
         f.restype = C.c_int
     L.gk_bfd_last_stats.argtypes = [P, C.POINTER(SpxStats)]
+    L.gk_ios_set_report.argtypes = [P, REPORT_FN, P]
+    L.gk_comm_create.restype = P
+    L.gk_comm_create.argtypes = [P, C.c_int, C.c_int, C.c_char_p, C.c_int]
+    L.gk_comm_destroy.argtypes = [P]
+    L.gk_comm_set_option.argtypes = [P, C.c_int, C.c_int]
+    L.gk_comm_backend.argtypes = [P]
+    L.gk_comm_allgather.argtypes = [P, P, C.c_size_t, P]
+    L.gk_comm_allgather.restype = C.c_int
+    L.gk_ios_driver_comm.argtypes = [P, C.POINTER(Mip), C.POINTER(Iocp), P]
+    L.gk_ios_driver_comm.restype = C.c_int
     L.gk_ios_driver.argtypes = [P, C.POINTER(Mip), C.POINTER(Iocp)]
     L.gk_ios_driver.restype = C.c_int
     L.gk_ios_driver_sharded.argtypes = [P, C.POINTER(Mip), C.POINTER(Iocp), C.POINTER(IosShard)]
@@ -197,6 +209,44 @@ class Context:
     def close(self):
         if getattr(self, "h", None):
             self.L.gk_ctx_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        self.close()
+
+
+GK_COMM_AUTO, GK_COMM_TCP, GK_COMM_RCCL = 0, 1, 2
+
+
+class Comm:
+    """The library's collective for the sharded branch and bound
+    (gk_comm_create): one per process, rank 0 listening on addr
+    ("host:port"); RCCL when every rank has a device of its own (backend
+    GK_COMM_AUTO), TCP through rank 0 otherwise.  ctx may be None for
+    GK_COMM_TCP (no device)."""
+
+    def __init__(self, ctx, rank: int, size: int, addr: str = "127.0.0.1:29533", backend: int = GK_COMM_AUTO):
+        self.L = load_library()
+        self.rank, self.size = int(rank), int(size)
+        self.h = self.L.gk_comm_create(ctx.h if ctx is not None else None, self.rank, self.size,
+                                       addr.encode(), int(backend))
+        if not self.h:
+            raise GkError(f"gk_comm_create failed: {_err(self.L)}")
+        self.backend = self.L.gk_comm_backend(self.h)
+
+    def allgather(self, block: bytes) -> list:
+        """every rank's block (all the same size), rank order"""
+        n = len(block)
+        src = C.create_string_buffer(block, n)
+        dst = C.create_string_buffer(n * self.size)
+        if self.L.gk_comm_allgather(self.h, src, n, dst) != 0:
+            raise GkError("gk_comm_allgather failed")
+        raw = dst.raw
+        return [raw[r * n:(r + 1) * n] for r in range(self.size)]
+
+    def close(self):
+        if getattr(self, "h", None):
+            self.L.gk_comm_destroy(self.h)
             self.h = None
 
     def __del__(self):
@@ -659,9 +709,53 @@ def glp_intopt(P: GkProblem, parm: Iocp | None = None, comm=None, ramp_nodes: in
     if np.any(iv & np.isin(t, (GLP_LO, GLP_DB, GLP_FX)) & (lb != np.floor(lb))) or \
             np.any(iv & np.isin(t, (GLP_UP, GLP_DB)) & (ub != np.floor(ub))):
         return GLP_EBOUND
+    if parm.msg_lev >= GLP_MSG_ALL:
+        # glp_intopt's header (glpapi09.js:368-383)
+        ni = int(np.count_nonzero(P.col_kind[1:] == GLP_IV))
+        nb = int(np.count_nonzero((P.col_kind[1:] == GLP_IV) & (P.col_type[1:] == GLP_DB) & (P.col_lb[1:] == 0.0) &
+                                  (P.col_ub[1:] == 1.0)))
+        s = ("none of" if nb == 0 else "" if (ni == 1 and nb == 1) else "one of" if nb == 1 else
+             "all of" if nb == ni else f"{nb} of")
+        _xprintf(f"GLPK Integer Optimizer, v{GLP_VERSION}")
+        _xprintf(f"{P.m} row{'' if P.m == 1 else 's'}, {P.n} column{'' if P.n == 1 else 's'}, "
+                 f"{P.nnz} non-zero{'' if P.nnz == 1 else 's'}")
+        _xprintf(f"{ni} integer variable{'' if ni == 1 else 's'}, {s} which {'is' if nb == 1 else 'are'} binary")
+    ret = _intopt(P, parm, comm, ramp_nodes)
+    # solve_mip's closing messages (glpapi09.js:80-111)
+    if ret == 0 and parm.msg_lev >= GLP_MSG_ALL:
+        _xprintf("INTEGER OPTIMAL SOLUTION FOUND" if P.mip_stat == GLP_OPT else "PROBLEM HAS NO INTEGER FEASIBLE SOLUTION")
+    elif ret == GLP_EMIPGAP and parm.msg_lev >= GLP_MSG_ALL:
+        _xprintf("RELATIVE MIP GAP TOLERANCE REACHED; SEARCH TERMINATED")
+    elif ret == GLP_ETMLIM and parm.msg_lev >= GLP_MSG_ALL:
+        _xprintf("TIME LIMIT EXCEEDED; SEARCH TERMINATED")
+    elif ret == GLP_EFAIL and parm.msg_lev >= GLP_MSG_ERR:
+        _xprintf("glp_intopt: cannot solve current LP relaxation")
+    return ret
+
+
+def _intopt(P: GkProblem, parm: Iocp, comm, ramp_nodes: int) -> int:
     # solve_mip: an optimal basis to the LP relaxation must be provided
     if not (P.valid and P.pbs_stat == GLP_FEAS and P.dbs_stat == GLP_FEAS):
+        if parm.msg_lev >= GLP_MSG_ERR:
+            _xprintf("glp_intopt: optimal basis to initial LP relaxation not provided")
         return GLP_EROOT
+    if parm.msg_lev >= GLP_MSG_ALL:
+        _xprintf("Integer optimization begins...")
+    # show_progress lines of the native driver (glpios03.js:2-48), printed
+    # after the search in the order they were reported
+    lines = []
+    rcb = REPORT_FN(lambda ud, kind, code, it, a, obj, bnd, d:
+                    lines.append(mip_progress_line(P.dir, code, it, a, obj, bnd, d)))
+    P.L.gk_ios_set_report(P.ctx.h, rcb, None)
+    try:
+        return _intopt_run(P, parm, comm, ramp_nodes)
+    finally:
+        P.L.gk_ios_set_report(P.ctx.h, REPORT_FN(), None)
+        for s in lines:
+            _xprintf(s)
+
+
+def _intopt_run(P: GkProblem, parm: Iocp, comm, ramp_nodes: int) -> int:
     mip = Mip()
     mip.lp = P._lp_struct()
     mip.lp.pbs_stat, mip.lp.dbs_stat, mip.lp.obj_val = P.pbs_stat, P.dbs_stat, P.obj_val
@@ -669,6 +763,17 @@ def glp_intopt(P: GkProblem, parm: Iocp | None = None, comm=None, ramp_nodes: in
     mip.col_kind = ptr(P.col_kind)
     mip.col_mipx = ptr(P.col_mipx)
     mip.row_mipx = ptr(P.row_mipx)
+    if isinstance(comm, Comm) and comm.size > 1:
+        # the library's own collective: the sharded search and the agreement
+        # on the winning incumbent in C (gk_ios_driver_comm)
+        P.L.gk_comm_set_option(comm.h, 1, int(ramp_nodes))
+        ret = P.L.gk_ios_driver_comm(P.ctx.h, C.byref(mip), C.byref(parm), comm.h)
+        if ret == GK_EABI:
+            raise GkError(_err(P.L))
+        P.mip_stat = mip.mip_stat
+        P.mip_obj = mip.mip_obj
+        P.mip_stats = _mip_stats(mip)
+        return ret
     if comm is None or comm.size == 1:
         ret = P.L.gk_ios_driver(P.ctx.h, C.byref(mip), C.byref(parm))
         if ret == GK_EABI:
@@ -780,6 +885,40 @@ def report_lines(kind, code, it, phase, obj, inf, aux) -> list:
         return [f"Error: unable to factorize the basis matrix ({aux})",
                 "Sorry, basis recovery procedure not implemented yet"]
     return [_REPORT_MSG[code]] if code in _REPORT_MSG else []
+
+
+def mip_progress_line(dir_, code, it, a_cnt, obj, bnd, deleted) -> str:
+    """show_progress (glpios03.js:2-48) for one GK_RPT_MIP record."""
+    from decimal import Decimal, ROUND_HALF_UP
+    have, empty = bool(code & 2), bool(code & 4)
+    best_mip = _js_num(obj) if have else "not found yet"
+    if empty:
+        best_bound = "tree is empty"
+    elif bnd <= -1.7976931348623157e308:
+        best_bound = "-inf"
+    elif bnd >= 1.7976931348623157e308:
+        best_bound = "+inf"
+    else:
+        best_bound = _js_num(bnd)
+    rho = ">=" if dir_ == GLP_MIN else "<="
+    # ios_relative_gap (glpios01.js:842)
+    if not have:
+        gap = 1.7976931348623157e308
+    elif empty:
+        gap = 0.0
+    else:
+        gap = abs(obj - bnd) / (abs(obj) + 2.220446049250313e-16)
+    if gap == 0.0:
+        rel = "  0.0%"
+    elif gap < 0.001:
+        rel = " < 0.1%"
+    elif gap <= 9.999:
+        # Number.prototype.toFixed(1): the nearest, the larger on a tie
+        rel = "  " + str(Decimal(100.0 * gap).quantize(Decimal("0.1"), rounding=ROUND_HALF_UP)) + "%"
+    else:
+        rel = ""
+    return (f"+{it}: {'>>>>>' if code & 1 else 'mip ='} {best_mip} {rho} {best_bound} {rel} "
+            f"({a_cnt}; {deleted})")
 
 
 def _js_num(x: float) -> str:

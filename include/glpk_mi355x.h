@@ -40,7 +40,7 @@
 extern "C" {
 #endif
 
-#define GK_ABI_VERSION 3
+#define GK_ABI_VERSION 4
 #include <stddef.h>
 #define GK_EABI (-1)          /* contract violation; see gk_last_error() */
 
@@ -268,16 +268,40 @@ typedef struct {
 
 int gk_ios_driver(gk_ctx *ctx, gk_mip *mip, const gk_iocp *parm);
 
+/* The reference's search progress lines (show_progress, glpios03.js:2-48,
+ * printed at :607, :780 and :943), reported instead of printed, on the
+ * calling thread during gk_ios_driver(_sharded) on this context, when
+ * parm->msg_lev >= GLP_MSG_ON: once at the start (the root), at every new
+ * incumbent, every out_frq milliseconds of search, and at the end.  Record
+ * kind GK_RPT_MIP:
+ *   code    bit 0: a new incumbent (">>>>>" instead of "mip ="), bit 1: an
+ *           incumbent exists, bit 2: no active subproblem ("tree is empty")
+ *   it_cnt  simplex iterations so far (the root LP's it_cnt plus every node LP)
+ *   phase   active subproblems (T.a_cnt)
+ *   obj     incumbent objective (original sense)
+ *   infeas  best local bound over the active subproblems (original sense;
+ *           +-DBL_MAX print as "+inf" / "-inf")
+ *   aux     subproblems fathomed so far (T.t_cnt - T.n_cnt; the driver keeps
+ *           no inactive nodes, so this is created minus active)
+ * The host formats "+it: mip = obj >= bound gap (a; d)" as glpios03.js:45. */
+#define GK_RPT_MIP 3
+void gk_ios_set_report(gk_ctx *ctx, gk_report_fn fn, void *ud);
+
 /* one GPU's share of a branch-and-bound run over several GPUs (one process
  * per GPU).  All ranks call gk_ios_driver_sharded on the same problem; they
  * evaluate the first batches identically, split the frontier round-robin
- * (node i -> rank i mod size), and exchange the incumbent value through
- * exchange() every sync_every batches.  exchange() is collective: it receives
- * this rank's best objective (internal minimisation form; DBL_MAX if none) and
- * whether it still has open nodes, must return the minimum over ranks in
- * *best and the number of ranks with work (0 ends the run).  On return each
- * rank holds its own incumbent (mip_stat GLP_OPT with a solution, else
- * GLP_NOFEAS); the caller picks the best over ranks. */
+ * (node i -> rank i mod size), and every sync_every batches run one epoch of
+ * the exchange.  The main path is allgather (gk_comm_allgather of this
+ * library, through gk_ios_driver_comm below, or a host's own): every epoch
+ * all-gathers {incumbent, best open bound, open nodes, active} and hands open
+ * nodes (bounds + warm-start basis) from the ranks with the most to idle
+ * ranks.  Without allgather, exchange() is the
+ * incumbent-only protocol: it receives this rank's best objective (internal
+ * minimisation form; DBL_MAX if none) and whether it still has open nodes,
+ * and must return the minimum over ranks in *best and the number of ranks
+ * with work (0 ends the run).  On return each rank holds its own incumbent
+ * (mip_stat GLP_OPT with a solution, else GLP_NOFEAS); gk_ios_driver_comm
+ * agrees on the best over ranks, a caller of this entry point picks it. */
 typedef struct {
     int rank, size;
     int ramp_nodes;                 /* frontier per rank before the split (0: 8) */
@@ -292,6 +316,41 @@ typedef struct {
     int (*allgather)(void *info, const void *send, size_t bytes, void *recv);
 } gk_ios_shard;
 int gk_ios_driver_sharded(gk_ctx *ctx, gk_mip *mip, const gk_iocp *parm, const gk_ios_shard *shard);
+
+/* ---- collective of the sharded branch and bound --------
+ * One process per GPU, each with a gk_comm.  Rank 0 listens on addr
+ * ("host:port"; the others connect to it: the bootstrap).  The epoch
+ * exchange of the sharded driver is an all-gather of fixed-size byte
+ * blocks: over RCCL (ncclAllGather, xGMI) when every rank drives a device of
+ * its own (GK_COMM_AUTO) or when asked (GK_COMM_RCCL), through rank 0 over
+ * TCP otherwise (ranks sharing a device, hosts without a device: ctx may be
+ * NULL for GK_COMM_TCP).  Blocking; every rank must call the collectives in
+ * the same order. */
+typedef struct gk_comm gk_comm;
+#define GK_COMM_AUTO 0
+#define GK_COMM_TCP 1
+#define GK_COMM_RCCL 2
+gk_comm *gk_comm_create(gk_ctx *ctx, int rank, int size, const char *addr, int backend);   /* NULL on failure */
+void     gk_comm_destroy(gk_comm *comm);
+int      gk_comm_backend(const gk_comm *comm);          /* GK_COMM_TCP | GK_COMM_RCCL */
+int      gk_comm_rank(const gk_comm *comm);
+int      gk_comm_size(const gk_comm *comm);
+/* recv[r * bytes .. (r + 1) * bytes) = rank r's send block; 0 on success.
+ * The signature of gk_ios_shard.allgather (info = the gk_comm). */
+int      gk_comm_allgather(void *comm, const void *send, size_t bytes, void *recv);
+/* options of the sharded search run through gk_ios_driver_comm:
+ * GK_COMM_OPT_RAMP  the frontier per rank before the split (gk_ios_shard.ramp_nodes;
+ *                   0 the default, < 0 split the root alone: rank 0 starts with all the work)
+ * GK_COMM_OPT_SYNC  batches between exchange epochs (gk_ios_shard.sync_every; 0 the default) */
+#define GK_COMM_OPT_RAMP 1
+#define GK_COMM_OPT_SYNC 2
+int      gk_comm_set_option(gk_comm *comm, int opt, int value);
+/* glp_intopt on every rank of comm: gk_ios_driver_sharded with this
+ * library's all-gather, then an all-gather of the ranks' incumbents so that
+ * every rank returns the same winner (best objective, lowest rank on ties),
+ * mip_stat GLP_OPT when the search finished on every rank.  With a
+ * one-rank comm it is gk_ios_driver. */
+int gk_ios_driver_comm(gk_ctx *ctx, gk_mip *mip, const gk_iocp *parm, gk_comm *comm);
 
 /* glp_scale_prob (glpscl.js:1-225) on the device: the
  * row and column scale factors of A (CSC: ptr[0..n] 0-based offsets, ind[]

@@ -30,6 +30,14 @@
             return NULL;                                                            \
         }                                                                           \
     } while (0)
+/* the same in a helper returning int (0: an exception is pending) */
+#define CHECK0(call)                                                                \
+    do {                                                                            \
+        if ((call) != napi_ok) {                                                    \
+            napi_throw_error(env, NULL, "gk_addon: N-API call failed: " #call);     \
+            return 0;                                                               \
+        }                                                                           \
+    } while (0)
 
 static napi_value throw_gk(napi_env env, const char *what)
 {
@@ -359,6 +367,29 @@ static void rpt_collect(void *ud, int kind, int code, int it_cnt, int phase, dou
     b->v[b->n++] = r;
 }
 
+/* L.reports = the collected records (frees them) */
+static int set_reports(napi_env env, napi_value L, rpt_buf *rb)
+{
+    napi_value arr;
+    CHECK0(napi_create_array_with_length(env, rb->n, &arr));
+    for (size_t k = 0; k < rb->n; k++) {
+        const rpt_rec *r = &rb->v[k];
+        const double f[7] = {r->kind, r->code, r->it_cnt, r->phase, r->obj, r->infeas, r->aux};
+        napi_value e, x;
+        CHECK0(napi_create_array_with_length(env, 7, &e));
+        for (uint32_t t = 0; t < 7; t++) {
+            CHECK0(napi_create_double(env, f[t], &x));
+            CHECK0(napi_set_element(env, e, t, x));
+        }
+        CHECK0(napi_set_element(env, arr, (uint32_t)k, e));
+    }
+    CHECK0(napi_set_named_property(env, L, "reports", arr));
+    free(rb->v);
+    rb->v = NULL;
+    rb->n = rb->cap = 0;
+    return 1;
+}
+
 static napi_value js_spx(napi_env env, napi_callback_info info)
 {
     napi_value argv[5];
@@ -389,23 +420,7 @@ static napi_value js_spx(napi_env env, napi_callback_info info)
     gk_bfd_set_report(b, rpt_collect, &rb);
     int ret = dual ? gk_spx_dual(c, &lp, b, &p) : gk_spx_primal(c, &lp, b, &p);
     gk_bfd_set_report(b, NULL, NULL);
-    {
-        napi_value arr;
-        CHECK(napi_create_array_with_length(env, rb.n, &arr));
-        for (size_t k = 0; k < rb.n; k++) {
-            const rpt_rec *r = &rb.v[k];
-            const double f[7] = {r->kind, r->code, r->it_cnt, r->phase, r->obj, r->infeas, r->aux};
-            napi_value e, x;
-            CHECK(napi_create_array_with_length(env, 7, &e));
-            for (uint32_t t = 0; t < 7; t++) {
-                CHECK(napi_create_double(env, f[t], &x));
-                CHECK(napi_set_element(env, e, t, x));
-            }
-            CHECK(napi_set_element(env, arr, (uint32_t)k, e));
-        }
-        CHECK(napi_set_named_property(env, L, "reports", arr));
-        free(rb.v);
-    }
+    if (!set_reports(env, L, &rb)) return NULL;
     if (ret == GK_EABI) return throw_gk(env, dual ? "spx_dual" : "spx_primal");
     set_num(env, L, "it_cnt", lp.it_cnt);
     set_num(env, L, "pbs_stat", lp.pbs_stat);
@@ -416,6 +431,54 @@ static napi_value js_spx(napi_env env, napi_callback_info info)
     return mk_int(env, ret);
 }
 
+/* ------------------------------------------------------------- collective */
+static void comm_fin(napi_env env, void *data, void *hint)
+{
+    (void)env; (void)hint;
+    if (!g_teardown) gk_comm_destroy((gk_comm *)data);
+}
+
+/* commCreate(ctx, rank, size, addr, backend): the library's collective for
+ * the sharded branch and bound (gk_comm_create); ctx may be null (TCP) */
+static napi_value js_comm_create(napi_env env, napi_callback_info info)
+{
+    napi_value argv[5];
+    if (!get_args(env, info, 5, argv)) return NULL;
+    napi_valuetype t;
+    CHECK(napi_typeof(env, argv[0], &t));
+    gk_ctx *c = (t == napi_external) ? (gk_ctx *)get_ext(env, argv[0]) : NULL;
+    int rank = 0, size = 1, backend = 0;
+    CHECK(napi_get_value_int32(env, argv[1], &rank));
+    CHECK(napi_get_value_int32(env, argv[2], &size));
+    CHECK(napi_get_value_int32(env, argv[4], &backend));
+    char addr[256];
+    size_t len = 0;
+    CHECK(napi_get_value_string_utf8(env, argv[3], addr, sizeof addr, &len));
+    gk_comm *m = gk_comm_create(c, rank, size, addr, backend);
+    if (!m) return throw_gk(env, "gk_comm_create");
+    napi_value r;
+    CHECK(napi_create_external(env, m, comm_fin, NULL, &r));
+    return r;
+}
+
+static napi_value js_comm_backend(napi_env env, napi_callback_info info)
+{
+    napi_value argv[1];
+    if (!get_args(env, info, 1, argv)) return NULL;
+    return mk_int(env, gk_comm_backend((gk_comm *)get_ext(env, argv[0])));
+}
+
+/* commOption(comm, opt, value): gk_comm_set_option */
+static napi_value js_comm_option(napi_env env, napi_callback_info info)
+{
+    napi_value argv[3];
+    if (!get_args(env, info, 3, argv)) return NULL;
+    int opt = 0, v = 0;
+    CHECK(napi_get_value_int32(env, argv[1], &opt));
+    CHECK(napi_get_value_int32(env, argv[2], &v));
+    return mk_int(env, gk_comm_set_option((gk_comm *)get_ext(env, argv[0]), opt, v));
+}
+
 /* -------------------------------------------------------------- ios_driver */
 /* ios(ctx, L, iocp): L = the marshalled root problem (solved to optimality,
  * pbs_stat/dbs_stat/obj_val set) plus col_kind (Int8Array [1..n]) and the
@@ -423,8 +486,21 @@ static napi_value js_spx(napi_env env, napi_callback_info info)
  * L.lp_solves; returns the ios_driver code (0 or GLP_ETMLIM) */
 static napi_value js_ios(napi_env env, napi_callback_info info)
 {
-    napi_value argv[3];
-    if (!get_args(env, info, 3, argv)) return NULL;
+    /* ios(ctx, L, iocp[, comm]): with a communicator of more than one rank
+     * the search is sharded over the ranks (gk_ios_driver_comm) */
+    napi_value argv[4];
+    size_t argc = 4;
+    CHECK(napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+    if (argc < 3) {
+        napi_throw_type_error(env, NULL, "ios: (ctx, L, iocp[, comm]) expected");
+        return NULL;
+    }
+    gk_comm *comm = NULL;
+    if (argc >= 4) {
+        napi_valuetype t;
+        CHECK(napi_typeof(env, argv[3], &t));
+        if (t == napi_external) comm = (gk_comm *)get_ext(env, argv[3]);
+    }
     gk_ctx *c = (gk_ctx *)get_ext(env, argv[0]);
     napi_value L = argv[1], I = argv[2];
     gk_mip mip;
@@ -452,7 +528,11 @@ static napi_value js_ios(napi_env env, napi_callback_info info)
     p.pp_tech = (int)dprop(env, I, "pp_tech", 2);
     p.mip_gap = dprop(env, I, "mip_gap", 0.0);
     p.presolve = (int)dprop(env, I, "presolve", 0);
-    int ret = gk_ios_driver(c, &mip, &p);
+    rpt_buf rb = {NULL, 0, 0};
+    gk_ios_set_report(c, rpt_collect, &rb);         /* show_progress lines (glpios03.js:2-48) */
+    int ret = comm ? gk_ios_driver_comm(c, &mip, &p, comm) : gk_ios_driver(c, &mip, &p);
+    gk_ios_set_report(c, NULL, NULL);
+    if (!set_reports(env, L, &rb)) return NULL;
     if (ret == GK_EABI) return throw_gk(env, "ios_driver");
     set_num(env, L, "mip_stat", mip.mip_stat);
     set_num(env, L, "mip_obj", mip.mip_obj);
@@ -572,6 +652,7 @@ static napi_value init(napi_env env, napi_value exports)
     if (getenv("GK_SEGV_TRACE")) signal(SIGSEGV, segv_trace);
     napi_add_env_cleanup_hook(env, teardown_hook, NULL);
     napi_property_descriptor d[] = {
+        FN("commCreate", js_comm_create), FN("commBackend", js_comm_backend), FN("commOption", js_comm_option),
         FN("create", js_create), FN("deviceCount", js_device_count), FN("abiVersion", js_abi_version),
         FN("lastError", js_last_error), FN("bfdCreate", js_bfd_create), FN("bfdSetParm", js_bfd_set_parm),
         FN("bfdFactorizeCsc", js_bfd_factorize_csc), FN("bfdFtran", js_bfd_ftran), FN("bfdBtran", js_bfd_btran),

@@ -199,13 +199,12 @@ function spx(lp, parm, dual, print) {
 var GLP_IV = 2, GLP_FEAS = 2, GLP_OPT = 5;
 
 // the requests the native driver serves: no callbacks (glpios03.js:533-897),
-// no MIP-gap stop, no cut generators / feasibility pump (they stay in JS),
+// no cut generators / feasibility pump (they stay in JS),
 // and node LPs whose work area fits the node kernel's limit (gk_mip.hip:
 // tableau in LDS up to 64 KiB, in HBM slices beyond, at most 8 GiB per node)
 function nativeIos(T) {
     var P = T.mip, parm = T.parm, m = P.m, n = P.n;
     if (parm.cb_func != null) return false;
-    if (parm.mip_gap > 0.0) return false;
     if (parm.gmi_cuts || parm.mir_cuts || parm.cov_cuts || parm.clq_cuts || parm.fp_heur) return false;
     var work = 8 * (m * (2 * m + n) + 4 * (m + n) + m) + 4 * m + (m + n) + 16;
     return work <= 8 * 1024 * 1024 * 1024;
@@ -216,7 +215,50 @@ function nativeIos(T) {
 // the reference's driver writes into the problem on an integer solution
 // (record_solution, glpios03.js:113-135): mip_stat = GLP_FEAS, mip_obj, mipx;
 // solve_mip then turns FEAS into OPT (glpapi09.js:82-92).
-function iosDriver(T) {
+// show_progress (glpios03.js:2-48) for one GK_RPT_MIP record of the native
+// driver: [kind, code (1 bingo | 2 incumbent | 4 tree empty), it_cnt,
+// a_cnt, obj, best bound, fathomed]
+function mipProgressLine(dir, r) {
+    var code = r[1], best_mip, best_bound, rho, rel_gap, temp;
+    best_mip = (code & 2) ? String(r[4]) : "not found yet";
+    if (code & 4) best_bound = "tree is empty";
+    else if (r[5] == -DBL_MAX) best_bound = "-inf";
+    else if (r[5] == +DBL_MAX) best_bound = "+inf";
+    else best_bound = r[5];
+    rho = dir == GLP_MIN ? ">=" : "<=";
+    if (!(code & 2)) temp = DBL_MAX;                      // ios_relative_gap (glpios01.js:842)
+    else if (code & 4) temp = 0.0;
+    else temp = Math.abs(r[4] - r[5]) / (Math.abs(r[4]) + DBL_EPSILON);
+    if (temp == 0.0) rel_gap = "  0.0%";
+    else if (temp < 0.001) rel_gap = " < 0.1%";
+    else if (temp <= 9.999) rel_gap = "  " + Number(100.0 * temp).toFixed(1) + "%";
+    else rel_gap = "";
+    return "+" + r[2] + ": " + ((code & 1) ? ">>>>>" : "mip =") + " " + best_mip + " " + rho + " " + best_bound +
+           " " + rel_gap + " (" + r[3] + "; " + r[6] + ")";
+}
+var GLP_MIN = 1, DBL_MAX = 1.7976931348623157e308, DBL_EPSILON = 2.220446049250313e-16;
+
+// one process per GPU (SURVEY.md §8(e)): with GK_WORLD_SIZE (or WORLD_SIZE)
+// above 1 in the environment, glp_intopt's search is sharded over the ranks
+// through the library's collective (gk_comm: RCCL between distinct devices,
+// TCP through rank 0 otherwise), rank from GK_RANK / RANK, rank 0's address
+// from GK_COMM_ADDR or MASTER_ADDR:MASTER_PORT; every rank returns the same
+// incumbent.  GK_RAMP_NODES < 0 hands the whole tree to rank 0 first (the
+// open-node exchange feeds the others).
+var __comm = undefined;
+function comm() {
+    if (__comm !== undefined) return __comm;
+    var env = process.env;
+    var size = parseInt(env.GK_WORLD_SIZE || env.WORLD_SIZE || '1', 10);
+    if (!(size > 1)) { __comm = null; return __comm; }
+    var rank = parseInt(env.GK_RANK || env.RANK || '0', 10);
+    var addr = env.GK_COMM_ADDR || ((env.MASTER_ADDR || '127.0.0.1') + ':' + (env.MASTER_PORT || '29533'));
+    __comm = addon.commCreate(context(), rank, size, addr, parseInt(env.GK_COMM_BACKEND || '0', 10));
+    if (env.GK_RAMP_NODES) addon.commOption(__comm, 1, parseInt(env.GK_RAMP_NODES, 10));
+    return __comm;
+}
+
+function iosDriver(T, print) {
     var P = T.mip, m = P.m, n = P.n, i, j;
     var g = arrays(P);
     var L = marshal(P, g);
@@ -228,7 +270,10 @@ function iosDriver(T) {
     for (j = 1; j <= n; j++) g.col_kind[j] = P.col[j].kind;
     L.col_kind = g.col_kind; L.row_mipx = g.row_mipx; L.col_mipx = g.col_mipx;
     L.pbs_stat = P.pbs_stat; L.dbs_stat = P.dbs_stat; L.obj_val = P.obj_val;
-    var ret = addon.ios(context(), L, T.parm);
+    var cm = comm();
+    var ret = cm ? addon.ios(context(), L, T.parm, cm) : addon.ios(context(), L, T.parm);
+    if (print && L.reports)
+        L.reports.forEach(function (r) { print(mipProgressLine(P.dir, r)); });
     if (L.mip_stat === GLP_OPT || (ret !== 0 && L.mip_stat === GLP_FEAS)) {
         P.mip_stat = GLP_FEAS;
         P.mip_obj = L.mip_obj;
@@ -242,7 +287,8 @@ module.exports = {
     addon: addon, context: context, nextVersion: nextVersion,
     bfdCreate: bfdCreate, bfdSetParm: bfdSetParm, bfdFactorize: bfdFactorize,
     bfdFtran: bfdFtran, bfdBtran: bfdBtran, bfdUpdate: bfdUpdate, bfdGetCount: bfdGetCount,
-    spx: spx, iosDriver: iosDriver, nativeIos: nativeIos, GLP_BS: GLP_BS
+    spx: spx, iosDriver: iosDriver, nativeIos: nativeIos, GLP_BS: GLP_BS, mipProgressLine: mipProgressLine,
+    comm: comm
 };
 
 // ---- glp_scale_prob (glpscl.js:1) -------------------------------------------

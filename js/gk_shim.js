@@ -19,7 +19,7 @@ bfd_get_count = function (bfd) { return __gk.bfdGetCount(bfd); };
 // ios_driver (glpios03.js:1, called by solve_mip glpapi09.js:79): the native
 // batched B&B when the request is one it serves, else the reference's driver
 var __gk_js_ios_driver = ios_driver;
-ios_driver = function (T) { return __gk.nativeIos(T) ? __gk.iosDriver(T) : __gk_js_ios_driver(T); };
+ios_driver = function (T) { return __gk.nativeIos(T) ? __gk.iosDriver(T, xprintf) : __gk_js_ios_driver(T); };
 
 // glp_scale_prob (glpscl.js:215-225): the factors from the device, the
 // reference's report lines through its own xprintf, the factors stored

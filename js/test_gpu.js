@@ -11,86 +11,9 @@ var fs = require('fs');
 var path = require('path');
 var core = require(path.join(__dirname, 'gk_core.js'));
 
-var GLP_BS = 1, GLP_PRIMAL = 1, GLP_DUALP = 2, GLP_DUAL = 3, GLP_EFAIL = 5;
-var DBL_MAX = Number.MAX_VALUE, INT_MAX = 0x7FFFFFFF;
 
-function smcp(o) {  // SMCP with the reference's `||` defaults (glpapi06.js:359-375)
-    o = o || {};
-    return {msg_lev: o.msg_lev || 3, meth: o.meth || GLP_PRIMAL, pricing: o.pricing || 0x22,
-            r_test: o.r_test || 0x22, tol_bnd: o.tol_bnd || 1e-7, tol_dj: o.tol_dj || 1e-7,
-            tol_piv: o.tol_piv || 1e-10, obj_ll: o.obj_ll || -DBL_MAX, obj_ul: o.obj_ul || +DBL_MAX,
-            it_lim: o.it_lim || INT_MAX, tm_lim: o.tm_lim || INT_MAX, out_frq: o.out_frq || 500,
-            out_dly: o.out_dly || 0, presolve: 0};
-}
-
-function buildLp(fx) {
-    var lp = {m: fx.m, n: fx.n, nnz: fx.nnz, dir: fx.dir, c0: fx.c0, row: [null], col: [null],
-              head: new Int32Array(fx.m + 1), valid: 0, bfd: null, it_cnt: 0};
-    for (var i = 1; i <= fx.m; i++)
-        lp.row.push({i: i, type: fx.row_type[i - 1], lb: fx.row_lb[i - 1], ub: fx.row_ub[i - 1],
-                     rii: fx.row_rii[i - 1], stat: fx.row_stat[i - 1], bind: 0, prim: 0, dual: 0});
-    for (var j = 1; j <= fx.n; j++) {
-        var col = {j: j, type: fx.col_type[j - 1], lb: fx.col_lb[j - 1], ub: fx.col_ub[j - 1],
-                   coef: fx.col_coef[j - 1], sjj: fx.col_sjj[j - 1], stat: fx.col_stat[j - 1],
-                   bind: 0, prim: 0, dual: 0, ptr: null};
-        var last = null;
-        for (var t = fx.A_ptr[j - 1]; t < fx.A_ptr[j]; t++) {
-            var aij = {row: lp.row[fx.A_ind[t]], col: col, val: fx.A_val[t], c_next: null};
-            if (last === null) col.ptr = aij; else last.c_next = aij;
-            last = aij;
-        }
-        lp.col.push(col);
-    }
-    return lp;
-}
-
-// glp_factorize (glpapi12.js:5-94) with b_col (:7-31)
-function factorize(lp) {
-    var m = lp.m, n = lp.n, j = 0;
-    lp.valid = 0;
-    for (var k = 1; k <= m + n; k++) {
-        var rec = k <= m ? lp.row[k] : lp.col[k - m];
-        rec.bind = 0;
-        if (rec.stat === GLP_BS) {
-            j++;
-            if (j > m) return 0x02;               // GLP_EBADB
-            lp.head[j] = k;
-            rec.bind = j;
-        }
-    }
-    if (j < m) return 0x02;
-    if (lp.bfd === null) lp.bfd = core.bfdCreate();
-    function bCol(lp, jj, ind, val) {
-        var kk = lp.head[jj];
-        if (kk <= m) { ind[1] = kk; val[1] = 1.0; return 1; }
-        var len = 0;
-        for (var aij = lp.col[kk - m].ptr; aij !== null; aij = aij.c_next) {
-            len++;
-            ind[len] = aij.row.i;
-            val[len] = -aij.row.rii * aij.val * aij.col.sjj;
-        }
-        return len;
-    }
-    var ret = core.bfdFactorize(lp.bfd, m, lp.head, bCol, lp);
-    if (ret === 1) return 0x03;                   // GLP_ESING
-    if (ret === 2) return 0x04;                   // GLP_ECOND
-    lp.valid = 1;
-    return 0;
-}
-
-function simplex(lp, parm, print) {   // solve_lp (glpapi06.js:3-37)
-    if (!lp.valid) {
-        var r = factorize(lp);
-        if (r) return r;
-    }
-    if (parm.meth === GLP_PRIMAL) return core.spx(lp, parm, false, print);
-    if (parm.meth === GLP_DUALP) {
-        var ret = core.spx(lp, parm, true, print);
-        if (ret === GLP_EFAIL && lp.valid) ret = core.spx(lp, parm, false, print);
-        return ret;
-    }
-    return core.spx(lp, parm, true, print);
-}
+var U = require(path.join(__dirname, 'test_util.js'));
+var smcp = U.smcp, buildLp = U.buildLp, factorize = U.factorize, simplex = U.simplex;
 
 // the display lines and messages the engine reported against the
 // reference's (tests/golden lp_* runs[].lines, minus glp_simplex's own header
@@ -144,24 +67,19 @@ if (global.gc) global.gc();   // finalize the LP section's factor handles now (n
 // through gk_core.iosDriver with the tree object ios_driver receives
 // (T.mip = the problem, T.parm = IOCP with the reference's defaults,
 // glpapi09.js:392-414); solve_mip's FEAS -> OPT / NOFEAS (glpapi09.js:82-92)
-function iocp() {
-    return {msg_lev: 3, br_tech: 4, bt_tech: 4, tol_int: 1e-5, tol_obj: 1e-7, tm_lim: INT_MAX, out_frq: 5000,
-            out_dly: 10000, cb_func: null, cb_info: null, cb_size: 0, pp_tech: 2, mip_gap: 0.0, mir_cuts: 0,
-            gmi_cuts: 0, cov_cuts: 0, clq_cuts: 0, presolve: 0, binarize: 0, fp_heur: 0};
-}
+var iocp = U.iocp;
 var nmip = 0;
-fs.readdirSync(dir).filter(function (f) { return /^mip_.*\.json$/.test(f) && !/12x30/.test(f); }).sort()
+// (C5s instances are stored with their generator: test_util.genC5sFixture
+// rebuilds A, so the deep 12 x 30 tree runs here too)
+fs.readdirSync(dir).filter(function (f) { return /^mip_.*\.json$/.test(f); }).sort()
     .forEach(function (f) {
         var fx = JSON.parse(fs.readFileSync(path.join(dir, f), 'utf8'));
-        if (fx.gen || fx.A_ptr === undefined) return;              // generated instances: Python tests
-        var lp = buildLp(fx);
-        for (var j = 1; j <= fx.n; j++) lp.col[j].kind = fx.col_kind[j - 1];
-        var ret = simplex(lp, smcp(fx.root.opts));
+        if (fx.A_ptr === undefined && !(fx.gen && fx.gen.kind === 'c5s')) return;
+        var mp = U.mipProblem(fx), lp = mp.lp, j;
+        fx = mp.fx;
+        var ret = mp.ret;
         assert.strictEqual(ret, fx.root.ret, f + ' root ret');
         if (lp.pbs_stat !== 2 || lp.dbs_stat !== 2) return;       // glp_intopt would return GLP_EROOT
-        lp.mip_stat = 1; lp.mip_obj = 0.0;
-        for (var i = 1; i <= fx.m; i++) lp.row[i].mipx = 0.0;
-        for (j = 1; j <= fx.n; j++) lp.col[j].mipx = 0.0;
         var T = {mip: lp, parm: iocp()};
         assert.ok(core.nativeIos(T), f + ' not served natively');
         ret = core.iosDriver(T);

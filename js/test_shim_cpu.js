@@ -10,7 +10,7 @@ var names = ['create', 'deviceCount', 'abiVersion', 'lastError', 'bfdCreate', 'b
              'bfdFtran', 'bfdBtran', 'bfdUpdate', 'bfdGetCount', 'bfdValid', 'spx', 'ios', 'stats', 'advBasis',
              'evalTabRows'];
 names.forEach(function (k) { assert.strictEqual(typeof core.addon[k], 'function', k); });
-assert.strictEqual(core.addon.abiVersion(), 3);
+assert.strictEqual(core.addon.abiVersion(), 4);
 
 var ref = process.env.GLPK_REF || '/root/reference';
 var fs = require('fs');
@@ -23,7 +23,11 @@ assert.ok(glpk.__gk_core, 'shim not concatenated');
 assert.ok(/nativeIos/.test(String(glpk.__gk_ios_driver)), 'ios_driver not rebound');
 // requests the native driver does not serve go to the reference's driver
 assert.strictEqual(core.nativeIos({mip: {m: 2, n: 3}, parm: {cb_func: function () {}}}), false);
-assert.strictEqual(core.nativeIos({mip: {m: 2, n: 3}, parm: {cb_func: null, mip_gap: 0.01}}), false);
+assert.strictEqual(core.nativeIos({mip: {m: 2, n: 3}, parm: {cb_func: null, mip_gap: 0.01}}), true);   // mip_gap is native
+// show_progress lines (glpios03.js:45) from the native driver's records
+assert.strictEqual(core.mipProgressLine(1, [3, 0, 57, 1, 0, -1.7976931348623157e308, 0]), '+57: mip = not found yet >= -inf  (1; 0)');
+assert.strictEqual(core.mipProgressLine(1, [3, 3, 529, 133, 284, 259, 10]), '+529: >>>>> 284 >= 259   8.8% (133; 10)');
+assert.strictEqual(core.mipProgressLine(1, [3, 6, 652, 0, 261, 0, 331]), '+652: mip = 261 >= tree is empty   0.0% (0; 331)');
 assert.strictEqual(core.nativeIos({mip: {m: 2, n: 3}, parm: {cb_func: null, mip_gap: 0, gmi_cuts: 1}}), false);
 assert.strictEqual(core.nativeIos({mip: {m: 2, n: 3}, parm: {cb_func: null, mip_gap: 0}}), true);
 // node LPs beyond 64 KiB of LDS run natively too (HBM work area); only a

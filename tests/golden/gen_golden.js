@@ -272,16 +272,19 @@ function lpCase(name, mk, gen, methods, traceCap, extraRuns) {
 // MIP instance: root primal glp_simplex then glp_intopt (default IOCP), the
 // flow of SURVEY.md §8(d) C4/C5.
 function mipCase(name, mk, gen) {
-    if (ONLY && name.indexOf(ONLY) !== 0) return;
+    if (ONLY && ('mip_' + name).indexOf(ONLY) !== 0) return;
     var P = mk();
     var d = dumpProb(P, gen);
     d.name = name; d.kind = 'mip';
     var root = runLp(P, {}, 0);
     delete root.trace;
     var s0 = glpk.__cnt.solve_node, f0 = glpk.__cnt.factorize, it0 = P.it_cnt;
+    var lines = [];
+    glpk.glp_set_print_func(function (s) { lines.push(s); });
     var t0 = process.hrtime.bigint();
     var ret = glpk.glp_intopt(P, new glpk.IOCP({}));
     var dt = Number(process.hrtime.bigint() - t0) / 1e9;
+    glpk.glp_set_print_func(function () {});
     var j, x = [];
     for (j = 1; j <= P.n; j++) x.push(P.col[j].mipx);
     var rx = [];
@@ -289,7 +292,7 @@ function mipCase(name, mk, gen) {
     d.root = root;
     d.mip = {ret: ret, mip_stat: P.mip_stat, mip_obj: P.mip_obj, col_mipx: x, row_mipx: rx,
              lp_solves: glpk.__cnt.solve_node - s0, factorizations: glpk.__cnt.factorize - f0,
-             pivots: P.it_cnt - it0, seconds: dt};
+             pivots: P.it_cnt - it0, seconds: dt, lines: lines};
     fs.writeFileSync(path.join(OUT, 'mip_' + name + '.json'), JSON.stringify(d));
     console.log('wrote mip', name, 'ret', ret, 'obj', P.mip_obj, 'lp', d.mip.lp_solves, 'piv', d.mip.pivots, 'sec', dt.toFixed(2));
 }
@@ -306,20 +309,24 @@ function mipOptsCase(name, mk, optsList) {
         var P = mk();
         var root = runLp(P, {}, 0);
         var s0 = glpk.__cnt.solve_node, it0 = P.it_cnt;
+        var lines = [];
+        glpk.glp_set_print_func(function (s) { lines.push(s); });
         var t0 = process.hrtime.bigint();
         var ret = glpk.glp_intopt(P, new glpk.IOCP(opts));
         var dt = Number(process.hrtime.bigint() - t0) / 1e9;
+        glpk.glp_set_print_func(function () {});
         var j, x = [];
         for (j = 1; j <= P.n; j++) x.push(P.col[j].mipx);
         d.runs.push({opts: opts, root_ret: root.ret, ret: ret, mip_stat: P.mip_stat, mip_obj: P.mip_obj, col_mipx: x,
-                     lp_solves: glpk.__cnt.solve_node - s0, pivots: P.it_cnt - it0, seconds: dt});
+                     lp_solves: glpk.__cnt.solve_node - s0, pivots: P.it_cnt - it0, seconds: dt, lines: lines});
     });
     fs.writeFileSync(path.join(OUT, 'mipopt_' + name + '.json'), JSON.stringify(d));
     console.log('wrote mipopt', name, d.runs.map(function (r) {
         return JSON.stringify(r.opts) + ':ret' + r.ret + ':mip' + r.mip_obj + ':lp' + r.lp_solves; }).join(' '));
 }
 var MIP_OPTS = [{br_tech: 1}, {br_tech: 2}, {br_tech: 3}, {br_tech: 5}, {bt_tech: 1}, {bt_tech: 2}, {bt_tech: 4},
-                {br_tech: 3, bt_tech: 1}, {br_tech: 5, bt_tech: 4}, {pp_tech: 1}, {br_tech: 1, bt_tech: 2, pp_tech: 1}];
+                {br_tech: 3, bt_tech: 1}, {br_tech: 5, bt_tech: 4}, {pp_tech: 1}, {br_tech: 1, bt_tech: 2, pp_tech: 1},
+                {mip_gap: 0.05}, {mip_gap: 0.01}, {mip_gap: 0.002, bt_tech: 2}];
 
 // ---- C3 at full size (BASELINE.json configs[2]): the headline instance -----
 // The reference's own timing run (BASELINE.md: first 300 dual pivots) as

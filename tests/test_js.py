@@ -34,3 +34,38 @@ def test_js_gpu_parity():
     r = subprocess.run([NODE, os.path.join(ROOT, "js", "test_gpu.js")], capture_output=True, text=True, timeout=600)
     assert r.returncode == 0, r.stdout + r.stderr
     assert "ok js gpu parity" in r.stdout
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("ramp", ["0", "-1"], ids=["split", "rank0-starts-with-all"])
+def test_js_sharded_bnb_two_processes(ramp):
+    """glp_intopt sharded over two node processes (one GPU here: the TCP
+    transport of the library's collective; RCCL between distinct GPUs) through
+    the N-API boundary, on gap and C5s 12x30: both ranks return the
+    reference's objective and the same incumbent, also when rank 1 starts
+    with no open node (GK_RAMP_NODES < 0: the open-node exchange feeds it)."""
+    import json
+    import socket
+    _addon()
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    names = ["gap", "c5s_12x30"]
+    procs = []
+    for rank in (0, 1):
+        env = dict(os.environ, GK_WORLD_SIZE="2", GK_RANK=str(rank), GK_COMM_ADDR=f"127.0.0.1:{port}",
+                   GK_RAMP_NODES=ramp)
+        procs.append(subprocess.Popen([NODE, os.path.join(ROOT, "js", "test_sharded.js")] + names, env=env,
+                                      stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True))
+    outs = [p.communicate(timeout=300) for p in procs]
+    for p, (o, e) in zip(procs, outs):
+        assert p.returncode == 0, o + e
+    res = [[json.loads(line) for line in o.strip().splitlines()] for o, _ in outs]
+    for k, name in enumerate(names):
+        ref = json.load(open(os.path.join(ROOT, "tests", "golden", f"mip_{name}.json")))["mip"]
+        a, b = res[0][k], res[1][k]
+        for r in (a, b):
+            assert r["name"] == name and r["ret"] == ref["ret"] and r["mip_stat"] == ref["mip_stat"], r
+            assert abs(r["mip_obj"] - ref["mip_obj"]) <= 1e-9 * max(1.0, abs(ref["mip_obj"])), r["mip_obj"]
+        assert a["x"] == b["x"], f"{name}: the ranks disagree on the incumbent"

@@ -20,7 +20,7 @@ def main():
     name = sys.argv[1] if len(sys.argv) > 1 else "c5s_12x30"
     d = json.load(open(os.path.join(ROOT, "tests", "golden", "mip_" + name + ".json")))
     ctx = gk.Context(0)
-    for rep in range(2):
+    for rep in range(3):
         P = gk.GkProblem(ctx, problems.from_fixture(d))
         assert gk.glp_simplex(P, gk.SMCP(msg_lev=gk.GLP_MSG_ERR)) == 0
         ctx.mark(1)
