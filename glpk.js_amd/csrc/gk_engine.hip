@@ -272,6 +272,15 @@ struct gk_bfd {
     void *rpt_ud = nullptr;
 };
 
+// updates the factor takes before it is rebuilt: nfs_max Forrest-Tomlin
+// updates (glpfhv.js:182), or nrs_max Schur-complement updates for BG / GR
+// (lpf_update_it's LPF_ELIMIT, glplpf.js:359)
+static int upd_limit_parm(const gk_bfcp &p)
+{
+    const int v = (p.type == 2 || p.type == 3) ? p.nrs_max : p.nfs_max;
+    return v > 0 ? v : 100;
+}
+
 static const size_t PARTIAL_CAP = (size_t)1 << 22;   // >= splits * rows of every gemv (see gemv_plan, dual_plan)
 static const int AW_SPLITS = 64;                      // splits of A w over the reference-space columns
 
@@ -763,8 +772,18 @@ struct Spx {
     }
     void push_state()
     {
-        *E->st_host = hs;
-        HIPCHK(hipMemcpyAsync(E->st.p, E->st_host, sizeof(DState), hipMemcpyHostToDevice, s));
+        // through its own slot of the staging ring: the copy may still be
+        // queued when the host writes the next state (init returns without
+        // waiting for its uploads)
+        char *stage = pin_take(sizeof(DState));
+        if (!stage) {
+            *E->st_host = hs;
+            HIPCHK(hipMemcpyAsync(E->st.p, E->st_host, sizeof(DState), hipMemcpyHostToDevice, s));
+            sync();
+            return;
+        }
+        std::memcpy(stage, &hs, sizeof(DState));
+        HIPCHK(hipMemcpyAsync(E->st.p, stage, sizeof(DState), hipMemcpyHostToDevice, s));
     }
     void pull_state()
     {
@@ -1433,7 +1452,9 @@ void Spx::init()
     // the drift of the updated values against a fresh evaluation, measured at
     // every re-inversion, stays far below the tolerances the reference's own
     // checks use (drift_adapt); a chain whose drift grows is shortened
-    const int nfs = f->parm.nfs_max > 0 ? f->parm.nfs_max : 100;
+    // (BG / GR: the Schur-complement factor takes nrs_max updates before it
+    // is rebuilt, glpbfd.js via lpf_create_it(nrs_max) and LPF_ELIMIT)
+    const int nfs = upd_limit_parm(f->parm);
     int lim = nfs;
     if (nfs == 100) {
         upd_cap = std::max(nfs, std::min(1000, m / 4));
@@ -1453,7 +1474,8 @@ void Spx::init()
     it_beg = L->it_cnt;
     tm_beg = now_s();
     push_state();
-    sync();
+    // no wait here: the uploads are staged in the pinned ring and ordered on
+    // the stream before everything the solve enqueues next
 }
 
 int Spx::batch(int K, int rigorous)
@@ -2255,7 +2277,7 @@ int gk_bfd_update(gk_bfd *f, int j, int len, const int *ind, int idx, const doub
         ABI_REQUIRE(f && f->valid, "bfd_update_it: factorization is not valid");
         const int m = f->m;
         ABI_REQUIRE(1 <= j && j <= m, "fhv_update_it: j = %d; column number out of range", j);
-        if (f->upd_cnt >= (f->parm.nfs_max > 0 ? f->parm.nfs_max : 100)) { f->valid = 0; return 4; }  // BFD_ELIMIT
+        if (f->upd_cnt >= upd_limit_parm(f->parm)) { f->valid = 0; return 4; }  // BFD_ELIMIT
         HIPCHK(hipSetDevice(f->ctx->device));
         hipStream_t s = f->ctx->stream;
         std::vector<double> a(m + 1, 0.0);

@@ -351,7 +351,7 @@ static void trivial_lp(orc_prob *P, const orc_smcp *parm)           /* :149 */
 
 int orc_simplex(orc_prob *P, const orc_smcp *parm)                    /* :1 */
 {
-    int i, j, ret;
+    int i, j, ret = 0;
     if (P->tree != NULL) { /* glp_simplex is allowed only outside callbacks (:265) */ }
     if (!(parm->msg_lev == GLP_MSG_OFF || parm->msg_lev == GLP_MSG_ERR || parm->msg_lev == GLP_MSG_ON ||
           parm->msg_lev == GLP_MSG_ALL || parm->msg_lev == GLP_MSG_DBG))
@@ -508,6 +508,15 @@ void orc_prob_set_bfcp(orc_prob *P, int type, int nfs_max, int nrs_max)
     if (nfs_max > 0) P->bfcp->nfs_max = nfs_max;
     if (nrs_max > 0) P->bfcp->nrs_max = nrs_max;
     if (P->bfcp->rs_size == 0) P->bfcp->rs_size = 20 * P->bfcp->nrs_max;
+    if (P->bfd != NULL) bfd_set_parm(P->bfd, P->bfcp);
+}
+
+void orc_prob_set_upd_tol(orc_prob *P, double upd_tol)
+{
+    /* glp_set_bfcp's upd_tol field (glpfhv.js:436-442 uses it), after
+     * orc_prob_set_bfcp */
+    ORC_ASSERT(P->bfcp != NULL);
+    P->bfcp->upd_tol = upd_tol;
     if (P->bfd != NULL) bfd_set_parm(P->bfd, P->bfcp);
 }
 

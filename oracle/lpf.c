@@ -8,12 +8,19 @@
  *
  * Reproduced as the JS behaves, including lpf_update_it's idx = 0 calls of
  * s_prod/rt_prod (glplpf.js:420/:422), which accumulate the new Schur row and
- * column into the f/v part of the work arrays instead of the g/w part. */
+ * column into the f/v part of the work arrays instead of the g/w part.
+ * orc_lpf_fixed != 0 (orc_set_lpf_fix) applies the offsets of the C original
+ * instead (idx = m0: the g = fg + m0 and w = vw + m0 parts that
+ * scf_update_exp reads), the variant tests/golden/gen_golden.js --lpf-fix runs
+ * through the reference. */
 #include <math.h>
 #include <string.h>
 #include "orc.h"
 
 #define SCF_EPS 1e-10
+
+int orc_lpf_fixed = 0;
+void orc_set_lpf_fix(int on) { orc_lpf_fixed = on != 0; }
 
 orc_scf *scf_create_it(int n_max)
 {
@@ -386,8 +393,8 @@ int lpf_update_it(orc_lpf *lpf, int j, int bh, int len, const int *ind, int idx,
         if (vw[i] != 0.0) { lpf->v_ind[v_ptr] = i; lpf->v_val[v_ptr] = vw[i]; v_ptr++; }
     lpf->S_len[n + 1] = v_ptr - lpf->v_ptr;
     lpf->v_ptr = v_ptr;
-    s_prod(lpf, fg, 0, -1.0, fg);            /* glplpf.js:420, idx 0 as in the JS */
-    rt_prod(lpf, vw, 0, -1.0, vw);           /* glplpf.js:422 */
+    s_prod(lpf, fg, orc_lpf_fixed ? m0 : 0, -1.0, fg);     /* glplpf.js:420, idx 0 as in the JS */
+    rt_prod(lpf, vw, orc_lpf_fixed ? m0 : 0, -1.0, vw);    /* glplpf.js:422 */
     z = 0.0;
     for (i = 1; i <= m0; i++) z -= vw[i] * fg[i];
     switch (scf_update_exp(lpf->scf, fg, m0, vw, m0, z)) {

@@ -187,6 +187,8 @@ extern orc_trace_fn orc_trace; extern void *orc_trace_ctx;
 /* "Warning: numerical instability" events (check_stab failures) since load */
 extern long orc_instab_events; extern int orc_instab_last_it;
 long orc_instab_count(int *last_it);
+void orc_prob_set_upd_tol(orc_prob *P, double upd_tol);
+void orc_set_lpf_fix(int on);
 
 /* glpapi06.js / glpapi12.js */
 void orc_smcp_default(orc_smcp *parm);

@@ -72,6 +72,8 @@ def lib():
         L.orc_prob_factorize.argtypes = [P]
         L.orc_prob_ftran.argtypes = [P, f8p, C.c_int]
         L.orc_prob_set_bfcp.argtypes = [P, C.c_int, C.c_int, C.c_int]
+        L.orc_prob_set_upd_tol.argtypes = [P, C.c_double]
+        L.orc_set_lpf_fix.argtypes = [C.c_int]
         L.orc_last_error.restype = C.c_char_p
         L.orc_scale_prob.argtypes = [C.c_int, C.c_int, i4p, i4p, f8p, C.c_int, f8p, f8p, f8p]
         L.orc_scale_prob.restype = C.c_int
@@ -106,8 +108,10 @@ class OracleProb:
             lib().orc_prob_delete(self.h)
             self.h = None
 
-    def set_bfcp(self, type_, nfs_max=0, nrs_max=0):
+    def set_bfcp(self, type_, nfs_max=0, nrs_max=0, upd_tol=None):
         lib().orc_prob_set_bfcp(self.h, type_, nfs_max, nrs_max)
+        if upd_tol is not None:
+            lib().orc_prob_set_upd_tol(self.h, upd_tol)
 
     def simplex(self, trace: list | None = None, **opts) -> int:
         f = SmcpFlat(**{k: v for k, v in opts.items() if k in dict(SmcpFlat._fields_)})
@@ -152,6 +156,12 @@ class OracleProb:
         out = {k: getattr(r, k) for k, _ in ResultFlat._fields_}
         out.update(a)
         return out
+
+
+def set_lpf_fix(on: bool):
+    """Schur-complement update with the C original's offsets (oracle/lpf.c)
+    instead of glplpf.js:420/:422's idx 0."""
+    lib().orc_set_lpf_fix(1 if on else 0)
 
 
 def instab_count():

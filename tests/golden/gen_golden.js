@@ -13,6 +13,7 @@
 //     (glpbfd.js:47), rebinding the closure names (SURVEY.md §0).
 //
 // usage: node tests/golden/gen_golden.js [--big] [--only PREFIX]
+//        node tests/golden/gen_golden.js --lpf-fix --only bfcpfix_
 //        node --max-old-space-size=12000 tests/golden/gen_golden.js --c3
 //          (C3 4096x16384 at full size only: the reference's state after its
 //           first 300 dual pivots, one it_lim=300 call and three it_lim=100
@@ -26,6 +27,11 @@ var OUT = __dirname;
 var BIG = process.argv.indexOf('--big') >= 0;
 var C3 = process.argv.indexOf('--c3') >= 0;
 var ONLY = process.argv.indexOf('--only') >= 0 ? process.argv[process.argv.indexOf('--only') + 1] : null;
+// --lpf-fix: the throw-away copy with the two offsets of lpf_update_it
+// corrected (glplpf.js:420, :422 pass 0 where the new column and row of C
+// live at g = fg + m0 and w = vw + m0, as scf_update_exp reads them at :427);
+// only the bfcp cases run, written as bfcpfix_*.json
+var LPF_FIX = process.argv.indexOf('--lpf-fix') >= 0;
 
 function buildBundle() {
     var lib = path.join(REF, 'lib');
@@ -42,6 +48,12 @@ function buildBundle() {
             src = src.replace('\n        change_basis(csa);',
                 '\n        if (__trace) __trace(2, csa.it_cnt, csa.phase, csa.p, csa.q, csa.head[csa.m+csa.q], csa.head[csa.p], csa.delta);' +
                 '\n        change_basis(csa);');
+        if (f === 'glplpf.js' && LPF_FIX) {
+            var fixed = src.replace('s_prod(lpf, x, 0, -1.0, f);', 's_prod(lpf, x, m0, -1.0, f);')
+                           .replace('rt_prod(lpf, y, 0, -1.0, v);', 'rt_prod(lpf, y, m0, -1.0, v);');
+            if (fixed === src) throw new Error('lpf-fix: pattern not found');
+            src = fixed;
+        }
         parts.push(src);
     });
     parts.push([
@@ -54,7 +66,7 @@ function buildBundle() {
         'exports["__glp_adv_basis"] = glp_adv_basis;',
         ''].join('\n'));
     parts.push(fs.readFileSync(path.join(REF, 'footer'), 'utf8'));
-    var dst = '/tmp/glpk_golden_bundle.js';
+    var dst = LPF_FIX ? '/tmp/glpk_golden_bundle_lpffix.js' : '/tmp/glpk_golden_bundle.js';
     fs.writeFileSync(dst, parts.join('\n'));
     return require(dst);
 }
@@ -269,6 +281,32 @@ function lpCase(name, mk, gen, methods, traceCap, extraRuns) {
     writeJson('lp_' + name, d);
 }
 
+// LP instance under glp_set_bfcp (glpapi12.js:133): the factorization type
+// (FT / BG / GR: glpfhv, glplpf + glpscf) and the refactorization limit
+// nfs_max / nrs_max; primal and dual from the initial basis, each on a fresh
+// copy, it_lim 2000 (glp_set_bfcp's BG / GR do not converge on the dense
+// LP: see --lpf-fix).  The records keep the factorization count of each run.
+var BFCP_RUNS = [{type: 2}, {type: 3}, {nfs_max: 20}, {type: 2, nrs_max: 15}, {upd_tol: 0.5}];
+function bfcpCase(name, mk, gen) {
+    var pre = LPF_FIX ? 'bfcpfix_' : 'bfcp_';
+    if (ONLY && (pre + name).indexOf(ONLY) !== 0) return;
+    var d = dumpProb(mk(), gen);
+    d.name = name; d.kind = 'lp'; d.runs = [];
+    BFCP_RUNS.forEach(function (b) {
+        [1, 3].forEach(function (meth) {
+            var P = mk(), parm = {};
+            glpk.glp_get_bfcp(P, parm);
+            Object.keys(b).forEach(function (k) { parm[k] = b[k]; });
+            glpk.glp_set_bfcp(P, parm);
+            var r = runLp(P, {meth: meth, it_lim: 2000}, 100000);
+            r.bfcp = b;
+            d.runs.push(r);
+        });
+    });
+    d.lpf_fix = LPF_FIX;
+    writeJson(pre + name, d);
+}
+
 // MIP instance: root primal glp_simplex then glp_intopt (default IOCP), the
 // flow of SURVEY.md §8(d) C4/C5.
 function mipCase(name, mk, gen) {
@@ -382,6 +420,11 @@ for (var sd = 1; sd <= 32; sd++) {
             lpCase('mix' + sd, function () { return genMix(sd, mm, nn, 0.35, false, true); }, null, [1, 2, 3]);
     })(sd, mm, nn);
 }
+bfcpCase('gap', function () { return readLp('gap.lpt'); }, null);
+bfcpCase('todd', function () { return readLp('todd.lpt'); }, null);
+bfcpCase('dense_64x256', function () { return genDense(64, 256, 42); }, {kind: 'dense', m: 64, n: 256, seed: 42});
+bfcpCase('mix20', function () { return genMix(20, 4 + (20 * 7) % 29, 5 + (20 * 13) % 41, 0.35, false, true); }, null);
+if (LPF_FIX) process.exit(0);
 mipCase('gap', function () { return readLp('gap.lpt'); }, null);
 mipCase('todd', function () { return readLp('todd.lpt'); }, null);
 mipCase('c5s_12x20', function () { return genC5s(12, 20, 42); }, {kind: 'c5s', m: 12, n: 20, seed: 42});

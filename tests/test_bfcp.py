@@ -1,0 +1,124 @@
+"""glp_set_bfcp (glpapi12.js:133): factorization type and update limits.
+
+Fixtures (tests/golden/gen_golden.js, bfcpCase) run the reference's
+glp_simplex under {type: GLP_BF_BG}, {type: GLP_BF_GR}, {nfs_max: 20},
+{type: GLP_BF_BG, nrs_max: 15} and {upd_tol: 0.5}, primal and dual, on gap,
+todd, dense 64x256 and mix20:
+
+  * bfcp_*.json    — the reference as it is.  Its BG / GR Schur-complement
+    update is broken: lpf_update_it passes offset 0 to s_prod / rt_prod
+    (glplpf.js:420, :422) where the new column and row of C live at
+    g = fg + m0 and w = vw + m0 (scf_update_exp reads them there, :427), so
+    from the second update on the factor solves a different matrix.  gap
+    ends in "unable to factorize" (GLP_EFAIL), dense 64x256 cycles to the
+    iteration limit, and the dual on mix20 stops "optimal" at a wrong
+    objective (-11.4943 against the FT optimum -11.4975).
+  * bfcpfix_*.json — the same runs through the reference with those two
+    offsets corrected (gen_golden.js --lpf-fix): every run reaches the FT
+    optimum.
+
+The oracle restates both (oracle/lpf.c, orc_set_lpf_fix) and is pinned bit
+for bit to each.  The device factor is an explicit inverse for every type
+(include/glpk_mi355x.h): it computes what a correct BG / GR factor computes,
+so the GPU runs are held to the bfcpfix_ fixtures, and to the bfcp_ ones on
+every run whose factor is not the broken one (FT with nfs_max / upd_tol)."""
+import os
+
+import numpy as np
+import pytest
+
+from conftest import golden_files, load_golden
+from glpk_js_amd import problems
+
+CASES = []
+for path in golden_files("bfcp_") + golden_files("bfcpfix_"):
+    d = load_golden(path)
+    for r, run in enumerate(d["runs"]):
+        b = ",".join(f"{k}{v}" for k, v in run["bfcp"].items())
+        CASES.append(pytest.param(path, r, id=f"{os.path.basename(path)[:-5]}-{b}-m{run['opts']['meth']}"))
+
+
+def _oracle_bfcp(o, b):
+    o.set_bfcp(b.get("type", 1), b.get("nfs_max", 0), b.get("nrs_max", 0), b.get("upd_tol"))
+
+
+@pytest.mark.parametrize("path,run_index", CASES)
+def test_oracle_bfcp_bit_exact(oracle, path, run_index):
+    d = load_golden(path)
+    run = d["runs"][run_index]
+    oracle.set_lpf_fix(bool(d.get("lpf_fix")))
+    try:
+        o = oracle.OracleProb(problems.from_fixture(d))
+        _oracle_bfcp(o, run["bfcp"])
+        trace = []
+        ret = o.simplex(trace=trace, **run["opts"])
+        r = o.result()
+    finally:
+        oracle.set_lpf_fix(False)
+    assert ret == run["ret"]
+    assert (r["pbs_stat"], r["dbs_stat"]) == (run["pbs_stat"], run["dbs_stat"])
+    assert r["it_cnt"] == run["it_cnt"]
+    assert r["obj_val"] == run["obj_val"]
+    for key in ("row_prim", "row_dual", "col_prim", "col_dual"):
+        np.testing.assert_array_equal(r[key], np.asarray(run[key], dtype=np.float64), err_msg=key)
+    assert [tuple(t) for t in trace[:len(run["trace"])]] == [tuple(t) for t in run["trace"]]
+
+
+def test_reference_bg_gr_defect_is_what_the_fixtures_show():
+    """The two fixture sets differ exactly on the BG / GR runs (the FT runs
+    with nfs_max / upd_tol are the same computation in both), and the
+    corrected BG / GR runs reach the FT objective of lp_* fixtures."""
+    for path in golden_files("bfcp_"):
+        a = load_golden(path)
+        b = load_golden(path.replace("bfcp_", "bfcpfix_"))
+        for ra, rb in zip(a["runs"], b["runs"]):
+            assert ra["bfcp"] == rb["bfcp"] and ra["opts"] == rb["opts"]
+            if ra["bfcp"].get("type", 1) == 1:
+                assert ra["trace"] == rb["trace"] and ra["obj_val"] == rb["obj_val"]
+            assert rb["ret"] == 0
+        ref_ft = {r["opts"]["meth"]: r["obj_val"] for r in b["runs"] if r["bfcp"].get("type", 1) == 1}
+        for rb in b["runs"]:
+            want = ref_ft[rb["opts"]["meth"]]
+            assert abs(rb["obj_val"] - want) <= 1e-9 * max(1.0, abs(want))
+    gap = load_golden(os.path.join(os.path.dirname(__file__), "golden", "bfcp_gap.json"))
+    assert any(r["ret"] == problems.GLP_EFAIL for r in gap["runs"] if r["bfcp"].get("type") == 2)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("path,run_index", CASES)
+def test_gpu_bfcp_matches_reference(gpu_ctx, path, run_index):
+    from glpk_js_amd import gk
+    d = load_golden(path)
+    run = d["runs"][run_index]
+    broken = not d.get("lpf_fix") and run["bfcp"].get("type", 1) in (2, 3)
+    if broken:
+        # the device's BG / GR factor is a correct one: compare with the
+        # corrected reference run
+        fixed = load_golden(path.replace("bfcp_", "bfcpfix_"))
+        run = fixed["runs"][run_index]
+    P = gk.GkProblem(gpu_ctx, problems.from_fixture(d))
+    P.set_bfcp(**run["bfcp"])
+    ret = gk.glp_simplex(P, gk.SMCP(**run["opts"]))
+    assert ret == run["ret"]
+    assert (P.pbs_stat, P.dbs_stat) == (run["pbs_stat"], run["dbs_stat"])
+    ref = run["obj_val"]
+    assert abs(P.obj_val - ref) <= 1e-9 * max(1.0, abs(ref)), (P.obj_val, ref)
+    for got, want in ((P.col_prim[1:], run["col_prim"]), (P.row_dual[1:], run["row_dual"])):
+        want = np.asarray(want, np.float64)
+        assert np.max(np.abs(np.asarray(got) - want), initial=0.0) <= 1e-7 * (1.0 + np.abs(want).max(initial=0.0))
+
+
+@pytest.mark.gpu
+def test_gpu_update_limit_follows_bfcp(gpu_ctx):
+    """nfs_max (FT) and nrs_max (BG / GR) bound the product-form chain of the
+    device inverse: a 300-pivot dual run on dense 256x1024 re-inverts at least
+    every limit updates (glpfhv.js:182 BFD_ELIMIT, glplpf.js:359 LPF_ELIMIT)."""
+    from glpk_js_amd import gk
+    d = load_golden(os.path.join(os.path.dirname(__file__), "golden", "lp_dense_256x1024.json"))
+    for kw, lim in (({"nfs_max": 20}, 20), ({"type": 2, "nrs_max": 15}, 15), ({"type": 3, "nfs_max": 7}, 100)):
+        P = gk.GkProblem(gpu_ctx, problems.from_fixture(d))
+        P.set_bfcp(**kw)
+        ret = gk.glp_simplex(P, gk.SMCP(meth=gk.GLP_DUAL, it_lim=300))
+        st = P.stats()
+        assert ret in (0, problems.GLP_EITLIM)
+        assert st.reinversions >= P.it_cnt // lim, (kw, st.reinversions, P.it_cnt)
