@@ -111,7 +111,9 @@ EXPORTS = ["gk_abi_version", "gk_device_count", "gk_ctx_create", "gk_ctx_destroy
            "gk_scale_prob", "gk_scale_prob_timed", "gk_adv_basis", "gk_bfd_set_report",
            "gk_bfd_eval_tab_rows", "gk_ios_set_report", "gk_ios_driver_sharded", "gk_comm_create",
            "gk_comm_destroy", "gk_comm_backend", "gk_comm_rank", "gk_comm_size", "gk_comm_allgather",
-           "gk_ios_driver_comm", "gk_comm_set_option"]
+           "gk_ios_driver_comm", "gk_comm_set_option", "gk_npp_create", "gk_npp_destroy", "gk_npp_load",
+           "gk_npp_simplex", "gk_npp_integer", "gk_npp_build_size", "gk_npp_build", "gk_npp_postprocess",
+           "gk_npp_unload_sol", "gk_npp_unload_mip"]
 
 # gk_report_fn (glpk_mi355x.h): one progress line or termination message of
 # a gk_spx_* call, in the order the reference prints them
@@ -592,7 +594,8 @@ def glp_eval_tab_row(P: GkProblem, k: int):
 
 
 def glp_simplex(P: GkProblem, parm: Smcp | None = None) -> int:
-    """glp_simplex (glpapi06.js:1) with presolve OFF."""
+    """glp_simplex (glpapi06.js:1); presolve = GLP_ON runs the native
+    preprocessor (presolve.preprocess_and_solve_lp, glpapi06.js:41)."""
     if parm is None:
         parm = SMCP()
     if parm.msg_lev not in (0, 1, 2, 3, 4):
@@ -609,8 +612,8 @@ def glp_simplex(P: GkProblem, parm: Smcp | None = None) -> int:
             raise GkError(f"glp_simplex: {name} = {v}; invalid parameter")
     if parm.it_lim < 0 or parm.tm_lim < 0 or parm.out_frq < 1 or parm.out_dly < 0:
         raise GkError("glp_simplex: invalid it_lim/tm_lim/out_frq/out_dly")
-    if parm.presolve:
-        raise GkError("glp_simplex: presolve is outside the MI355X core (stays in the JS host)")
+    if parm.presolve not in (0, 1):
+        raise GkError(f"glp_simplex: presolve = {parm.presolve}; invalid parameter")
     P.pbs_stat = P.dbs_stat = GLP_UNDEF
     P.obj_val = 0.0
     P.some = 0
@@ -628,7 +631,14 @@ def glp_simplex(P: GkProblem, parm: Smcp | None = None) -> int:
     if P.nnz == 0:
         _trivial_lp(P, parm)
         return 0
-    # solve_lp (glpapi06.js:3)
+    if parm.presolve:
+        from . import presolve
+        return presolve.preprocess_and_solve_lp(P, parm)
+    return _solve_lp(P, parm)
+
+
+def _solve_lp(P: GkProblem, parm: Smcp) -> int:
+    """solve_lp (glpapi06.js:3): factorize if needed, then the method."""
     if not (P.m == 0 or P.valid):
         ret = P.factorize()
         if ret != 0:

@@ -40,7 +40,7 @@
 extern "C" {
 #endif
 
-#define GK_ABI_VERSION 4
+#define GK_ABI_VERSION 5
 #include <stddef.h>
 #define GK_EABI (-1)          /* contract violation; see gk_last_error() */
 
@@ -378,6 +378,51 @@ int gk_scale_prob_timed(gk_ctx *ctx, int m, int n, const int *ptr, const int *in
  * m == 0 or n == 0 it is glp_std_basis (glpapi05.js:49).  Host code (no
  * context, no device).  Returns the size of the triangular part, or GK_EABI. */
 int gk_adv_basis(gk_lp *lp);
+
+/* ---- LP / MIP presolver (glpnpp01.js .. glpnpp05.js) ----------------------
+ * The preprocessor glp_simplex (glpapi06.js:41 preprocess_and_solve_lp) and
+ * glp_intopt (glpapi09.js:111 preprocess_and_solve_mip) run with presolve =
+ * GLP_ON.  Host code (no context, no device): the reduced problem is solved
+ * by gk_spx_* / gk_ios_driver like any other.  Sequence (each step replaces
+ * the reference routine named):
+ *   gk_npp_create                          npp_create_wksp  glpnpp01.js:2
+ *   gk_npp_load(npp, P, kind, sol)         npp_load_prob    :262 (names and
+ *       scaling off; P's problem arrays in list order; kind [1..n] for
+ *       sol = GLP_MIP (3), NULL for GLP_SOL (1))
+ *   gk_npp_simplex / gk_npp_integer        npp_simplex      glpnpp05.js:430
+ *                                          npp_integer      :437
+ *       -> 0 | GLP_ENOPFS (10) | GLP_ENODFS (11) | GK_EABI; msg[7] (or
+ *       NULL) gets the counts npp_integer prints: variables binarized,
+ *       binaries made, rows added, binarization failures, hidden packing,
+ *       hidden covering, reduced coefficients
+ *   gk_npp_build_size, gk_npp_build        npp_build_prob   glpnpp01.js:396
+ *       (arrays 1-based as gk_lp's; A by columns in the order the
+ *       reference's glp_set_mat_col leaves them; row_ref / col_ref map each
+ *       reduced row / column to the original one; *c0 the constant term)
+ *   gk_npp_postprocess(npp, s1, s2, ...)   npp_postprocess  :474
+ *       (GLP_SOL: s1 / s2 = pbs / dbs status, the reduced problem's row
+ *       statuses and duals, column statuses and primal values; GLP_MIP: s1 =
+ *       mip_stat, col_prim = mipx, the rest NULL)
+ *   gk_npp_unload_sol / gk_npp_unload_mip  npp_unload_sol   :572
+ *   gk_npp_destroy
+ * The transformations, their order and their arithmetic are the reference's
+ * (gk_npp.cc), so the reduced problem equals the reference's bit for bit. */
+typedef struct gk_npp gk_npp;
+gk_npp *gk_npp_create(void);
+void    gk_npp_destroy(gk_npp *npp);
+int     gk_npp_load(gk_npp *npp, const gk_lp *P, const signed char *col_kind, int sol);
+int     gk_npp_simplex(gk_npp *npp);
+int     gk_npp_integer(gk_npp *npp, int binarize, int *msg);
+int     gk_npp_build_size(gk_npp *npp, int *m, int *n, int *nnz);
+int     gk_npp_build(gk_npp *npp, signed char *row_type, double *row_lb, double *row_ub,
+                     signed char *col_type, double *col_lb, double *col_ub, double *col_coef,
+                     signed char *col_kind, int *A_ptr, int *A_ind, double *A_val,
+                     int *row_ref, int *col_ref, double *c0);
+int     gk_npp_postprocess(gk_npp *npp, int stat1, int stat2, const signed char *row_stat,
+                           const double *row_dual, const signed char *col_stat, const double *col_prim);
+int     gk_npp_unload_sol(gk_npp *npp, gk_lp *P);
+int     gk_npp_unload_mip(gk_npp *npp, const gk_lp *P, const signed char *col_kind, double *row_mipx,
+                          double *col_mipx, int *mip_stat, double *mip_obj);
 
 #ifdef __cplusplus
 }

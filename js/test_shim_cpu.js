@@ -10,7 +10,7 @@ var names = ['create', 'deviceCount', 'abiVersion', 'lastError', 'bfdCreate', 'b
              'bfdFtran', 'bfdBtran', 'bfdUpdate', 'bfdGetCount', 'bfdValid', 'spx', 'ios', 'stats', 'advBasis',
              'evalTabRows'];
 names.forEach(function (k) { assert.strictEqual(typeof core.addon[k], 'function', k); });
-assert.strictEqual(core.addon.abiVersion(), 4);
+assert.strictEqual(core.addon.abiVersion(), 5);
 
 var ref = process.env.GLPK_REF || '/root/reference';
 var fs = require('fs');

@@ -64,6 +64,12 @@ function buildBundle() {
         'ios_solve_node = (function(f){ return function(t){ __cnt.solve_node++; return f(t); }; })(ios_solve_node);',
         'bfd_factorize = (function(f){ return function(a,b,c,d,e){ __cnt.factorize++; return f(a,b,c,d,e); }; })(bfd_factorize);',
         'exports["__glp_adv_basis"] = glp_adv_basis;',
+        // presolve: the reduced problem npp_build_prob made and the solution
+        // npp_postprocess receives (glpapi06.js:87, :51)
+        'var __npp_hook = null;',
+        'exports["__set_npp_hook"] = function(f){ __npp_hook = f; };',
+        'npp_build_prob = (function(f){ return function(npp, prob){ f(npp, prob); if (__npp_hook) __npp_hook("build", npp, prob); }; })(npp_build_prob);',
+        'npp_postprocess = (function(f){ return function(npp, prob){ if (__npp_hook) __npp_hook("post", npp, prob); f(npp, prob); }; })(npp_postprocess);',
         ''].join('\n'));
     parts.push(fs.readFileSync(path.join(REF, 'footer'), 'utf8'));
     var dst = LPF_FIX ? '/tmp/glpk_golden_bundle_lpffix.js' : '/tmp/glpk_golden_bundle.js';
@@ -307,6 +313,38 @@ function bfcpCase(name, mk, gen) {
     writeJson(pre + name, d);
 }
 
+// LP instance through glp_simplex with presolve = GLP_ON (glpapi06.js:41,
+// preprocess_and_solve_lp): per method the reduced problem (rows / columns in
+// list order, A by columns in list order, row_ref / col_ref), the solution of
+// the reduced problem handed to npp_postprocess, and the final solution.
+function presolveCase(name, mk, gen) {
+    if (ONLY && ('presolve_' + name).indexOf(ONLY) !== 0) return;
+    var d = dumpProb(mk(), gen);
+    d.name = name; d.kind = 'lp'; d.runs = [];
+    [1, 3].forEach(function (meth) {
+        var P = mk(), red = null, redsol = null;
+        glpk.__set_npp_hook(function (what, npp, prob) {
+            if (what === 'build') {
+                red = dumpProb(prob, null);
+                red.row_ref = Array.from(npp.row_ref).slice(1);
+                red.col_ref = Array.from(npp.col_ref).slice(1);
+            } else {
+                var i, j, s = {pbs_stat: prob.pbs_stat, dbs_stat: prob.dbs_stat, obj_val: prob.obj_val,
+                               row_stat: [], row_dual: [], col_stat: [], col_prim: []};
+                for (i = 1; i <= prob.m; i++) { s.row_stat.push(prob.row[i].stat); s.row_dual.push(prob.row[i].dual); }
+                for (j = 1; j <= prob.n; j++) { s.col_stat.push(prob.col[j].stat); s.col_prim.push(prob.col[j].prim); }
+                redsol = s;
+            }
+        });
+        var r = runLp(P, {meth: meth, presolve: glpk.GLP_ON}, 0);
+        glpk.__set_npp_hook(null);
+        r.reduced = red;
+        r.reduced_sol = redsol;
+        d.runs.push(r);
+    });
+    writeJson('presolve_' + name, d);
+}
+
 // MIP instance: root primal glp_simplex then glp_intopt (default IOCP), the
 // flow of SURVEY.md §8(d) C4/C5.
 function mipCase(name, mk, gen) {
@@ -419,6 +457,20 @@ for (var sd = 1; sd <= 32; sd++) {
         else
             lpCase('mix' + sd, function () { return genMix(sd, mm, nn, 0.35, false, true); }, null, [1, 2, 3]);
     })(sd, mm, nn);
+}
+presolveCase('test', function () { return readLp('test.lpt'); }, null);
+presolveCase('todd', function () { return readLp('todd.lpt'); }, null);
+presolveCase('gap', function () { return readLp('gap.lpt'); }, null);
+presolveCase('dense_64x256', function () { return genDense(64, 256, 42); }, {kind: 'dense', m: 64, n: 256, seed: 42});
+for (var ps = 1; ps <= 32; ps++) {
+    (function (sd, mm, nn) {
+        presolveCase((sd <= 12 ? 'wild' : 'mix') + sd, function () { return genMix(sd, mm, nn, 0.35, false, sd > 12); }, null);
+    })(ps, 4 + (ps * 7) % 29, 5 + (ps * 13) % 41);
+}
+for (var pz = 1; pz <= 12; pz++) {
+    (function (sd) {
+        presolveCase('sparse' + sd, function () { return genMix(200 + sd, 20 + 3 * sd, 25 + 4 * sd, 0.08, false, true, sd % 3 !== 0); }, null);
+    })(pz);
 }
 bfcpCase('gap', function () { return readLp('gap.lpt'); }, null);
 bfcpCase('todd', function () { return readLp('todd.lpt'); }, null);

@@ -122,4 +122,5 @@ def test_gpu_update_limit_follows_bfcp(gpu_ctx):
         ret = gk.glp_simplex(P, gk.SMCP(meth=gk.GLP_DUAL, it_lim=300))
         st = P.stats()
         assert ret in (0, problems.GLP_EITLIM)
-        assert st.reinversions >= P.it_cnt // lim, (kw, st.reinversions, P.it_cnt)
+        # the factor glp_factorize made counts as the first one (not a re-inversion)
+        assert st.reinversions >= (P.it_cnt - 1) // lim, (kw, st.reinversions, P.it_cnt)
