@@ -4,7 +4,7 @@
 # profile (tools/profile_round.sh) and the graph-replay pivot trace.
 set -e
 mkdir -p gpurun_out/r03
-timeout -k 10 600 python -u -m pytest tests/test_bfcp.py tests/test_gpu_lp.py -m gpu -x -q --timeout 300 \
+timeout -k 10 600 python -u -m pytest tests/test_bfcp.py tests/test_presolve.py tests/test_gpu_lp.py -m gpu -x -q --timeout 300 \
     --timeout-method thread > gpurun_out/r03/tests_lp.log 2>&1
 timeout -k 10 300 python3 bench.py --no-cpu --no-extra > gpurun_out/r03/bench_quick.json 2> gpurun_out/r03/bench_quick.err
 bash tools/profile_round.sh r03
