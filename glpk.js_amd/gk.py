@@ -676,6 +676,8 @@ def IOCP(**options) -> Iocp:
     p = Iocp()
     for k, v in d.items():
         setattr(p, k, options.get(k) or v)
+    # binarize (GLP_ON / GLP_OFF) steers only the host's presolve path
+    p.binarize = options.get("binarize") or 0
     return p
 
 
@@ -706,8 +708,11 @@ def glp_intopt(P: GkProblem, parm: Iocp | None = None, comm=None, ramp_nodes: in
         raise GkError(f"glp_intopt: pp_tech = {parm.pp_tech}; invalid parameter")
     if parm.mip_gap < 0.0:
         raise GkError(f"glp_intopt: mip_gap = {parm.mip_gap}; invalid parameter")
-    if parm.presolve:
-        raise GkError("glp_intopt: the MIP presolver stays in the JS host (presolve must be OFF here)")
+    if parm.presolve not in (0, 1):
+        raise GkError(f"glp_intopt: presolve = {parm.presolve}; invalid parameter")
+    binarize = int(getattr(parm, "binarize", 0) or 0)
+    if binarize not in (0, 1):
+        raise GkError(f"glp_intopt: binarize = {binarize}; invalid parameter")
     P.mip_stat = GLP_UNDEF
     P.mip_obj = 0.0
     if np.any((P.row_type[1:] == GLP_DB) & (P.row_lb[1:] >= P.row_ub[1:])) or \
@@ -730,6 +735,14 @@ def glp_intopt(P: GkProblem, parm: Iocp | None = None, comm=None, ramp_nodes: in
         _xprintf(f"{P.m} row{'' if P.m == 1 else 's'}, {P.n} column{'' if P.n == 1 else 's'}, "
                  f"{P.nnz} non-zero{'' if P.nnz == 1 else 's'}")
         _xprintf(f"{ni} integer variable{'' if ni == 1 else 's'}, {s} which {'is' if nb == 1 else 'are'} binary")
+    if parm.presolve:
+        from . import presolve
+        return presolve.preprocess_and_solve_mip(P, parm, bool(binarize))
+    return _solve_mip(P, parm, comm, ramp_nodes)
+
+
+def _solve_mip(P: GkProblem, parm: Iocp, comm, ramp_nodes: int) -> int:
+    """solve_mip (glpapi09.js:62-111): the search, then its closing messages."""
     ret = _intopt(P, parm, comm, ramp_nodes)
     # solve_mip's closing messages (glpapi09.js:80-111)
     if ret == 0 and parm.msg_lev >= GLP_MSG_ALL:

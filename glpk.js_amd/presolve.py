@@ -15,7 +15,7 @@ import ctypes as C
 import numpy as np
 
 from . import gk
-from .problems import (GLP_BS, GLP_DB, GLP_FEAS, GLP_FR, GLP_FX, GLP_LO, GLP_NOFEAS, GLP_UP, Problem,
+from .problems import (GLP_BS, GLP_DB, GLP_FEAS, GLP_NOFEAS, GLP_UNBND, Problem,
                        _col_stat_for)
 
 GLP_SOL, GLP_MIP = 1, 3
@@ -227,3 +227,99 @@ def preprocess_and_solve_lp(P: gk.GkProblem, parm) -> int:
     npp.postprocess_sol(lp.pbs_stat, lp.dbs_stat, lp.row_stat, lp.row_dual, lp.col_stat, lp.col_prim)
     npp.unload_sol(P)
     return 0
+
+
+def _lp_status(lp: gk.GkProblem) -> int:
+    """glp_get_status (glpapi02.js) of a basic solution."""
+    st = lp.pbs_stat
+    if st == GLP_FEAS:
+        if lp.dbs_stat == GLP_NOFEAS:
+            st = GLP_UNBND
+        elif lp.dbs_stat == GLP_FEAS:
+            st = gk.GLP_OPT
+    return st
+
+
+def preprocess_and_solve_mip(P: gk.GkProblem, parm, binarize: bool = False) -> int:
+    """glpapi09.js:116-250."""
+    out = gk._xprintf
+    all_ = parm.msg_lev >= GLP_MSG_ALL
+    if all_:
+        out("Preprocessing...")
+    npp = Npp(P.L)
+    npp.load(P._lp_struct(), P.col_kind, GLP_MIP)
+    ret, msg = npp.integer(binarize)
+    if all_ and ret == 0:
+        # npp_integer's own lines (glpnpp04.js:92-97, glpnpp05.js:475-514)
+        if msg[0] > 0:
+            out(f"{msg[0]} integer variable(s) were replaced by {msg[1]} binary ones")
+        if msg[2] > 0:
+            out(f"{msg[2]} row(s) were added due to binarization")
+        if msg[3] > 0:
+            out(f"Binarization failed for {msg[3]} integer variable(s)")
+        if msg[4] > 0:
+            out(f"{msg[4]} hidden packing inequaliti(es) were detected")
+        if msg[5] > 0:
+            out(f"{msg[5]} hidden covering inequaliti(es) were detected")
+        if msg[6] > 0:
+            out(f"{msg[6]} constraint coefficient(s) were reduced")
+    if ret == gk.GLP_ENOPFS:
+        if all_:
+            out("PROBLEM HAS NO PRIMAL FEASIBLE SOLUTION")
+    elif ret == gk.GLP_ENODFS:
+        if all_:
+            out("LP RELAXATION HAS NO DUAL FEASIBLE SOLUTION")
+    if ret != 0:
+        return ret
+    red = npp.build(P.dir)
+    if red.m == 0 and red.n == 0:
+        if all_:
+            out(f"Objective value = {gk._js_num(red.c0)}")
+            out("INTEGER OPTIMAL SOLUTION FOUND BY MIP PREPROCESSOR")
+        npp.postprocess_mip(gk.GLP_OPT, np.zeros(1))
+        npp.unload_mip(P)
+        return 0
+    if all_:
+        iv = red.col_kind == gk.GLP_IV
+        ni = int(np.count_nonzero(iv))
+        nb = int(np.count_nonzero(iv & (red.col_type == GLP_DB) & (red.col_lb == 0.0) & (red.col_ub == 1.0)))
+        s = ("none of" if nb == 0 else "" if (ni == 1 and nb == 1) else "one of" if nb == 1 else
+             "all of" if nb == ni else f"{nb} of")
+        out(f"{red.m} row{'' if red.m == 1 else 's'}, {red.n} column{'' if red.n == 1 else 's'}, "
+            f"{red.nnz} non-zero{'' if red.nnz == 1 else 's'}")
+        out(f"{ni} integer variable{'' if ni == 1 else 's'}, {s} which {'is' if nb == 1 else 'are'} binary")
+    mip = _reduced(P, red)
+    with _term_out(all_):
+        gk.glp_scale_prob(mip, gk.GLP_SF_GM | gk.GLP_SF_EQ | gk.GLP_SF_2N | gk.GLP_SF_SKIP)
+    with _term_out(all_):
+        gk.glp_adv_basis(mip, 0)
+    if all_:
+        out("Solving LP relaxation...")
+    mip.it_cnt = P.it_cnt
+    ret = gk.glp_simplex(mip, gk.SMCP(msg_lev=parm.msg_lev))
+    P.it_cnt = mip.it_cnt
+    if ret != 0:
+        if parm.msg_lev >= GLP_MSG_ERR:
+            out("glp_intopt: cannot solve LP relaxation")
+        return gk.GLP_EFAIL
+    st = _lp_status(mip)
+    if st == gk.GLP_OPT:
+        ret = 0
+    elif st == GLP_NOFEAS:
+        ret = gk.GLP_ENOPFS
+    elif st == GLP_UNBND:
+        ret = gk.GLP_ENODFS
+    else:
+        raise gk.GkError(f"glp_intopt: LP relaxation status {st}")
+    if ret != 0:
+        return ret
+    mip.it_cnt = P.it_cnt
+    ret = gk._solve_mip(mip, parm, None, 0)
+    P.it_cnt = mip.it_cnt
+    P.mip_stats = mip.mip_stats
+    if not (mip.mip_stat == gk.GLP_OPT or mip.mip_stat == GLP_FEAS):
+        P.mip_stat = mip.mip_stat
+        return ret
+    npp.postprocess_mip(mip.mip_stat, mip.col_mipx)
+    npp.unload_mip(P)
+    return ret

@@ -373,6 +373,43 @@ function mipCase(name, mk, gen) {
     console.log('wrote mip', name, 'ret', ret, 'obj', P.mip_obj, 'lp', d.mip.lp_solves, 'piv', d.mip.pivots, 'sec', dt.toFixed(2));
 }
 
+// MIP instance through glp_intopt with presolve = GLP_ON (glpapi09.js:116,
+// preprocess_and_solve_mip), no root LP beforehand: per option set
+// ({presolve}, {presolve, binarize}) the reduced problem npp_build_prob made,
+// the MIP solution npp_postprocess received, the printed lines and the final
+// solution.
+function mipPresolveCase(name, mk, gen) {
+    if (ONLY && ('mippre_' + name).indexOf(ONLY) !== 0) return;
+    var d = dumpProb(mk(), gen);
+    d.name = name; d.kind = 'mip'; d.runs = [];
+    [{presolve: glpk.GLP_ON}, {presolve: glpk.GLP_ON, binarize: glpk.GLP_ON}].forEach(function (opts) {
+        var P = mk(), red = null, redsol = null, lines = [];
+        glpk.__set_npp_hook(function (what, npp, prob) {
+            if (what === 'build') {
+                red = dumpProb(prob, null);
+                red.row_ref = Array.from(npp.row_ref).slice(1);
+                red.col_ref = Array.from(npp.col_ref).slice(1);
+            } else {
+                var j, x = [];
+                for (j = 1; j <= prob.n; j++) x.push(prob.col[j].mipx);
+                redsol = {mip_stat: prob.mip_stat, mip_obj: prob.mip_obj, col_mipx: x};
+            }
+        });
+        glpk.glp_set_print_func(function (s) { lines.push(s); });
+        var s0 = glpk.__cnt.solve_node;
+        var ret = glpk.glp_intopt(P, new glpk.IOCP(opts));
+        glpk.glp_set_print_func(function () {});
+        glpk.__set_npp_hook(null);
+        var j, x = [], rx = [];
+        for (j = 1; j <= P.n; j++) x.push(P.col[j].mipx);
+        for (j = 1; j <= P.m; j++) rx.push(P.row[j].mipx);
+        d.runs.push({opts: opts, ret: ret, mip_stat: P.mip_stat, mip_obj: P.mip_obj, col_mipx: x, row_mipx: rx,
+                     lp_solves: glpk.__cnt.solve_node - s0, lines: lines, reduced: red, reduced_sol: redsol});
+    });
+    fs.writeFileSync(path.join(OUT, 'mippre_' + name + '.json'), JSON.stringify(d));
+    console.log('wrote mippre', name, d.runs.map(function (r) { return 'ret' + r.ret + ':stat' + r.mip_stat + ':obj' + r.mip_obj + ':lp' + r.lp_solves; }).join(' '));
+}
+
 // MIP instance under several IOCP option sets (branching rule br_tech,
 // node selection bt_tech, preprocessing pp_tech; glpios09.js:1,
 // glpios12.js:2, glpios03.js:643-656): one root solve per run, the
@@ -484,6 +521,19 @@ for (var ms = 1; ms <= 12; ms++) {
     (function (ms) {
         mipCase('mixint' + ms, function () { return genMix(100 + ms, 6 + ms, 8 + 2 * ms, 0.5, true, true); }, null);
     })(ms);
+}
+mipPresolveCase('gap', function () { return readLp('gap.lpt'); }, null);
+mipPresolveCase('todd', function () { return readLp('todd.lpt'); }, null);
+mipPresolveCase('c5s_12x20', function () { return genC5s(12, 20, 42); }, {kind: 'c5s', m: 12, n: 20, seed: 42});
+for (var mp = 1; mp <= 12; mp++) {
+    (function (ms) {
+        mipPresolveCase('mixint' + ms, function () { return genMix(100 + ms, 6 + ms, 8 + 2 * ms, 0.5, true, true); }, null);
+    })(mp);
+}
+for (var mq = 1; mq <= 8; mq++) {
+    (function (ms) {
+        mipPresolveCase('sparseint' + ms, function () { return genMix(400 + ms, 20 + 2 * ms, 24 + 3 * ms, 0.1, 0.6, true, ms % 2 === 0); }, null);
+    })(mq);
 }
 mipOptsCase('gap', function () { return readLp('gap.lpt'); }, MIP_OPTS);
 mipOptsCase('c5s_12x20', function () { return genC5s(12, 20, 42); }, MIP_OPTS);

@@ -1,5 +1,8 @@
-"""The native LP presolver (gk_npp_*, glpk.js_amd/csrc/gk_npp.cc) against the
-reference's glp_simplex with presolve = GLP_ON (glpapi06.js:41).
+"""The native LP / MIP presolver (gk_npp_*, glpk.js_amd/csrc/gk_npp.cc)
+against the reference's glp_simplex and glp_intopt with presolve = GLP_ON
+(glpapi06.js:41, glpapi09.js:116; mippre_* fixtures for the latter, with and
+without binarize: npp_integer's binarization, hidden packing / covering and
+coefficient reduction, glpnpp04.js).
 
 Fixtures (tests/golden/gen_golden.js, presolveCase) record, per method, the
 reduced problem the reference's npp_build_prob made (glpnpp01.js:396), the
@@ -120,3 +123,105 @@ def test_gpu_simplex_presolve_matches_reference(gpu_ctx, path, run_index):
     assert abs(P.obj_val - ref) <= 1e-9 * max(1.0, abs(ref)), (P.obj_val, ref)
     from test_gpu_lp import check_solution
     check_solution(P)
+
+
+# ---- glp_intopt with presolve = GLP_ON (glpapi09.js:116) -------------------
+MIP_CASES = []
+for path in golden_files("mippre_"):
+    d = load_golden(path)
+    for r, run in enumerate(d["runs"]):
+        MIP_CASES.append(pytest.param(path, r, id=f"{os.path.basename(path)[7:-5]}-{'bin' if run['opts'].get('binarize') else 'nobin'}"))
+
+
+def _presolve_mip(d, run):
+    from glpk_js_amd import presolve
+    orig = problems.from_fixture(d)
+    lp, arrays = presolve.problem_lp(orig)
+    npp = presolve.Npp()
+    npp.load(lp, arrays["col_kind"], presolve.GLP_MIP)
+    ret, msg = npp.integer(bool(run["opts"].get("binarize")))
+    return orig, lp, arrays, npp, ret, msg
+
+
+@pytest.mark.parametrize("path,run_index", MIP_CASES)
+def test_mip_presolve_reduced_problem_matches_reference(path, run_index):
+    d = load_golden(path)
+    run = d["runs"][run_index]
+    _, _, _, npp, ret, msg = _presolve_mip(d, run)
+    red = run["reduced"]
+    if red is None:
+        assert ret == run["ret"]
+        return
+    assert ret == 0
+    got = npp.build(d["dir"])
+    assert (got.m, got.n, got.nnz) == (red["m"], red["n"], red["nnz"])
+    assert list(npp.row_ref) == red["row_ref"] and list(npp.col_ref) == red["col_ref"]
+    assert got.c0 == red["c0"]
+    for key in ("row_type", "row_lb", "row_ub", "col_type", "col_lb", "col_ub", "col_coef", "col_kind"):
+        np.testing.assert_array_equal(getattr(got, key), np.asarray(red[key]), err_msg=key)
+    for key in ("A_ptr", "A_ind", "A_val"):
+        np.testing.assert_array_equal(getattr(got, key), np.asarray(red[key]), err_msg=key)
+    # the counts npp_integer prints (the reference's lines before the
+    # reduced problem's size line)
+    want = [s for s in run["lines"] if "were replaced by" in s or "row(s) were added" in s or
+            "hidden packing" in s or "hidden covering" in s or "were reduced" in s or "Binarization failed" in s]
+    made = []
+    if msg[0] > 0:
+        made.append(f"{msg[0]} integer variable(s) were replaced by {msg[1]} binary ones")
+    if msg[2] > 0:
+        made.append(f"{msg[2]} row(s) were added due to binarization")
+    if msg[3] > 0:
+        made.append(f"Binarization failed for {msg[3]} integer variable(s)")
+    if msg[4] > 0:
+        made.append(f"{msg[4]} hidden packing inequaliti(es) were detected")
+    if msg[5] > 0:
+        made.append(f"{msg[5]} hidden covering inequaliti(es) were detected")
+    if msg[6] > 0:
+        made.append(f"{msg[6]} constraint coefficient(s) were reduced")
+    assert made == want
+
+
+MIP_POST = [c for c in MIP_CASES if load_golden(c.values[0])["runs"][c.values[1]]["reduced_sol"] is not None]
+
+
+@pytest.mark.parametrize("path,run_index", MIP_POST)
+def test_mip_postprocess_recovers_reference_solution(path, run_index):
+    from glpk_js_amd import presolve
+    d = load_golden(path)
+    run = d["runs"][run_index]
+    orig, lp, a, npp, ret, _ = _presolve_mip(d, run)
+    npp.build(d["dir"])
+    s = run["reduced_sol"]
+    npp.postprocess_mip(s["mip_stat"], np.concatenate([[0.0], np.asarray(s["col_mipx"], np.float64)]))
+    st, obj = presolve.C.c_int(), presolve.C.c_double()
+    f = presolve._ptr
+    assert npp.L.gk_npp_unload_mip(npp.h, presolve.C.byref(lp), f(a["col_kind"]), f(a["row_mipx"]),
+                                   f(a["col_mipx"]), presolve.C.byref(st), presolve.C.byref(obj)) == 0
+    assert st.value == run["mip_stat"]
+    np.testing.assert_array_equal(a["col_mipx"][1:], np.asarray(run["col_mipx"]))
+    assert abs(obj.value - run["mip_obj"]) <= 1e-12 * max(1.0, abs(run["mip_obj"]))
+    want = np.asarray(run["row_mipx"], np.float64)
+    assert np.max(np.abs(a["row_mipx"][1:] - want), initial=0.0) <= 1e-12 * (1.0 + np.abs(want).max(initial=0.0))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("path,run_index", MIP_CASES)
+def test_gpu_intopt_presolve_matches_reference(gpu_ctx, path, run_index):
+    from glpk_js_amd import gk
+    d = load_golden(path)
+    run = d["runs"][run_index]
+    P = gk.GkProblem(gpu_ctx, problems.from_fixture(d))
+    lines = []
+    gk.glp_set_print_func(lines.append)
+    try:
+        ret = gk.glp_intopt(P, gk.IOCP(**run["opts"]))
+    finally:
+        gk.glp_set_print_func(None)
+    assert ret == run["ret"]
+    assert P.mip_stat == run["mip_stat"]
+    if P.mip_stat == gk.GLP_OPT:
+        ref = run["mip_obj"]
+        assert abs(P.mip_obj - ref) <= 1e-9 * max(1.0, abs(ref)), (P.mip_obj, ref)
+    # the preprocessor's lines up to the LP relaxation (bit-exact text)
+    cut = lambda ls: ls[:ls.index("Solving LP relaxation...")] if "Solving LP relaxation..." in ls else ls  # noqa: E731
+    assert cut(lines) == cut(run["lines"])
