@@ -15,6 +15,8 @@
  *   bfdGetCount(bfd), bfdValid(bfd)             (glpbfd.js:225)
  *   spx(ctx, bfd, lp, smcp, dual)  -> int       gk_spx_primal/dual (glpspx01.js:1 / glpspx02.js:1)
  *   stats(bfd)                     -> object    gk_bfd_last_stats
+ *   nppCreate/nppLoad/nppSimplex/nppInteger/nppBuildSize/nppBuild/
+ *   nppPostprocess/nppUnloadSol/nppUnloadMip   gk_npp_* (glpnpp01.js .. 05.js)
  */
 #define NAPI_VERSION 6
 #include <node_api.h>
@@ -634,6 +636,148 @@ static napi_value js_eval_tab_rows(napi_env env, napi_callback_info info)
     return mk_int(env, 0);
 }
 
+/* ------------------------------------------------------------- presolver */
+/* npp*: the LP / MIP preprocessor (gk_npp_*, glpnpp01.js .. glpnpp05.js);
+ * host code, no context.  The JS side (js/gk_core.js nppSolve, js/gk_shim.js)
+ * rebinds the reference's npp_* entry points to these. */
+static void npp_fin(napi_env env, void *data, void *hint)
+{
+    (void)env; (void)hint;
+    gk_npp_destroy((gk_npp *)data);
+}
+
+static napi_value js_npp_create(napi_env env, napi_callback_info info)
+{
+    (void)info;
+    gk_npp *w = gk_npp_create();
+    if (!w) return throw_gk(env, "npp_create_wksp");
+    napi_value r;
+    CHECK(napi_create_external(env, w, npp_fin, NULL, &r));
+    return r;
+}
+
+static int npp_ret(napi_env env, int ret, const char *what, napi_value *out)
+{
+    if (ret == GK_EABI) {
+        throw_gk(env, what);
+        return 0;
+    }
+    *out = mk_int(env, ret);
+    return 1;
+}
+
+/* nppLoad(npp, L, kind Int8Array | null, sol) */
+static napi_value js_npp_load(napi_env env, napi_callback_info info)
+{
+    napi_value argv[4], r;
+    if (!get_args(env, info, 4, argv)) return NULL;
+    gk_lp lp;
+    if (!fill_lp(env, argv[1], &lp)) return NULL;
+    int sol = 0;
+    CHECK(napi_get_value_int32(env, argv[3], &sol));
+    const signed char *kind = (const signed char *)ta(env, argv[2]);
+    return npp_ret(env, gk_npp_load((gk_npp *)get_ext(env, argv[0]), &lp, kind, sol), "npp_load_prob", &r) ? r : NULL;
+}
+
+static napi_value js_npp_simplex(napi_env env, napi_callback_info info)
+{
+    napi_value argv[1], r;
+    if (!get_args(env, info, 1, argv)) return NULL;
+    return npp_ret(env, gk_npp_simplex((gk_npp *)get_ext(env, argv[0])), "npp_simplex", &r) ? r : NULL;
+}
+
+/* nppInteger(npp, binarize, msg Int32Array(7)) */
+static napi_value js_npp_integer(napi_env env, napi_callback_info info)
+{
+    napi_value argv[3], r;
+    if (!get_args(env, info, 3, argv)) return NULL;
+    int bin = 0;
+    CHECK(napi_get_value_int32(env, argv[1], &bin));
+    int *msg = (int *)ta(env, argv[2]);
+    return npp_ret(env, gk_npp_integer((gk_npp *)get_ext(env, argv[0]), bin, msg), "npp_integer", &r) ? r : NULL;
+}
+
+/* nppBuildSize(npp, out Int32Array(3)) -> m, n, nnz in out */
+static napi_value js_npp_build_size(napi_env env, napi_callback_info info)
+{
+    napi_value argv[2], r;
+    if (!get_args(env, info, 2, argv)) return NULL;
+    int *o = (int *)ta(env, argv[1]);
+    if (!o) {
+        napi_throw_type_error(env, NULL, "nppBuildSize: Int32Array(3) expected");
+        return NULL;
+    }
+    return npp_ret(env, gk_npp_build_size((gk_npp *)get_ext(env, argv[0]), &o[0], &o[1], &o[2]), "npp_build_prob",
+                   &r) ? r : NULL;
+}
+
+/* nppBuild(npp, row_type, row_lb, row_ub, col_type, col_lb, col_ub, col_coef,
+ *          col_kind, A_ptr, A_ind, A_val, row_ref, col_ref, c0 Float64Array(1)) */
+static napi_value js_npp_build(napi_env env, napi_callback_info info)
+{
+    napi_value argv[15], r;
+    if (!get_args(env, info, 15, argv)) return NULL;
+    void *a[15];
+    for (int k = 1; k < 15; k++) {
+        a[k] = ta(env, argv[k]);
+        if (!a[k]) {
+            napi_throw_type_error(env, NULL, "nppBuild: typed arrays expected");
+            return NULL;
+        }
+    }
+    int ret = gk_npp_build((gk_npp *)get_ext(env, argv[0]), (signed char *)a[1], (double *)a[2], (double *)a[3],
+                           (signed char *)a[4], (double *)a[5], (double *)a[6], (double *)a[7], (signed char *)a[8],
+                           (int *)a[9], (int *)a[10], (double *)a[11], (int *)a[12], (int *)a[13], (double *)a[14]);
+    return npp_ret(env, ret, "npp_build_prob", &r) ? r : NULL;
+}
+
+/* nppPostprocess(npp, stat1, stat2, row_stat, row_dual, col_stat, col_prim)
+ * (the first three arrays null for a MIP solution; col_prim = mipx) */
+static napi_value js_npp_postprocess(napi_env env, napi_callback_info info)
+{
+    napi_value argv[7], r;
+    if (!get_args(env, info, 7, argv)) return NULL;
+    int s1 = 0, s2 = 0;
+    CHECK(napi_get_value_int32(env, argv[1], &s1));
+    CHECK(napi_get_value_int32(env, argv[2], &s2));
+    int ret = gk_npp_postprocess((gk_npp *)get_ext(env, argv[0]), s1, s2, (const signed char *)ta(env, argv[3]),
+                                 (const double *)ta(env, argv[4]), (const signed char *)ta(env, argv[5]),
+                                 (const double *)ta(env, argv[6]));
+    return npp_ret(env, ret, "npp_postprocess", &r) ? r : NULL;
+}
+
+/* nppUnloadSol(npp, L): statuses and values into L's arrays; L.pbs_stat,
+ * L.dbs_stat, L.obj_val */
+static napi_value js_npp_unload_sol(napi_env env, napi_callback_info info)
+{
+    napi_value argv[2], r;
+    if (!get_args(env, info, 2, argv)) return NULL;
+    gk_lp lp;
+    if (!fill_lp(env, argv[1], &lp)) return NULL;
+    if (!npp_ret(env, gk_npp_unload_sol((gk_npp *)get_ext(env, argv[0]), &lp), "npp_unload_sol", &r)) return NULL;
+    set_num(env, argv[1], "pbs_stat", lp.pbs_stat);
+    set_num(env, argv[1], "dbs_stat", lp.dbs_stat);
+    set_num(env, argv[1], "obj_val", lp.obj_val);
+    return r;
+}
+
+/* nppUnloadMip(npp, L, kind, row_mipx, col_mipx): L.mip_stat, L.mip_obj */
+static napi_value js_npp_unload_mip(napi_env env, napi_callback_info info)
+{
+    napi_value argv[5], r;
+    if (!get_args(env, info, 5, argv)) return NULL;
+    gk_lp lp;
+    if (!fill_lp(env, argv[1], &lp)) return NULL;
+    int st = 0;
+    double obj = 0.0;
+    int ret = gk_npp_unload_mip((gk_npp *)get_ext(env, argv[0]), &lp, (const signed char *)ta(env, argv[2]),
+                                (double *)ta(env, argv[3]), (double *)ta(env, argv[4]), &st, &obj);
+    if (!npp_ret(env, ret, "npp_unload_sol", &r)) return NULL;
+    set_num(env, argv[1], "mip_stat", st);
+    set_num(env, argv[1], "mip_obj", obj);
+    return r;
+}
+
 #define FN(name, f) { name, NULL, f, NULL, NULL, NULL, napi_enumerable, NULL }
 
 #include <execinfo.h>
@@ -659,6 +803,10 @@ static napi_value init(napi_env env, napi_value exports)
         FN("bfdUpdate", js_bfd_update), FN("bfdGetCount", js_bfd_get_count), FN("bfdValid", js_bfd_valid),
         FN("spx", js_spx), FN("ios", js_ios), FN("stats", js_stats), FN("scale", js_scale),
         FN("advBasis", js_adv_basis), FN("evalTabRows", js_eval_tab_rows),
+        FN("nppCreate", js_npp_create), FN("nppLoad", js_npp_load), FN("nppSimplex", js_npp_simplex),
+        FN("nppInteger", js_npp_integer), FN("nppBuildSize", js_npp_build_size), FN("nppBuild", js_npp_build),
+        FN("nppPostprocess", js_npp_postprocess), FN("nppUnloadSol", js_npp_unload_sol),
+        FN("nppUnloadMip", js_npp_unload_mip),
     };
     napi_define_properties(env, exports, sizeof d / sizeof d[0], d);
     return exports;

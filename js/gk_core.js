@@ -334,3 +334,99 @@ function evalTabRows(lp, ks, perRow) {
     return rows;
 }
 module.exports.evalTabRows = evalTabRows;
+
+// ---- LP / MIP preprocessor (glpnpp01.js .. glpnpp05.js) ----------------------
+// the native workspace (gk_npp_*) behind the reference's npp_* calls made by
+// glp_simplex / glp_intopt (glpapi06.js:41, glpapi09.js:116)
+var GLP_SOL = 1, GLP_MIP = 3;
+function nppLoad(orig, sol) {
+    var g = arrays(orig);
+    var L = marshal(orig, g);
+    var kind = null, j;
+    if (sol === GLP_MIP) {
+        kind = new Int8Array(orig.n + 1);
+        for (j = 1; j <= orig.n; j++) kind[j] = orig.col[j].kind;
+    }
+    var h = addon.nppCreate();
+    addon.nppLoad(h, L, kind, sol);
+    return {h: h, sol: sol, dir: orig.dir};
+}
+function nppSimplex(w) { return addon.nppSimplex(w.h); }
+// npp_integer's lines (glpnpp04.js:92-97, glpnpp05.js:475-514) through the
+// reference's xprintf (term_out as the caller set it)
+function nppInteger(w, parm, print) {
+    var msg = new Int32Array(7);
+    var ret = addon.nppInteger(w.h, parm && parm.binarize ? 1 : 0, msg);
+    if (ret === 0) {
+        if (msg[0] > 0) print(msg[0] + " integer variable(s) were replaced by " + msg[1] + " binary ones");
+        if (msg[2] > 0) print(msg[2] + " row(s) were added due to binarization");
+        if (msg[3] > 0) print("Binarization failed for " + msg[3] + " integer variable(s)");
+        if (msg[4] > 0) print(msg[4] + " hidden packing inequaliti(es) were detected");
+        if (msg[5] > 0) print(msg[5] + " hidden covering inequaliti(es) were detected");
+        if (msg[6] > 0) print(msg[6] + " constraint coefficient(s) were reduced");
+    }
+    return ret;
+}
+// the reduced problem as arrays (1-based; A by columns in the order the
+// reference's glp_set_mat_col leaves them)
+function nppBuild(w) {
+    var sz = new Int32Array(3);
+    addon.nppBuildSize(w.h, sz);
+    var m = sz[0], n = sz[1], nnz = sz[2];
+    var r = {m: m, n: n, nnz: nnz, dir: w.dir,
+             row_type: new Int8Array(m + 1), row_lb: new Float64Array(m + 1), row_ub: new Float64Array(m + 1),
+             col_type: new Int8Array(n + 1), col_lb: new Float64Array(n + 1), col_ub: new Float64Array(n + 1),
+             col_coef: new Float64Array(n + 1), col_kind: new Int8Array(n + 1), A_ptr: new Int32Array(n + 2),
+             A_ind: new Int32Array(nnz + 1), A_val: new Float64Array(nnz + 1), row_ref: new Int32Array(m + 1),
+             col_ref: new Int32Array(n + 1), c0: new Float64Array(1)};
+    addon.nppBuild(w.h, r.row_type, r.row_lb, r.row_ub, r.col_type, r.col_lb, r.col_ub, r.col_coef, r.col_kind,
+                   r.A_ptr, r.A_ind, r.A_val, r.row_ref, r.col_ref, r.c0);
+    w.m = m; w.n = n;
+    return r;
+}
+function nppPostprocess(w, prob) {
+    var i, j, m = prob.m, n = prob.n;
+    if (w.sol === GLP_MIP) {
+        var mx = new Float64Array(n + 1);
+        for (j = 1; j <= n; j++) mx[j] = prob.col[j].mipx;
+        addon.nppPostprocess(w.h, prob.mip_stat, 0, null, null, null, mx);
+        return;
+    }
+    var rs = new Int8Array(m + 1), rd = new Float64Array(m + 1), cs = new Int8Array(n + 1), cp = new Float64Array(n + 1);
+    for (i = 1; i <= m; i++) { rs[i] = prob.row[i].stat; rd[i] = prob.row[i].dual; }
+    for (j = 1; j <= n; j++) { cs[j] = prob.col[j].stat; cp[j] = prob.col[j].prim; }
+    addon.nppPostprocess(w.h, prob.pbs_stat, prob.dbs_stat, rs, rd, cs, cp);
+}
+function nppUnload(w, orig) {
+    var g = arrays(orig), L = marshal(orig, g), i, j, row, col;
+    if (w.sol === GLP_MIP) {
+        var kind = new Int8Array(orig.n + 1), rx = new Float64Array(orig.m + 1), cx = new Float64Array(orig.n + 1);
+        for (j = 1; j <= orig.n; j++) kind[j] = orig.col[j].kind;
+        addon.nppUnloadMip(w.h, L, kind, rx, cx);
+        orig.mip_stat = L.mip_stat;
+        orig.mip_obj = L.mip_obj;
+        for (j = 1; j <= orig.n; j++) orig.col[j].mipx = cx[j];
+        for (i = 1; i <= orig.m; i++) orig.row[i].mipx = rx[i];
+        return;
+    }
+    addon.nppUnloadSol(w.h, L);
+    orig.valid = 0;
+    orig.pbs_stat = L.pbs_stat;
+    orig.dbs_stat = L.dbs_stat;
+    orig.obj_val = L.obj_val;
+    orig.some = 0;
+    for (i = 1; i <= orig.m; i++) {
+        row = orig.row[i];
+        row.stat = g.row_stat[i]; row.prim = g.row_prim[i]; row.dual = g.row_dual[i];
+    }
+    for (j = 1; j <= orig.n; j++) {
+        col = orig.col[j];
+        col.stat = g.col_stat[j]; col.prim = g.col_prim[j]; col.dual = g.col_dual[j];
+    }
+}
+module.exports.nppLoad = nppLoad;
+module.exports.nppSimplex = nppSimplex;
+module.exports.nppInteger = nppInteger;
+module.exports.nppBuild = nppBuild;
+module.exports.nppPostprocess = nppPostprocess;
+module.exports.nppUnload = nppUnload;

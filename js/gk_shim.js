@@ -3,6 +3,7 @@
 // names rebinds every internal caller:
 //   solve_lp (glpapi06.js:27-37)          -> spx_primal / spx_dual
 //   glp_factorize / glp_ftran / glp_btran -> bfd_* (glpapi12.js:75-105, 211, 240)
+//   npp_* (glpnpp01.js .. glpnpp05.js)    -> gk_npp_* (presolve = GLP_ON)
 // Matrix and scale mutators bump lp.__gk_version so the device copy of A is
 // re-uploaded only when A or the scaling changed (SURVEY.md §8(b).1).
 var __gk = require(__gk_core_path);
@@ -63,6 +64,65 @@ glp_adv_basis = exports["glp_adv_basis"] = function (lp, flags) {
     for (i = 1; i <= lp.m; i++) glp_set_row_stat(lp, i, r.row_stat[i]);
     for (j = 1; j <= lp.n; j++) glp_set_col_stat(lp, j, r.col_stat[j]);
 };
+
+// the LP / MIP preprocessor (glpnpp01.js .. glpnpp05.js, called by
+// glp_simplex's preprocess_and_solve_lp glpapi06.js:41 and glp_intopt's
+// preprocess_and_solve_mip glpapi09.js:116): the native workspace (gk_npp_*)
+// for loads with names and scaling off, the reference's own otherwise; the
+// reduced problem is built through the reference's glp_* API, as its
+// npp_build_prob builds it (glpnpp01.js:396)
+(function () {
+    var js = {create: npp_create_wksp, load: npp_load_prob, simplex: npp_simplex, integer: npp_integer,
+              build: npp_build_prob, post: npp_postprocess, unload: npp_unload_sol};
+    npp_create_wksp = function () { return {__gk: null, __js: null}; };
+    npp_load_prob = function (npp, orig, names, sol, scaling) {
+        if (names || scaling || !(sol == GLP_SOL || sol == GLP_MIP)) {
+            npp.__js = js.create();
+            js.load(npp.__js, orig, names, sol, scaling);
+            return;
+        }
+        npp.__gk = __gk.nppLoad(orig, sol);
+    };
+    npp_simplex = function (npp, parm) { return npp.__js ? js.simplex(npp.__js, parm) : __gk.nppSimplex(npp.__gk); };
+    npp_integer = function (npp, parm) {
+        return npp.__js ? js.integer(npp.__js, parm) : __gk.nppInteger(npp.__gk, parm, xprintf);
+    };
+    npp_build_prob = function (npp, prob) {
+        if (npp.__js) { js.build(npp.__js, prob); return; }
+        var r = __gk.nppBuild(npp.__gk), i, j, k, len, ind, val;
+        glp_erase_prob(prob);
+        glp_set_obj_dir(prob, r.dir);
+        glp_set_obj_coef(prob, 0, r.c0[0]);
+        for (i = 1; i <= r.m; i++) {
+            glp_add_rows(prob, 1);
+            glp_set_row_bnds(prob, i, r.row_type[i], r.row_lb[i], r.row_ub[i]);
+        }
+        ind = new Int32Array(1 + r.m);
+        val = new Float64Array(1 + r.m);
+        for (j = 1; j <= r.n; j++) {
+            glp_add_cols(prob, 1);
+            glp_set_col_kind(prob, j, r.col_kind[j]);
+            glp_set_col_bnds(prob, j, r.col_type[j], r.col_lb[j], r.col_ub[j]);
+            glp_set_obj_coef(prob, j, r.col_coef[j]);
+            // the workspace's list order, which glp_set_mat_col reverses
+            len = 0;
+            for (k = r.A_ptr[j + 1] - 1; k >= r.A_ptr[j]; k--) {
+                len++;
+                ind[len] = r.A_ind[k];
+                val[len] = r.A_val[k];
+            }
+            glp_set_mat_col(prob, j, len, ind, val);
+        }
+    };
+    npp_postprocess = function (npp, prob) {
+        if (npp.__js) return js.post(npp.__js, prob);
+        __gk.nppPostprocess(npp.__gk, prob);
+    };
+    npp_unload_sol = function (npp, orig) {
+        if (npp.__js) return js.unload(npp.__js, orig);
+        __gk.nppUnload(npp.__gk, orig);
+    };
+})();
 
 (function () {
     function versioned(f) {

@@ -8,7 +8,8 @@ var core = require(path.join(__dirname, 'gk_core.js'));
 
 var names = ['create', 'deviceCount', 'abiVersion', 'lastError', 'bfdCreate', 'bfdSetParm', 'bfdFactorizeCsc',
              'bfdFtran', 'bfdBtran', 'bfdUpdate', 'bfdGetCount', 'bfdValid', 'spx', 'ios', 'stats', 'advBasis',
-             'evalTabRows'];
+             'evalTabRows', 'nppCreate', 'nppLoad', 'nppSimplex', 'nppInteger', 'nppBuildSize', 'nppBuild',
+             'nppPostprocess', 'nppUnloadSol', 'nppUnloadMip'];
 names.forEach(function (k) { assert.strictEqual(typeof core.addon[k], 'function', k); });
 assert.strictEqual(core.addon.abiVersion(), 5);
 
@@ -79,6 +80,47 @@ glpk.glp_set_print_func(function () {});
         }
     });
     console.log('ok adv basis (' + files.length + ' reference fixtures)');
+})();
+// glp_simplex / glp_intopt with presolve = GLP_ON go through the native
+// preprocessor (the shim's npp_* rebinding): the runs the reference's own
+// preprocessor stops (no primal / no dual feasible solution) end there
+// without a device, with the reference's return code and lines
+(function () {
+    var gdir = path.join(__dirname, '..', 'tests', 'golden');
+    var calls = 0, keep = core.nppLoad;
+    core.nppLoad = function () { calls++; return keep.apply(this, arguments); };
+    var files = fs.readdirSync(gdir).filter(function (f) { return /^presolve_(wild|mix|sparse).*\.json$/.test(f); }).sort();
+    var stopped = 0;
+    files.forEach(function (f) {
+        var d = JSON.parse(fs.readFileSync(path.join(gdir, f), 'utf8'));
+        d.runs.forEach(function (run) {
+            if (run.reduced !== null) return;
+            var P = glpk.glp_create_prob(), i, j, k;
+            glpk.glp_set_obj_dir(P, d.dir);
+            glpk.glp_set_obj_coef(P, 0, d.c0);
+            if (d.m) glpk.glp_add_rows(P, d.m);
+            if (d.n) glpk.glp_add_cols(P, d.n);
+            for (i = 1; i <= d.m; i++) glpk.glp_set_row_bnds(P, i, d.row_type[i - 1], d.row_lb[i - 1], d.row_ub[i - 1]);
+            for (j = 1; j <= d.n; j++) {
+                glpk.glp_set_col_bnds(P, j, d.col_type[j - 1], d.col_lb[j - 1], d.col_ub[j - 1]);
+                glpk.glp_set_obj_coef(P, j, d.col_coef[j - 1]);
+            }
+            var ia = [0], ja = [0], ar = [0];
+            for (j = 1; j <= d.n; j++)
+                for (k = d.A_ptr[j - 1]; k < d.A_ptr[j]; k++) { ia.push(d.A_ind[k]); ja.push(j); ar.push(d.A_val[k]); }
+            if (ia.length > 1) glpk.glp_load_matrix(P, ia.length - 1, ia, ja, ar);
+            var lines = [];
+            glpk.glp_set_print_func(function (s) { lines.push(s); });
+            var ret = glpk.glp_simplex(P, new glpk.SMCP({meth: run.opts.meth, presolve: glpk.GLP_ON}));
+            glpk.glp_set_print_func(function () {});
+            assert.strictEqual(ret, run.ret, f);
+            assert.deepStrictEqual(lines, run.lines, f + ': printed lines');
+            stopped++;
+        });
+    });
+    core.nppLoad = keep;
+    assert.ok(stopped >= 10 && calls === stopped, 'presolve runs ' + stopped + ', native loads ' + calls);
+    console.log('ok presolve stops (' + stopped + ' reference runs, native preprocessor)');
 })();
 var lp = glpk.glp_create_prob();
 glpk.glp_set_obj_dir(lp, glpk.GLP_MAX);

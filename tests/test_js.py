@@ -27,6 +27,17 @@ def test_addon_and_shim_cpu():
     assert r.stdout.startswith("ok"), r.stdout
 
 
+def test_js_native_presolver_cpu():
+    """The native preprocessor through the JS marshalling (gk_core npp*,
+    bound by the shim to the reference's npp_* names): reduced problems and
+    recovered solutions of the presolve_* / mippre_* reference runs."""
+    _addon()
+    r = subprocess.run([NODE, os.path.join(ROOT, "js", "test_npp_cpu.js")], capture_output=True, text=True,
+                       timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert r.stdout.startswith("ok js npp"), r.stdout
+
+
 @pytest.mark.gpu
 def test_js_gpu_parity():
     """Every explicit LP fixture through the JS marshalling and the addon on the device."""
