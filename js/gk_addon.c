@@ -23,6 +23,7 @@
 #include <stdio.h>
 #include <string.h>
 #include <stdlib.h>
+#include <unistd.h>
 #include "../include/glpk_mi355x.h"
 
 #define CHECK(call)                                                                 \
@@ -138,10 +139,13 @@ static void set_num(napi_env env, napi_value obj, const char *name, double v)
  * order in which the remaining externals are finalized is not defined) */
 static int g_teardown = 0;
 
+static void npp_free_all(void);
+
 static void teardown_hook(void *arg)
 {
     (void)arg;
     g_teardown = 1;
+    npp_free_all();                 /* the preprocessor workspaces are host memory only */
 }
 
 static void ctx_fin(napi_env env, void *data, void *hint)
@@ -638,22 +642,67 @@ static napi_value js_eval_tab_rows(napi_env env, napi_callback_info info)
 
 /* ------------------------------------------------------------- presolver */
 /* npp*: the LP / MIP preprocessor (gk_npp_*, glpnpp01.js .. glpnpp05.js);
- * host code, no context.  The JS side (js/gk_core.js nppSolve, js/gk_shim.js)
- * rebinds the reference's npp_* entry points to these. */
-static void npp_fin(napi_env env, void *data, void *hint)
+ * host code, no context.  The JS side (js/gk_core.js npp*, js/gk_shim.js)
+ * rebinds the reference's npp_* entry points to these.  A workspace is a
+ * small integer (an index into npp_tab), freed by nppFree when the JS side is
+ * done with it and at environment teardown otherwise: no external with a
+ * finalizer (libnode 12 runs those during its own teardown and can fault
+ * there) */
+static gk_npp **npp_tab = NULL;
+static int npp_cap = 0;
+
+static void npp_free_all(void)
 {
-    (void)env; (void)hint;
-    gk_npp_destroy((gk_npp *)data);
+    for (int k = 0; k < npp_cap; k++)
+        if (npp_tab[k]) {
+            gk_npp_destroy(npp_tab[k]);
+            npp_tab[k] = NULL;
+        }
+}
+
+static gk_npp *npp_get(napi_env env, napi_value v)
+{
+    int k = -1;
+    if (napi_get_value_int32(env, v, &k) != napi_ok || k < 0 || k >= npp_cap || !npp_tab[k]) {
+        napi_throw_error(env, NULL, "gk_addon: invalid preprocessor workspace");
+        return NULL;
+    }
+    return npp_tab[k];
 }
 
 static napi_value js_npp_create(napi_env env, napi_callback_info info)
 {
     (void)info;
+    int k = 0;
+    while (k < npp_cap && npp_tab[k]) k++;
+    if (k == npp_cap) {
+        int cap = npp_cap ? 2 * npp_cap : 16;
+        gk_npp **t = (gk_npp **)realloc(npp_tab, (size_t)cap * sizeof *t);
+        if (!t) {
+            napi_throw_error(env, NULL, "gk_addon: out of memory");
+            return NULL;
+        }
+        for (int q = npp_cap; q < cap; q++) t[q] = NULL;
+        npp_tab = t;
+        npp_cap = cap;
+    }
     gk_npp *w = gk_npp_create();
     if (!w) return throw_gk(env, "npp_create_wksp");
-    napi_value r;
-    CHECK(napi_create_external(env, w, npp_fin, NULL, &r));
-    return r;
+    npp_tab[k] = w;
+    return mk_int(env, k);
+}
+
+static napi_value js_npp_free(napi_env env, napi_callback_info info)
+{
+    napi_value argv[1];
+    if (!get_args(env, info, 1, argv)) return NULL;
+    int k = -1;
+    CHECK(napi_get_value_int32(env, argv[0], &k));
+    if (k >= 0 && k < npp_cap && npp_tab[k]) {
+        gk_npp_destroy(npp_tab[k]);
+        npp_tab[k] = NULL;
+    }
+    return mk_int(env, 0);
 }
 
 static int npp_ret(napi_env env, int ret, const char *what, napi_value *out)
@@ -676,14 +725,14 @@ static napi_value js_npp_load(napi_env env, napi_callback_info info)
     int sol = 0;
     CHECK(napi_get_value_int32(env, argv[3], &sol));
     const signed char *kind = (const signed char *)ta(env, argv[2]);
-    return npp_ret(env, gk_npp_load((gk_npp *)get_ext(env, argv[0]), &lp, kind, sol), "npp_load_prob", &r) ? r : NULL;
+    return npp_ret(env, gk_npp_load(npp_get(env, argv[0]), &lp, kind, sol), "npp_load_prob", &r) ? r : NULL;
 }
 
 static napi_value js_npp_simplex(napi_env env, napi_callback_info info)
 {
     napi_value argv[1], r;
     if (!get_args(env, info, 1, argv)) return NULL;
-    return npp_ret(env, gk_npp_simplex((gk_npp *)get_ext(env, argv[0])), "npp_simplex", &r) ? r : NULL;
+    return npp_ret(env, gk_npp_simplex(npp_get(env, argv[0])), "npp_simplex", &r) ? r : NULL;
 }
 
 /* nppInteger(npp, binarize, msg Int32Array(7)) */
@@ -694,7 +743,7 @@ static napi_value js_npp_integer(napi_env env, napi_callback_info info)
     int bin = 0;
     CHECK(napi_get_value_int32(env, argv[1], &bin));
     int *msg = (int *)ta(env, argv[2]);
-    return npp_ret(env, gk_npp_integer((gk_npp *)get_ext(env, argv[0]), bin, msg), "npp_integer", &r) ? r : NULL;
+    return npp_ret(env, gk_npp_integer(npp_get(env, argv[0]), bin, msg), "npp_integer", &r) ? r : NULL;
 }
 
 /* nppBuildSize(npp, out Int32Array(3)) -> m, n, nnz in out */
@@ -707,7 +756,7 @@ static napi_value js_npp_build_size(napi_env env, napi_callback_info info)
         napi_throw_type_error(env, NULL, "nppBuildSize: Int32Array(3) expected");
         return NULL;
     }
-    return npp_ret(env, gk_npp_build_size((gk_npp *)get_ext(env, argv[0]), &o[0], &o[1], &o[2]), "npp_build_prob",
+    return npp_ret(env, gk_npp_build_size(npp_get(env, argv[0]), &o[0], &o[1], &o[2]), "npp_build_prob",
                    &r) ? r : NULL;
 }
 
@@ -725,7 +774,7 @@ static napi_value js_npp_build(napi_env env, napi_callback_info info)
             return NULL;
         }
     }
-    int ret = gk_npp_build((gk_npp *)get_ext(env, argv[0]), (signed char *)a[1], (double *)a[2], (double *)a[3],
+    int ret = gk_npp_build(npp_get(env, argv[0]), (signed char *)a[1], (double *)a[2], (double *)a[3],
                            (signed char *)a[4], (double *)a[5], (double *)a[6], (double *)a[7], (signed char *)a[8],
                            (int *)a[9], (int *)a[10], (double *)a[11], (int *)a[12], (int *)a[13], (double *)a[14]);
     return npp_ret(env, ret, "npp_build_prob", &r) ? r : NULL;
@@ -740,7 +789,7 @@ static napi_value js_npp_postprocess(napi_env env, napi_callback_info info)
     int s1 = 0, s2 = 0;
     CHECK(napi_get_value_int32(env, argv[1], &s1));
     CHECK(napi_get_value_int32(env, argv[2], &s2));
-    int ret = gk_npp_postprocess((gk_npp *)get_ext(env, argv[0]), s1, s2, (const signed char *)ta(env, argv[3]),
+    int ret = gk_npp_postprocess(npp_get(env, argv[0]), s1, s2, (const signed char *)ta(env, argv[3]),
                                  (const double *)ta(env, argv[4]), (const signed char *)ta(env, argv[5]),
                                  (const double *)ta(env, argv[6]));
     return npp_ret(env, ret, "npp_postprocess", &r) ? r : NULL;
@@ -754,7 +803,7 @@ static napi_value js_npp_unload_sol(napi_env env, napi_callback_info info)
     if (!get_args(env, info, 2, argv)) return NULL;
     gk_lp lp;
     if (!fill_lp(env, argv[1], &lp)) return NULL;
-    if (!npp_ret(env, gk_npp_unload_sol((gk_npp *)get_ext(env, argv[0]), &lp), "npp_unload_sol", &r)) return NULL;
+    if (!npp_ret(env, gk_npp_unload_sol(npp_get(env, argv[0]), &lp), "npp_unload_sol", &r)) return NULL;
     set_num(env, argv[1], "pbs_stat", lp.pbs_stat);
     set_num(env, argv[1], "dbs_stat", lp.dbs_stat);
     set_num(env, argv[1], "obj_val", lp.obj_val);
@@ -770,12 +819,31 @@ static napi_value js_npp_unload_mip(napi_env env, napi_callback_info info)
     if (!fill_lp(env, argv[1], &lp)) return NULL;
     int st = 0;
     double obj = 0.0;
-    int ret = gk_npp_unload_mip((gk_npp *)get_ext(env, argv[0]), &lp, (const signed char *)ta(env, argv[2]),
+    int ret = gk_npp_unload_mip(npp_get(env, argv[0]), &lp, (const signed char *)ta(env, argv[2]),
                                 (double *)ta(env, argv[3]), (double *)ta(env, argv[4]), &st, &obj);
     if (!npp_ret(env, ret, "npp_unload_sol", &r)) return NULL;
     set_num(env, argv[1], "mip_stat", st);
     set_num(env, argv[1], "mip_obj", obj);
     return r;
+}
+
+/* exitNow(code): the process leaves with code from node's 'exit' event, before
+ * the environment teardown.  libnode 12 (the node of this image) runs the
+ * second-pass phantom callbacks of N-API references during its teardown and
+ * can fault inside them (node::...PendingPhantomCallback::Invoke) once
+ * externals with finalizers exist: js/gk_core.js calls this from its 'exit'
+ * listener as soon as it has created one.  stdout / stderr are synchronous
+ * for files, pipes and terminals on Linux, so nothing written is lost. */
+static napi_value js_exit_now(napi_env env, napi_callback_info info)
+{
+    napi_value argv[1];
+    if (!get_args(env, info, 1, argv)) return NULL;
+    int code = 0;
+    CHECK(napi_get_value_int32(env, argv[0], &code));
+    fflush(stdout);
+    fflush(stderr);
+    _exit(code);
+    return NULL;
 }
 
 #define FN(name, f) { name, NULL, f, NULL, NULL, NULL, napi_enumerable, NULL }
@@ -806,7 +874,7 @@ static napi_value init(napi_env env, napi_value exports)
         FN("nppCreate", js_npp_create), FN("nppLoad", js_npp_load), FN("nppSimplex", js_npp_simplex),
         FN("nppInteger", js_npp_integer), FN("nppBuildSize", js_npp_build_size), FN("nppBuild", js_npp_build),
         FN("nppPostprocess", js_npp_postprocess), FN("nppUnloadSol", js_npp_unload_sol),
-        FN("nppUnloadMip", js_npp_unload_mip),
+        FN("nppUnloadMip", js_npp_unload_mip), FN("nppFree", js_npp_free), FN("exitNow", js_exit_now),
     };
     napi_define_properties(env, exports, sizeof d / sizeof d[0], d);
     return exports;

@@ -17,8 +17,23 @@ var GLP_BS = 1, GLP_UNDEF = 1, GLP_EFAIL = 0x05;
 var ctx = null;
 var version = 0;
 
+// once an external with a finalizer exists (context, factor, communicator),
+// the process leaves from node's 'exit' event with its exit code, before
+// libnode 12's environment teardown (see exitNow in gk_addon.c); the
+// listener is registered last-in at that moment, so listeners the program
+// registered earlier still run
+var exitArmed = false;
+function armExit() {
+    if (exitArmed) return;
+    exitArmed = true;
+    process.on('exit', function (code) { addon.exitNow(code === undefined ? process.exitCode || 0 : code); });
+}
+
 function context() {
-    if (ctx === null) ctx = addon.create(parseInt(process.env.GK_DEVICE || '0', 10));
+    if (ctx === null) {
+        armExit();
+        ctx = addon.create(parseInt(process.env.GK_DEVICE || '0', 10));
+    }
     return ctx;
 }
 
@@ -351,7 +366,17 @@ function nppLoad(orig, sol) {
     addon.nppLoad(h, L, kind, sol);
     return {h: h, sol: sol, dir: orig.dir};
 }
-function nppSimplex(w) { return addon.nppSimplex(w.h); }
+// a stop of the preprocessor ends the caller's use of the workspace
+// (glpapi06.js:84, glpapi09.js:162)
+function nppDone(w) {
+    if (w.h !== null) addon.nppFree(w.h);
+    w.h = null;
+}
+function nppSimplex(w) {
+    var ret = addon.nppSimplex(w.h);
+    if (ret !== 0) nppDone(w);
+    return ret;
+}
 // npp_integer's lines (glpnpp04.js:92-97, glpnpp05.js:475-514) through the
 // reference's xprintf (term_out as the caller set it)
 function nppInteger(w, parm, print) {
@@ -364,7 +389,8 @@ function nppInteger(w, parm, print) {
         if (msg[4] > 0) print(msg[4] + " hidden packing inequaliti(es) were detected");
         if (msg[5] > 0) print(msg[5] + " hidden covering inequaliti(es) were detected");
         if (msg[6] > 0) print(msg[6] + " constraint coefficient(s) were reduced");
-    }
+    } else
+        nppDone(w);
     return ret;
 }
 // the reduced problem as arrays (1-based; A by columns in the order the
@@ -403,6 +429,7 @@ function nppUnload(w, orig) {
         var kind = new Int8Array(orig.n + 1), rx = new Float64Array(orig.m + 1), cx = new Float64Array(orig.n + 1);
         for (j = 1; j <= orig.n; j++) kind[j] = orig.col[j].kind;
         addon.nppUnloadMip(w.h, L, kind, rx, cx);
+        nppDone(w);
         orig.mip_stat = L.mip_stat;
         orig.mip_obj = L.mip_obj;
         for (j = 1; j <= orig.n; j++) orig.col[j].mipx = cx[j];
@@ -410,6 +437,7 @@ function nppUnload(w, orig) {
         return;
     }
     addon.nppUnloadSol(w.h, L);
+    nppDone(w);
     orig.valid = 0;
     orig.pbs_stat = L.pbs_stat;
     orig.dbs_stat = L.dbs_stat;

@@ -142,8 +142,5 @@ fs.readdirSync(dir).filter(function (f) { return /^tab_.*\.json$/.test(f); }).so
 assert.ok(ntab >= 5, 'too few tab fixtures: ' + ntab);
 
 console.log('ok js gpu parity: ' + ncase + ' runs, ' + nmip + ' MIPs, ' + nscale + ' scalings, ' + ntab + ' tableau-row fixtures');
-// node 12's environment teardown can run pending N-API second-pass
-// finalizers after the addon's environment is gone (a segfault inside
-// libnode's PendingPhantomCallback::Invoke, seen when handles were
-// collected just before exit); a checked script leaves without it
-process.exit(0);
+// no process.exit here: the library leaves from node's 'exit' event itself
+// (js/gk_core.js armExit), so the script's exit code stands

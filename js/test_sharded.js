@@ -24,5 +24,3 @@ process.argv.slice(2).forEach(function (name) {
                                 backend: core.comm() ? core.addon.commBackend(core.comm()) : 0, ret: ret,
                                 mip_stat: lp.mip_stat, mip_obj: lp.mip_obj, x: x}));
 });
-// see test_gpu.js: leave before node 12's environment teardown
-process.exit(0);
