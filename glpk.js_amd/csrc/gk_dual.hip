@@ -2424,6 +2424,13 @@ __global__ void __launch_bounds__(1024) k_dual_update(SpxDev d, int gn, int ncb,
     const double teta = delta / tp;
     const double ti = srow[0][rl];
     const double ui = (NRHS == 2) ? srow[NRHS - 1][rl] : 0.0;
+    // the books, as soon as the pivot is committed: their straight-line
+    // code runs once per launch with a cold instruction cache (≈2.5 µs of
+    // fetches), so the books wave starts it here, under wave 0's row and
+    // column updates and the phase-I barrier below, instead of after them.
+    // Nothing later in this kernel reads what it writes (the other blocks
+    // read the compact rho, not the lists, and st->nr / st->nwl in trip 1)
+    if (bk && w == wa && lane == 0) books_store<NRHS>(d, sbk, kp, kq, tkp, refkp, nr, ns, rowpath, bytes_fixed);
     // ---- product-form update of the entries held in registers
     {
         const bool z = (r == p - 1);
@@ -2521,9 +2528,6 @@ __global__ void __launch_bounds__(1024) k_dual_update(SpxDev d, int gn, int ncb,
         st->pend = 1;
         st->fxp = (tkp == FX);
         st->rclr = (tkp == FX && refkp);
-    }
-    if (bk && w == wa && lane == 0) {
-        books_store<NRHS>(d, sbk, kp, kq, tkp, refkp, nr, ns, rowpath, bytes_fixed);
     }
     TPH(3, 7);
 }
