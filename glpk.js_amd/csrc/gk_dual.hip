@@ -417,16 +417,27 @@ __global__ void __launch_bounds__(256) k_dual_prep(SpxDev d, int gm)
         Cand c = no_cand(0.0);
         if (i < m) {
             const int k = d.head[i];
-            c = chuzr_cand_v(i, k, d.type[k - 1], d.lb[k - 1], d.ub[k - 1], d.bbar[i], reset ? 1.0 : d.gamma[i],
-                             st->tol_bnd);
+            const signed char t = d.type[k - 1];
+            const double l = d.lb[k - 1], u = d.ub[k - 1];
+            // the attributes of the basic variable by position (SpxDev)
+            d.ptype[i] = t;
+            d.plb[i] = l;
+            d.pub[i] = u;
+            d.pref[i] = d.refsp[k - 1];
+            c = chuzr_cand_v(i, k, t, l, u, d.bbar[i], reset ? 1.0 : d.gamma[i], st->tol_bnd);
         }
         const Cand b = wave_best<0>(c);
         if ((threadIdx.x & 63) == 0) cand_chuzr(d)[blockIdx.x * 4 + (threadIdx.x >> 6)] = b;
     }
-    if (st->phase == 1) {
-        const int bad = (i < n) ? dual_bad(d, d.head[m + i], d.cbar[i], st->tol_dj) : 0;
-        if (__syncthreads_or(bad) && threadIdx.x == 0) atomicOr(&st->dinf, 1);
+    int bad = 0;
+    if (i < n) {
+        const int k = d.head[m + i];
+        const signed char ot = d.orig_type[k - 1];
+        d.notype[i] = ot;
+        const double cb = d.cbar[i], tol = st->tol_dj;
+        bad = (cb < -tol && (ot == LO || ot == FR)) || (cb > +tol && (ot == UP || ot == FR));   // dual_bad
     }
+    if (st->phase == 1 && __syncthreads_or(bad) && threadIdx.x == 0) atomicOr(&st->dinf, 1);
 }
 
 // ---------------------------------------------------------------------------
@@ -1824,16 +1835,22 @@ __global__ void __launch_bounds__(256) k_dual_commit(SpxDev d, int pse, int nvb,
         const double ui = (pse && in_m) ? d.u[i] : 0.0;
         double cb = in_n ? d.cbar[i] : 0.0;
         const double tri = in_n ? d.trow[i] : 0.0;
-        const int kn = in_n ? ((i == q - 1) ? kp : d.head[m + i]) : 1;
         const double piv1 = d.tcol[p - 1], piv2 = d.trow[q - 1];
         const int tkq = d.type[kq - 1], tkp = d.type[kp - 1];
         const bool refkp = pse && d.refsp[kp - 1] != 0;
+        const bool refkq = pse && d.refsp[kq - 1] != 0;
+        const double lbq = d.lb[kq - 1], ubq = d.ub[kq - 1];
+        const int otkp = d.orig_type[kp - 1];
         const int knew = (i == p - 1) ? kq : kold;
-        const int tkold = in_m ? d.type[kold - 1] : 0;
-        const bool refk = (pse && in_m) ? d.refsp[kold - 1] != 0 : false;
-        const int tknew = in_m ? d.type[knew - 1] : 0;
-        const double lbn = in_m ? d.lb[knew - 1] : 0.0, ubn = in_m ? d.ub[knew - 1] : 0.0;
-        const int ot = in_n ? d.orig_type[kn - 1] : 0;
+        // the basic variable's attributes by position (k_dual_prep keeps
+        // them), the entering variable's own at row p
+        const int ic = min(i, m - 1), jc = min(i, n - 1);
+        const int tkold = in_m ? (int)d.ptype[ic] : 0;
+        const bool refk = (pse && in_m) ? d.pref[ic] != 0 : false;
+        const double plbi = d.plb[ic], pubi = d.pub[ic];
+        const int tknew = in_m ? ((i == p - 1) ? tkq : tkold) : 0;
+        const double lbn = in_m ? ((i == p - 1) ? lbq : plbi) : 0.0, ubn = in_m ? ((i == p - 1) ? ubq : pubi) : 0.0;
+        const int ot = in_n ? ((i == q - 1) ? otkp : (int)d.notype[jc]) : 0;
         const double xq = (i == p - 1) ? get_xN(d.stat, d.lb, d.ub, kq, q) : 0.0;
         // list maintenance operands (block 0, wave 1)
         const bool maint = (blockIdx.x == 0 && threadIdx.x == 64);
@@ -1860,13 +1877,23 @@ __global__ void __launch_bounds__(256) k_dual_commit(SpxDev d, int pse, int nvb,
         const double tp = bad ? piv2 : piv1;
         const double teta = delta / tp;
         if (in_m) {
-            if (i == p - 1) bb = xq + teta;
-            else if (teta != 0.0) bb += ti * teta;
+            if (i == p - 1) {
+                bb = xq + teta;
+                // row p now holds the entering variable (SpxDev position arrays)
+                d.ptype[i] = (signed char)tkq;
+                d.plb[i] = lbq;
+                d.pub[i] = ubq;
+                d.pref[i] = refkq ? 1 : 0;
+            } else if (teta != 0.0)
+                bb += ti * teta;
             d.bbar[i] = bb;
         }
         if (in_n) {
-            if (i == q - 1) cb = new_dq;
-            else if (new_dq != 0.0) cb -= tri * new_dq;
+            if (i == q - 1) {
+                cb = new_dq;
+                d.notype[i] = (signed char)otkp;       // column q now holds the leaving variable
+            } else if (new_dq != 0.0)
+                cb -= tri * new_dq;
             d.cbar[i] = cb;
         }
         if (pse && in_m) {
@@ -2259,7 +2286,6 @@ __global__ void __launch_bounds__(1024) k_dual_update(SpxDev d, int gn, int ncb,
     const int jc = min(j, n - 1);
     double cb = d.cbar[jc];
     double tri = d.trow[jc];
-    int hkj = d.head[m + jc];
     // ---- the selections of trip 1
     pin.c = no_cand(0.0);
 #pragma unroll
@@ -2281,7 +2307,7 @@ __global__ void __launch_bounds__(1024) k_dual_update(SpxDev d, int gn, int ncb,
         if (gs + u * NSL > nr_cap) { c0[u] = 0; rv[u] = 0.0; }
     const int kold = rowlane ? kold_l : 1;
     if (!rowlane) { bb = 0.0; g = 0.0; }
-    if (!colth) { cb = 0.0; tri = 0.0; hkj = 1; }
+    if (!colth) { cb = 0.0; tri = 0.0; }
     TPH(3, 0);
     const double gsum = (NRHS == 2 && w == 0) ? wsum(pin.g) : 0.0;
     // ---- the entering choice (every wave)
@@ -2306,16 +2332,21 @@ __global__ void __launch_bounds__(1024) k_dual_update(SpxDev d, int gn, int ncb,
     const int tkp = d.type[kp - 1];
     const bool refkp = NRHS == 2 && d.refsp[kp - 1] != 0;
     const int knew = (r == p - 1) ? kqc : kold;
-    const int tkold_l = d.type[kold - 1];
-    const int refk_l = (NRHS == 2) ? d.refsp[kold - 1] : 0;
-    const int tknew_l = d.type[knew - 1];
-    const double lbn_l = d.lb[knew - 1], ubn_l = d.ub[knew - 1];
+    // the row's basic variable by position (coalesced; k_dual_prep / the
+    // pivot keep them), the entering variable's own at row p
+    const int tkold_l = d.ptype[rc];
+    const int refk_l = (NRHS == 2) ? d.pref[rc] : 0;
     const int stq_l = d.stat[qc - 1];
     const double lbq = d.lb[kqc - 1], ubq = d.ub[kqc - 1];
     const int tkq = d.type[kqc - 1];
+    const int refkq = (NRHS == 2) ? d.refsp[kqc - 1] : 0;
+    const double plb_l = d.plb[rc], pub_l = d.pub[rc];
+    const bool rowp = (r == p - 1);
+    const int tknew_l = rowp ? tkq : tkold_l;
+    const double lbn_l = rowp ? lbq : plb_l, ubn_l = rowp ? ubq : pub_l;
     const double piv2 = d.trow[qc - 1];
-    const int kn = colth ? ((j == q - 1) ? kp : hkj) : 1;
-    const int ot_l = d.orig_type[kn - 1];
+    const int otkp = d.orig_type[kp - 1];               // the leaving variable's, at column q
+    const int ot_l = colth ? ((j == q - 1) ? otkp : (int)d.notype[jc]) : 0;
     if (bk && w == wa) {
         Books b;
         books_load<NRHS>(d, b, nr, kqc);
@@ -2430,7 +2461,19 @@ __global__ void __launch_bounds__(1024) k_dual_update(SpxDev d, int gn, int ncb,
     // column updates and the phase-I barrier below, instead of after them.
     // Nothing later in this kernel reads what it writes (the other blocks
     // read the compact rho, not the lists, and st->nr / st->nwl in trip 1)
-    if (bk && w == wa && lane == 0) books_store<NRHS>(d, sbk, kp, kq, tkp, refkp, nr, ns, rowpath, bytes_fixed);
+    // The pivot's scalar state goes out with them, for the same reason (no
+    // other block of this kernel reads these fields)
+    if (bk && w == wa && lane == 0) {
+        books_store<NRHS>(d, sbk, kp, kq, tkp, refkp, nr, ns, rowpath, bytes_fixed);
+        st->q = q;
+        st->kq = kq;
+        st->new_dq = new_dq;
+        st->teta = teta;
+        st->pivot = tp;
+        st->pend = 1;
+        st->fxp = (tkp == FX);
+        st->rclr = (tkp == FX && refkp);
+    }
     // ---- product-form update of the entries held in registers
     {
         const bool z = (r == p - 1);
@@ -2489,6 +2532,12 @@ __global__ void __launch_bounds__(1024) k_dual_update(SpxDev d, int gn, int ncb,
             }
             const bool reset = (NRHS == 2 && refct == 1);
             cnd = chuzr_cand_v(r, knew, tknew, lbn, ubn, bb, reset ? 1.0 : g, tol_bnd);
+            if (r == p - 1) {                         // row p now holds the entering variable
+                d.ptype[r] = (signed char)tknew;
+                d.plb[r] = lbn;
+                d.pub[r] = ubn;
+                d.pref[r] = (signed char)refkq;
+            }
         }
         const Cand best = wave_best<0>(cnd);
         if (lane == 0) cand_chuzr(d)[blockIdx.x] = best;
@@ -2512,6 +2561,7 @@ __global__ void __launch_bounds__(1024) k_dual_update(SpxDev d, int gn, int ncb,
         if (j == q - 1) {
             cb = new_dq;
             st->cbar_q_old = cb_old;
+            d.notype[j] = (signed char)ot;            // column q now holds the leaving variable
         } else if (new_dq != 0.0)
             cb -= tri * new_dq;
         d.cbar[j] = cb;
@@ -2519,16 +2569,6 @@ __global__ void __launch_bounds__(1024) k_dual_update(SpxDev d, int gn, int ncb,
     }
     TPH(3, 6);
     if (phase == 1 && __syncthreads_or(badj) && threadIdx.x == 0) atomicOr(&st->dinf, 1);
-    if (lead) {
-        st->q = q;
-        st->kq = kq;
-        st->new_dq = new_dq;
-        st->teta = teta;
-        st->pivot = tp;
-        st->pend = 1;
-        st->fxp = (tkp == FX);
-        st->rclr = (tkp == FX && refkp);
-    }
     TPH(3, 7);
 }
 
