@@ -2332,21 +2332,10 @@ __global__ void __launch_bounds__(1024) k_dual_update(SpxDev d, int gn, int ncb,
     const int tkp = d.type[kp - 1];
     const bool refkp = NRHS == 2 && d.refsp[kp - 1] != 0;
     const int knew = (r == p - 1) ? kqc : kold;
-    // the row's basic variable by position (coalesced; k_dual_prep / the
-    // pivot keep them), the entering variable's own at row p
-    const int tkold_l = d.ptype[rc];
-    const int refk_l = (NRHS == 2) ? d.pref[rc] : 0;
     const int stq_l = d.stat[qc - 1];
     const double lbq = d.lb[kqc - 1], ubq = d.ub[kqc - 1];
     const int tkq = d.type[kqc - 1];
-    const int refkq = (NRHS == 2) ? d.refsp[kqc - 1] : 0;
-    const double plb_l = d.plb[rc], pub_l = d.pub[rc];
-    const bool rowp = (r == p - 1);
-    const int tknew_l = rowp ? tkq : tkold_l;
-    const double lbn_l = rowp ? lbq : plb_l, ubn_l = rowp ? ubq : pub_l;
     const double piv2 = d.trow[qc - 1];
-    const int otkp = d.orig_type[kp - 1];               // the leaving variable's, at column q
-    const int ot_l = colth ? ((j == q - 1) ? otkp : (int)d.notype[jc]) : 0;
     if (bk && w == wa) {
         Books b;
         books_load<NRHS>(d, b, nr, kqc);
@@ -2413,15 +2402,11 @@ __global__ void __launch_bounds__(1024) k_dual_update(SpxDev d, int gn, int ncb,
         s = wsum(s);
         if (lane == 0) salpha = s;
     }
-    // operands of the row updates that depend on the choice
-    const int tkold = rowlane ? tkold_l : 0;
-    const bool refk = (NRHS == 2 && rowlane) ? refk_l != 0 : false;
-    const int tknew = rowlane ? tknew_l : 0;
-    const double lbn = rowlane ? lbn_l : 0.0, ubn = rowlane ? ubn_l : 0.0;
+    // operands of the row updates that depend on the choice: the row's basic
+    // variable (position arrays, loaded below), the entering one at row p
     // get_xN (glpspx01.js:442) of the entering variable
     const double xq_v = (stq_l == NU) ? ubq : (stq_l == NF ? 0.0 : lbq);
     const double xq = (rowlane && r == p - 1) ? xq_v : 0.0;
-    const int ot = colth ? ot_l : 0;
     sp[0][w][lane] = a;
     if (NRHS == 2) sp[NRHS - 1][w][lane] = b;
     TPH(3, 2);
@@ -2444,6 +2429,22 @@ __global__ void __launch_bounds__(1024) k_dual_update(SpxDev d, int gn, int ncb,
     }
     __syncthreads();
     TPH(3, 3);
+    // the row's basic variable by position and the column's non-basic one
+    // (coalesced; k_dual_prep and the pivot keep them), loaded by wave 0 —
+    // the only wave that reads them — here, where their latency overlaps the
+    // product-form update below (held from trip 2 they cost registers the
+    // 1024-thread block does not have)
+    int tkold_l = 0, refk_l = 0, ot_l = 0, refkq = 0;
+    double plb_l = 0.0, pub_l = 0.0;
+    if (w == 0) {
+        tkold_l = d.ptype[rc];
+        refk_l = (NRHS == 2) ? d.pref[rc] : 0;
+        plb_l = d.plb[rc];
+        pub_l = d.pub[rc];
+        refkq = (NRHS == 2) ? d.refsp[kqc - 1] : 0;        // the entering variable's, at row p
+        // the leaving variable's original type, at column q
+        ot_l = (j == q - 1) ? (int)d.orig_type[kp - 1] : (int)d.notype[jc];
+    }
     const double piv1 = salpha;
     const bool bad = fabs(piv1 - piv2) > 1e-8 * (1.0 + fabs(piv1)) ||
                      !((piv1 > 0.0 && piv2 > 0.0) || (piv1 < 0.0 && piv2 < 0.0));
@@ -2455,6 +2456,12 @@ __global__ void __launch_bounds__(1024) k_dual_update(SpxDev d, int gn, int ncb,
     const double teta = delta / tp;
     const double ti = srow[0][rl];
     const double ui = (NRHS == 2) ? srow[NRHS - 1][rl] : 0.0;
+    const bool rowp = (r == p - 1);
+    const int tkold = rowlane ? tkold_l : 0;
+    const bool refk = (NRHS == 2 && rowlane) ? refk_l != 0 : false;
+    const int tknew = rowlane ? (rowp ? tkq : tkold_l) : 0;
+    const double lbn = rowlane ? (rowp ? lbq : plb_l) : 0.0, ubn = rowlane ? (rowp ? ubq : pub_l) : 0.0;
+    const int ot = colth ? ot_l : 0;
     // the books, as soon as the pivot is committed: their straight-line
     // code runs once per launch with a cold instruction cache (≈2.5 µs of
     // fetches), so the books wave starts it here, under wave 0's row and
