@@ -206,7 +206,6 @@ static __device__ void reset_refsp_dev(const SpxDev &d, int dual)
         for (int i = threadIdx.x; i < m; i += blockDim.x) {
             d.refsp[d.head[i] - 1] = 1;
             d.gamma[i] = 1.0;
-            if (d.pref) d.pref[i] = 1;           // every basic variable is in the reference space
         }
     } else {
         for (int j = threadIdx.x; j < n; j += blockDim.x) {

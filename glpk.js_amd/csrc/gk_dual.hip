@@ -417,27 +417,16 @@ __global__ void __launch_bounds__(256) k_dual_prep(SpxDev d, int gm)
         Cand c = no_cand(0.0);
         if (i < m) {
             const int k = d.head[i];
-            const signed char t = d.type[k - 1];
-            const double l = d.lb[k - 1], u = d.ub[k - 1];
-            // the attributes of the basic variable by position (SpxDev)
-            d.ptype[i] = t;
-            d.plb[i] = l;
-            d.pub[i] = u;
-            d.pref[i] = d.refsp[k - 1];
-            c = chuzr_cand_v(i, k, t, l, u, d.bbar[i], reset ? 1.0 : d.gamma[i], st->tol_bnd);
+            c = chuzr_cand_v(i, k, d.type[k - 1], d.lb[k - 1], d.ub[k - 1], d.bbar[i], reset ? 1.0 : d.gamma[i],
+                             st->tol_bnd);
         }
         const Cand b = wave_best<0>(c);
         if ((threadIdx.x & 63) == 0) cand_chuzr(d)[blockIdx.x * 4 + (threadIdx.x >> 6)] = b;
     }
-    int bad = 0;
-    if (i < n) {
-        const int k = d.head[m + i];
-        const signed char ot = d.orig_type[k - 1];
-        d.notype[i] = ot;
-        const double cb = d.cbar[i], tol = st->tol_dj;
-        bad = (cb < -tol && (ot == LO || ot == FR)) || (cb > +tol && (ot == UP || ot == FR));   // dual_bad
+    if (st->phase == 1) {
+        const int bad = (i < n) ? dual_bad(d, d.head[m + i], d.cbar[i], st->tol_dj) : 0;
+        if (__syncthreads_or(bad) && threadIdx.x == 0) atomicOr(&st->dinf, 1);
     }
-    if (st->phase == 1 && __syncthreads_or(bad) && threadIdx.x == 0) atomicOr(&st->dinf, 1);
 }
 
 // ---------------------------------------------------------------------------
@@ -1835,22 +1824,16 @@ __global__ void __launch_bounds__(256) k_dual_commit(SpxDev d, int pse, int nvb,
         const double ui = (pse && in_m) ? d.u[i] : 0.0;
         double cb = in_n ? d.cbar[i] : 0.0;
         const double tri = in_n ? d.trow[i] : 0.0;
+        const int kn = in_n ? ((i == q - 1) ? kp : d.head[m + i]) : 1;
         const double piv1 = d.tcol[p - 1], piv2 = d.trow[q - 1];
         const int tkq = d.type[kq - 1], tkp = d.type[kp - 1];
         const bool refkp = pse && d.refsp[kp - 1] != 0;
-        const bool refkq = pse && d.refsp[kq - 1] != 0;
-        const double lbq = d.lb[kq - 1], ubq = d.ub[kq - 1];
-        const int otkp = d.orig_type[kp - 1];
         const int knew = (i == p - 1) ? kq : kold;
-        // the basic variable's attributes by position (k_dual_prep keeps
-        // them), the entering variable's own at row p
-        const int ic = min(i, m - 1), jc = min(i, n - 1);
-        const int tkold = in_m ? (int)d.ptype[ic] : 0;
-        const bool refk = (pse && in_m) ? d.pref[ic] != 0 : false;
-        const double plbi = d.plb[ic], pubi = d.pub[ic];
-        const int tknew = in_m ? ((i == p - 1) ? tkq : tkold) : 0;
-        const double lbn = in_m ? ((i == p - 1) ? lbq : plbi) : 0.0, ubn = in_m ? ((i == p - 1) ? ubq : pubi) : 0.0;
-        const int ot = in_n ? ((i == q - 1) ? otkp : (int)d.notype[jc]) : 0;
+        const int tkold = in_m ? d.type[kold - 1] : 0;
+        const bool refk = (pse && in_m) ? d.refsp[kold - 1] != 0 : false;
+        const int tknew = in_m ? d.type[knew - 1] : 0;
+        const double lbn = in_m ? d.lb[knew - 1] : 0.0, ubn = in_m ? d.ub[knew - 1] : 0.0;
+        const int ot = in_n ? d.orig_type[kn - 1] : 0;
         const double xq = (i == p - 1) ? get_xN(d.stat, d.lb, d.ub, kq, q) : 0.0;
         // list maintenance operands (block 0, wave 1)
         const bool maint = (blockIdx.x == 0 && threadIdx.x == 64);
@@ -1877,23 +1860,13 @@ __global__ void __launch_bounds__(256) k_dual_commit(SpxDev d, int pse, int nvb,
         const double tp = bad ? piv2 : piv1;
         const double teta = delta / tp;
         if (in_m) {
-            if (i == p - 1) {
-                bb = xq + teta;
-                // row p now holds the entering variable (SpxDev position arrays)
-                d.ptype[i] = (signed char)tkq;
-                d.plb[i] = lbq;
-                d.pub[i] = ubq;
-                d.pref[i] = refkq ? 1 : 0;
-            } else if (teta != 0.0)
-                bb += ti * teta;
+            if (i == p - 1) bb = xq + teta;
+            else if (teta != 0.0) bb += ti * teta;
             d.bbar[i] = bb;
         }
         if (in_n) {
-            if (i == q - 1) {
-                cb = new_dq;
-                d.notype[i] = (signed char)otkp;       // column q now holds the leaving variable
-            } else if (new_dq != 0.0)
-                cb -= tri * new_dq;
+            if (i == q - 1) cb = new_dq;
+            else if (new_dq != 0.0) cb -= tri * new_dq;
             d.cbar[i] = cb;
         }
         if (pse && in_m) {
@@ -2286,6 +2259,7 @@ __global__ void __launch_bounds__(1024) k_dual_update(SpxDev d, int gn, int ncb,
     const int jc = min(j, n - 1);
     double cb = d.cbar[jc];
     double tri = d.trow[jc];
+    int hkj = d.head[m + jc];
     // ---- the selections of trip 1
     pin.c = no_cand(0.0);
 #pragma unroll
@@ -2307,7 +2281,7 @@ __global__ void __launch_bounds__(1024) k_dual_update(SpxDev d, int gn, int ncb,
         if (gs + u * NSL > nr_cap) { c0[u] = 0; rv[u] = 0.0; }
     const int kold = rowlane ? kold_l : 1;
     if (!rowlane) { bb = 0.0; g = 0.0; }
-    if (!colth) { cb = 0.0; tri = 0.0; }
+    if (!colth) { cb = 0.0; tri = 0.0; hkj = 1; }
     TPH(3, 0);
     const double gsum = (NRHS == 2 && w == 0) ? wsum(pin.g) : 0.0;
     // ---- the entering choice (every wave)
@@ -2332,10 +2306,16 @@ __global__ void __launch_bounds__(1024) k_dual_update(SpxDev d, int gn, int ncb,
     const int tkp = d.type[kp - 1];
     const bool refkp = NRHS == 2 && d.refsp[kp - 1] != 0;
     const int knew = (r == p - 1) ? kqc : kold;
+    const int tkold_l = d.type[kold - 1];
+    const int refk_l = (NRHS == 2) ? d.refsp[kold - 1] : 0;
+    const int tknew_l = d.type[knew - 1];
+    const double lbn_l = d.lb[knew - 1], ubn_l = d.ub[knew - 1];
     const int stq_l = d.stat[qc - 1];
     const double lbq = d.lb[kqc - 1], ubq = d.ub[kqc - 1];
     const int tkq = d.type[kqc - 1];
     const double piv2 = d.trow[qc - 1];
+    const int kn = colth ? ((j == q - 1) ? kp : hkj) : 1;
+    const int ot_l = d.orig_type[kn - 1];
     if (bk && w == wa) {
         Books b;
         books_load<NRHS>(d, b, nr, kqc);
@@ -2402,11 +2382,15 @@ __global__ void __launch_bounds__(1024) k_dual_update(SpxDev d, int gn, int ncb,
         s = wsum(s);
         if (lane == 0) salpha = s;
     }
-    // operands of the row updates that depend on the choice: the row's basic
-    // variable (position arrays, loaded below), the entering one at row p
+    // operands of the row updates that depend on the choice
+    const int tkold = rowlane ? tkold_l : 0;
+    const bool refk = (NRHS == 2 && rowlane) ? refk_l != 0 : false;
+    const int tknew = rowlane ? tknew_l : 0;
+    const double lbn = rowlane ? lbn_l : 0.0, ubn = rowlane ? ubn_l : 0.0;
     // get_xN (glpspx01.js:442) of the entering variable
     const double xq_v = (stq_l == NU) ? ubq : (stq_l == NF ? 0.0 : lbq);
     const double xq = (rowlane && r == p - 1) ? xq_v : 0.0;
+    const int ot = colth ? ot_l : 0;
     sp[0][w][lane] = a;
     if (NRHS == 2) sp[NRHS - 1][w][lane] = b;
     TPH(3, 2);
@@ -2429,22 +2413,6 @@ __global__ void __launch_bounds__(1024) k_dual_update(SpxDev d, int gn, int ncb,
     }
     __syncthreads();
     TPH(3, 3);
-    // the row's basic variable by position and the column's non-basic one
-    // (coalesced; k_dual_prep and the pivot keep them), loaded by wave 0 —
-    // the only wave that reads them — here, where their latency overlaps the
-    // product-form update below (held from trip 2 they cost registers the
-    // 1024-thread block does not have)
-    int tkold_l = 0, refk_l = 0, ot_l = 0, refkq = 0;
-    double plb_l = 0.0, pub_l = 0.0;
-    if (w == 0) {
-        tkold_l = d.ptype[rc];
-        refk_l = (NRHS == 2) ? d.pref[rc] : 0;
-        plb_l = d.plb[rc];
-        pub_l = d.pub[rc];
-        refkq = (NRHS == 2) ? d.refsp[kqc - 1] : 0;        // the entering variable's, at row p
-        // the leaving variable's original type, at column q
-        ot_l = (j == q - 1) ? (int)d.orig_type[kp - 1] : (int)d.notype[jc];
-    }
     const double piv1 = salpha;
     const bool bad = fabs(piv1 - piv2) > 1e-8 * (1.0 + fabs(piv1)) ||
                      !((piv1 > 0.0 && piv2 > 0.0) || (piv1 < 0.0 && piv2 < 0.0));
@@ -2456,31 +2424,13 @@ __global__ void __launch_bounds__(1024) k_dual_update(SpxDev d, int gn, int ncb,
     const double teta = delta / tp;
     const double ti = srow[0][rl];
     const double ui = (NRHS == 2) ? srow[NRHS - 1][rl] : 0.0;
-    const bool rowp = (r == p - 1);
-    const int tkold = rowlane ? tkold_l : 0;
-    const bool refk = (NRHS == 2 && rowlane) ? refk_l != 0 : false;
-    const int tknew = rowlane ? (rowp ? tkq : tkold_l) : 0;
-    const double lbn = rowlane ? (rowp ? lbq : plb_l) : 0.0, ubn = rowlane ? (rowp ? ubq : pub_l) : 0.0;
-    const int ot = colth ? ot_l : 0;
     // the books, as soon as the pivot is committed: their straight-line
     // code runs once per launch with a cold instruction cache (≈2.5 µs of
     // fetches), so the books wave starts it here, under wave 0's row and
     // column updates and the phase-I barrier below, instead of after them.
     // Nothing later in this kernel reads what it writes (the other blocks
     // read the compact rho, not the lists, and st->nr / st->nwl in trip 1)
-    // The pivot's scalar state goes out with them, for the same reason (no
-    // other block of this kernel reads these fields)
-    if (bk && w == wa && lane == 0) {
-        books_store<NRHS>(d, sbk, kp, kq, tkp, refkp, nr, ns, rowpath, bytes_fixed);
-        st->q = q;
-        st->kq = kq;
-        st->new_dq = new_dq;
-        st->teta = teta;
-        st->pivot = tp;
-        st->pend = 1;
-        st->fxp = (tkp == FX);
-        st->rclr = (tkp == FX && refkp);
-    }
+    if (bk && w == wa && lane == 0) books_store<NRHS>(d, sbk, kp, kq, tkp, refkp, nr, ns, rowpath, bytes_fixed);
     // ---- product-form update of the entries held in registers
     {
         const bool z = (r == p - 1);
@@ -2539,12 +2489,6 @@ __global__ void __launch_bounds__(1024) k_dual_update(SpxDev d, int gn, int ncb,
             }
             const bool reset = (NRHS == 2 && refct == 1);
             cnd = chuzr_cand_v(r, knew, tknew, lbn, ubn, bb, reset ? 1.0 : g, tol_bnd);
-            if (r == p - 1) {                         // row p now holds the entering variable
-                d.ptype[r] = (signed char)tknew;
-                d.plb[r] = lbn;
-                d.pub[r] = ubn;
-                d.pref[r] = (signed char)refkq;
-            }
         }
         const Cand best = wave_best<0>(cnd);
         if (lane == 0) cand_chuzr(d)[blockIdx.x] = best;
@@ -2568,7 +2512,6 @@ __global__ void __launch_bounds__(1024) k_dual_update(SpxDev d, int gn, int ncb,
         if (j == q - 1) {
             cb = new_dq;
             st->cbar_q_old = cb_old;
-            d.notype[j] = (signed char)ot;            // column q now holds the leaving variable
         } else if (new_dq != 0.0)
             cb -= tri * new_dq;
         d.cbar[j] = cb;
@@ -2576,6 +2519,16 @@ __global__ void __launch_bounds__(1024) k_dual_update(SpxDev d, int gn, int ncb,
     }
     TPH(3, 6);
     if (phase == 1 && __syncthreads_or(badj) && threadIdx.x == 0) atomicOr(&st->dinf, 1);
+    if (lead) {
+        st->q = q;
+        st->kq = kq;
+        st->new_dq = new_dq;
+        st->teta = teta;
+        st->pivot = tp;
+        st->pend = 1;
+        st->fxp = (tkp == FX);
+        st->rclr = (tkp == FX && refkp);
+    }
     TPH(3, 7);
 }
 

@@ -158,8 +158,6 @@ struct Engine {
     // working set
     DBuf<signed char> type, orig_type, stat, refsp;
     DBuf<double> lb, ub, coef, orig_lb, orig_ub, obj;
-    DBuf<signed char> ptype, pref, notype;      // per basis position (SpxDev)
-    DBuf<double> plb, pub;
     DBuf<int> head, bind;
     DBuf<double> bbar, cbar, gamma, tcol, trow, rho, rowp, u, s, h, wcol, ys, work, r1, r2, partial;
     DBuf<DState> st;
@@ -473,7 +471,6 @@ static void engine_alloc(Engine &E, int m, int n, gk_ctx *ctx)
             place(E.awcnt, (size_t)(m + 511) / 512 + 1);
             place(E.tslots, std::max((size_t)((n + 511) / 512) * 2048, 4 * gv) + 1);
             place(E.xslots, (size_t)(m + 15) / 16 + gv + (size_t)((m + 511) / 512) * 2048 + 1);
-            place(E.ptype, m); place(E.pref, m); place(E.notype, n); place(E.plb, m); place(E.pub, m);
         };
         layout();
         if (E.arena_cap < off) {
@@ -615,7 +612,6 @@ struct Spx {
         std::memset(&d, 0, sizeof(d));      // compared bytewise by the graph cache
         d.m = m; d.n = n; d.A = E->mat();
         d.type = E->type.p; d.orig_type = E->orig_type.p; d.stat = E->stat.p; d.refsp = E->refsp.p;
-        d.ptype = E->ptype.p; d.pref = E->pref.p; d.notype = E->notype.p; d.plb = E->plb.p; d.pub = E->pub.p;
         d.lb = E->lb.p; d.ub = E->ub.p; d.coef = E->coef.p; d.orig_lb = E->orig_lb.p; d.orig_ub = E->orig_ub.p;
         d.obj = E->obj.p; d.head = E->head.p; d.bind = E->bind.p;
         d.bbar = E->bbar.p; d.cbar = E->cbar.p; d.gamma = E->gamma.p;

@@ -147,14 +147,6 @@ struct SpxDev {
     unsigned long long *tslots;              // per-block end stamps of the pivot-row kernel
     unsigned long long *xslots;              // per-block exit stamps of the commit / update kernel
     unsigned long long *trace;               // profiling only: per-kernel, per-block entry / exit clock
-    // attributes of the variable at each basis position (dual batches): its
-    // type, bounds and reference-space flag by row i (head[i]), the original
-    // type of the non-basic variable by column j (head[m + j]) — coalesced
-    // reads where the pivot kernels would otherwise gather through head[];
-    // written by k_dual_prep at every batch start, kept by the pivot at
-    // positions p and q
-    signed char *ptype, *pref, *notype;
-    double *plb, *pub;
 };
 constexpr int TRACE_KERNELS = 8, TRACE_BLOCKS = 2048;   // trace[(kid * TRACE_BLOCKS + block) * 2 + {0, 1}]
 constexpr int TRACE_PHASES = 8;   // then phase stamps of wave 0: [TRACE_KERNELS * TRACE_BLOCKS * 2 + (kid * TRACE_BLOCKS + block) * 8 + ph]
