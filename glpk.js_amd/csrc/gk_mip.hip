@@ -1761,6 +1761,14 @@ extern "C" int gk_ios_driver_sharded(gk_ctx *ctx, gk_mip *mip, const gk_iocp *pa
     // to idle ranks (the collective is called by idle ranks too, until no
     // rank has work left)
     bool split_done = (size == 1), timed_out = false, gap_hit = false;
+    // batch width before the first incumbent (GK_BNB_PRECAP; 0: no limit).
+    // 8 measured best on gap (profiles/r03_bnb_precap_sweep.txt): 495 node
+    // LPs against 3959 uncapped (the reference: 196) at the same wall time
+    static const int pre_cap_env = [] {
+        const char *e = std::getenv("GK_BNB_PRECAP");
+        return e ? std::atoi(e) : 8;
+    }();
+    const int pre_cap = pre_cap_env > 0 ? pre_cap_env : 1 << 30;
     int since_sync = 0;
     // show_progress (glpios03.js:2-48) through the context's report hook, and
     // the relative gap of ios_relative_gap (glpios01.js:842): both need the
@@ -1878,21 +1886,25 @@ extern "C" int gk_ios_driver_sharded(gk_ctx *ctx, gk_mip *mip, const gk_iocp *pa
         if (inflight[cur]) { process(bf); inflight[cur] = 0; }
         if (S.err) break;
         bf.ents.clear();
+        // until the first incumbent prunes, a wide batch is mostly nodes a
+        // sequential walk never solves (the reference dives for an incumbent
+        // first): the batch widens to BMAX once one exists
+        const int cap = S.have ? S.BMAX : std::min(S.BMAX, pre_cap);
         {
             size_t k = 0;
-            for (; k < S.probeq.size() && (int)bf.ents.size() < S.BMAX; k++) bf.ents.push_back(S.probeq[k]);
+            for (; k < S.probeq.size() && (int)bf.ents.size() < cap; k++) bf.ents.push_back(S.probeq[k]);
             S.probeq.erase(S.probeq.begin(), S.probeq.begin() + k);
         }
         {
             std::vector<NodeRec> keep;
             for (const NodeRec &nd : S.dive) {
                 if (!S.hopeful(nd.bound)) { pool.release(nd.slot); continue; }
-                if ((int)bf.ents.size() < S.BMAX) bf.ents.push_back(Entry{0, nd, 0, 0, 0});
+                if ((int)bf.ents.size() < cap) bf.ents.push_back(Entry{0, nd, 0, 0, 0});
                 else S.push_open(nd);
             }
             S.dive.clear();
         }
-        while (!S.open.empty() && (int)bf.ents.size() < S.BMAX) {
+        while (!S.open.empty() && (int)bf.ents.size() < cap) {
             const NodeRec nd = S.pop_open();
             if (!S.hopeful(nd.bound)) { pool.release(nd.slot); continue; }
             bf.ents.push_back(Entry{0, nd, 0, 0, 0});
