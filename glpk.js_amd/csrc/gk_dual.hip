@@ -406,12 +406,15 @@ __device__ __forceinline__ int dual_bad(const SpxDev &d, int k, double cb, doubl
 // batch start: chuzr candidates (one per 64 rows) and the phase-I check of
 // the current state; the candidate slots [4 ceil(m / 256), gm) of a finer
 // layout (k_dual_update: one per 16 rows) are cleared
-__global__ void __launch_bounds__(256) k_dual_prep(SpxDev d, int gm)
+__global__ void __launch_bounds__(256) k_dual_prep(SpxDev d, int gm, int panel)
 {
     DState *st = d.st;
     const int m = d.m, n = d.n;
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     for (int s = 4 * ((m + 255) / 256) + i; s < gm; s += gridDim.x * blockDim.x) cand_chuzr(d)[s] = no_cand(0.0);
+    // a batch without the MFMA panel (gk_panel.hip) changes the basis without
+    // updating it: the panel is kept only across batches that maintain it
+    if (i == 0 && !panel) st->pvalid = 0;
     const bool reset = (st->pricing == PT_PSE && st->refct == 0);
     if ((int)blockIdx.x * 256 < m) {
         Cand c = no_cand(0.0);
@@ -2590,6 +2593,7 @@ DualPlan dual_plan(const SpxDev &d, int nr_max, int nwl_max, int pse, int rigoro
         pl.gm = rows_blocks;
     }
     pl.awone = (pse && d.A.dense && nwl_max <= 512) ? std::max(nwl_max, 1) : 0;
+    pl.panel = panel_wanted(d, pl);
     return pl;
 }
 
@@ -2615,7 +2619,7 @@ static double bytes_fixed(const SpxDev &d) { return 96.0 * ((double)d.m + d.n); 
 void dual_batch_begin(hipStream_t s, const SpxDev &d, const DualPlan &pl)
 {
     hipLaunchKernelGGL(k_dual_prep, dim3(cdiv(std::max(d.m, d.n), 256)), dim3(256), 0, s, d,
-                       std::max(pl.gm, 4 * cdiv(d.m, 256)));
+                       std::max(pl.gm, 4 * cdiv(d.m, 256)), pl.panel);
 }
 
 // blocks of the kernel that ends a pivot (their exit stamps: xslots)
@@ -2695,8 +2699,11 @@ void dual_iteration2(hipStream_t s, const SpxDev &d, const DualPlan &pl, hipEven
             hipLaunchKernelGGL(k_dual_top, dim3(1), dim3(TOP_WG), 0, s, d, pl.rowpath, pl.nr_cap);
         if (pl.rigorous) refine_rho_dev(s, d);
         if (ev0) (void)hipEventRecord(ev0, s);
-        colpass_gated(s, d.A, CP_TROW, m, n, d.head, d.stat, d.coef, nullptr, d.rho, nullptr, d.trow, nullptr,
-                      &d.st->trow_max_bits, d.st, 0);
+        if (pl.panel)   // the row of p from the MFMA panel (gk_panel.hip)
+            panel_trow(s, d, pl);
+        else
+            colpass_gated(s, d.A, CP_TROW, m, n, d.head, d.stat, d.coef, nullptr, d.rho, nullptr, d.trow, nullptr,
+                          &d.st->trow_max_bits, d.st, 0);
         if (ev1) (void)hipEventRecord(ev1, s);
         hipLaunchKernelGGL(k_trow_finish, dim3(gv), dim3(256), 0, s, d, pl.pse);
     }
@@ -2736,6 +2743,7 @@ void dual_iteration2(hipStream_t s, const SpxDev &d, const DualPlan &pl, hipEven
     const int nvb = gv;
     hipLaunchKernelGGL(k_dual_commit, dim3(nvb + tiles_m * pl.uchunks), dim3(256), 0, s, d, pl.pse, nvb, tiles_m,
                        pl.lpsu, pl.rowpath, bytes_fixed(d));
+    if (pl.panel) panel_update(s, d, pl);
 }
 
 // ---------------------------------------------------------------------------

@@ -169,6 +169,10 @@ struct Engine {
     DBuf<char> upstage;                         // device side of the coalesced uploads
     DBuf<int> xlist;                            // eval_cbar: basic slacks with a nonzero cost (primal phase I)
     DBuf<unsigned long long> tslots, xslots;
+    // MFMA pricing panel (gk_panel.hip), dense A only, sized for PANEL_MAX rows
+    DBuf<double> pnl, pnl_src;
+    DBuf<int> pslot, ppos;
+    int pnl_m = -1, pnl_n = -1;
     std::vector<GraphEntry> graphs;
     unsigned long long graph_clock = 0;
     int kbatch = 8;                           // batch length carried across calls
@@ -233,6 +237,7 @@ struct Engine {
         rlist.release(); rpos.release(); rho_idx.release(); rho_val.release();
         gpart.release(); awcnt.release(); tslots.release(); xslots.release(); trace.release(); wlist.release(); wpos.release(); cand.release();
         awpart.release();
+        pnl.release(); pnl_src.release(); pslot.release(); ppos.release();
         type.release(); orig_type.release(); stat.release(); refsp.release();
         lb.release(); ub.release(); coef.release(); orig_lb.release(); orig_ub.release(); obj.release();
         head.release(); bind.release();
@@ -624,6 +629,10 @@ struct Spx {
         d.gpart = E->gpart.p;
         d.wlist = E->wlist.p; d.wpos = E->wpos.p; d.cand = E->cand.p;
         d.awpart = E->awpart.p; d.awpart_cap = (size_t)AW_SPLITS * m; d.awcnt = E->awcnt.p;
+        if (E->pnl_m == m && E->pnl_n == n) {
+            d.pnl = E->pnl.p; d.pnl_src = E->pnl_src.p; d.pslot = E->pslot.p; d.ppos = E->ppos.p;
+            d.ldp = (n + 7) & ~7;
+        }
         // the roofline stamps (per-block exit clocks, kernel spans, algorithmic
         // bytes) cost stores and a reduction on the critical path of every
         // pivot: they run only while a profiling mode is on (gk_bfd_profile)
@@ -891,6 +900,7 @@ struct Spx {
     {
         pull();
         cbar_ok = bbar_ok = false;
+        hs.pvalid = 0;                          // the pricing panel is refilled from the fresh inverse
         BasisSplit bs;
         if (!split_from_head(m, head.data(), bs)) {
             fact_ret = 1;                       // BFD_ESING
@@ -1490,6 +1500,19 @@ int Spx::batch(int K, int rigorous)
     hs.dinf = 0;
     hs.pend = 0;
     push_state();
+    if (dual && E->dense && (E->pnl_m != m || E->pnl_n != n)) {
+        // the pricing panel's buffers; no slot is valid until a fill (pslot
+        // entries are validated against ppos)
+        const int ldp = (n + 7) & ~7;
+        E->pnl.ensure((size_t)PANEL_MAX * ldp);
+        E->pnl_src.ensure((size_t)PANEL_MAX * m);
+        E->pslot.ensure(m);
+        E->ppos.ensure(PANEL_MAX);
+        HIPCHK(hipMemsetAsync(E->pslot.p, 0xff, (size_t)m * sizeof(int), s));
+        HIPCHK(hipMemsetAsync(E->ppos.p, 0, PANEL_MAX * sizeof(int), s));
+        E->pnl_m = m;
+        E->pnl_n = n;
+    }
     SpxDev d = dev();
     const int pse = (parm->pricing == PT_PSE);
     if (dual) {
@@ -1543,6 +1566,8 @@ int Spx::batch(int K, int rigorous)
     f->stats.upd_dev_ms = hs.upd_ticks / (double)ctx->wall_khz;
     f->stats.upd_dev_launches = (long long)hs.upd_n;
     f->stats.upd_bytes = hs.bytes_upd;
+    f->stats.panel_hits = (long long)hs.phits;
+    f->stats.panel_refills = (long long)hs.pmisses;
     if (dual && (E->prof == 1 || E->prof == 2)) {
         for (int t = 0; t < hs.npiv; t++) {
             float ms = 0.f;

@@ -71,6 +71,11 @@ struct DState {
     unsigned long long tk_upd0, tk_pad3;    // entry of the last k_dual_update (block 0)
     double upd_ticks, upd_n;                // k_dual_update spans (entry of block 0 to the last block exit)
     double bytes_upd, upd_tol;              // algorithmic bytes of the k_dual_update launches; bfcp upd_tol
+    // MFMA panel pricing (gk_panel.hip): rows in the panel, slot of this
+    // pivot's row, 1 when this pivot refilled the panel, 0 until the first
+    // fill of the batch; hits and refills so far
+    int pk, pcur, pmiss, pvalid;
+    double phits, pmisses;
 };
 
 // ---- dense GEMV helpers ---------------------------------------------------
@@ -147,7 +152,16 @@ struct SpxDev {
     unsigned long long *tslots;              // per-block end stamps of the pivot-row kernel
     unsigned long long *xslots;              // per-block exit stamps of the commit / update kernel
     unsigned long long *trace;               // profiling only: per-kernel, per-block entry / exit clock
+    // MFMA panel pricing (gk_panel.hip): PANEL_MAX tableau rows over the
+    // structural columns (pnl[t * ldp + j]), the rows of inv(B) they were
+    // formed from (pnl_src[t * m + i]), the basis position of every slot
+    // (ppos, 1-based) and the slot of every position (pslot, validated
+    // against ppos)
+    double *pnl, *pnl_src;
+    int *pslot, *ppos;
+    int ldp;
 };
+constexpr int PANEL_MAX = 32;
 constexpr int TRACE_KERNELS = 8, TRACE_BLOCKS = 2048;   // trace[(kid * TRACE_BLOCKS + block) * 2 + {0, 1}]
 constexpr int TRACE_PHASES = 8;   // then phase stamps of wave 0: [TRACE_KERNELS * TRACE_BLOCKS * 2 + (kid * TRACE_BLOCKS + block) * 8 + ph]
 constexpr size_t TRACE_LEN = (size_t)TRACE_KERNELS * TRACE_BLOCKS * (2 + TRACE_PHASES);
@@ -170,6 +184,7 @@ struct DualPlan {
     int ugm, uwaves;              // k_dual_update: inv(B) entries per thread, waves per block
     int gm;                       // chuzr candidate slots (4 per 256 rows, or one per 16 rows with fupd)
     int awone;                    // dense A w in one pass over 64-row tiles: the cap of nwl (0: split path)
+    int panel;                    // rows of the MFMA pricing panel (0: the pivot row is a column pass over A)
 };
 void dual_batch_begin(hipStream_t s, const SpxDev &d, const DualPlan &pl);
 void dual_batch_end(hipStream_t s, const SpxDev &d, const DualPlan &pl);
@@ -193,6 +208,12 @@ void scatter_segments(hipStream_t s, const char *src, const UpSeg *segs, int nse
 // dual, dense A: CP_CBAR / CP_RESID of eval_cbar over the rows of AT in rlist
 void rowpass_pi(hipStream_t s, const SpxDev &d, int mode, int nr, const double *pi, const double *h, double *out,
                 const int *extra, int nextra);
+// MFMA panel pricing (gk_panel.hip), column-pass path on dense A: the chosen
+// row from the panel (refilled on a miss) in place of the column pass, and
+// the panel's update after the commit; panel_wanted: the plan's panel size
+int panel_wanted(const SpxDev &d, const DualPlan &pl);
+void panel_trow(hipStream_t s, const SpxDev &d, const DualPlan &pl);
+void panel_update(hipStream_t s, const SpxDev &d, const DualPlan &pl);
 // timing hook: the row-path pivot-row kernel alone (returns algorithmic bytes)
 double launch_trow_rows(hipStream_t s, const SpxDev &d, const DualPlan &pl, int ns);
 // y = inv(B) x and y = inv(B)' x over the nr dense columns of rlist and the

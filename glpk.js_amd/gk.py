@@ -99,7 +99,8 @@ class SpxStats(C.Structure):
                 ("trow_dev_ms", C.c_double), ("trow_dev_launches", C.c_longlong), ("trow_dev_ms_b", C.c_double),
                 ("trow_dev_ms_r", C.c_double), ("trow_dev_launches_r", C.c_longlong),
                 ("upd_dev_ms", C.c_double), ("upd_dev_launches", C.c_longlong), ("upd_bytes", C.c_double),
-                ("resident", C.c_int), ("evals_skipped", C.c_int)]
+                ("resident", C.c_int), ("evals_skipped", C.c_int),
+                ("panel_hits", C.c_longlong), ("panel_refills", C.c_longlong)]
 
 
 _lib = None

@@ -40,7 +40,7 @@
 extern "C" {
 #endif
 
-#define GK_ABI_VERSION 5
+#define GK_ABI_VERSION 6
 #include <stddef.h>
 #define GK_EABI (-1)          /* contract violation; see gk_last_error() */
 
@@ -194,6 +194,8 @@ typedef struct {
     double upd_bytes;           /* (profiling) algorithmic bytes of every k_dual_update launch */
     int resident;               /* 1: the call found its working set resident (no re-upload) */
     int evals_skipped;          /* eval_cbar / eval_bbar calls whose result was already resident */
+    long long panel_hits;       /* dual pivots whose pivot row came from the MFMA pricing panel */
+    long long panel_refills;    /* MFMA refills of the panel (one pass over A for up to 32 rows) */
 } gk_spx_stats;
 void gk_bfd_last_stats(const gk_bfd *bfd, gk_spx_stats *st);
 /* record HIP events around the pivot-row kernel of every dual pivot (benches) */

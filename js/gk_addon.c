@@ -560,6 +560,8 @@ static napi_value js_stats(napi_env env, napi_callback_info info)
     set_num(env, o, "batches", (double)st.batches);
     set_num(env, o, "seconds_total", st.seconds_total);
     set_num(env, o, "bytes_pivots", st.bytes_pivots);
+    set_num(env, o, "panel_hits", (double)st.panel_hits);
+    set_num(env, o, "panel_refills", (double)st.panel_refills);
     return o;
 }
 
