@@ -1918,6 +1918,11 @@ __global__ void __launch_bounds__(256) k_dual_commit(SpxDev d, int pse, int nvb,
                 atomicOr(&st->refact_pending, 1);
                 atomicAdd(&st->echk, 1);
             }
+            const double gr = (in_m && i != p - 1) ? fabs(ti) / fabs(tp) : 0.0;
+            if (__any(gr > 100.0)) {
+                const double gw = wmax(gr);
+                if ((threadIdx.x & 63) == 0) atomicMax(&st->grow_bits, dbits(gw));
+            }
         }
         if (phase == 1) {
             const double tol = tol_dj;
@@ -2506,6 +2511,11 @@ __global__ void __launch_bounds__(1024) k_dual_update(SpxDev d, int gn, int ncb,
             atomicOr(&st->refact_pending, 1);
             atomicAdd(&st->echk, 1);
         }
+        const double gr = (rowlane && r != p - 1) ? fabs(ti) / fabs(tp) : 0.0;
+        if (__any(gr > 100.0)) {
+            const double gw = wmax(gr);
+            if (lane == 0) atomicMax(&st->grow_bits, dbits(gw));
+        }
     }
     TPH(3, 5);
     // ---- columns: update_cbar (:1020), check_feas of phase I (:1296)
@@ -2594,6 +2604,7 @@ DualPlan dual_plan(const SpxDev &d, int nr_max, int nwl_max, int pse, int rigoro
     }
     pl.awone = (pse && d.A.dense && nwl_max <= 512) ? std::max(nwl_max, 1) : 0;
     pl.panel = panel_wanted(d, pl);
+    pl.panel_age = pl.panel ? panel_age_max() : 0;
     return pl;
 }
 

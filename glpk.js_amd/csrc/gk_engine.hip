@@ -584,6 +584,13 @@ static void engine_upload_matrix(gk_bfd *f, const gk_lp *lp)
     E.a_version = lp->a_version;
 }
 
+static double bits_double(unsigned long long b)
+{
+    double v;
+    std::memcpy(&v, &b, sizeof v);
+    return v;
+}
+
 // ---------------------------------------------------------------------------
 // the simplex driver
 // ---------------------------------------------------------------------------
@@ -1204,6 +1211,7 @@ struct Spx {
     int upd_cap = 0, upd_floor = 0;
     bool drift_armed = false;
     int drift_upd = 0;
+    double drift_grow = 0.0;
     std::vector<double> drift_ref;
     void drift_arm(const std::vector<double> &v, int st)
     {
@@ -1213,20 +1221,25 @@ struct Spx {
         if (!drift_armed) return;
         drift_ref = v;
         drift_upd = hs.upd_cnt;
+        drift_grow = hs.grow_bits ? bits_double(hs.grow_bits) : 0.0;
     }
     void drift_adapt(const std::vector<double> &fresh, int cnt, double tol)
     {
         if (!drift_armed) return;
         drift_armed = false;
+        // dual: a fixed non-basic variable (NS: every DB / FX one in phase I,
+        // glpspx02.js:1340-1353) has trow = 0, so its reduced cost is never
+        // updated and is no part of the chain's drift (check_stab skips it)
         double D = 0.0;
-        for (int j = 1; j <= cnt; j++) D = std::max(D, std::fabs(fresh[j] - drift_ref[j]));
+        for (int j = 1; j <= cnt; j++)
+            if (!dual || stat[j] != NS) D = std::max(D, std::fabs(fresh[j] - drift_ref[j]));
         int lim = f->upd_lim_adapt > 0 ? f->upd_lim_adapt : upd_cap;
         if (D > 0.05 * tol) lim = std::max(upd_floor, std::min(lim, drift_upd) / 2);
         else if (D < 0.005 * tol && drift_upd >= lim) lim = std::min(upd_cap, 2 * lim);
         static const bool log = std::getenv("GK_DRIFT_LOG") != nullptr;
         if (log)
-            fprintf(stderr, "[gk drift] %s it %d: %d updates, drift %.3e (tol %.1e) -> interval %d (growth checks %d)\n",
-                    dual ? "dual" : "primal", hs.it_cnt, drift_upd, D, tol, lim, hs.echk);
+            fprintf(stderr, "[gk drift] %s it %d: %d updates, drift %.3e (tol %.1e) -> interval %d (growth checks %d, "
+                    "max growth %.3e)\n", dual ? "dual" : "primal", hs.it_cnt, drift_upd, D, tol, lim, hs.echk, drift_grow);
         f->upd_lim_adapt = lim;
         hs.upd_lim = lim;
     }
@@ -1696,7 +1709,7 @@ int Spx::run_dual()
             }
             binv_st = 1;
             bbar_st = cbar_st = 0;
-            hs.upd_cnt = 0; hs.refact_pending = 0;
+            hs.upd_cnt = 0; hs.refact_pending = 0; hs.grow_bits = 0;
         }
         hs.binv_fresh = (binv_st == 1);
         if (cbar_st == 0) {
@@ -1713,6 +1726,18 @@ int Spx::run_dual()
                 bbar_st = 0;
             }
             if (dual_check_stab(P->tol_dj) != 0) {
+                static const bool dlog = std::getenv("GK_DRIFT_LOG") != nullptr;
+                if (dlog) {
+                    double worst = 0.0;
+                    int cnt = 0;
+                    for (int j = 1; j <= n; j++) {
+                        const double v = (stat[j] == NL) ? -cbar[j] : (stat[j] == NU) ? cbar[j]
+                                         : (stat[j] == NF) ? std::fabs(cbar[j]) : 0.0;
+                        if (v > P->tol_dj) { cnt++; worst = std::max(worst, v); }
+                    }
+                    fprintf(stderr, "[gk drift] dual it %d: check_stab failed, %d reduced costs off by up to %.3e "
+                            "(%d updates since the last re-inversion)\n", hs.it_cnt, cnt, worst, hs.upd_cnt);
+                }
                 report_msg(GK_MSG_INSTAB, 1, 2);
                 if (P->meth == 2) {            // GLP_DUALP
                     store_sol(1, 1, 0);
@@ -1891,7 +1916,7 @@ int Spx::run_primal()
             }
             binv_st = 1;
             bbar_st = cbar_st = 0;
-            hs.upd_cnt = 0; hs.refact_pending = 0;
+            hs.upd_cnt = 0; hs.refact_pending = 0; hs.grow_bits = 0;
         }
         hs.binv_fresh = (binv_st == 1);
         if (bbar_st == 0) {

@@ -63,8 +63,11 @@ struct DState {
     unsigned long long trow_max_bits, tcol_max_bits;
     int kp, kq, fxp, rclr;                  // dual: leaving / entering variable of the pivot; x_kp fixed;
                                             // refsp[kp] to clear at change_basis
-    int kq1, echk, pad3, pad4;              // variable of the pass-1 choice; echk: growth re-inversions requested
-    double alfa1, pad5;                     // |trow| of the pass-1 choice
+    int kq1, echk, page, pad4;              // variable of the pass-1 choice; echk: growth re-inversions requested;
+                                            // page: product-form updates the pricing panel's rows went through
+    double alfa1;                           // |trow| of the pass-1 choice
+    unsigned long long grow_bits;           // max |tcol_i / alpha_p| (as double bits) of the product-form updates since
+                                            // the last re-inversion, recorded when it exceeds 100
     unsigned long long tk_prev, tk_pad2;    // last block exit of the kernel before the pivot-row kernel
     double trow_ticks_r, trow_nr;           // pivot-row kernels, previous kernel's last exit to their last
                                             // exit (the bracket of a profiler's per-dispatch record)
@@ -185,6 +188,7 @@ struct DualPlan {
     int gm;                       // chuzr candidate slots (4 per 256 rows, or one per 16 rows with fupd)
     int awone;                    // dense A w in one pass over 64-row tiles: the cap of nwl (0: split path)
     int panel;                    // rows of the MFMA pricing panel (0: the pivot row is a column pass over A)
+    int panel_age;                // product-form updates a panel row may go through before a refill
 };
 void dual_batch_begin(hipStream_t s, const SpxDev &d, const DualPlan &pl);
 void dual_batch_end(hipStream_t s, const SpxDev &d, const DualPlan &pl);
@@ -212,6 +216,7 @@ void rowpass_pi(hipStream_t s, const SpxDev &d, int mode, int nr, const double *
 // row from the panel (refilled on a miss) in place of the column pass, and
 // the panel's update after the commit; panel_wanted: the plan's panel size
 int panel_wanted(const SpxDev &d, const DualPlan &pl);
+int panel_age_max();
 void panel_trow(hipStream_t s, const SpxDev &d, const DualPlan &pl);
 void panel_update(hipStream_t s, const SpxDev &d, const DualPlan &pl);
 // timing hook: the row-path pivot-row kernel alone (returns algorithmic bytes)

@@ -42,16 +42,20 @@ namespace gk {
 
 // the slots for this pivot: a hit, or a refill with p in slot 0 and the
 // next best per-wave chuzr candidates (better<0>: r^2 / gamma, ties by
-// position) in slots 1.., ranked by counting (gm <= 1024 candidates in LDS)
-__global__ void __launch_bounds__(256) k_panel_pick(SpxDev d, int gm, int cap)
+// position) in slots 1.., ranked by counting (gm <= 1024 candidates in LDS).
+// A panel whose rows went through `age_max` product-form updates is refilled
+// whatever the hit: its rows are then no older than the rows of a
+// Forrest-Tomlin factor refreshed every nfs_max = 100 updates (glpspx02's
+// default), so the drift of a served row stays that of a freshly formed one
+__global__ void __launch_bounds__(256) k_panel_pick(SpxDev d, int gm, int cap, int age_max)
 {
     __shared__ Cand cs[1024];
     __shared__ int nval;
     DState *st = d.st;
-    const int stop = st->stop, p = st->p, valid = st->pvalid, pk = st->pk;
+    const int stop = st->stop, p = st->p, valid = st->pvalid, pk = st->pk, age = st->page;
     if (stop || p <= 0) return;
     const int sl = d.pslot[p - 1];
-    const bool hit = valid && sl >= 0 && sl < pk && d.ppos[sl] == p;
+    const bool hit = valid && age < age_max && sl >= 0 && sl < pk && d.ppos[sl] == p;
     if (hit) {
         if (threadIdx.x == 0) {
             st->pcur = sl;
@@ -84,6 +88,7 @@ __global__ void __launch_bounds__(256) k_panel_pick(SpxDev d, int gm, int cap)
         d.ppos[0] = p;
         d.pslot[p - 1] = 0;
         st->pk = 1 + min(nval, cap - 1);
+        st->page = 0;
         st->pcur = 0;
         st->pmiss = 1;
         st->pvalid = 1;
@@ -211,6 +216,7 @@ __global__ void __launch_bounds__(256) k_panel_update(SpxDev d)
     const double tp = st->pivot;
     const int n = d.n;
     const int j = blockIdx.x * 256 + threadIdx.x;
+    if (j == 0) d.st->page = st->page + 1;
     if (j >= n) return;
     const size_t ldp = (size_t)d.ldp;
     const double gp = d.pnl[(size_t)cur * ldp + j];
@@ -240,10 +246,18 @@ int panel_wanted(const SpxDev &d, const DualPlan &pl)
     return k;
 }
 
+// updates a panel row may go through before the panel is refilled
+// (GK_PANEL_AGE, default 100; read at every plan, as GK_PANEL)
+int panel_age_max()
+{
+    const char *e = std::getenv("GK_PANEL_AGE");
+    return e ? std::max(1, std::atoi(e)) : 100;
+}
+
 void panel_trow(hipStream_t s, const SpxDev &d, const DualPlan &pl)
 {
     const int m = d.m, n = d.n;
-    hipLaunchKernelGGL(k_panel_pick, dim3(1), dim3(256), 0, s, d, 4 * cdiv(m, 256), pl.panel);
+    hipLaunchKernelGGL(k_panel_pick, dim3(1), dim3(256), 0, s, d, 4 * cdiv(m, 256), pl.panel, pl.panel_age);
     hipLaunchKernelGGL(k_panel_gather, dim3(cdiv(m, 256), pl.panel), dim3(256), 0, s, d);
     hipLaunchKernelGGL(k_panel_mfma, dim3(cdiv(n, 32)), dim3(256), 0, s, d);
     hipLaunchKernelGGL(k_panel_trow, dim3(cdiv(n, 256)), dim3(256), 0, s, d);

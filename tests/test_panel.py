@@ -37,7 +37,7 @@ DENSE_DUAL = [c for c in LP_CASES if _dense_dual(c)]
 
 @pytest.fixture
 def panel_env():
-    keys = ("GK_PANEL", "GK_PANEL_MIN_M")
+    keys = ("GK_PANEL", "GK_PANEL_MIN_M", "GK_PANEL_AGE")
     old = {k: os.environ.get(k) for k in keys}
 
     def set_(**kv):
@@ -56,10 +56,12 @@ def test_panel_fixture_coverage():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("rows", [32, 2])
+@pytest.mark.parametrize("rows,age", [(32, 100), (2, 100), (32, 3)], ids=["32", "2", "32-age3"])
 @pytest.mark.parametrize("path,run_index", DENSE_DUAL)
-def test_gpu_panel_forced_matches_reference(gpu_ctx, panel_env, rows, path, run_index):
-    panel_env(GK_PANEL=rows, GK_PANEL_MIN_M=0)
+def test_gpu_panel_forced_matches_reference(gpu_ctx, panel_env, rows, age, path, run_index):
+    """age 3: the panel is refilled whenever its rows went through three
+    product-form updates, hit or not"""
+    panel_env(GK_PANEL=rows, GK_PANEL_MIN_M=0, GK_PANEL_AGE=age)
     d = load_golden(path)
     run = d["runs"][run_index]
     P = gk.GkProblem(gpu_ctx, problems.from_fixture(d))
@@ -77,11 +79,12 @@ def test_gpu_panel_forced_matches_reference(gpu_ctx, panel_env, rows, path, run_
 
 
 @pytest.mark.gpu
-def test_gpu_panel_used_on_forced_fixture(gpu_ctx, panel_env):
+@pytest.mark.parametrize("age", [100, 1])
+def test_gpu_panel_used_on_forced_fixture(gpu_ctx, panel_env, age):
     """the forced panel really serves the pivot rows (hits and refills
-    counted by the device)"""
-    panel_env(GK_PANEL=32, GK_PANEL_MIN_M=0)
-    used = 0
+    counted by the device); at age 1 every pivot refills"""
+    panel_env(GK_PANEL=32, GK_PANEL_MIN_M=0, GK_PANEL_AGE=age)
+    used = hits = 0
     for c in DENSE_DUAL:
         d = load_golden(c.values[0])
         run = d["runs"][c.values[1]]
@@ -89,7 +92,10 @@ def test_gpu_panel_used_on_forced_fixture(gpu_ctx, panel_env):
         gk.glp_simplex(P, gk.SMCP(**run["opts"]))
         st = P.stats()
         used += st.panel_hits + st.panel_refills
+        hits += st.panel_hits
     assert used > 0
+    if age == 1:
+        assert hits == 0
 
 
 @pytest.mark.gpu
