@@ -334,19 +334,7 @@ def main():
                "port_over_reference_node": PORT_OVER_NODE,
                "reference_node_pivots_per_s": 9.4}
 
-    if not args.no_extra:
-        if world == 1:
-            del P
-            extra = run_extra(gk, problems, ctx, prob)
-        else:
-            # B&B sharded over all ranks (subtree per GPU) through the
-            # library's own collective (gk_comm: RCCL over xGMI between the
-            # ranks' devices), every epoch's exchange inside the C driver
-            port = int(os.environ.get("MASTER_PORT", "29500")) + 7
-            comm = gk.Comm(ctx, rank, world, f"{os.environ.get('MASTER_ADDR', '127.0.0.1')}:{port}")
-            extra = run_bnb(gk, problems, ctx, names=("c5s_12x30",), comm=comm)
-            extra["bnb_comm_backend"] = {1: "tcp", 2: "rccl"}.get(comm.backend, comm.backend)
-
+    line = None
     if rank == 0:
         line = {
             "metric": "simplex pivots/s (dual, C3 dense 4096x16384 fp64)",
@@ -375,11 +363,49 @@ def main():
                        "batches": int(st.batches), "host_syncs": int(st.host_syncs),
                        "restarts": restarts[0], "resident_calls": resident, "evals_skipped": skipped,
                        "kernels": kern},
-            "extra": extra,
+            "extra": {},
         }
+
+    if not args.no_extra:
+        if world == 1:
+            del P
+            extra = run_extra(gk, problems, ctx, prob)
+        else:
+            # B&B sharded over all ranks (subtree per GPU) through the
+            # library's own collective (gk_comm: RCCL over xGMI between the
+            # ranks' devices), every epoch's exchange inside the C driver.
+            # The headline is measured by now: a failure of this context leg
+            # is reported in the line, and a watchdog prints the line and
+            # ends every rank should the collective hang
+            import threading
+
+            def _expire():
+                if rank == 0:
+                    line["extra"] = {"error": f"multi-rank B&B leg exceeded {EXTRA_MULTI_S:.0f} s"}
+                    print(json.dumps(line), flush=True)
+                sys.stderr.flush()
+                os._exit(0)
+
+            dog = threading.Timer(EXTRA_MULTI_S, _expire)
+            dog.daemon = True
+            dog.start()
+            try:
+                port = int(os.environ.get("MASTER_PORT", "29500")) + 7
+                comm = gk.Comm(ctx, rank, world, f"{os.environ.get('MASTER_ADDR', '127.0.0.1')}:{port}")
+                extra = run_bnb(gk, problems, ctx, names=("c5s_12x30",), comm=comm)
+                extra["bnb_comm_backend"] = {1: "tcp", 2: "rccl"}.get(comm.backend, comm.backend)
+            except Exception as e:            # noqa: BLE001 (reported, the headline stands)
+                extra = {"error": f"multi-rank B&B leg: {type(e).__name__}: {e}"}
+            dog.cancel()
+
+    if rank == 0:
+        line["extra"] = extra
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+EXTRA_MULTI_S = 240.0      # the multi-rank B&B leg's watchdog
 
 
 def run_extra(gk, problems, ctx, c3):

@@ -1412,10 +1412,14 @@ void Spx::init()
         }
     ABI_REQUIRE(k == n, "gk_spx: basis header inconsistent with statuses (%d non-basic, n = %d)", k, n);
     for (int kk = 1; kk <= m + n; kk++) bind[head[kk]] = kk;
+    static const bool ilog = std::getenv("GK_INIT_LOG") != nullptr;      // host time split of init (diagnostics)
+    const double t_build = now_s();
     engine_alloc(*E, m, n, ctx);
     if (f->ext_upd) f->valid = 0;    // unit columns may be inexact after external updates
     // the working set the last call left on the device, when it is this one
+    const double t_alloc = now_s();
     const bool keep = resident_match();
+    const double t_match = now_s();
     Engine::Resident &R = E->res;
     R.ok = false;
     begin_up();
@@ -1433,6 +1437,10 @@ void Spx::init()
     }
     up(E->head, head, mn - 1); up(E->bind, bind, mn - 1); up(E->stat, stat, n);
     flush_up();
+    if (ilog)
+        fprintf(stderr, "[gk init] build %.1f us, alloc %.1f us, resident check %.1f us (%s), uploads %.1f us\n",
+                1e6 * (t_build - t0), 1e6 * (t_alloc - t_build), 1e6 * (t_match - t_alloc), keep ? "kept" : "rebuilt",
+                1e6 * (now_s() - t_match));
     if (keep) {
         // the dense-column list of inv(B) stays as the pivots left it (its
         // order is the order of the sums over it); the PSE reference space
