@@ -2209,6 +2209,7 @@ __global__ void __launch_bounds__(1024) k_dual_update(SpxDev d, int gn, int ncb,
     constexpr int SL = 64 / RPB;
     __shared__ double sp[NRHS][16][64];
     __shared__ double srow[NRHS][RPB];
+    __shared__ double sub[RPB];
     __shared__ double salp[16 * SL];
     __shared__ double salpha;
     __shared__ Books sbk;
@@ -2401,19 +2402,30 @@ __global__ void __launch_bounds__(1024) k_dual_update(SpxDev d, int gn, int ncb,
     const int ot = colth ? ot_l : 0;
     sp[0][w][lane] = a;
     if (NRHS == 2) sp[NRHS - 1][w][lane] = b;
+    if (NRHS == 2 && w == 0 && sl == 0) sub[rl] = ub;
     TPH(3, 2);
     __syncthreads();
-    if (w == 0 && sl == 0) {
-        double sa = 0.0, sb = 0.0;
-        for (int k = 0; k < nw; ++k)
+    // the three fixed-order sums (tcol and u of the block's rows, alpha_p)
+    // are independent chains of nw * SL dependent adds: each in its own wave
+    // (the lanes of the block's rows in the waves of tcol and u) so that they
+    // run side by side; one wave does all when the block has fewer
+    {
+        const int wb = NRHS == 2 ? min(1, nw - 1) : 0, wl = min(2, nw - 1);
+        if (w == 0 && sl == 0) {
+            double sa = 0.0;
+            for (int k = 0; k < nw; ++k)
 #pragma unroll
-            for (int z = 0; z < SL; ++z) {
-                sa += sp[0][k][rl + z * RPB];
-                if (NRHS == 2) sb += sp[NRHS - 1][k][rl + z * RPB];
-            }
-        srow[0][rl] = sa + ua;
-        if (NRHS == 2) srow[NRHS - 1][rl] = sb + ub;
-        if (!SP && rl == 0) {
+                for (int z = 0; z < SL; ++z) sa += sp[0][k][rl + z * RPB];
+            srow[0][rl] = sa + ua;
+        }
+        if (NRHS == 2 && w == wb && sl == 0) {
+            double sb = 0.0;
+            for (int k = 0; k < nw; ++k)
+#pragma unroll
+                for (int z = 0; z < SL; ++z) sb += sp[NRHS - 1][k][rl + z * RPB];
+            srow[NRHS - 1][rl] = sb + sub[rl];
+        }
+        if (!SP && w == wl && lane == 0) {
             double s = 0.0;
             for (int k = 0; k < NSL; ++k) s += salp[k];
             salpha = s;

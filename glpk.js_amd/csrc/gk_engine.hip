@@ -173,6 +173,17 @@ struct Engine {
     DBuf<double> pnl, pnl_src;
     DBuf<int> pslot, ppos;
     int pnl_m = -1, pnl_n = -1;
+    // the next call's phase-I basic values, evaluated at the end of a dual
+    // call stopped by it_lim / tm_lim in phase I (Spx::next_aux_launch): the
+    // auxiliary bounds and statuses that call's set_aux_bnds will derive from
+    // the same reduced costs, and the eval_bbar result under them
+    DBuf<double> lb_n, ub_n, bbar_n;
+    DBuf<signed char> stat_n;
+    struct NextAux {
+        bool ok = false;
+        unsigned long long fact_ver = 0;
+        std::vector<signed char> stat_var;    // the status by variable (1..m+n) it was evaluated with
+    } next_aux;
     std::vector<GraphEntry> graphs;
     unsigned long long graph_clock = 0;
     int kbatch = 8;                           // batch length carried across calls
@@ -238,6 +249,7 @@ struct Engine {
         gpart.release(); awcnt.release(); tslots.release(); xslots.release(); trace.release(); wlist.release(); wpos.release(); cand.release();
         awpart.release();
         pnl.release(); pnl_src.release(); pslot.release(); ppos.release();
+        lb_n.release(); ub_n.release(); bbar_n.release(); stat_n.release();
         type.release(); orig_type.release(); stat.release(); refsp.release();
         lb.release(); ub.release(); coef.release(); orig_lb.release(); orig_ub.release(); obj.release();
         head.release(); bind.release();
@@ -584,6 +596,26 @@ static void engine_upload_matrix(gk_bfd *f, const gk_lp *lp)
     E.a_version = lp->a_version;
 }
 
+// set_aux_bnds (glpspx02.js:1317-1359) on the device, into separate arrays:
+// the auxiliary bounds of every variable from its original type, and the
+// status of every non-basic position from the sign of its reduced cost
+__global__ void k_aux_bnds(int m, int n, const signed char *__restrict__ orig_type, const int *__restrict__ head,
+                           const double *__restrict__ cbar, double *__restrict__ lb, double *__restrict__ ub,
+                           signed char *__restrict__ stat)
+{
+    const int k = blockIdx.x * blockDim.x + threadIdx.x;       // variable k + 1
+    if (k < m + n) {
+        const int t = orig_type[k];
+        lb[k] = t == FR ? -1e3 : (t == LO ? 0.0 : (t == UP ? -1.0 : 0.0));
+        ub[k] = t == FR ? +1e3 : (t == LO ? +1.0 : (t == UP ? 0.0 : 0.0));
+    }
+    if (k < n) {
+        const int v = head[m + k] - 1;
+        const int t = orig_type[v];
+        stat[k] = (t != FR && t != LO && t != UP) ? NS : (cbar[k] >= 0.0 ? NL : NU);
+    }
+}
+
 static double bits_double(unsigned long long b)
 {
     double v;
@@ -883,11 +915,22 @@ struct Spx {
         if (bbar_ok) { evals_skipped++; return; }
         const double t0 = now_s();
         struct T { gk_bfd *f; double t0; ~T() { f->stats.seconds_eval += now_s() - t0; } } tt{f, t0};
-        SpxDev d = dev();
+        if (next_aux_take()) {
+            // evaluated at the end of the last call with exactly these bounds,
+            // statuses, basis and factor (the same kernels, so the same bits)
+            HIPCHK(hipMemcpyAsync(E->bbar.p, E->bbar_n.p, (size_t)m * sizeof(double), hipMemcpyDeviceToDevice, s));
+            evals_skipped++;
+        } else
+            eval_bbar_into(dev(), E->bbar.p);
+        down(bbar, E->bbar, m);
+        sync();
+        bbar_ok = true;
+    }
+    // h = -N xN over the statuses and bounds of d; beta = inv(B) h, refined once
+    void eval_bbar_into(const SpxDev &d, double *beta)
+    {
         MatDev A = E->mat();
-        double *w = E->s.p;   // n-sized scratch
-        double *ys = E->r1.p, *wc = E->wcol.p, *h = E->h.p, *beta = E->bbar.p, *t = E->r2.p, *dd = E->work.p;
-        (void)w;
+        double *ys = E->r1.p, *wc = E->wcol.p, *h = E->h.p, *t = E->r2.p, *dd = E->work.p;
         split_pos(s, d, 0, nullptr, ys, wc);
         aprod_neg(s, A, wc, ys, h, E->partial.p, PARTIAL_CAP);                  // h = ys - A wc
         ftran_(h, beta);
@@ -896,16 +939,65 @@ struct Spx {
         rsub_into(t, h);                                                       // t = h - B beta
         ftran_(t, dd);
         vec_axpy(s, beta, dd, 1.0, m);
-        down(bbar, E->bbar, m);
-        sync();
-        bbar_ok = true;
     }
+    // A dual call that stops on its iteration / time limit in phase I leaves
+    // its basis for the next call, which (the reference's spx_dual from the
+    // top: init_csa, eval_cbar, check_feas, set_aux_bnds) evaluates the basic
+    // values under the auxiliary bounds again.  The reduced costs that call
+    // derives the statuses from are the ones this call just evaluated, so the
+    // evaluation can run now, on the device, while the host returns and the
+    // caller prepares the next call — the same kernels on the same inputs,
+    // bit for bit the result that call would compute.  next_aux_take uses it
+    // only when everything it depends on is unchanged: the resident working
+    // set was kept (same matrix, bounds, costs, basis, factor), no pivot and
+    // no re-inversion happened yet in this call, and set_aux_bnds gave every
+    // non-basic variable the status the evaluation used.
+    void next_aux_launch()
+    {
+        Engine::NextAux &X = E->next_aux;
+        X.ok = false;
+        const char *ev = std::getenv("GK_NEXT_AUX");         // 0: off (A/B tests)
+        if (ev && std::atoi(ev) == 0) return;
+        if (!dual || phase != 1 || head_stale || vec_stale) return;
+        const size_t mn = (size_t)m + n;
+        E->lb_n.ensure(mn); E->ub_n.ensure(mn); E->stat_n.ensure(n); E->bbar_n.ensure(m);
+        hipLaunchKernelGGL(k_aux_bnds, dim3((unsigned)((std::max<size_t>(mn, n) + 255) / 256)), dim3(256), 0, s, m, n,
+                           E->orig_type.p, E->head.p, E->cbar.p, E->lb_n.p, E->ub_n.p, E->stat_n.p);
+        SpxDev d = dev();
+        d.lb = E->lb_n.p; d.ub = E->ub_n.p; d.stat = E->stat_n.p;
+        eval_bbar_into(d, E->bbar_n.p);
+        // the host record: the same rule on the host mirrors (cbar is the
+        // fresh evaluation the device holds)
+        X.stat_var.assign(mn + 1, 0);
+        for (int j = 1; j <= n; j++) {
+            const int k = head[m + j];
+            const int t = orig_type[k];
+            X.stat_var[k] = (t != FR && t != LO && t != UP) ? NS : (cbar[j] >= 0.0 ? NL : NU);
+        }
+        X.fact_ver = f->fact_ver;
+        X.ok = true;
+    }
+    bool next_aux_take()
+    {
+        Engine::NextAux &X = E->next_aux;
+        if (!X.ok) return false;
+        X.ok = false;                                  // one use
+        if (!dual || phase != 1 || !kept || reinv_calls || hs.it_cnt != it_beg || f->fact_ver != X.fact_ver ||
+            X.stat_var.size() != (size_t)m + n + 1)
+            return false;
+        for (int j = 1; j <= n; j++)
+            if (stat[j] != X.stat_var[head[m + j]]) return false;
+        return true;
+    }
+    bool kept = false;                                 // init kept the resident working set
+    int reinv_calls = 0;                               // re-inversions in this call
 
     void rsub_into(double *y, const double *a);   // y = a - y
 
     bool reinvert()
     {
         pull();
+        reinv_calls++;
         cbar_ok = bbar_ok = false;
         hs.pvalid = 0;                          // the pricing panel is refilled from the fresh inverse
         BasisSplit bs;
@@ -1362,10 +1454,15 @@ void Spx::init()
     s = ctx->stream;
     const size_t mn = (size_t)m + n + 1;
     swap_spare();
-    type.assign(mn, 0); orig_type.assign(mn, 0); lb.assign(mn, 0.0); ub.assign(mn, 0.0); coef.assign(mn, 0.0);
-    orig_lb.assign(mn, 0.0); orig_ub.assign(mn, 0.0); obj.assign(n + 1, 0.0);
-    head.assign(mn, 0); bind.assign(mn, 0); stat.assign(n + 1, 0);
-    bbar.assign(m + 1, 0.0); cbar.assign(n + 1, 0.0); gamma.assign(std::max(m, n) + 1, 0.0);
+    // every entry 1..m+n of type / lb / ub / coef / head (1..n of obj and
+    // stat) is written below: resized, not zero-filled (the spare set has the
+    // size of the last call; zero-filling these arrays was most of init's
+    // host time on C3); orig_* are copies of the built arrays
+    type.resize(mn); lb.resize(mn); ub.resize(mn); coef.resize(mn); obj.resize(n + 1);
+    head.resize(mn); stat.resize(n + 1);
+    type[0] = 0; lb[0] = ub[0] = coef[0] = 0.0; head[0] = 0; stat[0] = 0;
+    bind.assign(mn, 0);
+    gamma.assign(std::max(m, n) + 1, 0.0);
     // init_csa (glpspx01.js:42-145 / glpspx02.js:89-190)
     for (int i = 1; i <= m; i++) {
         type[i] = L->row_type[i];
@@ -1419,9 +1516,14 @@ void Spx::init()
     // the working set the last call left on the device, when it is this one
     const double t_alloc = now_s();
     const bool keep = resident_match();
+    kept = keep;
     const double t_match = now_s();
     Engine::Resident &R = E->res;
     R.ok = false;
+    if (!keep) {
+        bbar.assign(m + 1, 0.0);
+        cbar.assign(n + 1, 0.0);
+    }
     begin_up();
     if (!keep) {
         up(E->type, type, mn - 1); up(E->orig_type, orig_type, mn - 1);
@@ -1817,6 +1919,7 @@ int Spx::run_dual()
                 display(1);
                 report_msg(it_hit ? GK_MSG_ITLIM : GK_MSG_TMLIM, 3);
                 int d_stat;
+                const int ph = phase;
                 if (phase == 1) {
                     pull();
                     d_stat = 3;
@@ -1825,6 +1928,10 @@ int Spx::run_dual()
                 } else
                     d_stat = 2;
                 store_sol(3, d_stat, 0);
+                if (ph == 1) {
+                    phase = 1;                     // the phase the next call resumes in
+                    next_aux_launch();
+                }
                 return it_hit ? 8 : 9;
             }
         }

@@ -126,6 +126,7 @@ def load_library(path: str = LIB_PATH):
     global _lib
     if _lib is not None:
         return _lib
+    path = os.environ.get("GK_LIB_PATH", path)       # A/B experiments: another build of the library
     if not os.path.exists(path):
         raise GkError(f"{path} is missing: build it with __graft_entry__.build()")
     L = C.CDLL(path)

@@ -239,3 +239,38 @@ def test_gpu_c3_bench_window_matches_oracle(gpu_ctx):
         assert ret == want_ret and P.it_cnt == 100 * k
         if k in states:
             _assert_state(P, states[k])
+
+
+@pytest.mark.gpu
+def test_gpu_next_call_phase1_eval_bit_identical(gpu_ctx, monkeypatch):
+    """A dual call stopped by it_lim in phase I evaluates the next call's
+    phase-I basic values before it returns (gk_engine.hip next_aux_launch);
+    the next call takes them only when nothing they depend on changed.  A
+    chain of it_lim calls (with a bound changed between two of them) gives
+    bit for bit the same states with the precomputation on and off
+    (GK_NEXT_AUX=0), and the calls after an unchanged one do take it."""
+    prob = problems.gen_dense(1024, 4096, seed=42)
+
+    def chain(on):
+        if on:
+            monkeypatch.delenv("GK_NEXT_AUX", raising=False)
+        else:
+            monkeypatch.setenv("GK_NEXT_AUX", "0")
+        P = gk.GkProblem(gpu_ctx, prob)
+        out, skipped = [], 0
+        for k in range(8):
+            if k == 5:
+                P.col_ub[7] = P.col_ub[7] + 0.5 if P.col_ub[7] < 1e30 else 10.0   # the next call rebuilds
+            ret = gk.glp_simplex(P, gk.SMCP(meth=gk.GLP_DUAL, it_lim=60))
+            skipped += P.stats().evals_skipped
+            out.append((ret, P.it_cnt, P.obj_val, np.array(P.row_prim[1:]), np.array(P.col_prim[1:]),
+                        np.array(P.row_stat[1:]), np.array(P.col_stat[1:])))
+        return out, skipped
+
+    on, sk_on = chain(True)
+    off, sk_off = chain(False)
+    for a, b in zip(on, off):
+        assert a[:3] == b[:3]
+        for x, y in zip(a[3:], b[3:]):
+            assert np.array_equal(x, y)
+    assert sk_on > sk_off
