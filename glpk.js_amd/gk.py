@@ -119,6 +119,7 @@ EXPORTS = ["gk_abi_version", "gk_device_count", "gk_ctx_create", "gk_ctx_destroy
 # gk_report_fn (glpk_mi355x.h): one progress line or termination message of
 # a gk_spx_* call, in the order the reference prints them
 REPORT_FN = C.CFUNCTYPE(None, C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_double, C.c_double, C.c_int)
+_NULL_REPORT = REPORT_FN()
 
 
 def load_library(path: str = LIB_PATH):
@@ -348,19 +349,26 @@ class GkProblem:
         self.a_version = GkProblem._version
 
     # ------------------------------------------------------------------
+    _LP_ARRAYS = ("row_type", "row_lb", "row_ub", "rii", "col_type", "col_lb", "col_ub", "col_coef", "sjj",
+                  "A_ptr", "A_ind", "A_val", "head", "row_stat", "col_stat", "row_bind", "col_bind",
+                  "row_prim", "row_dual", "col_prim", "col_dual")
+
     def _lp_struct(self) -> Lp:
-        ptr = lambda a: a.ctypes.data_as(C.c_void_p)
+        # the array pointers are cached per array object (a numpy array's
+        # data never moves; an attribute rebound to another array is seen by
+        # the identity test): a fresh ctypes pointer per field and call cost
+        # ~0.1 ms per glp_simplex call, ~2.5 % of a C3 it_lim=100 step
+        cache = self.__dict__.setdefault("_ptr_cache", {})
         lp = Lp()
         lp.m, lp.n, lp.nnz, lp.dir, lp.c0 = self.m, self.n, self.nnz, self.dir, self.c0
-        lp.row_type, lp.row_lb, lp.row_ub, lp.rii = ptr(self.row_type), ptr(self.row_lb), ptr(self.row_ub), ptr(self.rii)
-        lp.col_type, lp.col_lb, lp.col_ub = ptr(self.col_type), ptr(self.col_lb), ptr(self.col_ub)
-        lp.col_coef, lp.sjj = ptr(self.col_coef), ptr(self.sjj)
-        lp.A_ptr, lp.A_ind, lp.A_val = ptr(self.A_ptr), ptr(self.A_ind), ptr(self.A_val)
+        for name in self._LP_ARRAYS:
+            arr = self.__dict__[name]
+            ent = cache.get(name)
+            if ent is None or ent[0] is not arr:
+                ent = (arr, arr.ctypes.data)
+                cache[name] = ent
+            setattr(lp, name, ent[1])
         lp.a_version = self.a_version
-        lp.head, lp.row_stat, lp.col_stat = ptr(self.head), ptr(self.row_stat), ptr(self.col_stat)
-        lp.row_bind, lp.col_bind = ptr(self.row_bind), ptr(self.col_bind)
-        lp.row_prim, lp.row_dual = ptr(self.row_prim), ptr(self.row_dual)
-        lp.col_prim, lp.col_dual = ptr(self.col_prim), ptr(self.col_dual)
         lp.it_cnt = self.it_cnt
         return lp
 
@@ -440,13 +448,19 @@ class GkProblem:
     def spx(self, parm: Smcp, dual: bool) -> int:
         lp = self._lp_struct()
         fn = self.L.gk_spx_dual if dual else self.L.gk_spx_primal
-        reports = []
-        cb = REPORT_FN(lambda ud, *r: reports.append(r))
-        self.L.gk_bfd_set_report(self.bfd, cb, None)
+        # one report callback per problem (a ctypes callback made per call
+        # costs as much as a fresh pointer per field)
+        if "_rpt_cb" not in self.__dict__:
+            box = []                         # the callback holds the list, not self (no cycle)
+            self._reports = box
+            self._rpt_cb = REPORT_FN(lambda ud, *r: box.append(r))
+        reports = self._reports
+        reports.clear()
+        self.L.gk_bfd_set_report(self.bfd, self._rpt_cb, None)
         try:
             ret = fn(self.ctx.h, C.byref(lp), self.bfd, C.byref(parm))
         finally:
-            self.L.gk_bfd_set_report(self.bfd, REPORT_FN(), None)
+            self.L.gk_bfd_set_report(self.bfd, _NULL_REPORT, None)
         # the display lines and messages (glpspx01.js:1587, glpspx02.js:1493),
         # printed in order after the solve
         for r in reports:
