@@ -32,6 +32,7 @@
 #include <cmath>
 #include <cstdlib>
 #include <cstring>
+#include <x86intrin.h>
 #include <queue>
 #include <string>
 #include <vector>
@@ -993,9 +994,11 @@ struct MipSolver {
     }
     void push_open(NodeRec r)
     {
+        const unsigned long long t0 = tsc_on ? tsc() : 0ull;
         set_keys(r);
         open.push_back(r);
         std::push_heap(open.begin(), open.end(), NodeWorse());
+        if (tsc_on) tsc_heap += tsc() - t0;
     }
     NodeRec pop_open()
     {
@@ -1013,6 +1016,10 @@ struct MipSolver {
     }
     int bingos = 0;                           // new incumbents not yet reported
     std::vector<int> cand_buf;                // node_done's fractional columns
+    // GK_BNB_LOG: time stamp counter ticks of node_done's parts (host profile)
+    bool tsc_on = false;
+    unsigned long long tsc_int = 0, tsc_choose = 0, tsc_child = 0, tsc_heap = 0;
+    static unsigned long long tsc() { return __rdtsc(); }
     void new_incumbent(double z, const double *x)
     {
         const double before = bestall();
@@ -1184,7 +1191,11 @@ struct MipSolver {
         if (!hopeful(bound)) return false;
         std::vector<int> &cand = cand_buf;           // reused: no allocation per node
         double ii = 0.0;
-        if (integrality(x, so, bl, bu, cand, ii) == 0) {
+        const unsigned long long ti0 = tsc_on ? tsc() : 0ull;
+        const int nfrac = integrality(x, so, bl, bu, cand, ii);
+        const unsigned long long ti1 = tsc_on ? tsc() : 0ull;
+        if (tsc_on) tsc_int += ti1 - ti0;
+        if (nfrac == 0) {
             if (!have || z < best) new_incumbent(z, x);
             return false;
         }
@@ -1243,7 +1254,10 @@ struct MipSolver {
             break;
         }
         const double dn = tableau ? dzb[2 * j] : 0.0, up = tableau ? dzb[2 * j + 1] : 0.0;
+        const unsigned long long tb0 = tsc_on ? tsc() : 0ull;
+        if (tsc_on) tsc_choose += tb0 - ti1;
         branch(nd, mt, z, bound, ii, x, so, bl, bu, j, next, dn, up);
+        if (tsc_on) tsc_child += tsc() - tb0;
         return false;
     }
 
@@ -1618,6 +1632,8 @@ extern "C" int gk_ios_driver_sharded(gk_ctx *ctx, gk_mip *mip, const gk_iocp *pa
     long long moved = 0;
     // GK_BNB_LOG=1: where the search's wall time goes (stderr)
     static const bool bnb_log = std::getenv("GK_BNB_LOG") != nullptr;
+    S.tsc_on = bnb_log;
+    const unsigned long long tsc_beg = bnb_log ? MipSolver::tsc() : 0ull;
     double t_launch = 0.0, t_wait = 0.0, t_proc = 0.0, t_nd = 0.0;
     long long n_batches = 0, n_ents = 0;
     auto secs = [](std::chrono::steady_clock::time_point a) {
@@ -1942,6 +1958,12 @@ extern "C" int gk_ios_driver_sharded(gk_ctx *ctx, gk_mip *mip, const gk_iocp *pa
                         "wait %.3f ms, process %.3f ms (node_done %.3f); open %zu; lp %lld, pp-fathomed %lld, created %lld\n",
                 1e3 * secs(t0), n_batches, n_ents, n_batches ? (double)n_ents / n_batches : 0.0, 1e3 * t_launch,
                 1e3 * t_wait, 1e3 * t_proc, 1e3 * t_nd, S.open.size(), S.lp_solves, S.pp_fathomed, S.created);
+    if (bnb_log) {
+        const double tpms = (double)(MipSolver::tsc() - tsc_beg) / (1e3 * secs(t0));     // ticks per ms
+        fprintf(stderr, "[gk bnb] node_done parts: integrality %.3f ms, choice %.3f ms, children (incl. heap) %.3f ms, "
+                        "heap pushes %.3f ms\n", S.tsc_int / tpms, S.tsc_choose / tpms, S.tsc_child / tpms,
+                S.tsc_heap / tpms);
+    }
     mip->lp_solves = S.lp_solves;
     mip->nodes_created = S.created;
     mip->pivots = S.pivots;
