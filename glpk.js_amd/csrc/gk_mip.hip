@@ -33,7 +33,12 @@
 #include <cstdlib>
 #include <cstring>
 #include <x86intrin.h>
+#include <atomic>
+#include <condition_variable>
+#include <functional>
+#include <mutex>
 #include <queue>
+#include <thread>
 #include <string>
 #include <vector>
 
@@ -876,10 +881,98 @@ struct Parked {
 // from one glp_intopt to the next (allocating them — hipHostMalloc of the
 // packed batch buffers above all — cost a search of gap several
 // milliseconds when it was done per call); the arrays only grow
+// host workers for the per-node parts of a batch's processing (integrality
+// scans and the children's bound / status arrays), persistent across
+// searches: for(n, fn) runs fn(i) for i < n on the workers and the caller,
+// chunks claimed from an atomic counter, and returns when all are done
+struct HostWorkers {
+    std::vector<std::thread> th;
+    std::mutex mu;
+    std::condition_variable cv, done;
+    std::function<void(int)> fn;
+    std::atomic<int> next{0};
+    int n = 0, chunk = 1, busy = 0;
+    unsigned long long gen = 0;
+    bool stop = false;
+    explicit HostWorkers(int k)
+    {
+        for (int t = 0; t < k; t++) th.emplace_back([this] { loop(); });
+    }
+    ~HostWorkers()
+    {
+        {
+            std::lock_guard<std::mutex> lk(mu);
+            stop = true;
+        }
+        cv.notify_all();
+        for (auto &t : th) t.join();
+    }
+    void work()
+    {
+        for (;;) {
+            const int i0 = next.fetch_add(chunk);
+            if (i0 >= n) return;
+            const int i1 = std::min(n, i0 + chunk);
+            for (int i = i0; i < i1; i++) fn(i);
+        }
+    }
+    void loop()
+    {
+        unsigned long long seen = 0;
+        for (;;) {
+            {
+                std::unique_lock<std::mutex> lk(mu);
+                cv.wait(lk, [&] { return stop || gen != seen; });
+                if (stop) return;
+                seen = gen;
+            }
+            work();
+            {
+                std::lock_guard<std::mutex> lk(mu);
+                if (--busy == 0) done.notify_one();
+            }
+        }
+    }
+    void run(int cnt, int ch, std::function<void(int)> f)
+    {
+        if (cnt <= 0) return;
+        if (th.empty() || cnt < 2 * ch) {
+            for (int i = 0; i < cnt; i++) f(i);
+            return;
+        }
+        {
+            std::lock_guard<std::mutex> lk(mu);
+            fn = std::move(f);
+            n = cnt;
+            chunk = ch;
+            next.store(0);
+            busy = (int)th.size();
+            gen++;
+        }
+        cv.notify_all();
+        work();
+        std::unique_lock<std::mutex> lk(mu);
+        done.wait(lk, [&] { return busy == 0; });
+    }
+};
+
+static int bnb_threads()
+{
+    static const int v = [] {
+        const char *e = std::getenv("GK_BNB_THREADS");
+        if (e) return std::max(0, std::min(std::atoi(e), 16));
+        const unsigned hc = std::thread::hardware_concurrency();
+        return (int)std::min(3u, hc > 1 ? hc - 1 : 0u);
+    }();
+    return v;
+}
+
 struct MipCache {
     BatchBuf bufs[2];
     DevArr<double> dA, dc, dscratch;
     DevArr<signed char> dint;
+    HostWorkers *workers = nullptr;          // made with the first search that has work for them
+    ~MipCache() { delete workers; }
 };
 
 }  // namespace
@@ -1126,6 +1219,36 @@ struct MipSolver {
         return jjj;
     }
 
+    // a child whose bound and status arrays are filled after the batch's
+    // sequential pass (process(): many children filled by the workers)
+    struct FillJob {
+        int slot, j, kase;
+        double beta;
+        const double *bl, *bu;
+        const signed char *so;
+    };
+    std::vector<FillJob> *defer = nullptr;
+    // per-entry scratch of a batch's processing: column bounds (bl | bu),
+    // fractional columns, their count and the sum of integer infeasibilities
+    std::vector<double> eb, eii;
+    std::vector<int> ecand, ecand_n;
+    std::vector<FillJob> jobs;
+    void fill_child(const FillJob &f)
+    {
+        double *l = pool.lb(f.slot), *u = pool.ub(f.slot);
+        std::memcpy(l, f.bl, n * sizeof(double));
+        std::memcpy(u, f.bu, n * sizeof(double));
+        if (f.kase == 0) u[f.j] = std::floor(f.beta);
+        else l[f.j] = std::ceil(f.beta);
+        signed char *cs = pool.stat(f.slot);
+        std::memcpy(cs, f.so, N);
+        for (int q = 0; q < n; q++) {                 // statuses follow the column types (glp_set_col_bnds)
+            if (cs[m + q] == BS) continue;
+            if (l[q] == u[q]) cs[m + q] = NS;
+            else if (cs[m + q] == NS) cs[m + q] = (l[q] != -DBL_MAX) ? NL : (u[q] != DBL_MAX ? NU : NF);
+        }
+    }
+
     // branch_on (glpios03.js:141): the two children, the preferred one
     // (T.child) first into the next batch
     void branch(const NodeRec &nd, const NodeMeta &mt, double z, double bound, double ii, const double *x,
@@ -1141,18 +1264,9 @@ struct MipSolver {
             const double cb = std::max(bound, round_bound(z + dz[kase]));
             if (!hopeful(cb)) continue;
             const int sl = pool.alloc();
-            std::memcpy(pool.lb(sl), bl, n * sizeof(double));
-            std::memcpy(pool.ub(sl), bu, n * sizeof(double));
-            if (kase == 0) pool.ub(sl)[j] = std::floor(beta);
-            else pool.lb(sl)[j] = std::ceil(beta);
-            signed char *cs = pool.stat(sl);
-            std::memcpy(cs, so, N);
-            for (int q = 0; q < n; q++) {             // statuses follow the column types (glp_set_col_bnds)
-                if (cs[m + q] == BS) continue;
-                const double l = pool.lb(sl)[q], u = pool.ub(sl)[q];
-                if (l == u) cs[m + q] = NS;
-                else if (cs[m + q] == NS) cs[m + q] = (l != -DBL_MAX) ? NL : (u != DBL_MAX ? NU : NF);
-            }
+            const FillJob fj{sl, j, kase, beta, bl, bu, so};
+            if (defer) defer->push_back(fj);
+            else fill_child(fj);
             NodeMeta &cm = pool.meta[sl];
             cm.level = mt.level + 1;
             cm.br_var = j;
@@ -1175,7 +1289,8 @@ struct MipSolver {
     // branching (ios_driver's "analyze" part, glpios03.js:670-905)
     // returns true when the node is parked (its pool slot stays in use)
     bool node_done(const NodeRec &nd, double z, const double *x, const signed char *so, const double *bl,
-                   const double *bu, const double *dzb, int kjj, int knext, bool tableau)
+                   const double *bu, const double *dzb, int kjj, int knext, bool tableau, const int *pcand = nullptr,
+                   int npcand = -1, double pii = 0.0)
     {
         const NodeMeta mt = pool.meta[nd.slot];
         // ios_pcost_update (glpios09.js:288)
@@ -1192,7 +1307,13 @@ struct MipSolver {
         std::vector<int> &cand = cand_buf;           // reused: no allocation per node
         double ii = 0.0;
         const unsigned long long ti0 = tsc_on ? tsc() : 0ull;
-        const int nfrac = integrality(x, so, bl, bu, cand, ii);
+        int nfrac;
+        if (npcand >= 0) {                           // scanned by the batch's workers
+            cand.assign(pcand, pcand + npcand);
+            ii = pii;
+            nfrac = npcand;
+        } else
+            nfrac = integrality(x, so, bl, bu, cand, ii);
         const unsigned long long ti1 = tsc_on ? tsc() : 0ull;
         if (tsc_on) tsc_int += ti1 - ti0;
         if (nfrac == 0) {
@@ -1584,6 +1705,7 @@ extern "C" int gk_ios_driver_sharded(gk_ctx *ctx, gk_mip *mip, const gk_iocp *pa
         (void)freer;
         S.cache = (MipCache *)*slot;
         S.bufs = S.cache->bufs;
+        if (!S.cache->workers && bnb_threads() > 0) S.cache->workers = new HostWorkers(bnb_threads());
         // the previous search may have left events in use: nothing of it is in flight
     }
     MipCache &Cc = *S.cache;
@@ -1711,13 +1833,45 @@ extern "C" int gk_ios_driver_sharded(gk_ctx *ctx, gk_mip *mip, const gk_iocp *pa
         const int *hstat = (const int *)(h + Y.stat), *hpiv = (const int *)(h + Y.piv);
         const int *hjj = (const int *)(h + Y.jj), *hnext = (const int *)(h + Y.next);
         const signed char *hso = (const signed char *)(h + Y.sto);
-        std::vector<double> fx, fbl(n), fbu(n);
+        std::vector<double> fx;
         std::vector<signed char> fso;
         const std::vector<double> zeros(2 * (size_t)n, 0.0);
+        // (1) per entry, on the workers: the column bounds the node kernel
+        // returned (interleaved lb / ub) into bl | bu, and for an optimal
+        // node LP its integrality scan (check_integrality, glpios03.js:55)
+        HostWorkers *W = S.cache->workers;
+        const bool par = W && parm->br_tech != 5;
+        S.eb.resize((size_t)nb * 2 * n);
+        S.ecand.resize((size_t)nb * n);
+        S.ecand_n.assign(nb, -1);
+        S.eii.resize(nb);
+        auto prep = [&](int b) {
+            const Entry &e = bf.ents[b];
+            if (e.kind != 0) return;
+            const double *bb = hb + (size_t)b * 2 * n;
+            double *bl = S.eb.data() + (size_t)b * 2 * n, *bu = bl + n;
+            for (int j = 0; j < n; j++) { bl[j] = bb[2 * j]; bu[j] = bb[2 * j + 1]; }
+            if (par && hstat[b] == NODE_OPT) {
+                thread_local std::vector<int> cb;
+                double ii = 0.0;
+                const int nc = S.integrality(hx + (size_t)b * S.N, hso + (size_t)b * S.N, bl, bu, cb, ii);
+                std::memcpy(S.ecand.data() + (size_t)b * n, cb.data(), (size_t)nc * sizeof(int));
+                S.ecand_n[b] = nc;
+                S.eii[b] = ii;
+            }
+        };
+        if (par) W->run(nb, 16, prep);
+        else
+            for (int b = 0; b < nb; b++) prep(b);
+        // (2) in entry order (the search's decisions): incumbent, pruning,
+        // branching; a child's bound and status arrays are only recorded
+        S.jobs.clear();
+        S.defer = par ? &S.jobs : nullptr;
         for (int b = 0; b < nb; b++) {
             const Entry &e = bf.ents[b];
             const int st = hstat[b];
-            const double *x = hx + (size_t)b * S.N, *bb = hb + (size_t)b * 2 * n;
+            const double *x = hx + (size_t)b * S.N;
+            const double *fbl = S.eb.data() + (size_t)b * 2 * n, *fbu = fbl + n;
             S.pivots += hpiv[b];
             if (e.kind == 1) {
                 // the probe's degradation (eval_degrad :337-392)
@@ -1736,21 +1890,33 @@ extern "C" int gk_ios_driver_sharded(gk_ctx *ctx, gk_mip *mip, const gk_iocp *pa
             const NodeRec &nd = e.nd;
             if (st == NODE_PPINF) S.pp_fathomed++;
             else S.lp_solves++;
-            for (int j = 0; j < n; j++) { fbl[j] = bb[2 * j]; fbu[j] = bb[2 * j + 1]; }
             if (st == NODE_OPT) {
                 const auto tn0 = bnb_log ? std::chrono::steady_clock::now() : std::chrono::steady_clock::time_point{};
-                S.node_done(nd, hobj[b], x, hso + (size_t)b * S.N, fbl.data(), fbu.data(), hdz + (size_t)b * 2 * n,
-                            hjj[b], hnext[b], true);
+                S.node_done(nd, hobj[b], x, hso + (size_t)b * S.N, fbl, fbu, hdz + (size_t)b * 2 * n, hjj[b], hnext[b],
+                            true, S.ecand.data() + (size_t)b * n, S.ecand_n[b], S.eii[b]);
                 if (bnb_log) t_nd += secs(tn0);
             } else if ((st == NODE_FAIL || st == NODE_ITLIM) && !S.err) {
                 double z = 0.0;
                 bool opt = false;
-                const int ret = S.fallback(nd, fbl.data(), fbu.data(), fx, fso, z, opt);
+                const int ret = S.fallback(nd, fbl, fbu, fx, fso, z, opt);
                 if (ret) S.err = ret;
-                else if (opt)
-                    S.node_done(nd, z, fx.data(), fso.data(), fbl.data(), fbu.data(), zeros.data(), 0, 0, false);
+                else if (opt) {
+                    // fx / fso are reused by the next fallback: its children are filled now
+                    std::vector<MipSolver::FillJob> *dj = S.defer;
+                    S.defer = nullptr;
+                    S.node_done(nd, z, fx.data(), fso.data(), fbl, fbu, zeros.data(), 0, 0, false);
+                    S.defer = dj;
+                }
             }
             pool.release(nd.slot);
+        }
+        S.defer = nullptr;
+        // (3) the children's arrays, on the workers (slots are final: the
+        // pool does not grow any more in this batch)
+        if (!S.jobs.empty()) {
+            const auto tf0 = bnb_log ? std::chrono::steady_clock::now() : std::chrono::steady_clock::time_point{};
+            W->run((int)S.jobs.size(), 16, [&](int i) { S.fill_child(S.jobs[i]); });
+            if (bnb_log) t_nd += secs(tf0);
         }
         bf.ents.clear();
         for (const NodeRec &c : S.next_dive) S.dive.push_back(c);
