@@ -281,6 +281,7 @@ struct gk_bfd {
     // re-inversion scratch
     DBuf<double> C, X, Y, CinvR, BS, G, vecx, vecy, partial;
     DBuf<int> idx_i, piv_step, piv, flag;
+    DBuf<unsigned long long> nwt_bits;         // max |I - C X| of a Newton step (gk_newton.hip)
     DBuf<int> bptr, brow;                      // basis given as CSC (gk_bfd_factorize*)
     DBuf<double> bval;
     Engine *eng = nullptr;
@@ -313,8 +314,11 @@ struct BasisSplit {
     std::vector<int> posJ, colJ, rowR, posS, rowS, rowmap;   // rowmap[r-1] = a (R) or -(s+1) (S)
 };
 
+// refine: inv(B) currently holds the product-form-updated inverse of exactly
+// this basis (the engine's scheduled re-inversion): the structural block may
+// be re-inverted by Newton refinement on the matrix cores (gk_newton.hip)
 static int reinvert_core(gk_bfd *f, const BasisSplit &bs, const MatDev *Adense, int from_csc, double sign,
-                         const int *csc_ptr, const int *csc_row, const double *csc_val)
+                         const int *csc_ptr, const int *csc_row, const double *csc_val, bool refine = false)
 {
     hipStream_t s = f->ctx->stream;
     const int m = f->m, k = bs.k, ms = bs.ms;
@@ -352,6 +356,31 @@ static int reinvert_core(gk_bfd *f, const BasisSplit &bs, const MatDev *Adense, 
             gather_csc_sel(s, k, d_colJ, csc_ptr, csc_row, csc_val, d_rowmap, f->X.p, f->BS.p, ms, sign);
         } else {
             gather_basis_blocks(s, *Adense, m, k, d_colJ, d_rowR, f->X.p, f->BS.p, ms, d_rowS);
+        }
+        const double *cinv = nullptr;
+        if (refine && f->valid && !f->ext_upd && newton_min_k() > 0 && k >= newton_min_k()) {
+            f->nwt_bits.ensure(1);
+            NewtonInfo ni;
+            cinv = newton_refine(s, k, f->X.p, f->Binv.p, f->ldb, d_posJ, d_rowR, f->CinvR.p, f->Y.p,
+                                 f->Y.p + (size_t)k * k, f->nwt_bits.p, &ni);
+            f->stats.refine_tries++;
+            f->stats.refine_resid_max = std::max(f->stats.refine_resid_max, ni.resid);
+            if (cinv) {
+                f->stats.refinements++;
+                f->stats.refine_steps += ni.steps;
+            }
+        }
+        if (cinv) {
+            if (ms > 0) gemm_bs_cinv(s, f->BS.p, ms, k, cinv, f->G.p, 1);
+            assemble_binv(s, f->Binv.p, m, f->ldb, k, ms, d_posJ, d_rowR, d_posS, d_rowS, cinv, f->G.p);
+            HIPCHK(hipStreamSynchronize(s));
+            f->fact_ver++;
+            f->valid = 1;
+            f->upd_cnt = 0;
+            f->ext_upd = 0;
+            f->stats.reinversions++;
+            f->stats.seconds_reinvert += now_s() - t0;
+            return 0;
         }
         f->piv_step.ensure(k);
         f->piv.ensure(k);
@@ -1007,14 +1036,22 @@ struct Spx {
         }
         MatDev A = E->mat();
         int ret;
+        const bool refine = refine_next;
+        refine_next = false;
+        echk_seen = hs.echk;
         if (E->dense)
-            ret = reinvert_core(f, bs, &A, 0, 1.0, nullptr, nullptr, nullptr);
+            ret = reinvert_core(f, bs, &A, 0, 1.0, nullptr, nullptr, nullptr, refine);
         else
-            ret = reinvert_core_csc(bs);
+            ret = reinvert_core_csc(bs, refine);
         fact_ret = ret;
         return ret == 0;
     }
     int fact_ret = 0;
+    // the next re-inversion is a scheduled one (update limit, no growth-check
+    // failure since the last): inv(B) is the updated inverse of the current
+    // basis and may be refined instead of rebuilt (gk_newton.hip)
+    bool refine_next = false;
+    int echk_seen = 0;
 
     // ---- the reference's terminal output (display, glpspx01.js:1550-1589 /
     // glpspx02.js:1452-1497, and the xprintf lines of the main loops), as
@@ -1068,7 +1105,7 @@ struct Spx {
         const int fr = std::max(parm->out_frq, 1);
         return std::max(1, std::min(K, fr - hs.it_cnt % fr));
     }
-    int reinvert_core_csc(const BasisSplit &bs);
+    int reinvert_core_csc(const BasisSplit &bs, bool refine = false);
 
     // ---- host-side logic on the mirrors -------------------------------------
     // dual: check_feas (glpspx02.js:1296)
@@ -1398,10 +1435,10 @@ void gather_csc_sel(hipStream_t s, int k, const int *colJ, const int *cptr, cons
     hipLaunchKernelGGL(k_gather_csc_sel, dim3(k), dim3(64), 0, s, k, colJ, cptr, crow, cval, rowmap, C, BS, ms, sign);
 }
 
-int Spx::reinvert_core_csc(const BasisSplit &bs)
+int Spx::reinvert_core_csc(const BasisSplit &bs, bool refine)
 {
     // structural basis columns are -A columns of the device CSC
-    return reinvert_core(f, bs, nullptr, 1, -1.0, E->cptr.p, E->cind.p, E->cval.p);
+    return reinvert_core(f, bs, nullptr, 1, -1.0, E->cptr.p, E->cind.p, E->cval.p, refine);
 }
 
 bool Spx::resident_match() const
@@ -1939,6 +1976,7 @@ int Spx::run_dual()
             // the update limit was reached at the end of the last batch:
             // re-invert before launching (a batch would stop at its first pivot)
             binv_st = 0;
+            refine_next = (hs.echk == echk_seen);
             continue;
         }
         display(0);
@@ -1966,6 +2004,7 @@ int Spx::run_dual()
             break;
         case ST_REFACT:
             binv_st = 0;
+            refine_next = (hs.echk == echk_seen);
             break;
         case ST_P0:
             if (bbar_st != 1 || cbar_st != 1) {
@@ -2097,6 +2136,7 @@ int Spx::run_primal()
             // the update limit was reached at the end of the last batch:
             // re-invert before launching (a batch would stop at its first pivot)
             binv_st = 0;
+            refine_next = (hs.echk == echk_seen);
             continue;
         }
         display(0);
@@ -2124,6 +2164,7 @@ int Spx::run_primal()
             break;
         case ST_REFACT:
             binv_st = 0;
+            refine_next = (hs.echk == echk_seen);
             break;
         case ST_Q0:
             if (bbar_st != 1 || cbar_st != 1) {

@@ -263,6 +263,18 @@ void extract_inverse_blocked(hipStream_t s, const double *M, int k, const int *p
 void gemm_bs_cinv(hipStream_t s, const double *BS, int ms, int k, const double *CinvR, double *G, int use_mfma);
 void assemble_binv(hipStream_t s, double *Binv, int m, int ldb, int k, int ms, const int *posJ, const int *rowR,
                    const int *posS, const int *rowS, const double *CinvR, const double *G);
+// scheduled re-inversion by Newton refinement of the updated inverse
+// (gk_newton.hip): C column-major in C, X0 / R / X1 k x k scratch; returns
+// the buffer holding inv(C) in the CinvR layout, or nullptr (use Gauss-Jordan)
+struct NewtonInfo {
+    int steps = 0;
+    double resid = 0.0;          // max |I - C X0| of the updated inverse
+    double final_bound = 0.0;    // (k max |R|)^2 of the last step
+};
+int newton_min_k();
+const double *newton_refine(hipStream_t s, int k, const double *C, const double *Binv, int ldb, const int *posJ,
+                            const int *rowR, double *X0, double *R, double *X1, unsigned long long *rbits,
+                            NewtonInfo *info);
 
 // basic helpers
 void vec_axpy(hipStream_t s, double *y, const double *x, double a, int n);

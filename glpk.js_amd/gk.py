@@ -100,7 +100,9 @@ class SpxStats(C.Structure):
                 ("trow_dev_ms_r", C.c_double), ("trow_dev_launches_r", C.c_longlong),
                 ("upd_dev_ms", C.c_double), ("upd_dev_launches", C.c_longlong), ("upd_bytes", C.c_double),
                 ("resident", C.c_int), ("evals_skipped", C.c_int),
-                ("panel_hits", C.c_longlong), ("panel_refills", C.c_longlong)]
+                ("panel_hits", C.c_longlong), ("panel_refills", C.c_longlong),
+                ("refine_tries", C.c_longlong), ("refinements", C.c_longlong), ("refine_steps", C.c_longlong),
+                ("refine_resid_max", C.c_double)]
 
 
 _lib = None

@@ -40,7 +40,7 @@
 extern "C" {
 #endif
 
-#define GK_ABI_VERSION 6
+#define GK_ABI_VERSION 7
 #include <stddef.h>
 #define GK_EABI (-1)          /* contract violation; see gk_last_error() */
 
@@ -196,6 +196,10 @@ typedef struct {
     int evals_skipped;          /* eval_cbar / eval_bbar calls whose result was already resident */
     long long panel_hits;       /* dual pivots whose pivot row came from the MFMA pricing panel */
     long long panel_refills;    /* MFMA refills of the panel (one pass over A for up to 32 rows) */
+    long long refine_tries;     /* scheduled re-inversions offered to Newton refinement (k >= GK_NEWTON_MIN_K) */
+    long long refinements;      /* ... served by it (two MFMA GEMMs per step; the rest: Gauss-Jordan) */
+    long long refine_steps;     /* Newton steps taken by those */
+    double refine_resid_max;    /* largest max|I - C X| of an updated inverse offered to it */
 } gk_spx_stats;
 void gk_bfd_last_stats(const gk_bfd *bfd, gk_spx_stats *st);
 /* record HIP events around the pivot-row kernel of every dual pivot (benches) */

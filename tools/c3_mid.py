@@ -23,17 +23,20 @@ def main():
     steps = int(sys.argv[2]) if len(sys.argv) > 2 else 10
     ctx = gk.Context(0)
     P = gk.GkProblem(ctx, problems.gen_dense(4096, 16384, seed=42))
+    t_adv = time.perf_counter()
     while P.it_cnt < warm:
         ret = gk.glp_simplex(P, gk.SMCP(meth=gk.GLP_DUAL, it_lim=min(2000, warm - P.it_cnt),
                                         msg_lev=gk.GLP_MSG_ERR))
         print(json.dumps({"it_cnt": P.it_cnt}), flush=True)
         assert ret == 8
+    t_adv = time.perf_counter() - t_adv
     parm = gk.SMCP(meth=gk.GLP_DUAL, it_lim=100, msg_lev=gk.GLP_MSG_ERR)
     gk.glp_simplex(P, parm)
     torch.cuda.synchronize()
     ctx.mark(1)
     t0 = time.perf_counter()
     piv, byts, split = 0, 0.0, {"init": 0.0, "eval": 0.0, "batches": 0.0, "reinvert": 0.0}
+    reinv = {"reinversions": 0, "refine_tries": 0, "refinements": 0, "refine_steps": 0, "refine_resid_max": 0.0}
     for _ in range(steps):
         it0 = P.it_cnt
         gk.glp_simplex(P, parm)
@@ -44,12 +47,17 @@ def main():
         split["eval"] += s.seconds_eval
         split["batches"] += s.seconds_batches
         split["reinvert"] += s.seconds_reinvert
+        for k in ("reinversions", "refine_tries", "refinements", "refine_steps"):
+            reinv[k] += getattr(s, k)
+        reinv["refine_resid_max"] = max(reinv["refine_resid_max"], s.refine_resid_max)
     dt = time.perf_counter() - t0
     ctx.mark(2)
-    print(json.dumps({"start": warm, "pivots": piv, "seconds": round(dt, 4), "pivots_per_s": round(piv / dt, 1),
+    print(json.dumps({"start": warm, "advance_seconds": round(t_adv, 2), "pivots": piv, "seconds": round(dt, 4), "pivots_per_s": round(piv / dt, 1),
                       "bytes_per_pivot": round(byts / max(piv, 1)),
                       "GBps_algorithmic": round(byts / dt / 1e9, 1),
-                      "ms_split": {k: round(1000 * v, 2) for k, v in split.items()}}), flush=True)
+                      "ms_split": {k: round(1000 * v, 2) for k, v in split.items()},
+                      "ms_per_reinversion": round(1000 * split["reinvert"] / max(reinv["reinversions"], 1), 2),
+                      "newton_min_k": os.environ.get("GK_NEWTON_MIN_K", "default (1024)"), **reinv}), flush=True)
 
 
 if __name__ == "__main__":
