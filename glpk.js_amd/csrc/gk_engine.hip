@@ -361,8 +361,10 @@ static int reinvert_core(gk_bfd *f, const BasisSplit &bs, const MatDev *Adense, 
         if (refine && f->valid && !f->ext_upd && newton_min_k() > 0 && k >= newton_min_k()) {
             f->nwt_bits.ensure(1);
             NewtonInfo ni;
+            // C sits in the first k^2 of X; the second half holds the
+            // column-major copy of the iterate
             cinv = newton_refine(s, k, f->X.p, f->Binv.p, f->ldb, d_posJ, d_rowR, f->CinvR.p, f->Y.p,
-                                 f->Y.p + (size_t)k * k, f->nwt_bits.p, &ni);
+                                 f->Y.p + (size_t)k * k, f->X.p + (size_t)k * k, f->nwt_bits.p, &ni);
             f->stats.refine_tries++;
             f->stats.refine_resid_max = std::max(f->stats.refine_resid_max, ni.resid);
             if (cinv) {

@@ -264,7 +264,7 @@ void gemm_bs_cinv(hipStream_t s, const double *BS, int ms, int k, const double *
 void assemble_binv(hipStream_t s, double *Binv, int m, int ldb, int k, int ms, const int *posJ, const int *rowR,
                    const int *posS, const int *rowS, const double *CinvR, const double *G);
 // scheduled re-inversion by Newton refinement of the updated inverse
-// (gk_newton.hip): C column-major in C, X0 / R / X1 k x k scratch; returns
+// (gk_newton.hip): C column-major in C, X0 / R / X1 / Xc k x k scratch; returns
 // the buffer holding inv(C) in the CinvR layout, or nullptr (use Gauss-Jordan)
 struct NewtonInfo {
     int steps = 0;
@@ -273,8 +273,8 @@ struct NewtonInfo {
 };
 int newton_min_k();
 const double *newton_refine(hipStream_t s, int k, const double *C, const double *Binv, int ldb, const int *posJ,
-                            const int *rowR, double *X0, double *R, double *X1, unsigned long long *rbits,
-                            NewtonInfo *info);
+                            const int *rowR, double *X0, double *R, double *X1, double *Xc,
+                            unsigned long long *rbits, NewtonInfo *info);
 
 // basic helpers
 void vec_axpy(hipStream_t s, double *y, const double *x, double a, int n);

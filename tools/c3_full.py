@@ -37,12 +37,16 @@ def main():
         st = P.stats()
         steps.append({"pivots": P.it_cnt - it0, "seconds": round(time.perf_counter() - s0, 3),
                       "reinversions": st.reinversions, "s_reinvert": round(st.seconds_reinvert, 3),
+                      "refinements": st.refinements,
                       "bytes_per_pivot": round(st.bytes_pivots / max(1, st.pivots))})
         print(json.dumps({"it_cnt": P.it_cnt, "ret": ret, **steps[-1]}), flush=True)
     dt = time.perf_counter() - t0
     out = {"m": m, "n": n, "meth": meth, "ret": ret, "obj": P.obj_val, "it_cnt": P.it_cnt,
            "pbs_stat": P.pbs_stat, "dbs_stat": P.dbs_stat, "seconds": round(dt, 3),
-           "pivots_per_s": round(P.it_cnt / dt, 1)}
+           "pivots_per_s": round(P.it_cnt / dt, 1),
+           "reinversions": sum(x["reinversions"] for x in steps), "refinements": sum(x["refinements"] for x in steps),
+           "s_reinvert": round(sum(x["s_reinvert"] for x in steps), 3),
+           "newton_min_k": os.environ.get("GK_NEWTON_MIN_K", "default (1024)")}
     if ret == 0:
         out["kkt"] = dense_kkt(P, prob)
     gold = os.path.join(ROOT, "tests", "golden", f"dense_full_{m}x{n}.json")
