@@ -24,9 +24,14 @@ def main():
     ctx = gk.Context(0)
     P = gk.GkProblem(ctx, problems.gen_dense(4096, 16384, seed=42))
     t_adv = time.perf_counter()
+    adv = {"reinversions": 0, "refinements": 0, "s_reinvert": 0.0}
     while P.it_cnt < warm:
         ret = gk.glp_simplex(P, gk.SMCP(meth=gk.GLP_DUAL, it_lim=min(2000, warm - P.it_cnt),
                                         msg_lev=gk.GLP_MSG_ERR))
+        s = P.stats()
+        adv["reinversions"] += s.reinversions
+        adv["refinements"] += s.refinements
+        adv["s_reinvert"] += s.seconds_reinvert
         print(json.dumps({"it_cnt": P.it_cnt}), flush=True)
         assert ret == 8
     t_adv = time.perf_counter() - t_adv
@@ -52,7 +57,8 @@ def main():
         reinv["refine_resid_max"] = max(reinv["refine_resid_max"], s.refine_resid_max)
     dt = time.perf_counter() - t0
     ctx.mark(2)
-    print(json.dumps({"start": warm, "advance_seconds": round(t_adv, 2), "pivots": piv, "seconds": round(dt, 4), "pivots_per_s": round(piv / dt, 1),
+    adv["s_reinvert"] = round(adv["s_reinvert"], 3)
+    print(json.dumps({"start": warm, "advance_seconds": round(t_adv, 2), "advance": adv, "pivots": piv, "seconds": round(dt, 4), "pivots_per_s": round(piv / dt, 1),
                       "bytes_per_pivot": round(byts / max(piv, 1)),
                       "GBps_algorithmic": round(byts / dt / 1e9, 1),
                       "ms_split": {k: round(1000 * v, 2) for k, v in split.items()},
