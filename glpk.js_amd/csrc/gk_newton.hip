@@ -19,7 +19,8 @@
 // (k * r < 1/2, the infinity norm of R bounded by k max |R|), and is repeated
 // until that bound, squared, is below k eps; anything else — a NaN, a residual that does not
 // shrink, three steps — hands the block back to Gauss-Jordan (the caller
-// still holds C untouched).  Only the engine's scheduled re-inversions (update
+// still holds C untouched).  Size threshold k >= GK_NEWTON_MIN_K (512).
+// Only the engine's scheduled re-inversions (update
 // count reached, no growth-check failure since the last one) use it: the
 // factor's own entry point (gk_bfd_factorize) and every recovery re-inversion
 // (check_stab, pivot checks, growth) stay with Gauss-Jordan from C.
@@ -222,7 +223,7 @@ static void nwt_update(hipStream_t s, int k, const double *X, const double *Xc, 
 int newton_min_k()
 {
     const char *e = std::getenv("GK_NEWTON_MIN_K");
-    return e ? std::atoi(e) : 1024;
+    return e ? std::atoi(e) : 512;
 }
 
 const double *newton_refine(hipStream_t s, int k, const double *C, const double *Binv, int ldb, const int *posJ,

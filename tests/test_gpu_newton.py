@@ -3,7 +3,7 @@
 
 The refinement replaces Gauss-Jordan only at the engine's scheduled
 re-inversions (the update limit, the device counterpart of nfs_max,
-glpfhv.js:182-187); GK_NEWTON_MIN_K lowers its size threshold (default 1024)
+glpfhv.js:182-187); GK_NEWTON_MIN_K lowers its size threshold (default 512)
 so that the small fixtures take it at every such point.  The bar is the one
 of test_gpu_lp.py: the reference's return code, statuses and objective to
 1e-9 relative; the counters show the refinement ran and converged."""

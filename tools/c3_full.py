@@ -46,7 +46,7 @@ def main():
            "pivots_per_s": round(P.it_cnt / dt, 1),
            "reinversions": sum(x["reinversions"] for x in steps), "refinements": sum(x["refinements"] for x in steps),
            "s_reinvert": round(sum(x["s_reinvert"] for x in steps), 3),
-           "newton_min_k": os.environ.get("GK_NEWTON_MIN_K", "default (1024)")}
+           "newton_min_k": os.environ.get("GK_NEWTON_MIN_K", "default (512)")}
     if ret == 0:
         out["kkt"] = dense_kkt(P, prob)
     gold = os.path.join(ROOT, "tests", "golden", f"dense_full_{m}x{n}.json")

@@ -63,7 +63,7 @@ def main():
                       "GBps_algorithmic": round(byts / dt / 1e9, 1),
                       "ms_split": {k: round(1000 * v, 2) for k, v in split.items()},
                       "ms_per_reinversion": round(1000 * split["reinvert"] / max(reinv["reinversions"], 1), 2),
-                      "newton_min_k": os.environ.get("GK_NEWTON_MIN_K", "default (1024)"), **reinv}), flush=True)
+                      "newton_min_k": os.environ.get("GK_NEWTON_MIN_K", "default (512)"), **reinv}), flush=True)
 
 
 if __name__ == "__main__":
