@@ -384,7 +384,7 @@ def main():
                     line["extra"] = {"error": f"multi-rank B&B leg exceeded {EXTRA_MULTI_S:.0f} s"}
                     print(json.dumps(line), flush=True)
                 sys.stderr.flush()
-                os._exit(0)
+                os._exit(3)            # a hang is a failure: non-zero exit after the line
 
             dog = threading.Timer(EXTRA_MULTI_S, _expire)
             dog.daemon = True

@@ -29,6 +29,7 @@
 #include <cerrno>
 #include <cfloat>
 #include <chrono>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <thread>
@@ -89,10 +90,20 @@ bool recv_all(int fd, void *p, size_t n)
     return true;
 }
 
+// data links: no Nagle delay, and a receive timeout (GK_COMM_TIMEOUT_S,
+// default 600 s) so that a rank whose peer died or left the collective
+// sequence gets an error return instead of blocking forever
 void nodelay(int fd)
 {
     int one = 1;
     (void)setsockopt(fd, IPPROTO_TCP, TCP_NODELAY, &one, sizeof one);
+    static const int tmo = [] {
+        const char *e = std::getenv("GK_COMM_TIMEOUT_S");
+        const int v = e ? std::atoi(e) : 600;
+        return v > 0 ? v : 600;
+    }();
+    timeval tv{tmo, 0};
+    (void)setsockopt(fd, SOL_SOCKET, SO_RCVTIMEO, &tv, sizeof tv);
 }
 
 }  // namespace
@@ -101,6 +112,7 @@ struct gk_comm {
     int rank = 0, size = 1, backend = GK_COMM_TCP;
     int ramp_nodes = 0, sync_every = 0;  // gk_comm_set_option: the sharded driver's ramp-up and epoch length
     int device = -1;
+    bool failed = false;                  // a collective of this communicator returned an error
     std::vector<int> fds;                 // rank 0: fds[r] for r >= 1; others: fds[0] = the link to rank 0
     // RCCL
     Rccl rccl;
@@ -219,8 +231,22 @@ extern "C" gk_comm *gk_comm_create(gk_ctx *ctx, int rank, int size, const char *
             return nullptr;
         }
     }
-    // RCCL when every rank has a device of its own (auto) or when asked
+    // RCCL when every rank has a device of its own (auto) or when asked; a
+    // one-rank communicator takes RCCL only when asked (ncclCommInitRank with
+    // nranks = 1 is valid: the transport check of a single process)
     c->backend = GK_COMM_TCP;
+    if (size == 1 && backend == GK_COMM_RCCL) {
+        ncclUniqueId id;
+        if (c->device < 0 || !c->rccl.load() || c->rccl.get_id(&id) != ncclSuccess ||
+            hipSetDevice(c->device) != hipSuccess ||
+            hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
+            c->rccl.init(&c->nc, 1, id, 0) != ncclSuccess) {
+            set_err("gk_comm_create: one-rank RCCL communicator could not be created");
+            delete c;
+            return nullptr;
+        }
+        c->backend = GK_COMM_RCCL;
+    }
     if (size > 1 && backend != GK_COMM_TCP) {
         std::vector<int> devs(size);
         int mine[2] = {c->device, 0};
@@ -278,11 +304,20 @@ extern "C" void gk_comm_destroy(gk_comm *c) { delete c; }
 
 extern "C" int gk_comm_backend(const gk_comm *c) { return c ? c->backend : -1; }
 
+static int comm_allgather(gk_comm *c, const void *send, size_t bytes, void *recv);
+
 extern "C" int gk_comm_allgather(void *comm, const void *send, size_t bytes, void *recv)
 {
     gk_comm *c = (gk_comm *)comm;
     if (!c || (!send && bytes) || (!recv && bytes)) return 1;
-    if (c->size == 1) {
+    const int r = comm_allgather(c, send, bytes, recv);
+    if (r) c->failed = true;
+    return r;
+}
+
+static int comm_allgather(gk_comm *c, const void *send, size_t bytes, void *recv)
+{
+    if (c->size == 1 && c->backend != GK_COMM_RCCL) {
         std::memcpy(recv, send, bytes);
         return 0;
     }
@@ -324,7 +359,7 @@ extern "C" int gk_ios_driver_comm(gk_ctx *ctx, gk_mip *mip, const gk_iocp *parm,
 {
     using gk::set_err;
     if (!comm) { set_err("gk_ios_driver_comm: null communicator"); return GK_EABI; }
-    if (comm->size == 1) return gk_ios_driver(ctx, mip, parm);
+    if (comm->size == 1 && comm->backend != GK_COMM_RCCL) return gk_ios_driver(ctx, mip, parm);
     gk_ios_shard sh{};
     sh.rank = comm->rank;
     sh.size = comm->size;
@@ -334,7 +369,13 @@ extern "C" int gk_ios_driver_comm(gk_ctx *ctx, gk_mip *mip, const gk_iocp *parm,
     sh.info = comm;
     sh.allgather = gk_comm_allgather;
     const int ret = gk_ios_driver_sharded(ctx, mip, parm, &sh);
-    if (ret == GK_EABI) return ret;
+    // a local failure inside the search reaches the other ranks through the
+    // sync epoch (every rank leaves the search together); this rank still
+    // joins the final all-gather, with its error in h[2], so that no peer
+    // waits for it.  After a failed collective the sequence is lost: return.
+    if (ret == GK_EABI && comm->failed) return ret;
+    std::string my_err;
+    if (ret == GK_EABI) my_err = gk_last_error();
     const int m = mip->lp.m, n = mip->lp.n;
     const size_t blk = 4 * sizeof(double) + ((size_t)m + n) * sizeof(double);
     std::vector<char> me(blk, 0), all(blk * comm->size);
@@ -350,6 +391,15 @@ extern "C" int gk_ios_driver_comm(gk_ctx *ctx, gk_mip *mip, const gk_iocp *parm,
         set_err("gk_ios_driver_comm: final all-gather failed");
         return GK_EABI;
     }
+    if (ret == GK_EABI) {
+        set_err("%s", my_err.c_str());
+        return ret;
+    }
+    for (int r = 0; r < comm->size; r++)
+        if ((int)((const double *)(all.data() + (size_t)r * blk))[2] == GK_EABI) {
+            set_err("gk_ios_driver_comm: rank %d failed", r);
+            return GK_EABI;
+        }
     const double sign = (mip->lp.dir == 1) ? 1.0 : -1.0;               // GLP_MIN
     int win = -1, worst_ret = 0;
     bool any_partial = false;

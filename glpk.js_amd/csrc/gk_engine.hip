@@ -274,6 +274,8 @@ struct gk_bfd {
     // left at its default): adapted to the reduced-cost / primal drift measured
     // at every re-inversion (Spx::drift_adapt); 0 = not set yet
     int upd_lim_adapt = 0;
+    int clean_runs = 0;                   // consecutive drift measurements below tol / 200
+    bool parm_default = true;             // no glp_set_bfcp: the interval is the engine's (gk_bfd_reset_parm)
     unsigned long long fact_ver = 0;           // bumped whenever inv(B) is rebuilt or updated outside a solve
     int ext_upd = 0;                           // updated through gk_bfd_update since the last re-inversion
     int prof = 0;                              // gk_bfd_profile
@@ -1364,9 +1366,20 @@ struct Spx {
         double D = 0.0;
         for (int j = 1; j <= cnt; j++)
             if (!dual || stat[j] != NS) D = std::max(D, std::fabs(fresh[j] - drift_ref[j]));
+        // conservative in both directions: a drift above tol / 20 drops the
+        // chain to the floor (nfs_max), one above tol / 200 halves it, and it
+        // doubles only after two consecutive full-length chains below tol / 200
         int lim = f->upd_lim_adapt > 0 ? f->upd_lim_adapt : upd_cap;
-        if (D > 0.05 * tol) lim = std::max(upd_floor, std::min(lim, drift_upd) / 2);
-        else if (D < 0.005 * tol && drift_upd >= lim) lim = std::min(upd_cap, 2 * lim);
+        if (D > 0.05 * tol) {
+            lim = upd_floor;
+            f->clean_runs = 0;
+        } else if (D > 0.005 * tol) {
+            lim = std::max(upd_floor, std::min(lim, drift_upd) / 2);
+            f->clean_runs = 0;
+        } else if (drift_upd >= lim && ++f->clean_runs >= 2) {
+            lim = std::min(upd_cap, 2 * lim);
+            f->clean_runs = 0;
+        }
         static const bool log = std::getenv("GK_DRIFT_LOG") != nullptr;
         if (log)
             fprintf(stderr, "[gk drift] %s it %d: %d updates, drift %.3e (tol %.1e) -> interval %d (growth checks %d, "
@@ -1628,9 +1641,11 @@ void Spx::init()
     // is rebuilt, glpbfd.js via lpf_create_it(nrs_max) and LPF_ELIMIT)
     const int nfs = upd_limit_parm(f->parm);
     int lim = nfs;
-    if (nfs == 100) {
+    if (f->parm_default) {
+        // the chain starts at the reference's nfs_max and grows only on
+        // measured clean intervals (drift_adapt)
         upd_cap = std::max(nfs, std::min(1000, m / 4));
-        if (f->upd_lim_adapt <= 0) f->upd_lim_adapt = upd_cap;
+        if (f->upd_lim_adapt <= 0) f->upd_lim_adapt = nfs;
         lim = std::min(std::max(f->upd_lim_adapt, nfs), upd_cap);
     } else
         upd_cap = nfs;
@@ -2318,6 +2333,26 @@ int gk_bfd_set_parm(gk_bfd *f, const gk_bfcp *parm)
     if (b.rs_size < 0) { set_err("glp_set_bfcp: rs_size = %d; invalid parameter", b.nrs_max); return GK_EABI; }
     f->parm = b;
     if (f->parm.rs_size == 0) f->parm.rs_size = 20 * f->parm.nrs_max;
+    // explicit parameters (glp_set_bfcp with a parm): nfs_max / nrs_max are
+    // honoured exactly, whatever their value — 100 included
+    f->parm_default = false;
+    f->upd_lim_adapt = 0;
+    f->clean_runs = 0;
+    return 0;
+}
+
+// glp_set_bfcp(lp, NULL) (glpapi12.js:135-139) / a factor whose problem has
+// no bfcp of its own: the defaults of glp_get_bfcp, with the re-inversion
+// interval left to the engine's drift measurement (gk_engine.hip drift_adapt)
+int gk_bfd_reset_parm(gk_bfd *f)
+{
+    if (!f) { set_err("gk_bfd_reset_parm: null argument"); return GK_EABI; }
+    f->parm.type = 1; f->parm.lu_size = 0; f->parm.piv_tol = 0.10; f->parm.piv_lim = 4; f->parm.suhl = 1;
+    f->parm.eps_tol = 1e-15; f->parm.max_gro = 1e10; f->parm.nfs_max = 100; f->parm.upd_tol = 1e-6;
+    f->parm.nrs_max = 100; f->parm.rs_size = 0;
+    f->parm_default = true;
+    f->upd_lim_adapt = 0;
+    f->clean_runs = 0;
     return 0;
 }
 

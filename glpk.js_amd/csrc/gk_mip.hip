@@ -1520,7 +1520,7 @@ static void setup_rounding(MipSolver &S, const gk_mip *mip)
 struct ShardMsg {
     double best, bound;
     long long open;
-    int active, pad;
+    int active, err;          // err: this rank's search failed (every rank then stops at this epoch)
 };
 constexpr int XFER_MAX = 32;
 
@@ -1558,8 +1558,16 @@ static void get_desc(MipSolver &S, const char *p)
 }
 
 // one sync epoch; returns the number of ranks with work (0 ends the run) or
-// -1 when a collective failed
-static int shard_epoch(MipSolver &S, const gk_ios_shard *sh, bool have_work, long long &moved)
+// -1 when a collective failed.  Every stop decision is taken from the
+// gathered blocks, which are the same on every rank, so all ranks leave the
+// loop at the same epoch and meet again in gk_ios_driver_comm's final
+// all-gather: a rank whose search failed (local_err) ends the epoch for all
+// (peer_err on the others), and the relative mip gap (glpios03.js:613-620)
+// is tested on the global incumbent against the global best open bound —
+// only while some rank still holds open nodes (the reference tests it for a
+// selected subproblem, never on an empty tree, glpios03.js:522-528)
+static int shard_epoch(MipSolver &S, const gk_ios_shard *sh, bool have_work, long long &moved, bool local_err,
+                       double mip_gap, bool &gap_stop, bool &peer_err)
 {
     const int size = sh->size, rank = sh->rank;
     ShardMsg me{};
@@ -1567,17 +1575,33 @@ static int shard_epoch(MipSolver &S, const gk_ios_shard *sh, bool have_work, lon
     me.bound = DBL_MAX;
     for (const NodeRec &r : S.open) me.bound = std::min(me.bound, r.bound);
     for (const NodeRec &r : S.dive) me.bound = std::min(me.bound, r.bound);
-    me.open = (long long)S.open.size();
-    me.active = have_work ? 1 : 0;
+    me.open = (long long)(S.open.size() + S.dive.size());
+    me.active = (have_work && !local_err) ? 1 : 0;
+    me.err = local_err ? 1 : 0;
     std::vector<ShardMsg> all(size);
     if (sh->allgather(sh->info, &me, sizeof me, all.data()) != 0) return -1;
-    int nact = 0;
-    double gb = DBL_MAX;
+    int nact = 0, nerr = 0;
+    long long nopen = 0;
+    double gb = DBL_MAX, gbound = DBL_MAX;
     for (const ShardMsg &x : all) {
         nact += x.active;
+        nerr += x.err;
+        nopen += x.open;
         gb = std::min(gb, x.best);
+        if (x.open > 0) gbound = std::min(gbound, x.bound);
     }
     S.set_gbest(gb);
+    if (nerr > 0) {
+        peer_err = !local_err;
+        return 0;
+    }
+    if (mip_gap > 0.0 && gb < DBL_MAX && nopen > 0) {
+        const double bm = S.c0 + S.sign * gb, bb = S.c0 + S.sign * gbound;
+        if (std::fabs(bm - bb) / (std::fabs(bm) + DBL_EPSILON) <= mip_gap) {
+            gap_stop = true;
+            return 0;
+        }
+    }
     if (nact == 0) return 0;
     // the plan (identical on every rank)
     std::vector<int> idle, donors;
@@ -1990,15 +2014,22 @@ extern "C" int gk_ios_driver_sharded(gk_ctx *ctx, gk_mip *mip, const gk_iocp *pa
         tm_lag = std::chrono::steady_clock::now();
         lag_set = true;
     };
+    // DBL_MAX (no stop) without an incumbent or once the tree is empty: the
+    // reference ends an exhausted search with GLP_OPT before any gap test
+    // (glpios03.js:522-528) and tests the gap only for a selected subproblem
     auto rel_gap = [&]() {
         if (!S.have) return DBL_MAX;
         double bnd;
-        if (active(bnd) == 0) return 0.0;
+        if (active(bnd) == 0) return DBL_MAX;
         const double bm = S.c0 + S.sign * S.best, bb = S.c0 + S.sign * bnd;
         return std::fabs(bm - bb) / (std::fabs(bm) + DBL_EPSILON);
     };
+    bool peer_err = false;
+    const bool sharded = size > 1 && shard && shard->allgather;
     for (;;) {
-        if (fail_sync || S.err) break;
+        // a failed rank of a sharded search leaves at the next epoch, with
+        // the others (shard_epoch), not on its own
+        if ((fail_sync || S.err) && !(sharded && split_done)) break;
         if (rpt_on) {
             if (S.bingos) { S.bingos = 0; report(1); }
             // every out_frq milliseconds (glpios03.js:603-607; the first line at the root)
@@ -2006,8 +2037,9 @@ extern "C" int gk_ios_driver_sharded(gk_ctx *ctx, gk_mip *mip, const gk_iocp *pa
                                 1000.0 * std::chrono::duration<double>(std::chrono::steady_clock::now() - tm_lag).count())
                 report(0);
         }
-        // the relative mip gap (glpios03.js:613-620)
-        if (parm->mip_gap > 0.0 && S.have && rel_gap() <= parm->mip_gap) {
+        // the relative mip gap (glpios03.js:613-620); a sharded search
+        // tests it on the global incumbent and bound inside shard_epoch
+        if (size == 1 && parm->mip_gap > 0.0 && S.have && rel_gap() <= parm->mip_gap) {
             gap_hit = true;
             drain();
             if (rpt_on && S.bingos) { S.bingos = 0; report(1); }
@@ -2015,7 +2047,7 @@ extern "C" int gk_ios_driver_sharded(gk_ctx *ctx, gk_mip *mip, const gk_iocp *pa
             break;
         }
         const bool any_inflight = inflight[0] || inflight[1];
-        bool have_work = !S.open.empty() || !S.dive.empty() || !S.probeq.empty() || any_inflight;
+        bool have_work = !S.err && !fail_sync && (!S.open.empty() || !S.dive.empty() || !S.probeq.empty() || any_inflight);
         if (have_work && parm->tm_lim < 0x7fffffff &&
             std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() * 1000.0 >= parm->tm_lim) {
             timed_out = true;
@@ -2046,8 +2078,16 @@ extern "C" int gk_ios_driver_sharded(gk_ctx *ctx, gk_mip *mip, const gk_iocp *pa
             since_sync = 0;
             if (shard->allgather) {
                 if (!have_work) drain();
-                const int act = shard_epoch(S, shard, have_work, moved);
+                bool gstop = false;
+                const int act = shard_epoch(S, shard, have_work, moved, S.err != 0 || fail_sync, parm->mip_gap, gstop,
+                                            peer_err);
                 if (act < 0) { set_err("gk_ios_driver: shard all-gather failed"); return GK_EABI; }
+                if (gstop) {
+                    gap_hit = true;
+                    drain();
+                    if (rpt_on && S.bingos) { S.bingos = 0; report(1); }
+                    release_all();
+                }
                 if (act == 0) break;
                 have_work = !S.open.empty() || !S.dive.empty() || !S.probeq.empty() || inflight[0] || inflight[1];
                 if (!have_work) continue;
@@ -2111,7 +2151,7 @@ extern "C" int gk_ios_driver_sharded(gk_ctx *ctx, gk_mip *mip, const gk_iocp *pa
         set_err("gk_ios_driver: node batch failed: %s", hipGetErrorString(hipGetLastError()));
         return GK_EABI;
     }
-    if (S.err) {                                          // the reference's "unable to solve current LP relaxation"
+    if (S.err || peer_err) {                              // the reference's "unable to solve current LP relaxation"
         drain();
         release_all();
     }
@@ -2138,16 +2178,17 @@ extern "C" int gk_ios_driver_sharded(gk_ctx *ctx, gk_mip *mip, const gk_iocp *pa
     mip->pp_fathomed = S.pp_fathomed;
     mip->nodes_moved = moved;
     if (S.have) {
-        mip->mip_stat = (timed_out || S.err || gap_hit) ? 2 : 5;     // GLP_FEAS / GLP_OPT
+        mip->mip_stat = (timed_out || S.err || gap_hit || peer_err) ? 2 : 5;     // GLP_FEAS / GLP_OPT
         mip->mip_obj = S.c0 + S.sign * S.best;
         for (int i = 0; i < m; i++) mip->row_mipx[i + 1] = S.xbest[i];
         for (int j = 0; j < n; j++)
             mip->col_mipx[j + 1] = S.isint[j] ? std::floor(S.xbest[m + j] + 0.5) : S.xbest[m + j];
     } else {
-        mip->mip_stat = (timed_out || S.err) ? 1 : 4;     // GLP_UNDEF / GLP_NOFEAS
+        mip->mip_stat = (timed_out || S.err || peer_err) ? 1 : 4;     // GLP_UNDEF / GLP_NOFEAS
         mip->mip_obj = 0.0;
     }
     if (S.err) return S.err;                              // GLP_EFAIL
+    if (peer_err) return 0x05;                            // another rank's GLP_EFAIL ends this one's search too
     if (gap_hit) return 0x0E;                             // GLP_EMIPGAP
     return timed_out ? 0x09 : 0;                          // GLP_ETMLIM
 }

@@ -108,7 +108,7 @@ class SpxStats(C.Structure):
 _lib = None
 
 EXPORTS = ["gk_abi_version", "gk_device_count", "gk_ctx_create", "gk_ctx_destroy", "gk_last_error",
-           "gk_bfd_create", "gk_bfd_destroy", "gk_bfd_set_parm", "gk_bfd_factorize", "gk_bfd_factorize_csc",
+           "gk_bfd_create", "gk_bfd_destroy", "gk_bfd_set_parm", "gk_bfd_reset_parm", "gk_bfd_factorize", "gk_bfd_factorize_csc",
            "gk_bfd_ftran", "gk_bfd_btran", "gk_bfd_update", "gk_bfd_get_count", "gk_bfd_valid",
            "gk_spx_primal", "gk_spx_dual", "gk_bfd_last_stats", "gk_bfd_profile", "gk_ios_driver",
            "gk_scale_prob", "gk_scale_prob_timed", "gk_adv_basis", "gk_bfd_set_report",
@@ -145,6 +145,8 @@ def load_library(path: str = LIB_PATH):
     L.gk_bfd_destroy.argtypes = [P]
     L.gk_bfd_set_parm.argtypes = [P, C.POINTER(Bfcp)]
     L.gk_bfd_set_parm.restype = C.c_int
+    L.gk_bfd_reset_parm.argtypes = [P]
+    L.gk_bfd_reset_parm.restype = C.c_int
     L.gk_bfd_factorize_csc.argtypes = [P, C.c_int, P, P, P]
     L.gk_bfd_factorize_csc.restype = C.c_int
     L.gk_bfd_ftran.argtypes = [P, P]
@@ -336,7 +338,14 @@ class GkProblem:
             self.bfd = None
 
     def set_bfcp(self, **kw):
-        """glp_set_bfcp (glpapi12.js:133)."""
+        """glp_set_bfcp (glpapi12.js:133).  With no arguments (glp_set_bfcp(lp,
+        NULL)): the defaults, re-inversion interval left to the engine; with
+        any argument the values hold exactly (nfs_max = 100 included)."""
+        if not kw:
+            if self.L.gk_bfd_reset_parm(self.bfd) != 0:
+                raise GkError(_err(self.L))
+            self.bfcp = None
+            return
         b = Bfcp(type=1, lu_size=0, piv_tol=0.10, piv_lim=4, suhl=1, eps_tol=1e-15, max_gro=1e10,
                  nfs_max=100, upd_tol=1e-6, nrs_max=100, rs_size=0)
         for k, v in kw.items():
@@ -804,7 +813,7 @@ def _intopt_run(P: GkProblem, parm: Iocp, comm, ramp_nodes: int) -> int:
     mip.col_kind = ptr(P.col_kind)
     mip.col_mipx = ptr(P.col_mipx)
     mip.row_mipx = ptr(P.row_mipx)
-    if isinstance(comm, Comm) and comm.size > 1:
+    if isinstance(comm, Comm) and (comm.size > 1 or comm.backend == GK_COMM_RCCL):
         # the library's own collective: the sharded search and the agreement
         # on the winning incumbent in C (gk_ios_driver_comm)
         P.L.gk_comm_set_option(comm.h, 1, int(ramp_nodes))

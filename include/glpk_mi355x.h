@@ -40,7 +40,7 @@
 extern "C" {
 #endif
 
-#define GK_ABI_VERSION 7
+#define GK_ABI_VERSION 8
 #include <stddef.h>
 #define GK_EABI (-1)          /* contract violation; see gk_last_error() */
 
@@ -82,6 +82,13 @@ typedef int (*gk_col_fn)(void *info, int j, int *ind, double *val);
 gk_bfd *gk_bfd_create(gk_ctx *ctx);
 void    gk_bfd_destroy(gk_bfd *bfd);
 int     gk_bfd_set_parm(gk_bfd *bfd, const gk_bfcp *parm);   /* 0 | GK_EABI (invalid field) */
+/* glp_set_bfcp(lp, NULL) / copy_bfcp of a problem without a bfcp of its own
+ * (glpapi12.js:127-139): the glp_get_bfcp defaults, with the re-inversion
+ * interval left to the engine (it starts at nfs_max = 100 and lengthens
+ * only over measured clean intervals).  gk_bfd_set_parm marks its values
+ * explicit: nfs_max / nrs_max then hold exactly, 100 included.  A new
+ * factor starts in the default state.  (ABI 8) */
+int     gk_bfd_reset_parm(gk_bfd *bfd);
 /* 0 | BFD_ESING(1) | BFD_ECOND(2); col(info, j, ind, val) fills column j of B
  * exactly like b_col/inv_col (glpapi12.js:7, glpspx01.js:147). */
 int     gk_bfd_factorize(gk_bfd *bfd, int m, gk_col_fn col, void *info);

@@ -231,6 +231,17 @@ static napi_value js_bfd_set_parm(napi_env env, napi_callback_info info)
     return NULL;
 }
 
+/* bfdResetParm(bfd): glp_get_bfcp's defaults with the engine's re-inversion
+ * interval (copy_bfcp of a problem without lp.bfcp, glpapi12.js:127-131) */
+static napi_value js_bfd_reset_parm(napi_env env, napi_callback_info info)
+{
+    napi_value argv[1];
+    if (!get_args(env, info, 1, argv)) return NULL;
+    gk_bfd *b = (gk_bfd *)get_ext(env, argv[0]);
+    if (gk_bfd_reset_parm(b) != 0) napi_throw_error(env, NULL, gk_last_error());
+    return NULL;
+}
+
 static napi_value js_bfd_factorize_csc(napi_env env, napi_callback_info info)
 {
     napi_value argv[5];
@@ -868,7 +879,7 @@ static napi_value init(napi_env env, napi_value exports)
     napi_property_descriptor d[] = {
         FN("commCreate", js_comm_create), FN("commBackend", js_comm_backend), FN("commOption", js_comm_option),
         FN("create", js_create), FN("deviceCount", js_device_count), FN("abiVersion", js_abi_version),
-        FN("lastError", js_last_error), FN("bfdCreate", js_bfd_create), FN("bfdSetParm", js_bfd_set_parm),
+        FN("lastError", js_last_error), FN("bfdCreate", js_bfd_create), FN("bfdSetParm", js_bfd_set_parm), FN("bfdResetParm", js_bfd_reset_parm),
         FN("bfdFactorizeCsc", js_bfd_factorize_csc), FN("bfdFtran", js_bfd_ftran), FN("bfdBtran", js_bfd_btran),
         FN("bfdUpdate", js_bfd_update), FN("bfdGetCount", js_bfd_get_count), FN("bfdValid", js_bfd_valid),
         FN("spx", js_spx), FN("ios", js_ios), FN("stats", js_stats), FN("scale", js_scale),

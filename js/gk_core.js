@@ -47,6 +47,7 @@ function bfdCreate() {
 }
 
 function bfdSetParm(bfd, parm) { addon.bfdSetParm(bfd.gk, parm); }
+function bfdResetParm(bfd) { addon.bfdResetParm(bfd.gk); }
 
 // bfd_factorize(bfd, m, bh, col, info) (glpbfd.js:47): the columns come from
 // the reference's own callback col(info, j, ind, val) (b_col, glpapi12.js:7)
@@ -300,7 +301,7 @@ function iosDriver(T, print) {
 
 module.exports = {
     addon: addon, context: context, nextVersion: nextVersion,
-    bfdCreate: bfdCreate, bfdSetParm: bfdSetParm, bfdFactorize: bfdFactorize,
+    bfdCreate: bfdCreate, bfdSetParm: bfdSetParm, bfdResetParm: bfdResetParm, bfdFactorize: bfdFactorize,
     bfdFtran: bfdFtran, bfdBtran: bfdBtran, bfdUpdate: bfdUpdate, bfdGetCount: bfdGetCount,
     spx: spx, iosDriver: iosDriver, nativeIos: nativeIos, GLP_BS: GLP_BS, mipProgressLine: mipProgressLine,
     comm: comm

@@ -12,6 +12,16 @@ spx_primal = function (lp, parm) { return __gk.spx(lp, parm, false, xprintf); };
 spx_dual = function (lp, parm) { return __gk.spx(lp, parm, true, xprintf); };
 bfd_create_it = function () { return __gk.bfdCreate(); };
 bfd_set_parm = function (bfd, parm) { __gk.bfdSetParm(bfd, parm); };
+// copy_bfcp (glpapi12.js:127-131, from glp_factorize and glp_set_bfcp): a
+// problem with its own bfcp (glp_set_bfcp called with a parm) hands over
+// exact values — nfs_max = 100 included; one without hands over the
+// defaults, the re-inversion interval then left to the engine
+copy_bfcp = function (lp) {
+    if (lp.bfcp == null) { __gk.bfdResetParm(lp.bfd); return; }
+    var parm = {};
+    glp_get_bfcp(lp, parm);
+    __gk.bfdSetParm(lp.bfd, parm);
+};
 bfd_factorize = function (bfd, m, bh, col, info) { return __gk.bfdFactorize(bfd, m, bh, col, info); };
 bfd_ftran = function (bfd, x) { __gk.bfdFtran(bfd, x); };
 bfd_btran = function (bfd, x) { __gk.bfdBtran(bfd, x); };

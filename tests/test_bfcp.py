@@ -124,3 +124,29 @@ def test_gpu_update_limit_follows_bfcp(gpu_ctx):
         assert ret in (0, problems.GLP_EITLIM)
         # the factor glp_factorize made counts as the first one (not a re-inversion)
         assert st.reinversions >= (P.it_cnt - 1) // lim, (kw, st.reinversions, P.it_cnt)
+
+
+@pytest.mark.gpu
+def test_gpu_explicit_nfs_max_100_is_exact(gpu_ctx):
+    """An explicit glp_set_bfcp(nfs_max = 100) — the reference's default
+    value, set by the user — is honoured exactly: dense 512x2048 (where the
+    engine's own interval could grow to m / 4 = 128) re-inverts at least
+    every 100 updates.  Without glp_set_bfcp (or after glp_set_bfcp(NULL))
+    the interval is the engine's: it starts at 100 and lengthens only over
+    measured clean chains (gk_engine.hip drift_adapt), never past m / 4."""
+    from glpk_js_amd import gk
+    d = load_golden(os.path.join(os.path.dirname(__file__), "golden", "lp_dense_512x2048.json"))
+    P = gk.GkProblem(gpu_ctx, problems.from_fixture(d))
+    P.set_bfcp(nfs_max=100)
+    ret = gk.glp_simplex(P, gk.SMCP(meth=gk.GLP_DUAL, it_lim=1000))
+    st = P.stats()
+    assert ret in (0, problems.GLP_EITLIM)
+    assert st.reinversions >= (P.it_cnt - 1) // 100, (st.reinversions, P.it_cnt)
+    Q = gk.GkProblem(gpu_ctx, problems.from_fixture(d))
+    Q.set_bfcp(nfs_max=100)
+    Q.set_bfcp()                          # glp_set_bfcp(lp, NULL): back to the engine's interval
+    ret = gk.glp_simplex(Q, gk.SMCP(meth=gk.GLP_DUAL, it_lim=1000))
+    st = Q.stats()
+    assert ret in (0, problems.GLP_EITLIM)
+    assert st.reinversions >= (Q.it_cnt - 1) // 128, (st.reinversions, Q.it_cnt)
+    print("explicit 100:", P.it_cnt, "pivots; default:", Q.it_cnt, "pivots,", st.reinversions, "re-inversions")

@@ -61,7 +61,7 @@ def test_comm_tcp_allgather_cpu(size):
             assert out[k] == want
 
 
-def _mip_worker(rank, size, port, name, ramp, q):
+def _mip_worker(rank, size, port, name, ramp, q, iocp=None):
     try:
         import sys
         root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -74,7 +74,7 @@ def _mip_worker(rank, size, port, name, ramp, q):
         comm = g.Comm(ctx, rank, size, f"127.0.0.1:{port}")
         P = g.GkProblem(ctx, pr.from_fixture(d))
         assert g.glp_simplex(P, g.SMCP(msg_lev=g.GLP_MSG_OFF)) == 0
-        ret = g.glp_intopt(P, g.IOCP(msg_lev=g.GLP_MSG_OFF), comm=comm, ramp_nodes=ramp)
+        ret = g.glp_intopt(P, g.IOCP(msg_lev=g.GLP_MSG_OFF, **(iocp or {})), comm=comm, ramp_nodes=ramp)
         q.put((rank, comm.backend, ret, P.mip_stat, P.mip_obj, P.col_mipx[1:].tolist(), P.mip_stats))
         comm.close()
     except Exception as e:
@@ -103,3 +103,84 @@ def test_gpu_sharded_bnb_library_comm(name, ramp):
         xs.append(x)
         print(name, "ramp", ramp, "rank", rank, stats)
     assert xs[0] == xs[1], "ranks disagree on the incumbent"
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name,gap", [("gap", 0.05), ("gap", 0.002), ("c5s_12x20", 0.01)])
+def test_gpu_sharded_bnb_mip_gap(name, gap):
+    """mip_gap > 0 in a sharded search: the stop is decided inside the sync
+    epoch from the gathered incumbents and open bounds, so both ranks leave
+    the search at the same epoch and meet in the final all-gather (no rank
+    stops on its local gap and leaves the other waiting).  Both return the
+    same code (0 or GLP_EMIPGAP) and incumbent, within the gap of the
+    reference's optimum."""
+    d = load_golden(os.path.join(os.path.dirname(__file__), "golden", f"mip_{name}.json"))
+    opt = d["mip"]["mip_obj"]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = free_port()
+    ps = [ctx.Process(target=_mip_worker, args=(r, 2, port, name, 0, q, {"mip_gap": gap})) for r in range(2)]
+    for p in ps:
+        p.start()
+    res = sorted([q.get(timeout=240) for _ in range(2)], key=lambda t: t[0])
+    for p in ps:
+        p.join(timeout=60)
+    assert res[0][2] == res[1][2], res
+    for rank, backend, ret, stat, obj, x, stats in res:
+        assert ret in (0, gk.GLP_EMIPGAP), (rank, ret)
+        assert stat == (problems.GLP_OPT if ret == 0 else problems.GLP_FEAS), (rank, stat)
+        assert abs(obj - opt) / (abs(obj) + 2.220446049250313e-16) <= gap + 1e-12, (rank, obj, opt)
+        if ret == 0:
+            assert abs(obj - opt) <= 1e-9 * max(1.0, abs(opt))
+    assert res[0][5] == res[1][5], "ranks disagree on the incumbent"
+
+
+@pytest.mark.gpu
+def test_gpu_rccl_one_rank_after_torch_nccl():
+    """The RCCL transport of gk_comm on hardware: torch.distributed first
+    initialises its own NCCL (= RCCL) group in this process, then a one-rank
+    gk_comm with GK_COMM_RCCL (ncclCommInitRank, nranks = 1, over the
+    library's own dlopen'd librccl) all-gathers blocks and carries a
+    glp_intopt through gk_ios_driver_comm (its final all-gather on RCCL)."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_rccl_one_rank_worker, args=(free_port(), q))
+    p.start()
+    res = q.get(timeout=240)
+    p.join(timeout=60)
+    assert res[0] == "ok", res
+    backend, blocks, ret, stat, obj, ref = res[1:]
+    assert backend == gk.GK_COMM_RCCL
+    assert blocks == [b"rccl-one-rank" * 100]
+    assert ret == 0 and stat == problems.GLP_OPT
+    assert abs(obj - ref) <= 1e-9 * max(1.0, abs(ref))
+
+
+def _rccl_one_rank_worker(port, q):
+    try:
+        import sys
+        root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+        sys.path.insert(0, root)
+        import torch
+        import torch.distributed as dist
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK="0", WORLD_SIZE="1")
+        torch.cuda.set_device(0)
+        dist.init_process_group("nccl", rank=0, world_size=1)
+        t = torch.ones(4, device="cuda")
+        dist.all_reduce(t)
+        torch.cuda.synchronize()
+        import __graft_entry__
+        __graft_entry__.load_package()
+        from glpk_js_amd import gk as g, problems as pr
+        ctx = g.Context(0)
+        comm = g.Comm(ctx, 0, 1, f"127.0.0.1:{port + 1}", g.GK_COMM_RCCL)
+        blocks = comm.allgather(b"rccl-one-rank" * 100)
+        d = load_golden(os.path.join(root, "tests", "golden", "mip_gap.json"))
+        P = g.GkProblem(ctx, pr.from_fixture(d))
+        assert g.glp_simplex(P, g.SMCP(msg_lev=g.GLP_MSG_OFF)) == 0
+        ret = g.glp_intopt(P, g.IOCP(msg_lev=g.GLP_MSG_OFF), comm=comm)
+        q.put(("ok", comm.backend, blocks, ret, P.mip_stat, P.mip_obj, d["mip"]["mip_obj"]))
+        comm.close()
+        dist.destroy_process_group()
+    except Exception as e:
+        q.put(("error", repr(e)))

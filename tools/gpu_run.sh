@@ -1,0 +1,38 @@
+#!/bin/bash
+# One GPU session through gpurun, from the repo root:
+#   /usr/local/graft/bin/gpurun --timeout 1200 -- bash tools/gpu_run.sh NAME STEP [STEP ...]
+# Output goes to gpurun_out/NAME/.  Every step runs under its own time limit
+# and the script stops at the first failure (set -e), so nothing more touches
+# the GPU after a fault, an abort or a timeout.  Steps:
+#   tests            the whole -m gpu suite (the driver's round-end command)
+#   tests:F1,F2      -m gpu tests of the named files (tests/F1 ...)
+#   k:EXPR           -m gpu tests selected by -k EXPR
+#   smoke            __graft_entry__.py smoke
+#   bench            python bench.py (defaults: the driver's command)
+#   bench:ARGS       python bench.py ARGS (commas for spaces)
+#   profile          tools/profile_round.sh (rocprofv3 stats + PMC passes)
+#   py:SCRIPT,ARGS   python3 -u SCRIPT ARGS (tools/…; commas for spaces)
+set -e
+NAME=$1; shift
+O="$PWD/gpurun_out/$NAME"
+mkdir -p "$O"
+export TMPDIR=/tmp
+PYT="python -u -m pytest -x -v --timeout 300 --timeout-method thread -m gpu"
+for step in "$@"; do
+    case "$step" in
+        tests) timeout -k 10 900 $PYT tests > "$O/tests.log" 2>&1 ;;
+        tests:*) f=${step#tests:}; timeout -k 10 900 $PYT $(echo "$f" | tr ',' '\n' | sed 's|^|tests/|') \
+                     > "$O/tests_$(echo "$f" | tr ',/' '__').log" 2>&1 ;;
+        k:*) timeout -k 10 900 $PYT tests -k "${step#k:}" > "$O/tests_k.log" 2>&1 ;;
+        smoke) timeout -k 10 300 python -u __graft_entry__.py smoke > "$O/smoke.log" 2>&1 ;;
+        bench) timeout -k 10 900 python -u bench.py > "$O/bench.json" 2> "$O/bench.err" ;;
+        bench:*) a=$(echo "${step#bench:}" | tr ',' ' ');
+                 timeout -k 10 900 python -u bench.py $a > "$O/bench_args.json" 2> "$O/bench_args.err" ;;
+        profile) bash tools/profile_round.sh "$NAME/profile" ;;
+        py:*) a=$(echo "${step#py:}" | tr ',' ' '); s=$(basename ${a%% *} .py);
+              timeout -k 10 900 python3 -u $a > "$O/$s.log" 2> "$O/$s.err" ;;
+        *) echo "unknown step $step"; exit 2 ;;
+    esac
+    echo "step $step ok"
+done
+echo done
