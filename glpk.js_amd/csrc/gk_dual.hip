@@ -825,6 +825,10 @@ __global__ void __launch_bounds__(1024) k_trow_rows(SpxDev d, int pse)
 // 0 also publishes the compact rho (rho_idx / rho_val, read by the commit),
 // the scalar state and, every 1000 pivots, the reference-space reset.
 // ---------------------------------------------------------------------------
+// NP: list entries per wave loaded in trips 1-2 (8, or 16 when ns may exceed
+// 8 per wave: the entries past them are read by a loop whose every
+// iteration is two dependent trips)
+template <int NP>
 __global__ void __launch_bounds__(1024) k_dual_row(SpxDev d, int pse, int nr_cap, int gm)
 {
     const TraceScope trace_(d, 1);
@@ -849,9 +853,9 @@ __global__ void __launch_bounds__(1024) k_dual_row(SpxDev d, int pse, int nr_cap
     Cand ce[4];
 #pragma unroll
     for (int u = 0; u < 4; ++u) ce[u] = cand_chuzr(d)[min(lane + 64 * u, gm - 1)];
-    int c0[8];
+    int c0[NP];
 #pragma unroll
-    for (int u = 0; u < 8; ++u) c0[u] = d.rlist[min(w + u * nw, m - 1)];
+    for (int u = 0; u < NP; ++u) c0[u] = d.rlist[min(w + u * nw, m - 1)];
     int pos1 = d.bind[m + min(idx, n - 1)];
     int pos2 = d.bind[min(idx, m - 1)];
     Cand cc = no_cand(0.0);
@@ -863,7 +867,7 @@ __global__ void __launch_bounds__(1024) k_dual_row(SpxDev d, int pse, int nr_cap
         if (better<0>(e, cc)) cc = e;
     }
 #pragma unroll
-    for (int u = 0; u < 8; ++u) c0[u] = (w + u * nw < nr_cap) ? c0[u] : 0;
+    for (int u = 0; u < NP; ++u) c0[u] = (w + u * nw < nr_cap) ? c0[u] : 0;
     if (w != 0 || idx >= n) pos1 = 0;
     if (w != 0 || idx >= m) pos2 = 0;
     if (stop) return;
@@ -915,9 +919,9 @@ __global__ void __launch_bounds__(1024) k_dual_row(SpxDev d, int pse, int nr_cap
     const size_t ldb = (size_t)d.ldb;
     const double *__restrict__ col = d.A.AT + min(idx, n - 1);
     const size_t ldt = (size_t)d.A.ldt;
-    double v0[8], a0[8];
+    double v0[NP], a0[NP];
 #pragma unroll
-    for (int u = 0; u < 8; ++u) {
+    for (int u = 0; u < NP; ++u) {
         const int t = w + u * nw;
         int c = c0[u];
         if (t == nr) c = kp - 1;             // the unit entry (only when kp <= m: t < ns)
@@ -954,11 +958,11 @@ __global__ void __launch_bounds__(1024) k_dual_row(SpxDev d, int pse, int nr_cap
     }
     double acc = 0.0;
 #pragma unroll
-    for (int u = 0; u < 8; ++u)
+    for (int u = 0; u < NP; ++u)
         if (w + u * nw < ns) acc += v0[u] * a0[u];
     if (lead && lane == 0) {
 #pragma unroll
-        for (int u = 0; u < 8; ++u) {
+        for (int u = 0; u < NP; ++u) {
             const int t = w + u * nw;
             if (t < ns) {
                 d.rho_idx[t] = c0[u];
@@ -968,7 +972,7 @@ __global__ void __launch_bounds__(1024) k_dual_row(SpxDev d, int pse, int nr_cap
     }
     TPH(1, 0);
     {
-        int t = w + 8 * nw;
+        int t = w + NP * nw;
         for (; t < ns; t += 4 * nw) {
             int c[4];
             double v[4], a[4];
@@ -2713,7 +2717,10 @@ void dual_iteration2(hipStream_t s, const SpxDev &d, const DualPlan &pl, hipEven
         // chuzr, rho and the pivot row in one kernel
         ncb = cdiv(std::max(m, n), 64);
         if (ev0) (void)hipEventRecord(ev0, s);
-        hipLaunchKernelGGL(k_dual_row, dim3(ncb), dim3(64 * pl.twaves), 0, s, d, pl.pse, pl.nr_cap, pl.gm);
+        if (pl.ns_cap > 8 * pl.twaves)
+            hipLaunchKernelGGL(k_dual_row<16>, dim3(ncb), dim3(64 * pl.twaves), 0, s, d, pl.pse, pl.nr_cap, pl.gm);
+        else
+            hipLaunchKernelGGL(k_dual_row<8>, dim3(ncb), dim3(64 * pl.twaves), 0, s, d, pl.pse, pl.nr_cap, pl.gm);
         if (ev1) (void)hipEventRecord(ev1, s);
     } else {
         if (!pl.rigorous && d.A.dense && m >= 1024)

@@ -1642,10 +1642,11 @@ void Spx::init()
     const int nfs = upd_limit_parm(f->parm);
     int lim = nfs;
     if (f->parm_default) {
-        // the chain starts at the reference's nfs_max and grows only on
-        // measured clean intervals (drift_adapt)
+        // the chain starts at the cap; drift_adapt drops it to nfs_max at the
+        // first measured drift above tol / 20, halves it above tol / 200 and
+        // lengthens it again only after two clean full-length chains
         upd_cap = std::max(nfs, std::min(1000, m / 4));
-        if (f->upd_lim_adapt <= 0) f->upd_lim_adapt = nfs;
+        if (f->upd_lim_adapt <= 0) f->upd_lim_adapt = upd_cap;
         lim = std::min(std::max(f->upd_lim_adapt, nfs), upd_cap);
     } else
         upd_cap = nfs;

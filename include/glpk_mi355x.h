@@ -84,8 +84,10 @@ void    gk_bfd_destroy(gk_bfd *bfd);
 int     gk_bfd_set_parm(gk_bfd *bfd, const gk_bfcp *parm);   /* 0 | GK_EABI (invalid field) */
 /* glp_set_bfcp(lp, NULL) / copy_bfcp of a problem without a bfcp of its own
  * (glpapi12.js:127-139): the glp_get_bfcp defaults, with the re-inversion
- * interval left to the engine (it starts at nfs_max = 100 and lengthens
- * only over measured clean intervals).  gk_bfd_set_parm marks its values
+ * interval left to the engine (up to min(1000, m / 4) updates while the
+ * drift measured at each re-inversion stays below tol / 200; the first
+ * drift above tol / 20 drops it to nfs_max = 100, and it lengthens again
+ * only over two clean chains).  gk_bfd_set_parm marks its values
  * explicit: nfs_max / nrs_max then hold exactly, 100 included.  A new
  * factor starts in the default state.  (ABI 8) */
 int     gk_bfd_reset_parm(gk_bfd *bfd);

@@ -132,8 +132,8 @@ def test_gpu_explicit_nfs_max_100_is_exact(gpu_ctx):
     value, set by the user — is honoured exactly: dense 512x2048 (where the
     engine's own interval could grow to m / 4 = 128) re-inverts at least
     every 100 updates.  Without glp_set_bfcp (or after glp_set_bfcp(NULL))
-    the interval is the engine's: it starts at 100 and lengthens only over
-    measured clean chains (gk_engine.hip drift_adapt), never past m / 4."""
+    the interval is the engine's (gk_engine.hip drift_adapt), never past
+    m / 4."""
     from glpk_js_amd import gk
     d = load_golden(os.path.join(os.path.dirname(__file__), "golden", "lp_dense_512x2048.json"))
     P = gk.GkProblem(gpu_ctx, problems.from_fixture(d))
