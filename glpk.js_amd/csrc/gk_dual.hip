@@ -499,6 +499,19 @@ __global__ void __launch_bounds__(TOP_WG) k_dual_top(SpxDev d, int rowpath, int 
         return;
     }
     const int p = best.idx, kp = best.aux;
+    if (rowpath == 3) {
+        // sparse factor: rho = inv(B)' e_p is the BTRAN that follows
+        // (gk_sparse.hip sp_pivot_btran), nothing of inv(B) is stored here
+        if (threadIdx.x == 0) {
+            st->p = p;
+            st->kp = kp;
+            st->delta = best.k2;
+            st->trow_max_bits = 0ull;
+            st->ns = 0;
+            st->dinf = 0;
+        }
+        return;
+    }
     if (!rowpath) {
         for (int l = threadIdx.x; l < m; l += blockDim.x) d.rho[l] = 0.0;
         __syncthreads();
@@ -2689,6 +2702,27 @@ void dual_iteration2(hipStream_t s, const SpxDev &d, const DualPlan &pl, hipEven
     const int m = d.m, n = d.n;
     const int gv = cdiv(std::max(m, n), 256), gn = cdiv(n, 256), tiles_m = cdiv(m, 512);
     int ncb = 4 * gv;                                  // 64-slot groups of the pivot row
+    if (pl.sparse) {
+        // sparse factor (gk_sparse.hip): chuzr, BTRAN of e_p, the pivot row
+        // as a CSC column pass, the ratio test (with update_gamma's A w over
+        // the CSR rows), the pick and h = -N[q], the 2-RHS FTRAN (tcol, u),
+        // the vector updates, then the Schur-complement update of the factor
+        hipLaunchKernelGGL(k_dual_top, dim3(1), dim3(TOP_WG), 0, s, d, 3, 0);
+        sp_pivot_btran(*d.sp, s, d.st, d.rho);
+        if (ev0) (void)hipEventRecord(ev0, s);
+        colpass_gated(s, d.A, CP_TROW, m, n, d.head, d.stat, d.coef, nullptr, d.rho, nullptr, d.trow, nullptr,
+                      &d.st->trow_max_bits, d.st, 0);
+        if (ev1) (void)hipEventRecord(ev1, s);
+        hipLaunchKernelGGL(k_trow_finish, dim3(gv), dim3(256), 0, s, d, pl.pse);
+        hipLaunchKernelGGL(k_dual_ratio, dim3(gn + (pl.pse ? cdiv(m, 256) : 0)), dim3(256), 0, s, d, gn, tiles_m, 0,
+                           ncb, 0, 0);
+        hipLaunchKernelGGL(k_dual_pick, dim3(1), dim3(1024), 0, s, d, pl.pse, gn, ncb);
+        sp_pivot_ftran(*d.sp, s, d.st, d.h, d.work, d.tcol, d.u, pl.pse);
+        hipLaunchKernelGGL(k_dual_commit, dim3(gv), dim3(256), 0, s, d, pl.pse, gv, tiles_m, pl.lpsu, 0,
+                           bytes_fixed(d));
+        sp_pivot_update(*d.sp, s, d.st);
+        return;
+    }
     if (pl.colpath) {
         // sparse A: four kernels, as the dense row path
         if (ev0) (void)hipEventRecord(ev0, s);
@@ -2717,10 +2751,10 @@ void dual_iteration2(hipStream_t s, const SpxDev &d, const DualPlan &pl, hipEven
         // chuzr, rho and the pivot row in one kernel
         ncb = cdiv(std::max(m, n), 64);
         if (ev0) (void)hipEventRecord(ev0, s);
-        if (pl.ns_cap > 8 * pl.twaves)
-            hipLaunchKernelGGL(k_dual_row<16>, dim3(ncb), dim3(64 * pl.twaves), 0, s, d, pl.pse, pl.nr_cap, pl.gm);
-        else
-            hipLaunchKernelGGL(k_dual_row<8>, dim3(ncb), dim3(64 * pl.twaves), 0, s, d, pl.pse, pl.nr_cap, pl.gm);
+        // (16 entries per wave in trips 1-2 measured slower on C3 — 11.6 against
+        // 9.0 us of span, profiles/r04_trace_pivot_np16_reverted.txt — than 8
+        // plus the dependent loop: k_dual_row<16> is kept for experiments)
+        hipLaunchKernelGGL(k_dual_row<8>, dim3(ncb), dim3(64 * pl.twaves), 0, s, d, pl.pse, pl.nr_cap, pl.gm);
         if (ev1) (void)hipEventRecord(ev1, s);
     } else {
         if (!pl.rigorous && d.A.dense && m >= 1024)

@@ -150,6 +150,8 @@ struct GraphEntry {
 struct Engine {
     int m = 0, n = 0, nnz = 0;
     int dense = 0, lda = 0;
+    std::vector<int> hcptr, hcind;            // host copy of the scaled CSC (sparse A: the basis factor is built from it)
+    std::vector<double> hcval;
     unsigned long long a_version = 0;
     DBuf<double> A, AT;                     // dense column-major and row-major
     int ldt = 0;
@@ -287,6 +289,10 @@ struct gk_bfd {
     DBuf<int> bptr, brow;                      // basis given as CSC (gk_bfd_factorize*)
     DBuf<double> bval;
     Engine *eng = nullptr;
+    // the sparse factor (gk_sparse.hip) in place of the explicit inverse:
+    // large sparse LPs (m > 65535, or GK_SPARSE=1), dual simplex
+    SpFactor *sp = nullptr;
+    int sparse = 0;
     gk_spx_stats stats{};
     gk_report_fn rpt = nullptr;                // progress / termination reports (gk_bfd_set_report)
     void *rpt_ud = nullptr;
@@ -587,6 +593,13 @@ static void engine_upload_matrix(gk_bfd *f, const gk_lp *lp)
     cptr[n] = t;
     ABI_REQUIRE(t == nnz, "gk_spx: A_ptr describes %d entries, nnz = %d", t, nnz);
     E.dense = ((double)nnz >= 0.5 * (double)m * (double)n) ? 1 : 0;
+    if (!E.dense) {
+        E.hcptr = cptr;
+        E.hcind = cind;
+        E.hcval = cval;
+    } else {
+        E.hcptr.clear(); E.hcind.clear(); E.hcval.clear();
+    }
     E.cptr.ensure(n + 1);
     E.cind.ensure(std::max(nnz, 1));
     E.cval.ensure(std::max(nnz, 1));
@@ -708,6 +721,7 @@ struct Spx {
         // the roofline stamps (per-block exit clocks, kernel spans, algorithmic
         // bytes) cost stores and a reduction on the critical path of every
         // pivot: they run only while a profiling mode is on (gk_bfd_profile)
+        d.sp = f->sparse ? f->sp : nullptr;
         d.tslots = E->prof ? E->tslots.p : nullptr;
         d.xslots = E->prof ? E->xslots.p : nullptr;
         d.trace = nullptr;
@@ -893,11 +907,13 @@ struct Spx {
     bool lists_ok() const { return dual || !lists_stale; }
     void ftran_(const double *x, double *y)
     {
+        if (f->sparse) { sp_ftran(*f->sp, s, x, y); return; }
         if (lists_ok() && hs.nr <= LIST_FTRAN_MAX) binv_ftran_list(s, dev(), hs.nr, x, y);
         else gemv_n(s, f->Binv.p, m, m, f->ldb, x, E->partial.p, PARTIAL_CAP, y, 1.0, nullptr, 0.0);
     }
     void btran_(const double *x, double *y)
     {
+        if (f->sparse) { sp_btran(*f->sp, s, x, y); return; }
         if (lists_ok()) binv_btran_list(s, dev(), hs.nr, x, y);
         else gemv_t(s, f->Binv.p, m, m, f->ldb, x, y, 1.0);
     }
@@ -1043,6 +1059,11 @@ struct Spx {
         const bool refine = refine_next;
         refine_next = false;
         echk_seen = hs.echk;
+        if (f->sparse) {
+            ret = sparse_reinvert();
+            fact_ret = ret;
+            return ret == 0;
+        }
         if (E->dense)
             ret = reinvert_core(f, bs, &A, 0, 1.0, nullptr, nullptr, nullptr, refine);
         else
@@ -1051,6 +1072,25 @@ struct Spx {
         return ret == 0;
     }
     int fact_ret = 0;
+    // B0 = L U of the current basis on the host (gk_sparse.hip), uploaded
+    int sparse_reinvert()
+    {
+        const double t0 = now_s();
+        int ret;
+        try {
+            ret = sp_factorize(*f->sp, s, m, head.data(), E->hcptr.data(), E->hcind.data(), E->hcval.data(),
+                               f->parm.piv_tol, f->parm.piv_lim, f->parm.eps_tol);
+        } catch (const std::exception &e) {
+            throw AbiError{e.what()};
+        }
+        f->fact_ver++;
+        f->valid = ret == 0;
+        f->upd_cnt = 0;
+        f->ext_upd = 0;
+        f->stats.reinversions++;
+        f->stats.seconds_reinvert += now_s() - t0;
+        return ret ? 1 : 0;
+    }
     // the next re-inversion is a scheduled one (update limit, no growth-check
     // failure since the last): inv(B) is the updated inverse of the current
     // basis and may be refined instead of rebuilt (gk_newton.hip)
@@ -1367,13 +1407,13 @@ struct Spx {
         for (int j = 1; j <= cnt; j++)
             if (!dual || stat[j] != NS) D = std::max(D, std::fabs(fresh[j] - drift_ref[j]));
         // conservative in both directions: a drift above tol / 20 drops the
-        // chain to the floor (nfs_max), one above tol / 200 halves it, and it
+        // chain to the floor (nfs_max), one above tol / 100 halves it, and it
         // doubles only after two consecutive full-length chains below tol / 200
         int lim = f->upd_lim_adapt > 0 ? f->upd_lim_adapt : upd_cap;
         if (D > 0.05 * tol) {
             lim = upd_floor;
             f->clean_runs = 0;
-        } else if (D > 0.005 * tol) {
+        } else if (D > 0.01 * tol) {
             lim = std::max(upd_floor, std::min(lim, drift_upd) / 2);
             f->clean_runs = 0;
         } else if (drift_upd >= lim && ++f->clean_runs >= 2) {
@@ -1650,7 +1690,13 @@ void Spx::init()
         lim = std::min(std::max(f->upd_lim_adapt, nfs), upd_cap);
     } else
         upd_cap = nfs;
-    upd_floor = nfs;
+    if (f->sparse) {
+        // the Schur-complement chain holds at most SP_KMAX updates
+        // (gk_sparse.hip); no lengthening past nfs_max
+        upd_cap = std::min(nfs, SP_KMAX);
+        lim = upd_cap;
+    }
+    upd_floor = std::min(nfs, upd_cap);
     hs.upd_lim = lim;
     hs.upd_tol = f->parm.upd_tol > 0.0 ? f->parm.upd_tol : 1e-6;
     // the product-form updates of the factor persist across calls, as the
@@ -1699,14 +1745,15 @@ int Spx::batch(int K, int rigorous)
             int g = std::max(64, x / 8);
             return std::min(cap, (x + g - 1) / g * g);
         };
-        const DualPlan pl = dual_plan(d, bucket(hs.nr + K + 1, m), bucket(hs.nwl + K + 1, n), pse, rigorous);
+        DualPlan pl = dual_plan(d, bucket(hs.nr + K + 1, m), bucket(hs.nwl + K + 1, n), pse, rigorous);
+        pl.sparse = f->sparse ? 1 : 0;
         // profiling launches eagerly: event-record nodes inside captured
         // graphs are not timed by every HIP runtime this library may bind to
         // prof 1/2 launch eagerly (events around the pivot-row kernel); prof 3
         // keeps the graphs and records only the per-block clock stamps
         const int evp = E->prof == 1 || E->prof == 2;
         if (evp) prof_events(K);
-        if (!rigorous && K >= 4 && !evp) run_graph(d, pl, K);
+        if (!rigorous && K >= 4 && !evp && !f->sparse) run_graph(d, pl, K);
         else {
             dual_batch_begin(s, d, pl);
             for (int t = 0; t < K; t++) dual_iteration2(s, d, pl, ev0(t), ev1(t));
@@ -2304,6 +2351,7 @@ void gk_bfd_destroy(gk_bfd *f)
     (void)hipSetDevice(f->ctx->device);
     if (f->ctx->stream) (void)hipStreamSynchronize(f->ctx->stream);
     delete f->eng;
+    if (f->sp) sp_destroy(f->sp);
     f->Binv.release(); f->C.release(); f->X.release(); f->Y.release(); f->CinvR.release(); f->BS.release();
     f->G.release(); f->vecx.release(); f->vecy.release(); f->partial.release(); f->idx_i.release();
     f->piv_step.release(); f->piv.release(); f->flag.release(); f->bptr.release(); f->brow.release(); f->bval.release();
@@ -2406,6 +2454,7 @@ int gk_bfd_factorize_csc(gk_bfd *f, int m, const int *ptr, const int *ind, const
         ABI_REQUIRE(f && m >= 1, "bfd_factorize: m = %d; invalid parameter", m);
         bfd_prepare(f, m);
         f->valid = 0;
+        f->sparse = 0;                       // the explicit inverse (glp_factorize's factor)
         hipStream_t s = f->ctx->stream;
         // classify unit columns (+1 on a single row) as slack-like
         BasisSplit bs;
@@ -2499,7 +2548,14 @@ static void bfd_solve(gk_bfd *f, double *x, int tr)
     f->vecy.ensure(m);
     f->partial.ensure(PARTIAL_CAP);
     HIPCHK(hipMemcpyAsync(f->vecx.p, x + 1, m * sizeof(double), hipMemcpyHostToDevice, s));
-    if (tr) gemv_t(s, f->Binv.p, m, m, f->ldb, f->vecx.p, f->vecy.p, 1.0);
+    if (f->sparse) {
+        try {
+            if (tr) sp_btran(*f->sp, s, f->vecx.p, f->vecy.p);
+            else sp_ftran(*f->sp, s, f->vecx.p, f->vecy.p);
+        } catch (const std::exception &e) {
+            throw AbiError{e.what()};
+        }
+    } else if (tr) gemv_t(s, f->Binv.p, m, m, f->ldb, f->vecx.p, f->vecy.p, 1.0);
     else gemv_n(s, f->Binv.p, m, m, f->ldb, f->vecx.p, f->partial.p, PARTIAL_CAP, f->vecy.p, 1.0, nullptr, 0.0);
     HIPCHK(hipMemcpyAsync(x + 1, f->vecy.p, m * sizeof(double), hipMemcpyDeviceToHost, s));
     HIPCHK(hipStreamSynchronize(s));
@@ -2522,6 +2578,9 @@ int gk_bfd_update(gk_bfd *f, int j, int len, const int *ind, int idx, const doub
         const int m = f->m;
         ABI_REQUIRE(1 <= j && j <= m, "fhv_update_it: j = %d; column number out of range", j);
         if (f->upd_cnt >= upd_limit_parm(f->parm)) { f->valid = 0; return 4; }  // BFD_ELIMIT
+        // the sparse factor's updates are the engine's own (Schur complement on
+        // the device); an external update asks for a refactorization instead
+        if (f->sparse) { f->valid = 0; return 4; }
         HIPCHK(hipSetDevice(f->ctx->device));
         hipStream_t s = f->ctx->stream;
         std::vector<double> a(m + 1, 0.0);
@@ -2564,7 +2623,6 @@ static int spx_entry(gk_ctx *ctx, gk_lp *lp, gk_bfd *f, const gk_smcp *parm, int
     try {
         ABI_REQUIRE(ctx && lp && f && parm, "gk_spx: null argument");
         ABI_REQUIRE(lp->m > 0 && lp->n > 0, "spx: m = %d, n = %d; invalid dimensions", lp->m, lp->n);
-        ABI_REQUIRE(lp->m <= 65535, "spx: m = %d exceeds this build's grid limit 65535", lp->m);
         HIPCHK(hipSetDevice(ctx->device));
         if (f->ctx != ctx) {                  // the factor moves to the caller's context
             ctx->refs++;
@@ -2577,6 +2635,25 @@ static int spx_entry(gk_ctx *ctx, gk_lp *lp, gk_bfd *f, const gk_smcp *parm, int
         if (!f->eng) f->eng = new Engine;
         f->eng->prof = f->prof;
         engine_upload_matrix(f, lp);
+        // the factor: the explicit inverse (dense and mid-size LPs), or the
+        // sparse LU with Schur-complement updates (gk_sparse.hip) for sparse
+        // A when m exceeds the explicit inverse's limit (GK_SPARSE=1 also
+        // takes it for the dual on any sparse A); it serves the dual simplex
+        {
+            const char *ev = std::getenv("GK_SPARSE");
+            const int want = ev ? std::atoi(ev) : -1;
+            const bool big = lp->m > 65535;
+            const int sp = (!f->eng->dense && (big || (want == 1 && dual))) ? 1 : 0;
+            ABI_REQUIRE(sp || !big, "spx: m = %d exceeds the explicit inverse's limit 65535 (sparse A: the sparse "
+                        "factor serves m > 65535)", lp->m);
+            ABI_REQUIRE(!sp || dual, "spx_primal: m = %d; beyond the explicit inverse the sparse factor serves the "
+                        "dual simplex (GLP_DUAL / GLP_DUALP)", lp->m);
+            if (sp != f->sparse) {
+                f->valid = 0;
+                f->sparse = sp;
+            }
+            if (sp && !f->sp) f->sp = sp_create();
+        }
         Spx S;
         S.ctx = ctx; S.f = f; S.E = f->eng; S.lp = lp; S.parm = parm; S.dual = dual;
         S.init();
@@ -2619,6 +2696,7 @@ extern "C" int gk_bfd_eval_tab_rows(gk_bfd *f, gk_lp *lp, int nk, const int *k, 
         ABI_REQUIRE(f && lp && (nk == 0 || (k && alfa)), "glp_eval_tab_row: null argument");
         ABI_REQUIRE(lp->m > 0 && lp->n > 0 && nk >= 0, "glp_eval_tab_row: m = %d, n = %d, nk = %d", lp->m, lp->n, nk);
         ABI_REQUIRE(f->valid && f->m == lp->m, "glp_eval_tab_row: basis factorization does not exist");
+        ABI_REQUIRE(!f->sparse, "glp_eval_tab_row: batched tableau rows need the explicit inverse (m <= 65535)");
         if (nk == 0) return 0;
         HIPCHK(hipSetDevice(f->ctx->device));
         const int m = lp->m, n = lp->n;

@@ -129,6 +129,24 @@ void aprod_neg(hipStream_t s, const MatDev &A, const double *w, const double *ba
 void scatter_pos(hipStream_t s, int m, int off, int cnt, const int *head, const double *w, double *ys, double *wc);
 
 // ---- simplex pivot kernels --------------------------------------------------
+// ---- sparse basis factor (gk_sparse.hip): B0 = L U on the host, level-
+// scheduled sweeps on the device, Schur-complement updates (k <= SP_KMAX)
+constexpr int SP_KMAX = 128;
+struct SpFactor;
+SpFactor *sp_create();
+void sp_destroy(SpFactor *F);
+void sp_info(const SpFactor *F, long long *nnz_lu, int *levels, double *t_lu);
+// 0, or 1 when B0 is singular; head1 1-based over (I | -A); A CSC, 0-based rows
+int sp_factorize(SpFactor &F, hipStream_t s, int m, const int *head1, const int *Aptr, const int *Aind,
+                 const double *Aval, double piv_tol, int piv_lim, double eps_tol);
+void sp_ftran(SpFactor &F, hipStream_t s, const double *x, double *y);   // y = inv(B) x
+void sp_btran(SpFactor &F, hipStream_t s, const double *x, double *y);   // y = inv(B)' x
+struct DState;
+void sp_pivot_btran(SpFactor &F, hipStream_t s, DState *st, double *rho);
+void sp_pivot_ftran(SpFactor &F, hipStream_t s, const DState *st, double *h, double *work, double *tcol, double *u,
+                    int pse);
+void sp_pivot_update(SpFactor &F, hipStream_t s, DState *st);
+
 struct SpxDev {
     int m, n;
     MatDev A;
@@ -163,6 +181,7 @@ struct SpxDev {
     double *pnl, *pnl_src;
     int *pslot, *ppos;
     int ldp;
+    SpFactor *sp;                            // host pointer: the sparse factor (nullptr: explicit inverse)
 };
 constexpr int PANEL_MAX = 32;
 constexpr int TRACE_KERNELS = 8, TRACE_BLOCKS = 2048;   // trace[(kid * TRACE_BLOCKS + block) * 2 + {0, 1}]
@@ -189,6 +208,7 @@ struct DualPlan {
     int awone;                    // dense A w in one pass over 64-row tiles: the cap of nwl (0: split path)
     int panel;                    // rows of the MFMA pricing panel (0: the pivot row is a column pass over A)
     int panel_age;                // product-form updates a panel row may go through before a refill
+    int sparse;                   // 1: sparse factor (gk_sparse.hip): BTRAN / FTRAN / update hooks
 };
 void dual_batch_begin(hipStream_t s, const SpxDev &d, const DualPlan &pl);
 void dual_batch_end(hipStream_t s, const SpxDev &d, const DualPlan &pl);

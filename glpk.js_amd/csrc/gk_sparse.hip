@@ -1,0 +1,943 @@
+// Sparse basis factor for large sparse LPs (SURVEY.md §8(a) rows luf_* /
+// fhv_* / lpf_* / scf_*): B0 = L U by a Markowitz elimination with threshold
+// pivoting on the host (the role of luf_factorize, glpluf.js:1105), the
+// triangular solves on the device as level-scheduled sweeps (the role of
+// luf_f_solve / luf_v_solve, glpluf.js:1227 / :1268), and the updates of the
+// basis between refactorizations in Schur-complement form (the reference's
+// lpf / scf factor of GLP_BF_BG / GR, glplpf.js:331, glpscf.js:217):
+//
+//   B_k = B0 + D S'   (S = the unit columns of the k replaced positions,
+//                      D = new column - column of B0 at that position)
+//   Y   = inv(B0) D = [inv(B0) a_t - e_{p_t}]            (m x k, dense)
+//   M   = I + S' Y                                       (k x k, inverse kept)
+//   inv(B_k) b  = z - Y (inv(M) z[P]),     z = inv(B0) b
+//   inv(B_k)' e = inv(B0)' (e - S inv(M)' (Y' e))
+//
+// An update is one new (or replaced) column of Y, the inv(B0) a_q the pivot's
+// FTRAN already formed, and a bordered / rank-1 update of inv(M): O(m + k^2)
+// — no dependent chain over the updates, unlike an eta file or the
+// Forrest–Tomlin row eliminations (glpfhv.js:148-447), whose steps each need
+// the previous one's result.  k <= nfs_max (<= SP_KMAX) updates, then B0 is
+// refactorized, as the reference's LPF_ELIMIT (glplpf.js:359).
+//
+// Why this shape on the MI355X: the explicit dense inverse the engine uses
+// for dense and mid-size LPs (gk_reinvert.hip) costs 8 m^2 bytes and a rank-1
+// pass over m x nr entries per pivot; at m = 100,000 that is 80 GB and
+// ~10 ms per pivot.  The sparse LU of an LP basis is a few entries per row,
+// so a solve is O(nnz(L + U)) traffic; its dependency depth (levels) is what
+// bounds it, and each level is one barrier of a single workgroup whose
+// working vector stays in the L2.  Basis factor CPU parity is not claimed
+// bit-for-bit (the reference's FT-LU rounds differently); the objective,
+// statuses and KKT conditions are (tests/test_gpu_sparse.py).
+#include "gk_internal.h"
+#include "gk_device.h"
+
+#include <algorithm>
+#include <chrono>
+#include <cmath>
+#include <cstring>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+namespace gk {
+
+#define SPCHK(x)                                                                              \
+    do {                                                                                      \
+        hipError_t e__ = (x);                                                                 \
+        if (e__ != hipSuccess) throw std::runtime_error(std::string("sparse factor: ") + #x + \
+                                                        ": " + hipGetErrorString(e__));       \
+    } while (0)
+
+static double sp_now() { return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count(); }
+
+template <typename T>
+struct SBuf {
+    T *p = nullptr;
+    size_t n = 0;
+    void ensure(size_t cnt)
+    {
+        cnt = std::max<size_t>(cnt, 1);
+        if (cnt <= n && p) return;
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        n = 0;
+        SPCHK(hipMalloc((void **)&p, cnt * sizeof(T)));
+        n = cnt;
+    }
+    void release()
+    {
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        n = 0;
+    }
+};
+
+// L U of B0: step k pivots row pr[k] (constraint row) and position pc[k]
+struct SpLU {
+    int m = 0;
+    std::vector<int> pr, pc;
+    std::vector<int> Lptr, Lrow;          // eta of step k: multipliers of the rows it eliminated
+    std::vector<double> Lval;
+    std::vector<int> Uptr, Ucol;          // row of step k without its diagonal (positions)
+    std::vector<double> Uval, Udiag;
+};
+
+// one triangular sweep in gather form, steps in level order
+struct SpTriHost {
+    int nlev = 0;
+    std::vector<int> lvptr, iin, iout, eptr, eidx;
+    std::vector<double> diag, eval;
+};
+
+struct SpSolves {
+    SpTriHost fl, fu, bu, bl;
+};
+
+struct SpTriDevBufs {
+    SBuf<int> lvptr, iin, iout, eptr, eidx;
+    SBuf<double> diag, eval;
+    void release()
+    {
+        lvptr.release(); iin.release(); iout.release(); eptr.release(); eidx.release(); diag.release();
+        eval.release();
+    }
+};
+
+struct SpFactor {
+    int m = -1;
+    SpTriDevBufs fl, fu, bu, bl;
+    SBuf<double> Y, Minv, zq, tpart, bt, scr;
+    SBuf<int> P, hdr;                     // hdr: nlev of fl, fu, bu, bl; k (updates in the chain)
+    long long nnz_l = 0, nnz_u = 0;
+    int levels[4] = {0, 0, 0, 0};
+    double t_lu = 0.0, t_total = 0.0;
+    ~SpFactor()
+    {
+        fl.release(); fu.release(); bu.release(); bl.release();
+        Y.release(); Minv.release(); zq.release(); tpart.release(); bt.release(); scr.release(); P.release();
+        hdr.release();
+    }
+};
+
+// ---------------------------------------------------------------------------
+// host: Markowitz LU with threshold pivoting
+// ---------------------------------------------------------------------------
+// The active submatrix is kept by rows (column index, value) and by columns
+// (row patterns); rows and columns sit in count buckets.  A pivot is a column
+// singleton, else a row singleton, else the candidate of least Markowitz cost
+// (r - 1)(c - 1) among the elements passing the threshold |a_ij| >= piv_tol
+// max_j |a_ij| in the columns and rows of smallest count (at most piv_lim
+// candidates, the search order of luf's find_pivot, glpluf.js:437-628).
+// Elimination forms the multipliers of the pivot column (an L eta), updates
+// the other rows with fill-in and drops entries below eps_tol
+// (eliminate, glpluf.js:637-812); the pivot row goes to U.
+namespace {
+
+struct Buckets {
+    std::vector<int> head, next, prev, cnt;
+    void init(int n, int maxc)
+    {
+        head.assign(maxc + 2, -1);
+        next.assign(n, -1);
+        prev.assign(n, -1);
+        cnt.assign(n, 0);
+    }
+    void add(int i, int c)
+    {
+        cnt[i] = c;
+        prev[i] = -1;
+        next[i] = head[c];
+        if (head[c] >= 0) prev[head[c]] = i;
+        head[c] = i;
+    }
+    void del(int i)
+    {
+        const int c = cnt[i];
+        if (prev[i] >= 0) next[prev[i]] = next[i];
+        else head[c] = next[i];
+        if (next[i] >= 0) prev[next[i]] = prev[i];
+        next[i] = prev[i] = -1;
+    }
+    void move(int i, int c)
+    {
+        del(i);
+        add(i, c);
+    }
+};
+
+}  // namespace
+
+// returns 0, or 1 when B0 is singular (BFD_ESING); rank in *rank
+static int sp_lu_factor(SpLU &F, int m, const std::vector<int> &cptr, const std::vector<int> &crow,
+                 const std::vector<double> &cval, double piv_tol, int piv_lim, double eps_tol, int *rank)
+{
+    F.m = m;
+    F.pr.assign(m, -1);
+    F.pc.assign(m, -1);
+    F.Lptr.assign(1, 0);
+    F.Lrow.clear(); F.Lval.clear();
+    F.Uptr.assign(1, 0);
+    F.Ucol.clear(); F.Uval.clear(); F.Udiag.assign(m, 0.0);
+    std::vector<std::vector<int>> rc(m);           // row i: columns
+    std::vector<std::vector<double>> rv(m);        // row i: values
+    std::vector<std::vector<int>> cr(m);           // column j: rows
+    for (int j = 0; j < m; j++)
+        for (int t = cptr[j]; t < cptr[j + 1]; t++) {
+            const int i = crow[t];
+            if (cval[t] == 0.0) continue;
+            rc[i].push_back(j);
+            rv[i].push_back(cval[t]);
+            cr[j].push_back(i);
+        }
+    Buckets R, C;
+    R.init(m, m);
+    C.init(m, m);
+    for (int i = 0; i < m; i++) R.add(i, (int)rc[i].size());
+    for (int j = 0; j < m; j++) C.add(j, (int)cr[j].size());
+    std::vector<char> ract(m, 1), cact(m, 1);
+    std::vector<double> rmax(m, -1.0);             // cached max |a_ij| of row i (< 0: stale)
+    auto row_max = [&](int i) {
+        if (rmax[i] < 0.0) {
+            double b = 0.0;
+            for (double v : rv[i]) b = std::max(b, std::fabs(v));
+            rmax[i] = b;
+        }
+        return rmax[i];
+    };
+    auto find_in_row = [&](int i, int j) {
+        const std::vector<int> &r = rc[i];
+        for (size_t t = 0; t < r.size(); t++)
+            if (r[t] == j) return (int)t;
+        return -1;
+    };
+    std::vector<int> wpos(m, -1);                  // column -> index in the row being updated
+    int k;
+    for (k = 0; k < m; k++) {
+        int pi = -1, pj = -1;
+        // column singleton, then row singleton
+        if (C.head[1] >= 0) {
+            pj = C.head[1];
+            pi = cr[pj][0];
+        } else if (R.head[1] >= 0) {
+            pi = R.head[1];
+            pj = rc[pi][0];
+        } else {
+            long long best = -1;
+            double bestv = 0.0;
+            int ncand = 0;
+            for (int c = 2; c <= m && ncand < piv_lim; c++) {
+                for (int j = C.head[c]; j >= 0 && ncand < piv_lim; j = C.next[j]) {
+                    for (int i : cr[j]) {
+                        const int t = find_in_row(i, j);
+                        const double v = std::fabs(rv[i][t]);
+                        if (v < piv_tol * row_max(i) || v == 0.0) continue;
+                        const long long cost = (long long)(rc[i].size() - 1) * (c - 1);
+                        if (best < 0 || cost < best || (cost == best && v > bestv)) {
+                            best = cost; bestv = v; pi = i; pj = j;
+                        }
+                    }
+                    ncand++;
+                }
+                for (int i = R.head[c]; i >= 0 && ncand < piv_lim; i = R.next[i]) {
+                    const double big = row_max(i);
+                    for (size_t t = 0; t < rc[i].size(); t++) {
+                        const double v = std::fabs(rv[i][t]);
+                        if (v < piv_tol * big || v == 0.0) continue;
+                        const int j = rc[i][t];
+                        const long long cost = (long long)(c - 1) * (cr[j].size() - 1);
+                        if (best < 0 || cost < best || (cost == best && v > bestv)) {
+                            best = cost; bestv = v; pi = i; pj = j;
+                        }
+                    }
+                    ncand++;
+                }
+                if (best >= 0 && best <= (long long)(c - 1) * (c - 1)) break;
+            }
+            if (best < 0) {
+                // no element passes the threshold: the largest element of
+                // any active row (a rank test of the rest)
+                double bv = 0.0;
+                for (int i = 0; i < m; i++)
+                    if (ract[i])
+                        for (size_t t = 0; t < rc[i].size(); t++)
+                            if (std::fabs(rv[i][t]) > bv) { bv = std::fabs(rv[i][t]); pi = i; pj = rc[i][t]; }
+                if (bv == 0.0) break;   // the rest of the active matrix is zero: singular
+            }
+        }
+        if (pi < 0 || pj < 0) break;
+        // the pivot
+        const int tp = find_in_row(pi, pj);
+        const double vp = rv[pi][tp];
+        if (vp == 0.0) break;
+        F.pr[k] = pi;
+        F.pc[k] = pj;
+        F.Udiag[k] = vp;
+        // U row: the pivot row's other entries
+        for (size_t t = 0; t < rc[pi].size(); t++)
+            if ((int)t != tp) {
+                F.Ucol.push_back(rc[pi][t]);
+                F.Uval.push_back(rv[pi][t]);
+            }
+        F.Uptr.push_back((int)F.Ucol.size());
+        // the pivot row leaves the column patterns
+        for (int j : rc[pi]) {
+            std::vector<int> &cj = cr[j];
+            for (size_t t = 0; t < cj.size(); t++)
+                if (cj[t] == pi) { cj[t] = cj.back(); cj.pop_back(); break; }
+            if (j != pj) C.move(j, (int)cj.size());
+        }
+        R.del(pi);
+        ract[pi] = 0;
+        // eliminate the pivot column from the other rows
+        std::vector<int> rows = cr[pj];
+        C.del(pj);
+        cact[pj] = 0;
+        cr[pj].clear();
+        for (int i : rows) {
+            const int ti = find_in_row(i, pj);
+            const double f = rv[i][ti] / vp;
+            F.Lrow.push_back(i);
+            F.Lval.push_back(f);
+            // remove a_{i,pj}
+            rc[i][ti] = rc[i].back(); rc[i].pop_back();
+            rv[i][ti] = rv[i].back(); rv[i].pop_back();
+            for (size_t t = 0; t < rc[i].size(); t++) wpos[rc[i][t]] = (int)t;
+            for (size_t t = 0; t < rc[pi].size(); t++) {
+                const int j = rc[pi][t];
+                if (j == pj) continue;
+                const double d = f * rv[pi][t];
+                if (wpos[j] >= 0) rv[i][wpos[j]] -= d;
+                else {
+                    wpos[j] = (int)rc[i].size();
+                    rc[i].push_back(j);
+                    rv[i].push_back(-d);
+                    cr[j].push_back(i);
+                    C.move(j, (int)cr[j].size());
+                }
+            }
+            // drop what cancelled (|a| < eps_tol)
+            for (size_t t = 0; t < rc[i].size();) {
+                if (std::fabs(rv[i][t]) < eps_tol) {
+                    const int j = rc[i][t];
+                    std::vector<int> &cj = cr[j];
+                    for (size_t u = 0; u < cj.size(); u++)
+                        if (cj[u] == i) { cj[u] = cj.back(); cj.pop_back(); break; }
+                    C.move(j, (int)cj.size());
+                    wpos[j] = -1;
+                    rc[i][t] = rc[i].back(); rc[i].pop_back();
+                    rv[i][t] = rv[i].back(); rv[i].pop_back();
+                } else t++;
+            }
+            for (int j : rc[i]) wpos[j] = -1;
+            rmax[i] = -1.0;
+            R.move(i, (int)rc[i].size());
+        }
+        F.Lptr.push_back((int)F.Lrow.size());
+        rc[pi].clear();
+        rv[pi].clear();
+    }
+    *rank = k;
+    if (k < m) return 1;
+    return 0;
+}
+
+// the four gather-form triangular sweeps of a factor, each in level order
+// (a step's level is one more than the deepest step it reads):
+//   FTRAN L   z[r_k] = b[r_k] - sum_{t<k, r_k in L_t} l * z[r_t]   (in place)
+//   FTRAN U   x[c_k] = (z[r_k] - sum_{(j, u) in U_k} u x[j]) / u_kk
+//   BTRAN U'  w[k]   = (e[c_k] - sum_{t<k, c_k in U_t} u w[t]) / u_kk
+//   BTRAN L'  y[r_k] = w[k] - sum_{(i, l) in L_k} l y[i]
+static void sp_build_tri(SpTriHost &T, int m, int nsteps, const std::vector<int> &iin, const std::vector<int> &iout,
+                         const std::vector<double> &diag, const std::vector<std::vector<std::pair<int, double>>> &deps,
+                         const std::vector<int> &dep_step, bool reverse)
+{
+    // dep_step[e] of deps[k][e]: the step producing the entry read (level order)
+    std::vector<int> lev(nsteps, 0);
+    int nlev = 0;
+    std::vector<size_t> off(nsteps + 1, 0);
+    for (int k = 0; k < nsteps; k++) off[k + 1] = off[k] + deps[k].size();
+    for (int s = 0; s < nsteps; s++) {
+        const int k = reverse ? nsteps - 1 - s : s;
+        int l = 0;
+        for (size_t e = 0; e < deps[k].size(); e++) l = std::max(l, lev[dep_step[off[k] + e]] + 1);
+        lev[k] = l;
+        nlev = std::max(nlev, l + 1);
+    }
+    std::vector<int> cnt(nlev + 1, 0);
+    for (int k = 0; k < nsteps; k++) cnt[lev[k] + 1]++;
+    for (int l = 0; l < nlev; l++) cnt[l + 1] += cnt[l];
+    T.lvptr.assign(cnt.begin(), cnt.end());
+    T.nlev = nlev;
+    std::vector<int> pos(nlev, 0);
+    std::vector<int> order(nsteps);
+    for (int k = 0; k < nsteps; k++) order[T.lvptr[lev[k]] + pos[lev[k]]++] = k;
+    T.iin.resize(nsteps); T.iout.resize(nsteps); T.diag.resize(nsteps); T.eptr.assign(nsteps + 1, 0);
+    T.eidx.clear(); T.eval.clear();
+    for (int s = 0; s < nsteps; s++) {
+        const int k = order[s];
+        T.iin[s] = iin[k];
+        T.iout[s] = iout[k];
+        T.diag[s] = diag[k];
+        for (const auto &pr : deps[k]) {
+            T.eidx.push_back(pr.first);
+            T.eval.push_back(pr.second);
+        }
+        T.eptr[s + 1] = (int)T.eidx.size();
+    }
+    (void)m;
+}
+
+static void sp_build_solves(const SpLU &F, SpSolves &S)
+{
+    const int m = F.m;
+    std::vector<int> step_of_row(m), step_of_pos(m);
+    for (int k = 0; k < m; k++) { step_of_row[F.pr[k]] = k; step_of_pos[F.pc[k]] = k; }
+    std::vector<double> ones(m, 1.0);
+    // FTRAN L: deps of step k' = (z index r_t, l) for every eta t < k' holding row r_k'
+    {
+        std::vector<std::vector<std::pair<int, double>>> deps(m);
+        std::vector<std::vector<int>> dst(m);
+        for (int t = 0; t < m; t++)
+            for (int e = F.Lptr[t]; e < F.Lptr[t + 1]; e++) {
+                const int k = step_of_row[F.Lrow[e]];
+                deps[k].push_back({F.pr[t], F.Lval[e]});
+                dst[k].push_back(t);
+            }
+        std::vector<int> ds;
+        for (int k = 0; k < m; k++) ds.insert(ds.end(), dst[k].begin(), dst[k].end());
+        std::vector<int> io(m);
+        for (int k = 0; k < m; k++) io[k] = F.pr[k];
+        sp_build_tri(S.fl, m, m, io, io, ones, deps, ds, false);
+    }
+    // FTRAN U: deps of step k = (x index c_t, u) for the entries of U row k
+    {
+        std::vector<std::vector<std::pair<int, double>>> deps(m);
+        std::vector<int> ds;
+        for (int k = 0; k < m; k++)
+            for (int e = F.Uptr[k]; e < F.Uptr[k + 1]; e++) {
+                deps[k].push_back({F.Ucol[e], F.Uval[e]});
+                ds.push_back(step_of_pos[F.Ucol[e]]);
+            }
+        std::vector<int> in(m), out(m);
+        for (int k = 0; k < m; k++) { in[k] = F.pr[k]; out[k] = F.pc[k]; }
+        sp_build_tri(S.fu, m, m, in, out, F.Udiag, deps, ds, true);
+    }
+    // BTRAN U': deps of step k = (w index t, u) for every U row t < k holding column c_k
+    {
+        std::vector<std::vector<std::pair<int, double>>> deps(m);
+        std::vector<std::vector<int>> dst(m);
+        for (int t = 0; t < m; t++)
+            for (int e = F.Uptr[t]; e < F.Uptr[t + 1]; e++) {
+                const int k = step_of_pos[F.Ucol[e]];
+                deps[k].push_back({t, F.Uval[e]});
+                dst[k].push_back(t);
+            }
+        std::vector<int> ds;
+        for (int k = 0; k < m; k++) ds.insert(ds.end(), dst[k].begin(), dst[k].end());
+        std::vector<int> in(m), out(m);
+        for (int k = 0; k < m; k++) { in[k] = F.pc[k]; out[k] = k; }
+        sp_build_tri(S.bu, m, m, in, out, F.Udiag, deps, ds, false);
+    }
+    // BTRAN L': deps of step k = (y index i, l) for the entries of eta k
+    {
+        std::vector<std::vector<std::pair<int, double>>> deps(m);
+        std::vector<int> ds;
+        for (int k = 0; k < m; k++)
+            for (int e = F.Lptr[k]; e < F.Lptr[k + 1]; e++) {
+                deps[k].push_back({F.Lrow[e], F.Lval[e]});
+                ds.push_back(step_of_row[F.Lrow[e]]);
+            }
+        std::vector<int> in(m), out(m);
+        for (int k = 0; k < m; k++) { in[k] = k; out[k] = F.pr[k]; }
+        sp_build_tri(S.bl, m, m, in, out, ones, deps, ds, true);
+    }
+}
+
+// ---------------------------------------------------------------------------
+// device: level-scheduled sweeps (one workgroup; each level is one barrier,
+// the vectors stay in L2), two right-hand sides at once for the pivot FTRAN
+// ---------------------------------------------------------------------------
+struct TriDev {
+    const int *lvptr, *iin, *iout, *eptr, *eidx;
+    const double *diag, *eval;
+    const int *nlev;                              // device word: levels of the current factor
+};
+
+template <int NRHS>
+__device__ void tri_sweep(const TriDev &t, const double *in0, const double *in1, double *out0, double *out1)
+{
+    const int nlev = *t.nlev;
+    for (int l = 0; l < nlev; l++) {
+        const int b = t.lvptr[l], e = t.lvptr[l + 1];
+        for (int s = b + (int)threadIdx.x; s < e; s += blockDim.x) {
+            double a0 = in0[t.iin[s]], a1 = (NRHS == 2) ? in1[t.iin[s]] : 0.0;
+            const int eb = t.eptr[s], ee = t.eptr[s + 1];
+            int q = eb;
+            for (; q + 4 <= ee; q += 4) {
+                int ix[4];
+                double v[4], x0[4], x1[4];
+#pragma unroll
+                for (int u = 0; u < 4; u++) { ix[u] = t.eidx[q + u]; v[u] = t.eval[q + u]; }
+#pragma unroll
+                for (int u = 0; u < 4; u++) {
+                    x0[u] = out0[ix[u]];
+                    x1[u] = (NRHS == 2) ? out1[ix[u]] : 0.0;
+                }
+#pragma unroll
+                for (int u = 0; u < 4; u++) {
+                    a0 -= v[u] * x0[u];
+                    if (NRHS == 2) a1 -= v[u] * x1[u];
+                }
+            }
+            for (; q < ee; q++) {
+                const int ix = t.eidx[q];
+                a0 -= t.eval[q] * out0[ix];
+                if (NRHS == 2) a1 -= t.eval[q] * out1[ix];
+            }
+            const double dg = t.diag[s];
+            out0[t.iout[s]] = a0 / dg;
+            if (NRHS == 2) out1[t.iout[s]] = a1 / dg;
+        }
+        __syncthreads();
+    }
+}
+
+struct WoodDev {
+    double *Y;                                    // m x SP_KMAX, row-major by position
+    int *P;                                       // replaced positions (0-based)
+    double *Minv;                                 // SP_KMAX x SP_KMAX, row-major
+    int *k;                                       // device word: updates in the chain
+    double *zq;                                   // inv(B0) h of the last pivot's FTRAN
+    double *tpart;                                // Y' e partials of a general BTRAN (SP_KMAX per block)
+    double *bt;                                   // BTRAN scratch (positions), FTRAN scratch z (2 x m)
+};
+
+struct SpDev {
+    TriDev fl, fu, bu, bl;
+    WoodDev w;
+    int m;
+};
+
+// FTRAN part 1 (one workgroup): z = inv(B0) [h, work]; L in place, U into
+// the scratch; the z of h is kept (zq) for the update of this pivot
+template <int NRHS>
+__global__ void __launch_bounds__(1024) k_sp_ftran_lu(SpDev sp, const DState *st, double *h0, double *h1, int gated)
+{
+    if (gated && st->stop) return;
+    const int m = sp.m;
+    tri_sweep<NRHS>(sp.fl, h0, h1, h0, h1);      // in place: z[r] (row space)
+    double *x0 = sp.w.bt, *x1 = sp.w.bt + m;
+    tri_sweep<NRHS>(sp.fu, h0, h1, x0, x1);      // positions
+}
+
+// FTRAN part 2 (grid): x = z - Y inv(M) z[P] for each right-hand side; every
+// block forms inv(M) z[P] itself (k <= SP_KMAX: k^2 per block)
+template <int NRHS>
+__global__ void __launch_bounds__(256) k_sp_ftran_wood(SpDev sp, const DState *st, double *out0, double *out1,
+                                                       int gated, int keep)
+{
+    if (gated && st->stop) return;
+    const int m = sp.m;
+    const int k = *sp.w.k;
+    const double *z0 = sp.w.bt, *z1 = sp.w.bt + m;
+    __shared__ double g[2][SP_KMAX], hh[2][SP_KMAX];
+    for (int t = threadIdx.x; t < k; t += blockDim.x) {
+        const int p = sp.w.P[t];
+        g[0][t] = z0[p];
+        if (NRHS == 2) g[1][t] = z1[p];
+    }
+    __syncthreads();
+    for (int t = threadIdx.x; t < k; t += blockDim.x) {
+        const double *mr = sp.w.Minv + (size_t)t * SP_KMAX;
+        double a0 = 0.0, a1 = 0.0;
+        for (int u = 0; u < k; u++) {
+            a0 += mr[u] * g[0][u];
+            if (NRHS == 2) a1 += mr[u] * g[1][u];
+        }
+        hh[0][t] = a0;
+        if (NRHS == 2) hh[1][t] = a1;
+    }
+    __syncthreads();
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= m) return;
+    const double *yr = sp.w.Y + (size_t)i * SP_KMAX;
+    double a0 = z0[i], a1 = (NRHS == 2) ? z1[i] : 0.0;
+    for (int t = 0; t < k; t++) {
+        const double y = yr[t];
+        a0 -= y * hh[0][t];
+        if (NRHS == 2) a1 -= y * hh[1][t];
+    }
+    if (keep) sp.w.zq[i] = z0[i];
+    out0[i] = a0;
+    if (NRHS == 2) out1[i] = a1;
+}
+
+// BTRAN of a general right-hand side, part 1 (grid): partials of Y' e
+__global__ void __launch_bounds__(256) k_sp_btran_part(SpDev sp, const double *e)
+{
+    const int m = sp.m, k = *sp.w.k;
+    __shared__ double red[SP_KMAX][8];
+    const int lane = threadIdx.x & 31, grp = threadIdx.x >> 5;   // 8 groups of 32 threads
+    const int i0 = blockIdx.x * 256;
+    for (int t = grp; t < k; t += 8) {
+        double a = 0.0;
+        for (int i = i0 + lane; i < min(i0 + 256, m); i += 32) a += sp.w.Y[(size_t)i * SP_KMAX + t] * e[i];
+        for (int o = 16; o > 0; o >>= 1) a += __shfl_xor(a, o, 32);
+        if (lane == 0) red[t][0] = a;
+    }
+    __syncthreads();
+    for (int t = threadIdx.x; t < k; t += blockDim.x) sp.w.tpart[(size_t)blockIdx.x * SP_KMAX + t] = red[t][0];
+}
+
+// BTRAN part 2 (one workgroup): e' = e - S inv(M)' (Y' e), then y = inv(B0)' e'
+// mode 0: e general (partials from k_sp_btran_part over nparts blocks);
+// mode 1: e = e_p of the pivot (st->p): Y' e_p is row p of Y
+__global__ void __launch_bounds__(1024) k_sp_btran(SpDev sp, DState *st, const double *e, double *y, int mode,
+                                                   int nparts)
+{
+    if (mode == 1 && st->stop) return;
+    const int m = sp.m, k = *sp.w.k;
+    const int p = (mode == 1) ? st->p - 1 : -1;
+    __shared__ double tv[SP_KMAX], sv[SP_KMAX];
+    double *b = sp.w.bt;                          // positions
+    double *w = sp.w.bt + m;                      // step space
+    for (int t = threadIdx.x; t < k; t += blockDim.x) {
+        double a = 0.0;
+        if (mode == 1) a = sp.w.Y[(size_t)p * SP_KMAX + t];
+        else
+            for (int q = 0; q < nparts; q++) a += sp.w.tpart[(size_t)q * SP_KMAX + t];
+        tv[t] = a;
+    }
+    for (int i = threadIdx.x; i < m; i += blockDim.x) b[i] = (mode == 1) ? (i == p ? 1.0 : 0.0) : e[i];
+    __syncthreads();
+    for (int t = threadIdx.x; t < k; t += blockDim.x) {
+        double a = 0.0;
+        for (int u = 0; u < k; u++) a += sp.w.Minv[(size_t)u * SP_KMAX + t] * tv[u];   // inv(M)'
+        sv[t] = a;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0)
+        for (int t = 0; t < k; t++) b[sp.w.P[t]] -= sv[t];   // positions may repeat only in order
+    __syncthreads();
+    tri_sweep<1>(sp.bu, b, nullptr, w, nullptr);
+    tri_sweep<1>(sp.bl, w, nullptr, y, nullptr);
+}
+
+// the update of this pivot (one workgroup, after the commit): the column
+// entering at position p is N_q = -h, so inv(B0) N_q = -zq and
+// y = -zq - e_p; a new position borders inv(M), a repeated one replaces
+// its column (Sherman-Morrison).  A Schur pivot too small for a stable
+// inverse ends the chain (refact_pending), as the growth check does for the
+// dense inverse.
+__global__ void __launch_bounds__(1024) k_sp_update(SpDev sp, DState *st)
+{
+    if (st->stop) return;
+    const int m = sp.m, k = *sp.w.k;
+    const int p = st->p - 1;
+    __shared__ int slot;
+    __shared__ double c[SP_KMAX], r[SP_KMAX], ac[SP_KMAX], ra[SP_KMAX], col_old[SP_KMAX];
+    __shared__ double sch;
+    if (threadIdx.x == 0) {
+        slot = -1;
+        for (int t = 0; t < k; t++)
+            if (sp.w.P[t] == p) slot = t;
+    }
+    __syncthreads();
+    const int t0 = slot;
+    double *Y = sp.w.Y, *Mi = sp.w.Minv;
+    if (t0 < 0) {
+        if (k >= SP_KMAX) {
+            if (threadIdx.x == 0) st->refact_pending = 1;
+            return;
+        }
+        // border: c_i = y[P_i], r_t = Y[p, t], d = 1 + y[p]
+        for (int t = threadIdx.x; t < k; t += blockDim.x) {
+            c[t] = -sp.w.zq[sp.w.P[t]] - (sp.w.P[t] == p ? 1.0 : 0.0);
+            r[t] = Y[(size_t)p * SP_KMAX + t];
+        }
+        __syncthreads();
+        for (int t = threadIdx.x; t < k; t += blockDim.x) {
+            double a = 0.0, b = 0.0;
+            for (int u = 0; u < k; u++) {
+                a += Mi[(size_t)t * SP_KMAX + u] * c[u];     // inv(M) c
+                b += r[u] * Mi[(size_t)u * SP_KMAX + t];     // r inv(M)
+            }
+            ac[t] = a;
+            ra[t] = b;
+        }
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            double s = 1.0 + (-sp.w.zq[p] - 1.0);
+            for (int u = 0; u < k; u++) s -= r[u] * ac[u];
+            sch = s;
+        }
+        __syncthreads();
+        const double s = sch;
+        double dmax = 0.0;
+        for (int u = 0; u < k; u++) dmax = fmax(dmax, fabs(ac[u]));
+        if (!(fabs(s) > 1e-11 * (1.0 + dmax))) {
+            if (threadIdx.x == 0) st->refact_pending = 1;
+            return;
+        }
+        for (int e = threadIdx.x; e < k * k; e += blockDim.x) {
+            const int t = e / k, u = e % k;
+            Mi[(size_t)t * SP_KMAX + u] += ac[t] * ra[u] / s;
+        }
+        for (int t = threadIdx.x; t < k; t += blockDim.x) {
+            Mi[(size_t)t * SP_KMAX + k] = -ac[t] / s;
+            Mi[(size_t)k * SP_KMAX + t] = -ra[t] / s;
+        }
+        if (threadIdx.x == 0) {
+            Mi[(size_t)k * SP_KMAX + k] = 1.0 / s;
+            sp.w.P[k] = p;
+            *sp.w.k = k + 1;
+        }
+        for (int i = threadIdx.x; i < m; i += blockDim.x) Y[(size_t)i * SP_KMAX + k] = -sp.w.zq[i] - (i == p ? 1.0 : 0.0);
+        return;
+    }
+    // replace column t0: M' = M + u e_t0', u_i = ynew[P_i] - Yold[P_i, t0]
+    for (int t = threadIdx.x; t < k; t += blockDim.x) {
+        const int pi = sp.w.P[t];
+        col_old[t] = Y[(size_t)pi * SP_KMAX + t0];
+        c[t] = (-sp.w.zq[pi] - (pi == p ? 1.0 : 0.0)) - col_old[t];
+    }
+    __syncthreads();
+    for (int t = threadIdx.x; t < k; t += blockDim.x) {
+        double a = 0.0;
+        for (int u = 0; u < k; u++) a += Mi[(size_t)t * SP_KMAX + u] * c[u];
+        ac[t] = a;                                   // inv(M) u
+        ra[t] = Mi[(size_t)t0 * SP_KMAX + t];        // row t0 of inv(M)
+    }
+    __syncthreads();
+    const double den = 1.0 + ac[t0];
+    double amax = 0.0;
+    for (int u = 0; u < k; u++) amax = fmax(amax, fabs(ac[u]));
+    if (!(fabs(den) > 1e-11 * (1.0 + amax))) {
+        if (threadIdx.x == 0) st->refact_pending = 1;
+        return;
+    }
+    __syncthreads();
+    for (int e = threadIdx.x; e < k * k; e += blockDim.x) {
+        const int t = e / k, u = e % k;
+        Mi[(size_t)t * SP_KMAX + u] -= ac[t] * ra[u] / den;
+    }
+    for (int i = threadIdx.x; i < m; i += blockDim.x) Y[(size_t)i * SP_KMAX + t0] = -sp.w.zq[i] - (i == p ? 1.0 : 0.0);
+}
+
+// ---------------------------------------------------------------------------
+// host side: upload of a factor, the solves between batches, the pivot hooks
+// ---------------------------------------------------------------------------
+static void up_tri(hipStream_t s, SpTriDevBufs &B, const SpTriHost &T, int *d_nlev)
+{
+    B.lvptr.ensure(T.lvptr.size());
+    B.iin.ensure(std::max<size_t>(T.iin.size(), 1));
+    B.iout.ensure(std::max<size_t>(T.iout.size(), 1));
+    B.eptr.ensure(T.eptr.size());
+    B.eidx.ensure(std::max<size_t>(T.eidx.size(), 1));
+    B.diag.ensure(std::max<size_t>(T.diag.size(), 1));
+    B.eval.ensure(std::max<size_t>(T.eval.size(), 1));
+    SPCHK(hipMemcpyAsync(B.lvptr.p, T.lvptr.data(), T.lvptr.size() * sizeof(int), hipMemcpyHostToDevice, s));
+    SPCHK(hipMemcpyAsync(B.iin.p, T.iin.data(), T.iin.size() * sizeof(int), hipMemcpyHostToDevice, s));
+    SPCHK(hipMemcpyAsync(B.iout.p, T.iout.data(), T.iout.size() * sizeof(int), hipMemcpyHostToDevice, s));
+    SPCHK(hipMemcpyAsync(B.eptr.p, T.eptr.data(), T.eptr.size() * sizeof(int), hipMemcpyHostToDevice, s));
+    if (!T.eidx.empty()) {
+        SPCHK(hipMemcpyAsync(B.eidx.p, T.eidx.data(), T.eidx.size() * sizeof(int), hipMemcpyHostToDevice, s));
+        SPCHK(hipMemcpyAsync(B.eval.p, T.eval.data(), T.eval.size() * sizeof(double), hipMemcpyHostToDevice, s));
+    }
+    SPCHK(hipMemcpyAsync(B.diag.p, T.diag.data(), T.diag.size() * sizeof(double), hipMemcpyHostToDevice, s));
+    SPCHK(hipMemcpyAsync(d_nlev, &T.nlev, sizeof(int), hipMemcpyHostToDevice, s));
+}
+
+static TriDev tri_dev(const SpTriDevBufs &B, const int *nlev)
+{
+    TriDev t;
+    t.lvptr = B.lvptr.p; t.iin = B.iin.p; t.iout = B.iout.p; t.eptr = B.eptr.p; t.eidx = B.eidx.p;
+    t.diag = B.diag.p; t.eval = B.eval.p; t.nlev = nlev;
+    return t;
+}
+
+static SpDev sp_dev(SpFactor &F)
+{
+    SpDev d;
+    d.m = F.m;
+    d.fl = tri_dev(F.fl, F.hdr.p + 0);
+    d.fu = tri_dev(F.fu, F.hdr.p + 1);
+    d.bu = tri_dev(F.bu, F.hdr.p + 2);
+    d.bl = tri_dev(F.bl, F.hdr.p + 3);
+    d.w.Y = F.Y.p; d.w.P = F.P.p; d.w.Minv = F.Minv.p; d.w.k = F.hdr.p + 4; d.w.zq = F.zq.p;
+    d.w.tpart = F.tpart.p; d.w.bt = F.bt.p;
+    return d;
+}
+
+SpFactor *sp_create() { return new SpFactor; }
+void sp_destroy(SpFactor *F) { delete F; }
+
+void sp_info(const SpFactor *F, long long *nnz_lu, int *levels, double *t_lu)
+{
+    *nnz_lu = F->nnz_l + F->nnz_u;
+    for (int i = 0; i < 4; i++) levels[i] = F->levels[i];
+    *t_lu = F->t_lu;
+}
+
+// B0 from the basis header of (I | -A) (head 1-based; A in CSC, 0-based
+// rows, the engine's scaled copy): factorize on the host, upload
+int sp_factorize(SpFactor &F, hipStream_t s, int m, const int *head1, const int *Aptr, const int *Aind,
+                 const double *Aval, double piv_tol, int piv_lim, double eps_tol)
+{
+    const double t0 = sp_now();
+    std::vector<int> cptr(m + 1, 0), crow;
+    std::vector<double> cval;
+    crow.reserve((size_t)4 * m);
+    cval.reserve((size_t)4 * m);
+    for (int i = 1; i <= m; i++) {
+        const int k = head1[i];
+        if (k <= m) {
+            crow.push_back(k - 1);
+            cval.push_back(1.0);
+        } else {
+            const int j = k - m - 1;
+            for (int t = Aptr[j]; t < Aptr[j + 1]; t++) {
+                crow.push_back(Aind[t]);
+                cval.push_back(-Aval[t]);
+            }
+        }
+        cptr[i] = (int)crow.size();
+    }
+    SpLU lu;
+    int rank = 0;
+    const int ret = sp_lu_factor(lu, m, cptr, crow, cval, piv_tol > 0.0 ? piv_tol : 0.1, piv_lim > 0 ? piv_lim : 4,
+                                 eps_tol > 0.0 ? eps_tol : 1e-15, &rank);
+    F.t_lu = sp_now() - t0;
+    if (ret) return 1;
+    SpSolves S;
+    sp_build_solves(lu, S);
+    F.nnz_l = (long long)lu.Lrow.size();
+    F.nnz_u = (long long)lu.Ucol.size() + m;
+    F.levels[0] = S.fl.nlev; F.levels[1] = S.fu.nlev; F.levels[2] = S.bu.nlev; F.levels[3] = S.bl.nlev;
+    if (F.m != m) {
+        F.m = m;
+        F.Y.ensure((size_t)m * SP_KMAX);
+        F.zq.ensure(m);
+        F.bt.ensure((size_t)2 * m);
+        F.scr.ensure(m);
+        F.tpart.ensure((size_t)SP_KMAX * ((m + 255) / 256 + 1));
+    }
+    F.P.ensure(SP_KMAX);
+    F.Minv.ensure((size_t)SP_KMAX * SP_KMAX);
+    F.hdr.ensure(8);
+    up_tri(s, F.fl, S.fl, F.hdr.p + 0);
+    up_tri(s, F.fu, S.fu, F.hdr.p + 1);
+    up_tri(s, F.bu, S.bu, F.hdr.p + 2);
+    up_tri(s, F.bl, S.bl, F.hdr.p + 3);
+    const int zero = 0;
+    SPCHK(hipMemcpyAsync(F.hdr.p + 4, &zero, sizeof(int), hipMemcpyHostToDevice, s));
+    SPCHK(hipStreamSynchronize(s));          // the host vectors of S go out of scope
+    F.t_total = sp_now() - t0;
+    return 0;
+}
+
+// y = inv(B) x (positions), x untouched (device vectors)
+void sp_ftran(SpFactor &F, hipStream_t s, const double *x, double *y)
+{
+    const int m = F.m;
+    double *scratch = F.scr.p;
+    SpDev d = sp_dev(F);
+    SPCHK(hipMemcpyAsync(scratch, x, (size_t)m * sizeof(double), hipMemcpyDeviceToDevice, s));
+    hipLaunchKernelGGL((k_sp_ftran_lu<1>), dim3(1), dim3(1024), 0, s, d, (const DState *)nullptr, scratch,
+                       (double *)nullptr, 0);
+    hipLaunchKernelGGL((k_sp_ftran_wood<1>), dim3((m + 255) / 256), dim3(256), 0, s, d, (const DState *)nullptr, y,
+                       (double *)nullptr, 0, 0);
+}
+
+// y = inv(B)' x (rows)
+void sp_btran(SpFactor &F, hipStream_t s, const double *x, double *y)
+{
+    const int m = F.m;
+    SpDev d = sp_dev(F);
+    const int nb = (m + 255) / 256;
+    hipLaunchKernelGGL(k_sp_btran_part, dim3(nb), dim3(256), 0, s, d, x);
+    hipLaunchKernelGGL(k_sp_btran, dim3(1), dim3(1024), 0, s, d, (DState *)nullptr, x, y, 0, nb);
+}
+
+// the pivot's hooks (gated on the stop word, captured with the rest)
+void sp_pivot_btran(SpFactor &F, hipStream_t s, DState *st, double *rho)
+{
+    SpDev d = sp_dev(F);
+    hipLaunchKernelGGL(k_sp_btran, dim3(1), dim3(1024), 0, s, d, st, (const double *)nullptr, rho, 1, 0);
+}
+
+void sp_pivot_ftran(SpFactor &F, hipStream_t s, const DState *st, double *h, double *work, double *tcol, double *u,
+                    int pse)
+{
+    const int m = F.m;
+    SpDev d = sp_dev(F);
+    if (pse) {
+        hipLaunchKernelGGL((k_sp_ftran_lu<2>), dim3(1), dim3(1024), 0, s, d, st, h, work, 1);
+        hipLaunchKernelGGL((k_sp_ftran_wood<2>), dim3((m + 255) / 256), dim3(256), 0, s, d, st, tcol, u, 1, 1);
+    } else {
+        hipLaunchKernelGGL((k_sp_ftran_lu<1>), dim3(1), dim3(1024), 0, s, d, st, h, (double *)nullptr, 1);
+        hipLaunchKernelGGL((k_sp_ftran_wood<1>), dim3((m + 255) / 256), dim3(256), 0, s, d, st, tcol,
+                           (double *)nullptr, 1, 1);
+    }
+}
+
+void sp_pivot_update(SpFactor &F, hipStream_t s, DState *st)
+{
+    SpDev d = sp_dev(F);
+    hipLaunchKernelGGL(k_sp_update, dim3(1), dim3(1024), 0, s, d, st);
+}
+
+// ---------------------------------------------------------------------------
+// diagnostics (host only, no device): the factor of a basis given as CSC
+// (1-based like gk_bfd_factorize_csc: ptr[1..m+1], ind 1-based) and the four
+// sweeps run on the host in the same level order the device runs them:
+// x = inv(B) b, y = inv(B)' e.  Returns 0, 1 (singular) or -1 (bad input);
+// stats[0..5] = nnz(L), nnz(U) incl. diagonal, levels FTRAN L / U,
+// BTRAN U' / L'.  Lets the CPU tests pin the elimination and the level
+// schedules against numpy without a GPU.
+// ---------------------------------------------------------------------------
+static void host_sweep(const SpTriHost &t, const double *in, double *out)
+{
+    for (int l = 0; l < t.nlev; l++)
+        for (int s = t.lvptr[l]; s < t.lvptr[l + 1]; s++) {
+            double a = in[t.iin[s]];
+            for (int e = t.eptr[s]; e < t.eptr[s + 1]; e++) a -= t.eval[e] * out[t.eidx[e]];
+            out[t.iout[s]] = a / t.diag[s];
+        }
+}
+
+}  // namespace gk
+
+extern "C" int gk_sp_selftest(int m, const int *ptr, const int *ind, const double *val, const double *b,
+                              const double *e, double *x, double *y, long long *stats)
+{
+    using namespace gk;
+    if (m < 1 || !ptr || !ind || !val) return -1;
+    std::vector<int> cptr(m + 1, 0), crow;
+    std::vector<double> cval;
+    for (int j = 1; j <= m; j++) {
+        for (int t = ptr[j]; t < ptr[j + 1]; t++) {
+            if (ind[t] < 1 || ind[t] > m) return -1;
+            crow.push_back(ind[t] - 1);
+            cval.push_back(val[t]);
+        }
+        cptr[j] = (int)crow.size();
+    }
+    SpLU lu;
+    int rank = 0;
+    if (sp_lu_factor(lu, m, cptr, crow, cval, 0.1, 4, 1e-15, &rank)) return 1;
+    SpSolves S;
+    sp_build_solves(lu, S);
+    if (stats) {
+        stats[0] = (long long)lu.Lrow.size();
+        stats[1] = (long long)lu.Ucol.size() + m;
+        stats[2] = S.fl.nlev; stats[3] = S.fu.nlev; stats[4] = S.bu.nlev; stats[5] = S.bl.nlev;
+    }
+    std::vector<double> z(b, b + m), w(m);
+    host_sweep(S.fl, z.data(), z.data());
+    host_sweep(S.fu, z.data(), x);
+    host_sweep(S.bu, e, w.data());
+    host_sweep(S.bl, w.data(), y);
+    return 0;
+}

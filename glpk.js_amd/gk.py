@@ -116,7 +116,7 @@ EXPORTS = ["gk_abi_version", "gk_device_count", "gk_ctx_create", "gk_ctx_destroy
            "gk_comm_destroy", "gk_comm_backend", "gk_comm_rank", "gk_comm_size", "gk_comm_allgather",
            "gk_ios_driver_comm", "gk_comm_set_option", "gk_npp_create", "gk_npp_destroy", "gk_npp_load",
            "gk_npp_simplex", "gk_npp_integer", "gk_npp_build_size", "gk_npp_build", "gk_npp_postprocess",
-           "gk_npp_unload_sol", "gk_npp_unload_mip"]
+           "gk_npp_unload_sol", "gk_npp_unload_mip", "gk_sp_selftest"]
 
 # gk_report_fn (glpk_mi355x.h): one progress line or termination message of
 # a gk_spx_* call, in the order the reference prints them

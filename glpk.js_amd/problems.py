@@ -196,6 +196,46 @@ def gen_c2s(m: int = 821, n: int = 1571, nzc: int = 7, seed: int = 42) -> Proble
                    name=f"c2s_{m}x{n}")
 
 
+def gen_blocks(blocks: int = 1000, mb: int = 100, nb: int = 200, links: int = 50, nzc: int = 7,
+               seed: int = 42) -> Problem:
+    """Block-angular sparse LP (the sparse factor path's large instance, DESIGN
+    §2f): `blocks` independent C2s-like blocks of mb rows x nb columns (nzc
+    distinct rows of its block per column, drawn by rejection, a = 0.5 + u)
+    plus `links` linking rows, column j entering linking row j mod links with
+    0.5 + u.  Maximize c'x (c_j = u), block rows <= 1 + 9u, linking rows
+    <= 0.25 blocks mb / links, x >= 0.  splitmix64 in the order c, then per
+    column its rows and values, then the block bounds.  m = blocks mb + links,
+    n = blocks nb; the default is m = 100,050, n = 200,000."""
+    r = SplitMix(seed)
+    m, n = blocks * mb + links, blocks * nb
+    c = np.array([r.u() for _ in range(n)])
+    A_ptr = np.zeros(n + 1, dtype=np.int32)
+    inds, vals = [], []
+    for j in range(n):
+        k = j // nb
+        used, ent = set(), []
+        while len(ent) < nzc:
+            i = k * mb + 1 + int(math.floor(r.u() * mb))
+            if i in used:
+                continue
+            used.add(i)
+            ent.append((i, 0.5 + r.u()))
+        ent.append((blocks * mb + 1 + j % links, 0.5 + r.u()))
+        ent.sort(key=lambda t: -t[0])                    # descending row order (glp_load_matrix)
+        inds.extend(t[0] for t in ent)
+        vals.extend(t[1] for t in ent)
+        A_ptr[j + 1] = len(inds)
+    b = np.concatenate([np.array([1 + 9 * r.u() for _ in range(blocks * mb)]),
+                        np.full(links, 0.25 * blocks * mb / links)])
+    return Problem(m=m, n=n, dir=GLP_MAX, c0=0.0,
+                   row_type=_i8(np.full(m, GLP_UP)), row_lb=np.zeros(m), row_ub=_f8(b),
+                   rii=np.ones(m), row_stat=_i8(np.full(m, GLP_BS)),
+                   col_type=_i8(np.full(n, GLP_LO)), col_lb=np.zeros(n), col_ub=np.zeros(n),
+                   col_coef=_f8(c), sjj=np.ones(n), col_stat=_i8(np.full(n, GLP_NL)),
+                   col_kind=_i8(np.full(n, GLP_CV)), A_ptr=A_ptr, A_ind=_i4(inds), A_val=_f8(vals),
+                   name=f"blocks_{blocks}x{mb}x{nb}+{links}")
+
+
 def gen_c5s(m: int = 12, n: int = 30, seed: int = 42) -> Problem:
     """C5s correlated multi-knapsack surrogate for mas76."""
     u = splitmix_uniform(seed, m * n).reshape(m, n)

@@ -91,6 +91,14 @@ int     gk_bfd_set_parm(gk_bfd *bfd, const gk_bfcp *parm);   /* 0 | GK_EABI (inv
  * explicit: nfs_max / nrs_max then hold exactly, 100 included.  A new
  * factor starts in the default state.  (ABI 8) */
 int     gk_bfd_reset_parm(gk_bfd *bfd);
+/* diagnostics of the sparse factor (gk_sparse.hip; ABI 8), host only: the
+ * Markowitz L U of a basis given as CSC (as gk_bfd_factorize_csc: ptr[1..m+1],
+ * 1-based ind) and its four level-scheduled sweeps run on the host in the
+ * order the device runs them: x = inv(B) b, y = inv(B)' e ([0..m), 0-based).
+ * stats[0..5]: nnz(L), nnz(U) with its diagonal, levels of FTRAN L / U and
+ * BTRAN U' / L'.  0 | 1 (singular) | -1 (invalid input). */
+int     gk_sp_selftest(int m, const int *ptr, const int *ind, const double *val, const double *b,
+                       const double *e, double *x, double *y, long long *stats);
 /* 0 | BFD_ESING(1) | BFD_ECOND(2); col(info, j, ind, val) fills column j of B
  * exactly like b_col/inv_col (glpapi12.js:7, glpspx01.js:147). */
 int     gk_bfd_factorize(gk_bfd *bfd, int m, gk_col_fn col, void *info);

@@ -35,3 +35,32 @@ def dense_kkt(P, prob, tol=1e-7):
     for k, v in res.items():
         assert v <= (1e-9 if k in ("gap", "obj_vs_reported") else tol), (k, v, res)
     return res
+
+
+def sparse_kkt(P, prob, tol=1e-7):
+    """The certificate of dense_kkt for a sparse problem of the generators'
+    form (maximize c'x, A x <= b, x >= 0; A in the Problem's CSC arrays)."""
+    import scipy.sparse as sp
+    cols = np.repeat(np.arange(prob.n), np.diff(prob.A_ptr))
+    A = sp.csc_matrix((prob.A_val, (prob.A_ind - 1, cols)), shape=(prob.m, prob.n))
+    b, c = prob.row_ub, prob.col_coef
+    x, y, d = P.col_prim[1:], P.row_dual[1:], P.col_dual[1:]
+    ax = A @ x
+    aty = A.T @ y
+    scale_b = 1.0 + np.abs(b).max()
+    res = {
+        "primal_bound": float(max(0.0, -x.min())),
+        "primal_rows": float(max(0.0, (ax - b).max()) / scale_b),
+        "row_act": float(np.abs(ax - P.row_prim[1:]).max() / scale_b),
+        "dual_rows": float(max(0.0, -y.min())),
+        "dual_cols": float(max(0.0, (c - aty).max()) / (1.0 + np.abs(c).max())),
+        "reduced_costs": float(np.abs((c - aty) - d).max() / (1.0 + np.abs(c).max())),
+        "compl_cols": float(np.abs(d * x).max() / (1.0 + np.abs(c @ x))),
+        "compl_rows": float(np.abs(y * (b - ax)).max() / (1.0 + np.abs(c @ x))),
+    }
+    pobj, dobj = float(c @ x), float(b @ y)
+    res["gap"] = abs(pobj - dobj) / max(1.0, abs(pobj))
+    res["obj_vs_reported"] = abs(pobj + prob.c0 - P.obj_val) / max(1.0, abs(pobj))
+    for k, v in res.items():
+        assert v <= (1e-9 if k in ("gap", "obj_vs_reported") else tol), (k, v, res)
+    return res

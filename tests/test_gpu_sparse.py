@@ -1,0 +1,111 @@
+"""The sparse factor path on the GPU (gk_sparse.hip: B0 = L U, level-
+scheduled sweeps, Schur-complement updates), forced onto
+problems the explicit inverse would serve (GK_SPARSE=1) and taken by itself
+beyond its limit (m > 65535).
+
+Bar (north star): the reference's return code and statuses, objective
+within 1e-9 relative (tests/golden lp_* dual runs, pinned by the reference
+itself; the block-angular generator pinned by the oracle — the bit-faithful
+C restatement of the reference's dual simplex — run in the test), and a KKT
+certificate of every optimum (tests/kkt.py).  The pivot path is not
+compared: the factor rounds differently from the reference's FT-LU."""
+import os
+import sys
+
+import numpy as np
+import pytest
+
+from conftest import golden_files, load_golden
+from glpk_js_amd import gk, problems
+from kkt import sparse_kkt
+from test_gpu_lp import check_solution
+
+pytestmark = pytest.mark.gpu
+
+SPARSE_DUAL = []
+for path in golden_files("lp_"):
+    d = load_golden(path)
+    if d.get("gen", {}).get("kind") == "dense":
+        continue
+    for r, run in enumerate(d["runs"]):
+        if run["opts"].get("meth") in (2, 3) and not run["opts"].get("it_lim"):
+            SPARSE_DUAL.append(pytest.param(path, r, id=f"{os.path.basename(path)[3:-5]}-{r}"))
+
+
+@pytest.fixture
+def sparse_on(monkeypatch):
+    monkeypatch.setenv("GK_SPARSE", "1")
+
+
+@pytest.mark.parametrize("path,run_index", SPARSE_DUAL)
+def test_gpu_sparse_dual_matches_reference(gpu_ctx, sparse_on, path, run_index):
+    d = load_golden(path)
+    run = d["runs"][run_index]
+    prob = problems.from_fixture(d)
+    P = gk.GkProblem(gpu_ctx, prob)
+    ret = gk.glp_simplex(P, gk.SMCP(**run["opts"]))
+    assert ret == run["ret"]
+    assert (P.pbs_stat, P.dbs_stat) == (run["pbs_stat"], run["dbs_stat"])
+    if P.pbs_stat == problems.GLP_FEAS and P.dbs_stat == problems.GLP_FEAS:
+        ref = run["obj_val"]
+        assert abs(P.obj_val - ref) <= 1e-9 * max(1.0, abs(ref)), (P.obj_val, ref)
+        check_solution(P)
+
+
+def test_gpu_sparse_c2s_full_dual(gpu_ctx, sparse_on):
+    """C2s 821 x 1571 (the configs[1] surrogate), whole dual solve on the
+    sparse factor: the reference's objective 357.82820943518834 (SURVEY.md
+    §4), KKT-certified."""
+    prob = problems.gen_c2s()
+    P = gk.GkProblem(gpu_ctx, prob)
+    assert gk.glp_simplex(P, gk.SMCP(meth=gk.GLP_DUAL, msg_lev=gk.GLP_MSG_ERR)) == 0
+    assert abs(P.obj_val - 357.82820943518834) <= 1e-9 * 357.82820943518834, P.obj_val
+    sparse_kkt(P, prob)
+    st = P.stats()
+    print("c2s sparse:", P.it_cnt, "pivots", st.reinversions, "refactorizations", st.seconds_total, "s")
+
+
+@pytest.mark.parametrize("blocks,links", [(10, 5), (40, 10)])
+def test_gpu_sparse_blocks_match_oracle(gpu_ctx, sparse_on, oracle, blocks, links):
+    """Block-angular LPs (problems.gen_blocks, 100 x 200 blocks + linking
+    rows): the oracle's objective (≤ 1e-9), KKT-certified."""
+    prob = problems.gen_blocks(blocks, 100, 200, links)
+    o = oracle.OracleProb(prob)
+    assert o.simplex(meth=3) == 0
+    ref = o.result()["obj_val"]
+    P = gk.GkProblem(gpu_ctx, prob)
+    assert gk.glp_simplex(P, gk.SMCP(meth=gk.GLP_DUAL, msg_lev=gk.GLP_MSG_ERR)) == 0
+    assert (P.pbs_stat, P.dbs_stat) == (problems.GLP_FEAS, problems.GLP_FEAS)
+    assert abs(P.obj_val - ref) <= 1e-9 * max(1.0, abs(ref)), (P.obj_val, ref)
+    sparse_kkt(P, prob)
+    st = P.stats()
+    print(f"blocks {blocks}: {P.it_cnt} pivots, {st.reinversions} refactorizations, {st.seconds_total:.2f} s "
+          f"({P.it_cnt / st.seconds_total:.0f} pivots/s), refactor {st.seconds_reinvert:.2f} s")
+
+
+def test_gpu_sparse_primal_beyond_limit_fails_loudly(gpu_ctx):
+    """Beyond the explicit inverse (m > 65535) the sparse factor serves the
+    dual simplex; a primal request there is refused with a message (no
+    silent fallback).  Below it, GK_SPARSE=1 leaves the primal (and the
+    primal leg of GLP_DUALP) on the explicit inverse."""
+    P = gk.GkProblem(gpu_ctx, problems.gen_blocks(656, 100, 200, 50))
+    assert P.p.m > 65535
+    with pytest.raises(gk.GkError, match="sparse factor"):
+        gk.glp_simplex(P, gk.SMCP(meth=gk.GLP_PRIMAL, msg_lev=gk.GLP_MSG_ERR))
+
+
+def test_gpu_sparse_phase_and_limits(gpu_ctx, sparse_on):
+    """it_lim stops and continuation on the sparse factor: a chain of short
+    calls reaches the same optimum as one call (the factor, its Schur chain
+    and the resident working set carried across calls)."""
+    prob = problems.gen_blocks(10, 100, 200, 5)
+    P = gk.GkProblem(gpu_ctx, prob)
+    while True:
+        ret = gk.glp_simplex(P, gk.SMCP(meth=gk.GLP_DUAL, it_lim=250, msg_lev=gk.GLP_MSG_ERR))
+        assert ret in (0, problems.GLP_EITLIM)
+        if ret == 0:
+            break
+    Q = gk.GkProblem(gpu_ctx, prob.copy())
+    assert gk.glp_simplex(Q, gk.SMCP(meth=gk.GLP_DUAL, msg_lev=gk.GLP_MSG_ERR)) == 0
+    assert abs(P.obj_val - Q.obj_val) <= 1e-9 * abs(Q.obj_val)
+    sparse_kkt(P, prob)
