@@ -3,7 +3,8 @@
 GPU: the block-angular generator (problems.gen_blocks) or C2s, whole dual
 solve, progress lines every out_frq pivots (stderr), then one JSON line with
 pivots/s, refactorization time, the factor's size and a KKT certificate.
-Usage: sparse_big.py blocks K [links] | c2s M N"""
+Usage: sparse_big.py [--sparse] blocks K [links] | c2s M N
+(--sparse: GK_SPARSE=1, the sparse factor also below m = 65536)"""
 import json
 import os
 import sys
@@ -21,6 +22,9 @@ from kkt import sparse_kkt  # noqa: E402
 
 
 def main():
+    if sys.argv[1] == "--sparse":
+        os.environ["GK_SPARSE"] = "1"
+        del sys.argv[1]
     kind = sys.argv[1]
     t0 = time.time()
     if kind == "blocks":
