@@ -464,43 +464,90 @@ struct TriDev {
     const int *nlev;                              // device word: levels of the current factor
 };
 
+// one step of a sweep: its metadata and right-hand side(s) do not depend on
+// the sweep's own output, so they are loaded one level ahead (before the
+// barrier that ends the previous level); after the barrier a level costs
+// one trip — the gathers of the entries it reads — and its stores
+template <int NRHS>
+struct StepPre {
+    int s, iout, eb, ee;
+    double a0, a1, dg;
+    int ix[4];
+    double v[4];
+};
+
+template <int NRHS>
+__device__ __forceinline__ void step_load(const TriDev &t, const double *in0, const double *in1, int s, int lim,
+                                          StepPre<NRHS> &q)
+{
+    q.s = s;
+    if (s >= lim) return;
+    const int ii = t.iin[s];
+    q.iout = t.iout[s];
+    q.eb = t.eptr[s];
+    q.ee = t.eptr[s + 1];
+    q.dg = t.diag[s];
+    q.a0 = in0[ii];
+    q.a1 = (NRHS == 2) ? in1[ii] : 0.0;
+#pragma unroll
+    for (int u = 0; u < 4; u++) {
+        const bool ok = q.eb + u < q.ee;
+        q.ix[u] = ok ? t.eidx[q.eb + u] : 0;
+        q.v[u] = ok ? t.eval[q.eb + u] : 0.0;
+    }
+}
+
+template <int NRHS>
+__device__ __forceinline__ void step_run(const TriDev &t, const StepPre<NRHS> &q, double *out0, double *out1)
+{
+    double a0 = q.a0, a1 = q.a1;
+    double x0[4], x1[4];
+#pragma unroll
+    for (int u = 0; u < 4; u++) {
+        const bool ok = q.eb + u < q.ee;
+        x0[u] = ok ? out0[q.ix[u]] : 0.0;
+        x1[u] = (NRHS == 2 && ok) ? out1[q.ix[u]] : 0.0;
+    }
+#pragma unroll
+    for (int u = 0; u < 4; u++) {
+        a0 -= q.v[u] * x0[u];
+        if (NRHS == 2) a1 -= q.v[u] * x1[u];
+    }
+    for (int e = q.eb + 4; e < q.ee; e++) {
+        const int ix = t.eidx[e];
+        a0 -= t.eval[e] * out0[ix];
+        if (NRHS == 2) a1 -= t.eval[e] * out1[ix];
+    }
+    out0[q.iout] = a0 / q.dg;
+    if (NRHS == 2) out1[q.iout] = a1 / q.dg;
+}
+
 template <int NRHS>
 __device__ void tri_sweep(const TriDev &t, const double *in0, const double *in1, double *out0, double *out1)
 {
     const int nlev = *t.nlev;
+    const int T = blockDim.x;
+    if (nlev <= 0) return;
+    int lb = t.lvptr[0], le = t.lvptr[1];
+    StepPre<NRHS> cur;
+    step_load<NRHS>(t, in0, in1, lb + (int)threadIdx.x, le, cur);
     for (int l = 0; l < nlev; l++) {
-        const int b = t.lvptr[l], e = t.lvptr[l + 1];
-        for (int s = b + (int)threadIdx.x; s < e; s += blockDim.x) {
-            double a0 = in0[t.iin[s]], a1 = (NRHS == 2) ? in1[t.iin[s]] : 0.0;
-            const int eb = t.eptr[s], ee = t.eptr[s + 1];
-            int q = eb;
-            for (; q + 4 <= ee; q += 4) {
-                int ix[4];
-                double v[4], x0[4], x1[4];
-#pragma unroll
-                for (int u = 0; u < 4; u++) { ix[u] = t.eidx[q + u]; v[u] = t.eval[q + u]; }
-#pragma unroll
-                for (int u = 0; u < 4; u++) {
-                    x0[u] = out0[ix[u]];
-                    x1[u] = (NRHS == 2) ? out1[ix[u]] : 0.0;
-                }
-#pragma unroll
-                for (int u = 0; u < 4; u++) {
-                    a0 -= v[u] * x0[u];
-                    if (NRHS == 2) a1 -= v[u] * x1[u];
-                }
-            }
-            for (; q < ee; q++) {
-                const int ix = t.eidx[q];
-                a0 -= t.eval[q] * out0[ix];
-                if (NRHS == 2) a1 -= t.eval[q] * out1[ix];
-            }
-            const double dg = t.diag[s];
-            out0[t.iout[s]] = a0 / dg;
-            if (NRHS == 2) out1[t.iout[s]] = a1 / dg;
+        // the next level's bounds and this thread's first step of it
+        const int nb = le, ne = (l + 1 < nlev) ? t.lvptr[l + 2] : le;
+        StepPre<NRHS> nxt;
+        step_load<NRHS>(t, in0, in1, nb + (int)threadIdx.x, ne, nxt);
+        if (cur.s < le) step_run<NRHS>(t, cur, out0, out1);
+        for (int s = cur.s + T; s < le; s += T) {          // levels wider than the workgroup
+            StepPre<NRHS> q;
+            step_load<NRHS>(t, in0, in1, s, le, q);
+            step_run<NRHS>(t, q, out0, out1);
         }
         __syncthreads();
+        cur = nxt;
+        lb = nb;
+        le = ne;
     }
+    (void)lb;
 }
 
 struct WoodDev {
