@@ -1089,6 +1089,16 @@ struct Spx {
         f->ext_upd = 0;
         f->stats.reinversions++;
         f->stats.seconds_reinvert += now_s() - t0;
+        static const bool slog = std::getenv("GK_SPARSE_LOG") != nullptr;
+        if (slog && ret == 0) {
+            long long nnz = 0;
+            int lev[4];
+            double tlu = 0.0;
+            sp_info(f->sp, &nnz, lev, &tlu);
+            fprintf(stderr, "[gk sparse] it %d: nnz(L+U) %lld, levels FTRAN %d + %d, BTRAN %d + %d, host LU %.2f ms, "
+                    "refactor %.2f ms\n", hs.it_cnt, nnz, lev[0], lev[1], lev[2], lev[3], 1e3 * tlu,
+                    1e3 * (now_s() - t0));
+        }
         return ret ? 1 : 0;
     }
     // the next re-inversion is a scheduled one (update limit, no growth-check

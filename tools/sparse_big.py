@@ -25,6 +25,7 @@ def main():
     if sys.argv[1] == "--sparse":
         os.environ["GK_SPARSE"] = "1"
         del sys.argv[1]
+    os.environ.setdefault("GK_SPARSE_LOG", "1")
     kind = sys.argv[1]
     t0 = time.time()
     if kind == "blocks":
