@@ -25,6 +25,38 @@ extern "C" __device__ __attribute__((const)) unsigned int __ockl_wfred_min_u32(u
 // sum over the wave in a fixed order (deterministic)
 __device__ __forceinline__ double wsum(double v) { return __ockl_wfred_add_f64(v); }
 
+// rows of a CSR matrix longer than CSR_LONG entries are summed by the whole
+// wave (lanes stride the entries, a fixed-order wave reduction) instead of
+// by their own thread: a dense row (a linking row of a block-angular LP has
+// thousands of entries) would otherwise be a serial chain of dependent
+// loads.  Call with every lane of the wave; lanes flag their long rows.
+constexpr int CSR_LONG = 32;
+template <typename F>
+__device__ __forceinline__ void csr_long_rows(bool is_long, int beg, int end, const int *__restrict__ rcol,
+                                              const double *__restrict__ rval, const double *__restrict__ x, F &&done)
+{
+    const int lane = threadIdx.x & 63;
+    unsigned long long mask = __ballot(is_long);
+    while (mask) {
+        const int src = __ffsll((long long)mask) - 1;
+        mask &= mask - 1;
+        const int b = __shfl(beg, src), e = __shfl(end, src);
+        double acc = 0.0;
+        int t = b + lane;
+        for (; t + 192 < e; t += 256) {
+            const int c0 = rcol[t], c1 = rcol[t + 64], c2 = rcol[t + 128], c3 = rcol[t + 192];
+            const double v0 = rval[t], v1 = rval[t + 64], v2 = rval[t + 128], v3 = rval[t + 192];
+            acc += v0 * x[c0];
+            acc += v1 * x[c1];
+            acc += v2 * x[c2];
+            acc += v3 * x[c3];
+        }
+        for (; t < e; t += 64) acc += rval[t] * x[rcol[t]];
+        acc = wsum(acc);
+        done(src, acc);
+    }
+}
+
 __device__ __forceinline__ double wmax(double v) { return __ockl_wfred_max_f64(v); }
 
 // block-wide reductions for blockDim.x <= 1024 (16 waves)

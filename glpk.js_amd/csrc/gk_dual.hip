@@ -1317,28 +1317,36 @@ __global__ void __launch_bounds__(256) k_dual_ratio(SpxDev d, int gn, int tiles_
     if ((int)blockIdx.x >= gn && !d.A.dense) {
         // sparse A: work = ys - A w, one row per thread over its CSR entries
         // (update_gamma :1103-1134; entries loaded ahead, fixed order)
+        // (rows longer than CSR_LONG: the whole wave, below)
         const int r = (blockIdx.x - gn) * 256 + threadIdx.x;
-        if (r >= m) return;
-        const int beg = d.A.rptr[r], end = d.A.rptr[r + 1];
+        const int rc = min(r, m - 1);
+        const int beg = d.A.rptr[rc], end = (r < m) ? d.A.rptr[rc + 1] : beg;
+        const bool lng = end - beg > CSR_LONG;
         constexpr int RU = 16;
         int cc[RU];
         double av[RU];
 #pragma unroll
         for (int u = 0; u < RU; ++u) {
-            const bool ok = beg + u < end;
+            const bool ok = !lng && beg + u < end;
             cc[u] = ok ? d.A.rcol[beg + u] : 0;
             av[u] = ok ? d.A.rval[beg + u] : 0.0;
         }
-        const double ysr = d.ys[r];
+        const double ysr = d.ys[rc];
         if (stop) return;
-        double wv[RU];
+        if (!lng && r < m) {
+            double wv[RU];
 #pragma unroll
-        for (int u = 0; u < RU; ++u) wv[u] = (beg + u < end) ? d.wcol[cc[u]] : 0.0;
-        double acc = 0.0;
+            for (int u = 0; u < RU; ++u) wv[u] = (beg + u < end) ? d.wcol[cc[u]] : 0.0;
+            double acc = 0.0;
 #pragma unroll
-        for (int u = 0; u < RU; ++u) acc += av[u] * wv[u];
-        for (int t = beg + RU; t < end; ++t) acc += d.A.rval[t] * d.wcol[d.A.rcol[t]];
-        d.work[r] = ysr - acc;
+            for (int u = 0; u < RU; ++u) acc += av[u] * wv[u];
+            for (int t = beg + RU; t < end; ++t) acc += d.A.rval[t] * d.wcol[d.A.rcol[t]];
+            d.work[r] = ysr - acc;
+        }
+        const int rb = r - (int)(threadIdx.x & 63);
+        csr_long_rows(lng, beg, end, d.A.rcol, d.A.rval, d.wcol, [&](int src, double acc) {
+            if ((int)(threadIdx.x & 63) == 0) d.work[rb + src] = d.ys[rb + src] - acc;
+        });
         return;
     }
     if ((int)blockIdx.x >= gn) {

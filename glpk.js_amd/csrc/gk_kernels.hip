@@ -383,13 +383,21 @@ __global__ void __launch_bounds__(256) k_csr_neg(int m, const int *__restrict__ 
 {
     GATE(st, need_p);
     const int r = blockIdx.x * blockDim.x + threadIdx.x;
-    if (r >= m) return;
-    double acc = 0.0;
-    for (int t = rptr[r]; t < rptr[r + 1]; ++t) {
-        const double wv = w[rcol[t]];
-        if (wv != 0.0) acc += rval[t] * wv;
+    const int rc = min(r, m - 1);
+    const int beg = rptr[rc], end = (r < m) ? rptr[rc + 1] : beg;
+    const bool lng = end - beg > CSR_LONG;           // the wave sums it (csr_long_rows)
+    if (!lng && r < m) {
+        double acc = 0.0;
+        for (int t = beg; t < end; ++t) {
+            const double wv = w[rcol[t]];
+            if (wv != 0.0) acc += rval[t] * wv;
+        }
+        y[r] = (base ? base[r] : 0.0) - acc;
     }
-    y[r] = (base ? base[r] : 0.0) - acc;
+    const int rb = r - (int)(threadIdx.x & 63);
+    csr_long_rows(lng, beg, end, rcol, rval, w, [&](int src, double acc) {
+        if ((int)(threadIdx.x & 63) == 0) y[rb + src] = (base ? base[rb + src] : 0.0) - acc;
+    });
 }
 
 void aprod_neg_gated(hipStream_t s, const MatDev &A, const double *w, const double *base, double *y,

@@ -86,7 +86,7 @@ struct SpLU {
 // one triangular sweep in gather form, steps in level order
 struct SpTriHost {
     int nlev = 0;
-    std::vector<int> lvptr, iin, iout, eptr, eidx;
+    std::vector<int> lvptr, lvlong, iin, iout, eptr, eidx;   // lvlong[l]: first step of level l with > TRI_LONG entries
     std::vector<double> diag, eval;
 };
 
@@ -95,11 +95,11 @@ struct SpSolves {
 };
 
 struct SpTriDevBufs {
-    SBuf<int> lvptr, iin, iout, eptr, eidx;
+    SBuf<int> lvptr, lvlong, iin, iout, eptr, eidx;
     SBuf<double> diag, eval;
     void release()
     {
-        lvptr.release(); iin.release(); iout.release(); eptr.release(); eidx.release(); diag.release();
+        lvptr.release(); lvlong.release(); iin.release(); iout.release(); eptr.release(); eidx.release(); diag.release();
         eval.release();
     }
 };
@@ -119,6 +119,8 @@ struct SpFactor {
         hdr.release();
     }
 };
+
+constexpr int TRI_LONG = 32;   // sweep steps with more entries run on a whole wave
 
 // ---------------------------------------------------------------------------
 // host: Markowitz LU with threshold pivoting
@@ -372,6 +374,14 @@ static void sp_build_tri(SpTriHost &T, int m, int nsteps, const std::vector<int>
     std::vector<int> pos(nlev, 0);
     std::vector<int> order(nsteps);
     for (int k = 0; k < nsteps; k++) order[T.lvptr[lev[k]] + pos[lev[k]]++] = k;
+    // within a level: the steps of at most TRI_LONG entries (one thread each)
+    // first, the longer ones (one wave each) after them
+    T.lvlong.assign(nlev, 0);
+    for (int l = 0; l < nlev; l++) {
+        auto b = order.begin() + T.lvptr[l], e = order.begin() + T.lvptr[l + 1];
+        auto mid = std::stable_partition(b, e, [&](int k) { return deps[k].size() <= (size_t)TRI_LONG; });
+        T.lvlong[l] = (int)(mid - order.begin());
+    }
     T.iin.resize(nsteps); T.iout.resize(nsteps); T.diag.resize(nsteps); T.eptr.assign(nsteps + 1, 0);
     T.eidx.clear(); T.eval.clear();
     for (int s = 0; s < nsteps; s++) {
@@ -459,7 +469,7 @@ static void sp_build_solves(const SpLU &F, SpSolves &S)
 // the vectors stay in L2), two right-hand sides at once for the pivot FTRAN
 // ---------------------------------------------------------------------------
 struct TriDev {
-    const int *lvptr, *iin, *iout, *eptr, *eidx;
+    const int *lvptr, *lvlong, *iin, *iout, *eptr, *eidx;
     const double *diag, *eval;
     const int *nlev;                              // device word: levels of the current factor
 };
@@ -522,30 +532,69 @@ __device__ __forceinline__ void step_run(const TriDev &t, const StepPre<NRHS> &q
     if (NRHS == 2) out1[q.iout] = a1 / q.dg;
 }
 
+// a step of more than TRI_LONG entries: the calling wave strides them and
+// reduces in a fixed order (deterministic), lane 0 stores
+template <int NRHS>
+__device__ __forceinline__ void step_wave(const TriDev &t, const double *in0, const double *in1, int s, double *out0,
+                                          double *out1)
+{
+    const int lane = threadIdx.x & 63;
+    const int ii = t.iin[s], io = t.iout[s], eb = t.eptr[s], ee = t.eptr[s + 1];
+    const double dg = t.diag[s];
+    const double b0 = in0[ii], b1 = (NRHS == 2) ? in1[ii] : 0.0;
+    double a0 = 0.0, a1 = 0.0;
+    int e = eb + lane;
+    for (; e + 64 < ee; e += 128) {
+        const int i0 = t.eidx[e], i1 = t.eidx[e + 64];
+        const double v0 = t.eval[e], v1 = t.eval[e + 64];
+        const double x0 = out0[i0], x1 = out0[i1];
+        a0 += v0 * x0;
+        a0 += v1 * x1;
+        if (NRHS == 2) {
+            a1 += v0 * out1[i0];
+            a1 += v1 * out1[i1];
+        }
+    }
+    for (; e < ee; e += 64) {
+        const int ix = t.eidx[e];
+        a0 += t.eval[e] * out0[ix];
+        if (NRHS == 2) a1 += t.eval[e] * out1[ix];
+    }
+    a0 = wsum(a0);
+    if (NRHS == 2) a1 = wsum(a1);
+    if (lane == 0) {
+        out0[io] = (b0 - a0) / dg;
+        if (NRHS == 2) out1[io] = (b1 - a1) / dg;
+    }
+}
+
 template <int NRHS>
 __device__ void tri_sweep(const TriDev &t, const double *in0, const double *in1, double *out0, double *out1)
 {
     const int nlev = *t.nlev;
     const int T = blockDim.x;
+    const int w = threadIdx.x >> 6, nw = blockDim.x >> 6;
     if (nlev <= 0) return;
-    int lb = t.lvptr[0], le = t.lvptr[1];
+    int lb = t.lvptr[0], le = t.lvptr[1], ls = t.lvlong[0];
     StepPre<NRHS> cur;
-    step_load<NRHS>(t, in0, in1, lb + (int)threadIdx.x, le, cur);
+    step_load<NRHS>(t, in0, in1, lb + (int)threadIdx.x, ls, cur);
     for (int l = 0; l < nlev; l++) {
-        // the next level's bounds and this thread's first step of it
-        const int nb = le, ne = (l + 1 < nlev) ? t.lvptr[l + 2] : le;
+        // the next level's bounds and this thread's first (short) step of it
+        const int nb = le, ne = (l + 1 < nlev) ? t.lvptr[l + 2] : le, nls = (l + 1 < nlev) ? t.lvlong[l + 1] : le;
         StepPre<NRHS> nxt;
-        step_load<NRHS>(t, in0, in1, nb + (int)threadIdx.x, ne, nxt);
-        if (cur.s < le) step_run<NRHS>(t, cur, out0, out1);
-        for (int s = cur.s + T; s < le; s += T) {          // levels wider than the workgroup
+        step_load<NRHS>(t, in0, in1, nb + (int)threadIdx.x, nls, nxt);
+        if (cur.s < ls) step_run<NRHS>(t, cur, out0, out1);
+        for (int s = cur.s + T; s < ls; s += T) {          // short steps beyond one per thread
             StepPre<NRHS> q;
-            step_load<NRHS>(t, in0, in1, s, le, q);
+            step_load<NRHS>(t, in0, in1, s, ls, q);
             step_run<NRHS>(t, q, out0, out1);
         }
+        for (int s = ls + w; s < le; s += nw) step_wave<NRHS>(t, in0, in1, s, out0, out1);
         __syncthreads();
         cur = nxt;
         lb = nb;
         le = ne;
+        ls = nls;
     }
     (void)lb;
 }
@@ -778,6 +827,7 @@ __global__ void __launch_bounds__(1024) k_sp_update(SpDev sp, DState *st)
 static void up_tri(hipStream_t s, SpTriDevBufs &B, const SpTriHost &T, int *d_nlev)
 {
     B.lvptr.ensure(T.lvptr.size());
+    B.lvlong.ensure(std::max<size_t>(T.lvlong.size(), 1));
     B.iin.ensure(std::max<size_t>(T.iin.size(), 1));
     B.iout.ensure(std::max<size_t>(T.iout.size(), 1));
     B.eptr.ensure(T.eptr.size());
@@ -785,6 +835,8 @@ static void up_tri(hipStream_t s, SpTriDevBufs &B, const SpTriHost &T, int *d_nl
     B.diag.ensure(std::max<size_t>(T.diag.size(), 1));
     B.eval.ensure(std::max<size_t>(T.eval.size(), 1));
     SPCHK(hipMemcpyAsync(B.lvptr.p, T.lvptr.data(), T.lvptr.size() * sizeof(int), hipMemcpyHostToDevice, s));
+    if (!T.lvlong.empty())
+        SPCHK(hipMemcpyAsync(B.lvlong.p, T.lvlong.data(), T.lvlong.size() * sizeof(int), hipMemcpyHostToDevice, s));
     SPCHK(hipMemcpyAsync(B.iin.p, T.iin.data(), T.iin.size() * sizeof(int), hipMemcpyHostToDevice, s));
     SPCHK(hipMemcpyAsync(B.iout.p, T.iout.data(), T.iout.size() * sizeof(int), hipMemcpyHostToDevice, s));
     SPCHK(hipMemcpyAsync(B.eptr.p, T.eptr.data(), T.eptr.size() * sizeof(int), hipMemcpyHostToDevice, s));
@@ -799,7 +851,7 @@ static void up_tri(hipStream_t s, SpTriDevBufs &B, const SpTriHost &T, int *d_nl
 static TriDev tri_dev(const SpTriDevBufs &B, const int *nlev)
 {
     TriDev t;
-    t.lvptr = B.lvptr.p; t.iin = B.iin.p; t.iout = B.iout.p; t.eptr = B.eptr.p; t.eidx = B.eidx.p;
+    t.lvptr = B.lvptr.p; t.lvlong = B.lvlong.p; t.iin = B.iin.p; t.iout = B.iout.p; t.eptr = B.eptr.p; t.eidx = B.eidx.p;
     t.diag = B.diag.p; t.eval = B.eval.p; t.nlev = nlev;
     return t;
 }
