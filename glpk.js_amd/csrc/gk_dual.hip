@@ -790,8 +790,15 @@ __global__ void __launch_bounds__(1024) k_trow_rows(SpxDev d, int pse)
     __syncthreads();
     TPH(1, 2);
     if (w != 0) return;                      // wave 0 only from here: no block barriers
+    // the waves' partial sums in wave order; the LDS loads issued together
+    // (a loop over the runtime wave count waited for each load in turn)
+    double tp16[16];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) tp16[k] = (k < nw) ? sp[k][lane] : 0.0;
     double tsum = 0.0;
-    for (int k = 0; k < nw; ++k) tsum += sp[k][lane];
+#pragma unroll
+    for (int k = 0; k < 16; ++k)
+        if (k < nw) tsum += tp16[k];
     double tv1 = (j1 >= 0) ? tsum : 0.0;
     double tv2 = (j2 >= 0) ? -rho2 : 0.0;    // a non-basic slack is a dense column of inv(B)
     if (s1 == NS) tv1 = 0.0;
@@ -1028,8 +1035,15 @@ __global__ void __launch_bounds__(1024) k_dual_row(SpxDev d, int pse, int nr_cap
         st->ns = ns;
         st->dinf = 0;
     }
+    // the waves' partial sums in wave order; the LDS loads issued together
+    // (a loop over the runtime wave count waited for each load in turn)
+    double tp16[16];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) tp16[k] = (k < nw) ? sp[k][lane] : 0.0;
     double tsum = 0.0;
-    for (int k = 0; k < nw; ++k) tsum += sp[k][lane];
+#pragma unroll
+    for (int k = 0; k < 16; ++k)
+        if (k < nw) tsum += tp16[k];
     double tv1 = (j1 >= 0) ? tsum : 0.0;
     double tv2 = (j2 >= 0) ? -rho2 : 0.0;
     if (s1 == NS) tv1 = 0.0;
@@ -2436,8 +2450,11 @@ __global__ void __launch_bounds__(1024) k_dual_update(SpxDev d, int gn, int ncb,
     // run side by side; one wave does all when the block has fewer
     {
         const int wb = NRHS == 2 ? min(1, nw - 1) : 0, wl = min(2, nw - 1);
+        // each sum in its fixed order (waves, then slices); the outer loop
+        // unrolled so that the LDS loads of several waves are in flight
         if (w == 0 && sl == 0) {
             double sa = 0.0;
+#pragma unroll 4
             for (int k = 0; k < nw; ++k)
 #pragma unroll
                 for (int z = 0; z < SL; ++z) sa += sp[0][k][rl + z * RPB];
@@ -2445,15 +2462,19 @@ __global__ void __launch_bounds__(1024) k_dual_update(SpxDev d, int gn, int ncb,
         }
         if (NRHS == 2 && w == wb && sl == 0) {
             double sb = 0.0;
+#pragma unroll 4
             for (int k = 0; k < nw; ++k)
 #pragma unroll
                 for (int z = 0; z < SL; ++z) sb += sp[NRHS - 1][k][rl + z * RPB];
             srow[NRHS - 1][rl] = sb + sub[rl];
         }
-        if (!SP && w == wl && lane == 0) {
+        if (!SP && w == wl) {
+            // alpha_p: one slice partial per lane, summed in slice order from
+            // registers (readlane), not by NSL dependent LDS loads
+            const double v = (lane < NSL) ? salp[lane] : 0.0;
             double s = 0.0;
-            for (int k = 0; k < NSL; ++k) s += salp[k];
-            salpha = s;
+            for (int k = 0; k < NSL; ++k) s += __shfl(v, k);
+            if (lane == 0) salpha = s;
         }
     }
     __syncthreads();
