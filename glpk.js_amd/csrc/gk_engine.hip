@@ -209,7 +209,9 @@ struct Engine {
     struct Resident {
         bool ok = false;
         int dual = -1, m = 0, n = 0, nr = 0;
-        unsigned long long a_version = 0, fact_ver = 0;
+        unsigned long long a_version = 0, fact_ver = 0, b_version = 0;
+        int dir = 0;
+        double c0 = 0.0;
         double zeta = 0.0;
         std::vector<signed char> type, orig_type, stat;
         std::vector<double> lb, ub, coef, orig_lb, orig_ub, obj, bbar, cbar;
@@ -1440,6 +1442,7 @@ struct Spx {
 
     bool resident_match() const;
     void save_resident();
+    bool fastv = false;                     // init took the resident arrays over (b_version)
     // move the host mirrors to / from the engine's spare set
     void swap_spare()
     {
@@ -1516,8 +1519,10 @@ bool Spx::resident_match() const
     auto same = [](const auto &a, const auto &b) {
         return a.size() == b.size() && std::memcmp(a.data(), b.data(), a.size() * sizeof(a[0])) == 0;
     };
-    if (!same(type, R.type) || !same(orig_type, R.orig_type) || !same(lb, R.lb) || !same(ub, R.ub) ||
-        !same(orig_lb, R.orig_lb) || !same(orig_ub, R.orig_ub) || !same(coef, R.coef) || !same(obj, R.obj))
+    // (with the bounds version the arrays are the resident ones themselves)
+    if (!fastv && (!same(type, R.type) || !same(orig_type, R.orig_type) || !same(lb, R.lb) || !same(ub, R.ub) ||
+                   !same(orig_lb, R.orig_lb) || !same(orig_ub, R.orig_ub) || !same(coef, R.coef) ||
+                   !same(obj, R.obj)))
         return false;
     for (int i = 1; i <= m; i++)
         if (head[i] != R.head[i]) return false;
@@ -1537,6 +1542,9 @@ void Spx::save_resident()
     if (!R.ok) return;
     R.dual = dual; R.m = m; R.n = n; R.nr = hs.nr;
     R.a_version = lp->a_version;
+    R.b_version = lp->b_version;
+    R.dir = lp->dir;
+    R.c0 = lp->c0;
     R.fact_ver = f->fact_ver;
     R.zeta = zeta;
     R.type.swap(type); R.orig_type.swap(orig_type); R.stat.swap(stat);
@@ -1560,11 +1568,26 @@ void Spx::init()
     // stat) is written below: resized, not zero-filled (the spare set has the
     // size of the last call; zero-filling these arrays was most of init's
     // host time on C3); orig_* are copies of the built arrays
-    type.resize(mn); lb.resize(mn); ub.resize(mn); coef.resize(mn); obj.resize(n + 1);
+    // the host declares the bounds, types, costs and scale factors unchanged
+    // since the call that left the resident working set (b_version, which the
+    // JS shim bumps on every mutator; 0 = unknown): that call's built arrays
+    // are taken over instead of rebuilt and compared (resident_match then
+    // checks the basis only)
+    Engine::Resident &R0 = E->res;
+    fastv = L->b_version != 0 && R0.ok && R0.b_version == L->b_version && L->a_version != 0 &&
+            R0.a_version == L->a_version && R0.m == m && R0.n == n && R0.dual == dual && R0.dir == L->dir &&
+            std::memcmp(&R0.c0, &L->c0, sizeof(double)) == 0;
     head.resize(mn); stat.resize(n + 1);
-    type[0] = 0; lb[0] = ub[0] = coef[0] = 0.0; head[0] = 0; stat[0] = 0;
+    head[0] = 0; stat[0] = 0;
     bind.assign(mn, 0);
     gamma.assign(std::max(m, n) + 1, 0.0);
+    if (fastv) {
+        type.swap(R0.type); orig_type.swap(R0.orig_type); lb.swap(R0.lb); ub.swap(R0.ub);
+        orig_lb.swap(R0.orig_lb); orig_ub.swap(R0.orig_ub); coef.swap(R0.coef); obj.swap(R0.obj);
+        zeta = R0.zeta;
+    } else {
+    type.resize(mn); lb.resize(mn); ub.resize(mn); coef.resize(mn); obj.resize(n + 1);
+    type[0] = 0; lb[0] = ub[0] = coef[0] = 0.0;
     // init_csa (glpspx01.js:42-145 / glpspx02.js:89-190)
     for (int i = 1; i <= m; i++) {
         type[i] = L->row_type[i];
@@ -1590,6 +1613,7 @@ void Spx::init()
     if (std::fabs(zeta) < 1.0) zeta *= 1000.0;
     if (dual)
         for (int j = 1; j <= n; j++) coef[m + j] *= zeta;
+    }
     for (int i = 1; i <= m; i++) {
         head[i] = L->head[i];
         ABI_REQUIRE(1 <= head[i] && head[i] <= m + n, "gk_spx: head[%d] = %d; out of range", i, head[i]);

@@ -65,7 +65,7 @@ class Lp(C.Structure):
                 ("row_prim", C.c_void_p), ("row_dual", C.c_void_p), ("col_prim", C.c_void_p),
                 ("col_dual", C.c_void_p),
                 ("it_cnt", C.c_int), ("pbs_stat", C.c_int), ("dbs_stat", C.c_int), ("some", C.c_int),
-                ("obj_val", C.c_double), ("valid", C.c_int)]
+                ("obj_val", C.c_double), ("valid", C.c_int), ("b_version", C.c_ulonglong)]
 
 
 class Iocp(C.Structure):
@@ -327,6 +327,14 @@ class GkProblem:
         self.mip_stats = {}
         GkProblem._version += 1
         self.a_version = GkProblem._version
+        # bounds / types / costs / scale version (gk_lp.b_version): 0 = unknown,
+        # the engine rebuilds init_csa's arrays and compares them with the
+        # resident copy on every call.  A caller that does not change them
+        # between calls (numpy arrays can be changed in place, so the Python
+        # host cannot know by itself) may declare it with touch_bounds() and
+        # must call it again after every change, as the JS shim does on every
+        # mutator
+        self.b_version = 0
         self.bfcp = None
         self.bfd = self.L.gk_bfd_create(ctx.h)
         if not self.bfd:
@@ -358,6 +366,15 @@ class GkProblem:
         """Invalidate the device copy of A (the shim's version counter)."""
         GkProblem._version += 1
         self.a_version = GkProblem._version
+        if self.b_version:
+            self.touch_bounds()
+
+    def touch_bounds(self):
+        """Declare the current bounds, types, costs, dir, c0 and scale
+        factors as one version (gk_lp.b_version): later calls with the same
+        version skip init_csa's rebuild.  Call again after every change."""
+        GkProblem._version += 1
+        self.b_version = GkProblem._version
 
     # ------------------------------------------------------------------
     _LP_ARRAYS = ("row_type", "row_lb", "row_ub", "rii", "col_type", "col_lb", "col_ub", "col_coef", "sjj",
@@ -380,6 +397,7 @@ class GkProblem:
                 cache[name] = ent
             setattr(lp, name, ent[1])
         lp.a_version = self.a_version
+        lp.b_version = self.b_version
         lp.it_cnt = self.it_cnt
         return lp
 

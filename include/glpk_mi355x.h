@@ -147,6 +147,11 @@ typedef struct {
     int pbs_stat, dbs_stat, some;            /* out */
     double obj_val;                          /* out */
     int valid;                               /* out: lp.valid */
+    unsigned long long b_version;            /* !=0: bounds, types, costs, dir, c0 and the scale
+                                                factors unchanged since the last call with this
+                                                version (and a_version) => init_csa's rebuild and
+                                                its comparison with the resident working set are
+                                                skipped; 0: always rebuilt and compared (ABI 8) */
 } gk_lp;
 
 /* The factor handle must be valid for lp->head (as after glp_factorize);

@@ -339,6 +339,7 @@ static int fill_lp(napi_env env, napi_value L, gk_lp *out)
     lp.A_ind = (const int *)tprop(env, L, "A_ind");
     lp.A_val = (const double *)tprop(env, L, "A_val");
     lp.a_version = (unsigned long long)dprop(env, L, "a_version", 0);
+    lp.b_version = (unsigned long long)dprop(env, L, "b_version", 0);
     lp.head = (int *)tprop(env, L, "head");
     lp.row_stat = (signed char *)tprop(env, L, "row_stat");
     lp.col_stat = (signed char *)tprop(env, L, "col_stat");

@@ -139,6 +139,7 @@ function marshal(lp, g) {
     marshalMatrix(lp, g);
     return {
         m: m, n: n, nnz: lp.nnz, dir: lp.dir, c0: lp.c0, a_version: g.a_version, it_cnt: lp.it_cnt,
+        b_version: lp.__gk_bversion || 0,
         row_type: g.row_type, row_lb: g.row_lb, row_ub: g.row_ub, rii: g.rii,
         col_type: g.col_type, col_lb: g.col_lb, col_ub: g.col_ub, col_coef: g.col_coef, sjj: g.sjj,
         A_ptr: g.A_ptr, A_ind: g.A_ind, A_val: g.A_val, head: g.head,

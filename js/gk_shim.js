@@ -142,6 +142,33 @@ glp_adv_basis = exports["glp_adv_basis"] = function (lp, flags) {
             return r;
         };
     }
+    // bounds, types, costs, dir and scale factors: lp.__gk_bversion (the
+    // engine skips init_csa's rebuild while it is unchanged).  The reference
+    // writes bounds directly only inside glp_analyze_bound / _coef
+    // (glpapi12.js:1098-1120): the version is unknown (0) during those calls
+    function bversioned(f) {
+        return function (lp) {
+            var r = f.apply(this, arguments);
+            lp.__gk_bversion = __gk.nextVersion();
+            return r;
+        };
+    }
+    function bunknown(f) {
+        return function (lp) {
+            lp.__gk_bversion = 0;
+            try { return f.apply(this, arguments); } finally { lp.__gk_bversion = __gk.nextVersion(); }
+        };
+    }
+    ["glp_set_row_bnds", "glp_set_col_bnds", "glp_set_obj_coef", "glp_set_obj_dir", "glp_set_rii", "glp_set_sjj",
+     "glp_unscale_prob", "glp_add_rows", "glp_add_cols", "glp_del_rows", "glp_del_cols", "glp_copy_prob",
+     "glp_erase_prob"].forEach(function (name) {
+        var f = eval(name);
+        eval(name + " = exports[name] = bversioned(f)");
+    });
+    ["glp_analyze_bound", "glp_analyze_coef"].forEach(function (name) {
+        var f = eval(name);
+        eval(name + " = exports[name] = bunknown(f)");
+    });
     glp_set_mat_row = exports["glp_set_mat_row"] = versioned(glp_set_mat_row);
     glp_set_mat_col = exports["glp_set_mat_col"] = versioned(glp_set_mat_col);
     glp_load_matrix = exports["glp_load_matrix"] = versioned(glp_load_matrix);

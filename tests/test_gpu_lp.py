@@ -274,3 +274,27 @@ def test_gpu_next_call_phase1_eval_bit_identical(gpu_ctx, monkeypatch):
         for x, y in zip(a[3:], b[3:]):
             assert np.array_equal(x, y)
     assert sk_on > sk_off
+
+
+def test_gpu_bounds_version_fast_init_bit_identical(gpu_ctx):
+    """gk_lp.b_version (ABI 8): a chain of it_lim calls with the bounds
+    version declared (init_csa's arrays taken over from the resident working
+    set, no rebuild, no comparison) ends bit for bit where the same chain with
+    version 0 (rebuilt and compared every call) ends; a bound changed and
+    declared with touch_bounds() is seen by the next call."""
+    outs = []
+    for declared in (False, True):
+        prob = problems.gen_dense(256, 1024, seed=3)
+        P = gk.GkProblem(gpu_ctx, prob)
+        if declared:
+            P.touch_bounds()
+        trace = []
+        for k in range(12):
+            if k == 6:                      # a bound change in the middle of the chain
+                P.row_ub[5] *= 0.5
+                if declared:
+                    P.touch_bounds()
+            ret = gk.glp_simplex(P, gk.SMCP(meth=gk.GLP_DUAL, it_lim=40, msg_lev=gk.GLP_MSG_OFF))
+            trace.append((ret, P.it_cnt, P.obj_val, bytes(P.row_stat), bytes(P.col_stat)))
+        outs.append(trace)
+    assert outs[0] == outs[1]
