@@ -2468,13 +2468,11 @@ __global__ void __launch_bounds__(1024) k_dual_update(SpxDev d, int gn, int ncb,
                 for (int z = 0; z < SL; ++z) sb += sp[NRHS - 1][k][rl + z * RPB];
             srow[NRHS - 1][rl] = sb + sub[rl];
         }
-        if (!SP && w == wl) {
-            // alpha_p: one slice partial per lane, summed in slice order from
-            // registers (readlane), not by NSL dependent LDS loads
-            const double v = (lane < NSL) ? salp[lane] : 0.0;
+        if (!SP && w == wl && lane == 0) {
             double s = 0.0;
-            for (int k = 0; k < NSL; ++k) s += __shfl(v, k);
-            if (lane == 0) salpha = s;
+#pragma unroll 8
+            for (int k = 0; k < NSL; ++k) s += salp[k];
+            salpha = s;
         }
     }
     __syncthreads();

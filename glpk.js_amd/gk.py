@@ -662,13 +662,20 @@ def glp_simplex(P: GkProblem, parm: Smcp | None = None) -> int:
     P.pbs_stat = P.dbs_stat = GLP_UNDEF
     P.obj_val = 0.0
     P.some = 0
-    for what, typ, lb, ub in (("row", P.row_type, P.row_lb, P.row_ub), ("column", P.col_type, P.col_lb, P.col_ub)):
+    # the double-bound check (glpapi06.js:306-323) runs once per bounds
+    # version when the caller declares one (touch_bounds), on every call else
+    bv = getattr(P, "b_version", 0)
+    checked = bv != 0 and P.__dict__.get("_db_checked") == bv
+    for what, typ, lb, ub in (() if checked else
+                              (("row", P.row_type, P.row_lb, P.row_ub), ("column", P.col_type, P.col_lb, P.col_ub))):
         bad = np.nonzero((typ[1:] == GLP_DB) & (lb[1:] >= ub[1:]))[0]
         if bad.size:
             k = int(bad[0]) + 1
             if parm.msg_lev >= GLP_MSG_ERR:
                 _xprintf(f"glp_simplex: {what} {k}: lb = {_js_num(lb[k])}, ub = {_js_num(ub[k])}; incorrect bounds")
             return GLP_EBOUND
+    if bv:
+        P._db_checked = bv
     if parm.msg_lev >= GLP_MSG_ALL:
         _xprintf(f"GLPK Simplex Optimizer, v{GLP_VERSION}")
         _xprintf(f"{P.m} row{'' if P.m == 1 else 's'}, {P.n} column{'' if P.n == 1 else 's'}, "
