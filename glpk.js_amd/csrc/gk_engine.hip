@@ -1793,6 +1793,11 @@ int Spx::batch(int K, int rigorous)
             for (int t = 0; t < K; t++) dual_iteration2(s, d, pl, ev0(t), ev1(t));
             dual_batch_end(s, d, pl);
         }
+    } else if (f->sparse) {
+        // the primal pivot on the sparse factor (rigorous mode included: no
+        // refinement, the checks re-factorize as after any failure)
+        primal_batch_begin(s, d);
+        for (int t = 0; t < K; t++) primal_iteration_sparse(s, d, pse);
     } else if (!rigorous && primal_fast_ok(d)) {
         if (lists_stale) {
             rebuild_lists();
@@ -2671,17 +2676,15 @@ static int spx_entry(gk_ctx *ctx, gk_lp *lp, gk_bfd *f, const gk_smcp *parm, int
         engine_upload_matrix(f, lp);
         // the factor: the explicit inverse (dense and mid-size LPs), or the
         // sparse LU with Schur-complement updates (gk_sparse.hip) for sparse
-        // A when m exceeds the explicit inverse's limit (GK_SPARSE=1 also
-        // takes it for the dual on any sparse A); it serves the dual simplex
+        // A when m exceeds the explicit inverse's limit (GK_SPARSE=1 takes it
+        // for any sparse A), both simplex methods
         {
             const char *ev = std::getenv("GK_SPARSE");
             const int want = ev ? std::atoi(ev) : -1;
             const bool big = lp->m > 65535;
-            const int sp = (!f->eng->dense && (big || (want == 1 && dual))) ? 1 : 0;
+            const int sp = (!f->eng->dense && (big || want == 1)) ? 1 : 0;
             ABI_REQUIRE(sp || !big, "spx: m = %d exceeds the explicit inverse's limit 65535 (sparse A: the sparse "
                         "factor serves m > 65535)", lp->m);
-            ABI_REQUIRE(!sp || dual, "spx_primal: m = %d; beyond the explicit inverse the sparse factor serves the "
-                        "dual simplex (GLP_DUAL / GLP_DUALP)", lp->m);
             if (sp != f->sparse) {
                 f->valid = 0;
                 f->sparse = sp;

@@ -146,6 +146,7 @@ void sp_pivot_btran(SpFactor &F, hipStream_t s, DState *st, double *rho);
 void sp_pivot_ftran(SpFactor &F, hipStream_t s, const DState *st, double *h, double *work, double *tcol, double *u,
                     int pse);
 void sp_pivot_update(SpFactor &F, hipStream_t s, DState *st);
+void sp_pivot_btran2(SpFactor &F, hipStream_t s, DState *st, const double *v, double *rho, double *u);
 
 struct SpxDev {
     int m, n;
@@ -222,6 +223,8 @@ DualPlan primal_plan(const SpxDev &d, int nr_max, int pse);
 bool primal_fast_ok(const SpxDev &d);
 void primal_batch_begin(hipStream_t s, const SpxDev &d);
 void primal_iteration2(hipStream_t s, const SpxDev &d, const DualPlan &pl);
+// the primal pivot on the sparse factor (gk_sparse.hip hooks)
+void primal_iteration_sparse(hipStream_t s, const SpxDev &d, int pse);
 // coalesced host->device uploads: segment g of a staged region goes to g.dst
 struct UpSeg {
     size_t off;

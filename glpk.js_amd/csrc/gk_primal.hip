@@ -1076,6 +1076,150 @@ __global__ void __launch_bounds__(256) k_primal_commit(SpxDev d, int pse, int nv
 }
 
 // ---------------------------------------------------------------------------
+// the primal pivot on the sparse factor (gk_sparse.hip): the
+// same stages with the inverse's reads replaced by solves —
+//   k_sp_primal_top     1 WG  stop tests, PSE reset, chuzc (:646), h = -N[q]
+//   FTRAN               tcol = inv(B) h (eval_tcol :690)
+//   k_sp_primal_groups  grid  per 64-row group: max |tcol|, the d_q check
+//                       sum, the PSE vector v and its sum of squares, the
+//                       Harris pass-1 candidate (the tail of k_primal_ftran)
+//   k_primal_ratio      grid  (its pass blocks only) d_q check, pass 1, bound
+//                       flip, pass-2 candidates
+//   k_sp_primal_pick    1 WG  the pass-2 choice p (ppick)
+//   BTRAN x 2           rho = inv(B)' e_p, u = inv(B)' v (eval_rho :1030,
+//                       update_gamma :1220)
+//   column pass         trow_j = -rho' N_j, s_j = N_j' u (:1058, :1230-1241)
+//   k_primal_commit     (vector blocks only) the updates, change_basis
+//   factor update       the Schur-complement column of the pivot
+// ---------------------------------------------------------------------------
+__global__ void __launch_bounds__(1024) k_sp_primal_top(SpxDev d, int pse, int ncc)
+{
+    DState *st = d.st;
+    const int lane = threadIdx.x & 63;
+    const int stop = st->stop;
+    const int iter_left = st->iter_left, refact = st->refact_pending, refct = st->refct, phase = st->phase;
+    const int pinf = st->dinf;
+    Cand cc = no_cand(0.0);
+    for (int b = lane; b < ncc; b += 64) {
+        const Cand e = cand_chuzr(d)[b];
+        if (better<0>(e, cc)) cc = e;
+    }
+    if (stop) return;
+    int why = ST_RUN;
+    if (iter_left <= 0 || refact) why = refact ? ST_REFACT : ST_BATCH;
+    const bool reset = (why == ST_RUN && pse && refct == 0);
+    if (why == ST_RUN && phase == 1 && !pinf) why = ST_PHASE;
+    const Cand best = wave_best<0>(cc);
+    if (why == ST_RUN && best.idx == 0) why = ST_Q0;
+    if (why != ST_RUN) {
+        if (threadIdx.x == 0) {
+            if (why == ST_Q0) st->q = 0;
+            st->stop = why;
+        }
+        return;
+    }
+    if (reset) {
+        const int nsl = st->nwl;
+        for (int l = threadIdx.x; l < nsl; l += blockDim.x) d.wpos[d.wlist[l]] = -1;
+        reset_refsp_dev(d, 0);                // refsp := non-basic variables, gamma := 1 (syncs)
+        if (threadIdx.x == 0) st->nwl = 0;
+    }
+    const int q = best.idx, kq = best.aux;
+    build_hq(d, q);                           // h = -N[q] (syncs)
+    if (threadIdx.x == 0) {
+        st->q = q;
+        st->kq = kq;
+    }
+}
+
+__global__ void __launch_bounds__(256) k_sp_primal_groups(SpxDev d, int pse)
+{
+    DState *st = d.st;
+    const int m = d.m;
+    const int lane = threadIdx.x & 63;
+    const int grp = blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int r = blockIdx.x * 256 + threadIdx.x;
+    const bool act = r < m;
+    const int stop = st->stop;
+    const int q = max(st->q, 1), phase = st->phase, rtest = st->rtest;
+    const double tol_piv = st->tol_piv, tol_bnd = st->tol_bnd;
+    const double tv = act ? d.tcol[r] : 0.0, bb = act ? d.bbar[r] : 0.0;
+    const int kh = act ? d.head[r] : 1;
+    const int tk = act ? d.type[kh - 1] : 0;
+    const double lbk = act ? d.lb[kh - 1] : 0.0, ubk = act ? d.ub[kh - 1] : 0.0, ck = act ? d.coef[kh - 1] : 0.0;
+    const bool refk = act && pse && d.refsp[kh - 1] != 0;
+    const double dq = d.cbar[q - 1];
+    if (stop) return;
+    const double bmax = wmax(fabs(tv));
+    const double ds = wsum((tv != 0.0) ? ck * tv : 0.0);
+    double vs = 0.0;
+    if (pse) {
+        const double v = (tv != 0.0 && refk) ? tv : 0.0;
+        if (act) d.h[r] = v;                  // v for update_gamma's BTRAN (h is free after the FTRAN)
+        vs = wsum(v * v);
+    }
+    PRatio x;
+    x.eps = tol_piv * (1.0 + 0.01 * bmax);    // group-local tolerance <= the global one
+    x.s = (dq > 0.0 ? -1.0 : +1.0);
+    x.rtol = (rtest == RT_HAR) ? 0.30 * tol_bnd : 0.0;
+    x.phase = phase;
+    Cand c = no_cand(DBL_MAX);
+    Cand e;
+    if (act && prow_cand<1>(x, tv, bb, tk, lbk, ubk, ck, r, kh, 0.0, e)) c = e;
+    const Cand b1 = wave_best<1>(c);
+    if (lane == 0) {
+        ptmax(d)[grp] = bmax;
+        pdsum(d)[grp] = ds;
+        if (pse) pvsum(d)[grp] = vs;
+        pcand1(d)[grp] = b1;
+    }
+}
+
+__global__ void __launch_bounds__(1024) k_sp_primal_pick(SpxDev d, int gm)
+{
+    DState *st = d.st;
+    const int m = d.m;
+    const int stop = st->stop, nr = st->nr;
+    const PPick pk = ppick_load(d, gm);
+    if (stop) return;
+    int kp = 0, ps = 0;
+    double teta = 0.0;
+    const int p = ppick_resolve(d, pk, true, &kp, &ps, &teta);
+    if (p == 0) return;
+    if (threadIdx.x == 0) {
+        st->p = p;
+        st->kp = kp;
+        st->p_stat = (p > 0 && d.type[kp - 1] == FX) ? NS : ps;
+        st->teta = teta;
+        st->ns = (p > 0) ? nr + (kp <= m ? 1 : 0) : 0;
+        st->dinf = 0;
+    }
+}
+
+void colpass_gated(hipStream_t s, const MatDev &A, int mode, int off, int cnt, const int *head,
+                   const signed char *stat, const double *coef, const double *h, const double *x,
+                   const double *y, double *out1, double *out2, unsigned long long *maxbits,
+                   const DState *st, int need_p);
+
+void primal_iteration_sparse(hipStream_t s, const SpxDev &d, int pse)
+{
+    const int m = d.m, n = d.n;
+    const int gv = cdiv(std::max(m, n), 256), gm = cdiv(m, 256), tiles_m = cdiv(m, 512);
+    const int ng = cdiv(m, 64);
+    hipLaunchKernelGGL(k_sp_primal_top, dim3(1), dim3(1024), 0, s, d, pse, 4 * gv);
+    sp_pivot_ftran(*d.sp, s, d.st, d.h, nullptr, d.tcol, nullptr, 0);
+    hipLaunchKernelGGL(k_sp_primal_groups, dim3(gm), dim3(256), 0, s, d, pse);
+    hipLaunchKernelGGL(k_primal_ratio, dim3(gm), dim3(256), 0, s, d, gm, ng, 64, pse);
+    hipLaunchKernelGGL(k_sp_primal_pick, dim3(1), dim3(1024), 0, s, d, gm);
+    if (pse) sp_pivot_btran2(*d.sp, s, d.st, d.h, d.rho, d.u);
+    else sp_pivot_btran(*d.sp, s, d.st, d.rho);
+    colpass_gated(s, d.A, pse ? CP_TROW_S : CP_TROW, m, n, d.head, d.stat, d.coef, nullptr, d.rho, pse ? d.u : nullptr,
+                  d.trow, pse ? d.s : nullptr, nullptr, d.st, 1);
+    hipLaunchKernelGGL(k_primal_commit, dim3(gv), dim3(256), 0, s, d, pse, gv, tiles_m, 1, 96.0 * ((double)m + n), 0);
+    sp_pivot_update(*d.sp, s, d.st);
+}
+
+// ---------------------------------------------------------------------------
 // host side
 // ---------------------------------------------------------------------------
 DualPlan primal_plan(const SpxDev &d, int nr_max, int pse)

@@ -107,7 +107,7 @@ struct SpTriDevBufs {
 struct SpFactor {
     int m = -1;
     SpTriDevBufs fl, fu, bu, bl;
-    SBuf<double> Y, Minv, zq, tpart, bt, scr;
+    SBuf<double> Y, Minv, zq, tpart, bt, scr, scr2;
     SBuf<int> P, hdr;                     // hdr: nlev of fl, fu, bu, bl; k (updates in the chain)
     long long nnz_l = 0, nnz_u = 0;
     int levels[4] = {0, 0, 0, 0};
@@ -115,7 +115,8 @@ struct SpFactor {
     ~SpFactor()
     {
         fl.release(); fu.release(); bu.release(); bl.release();
-        Y.release(); Minv.release(); zq.release(); tpart.release(); bt.release(); scr.release(); P.release();
+        Y.release(); Minv.release(); zq.release(); tpart.release(); bt.release(); scr.release(); scr2.release();
+        P.release();
         hdr.release();
     }
 };
@@ -607,6 +608,7 @@ struct WoodDev {
     double *zq;                                   // inv(B0) h of the last pivot's FTRAN
     double *tpart;                                // Y' e partials of a general BTRAN (SP_KMAX per block)
     double *bt;                                   // BTRAN scratch (positions), FTRAN scratch z (2 x m)
+    double *scr2;                                 // BTRAN step-space scratch (2 x m)
 };
 
 struct SpDev {
@@ -688,36 +690,53 @@ __global__ void __launch_bounds__(256) k_sp_btran_part(SpDev sp, const double *e
 
 // BTRAN part 2 (one workgroup): e' = e - S inv(M)' (Y' e), then y = inv(B0)' e'
 // mode 0: e general (partials from k_sp_btran_part over nparts blocks);
-// mode 1: e = e_p of the pivot (st->p): Y' e_p is row p of Y
+// mode 1: e = e_p of the pivot (st->p): Y' e_p is row p of Y;
+// mode 2: both — e_p into y, e1 (general, partials) into y1 (the primal's
+//         rho and update_gamma's u = inv(B)' v in one sweep pair)
+template <int NRHS>
 __global__ void __launch_bounds__(1024) k_sp_btran(SpDev sp, DState *st, const double *e, double *y, int mode,
-                                                   int nparts)
+                                                   int nparts, const double *e1, double *y1)
 {
-    if (mode == 1 && st->stop) return;
+    if (mode >= 1 && (st->stop || st->p <= 0)) return;
     const int m = sp.m, k = *sp.w.k;
-    const int p = (mode == 1) ? st->p - 1 : -1;
-    __shared__ double tv[SP_KMAX], sv[SP_KMAX];
-    double *b = sp.w.bt;                          // positions
-    double *w = sp.w.bt + m;                      // step space
+    const int p = (mode >= 1) ? st->p - 1 : -1;
+    __shared__ double tv[2][SP_KMAX], sv[2][SP_KMAX];
+    double *b0 = sp.w.bt, *b1 = sp.w.bt + m;      // positions
+    double *w0 = sp.w.scr2, *w1 = sp.w.scr2 + m;  // step space
     for (int t = threadIdx.x; t < k; t += blockDim.x) {
-        double a = 0.0;
-        if (mode == 1) a = sp.w.Y[(size_t)p * SP_KMAX + t];
+        double a = 0.0, a1 = 0.0;
+        if (mode >= 1) a = sp.w.Y[(size_t)p * SP_KMAX + t];
         else
             for (int q = 0; q < nparts; q++) a += sp.w.tpart[(size_t)q * SP_KMAX + t];
-        tv[t] = a;
+        if (NRHS == 2)
+            for (int q = 0; q < nparts; q++) a1 += sp.w.tpart[(size_t)q * SP_KMAX + t];
+        tv[0][t] = a;
+        tv[1][t] = a1;
     }
-    for (int i = threadIdx.x; i < m; i += blockDim.x) b[i] = (mode == 1) ? (i == p ? 1.0 : 0.0) : e[i];
+    for (int i = threadIdx.x; i < m; i += blockDim.x) {
+        b0[i] = (mode >= 1) ? (i == p ? 1.0 : 0.0) : e[i];
+        if (NRHS == 2) b1[i] = e1[i];
+    }
     __syncthreads();
     for (int t = threadIdx.x; t < k; t += blockDim.x) {
-        double a = 0.0;
-        for (int u = 0; u < k; u++) a += sp.w.Minv[(size_t)u * SP_KMAX + t] * tv[u];   // inv(M)'
-        sv[t] = a;
+        double a = 0.0, a1 = 0.0;
+        for (int u = 0; u < k; u++) {
+            const double mi = sp.w.Minv[(size_t)u * SP_KMAX + t];    // inv(M)'
+            a += mi * tv[0][u];
+            if (NRHS == 2) a1 += mi * tv[1][u];
+        }
+        sv[0][t] = a;
+        sv[1][t] = a1;
     }
     __syncthreads();
     if (threadIdx.x == 0)
-        for (int t = 0; t < k; t++) b[sp.w.P[t]] -= sv[t];   // positions may repeat only in order
+        for (int t = 0; t < k; t++) {                  // positions may repeat only in order
+            b0[sp.w.P[t]] -= sv[0][t];
+            if (NRHS == 2) b1[sp.w.P[t]] -= sv[1][t];
+        }
     __syncthreads();
-    tri_sweep<1>(sp.bu, b, nullptr, w, nullptr);
-    tri_sweep<1>(sp.bl, w, nullptr, y, nullptr);
+    tri_sweep<NRHS>(sp.bu, b0, b1, w0, w1);
+    tri_sweep<NRHS>(sp.bl, w0, w1, y, y1);
 }
 
 // the update of this pivot (one workgroup, after the commit): the column
@@ -728,7 +747,7 @@ __global__ void __launch_bounds__(1024) k_sp_btran(SpDev sp, DState *st, const d
 // dense inverse.
 __global__ void __launch_bounds__(1024) k_sp_update(SpDev sp, DState *st)
 {
-    if (st->stop) return;
+    if (st->stop || st->p <= 0) return;          // (primal: p = -1 is a bound flip, no basis change)
     const int m = sp.m, k = *sp.w.k;
     const int p = st->p - 1;
     __shared__ int slot;
@@ -865,7 +884,7 @@ static SpDev sp_dev(SpFactor &F)
     d.bu = tri_dev(F.bu, F.hdr.p + 2);
     d.bl = tri_dev(F.bl, F.hdr.p + 3);
     d.w.Y = F.Y.p; d.w.P = F.P.p; d.w.Minv = F.Minv.p; d.w.k = F.hdr.p + 4; d.w.zq = F.zq.p;
-    d.w.tpart = F.tpart.p; d.w.bt = F.bt.p;
+    d.w.tpart = F.tpart.p; d.w.bt = F.bt.p; d.w.scr2 = F.scr2.p;
     return d;
 }
 
@@ -920,6 +939,7 @@ int sp_factorize(SpFactor &F, hipStream_t s, int m, const int *head1, const int 
         F.zq.ensure(m);
         F.bt.ensure((size_t)2 * m);
         F.scr.ensure(m);
+        F.scr2.ensure((size_t)2 * m);
         F.tpart.ensure((size_t)SP_KMAX * ((m + 255) / 256 + 1));
     }
     F.P.ensure(SP_KMAX);
@@ -956,14 +976,27 @@ void sp_btran(SpFactor &F, hipStream_t s, const double *x, double *y)
     SpDev d = sp_dev(F);
     const int nb = (m + 255) / 256;
     hipLaunchKernelGGL(k_sp_btran_part, dim3(nb), dim3(256), 0, s, d, x);
-    hipLaunchKernelGGL(k_sp_btran, dim3(1), dim3(1024), 0, s, d, (DState *)nullptr, x, y, 0, nb);
+    hipLaunchKernelGGL(k_sp_btran<1>, dim3(1), dim3(1024), 0, s, d, (DState *)nullptr, x, y, 0, nb,
+                       (const double *)nullptr, (double *)nullptr);
 }
 
 // the pivot's hooks (gated on the stop word, captured with the rest)
 void sp_pivot_btran(SpFactor &F, hipStream_t s, DState *st, double *rho)
 {
     SpDev d = sp_dev(F);
-    hipLaunchKernelGGL(k_sp_btran, dim3(1), dim3(1024), 0, s, d, st, (const double *)nullptr, rho, 1, 0);
+    hipLaunchKernelGGL(k_sp_btran<1>, dim3(1), dim3(1024), 0, s, d, st, (const double *)nullptr, rho, 1, 0,
+                       (const double *)nullptr, (double *)nullptr);
+}
+
+// the primal's BTRANs of a pivot (p > 0 only): rho = inv(B)' e_p and
+// update_gamma's u = inv(B)' v in one sweep pair
+void sp_pivot_btran2(SpFactor &F, hipStream_t s, DState *st, const double *v, double *rho, double *u)
+{
+    const int m = F.m;
+    SpDev d = sp_dev(F);
+    const int nb = (m + 255) / 256;
+    hipLaunchKernelGGL(k_sp_btran_part, dim3(nb), dim3(256), 0, s, d, v);
+    hipLaunchKernelGGL(k_sp_btran<2>, dim3(1), dim3(1024), 0, s, d, st, (const double *)nullptr, rho, 2, nb, v, u);
 }
 
 void sp_pivot_ftran(SpFactor &F, hipStream_t s, const DState *st, double *h, double *work, double *tcol, double *u,

@@ -22,14 +22,14 @@ from test_gpu_lp import check_solution
 
 pytestmark = pytest.mark.gpu
 
-SPARSE_DUAL = []
+SPARSE_RUNS = []
 for path in golden_files("lp_"):
     d = load_golden(path)
     if d.get("gen", {}).get("kind") == "dense":
         continue
     for r, run in enumerate(d["runs"]):
-        if run["opts"].get("meth") in (2, 3) and not run["opts"].get("it_lim"):
-            SPARSE_DUAL.append(pytest.param(path, r, id=f"{os.path.basename(path)[3:-5]}-{r}"))
+        if not run["opts"].get("it_lim"):
+            SPARSE_RUNS.append(pytest.param(path, r, id=f"{os.path.basename(path)[3:-5]}-{r}-m{run['opts'].get('meth', 1)}"))
 
 
 @pytest.fixture
@@ -37,8 +37,10 @@ def sparse_on(monkeypatch):
     monkeypatch.setenv("GK_SPARSE", "1")
 
 
-@pytest.mark.parametrize("path,run_index", SPARSE_DUAL)
-def test_gpu_sparse_dual_matches_reference(gpu_ctx, sparse_on, path, run_index):
+@pytest.mark.parametrize("path,run_index", SPARSE_RUNS)
+def test_gpu_sparse_matches_reference(gpu_ctx, sparse_on, path, run_index):
+    """Every LP fixture with sparse A, both methods (primal, dual, dual-then-
+    primal), on the sparse factor."""
     d = load_golden(path)
     run = d["runs"][run_index]
     prob = problems.from_fixture(d)
@@ -83,15 +85,40 @@ def test_gpu_sparse_blocks_match_oracle(gpu_ctx, sparse_on, oracle, blocks, link
           f"({P.it_cnt / st.seconds_total:.0f} pivots/s), refactor {st.seconds_reinvert:.2f} s")
 
 
-def test_gpu_sparse_primal_beyond_limit_fails_loudly(gpu_ctx):
-    """Beyond the explicit inverse (m > 65535) the sparse factor serves the
-    dual simplex; a primal request there is refused with a message (no
-    silent fallback).  Below it, GK_SPARSE=1 leaves the primal (and the
-    primal leg of GLP_DUALP) on the explicit inverse."""
-    P = gk.GkProblem(gpu_ctx, problems.gen_blocks(656, 100, 200, 50))
-    assert P.p.m > 65535
-    with pytest.raises(gk.GkError, match="sparse factor"):
-        gk.glp_simplex(P, gk.SMCP(meth=gk.GLP_PRIMAL, msg_lev=gk.GLP_MSG_ERR))
+def test_gpu_sparse_c2s_full_primal(gpu_ctx, sparse_on):
+    """C2s, whole primal solve on the sparse factor: the reference's primal
+    objective 357.82820943518863, KKT-certified."""
+    prob = problems.gen_c2s()
+    P = gk.GkProblem(gpu_ctx, prob)
+    assert gk.glp_simplex(P, gk.SMCP(meth=gk.GLP_PRIMAL, msg_lev=gk.GLP_MSG_ERR)) == 0
+    assert abs(P.obj_val - 357.82820943518863) <= 1e-9 * 357.82820943518863, P.obj_val
+    sparse_kkt(P, prob)
+
+
+@pytest.mark.parametrize("blocks,links", [(10, 5), (40, 10)])
+def test_gpu_sparse_blocks_primal_match_oracle(gpu_ctx, sparse_on, oracle, blocks, links):
+    prob = problems.gen_blocks(blocks, 100, 200, links)
+    o = oracle.OracleProb(prob)
+    assert o.simplex(meth=1) == 0
+    ref = o.result()["obj_val"]
+    P = gk.GkProblem(gpu_ctx, prob)
+    assert gk.glp_simplex(P, gk.SMCP(meth=gk.GLP_PRIMAL, msg_lev=gk.GLP_MSG_ERR)) == 0
+    assert abs(P.obj_val - ref) <= 1e-9 * max(1.0, abs(ref)), (P.obj_val, ref)
+    sparse_kkt(P, prob)
+
+
+def test_gpu_sparse_beyond_explicit_limit(gpu_ctx):
+    """m > 65535 takes the sparse factor by itself (no GK_SPARSE): a block-
+    angular LP of 65,650 rows, the first 2,000 pivots of each method through
+    it (it_lim), statuses and bounds kept (the whole solves are
+    tools/sparse_big.py runs, profiles/r04_sparse_*)."""
+    prob = problems.gen_blocks(656, 100, 200, 50)
+    assert prob.m > 65535
+    for meth in (gk.GLP_DUAL, gk.GLP_PRIMAL):
+        P = gk.GkProblem(gpu_ctx, prob.copy())
+        ret = gk.glp_simplex(P, gk.SMCP(meth=meth, it_lim=2000, msg_lev=gk.GLP_MSG_ERR))
+        assert ret == problems.GLP_EITLIM and P.it_cnt == 2000
+        check_solution(P)
 
 
 def test_gpu_sparse_phase_and_limits(gpu_ctx, sparse_on):
