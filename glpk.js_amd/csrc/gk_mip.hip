@@ -58,6 +58,7 @@ struct NodeProb {
     const double *A;              // dense col-major m x n (unscaled)
     const double *c;              // internal minimisation costs, [m+n] (0 for rows)
     const signed char *isint;     // [n]
+    const double *rlb, *rub;      // [m] row bounds (the same at every node)
     double tol_int;
     int dth;                      // 1: choose the branching column by branch_drtom
 };
@@ -75,7 +76,33 @@ struct NodeIO {
     signed char *stat_out;        // [nb][m+n]
     double *scratch;              // GLOBAL kernel: per-node work area (node_lp_lds(m, n) bytes each)
     size_t scratch_stride;        // in doubles
+    // node records in HBM (the B&B bookkeeping on the device): an optimal
+    // node stores its final tableau, column bounds and statuses; a child
+    // starts from its parent's record — the tableau instead of inverting its
+    // basis again (warm start), and, when br_j[b] >= 0, the bounds and
+    // statuses with the branching change applied here (the host keeps no
+    // arrays for such a child).  tab_in[b]: the parent's record or null;
+    // tab_out[b]: where this node's goes (or null).  Record layout:
+    // [0] pivots since the last inversion, [1..m] head, T (m x (m+n),
+    // row-major), lb[n], ub[n] of the columns, stat[m+n] (bytes)
+    const double *const *tab_in;
+    double *const *tab_out;
+    int tab_age_max;              // an older tableau is inverted again
+    const int *br_j, *br_dir;     // [nb] branching column (-1: bounds from lb / ub / stat_in), 0 down / 1 up
+    const double *br_val;         // [nb] the column's value in the parent's solution
+    // check_integrality (glpios03.js:55) on the node's final bounds, and the
+    // branching rules' candidates: fractional count, sum of integer
+    // infeasibilities, first / last / most fractional column (0-based, -1:
+    // none) and branch_mostf's direction
+    int *nfrac, *jfirst, *jlast, *jmost, *nmost;
+    double *iisum;
 };
+
+__host__ __device__ inline size_t node_rec_bounds(int m, int n) { return 1 + (size_t)m + (size_t)m * (m + n); }
+__host__ __device__ inline size_t node_rec_doubles(int m, int n)
+{
+    return node_rec_bounds(m, n) + 2 * (size_t)n + ((size_t)m + n + 7) / 8;
+}
 
 // ---- small block helpers (blockDim.x = 256) --------------------------------
 // argmax of key (ties: lowest idx); idx < 0 = none
@@ -331,13 +358,42 @@ __global__ void __launch_bounds__(256) k_node_lp(NodeProb P, NodeIO io)
     int *head = (int *)(rinfo + 6 * (m + 1));
     signed char *stat = (signed char *)(head + m);
     signed char *chg = stat + N;              // n
-    const double *glb = io.lb + (size_t)b * N, *gub = io.ub + (size_t)b * N;
-    const signed char *gst = io.stat_in + (size_t)b * N;
     double *gbnd = io.bnd + (size_t)b * 2 * n, *gdz = io.dzb + (size_t)b * 2 * n;
-    for (int k = threadIdx.x; k < N; k += blockDim.x) {
-        lb[k] = glb[k];
-        ub[k] = gub[k];
-        stat[k] = gst[k];
+    const double *tin = io.tab_in ? io.tab_in[b] : nullptr;
+    const int brj = io.br_j ? io.br_j[b] : -1;
+    if (brj >= 0) {
+        // a child built here from its parent's stored record (fill_child of
+        // the host driver, on the device): the parent's final column bounds
+        // and statuses, the branching bound (glpios03.js:141-186), statuses
+        // that follow the column types (glp_set_col_bnds)
+        const double *rb = tin + node_rec_bounds(m, n);
+        const signed char *rs = (const signed char *)(rb + 2 * (size_t)n);
+        for (int k = threadIdx.x; k < N; k += blockDim.x) {
+            double l, u;
+            if (k < m) { l = P.rlb[k]; u = P.rub[k]; }
+            else { l = rb[k - m]; u = rb[n + k - m]; }
+            signed char s = rs[k];
+            if (k - m == brj) {
+                const double beta = io.br_val[b];
+                if (io.br_dir[b] == 0) u = floor(beta);
+                else l = ceil(beta);
+            }
+            if (k >= m && s != BS) {
+                if (l == u) s = NS;
+                else if (s == NS) s = (l != -DBL_MAX) ? NL : (u != DBL_MAX ? NU : NF);
+            }
+            lb[k] = l;
+            ub[k] = u;
+            stat[k] = s;
+        }
+    } else {
+        const double *glb = io.lb + (size_t)b * N, *gub = io.ub + (size_t)b * N;
+        const signed char *gst = io.stat_in + (size_t)b * N;
+        for (int k = threadIdx.x; k < N; k += blockDim.x) {
+            lb[k] = glb[k];
+            ub[k] = gub[k];
+            stat[k] = gst[k];
+        }
     }
     for (int j = threadIdx.x; j < n; j += blockDim.x) {
         chg[j] = 0;
@@ -358,6 +414,50 @@ __global__ void __launch_bounds__(256) k_node_lp(NodeProb P, NodeIO io)
         return;
     }
     put_bounds();
+    // warm start: the parent's tableau, when its basis is still this node's
+    // (the node's statuses come from the parent's final ones; preprocessing
+    // only moves non-basic columns) and it is young enough
+    int age = 0;
+    if (tin) {
+        age = (int)tin[0];
+        if (threadIdx.x == 0) {
+            int ok = age < io.tab_age_max;
+            for (int i = 0; i < m && ok; ++i) {
+                const int k = (int)tin[1 + i];
+                if (k < 0 || k >= N || stat[k] != BS) ok = 0;
+            }
+            if (ok) {
+                int nbs = 0;
+                for (int k = 0; k < N; ++k) nbs += stat[k] == BS;
+                ok = nbs == m;
+            }
+            sh_flag = ok ? 2 : 0;
+        }
+        __syncthreads();
+        if (sh_flag != 2) { tin = nullptr; age = 0; }
+        __syncthreads();
+    }
+#define T_(i, j) M[(size_t)(i) * W + m + (j)]
+    if (tin) {
+        // the rows in variable order, as the inversion below leaves them
+        // (the dual ratio tests break ties by row: a warm-started node then
+        // takes the pivots a cold-started one would)
+        int *rk = (int *)fcol;
+        for (int i = threadIdx.x; i < m; i += blockDim.x) {
+            const int k = (int)tin[1 + i];
+            int r = 0;
+            for (int i2 = 0; i2 < m; ++i2) r += (int)tin[1 + i2] < k;
+            rk[i] = r;
+            head[r] = k;
+        }
+        __syncthreads();
+        const double *tt = tin + 1 + m;
+        for (int e = threadIdx.x; e < m * N; e += blockDim.x) {
+            const int i = e / N, k = e - i * N;
+            T_(rk[i], k) = tt[e];
+        }
+        __syncthreads();
+    } else {
     // basis header in variable order (glp_factorize's head, glpapi12.js:44-67)
     if (threadIdx.x == 0) {
         int j = 0;
@@ -424,7 +524,7 @@ __global__ void __launch_bounds__(256) k_node_lp(NodeProb P, NodeIO io)
         __syncthreads();
     }
     // T[i][j] = M[i][m + j]  (row length W kept; T(i, j) = M[i*W + m + j])
-#define T_(i, j) M[(size_t)(i) * W + m + (j)]
+    }
     // d = c - c_B' T
     for (int k = threadIdx.x; k < N; k += blockDim.x) {
         if (stat[k] == BS) { d[k] = 0.0; continue; }
@@ -567,6 +667,17 @@ __global__ void __launch_bounds__(256) k_node_lp(NodeProb P, NodeIO io)
         it++;
     }
     __syncthreads();
+    // the children's warm start
+    double *tout = io.tab_out ? io.tab_out[b] : nullptr;
+    if (tout && status == NODE_OPT) {
+        if (threadIdx.x == 0) tout[0] = (double)(age + it);
+        for (int i = threadIdx.x; i < m; i += blockDim.x) tout[1 + i] = (double)head[i];
+        double *tt = tout + 1 + m;
+        for (int e = threadIdx.x; e < m * N; e += blockDim.x) {
+            const int i = e / N, k = e - i * N;
+            tt[e] = T_(i, k);
+        }
+    }
     double zs = 0.0;
     for (int k = threadIdx.x; k < N; k += blockDim.x) zs += P.c[k] * x[k];
     const double z = block_sum256(zs, shk);
@@ -709,11 +820,63 @@ __global__ void __launch_bounds__(256) k_node_lp(NodeProb P, NodeIO io)
                 }
             }
         }
+        // check_integrality (glpios03.js:55) as the host driver states it
+        // (MipSolver::integrality), in column order: the count, the sum of
+        // integer infeasibilities, and the candidates of branch_first /
+        // branch_last / branch_mostf (glpios09.js:28-82)
+        int nf = 0, jf = -1, jl = -1, jm = -1, nm = 0;
+        double ii = 0.0, most = DBL_MAX;
+        bool jj_cand = false;
+        const double tol = P.tol_int;
+        for (int j = 0; j < n; ++j) {
+            const int k = m + j;
+            if (!P.isint[j] || stat[k] != BS) continue;
+            const double v = x[k], l = lb[k], u = ub[k];
+            if (l != -DBL_MAX) {
+                if (l - tol <= v && v <= l + tol) continue;
+                if (v < l) continue;
+            }
+            if (u != DBL_MAX) {
+                if (u - tol <= v && v <= u + tol) continue;
+                if (v > u) continue;
+            }
+            const double r = floor(v + 0.5);
+            if (r - tol <= v && v <= r + tol) continue;
+            nf++;
+            if (jf < 0) jf = j;
+            jl = j;
+            if (jj == j + 1) jj_cand = true;
+            const double t1 = v - floor(v), t2 = ceil(v) - v;
+            ii += (t1 <= t2 ? t1 : t2);
+            const double temp = floor(v) + 0.5;
+            if (most > fabs(v - temp)) {
+                jm = j;
+                most = fabs(v - temp);
+                nm = v < temp ? -1 : +1;
+            }
+        }
+        io.nfrac[b] = nf;
+        io.iisum[b] = ii;
+        io.jfirst[b] = jf;
+        io.jlast[b] = jl;
+        io.jmost[b] = jm;
+        io.nmost[b] = nm;
         io.status[b] = NODE_OPT;
         io.obj[b] = z;
         io.pivots[b] = it;
-        io.jj[b] = any_frac ? jj : 0;
+        // the tableau's choice only if it is a candidate of the host's test
+        io.jj[b] = (any_frac && jj_cand) ? jj : 0;
         io.next[b] = next;
+    }
+    // the children's record: final column bounds and statuses
+    if (tout) {
+        double *rb = tout + node_rec_bounds(m, n);
+        signed char *rs = (signed char *)(rb + 2 * (size_t)n);
+        for (int j = threadIdx.x; j < n; j += blockDim.x) {
+            rb[j] = lb[m + j];
+            rb[n + j] = ub[m + j];
+        }
+        for (int k = threadIdx.x; k < N; k += blockDim.x) rs[k] = stat[k];
     }
 #undef T_
 }
@@ -775,9 +938,71 @@ struct HostArr {
     }
 };
 
+// the node records kept in HBM (NodeIO tab_in / tab_out): slots of
+// node_rec_doubles(m, n) in chunks that never move (a slot's address goes
+// into the kernel's tab_in / tab_out), reference counted — one reference for
+// the batch that writes the record, one per child or parked node reading it.
+// At most cap_bytes of them (GK_BNB_TAB_MB, default 8 GiB of the 288 GiB);
+// beyond that a node stores none: the host fills its children's arrays and
+// they invert their basis
+struct TabStore {
+    static constexpr int CHUNK = 1024;
+    std::vector<double *> chunks;
+    std::vector<int> ref, freel;
+    size_t slot = 0, cap_bytes = 0;
+    ~TabStore() { clear(); }
+    void clear()
+    {
+        for (double *p : chunks) (void)hipFree(p);
+        chunks.clear();
+        ref.clear();
+        freel.clear();
+    }
+    // a new search: keep the chunks when the slot size is the same
+    void reset(size_t doubles, size_t cap)
+    {
+        if (doubles != slot) clear();
+        slot = doubles;
+        cap_bytes = cap;
+        freel.clear();
+        for (int i = (int)ref.size() - 1; i >= 0; i--) freel.push_back(i);
+        std::fill(ref.begin(), ref.end(), 0);
+    }
+    int alloc()
+    {
+        if (freel.empty()) {
+            const size_t bytes = slot * sizeof(double) * CHUNK;
+            if ((chunks.size() + 1) * bytes > cap_bytes) return -1;
+            double *p = nullptr;
+            if (hipMalloc((void **)&p, bytes) != hipSuccess) return -1;
+            chunks.push_back(p);
+            const int base = (int)ref.size();
+            ref.resize(ref.size() + CHUNK, 0);
+            for (int i = CHUNK - 1; i >= 0; i--) freel.push_back(base + i);
+        }
+        const int t = freel.back();
+        freel.pop_back();
+        ref[t] = 1;
+        return t;
+    }
+    void inc(int t)
+    {
+        if (t >= 0) ref[t]++;
+    }
+    void dec(int t)
+    {
+        if (t >= 0 && --ref[t] == 0) freel.push_back(t);
+    }
+    double *ptr(int t) const { return t < 0 ? nullptr : chunks[t / CHUNK] + (size_t)(t % CHUNK) * slot; }
+};
+
 // what a node knows about its parent (the reference keeps it in node.up and
 // in the branching fields of the parent: glpios01.js, glpios03.js:141)
 struct NodeMeta {
+    int tab = -1;                 // the parent's record (TabStore slot), -1: none
+    bool inl = true;              // the pool slot holds the node's bounds and statuses;
+                                  // false: the kernel builds them from the record tab
+    int br_dir = 0;               // 0: the down branch (ub = floor), 1: up (lb = ceil)
     int level = 0;
     int br_var = -1;              // column the parent branched on (0-based); -1: root
     double br_val = 0.0;          // its value in the parent's LP solution (ios_pcost_update)
@@ -808,6 +1033,7 @@ struct NodeWorse {                // heap order: a is selected after b
 // parent information, recycled through a free list
 struct NodePool {
     int n = 0, N = 0;
+    TabStore *tabs = nullptr;
     std::vector<double> bnd;
     std::vector<signed char> st;
     std::vector<NodeMeta> meta;
@@ -825,10 +1051,22 @@ struct NodePool {
         meta.emplace_back();
         return sl;
     }
-    void release(int sl) { freel.push_back(sl); }
+    void release(int sl)
+    {
+        if (tabs) tabs->dec(meta[sl].tab);
+        meta[sl].tab = -1;
+        meta[sl].inl = true;
+        freel.push_back(sl);
+    }
     double *lb(int sl) { return bnd.data() + (size_t)sl * 2 * n; }
     double *ub(int sl) { return bnd.data() + (size_t)sl * 2 * n + n; }
     signed char *stat(int sl) { return st.data() + (size_t)sl * N; }
+};
+
+// check_integrality's results from the node kernel (NodeIO nfrac ...)
+struct KInt {
+    int nfrac, jf, jl, jm, nm;
+    double ii;
 };
 
 // one batch entry: a node LP, or a pseudocost probe (a node with one
@@ -837,18 +1075,22 @@ struct Entry {
     int kind;                     // 0 node, 1 probe
     NodeRec nd;
     int pid, j, dir;              // probe: parked node, column, 0 down / 1 up
+    int tab_out = -1;             // node: the TabStore slot its tableau goes to
 };
 
 // packed batch buffers (one copy each way): byte offsets for nb entries
 struct Layout {
-    size_t lb, ub, cut, itl, pp, st, in_end;
-    size_t obj, dz, x, bnd, stat, piv, jj, next, sto, out_end;
+    size_t lb, ub, cut, brv, tin, tout, itl, pp, brj, brd, st, in_end;
+    size_t obj, ii, dz, x, bnd, stat, piv, jj, next, nf, jf, jl, jm, nm, sto, out_end;
     Layout(size_t N, size_t n, size_t nb)
     {
-        lb = 0; ub = lb + 8 * nb * N; cut = ub + 8 * nb * N; itl = cut + 8 * nb; pp = itl + 4 * nb;
-        st = pp + 4 * nb; in_end = st + nb * N;
-        obj = 0; dz = obj + 8 * nb; x = dz + 16 * nb * n; bnd = x + 8 * nb * N; stat = bnd + 16 * nb * n;
-        piv = stat + 4 * nb; jj = piv + 4 * nb; next = jj + 4 * nb; sto = next + 4 * nb; out_end = sto + nb * N;
+        lb = 0; ub = lb + 8 * nb * N; cut = ub + 8 * nb * N; brv = cut + 8 * nb; tin = brv + 8 * nb;
+        tout = tin + 8 * nb; itl = tout + 8 * nb; pp = itl + 4 * nb; brj = pp + 4 * nb; brd = brj + 4 * nb;
+        st = brd + 4 * nb; in_end = st + nb * N;
+        obj = 0; ii = obj + 8 * nb; dz = ii + 8 * nb; x = dz + 16 * nb * n; bnd = x + 8 * nb * N;
+        stat = bnd + 16 * nb * n; piv = stat + 4 * nb; jj = piv + 4 * nb; next = jj + 4 * nb; nf = next + 4 * nb;
+        jf = nf + 4 * nb; jl = jf + 4 * nb; jm = jl + 4 * nb; nm = jm + 4 * nb; sto = nm + 4 * nb;
+        out_end = sto + nb * N;
     }
 };
 
@@ -875,6 +1117,7 @@ struct Parked {
     std::vector<signed char> so;
     std::vector<int> cand;
     int pending = 0;
+    int tab = -1;                        // its tableau (the probes' and the children's warm start)
 };
 
 // the device and pinned host buffers of the driver, kept by the context
@@ -969,8 +1212,9 @@ static int bnb_threads()
 
 struct MipCache {
     BatchBuf bufs[2];
-    DevArr<double> dA, dc, dscratch;
+    DevArr<double> dA, dc, dscratch, drb;
     DevArr<signed char> dint;
+    TabStore tabs;
     HostWorkers *workers = nullptr;          // made with the first search that has work for them
     ~MipCache() { delete workers; }
 };
@@ -1107,6 +1351,7 @@ struct MipSolver {
         for (NodeRec &r : open) set_keys(r);
         std::make_heap(open.begin(), open.end(), NodeWorse());
     }
+    int cur_tab = -1;                         // the tableau of the node being analysed (its children's warm start)
     int bingos = 0;                           // new incumbents not yet reported
     std::vector<int> cand_buf;                // node_done's fractional columns
     // GK_BNB_LOG: time stamp counter ticks of node_done's parts (host profile)
@@ -1230,8 +1475,7 @@ struct MipSolver {
     std::vector<FillJob> *defer = nullptr;
     // per-entry scratch of a batch's processing: column bounds (bl | bu),
     // fractional columns, their count and the sum of integer infeasibilities
-    std::vector<double> eb, eii;
-    std::vector<int> ecand, ecand_n;
+    std::vector<double> eb;
     std::vector<FillJob> jobs;
     void fill_child(const FillJob &f)
     {
@@ -1264,10 +1508,19 @@ struct MipSolver {
             const double cb = std::max(bound, round_bound(z + dz[kase]));
             if (!hopeful(cb)) continue;
             const int sl = pool.alloc();
-            const FillJob fj{sl, j, kase, beta, bl, bu, so};
-            if (defer) defer->push_back(fj);
-            else fill_child(fj);
             NodeMeta &cm = pool.meta[sl];
+            cm.tab = cur_tab;
+            cm.br_dir = kase;
+            if (cur_tab >= 0) {
+                // the parent's record holds the arrays: the kernel builds the child
+                pool.tabs->inc(cur_tab);
+                cm.inl = false;
+            } else {
+                cm.inl = true;
+                const FillJob fj{sl, j, kase, beta, bl, bu, so};
+                if (defer) defer->push_back(fj);
+                else fill_child(fj);
+            }
             cm.level = mt.level + 1;
             cm.br_var = j;
             cm.br_val = beta;
@@ -1290,7 +1543,7 @@ struct MipSolver {
     // returns true when the node is parked (its pool slot stays in use)
     bool node_done(const NodeRec &nd, double z, const double *x, const signed char *so, const double *bl,
                    const double *bu, const double *dzb, int kjj, int knext, bool tableau, const int *pcand = nullptr,
-                   int npcand = -1, double pii = 0.0)
+                   int npcand = -1, double pii = 0.0, const KInt *ki = nullptr)
     {
         const NodeMeta mt = pool.meta[nd.slot];
         // ios_pcost_update (glpios09.js:288)
@@ -1308,7 +1561,10 @@ struct MipSolver {
         double ii = 0.0;
         const unsigned long long ti0 = tsc_on ? tsc() : 0ull;
         int nfrac;
-        if (npcand >= 0) {                           // scanned by the batch's workers
+        if (ki) {                                    // scanned by the node kernel
+            nfrac = ki->nfrac;
+            ii = ki->ii;
+        } else if (npcand >= 0) {                    // scanned by the batch's workers
             cand.assign(pcand, pcand + npcand);
             ii = pii;
             nfrac = npcand;
@@ -1326,7 +1582,18 @@ struct MipSolver {
             root_ii = ii;
         }
         int j = -1, next = 0;
-        switch (parm->br_tech) {
+        if (ki && parm->br_tech != 5) {
+            // the kernel's candidates (the same rules as choose_simple)
+            switch (parm->br_tech) {
+            case 1: j = ki->jf; next = next_of(x[m + j]); break;
+            case 2: j = ki->jl; next = next_of(x[m + j]); break;
+            case 3: j = ki->jm; next = ki->nm; break;
+            default:
+                if (kjj > 0) { j = kjj - 1; next = knext; }
+                else { j = ki->jm; next = ki->nm; }
+                break;
+            }
+        } else switch (parm->br_tech) {
         case 1: case 2: case 3:
             j = choose_simple(parm->br_tech, cand, x, next);
             break;
@@ -1359,6 +1626,8 @@ struct MipSolver {
                     pk.probe.assign(2 * (size_t)n, 0.0);
                     pk.cand = cand;
                     pk.pending = (int)need.size();
+                    pk.tab = cur_tab;
+                    if (pool.tabs) pool.tabs->inc(cur_tab);
                     for (auto &pr : need) {
                         Entry e{};
                         e.kind = 1; e.nd = nd; e.pid = pid; e.j = pr.first; e.dir = pr.second;
@@ -1382,6 +1651,22 @@ struct MipSolver {
         return false;
     }
 
+    // a record child's bounds and statuses into its pool slot (the
+    // sharded exchange and the engine fallback read them on the host); its
+    // record stays referenced for the warm start
+    void materialize(int sl)
+    {
+        NodeMeta &mt = pool.meta[sl];
+        if (mt.inl) return;
+        const size_t bytes = 2 * (size_t)n * sizeof(double) + (size_t)N;
+        std::vector<double> rec((bytes + 7) / 8);
+        (void)hipMemcpy(rec.data(), pool.tabs->ptr(mt.tab) + node_rec_bounds(m, n), bytes, hipMemcpyDeviceToHost);
+        std::vector<signed char> so(N);
+        std::memcpy(so.data(), rec.data() + 2 * n, N);
+        fill_child(FillJob{sl, mt.br_var, mt.br_dir, mt.br_val, rec.data(), rec.data() + n, so.data()});
+        mt.inl = true;
+    }
+
     void parked_done(int pid)
     {
         Parked &pk = parked[pid];
@@ -1389,7 +1674,11 @@ struct MipSolver {
         const int j = choose_pcost(pk.cand, pk.x.data(), pk.probe.data(), next);
         const double *bl = pk.bnd.data(), *bu = pk.bnd.data() + n;
         const double dn = pk.dzb[2 * j], up = pk.dzb[2 * j + 1];
+        cur_tab = pk.tab;
         branch(pk.nd, pk.meta, pk.z, pk.bound, pk.ii, pk.x.data(), pk.so.data(), bl, bu, j, next, dn, up);
+        cur_tab = -1;
+        if (pool.tabs) pool.tabs->dec(pk.tab);
+        pk.tab = -1;
         parked_free.push_back(pid);
     }
 
@@ -1434,6 +1723,7 @@ int MipSolver::fallback(const NodeRec &nd, const double *bl, const double *bu, s
         if (sign > 0) sp.obj_ul = mo; else sp.obj_ll = mo;
     }
     sp.it_lim = 0x7fffffff; sp.tm_lim = 0x7fffffff; sp.out_frq = 500; sp.out_dly = 0;
+    materialize(nd.slot);
     for (int attempt = 0; attempt < 2; attempt++) {
         const signed char *st0 = pool.stat(nd.slot);
         for (int i = 0; i < m; i++) rstat[i + 1] = attempt == 0 ? st0[i] : (signed char)BS;
@@ -1531,6 +1821,7 @@ static size_t desc_bytes(int n, int N)
 
 static void put_desc(MipSolver &S, const NodeRec &r, char *p)
 {
+    S.materialize(r.slot);
     const NodeMeta &mt = S.pool.meta[r.slot];
     double *d = (double *)p;
     d[0] = r.bound; d[1] = mt.br_val; d[2] = mt.up_lpobj; d[3] = mt.up_bound; d[4] = mt.up_ii; d[5] = 0.0;
@@ -1547,6 +1838,7 @@ static void get_desc(MipSolver &S, const char *p)
     const double *d = (const double *)p;
     const int sl = S.pool.alloc();
     NodeMeta &mt = S.pool.meta[sl];
+    mt.tab = -1;                          // the sender's tableau stays on its GPU
     mt.br_val = d[1]; mt.up_lpobj = d[2]; mt.up_bound = d[3]; mt.up_ii = d[4];
     const int *iv = (const int *)(d + 6);
     mt.level = iv[0]; mt.br_var = iv[1];
@@ -1733,25 +2025,38 @@ extern "C" int gk_ios_driver_sharded(gk_ctx *ctx, gk_mip *mip, const gk_iocp *pa
         // the previous search may have left events in use: nothing of it is in flight
     }
     MipCache &Cc = *S.cache;
-    Cc.dA.ensure(S.A.size()); Cc.dc.ensure(S.N); Cc.dint.ensure(n);
+    Cc.dA.ensure(S.A.size()); Cc.dc.ensure(S.N); Cc.dint.ensure(n); Cc.drb.ensure(2 * (size_t)m);
     const int BMAX = (lds <= NODE_LDS_MAX) ? 1024 : (int)std::max<size_t>(1, std::min<size_t>(1024, SCRATCH_MAX / lds));
     S.stride = (lds + 255) / 256 * 32;                    // doubles, 256-byte aligned slices
     if (lds > NODE_LDS_MAX) {
         Cc.dscratch.ensure(S.stride * BMAX);
         if (!Cc.dscratch.p) { set_err("gk_ios_driver: out of memory (node work area)"); return GK_EABI; }
     }
-    if (!S.alloc_batch(BMAX) || !Cc.dA.p || !Cc.dc.p || !Cc.dint.p) {
+    if (!S.alloc_batch(BMAX) || !Cc.dA.p || !Cc.dc.p || !Cc.dint.p || !Cc.drb.p) {
         set_err("gk_ios_driver: out of memory");
         return GK_EABI;
     }
     (void)hipMemcpyAsync(Cc.dA.p, S.A.data(), S.A.size() * sizeof(double), hipMemcpyHostToDevice, s);
     (void)hipMemcpyAsync(Cc.dc.p, S.c.data(), S.N * sizeof(double), hipMemcpyHostToDevice, s);
     (void)hipMemcpyAsync(Cc.dint.p, S.isint.data(), n, hipMemcpyHostToDevice, s);
+    (void)hipMemcpyAsync(Cc.drb.p, S.rlb.data(), m * sizeof(double), hipMemcpyHostToDevice, s);
+    (void)hipMemcpyAsync(Cc.drb.p + m, S.rub.data(), m * sizeof(double), hipMemcpyHostToDevice, s);
     NodeProb &P = S.P;
     P.m = m; P.n = n; P.ld = S.N; P.A = Cc.dA.p; P.c = Cc.dc.p; P.isint = Cc.dint.p; P.tol_int = parm->tol_int;
+    P.rlb = Cc.drb.p; P.rub = Cc.drb.p + m;
     P.dth = (parm->br_tech == 4) ? 1 : 0;
     NodePool &pool = S.pool;
     pool.n = n; pool.N = S.N;
+    // warm start store (GK_BNB_WARM=0: every node inverts its basis;
+    // GK_BNB_TAB_MB: its size limit)
+    const size_t tab_cap = [] {
+        const char *w = std::getenv("GK_BNB_WARM");
+        if (w && std::atoi(w) == 0) return (size_t)0;
+        const char *e = std::getenv("GK_BNB_TAB_MB");
+        return (size_t)(e ? std::max(0, std::atoi(e)) : 8192) << 20;
+    }();
+    Cc.tabs.reset(node_rec_doubles(m, n), tab_cap);
+    pool.tabs = &Cc.tabs;
     // root node: the optimal basis of the initial LP relaxation
     {
         const int sl = pool.alloc();
@@ -1798,28 +2103,50 @@ extern "C" int gk_ios_driver_sharded(gk_ctx *ctx, gk_mip *mip, const gk_iocp *pa
         double *hl = (double *)(h + Y.lb), *hu = (double *)(h + Y.ub), *hc = (double *)(h + Y.cut);
         int *hit = (int *)(h + Y.itl), *hpp = (int *)(h + Y.pp);
         signed char *hs = (signed char *)(h + Y.st);
+        const double **htin = (const double **)(h + Y.tin);
+        double **htout = (double **)(h + Y.tout);
+        int *hbj = (int *)(h + Y.brj), *hbd = (int *)(h + Y.brd);
+        double *hbv = (double *)(h + Y.brv);
         for (int b = 0; b < nb; b++) {
-            const Entry &e = bf.ents[b];
+            Entry &e = bf.ents[b];
             double *l = hl + (size_t)b * S.N, *u = hu + (size_t)b * S.N;
-            std::memcpy(l, S.rlb.data(), m * sizeof(double));
-            std::memcpy(u, S.rub.data(), m * sizeof(double));
+            hbj[b] = -1;
+            hbd[b] = 0;
+            hbv[b] = 0.0;
             if (e.kind == 0) {
                 const int sl = e.nd.slot;
-                std::memcpy(l + m, pool.lb(sl), n * sizeof(double));
-                std::memcpy(u + m, pool.ub(sl), n * sizeof(double));
-                std::memcpy(hs + (size_t)b * S.N, pool.stat(sl), S.N);
+                const NodeMeta &mt = pool.meta[sl];
+                htin[b] = Cc.tabs.ptr(mt.tab);
+                e.tab_out = tab_cap ? Cc.tabs.alloc() : -1;
+                htout[b] = Cc.tabs.ptr(e.tab_out);
+                if (!mt.inl) {
+                    // the kernel builds the node from its parent's record
+                    hbj[b] = mt.br_var;
+                    hbd[b] = mt.br_dir;
+                    hbv[b] = mt.br_val;
+                } else {
+                    std::memcpy(l, S.rlb.data(), m * sizeof(double));
+                    std::memcpy(u, S.rub.data(), m * sizeof(double));
+                    std::memcpy(l + m, pool.lb(sl), n * sizeof(double));
+                    std::memcpy(u + m, pool.ub(sl), n * sizeof(double));
+                    std::memcpy(hs + (size_t)b * S.N, pool.stat(sl), S.N);
+                }
                 hc[b] = cut;
                 hit[b] = S.node_it_lim;
-                hpp[b] = pp_passes(pool.meta[sl].level);
+                hpp[b] = pp_passes(mt.level);
             } else {
                 // eval_degrad (glpios09.js:337): x_j fixed at floor / ceil,
                 // 30 dual pivots from the node's optimal basis
                 const Parked &pk = S.parked[e.pid];
+                std::memcpy(l, S.rlb.data(), m * sizeof(double));
+                std::memcpy(u, S.rub.data(), m * sizeof(double));
                 std::memcpy(l + m, pk.bnd.data(), n * sizeof(double));
                 std::memcpy(u + m, pk.bnd.data() + n, n * sizeof(double));
                 const double beta = pk.x[m + e.j], v = e.dir == 0 ? std::floor(beta) : std::ceil(beta);
                 l[m + e.j] = u[m + e.j] = v;
                 std::memcpy(hs + (size_t)b * S.N, pk.so.data(), S.N);
+                htin[b] = Cc.tabs.ptr(pk.tab);
+                htout[b] = nullptr;
                 hc[b] = INF;
                 hit[b] = 30;
                 hpp[b] = 0;
@@ -1837,6 +2164,13 @@ extern "C" int gk_ios_driver_sharded(gk_ctx *ctx, gk_mip *mip, const gk_iocp *pa
         io.jj = (int *)(dout + Y.jj); io.next = (int *)(dout + Y.next); io.stat_out = (signed char *)(dout + Y.sto);
         io.scratch = Cc.dscratch.p;
         io.scratch_stride = S.stride;
+        io.tab_in = (const double *const *)(din + Y.tin);
+        io.tab_out = (double *const *)(din + Y.tout);
+        io.tab_age_max = 100;
+        io.br_j = (const int *)(din + Y.brj); io.br_dir = (const int *)(din + Y.brd);
+        io.br_val = (const double *)(din + Y.brv);
+        io.nfrac = (int *)(dout + Y.nf); io.jfirst = (int *)(dout + Y.jf); io.jlast = (int *)(dout + Y.jl);
+        io.jmost = (int *)(dout + Y.jm); io.nmost = (int *)(dout + Y.nm); io.iisum = (double *)(dout + Y.ii);
         launch_node_lp(s, P, io, nb);
         (void)hipMemcpyAsync(bf.hout.p, bf.dout.p, Y.out_end, hipMemcpyDeviceToHost, s);
         (void)hipEventRecord(bf.done, s);
@@ -1857,32 +2191,29 @@ extern "C" int gk_ios_driver_sharded(gk_ctx *ctx, gk_mip *mip, const gk_iocp *pa
         const int *hstat = (const int *)(h + Y.stat), *hpiv = (const int *)(h + Y.piv);
         const int *hjj = (const int *)(h + Y.jj), *hnext = (const int *)(h + Y.next);
         const signed char *hso = (const signed char *)(h + Y.sto);
+        const int *hnf = (const int *)(h + Y.nf), *hjf = (const int *)(h + Y.jf), *hjl = (const int *)(h + Y.jl);
+        const int *hjm = (const int *)(h + Y.jm), *hnm = (const int *)(h + Y.nm);
+        const double *hii = (const double *)(h + Y.ii);
         std::vector<double> fx;
         std::vector<signed char> fso;
         const std::vector<double> zeros(2 * (size_t)n, 0.0);
         // (1) per entry, on the workers: the column bounds the node kernel
-        // returned (interleaved lb / ub) into bl | bu, and for an optimal
-        // node LP its integrality scan (check_integrality, glpios03.js:55)
+        // returned (interleaved lb / ub) into bl | bu — only where the host
+        // reads them: the engine fallback, pseudocost branching (its
+        // integrality scan and parked nodes), and children that get no
+        // record (the record store is full).  The integrality scan itself
+        // comes from the kernel (NodeIO nfrac ...) except for PCH
         HostWorkers *W = S.cache->workers;
-        const bool par = W && parm->br_tech != 5;
+        const bool pch = parm->br_tech == 5;
+        const bool par = W && !pch;
         S.eb.resize((size_t)nb * 2 * n);
-        S.ecand.resize((size_t)nb * n);
-        S.ecand_n.assign(nb, -1);
-        S.eii.resize(nb);
         auto prep = [&](int b) {
             const Entry &e = bf.ents[b];
             if (e.kind != 0) return;
+            if (hstat[b] == NODE_OPT && e.tab_out >= 0 && !pch) return;
             const double *bb = hb + (size_t)b * 2 * n;
             double *bl = S.eb.data() + (size_t)b * 2 * n, *bu = bl + n;
             for (int j = 0; j < n; j++) { bl[j] = bb[2 * j]; bu[j] = bb[2 * j + 1]; }
-            if (par && hstat[b] == NODE_OPT) {
-                thread_local std::vector<int> cb;
-                double ii = 0.0;
-                const int nc = S.integrality(hx + (size_t)b * S.N, hso + (size_t)b * S.N, bl, bu, cb, ii);
-                std::memcpy(S.ecand.data() + (size_t)b * n, cb.data(), (size_t)nc * sizeof(int));
-                S.ecand_n[b] = nc;
-                S.eii[b] = ii;
-            }
         };
         if (par) W->run(nb, 16, prep);
         else
@@ -1916,8 +2247,11 @@ extern "C" int gk_ios_driver_sharded(gk_ctx *ctx, gk_mip *mip, const gk_iocp *pa
             else S.lp_solves++;
             if (st == NODE_OPT) {
                 const auto tn0 = bnb_log ? std::chrono::steady_clock::now() : std::chrono::steady_clock::time_point{};
+                S.cur_tab = e.tab_out;
+                const KInt ki{hnf[b], hjf[b], hjl[b], hjm[b], hnm[b], hii[b]};
                 S.node_done(nd, hobj[b], x, hso + (size_t)b * S.N, fbl, fbu, hdz + (size_t)b * 2 * n, hjj[b], hnext[b],
-                            true, S.ecand.data() + (size_t)b * n, S.ecand_n[b], S.eii[b]);
+                            true, nullptr, -1, 0.0, pch ? nullptr : &ki);
+                S.cur_tab = -1;
                 if (bnb_log) t_nd += secs(tn0);
             } else if ((st == NODE_FAIL || st == NODE_ITLIM) && !S.err) {
                 double z = 0.0;
@@ -1932,6 +2266,7 @@ extern "C" int gk_ios_driver_sharded(gk_ctx *ctx, gk_mip *mip, const gk_iocp *pa
                     S.defer = dj;
                 }
             }
+            Cc.tabs.dec(e.tab_out);
             pool.release(nd.slot);
         }
         S.defer = nullptr;
