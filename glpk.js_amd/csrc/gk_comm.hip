@@ -12,6 +12,14 @@
 // The bootstrap is always the TCP star: rank 0 listens on addr ("host:port"),
 // the others connect and announce their rank.  RCCL is loaded with dlopen
 // (RTLD_LOCAL): the process may already carry another RCCL build (torch's).
+//
+// Between the epochs, ranks on one host share the incumbent through one word
+// of shared memory (an atomic min on an order-preserving image
+// of the objective): every rank publishes its incumbent after each batch and
+// prunes its next batch with the best of all, instead of waiting for the
+// next all-gather.  Rank 0 creates the segment (POSIX shm, unlinked as soon
+// as every rank has mapped it, so nothing outlives the processes); ranks on
+// different hosts fall back to the epoch exchange alone.
 #include "../../include/glpk_mi355x.h"
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
@@ -21,16 +29,21 @@
 #include <netdb.h>
 #include <netinet/in.h>
 #include <netinet/tcp.h>
+#include <fcntl.h>
+#include <sys/mman.h>
 #include <sys/socket.h>
+#include <sys/stat.h>
 #include <sys/time.h>
 #include <unistd.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cerrno>
 #include <cfloat>
 #include <chrono>
 #include <cstdlib>
 #include <cstring>
+#include <new>
 #include <string>
 #include <thread>
 #include <vector>
@@ -39,6 +52,9 @@ namespace gk {
 void set_err(const char *fmt, ...);
 }
 int gk_ctx_device(gk_ctx *);
+// gk_ios_driver_sharded with a live incumbent between the epochs (gk_mip.hip)
+extern "C" int gk_ios_driver_sharded_inc(gk_ctx *ctx, gk_mip *mip, const gk_iocp *parm, const gk_ios_shard *shard,
+                                         double (*inc)(void *info, double mine), void *inc_info);
 
 namespace {
 
@@ -106,6 +122,22 @@ void nodelay(int fd)
     (void)setsockopt(fd, SOL_SOCKET, SO_RCVTIMEO, &tv, sizeof tv);
 }
 
+// a double's order as an unsigned integer's (non-negative: the sign bit set;
+// negative: all bits inverted), so that the minimum is one integer atomic
+unsigned long long ord_key(double v)
+{
+    unsigned long long b;
+    std::memcpy(&b, &v, sizeof b);
+    return (b >> 63) ? ~b : (b | 0x8000000000000000ull);
+}
+double ord_val(unsigned long long k)
+{
+    const unsigned long long b = (k >> 63) ? (k & 0x7fffffffffffffffull) : ~k;
+    double v;
+    std::memcpy(&v, &b, sizeof v);
+    return v;
+}
+
 }  // namespace
 
 struct gk_comm {
@@ -120,8 +152,10 @@ struct gk_comm {
     hipStream_t stream = nullptr;
     char *dbuf = nullptr;                 // device staging: send block | gathered blocks
     size_t dcap = 0;
+    std::atomic<unsigned long long> *inc = nullptr;   // the shared incumbent word (same host), or null
     ~gk_comm()
     {
+        if (inc) (void)munmap((void *)inc, 4096);
         if (nc && rccl.destroy) (void)rccl.destroy(nc);
         if (dbuf) (void)hipFree(dbuf);
         if (stream) (void)hipStreamDestroy(stream);
@@ -229,6 +263,56 @@ extern "C" gk_comm *gk_comm_create(gk_ctx *ctx, int rank, int size, const char *
         if (!ok) {
             delete c;
             return nullptr;
+        }
+    }
+    if (size > 1) {
+        // the shared incumbent word, when every rank runs on this host
+        char hn[64] = {0};
+        (void)gethostname(hn, sizeof hn - 1);
+        long long me[2] = {0, (long long)getpid()};
+        for (const char *p = hn; *p; ++p) me[0] = me[0] * 131 + *p;
+        std::vector<long long> all(2 * size);
+        if (!c->tcp_allgather(me, sizeof me, all.data())) {
+            set_err("gk_comm_create: bootstrap exchange failed");
+            delete c;
+            return nullptr;
+        }
+        bool one_host = true;
+        for (int r = 1; r < size; r++) one_host = one_host && all[2 * r] == all[0];
+        if (one_host) {
+            std::string host;
+            int port = 0;
+            (void)split_addr(addr, host, port);
+            const std::string name = "/gk_inc_" + std::to_string(all[1]) + "_" + std::to_string(port);
+            int ok = 1;
+            void *p = MAP_FAILED;
+            int fd = rank == 0 ? shm_open(name.c_str(), O_CREAT | O_EXCL | O_RDWR, 0600) : -1;
+            if (rank == 0) {
+                ok = fd >= 0 && ftruncate(fd, 4096) == 0;
+                if (ok) p = mmap(nullptr, 4096, PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
+                ok = ok && p != MAP_FAILED;
+                if (ok) new (p) std::atomic<unsigned long long>(ord_key(DBL_MAX));
+            }
+            std::vector<int> oks(size);
+            // rank 0's segment exists (or not) before the others open it
+            if (!c->tcp_allgather(&ok, sizeof ok, oks.data())) { delete c; return nullptr; }
+            if (rank != 0 && oks[0]) {
+                fd = shm_open(name.c_str(), O_RDWR, 0600);
+                ok = fd >= 0;
+                if (ok) p = mmap(nullptr, 4096, PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
+                ok = ok && p != MAP_FAILED;
+            }
+            if (fd >= 0) ::close(fd);
+            if (!c->tcp_allgather(&ok, sizeof ok, oks.data())) {
+                if (p != MAP_FAILED) (void)munmap(p, 4096);
+                if (rank == 0) (void)shm_unlink(name.c_str());
+                delete c;
+                return nullptr;
+            }
+            if (rank == 0) (void)shm_unlink(name.c_str());   // every rank has mapped it (or given up)
+            const bool every = std::all_of(oks.begin(), oks.end(), [](int v) { return v == 1; });
+            if (every) c->inc = (std::atomic<unsigned long long> *)p;
+            else if (p != MAP_FAILED) (void)munmap(p, 4096);
         }
     }
     // RCCL when every rank has a device of its own (auto) or when asked; a
@@ -341,6 +425,17 @@ static int comm_allgather(gk_comm *c, const void *send, size_t bytes, void *recv
 
 extern "C" int gk_comm_rank(const gk_comm *c) { return c ? c->rank : -1; }
 
+extern "C" double gk_comm_incumbent(gk_comm *c, double mine)
+{
+    if (!c || !c->inc) return mine;
+    const unsigned long long k = ord_key(mine);
+    unsigned long long cur = c->inc->load(std::memory_order_relaxed);
+    while (k < cur && !c->inc->compare_exchange_weak(cur, k, std::memory_order_acq_rel)) {}
+    return ord_val(std::min(k, c->inc->load(std::memory_order_acquire)));
+}
+
+extern "C" int gk_comm_shared_incumbent(const gk_comm *c) { return c && c->inc ? 1 : 0; }
+
 extern "C" int gk_comm_set_option(gk_comm *c, int opt, int value)
 {
     if (!c) return GK_EABI;
@@ -368,7 +463,9 @@ extern "C" int gk_ios_driver_comm(gk_ctx *ctx, gk_mip *mip, const gk_iocp *parm,
     sh.exchange = nullptr;
     sh.info = comm;
     sh.allgather = gk_comm_allgather;
-    const int ret = gk_ios_driver_sharded(ctx, mip, parm, &sh);
+    // the shared incumbent word between the epochs (ranks on one host)
+    auto inc = [](void *info, double mine) { return gk_comm_incumbent((gk_comm *)info, mine); };
+    const int ret = gk_ios_driver_sharded_inc(ctx, mip, parm, &sh, comm->inc ? +inc : nullptr, comm);
     // a local failure inside the search reaches the other ranks through the
     // sync epoch (every rank leaves the search together); this rank still
     // joins the final all-gather, with its error in h[2], so that no peer

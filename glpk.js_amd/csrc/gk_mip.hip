@@ -96,6 +96,7 @@ struct NodeIO {
     // none) and branch_mostf's direction
     int *nfrac, *jfirst, *jlast, *jmost, *nmost;
     double *iisum;
+    unsigned long long *stamps;   // GK_BNB_LOG=2: [nb][8] device clock at the kernel's phases (null: off)
 };
 
 __host__ __device__ inline size_t node_rec_bounds(int m, int n) { return 1 + (size_t)m + (size_t)m * (m + n); }
@@ -160,6 +161,32 @@ __device__ int block_ratio(double t, double a, int idx, double *shk, double *sha
     return r;
 }
 
+// block_argmax's order within one wave (every lane returns the choice)
+__device__ int wave_argmax(double key, int idx)
+{
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        const double k2 = __shfl_xor(key, o);
+        const int i2 = __shfl_xor(idx, o);
+        if (i2 >= 0 && (idx < 0 || k2 > key || (k2 == key && i2 < idx))) { key = k2; idx = i2; }
+    }
+    return idx;
+}
+
+// block_ratio's order within one wave (every lane returns the choice)
+__device__ int wave_ratio(double t, double a, int idx)
+{
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        const double t2 = __shfl_xor(t, o), a2 = __shfl_xor(a, o);
+        const int i2 = __shfl_xor(idx, o);
+        if (i2 >= 0 && (idx < 0 || t2 < t || (t2 == t && (a2 > a || (a2 == a && i2 < idx))))) {
+            t = t2; a = a2; idx = i2;
+        }
+    }
+    return idx;
+}
+
 __device__ double block_sum256(double v, double *sh)
 {
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -199,10 +226,14 @@ __device__ __forceinline__ double nb_value(int st, double lb, double ub)
 // objective, sum c_j x_j <= incumbent in minimisation form).
 // Returns 1 when the node is infeasible.  Called by the whole block.
 // ---------------------------------------------------------------------------
-__device__ int node_preprocess(const NodeProb &P, double objU, double *lb, double *ub, signed char *stat,
-                               signed char *chg, double *ri, int max_pass)
+template <int ALDS>
+__device__ int node_preprocess(const NodeProb &P, const double *cl, const signed char *isl, const double *Ar,
+                               double objU, double *lb, double *ub, signed char *stat, signed char *chg, double *ri,
+                               int max_pass)
 {
     const int m = P.m, n = P.n;
+    // a_ij: the row-major LDS copy (ALDS) or the column-major matrix in HBM
+    auto aij = [&](int i, int j) { return ALDS ? Ar[(size_t)i * n + j] : P.A[(size_t)j * m + i]; };
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, nw = blockDim.x >> 6;
     for (int i = threadIdx.x; i <= m; i += blockDim.x) {
         ri[6 * i + 4] = (i == 0) ? -DBL_MAX : lb[i - 1];
@@ -217,7 +248,7 @@ __device__ int node_preprocess(const NodeProb &P, double objU, double *lb, doubl
             if (L == -DBL_MAX && U == DBL_MAX) continue;           // free row (wave-uniform)
             double smin = 0.0, smax = 0.0, cmin = 0.0, cmax = 0.0, jmin = 0.0, jmax = 0.0;
             for (int j = lane; j < n; j += 64) {
-                const double a = (i == 0) ? P.c[m + j] : P.A[(size_t)j * m + (i - 1)];
+                const double a = (i == 0) ? cl[m + j] : aij(i - 1, j);
                 if (a == 0.0) continue;
                 const double l = lb[m + j], u = ub[m + j];
                 const double lo = a > 0.0 ? l : u, hi = a > 0.0 ? u : l;
@@ -249,12 +280,12 @@ __device__ int node_preprocess(const NodeProb &P, double objU, double *lb, doubl
         int eff = 0;
         for (int j = threadIdx.x; j < n; j += blockDim.x) {
             const double l0 = lb[m + j], u0 = ub[m + j];
-            const bool flag = P.isint[j] != 0;
+            const bool flag = isl[j] != 0;
             double lj = l0, uj = u0;
             for (int i = 0; i <= m && !bad; ++i) {
                 const double L = ri[6 * i + 4], U = ri[6 * i + 5];
                 if (L == -DBL_MAX && U == DBL_MAX) continue;
-                const double a = (i == 0) ? P.c[m + j] : P.A[(size_t)j * m + (i - 1)];
+                const double a = (i == 0) ? cl[m + j] : aij(i - 1, j);
                 if (a == 0.0) continue;
                 const double fmin = ri[6 * i + 0], fmax = ri[6 * i + 1];
                 const int jn = (int)ri[6 * i + 2], jx = (int)ri[6 * i + 3];
@@ -341,23 +372,43 @@ __device__ int node_preprocess(const NodeProb &P, double objU, double *lb, doubl
 // GLOBAL = 1: the same work area in a per-node slice of HBM (node LPs beyond
 // 64 KiB of LDS; L2 serves the workgroup's sweeps).
 // ---------------------------------------------------------------------------
-template <int GLOBAL>
+template <int GLOBAL, int ALDS>
 __global__ void __launch_bounds__(256) k_node_lp(NodeProb P, NodeIO io)
 {
     extern __shared__ double lds_[];
     double *lds = GLOBAL ? io.scratch + (size_t)blockIdx.x * io.scratch_stride : lds_;
-    __shared__ double shk[4], sha[4];
+    __shared__ double shk[4];
     __shared__ int shi[4];
     __shared__ int sh_flag;
     const int m = P.m, n = P.n, N = m + n, b = blockIdx.x;
     const int W = 2 * m + n;                 // width of [B | I | -A]
+    // phases: 0 entry, 5 bounds loaded, 1 preprocessed, 2 tableau (warm or
+    // inverted), 3 x / d formed, 4 simplex done, 7 exit
+#define NODE_STAMP(ph) \
+    do { if (io.stamps && threadIdx.x == 0) io.stamps[(size_t)b * 8 + (ph)] = wall_clock64(); } while (0)
+    NODE_STAMP(0);
     double *M = lds;                          // m * W
     double *lb = M + (size_t)m * W, *ub = lb + N, *x = ub + N, *d = x + N;
     double *fcol = d + N;                     // m
     double *rinfo = fcol + m;                 // 6 (m + 1)
-    int *head = (int *)(rinfo + 6 * (m + 1));
-    signed char *stat = (signed char *)(head + m);
+    double *cl = rinfo + 6 * (m + 1);         // N: the costs
+    double *dzt = cl + N;                     // 4 m: branching degradations of the candidates
+    double *Ar = dzt + 4 * m;                 // ALDS: A row-major (m x n)
+    int *head = (int *)(Ar + (ALDS ? (size_t)m * n : 0));
+    int *rowof = head + m;                    // N: row of a basic variable
+    int *cand = rowof + N;                    // m: fractional basic integer columns
+    signed char *stat = (signed char *)(cand + m);
     signed char *chg = stat + N;              // n
+    signed char *isl = chg + n;               // n: integer flags
+    // the problem's costs, integer flags and (ALDS) matrix staged in LDS:
+    // every loop below reads them many times, some from one thread
+    for (int k = threadIdx.x; k < N; k += blockDim.x) cl[k] = P.c[k];
+    for (int j = threadIdx.x; j < n; j += blockDim.x) isl[j] = P.isint[j];
+    if (ALDS)
+        for (int e = threadIdx.x; e < m * n; e += blockDim.x) {
+            const int j = e / m, i = e - j * m;
+            Ar[(size_t)i * n + j] = P.A[e];
+        }
     double *gbnd = io.bnd + (size_t)b * 2 * n, *gdz = io.dzb + (size_t)b * 2 * n;
     const double *tin = io.tab_in ? io.tab_in[b] : nullptr;
     const int brj = io.br_j ? io.br_j[b] : -1;
@@ -407,13 +458,16 @@ __global__ void __launch_bounds__(256) k_node_lp(NodeProb P, NodeIO io)
             gbnd[2 * j + 1] = ub[m + j];
         }
     };
+    NODE_STAMP(5);
     const int max_pass = io.pp_pass[b];
-    if (max_pass > 0 && node_preprocess(P, io.obj_bound, lb, ub, stat, chg, rinfo, max_pass)) {
+    if (max_pass > 0 && node_preprocess<ALDS>(P, cl, isl, Ar, io.obj_bound, lb, ub, stat, chg, rinfo, max_pass)) {
         put_bounds();
         if (threadIdx.x == 0) { io.status[b] = NODE_PPINF; io.pivots[b] = 0; io.jj[b] = 0; io.obj[b] = 0.0; }
+        NODE_STAMP(7);
         return;
     }
     put_bounds();
+    NODE_STAMP(1);
     // warm start: the parent's tableau, when its basis is still this node's
     // (the node's statuses come from the parent's final ones; preprocessing
     // only moves non-basic columns) and it is young enough
@@ -479,11 +533,11 @@ __global__ void __launch_bounds__(256) k_node_lp(NodeProb P, NodeIO io)
         double v;
         if (c < m) {
             const int k = head[c];
-            v = (k < m) ? (i == k ? 1.0 : 0.0) : -P.A[(size_t)(k - m) * m + i];
+            v = (k < m) ? (i == k ? 1.0 : 0.0) : -(ALDS ? Ar[(size_t)i * n + (k - m)] : P.A[(size_t)(k - m) * m + i]);
         } else if (c < 2 * m) {
             v = (i == c - m) ? 1.0 : 0.0;
         } else {
-            v = -P.A[(size_t)(c - 2 * m) * m + i];
+            v = -(ALDS ? Ar[(size_t)i * n + (c - 2 * m)] : P.A[(size_t)(c - 2 * m) * m + i]);
         }
         M[(size_t)i * W + c] = v;
     }
@@ -525,12 +579,13 @@ __global__ void __launch_bounds__(256) k_node_lp(NodeProb P, NodeIO io)
     }
     // T[i][j] = M[i][m + j]  (row length W kept; T(i, j) = M[i*W + m + j])
     }
+    NODE_STAMP(2);
     // d = c - c_B' T
     for (int k = threadIdx.x; k < N; k += blockDim.x) {
         if (stat[k] == BS) { d[k] = 0.0; continue; }
-        double s = P.c[k];
+        double s = cl[k];
         for (int i = 0; i < m; ++i) {
-            const double cb = P.c[head[i]];
+            const double cb = cl[head[i]];
             if (cb != 0.0) s -= cb * T_(i, k);
         }
         d[k] = s;
@@ -556,79 +611,100 @@ __global__ void __launch_bounds__(256) k_node_lp(NodeProb P, NodeIO io)
     // x_N and x_B = -T_N x_N
     for (int k = threadIdx.x; k < N; k += blockDim.x) x[k] = (stat[k] == BS) ? 0.0 : nb_value(stat[k], lb[k], ub[k]);
     __syncthreads();
-    for (int i = threadIdx.x; i < m; i += blockDim.x) {
-        double s = 0.0;
-        for (int k = 0; k < N; ++k)
-            if (stat[k] != BS && x[k] != 0.0) s += T_(i, k) * x[k];
-        x[head[i]] = -s;
+    {
+        // one wave per row, lanes over the columns
+        const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, nwv = blockDim.x >> 6;
+        for (int i = wv; i < m; i += nwv) {
+            double sx = 0.0;
+            for (int k = lane; k < N; k += 64)
+                if (stat[k] != BS && x[k] != 0.0) sx += T_(i, k) * x[k];
+            sx = wsum(sx);
+            if (lane == 0) x[head[i]] = -sx;
+        }
     }
     __syncthreads();
+    NODE_STAMP(3);
     // ---- bounded dual simplex ------------------------------------------
     const double tol_p = 1e-7, tol_piv = 1e-7;
     const double cutoff = io.cutoff[b];
     const int it_lim = io.it_lim[b];
     int it = 0, status = NODE_OPT;
+    // a pivot is three barriers: wave 0 takes the whole decision (objective
+    // and cutoff, chuzr, the ratio test on row p: wave reductions only) while
+    // the other waves wait; then one update phase that reads row p and
+    // column q as they were (x, d and every other entry of T) and one that
+    // rewrites row p, column q and the header
+    __shared__ int sh_st, sh_p, sh_q;
+    __shared__ double sh_tq, sh_dq, sh_apq;
     for (;;) {
-        // objective (dual objective of the current dual feasible basis)
-        double zs = 0.0;
-        for (int k = threadIdx.x; k < N; k += blockDim.x) zs += P.c[k] * x[k];
-        const double z = block_sum256(zs, shk);
-        if (z >= cutoff) { status = NODE_CUTOFF; break; }
-        // chuzr: largest bound violation
-        double key = 0.0;
-        int idx = -1;
-        for (int i = threadIdx.x; i < m; i += blockDim.x) {
-            const int k = head[i];
-            const double v = x[k];
-            double r = 0.0;
-            if (v < lb[k] - tol_p * (1.0 + fabs(lb[k]))) r = lb[k] - v;
-            else if (v > ub[k] + tol_p * (1.0 + fabs(ub[k]))) r = v - ub[k];
-            if (r > 0.0 && (idx < 0 || r > key)) { key = r; idx = i; }
+        if (threadIdx.x < 64) {
+            const int lane = threadIdx.x;
+            int dec = -1, p = -1, q = -1;
+            // objective (dual objective of the current dual feasible basis)
+            double zs = 0.0;
+            for (int k = lane; k < N; k += 64) zs += cl[k] * x[k];
+            const double z = wsum(zs);
+            if (z >= cutoff) dec = NODE_CUTOFF;
+            else {
+                // chuzr: largest bound violation
+                double key = 0.0;
+                int idx = -1;
+                for (int i = lane; i < m; i += 64) {
+                    const int k = head[i];
+                    const double v = x[k];
+                    double r = 0.0;
+                    if (v < lb[k] - tol_p * (1.0 + fabs(lb[k]))) r = lb[k] - v;
+                    else if (v > ub[k] + tol_p * (1.0 + fabs(ub[k]))) r = v - ub[k];
+                    if (r > 0.0 && (idx < 0 || r > key)) { key = r; idx = i; }
+                }
+                p = wave_argmax(key, idx);
+                if (p < 0) dec = NODE_OPT;                 // primal feasible: optimal
+                else if (it >= it_lim) dec = NODE_ITLIM;
+            }
+            if (dec < 0) {
+                const int kp = head[p];
+                const bool to_lb = x[kp] < lb[kp];
+                // ratio test on row p: x_p = -sum T[p,j] x_j
+                double rmax = 0.0;
+                for (int k = lane; k < N; k += 64)
+                    if (stat[k] != BS) rmax = fmax(rmax, fabs(T_(p, k)));
+                rmax = wmax(rmax);
+                const double eps = tol_piv * (1.0 + 0.01 * rmax);
+                double bt = 0.0, ba = 0.0;
+                int bq = -1;
+                for (int k = lane; k < N; k += 64) {
+                    const int st = stat[k];
+                    if (st == BS || st == NS) continue;
+                    const double a = T_(p, k);
+                    if (fabs(a) < eps) continue;
+                    // x_p changes by -a per unit increase of x_k
+                    bool ok;
+                    if (to_lb) ok = (st == NL && a < 0.0) || (st == NU && a > 0.0) || (st == NF);
+                    else ok = (st == NL && a > 0.0) || (st == NU && a < 0.0) || (st == NF);
+                    if (!ok) continue;
+                    // the step that keeps d dual feasible: d_k - (d_q / a_pq) a_k
+                    double t = (st == NF) ? fabs(d[k]) / fabs(a) : (to_lb ? -d[k] / a : d[k] / a);
+                    if (t < 0.0) t = 0.0;
+                    if (bq < 0 || t < bt || (t == bt && fabs(a) > ba)) { bt = t; ba = fabs(a); bq = k; }
+                }
+                q = wave_ratio(bt, ba, bq);
+                if (q < 0) dec = NODE_INFEAS;              // dual unbounded
+                else if (lane == 0) {
+                    const double apq = T_(p, q);
+                    const double bound = to_lb ? lb[kp] : ub[kp];
+                    sh_apq = apq;
+                    sh_tq = (x[kp] - bound) / apq;         // step of x_q
+                    sh_dq = d[q] / apq;
+                }
+            }
+            if (lane == 0) { sh_st = dec; sh_p = p; sh_q = q; }
         }
-        const int p = block_argmax(key, idx, shk, shi);
-        if (p < 0) break;                                  // primal feasible: optimal
-        if (it >= it_lim) { status = NODE_ITLIM; break; }
-        const int kp = head[p];
-        const bool to_lb = x[kp] < lb[kp];
-        // ratio test on row p: x_p = -sum T[p,j] x_j
-        double rmax = 0.0;
-        for (int k = threadIdx.x; k < N; k += blockDim.x)
-            if (stat[k] != BS) rmax = fmax(rmax, fabs(T_(p, k)));
-        {
-            __syncthreads();
-            const double r = wmax(rmax);
-            if ((threadIdx.x & 63) == 0) shk[threadIdx.x >> 6] = r;
-            __syncthreads();
-            rmax = fmax(fmax(shk[0], shk[1]), fmax(shk[2], shk[3]));
-            __syncthreads();
-        }
-        const double eps = tol_piv * (1.0 + 0.01 * rmax);
-        double bt = 0.0, ba = 0.0;
-        int bq = -1;
-        for (int k = threadIdx.x; k < N; k += blockDim.x) {
-            const int st = stat[k];
-            if (st == BS || st == NS) continue;
-            const double a = T_(p, k);
-            if (fabs(a) < eps) continue;
-            // x_p changes by -a per unit increase of x_k
-            bool ok;
-            if (to_lb) ok = (st == NL && a < 0.0) || (st == NU && a > 0.0) || (st == NF);
-            else ok = (st == NL && a > 0.0) || (st == NU && a < 0.0) || (st == NF);
-            if (!ok) continue;
-            // the step that keeps d dual feasible: d_k - (d_q / a_pq) a_k
-            double t = (st == NF) ? fabs(d[k]) / fabs(a) : (to_lb ? -d[k] / a : d[k] / a);
-            if (t < 0.0) t = 0.0;
-            if (bq < 0 || t < bt || (t == bt && fabs(a) > ba)) { bt = t; ba = fabs(a); bq = k; }
-        }
-        const int q = block_ratio(bt, ba, bq, shk, sha, shi);
-        if (q < 0) { status = NODE_INFEAS; break; }        // dual unbounded
-        // pivot (p, q)
-        const double apq = T_(p, q);
-        const double bound = to_lb ? lb[kp] : ub[kp];
-        const double tq = (x[kp] - bound) / apq;         // step of x_q
-        const double dq = d[q] / apq;
         __syncthreads();
-        // x update
+        if (sh_st >= 0) { status = sh_st; break; }
+        // pivot (p, q)
+        const int p = sh_p, q = sh_q, kp = head[p];
+        const double apq = sh_apq, tq = sh_tq, dq = sh_dq;
+        // x update (basic variables of rows i != p)
         for (int i = threadIdx.x; i < m; i += blockDim.x) {
             if (i == p) continue;
             const double a = T_(i, q);
@@ -640,8 +716,20 @@ __global__ void __launch_bounds__(256) k_node_lp(NodeProb P, NodeIO io)
             const double a = T_(p, k);
             if (a != 0.0) d[k] -= dq * a;
         }
+        // T update outside row p and column q: row i -= T[i,q] (row p / apq)
+        for (int e = threadIdx.x; e < m * N; e += blockDim.x) {
+            const int i = e / N, k = e - i * N;
+            if (i == p || k == q) continue;
+            const double f = T_(i, q);
+            if (f != 0.0) T_(i, k) -= f * (T_(p, k) / apq);
+        }
         __syncthreads();
+        for (int k = threadIdx.x; k < N; k += blockDim.x) T_(p, k) /= apq;
+        for (int i = threadIdx.x; i < m; i += blockDim.x)
+            if (i != p) T_(i, q) = 0.0;
         if (threadIdx.x == 0) {
+            const bool to_lb = x[kp] < lb[kp];
+            const double bound = to_lb ? lb[kp] : ub[kp];
             x[q] += tq;
             x[kp] = bound;
             d[q] = 0.0;
@@ -650,23 +738,11 @@ __global__ void __launch_bounds__(256) k_node_lp(NodeProb P, NodeIO io)
             stat[q] = BS;
             head[p] = q;
         }
-        // T update: row p /= apq; row i -= T[i,q] row p
-        __syncthreads();
-        for (int k = threadIdx.x; k < N; k += blockDim.x) T_(p, k) /= apq;
-        __syncthreads();
-        for (int e = threadIdx.x; e < m * N; e += blockDim.x) {
-            const int i = e / N, k = e % N;
-            if (i == p) continue;
-            const double f = T_(i, q);
-            if (f != 0.0 && k != q) T_(i, k) -= f * T_(p, k);
-        }
-        __syncthreads();
-        for (int i = threadIdx.x; i < m; i += blockDim.x)
-            if (i != p) T_(i, q) = 0.0;
         __syncthreads();
         it++;
     }
     __syncthreads();
+    NODE_STAMP(4);
     // the children's warm start
     double *tout = io.tab_out ? io.tab_out[b] : nullptr;
     if (tout && status == NODE_OPT) {
@@ -679,7 +755,7 @@ __global__ void __launch_bounds__(256) k_node_lp(NodeProb P, NodeIO io)
         }
     }
     double zs = 0.0;
-    for (int k = threadIdx.x; k < N; k += blockDim.x) zs += P.c[k] * x[k];
+    for (int k = threadIdx.x; k < N; k += blockDim.x) zs += cl[k] * x[k];
     const double z = block_sum256(zs, shk);
     // outputs
     double *gx = io.x + (size_t)b * N;
@@ -695,6 +771,7 @@ __global__ void __launch_bounds__(256) k_node_lp(NodeProb P, NodeIO io)
             io.pivots[b] = it;
             io.jj[b] = 0;
         }
+        NODE_STAMP(7);
         return;
     }
     // ---- fix_by_red_cost (glpios03.js:307, called at :801 once an incumbent
@@ -706,7 +783,7 @@ __global__ void __launch_bounds__(256) k_node_lp(NodeProb P, NodeIO io)
         const double best = io.obj_bound;
         for (int j = threadIdx.x; j < n; j += blockDim.x) {
             const int k = m + j;
-            if (!P.isint[j]) continue;
+            if (!isl[j]) continue;
             double dj = d[k];
             if (stat[k] == NL) {
                 if (dj < 0.0) dj = 0.0;
@@ -727,91 +804,121 @@ __global__ void __launch_bounds__(256) k_node_lp(NodeProb P, NodeIO io)
     // bound of each branch, DBL_MAX: the branch has no feasible point) goes
     // to the host for whichever column the branching rule picks; with DTH
     // the choice uses Tomlin's rounding of delta x_k on integer columns
-    __shared__ int sh_jj, sh_next, sh_brk;
+    // The candidates are evaluated in parallel, one wave per column (a
+    // wave-wide ratio test per branch, no block barrier), and the choice
+    // then walks them in column order as the reference does, stopping at
+    // the first column with a branch that has no feasible point
+    __shared__ int sh_jj, sh_next;
     __shared__ double sh_degrad;
-    if (threadIdx.x == 0) { sh_jj = 0; sh_next = 0; sh_degrad = -1.0; sh_brk = 0; }
-    __syncthreads();
-    int any_frac = 0;
-    // visit the basic structural columns in increasing j
-    for (int j = 0; j < n; ++j) {
-        const int k = m + j;
-        if (stat[k] != BS || !P.isint[j]) continue;
-        const double xv = x[k];
-        if (fabs(xv - floor(xv + 0.5)) <= P.tol_int) continue;
-        any_frac = 1;
-        int row = -1;
-        for (int i = 0; i < m; ++i)
-            if (head[i] == k) { row = i; break; }
-        double dz[2], dzb[2];
-        for (int kase = 0; kase < 2; ++kase) {
-            const double dir = kase == 0 ? -1.0 : +1.0;
-            double bt = 0.0, ba = 0.0;
-            int bq = -1;
-            for (int kk = threadIdx.x; kk < N; kk += blockDim.x) {
+    __shared__ int sh_wc[4];
+    for (int i = threadIdx.x; i < m; i += blockDim.x) rowof[head[i]] = i;
+    if (threadIdx.x == 0) { sh_jj = 0; sh_next = 0; sh_degrad = -1.0; }
+    // the fractional basic integer columns in column order (ballot compaction)
+    int ncand = 0;
+    for (int j0 = 0; j0 < n; j0 += blockDim.x) {
+        const int j = j0 + threadIdx.x, lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+        bool f = false;
+        if (j < n && stat[m + j] == BS && isl[j]) {
+            const double xv = x[m + j];
+            f = fabs(xv - floor(xv + 0.5)) > P.tol_int;
+        }
+        const unsigned long long msk = __ballot(f);
+        if (lane == 0) sh_wc[wv] = __popcll(msk);
+        __syncthreads();
+        int base = ncand, tot = 0;
+        for (int v = 0; v < (int)(blockDim.x >> 6); ++v) {
+            if (v < wv) base += sh_wc[v];
+            tot += sh_wc[v];
+        }
+        if (f) cand[base + __popcll(msk & ((1ull << lane) - 1ull))] = j;
+        ncand += tot;
+        __syncthreads();
+    }
+    const int any_frac = ncand > 0;
+    {
+        const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, nwv = blockDim.x >> 6;
+        for (int c = wv; c < ncand; c += nwv) {
+            const int j = cand[c], k = m + j, row = rowof[k];
+            const double xv = x[k];
+            // both branches in one sweep: dir -1 (down), +1 (up)
+            double bt0 = 0.0, ba0 = 0.0, bt1 = 0.0, ba1 = 0.0;
+            int bq0 = -1, bq1 = -1;
+            for (int kk = lane; kk < N; kk += 64) {
                 const int st = stat[kk];
                 if (st == BS || st == NS) continue;
-                const double alfa = dir * (-T_(row, kk));
-                double t;
-                if (st == NL) {
-                    if (alfa < +1e-9) continue;
-                    t = d[kk] / alfa;
-                } else if (st == NU) {
-                    if (alfa > -1e-9) continue;
-                    t = d[kk] / alfa;
-                } else {
-                    if (-1e-9 < alfa && alfa < +1e-9) continue;
-                    t = 0.0;
+                const double tr = T_(row, kk), dk = d[kk];
+#pragma unroll
+                for (int kase = 0; kase < 2; ++kase) {
+                    const double alfa = kase == 0 ? tr : -tr;      // dir * (-T[row, kk])
+                    double t;
+                    if (st == NL) {
+                        if (alfa < +1e-9) continue;
+                        t = dk / alfa;
+                    } else if (st == NU) {
+                        if (alfa > -1e-9) continue;
+                        t = dk / alfa;
+                    } else {
+                        if (-1e-9 < alfa && alfa < +1e-9) continue;
+                        t = 0.0;
+                    }
+                    if (t < 0.0) t = 0.0;
+                    double &bt = kase == 0 ? bt0 : bt1, &ba = kase == 0 ? ba0 : ba1;
+                    int &bq = kase == 0 ? bq0 : bq1;
+                    if (bq < 0 || t < bt || (t == bt && fabs(alfa) > ba)) { bt = t; ba = fabs(alfa); bq = kk; }
                 }
-                if (t < 0.0) t = 0.0;
-                if (bq < 0 || t < bt || (t == bt && fabs(alfa) > ba)) { bt = t; ba = fabs(alfa); bq = kk; }
             }
-            const int kq = block_ratio(bt, ba, bq, shk, sha, shi);
-            if (kq < 0) dz[kase] = dzb[kase] = DBL_MAX;
-            else {
-                const double alfa = -T_(row, kq);
-                const double delta_j = (kase == 0 ? floor(xv) : ceil(xv)) - xv;
-                double delta_k = delta_j / alfa;
-                double dk = d[kq];
-                const int st = stat[kq];
-                if ((st == NL && dk < 0.0) || (st == NU && dk > 0.0) || st == NF) dk = 0.0;
-                // the objective after this one dual pivot bounds the branch
-                dzb[kase] = fabs(dk * delta_k);
-                if (kq >= m && P.isint[kq - m] && fabs(delta_k - floor(delta_k + 0.5)) > 1e-3)
-                    delta_k = delta_k > 0.0 ? ceil(delta_k) : floor(delta_k);
-                dz[kase] = fabs(dk * delta_k);   // Tomlin's estimate: choice only
+            double dz[2], dzb[2];
+#pragma unroll
+            for (int kase = 0; kase < 2; ++kase) {
+                const int kq = wave_ratio(kase == 0 ? bt0 : bt1, kase == 0 ? ba0 : ba1, kase == 0 ? bq0 : bq1);
+                if (kq < 0) dz[kase] = dzb[kase] = DBL_MAX;
+                else {
+                    const double alfa = -T_(row, kq);
+                    const double delta_j = (kase == 0 ? floor(xv) : ceil(xv)) - xv;
+                    double delta_k = delta_j / alfa;
+                    double dk = d[kq];
+                    const int st = stat[kq];
+                    if ((st == NL && dk < 0.0) || (st == NU && dk > 0.0) || st == NF) dk = 0.0;
+                    // the objective after this one dual pivot bounds the branch
+                    dzb[kase] = fabs(dk * delta_k);
+                    if (kq >= m && isl[kq - m] && fabs(delta_k - floor(delta_k + 0.5)) > 1e-3)
+                        delta_k = delta_k > 0.0 ? ceil(delta_k) : floor(delta_k);
+                    dz[kase] = fabs(dk * delta_k);   // Tomlin's estimate: choice only
+                }
+            }
+            if (lane == 0) {
+                dzt[4 * c] = dz[0]; dzt[4 * c + 1] = dz[1];
+                dzt[4 * c + 2] = dzb[0]; dzt[4 * c + 3] = dzb[1];
             }
         }
-        if (threadIdx.x == 0) {
-            gdz[2 * j] = dzb[0];
-            gdz[2 * j + 1] = dzb[1];
-            if (P.dth && (sh_degrad < dz[0] || sh_degrad < dz[1])) {
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        for (int c = 0; c < ncand; ++c) {
+            const int j = cand[c];
+            const double dz0 = dzt[4 * c], dz1 = dzt[4 * c + 1];
+            gdz[2 * j] = dzt[4 * c + 2];
+            gdz[2 * j + 1] = dzt[4 * c + 3];
+            if (P.dth && (sh_degrad < dz0 || sh_degrad < dz1)) {
                 sh_jj = j + 1;
-                if (dz[0] < dz[1]) { sh_next = -1; sh_degrad = dz[1]; }
-                else { sh_next = +1; sh_degrad = dz[0]; }
-                if (sh_degrad == DBL_MAX) sh_brk = 1;
+                if (dz0 < dz1) { sh_next = -1; sh_degrad = dz1; }
+                else { sh_next = +1; sh_degrad = dz0; }
+                if (sh_degrad == DBL_MAX) break;
             }
         }
-        __syncthreads();
-        if (sh_brk) break;
     }
     if (threadIdx.x == 0) {
         int jj = sh_jj, next = sh_next;
         if (!P.dth) {
             // the host applies the branching rule; report the first candidate
-            jj = 0;
-            for (int j = 0; j < n && !jj; ++j) {
-                const int k = m + j;
-                if (stat[k] == BS && P.isint[j] && fabs(x[k] - floor(x[k] + 0.5)) > P.tol_int) jj = j + 1;
-            }
+            jj = ncand ? cand[0] + 1 : 0;
         } else if (any_frac && sh_degrad < 1e-6 * (1.0 + 0.001 * fabs(z))) {
             // branch_mostf (glpios09.js:62): value closest to floor + 1/2
             double most = DBL_MAX;
             jj = 0;
-            for (int j = 0; j < n; ++j) {
-                const int k = m + j;
-                if (stat[k] != BS || !P.isint[j]) continue;
-                const double beta = x[k];
-                if (fabs(beta - floor(beta + 0.5)) <= P.tol_int) continue;
+            for (int c = 0; c < ncand; ++c) {
+                const int j = cand[c];
+                const double beta = x[m + j];
                 const double temp = floor(beta) + 0.5;
                 if (most > fabs(beta - temp)) {
                     jj = j + 1;
@@ -824,13 +931,14 @@ __global__ void __launch_bounds__(256) k_node_lp(NodeProb P, NodeIO io)
         // (MipSolver::integrality), in column order: the count, the sum of
         // integer infeasibilities, and the candidates of branch_first /
         // branch_last / branch_mostf (glpios09.js:28-82)
+        // (a subset of the candidates above: integer columns have integral
+        // bounds, glp_intopt's precondition kept by the preprocessing)
         int nf = 0, jf = -1, jl = -1, jm = -1, nm = 0;
         double ii = 0.0, most = DBL_MAX;
         bool jj_cand = false;
         const double tol = P.tol_int;
-        for (int j = 0; j < n; ++j) {
-            const int k = m + j;
-            if (!P.isint[j] || stat[k] != BS) continue;
+        for (int c = 0; c < ncand; ++c) {
+            const int j = cand[c], k = m + j;
             const double v = x[k], l = lb[k], u = ub[k];
             if (l != -DBL_MAX) {
                 if (l - tol <= v && v <= l + tol) continue;
@@ -878,22 +986,29 @@ __global__ void __launch_bounds__(256) k_node_lp(NodeProb P, NodeIO io)
         }
         for (int k = threadIdx.x; k < N; k += blockDim.x) rs[k] = stat[k];
     }
+    NODE_STAMP(7);
 #undef T_
+#undef NODE_STAMP
 }
 
-size_t node_lp_lds(int m, int n)
+// the node kernel's work area (alds: with the row-major copy of A)
+size_t node_lp_lds(int m, int n, int alds = 0)
 {
     const size_t N = (size_t)m + n;
-    return sizeof(double) * ((size_t)m * (2 * m + n) + 4 * N + m + 6 * ((size_t)m + 1)) + sizeof(int) * m + N + n + 16;
+    return sizeof(double) * ((size_t)m * (2 * m + n) + 5 * N + 5 * (size_t)m + 6 * ((size_t)m + 1) +
+                             (alds ? (size_t)m * n : 0)) +
+           sizeof(int) * (2 * (size_t)m + N) + N + 2 * (size_t)n + 16;
 }
 
 constexpr size_t NODE_LDS_MAX = 64 * 1024;
 
 void launch_node_lp(hipStream_t s, const NodeProb &P, const NodeIO &io, int nb)
 {
-    const size_t lds = node_lp_lds(P.m, P.n);
-    if (lds <= NODE_LDS_MAX) hipLaunchKernelGGL(k_node_lp<0>, dim3(nb), dim3(256), lds, s, P, io);
-    else hipLaunchKernelGGL(k_node_lp<1>, dim3(nb), dim3(256), 0, s, P, io);
+    if (node_lp_lds(P.m, P.n, 1) <= NODE_LDS_MAX)
+        hipLaunchKernelGGL((k_node_lp<0, 1>), dim3(nb), dim3(256), node_lp_lds(P.m, P.n, 1), s, P, io);
+    else if (node_lp_lds(P.m, P.n) <= NODE_LDS_MAX)
+        hipLaunchKernelGGL((k_node_lp<0, 0>), dim3(nb), dim3(256), node_lp_lds(P.m, P.n), s, P, io);
+    else hipLaunchKernelGGL((k_node_lp<1, 0>), dim3(nb), dim3(256), 0, s, P, io);
 }
 
 // ---------------------------------------------------------------------------
@@ -1096,6 +1211,7 @@ struct Layout {
 
 struct BatchBuf {
     DevArr<char> din, dout;
+    DevArr<unsigned long long> dstamp;      // GK_BNB_LOG=2: the node kernel's phase stamps
     HostArr<char> hin, hout;
     hipEvent_t done = nullptr;
     std::vector<Entry> ents;
@@ -1942,7 +2058,19 @@ extern "C" int gk_ios_driver(gk_ctx *ctx, gk_mip *mip, const gk_iocp *parm)
     return gk_ios_driver_sharded(ctx, mip, parm, nullptr);
 }
 
+extern "C" int gk_ios_driver_sharded_inc(gk_ctx *ctx, gk_mip *mip, const gk_iocp *parm, const gk_ios_shard *shard,
+                                         double (*inc)(void *info, double mine), void *inc_info);
+
 extern "C" int gk_ios_driver_sharded(gk_ctx *ctx, gk_mip *mip, const gk_iocp *parm, const gk_ios_shard *shard)
+{
+    return gk_ios_driver_sharded_inc(ctx, mip, parm, shard, nullptr, nullptr);
+}
+
+// inc (optional): publishes this rank's incumbent (internal minimisation
+// form, DBL_MAX: none) and returns the best over the ranks; called before
+// every batch of the split search (gk_comm's shared word)
+extern "C" int gk_ios_driver_sharded_inc(gk_ctx *ctx, gk_mip *mip, const gk_iocp *parm, const gk_ios_shard *shard,
+                                         double (*inc)(void *info, double mine), void *inc_info)
 {
     if (!ctx || !mip || !parm) { set_err("gk_ios_driver: null argument"); return GK_EABI; }
     const int rank = shard ? shard->rank : 0, size = shard ? shard->size : 1;
@@ -2082,7 +2210,16 @@ extern "C" int gk_ios_driver_sharded(gk_ctx *ctx, gk_mip *mip, const gk_iocp *pa
     bool fail_sync = false;
     long long moved = 0;
     // GK_BNB_LOG=1: where the search's wall time goes (stderr)
-    static const bool bnb_log = std::getenv("GK_BNB_LOG") != nullptr;
+    static const int bnb_lvl = [] {
+        const char *e = std::getenv("GK_BNB_LOG");
+        return e ? std::max(1, std::atoi(e)) : 0;
+    }();
+    static const bool bnb_log = bnb_lvl > 0;
+    // GK_BNB_LOG=2: device time of the node kernel's phases (sums over the
+    // entries that reach the end, in device clock ticks) and batch spans
+    double ph_sum[7] = {0, 0, 0, 0, 0, 0, 0}, span_sum = 0.0;
+    long long ph_cnt = 0, pp_cnt = 0;
+    std::vector<unsigned long long> hst;
     S.tsc_on = bnb_log;
     const unsigned long long tsc_beg = bnb_log ? MipSolver::tsc() : 0ull;
     double t_launch = 0.0, t_wait = 0.0, t_proc = 0.0, t_nd = 0.0;
@@ -2169,6 +2306,12 @@ extern "C" int gk_ios_driver_sharded(gk_ctx *ctx, gk_mip *mip, const gk_iocp *pa
         io.tab_age_max = 100;
         io.br_j = (const int *)(din + Y.brj); io.br_dir = (const int *)(din + Y.brd);
         io.br_val = (const double *)(din + Y.brv);
+        io.stamps = nullptr;
+        if (bnb_lvl >= 2) {
+            bf.dstamp.ensure((size_t)S.BMAX * 8);
+            (void)hipMemsetAsync(bf.dstamp.p, 0, (size_t)nb * 8 * sizeof(unsigned long long), s);
+            io.stamps = bf.dstamp.p;
+        }
         io.nfrac = (int *)(dout + Y.nf); io.jfirst = (int *)(dout + Y.jf); io.jlast = (int *)(dout + Y.jl);
         io.jmost = (int *)(dout + Y.jm); io.nmost = (int *)(dout + Y.nm); io.iisum = (double *)(dout + Y.ii);
         launch_node_lp(s, P, io, nb);
@@ -2180,6 +2323,26 @@ extern "C" int gk_ios_driver_sharded(gk_ctx *ctx, gk_mip *mip, const gk_iocp *pa
         const auto tw0 = std::chrono::steady_clock::now();
         if (hipEventSynchronize(bf.done) != hipSuccess) { fail_sync = true; return; }
         t_wait += secs(tw0);
+        if (bnb_lvl >= 2 && bf.nb > 0) {
+            hst.resize((size_t)bf.nb * 8);
+            (void)hipMemcpy(hst.data(), bf.dstamp.p, hst.size() * sizeof(unsigned long long), hipMemcpyDeviceToHost);
+            unsigned long long lo = ~0ull, hi = 0;
+            for (int b = 0; b < bf.nb; b++) {
+                const unsigned long long *t = hst.data() + (size_t)b * 8;
+                if (t[0]) lo = std::min(lo, t[0]);
+                if (t[7]) hi = std::max(hi, t[7]);
+                if (t[0] && t[7] && !t[1]) { pp_cnt++; ph_sum[5] += (double)(t[7] - t[0]); }
+                if (!(t[0] && t[5] && t[1] && t[2] && t[3] && t[4] && t[7])) continue;
+                ph_cnt++;
+                ph_sum[6] += (double)(t[5] - t[0]);
+                ph_sum[0] += (double)(t[1] - t[5]);
+                ph_sum[1] += (double)(t[2] - t[1]);
+                ph_sum[2] += (double)(t[3] - t[2]);
+                ph_sum[3] += (double)(t[4] - t[3]);
+                ph_sum[4] += (double)(t[7] - t[4]);
+            }
+            if (hi > lo) span_sum += (double)(hi - lo);
+        }
         const auto tp0 = std::chrono::steady_clock::now();
         struct Acc { double &t; std::chrono::steady_clock::time_point a; ~Acc() {
             t += std::chrono::duration<double>(std::chrono::steady_clock::now() - a).count(); } } acc_{t_proc, tp0};
@@ -2436,6 +2599,7 @@ extern "C" int gk_ios_driver_sharded(gk_ctx *ctx, gk_mip *mip, const gk_iocp *pa
         }
         if (!have_work) break;
         since_sync++;
+        if (inc && split_done) S.set_gbest(inc(inc_info, S.best));
         // assemble the next batch into the free buffer set: pseudocost
         // probes first (they unblock parked nodes), then the preferred
         // children, then the open nodes in the order of bt_tech
@@ -2499,6 +2663,15 @@ extern "C" int gk_ios_driver_sharded(gk_ctx *ctx, gk_mip *mip, const gk_iocp *pa
                         "wait %.3f ms, process %.3f ms (node_done %.3f); open %zu; lp %lld, pp-fathomed %lld, created %lld\n",
                 1e3 * secs(t0), n_batches, n_ents, n_batches ? (double)n_ents / n_batches : 0.0, 1e3 * t_launch,
                 1e3 * t_wait, 1e3 * t_proc, 1e3 * t_nd, S.open.size(), S.lp_solves, S.pp_fathomed, S.created);
+    if (bnb_lvl >= 2) {
+        const double us = 0.01;                           // device clock: 100 MHz
+        const double c = ph_cnt ? 1.0 / (double)ph_cnt : 0.0;
+        fprintf(stderr, "[gk bnb] node kernel, mean us per node LP (%lld): load %.2f, preprocess %.2f, tableau %.2f, "
+                        "x/d %.2f, simplex %.2f, branching+records %.2f; preprocess-fathomed (%lld) %.2f; "
+                        "batch spans %.3f ms in all\n", ph_cnt, ph_sum[6] * c * us, ph_sum[0] * c * us, ph_sum[1] * c * us,
+                ph_sum[2] * c * us, ph_sum[3] * c * us, ph_sum[4] * c * us, pp_cnt,
+                pp_cnt ? ph_sum[5] / (double)pp_cnt * us : 0.0, span_sum * us * 1e-3);
+    }
     if (bnb_log) {
         const double tpms = (double)(MipSolver::tsc() - tsc_beg) / (1e3 * secs(t0));     // ticks per ms
         fprintf(stderr, "[gk bnb] node_done parts: integrality %.3f ms, choice %.3f ms, children (incl. heap) %.3f ms, "

@@ -116,7 +116,8 @@ EXPORTS = ["gk_abi_version", "gk_device_count", "gk_ctx_create", "gk_ctx_destroy
            "gk_comm_destroy", "gk_comm_backend", "gk_comm_rank", "gk_comm_size", "gk_comm_allgather",
            "gk_ios_driver_comm", "gk_comm_set_option", "gk_npp_create", "gk_npp_destroy", "gk_npp_load",
            "gk_npp_simplex", "gk_npp_integer", "gk_npp_build_size", "gk_npp_build", "gk_npp_postprocess",
-           "gk_npp_unload_sol", "gk_npp_unload_mip", "gk_sp_selftest"]
+           "gk_npp_unload_sol", "gk_npp_unload_mip", "gk_sp_selftest", "gk_comm_incumbent",
+           "gk_comm_shared_incumbent"]
 
 # gk_report_fn (glpk_mi355x.h): one progress line or termination message of
 # a gk_spx_* call, in the order the reference prints them
@@ -170,6 +171,10 @@ def load_library(path: str = LIB_PATH):
     L.gk_comm_backend.argtypes = [P]
     L.gk_comm_allgather.argtypes = [P, P, C.c_size_t, P]
     L.gk_comm_allgather.restype = C.c_int
+    L.gk_comm_incumbent.argtypes = [P, C.c_double]
+    L.gk_comm_incumbent.restype = C.c_double
+    L.gk_comm_shared_incumbent.argtypes = [P]
+    L.gk_comm_shared_incumbent.restype = C.c_int
     L.gk_ios_driver_comm.argtypes = [P, C.POINTER(Mip), C.POINTER(Iocp), P]
     L.gk_ios_driver_comm.restype = C.c_int
     L.gk_ios_driver.argtypes = [P, C.POINTER(Mip), C.POINTER(Iocp)]
@@ -252,6 +257,15 @@ class Comm:
             raise GkError("gk_comm_allgather failed")
         raw = dst.raw
         return [raw[r * n:(r + 1) * n] for r in range(self.size)]
+
+    @property
+    def shared_incumbent(self) -> bool:
+        """every rank on this host: the incumbent word in shared memory"""
+        return bool(self.L.gk_comm_shared_incumbent(self.h))
+
+    def incumbent(self, mine: float) -> float:
+        """publish mine, return the best (minimum) published by any rank"""
+        return float(self.L.gk_comm_incumbent(self.h, float(mine)))
 
     def close(self):
         if getattr(self, "h", None):

@@ -366,6 +366,15 @@ int      gk_comm_size(const gk_comm *comm);
 /* recv[r * bytes .. (r + 1) * bytes) = rank r's send block; 0 on success.
  * The signature of gk_ios_shard.allgather (info = the gk_comm). */
 int      gk_comm_allgather(void *comm, const void *send, size_t bytes, void *recv);
+/* the incumbent shared by the ranks between the exchange epochs: when every
+ * rank of comm runs on one host, one word of shared memory holds the best
+ * objective published so far (an atomic min on an order-preserving image of
+ * the double).  gk_comm_incumbent publishes mine and returns the best over
+ * the ranks (mine itself without a shared word); the sharded search calls it
+ * before every batch (internal minimisation form, DBL_MAX: none).
+ * gk_comm_shared_incumbent: 1 when the word exists. */
+double   gk_comm_incumbent(gk_comm *comm, double mine);
+int      gk_comm_shared_incumbent(const gk_comm *comm);
 /* options of the sharded search run through gk_ios_driver_comm:
  * GK_COMM_OPT_RAMP  the frontier per rank before the split (gk_ios_shard.ramp_nodes;
  *                   0 the default, < 0 split the root alone: rank 0 starts with all the work)

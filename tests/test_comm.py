@@ -61,6 +61,56 @@ def test_comm_tcp_allgather_cpu(size):
             assert out[k] == want
 
 
+def _incumbent_worker(rank, size, port, q):
+    try:
+        import sys
+        root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+        sys.path.insert(0, root)
+        import __graft_entry__
+        __graft_entry__.load_package()
+        from glpk_js_amd import gk as g
+        c = g.Comm(None, rank, size, f"127.0.0.1:{port}", g.GK_COMM_TCP)
+        seen = [c.incumbent(1.7976931348623157e308)]          # nothing published yet: DBL_MAX
+        c.allgather(b"x")                                      # every rank has read the empty word
+        vals = {0: [5.0, -3.25, 7.0], 1: [4.0, 2.0, -1e300], 2: [-0.0, 6.0, 1.0]}[rank]
+        for v in vals:
+            seen.append(c.incumbent(v))
+        c.allgather(b"y")                                      # every rank has published all of its values
+        seen.append(c.incumbent(1e308))
+        q.put((rank, c.shared_incumbent, seen))
+        c.close()
+    except Exception as e:
+        q.put((rank, None, repr(e)))
+
+
+@pytest.mark.parametrize("size", [2, 3])
+def test_comm_shared_incumbent_cpu(size):
+    """The incumbent word the ranks of one host share between the exchange
+    epochs (gk_comm_incumbent): an atomic minimum over an order-preserving
+    image of the double — negative values, -0.0 and -1e300 included — so
+    every rank reads the best objective any rank has published, and never a
+    value worse than its own."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = free_port()
+    ps = [ctx.Process(target=_incumbent_worker, args=(r, size, port, q)) for r in range(size)]
+    for p in ps:
+        p.start()
+    res = [q.get(timeout=120) for _ in range(size)]
+    for p in ps:
+        p.join(timeout=60)
+    vals = {0: [5.0, -3.25, 7.0], 1: [4.0, 2.0, -1e300], 2: [-0.0, 6.0, 1.0]}
+    best = min(v for r in range(size) for v in vals[r])
+    for rank, shared, seen in res:
+        assert shared is True, seen
+        assert seen[0] == 1.7976931348623157e308
+        run = seen[0]
+        for v, got in zip(vals[rank], seen[1:4]):
+            run = min(run, v)
+            assert got <= run                  # at least as good as everything this rank published
+        assert seen[-1] == best                # after the barrier: the best of all ranks
+
+
 def _mip_worker(rank, size, port, name, ramp, q, iocp=None):
     try:
         import sys

@@ -11,6 +11,9 @@
 #   bench            python bench.py (defaults: the driver's command)
 #   bench:ARGS       python bench.py ARGS (commas for spaces)
 #   profile          tools/profile_round.sh (rocprofv3 stats + PMC passes)
+#   apitrace         rocprofv3 HIP API + kernel + copy traces (CSV) of a short bench
+#   ktrace           rocprofv3 kernel trace of the bench's timed region: stats
+#                    and the idle gaps between consecutive kernels
 #   py:SCRIPT,ARGS   python3 -u SCRIPT ARGS (tools/…; commas for spaces)
 set -e
 NAME=$1; shift
@@ -29,6 +32,16 @@ for step in "$@"; do
         bench:*) a=$(echo "${step#bench:}" | tr ',' ' ');
                  timeout -k 10 900 python -u bench.py $a > "$O/bench_args.json" 2> "$O/bench_args.err" ;;
         profile) bash tools/profile_round.sh "$NAME/profile" ;;
+        apitrace) cd /tmp && cd "$GRAFT_REPO_ROOT";
+                timeout -k 10 400 rocprofv3 --hip-trace --kernel-trace --memory-copy-trace --output-format csv \
+                    -d /tmp/at_$NAME -o run -- python3 bench.py --gpus 1 --steps 3 --warmup 2 --no-cpu --no-extra \
+                    > "$O/at_bench.json" 2> "$O/at.err";
+                mkdir -p "$O/apitrace"; find /tmp/at_$NAME -name '*.csv' -exec cp {} "$O/apitrace/" \; ;;
+        ktrace) cd /tmp && cd "$GRAFT_REPO_ROOT";
+                timeout -k 10 400 rocprofv3 --kernel-trace --stats -d /tmp/kt_$NAME -o run -- python3 bench.py \
+                    --gpus 1 --steps 20 --warmup 5 --no-cpu --no-extra > "$O/kt_bench.json" 2> "$O/kt.err";
+                python3 tools/prof_stats.py /tmp/kt_$NAME/run_results.db --marked --csv "$O/kt_stats.csv" \
+                    --gaps "$O/kt_gaps.txt" > "$O/kt_grid.txt" ;;
         py:*) a=$(echo "${step#py:}" | tr ',' ' '); s=$(basename ${a%% *} .py);
               timeout -k 10 900 python3 -u $a > "$O/$s.log" 2> "$O/$s.err" ;;
         *) echo "unknown step $step"; exit 2 ;;

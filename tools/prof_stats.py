@@ -22,6 +22,7 @@ def main():
     ap.add_argument("--window", type=int, default=0,
                     help="with --marked: the i-th pair of k_gk_mark launches (0-based)")
     ap.add_argument("--json", help="write {kernel: {calls, avg_ns}} of the selection")
+    ap.add_argument("--gaps", help="write the idle time between consecutive kernels, per (previous, next) pair")
     a = ap.parse_args()
     c = sqlite3.connect(a.db)
     rows = c.execute("select name, duration, grid_x, workgroup_x, start from kernels order by start").fetchall()
@@ -30,6 +31,20 @@ def main():
         w = 2 * a.window
         assert len(marks) >= w + 2, "no such k_gk_mark window in the trace"
         rows = [r for r in rows if marks[w] < r[4] < marks[w + 1]]
+    if a.gaps:
+        # end of kernel i to start of kernel i + 1 (one stream: the engine's)
+        short = lambda nm: nm.split("(")[0].replace("void ", "").replace("gk::", "")[:40]
+        pairs = {}
+        for r0, r1 in zip(rows, rows[1:]):
+            g = r1[4] - (r0[4] + r0[1])
+            if 0 <= g < 200000:           # within one graph / batch (< 200 us)
+                pairs.setdefault((short(r0[0]), short(r1[0])), []).append(g)
+        with open(a.gaps, "w") as f:
+            f.write(f"{'previous':40s} {'next':40s} {'count':>7s} {'median_us':>9s} {'mean_us':>8s} {'p10_us':>7s} {'p90_us':>7s}\n")
+            for (k0, k1), v in sorted(pairs.items(), key=lambda kv: -len(kv[1])):
+                v = sorted(v)
+                q = lambda f_: v[min(len(v) - 1, int(f_ * len(v)))] / 1000
+                f.write(f"{k0:40s} {k1:40s} {len(v):7d} {q(0.5):9.2f} {sum(v)/len(v)/1000:8.2f} {q(0.1):7.2f} {q(0.9):7.2f}\n")
     by = {}
     for name, dur, gx, wx, _ in rows:
         e = by.setdefault(name, {"d": [], "grids": set()})
