@@ -28,7 +28,7 @@ import __graft_entry__  # noqa: E402
 HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 ROOF_KERNEL = "k_dual_update"
 ROW_KERNEL = "k_dual_row"
-ROUND = "r03"
+ROUND = "r04"
 # the C port (oracle/) against the reference itself, both on one core of the
 # build container on C3 from the slack basis: the port 285.8 pivots/s over a
 # 20 s window (6,874 pivots, init_csa included), the reference node 9.4
@@ -215,20 +215,23 @@ def main():
             dev["upd_bytes"] += s_.upd_bytes
         P.profile(0)
 
-    # cross-check pass: the same number of steps again with HIP events
-    # recorded on the engine stream around every pivot-row kernel (eager
-    # launches: the HIP runtime torch carries does not time event nodes inside
-    # captured graphs); the event interval includes the launch gap
-    trow = {"ms": 0.0, "launches": 0, "bytes": 0.0}
+    # event pass: the same steps again, launched eagerly (event nodes inside
+    # captured graphs are not timed by every HIP runtime), the pivot-row and
+    # the fused update kernels each through hipExtLaunchKernelGGL with a
+    # start and a stop event on the engine stream — the command processor's
+    # timestamps of the dispatch itself, which is what a profiler reports
+    trow = {"ms": 0.0, "launches": 0, "bytes": 0.0, "upd_ms": 0.0, "upd_launches": 0}
     if rank == 0:
         rewind()
         P.profile(True)
         for _ in range(args.steps):
-            step("events cross-check")
+            step("events pass")
             s_ = P.stats()
             trow["ms"] += s_.trow_ms
             trow["launches"] += s_.trow_launches
             trow["bytes"] += s_.trow_bytes
+            trow["upd_ms"] += s_.upd_dev_ms
+            trow["upd_launches"] += s_.upd_dev_launches
         P.profile(False)
 
     tot_piv, max_dt = piv, dt
@@ -241,19 +244,17 @@ def main():
         max_dt = float(t.item())
     value = tot_piv / max_dt
 
-    # roofline of the dominant kernel, k_dual_update (pass-2 choice, FTRAN
-    # of the entering column and the PSE vector over the dense columns of
-    # inv(B), the product-form update of those entries, update_bbar / cbar /
-    # gamma and the next chuzr candidates: 31% of the pivot's kernel time),
-    # and beside it k_dual_row (chuzr, rho, the pivot row over the rows of AT
-    # in the support of rho), both timed live in the roofline pass with the
-    # device wall clock (s_memrealtime, stamped inside the captured graphs):
-    # k_dual_update from its block 0's entry to its last block exit;
-    # k_dual_row from the last block exit of the kernel before it to its own
-    # last block exit (a profiler's per-dispatch bracket).  Algorithmic bytes
-    # per launch are accumulated on the device for the same launches
-    # (16 m ns + 64 m + 29 n for k_dual_update, 8 ns n for
-    # k_dual_row).
+    # roofline of the dominant kernel: of the two kernels that carry the
+    # pivot's time, k_dual_row (chuzr, rho, the pivot row over the rows of AT
+    # in the support of rho) and k_dual_update (pass-2 choice, FTRAN of the
+    # entering column and the PSE vector over the dense columns of inv(B),
+    # their product-form update, update_bbar / cbar / gamma, the next chuzr
+    # candidates), the one with the larger total event time.  Per launch:
+    # algorithmic bytes accumulated on the device in the stamp pass (DESIGN.md
+    # §4: 8 ns n for k_dual_row; 16 m ns + 64 m + 29 n for k_dual_update, over
+    # every update launch) over the duration between the kernel's start and
+    # stop events (event pass).  The device-clock stamp timings and the
+    # committed rocprof averages of the same command are reported beside it.
     roof = None
     kern = {}
     if rank == 0:
@@ -261,60 +262,57 @@ def main():
                             (3, "binv_rank1_dense")):
             ms_k, b_k = P.time_kernel(which, reps=10)
             kern[name] = {"ms": round(ms_k, 5), "bytes": b_k, "GBps": round(b_k / (ms_k * 1e-3) / 1e9, 1)}
-        nl = max(1, dev["launches"])
-        b_row = dev["bytes"] / nl
-        nr_ = max(1, dev["launches_r"])
-        ms_row = dev["ms_r"] / nr_
-        ach_row = b_row / (ms_row * 1e-3) / 1e9 if ms_row > 0 else 0.0
-        nu = max(1, dev["upd_launches"])
-        b = dev["upd_bytes"] / max(1, dev["pivots"])
-        ms = dev["upd_ms"] / nu
-        achieved = b / (ms * 1e-3) / 1e9 if ms > 0 else 0.0
-        ne = max(1, trow["launches"])
-        # the committed profiles of this same command (tools/profile_round.sh
-        # writes profiles/<round>_profile_meta.json with the command it
-        # profiled): rocprofv3's average duration of the kernel over the timed
-        # region, and HBM bytes per launch from the --pmc FETCH_SIZE /
-        # WRITE_SIZE passes; used only when the profiled command matches
         prof = load_profile(args)
-        pu, pr = prof.get(ROOF_KERNEL, {}), prof.get(ROW_KERNEL, {})
-        # the whole pivot (all kernels): the roofline pass's algorithmic bytes
+        nl = max(1, dev["launches"])
+        nr_ = max(1, dev["launches_r"])
+        nu_ev = max(1, trow["upd_launches"])
+        ne = max(1, trow["launches"])
+        cands = {
+            ROW_KERNEL: {"desc": "chuzr, rho = row p of inv(B), pivot row trow = -rho' N over the rows of A in the "
+                                 "support of rho, ratio-test candidates",
+                         "bytes": dev["bytes"] / nl, "ms": trow["ms"] / ne, "launches": trow["launches"],
+                         "stamp_ms": dev["ms_r"] / nr_,
+                         "stamp_timing": "last block exit of the kernel before it to its own last block exit"},
+            ROOF_KERNEL: {"desc": "pass-2 choice, FTRAN of the entering column and the PSE vector over the dense "
+                                  "columns of inv(B), their product-form update, update_bbar/cbar/gamma, next chuzr "
+                                  "candidates: one kernel",
+                          "bytes": dev["upd_bytes"] / nu_ev, "ms": trow["upd_ms"] / nu_ev,
+                          "launches": trow["upd_launches"],
+                          "stamp_ms": dev["upd_ms"] / max(1, dev["upd_launches"]),
+                          "stamp_timing": "block 0 entry to the last block exit"},
+        }
+
+        def entry(k):
+            c = cands[k]
+            pk = prof.get(k, {})
+            ach = c["bytes"] / (c["ms"] * 1e-3) / 1e9 if c["ms"] > 0 else 0.0
+            return {"kernel": k + " (" + c["desc"] + ")", "achieved": round(ach, 1),
+                    "frac": round(ach / HBM_PEAK_GBS, 4), "ms_per_launch": round(c["ms"], 5),
+                    "launches": c["launches"], "bytes_per_launch": round(c["bytes"]),
+                    "traffic": pk.get("traffic"),
+                    "traffic_over_algorithmic": round(pk["traffic"] / c["bytes"], 3)
+                    if pk.get("traffic") and c["bytes"] > 0 else None,
+                    "timing": "hipExtLaunchKernelGGL start/stop events of every launch of the event pass (the timed "
+                              "region's steps replayed eagerly on the engine stream)",
+                    "stamp_ms_per_launch": round(c["stamp_ms"], 5), "stamp_timing": c["stamp_timing"],
+                    "rocprof_ms_per_launch": pk.get("rocprof_ms"),
+                    "rocprof_frac": round(c["bytes"] / (pk["rocprof_ms"] * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
+                    if pk.get("rocprof_ms") else None}
+
+        dom = max(cands, key=lambda k: cands[k]["ms"] * cands[k]["launches"])
+        other = ROW_KERNEL if dom == ROOF_KERNEL else ROOF_KERNEL
+        e_dom = entry(dom)
+        # the whole pivot (all kernels): the stamp pass's algorithmic bytes
         # per pivot times the timed region's pivots over its time
         step_bpp = dev["bytes_pivots"] / max(1, dev["pivots"])
         step_gbps = step_bpp * piv / max_dt / 1e9 if max_dt > 0 else 0.0
-        roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": round(achieved / HBM_PEAK_GBS, 4),
-                "traffic": pu.get("traffic"),
-                "traffic_over_algorithmic": round(pu["traffic"] / b, 3) if pu.get("traffic") else None,
-                "kernel": ROOF_KERNEL + " (pass-2 choice, FTRAN of the entering column and the PSE vector over the "
-                                        "dense columns of inv(B), their product-form update, update_bbar/cbar/gamma, "
-                                        "next chuzr candidates: one kernel)",
-                "ms_per_launch": round(ms, 5), "launches": dev["upd_launches"],
-                "bytes_per_launch": round(b),
-                "timing": "device wall clock over every launch of the roofline pass (the timed region's steps "
-                          "repeated with kernel stamps on): block 0 entry to the last block exit",
-                "rocprof_ms_per_launch": pu.get("rocprof_ms"),
-                "rocprof_frac": round(b / (pu["rocprof_ms"] * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
-                if pu.get("rocprof_ms") else None,
-                "profile_source": prof.get("source"),
-                "pivot_row_kernel": {
-                    "kernel": ROW_KERNEL + " (chuzr, rho = row p of inv(B), pivot row trow = -rho' N over the rows of "
-                                           "A in the support of rho, ratio-test candidates)",
-                    "achieved": round(ach_row, 1), "frac": round(ach_row / HBM_PEAK_GBS, 4),
-                    "ms_per_launch": round(ms_row, 5), "launches": dev["launches_r"],
-                    "bytes_per_launch": round(b_row), "traffic": pr.get("traffic"),
-                    "traffic_over_algorithmic": round(pr["traffic"] / b_row, 3) if pr.get("traffic") else None,
-                    "rocprof_ms_per_launch": pr.get("rocprof_ms"),
-                    "timing": "last block exit of the kernel before it to its own last block exit",
-                    "entry_to_next_entry_ms": round(dev["ms_b"] / nl, 5),
-                    "exec_ms_per_launch": round(dev["ms"] / nl, 5)},
-                "hip_events_cross_check": {"kernel": ROW_KERNEL, "ms_per_launch": round(trow["ms"] / ne, 5),
-                                           "launches": trow["launches"],
-                                           "bytes_per_launch": round(trow["bytes"] / ne),
-                                           "note": "third pass, eager launches, HIP events on the engine stream "
-                                                   "around the kernel; the interval includes the launch gap"},
-                "step_achieved": round(step_gbps, 1), "step_frac": round(step_gbps / HBM_PEAK_GBS, 4),
-                "step_bytes_per_pivot": round(step_bpp)}
+        roof = {"bound": "hbm", "achieved": e_dom["achieved"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": e_dom["frac"], "traffic": e_dom["traffic"]}
+        roof.update({k: v for k, v in e_dom.items() if k not in roof})
+        roof.update({"dominance": {k: round(cands[k]["ms"] * cands[k]["launches"], 3) for k in cands},
+                     "profile_source": prof.get("source"), "second_kernel": entry(other),
+                     "step_achieved": round(step_gbps, 1), "step_frac": round(step_gbps / HBM_PEAK_GBS, 4),
+                     "step_bytes_per_pivot": round(step_bpp)})
 
     cpu = None
     extra = {}

@@ -33,6 +33,7 @@
 //                        (:1020-1134), rank-1 update of inv(B); chuzr candidates
 //                        and the phase-I check of the next iteration
 #include "gk_device.h"
+#include <hip/hip_ext.h>
 #include <algorithm>
 #include <cstdlib>
 
@@ -2697,15 +2698,26 @@ static int prev_blocks(const SpxDev &d, const DualPlan &pl)
 }
 
 template <int NRHS, int SP>
-static void launch_update(hipStream_t s, const SpxDev &d, const DualPlan &pl, int gn, int ncb, int rowpath)
+static void launch_update(hipStream_t s, const SpxDev &d, const DualPlan &pl, int gn, int ncb, int rowpath,
+                          hipEvent_t e0 = nullptr, hipEvent_t e1 = nullptr)
 {
     const dim3 grid(cdiv(d.m, pl.ugm == 8 ? 32 : 16)), block(64 * pl.uwaves);
-    if (pl.ugm == 8)
-        hipLaunchKernelGGL((k_dual_update<NRHS, SP, 8, 32>), grid, block, 0, s, d, gn, ncb, pl.nr_cap, rowpath,
-                           bytes_fixed(d));
-    else
-        hipLaunchKernelGGL((k_dual_update<NRHS, SP, 4, 16>), grid, block, 0, s, d, gn, ncb, pl.nr_cap, rowpath,
-                           bytes_fixed(d));
+    // (the extended launch only with events: graph capture takes the plain one)
+    if (pl.ugm == 8) {
+        if (e0)
+            hipExtLaunchKernelGGL((k_dual_update<NRHS, SP, 8, 32>), grid, block, 0, s, e0, e1, 0, d, gn, ncb,
+                                  pl.nr_cap, rowpath, bytes_fixed(d));
+        else
+            hipLaunchKernelGGL((k_dual_update<NRHS, SP, 8, 32>), grid, block, 0, s, d, gn, ncb, pl.nr_cap, rowpath,
+                               bytes_fixed(d));
+    } else {
+        if (e0)
+            hipExtLaunchKernelGGL((k_dual_update<NRHS, SP, 4, 16>), grid, block, 0, s, e0, e1, 0, d, gn, ncb,
+                                  pl.nr_cap, rowpath, bytes_fixed(d));
+        else
+            hipLaunchKernelGGL((k_dual_update<NRHS, SP, 4, 16>), grid, block, 0, s, d, gn, ncb, pl.nr_cap, rowpath,
+                               bytes_fixed(d));
+    }
 }
 
 void dual_batch_end(hipStream_t s, const SpxDev &d, const DualPlan &pl)
@@ -2724,7 +2736,8 @@ static void launch_ftran(hipStream_t s, const SpxDev &d, const DualPlan &pl, int
                        pl.awsplits);
 }
 
-void dual_iteration2(hipStream_t s, const SpxDev &d, const DualPlan &pl, hipEvent_t ev0, hipEvent_t ev1)
+void dual_iteration2(hipStream_t s, const SpxDev &d, const DualPlan &pl, hipEvent_t ev0, hipEvent_t ev1,
+                     hipEvent_t ev2, hipEvent_t ev3)
 {
     const int m = d.m, n = d.n;
     const int gv = cdiv(std::max(m, n), 256), gn = cdiv(n, 256), tiles_m = cdiv(m, 512);
@@ -2777,12 +2790,14 @@ void dual_iteration2(hipStream_t s, const SpxDev &d, const DualPlan &pl, hipEven
     if (pl.rowpath) {
         // chuzr, rho and the pivot row in one kernel
         ncb = cdiv(std::max(m, n), 64);
-        if (ev0) (void)hipEventRecord(ev0, s);
         // (16 entries per wave in trips 1-2 measured slower on C3 — 11.6 against
         // 9.0 us of span, profiles/r04_trace_pivot_np16_reverted.txt — than 8
         // plus the dependent loop: k_dual_row<16> is kept for experiments)
-        hipLaunchKernelGGL(k_dual_row<8>, dim3(ncb), dim3(64 * pl.twaves), 0, s, d, pl.pse, pl.nr_cap, pl.gm);
-        if (ev1) (void)hipEventRecord(ev1, s);
+        if (ev0)
+            hipExtLaunchKernelGGL(k_dual_row<8>, dim3(ncb), dim3(64 * pl.twaves), 0, s, ev0, ev1, 0, d, pl.pse,
+                                  pl.nr_cap, pl.gm);
+        else
+            hipLaunchKernelGGL(k_dual_row<8>, dim3(ncb), dim3(64 * pl.twaves), 0, s, d, pl.pse, pl.nr_cap, pl.gm);
     } else {
         if (!pl.rigorous && d.A.dense && m >= 1024)
             hipLaunchKernelGGL(k_dual_top_grid, dim3(cdiv(m, 256)), dim3(256), 0, s, d);
@@ -2803,8 +2818,8 @@ void dual_iteration2(hipStream_t s, const SpxDev &d, const DualPlan &pl, hipEven
     hipLaunchKernelGGL(k_dual_ratio, dim3(gn + (aw ? (awone ? cdiv(m, 64) : tiles_m * pl.awsplits) : 0)), dim3(256), 0,
                        s, d, gn, tiles_m, pl.rowpath, ncb, awone, prev_blocks(d, pl));
     if (pl.fupd) {
-        if (pl.pse) launch_update<2, 0>(s, d, pl, gn, ncb, pl.rowpath);
-        else launch_update<1, 0>(s, d, pl, gn, ncb, pl.rowpath);
+        if (pl.pse) launch_update<2, 0>(s, d, pl, gn, ncb, pl.rowpath, ev2, ev3);
+        else launch_update<1, 0>(s, d, pl, gn, ncb, pl.rowpath, ev2, ev3);
         return;
     }
     if (pl.fused) {

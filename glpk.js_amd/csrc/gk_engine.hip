@@ -1458,14 +1458,19 @@ struct Spx {
     void rebuild_lists();
     void prof_events(int K)
     {
-        while ((int)E->ev.size() < 2 * K) {
+        while ((int)E->ev.size() < 4 * K) {
             hipEvent_t e;
             HIPCHK(hipEventCreate(&e));
             E->ev.push_back(e);
         }
     }
-    hipEvent_t ev0(int t) const { return (E->prof == 1 || E->prof == 2) ? E->ev[2 * t] : nullptr; }
-    hipEvent_t ev1(int t) const { return (E->prof == 1 || E->prof == 2) ? E->ev[2 * t + 1] : nullptr; }
+    // prof 1 / 2: per pivot t, the start / stop events of the pivot-row
+    // kernel (4 t, 4 t + 1) and of the fused update kernel (4 t + 2, 4 t + 3)
+    hipEvent_t ev0(int t) const { return (E->prof == 1 || E->prof == 2) ? E->ev[4 * t] : nullptr; }
+    hipEvent_t ev1(int t) const { return (E->prof == 1 || E->prof == 2) ? E->ev[4 * t + 1] : nullptr; }
+    hipEvent_t ev2(int t) const { return (E->prof == 1 || E->prof == 2) ? E->ev[4 * t + 2] : nullptr; }
+    hipEvent_t ev3(int t) const { return (E->prof == 1 || E->prof == 2) ? E->ev[4 * t + 3] : nullptr; }
+    bool ev_upd = false;                        // the last eager batch ran the fused update (its events recorded)
     int run_dual();
     int run_primal();
     int batch(int K, int rigorous);
@@ -1790,8 +1795,9 @@ int Spx::batch(int K, int rigorous)
         if (!rigorous && K >= 4 && !evp && !f->sparse) run_graph(d, pl, K);
         else {
             dual_batch_begin(s, d, pl);
-            for (int t = 0; t < K; t++) dual_iteration2(s, d, pl, ev0(t), ev1(t));
+            for (int t = 0; t < K; t++) dual_iteration2(s, d, pl, ev0(t), ev1(t), ev2(t), ev3(t));
             dual_batch_end(s, d, pl);
+            ev_upd = evp && pl.fupd && pl.rowpath;
         }
     } else if (f->sparse) {
         // the primal pivot on the sparse factor (rigorous mode included: no
@@ -1827,23 +1833,31 @@ int Spx::batch(int K, int rigorous)
     f->stats.trow_dev_launches = (long long)hs.trow_n;
     f->stats.trow_dev_ms_r = hs.trow_ticks_r / (double)ctx->wall_khz;
     f->stats.trow_dev_launches_r = (long long)hs.trow_nr;
-    f->stats.upd_dev_ms = hs.upd_ticks / (double)ctx->wall_khz;
-    f->stats.upd_dev_launches = (long long)hs.upd_n;
+    if (E->prof != 1 && E->prof != 2) {                 // (prof 1 / 2: the update's events, below)
+        f->stats.upd_dev_ms = hs.upd_ticks / (double)ctx->wall_khz;
+        f->stats.upd_dev_launches = (long long)hs.upd_n;
+    }
     f->stats.upd_bytes = hs.bytes_upd;
     f->stats.panel_hits = (long long)hs.phits;
     f->stats.panel_refills = (long long)hs.pmisses;
     if (dual && (E->prof == 1 || E->prof == 2)) {
         for (int t = 0; t < hs.npiv; t++) {
             float ms = 0.f;
-            hipError_t e = hipEventElapsedTime(&ms, E->ev[2 * t], E->ev[2 * t + 1]);
+            hipError_t e = hipEventElapsedTime(&ms, E->ev[4 * t], E->ev[4 * t + 1]);
             if (e != hipSuccess)
                 throw AbiError{std::string("event timing: ") + hipGetErrorName(e) + " t=" + std::to_string(t) +
                                " K=" + std::to_string(K) + " npiv=" + std::to_string(hs.npiv) +
                                " graph=" + std::to_string(!rigorous && K >= 4) + " nev=" + std::to_string(E->ev.size()) +
-                               " q0=" + hipGetErrorName(hipEventQuery(E->ev[2 * t])) +
-                               " q1=" + hipGetErrorName(hipEventQuery(E->ev[2 * t + 1]))};
+                               " q0=" + hipGetErrorName(hipEventQuery(E->ev[4 * t])) +
+                               " q1=" + hipGetErrorName(hipEventQuery(E->ev[4 * t + 1]))};
             f->stats.trow_ms += ms;
             f->stats.trow_launches++;
+            // the fused update's events (the same extended launch); with
+            // prof 1 / 2 these fields carry them instead of clock stamps
+            if (ev_upd && hipEventElapsedTime(&ms, E->ev[4 * t + 2], E->ev[4 * t + 3]) == hipSuccess) {
+                f->stats.upd_dev_ms += ms;
+                f->stats.upd_dev_launches++;
+            }
         }
     }
     if (hs.npiv > 0) {

@@ -214,9 +214,11 @@ struct DualPlan {
 void dual_batch_begin(hipStream_t s, const SpxDev &d, const DualPlan &pl);
 void dual_batch_end(hipStream_t s, const SpxDev &d, const DualPlan &pl);
 DualPlan dual_plan(const SpxDev &d, int nr_max, int nwl_max, int pse, int rigorous);
-// ev0/ev1 (optional, eager launches only): events recorded around the pivot-row kernel
+// ev0/ev1, ev2/ev3 (optional, eager launches only): the start / stop events
+// of the pivot-row kernel and of the fused update kernel (hipExtLaunchKernelGGL:
+// the command processor's timestamps of the dispatch itself, as a profiler's)
 void dual_iteration2(hipStream_t s, const SpxDev &d, const DualPlan &pl, hipEvent_t ev0 = nullptr,
-                     hipEvent_t ev1 = nullptr);
+                     hipEvent_t ev1 = nullptr, hipEvent_t ev2 = nullptr, hipEvent_t ev3 = nullptr);
 void transpose_dense(hipStream_t s, const double *A, int m, int n, int lda, double *AT, int ldt);
 // primal pivot pipeline (gk_primal.hip); the plan reuses DualPlan's fields
 DualPlan primal_plan(const SpxDev &d, int nr_max, int pse);

@@ -25,6 +25,7 @@
 // parity); the order in which nodes are evaluated — and hence node counts —
 // differs from the reference's sequential walk (SURVEY.md §8(a) design note).
 #include "gk_device.h"
+#include "gk_hostprof.h"
 #include "../../include/glpk_mi355x.h"
 #include <algorithm>
 #include <cfloat>
@@ -59,6 +60,12 @@ struct NodeProb {
     const double *c;              // internal minimisation costs, [m+n] (0 for rows)
     const signed char *isint;     // [n]
     const double *rlb, *rub;      // [m] row bounds (the same at every node)
+    // a sparse A (nnz <= m n / 2; nnz = 0: dense) also by rows and by
+    // columns for the preprocessing: rptr[m+1] / rind / rval (column indices,
+    // ascending) and cptr[n+1] / cind / cval (row indices, ascending)
+    int nnz;
+    const int *rptr, *rind, *cptr, *cind;
+    const double *rval, *cval;
     double tol_int;
     int dth;                      // 1: choose the branching column by branch_drtom
 };
@@ -226,10 +233,15 @@ __device__ __forceinline__ double nb_value(int st, double lb, double ub)
 // objective, sum c_j x_j <= incumbent in minimisation form).
 // Returns 1 when the node is infeasible.  Called by the whole block.
 // ---------------------------------------------------------------------------
+struct NodeSp {                   // the sparse copies of A the kernel staged (null: dense A)
+    const int *rptr, *rind, *cptr, *cind;
+    const double *rval, *cval;
+};
+
 template <int ALDS>
 __device__ int node_preprocess(const NodeProb &P, const double *cl, const signed char *isl, const double *Ar,
-                               double objU, double *lb, double *ub, signed char *stat, signed char *chg, double *ri,
-                               int max_pass)
+                               const NodeSp &sp, double objU, double *lb, double *ub, signed char *stat,
+                               signed char *chg, double *ri, int max_pass)
 {
     const int m = P.m, n = P.n;
     // a_ij: the row-major LDS copy (ALDS) or the column-major matrix in HBM
@@ -247,16 +259,19 @@ __device__ int node_preprocess(const NodeProb &P, const double *cl, const signed
             double L = ri[6 * i + 4], U = ri[6 * i + 5];
             if (L == -DBL_MAX && U == DBL_MAX) continue;           // free row (wave-uniform)
             double smin = 0.0, smax = 0.0, cmin = 0.0, cmax = 0.0, jmin = 0.0, jmax = 0.0;
-            for (int j = lane; j < n; j += 64) {
-                const double a = (i == 0) ? cl[m + j] : aij(i - 1, j);
-                if (a == 0.0) continue;
+            auto term = [&](int j, double a) {
+                if (a == 0.0) return;
                 const double l = lb[m + j], u = ub[m + j];
                 const double lo = a > 0.0 ? l : u, hi = a > 0.0 ? u : l;
-                if ((a > 0.0 && l == -DBL_MAX) || (a < 0.0 && u == DBL_MAX)) { cmin += 1.0; jmin = j + 1; }
+                if ((a > 0.0 && l == -DBL_MAX) || (a < 0.0 && u == DBL_MAX)) { cmin += 1.0; jmin = fmax(jmin, j + 1); }
                 else smin += a * lo;
-                if ((a > 0.0 && u == DBL_MAX) || (a < 0.0 && l == -DBL_MAX)) { cmax += 1.0; jmax = j + 1; }
+                if ((a > 0.0 && u == DBL_MAX) || (a < 0.0 && l == -DBL_MAX)) { cmax += 1.0; jmax = fmax(jmax, j + 1); }
                 else smax += a * hi;
-            }
+            };
+            if (i > 0 && sp.rptr)
+                for (int t = sp.rptr[i - 1] + lane; t < sp.rptr[i]; t += 64) term(sp.rind[t], sp.rval[t]);
+            else
+                for (int j = lane; j < n; j += 64) term(j, (i == 0) ? cl[m + j] : aij(i - 1, j));
             smin = wsum(smin); smax = wsum(smax);
             cmin = wsum(cmin); cmax = wsum(cmax);
             jmin = wmax(jmin); jmax = wmax(jmax);
@@ -282,10 +297,13 @@ __device__ int node_preprocess(const NodeProb &P, const double *cl, const signed
             const double l0 = lb[m + j], u0 = ub[m + j];
             const bool flag = isl[j] != 0;
             double lj = l0, uj = u0;
-            for (int i = 0; i <= m && !bad; ++i) {
+            // rows in order: the objective, then the rows of column j
+            const int t0 = sp.cptr ? sp.cptr[j] : 0, t1 = sp.cptr ? sp.cptr[j + 1] : m;
+            for (int t = t0 - 1; t < t1 && !bad; ++t) {
+                const int i = (t < t0) ? 0 : (sp.cptr ? sp.cind[t] + 1 : t + 1);
                 const double L = ri[6 * i + 4], U = ri[6 * i + 5];
                 if (L == -DBL_MAX && U == DBL_MAX) continue;
-                const double a = (i == 0) ? cl[m + j] : aij(i - 1, j);
+                const double a = (t < t0) ? cl[m + j] : (sp.cptr ? sp.cval[t] : aij(i - 1, j));
                 if (a == 0.0) continue;
                 const double fmin = ri[6 * i + 0], fmax = ri[6 * i + 1];
                 const int jn = (int)ri[6 * i + 2], jx = (int)ri[6 * i + 3];
@@ -394,10 +412,13 @@ __global__ void __launch_bounds__(256) k_node_lp(NodeProb P, NodeIO io)
     double *cl = rinfo + 6 * (m + 1);         // N: the costs
     double *dzt = cl + N;                     // 4 m: branching degradations of the candidates
     double *Ar = dzt + 4 * m;                 // ALDS: A row-major (m x n)
-    int *head = (int *)(Ar + (ALDS ? (size_t)m * n : 0));
+    const int nzl = ALDS ? P.nnz : 0;         // sparse copies staged in LDS
+    double *rv = Ar + (ALDS ? (size_t)m * n : 0), *cv = rv + nzl;
+    int *head = (int *)(cv + nzl);
     int *rowof = head + m;                    // N: row of a basic variable
     int *cand = rowof + N;                    // m: fractional basic integer columns
-    signed char *stat = (signed char *)(cand + m);
+    int *rp = cand + m, *ri_ = rp + (nzl ? m + 1 : 0), *cp = ri_ + nzl, *ci = cp + (nzl ? n + 1 : 0);
+    signed char *stat = (signed char *)(ci + nzl);
     signed char *chg = stat + N;              // n
     signed char *isl = chg + n;               // n: integer flags
     // the problem's costs, integer flags and (ALDS) matrix staged in LDS:
@@ -409,6 +430,18 @@ __global__ void __launch_bounds__(256) k_node_lp(NodeProb P, NodeIO io)
             const int j = e / m, i = e - j * m;
             Ar[(size_t)i * n + j] = P.A[e];
         }
+    NodeSp sp{nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
+    if (P.nnz > 0) {
+        if (nzl) {
+            for (int t = threadIdx.x; t < nzl; t += blockDim.x) {
+                rv[t] = P.rval[t]; cv[t] = P.cval[t];
+                ri_[t] = P.rind[t]; ci[t] = P.cind[t];
+            }
+            for (int i = threadIdx.x; i <= m; i += blockDim.x) rp[i] = P.rptr[i];
+            for (int j = threadIdx.x; j <= n; j += blockDim.x) cp[j] = P.cptr[j];
+            sp = NodeSp{rp, ri_, cp, ci, rv, cv};
+        } else sp = NodeSp{P.rptr, P.rind, P.cptr, P.cind, P.rval, P.cval};
+    }
     double *gbnd = io.bnd + (size_t)b * 2 * n, *gdz = io.dzb + (size_t)b * 2 * n;
     const double *tin = io.tab_in ? io.tab_in[b] : nullptr;
     const int brj = io.br_j ? io.br_j[b] : -1;
@@ -460,7 +493,7 @@ __global__ void __launch_bounds__(256) k_node_lp(NodeProb P, NodeIO io)
     };
     NODE_STAMP(5);
     const int max_pass = io.pp_pass[b];
-    if (max_pass > 0 && node_preprocess<ALDS>(P, cl, isl, Ar, io.obj_bound, lb, ub, stat, chg, rinfo, max_pass)) {
+    if (max_pass > 0 && node_preprocess<ALDS>(P, cl, isl, Ar, sp, io.obj_bound, lb, ub, stat, chg, rinfo, max_pass)) {
         put_bounds();
         if (threadIdx.x == 0) { io.status[b] = NODE_PPINF; io.pivots[b] = 0; io.jj[b] = 0; io.obj[b] = 0.0; }
         NODE_STAMP(7);
@@ -991,21 +1024,22 @@ __global__ void __launch_bounds__(256) k_node_lp(NodeProb P, NodeIO io)
 #undef NODE_STAMP
 }
 
-// the node kernel's work area (alds: with the row-major copy of A)
-size_t node_lp_lds(int m, int n, int alds = 0)
+// the node kernel's work area (alds: with the row-major copy of A and, for
+// a sparse A, its copies by rows and columns)
+size_t node_lp_lds(int m, int n, int alds = 0, int nnz = 0)
 {
-    const size_t N = (size_t)m + n;
+    const size_t N = (size_t)m + n, z = alds ? (size_t)nnz : 0;
     return sizeof(double) * ((size_t)m * (2 * m + n) + 5 * N + 5 * (size_t)m + 6 * ((size_t)m + 1) +
-                             (alds ? (size_t)m * n : 0)) +
-           sizeof(int) * (2 * (size_t)m + N) + N + 2 * (size_t)n + 16;
+                             (alds ? (size_t)m * n : 0) + 2 * z) +
+           sizeof(int) * (2 * (size_t)m + N + (z ? (size_t)m + n + 2 + 2 * z : 0)) + N + 2 * (size_t)n + 16;
 }
 
 constexpr size_t NODE_LDS_MAX = 64 * 1024;
 
 void launch_node_lp(hipStream_t s, const NodeProb &P, const NodeIO &io, int nb)
 {
-    if (node_lp_lds(P.m, P.n, 1) <= NODE_LDS_MAX)
-        hipLaunchKernelGGL((k_node_lp<0, 1>), dim3(nb), dim3(256), node_lp_lds(P.m, P.n, 1), s, P, io);
+    if (node_lp_lds(P.m, P.n, 1, P.nnz) <= NODE_LDS_MAX)
+        hipLaunchKernelGGL((k_node_lp<0, 1>), dim3(nb), dim3(256), node_lp_lds(P.m, P.n, 1, P.nnz), s, P, io);
     else if (node_lp_lds(P.m, P.n) <= NODE_LDS_MAX)
         hipLaunchKernelGGL((k_node_lp<0, 0>), dim3(nb), dim3(256), node_lp_lds(P.m, P.n), s, P, io);
     else hipLaunchKernelGGL((k_node_lp<1, 0>), dim3(nb), dim3(256), 0, s, P, io);
@@ -1118,6 +1152,7 @@ struct NodeMeta {
     bool inl = true;              // the pool slot holds the node's bounds and statuses;
                                   // false: the kernel builds them from the record tab
     int br_dir = 0;               // 0: the down branch (ub = floor), 1: up (lb = ceil)
+    int arr = -1;                 // inline nodes: the slot of their arrays in NodePool::bnd / st
     int level = 0;
     int br_var = -1;              // column the parent branched on (0-based); -1: root
     double br_val = 0.0;          // its value in the parent's LP solution (ios_pcost_update)
@@ -1144,38 +1179,72 @@ struct NodeWorse {                // heap order: a is selected after b
     }
 };
 
-// slots of 2 n doubles (lb | ub of the structurals), m + n statuses and the
-// parent information, recycled through a free list
+// node slots (the parent information), recycled through a free list, and —
+// only for the nodes that need them on the host (inline: the root, nodes
+// received from another rank, children whose parent has no record) — array
+// slots of 2 n doubles (lb | ub of the structurals) and m + n statuses.  The
+// storage is kept by the context from one search to the next (take / give)
 struct NodePool {
     int n = 0, N = 0;
     TabStore *tabs = nullptr;
     std::vector<double> bnd;
     std::vector<signed char> st;
     std::vector<NodeMeta> meta;
-    std::vector<int> freel;
+    std::vector<int> freel, afree;
+    int narr = 0;
     int alloc()
     {
+        int sl;
         if (!freel.empty()) {
-            const int sl = freel.back();
+            sl = freel.back();
             freel.pop_back();
-            return sl;
+            meta[sl] = NodeMeta{};
+        } else {
+            sl = (int)meta.size();
+            meta.emplace_back();
         }
-        const int sl = (int)meta.size();
-        bnd.resize(bnd.size() + 2 * (size_t)n);
-        st.resize(st.size() + (size_t)N);
-        meta.emplace_back();
         return sl;
+    }
+    // the node's bound and status arrays (inline nodes); called on the
+    // search's own thread (the storage may grow), before any worker fills them
+    void need_arrays(int sl)
+    {
+        NodeMeta &mt = meta[sl];
+        if (mt.arr >= 0) return;
+        if (!afree.empty()) {
+            mt.arr = afree.back();
+            afree.pop_back();
+            return;
+        }
+        mt.arr = narr++;
+        if ((size_t)narr * 2 * n > bnd.size()) {
+            bnd.resize(std::max<size_t>((size_t)narr * 2 * n, 2 * bnd.size()));
+            st.resize(std::max<size_t>((size_t)narr * N, 2 * st.size()));
+        }
     }
     void release(int sl)
     {
         if (tabs) tabs->dec(meta[sl].tab);
         meta[sl].tab = -1;
         meta[sl].inl = true;
+        if (meta[sl].arr >= 0) afree.push_back(meta[sl].arr);
+        meta[sl].arr = -1;
         freel.push_back(sl);
     }
-    double *lb(int sl) { return bnd.data() + (size_t)sl * 2 * n; }
-    double *ub(int sl) { return bnd.data() + (size_t)sl * 2 * n + n; }
-    signed char *stat(int sl) { return st.data() + (size_t)sl * N; }
+    double *lb(int sl) { return bnd.data() + (size_t)meta[sl].arr * 2 * n; }
+    double *ub(int sl) { return bnd.data() + (size_t)meta[sl].arr * 2 * n + n; }
+    signed char *stat(int sl) { return st.data() + (size_t)meta[sl].arr * N; }
+    // a new search: every slot free, the storage's capacity kept
+    void reset(int n_, int N_)
+    {
+        if (n_ != n || N_ != N) { bnd.clear(); st.clear(); }
+        n = n_;
+        N = N_;
+        meta.clear();
+        freel.clear();
+        afree.clear();
+        narr = 0;
+    }
 };
 
 // check_integrality's results from the node kernel (NodeIO nfrac ...)
@@ -1328,9 +1397,11 @@ static int bnb_threads()
 
 struct MipCache {
     BatchBuf bufs[2];
-    DevArr<double> dA, dc, dscratch, drb;
+    DevArr<double> dA, dc, dscratch, drb, dspv;
+    DevArr<int> dspi;
     DevArr<signed char> dint;
     TabStore tabs;
+    NodePool pool;                           // the node storage, kept between searches
     HostWorkers *workers = nullptr;          // made with the first search that has work for them
     ~MipCache() { delete workers; }
 };
@@ -1633,6 +1704,7 @@ struct MipSolver {
                 cm.inl = false;
             } else {
                 cm.inl = true;
+                pool.need_arrays(sl);
                 const FillJob fj{sl, j, kase, beta, bl, bu, so};
                 if (defer) defer->push_back(fj);
                 else fill_child(fj);
@@ -1779,8 +1851,9 @@ struct MipSolver {
         (void)hipMemcpy(rec.data(), pool.tabs->ptr(mt.tab) + node_rec_bounds(m, n), bytes, hipMemcpyDeviceToHost);
         std::vector<signed char> so(N);
         std::memcpy(so.data(), rec.data() + 2 * n, N);
+        pool.need_arrays(sl);
         fill_child(FillJob{sl, mt.br_var, mt.br_dir, mt.br_val, rec.data(), rec.data() + n, so.data()});
-        mt.inl = true;
+        pool.meta[sl].inl = true;
     }
 
     void parked_done(int pid)
@@ -1953,6 +2026,7 @@ static void get_desc(MipSolver &S, const char *p)
 {
     const double *d = (const double *)p;
     const int sl = S.pool.alloc();
+    S.pool.need_arrays(sl);
     NodeMeta &mt = S.pool.meta[sl];
     mt.tab = -1;                          // the sender's tableau stays on its GPU
     mt.br_val = d[1]; mt.up_lpobj = d[2]; mt.up_bound = d[3]; mt.up_ii = d[4];
@@ -2104,6 +2178,7 @@ extern "C" int gk_ios_driver_sharded_inc(gk_ctx *ctx, gk_mip *mip, const gk_iocp
     if (hipSetDevice(gk_ctx_device(ctx)) != hipSuccess) { set_err("gk_ios_driver: hipSetDevice failed"); return GK_EABI; }
     hipStream_t s = gk_ctx_stream(ctx);
     const auto t0 = std::chrono::steady_clock::now();
+    HostProf host_prof_;                                  // GK_HOST_PROF (diagnostics)
     MipSolver S;
     S.ctx = ctx; S.s = s; S.mip = mip; S.parm = parm;
     S.m = m; S.n = n; S.N = m + n;
@@ -2172,9 +2247,56 @@ extern "C" int gk_ios_driver_sharded_inc(gk_ctx *ctx, gk_mip *mip, const gk_iocp
     NodeProb &P = S.P;
     P.m = m; P.n = n; P.ld = S.N; P.A = Cc.dA.p; P.c = Cc.dc.p; P.isint = Cc.dint.p; P.tol_int = parm->tol_int;
     P.rlb = Cc.drb.p; P.rub = Cc.drb.p + m;
+    // a sparse A by rows and by columns for the node preprocessing
+    P.nnz = 0;
+    P.rptr = P.rind = P.cptr = P.cind = nullptr;
+    P.rval = P.cval = nullptr;
+    {
+        size_t nz = 0;
+        for (double v : S.A) nz += v != 0.0;
+        if (nz > 0 && 2 * nz <= (size_t)m * n) {
+            std::vector<int> rptr(m + 1, 0), cptr(n + 1, 0), rind(nz), cind(nz);
+            std::vector<double> rval(nz), cval(nz);
+            for (int j = 0; j < n; j++)
+                for (int i = 0; i < m; i++)
+                    if (S.A[(size_t)j * m + i] != 0.0) { rptr[i + 1]++; cptr[j + 1]++; }
+            for (int i = 0; i < m; i++) rptr[i + 1] += rptr[i];
+            for (int j = 0; j < n; j++) cptr[j + 1] += cptr[j];
+            std::vector<int> rfill(rptr.begin(), rptr.end() - 1);
+            size_t t = 0;
+            for (int j = 0; j < n; j++)
+                for (int i = 0; i < m; i++) {
+                    const double v = S.A[(size_t)j * m + i];
+                    if (v == 0.0) continue;
+                    cind[t] = i; cval[t] = v; t++;
+                    rind[rfill[i]] = j; rval[rfill[i]] = v; rfill[i]++;
+                }
+            Cc.dspi.ensure((size_t)m + n + 2 + 2 * nz);
+            Cc.dspv.ensure(2 * nz);
+            if (Cc.dspi.p && Cc.dspv.p) {
+                int *pi = Cc.dspi.p;
+                double *pv = Cc.dspv.p;
+                (void)hipMemcpy(pi, rptr.data(), (m + 1) * sizeof(int), hipMemcpyHostToDevice);
+                (void)hipMemcpy(pi + m + 1, cptr.data(), (n + 1) * sizeof(int), hipMemcpyHostToDevice);
+                (void)hipMemcpy(pi + m + n + 2, rind.data(), nz * sizeof(int), hipMemcpyHostToDevice);
+                (void)hipMemcpy(pi + m + n + 2 + nz, cind.data(), nz * sizeof(int), hipMemcpyHostToDevice);
+                (void)hipMemcpy(pv, rval.data(), nz * sizeof(double), hipMemcpyHostToDevice);
+                (void)hipMemcpy(pv + nz, cval.data(), nz * sizeof(double), hipMemcpyHostToDevice);
+                P.nnz = (int)nz;
+                P.rptr = pi; P.cptr = pi + m + 1; P.rind = pi + m + n + 2; P.cind = pi + m + n + 2 + nz;
+                P.rval = pv; P.cval = pv + nz;
+            }
+        }
+    }
     P.dth = (parm->br_tech == 4) ? 1 : 0;
     NodePool &pool = S.pool;
-    pool.n = n; pool.N = S.N;
+    // the node storage of the previous search on this context (capacity kept)
+    std::swap(S.pool, Cc.pool);
+    struct PoolBack {
+        NodePool &a, &b;
+        ~PoolBack() { std::swap(a, b); }
+    } pool_back{S.pool, Cc.pool};
+    pool.reset(n, S.N);
     // warm start store (GK_BNB_WARM=0: every node inverts its basis;
     // GK_BNB_TAB_MB: its size limit)
     const size_t tab_cap = [] {
@@ -2188,12 +2310,12 @@ extern "C" int gk_ios_driver_sharded_inc(gk_ctx *ctx, gk_mip *mip, const gk_iocp
     // root node: the optimal basis of the initial LP relaxation
     {
         const int sl = pool.alloc();
+        pool.need_arrays(sl);
         std::memcpy(pool.lb(sl), S.clb.data(), n * sizeof(double));
         std::memcpy(pool.ub(sl), S.cub.data(), n * sizeof(double));
         signed char *st = pool.stat(sl);
         for (int i = 0; i < m; i++) st[i] = L.row_stat[i + 1];
         for (int j = 0; j < n; j++) st[m + j] = L.col_stat[j + 1];
-        pool.meta[sl] = NodeMeta{};
         S.push_open(NodeRec{-INF, 0.0, 0.0, S.seq++, sl});
     }
     // ios_preprocess_node passes of a node (glpios03.js:643-656)

@@ -211,7 +211,8 @@ typedef struct {
                                    own last block exit (a profiler's per-dispatch bracket) */
     long long trow_dev_launches_r;
     double upd_dev_ms;          /* (profiling) device span of the k_dual_update launches: entry of
-                                   block 0 to the last block exit, summed */
+                                   block 0 to the last block exit, summed (gk_bfd_profile 3 / 4); with
+                                   gk_bfd_profile 1 / 2 the kernels' start / stop events instead */
     long long upd_dev_launches;
     double upd_bytes;           /* (profiling) algorithmic bytes of every k_dual_update launch */
     int resident;               /* 1: the call found its working set resident (no re-upload) */

@@ -2,7 +2,7 @@
 node records on and off (GK_BNB_WARM is read per search)
 (set GK_BNB_LOG=1 for the driver's own time split on stderr; its
 time stamps cost ~0.1 us a node, so time without it).  Usage:
-    python tools/bnb_time.py [--log=N] [reps] [names...]"""
+    python tools/bnb_time.py [--log=N] [--hostprof=US] [reps] [names...]"""
 import json
 import os
 import sys
@@ -13,6 +13,9 @@ sys.path.insert(0, ROOT)
 for a in list(sys.argv[1:]):
     if a.startswith("--log="):                  # GK_BNB_LOG level (read once per process)
         os.environ["GK_BNB_LOG"] = a[6:]
+        sys.argv.remove(a)
+    elif a.startswith("--hostprof="):           # GK_HOST_PROF sampling interval (us)
+        os.environ["GK_HOST_PROF"] = a[11:]
         sys.argv.remove(a)
 
 import torch  # noqa: F401,E402  (one HIP runtime: torch first)
