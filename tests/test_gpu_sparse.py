@@ -85,6 +85,28 @@ def test_gpu_sparse_blocks_match_oracle(gpu_ctx, sparse_on, oracle, blocks, link
           f"({P.it_cnt / st.seconds_total:.0f} pivots/s), refactor {st.seconds_reinvert:.2f} s")
 
 
+SPARSE_FIXTURES = [pytest.param(p, id=os.path.basename(p)[len("sparse_oracle_"):-5])
+                   for p in golden_files("sparse_oracle_")]
+
+
+@pytest.mark.parametrize("path", SPARSE_FIXTURES)
+def test_gpu_sparse_large_matches_oracle_fixture(gpu_ctx, sparse_on, path):
+    """Sparse LPs the oracle needs minutes to hours for, solved once in the
+    build container by tests/golden/gen_sparse_oracle.py (the C restatement
+    of the reference's dual simplex): return code and objective (≤ 1e-9) of
+    the fixture, KKT-certified.  blocks_200x100x200+20 (m = 20,020, n =
+    40,000): the oracle took 89,265 iterations in 275 s."""
+    d = load_golden(path)
+    prob = (problems.gen_blocks(*d["args"]) if d["kind"] == "blocks" else problems.gen_c2s(*d["args"]))
+    assert (prob.m, prob.n, len(prob.A_val)) == (d["m"], d["n"], d["nnz"])
+    P = gk.GkProblem(gpu_ctx, prob)
+    assert gk.glp_simplex(P, gk.SMCP(meth=gk.GLP_DUAL, msg_lev=gk.GLP_MSG_ERR)) == d["ret"]
+    assert abs(P.obj_val - d["obj"]) <= 1e-9 * max(1.0, abs(d["obj"])), (P.obj_val, d["obj"])
+    sparse_kkt(P, prob)
+    st = P.stats()
+    print(f"{d['problem']}: {P.it_cnt} pivots (oracle {d['it_cnt']}), {st.seconds_total:.1f} s")
+
+
 def test_gpu_sparse_c2s_full_primal(gpu_ctx, sparse_on):
     """C2s, whole primal solve on the sparse factor: the reference's primal
     objective 357.82820943518863, KKT-certified."""

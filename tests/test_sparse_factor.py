@@ -7,6 +7,7 @@ in the order the device runs them (gk_sp_selftest), against numpy on bases of
 singular and permuted cases.  Tolerance: 1e-9 relative to the solution's
 largest entry (the elimination order differs from numpy's LAPACK LU)."""
 import ctypes as C
+import os
 
 import numpy as np
 import pytest
@@ -134,3 +135,20 @@ def test_sparse_factor_block_angular():
     rows = [i for i in range(m) if i not in used]
     B = np.concatenate([B, np.eye(m)[:, rows]], axis=1)
     check(B)
+
+
+def test_sparse_oracle_fixtures_regenerate_their_problems():
+    """The large sparse oracle fixtures (tests/golden/sparse_oracle_*.json,
+    written by gen_sparse_oracle.py) name problems the generators still
+    produce: the same size and number of nonzeros, and a finite objective."""
+    import glob
+    import json
+    import math
+    from glpk_js_amd import problems
+    paths = sorted(glob.glob(os.path.join(os.path.dirname(__file__), "golden", "sparse_oracle_*.json")))
+    assert paths
+    for p in paths:
+        d = json.load(open(p))
+        prob = problems.gen_blocks(*d["args"]) if d["kind"] == "blocks" else problems.gen_c2s(*d["args"])
+        assert (prob.m, prob.n, len(prob.A_val)) == (d["m"], d["n"], d["nnz"]), p
+        assert d["ret"] == 0 and math.isfinite(d["obj"])
