@@ -828,10 +828,19 @@ struct Spx {
         pin_off = 0;
     }
 
+    // GK_CALL_LOG: the host timeline of one call (label, seconds), printed
+    // at its end — where the host time between the device's work goes
+    std::vector<std::pair<const char *, double>> marks;
+    void mark(const char *what)
+    {
+        static const bool on = std::getenv("GK_CALL_LOG") != nullptr;
+        if (on) marks.emplace_back(what, now_s());
+    }
     // bring the host mirrors of the pivot-updated arrays up to date
     void pull()
     {
         if (!head_stale && !vec_stale) return;
+        mark("pull");
         // head | bind | stat | bbar | cbar (| coef) lie contiguous in the
         // arena (engine_alloc): one copy into the pinned staging buffer
         const char *lo = (const char *)E->head.p;
@@ -858,6 +867,7 @@ struct Spx {
         }
         sync();
         head_stale = vec_stale = false;
+        mark("pull done");
     }
     void push_bounds()
     {
@@ -923,6 +933,7 @@ struct Spx {
     void eval_cbar()
     {
         if (cbar_ok) { evals_skipped++; return; }
+        mark("eval_cbar");
         const double t0 = now_s();
         struct T { gk_bfd *f; double t0; ~T() { f->stats.seconds_eval += now_s() - t0; } } tt{f, t0};
         SpxDev d = dev();
@@ -957,6 +968,7 @@ struct Spx {
         down(cbar, E->cbar, n);
         sync();
         cbar_ok = true;
+        mark("eval_cbar done");
     }
 
     // eval_beta (glpspx01.js:473): h = -N xN; beta = inv(B) h, refined once
@@ -964,6 +976,7 @@ struct Spx {
     void eval_bbar()
     {
         if (bbar_ok) { evals_skipped++; return; }
+        mark("eval_bbar");
         const double t0 = now_s();
         struct T { gk_bfd *f; double t0; ~T() { f->stats.seconds_eval += now_s() - t0; } } tt{f, t0};
         if (next_aux_take()) {
@@ -976,6 +989,7 @@ struct Spx {
         down(bbar, E->bbar, m);
         sync();
         bbar_ok = true;
+        mark("eval_bbar done");
     }
     // h = -N xN over the statuses and bounds of d; beta = inv(B) h, refined once
     void eval_bbar_into(const SpxDev &d, double *beta)
@@ -1323,6 +1337,7 @@ struct Spx {
     }
     void store_sol(int p_stat, int d_stat, int ray)         // glpspx01.js:1591
     {
+        mark("store_sol");
         pull();
         lp->valid = 1;
         f->valid = 1;
@@ -1753,6 +1768,7 @@ void Spx::init()
 
 int Spx::batch(int K, int rigorous)
 {
+    mark("batch");
     const double t0 = now_s();
     struct T { gk_bfd *f; double t0; ~T() { f->stats.seconds_batches += now_s() - t0; } } tt{f, t0};
     hs.stop = ST_RUN;
@@ -1823,7 +1839,9 @@ int Spx::batch(int K, int rigorous)
         for (int t = 0; t < K; t++) primal_iteration(s, d, pse, rigorous);
         lists_stale = true;                   // the single-workgroup kernels do not maintain rlist
     }
+    mark("batch launched");
     pull_state();
+    mark("batch done");
     f->stats.batches++;
     f->stats.pivots += hs.npiv;
     f->stats.bytes_pivots = hs.bytes;
@@ -2071,8 +2089,10 @@ int Spx::run_dual()
                     if (cbar_st != 1) cbar_st = 0;
                     continue;
                 }
+                mark("it_lim");
                 display(1);
                 report_msg(it_hit ? GK_MSG_ITLIM : GK_MSG_TMLIM, 3);
+                mark("reported");
                 int d_stat;
                 const int ph = phase;
                 if (phase == 1) {
@@ -2085,7 +2105,9 @@ int Spx::run_dual()
                 store_sol(3, d_stat, 0);
                 if (ph == 1) {
                     phase = 1;                     // the phase the next call resumes in
+                    mark("next_aux");
                     next_aux_launch();
+                    mark("next_aux launched");
                 }
                 return it_hit ? 8 : 9;
             }
@@ -2707,14 +2729,27 @@ static int spx_entry(gk_ctx *ctx, gk_lp *lp, gk_bfd *f, const gk_smcp *parm, int
         }
         Spx S;
         S.ctx = ctx; S.f = f; S.E = f->eng; S.lp = lp; S.parm = parm; S.dual = dual;
+        S.mark("entry");
         S.init();
+        S.mark("init done");
         lp->valid = 0;
         int ret = dual ? S.run_dual() : S.run_primal();
+        S.mark("run done");
         f->upd_cnt = S.hs.upd_cnt;
         f->stats.evals_skipped = S.evals_skipped;
         if (ret == 0 || (ret >= 6 && ret <= 9)) S.save_resident();
         S.swap_spare();
+        S.mark("exit");
         f->stats.seconds_total = now_s() - t0;
+        if (!S.marks.empty()) {
+            std::string line = "[gk call]";
+            char buf[64];
+            for (auto &mk : S.marks) {
+                std::snprintf(buf, sizeof buf, " %s %.1f", mk.first, 1e6 * (mk.second - S.marks[0].second));
+                line += buf;
+            }
+            fprintf(stderr, "%s\n", line.c_str());
+        }
         return ret;
     } catch (const AbiError &e) {
         g_err = e.msg;

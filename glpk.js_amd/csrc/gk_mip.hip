@@ -1726,6 +1726,88 @@ struct MipSolver {
         }
     }
 
+    // node_done split for the batch's workers: everything that does not
+    // depend on the search state (the rounded local bound, the branching
+    // column and direction from the kernel's candidates, the children's
+    // rounded bounds) is planned in parallel; node_done_planned then takes
+    // the decisions in entry order exactly as node_done does (the same
+    // hopeful tests against the same incumbent, the same allocations and
+    // queue pushes).  For a kernel-solved node whose children get records,
+    // with any branching rule but pseudocosts
+    struct Plan {
+        double bound, beta, ii, dz[2], cb[2];
+        int j, next, nfrac;
+    };
+    std::vector<Plan> plans;                  // per batch entry
+    std::vector<char> planned;
+    void plan_node(Plan &pl, const NodeRec &nd, double z, const double *x, const double *dzb, int kjj, int knext,
+                   const KInt &ki) const
+    {
+        pl.bound = std::max(nd.bound, round_bound(z));
+        pl.nfrac = ki.nfrac;
+        pl.ii = ki.ii;
+        if (pl.nfrac == 0) return;
+        int j, next;
+        switch (parm->br_tech) {
+        case 1: j = ki.jf; next = next_of(x[m + j]); break;
+        case 2: j = ki.jl; next = next_of(x[m + j]); break;
+        case 3: j = ki.jm; next = ki.nm; break;
+        default:
+            if (kjj > 0) { j = kjj - 1; next = knext; }
+            else { j = ki.jm; next = ki.nm; }
+            break;
+        }
+        pl.j = j;
+        pl.next = next;
+        pl.beta = x[m + j];
+        for (int kase = 0; kase < 2; kase++) {
+            pl.dz[kase] = dzb[2 * j + kase];
+            pl.cb[kase] = pl.dz[kase] == DBL_MAX ? DBL_MAX : std::max(pl.bound, round_bound(z + pl.dz[kase]));
+        }
+    }
+    void node_done_planned(const NodeRec &nd, double z, const double *x, const Plan &pl)
+    {
+        const NodeMeta &mt0 = pool.meta[nd.slot];
+        if (!hopeful(pl.bound)) return;
+        if (pl.nfrac == 0) {
+            if (!have || z < best) new_incumbent(z, x);
+            return;
+        }
+        const int level = mt0.level;
+        if (level == 0 && !root_seen) {
+            root_seen = true;
+            root_bound = pl.bound;
+            root_ii = pl.ii;
+        }
+        const int first = pl.next < 0 ? 0 : 1;
+        bool dived = false;
+        for (int r = 0; r < 2; r++) {
+            const int kase = (r == 0) ? first : 1 - first;
+            if (pl.dz[kase] == DBL_MAX) continue;     // that branch has no feasible point
+            if (!hopeful(pl.cb[kase])) continue;
+            const int sl = pool.alloc();               // (may move pool.meta: mt0 is not used below)
+            NodeMeta &cm = pool.meta[sl];
+            cm.tab = cur_tab;
+            cm.br_dir = kase;
+            pool.tabs->inc(cur_tab);
+            cm.inl = false;
+            cm.level = level + 1;
+            cm.br_var = pl.j;
+            cm.br_val = pl.beta;
+            cm.up_lpobj = z;
+            cm.up_bound = pl.bound;
+            cm.up_ii = pl.ii;
+            NodeRec c{pl.cb[kase], 0.0, 0.0, seq++, sl};
+            if (!dived) {
+                set_keys(c);
+                next_dive.push_back(c);
+                dived = true;
+            } else
+                push_open(c);
+            created++;
+        }
+    }
+
     // the result of one node LP (kernel or fallback): incumbent, pruning,
     // branching (ios_driver's "analyze" part, glpios03.js:670-905)
     // returns true when the node is parked (its pool slot stays in use)
@@ -2500,9 +2582,21 @@ extern "C" int gk_ios_driver_sharded_inc(gk_ctx *ctx, gk_mip *mip, const gk_iocp
             double *bl = S.eb.data() + (size_t)b * 2 * n, *bu = bl + n;
             for (int j = 0; j < n; j++) { bl[j] = bb[2 * j]; bu[j] = bb[2 * j + 1]; }
         };
-        if (par) W->run(nb, 16, prep);
+        // the search-state-free part of node_done, planned on the workers
+        S.plans.resize(nb);
+        S.planned.assign(nb, 0);
+        auto plan = [&](int b) {
+            const Entry &e = bf.ents[b];
+            if (e.kind != 0) return;
+            prep(b);
+            if (hstat[b] != NODE_OPT || e.tab_out < 0 || pch) return;
+            const KInt ki{hnf[b], hjf[b], hjl[b], hjm[b], hnm[b], hii[b]};
+            S.plan_node(S.plans[b], e.nd, hobj[b], hx + (size_t)b * S.N, hdz + (size_t)b * 2 * n, hjj[b], hnext[b], ki);
+            S.planned[b] = 1;
+        };
+        if (par) W->run(nb, 16, plan);
         else
-            for (int b = 0; b < nb; b++) prep(b);
+            for (int b = 0; b < nb; b++) plan(b);
         // (2) in entry order (the search's decisions): incumbent, pruning,
         // branching; a child's bound and status arrays are only recorded
         S.jobs.clear();
@@ -2533,9 +2627,13 @@ extern "C" int gk_ios_driver_sharded_inc(gk_ctx *ctx, gk_mip *mip, const gk_iocp
             if (st == NODE_OPT) {
                 const auto tn0 = bnb_log ? std::chrono::steady_clock::now() : std::chrono::steady_clock::time_point{};
                 S.cur_tab = e.tab_out;
-                const KInt ki{hnf[b], hjf[b], hjl[b], hjm[b], hnm[b], hii[b]};
-                S.node_done(nd, hobj[b], x, hso + (size_t)b * S.N, fbl, fbu, hdz + (size_t)b * 2 * n, hjj[b], hnext[b],
-                            true, nullptr, -1, 0.0, pch ? nullptr : &ki);
+                if (S.planned[b])
+                    S.node_done_planned(nd, hobj[b], x, S.plans[b]);
+                else {
+                    const KInt ki{hnf[b], hjf[b], hjl[b], hjm[b], hnm[b], hii[b]};
+                    S.node_done(nd, hobj[b], x, hso + (size_t)b * S.N, fbl, fbu, hdz + (size_t)b * 2 * n, hjj[b],
+                                hnext[b], true, nullptr, -1, 0.0, pch ? nullptr : &ki);
+                }
                 S.cur_tab = -1;
                 if (bnb_log) t_nd += secs(tn0);
             } else if ((st == NODE_FAIL || st == NODE_ITLIM) && !S.err) {

@@ -14,12 +14,13 @@
 #   apitrace         rocprofv3 HIP API + kernel + copy traces (CSV) of a short bench
 #   ktrace           rocprofv3 kernel trace of the bench's timed region: stats
 #                    and the idle gaps between consecutive kernels
-#   py:SCRIPT,ARGS   python3 -u SCRIPT ARGS (tools/…; commas for spaces)
+#   py:SCRIPT,ARGS   python3 -u SCRIPT ARGS (tools/…; commas for spaces) -> SCRIPT.<k>.log / .err
 set -e
 NAME=$1; shift
 O="$PWD/gpurun_out/$NAME"
 mkdir -p "$O"
 export TMPDIR=/tmp
+k=0
 PYT="python -u -m pytest -x -v --timeout 300 --timeout-method thread -m gpu"
 for step in "$@"; do
     case "$step" in
@@ -42,8 +43,8 @@ for step in "$@"; do
                     --gpus 1 --steps 20 --warmup 5 --no-cpu --no-extra > "$O/kt_bench.json" 2> "$O/kt.err";
                 python3 tools/prof_stats.py /tmp/kt_$NAME/run_results.db --marked --csv "$O/kt_stats.csv" \
                     --gaps "$O/kt_gaps.txt" > "$O/kt_grid.txt" ;;
-        py:*) a=$(echo "${step#py:}" | tr ',' ' '); s=$(basename ${a%% *} .py);
-              timeout -k 10 900 python3 -u $a > "$O/$s.log" 2> "$O/$s.err" ;;
+        py:*) a=$(echo "${step#py:}" | tr ',' ' '); s=$(basename ${a%% *} .py); k=$((k + 1));
+              timeout -k 10 900 python3 -u $a > "$O/$s.$k.log" 2> "$O/$s.$k.err" ;;
         *) echo "unknown step $step"; exit 2 ;;
     esac
     echo "step $step ok"
