@@ -168,30 +168,27 @@ __device__ int block_ratio(double t, double a, int idx, double *shk, double *sha
     return r;
 }
 
-// block_argmax's order within one wave (every lane returns the choice)
+// block_argmax's order within one wave (every lane returns the choice): the
+// largest key, then the lowest index — three DPP reductions instead of a
+// six-round permute butterfly
 __device__ int wave_argmax(double key, int idx)
 {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-        const double k2 = __shfl_xor(key, o);
-        const int i2 = __shfl_xor(idx, o);
-        if (i2 >= 0 && (idx < 0 || k2 > key || (k2 == key && i2 < idx))) { key = k2; idx = i2; }
-    }
-    return idx;
+    const double km = wmax(idx >= 0 ? key : -DBL_MAX);
+    const unsigned c = (idx >= 0 && key == km) ? (unsigned)idx : 0x7fffffffu;
+    const unsigned r = __ockl_wfred_min_u32(c);
+    return r == 0x7fffffffu ? -1 : (int)r;
 }
 
-// block_ratio's order within one wave (every lane returns the choice)
+// block_ratio's order within one wave (every lane returns the choice): the
+// smallest ratio, then the largest |alfa|, then the lowest index
 __device__ int wave_ratio(double t, double a, int idx)
 {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-        const double t2 = __shfl_xor(t, o), a2 = __shfl_xor(a, o);
-        const int i2 = __shfl_xor(idx, o);
-        if (i2 >= 0 && (idx < 0 || t2 < t || (t2 == t && (a2 > a || (a2 == a && i2 < idx))))) {
-            t = t2; a = a2; idx = i2;
-        }
-    }
-    return idx;
+    const double tm = -wmax(idx >= 0 ? -t : -DBL_MAX);
+    const bool at = idx >= 0 && t == tm;
+    const double am = wmax(at ? a : -1.0);
+    const unsigned c = (at && a == am) ? (unsigned)idx : 0x7fffffffu;
+    const unsigned r = __ockl_wfred_min_u32(c);
+    return r == 0x7fffffffu ? -1 : (int)r;
 }
 
 __device__ double block_sum256(double v, double *sh)
@@ -252,9 +249,16 @@ __device__ int node_preprocess(const NodeProb &P, const double *cl, const signed
         ri[6 * i + 5] = (i == 0) ? objU : ub[i - 1];
     }
     __syncthreads();
+    // "some column changed efficiently" of each pass, in three rotating
+    // flags: the pass's last barrier publishes it together with the
+    // infeasibility test; thread 0 clears the flag of the next pass, which no
+    // thread still reads (a slow thread may still read the previous pass's)
+    __shared__ int sh_eff[3];
+    if (threadIdx.x == 0) sh_eff[0] = 0;
     for (int pass = 0; pass < max_pass; ++pass) {
         // ---- rows: activity bounds, infeasibility, redundant row bounds
         int bad = 0;
+        if (threadIdx.x == 0) sh_eff[(pass + 1) % 3] = 0;
         for (int i = w; i <= m; i += nw) {
             double L = ri[6 * i + 4], U = ri[6 * i + 5];
             if (L == -DBL_MAX && U == DBL_MAX) continue;           // free row (wave-uniform)
@@ -361,8 +365,9 @@ __device__ int node_preprocess(const NodeProb &P, const double *cl, const signed
             lb[m + j] = lj;
             ub[m + j] = uj;
         }
+        if (eff) sh_eff[pass % 3] = 1;
         if (__syncthreads_or(bad)) return 1;
-        if (!__syncthreads_or(eff)) break;
+        if (!sh_eff[pass % 3]) break;
     }
     // relaxed bounds of the basic rows (non-active: dual feasibility kept);
     // statuses of non-basic columns whose type changed (glp_set_col_bnds):
@@ -506,23 +511,23 @@ __global__ void __launch_bounds__(256) k_node_lp(NodeProb P, NodeIO io)
     // only moves non-basic columns) and it is young enough
     int age = 0;
     if (tin) {
+        // the parent's header staged in LDS (cand: m ints, free until the
+        // branching), then checked by every thread at once
+        int *hin = cand;
         age = (int)tin[0];
-        if (threadIdx.x == 0) {
-            int ok = age < io.tab_age_max;
-            for (int i = 0; i < m && ok; ++i) {
-                const int k = (int)tin[1 + i];
-                if (k < 0 || k >= N || stat[k] != BS) ok = 0;
-            }
-            if (ok) {
-                int nbs = 0;
-                for (int k = 0; k < N; ++k) nbs += stat[k] == BS;
-                ok = nbs == m;
-            }
-            sh_flag = ok ? 2 : 0;
+        for (int i = threadIdx.x; i < m; i += blockDim.x) hin[i] = (int)tin[1 + i];
+        __syncthreads();
+        int bad = age >= io.tab_age_max;
+        for (int i = threadIdx.x; i < m; i += blockDim.x) {
+            const int k = hin[i];
+            if (k < 0 || k >= N || stat[k] != BS) bad = 1;
         }
-        __syncthreads();
-        if (sh_flag != 2) { tin = nullptr; age = 0; }
-        __syncthreads();
+        int nbs = 0;
+        for (int k0 = 0; k0 < N; k0 += blockDim.x) {
+            const int k = k0 + threadIdx.x;
+            nbs += __syncthreads_count(k < N && stat[k] == BS);
+        }
+        if (__syncthreads_or(bad || nbs != m)) { tin = nullptr; age = 0; }
     }
 #define T_(i, j) M[(size_t)(i) * W + m + (j)]
     if (tin) {
@@ -530,10 +535,11 @@ __global__ void __launch_bounds__(256) k_node_lp(NodeProb P, NodeIO io)
         // (the dual ratio tests break ties by row: a warm-started node then
         // takes the pivots a cold-started one would)
         int *rk = (int *)fcol;
+        const int *hin = cand;
         for (int i = threadIdx.x; i < m; i += blockDim.x) {
-            const int k = (int)tin[1 + i];
+            const int k = hin[i];
             int r = 0;
-            for (int i2 = 0; i2 < m; ++i2) r += (int)tin[1 + i2] < k;
+            for (int i2 = 0; i2 < m; ++i2) r += hin[i2] < k;
             rk[i] = r;
             head[r] = k;
         }
@@ -613,12 +619,14 @@ __global__ void __launch_bounds__(256) k_node_lp(NodeProb P, NodeIO io)
     // T[i][j] = M[i][m + j]  (row length W kept; T(i, j) = M[i*W + m + j])
     }
     NODE_STAMP(2);
-    // d = c - c_B' T
+    // d = c - c_B' T  (c_B staged in fcol)
+    for (int i = threadIdx.x; i < m; i += blockDim.x) fcol[i] = cl[head[i]];
+    __syncthreads();
     for (int k = threadIdx.x; k < N; k += blockDim.x) {
         if (stat[k] == BS) { d[k] = 0.0; continue; }
         double s = cl[k];
         for (int i = 0; i < m; ++i) {
-            const double cb = cl[head[i]];
+            const double cb = fcol[i];
             if (cb != 0.0) s -= cb * T_(i, k);
         }
         d[k] = s;
@@ -749,12 +757,17 @@ __global__ void __launch_bounds__(256) k_node_lp(NodeProb P, NodeIO io)
             const double a = T_(p, k);
             if (a != 0.0) d[k] -= dq * a;
         }
-        // T update outside row p and column q: row i -= T[i,q] (row p / apq)
-        for (int e = threadIdx.x; e < m * N; e += blockDim.x) {
-            const int i = e / N, k = e - i * N;
-            if (i == p || k == q) continue;
-            const double f = T_(i, q);
-            if (f != 0.0) T_(i, k) -= f * (T_(p, k) / apq);
+        // T update outside row p and column q: row i -= T[i,q] (row p / apq),
+        // a wave per row, lanes along it
+        {
+            const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, nwv = blockDim.x >> 6;
+            for (int i = wv; i < m; i += nwv) {
+                if (i == p) continue;
+                const double f = T_(i, q);
+                if (f == 0.0) continue;
+                for (int k = lane; k < N; k += 64)
+                    if (k != q) T_(i, k) -= f * (T_(p, k) / apq);
+            }
         }
         __syncthreads();
         for (int k = threadIdx.x; k < N; k += blockDim.x) T_(p, k) /= apq;
