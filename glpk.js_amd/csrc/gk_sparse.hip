@@ -171,8 +171,20 @@ struct Buckets {
 
 }  // namespace
 
+// the elimination's working storage, kept from one factorization to the next
+// (the per-row / per-column vectors keep their capacity: a factorization of
+// m = 100k allocated some 10^6 small vectors otherwise)
+struct SpLUWork {
+    std::vector<std::vector<int>> rc, cr;
+    std::vector<std::vector<double>> rv;
+    std::vector<double> rmax;
+    std::vector<char> ract, cact;
+    std::vector<int> wpos, rows;
+    Buckets R, C;
+};
+
 // returns 0, or 1 when B0 is singular (BFD_ESING); rank in *rank
-static int sp_lu_factor(SpLU &F, int m, const std::vector<int> &cptr, const std::vector<int> &crow,
+static int sp_lu_factor(SpLU &F, SpLUWork &Wk, int m, const std::vector<int> &cptr, const std::vector<int> &crow,
                  const std::vector<double> &cval, double piv_tol, int piv_lim, double eps_tol, int *rank)
 {
     F.m = m;
@@ -182,9 +194,11 @@ static int sp_lu_factor(SpLU &F, int m, const std::vector<int> &cptr, const std:
     F.Lrow.clear(); F.Lval.clear();
     F.Uptr.assign(1, 0);
     F.Ucol.clear(); F.Uval.clear(); F.Udiag.assign(m, 0.0);
-    std::vector<std::vector<int>> rc(m);           // row i: columns
-    std::vector<std::vector<double>> rv(m);        // row i: values
-    std::vector<std::vector<int>> cr(m);           // column j: rows
+    std::vector<std::vector<int>> &rc = Wk.rc;     // row i: columns
+    std::vector<std::vector<double>> &rv = Wk.rv;  // row i: values
+    std::vector<std::vector<int>> &cr = Wk.cr;     // column j: rows
+    if ((int)rc.size() < m) { rc.resize(m); rv.resize(m); cr.resize(m); }
+    for (int i = 0; i < m; i++) { rc[i].clear(); rv[i].clear(); cr[i].clear(); }
     for (int j = 0; j < m; j++)
         for (int t = cptr[j]; t < cptr[j + 1]; t++) {
             const int i = crow[t];
@@ -193,13 +207,16 @@ static int sp_lu_factor(SpLU &F, int m, const std::vector<int> &cptr, const std:
             rv[i].push_back(cval[t]);
             cr[j].push_back(i);
         }
-    Buckets R, C;
+    Buckets &R = Wk.R, &C = Wk.C;
     R.init(m, m);
     C.init(m, m);
     for (int i = 0; i < m; i++) R.add(i, (int)rc[i].size());
     for (int j = 0; j < m; j++) C.add(j, (int)cr[j].size());
-    std::vector<char> ract(m, 1), cact(m, 1);
-    std::vector<double> rmax(m, -1.0);             // cached max |a_ij| of row i (< 0: stale)
+    std::vector<char> &ract = Wk.ract, &cact = Wk.cact;
+    ract.assign(m, 1);
+    cact.assign(m, 1);
+    std::vector<double> &rmax = Wk.rmax;           // cached max |a_ij| of row i (< 0: stale)
+    rmax.assign(m, -1.0);
     auto row_max = [&](int i) {
         if (rmax[i] < 0.0) {
             double b = 0.0;
@@ -214,7 +231,8 @@ static int sp_lu_factor(SpLU &F, int m, const std::vector<int> &cptr, const std:
             if (r[t] == j) return (int)t;
         return -1;
     };
-    std::vector<int> wpos(m, -1);                  // column -> index in the row being updated
+    std::vector<int> &wpos = Wk.wpos;              // column -> index in the row being updated
+    wpos.assign(m, -1);
     int k;
     for (k = 0; k < m; k++) {
         int pi = -1, pj = -1;
@@ -293,7 +311,8 @@ static int sp_lu_factor(SpLU &F, int m, const std::vector<int> &cptr, const std:
         R.del(pi);
         ract[pi] = 0;
         // eliminate the pivot column from the other rows
-        std::vector<int> rows = cr[pj];
+        std::vector<int> &rows = Wk.rows;
+        rows.assign(cr[pj].begin(), cr[pj].end());
         C.del(pj);
         cact[pj] = 0;
         cr[pj].clear();
@@ -351,118 +370,130 @@ static int sp_lu_factor(SpLU &F, int m, const std::vector<int> &cptr, const std:
 //   FTRAN U   x[c_k] = (z[r_k] - sum_{(j, u) in U_k} u x[j]) / u_kk
 //   BTRAN U'  w[k]   = (e[c_k] - sum_{t<k, c_k in U_t} u w[t]) / u_kk
 //   BTRAN L'  y[r_k] = w[k] - sum_{(i, l) in L_k} l y[i]
-static void sp_build_tri(SpTriHost &T, int m, int nsteps, const std::vector<int> &iin, const std::vector<int> &iout,
-                         const std::vector<double> &diag, const std::vector<std::vector<std::pair<int, double>>> &deps,
-                         const std::vector<int> &dep_step, bool reverse)
+// the dependences of every step of a sweep, in CSR form (ptr over the
+// steps; idx / val the entries read and their coefficients; step the step
+// that produces each entry read)
+struct SpDeps {
+    std::vector<int> ptr, idx, step;
+    std::vector<double> val;
+};
+
+static void sp_build_tri(SpTriHost &T, int nsteps, const std::vector<int> &iin, const std::vector<int> &iout,
+                         const std::vector<double> &diag, const SpDeps &D, bool reverse)
 {
-    // dep_step[e] of deps[k][e]: the step producing the entry read (level order)
-    std::vector<int> lev(nsteps, 0);
+    thread_local std::vector<int> lev, cnt, pos, order;
+    lev.assign(nsteps, 0);
     int nlev = 0;
-    std::vector<size_t> off(nsteps + 1, 0);
-    for (int k = 0; k < nsteps; k++) off[k + 1] = off[k] + deps[k].size();
     for (int s = 0; s < nsteps; s++) {
         const int k = reverse ? nsteps - 1 - s : s;
         int l = 0;
-        for (size_t e = 0; e < deps[k].size(); e++) l = std::max(l, lev[dep_step[off[k] + e]] + 1);
+        for (int e = D.ptr[k]; e < D.ptr[k + 1]; e++) l = std::max(l, lev[D.step[e]] + 1);
         lev[k] = l;
         nlev = std::max(nlev, l + 1);
     }
-    std::vector<int> cnt(nlev + 1, 0);
+    cnt.assign(nlev + 1, 0);
     for (int k = 0; k < nsteps; k++) cnt[lev[k] + 1]++;
     for (int l = 0; l < nlev; l++) cnt[l + 1] += cnt[l];
     T.lvptr.assign(cnt.begin(), cnt.end());
     T.nlev = nlev;
-    std::vector<int> pos(nlev, 0);
-    std::vector<int> order(nsteps);
+    pos.assign(nlev, 0);
+    order.resize(nsteps);
     for (int k = 0; k < nsteps; k++) order[T.lvptr[lev[k]] + pos[lev[k]]++] = k;
     // within a level: the steps of at most TRI_LONG entries (one thread each)
     // first, the longer ones (one wave each) after them
     T.lvlong.assign(nlev, 0);
     for (int l = 0; l < nlev; l++) {
         auto b = order.begin() + T.lvptr[l], e = order.begin() + T.lvptr[l + 1];
-        auto mid = std::stable_partition(b, e, [&](int k) { return deps[k].size() <= (size_t)TRI_LONG; });
+        auto mid = std::stable_partition(b, e, [&](int k) { return D.ptr[k + 1] - D.ptr[k] <= TRI_LONG; });
         T.lvlong[l] = (int)(mid - order.begin());
     }
     T.iin.resize(nsteps); T.iout.resize(nsteps); T.diag.resize(nsteps); T.eptr.assign(nsteps + 1, 0);
-    T.eidx.clear(); T.eval.clear();
+    T.eidx.resize(D.idx.size()); T.eval.resize(D.idx.size());
+    int ne = 0;
     for (int s = 0; s < nsteps; s++) {
         const int k = order[s];
         T.iin[s] = iin[k];
         T.iout[s] = iout[k];
         T.diag[s] = diag[k];
-        for (const auto &pr : deps[k]) {
-            T.eidx.push_back(pr.first);
-            T.eval.push_back(pr.second);
+        for (int e = D.ptr[k]; e < D.ptr[k + 1]; e++) {
+            T.eidx[ne] = D.idx[e];
+            T.eval[ne] = D.val[e];
+            ne++;
         }
-        T.eptr[s + 1] = (int)T.eidx.size();
+        T.eptr[s + 1] = ne;
     }
-    (void)m;
+}
+
+// the transposed dependences (a step reads the entries other steps' lists
+// point at): for src = 0..m-1 in order, every entry e of src's list goes to
+// the step key(e), recording (idx(src), val[e], src) — the same order as
+// pushing them one by one
+template <typename Key, typename Idx>
+static void sp_deps_transposed(SpDeps &D, int m, const std::vector<int> &sptr, const std::vector<double> &sval,
+                               Key key, Idx idx)
+{
+    D.ptr.assign(m + 1, 0);
+    for (int t = 0; t < m; t++)
+        for (int e = sptr[t]; e < sptr[t + 1]; e++) D.ptr[key(e) + 1]++;
+    for (int k = 0; k < m; k++) D.ptr[k + 1] += D.ptr[k];
+    const size_t nz = (size_t)D.ptr[m];
+    D.idx.resize(nz); D.val.resize(nz); D.step.resize(nz);
+    thread_local std::vector<int> fill;
+    fill.assign(D.ptr.begin(), D.ptr.end() - 1);
+    for (int t = 0; t < m; t++)
+        for (int e = sptr[t]; e < sptr[t + 1]; e++) {
+            const int k = key(e), f = fill[k]++;
+            D.idx[f] = idx(t);
+            D.val[f] = sval[e];
+            D.step[f] = t;
+        }
+}
+
+// the direct dependences (a step reads its own list)
+template <typename Idx, typename Step>
+static void sp_deps_direct(SpDeps &D, int m, const std::vector<int> &sptr, const std::vector<int> &sidx,
+                           const std::vector<double> &sval, Idx idx, Step step)
+{
+    D.ptr.assign(sptr.begin(), sptr.begin() + m + 1);
+    const size_t nz = (size_t)sptr[m];
+    D.idx.resize(nz); D.val.resize(nz); D.step.resize(nz);
+    for (size_t e = 0; e < nz; e++) {
+        D.idx[e] = idx(sidx[e]);
+        D.val[e] = sval[e];
+        D.step[e] = step(sidx[e]);
+    }
 }
 
 static void sp_build_solves(const SpLU &F, SpSolves &S)
 {
     const int m = F.m;
-    std::vector<int> step_of_row(m), step_of_pos(m);
+    thread_local std::vector<int> step_of_row, step_of_pos, in, out;
+    thread_local std::vector<double> ones;
+    thread_local SpDeps D;
+    step_of_row.resize(m);
+    step_of_pos.resize(m);
     for (int k = 0; k < m; k++) { step_of_row[F.pr[k]] = k; step_of_pos[F.pc[k]] = k; }
-    std::vector<double> ones(m, 1.0);
+    ones.assign(m, 1.0);
+    in.resize(m);
+    out.resize(m);
     // FTRAN L: deps of step k' = (z index r_t, l) for every eta t < k' holding row r_k'
-    {
-        std::vector<std::vector<std::pair<int, double>>> deps(m);
-        std::vector<std::vector<int>> dst(m);
-        for (int t = 0; t < m; t++)
-            for (int e = F.Lptr[t]; e < F.Lptr[t + 1]; e++) {
-                const int k = step_of_row[F.Lrow[e]];
-                deps[k].push_back({F.pr[t], F.Lval[e]});
-                dst[k].push_back(t);
-            }
-        std::vector<int> ds;
-        for (int k = 0; k < m; k++) ds.insert(ds.end(), dst[k].begin(), dst[k].end());
-        std::vector<int> io(m);
-        for (int k = 0; k < m; k++) io[k] = F.pr[k];
-        sp_build_tri(S.fl, m, m, io, io, ones, deps, ds, false);
-    }
+    sp_deps_transposed(D, m, F.Lptr, F.Lval, [&](int e) { return step_of_row[F.Lrow[e]]; },
+                       [&](int t) { return F.pr[t]; });
+    for (int k = 0; k < m; k++) in[k] = F.pr[k];
+    sp_build_tri(S.fl, m, in, in, ones, D, false);
     // FTRAN U: deps of step k = (x index c_t, u) for the entries of U row k
-    {
-        std::vector<std::vector<std::pair<int, double>>> deps(m);
-        std::vector<int> ds;
-        for (int k = 0; k < m; k++)
-            for (int e = F.Uptr[k]; e < F.Uptr[k + 1]; e++) {
-                deps[k].push_back({F.Ucol[e], F.Uval[e]});
-                ds.push_back(step_of_pos[F.Ucol[e]]);
-            }
-        std::vector<int> in(m), out(m);
-        for (int k = 0; k < m; k++) { in[k] = F.pr[k]; out[k] = F.pc[k]; }
-        sp_build_tri(S.fu, m, m, in, out, F.Udiag, deps, ds, true);
-    }
+    sp_deps_direct(D, m, F.Uptr, F.Ucol, F.Uval, [](int c) { return c; }, [&](int c) { return step_of_pos[c]; });
+    for (int k = 0; k < m; k++) { in[k] = F.pr[k]; out[k] = F.pc[k]; }
+    sp_build_tri(S.fu, m, in, out, F.Udiag, D, true);
     // BTRAN U': deps of step k = (w index t, u) for every U row t < k holding column c_k
-    {
-        std::vector<std::vector<std::pair<int, double>>> deps(m);
-        std::vector<std::vector<int>> dst(m);
-        for (int t = 0; t < m; t++)
-            for (int e = F.Uptr[t]; e < F.Uptr[t + 1]; e++) {
-                const int k = step_of_pos[F.Ucol[e]];
-                deps[k].push_back({t, F.Uval[e]});
-                dst[k].push_back(t);
-            }
-        std::vector<int> ds;
-        for (int k = 0; k < m; k++) ds.insert(ds.end(), dst[k].begin(), dst[k].end());
-        std::vector<int> in(m), out(m);
-        for (int k = 0; k < m; k++) { in[k] = F.pc[k]; out[k] = k; }
-        sp_build_tri(S.bu, m, m, in, out, F.Udiag, deps, ds, false);
-    }
+    sp_deps_transposed(D, m, F.Uptr, F.Uval, [&](int e) { return step_of_pos[F.Ucol[e]]; },
+                       [](int t) { return t; });
+    for (int k = 0; k < m; k++) { in[k] = F.pc[k]; out[k] = k; }
+    sp_build_tri(S.bu, m, in, out, F.Udiag, D, false);
     // BTRAN L': deps of step k = (y index i, l) for the entries of eta k
-    {
-        std::vector<std::vector<std::pair<int, double>>> deps(m);
-        std::vector<int> ds;
-        for (int k = 0; k < m; k++)
-            for (int e = F.Lptr[k]; e < F.Lptr[k + 1]; e++) {
-                deps[k].push_back({F.Lrow[e], F.Lval[e]});
-                ds.push_back(step_of_row[F.Lrow[e]]);
-            }
-        std::vector<int> in(m), out(m);
-        for (int k = 0; k < m; k++) { in[k] = k; out[k] = F.pr[k]; }
-        sp_build_tri(S.bl, m, m, in, out, ones, deps, ds, true);
-    }
+    sp_deps_direct(D, m, F.Lptr, F.Lrow, F.Lval, [](int i) { return i; }, [&](int i) { return step_of_row[i]; });
+    for (int k = 0; k < m; k++) { in[k] = k; out[k] = F.pr[k]; }
+    sp_build_tri(S.bl, m, in, out, ones, D, true);
 }
 
 // ---------------------------------------------------------------------------
@@ -922,13 +953,14 @@ int sp_factorize(SpFactor &F, hipStream_t s, int m, const int *head1, const int 
         }
         cptr[i] = (int)crow.size();
     }
-    SpLU lu;
+    thread_local SpLU lu;
+    thread_local SpLUWork wk;
     int rank = 0;
-    const int ret = sp_lu_factor(lu, m, cptr, crow, cval, piv_tol > 0.0 ? piv_tol : 0.1, piv_lim > 0 ? piv_lim : 4,
+    const int ret = sp_lu_factor(lu, wk, m, cptr, crow, cval, piv_tol > 0.0 ? piv_tol : 0.1, piv_lim > 0 ? piv_lim : 4,
                                  eps_tol > 0.0 ? eps_tol : 1e-15, &rank);
     F.t_lu = sp_now() - t0;
     if (ret) return 1;
-    SpSolves S;
+    thread_local SpSolves S;
     sp_build_solves(lu, S);
     F.nnz_l = (long long)lu.Lrow.size();
     F.nnz_u = (long long)lu.Ucol.size() + m;
@@ -1057,8 +1089,9 @@ extern "C" int gk_sp_selftest(int m, const int *ptr, const int *ind, const doubl
         cptr[j] = (int)crow.size();
     }
     SpLU lu;
+    SpLUWork wk;
     int rank = 0;
-    if (sp_lu_factor(lu, m, cptr, crow, cval, 0.1, 4, 1e-15, &rank)) return 1;
+    if (sp_lu_factor(lu, wk, m, cptr, crow, cval, 0.1, 4, 1e-15, &rank)) return 1;
     SpSolves S;
     sp_build_solves(lu, S);
     if (stats) {

@@ -15,6 +15,7 @@
 #   ktrace           rocprofv3 kernel trace of the bench's timed region: stats
 #                    and the idle gaps between consecutive kernels
 #   py:SCRIPT,ARGS   python3 -u SCRIPT ARGS (tools/…; commas for spaces) -> SCRIPT.<k>.log / .err
+#   pytSECS:SCRIPT,ARGS  the same under a limit of SECS seconds (default 900)
 set -e
 NAME=$1; shift
 O="$PWD/gpurun_out/$NAME"
@@ -45,6 +46,8 @@ for step in "$@"; do
                     --gaps "$O/kt_gaps.txt" > "$O/kt_grid.txt" ;;
         py:*) a=$(echo "${step#py:}" | tr ',' ' '); s=$(basename ${a%% *} .py); k=$((k + 1));
               timeout -k 10 900 python3 -u $a > "$O/$s.$k.log" 2> "$O/$s.$k.err" ;;
+        pyt*:*) lim=${step%%:*}; lim=${lim#pyt}; a=$(echo "${step#*:}" | tr ',' ' '); s=$(basename ${a%% *} .py);
+              k=$((k + 1)); timeout -k 10 "$lim" python3 -u $a > "$O/$s.$k.log" 2> "$O/$s.$k.err" ;;
         *) echo "unknown step $step"; exit 2 ;;
     esac
     echo "step $step ok"

@@ -3,7 +3,7 @@
 GPU: the block-angular generator (problems.gen_blocks) or C2s, whole dual
 solve, progress lines every out_frq pivots (stderr), then one JSON line with
 pivots/s, refactorization time, the factor's size and a KKT certificate.
-Usage: sparse_big.py [--sparse] blocks K [links] | c2s M N
+Usage: sparse_big.py [--sparse] blocks K [links [mb nb]] | c2s M N
 (--sparse: GK_SPARSE=1, the sparse factor also below m = 65536)"""
 import json
 import os
@@ -31,7 +31,9 @@ def main():
     if kind == "blocks":
         K = int(sys.argv[2])
         L = int(sys.argv[3]) if len(sys.argv) > 3 else max(5, K // 20)
-        prob = problems.gen_blocks(K, 100, 200, L)
+        mb = int(sys.argv[4]) if len(sys.argv) > 4 else 100
+        nb = int(sys.argv[5]) if len(sys.argv) > 5 else 200
+        prob = problems.gen_blocks(K, mb, nb, L)
     else:
         prob = problems.gen_c2s(int(sys.argv[2]), int(sys.argv[3]))
     t_gen = time.time() - t0
