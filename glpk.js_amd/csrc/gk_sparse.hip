@@ -31,6 +31,7 @@
 // statuses and KKT conditions are (tests/test_gpu_sparse.py).
 #include "gk_internal.h"
 #include "gk_device.h"
+#include "gk_hostprof.h"
 
 #include <algorithm>
 #include <chrono>
@@ -181,7 +182,13 @@ struct SpLUWork {
     std::vector<char> ract, cact;
     std::vector<int> wpos, rows;
     Buckets R, C;
+    std::vector<int> lid;                  // long rows: their slot in lmap (-1: short)
+    std::vector<std::vector<int>> lmap;    // per long row: column -> index in the row (-1: none)
 };
+
+// rows longer than this keep a dense position map (the linking rows of a
+// block-angular basis: every elimination that touches one would rescan it)
+constexpr int LU_LONG = 64;
 
 // returns 0, or 1 when B0 is singular (BFD_ESING); rank in *rank
 static int sp_lu_factor(SpLU &F, SpLUWork &Wk, int m, const std::vector<int> &cptr, const std::vector<int> &crow,
@@ -210,6 +217,32 @@ static int sp_lu_factor(SpLU &F, SpLUWork &Wk, int m, const std::vector<int> &cp
     Buckets &R = Wk.R, &C = Wk.C;
     R.init(m, m);
     C.init(m, m);
+    std::vector<int> &lid = Wk.lid;
+    std::vector<std::vector<int>> &lmap = Wk.lmap;
+    lid.assign(m, -1);
+    int nlong = 0;
+    auto make_long = [&](int i) {
+        if (lid[i] >= 0) return;
+        if (nlong == (int)lmap.size()) lmap.emplace_back();
+        std::vector<int> &mp = lmap[nlong];
+        if ((int)mp.size() != m) mp.assign(m, -1);          // (slots come back all -1)
+        lid[i] = nlong++;
+        for (size_t t = 0; t < rc[i].size(); t++) mp[rc[i][t]] = (int)t;
+    };
+    // swap-remove entry t of row i (the map follows)
+    auto row_remove = [&](int i, size_t t) {
+        const int j = rc[i][t];
+        const int last = rc[i].back();
+        rc[i][t] = last; rc[i].pop_back();
+        rv[i][t] = rv[i].back(); rv[i].pop_back();
+        if (lid[i] >= 0) {
+            std::vector<int> &mp = lmap[lid[i]];
+            mp[j] = -1;
+            if (t < rc[i].size()) mp[last] = (int)t;
+        }
+    };
+    for (int i = 0; i < m; i++)
+        if ((int)rc[i].size() > LU_LONG) make_long(i);
     for (int i = 0; i < m; i++) R.add(i, (int)rc[i].size());
     for (int j = 0; j < m; j++) C.add(j, (int)cr[j].size());
     std::vector<char> &ract = Wk.ract, &cact = Wk.cact;
@@ -226,6 +259,7 @@ static int sp_lu_factor(SpLU &F, SpLUWork &Wk, int m, const std::vector<int> &cp
         return rmax[i];
     };
     auto find_in_row = [&](int i, int j) {
+        if (lid[i] >= 0) return lmap[lid[i]][j];
         const std::vector<int> &r = rc[i];
         for (size_t t = 0; t < r.size(); t++)
             if (r[t] == j) return (int)t;
@@ -322,44 +356,81 @@ static int sp_lu_factor(SpLU &F, SpLUWork &Wk, int m, const std::vector<int> &cp
             F.Lrow.push_back(i);
             F.Lval.push_back(f);
             // remove a_{i,pj}
-            rc[i][ti] = rc[i].back(); rc[i].pop_back();
-            rv[i][ti] = rv[i].back(); rv[i].pop_back();
-            for (size_t t = 0; t < rc[i].size(); t++) wpos[rc[i][t]] = (int)t;
-            for (size_t t = 0; t < rc[pi].size(); t++) {
-                const int j = rc[pi][t];
-                if (j == pj) continue;
-                const double d = f * rv[pi][t];
-                if (wpos[j] >= 0) rv[i][wpos[j]] -= d;
-                else {
-                    wpos[j] = (int)rc[i].size();
-                    rc[i].push_back(j);
-                    rv[i].push_back(-d);
-                    cr[j].push_back(i);
-                    C.move(j, (int)cr[j].size());
+            row_remove(i, ti);
+            if (lid[i] >= 0) {
+                // a long row: its map finds the pivot row's columns; only the
+                // entries the update touched can have cancelled
+                std::vector<int> &mp = lmap[lid[i]];
+                for (size_t t = 0; t < rc[pi].size(); t++) {
+                    const int j = rc[pi][t];
+                    if (j == pj) continue;
+                    const double d = f * rv[pi][t];
+                    const int pos = mp[j];
+                    if (pos >= 0) rv[i][pos] -= d;
+                    else {
+                        mp[j] = (int)rc[i].size();
+                        rc[i].push_back(j);
+                        rv[i].push_back(-d);
+                        cr[j].push_back(i);
+                        C.move(j, (int)cr[j].size());
+                    }
                 }
-            }
-            // drop what cancelled (|a| < eps_tol)
-            for (size_t t = 0; t < rc[i].size();) {
-                if (std::fabs(rv[i][t]) < eps_tol) {
-                    const int j = rc[i][t];
+                for (size_t t = 0; t < rc[pi].size(); t++) {
+                    const int j = rc[pi][t];
+                    if (j == pj) continue;
+                    const int pos = mp[j];
+                    if (pos < 0 || std::fabs(rv[i][pos]) >= eps_tol) continue;
                     std::vector<int> &cj = cr[j];
                     for (size_t u = 0; u < cj.size(); u++)
                         if (cj[u] == i) { cj[u] = cj.back(); cj.pop_back(); break; }
                     C.move(j, (int)cj.size());
-                    wpos[j] = -1;
-                    rc[i][t] = rc[i].back(); rc[i].pop_back();
-                    rv[i][t] = rv[i].back(); rv[i].pop_back();
-                } else t++;
+                    row_remove(i, pos);
+                }
+            } else {
+                for (size_t t = 0; t < rc[i].size(); t++) wpos[rc[i][t]] = (int)t;
+                for (size_t t = 0; t < rc[pi].size(); t++) {
+                    const int j = rc[pi][t];
+                    if (j == pj) continue;
+                    const double d = f * rv[pi][t];
+                    if (wpos[j] >= 0) rv[i][wpos[j]] -= d;
+                    else {
+                        wpos[j] = (int)rc[i].size();
+                        rc[i].push_back(j);
+                        rv[i].push_back(-d);
+                        cr[j].push_back(i);
+                        C.move(j, (int)cr[j].size());
+                    }
+                }
+                // drop what cancelled (|a| < eps_tol)
+                for (size_t t = 0; t < rc[i].size();) {
+                    if (std::fabs(rv[i][t]) < eps_tol) {
+                        const int j = rc[i][t];
+                        std::vector<int> &cj = cr[j];
+                        for (size_t u = 0; u < cj.size(); u++)
+                            if (cj[u] == i) { cj[u] = cj.back(); cj.pop_back(); break; }
+                        C.move(j, (int)cj.size());
+                        wpos[j] = -1;
+                        rc[i][t] = rc[i].back(); rc[i].pop_back();
+                        rv[i][t] = rv[i].back(); rv[i].pop_back();
+                    } else t++;
+                }
+                for (int j : rc[i]) wpos[j] = -1;
+                if ((int)rc[i].size() > LU_LONG) make_long(i);
             }
-            for (int j : rc[i]) wpos[j] = -1;
             rmax[i] = -1.0;
             R.move(i, (int)rc[i].size());
         }
         F.Lptr.push_back((int)F.Lrow.size());
+        if (lid[pi] >= 0)
+            for (int j : rc[pi]) lmap[lid[pi]][j] = -1;      // the slot goes back all -1
         rc[pi].clear();
         rv[pi].clear();
     }
     *rank = k;
+    // (singular: rows left active keep entries in their maps)
+    for (int i = 0; i < m; i++)
+        if (lid[i] >= 0)
+            for (int j : rc[i]) lmap[lid[i]][j] = -1;
     if (k < m) return 1;
     return 0;
 }
@@ -1077,6 +1148,7 @@ extern "C" int gk_sp_selftest(int m, const int *ptr, const int *ind, const doubl
                               const double *e, double *x, double *y, long long *stats)
 {
     using namespace gk;
+    HostProf host_prof_;                      // GK_HOST_PROF (diagnostics)
     if (m < 1 || !ptr || !ind || !val) return -1;
     std::vector<int> cptr(m + 1, 0), crow;
     std::vector<double> cval;
