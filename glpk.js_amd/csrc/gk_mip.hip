@@ -1412,6 +1412,8 @@ struct MipCache {
     BatchBuf bufs[2];
     DevArr<double> dA, dc, dscratch, drb, dspv;
     DevArr<int> dspi;
+    std::vector<int> hspi;                   // host staging of the sparse copies (alive until the copies ran)
+    std::vector<double> hspv;
     DevArr<signed char> dint;
     TabStore tabs;
     NodePool pool;                           // the node storage, kept between searches
@@ -2371,12 +2373,15 @@ extern "C" int gk_ios_driver_sharded_inc(gk_ctx *ctx, gk_mip *mip, const gk_iocp
             if (Cc.dspi.p && Cc.dspv.p) {
                 int *pi = Cc.dspi.p;
                 double *pv = Cc.dspv.p;
-                (void)hipMemcpy(pi, rptr.data(), (m + 1) * sizeof(int), hipMemcpyHostToDevice);
-                (void)hipMemcpy(pi + m + 1, cptr.data(), (n + 1) * sizeof(int), hipMemcpyHostToDevice);
-                (void)hipMemcpy(pi + m + n + 2, rind.data(), nz * sizeof(int), hipMemcpyHostToDevice);
-                (void)hipMemcpy(pi + m + n + 2 + nz, cind.data(), nz * sizeof(int), hipMemcpyHostToDevice);
-                (void)hipMemcpy(pv, rval.data(), nz * sizeof(double), hipMemcpyHostToDevice);
-                (void)hipMemcpy(pv + nz, cval.data(), nz * sizeof(double), hipMemcpyHostToDevice);
+                // one copy each way, ordered on the search's stream before its first batch
+                Cc.hspi.assign(rptr.begin(), rptr.end());
+                Cc.hspi.insert(Cc.hspi.end(), cptr.begin(), cptr.end());
+                Cc.hspi.insert(Cc.hspi.end(), rind.begin(), rind.end());
+                Cc.hspi.insert(Cc.hspi.end(), cind.begin(), cind.end());
+                Cc.hspv.assign(rval.begin(), rval.end());
+                Cc.hspv.insert(Cc.hspv.end(), cval.begin(), cval.end());
+                (void)hipMemcpyAsync(pi, Cc.hspi.data(), Cc.hspi.size() * sizeof(int), hipMemcpyHostToDevice, s);
+                (void)hipMemcpyAsync(pv, Cc.hspv.data(), Cc.hspv.size() * sizeof(double), hipMemcpyHostToDevice, s);
                 P.nnz = (int)nz;
                 P.rptr = pi; P.cptr = pi + m + 1; P.rind = pi + m + n + 2; P.cind = pi + m + n + 2 + nz;
                 P.rval = pv; P.cval = pv + nz;
