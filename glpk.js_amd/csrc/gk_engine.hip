@@ -1746,9 +1746,18 @@ void Spx::init()
         upd_cap = nfs;
     if (f->sparse) {
         // the Schur-complement chain holds at most SP_KMAX updates
-        // (gk_sparse.hip); no lengthening past nfs_max
-        upd_cap = std::min(nfs, SP_KMAX);
-        lim = upd_cap;
+        // (gk_sparse.hip); under the default parameters it starts at
+        // min(SP_KMAX, m/4) and drift_adapt shortens it as for the dense
+        // inverse (the host L U costs ~0.1 s at m = 100,000: the interval sets
+        // the amortized refactorization cost per pivot)
+        if (f->parm_default) {
+            upd_cap = std::min(std::max(nfs, std::min(SP_KMAX, m / 4)), SP_KMAX);
+            if (f->upd_lim_adapt <= 0 || f->upd_lim_adapt > upd_cap) f->upd_lim_adapt = upd_cap;
+            lim = std::min(std::max(f->upd_lim_adapt, std::min(nfs, upd_cap)), upd_cap);
+        } else {
+            upd_cap = std::min(nfs, SP_KMAX);
+            lim = upd_cap;
+        }
     }
     upd_floor = std::min(nfs, upd_cap);
     hs.upd_lim = lim;

@@ -131,7 +131,7 @@ void scatter_pos(hipStream_t s, int m, int off, int cnt, const int *head, const 
 // ---- simplex pivot kernels --------------------------------------------------
 // ---- sparse basis factor (gk_sparse.hip): B0 = L U on the host, level-
 // scheduled sweeps on the device, Schur-complement updates (k <= SP_KMAX)
-constexpr int SP_KMAX = 128;
+constexpr int SP_KMAX = 256;
 struct SpFactor;
 SpFactor *sp_create();
 void sp_destroy(SpFactor *F);

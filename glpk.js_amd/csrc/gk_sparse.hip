@@ -777,17 +777,17 @@ __global__ void __launch_bounds__(256) k_sp_ftran_wood(SpDev sp, const DState *s
 __global__ void __launch_bounds__(256) k_sp_btran_part(SpDev sp, const double *e)
 {
     const int m = sp.m, k = *sp.w.k;
-    __shared__ double red[SP_KMAX][8];
+    __shared__ double red[SP_KMAX];
     const int lane = threadIdx.x & 31, grp = threadIdx.x >> 5;   // 8 groups of 32 threads
     const int i0 = blockIdx.x * 256;
     for (int t = grp; t < k; t += 8) {
         double a = 0.0;
         for (int i = i0 + lane; i < min(i0 + 256, m); i += 32) a += sp.w.Y[(size_t)i * SP_KMAX + t] * e[i];
         for (int o = 16; o > 0; o >>= 1) a += __shfl_xor(a, o, 32);
-        if (lane == 0) red[t][0] = a;
+        if (lane == 0) red[t] = a;
     }
     __syncthreads();
-    for (int t = threadIdx.x; t < k; t += blockDim.x) sp.w.tpart[(size_t)blockIdx.x * SP_KMAX + t] = red[t][0];
+    for (int t = threadIdx.x; t < k; t += blockDim.x) sp.w.tpart[(size_t)blockIdx.x * SP_KMAX + t] = red[t];
 }
 
 // BTRAN part 2 (one workgroup): e' = e - S inv(M)' (Y' e), then y = inv(B0)' e'
@@ -831,11 +831,10 @@ __global__ void __launch_bounds__(1024) k_sp_btran(SpDev sp, DState *st, const d
         sv[1][t] = a1;
     }
     __syncthreads();
-    if (threadIdx.x == 0)
-        for (int t = 0; t < k; t++) {                  // positions may repeat only in order
-            b0[sp.w.P[t]] -= sv[0][t];
-            if (NRHS == 2) b1[sp.w.P[t]] -= sv[1][t];
-        }
+    for (int t = threadIdx.x; t < k; t += blockDim.x) {   // P holds distinct positions (k_sp_update)
+        b0[sp.w.P[t]] -= sv[0][t];
+        if (NRHS == 2) b1[sp.w.P[t]] -= sv[1][t];
+    }
     __syncthreads();
     tri_sweep<NRHS>(sp.bu, b0, b1, w0, w1);
     tri_sweep<NRHS>(sp.bl, w0, w1, y, y1);
@@ -855,11 +854,10 @@ __global__ void __launch_bounds__(1024) k_sp_update(SpDev sp, DState *st)
     __shared__ int slot;
     __shared__ double c[SP_KMAX], r[SP_KMAX], ac[SP_KMAX], ra[SP_KMAX], col_old[SP_KMAX];
     __shared__ double sch;
-    if (threadIdx.x == 0) {
-        slot = -1;
-        for (int t = 0; t < k; t++)
-            if (sp.w.P[t] == p) slot = t;
-    }
+    if (threadIdx.x == 0) slot = -1;
+    __syncthreads();
+    for (int t = threadIdx.x; t < k; t += blockDim.x)
+        if (sp.w.P[t] == p) slot = t;                // at most one: positions are distinct
     __syncthreads();
     const int t0 = slot;
     double *Y = sp.w.Y, *Mi = sp.w.Minv;
