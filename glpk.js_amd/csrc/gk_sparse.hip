@@ -108,21 +108,34 @@ struct SpTriDevBufs {
 struct SpFactor {
     int m = -1;
     SpTriDevBufs fl, fu, bu, bl;
-    SBuf<double> Y, Minv, zq, tpart, bt, scr, scr2;
-    SBuf<int> P, hdr;                     // hdr: nlev of fl, fu, bu, bl; k (updates in the chain)
+    SBuf<double> Y, Minv, zq, tpart, bt, scr, scr2, hh;
+    SBuf<int> P, hdr;                     // hdr: nlev of fl, fu, bu, bl; k (updates in the chain); Y column of the last update
     long long nnz_l = 0, nnz_u = 0;
     int levels[4] = {0, 0, 0, 0};
+    int wide[4] = {0, 0, 0, 0};           // level 0 of fl / fu / bu / bl runs on the grid (k_sp_level0)
+    int w0blk[4] = {0, 0, 0, 0};          // its grid
     double t_lu = 0.0, t_total = 0.0;
     ~SpFactor()
     {
         fl.release(); fu.release(); bu.release(); bl.release();
         Y.release(); Minv.release(); zq.release(); tpart.release(); bt.release(); scr.release(); scr2.release();
+        hh.release();
         P.release();
         hdr.release();
     }
 };
 
 constexpr int TRI_LONG = 32;   // sweep steps with more entries run on a whole wave
+// a level 0 of at least this many steps runs on the grid (k_sp_level0):
+// below it the extra launch costs more than the workgroup's trips
+static int sp_wide_min()
+{
+    static const int w = [] {
+        const char *e = std::getenv("GK_SP_WIDE");
+        return e ? std::max(1, atoi(e)) : 8192;
+    }();
+    return w;
+}
 
 // ---------------------------------------------------------------------------
 // host: Markowitz LU with threshold pivoting
@@ -449,27 +462,39 @@ struct SpDeps {
     std::vector<double> val;
 };
 
+// inplace: the sweep writes the vector it reads (FTRAN L), so a step with
+// no entries, iin = iout and a unit diagonal leaves its entry as it is and is
+// dropped from the schedule (most steps of a slack-heavy basis: the
+// single-workgroup sweep no longer walks them)
 static void sp_build_tri(SpTriHost &T, int nsteps, const std::vector<int> &iin, const std::vector<int> &iout,
-                         const std::vector<double> &diag, const SpDeps &D, bool reverse)
+                         const std::vector<double> &diag, const SpDeps &D, bool reverse, bool inplace = false)
 {
     thread_local std::vector<int> lev, cnt, pos, order;
     lev.assign(nsteps, 0);
-    int nlev = 0;
+    int nlev = 0, nkeep = 0;
     for (int s = 0; s < nsteps; s++) {
         const int k = reverse ? nsteps - 1 - s : s;
+        if (inplace && D.ptr[k + 1] == D.ptr[k] && iin[k] == iout[k] && diag[k] == 1.0) {
+            lev[k] = -1;
+            continue;
+        }
         int l = 0;
         for (int e = D.ptr[k]; e < D.ptr[k + 1]; e++) l = std::max(l, lev[D.step[e]] + 1);
         lev[k] = l;
         nlev = std::max(nlev, l + 1);
+        nkeep++;
     }
     cnt.assign(nlev + 1, 0);
-    for (int k = 0; k < nsteps; k++) cnt[lev[k] + 1]++;
+    for (int k = 0; k < nsteps; k++)
+        if (lev[k] >= 0) cnt[lev[k] + 1]++;
     for (int l = 0; l < nlev; l++) cnt[l + 1] += cnt[l];
     T.lvptr.assign(cnt.begin(), cnt.end());
     T.nlev = nlev;
     pos.assign(nlev, 0);
-    order.resize(nsteps);
-    for (int k = 0; k < nsteps; k++) order[T.lvptr[lev[k]] + pos[lev[k]]++] = k;
+    order.resize(nkeep);
+    for (int k = 0; k < nsteps; k++)
+        if (lev[k] >= 0) order[T.lvptr[lev[k]] + pos[lev[k]]++] = k;
+    nsteps = nkeep;
     // within a level: the steps of at most TRI_LONG entries (one thread each)
     // first, the longer ones (one wave each) after them
     T.lvlong.assign(nlev, 0);
@@ -551,7 +576,7 @@ static void sp_build_solves(const SpLU &F, SpSolves &S)
     sp_deps_transposed(D, m, F.Lptr, F.Lval, [&](int e) { return step_of_row[F.Lrow[e]]; },
                        [&](int t) { return F.pr[t]; });
     for (int k = 0; k < m; k++) in[k] = F.pr[k];
-    sp_build_tri(S.fl, m, in, in, ones, D, false);
+    sp_build_tri(S.fl, m, in, in, ones, D, false, true);
     // FTRAN U: deps of step k = (x index c_t, u) for the entries of U row k
     sp_deps_direct(D, m, F.Uptr, F.Ucol, F.Uval, [](int c) { return c; }, [&](int c) { return step_of_pos[c]; });
     for (int k = 0; k < m; k++) { in[k] = F.pr[k]; out[k] = F.pc[k]; }
@@ -671,17 +696,19 @@ __device__ __forceinline__ void step_wave(const TriDev &t, const double *in0, co
     }
 }
 
+// levels l0 .. nlev-1 (l0 = 1: level 0 ran on the whole grid, k_sp_level0)
 template <int NRHS>
-__device__ void tri_sweep(const TriDev &t, const double *in0, const double *in1, double *out0, double *out1)
+__device__ void tri_sweep(const TriDev &t, const double *in0, const double *in1, double *out0, double *out1,
+                          int l0 = 0)
 {
     const int nlev = *t.nlev;
     const int T = blockDim.x;
     const int w = threadIdx.x >> 6, nw = blockDim.x >> 6;
-    if (nlev <= 0) return;
-    int lb = t.lvptr[0], le = t.lvptr[1], ls = t.lvlong[0];
+    if (nlev <= l0) return;
+    int lb = t.lvptr[l0], le = t.lvptr[l0 + 1], ls = t.lvlong[l0];
     StepPre<NRHS> cur;
     step_load<NRHS>(t, in0, in1, lb + (int)threadIdx.x, ls, cur);
-    for (int l = 0; l < nlev; l++) {
+    for (int l = l0; l < nlev; l++) {
         // the next level's bounds and this thread's first (short) step of it
         const int nb = le, ne = (l + 1 < nlev) ? t.lvptr[l + 2] : le, nls = (l + 1 < nlev) ? t.lvlong[l + 1] : le;
         StepPre<NRHS> nxt;
@@ -711,6 +738,8 @@ struct WoodDev {
     double *tpart;                                // Y' e partials of a general BTRAN (SP_KMAX per block)
     double *bt;                                   // BTRAN scratch (positions), FTRAN scratch z (2 x m)
     double *scr2;                                 // BTRAN step-space scratch (2 x m)
+    double *hh;                                   // inv(M) z[P] of the FTRAN (2 x SP_KMAX)
+    int *ycol;                                    // device word: Y column the last update wrote (-1: none)
 };
 
 struct SpDev {
@@ -719,20 +748,76 @@ struct SpDev {
     int m;
 };
 
-// FTRAN part 1 (one workgroup): z = inv(B0) [h, work]; L in place, U into
-// the scratch; the z of h is kept (zq) for the update of this pivot
+// gate of the pivot's kernels: 0 none, 1 the stop word, 2 stop or no
+// leaving row (the BTRAN of e_p)
+__device__ __forceinline__ bool sp_gated(const DState *st, int gate)
+{
+    return gate && (st->stop || (gate == 2 && st->p <= 0));
+}
+
+// level 0 of a sweep on the whole grid: its steps read no other step's
+// output, so a level of SP_WIDE or more steps (the slack part of the basis)
+// runs as a gather at HBM rate instead of m / 1024 dependent trips of the
+// single workgroup; the workgroup's sweep then starts at level 1
 template <int NRHS>
-__global__ void __launch_bounds__(1024) k_sp_ftran_lu(SpDev sp, const DState *st, double *h0, double *h1, int gated)
+__global__ void __launch_bounds__(256) k_sp_level0(TriDev t, const DState *st, int gate, const double *in0,
+                                                   const double *in1, double *out0, double *out1)
+{
+    if (sp_gated(st, gate)) return;
+    const int lb = t.lvptr[0], ls = t.lvlong[0], le = t.lvptr[1];
+    const int g = blockIdx.x * blockDim.x + threadIdx.x;
+    if (lb + g < ls) {
+        StepPre<NRHS> q;
+        step_load<NRHS>(t, in0, in1, lb + g, ls, q);
+        step_run<NRHS>(t, q, out0, out1);
+    }
+    const int gw = g >> 6, nw = (gridDim.x * blockDim.x) >> 6;
+    for (int s = ls + gw; s < le; s += nw) step_wave<NRHS>(t, in0, in1, s, out0, out1);
+}
+
+// FTRAN part 1 (one workgroup): z = inv(B0) [h, work]; L in place, U into
+// the scratch; the z of h is kept (zq) for the update of this pivot.
+// parts: bit 0 the L sweep (from level l0l), bit 1 the U sweep (from l0u)
+template <int NRHS>
+__global__ void __launch_bounds__(1024) k_sp_ftran_lu(SpDev sp, const DState *st, double *h0, double *h1, int gated,
+                                                      int parts, int l0l, int l0u)
 {
     if (gated && st->stop) return;
     const int m = sp.m;
-    tri_sweep<NRHS>(sp.fl, h0, h1, h0, h1);      // in place: z[r] (row space)
+    if (parts & 1) tri_sweep<NRHS>(sp.fl, h0, h1, h0, h1, l0l);      // in place: z[r] (row space)
     double *x0 = sp.w.bt, *x1 = sp.w.bt + m;
-    tri_sweep<NRHS>(sp.fu, h0, h1, x0, x1);      // positions
+    if (!(parts & 2)) return;
+    tri_sweep<NRHS>(sp.fu, h0, h1, x0, x1, l0u);                      // positions
+    // hh = inv(M) z[P] for k_sp_ftran_wood, once: one wave per row of
+    // inv(M), its lanes along the row (coalesced), fixed-order reduction
+    const int k = *sp.w.k;
+    if (k == 0) return;
+    __shared__ double g[2][SP_KMAX];
+    for (int t = threadIdx.x; t < k; t += blockDim.x) {
+        const int p = sp.w.P[t];
+        g[0][t] = x0[p];
+        if (NRHS == 2) g[1][t] = x1[p];
+    }
+    __syncthreads();
+    const int lane = threadIdx.x & 63;
+    for (int t = threadIdx.x >> 6; t < k; t += blockDim.x >> 6) {
+        const double *mr = sp.w.Minv + (size_t)t * SP_KMAX;
+        double a0 = 0.0, a1 = 0.0;
+        for (int u = lane; u < k; u += 64) {
+            a0 += mr[u] * g[0][u];
+            if (NRHS == 2) a1 += mr[u] * g[1][u];
+        }
+        a0 = wsum(a0);
+        if (NRHS == 2) a1 = wsum(a1);
+        if (lane == 0) {
+            sp.w.hh[t] = a0;
+            if (NRHS == 2) sp.w.hh[SP_KMAX + t] = a1;
+        }
+    }
 }
 
-// FTRAN part 2 (grid): x = z - Y inv(M) z[P] for each right-hand side; every
-// block forms inv(M) z[P] itself (k <= SP_KMAX: k^2 per block)
+// FTRAN part 2 (grid): x = z - Y inv(M) z[P] for each right-hand side
+// (inv(M) z[P] formed once by k_sp_ftran_lu's tail)
 template <int NRHS>
 __global__ void __launch_bounds__(256) k_sp_ftran_wood(SpDev sp, const DState *st, double *out0, double *out1,
                                                        int gated, int keep)
@@ -741,22 +826,10 @@ __global__ void __launch_bounds__(256) k_sp_ftran_wood(SpDev sp, const DState *s
     const int m = sp.m;
     const int k = *sp.w.k;
     const double *z0 = sp.w.bt, *z1 = sp.w.bt + m;
-    __shared__ double g[2][SP_KMAX], hh[2][SP_KMAX];
+    __shared__ double hh[2][SP_KMAX];
     for (int t = threadIdx.x; t < k; t += blockDim.x) {
-        const int p = sp.w.P[t];
-        g[0][t] = z0[p];
-        if (NRHS == 2) g[1][t] = z1[p];
-    }
-    __syncthreads();
-    for (int t = threadIdx.x; t < k; t += blockDim.x) {
-        const double *mr = sp.w.Minv + (size_t)t * SP_KMAX;
-        double a0 = 0.0, a1 = 0.0;
-        for (int u = 0; u < k; u++) {
-            a0 += mr[u] * g[0][u];
-            if (NRHS == 2) a1 += mr[u] * g[1][u];
-        }
-        hh[0][t] = a0;
-        if (NRHS == 2) hh[1][t] = a1;
+        hh[0][t] = sp.w.hh[t];
+        if (NRHS == 2) hh[1][t] = sp.w.hh[SP_KMAX + t];
     }
     __syncthreads();
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -795,9 +868,12 @@ __global__ void __launch_bounds__(256) k_sp_btran_part(SpDev sp, const double *e
 // mode 1: e = e_p of the pivot (st->p): Y' e_p is row p of Y;
 // mode 2: both — e_p into y, e1 (general, partials) into y1 (the primal's
 //         rho and update_gamma's u = inv(B)' v in one sweep pair)
+// parts: bit 0 the Schur correction into b, bit 1 the U' sweep (from level
+// l0u), bit 2 the L' sweep (from l0l)
 template <int NRHS>
 __global__ void __launch_bounds__(1024) k_sp_btran(SpDev sp, DState *st, const double *e, double *y, int mode,
-                                                   int nparts, const double *e1, double *y1)
+                                                   int nparts, const double *e1, double *y1, int parts, int l0u,
+                                                   int l0l)
 {
     if (mode >= 1 && (st->stop || st->p <= 0)) return;
     const int m = sp.m, k = *sp.w.k;
@@ -805,6 +881,11 @@ __global__ void __launch_bounds__(1024) k_sp_btran(SpDev sp, DState *st, const d
     __shared__ double tv[2][SP_KMAX], sv[2][SP_KMAX];
     double *b0 = sp.w.bt, *b1 = sp.w.bt + m;      // positions
     double *w0 = sp.w.scr2, *w1 = sp.w.scr2 + m;  // step space
+    if (!(parts & 1)) {
+        if (parts & 2) tri_sweep<NRHS>(sp.bu, b0, b1, w0, w1, l0u);
+        if (parts & 4) tri_sweep<NRHS>(sp.bl, w0, w1, y, y1, l0l);
+        return;
+    }
     for (int t = threadIdx.x; t < k; t += blockDim.x) {
         double a = 0.0, a1 = 0.0;
         if (mode >= 1) a = sp.w.Y[(size_t)p * SP_KMAX + t];
@@ -836,8 +917,9 @@ __global__ void __launch_bounds__(1024) k_sp_btran(SpDev sp, DState *st, const d
         if (NRHS == 2) b1[sp.w.P[t]] -= sv[1][t];
     }
     __syncthreads();
-    tri_sweep<NRHS>(sp.bu, b0, b1, w0, w1);
-    tri_sweep<NRHS>(sp.bl, w0, w1, y, y1);
+    __syncthreads();
+    if (parts & 2) tri_sweep<NRHS>(sp.bu, b0, b1, w0, w1, l0u);
+    if (parts & 4) tri_sweep<NRHS>(sp.bl, w0, w1, y, y1, l0l);
 }
 
 // the update of this pivot (one workgroup, after the commit): the column
@@ -846,15 +928,34 @@ __global__ void __launch_bounds__(1024) k_sp_btran(SpDev sp, DState *st, const d
 // its column (Sherman-Morrison).  A Schur pivot too small for a stable
 // inverse ends the chain (refact_pending), as the growth check does for the
 // dense inverse.
+// out[t] = sum_u M[t][u] c[u] for t < k (M row-major, stride SP_KMAX): one
+// wave per row, lanes along it (coalesced), fixed-order reduction; ends
+// with a barrier
+__device__ __forceinline__ void rows_dot(const double *M, const double *c, int k, double *out)
+{
+    const int lane = threadIdx.x & 63;
+    for (int t = threadIdx.x >> 6; t < k; t += blockDim.x >> 6) {
+        const double *mr = M + (size_t)t * SP_KMAX;
+        double a = 0.0;
+        for (int u = lane; u < k; u += 64) a += mr[u] * c[u];
+        a = wsum(a);
+        if (lane == 0) out[t] = a;
+    }
+    __syncthreads();
+}
+
 __global__ void __launch_bounds__(1024) k_sp_update(SpDev sp, DState *st)
 {
     if (st->stop || st->p <= 0) return;          // (primal: p = -1 is a bound flip, no basis change)
-    const int m = sp.m, k = *sp.w.k;
+    const int k = *sp.w.k;
     const int p = st->p - 1;
     __shared__ int slot;
     __shared__ double c[SP_KMAX], r[SP_KMAX], ac[SP_KMAX], ra[SP_KMAX], col_old[SP_KMAX];
     __shared__ double sch;
-    if (threadIdx.x == 0) slot = -1;
+    if (threadIdx.x == 0) {
+        slot = -1;
+        *sp.w.ycol = -1;
+    }
     __syncthreads();
     for (int t = threadIdx.x; t < k; t += blockDim.x)
         if (sp.w.P[t] == p) slot = t;                // at most one: positions are distinct
@@ -872,13 +973,10 @@ __global__ void __launch_bounds__(1024) k_sp_update(SpDev sp, DState *st)
             r[t] = Y[(size_t)p * SP_KMAX + t];
         }
         __syncthreads();
+        rows_dot(Mi, c, k, ac);                          // inv(M) c
         for (int t = threadIdx.x; t < k; t += blockDim.x) {
-            double a = 0.0, b = 0.0;
-            for (int u = 0; u < k; u++) {
-                a += Mi[(size_t)t * SP_KMAX + u] * c[u];     // inv(M) c
-                b += r[u] * Mi[(size_t)u * SP_KMAX + t];     // r inv(M)
-            }
-            ac[t] = a;
+            double b = 0.0;
+            for (int u = 0; u < k; u++) b += r[u] * Mi[(size_t)u * SP_KMAX + t];     // r inv(M)
             ra[t] = b;
         }
         __syncthreads();
@@ -907,8 +1005,8 @@ __global__ void __launch_bounds__(1024) k_sp_update(SpDev sp, DState *st)
             Mi[(size_t)k * SP_KMAX + k] = 1.0 / s;
             sp.w.P[k] = p;
             *sp.w.k = k + 1;
+            *sp.w.ycol = k;                              // k_sp_ycol writes the column
         }
-        for (int i = threadIdx.x; i < m; i += blockDim.x) Y[(size_t)i * SP_KMAX + k] = -sp.w.zq[i] - (i == p ? 1.0 : 0.0);
         return;
     }
     // replace column t0: M' = M + u e_t0', u_i = ynew[P_i] - Yold[P_i, t0]
@@ -918,12 +1016,8 @@ __global__ void __launch_bounds__(1024) k_sp_update(SpDev sp, DState *st)
         c[t] = (-sp.w.zq[pi] - (pi == p ? 1.0 : 0.0)) - col_old[t];
     }
     __syncthreads();
-    for (int t = threadIdx.x; t < k; t += blockDim.x) {
-        double a = 0.0;
-        for (int u = 0; u < k; u++) a += Mi[(size_t)t * SP_KMAX + u] * c[u];
-        ac[t] = a;                                   // inv(M) u
-        ra[t] = Mi[(size_t)t0 * SP_KMAX + t];        // row t0 of inv(M)
-    }
+    rows_dot(Mi, c, k, ac);                          // inv(M) u
+    for (int t = threadIdx.x; t < k; t += blockDim.x) ra[t] = Mi[(size_t)t0 * SP_KMAX + t];   // row t0 of inv(M)
     __syncthreads();
     const double den = 1.0 + ac[t0];
     double amax = 0.0;
@@ -937,7 +1031,19 @@ __global__ void __launch_bounds__(1024) k_sp_update(SpDev sp, DState *st)
         const int t = e / k, u = e % k;
         Mi[(size_t)t * SP_KMAX + u] -= ac[t] * ra[u] / den;
     }
-    for (int i = threadIdx.x; i < m; i += blockDim.x) Y[(size_t)i * SP_KMAX + t0] = -sp.w.zq[i] - (i == p ? 1.0 : 0.0);
+    if (threadIdx.x == 0) *sp.w.ycol = t0;
+}
+
+// the column of Y the update of this pivot bordered or replaced (grid; the
+// single-workgroup update would need m / 1024 trips of strided stores):
+// y = -zq - e_p
+__global__ void __launch_bounds__(256) k_sp_ycol(SpDev sp, const DState *st)
+{
+    if (st->stop || st->p <= 0) return;
+    const int c = *sp.w.ycol;
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (c < 0 || i >= sp.m) return;
+    sp.w.Y[(size_t)i * SP_KMAX + c] = -sp.w.zq[i] - (i == st->p - 1 ? 1.0 : 0.0);
 }
 
 // ---------------------------------------------------------------------------
@@ -984,7 +1090,7 @@ static SpDev sp_dev(SpFactor &F)
     d.bu = tri_dev(F.bu, F.hdr.p + 2);
     d.bl = tri_dev(F.bl, F.hdr.p + 3);
     d.w.Y = F.Y.p; d.w.P = F.P.p; d.w.Minv = F.Minv.p; d.w.k = F.hdr.p + 4; d.w.zq = F.zq.p;
-    d.w.tpart = F.tpart.p; d.w.bt = F.bt.p; d.w.scr2 = F.scr2.p;
+    d.w.tpart = F.tpart.p; d.w.bt = F.bt.p; d.w.scr2 = F.scr2.p; d.w.hh = F.hh.p; d.w.ycol = F.hdr.p + 5;
     return d;
 }
 
@@ -1034,6 +1140,14 @@ int sp_factorize(SpFactor &F, hipStream_t s, int m, const int *head1, const int 
     F.nnz_l = (long long)lu.Lrow.size();
     F.nnz_u = (long long)lu.Ucol.size() + m;
     F.levels[0] = S.fl.nlev; F.levels[1] = S.fu.nlev; F.levels[2] = S.bu.nlev; F.levels[3] = S.bl.nlev;
+    const SpTriHost *T4[4] = {&S.fl, &S.fu, &S.bu, &S.bl};
+    for (int i = 0; i < 4; i++) {
+        const SpTriHost &T = *T4[i];
+        const int nshort = T.nlev > 0 ? T.lvlong[0] - T.lvptr[0] : 0;
+        const int nlong = T.nlev > 0 ? T.lvptr[1] - T.lvlong[0] : 0;
+        F.wide[i] = T.nlev > 0 && nshort + nlong >= sp_wide_min();
+        F.w0blk[i] = std::max(1, std::max((nshort + 255) / 256, std::min((nlong + 3) / 4, 1024)));
+    }
     if (F.m != m) {
         F.m = m;
         F.Y.ensure((size_t)m * SP_KMAX);
@@ -1044,6 +1158,7 @@ int sp_factorize(SpFactor &F, hipStream_t s, int m, const int *head1, const int 
         F.tpart.ensure((size_t)SP_KMAX * ((m + 255) / 256 + 1));
     }
     F.P.ensure(SP_KMAX);
+    F.hh.ensure((size_t)2 * SP_KMAX);
     F.Minv.ensure((size_t)SP_KMAX * SP_KMAX);
     F.hdr.ensure(8);
     up_tri(s, F.fl, S.fl, F.hdr.p + 0);
@@ -1057,6 +1172,58 @@ int sp_factorize(SpFactor &F, hipStream_t s, int m, const int *head1, const int 
     return 0;
 }
 
+template <int NRHS>
+static void level0(const SpFactor &F, int i, const TriDev &t, hipStream_t s, const DState *st, int gate,
+                   const double *in0, const double *in1, double *out0, double *out1)
+{
+    hipLaunchKernelGGL((k_sp_level0<NRHS>), dim3(F.w0blk[i]), dim3(256), 0, s, t, st, gate, in0, in1, out0, out1);
+}
+
+// z = inv(L U) [h0, h1] (L in place, U into bt): one workgroup launch, or
+// with a wide level 0 the grid launch of that level before the workgroup's
+template <int NRHS>
+static void ftran_lu(SpFactor &F, hipStream_t s, const SpDev &d, const DState *st, int gated, double *h0, double *h1)
+{
+    const int wl = F.wide[0], wu = F.wide[1];
+    double *x0 = F.bt.p, *x1 = F.bt.p + F.m;
+    if (wl) level0<NRHS>(F, 0, d.fl, s, st, gated, h0, h1, h0, h1);
+    if (wu) {
+        hipLaunchKernelGGL((k_sp_ftran_lu<NRHS>), dim3(1), dim3(1024), 0, s, d, st, h0, h1, gated, 1, wl, 0);
+        level0<NRHS>(F, 1, d.fu, s, st, gated, h0, h1, x0, x1);
+        hipLaunchKernelGGL((k_sp_ftran_lu<NRHS>), dim3(1), dim3(1024), 0, s, d, st, h0, h1, gated, 2, 0, 1);
+    } else
+        hipLaunchKernelGGL((k_sp_ftran_lu<NRHS>), dim3(1), dim3(1024), 0, s, d, st, h0, h1, gated, 3, wl, 0);
+}
+
+// the BTRAN workgroup kernel (Schur correction, U', L'), split around the
+// grid launches of wide level-0s
+template <int NRHS>
+static void btran_seq(SpFactor &F, hipStream_t s, const SpDev &d, DState *st, const double *e, double *y, int mode,
+                      int nparts, const double *e1, double *y1)
+{
+    const int gate = mode >= 1 ? 2 : 0, m = F.m;
+    double *b0 = F.bt.p, *b1 = F.bt.p + m, *w0 = F.scr2.p, *w1 = F.scr2.p + m;
+    int parts = 1, l0u = 0, l0l = 0;
+    auto flush = [&] {
+        hipLaunchKernelGGL((k_sp_btran<NRHS>), dim3(1), dim3(1024), 0, s, d, st, e, y, mode, nparts, e1, y1, parts,
+                           l0u, l0l);
+        parts = 0;
+    };
+    if (F.wide[2]) {
+        flush();
+        level0<NRHS>(F, 2, d.bu, s, st, gate, b0, b1, w0, w1);
+        l0u = 1;
+    }
+    parts |= 2;
+    if (F.wide[3]) {
+        flush();
+        level0<NRHS>(F, 3, d.bl, s, st, gate, w0, w1, y, y1);
+        l0l = 1;
+    }
+    parts |= 4;
+    flush();
+}
+
 // y = inv(B) x (positions), x untouched (device vectors)
 void sp_ftran(SpFactor &F, hipStream_t s, const double *x, double *y)
 {
@@ -1064,8 +1231,7 @@ void sp_ftran(SpFactor &F, hipStream_t s, const double *x, double *y)
     double *scratch = F.scr.p;
     SpDev d = sp_dev(F);
     SPCHK(hipMemcpyAsync(scratch, x, (size_t)m * sizeof(double), hipMemcpyDeviceToDevice, s));
-    hipLaunchKernelGGL((k_sp_ftran_lu<1>), dim3(1), dim3(1024), 0, s, d, (const DState *)nullptr, scratch,
-                       (double *)nullptr, 0);
+    ftran_lu<1>(F, s, d, nullptr, 0, scratch, nullptr);
     hipLaunchKernelGGL((k_sp_ftran_wood<1>), dim3((m + 255) / 256), dim3(256), 0, s, d, (const DState *)nullptr, y,
                        (double *)nullptr, 0, 0);
 }
@@ -1077,16 +1243,14 @@ void sp_btran(SpFactor &F, hipStream_t s, const double *x, double *y)
     SpDev d = sp_dev(F);
     const int nb = (m + 255) / 256;
     hipLaunchKernelGGL(k_sp_btran_part, dim3(nb), dim3(256), 0, s, d, x);
-    hipLaunchKernelGGL(k_sp_btran<1>, dim3(1), dim3(1024), 0, s, d, (DState *)nullptr, x, y, 0, nb,
-                       (const double *)nullptr, (double *)nullptr);
+    btran_seq<1>(F, s, d, nullptr, x, y, 0, nb, nullptr, nullptr);
 }
 
 // the pivot's hooks (gated on the stop word, captured with the rest)
 void sp_pivot_btran(SpFactor &F, hipStream_t s, DState *st, double *rho)
 {
     SpDev d = sp_dev(F);
-    hipLaunchKernelGGL(k_sp_btran<1>, dim3(1), dim3(1024), 0, s, d, st, (const double *)nullptr, rho, 1, 0,
-                       (const double *)nullptr, (double *)nullptr);
+    btran_seq<1>(F, s, d, st, nullptr, rho, 1, 0, nullptr, nullptr);
 }
 
 // the primal's BTRANs of a pivot (p > 0 only): rho = inv(B)' e_p and
@@ -1097,7 +1261,7 @@ void sp_pivot_btran2(SpFactor &F, hipStream_t s, DState *st, const double *v, do
     SpDev d = sp_dev(F);
     const int nb = (m + 255) / 256;
     hipLaunchKernelGGL(k_sp_btran_part, dim3(nb), dim3(256), 0, s, d, v);
-    hipLaunchKernelGGL(k_sp_btran<2>, dim3(1), dim3(1024), 0, s, d, st, (const double *)nullptr, rho, 2, nb, v, u);
+    btran_seq<2>(F, s, d, st, nullptr, rho, 2, nb, v, u);
 }
 
 void sp_pivot_ftran(SpFactor &F, hipStream_t s, const DState *st, double *h, double *work, double *tcol, double *u,
@@ -1106,10 +1270,10 @@ void sp_pivot_ftran(SpFactor &F, hipStream_t s, const DState *st, double *h, dou
     const int m = F.m;
     SpDev d = sp_dev(F);
     if (pse) {
-        hipLaunchKernelGGL((k_sp_ftran_lu<2>), dim3(1), dim3(1024), 0, s, d, st, h, work, 1);
+        ftran_lu<2>(F, s, d, st, 1, h, work);
         hipLaunchKernelGGL((k_sp_ftran_wood<2>), dim3((m + 255) / 256), dim3(256), 0, s, d, st, tcol, u, 1, 1);
     } else {
-        hipLaunchKernelGGL((k_sp_ftran_lu<1>), dim3(1), dim3(1024), 0, s, d, st, h, (double *)nullptr, 1);
+        ftran_lu<1>(F, s, d, st, 1, h, nullptr);
         hipLaunchKernelGGL((k_sp_ftran_wood<1>), dim3((m + 255) / 256), dim3(256), 0, s, d, st, tcol,
                            (double *)nullptr, 1, 1);
     }
@@ -1119,6 +1283,7 @@ void sp_pivot_update(SpFactor &F, hipStream_t s, DState *st)
 {
     SpDev d = sp_dev(F);
     hipLaunchKernelGGL(k_sp_update, dim3(1), dim3(1024), 0, s, d, st);
+    hipLaunchKernelGGL(k_sp_ycol, dim3((F.m + 255) / 256), dim3(256), 0, s, d, (const DState *)st);
 }
 
 // ---------------------------------------------------------------------------

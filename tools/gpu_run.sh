@@ -48,6 +48,12 @@ for step in "$@"; do
               timeout -k 10 900 python3 -u $a > "$O/$s.$k.log" 2> "$O/$s.$k.err" ;;
         pyt*:*) lim=${step%%:*}; lim=${lim#pyt}; a=$(echo "${step#*:}" | tr ',' ' '); s=$(basename ${a%% *} .py);
               k=$((k + 1)); timeout -k 10 "$lim" python3 -u $a > "$O/$s.$k.log" 2> "$O/$s.$k.err" ;;
+        rprof:*) a=$(echo "${step#rprof:}" | tr ',' ' '); s=$(basename ${a%% *} .py); k=$((k + 1));
+              cd /tmp && cd "$GRAFT_REPO_ROOT";
+              timeout -k 10 600 rocprofv3 --kernel-trace --stats -d /tmp/rp_${NAME}_$k -o run -- python3 -u $a \
+                  > "$O/rp_$s.$k.log" 2> "$O/rp_$s.$k.err";
+              python3 tools/prof_stats.py /tmp/rp_${NAME}_$k/run_results.db --csv "$O/rp_$s.$k.csv" --gaps "$O/rp_$s.$k.gaps" \
+                  > "$O/rp_$s.$k.txt" ;;
         *) echo "unknown step $step"; exit 2 ;;
     esac
     echo "step $step ok"

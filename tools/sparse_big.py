@@ -3,13 +3,14 @@
 GPU: the block-angular generator (problems.gen_blocks) or C2s, whole dual
 solve, progress lines every out_frq pivots (stderr), then one JSON line with
 pivots/s, refactorization time, the factor's size and a KKT certificate.
-Usage: sparse_big.py [--sparse] [--tm SECS] [--save F] [--load F] blocks K [links [mb nb]] | c2s M N
+Usage: sparse_big.py [--sparse] [--tm SECS] [--save F] [--load F] [--wide N] blocks K [links [mb nb]] | c2s M N
 (--sparse: GK_SPARSE=1, the sparse factor also below m = 65536; --tm: the
 call's tm_lim in seconds (GLP_ETMLIM at the limit); --save F: the final
 row / column statuses into F (.npz); --load F: start from the statuses in F,
 as glp_set_row_stat / glp_set_col_stat would set them — a solve longer than
 one GPU session runs as a chain of tm_lim calls, each warm-started from the
-basis the previous one saved)"""
+basis the previous one saved; --wide N: GK_SP_WIDE, the level-0 size from
+which a sweep's first level runs on the whole grid)"""
 import json
 import os
 import sys
@@ -40,6 +41,8 @@ def main():
             save = sys.argv.pop(1)
         elif opt == "--load":
             load = sys.argv.pop(1)
+        elif opt == "--wide":
+            os.environ["GK_SP_WIDE"] = sys.argv.pop(1)
         else:
             raise SystemExit(f"unknown option {opt}")
     os.environ.setdefault("GK_SPARSE_LOG", "1")
@@ -56,7 +59,8 @@ def main():
     t_gen = time.time() - t0
     print(f"[sparse_big] {prob.name}: m={prob.m} n={prob.n} nnz={len(prob.A_val)} generated in {t_gen:.1f}s",
           file=sys.stderr, flush=True)
-    gk.glp_set_print_func(lambda s: print(s, file=sys.stderr, flush=True))
+    t_beg = time.time()
+    gk.glp_set_print_func(lambda s: print(f"[{time.time() - t_beg:8.1f}s] {s}", file=sys.stderr, flush=True))
     ctx = gk.Context(0)
     P = gk.GkProblem(ctx, prob)
     if load:
