@@ -108,7 +108,7 @@ struct SpTriDevBufs {
 struct SpFactor {
     int m = -1;
     SpTriDevBufs fl, fu, bu, bl;
-    SBuf<double> Y, Minv, zq, tpart, bt, scr, scr2, hh;
+    SBuf<double> Y, Minv, zq, tpart, bt, scr, scr2, hh, bz;
     SBuf<int> P, hdr;                     // hdr: nlev of fl, fu, bu, bl; k (updates in the chain); Y column of the last update
     long long nnz_l = 0, nnz_u = 0;
     int levels[4] = {0, 0, 0, 0};
@@ -119,7 +119,7 @@ struct SpFactor {
     {
         fl.release(); fu.release(); bu.release(); bl.release();
         Y.release(); Minv.release(); zq.release(); tpart.release(); bt.release(); scr.release(); scr2.release();
-        hh.release();
+        hh.release(); bz.release();
         P.release();
         hdr.release();
     }
@@ -740,6 +740,7 @@ struct WoodDev {
     double *scr2;                                 // BTRAN step-space scratch (2 x m)
     double *hh;                                   // inv(M) z[P] of the FTRAN (2 x SP_KMAX)
     int *ycol;                                    // device word: Y column the last update wrote (-1: none)
+    double *bz;                                   // e_p of the pivot's BTRAN (m; zero between uses)
 };
 
 struct SpDev {
@@ -868,6 +869,14 @@ __global__ void __launch_bounds__(256) k_sp_btran_part(SpDev sp, const double *e
 // mode 1: e = e_p of the pivot (st->p): Y' e_p is row p of Y;
 // mode 2: both — e_p into y, e1 (general, partials) into y1 (the primal's
 //         rho and update_gamma's u = inv(B)' v in one sweep pair)
+// back to zero: the entries of bz the BTRAN of e_p set (the U' sweep that
+// read them has finished: its last level ended with a barrier)
+__device__ __forceinline__ void bz_clear(const SpDev &sp, int p, int k)
+{
+    if (threadIdx.x == 0) sp.w.bz[p] = 0.0;
+    for (int t = threadIdx.x; t < k; t += blockDim.x) sp.w.bz[sp.w.P[t]] = 0.0;
+}
+
 // parts: bit 0 the Schur correction into b, bit 1 the U' sweep (from level
 // l0u), bit 2 the L' sweep (from l0l)
 template <int NRHS>
@@ -878,12 +887,17 @@ __global__ void __launch_bounds__(1024) k_sp_btran(SpDev sp, DState *st, const d
     if (mode >= 1 && (st->stop || st->p <= 0)) return;
     const int m = sp.m, k = *sp.w.k;
     const int p = (mode >= 1) ? st->p - 1 : -1;
-    __shared__ double tv[2][SP_KMAX], sv[2][SP_KMAX];
-    double *b0 = sp.w.bt, *b1 = sp.w.bt + m;      // positions
+    __shared__ double tv[2][SP_KMAX], sv[2][SP_KMAX], svp[4][2][SP_KMAX];
+    // mode 1: e_p lives in bz, zero everywhere but the k + 1 entries this
+    // BTRAN sets (p and P) and clears again at its end — no O(m) fill
+    double *b0 = (mode == 1) ? sp.w.bz : sp.w.bt, *b1 = sp.w.bt + m;      // positions
     double *w0 = sp.w.scr2, *w1 = sp.w.scr2 + m;  // step space
     if (!(parts & 1)) {
         if (parts & 2) tri_sweep<NRHS>(sp.bu, b0, b1, w0, w1, l0u);
-        if (parts & 4) tri_sweep<NRHS>(sp.bl, w0, w1, y, y1, l0l);
+        if (parts & 4) {
+            tri_sweep<NRHS>(sp.bl, w0, w1, y, y1, l0l);
+            if (mode == 1) bz_clear(sp, p, k);
+        }
         return;
     }
     for (int t = threadIdx.x; t < k; t += blockDim.x) {
@@ -896,20 +910,35 @@ __global__ void __launch_bounds__(1024) k_sp_btran(SpDev sp, DState *st, const d
         tv[0][t] = a;
         tv[1][t] = a1;
     }
-    for (int i = threadIdx.x; i < m; i += blockDim.x) {
-        b0[i] = (mode >= 1) ? (i == p ? 1.0 : 0.0) : e[i];
-        if (NRHS == 2) b1[i] = e1[i];
-    }
-    __syncthreads();
-    for (int t = threadIdx.x; t < k; t += blockDim.x) {
-        double a = 0.0, a1 = 0.0;
-        for (int u = 0; u < k; u++) {
-            const double mi = sp.w.Minv[(size_t)u * SP_KMAX + t];    // inv(M)'
-            a += mi * tv[0][u];
-            if (NRHS == 2) a1 += mi * tv[1][u];
+    if (mode == 1) {
+        if (threadIdx.x == 0) b0[p] = 1.0;
+    } else
+        for (int i = threadIdx.x; i < m; i += blockDim.x) {
+            b0[i] = (mode >= 1) ? (i == p ? 1.0 : 0.0) : e[i];
+            if (NRHS == 2) b1[i] = e1[i];
         }
-        sv[0][t] = a;
-        sv[1][t] = a1;
+    __syncthreads();
+    // sv = inv(M)' tv: four quarters of u per column t (coalesced along t),
+    // partials summed in quarter order
+    {
+        const int q = threadIdx.x >> 8, t = threadIdx.x & 255;
+        const int ub = q * ((k + 3) / 4), ue = min(k, ub + (k + 3) / 4);
+        double a = 0.0, a1 = 0.0;
+        if (t < k && q < 4)
+            for (int u = ub; u < ue; u++) {
+                const double mi = sp.w.Minv[(size_t)u * SP_KMAX + t];    // inv(M)'
+                a += mi * tv[0][u];
+                if (NRHS == 2) a1 += mi * tv[1][u];
+            }
+        if (t < k && q < 4) {
+            svp[q][0][t] = a;
+            svp[q][1][t] = a1;
+        }
+        __syncthreads();
+        for (int t2 = threadIdx.x; t2 < k; t2 += blockDim.x) {
+            sv[0][t2] = ((svp[0][0][t2] + svp[1][0][t2]) + svp[2][0][t2]) + svp[3][0][t2];
+            sv[1][t2] = ((svp[0][1][t2] + svp[1][1][t2]) + svp[2][1][t2]) + svp[3][1][t2];
+        }
     }
     __syncthreads();
     for (int t = threadIdx.x; t < k; t += blockDim.x) {   // P holds distinct positions (k_sp_update)
@@ -917,9 +946,11 @@ __global__ void __launch_bounds__(1024) k_sp_btran(SpDev sp, DState *st, const d
         if (NRHS == 2) b1[sp.w.P[t]] -= sv[1][t];
     }
     __syncthreads();
-    __syncthreads();
     if (parts & 2) tri_sweep<NRHS>(sp.bu, b0, b1, w0, w1, l0u);
-    if (parts & 4) tri_sweep<NRHS>(sp.bl, w0, w1, y, y1, l0l);
+    if (parts & 4) {
+        tri_sweep<NRHS>(sp.bl, w0, w1, y, y1, l0l);
+        if (mode == 1) bz_clear(sp, p, k);
+    }
 }
 
 // the update of this pivot (one workgroup, after the commit): the column
@@ -1090,7 +1121,7 @@ static SpDev sp_dev(SpFactor &F)
     d.bu = tri_dev(F.bu, F.hdr.p + 2);
     d.bl = tri_dev(F.bl, F.hdr.p + 3);
     d.w.Y = F.Y.p; d.w.P = F.P.p; d.w.Minv = F.Minv.p; d.w.k = F.hdr.p + 4; d.w.zq = F.zq.p;
-    d.w.tpart = F.tpart.p; d.w.bt = F.bt.p; d.w.scr2 = F.scr2.p; d.w.hh = F.hh.p; d.w.ycol = F.hdr.p + 5;
+    d.w.tpart = F.tpart.p; d.w.bt = F.bt.p; d.w.scr2 = F.scr2.p; d.w.hh = F.hh.p; d.w.ycol = F.hdr.p + 5; d.w.bz = F.bz.p;
     return d;
 }
 
@@ -1156,6 +1187,8 @@ int sp_factorize(SpFactor &F, hipStream_t s, int m, const int *head1, const int 
         F.scr.ensure(m);
         F.scr2.ensure((size_t)2 * m);
         F.tpart.ensure((size_t)SP_KMAX * ((m + 255) / 256 + 1));
+        F.bz.ensure(m);
+        SPCHK(hipMemsetAsync(F.bz.p, 0, (size_t)m * sizeof(double), s));
     }
     F.P.ensure(SP_KMAX);
     F.hh.ensure((size_t)2 * SP_KMAX);
@@ -1202,7 +1235,7 @@ static void btran_seq(SpFactor &F, hipStream_t s, const SpDev &d, DState *st, co
                       int nparts, const double *e1, double *y1)
 {
     const int gate = mode >= 1 ? 2 : 0, m = F.m;
-    double *b0 = F.bt.p, *b1 = F.bt.p + m, *w0 = F.scr2.p, *w1 = F.scr2.p + m;
+    double *b0 = (mode == 1) ? F.bz.p : F.bt.p, *b1 = F.bt.p + m, *w0 = F.scr2.p, *w1 = F.scr2.p + m;
     int parts = 1, l0u = 0, l0l = 0;
     auto flush = [&] {
         hipLaunchKernelGGL((k_sp_btran<NRHS>), dim3(1), dim3(1024), 0, s, d, st, e, y, mode, nparts, e1, y1, parts,
