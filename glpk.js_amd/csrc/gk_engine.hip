@@ -2538,8 +2538,38 @@ int gk_bfd_factorize_csc(gk_bfd *f, int m, const int *ptr, const int *ind, const
         ABI_REQUIRE(f && m >= 1, "bfd_factorize: m = %d; invalid parameter", m);
         bfd_prepare(f, m);
         f->valid = 0;
-        f->sparse = 0;                       // the explicit inverse (glp_factorize's factor)
         hipStream_t s = f->ctx->stream;
+        const char *spe = std::getenv("GK_SPARSE");
+        if (m > 65535 || (spe && std::atoi(spe) == 1)) {
+            // beyond the explicit inverse's limit (8 m^2 bytes, an O(m^3)
+            // inversion): the sparse factor, which spx_entry takes for such an
+            // LP, so a glp_factorize of an advanced basis before glp_simplex
+            // is the factor the solve then uses (GK_SPARSE=1: at any m, as
+            // spx_entry; a dense A there re-factors with the explicit inverse)
+            for (int j = 1; j <= m; j++) {
+                const int len = ptr[j + 1] - ptr[j];
+                ABI_REQUIRE(0 <= len && len <= m, "luf_factorize: j = %d; len = %d; invalid column length", j, len);
+                for (int p = ptr[j]; p < ptr[j + 1]; p++) {
+                    ABI_REQUIRE(1 <= ind[p] && ind[p] <= m, "luf_factorize: i = %d; j = %d; invalid row index", ind[p],
+                                j);
+                    ABI_REQUIRE(val[p] != 0.0, "luf_factorize: i = %d; j = %d; zero element not allowed", ind[p], j);
+                }
+            }
+            if (!f->sp) f->sp = sp_create();
+            f->sparse = 1;
+            int ret;
+            try {
+                ret = sp_factorize_csc(*f->sp, s, m, ptr, ind, val, f->parm.piv_tol, f->parm.piv_lim, f->parm.eps_tol);
+            } catch (const std::exception &e) {
+                throw AbiError{e.what()};
+            }
+            f->fact_ver++;
+            f->valid = ret == 0;
+            f->upd_cnt = 0;
+            f->ext_upd = 0;
+            return ret ? 1 : 0;   // BFD_ESING
+        }
+        f->sparse = 0;                       // the explicit inverse (glp_factorize's factor)
         // classify unit columns (+1 on a single row) as slack-like
         BasisSplit bs;
         std::vector<int> srow_pos(m + 1, 0), cptr(m + 1), crow, colJ_all;

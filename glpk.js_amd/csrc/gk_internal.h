@@ -139,6 +139,8 @@ void sp_info(const SpFactor *F, long long *nnz_lu, int *levels, double *t_lu);
 // 0, or 1 when B0 is singular; head1 1-based over (I | -A); A CSC, 0-based rows
 int sp_factorize(SpFactor &F, hipStream_t s, int m, const int *head1, const int *Aptr, const int *Aind,
                  const double *Aval, double piv_tol, int piv_lim, double eps_tol);
+int sp_factorize_csc(SpFactor &F, hipStream_t s, int m, const int *ptr, const int *ind, const double *val,
+                     double piv_tol, int piv_lim, double eps_tol);
 void sp_ftran(SpFactor &F, hipStream_t s, const double *x, double *y);   // y = inv(B) x
 void sp_btran(SpFactor &F, hipStream_t s, const double *x, double *y);   // y = inv(B)' x
 struct DState;

@@ -1137,6 +1137,10 @@ void sp_info(const SpFactor *F, long long *nnz_lu, int *levels, double *t_lu)
 
 // B0 from the basis header of (I | -A) (head 1-based; A in CSC, 0-based
 // rows, the engine's scaled copy): factorize on the host, upload
+static int sp_factorize_cols(SpFactor &F, hipStream_t s, int m, const std::vector<int> &cptr,
+                             const std::vector<int> &crow, const std::vector<double> &cval, double piv_tol,
+                             int piv_lim, double eps_tol, double t0);
+
 int sp_factorize(SpFactor &F, hipStream_t s, int m, const int *head1, const int *Aptr, const int *Aind,
                  const double *Aval, double piv_tol, int piv_lim, double eps_tol)
 {
@@ -1159,6 +1163,32 @@ int sp_factorize(SpFactor &F, hipStream_t s, int m, const int *head1, const int 
         }
         cptr[i] = (int)crow.size();
     }
+    return sp_factorize_cols(F, s, m, cptr, crow, cval, piv_tol, piv_lim, eps_tol, t0);
+}
+
+// B given by its columns (1-based CSC as gk_bfd_factorize_csc takes it:
+// ptr[1..m+1], 1-based rows) — glp_factorize of a basis beyond the explicit
+// inverse's limit
+int sp_factorize_csc(SpFactor &F, hipStream_t s, int m, const int *ptr, const int *ind, const double *val,
+                     double piv_tol, int piv_lim, double eps_tol)
+{
+    const double t0 = sp_now();
+    std::vector<int> cptr(m + 1, 0), crow((size_t)(ptr[m + 1] - ptr[1]));
+    std::vector<double> cval(crow.size());
+    for (int j = 1; j <= m; j++) {
+        for (int t = ptr[j]; t < ptr[j + 1]; t++) {
+            crow[t - ptr[1]] = ind[t] - 1;
+            cval[t - ptr[1]] = val[t];
+        }
+        cptr[j] = ptr[j + 1] - ptr[1];
+    }
+    return sp_factorize_cols(F, s, m, cptr, crow, cval, piv_tol, piv_lim, eps_tol, t0);
+}
+
+static int sp_factorize_cols(SpFactor &F, hipStream_t s, int m, const std::vector<int> &cptr,
+                             const std::vector<int> &crow, const std::vector<double> &cval, double piv_tol,
+                             int piv_lim, double eps_tol, double t0)
+{
     thread_local SpLU lu;
     thread_local SpLUWork wk;
     int rank = 0;

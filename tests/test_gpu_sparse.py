@@ -158,3 +158,40 @@ def test_gpu_sparse_phase_and_limits(gpu_ctx, sparse_on):
     assert gk.glp_simplex(Q, gk.SMCP(meth=gk.GLP_DUAL, msg_lev=gk.GLP_MSG_ERR)) == 0
     assert abs(P.obj_val - Q.obj_val) <= 1e-9 * abs(Q.obj_val)
     sparse_kkt(P, prob)
+
+
+def test_gpu_sparse_warm_start_from_statuses(gpu_ctx, sparse_on):
+    """A solve continued from saved row / column statuses (glp_set_row_stat /
+    glp_set_col_stat, then glp_simplex: glp_factorize of the advanced basis
+    through the sparse factor, gk_bfd_factorize_csc) reaches the optimum of
+    one uninterrupted solve; the factor glp_factorize leaves serves FTRAN /
+    BTRAN (glp_ftran / glp_btran) against numpy."""
+    prob = problems.gen_blocks(10, 100, 200, 5)
+    P = gk.GkProblem(gpu_ctx, prob)
+    assert gk.glp_simplex(P, gk.SMCP(meth=gk.GLP_DUAL, it_lim=1500, msg_lev=gk.GLP_MSG_ERR)) == problems.GLP_EITLIM
+    Q = gk.GkProblem(gpu_ctx, prob.copy())
+    Q.row_stat[1:prob.m + 1] = P.row_stat[1:prob.m + 1]
+    Q.col_stat[1:prob.n + 1] = P.col_stat[1:prob.n + 1]
+    Q.valid = 0
+    assert Q.factorize() == 0 and Q.valid
+    # B x = b through the factor glp_factorize built
+    m = prob.m
+    rng = np.random.default_rng(3)
+    b = rng.standard_normal(m)
+    B = np.zeros((m, m))                   # columns of (I | -A) for the basic variables
+    for j in range(1, m + 1):
+        k = Q.head[j]
+        if k <= m:
+            B[k - 1, j - 1] = 1.0
+        else:
+            lo, hi = prob.A_ptr[k - m - 1], prob.A_ptr[k - m]
+            B[prob.A_ind[lo:hi] - 1, j - 1] = -prob.A_val[lo:hi]
+    x = Q.ftran(b.copy())
+    assert np.abs(B @ x - b).max() <= 1e-9 * max(1.0, np.abs(b).max())
+    y = Q.ftran(b.copy(), tr=True)
+    assert np.abs(B.T @ y - b).max() <= 1e-9 * max(1.0, np.abs(b).max())
+    assert gk.glp_simplex(Q, gk.SMCP(meth=gk.GLP_DUAL, msg_lev=gk.GLP_MSG_ERR)) == 0
+    R = gk.GkProblem(gpu_ctx, prob.copy())
+    assert gk.glp_simplex(R, gk.SMCP(meth=gk.GLP_DUAL, msg_lev=gk.GLP_MSG_ERR)) == 0
+    assert abs(Q.obj_val - R.obj_val) <= 1e-9 * max(1.0, abs(R.obj_val)), (Q.obj_val, R.obj_val)
+    sparse_kkt(Q, prob)
