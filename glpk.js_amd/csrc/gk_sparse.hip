@@ -112,8 +112,15 @@ struct SpFactor {
     SBuf<int> P, hdr;                     // hdr: nlev of fl, fu, bu, bl; k (updates in the chain); Y column of the last update
     long long nnz_l = 0, nnz_u = 0;
     int levels[4] = {0, 0, 0, 0};
-    int wide[4] = {0, 0, 0, 0};           // level 0 of fl / fu / bu / bl runs on the grid (k_sp_level0)
-    int w0blk[4] = {0, 0, 0, 0};          // its grid
+    // the launch plan of each sweep (fl, fu, bu, bl): wide levels (>= SP_WIDE
+    // steps) as grid launches (k_sp_level), the runs of narrow levels
+    // between them in one workgroup (k_sp_sweep); wide[i] = 0: the whole
+    // sweep in the fused one-workgroup kernels
+    struct Seg {
+        int grid, l0, l1, blocks;
+    };
+    std::vector<Seg> plan[4];
+    int wide[4] = {0, 0, 0, 0};
     double t_lu = 0.0, t_total = 0.0;
     ~SpFactor()
     {
@@ -132,7 +139,7 @@ static int sp_wide_min()
 {
     static const int w = [] {
         const char *e = std::getenv("GK_SP_WIDE");
-        return e ? std::max(1, atoi(e)) : 8192;
+        return e ? std::max(1, atoi(e)) : 4096;
     }();
     return w;
 }
@@ -503,6 +510,19 @@ static void sp_build_tri(SpTriHost &T, int nsteps, const std::vector<int> &iin, 
         auto mid = std::stable_partition(b, e, [&](int k) { return D.ptr[k + 1] - D.ptr[k] <= TRI_LONG; });
         T.lvlong[l] = (int)(mid - order.begin());
     }
+    static const bool lvlog = std::getenv("GK_SP_LEVELS") != nullptr;
+    if (lvlog) {
+        std::string line = "[gk sp levels]";
+        long long tot = 0;
+        for (int l = 0; l < nlev; l++) {
+            long long ent = 0;
+            for (int q = T.lvptr[l]; q < T.lvptr[l + 1]; q++) ent += D.ptr[order[q] + 1] - D.ptr[order[q]];
+            tot += ent;
+            line += " " + std::to_string(T.lvptr[l + 1] - T.lvptr[l]) + "/" + std::to_string(ent) + "/" +
+                    std::to_string(T.lvptr[l + 1] - T.lvlong[l]);
+        }
+        fprintf(stderr, "%s (steps/entries/long per level; %lld entries)\n", line.c_str(), tot);
+    }
     T.iin.resize(nsteps); T.iout.resize(nsteps); T.diag.resize(nsteps); T.eptr.assign(nsteps + 1, 0);
     T.eidx.resize(D.idx.size()); T.eval.resize(D.idx.size());
     int ne = 0;
@@ -699,11 +719,12 @@ __device__ __forceinline__ void step_wave(const TriDev &t, const double *in0, co
 // levels l0 .. nlev-1 (l0 = 1: level 0 ran on the whole grid, k_sp_level0)
 template <int NRHS>
 __device__ void tri_sweep(const TriDev &t, const double *in0, const double *in1, double *out0, double *out1,
-                          int l0 = 0)
+                          int l0 = 0, int l1 = -1)
 {
-    const int nlev = *t.nlev;
+    const int nlev = (l1 < 0) ? *t.nlev : l1;
     const int T = blockDim.x;
     const int w = threadIdx.x >> 6, nw = blockDim.x >> 6;
+    __shared__ double red[2][16];
     if (nlev <= l0) return;
     int lb = t.lvptr[l0], le = t.lvptr[l0 + 1], ls = t.lvlong[l0];
     StepPre<NRHS> cur;
@@ -719,7 +740,45 @@ __device__ void tri_sweep(const TriDev &t, const double *in0, const double *in1,
             step_load<NRHS>(t, in0, in1, s, ls, q);
             step_run<NRHS>(t, q, out0, out1);
         }
-        for (int s = ls + w; s < le; s += nw) step_wave<NRHS>(t, in0, in1, s, out0, out1);
+        const int nl = le - ls;
+        if (nl > 0 && 4 * nl <= nw) {
+            // few long steps (a linking row's L step gathers thousands of
+            // entries, alone on its level): nw / nl waves per step, their
+            // partials summed in wave order by the step's first wave
+            const int g = nw / nl, sidx = w / g, sub = w % g;
+            const int lane = threadIdx.x & 63;
+            double a0 = 0.0, a1 = 0.0;
+            int eb = 0, ee = 0;
+            if (sidx < nl) {
+                eb = t.eptr[ls + sidx];
+                ee = t.eptr[ls + sidx + 1];
+                for (int e = eb + sub * 64 + lane; e < ee; e += g * 64) {
+                    const int ix = t.eidx[e];
+                    a0 += t.eval[e] * out0[ix];
+                    if (NRHS == 2) a1 += t.eval[e] * out1[ix];
+                }
+            }
+            a0 = wsum(a0);
+            if (NRHS == 2) a1 = wsum(a1);
+            if (lane == 0) {
+                red[0][w] = a0;
+                red[1][w] = a1;
+            }
+            __syncthreads();
+            if (sidx < nl && sub == 0 && lane == 0) {
+                const int st = ls + sidx;
+                double s0 = 0.0, s1 = 0.0;
+                for (int u = 0; u < g; u++) {
+                    s0 += red[0][w + u];
+                    s1 += red[1][w + u];
+                }
+                const int ii = t.iin[st], io = t.iout[st];
+                const double dg = t.diag[st];
+                out0[io] = (in0[ii] - s0) / dg;
+                if (NRHS == 2) out1[io] = (in1[ii] - s1) / dg;
+            }
+        } else
+            for (int s = ls + w; s < le; s += nw) step_wave<NRHS>(t, in0, in1, s, out0, out1);
         __syncthreads();
         cur = nxt;
         lb = nb;
@@ -761,11 +820,11 @@ __device__ __forceinline__ bool sp_gated(const DState *st, int gate)
 // runs as a gather at HBM rate instead of m / 1024 dependent trips of the
 // single workgroup; the workgroup's sweep then starts at level 1
 template <int NRHS>
-__global__ void __launch_bounds__(256) k_sp_level0(TriDev t, const DState *st, int gate, const double *in0,
-                                                   const double *in1, double *out0, double *out1)
+__global__ void __launch_bounds__(256) k_sp_level(TriDev t, const DState *st, int gate, const double *in0,
+                                                  const double *in1, double *out0, double *out1, int l)
 {
     if (sp_gated(st, gate)) return;
-    const int lb = t.lvptr[0], ls = t.lvlong[0], le = t.lvptr[1];
+    const int lb = t.lvptr[l], ls = t.lvlong[l], le = t.lvptr[l + 1];
     const int g = blockIdx.x * blockDim.x + threadIdx.x;
     if (lb + g < ls) {
         StepPre<NRHS> q;
@@ -775,6 +834,9 @@ __global__ void __launch_bounds__(256) k_sp_level0(TriDev t, const DState *st, i
     const int gw = g >> 6, nw = (gridDim.x * blockDim.x) >> 6;
     for (int s = ls + gw; s < le; s += nw) step_wave<NRHS>(t, in0, in1, s, out0, out1);
 }
+
+template <int NRHS>
+__device__ void ftran_hh(const SpDev &sp);
 
 // FTRAN part 1 (one workgroup): z = inv(B0) [h, work]; L in place, U into
 // the scratch; the z of h is kept (zq) for the update of this pivot.
@@ -789,8 +851,16 @@ __global__ void __launch_bounds__(1024) k_sp_ftran_lu(SpDev sp, const DState *st
     double *x0 = sp.w.bt, *x1 = sp.w.bt + m;
     if (!(parts & 2)) return;
     tri_sweep<NRHS>(sp.fu, h0, h1, x0, x1, l0u);                      // positions
-    // hh = inv(M) z[P] for k_sp_ftran_wood, once: one wave per row of
-    // inv(M), its lanes along the row (coalesced), fixed-order reduction
+    ftran_hh<NRHS>(sp);
+}
+
+// hh = inv(M) z[P] for k_sp_ftran_wood, once per FTRAN: one wave per row of
+// inv(M), its lanes along the row (coalesced), fixed-order reduction
+template <int NRHS>
+__device__ void ftran_hh(const SpDev &sp)
+{
+    const int m = sp.m;
+    const double *x0 = sp.w.bt, *x1 = sp.w.bt + m;
     const int k = *sp.w.k;
     if (k == 0) return;
     __shared__ double g[2][SP_KMAX];
@@ -875,6 +945,32 @@ __device__ __forceinline__ void bz_clear(const SpDev &sp, int p, int k)
 {
     if (threadIdx.x == 0) sp.w.bz[p] = 0.0;
     for (int t = threadIdx.x; t < k; t += blockDim.x) sp.w.bz[sp.w.P[t]] = 0.0;
+}
+
+// one workgroup: levels [l0, l1) of sweep `which` (0 fl, 1 fu, 2 bu, 3 bl)
+// between the grid launches of the wide levels; clr: the BTRAN of e_p ends
+// here (bz back to zero)
+template <int NRHS>
+__global__ void __launch_bounds__(1024) k_sp_sweep(SpDev sp, int which, const DState *st, int gate,
+                                                   const double *in0, const double *in1, double *out0,
+                                                   double *out1, int l0, int l1, int clr)
+{
+    if (sp_gated(st, gate)) return;
+    const TriDev &t = which == 0 ? sp.fl : which == 1 ? sp.fu : which == 2 ? sp.bu : sp.bl;
+    tri_sweep<NRHS>(t, in0, in1, out0, out1, l0, l1);
+    if (clr) {
+        __syncthreads();
+        bz_clear(sp, st->p - 1, *sp.w.k);
+    }
+}
+
+// the FTRAN's inv(M) z[P] (k_sp_ftran_lu's tail) as its own launch, after a
+// U sweep that ended on the grid or in a k_sp_sweep
+template <int NRHS>
+__global__ void __launch_bounds__(1024) k_sp_hh(SpDev sp, const DState *st, int gated)
+{
+    if (gated && st->stop) return;
+    ftran_hh<NRHS>(sp);
 }
 
 // parts: bit 0 the Schur correction into b, bit 1 the U' sweep (from level
@@ -1204,10 +1300,21 @@ static int sp_factorize_cols(SpFactor &F, hipStream_t s, int m, const std::vecto
     const SpTriHost *T4[4] = {&S.fl, &S.fu, &S.bu, &S.bl};
     for (int i = 0; i < 4; i++) {
         const SpTriHost &T = *T4[i];
-        const int nshort = T.nlev > 0 ? T.lvlong[0] - T.lvptr[0] : 0;
-        const int nlong = T.nlev > 0 ? T.lvptr[1] - T.lvlong[0] : 0;
-        F.wide[i] = T.nlev > 0 && nshort + nlong >= sp_wide_min();
-        F.w0blk[i] = std::max(1, std::max((nshort + 255) / 256, std::min((nlong + 3) / 4, 1024)));
+        F.plan[i].clear();
+        F.wide[i] = 0;
+        int run = -1;                        // first level of the current narrow run
+        for (int l = 0; l < T.nlev; l++) {
+            const int nshort = T.lvlong[l] - T.lvptr[l], nlong = T.lvptr[l + 1] - T.lvlong[l];
+            if (nshort + nlong >= sp_wide_min()) {
+                if (run >= 0) F.plan[i].push_back({0, run, l, 1});
+                run = -1;
+                F.plan[i].push_back({1, l, l + 1, std::max(1, std::max((nshort + 255) / 256,
+                                                                       std::min((nlong + 3) / 4, 1024)))});
+                F.wide[i] = 1;
+            } else if (run < 0)
+                run = l;
+        }
+        if (run >= 0) F.plan[i].push_back({0, run, T.nlev, 1});
     }
     if (F.m != m) {
         F.m = m;
@@ -1235,56 +1342,60 @@ static int sp_factorize_cols(SpFactor &F, hipStream_t s, int m, const std::vecto
     return 0;
 }
 
+// one sweep by its plan; clr: the last launch clears bz (BTRAN of e_p)
 template <int NRHS>
-static void level0(const SpFactor &F, int i, const TriDev &t, hipStream_t s, const DState *st, int gate,
-                   const double *in0, const double *in1, double *out0, double *out1)
+static void run_plan(const SpFactor &F, int which, const SpDev &d, hipStream_t s, const DState *st, int gate,
+                     const double *in0, const double *in1, double *out0, double *out1, int clr)
 {
-    hipLaunchKernelGGL((k_sp_level0<NRHS>), dim3(F.w0blk[i]), dim3(256), 0, s, t, st, gate, in0, in1, out0, out1);
+    const TriDev &t = which == 0 ? d.fl : which == 1 ? d.fu : which == 2 ? d.bu : d.bl;
+    const auto &pl = F.plan[which];
+    for (size_t q = 0; q < pl.size(); q++) {
+        const int last = clr && q + 1 == pl.size();
+        if (pl[q].grid) {
+            hipLaunchKernelGGL((k_sp_level<NRHS>), dim3(pl[q].blocks), dim3(256), 0, s, t, st, gate, in0, in1, out0,
+                               out1, pl[q].l0);
+            if (last)
+                hipLaunchKernelGGL((k_sp_sweep<NRHS>), dim3(1), dim3(1024), 0, s, d, which, st, gate, in0, in1, out0,
+                                   out1, 0, 0, 1);
+        } else
+            hipLaunchKernelGGL((k_sp_sweep<NRHS>), dim3(1), dim3(1024), 0, s, d, which, st, gate, in0, in1, out0,
+                               out1, pl[q].l0, pl[q].l1, last);
+    }
+    if (pl.empty() && clr)
+        hipLaunchKernelGGL((k_sp_sweep<NRHS>), dim3(1), dim3(1024), 0, s, d, which, st, gate, in0, in1, out0, out1, 0,
+                           0, 1);
 }
 
-// z = inv(L U) [h0, h1] (L in place, U into bt): one workgroup launch, or
-// with a wide level 0 the grid launch of that level before the workgroup's
+// z = inv(L U) [h0, h1] (L in place, U into bt) and inv(M) z[P]: one fused
+// workgroup launch, or with wide levels the plans of both sweeps
 template <int NRHS>
 static void ftran_lu(SpFactor &F, hipStream_t s, const SpDev &d, const DState *st, int gated, double *h0, double *h1)
 {
-    const int wl = F.wide[0], wu = F.wide[1];
+    if (!F.wide[0] && !F.wide[1]) {
+        hipLaunchKernelGGL((k_sp_ftran_lu<NRHS>), dim3(1), dim3(1024), 0, s, d, st, h0, h1, gated, 3, 0, 0);
+        return;
+    }
     double *x0 = F.bt.p, *x1 = F.bt.p + F.m;
-    if (wl) level0<NRHS>(F, 0, d.fl, s, st, gated, h0, h1, h0, h1);
-    if (wu) {
-        hipLaunchKernelGGL((k_sp_ftran_lu<NRHS>), dim3(1), dim3(1024), 0, s, d, st, h0, h1, gated, 1, wl, 0);
-        level0<NRHS>(F, 1, d.fu, s, st, gated, h0, h1, x0, x1);
-        hipLaunchKernelGGL((k_sp_ftran_lu<NRHS>), dim3(1), dim3(1024), 0, s, d, st, h0, h1, gated, 2, 0, 1);
-    } else
-        hipLaunchKernelGGL((k_sp_ftran_lu<NRHS>), dim3(1), dim3(1024), 0, s, d, st, h0, h1, gated, 3, wl, 0);
+    run_plan<NRHS>(F, 0, d, s, st, gated, h0, h1, h0, h1, 0);
+    run_plan<NRHS>(F, 1, d, s, st, gated, h0, h1, x0, x1, 0);
+    hipLaunchKernelGGL((k_sp_hh<NRHS>), dim3(1), dim3(1024), 0, s, d, st, gated);
 }
 
-// the BTRAN workgroup kernel (Schur correction, U', L'), split around the
-// grid launches of wide level-0s
+// the BTRAN (Schur correction, U', L'): one fused workgroup launch, or the
+// correction alone and then the plans of both sweeps
 template <int NRHS>
 static void btran_seq(SpFactor &F, hipStream_t s, const SpDev &d, DState *st, const double *e, double *y, int mode,
                       int nparts, const double *e1, double *y1)
 {
+    if (!F.wide[2] && !F.wide[3]) {
+        hipLaunchKernelGGL((k_sp_btran<NRHS>), dim3(1), dim3(1024), 0, s, d, st, e, y, mode, nparts, e1, y1, 7, 0, 0);
+        return;
+    }
     const int gate = mode >= 1 ? 2 : 0, m = F.m;
     double *b0 = (mode == 1) ? F.bz.p : F.bt.p, *b1 = F.bt.p + m, *w0 = F.scr2.p, *w1 = F.scr2.p + m;
-    int parts = 1, l0u = 0, l0l = 0;
-    auto flush = [&] {
-        hipLaunchKernelGGL((k_sp_btran<NRHS>), dim3(1), dim3(1024), 0, s, d, st, e, y, mode, nparts, e1, y1, parts,
-                           l0u, l0l);
-        parts = 0;
-    };
-    if (F.wide[2]) {
-        flush();
-        level0<NRHS>(F, 2, d.bu, s, st, gate, b0, b1, w0, w1);
-        l0u = 1;
-    }
-    parts |= 2;
-    if (F.wide[3]) {
-        flush();
-        level0<NRHS>(F, 3, d.bl, s, st, gate, w0, w1, y, y1);
-        l0l = 1;
-    }
-    parts |= 4;
-    flush();
+    hipLaunchKernelGGL((k_sp_btran<NRHS>), dim3(1), dim3(1024), 0, s, d, st, e, y, mode, nparts, e1, y1, 1, 0, 0);
+    run_plan<NRHS>(F, 2, d, s, st, gate, b0, b1, w0, w1, 0);
+    run_plan<NRHS>(F, 3, d, s, st, gate, w0, w1, y, y1, mode == 1);
 }
 
 // y = inv(B) x (positions), x untouched (device vectors)
