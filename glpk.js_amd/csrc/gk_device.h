@@ -30,7 +30,6 @@ __device__ __forceinline__ double wsum(double v) { return __ockl_wfred_add_f64(v
 // by their own thread: a dense row (a linking row of a block-angular LP has
 // thousands of entries) would otherwise be a serial chain of dependent
 // loads.  Call with every lane of the wave; lanes flag their long rows.
-constexpr int CSR_LONG = 32;
 template <typename F>
 __device__ __forceinline__ void csr_long_rows(bool is_long, int beg, int end, const int *__restrict__ rcol,
                                               const double *__restrict__ rval, const double *__restrict__ x, F &&done)

@@ -1329,6 +1329,22 @@ __global__ void __launch_bounds__(256) k_dual_ratio(SpxDev d, int gn, int tiles_
         if (w4 == 0 && r < m) d.work[r] = ysr - (((sw[0][lane] + sw[1][lane]) + sw[2][lane]) + sw[3][lane]);
         return;
     }
+    if (!d.A.dense && (int)blockIdx.x >= gn + (m + 255) / 256) {
+        // sparse A, one long row per block: the 4 waves stride its entries,
+        // partials summed in wave order
+        __shared__ double lw[4];
+        const int r = d.A.lrow[blockIdx.x - gn - (m + 255) / 256];
+        const int beg = d.A.rptr[r], end = d.A.rptr[r + 1];
+        const double ysr = d.ys[r];
+        if (stop) return;
+        double acc = 0.0;
+        for (int t = beg + (int)threadIdx.x; t < end; t += 256) acc += d.A.rval[t] * d.wcol[d.A.rcol[t]];
+        acc = wsum(acc);
+        if ((threadIdx.x & 63) == 0) lw[threadIdx.x >> 6] = acc;
+        __syncthreads();
+        if (threadIdx.x == 0) d.work[r] = ysr - (((lw[0] + lw[1]) + lw[2]) + lw[3]);
+        return;
+    }
     if ((int)blockIdx.x >= gn && !d.A.dense) {
         // sparse A: work = ys - A w, one row per thread over its CSR entries
         // (update_gamma :1103-1134; entries loaded ahead, fixed order)
@@ -1358,11 +1374,7 @@ __global__ void __launch_bounds__(256) k_dual_ratio(SpxDev d, int gn, int tiles_
             for (int t = beg + RU; t < end; ++t) acc += d.A.rval[t] * d.wcol[d.A.rcol[t]];
             d.work[r] = ysr - acc;
         }
-        const int rb = r - (int)(threadIdx.x & 63);
-        csr_long_rows(lng, beg, end, d.A.rcol, d.A.rval, d.wcol, [&](int src, double acc) {
-            if ((int)(threadIdx.x & 63) == 0) d.work[rb + src] = d.ys[rb + src] - acc;
-        });
-        return;
+        return;                                  // long rows: the blocks above
     }
     if ((int)blockIdx.x >= gn) {
         const int b = blockIdx.x - gn;
@@ -2754,8 +2766,8 @@ void dual_iteration2(hipStream_t s, const SpxDev &d, const DualPlan &pl, hipEven
                       &d.st->trow_max_bits, d.st, 0);
         if (ev1) (void)hipEventRecord(ev1, s);
         hipLaunchKernelGGL(k_trow_finish, dim3(gv), dim3(256), 0, s, d, pl.pse);
-        hipLaunchKernelGGL(k_dual_ratio, dim3(gn + (pl.pse ? cdiv(m, 256) : 0)), dim3(256), 0, s, d, gn, tiles_m, 0,
-                           ncb, 0, 0);
+        hipLaunchKernelGGL(k_dual_ratio, dim3(gn + (pl.pse ? cdiv(m, 256) + d.A.nlr : 0)), dim3(256), 0, s, d, gn,
+                           tiles_m, 0, ncb, 0, 0);
         hipLaunchKernelGGL(k_dual_pick, dim3(1), dim3(1024), 0, s, d, pl.pse, gn, ncb);
         sp_pivot_ftran(*d.sp, s, d.st, d.h, d.work, d.tcol, d.u, pl.pse);
         hipLaunchKernelGGL(k_dual_commit, dim3(gv), dim3(256), 0, s, d, pl.pse, gv, tiles_m, pl.lpsu, 0,
@@ -2768,8 +2780,8 @@ void dual_iteration2(hipStream_t s, const SpxDev &d, const DualPlan &pl, hipEven
         if (ev0) (void)hipEventRecord(ev0, s);
         hipLaunchKernelGGL(k_dual_col, dim3(gv), dim3(256), 0, s, d, pl.pse, pl.nr_cap, pl.gm);
         if (ev1) (void)hipEventRecord(ev1, s);
-        hipLaunchKernelGGL(k_dual_ratio, dim3(gn + (pl.pse ? cdiv(m, 256) : 0)), dim3(256), 0, s, d, gn, tiles_m, 2,
-                           ncb, 0, prev_blocks(d, pl));
+        hipLaunchKernelGGL(k_dual_ratio, dim3(gn + (pl.pse ? cdiv(m, 256) + d.A.nlr : 0)), dim3(256), 0, s, d, gn,
+                           tiles_m, 2, ncb, 0, prev_blocks(d, pl));
         if (pl.fupd) {
             if (pl.pse) launch_update<2, 1>(s, d, pl, gn, ncb, 2);
             else launch_update<1, 1>(s, d, pl, gn, ncb, 2);

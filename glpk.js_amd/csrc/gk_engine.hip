@@ -156,6 +156,8 @@ struct Engine {
     DBuf<double> A, AT;                     // dense column-major and row-major
     int ldt = 0;
     DBuf<int> cptr, cind, rptr, rcol;        // CSC / CSR
+    DBuf<int> lrow;                          // CSR rows longer than CSR_LONG
+    int nlr = 0;
     DBuf<double> cval, rval;
     // working set
     DBuf<signed char> type, orig_type, stat, refsp;
@@ -233,6 +235,7 @@ struct Engine {
         M.A = A.p; M.lda = lda;
         M.cptr = cptr.p; M.cind = cind.p; M.cval = cval.p;
         M.rptr = rptr.p; M.rcol = rcol.p; M.rval = rval.p;
+        M.lrow = lrow.p; M.nlr = dense ? 0 : nlr;
         M.AT = dense ? AT.p : nullptr; M.ldt = ldt;
         int avg = n > 0 ? nnz / n : 0;
         M.lpc = avg >= 48 ? 64 : (avg >= 6 ? 8 : 1);
@@ -635,6 +638,15 @@ static void engine_upload_matrix(gk_bfd *f, const gk_lp *lp)
         HIPCHK(hipMemcpyAsync(E.rptr.p, rptr.data(), (m + 1) * sizeof(int), hipMemcpyHostToDevice, s));
         HIPCHK(hipMemcpyAsync(E.rcol.p, rcol.data(), (size_t)nnz * sizeof(int), hipMemcpyHostToDevice, s));
         HIPCHK(hipMemcpyAsync(E.rval.p, rval.data(), (size_t)nnz * sizeof(double), hipMemcpyHostToDevice, s));
+        // the long rows (linking rows of a block-angular LP) get a block
+        // each in k_dual_ratio's A w instead of one wave for every 64 rows
+        std::vector<int> lr;
+        for (int r = 0; r < m; r++)
+            if (rptr[r + 1] - rptr[r] > CSR_LONG) lr.push_back(r);
+        E.nlr = (int)lr.size();
+        E.lrow.ensure(std::max<size_t>(lr.size(), 1));
+        if (!lr.empty())
+            HIPCHK(hipMemcpyAsync(E.lrow.p, lr.data(), lr.size() * sizeof(int), hipMemcpyHostToDevice, s));
     }
     HIPCHK(hipStreamSynchronize(s));
     if (E.dense) {   // the dense copy is the only one the passes read

@@ -95,6 +95,9 @@ void gemv_n(hipStream_t s, const double *M, int rows, int cols, int ld, const do
 void gemv_t(hipStream_t s, const double *M, int rows, int cols, int ld, const double *x, double *y, double alpha);
 
 // ---- the (I | -A) column passes -------------------------------------------
+// rows of a CSR matrix longer than this are summed by a whole wave (or, in
+// k_dual_ratio's A w, a whole block) instead of by their own thread
+constexpr int CSR_LONG = 32;
 struct MatDev {
     int m, n, nnz;
     int dense;                    // 1: A dense column-major
@@ -103,6 +106,7 @@ struct MatDev {
     const int *rptr, *rcol; const double *rval;   // CSR, 0-based cols
     const double *AT; int ldt;    // dense: row-major copy (AT[r*ldt + c] = A[r, c]) for row-wise pivot rows
     int lpc;                      // lanes per column for CSC passes (1, 8 or 64)
+    const int *lrow; int nlr;     // sparse: the rows longer than CSR_LONG (k_dual_ratio's A w: a block each)
 };
 
 enum : int { CP_TROW = 0, CP_CBAR = 1, CP_RESID = 2, CP_TROW_S = 3, CP_DOT = 4 };
