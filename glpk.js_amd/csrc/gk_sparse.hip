@@ -717,6 +717,48 @@ __device__ __forceinline__ void step_wave(const TriDev &t, const double *in0, co
 }
 
 // levels l0 .. nlev-1 (l0 = 1: level 0 ran on the whole grid, k_sp_level0)
+// a level of few long steps, split over the workgroup's waves: this
+// thread's first LPF entries of its step and (the step's leader) the step's
+// metadata and right-hand side — none depends on the sweep's output, so they
+// are loaded a level ahead like the short steps' (StepPre)
+constexpr int LPF = 4;
+template <int NRHS>
+struct LongPre {
+    int split, eb, ee, ii, io;
+    double dg, a0, a1;
+    int ix[LPF];
+    double v[LPF];
+};
+
+template <int NRHS>
+__device__ __forceinline__ void long_load(const TriDev &t, const double *in0, const double *in1, int ls, int le,
+                                          LongPre<NRHS> &q)
+{
+    const int nw = blockDim.x >> 6, w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int nl = le - ls;
+    q.split = nl > 0 && 4 * nl <= nw;
+    q.eb = q.ee = 0;
+    if (!q.split) return;
+    const int g = nw / nl, sidx = w / g, sub = w % g;
+    if (sidx >= nl) return;
+    q.eb = t.eptr[ls + sidx];
+    q.ee = t.eptr[ls + sidx + 1];
+#pragma unroll
+    for (int u = 0; u < LPF; u++) {
+        const int e = q.eb + (sub + u * g) * 64 + lane;
+        const bool ok = e < q.ee;
+        q.ix[u] = ok ? t.eidx[e] : 0;
+        q.v[u] = ok ? t.eval[e] : 0.0;
+    }
+    if (sub == 0 && lane == 0) {
+        q.ii = t.iin[ls + sidx];
+        q.io = t.iout[ls + sidx];
+        q.dg = t.diag[ls + sidx];
+        q.a0 = in0[q.ii];
+        q.a1 = (NRHS == 2) ? in1[q.ii] : 0.0;
+    }
+}
+
 template <int NRHS>
 __device__ void tri_sweep(const TriDev &t, const double *in0, const double *in1, double *out0, double *out1,
                           int l0 = 0, int l1 = -1)
@@ -729,11 +771,15 @@ __device__ void tri_sweep(const TriDev &t, const double *in0, const double *in1,
     int lb = t.lvptr[l0], le = t.lvptr[l0 + 1], ls = t.lvlong[l0];
     StepPre<NRHS> cur;
     step_load<NRHS>(t, in0, in1, lb + (int)threadIdx.x, ls, cur);
+    LongPre<NRHS> lcur;
+    long_load<NRHS>(t, in0, in1, ls, le, lcur);
     for (int l = l0; l < nlev; l++) {
         // the next level's bounds and this thread's first (short) step of it
         const int nb = le, ne = (l + 1 < nlev) ? t.lvptr[l + 2] : le, nls = (l + 1 < nlev) ? t.lvlong[l + 1] : le;
         StepPre<NRHS> nxt;
         step_load<NRHS>(t, in0, in1, nb + (int)threadIdx.x, nls, nxt);
+        LongPre<NRHS> lnxt;
+        long_load<NRHS>(t, in0, in1, nls, ne, lnxt);
         if (cur.s < ls) step_run<NRHS>(t, cur, out0, out1);
         for (int s = cur.s + T; s < ls; s += T) {          // short steps beyond one per thread
             StepPre<NRHS> q;
@@ -741,18 +787,29 @@ __device__ void tri_sweep(const TriDev &t, const double *in0, const double *in1,
             step_run<NRHS>(t, q, out0, out1);
         }
         const int nl = le - ls;
-        if (nl > 0 && 4 * nl <= nw) {
+        if (lcur.split) {
             // few long steps (a linking row's L step gathers thousands of
             // entries, alone on its level): nw / nl waves per step, their
-            // partials summed in wave order by the step's first wave
+            // partials summed in wave order by the step's first wave; the
+            // first LPF entries per lane and the step's data came a level ahead
             const int g = nw / nl, sidx = w / g, sub = w % g;
             const int lane = threadIdx.x & 63;
             double a0 = 0.0, a1 = 0.0;
-            int eb = 0, ee = 0;
+            const int eb = lcur.eb, ee = lcur.ee;
             if (sidx < nl) {
-                eb = t.eptr[ls + sidx];
-                ee = t.eptr[ls + sidx + 1];
-                for (int e = eb + sub * 64 + lane; e < ee; e += g * 64) {
+                double x0[LPF], x1[LPF];
+#pragma unroll
+                for (int u = 0; u < LPF; u++) {
+                    const bool ok = eb + (sub + u * g) * 64 + lane < ee;
+                    x0[u] = ok ? out0[lcur.ix[u]] : 0.0;
+                    x1[u] = (NRHS == 2 && ok) ? out1[lcur.ix[u]] : 0.0;
+                }
+#pragma unroll
+                for (int u = 0; u < LPF; u++) {
+                    a0 += lcur.v[u] * x0[u];
+                    if (NRHS == 2) a1 += lcur.v[u] * x1[u];
+                }
+                for (int e = eb + (sub + LPF * g) * 64 + lane; e < ee; e += g * 64) {
                     const int ix = t.eidx[e];
                     a0 += t.eval[e] * out0[ix];
                     if (NRHS == 2) a1 += t.eval[e] * out1[ix];
@@ -766,21 +823,19 @@ __device__ void tri_sweep(const TriDev &t, const double *in0, const double *in1,
             }
             __syncthreads();
             if (sidx < nl && sub == 0 && lane == 0) {
-                const int st = ls + sidx;
                 double s0 = 0.0, s1 = 0.0;
                 for (int u = 0; u < g; u++) {
                     s0 += red[0][w + u];
                     s1 += red[1][w + u];
                 }
-                const int ii = t.iin[st], io = t.iout[st];
-                const double dg = t.diag[st];
-                out0[io] = (in0[ii] - s0) / dg;
-                if (NRHS == 2) out1[io] = (in1[ii] - s1) / dg;
+                out0[lcur.io] = (lcur.a0 - s0) / lcur.dg;
+                if (NRHS == 2) out1[lcur.io] = (lcur.a1 - s1) / lcur.dg;
             }
         } else
             for (int s = ls + w; s < le; s += nw) step_wave<NRHS>(t, in0, in1, s, out0, out1);
         __syncthreads();
         cur = nxt;
+        lcur = lnxt;
         lb = nb;
         le = ne;
         ls = nls;
@@ -947,16 +1002,18 @@ __device__ __forceinline__ void bz_clear(const SpDev &sp, int p, int k)
     for (int t = threadIdx.x; t < k; t += blockDim.x) sp.w.bz[sp.w.P[t]] = 0.0;
 }
 
-// one workgroup: levels [l0, l1) of sweep `which` (0 fl, 1 fu, 2 bu, 3 bl)
+// one workgroup: levels [l0, l1) of sweep t
 // between the grid launches of the wide levels; clr: the BTRAN of e_p ends
 // here (bz back to zero)
 template <int NRHS>
-__global__ void __launch_bounds__(1024) k_sp_sweep(SpDev sp, int which, const DState *st, int gate,
+__global__ void __launch_bounds__(1024) k_sp_sweep(SpDev sp, TriDev t, const DState *st, int gate,
                                                    const double *in0, const double *in1, double *out0,
                                                    double *out1, int l0, int l1, int clr)
 {
+    // (the sweep's TriDev is its own argument: one selected from sp by a
+    // run-time index would be copied to scratch and every level's metadata
+    // read through it)
     if (sp_gated(st, gate)) return;
-    const TriDev &t = which == 0 ? sp.fl : which == 1 ? sp.fu : which == 2 ? sp.bu : sp.bl;
     tri_sweep<NRHS>(t, in0, in1, out0, out1, l0, l1);
     if (clr) {
         __syncthreads();
@@ -1355,14 +1412,14 @@ static void run_plan(const SpFactor &F, int which, const SpDev &d, hipStream_t s
             hipLaunchKernelGGL((k_sp_level<NRHS>), dim3(pl[q].blocks), dim3(256), 0, s, t, st, gate, in0, in1, out0,
                                out1, pl[q].l0);
             if (last)
-                hipLaunchKernelGGL((k_sp_sweep<NRHS>), dim3(1), dim3(1024), 0, s, d, which, st, gate, in0, in1, out0,
+                hipLaunchKernelGGL((k_sp_sweep<NRHS>), dim3(1), dim3(1024), 0, s, d, t, st, gate, in0, in1, out0,
                                    out1, 0, 0, 1);
         } else
-            hipLaunchKernelGGL((k_sp_sweep<NRHS>), dim3(1), dim3(1024), 0, s, d, which, st, gate, in0, in1, out0,
+            hipLaunchKernelGGL((k_sp_sweep<NRHS>), dim3(1), dim3(1024), 0, s, d, t, st, gate, in0, in1, out0,
                                out1, pl[q].l0, pl[q].l1, last);
     }
     if (pl.empty() && clr)
-        hipLaunchKernelGGL((k_sp_sweep<NRHS>), dim3(1), dim3(1024), 0, s, d, which, st, gate, in0, in1, out0, out1, 0,
+        hipLaunchKernelGGL((k_sp_sweep<NRHS>), dim3(1), dim3(1024), 0, s, d, t, st, gate, in0, in1, out0, out1, 0,
                            0, 1);
 }
 
