@@ -250,12 +250,14 @@ static __device__ void reset_refsp_dev(const SpxDev &d, int dual)
 }
 
 // h = -N[q] (eval_tcol, glpspx01.js:702-719); runs inside a single workgroup
-static __device__ void build_hq(const SpxDev &d, int q)
+static __device__ void build_hq(const SpxDev &d, int q, bool zeroed = false)
 {
     const int m = d.m;
     const int k = d.head[m + q - 1];
-    for (int i = threadIdx.x; i < m; i += blockDim.x) d.h[i] = 0.0;
-    __syncthreads();
+    if (!zeroed) {                      // (the dual on the sparse factor: zeroed by k_trow_finish)
+        for (int i = threadIdx.x; i < m; i += blockDim.x) d.h[i] = 0.0;
+        __syncthreads();
+    }
     if (k <= m) {
         if (threadIdx.x == 0) d.h[k - 1] = -1.0;
     } else {

@@ -652,6 +652,10 @@ __global__ void __launch_bounds__(256) k_trow_finish(SpxDev d, int pse)
     if (st->stop) return;
     const int m = d.m, n = d.n;
     const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+    // sparse factor: h is free from the previous pivot's FTRAN to this
+    // pivot's pick, so its zero fill runs here on the grid instead of in the
+    // pick's single workgroup (build_hq then writes the column only)
+    if (d.sp && idx < m) d.h[idx] = 0.0;
     const int pos1 = (idx < n) ? d.bind[m + idx] : 0;
     const int pos2 = (idx < m) ? d.bind[idx] : 0;
     const int j1 = (pos1 > m) ? pos1 - m - 1 : -1;
@@ -1618,7 +1622,7 @@ __global__ void __launch_bounds__(1024) k_dual_pick(SpxDev d, int pse, int gn, i
     if (d.st->stop) return;
     int kq = 0;
     const int q = dual_pick(d, pse, gn, ncb, &kq);
-    if (q) build_hq(d, q);
+    if (q) build_hq(d, q, d.sp != nullptr);
 }
 
 // work_c = ys_c - (A w)_c from the partials, fixed order
