@@ -111,6 +111,43 @@ static __device__ int block_or(int v, int *sh)
 
 __device__ __forceinline__ unsigned long long dbits(double v) { return (unsigned long long)__double_as_longlong(v); }
 
+// ---- the entry gate of a multi-block pivot kernel ---------------------------
+// Every block of a pivot kernel reads the scalar state (DState) and the
+// basis header at entry, and one block (the writer) rewrites some of it for
+// the kernels that follow.  The blocks of a launch start on the 8 XCDs
+// independently, so a block can issue its entry loads after the writer has
+// finished and would then read the next pivot's state: the same solve took
+// different pivot paths from run to run (round 4, tools/det_probe.py).  So
+// every block passes gate_arrive once its entry loads have returned, and the
+// writer's stores to anything another block reads at entry wait in
+// gate_wait until every block of the launch has arrived.  Eight arrival words
+// (blockIdx & 7, one per XCD) keep the atomics off a single address.  Only
+// the writer waits, and the other blocks never wait on anything, so the
+// launch drains however its blocks are scheduled.
+//
+// gate_arrive: every thread of the block (a block barrier inside); the
+// s_waitcnt makes each wave's outstanding loads complete before the barrier
+__device__ __forceinline__ void gate_arrive(DState *st)
+{
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) __hip_atomic_fetch_add(&st->gate[blockIdx.x & 7], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// gate_wait: ONE thread of the writer block, after its own block arrived;
+// resets the words for the next launch
+__device__ __forceinline__ void gate_wait(DState *st)
+{
+    const int blocks = (int)gridDim.x;
+    for (int x = 0; x < 8; ++x) {
+        const int want = (blocks - x + 7) >> 3;
+        while (__hip_atomic_load(&st->gate[x], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < want)
+            __builtin_amdgcn_s_sleep(1);
+    }
+    for (int x = 0; x < 8; ++x) __hip_atomic_store(&st->gate[x], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    asm volatile("" ::: "memory");           // the writer's stores stay after the wait
+}
+
 // candidate of an index-choosing scan: key1 (primary), key2 (secondary), idx
 struct Cand {
     double k1, k2;
@@ -228,7 +265,7 @@ __device__ __forceinline__ double get_xN(const signed char *stat, const double *
 }
 
 // reset_refsp (glpspx01.js:586 / glpspx02.js:497)
-static __device__ void reset_refsp_dev(const SpxDev &d, int dual)
+static __device__ void reset_refsp_dev(const SpxDev &d, int dual, bool set_refct = true)
 {
     const int m = d.m, n = d.n;
     for (int k = threadIdx.x; k < m + n; k += blockDim.x) d.refsp[k] = 0;
@@ -245,7 +282,9 @@ static __device__ void reset_refsp_dev(const SpxDev &d, int dual)
         }
     }
     __syncthreads();
-    if (threadIdx.x == 0) d.st->refct = 1000;
+    // (a gated multi-block kernel stores refct with its other scalars, after
+    // gate_wait: set_refct false)
+    if (set_refct && threadIdx.x == 0) d.st->refct = 1000;
     __syncthreads();
 }
 

@@ -364,6 +364,48 @@ __device__ TopState finish_apply(const SpxDev &d, const FinishIn &f, bool tail_s
     return f.t;
 }
 
+// finish_apply split for the gated multi-block kernels (k_dual_row,
+// k_dual_top_grid, k_dual_col): the header arrays early (every other block
+// patches what they change, idempotently), the scalars by one thread of the
+// writer after gate_wait — refct = 1000 when the reference space was reset
+// in between (reset_refsp_dev with set_refct false)
+__device__ __forceinline__ void finish_arrays(const SpxDev &d, const FinishIn &f)
+{
+    const int m = d.m;
+    __syncthreads();                          // every wave of this block has read the header
+    if (f.pend) {
+        if (threadIdx.x == 0) {
+            d.head[f.p - 1] = f.kq;
+            d.head[m + f.q - 1] = f.kp;
+            d.bind[f.kq - 1] = f.p;
+            d.bind[f.kp - 1] = m + f.q;
+            d.stat[f.q - 1] = f.fxp ? NS : (f.delta > 0.0 ? NL : NU);
+        } else if (threadIdx.x == 64) {
+            if (f.rclr) d.refsp[f.kp - 1] = 0;
+        }
+    }
+    __syncthreads();
+}
+
+__device__ __forceinline__ void finish_scalars(const SpxDev &d, const FinishIn &f, bool refsp_reset)
+{
+    DState *st = d.st;
+    if (f.pend) {
+        st->obj = f.t.obj;
+        st->upd_cnt = f.upd_cnt + 1;
+        st->binv_fresh = 0;
+        st->cbar_fresh = 0;
+        st->refact_pending = f.t.refact;
+        st->it_cnt = f.it_cnt + 1;
+        st->npiv = f.npiv + 1;
+        st->iter_left = f.t.iter_left;
+        if (f.rig > 0) st->rigorous = f.rig - 1;
+        st->refct = f.t.refct;
+        st->pend = 0;
+    }
+    if (refsp_reset) st->refct = 1000;
+}
+
 __device__ TopState dual_finish_block(const SpxDev &d, bool tail_sync)
 {
     return finish_apply(d, finish_load(d), tail_sync);
@@ -596,22 +638,32 @@ __global__ void __launch_bounds__(256) k_dual_top_grid(SpxDev d)
         why = ST_OBJLIM;
     const Cand best = wave_best<0>(cc);
     if (why == ST_RUN && best.idx == 0) why = ST_P0;
-    if (lead) {
-        (void)finish_apply(d, fin, true);
-        if (why != ST_RUN) {
+    // every block passes the entry gate before block 0 stores the state
+    // (gk_device.h); the header arrays it changes are not read here
+    gate_arrive(st);
+    if (why != ST_RUN) {
+        if (lead) {
+            if (threadIdx.x == 0) gate_wait(st);
+            finish_arrays(d, fin);
             if (threadIdx.x == 0) {
+                finish_scalars(d, fin, false);
                 if (why == ST_P0) st->p = 0;
                 st->stop = why;
             }
-            return;
         }
-        if (pricing == PT_PSE && ts.refct == 0) {
-            reset_refsp_dev(d, 1);            // refsp := basic variables, gamma := 1
+        return;
+    }
+    const bool reset = pricing == PT_PSE && ts.refct == 0;
+    if (lead) {
+        if (threadIdx.x == 0) gate_wait(st);
+        finish_arrays(d, fin);
+        if (reset) {
+            reset_refsp_dev(d, 1, false);     // refsp := basic variables, gamma := 1
             for (int l = threadIdx.x; l < n; l += blockDim.x) d.wpos[l] = -1;
             if (threadIdx.x == 0) st->nwl = 0;
         }
+        if (threadIdx.x == 0) finish_scalars(d, fin, reset);
     }
-    if (why != ST_RUN) return;
     const int p = best.idx, kp = best.aux;
     const double *brow = d.Binv + (p - 1);
     const size_t ldb = (size_t)d.ldb;
@@ -908,22 +960,29 @@ __global__ void __launch_bounds__(1024) k_dual_row(SpxDev d, int pse, int nr_cap
     const Cand best = wave_best<0>(cc);
     if (why == ST_RUN && best.idx == 0) why = ST_P0;
     const bool reset = (why == ST_RUN && pricing == PT_PSE && ts.refct == 0);
-    if (lead) {
-        (void)finish_apply(d, fin, true);
-        if (why != ST_RUN) {
+    if (why != ST_RUN) {
+        // (every block agrees: the state it decided on is not stored until
+        // all blocks have read it)
+        gate_arrive(st);
+        if (lead) {
+            if (threadIdx.x == 0) gate_wait(st);
+            finish_arrays(d, fin);
             if (threadIdx.x == 0) {
+                finish_scalars(d, fin, false);
                 if (why == ST_P0) st->p = 0;
                 st->stop = why;
             }
-            return;
         }
+        return;
+    }
+    if (lead) {
+        finish_arrays(d, fin);
         if (reset) {
-            reset_refsp_dev(d, 1);            // refsp := basic variables, gamma := 1
+            reset_refsp_dev(d, 1, false);     // refsp := basic variables, gamma := 1
             for (int l = threadIdx.x; l < n; l += blockDim.x) d.wpos[l] = -1;
             if (threadIdx.x == 0) st->nwl = 0;
         }
     }
-    if (why != ST_RUN) return;
     const int p = best.idx, kp = best.aux;
     const int ns = nr + (kp <= m ? 1 : 0);
     // the pending change of basis, as seen by this block
@@ -1029,10 +1088,12 @@ __global__ void __launch_bounds__(1024) k_dual_row(SpxDev d, int pse, int nr_cap
     }
     TPH(1, 1);
     sp[w][lane] = (idx < n) ? acc : 0.0;
-    __syncthreads();
+    gate_arrive(st);                         // (the block barrier of the LDS combine)
     TPH(1, 2);
     if (w != 0) return;                      // wave 0 only from here: no block barriers
     if (lead && lane == 0) {
+        gate_wait(st);
+        finish_scalars(d, fin, reset);
         st->p = p;
         st->kp = kp;
         st->delta = best.k2;
@@ -1156,22 +1217,29 @@ __global__ void __launch_bounds__(256) k_dual_col(SpxDev d, int pse, int nr_cap,
     const Cand best = wave_best<0>(cc);
     if (why == ST_RUN && best.idx == 0) why = ST_P0;
     const bool reset = (why == ST_RUN && pricing == PT_PSE && ts.refct == 0);
-    if (lead) {
-        (void)finish_apply(d, fin, true);
-        if (why != ST_RUN) {
+    // every block passes the entry gate before block 0 stores the state
+    // (gk_device.h); the header arrays it changes early are patched below
+    gate_arrive(st);
+    if (why != ST_RUN) {
+        if (lead) {
+            if (threadIdx.x == 0) gate_wait(st);
+            finish_arrays(d, fin);
             if (threadIdx.x == 0) {
+                finish_scalars(d, fin, false);
                 if (why == ST_P0) st->p = 0;
                 st->stop = why;
             }
-            return;
         }
+        return;
+    }
+    if (lead) {
+        finish_arrays(d, fin);
         if (reset) {
-            reset_refsp_dev(d, 1);            // refsp := basic variables, gamma := 1
+            reset_refsp_dev(d, 1, false);     // refsp := basic variables, gamma := 1
             for (int l = threadIdx.x; l < n; l += blockDim.x) d.wpos[l] = -1;
             if (threadIdx.x == 0) st->nwl = 0;
         }
     }
-    if (why != ST_RUN) return;
     const int p = best.idx, kp = best.aux;
     const int ns = nr + (kp <= m ? 1 : 0);
     auto bind_new = [&](int k1, int v) {
@@ -1234,15 +1302,15 @@ __global__ void __launch_bounds__(256) k_dual_col(SpxDev d, int pse, int nr_cap,
             d.rho_val[t] = (t < nr) ? brow[(size_t)c * ldb] : 1.0;
         }
     }
-    if (lead) {
-        if (threadIdx.x == 0) {
-            st->p = p;
-            st->kp = kp;
-            st->delta = best.k2;
-            st->trow_max_bits = 0ull;
-            st->ns = ns;
-            st->dinf = 0;
-        }
+    if (lead && threadIdx.x == 0) {
+        gate_wait(st);
+        finish_scalars(d, fin, reset);
+        st->p = p;
+        st->kp = kp;
+        st->delta = best.k2;
+        st->trow_max_bits = 0ull;
+        st->ns = ns;
+        st->dinf = 0;
     }
     double tv1 = (j1 >= 0) ? acc : 0.0;
     double tv2 = (j2 >= 0) ? -rho2 : 0.0;
@@ -2460,7 +2528,9 @@ __global__ void __launch_bounds__(1024) k_dual_update(SpxDev d, int gn, int ncb,
     if (NRHS == 2) sp[NRHS - 1][w][lane] = b;
     if (NRHS == 2 && w == 0 && sl == 0) sub[rl] = ub;
     TPH(3, 2);
-    __syncthreads();
+    // (the block barrier of the LDS combine) every block's entry loads —
+    // st->nr among them — are done before block 0's books store the lists
+    gate_arrive(st);
     // the three fixed-order sums (tcol and u of the block's rows, alpha_p)
     // are independent chains of nw * SL dependent adds: each in its own wave
     // (the lanes of the block's rows in the waves of tcol and u) so that they
@@ -2498,7 +2568,10 @@ __global__ void __launch_bounds__(1024) k_dual_update(SpxDev d, int gn, int ncb,
     const bool bad = fabs(piv1 - piv2) > 1e-8 * (1.0 + fabs(piv1)) ||
                      !((piv1 > 0.0 && piv2 > 0.0) || (piv1 < 0.0 && piv2 < 0.0));
     if (bad && (!binv_fresh || !rig)) {
-        if (lead) { st->q = q; st->kq = kq; st->stop = ST_PIVCHK; }
+        if (lead) {
+            gate_wait(st);                          // (resets the gate: no books this launch)
+            st->q = q; st->kq = kq; st->stop = ST_PIVCHK;
+        }
         return;
     }
     const double tp = bad ? piv2 : piv1;
@@ -2510,8 +2583,12 @@ __global__ void __launch_bounds__(1024) k_dual_update(SpxDev d, int gn, int ncb,
     // fetches), so the books wave starts it here, under wave 0's row and
     // column updates and the phase-I barrier below, instead of after them.
     // Nothing later in this kernel reads what it writes (the other blocks
-    // read the compact rho, not the lists, and st->nr / st->nwl in trip 1)
-    if (bk && w == wa && lane == 0) books_store<NRHS>(d, sbk, kp, kq, tkp, refkp, nr, ns, rowpath, bytes_fixed);
+    // read the compact rho, not the lists); st->nr / st->nwl, which every
+    // block reads in trip 1, only once all blocks have passed the gate
+    if (bk && w == wa && lane == 0) {
+        gate_wait(st);
+        books_store<NRHS>(d, sbk, kp, kq, tkp, refkp, nr, ns, rowpath, bytes_fixed);
+    }
     // ---- product-form update of the entries held in registers
     {
         const bool z = (r == p - 1);

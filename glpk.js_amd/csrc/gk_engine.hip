@@ -173,6 +173,7 @@ struct Engine {
     DBuf<char> upstage;                         // device side of the coalesced uploads
     DBuf<int> xlist;                            // eval_cbar: basic slacks with a nonzero cost (primal phase I)
     DBuf<unsigned long long> tslots, xslots;
+    DBuf<unsigned long long> dethash;           // GK_DET_LOG fingerprints
     // MFMA pricing panel (gk_panel.hip), dense A only, sized for PANEL_MAX rows
     DBuf<double> pnl, pnl_src;
     DBuf<int> pslot, ppos;
@@ -267,7 +268,7 @@ struct Engine {
         if (arena) (void)hipFree(arena);
         if (st_host) (void)hipHostFree(st_host);
         if (pin) (void)hipHostFree(pin);
-        upstage.release(); xlist.release();
+        upstage.release(); xlist.release(); dethash.release();
     }
 };
 
@@ -683,6 +684,29 @@ static double bits_double(unsigned long long b)
     return v;
 }
 
+// GK_DET_LOG=<file> (tools/det_probe.py): a fingerprint of the device state
+// after every batch and re-inversion — a wrapping sum of mixed (index, word)
+// pairs, independent of the summation order — so that two solves of the same
+// input can be compared batch by batch and the first divergence located
+__global__ void k_det_hash(const unsigned *__restrict__ w, size_t nw, unsigned long long *out)
+{
+    unsigned long long acc = 0;
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < nw; i += (size_t)gridDim.x * blockDim.x) {
+        unsigned long long z = (i + 1) * 0x9E3779B97F4A7C15ull ^ ((unsigned long long)w[i] << 17 | w[i]);
+        z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+        z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+        acc += z ^ (z >> 31);
+    }
+    for (int o = 32; o > 0; o >>= 1) acc += __shfl_down(acc, o);
+    if ((threadIdx.x & 63) == 0) atomicAdd(out, acc);
+}
+
+static const char *det_log_path()
+{
+    static const char *p = std::getenv("GK_DET_LOG");
+    return p;
+}
+
 // ---------------------------------------------------------------------------
 // the simplex driver
 // ---------------------------------------------------------------------------
@@ -1068,6 +1092,33 @@ struct Spx {
     }
     bool kept = false;                                 // init kept the resident working set
     int reinv_calls = 0;                               // re-inversions in this call
+
+    // one GK_DET_LOG line: the state fingerprints after a batch / re-inversion
+    void det_log(const char *what, int K = 0, int why = 0)
+    {
+        const char *path = det_log_path();
+        if (!path) return;
+        const size_t ldb = f->sparse ? 0 : (size_t)f->ldb;
+        struct Part { const void *p; size_t bytes; } parts[6] = {
+            {E->head.p, ((size_t)m + n) * sizeof(int)}, {E->stat.p, (size_t)n & ~(size_t)3},
+            {E->bbar.p, (size_t)m * sizeof(double)}, {E->cbar.p, (size_t)n * sizeof(double)},
+            {E->gamma.p, (size_t)(dual ? m : n) * sizeof(double)}, {f->Binv.p, ldb * m * sizeof(double)}};
+        E->dethash.ensure(6);
+        HIPCHK(hipMemsetAsync(E->dethash.p, 0, 6 * sizeof(unsigned long long), s));
+        for (int t = 0; t < 6; t++)
+            if (parts[t].p && parts[t].bytes >= 4)
+                hipLaunchKernelGGL(k_det_hash, dim3(512), dim3(256), 0, s, (const unsigned *)parts[t].p,
+                                   parts[t].bytes / 4, E->dethash.p + t);
+        unsigned long long hsh[6];
+        HIPCHK(hipMemcpyAsync(hsh, E->dethash.p, sizeof hsh, hipMemcpyDeviceToHost, s));
+        HIPCHK(hipStreamSynchronize(s));
+        FILE *fp = std::fopen(path, "a");
+        if (!fp) return;
+        std::fprintf(fp, "%s it %d K %d why %d p %d q %d ph %d nr %d upd %d/%d head %016llx stat %016llx bbar %016llx "
+                     "cbar %016llx gamma %016llx binv %016llx\n", what, hs.it_cnt, K, why, hs.p, hs.q, phase, hs.nr,
+                     hs.upd_cnt, hs.upd_lim, hsh[0], hsh[1], hsh[2], hsh[3], hsh[4], hsh[5]);
+        std::fclose(fp);
+    }
 
     void rsub_into(double *y, const double *a);   // y = a - y
 
@@ -1793,6 +1844,7 @@ int Spx::batch(int K, int rigorous)
     const double t0 = now_s();
     struct T { gk_bfd *f; double t0; ~T() { f->stats.seconds_batches += now_s() - t0; } } tt{f, t0};
     hs.stop = ST_RUN;
+    std::memset(hs.gate, 0, sizeof hs.gate);   // (0 between launches; a clean start whatever a failed run left)
     hs.iter_left = K;
     hs.npiv = 0;
     hs.phase = phase;
@@ -2007,10 +2059,12 @@ int Spx::run_dual()
         if (binv_st == 0) {
             pull();
             drift_arm(cbar, cbar_st);
+            const long long nref0 = f->stats.refinements;
             if (!reinvert()) {
                 report_msg(GK_MSG_FACTERR, 1, fact_ret);     // GLP_MSG_ERR
                 return fail_return();
             }
+            det_log(f->stats.refinements != nref0 ? "reinv-newton" : "reinv");
             binv_st = 1;
             bbar_st = cbar_st = 0;
             hs.upd_cnt = 0; hs.refact_pending = 0; hs.grow_bits = 0;
@@ -2150,6 +2204,7 @@ int Spx::run_dual()
         K = align_to_refactor(K, hs.upd_lim - hs.upd_cnt);
         K = align_to_display(K);
         int why = batch(K, rigorous);
+        det_log("batch", K, why);
         E->kbatch = next_batch(E->kbatch, why);
         dinf_known = (why == ST_BATCH && hs.npiv > 0);
         if (hs.npiv > 0) {
@@ -2225,10 +2280,12 @@ int Spx::run_primal()
         if (binv_st == 0) {
             pull();
             drift_arm(bbar, bbar_st);
+            const long long nref0 = f->stats.refinements;
             if (!reinvert()) {
                 report_msg(GK_MSG_FACTERR, 1, fact_ret);     // GLP_MSG_ERR
                 return fail_return();
             }
+            det_log(f->stats.refinements != nref0 ? "reinv-newton" : "reinv");
             binv_st = 1;
             bbar_st = cbar_st = 0;
             hs.upd_cnt = 0; hs.refact_pending = 0; hs.grow_bits = 0;
@@ -2310,6 +2367,7 @@ int Spx::run_primal()
         K = align_to_refactor(K, hs.upd_lim - hs.upd_cnt);
         K = align_to_display(K);
         int why = batch(K, rigorous);
+        det_log("batch", K, why);
         E->kbatch = next_batch(E->kbatch, why);
         if (hs.npiv > 0) {
             bbar_st = 2;

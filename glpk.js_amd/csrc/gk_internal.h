@@ -79,6 +79,10 @@ struct DState {
     // fill of the batch; hits and refills so far
     int pk, pcur, pmiss, pvalid;
     double phits, pmisses;
+    // the entry gate of the multi-block pivot kernels (gk_device.h,
+    // gate_arrive / gate_wait): arrivals per XCD slot of blockIdx, 0 between
+    // launches
+    int gate[8];
 };
 
 // ---- dense GEMV helpers ---------------------------------------------------

@@ -876,12 +876,18 @@ __global__ void __launch_bounds__(256) k_primal_commit(SpxDev d, int pse, int nv
             }
         }
         if (stop) return;
+        // every block's entry loads (the header and the counters block 0
+        // rewrites below) are done before block 0 stores them (gk_device.h)
+        gate_arrive(st);
         double pivot = 0.0, new_dq = 0.0, cq_new = 0.0;
         if (p > 0) {
             const bool bad = fabs(piv1 - piv2) > 1e-8 * (1.0 + fabs(piv1)) ||
                              !((piv1 > 0.0 && piv2 > 0.0) || (piv1 < 0.0 && piv2 < 0.0));
             if (bad && (!binv_fresh || !rig)) {
-                if (blockIdx.x == 0 && threadIdx.x == 0) st->stop = ST_PIVCHK;
+                if (blockIdx.x == 0 && threadIdx.x == 0) {
+                    gate_wait(st);
+                    st->stop = ST_PIVCHK;
+                }
                 return;
             }
             pivot = bad ? piv1 : piv2;
@@ -939,6 +945,7 @@ __global__ void __launch_bounds__(256) k_primal_commit(SpxDev d, int pse, int nv
             if (__syncthreads_or(bad) && threadIdx.x == 0) atomicOr(&st->dinf, 1);
         }
         if (blockIdx.x == 0 && threadIdx.x == 0) {
+            gate_wait(st);
             // change_basis (:2035-2055) and the counters of finish_pivot
             if (p > 0) {
                 d.head[p - 1] = kq;
@@ -1005,15 +1012,15 @@ __global__ void __launch_bounds__(256) k_primal_commit(SpxDev d, int pse, int nv
         }
         return;
     }
-    if (p <= 0) return;
-    // rank-1 update over the dense columns (the compact rho: ns entries)
+    // rank-1 update over the dense columns (the compact rho: ns entries);
+    // every thread loads, then passes the entry gate, then works (or not)
     const int b = blockIdx.x - nvb;
     const int tile = b % tiles, chunk = b / tiles;
     const int t0 = chunk * lpsu;
     const int r = (tile * 256 + threadIdx.x) * 2;
-    if (r >= m) return;
-    const bool two = (r + 1 < m);
-    const double tr0 = d.tcol[r], tr1 = two ? d.tcol[r + 1] : 0.0;
+    const bool act = p > 0 && r < m;
+    const bool two = act && (r + 1 < m);
+    const double tr0 = act ? d.tcol[r] : 0.0, tr1 = two ? d.tcol[r + 1] : 0.0;
     constexpr int U = 4;
     int cc[U];
     double rl[U];
@@ -1025,14 +1032,16 @@ __global__ void __launch_bounds__(256) k_primal_commit(SpxDev d, int pse, int nv
     }
     const int ns = st->ns;
     const int binv_fresh = st->binv_fresh, rig = st->rigorous;
-    const int t1 = min(ns, t0 + lpsu);
-    const double piv1 = d.tcol[p - 1], piv2 = d.trow[q - 1];
+    const int t1 = act ? min(ns, t0 + lpsu) : t0;
+    const double piv1 = d.tcol[pp - 1], piv2 = d.trow[q - 1];
     const int ce = (kq <= m) ? kq - 1 : -1;
     double2 v0[U];
 #pragma unroll
     for (int u = 0; u < U; ++u)
         if (t0 + u < t1) v0[u] = *(const double2 *)(d.Binv + (size_t)cc[u] * d.ldb + r);
     if (stop) return;
+    gate_arrive(st);
+    if (!act) return;
     const bool bad = fabs(piv1 - piv2) > 1e-8 * (1.0 + fabs(piv1)) ||
                      !((piv1 > 0.0 && piv2 > 0.0) || (piv1 < 0.0 && piv2 < 0.0));
     if (bad && (!binv_fresh || !rig)) return;
