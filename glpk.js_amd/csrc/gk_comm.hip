@@ -152,7 +152,15 @@ struct gk_comm {
     hipStream_t stream = nullptr;
     char *dbuf = nullptr;                 // device staging: send block | gathered blocks
     size_t dcap = 0;
-    std::atomic<unsigned long long> *inc = nullptr;   // the shared incumbent word (same host), or null
+    // the shared incumbent words (same host), or null: word (search & 1)
+    // serves the current sharded search.  Every rank enters each search of
+    // the communicator in the same order, so `search` agrees; a search resets
+    // the NEXT search's word at entry, when no rank can be publishing into it
+    // (the previous search ended in an all-gather every rank joined, and the
+    // next has not begun), so a second glp_intopt on the same communicator
+    // never sees the first one's incumbent
+    std::atomic<unsigned long long> *inc = nullptr;
+    unsigned search = 0;
     ~gk_comm()
     {
         if (inc) (void)munmap((void *)inc, 4096);
@@ -291,7 +299,10 @@ extern "C" gk_comm *gk_comm_create(gk_ctx *ctx, int rank, int size, const char *
                 ok = fd >= 0 && ftruncate(fd, 4096) == 0;
                 if (ok) p = mmap(nullptr, 4096, PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
                 ok = ok && p != MAP_FAILED;
-                if (ok) new (p) std::atomic<unsigned long long>(ord_key(DBL_MAX));
+                if (ok) {
+                    new (p) std::atomic<unsigned long long>(ord_key(DBL_MAX));
+                    new ((std::atomic<unsigned long long> *)p + 1) std::atomic<unsigned long long>(ord_key(DBL_MAX));
+                }
             }
             std::vector<int> oks(size);
             // rank 0's segment exists (or not) before the others open it
@@ -428,10 +439,11 @@ extern "C" int gk_comm_rank(const gk_comm *c) { return c ? c->rank : -1; }
 extern "C" double gk_comm_incumbent(gk_comm *c, double mine)
 {
     if (!c || !c->inc) return mine;
+    std::atomic<unsigned long long> *w = c->inc + (c->search & 1);
     const unsigned long long k = ord_key(mine);
-    unsigned long long cur = c->inc->load(std::memory_order_relaxed);
-    while (k < cur && !c->inc->compare_exchange_weak(cur, k, std::memory_order_acq_rel)) {}
-    return ord_val(std::min(k, c->inc->load(std::memory_order_acquire)));
+    unsigned long long cur = w->load(std::memory_order_relaxed);
+    while (k < cur && !w->compare_exchange_weak(cur, k, std::memory_order_acq_rel)) {}
+    return ord_val(std::min(k, w->load(std::memory_order_acquire)));
 }
 
 extern "C" int gk_comm_shared_incumbent(const gk_comm *c) { return c && c->inc ? 1 : 0; }
@@ -455,6 +467,15 @@ extern "C" int gk_ios_driver_comm(gk_ctx *ctx, gk_mip *mip, const gk_iocp *parm,
     using gk::set_err;
     if (!comm) { set_err("gk_ios_driver_comm: null communicator"); return GK_EABI; }
     if (comm->size == 1 && comm->backend != GK_COMM_RCCL) return gk_ios_driver(ctx, mip, parm);
+    // this search's incumbent word (gk_comm::inc); the next one's is cleared
+    struct SearchScope {
+        gk_comm *c;
+        explicit SearchScope(gk_comm *cc) : c(cc)
+        {
+            if (c->inc) c->inc[(c->search + 1) & 1].store(ord_key(DBL_MAX), std::memory_order_relaxed);
+        }
+        ~SearchScope() { c->search++; }
+    } scope(comm);
     gk_ios_shard sh{};
     sh.rank = comm->rank;
     sh.size = comm->size;

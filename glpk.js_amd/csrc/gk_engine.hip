@@ -1595,7 +1595,8 @@ int Spx::reinvert_core_csc(const BasisSplit &bs, bool refine)
 bool Spx::resident_match() const
 {
     const Engine::Resident &R = E->res;
-    if (!R.ok || R.dual != dual || R.m != m || R.n != n) return false;
+    // (fastv: init found the record valid and took its arrays, clearing ok)
+    if (!(R.ok || fastv) || R.dual != dual || R.m != m || R.n != n) return false;
     if (lp->a_version == 0 || lp->a_version != R.a_version) return false;
     if (!f->valid || f->ext_upd || R.fact_ver != f->fact_ver || lists_stale) return false;
     if (std::memcmp(&R.zeta, &zeta, sizeof zeta) != 0) return false;
@@ -1665,6 +1666,10 @@ void Spx::init()
     bind.assign(mn, 0);
     gamma.assign(std::max(m, n) + 1, 0.0);
     if (fastv) {
+        // the record gives its arrays away here: it is no longer valid, even
+        // if a check below throws before the call gets under way (a retry
+        // with the same versions must rebuild, not take the spare vectors)
+        R0.ok = false;
         type.swap(R0.type); orig_type.swap(R0.orig_type); lb.swap(R0.lb); ub.swap(R0.ub);
         orig_lb.swap(R0.orig_lb); orig_ub.swap(R0.orig_ub); coef.swap(R0.coef); obj.swap(R0.obj);
         zeta = R0.zeta;

@@ -88,7 +88,9 @@ int     gk_bfd_set_parm(gk_bfd *bfd, const gk_bfcp *parm);   /* 0 | GK_EABI (inv
  * drift measured at each re-inversion stays below tol / 200; the first
  * drift above tol / 20 drops it to nfs_max = 100, and it lengthens again
  * only over two clean chains).  gk_bfd_set_parm marks its values
- * explicit: nfs_max / nrs_max then hold exactly, 100 included.  A new
+ * explicit: nfs_max / nrs_max then hold exactly, 100 included — on the
+ * explicit inverse; the sparse factor's Schur-complement chain holds at most
+ * 256 updates, so there an explicit value above 256 is capped at 256.  A new
  * factor starts in the default state.  (ABI 8) */
 int     gk_bfd_reset_parm(gk_bfd *bfd);
 /* diagnostics of the sparse factor (gk_sparse.hip; ABI 8), host only: the
@@ -372,7 +374,9 @@ int      gk_comm_allgather(void *comm, const void *send, size_t bytes, void *rec
  * objective published so far (an atomic min on an order-preserving image of
  * the double).  gk_comm_incumbent publishes mine and returns the best over
  * the ranks (mine itself without a shared word); the sharded search calls it
- * before every batch (internal minimisation form, DBL_MAX: none).
+ * before every batch (internal minimisation form, DBL_MAX: none).  Each
+ * gk_ios_driver_comm search of comm has a word of its own: a later search on
+ * the same communicator starts from DBL_MAX, not from an earlier one's best.
  * gk_comm_shared_incumbent: 1 when the word exists. */
 double   gk_comm_incumbent(gk_comm *comm, double mine);
 int      gk_comm_shared_incumbent(const gk_comm *comm);

@@ -38,6 +38,11 @@ function context() {
 }
 
 function nextVersion() { return ++version; }
+// while > 0 every solve hands the engine b_version 0 (bounds / costs
+// unknown: init_csa rebuilds and compares): the shim holds it around
+// reference code that writes an lp's bounds or costs directly
+var bvHold = 0;
+function bversionHold(d) { bvHold += d; return bvHold; }
 
 // ---- lp.bfd (glpbfd.js) ------------------------------------------------------
 function bfdCreate() {
@@ -139,7 +144,7 @@ function marshal(lp, g) {
     marshalMatrix(lp, g);
     return {
         m: m, n: n, nnz: lp.nnz, dir: lp.dir, c0: lp.c0, a_version: g.a_version, it_cnt: lp.it_cnt,
-        b_version: lp.__gk_bversion || 0,
+        b_version: bvHold > 0 ? 0 : (lp.__gk_bversion || 0),
         row_type: g.row_type, row_lb: g.row_lb, row_ub: g.row_ub, rii: g.rii,
         col_type: g.col_type, col_lb: g.col_lb, col_ub: g.col_ub, col_coef: g.col_coef, sjj: g.sjj,
         A_ptr: g.A_ptr, A_ind: g.A_ind, A_val: g.A_val, head: g.head,
@@ -301,7 +306,7 @@ function iosDriver(T, print) {
 }
 
 module.exports = {
-    addon: addon, context: context, nextVersion: nextVersion,
+    addon: addon, context: context, nextVersion: nextVersion, bversionHold: bversionHold,
     bfdCreate: bfdCreate, bfdSetParm: bfdSetParm, bfdResetParm: bfdResetParm, bfdFactorize: bfdFactorize,
     bfdFtran: bfdFtran, bfdBtran: bfdBtran, bfdUpdate: bfdUpdate, bfdGetCount: bfdGetCount,
     spx: spx, iosDriver: iosDriver, nativeIos: nativeIos, GLP_BS: GLP_BS, mipProgressLine: mipProgressLine,

@@ -143,9 +143,13 @@ glp_adv_basis = exports["glp_adv_basis"] = function (lp, flags) {
         };
     }
     // bounds, types, costs, dir and scale factors: lp.__gk_bversion (the
-    // engine skips init_csa's rebuild while it is unchanged).  The reference
-    // writes bounds directly only inside glp_analyze_bound / _coef
-    // (glpapi12.js:1098-1120): the version is unknown (0) during those calls
+    // engine skips init_csa's rebuild while it is unchanged).  Outside the
+    // wrapped mutators the reference writes them directly in two places:
+    // glp_analyze_bound / _coef (glpapi12.js:1098-1120) on the lp they are
+    // given — its version is unknown (0) during those calls — and
+    // ios_feas_pump (glpios10.js:186-247) on its working copy of the MIP
+    // (objective, dir, c0, column bounds and types between its glp_simplex
+    // calls) — every solve runs without a version while it is active
     function bversioned(f) {
         return function (lp) {
             var r = f.apply(this, arguments);
@@ -169,6 +173,12 @@ glp_adv_basis = exports["glp_adv_basis"] = function (lp, flags) {
         var f = eval(name);
         eval(name + " = exports[name] = bunknown(f)");
     });
+    var feas_pump = ios_feas_pump;
+    ios_feas_pump = function (T) {
+        __gk.bversionHold(+1);
+        try { return feas_pump(T); } finally { __gk.bversionHold(-1); }
+    };
+    exports["__gk_ios_feas_pump"] = ios_feas_pump;
     glp_set_mat_row = exports["glp_set_mat_row"] = versioned(glp_set_mat_row);
     glp_set_mat_col = exports["glp_set_mat_col"] = versioned(glp_set_mat_col);
     glp_load_matrix = exports["glp_load_matrix"] = versioned(glp_load_matrix);

@@ -36,6 +36,16 @@ assert.strictEqual(core.nativeIos({mip: {m: 2, n: 3}, parm: {cb_func: null, mip_
 assert.strictEqual(core.nativeIos({mip: {m: 80, n: 200}, parm: {cb_func: null, mip_gap: 0}}), true);
 assert.strictEqual(core.nativeIos({mip: {m: 30000, n: 40000}, parm: {cb_func: null, mip_gap: 0}}), false);
 glpk.glp_set_print_func(function () {});
+// the feasibility pump writes its working lp's objective and bounds
+// directly (glpios10.js:186-247): while it runs, every solve hands the
+// engine b_version 0 (the hold is released on every exit, a throw included)
+(function () {
+    var seen = -1, fake = {};
+    Object.defineProperty(fake, 'mip', {get: function () { seen = core.bversionHold(0); throw new Error('probe'); }});
+    assert.throws(function () { glpk.__gk_ios_feas_pump(fake); }, /probe/);
+    assert.strictEqual(seen, 1, 'b_version held inside ios_feas_pump');
+    assert.strictEqual(core.bversionHold(0), 0, 'hold released');
+})();
 // glp_adv_basis through the shim (host code in the library, no device): the
 // reference's statuses and printed lines on its fixtures (tests/golden/adv_*)
 (function () {

@@ -155,6 +155,58 @@ def test_gpu_sharded_bnb_library_comm(name, ramp):
     assert xs[0] == xs[1], "ranks disagree on the incumbent"
 
 
+def _two_mips_worker(rank, size, port, names, q):
+    try:
+        import sys
+        root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+        sys.path.insert(0, root)
+        import __graft_entry__
+        __graft_entry__.load_package()
+        from glpk_js_amd import gk as g, problems as pr
+        ctx = g.Context(0)
+        comm = g.Comm(ctx, rank, size, f"127.0.0.1:{port}")
+        out = []
+        for name in names:
+            d = load_golden(os.path.join(root, "tests", "golden", f"mip_{name}.json"))
+            P = g.GkProblem(ctx, pr.from_fixture(d))
+            assert g.glp_simplex(P, g.SMCP(msg_lev=g.GLP_MSG_OFF)) == 0
+            ret = g.glp_intopt(P, g.IOCP(msg_lev=g.GLP_MSG_OFF), comm=comm)
+            out.append((name, ret, P.mip_stat, P.mip_obj, P.col_mipx[1:].tolist()))
+            del P
+        q.put((rank, comm.shared_incumbent, out))
+        comm.close()
+    except Exception as e:
+        q.put((rank, None, repr(e)))
+
+
+@pytest.mark.gpu
+def test_gpu_sharded_two_searches_one_comm():
+    """Two different MIPs one after the other on ONE 2-rank communicator
+    (the ranks share the incumbent word between epochs): the second search
+    must not inherit the first one's incumbent — a maximisation with a large
+    objective (C5s, 15039 -> -15039 in minimisation form) before a
+    minimisation (gap, 261) would otherwise prune the whole second tree.
+    Both searches reach the reference's optimum on both ranks."""
+    names = ["c5s_12x20", "gap", "c5s_12x20"]
+    refs = {n: load_golden(os.path.join(os.path.dirname(__file__), "golden", f"mip_{n}.json"))["mip"] for n in names}
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = free_port()
+    ps = [ctx.Process(target=_two_mips_worker, args=(r, 2, port, names, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    res = sorted([q.get(timeout=240) for _ in range(2)], key=lambda t: t[0])
+    for p in ps:
+        p.join(timeout=60)
+    for rank, shared, out in res:
+        assert shared is True, (rank, out)
+        for name, ret, stat, obj, x in out:
+            ref = refs[name]
+            assert ret == ref["ret"] and stat == ref["mip_stat"], (rank, name, ret, stat)
+            assert abs(obj - ref["mip_obj"]) <= 1e-9 * max(1.0, abs(ref["mip_obj"])), (rank, name, obj)
+    assert [o[4] for o in res[0][2]] == [o[4] for o in res[1][2]], "ranks disagree on an incumbent"
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("name,gap", [("gap", 0.05), ("gap", 0.002), ("c5s_12x20", 0.01)])
 def test_gpu_sharded_bnb_mip_gap(name, gap):
