@@ -134,15 +134,54 @@ __device__ __forceinline__ void gate_arrive(DState *st)
     if (threadIdx.x == 0) __hip_atomic_fetch_add(&st->gate[blockIdx.x & 7], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// The same gate without a waiting writer, for state every block can compute
+// itself: each block arrives with a returning add (thread 0, after the
+// s_waitcnt and the block barrier, as gate_arrive), and the block whose add
+// completes the count — the last of its XCD slot, then the last of the slots
+// on gate_top — is the one that stores the state (its own entry loads and
+// every other block's are done by then) and clears the words.  The add's
+// round trip overlaps the block's remaining work: gate_last is called at its
+// end.  gate_arrive_ret: every thread; returns the slot count before the add
+// in thread 0.
+__device__ __forceinline__ int gate_arrive_ret(DState *st)
+{
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    int a = 0;
+    if (threadIdx.x == 0) a = __hip_atomic_fetch_add(&st->gate[blockIdx.x & 7], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return a;
+}
+
+// thread 0 of every block, with gate_arrive_ret's value: true in the last block
+__device__ __forceinline__ bool gate_last(DState *st, int a)
+{
+    const int blocks = (int)gridDim.x, x = (int)(blockIdx.x & 7);
+    if (a != ((blocks - x + 7) >> 3) - 1) return false;
+    const int slots = blocks < 8 ? blocks : 8;
+    if (__hip_atomic_fetch_add(&st->gate_top, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != slots - 1) return false;
+#pragma unroll
+    for (int y = 0; y < 8; ++y) __hip_atomic_store(&st->gate[y], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(&st->gate_top, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    asm volatile("" ::: "memory");
+    return true;
+}
+
 // gate_wait: ONE thread of the writer block, after its own block arrived;
 // resets the words for the next launch
 __device__ __forceinline__ void gate_wait(DState *st)
 {
     const int blocks = (int)gridDim.x;
-    for (int x = 0; x < 8; ++x) {
-        const int want = (blocks - x + 7) >> 3;
-        while (__hip_atomic_load(&st->gate[x], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < want)
-            __builtin_amdgcn_s_sleep(1);
+    // the eight words polled together (one memory round trip per poll, not
+    // eight dependent ones)
+    for (;;) {
+        int v[8];
+#pragma unroll
+        for (int x = 0; x < 8; ++x) v[x] = __hip_atomic_load(&st->gate[x], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        bool all = true;
+#pragma unroll
+        for (int x = 0; x < 8; ++x) all = all && v[x] >= ((blocks - x + 7) >> 3);
+        if (all) break;
+        __builtin_amdgcn_s_sleep(1);
     }
     for (int x = 0; x < 8; ++x) __hip_atomic_store(&st->gate[x], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     asm volatile("" ::: "memory");           // the writer's stores stay after the wait

@@ -1088,19 +1088,9 @@ __global__ void __launch_bounds__(1024) k_dual_row(SpxDev d, int pse, int nr_cap
     }
     TPH(1, 1);
     sp[w][lane] = (idx < n) ? acc : 0.0;
-    gate_arrive(st);                         // (the block barrier of the LDS combine)
+    __syncthreads();
     TPH(1, 2);
     if (w != 0) return;                      // wave 0 only from here: no block barriers
-    if (lead && lane == 0) {
-        gate_wait(st);
-        finish_scalars(d, fin, reset);
-        st->p = p;
-        st->kp = kp;
-        st->delta = best.k2;
-        st->trow_max_bits = 0ull;
-        st->ns = ns;
-        st->dinf = 0;
-    }
     // the waves' partial sums in wave order; the LDS loads issued together
     // (a loop over the runtime wave count waited for each load in turn)
     double tp16[16];
@@ -1141,6 +1131,16 @@ __global__ void __launch_bounds__(1024) k_dual_row(SpxDev d, int pse, int nr_cap
         if (pse) d.gpart[blockIdx.x] = g;
         cand_pass1(d)[blockIdx.x] = b;
         if (d.tslots) d.tslots[blockIdx.x] = wall_clock64();
+        // the choice goes to the outbox, which no block of this launch reads;
+        // the scalar state every block read at entry (the pending pivot, the
+        // counters, dinf) is rewritten by k_dual_ratio's block 0 from it
+        if (lead) {
+            st->ob_p = p;
+            st->ob_kp = kp;
+            st->ob_delta = best.k2;
+            st->ob_ns = ns;
+            st->ob_reset = reset ? 1 : 0;
+        }
     }
 }
 
@@ -1483,7 +1483,10 @@ __global__ void __launch_bounds__(256) k_dual_ratio(SpxDev d, int gn, int tiles_
     // per-block exit stamps by block 0's first wave
     const bool stamps = d.tslots != nullptr;
     const unsigned long long t_entry = (stamps && rowpath && blockIdx.x == 0 && threadIdx.x == 0) ? wall_clock64() : 0ull;
-    const RatioIn rin = ratio_in(st);
+    // the row path's k_dual_row left the new pivot's delta in the outbox
+    // (st->delta still holds the pending pivot's until block 0 below)
+    RatioIn rin = ratio_in(st);
+    if (rowpath == 1) rin.delta = st->ob_delta;
     const int j = blockIdx.x * blockDim.x + threadIdx.x;
     const int jc = min(j, n - 1);
     // unconditional loads at clamped indices, selected afterwards (no load
@@ -1528,6 +1531,20 @@ __global__ void __launch_bounds__(256) k_dual_ratio(SpxDev d, int gn, int tiles_
     for (int b = lane + CPL * 64; b < ncb; b += 64) v = fmax(v, tmax_part(d)[b]);
     const double big = wmax(v);
     if (stop) return;
+    if (rowpath == 1 && blockIdx.x == 0 && threadIdx.x == 0) {
+        // k_dual_row's outbox: the pending pivot's counters (finish_apply's
+        // scalar half, from the state every block of k_dual_row read), then
+        // the new pivot — no other block of this launch reads these fields
+        const FinishIn f = finish_load(d);
+        const int ob_p = st->ob_p, ob_kp = st->ob_kp, ob_ns = st->ob_ns, ob_reset = st->ob_reset;
+        const double ob_delta = st->ob_delta;
+        finish_scalars(d, f, ob_reset != 0);
+        st->p = ob_p;
+        st->kp = ob_kp;
+        st->delta = ob_delta;
+        st->ns = ob_ns;
+        st->dinf = 0;
+    }
     TPH(2, 0);
     if (lead) {
         // publish max |trow| and the end of the pivot-row kernel (latest

@@ -1168,6 +1168,13 @@ struct Spx {
         f->ext_upd = 0;
         f->stats.reinversions++;
         f->stats.seconds_reinvert += now_s() - t0;
+        {
+            long long nnz_lu = 0;
+            int lv[4];
+            double tl = 0.0;
+            sp_info(f->sp, &nnz_lu, lv, &tl);
+            f->stats.seconds_lu += tl;
+        }
         static const bool slog = std::getenv("GK_SPARSE_LOG") != nullptr;
         if (slog && ret == 0) {
             long long nnz = 0;
@@ -2597,6 +2604,31 @@ int gk_bfd_trace(gk_bfd *f, unsigned long long *out, size_t cnt)
     return (int)nn;
 }
 
+// Which factor a solve runs on.  The explicit inverse
+// serves dense A (the row path over AT, the MFMA panel and re-inversion) and
+// small or dense-basis LPs.  Sparse A takes the sparse LU (gk_sparse.hip)
+// beyond the inverse's limit (m > 65535) and whenever the basis is both large
+// and sparse: the inverse costs 8 m^2 bytes, a rank-1 pass over m x nr of them
+// per pivot and O(k^3) re-inversions, against level sweeps over the LU's
+// entries — on the block-angular m = 4,005 LP 7.7k against 3.2k pivots/s
+// (profiles/r04_sparse_blocks40*).  col_nnz: the average entries per column
+// of A (a solve) or of B (glp_factorize without a resident problem).
+// GK_SPARSE=1 / 0 force one (0 only up to m = 65535); GK_SPARSE_MIN_M moves
+// the size threshold (default 2048).
+static int factor_choice(int m, double col_nnz, bool dense)
+{
+    const char *ev = std::getenv("GK_SPARSE");
+    const int want = ev ? std::atoi(ev) : -1;
+    if (dense) return 0;
+    if (m > 65535 || want == 1) return 1;
+    if (want == 0) return 0;
+    static const int min_m = [] {
+        const char *e = std::getenv("GK_SPARSE_MIN_M");
+        return e ? std::max(1, std::atoi(e)) : 2048;
+    }();
+    return (m >= min_m && 16.0 * col_nnz <= (double)m) ? 1 : 0;
+}
+
 static void bfd_prepare(gk_bfd *f, int m)
 {
     HIPCHK(hipSetDevice(f->ctx->device));
@@ -2614,13 +2646,16 @@ int gk_bfd_factorize_csc(gk_bfd *f, int m, const int *ptr, const int *ind, const
         bfd_prepare(f, m);
         f->valid = 0;
         hipStream_t s = f->ctx->stream;
-        const char *spe = std::getenv("GK_SPARSE");
-        if (m > 65535 || (spe && std::atoi(spe) == 1)) {
-            // beyond the explicit inverse's limit (8 m^2 bytes, an O(m^3)
-            // inversion): the sparse factor, which spx_entry takes for such an
-            // LP, so a glp_factorize of an advanced basis before glp_simplex
-            // is the factor the solve then uses (GK_SPARSE=1: at any m, as
-            // spx_entry; a dense A there re-factors with the explicit inverse)
+        // the factor spx_entry would choose, so that a glp_factorize of an
+        // advanced basis before glp_simplex is the factor the solve then
+        // uses: by the resident problem's A when there is one, else by the
+        // density of B itself (a mismatch only costs the solve a re-factor)
+        const Engine *E0 = f->eng;
+        const bool known = E0 && E0->m == m && E0->n > 0;
+        const long long nnzb = (long long)ptr[m + 1] - ptr[1];
+        const int sparse = known ? factor_choice(m, (double)E0->nnz / E0->n, E0->dense != 0)
+                                 : factor_choice(m, (double)nnzb / m, false);
+        if (sparse) {
             for (int j = 1; j <= m; j++) {
                 const int len = ptr[j + 1] - ptr[j];
                 ABI_REQUIRE(0 <= len && len <= m, "luf_factorize: j = %d; len = %d; invalid column length", j, len);
@@ -2824,15 +2859,12 @@ static int spx_entry(gk_ctx *ctx, gk_lp *lp, gk_bfd *f, const gk_smcp *parm, int
         if (!f->eng) f->eng = new Engine;
         f->eng->prof = f->prof;
         engine_upload_matrix(f, lp);
-        // the factor: the explicit inverse (dense and mid-size LPs), or the
-        // sparse LU with Schur-complement updates (gk_sparse.hip) for sparse
-        // A when m exceeds the explicit inverse's limit (GK_SPARSE=1 takes it
-        // for any sparse A), both simplex methods
+        // the factor: the explicit inverse, or the sparse LU with Schur-
+        // complement updates (gk_sparse.hip), both simplex methods, as
+        // factor_choice decides
         {
-            const char *ev = std::getenv("GK_SPARSE");
-            const int want = ev ? std::atoi(ev) : -1;
             const bool big = lp->m > 65535;
-            const int sp = (!f->eng->dense && (big || want == 1)) ? 1 : 0;
+            const int sp = factor_choice(lp->m, (double)f->eng->nnz / std::max(1, f->eng->n), f->eng->dense != 0);
             ABI_REQUIRE(sp || !big, "spx: m = %d exceeds the explicit inverse's limit 65535 (sparse A: the sparse "
                         "factor serves m > 65535)", lp->m);
             if (sp != f->sparse) {
@@ -2840,6 +2872,7 @@ static int spx_entry(gk_ctx *ctx, gk_lp *lp, gk_bfd *f, const gk_smcp *parm, int
                 f->sparse = sp;
             }
             if (sp && !f->sp) f->sp = sp_create();
+            f->stats.factor_sparse = sp;
         }
         Spx S;
         S.ctx = ctx; S.f = f; S.E = f->eng; S.lp = lp; S.parm = parm; S.dual = dual;
@@ -2890,13 +2923,19 @@ int gk_spx_node(gk_ctx *ctx, gk_lp *lp, gk_bfd *bfd, const gk_smcp *parm)
 }
 }  // namespace gk
 
+// u[t * m + pos[t]] = 1 (the unit right-hand sides of the batched BTRANs)
+__global__ void k_unit_rows(double *u, int m, int nk, const int *pos)
+{
+    const int t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t < nk) u[(size_t)t * m + pos[t]] = 1.0;
+}
+
 extern "C" int gk_bfd_eval_tab_rows(gk_bfd *f, gk_lp *lp, int nk, const int *k, double *alfa, int flags)
 {
     try {
         ABI_REQUIRE(f && lp && (nk == 0 || (k && alfa)), "glp_eval_tab_row: null argument");
         ABI_REQUIRE(lp->m > 0 && lp->n > 0 && nk >= 0, "glp_eval_tab_row: m = %d, n = %d, nk = %d", lp->m, lp->n, nk);
         ABI_REQUIRE(f->valid && f->m == lp->m, "glp_eval_tab_row: basis factorization does not exist");
-        ABI_REQUIRE(!f->sparse, "glp_eval_tab_row: batched tableau rows need the explicit inverse (m <= 65535)");
         if (nk == 0) return 0;
         HIPCHK(hipSetDevice(f->ctx->device));
         const int m = lp->m, n = lp->n;
@@ -2936,8 +2975,26 @@ extern "C" int gk_bfd_eval_tab_rows(gk_bfd *f, gk_lp *lp, int nk, const int *k, 
         HIPCHK(hipMemcpyAsync(sc.p, rs.data(), nk * sizeof(double), hipMemcpyHostToDevice, s));
         HIPCHK(hipMemcpyAsync(sc.p + nk, cs.data(), n * sizeof(double), hipMemcpyHostToDevice, s));
         HIPCHK(hipMemcpyAsync(sc.p + nk + n, aux.data(), m * sizeof(double), hipMemcpyHostToDevice, s));
-        tab_rows(s, f->Binv.p, f->ldb, f->eng->mat(), nk, dpos.p, G.p, sc.p + nk + n, sc.p + nk, sc.p, out.p,
-                 (flags & 1) ? 0 : 1);
+        if (f->sparse) {
+            // the rows of inv(B) by BTRANs of e_pos on the sparse factor
+            // (glp_eval_tab_row's own glp_btran, glpapi12.js:430), then the
+            // same products with A
+            DBuf<double> units;                     // e_pos of every row, on the stream (no host copies in between)
+            units.ensure((size_t)nk * m);
+            fill_d(s, units.p, 0.0, (size_t)nk * m);
+            hipLaunchKernelGGL(k_unit_rows, dim3((nk + 63) / 64), dim3(64), 0, s, units.p, m, nk, dpos.p);
+            for (int t = 0; t < nk; t++) {
+                try {
+                    sp_btran(*f->sp, s, units.p + (size_t)t * m, G.p + (size_t)t * m);
+                } catch (const std::exception &e) {
+                    throw AbiError{e.what()};
+                }
+            }
+            HIPCHK(hipStreamSynchronize(s));
+            units.release();
+        }
+        tab_rows(s, f->sparse ? nullptr : f->Binv.p, f->ldb, f->eng->mat(), nk, dpos.p, G.p, sc.p + nk + n, sc.p + nk,
+                 sc.p, out.p, (flags & 1) ? 0 : 1);
         HIPCHK(hipGetLastError());
         // through a pinned buffer of our own: a direct copy into the host's
         // array leaves that (pageable, host-runtime-owned) memory registered

@@ -82,7 +82,18 @@ struct DState {
     // the entry gate of the multi-block pivot kernels (gk_device.h,
     // gate_arrive / gate_wait): arrivals per XCD slot of blockIdx, 0 between
     // launches
-    int gate[8];
+    int gate[8], gate_top, gate_pad;
+    // the outbox of k_dual_row: the pivot it chose (p, kp, delta, ns) and the
+    // reference-space reset, stored by its last block where no block of the
+    // launch reads them; k_dual_ratio's block 0 applies them (and the pending
+    // change of basis' counters) before any later kernel reads the state
+    int ob_p, ob_kp, ob_ns, ob_reset;
+    double ob_delta;
+    // primal: the reduced cost of xN[q] after k_primal_ratio's d_q check (the
+    // value it stores in cbar[q]); k_primal_commit reads it here, since the
+    // commit thread owning cbar[q] overwrites that entry while other blocks
+    // still need the old value
+    double dq_ratio;
 };
 
 // ---- dense GEMV helpers ---------------------------------------------------

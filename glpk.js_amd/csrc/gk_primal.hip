@@ -463,6 +463,7 @@ __global__ void __launch_bounds__(256) k_primal_ratio(SpxDev d, int gm, int ng, 
         const double vsum = pse ? wsum(vsl) : 0.0;
         if (threadIdx.x == 0) {
             d.cbar[q - 1] = cq;
+            st->dq_ratio = cq;
             st->q1 = p;
             st->teta1 = teta;
             st->kq1 = paux;
@@ -847,7 +848,7 @@ __global__ void __launch_bounds__(256) k_primal_commit(SpxDev d, int pse, int nv
         const int sn_old = in_n ? d.stat[i] : 0;
         const bool refn = (pse && in_n) ? d.refsp[kn_old - 1] != 0 : false;
         const double piv1 = d.tcol[pp - 1], piv2 = d.trow[q - 1];
-        const double cbq = d.cbar[q - 1];
+        const double cbq = st->dq_ratio;          // = cbar[q] (its owner rewrites the entry below)
         const int sq = d.stat[q - 1];
         const double xq = get_xN(d.stat, d.lb, d.ub, kq, q);
         const int tkp = d.type[kp - 1];

@@ -213,7 +213,8 @@ void tab_rows(hipStream_t s, const double *Binv, int ldb, const MatDev &A, int n
     const int m = A.m, n = A.n;
     const size_t ldo = (size_t)m + n;
     if (nk <= 0) return;
-    hipLaunchKernelGGL(k_tab_gather, dim3((m + 255) / 256, nk), dim3(256), 0, s, Binv, ldb, m, pos, G);
+    // (Binv null: G holds the rows of inv(B) already — the sparse factor's BTRANs)
+    if (Binv) hipLaunchKernelGGL(k_tab_gather, dim3((m + 255) / 256, nk), dim3(256), 0, s, Binv, ldb, m, pos, G);
     hipLaunchKernelGGL(k_tab_aux, dim3((m + 255) / 256, nk), dim3(256), 0, s, G, m, aux, rs, out, ldo);
     if (A.dense) {
         if (!use_mfma) {

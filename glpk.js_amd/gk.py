@@ -102,7 +102,8 @@ class SpxStats(C.Structure):
                 ("resident", C.c_int), ("evals_skipped", C.c_int),
                 ("panel_hits", C.c_longlong), ("panel_refills", C.c_longlong),
                 ("refine_tries", C.c_longlong), ("refinements", C.c_longlong), ("refine_steps", C.c_longlong),
-                ("refine_resid_max", C.c_double)]
+                ("refine_resid_max", C.c_double), ("factor_sparse", C.c_int), ("lu_ahead", C.c_int),
+                ("seconds_lu", C.c_double)]
 
 
 _lib = None

@@ -40,7 +40,7 @@
 extern "C" {
 #endif
 
-#define GK_ABI_VERSION 8
+#define GK_ABI_VERSION 9
 #include <stddef.h>
 #define GK_EABI (-1)          /* contract violation; see gk_last_error() */
 
@@ -225,6 +225,12 @@ typedef struct {
     long long refinements;      /* ... served by it (two MFMA GEMMs per step; the rest: Gauss-Jordan) */
     long long refine_steps;     /* Newton steps taken by those */
     double refine_resid_max;    /* largest max|I - C X| of an updated inverse offered to it */
+    /* ABI 9: the factor the call ran on (gk_bfd_factor_kind), the host
+     * Markowitz LU time of its sparse refactorizations, and how many of
+     * those were factored ahead on a host thread while the device pivoted */
+    int factor_sparse;          /* 1: the sparse LU (gk_sparse.hip), 0: the explicit inverse */
+    int lu_ahead;               /* sparse refactorizations taken from the look-ahead thread */
+    double seconds_lu;          /* host wall time of the Markowitz LU factorizations (all threads) */
 } gk_spx_stats;
 void gk_bfd_last_stats(const gk_bfd *bfd, gk_spx_stats *st);
 /* record HIP events around the pivot-row kernel of every dual pivot (benches) */

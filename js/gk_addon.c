@@ -574,6 +574,8 @@ static napi_value js_stats(napi_env env, napi_callback_info info)
     set_num(env, o, "bytes_pivots", st.bytes_pivots);
     set_num(env, o, "panel_hits", (double)st.panel_hits);
     set_num(env, o, "panel_refills", (double)st.panel_refills);
+    set_num(env, o, "factor_sparse", (double)st.factor_sparse);
+    set_num(env, o, "seconds_lu", st.seconds_lu);
     return o;
 }
 

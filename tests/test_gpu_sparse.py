@@ -195,3 +195,90 @@ def test_gpu_sparse_warm_start_from_statuses(gpu_ctx, sparse_on):
     assert gk.glp_simplex(R, gk.SMCP(meth=gk.GLP_DUAL, msg_lev=gk.GLP_MSG_ERR)) == 0
     assert abs(Q.obj_val - R.obj_val) <= 1e-9 * max(1.0, abs(R.obj_val)), (Q.obj_val, R.obj_val)
     sparse_kkt(Q, prob)
+
+
+def test_gpu_factor_choice_default(gpu_ctx, oracle, monkeypatch):
+    """Without GK_SPARSE the factor follows the cost model (gk_engine.hip
+    factor_choice): the block-angular m = 4,005 LP runs on the sparse LU and
+    reaches the oracle's objective; C2s (m = 821) and dense A keep the
+    explicit inverse."""
+    monkeypatch.delenv("GK_SPARSE", raising=False)
+    prob = problems.gen_blocks(40, 100, 200, 10)
+    o = oracle.OracleProb(prob)
+    assert o.simplex(meth=3) == 0
+    ref = o.result()["obj_val"]
+    P = gk.GkProblem(gpu_ctx, prob)
+    assert gk.glp_simplex(P, gk.SMCP(meth=gk.GLP_DUAL, msg_lev=gk.GLP_MSG_ERR)) == 0
+    st = P.stats()
+    assert st.factor_sparse == 1
+    assert abs(P.obj_val - ref) <= 1e-9 * max(1.0, abs(ref)), (P.obj_val, ref)
+    print(f"blocks 40 default: {P.it_cnt} pivots in {st.seconds_total:.2f} s ({P.it_cnt / st.seconds_total:.0f}/s), "
+          f"host LU {st.seconds_lu:.2f} s")
+    for prob in (problems.gen_c2s(), problems.gen_dense(256, 1024, seed=42)):
+        Q = gk.GkProblem(gpu_ctx, prob)
+        assert gk.glp_simplex(Q, gk.SMCP(meth=gk.GLP_DUAL, it_lim=50, msg_lev=gk.GLP_MSG_ERR)) in (0, 8)
+        assert Q.stats().factor_sparse == 0
+
+
+def test_gpu_warm_start_beyond_limit_default_factor(gpu_ctx, monkeypatch):
+    """The path that hung in round 4, without GK_SPARSE: m > 65535, an
+    it_lim solve, its statuses loaded into a new problem, glp_factorize of
+    that advanced basis (the sparse factor by itself: the explicit m^2
+    inverse is not built), FTRAN / BTRAN against scipy, then glp_simplex
+    continuing from it."""
+    import scipy.sparse as sps
+    import scipy.sparse.linalg as spla
+    monkeypatch.delenv("GK_SPARSE", raising=False)
+    prob = problems.gen_blocks(656, 100, 200, 50)
+    m = prob.m
+    assert m > 65535
+    P = gk.GkProblem(gpu_ctx, prob)
+    assert gk.glp_simplex(P, gk.SMCP(meth=gk.GLP_DUAL, it_lim=1500, msg_lev=gk.GLP_MSG_ERR)) == problems.GLP_EITLIM
+    Q = gk.GkProblem(gpu_ctx, prob.copy())
+    Q.row_stat[1:m + 1] = P.row_stat[1:m + 1]
+    Q.col_stat[1:prob.n + 1] = P.col_stat[1:prob.n + 1]
+    Q.valid = 0
+    assert Q.factorize() == 0 and Q.valid
+    rows, cols, vals = [], [], []
+    for j in range(1, m + 1):
+        k = Q.head[j]
+        if k <= m:
+            rows.append(k - 1); cols.append(j - 1); vals.append(1.0)
+        else:
+            lo, hi = prob.A_ptr[k - m - 1], prob.A_ptr[k - m]
+            rows += (np.asarray(prob.A_ind[lo:hi]) - 1).tolist()
+            cols += [j - 1] * (hi - lo)
+            vals += (-np.asarray(prob.A_val[lo:hi])).tolist()
+    B = sps.csc_matrix((vals, (rows, cols)), shape=(m, m))
+    b = np.random.default_rng(5).standard_normal(m)
+    x = Q.ftran(b.copy())
+    assert np.abs(B @ x - b).max() <= 1e-9 * max(1.0, np.abs(b).max())
+    y = Q.ftran(b.copy(), tr=True)
+    assert np.abs(B.T @ y - b).max() <= 1e-9 * max(1.0, np.abs(b).max())
+    assert gk.glp_simplex(Q, gk.SMCP(meth=gk.GLP_DUAL, it_lim=500, msg_lev=gk.GLP_MSG_ERR)) == problems.GLP_EITLIM
+    assert Q.stats().factor_sparse == 1
+    check_solution(Q)
+
+
+def test_gpu_tab_rows_on_sparse_factor(gpu_ctx, monkeypatch):
+    """glp_eval_tab_row in a batch (gk_bfd_eval_tab_rows) on the sparse
+    factor (rows of inv(B) by BTRANs): the rows the explicit inverse gives on
+    the same optimal basis (glp_factorize of it each way), within 1e-9 of
+    each row's largest entry."""
+    prob = problems.gen_blocks(10, 100, 200, 5)
+    P = gk.GkProblem(gpu_ctx, prob.copy())
+    assert gk.glp_simplex(P, gk.SMCP(meth=gk.GLP_DUAL, msg_lev=gk.GLP_MSG_ERR)) == 0
+    ks = [k for k in range(1, prob.m + prob.n + 1)
+          if (P.row_stat[k] if k <= prob.m else P.col_stat[k - prob.m]) == problems.GLP_BS][:40]
+    rows = {}
+    for flag in ("1", "0"):
+        monkeypatch.setenv("GK_SPARSE", flag)
+        Q = gk.GkProblem(gpu_ctx, prob.copy())
+        Q.row_stat[1:prob.m + 1] = P.row_stat[1:prob.m + 1]
+        Q.col_stat[1:prob.n + 1] = P.col_stat[1:prob.n + 1]
+        Q.valid = 0
+        assert Q.factorize() == 0
+        rows[flag] = Q.eval_tab_rows(ks)
+    a, b = rows["1"], rows["0"]
+    big = np.maximum(1.0, np.abs(b).max(axis=1, keepdims=True))
+    assert np.all(np.abs(a - b) <= 1e-9 * big)

@@ -4,7 +4,7 @@ solve REPS times in one process, every batch and re-inversion fingerprinted
 by the engine (GK_DET_LOG, gk_engine.hip det_log), then the runs compared
 line by line and the first divergent line printed.
 
-usage: GK_DET_LOG=gpurun_out/det.log python tools/det_probe.py M N IT_LIM REPS [CALL_LIM]
+usage: GK_DET_LOG=gpurun_out/det.log python tools/det_probe.py M N IT_LIM REPS [CALL_LIM [primal]]
        python tools/det_probe.py --compare gpurun_out/det.log [other.log]
 CALL_LIM (default 0 = one call): it_lim of each glp_simplex call.
 """
@@ -63,6 +63,7 @@ def main():
     from glpk_js_amd import gk, problems
     m, n, it_lim, reps = (int(x) for x in sys.argv[1:5])
     call_lim = int(sys.argv[5]) if len(sys.argv) > 5 else 0
+    meth = gk.GLP_PRIMAL if len(sys.argv) > 6 and sys.argv[6] == "primal" else gk.GLP_DUAL
     log = os.environ.get("GK_DET_LOG")
     ctx = gk.Context(0)
     prob = problems.gen_dense(m, n, seed=42)
@@ -75,7 +76,7 @@ def main():
         ret = 8
         while ret == 8 and P.it_cnt < it_lim:
             lim = min(call_lim or it_lim, it_lim - P.it_cnt)
-            ret = gk.glp_simplex(P, gk.SMCP(meth=gk.GLP_DUAL, it_lim=lim, msg_lev=gk.GLP_MSG_ERR))
+            ret = gk.glp_simplex(P, gk.SMCP(meth=meth, it_lim=lim, msg_lev=gk.GLP_MSG_ERR))
         st = P.stats()
         print(json.dumps({"rep": rep, "ret": ret, "it_cnt": P.it_cnt, "obj": P.obj_val,
                           "seconds": round(time.perf_counter() - t0, 2), "reinversions": st.reinversions,
