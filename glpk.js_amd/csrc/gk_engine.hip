@@ -2217,6 +2217,7 @@ int Spx::run_dual()
         K = align_to_display(K);
         int why = batch(K, rigorous);
         det_log("batch", K, why);
+        if (f->sparse) sp_stamps_dump(*f->sp, s, ctx->wall_khz);
         E->kbatch = next_batch(E->kbatch, why);
         dinf_known = (why == ST_BATCH && hs.npiv > 0);
         if (hs.npiv > 0) {

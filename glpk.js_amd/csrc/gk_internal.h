@@ -168,6 +168,7 @@ void sp_pivot_ftran(SpFactor &F, hipStream_t s, const DState *st, double *h, dou
                     int pse);
 void sp_pivot_update(SpFactor &F, hipStream_t s, DState *st);
 void sp_pivot_btran2(SpFactor &F, hipStream_t s, DState *st, const double *v, double *rho, double *u);
+void sp_stamps_dump(SpFactor &F, hipStream_t s, int wall_khz);   // GK_SP_STAMPS (diagnostics)
 
 struct SpxDev {
     int m, n;

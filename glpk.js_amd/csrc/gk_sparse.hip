@@ -121,12 +121,14 @@ struct SpFactor {
     };
     std::vector<Seg> plan[4];
     int wide[4] = {0, 0, 0, 0};
+    SBuf<unsigned long long> stamps;      // GK_SP_STAMPS: 4 x SP_STAMP_MAX level stamps of the last solves
+    std::vector<int> lv_host[4];          // (with stamps) the level sizes, for the dump
     double t_lu = 0.0, t_total = 0.0;
     ~SpFactor()
     {
         fl.release(); fu.release(); bu.release(); bl.release();
         Y.release(); Minv.release(); zq.release(); tpart.release(); bt.release(); scr.release(); scr2.release();
-        hh.release(); bz.release();
+        hh.release(); bz.release(); stamps.release();
         P.release();
         hdr.release();
     }
@@ -620,7 +622,9 @@ struct TriDev {
     const int *lvptr, *lvlong, *iin, *iout, *eptr, *eidx;
     const double *diag, *eval;
     const int *nlev;                              // device word: levels of the current factor
+    unsigned long long *stamps;                   // GK_SP_STAMPS: device clock after each level (null: off)
 };
+constexpr int SP_STAMP_MAX = 2048;                // levels stamped per sweep
 
 // one step of a sweep: its metadata and right-hand side(s) do not depend on
 // the sweep's own output, so they are loaded one level ahead (before the
@@ -773,6 +777,7 @@ __device__ void tri_sweep(const TriDev &t, const double *in0, const double *in1,
     step_load<NRHS>(t, in0, in1, lb + (int)threadIdx.x, ls, cur);
     LongPre<NRHS> lcur;
     long_load<NRHS>(t, in0, in1, ls, le, lcur);
+    if (t.stamps && threadIdx.x == 0 && l0 < SP_STAMP_MAX) t.stamps[l0] = wall_clock64();
     for (int l = l0; l < nlev; l++) {
         // the next level's bounds and this thread's first (short) step of it
         const int nb = le, ne = (l + 1 < nlev) ? t.lvptr[l + 2] : le, nls = (l + 1 < nlev) ? t.lvlong[l + 1] : le;
@@ -834,6 +839,7 @@ __device__ void tri_sweep(const TriDev &t, const double *in0, const double *in1,
         } else
             for (int s = ls + w; s < le; s += nw) step_wave<NRHS>(t, in0, in1, s, out0, out1);
         __syncthreads();
+        if (t.stamps && threadIdx.x == 0 && l + 1 < SP_STAMP_MAX) t.stamps[l + 1] = wall_clock64();
         cur = nxt;
         lcur = lnxt;
         lb = nb;
@@ -1257,22 +1263,29 @@ static void up_tri(hipStream_t s, SpTriDevBufs &B, const SpTriHost &T, int *d_nl
     SPCHK(hipMemcpyAsync(d_nlev, &T.nlev, sizeof(int), hipMemcpyHostToDevice, s));
 }
 
-static TriDev tri_dev(const SpTriDevBufs &B, const int *nlev)
+static TriDev tri_dev(const SpTriDevBufs &B, const int *nlev, unsigned long long *stamps)
 {
     TriDev t;
     t.lvptr = B.lvptr.p; t.lvlong = B.lvlong.p; t.iin = B.iin.p; t.iout = B.iout.p; t.eptr = B.eptr.p; t.eidx = B.eidx.p;
-    t.diag = B.diag.p; t.eval = B.eval.p; t.nlev = nlev;
+    t.diag = B.diag.p; t.eval = B.eval.p; t.nlev = nlev; t.stamps = stamps;
     return t;
+}
+
+static const char *sp_stamps_path()
+{
+    static const char *p = std::getenv("GK_SP_STAMPS");
+    return p;
 }
 
 static SpDev sp_dev(SpFactor &F)
 {
     SpDev d;
     d.m = F.m;
-    d.fl = tri_dev(F.fl, F.hdr.p + 0);
-    d.fu = tri_dev(F.fu, F.hdr.p + 1);
-    d.bu = tri_dev(F.bu, F.hdr.p + 2);
-    d.bl = tri_dev(F.bl, F.hdr.p + 3);
+    unsigned long long *sb = F.stamps.p;
+    d.fl = tri_dev(F.fl, F.hdr.p + 0, sb ? sb + 0 * SP_STAMP_MAX : nullptr);
+    d.fu = tri_dev(F.fu, F.hdr.p + 1, sb ? sb + 1 * SP_STAMP_MAX : nullptr);
+    d.bu = tri_dev(F.bu, F.hdr.p + 2, sb ? sb + 2 * SP_STAMP_MAX : nullptr);
+    d.bl = tri_dev(F.bl, F.hdr.p + 3, sb ? sb + 3 * SP_STAMP_MAX : nullptr);
     d.w.Y = F.Y.p; d.w.P = F.P.p; d.w.Minv = F.Minv.p; d.w.k = F.hdr.p + 4; d.w.zq = F.zq.p;
     d.w.tpart = F.tpart.p; d.w.bt = F.bt.p; d.w.scr2 = F.scr2.p; d.w.hh = F.hh.p; d.w.ycol = F.hdr.p + 5; d.w.bz = F.bz.p;
     return d;
@@ -1388,6 +1401,18 @@ static int sp_factorize_cols(SpFactor &F, hipStream_t s, int m, const std::vecto
     F.hh.ensure((size_t)2 * SP_KMAX);
     F.Minv.ensure((size_t)SP_KMAX * SP_KMAX);
     F.hdr.ensure(8);
+    if (sp_stamps_path()) {
+        F.stamps.ensure((size_t)4 * SP_STAMP_MAX);
+        SPCHK(hipMemsetAsync(F.stamps.p, 0, (size_t)4 * SP_STAMP_MAX * sizeof(unsigned long long), s));
+        for (int i = 0; i < 4; i++) {
+            const SpTriHost &T = *T4[i];
+            F.lv_host[i].clear();
+            for (int l = 0; l < T.nlev; l++) {
+                F.lv_host[i].push_back(T.lvptr[l + 1] - T.lvptr[l]);
+                F.lv_host[i].push_back(T.eptr[T.lvptr[l + 1]] - T.eptr[T.lvptr[l]]);
+            }
+        }
+    }
     up_tri(s, F.fl, S.fl, F.hdr.p + 0);
     up_tri(s, F.fu, S.fu, F.hdr.p + 1);
     up_tri(s, F.bu, S.bu, F.hdr.p + 2);
@@ -1515,6 +1540,33 @@ void sp_pivot_update(SpFactor &F, hipStream_t s, DState *st)
     SpDev d = sp_dev(F);
     hipLaunchKernelGGL(k_sp_update, dim3(1), dim3(1024), 0, s, d, st);
     hipLaunchKernelGGL(k_sp_ycol, dim3((F.m + 255) / 256), dim3(256), 0, s, d, (const DState *)st);
+}
+
+// GK_SP_STAMPS=<file>: the device-clock duration of every level of the four
+// sweeps in the last pivot (stamped by tri_sweep's thread 0 after each level
+// barrier; levels that ran on the grid are not stamped), with the level's
+// steps and entries; one line per sweep, appended to the file
+void sp_stamps_dump(SpFactor &F, hipStream_t s, int wall_khz)
+{
+    const char *path = sp_stamps_path();
+    if (!path || !F.stamps.p) return;
+    std::vector<unsigned long long> h((size_t)4 * SP_STAMP_MAX);
+    SPCHK(hipMemcpyAsync(h.data(), F.stamps.p, h.size() * sizeof(unsigned long long), hipMemcpyDeviceToHost, s));
+    SPCHK(hipStreamSynchronize(s));
+    FILE *fp = std::fopen(path, "a");
+    if (!fp) return;
+    static const char *names[4] = {"ftran_L", "ftran_U", "btran_U'", "btran_L'"};
+    for (int i = 0; i < 4; i++) {
+        const int nl = (int)F.lv_host[i].size() / 2;
+        std::fprintf(fp, "%s levels %d:", names[i], nl);
+        for (int l = 0; l < nl && l + 1 < SP_STAMP_MAX; l++) {
+            const unsigned long long a = h[(size_t)i * SP_STAMP_MAX + l], b = h[(size_t)i * SP_STAMP_MAX + l + 1];
+            const double us = (a && b > a) ? 1e3 * (double)(b - a) / wall_khz : -1.0;
+            std::fprintf(fp, " %d/%d:%.2f", F.lv_host[i][2 * l], F.lv_host[i][2 * l + 1], us);
+        }
+        std::fprintf(fp, "\n");
+    }
+    std::fclose(fp);
 }
 
 // ---------------------------------------------------------------------------

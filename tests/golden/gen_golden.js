@@ -14,6 +14,7 @@
 //
 // usage: node tests/golden/gen_golden.js [--big] [--only PREFIX]
 //        node tests/golden/gen_golden.js --lpf-fix --only bfcpfix_
+//        node tests/golden/gen_golden.js --deep 12x34   (one deep C5s MIP)
 //        node --max-old-space-size=12000 tests/golden/gen_golden.js --c3
 //          (C3 4096x16384 at full size only: the reference's state after its
 //           first 300 dual pivots, one it_lim=300 call and three it_lim=100
@@ -476,6 +477,15 @@ function c3Case() {
     console.log('wrote c3_itlim.json.gz');
 }
 if (C3) { c3Case(); process.exit(0); }
+// --deep MxN: one deep C5s instance (the multi-GPU B&B workload, SURVEY.md
+// §8(d) generator) — the reference's glp_intopt on it, as mipCase records
+// every MIP; minutes to hours of node time
+if (process.argv.indexOf('--deep') >= 0) {
+    var dm = process.argv[process.argv.indexOf('--deep') + 1].split('x').map(Number);
+    mipCase('c5s_' + dm[0] + 'x' + dm[1], function () { return genC5s(dm[0], dm[1], 42); },
+            {kind: 'c5s', m: dm[0], n: dm[1], seed: 42});
+    process.exit(0);
+}
 
 // ---- instances ------------------------------------------------------------
 lpCase('test', function () { return readLp('test.lpt'); }, null);
