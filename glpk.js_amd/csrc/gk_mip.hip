@@ -191,6 +191,13 @@ __device__ int wave_ratio(double t, double a, int idx)
     return r == 0x7fffffffu ? -1 : (int)r;
 }
 
+// the value v of the lane whose candidate is the wave's choice q (v >= 0;
+// each index belongs to one lane)
+__device__ __forceinline__ double wave_pick(double v, int mine, int q)
+{
+    return wmax(mine == q ? v : -DBL_MAX);
+}
+
 __device__ double block_sum256(double v, double *sh)
 {
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -416,7 +423,8 @@ __global__ void __launch_bounds__(256) k_node_lp(NodeProb P, NodeIO io)
     double *rinfo = fcol + m;                 // 6 (m + 1)
     double *cl = rinfo + 6 * (m + 1);         // N: the costs
     double *dzt = cl + N;                     // 4 m: branching degradations of the candidates
-    double *Ar = dzt + 4 * m;                 // ALDS: A row-major (m x n)
+    double *gam = dzt + 4 * m;                // m: projected steepest-edge weights of the rows
+    double *Ar = gam + m;                     // ALDS: A row-major (m x n)
     const int nzl = ALDS ? P.nnz : 0;         // sparse copies staged in LDS
     double *rv = Ar + (ALDS ? (size_t)m * n : 0), *cv = rv + nzl;
     int *head = (int *)(cv + nzl);
@@ -426,6 +434,7 @@ __global__ void __launch_bounds__(256) k_node_lp(NodeProb P, NodeIO io)
     signed char *stat = (signed char *)(ci + nzl);
     signed char *chg = stat + N;              // n
     signed char *isl = chg + n;               // n: integer flags
+    signed char *refsp = isl + n;             // N: the pricing's reference space
     // the problem's costs, integer flags and (ALDS) matrix staged in LDS:
     // every loop below reads them many times, some from one thread
     for (int k = threadIdx.x; k < N; k += blockDim.x) cl[k] = P.c[k];
@@ -666,7 +675,12 @@ __global__ void __launch_bounds__(256) k_node_lp(NodeProb P, NodeIO io)
     __syncthreads();
     NODE_STAMP(3);
     // ---- bounded dual simplex ------------------------------------------
-    const double tol_p = 1e-7, tol_piv = 1e-7;
+    // the reference's node LP is glp_simplex with meth GLP_DUALP and the
+    // default SMCP (glpios01.js:866-910): projected steepest-edge chuzr
+    // (glpspx02.js:572) and the Harris two-pass chuzc with rtol = 0.30 tol_dj
+    // (glpspx02.js:793, called at :1859) on the row sorted with tol_bnd
+    // (sort_trow :754, called at :1851)
+    const double tol_bnd = 1e-7, tol_dj = 1e-7, kappa = 0.10, rtol = 0.30 * tol_dj;
     const double cutoff = io.cutoff[b];
     const int it_lim = io.it_lim[b];
     int it = 0, status = NODE_OPT;
@@ -678,6 +692,14 @@ __global__ void __launch_bounds__(256) k_node_lp(NodeProb P, NodeIO io)
     __shared__ int sh_st, sh_p, sh_q;
     __shared__ double sh_tq, sh_dq, sh_apq;
     for (;;) {
+        if (it % 1000 == 0) {
+            // reset_refsp (glpspx02.js:497): the reference space is the
+            // current basic set, every weight 1 — at the start of the node's
+            // solve (refct = 0) and after every 1000 weight updates
+            for (int k = threadIdx.x; k < N; k += blockDim.x) refsp[k] = stat[k] == BS;
+            for (int i = threadIdx.x; i < m; i += blockDim.x) gam[i] = 1.0;
+            __syncthreads();
+        }
         if (threadIdx.x < 64) {
             const int lane = threadIdx.x;
             int dec = -1, p = -1, q = -1;
@@ -687,16 +709,19 @@ __global__ void __launch_bounds__(256) k_node_lp(NodeProb P, NodeIO io)
             const double z = wsum(zs);
             if (z >= cutoff) dec = NODE_CUTOFF;
             else {
-                // chuzr: largest bound violation
+                // chuzr: the largest squared bound violation over the row's
+                // weight; the first row among equals
                 double key = 0.0;
                 int idx = -1;
                 for (int i = lane; i < m; i += 64) {
                     const int k = head[i];
                     const double v = x[k];
                     double r = 0.0;
-                    if (v < lb[k] - tol_p * (1.0 + fabs(lb[k]))) r = lb[k] - v;
-                    else if (v > ub[k] + tol_p * (1.0 + fabs(ub[k]))) r = v - ub[k];
-                    if (r > 0.0 && (idx < 0 || r > key)) { key = r; idx = i; }
+                    if (lb[k] != -DBL_MAX && v < lb[k] - tol_bnd * (1.0 + kappa * fabs(lb[k]))) r = lb[k] - v;
+                    if (ub[k] != DBL_MAX && v > ub[k] + tol_bnd * (1.0 + kappa * fabs(ub[k]))) r = ub[k] - v;
+                    if (r == 0.0) continue;
+                    const double g = fmax(gam[i], DBL_EPSILON), s = r * r / g;
+                    if (s > key) { key = s; idx = i; }
                 }
                 p = wave_argmax(key, idx);
                 if (p < 0) dec = NODE_OPT;                 // primal feasible: optimal
@@ -705,12 +730,16 @@ __global__ void __launch_bounds__(256) k_node_lp(NodeProb P, NodeIO io)
             if (dec < 0) {
                 const int kp = head[p];
                 const bool to_lb = x[kp] < lb[kp];
-                // ratio test on row p: x_p = -sum T[p,j] x_j
+                // x_p = -sum T[p,k] x_k: the reference's row trow_k = -T[p,k];
+                // alfa = s trow_k with s = sign(delta) (+1: x_p rises to lb)
+                const double s = to_lb ? 1.0 : -1.0;
                 double rmax = 0.0;
                 for (int k = lane; k < N; k += 64)
-                    if (stat[k] != BS) rmax = fmax(rmax, fabs(T_(p, k)));
+                    if (stat[k] != BS && stat[k] != NS) rmax = fmax(rmax, fabs(T_(p, k)));
                 rmax = wmax(rmax);
-                const double eps = tol_piv * (1.0 + 0.01 * rmax);
+                const double eps = tol_bnd * (1.0 + 0.01 * rmax);
+                // first pass: the bounds relaxed by rtol, smallest step
+                // (the larger |alfa| among equal steps)
                 double bt = 0.0, ba = 0.0;
                 int bq = -1;
                 for (int k = lane; k < N; k += 64) {
@@ -718,24 +747,49 @@ __global__ void __launch_bounds__(256) k_node_lp(NodeProb P, NodeIO io)
                     if (st == BS || st == NS) continue;
                     const double a = T_(p, k);
                     if (fabs(a) < eps) continue;
-                    // x_p changes by -a per unit increase of x_k
-                    bool ok;
-                    if (to_lb) ok = (st == NL && a < 0.0) || (st == NU && a > 0.0) || (st == NF);
-                    else ok = (st == NL && a > 0.0) || (st == NU && a < 0.0) || (st == NF);
-                    if (!ok) continue;
-                    // the step that keeps d dual feasible: d_k - (d_q / a_pq) a_k
-                    double t = (st == NF) ? fabs(d[k]) / fabs(a) : (to_lb ? -d[k] / a : d[k] / a);
+                    const double alfa = -s * a;
+                    double t;
+                    if (alfa > 0.0) {
+                        if (st != NL && st != NF) continue;
+                        t = (d[k] + rtol) / alfa;
+                    } else {
+                        if (st != NU && st != NF) continue;
+                        t = (d[k] - rtol) / alfa;
+                    }
                     if (t < 0.0) t = 0.0;
-                    if (bq < 0 || t < bt || (t == bt && fabs(a) > ba)) { bt = t; ba = fabs(a); bq = k; }
+                    if (bq < 0 || t < bt || (t == bt && fabs(alfa) > ba)) { bt = t; ba = fabs(alfa); bq = k; }
                 }
                 q = wave_ratio(bt, ba, bq);
+                double teta = 0.0;
+                if (q >= 0) {
+                    const double tmax = wave_pick(bt, bq, q);
+                    teta = tmax;
+                    if (tmax > 0.0) {
+                        // second pass: within the relaxed step, the largest |alfa|
+                        double ka = -1.0, kt = 0.0;
+                        int kq = -1;
+                        for (int k = lane; k < N; k += 64) {
+                            const int st = stat[k];
+                            if (st == BS || st == NS) continue;
+                            const double a = T_(p, k);
+                            if (fabs(a) < eps) continue;
+                            const double alfa = -s * a;
+                            if (alfa > 0.0 ? (st != NL && st != NF) : (st != NU && st != NF)) continue;
+                            double t = d[k] / alfa;
+                            if (t < 0.0) t = 0.0;
+                            if (t <= tmax && fabs(alfa) > ka) { ka = fabs(alfa); kq = k; kt = t; }
+                        }
+                        q = wave_argmax(ka, kq);
+                        teta = wave_pick(kt, kq, q);
+                    }
+                }
                 if (q < 0) dec = NODE_INFEAS;              // dual unbounded
                 else if (lane == 0) {
                     const double apq = T_(p, q);
                     const double bound = to_lb ? lb[kp] : ub[kp];
                     sh_apq = apq;
                     sh_tq = (x[kp] - bound) / apq;         // step of x_q
-                    sh_dq = d[q] / apq;
+                    sh_dq = -s * teta;                     // -new_dq: d_k -= dq T[p,k], d_kp = -dq
                 }
             }
             if (lane == 0) { sh_st = dec; sh_p = p; sh_q = q; }
@@ -758,15 +812,34 @@ __global__ void __launch_bounds__(256) k_node_lp(NodeProb P, NodeIO io)
             if (a != 0.0) d[k] -= dq * a;
         }
         // T update outside row p and column q: row i -= T[i,q] (row p / apq),
-        // a wave per row, lanes along it
+        // a wave per row, lanes along it.  The rows' projected steepest-edge
+        // weights of the adjacent basis come from the rows themselves:
+        // gamma_i = [x_B(i) in the reference space] + sum of T[i,k]^2 over
+        // the non-basic non-fixed k of the reference space — the quantity
+        // update_gamma (glpspx02.js:1075) carries by recurrence, exact here
+        // because the tableau is explicit.  A row with T[i,q] = 0 keeps its
+        // weight (its entries in columns q and kp are zero before and after).
         {
             const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, nwv = blockDim.x >> 6;
+            const bool kp_in = refsp[kp] && lb[kp] != ub[kp];     // x_kp leaves non-fixed
             for (int i = wv; i < m; i += nwv) {
-                if (i == p) continue;
-                const double f = T_(i, q);
-                if (f == 0.0) continue;
-                for (int k = lane; k < N; k += 64)
-                    if (k != q) T_(i, k) -= f * (T_(p, k) / apq);
+                const double f = (i == p) ? 0.0 : T_(i, q);
+                if (i != p && f == 0.0) continue;
+                double g = 0.0;
+                for (int k = lane; k < N; k += 64) {
+                    if (k == q) continue;
+                    const double r = T_(p, k) / apq;
+                    double v;
+                    if (i == p) v = r;
+                    else {
+                        v = T_(i, k) - f * r;
+                        T_(i, k) = v;
+                    }
+                    const bool in = (k == kp) ? kp_in : (refsp[k] && stat[k] != BS && stat[k] != NS);
+                    if (in) g += v * v;
+                }
+                g = wsum(g);
+                if (lane == 0) gam[i] = (refsp[i == p ? q : head[i]] ? 1.0 : 0.0) + g;
             }
         }
         __syncthreads();
@@ -1042,9 +1115,9 @@ __global__ void __launch_bounds__(256) k_node_lp(NodeProb P, NodeIO io)
 size_t node_lp_lds(int m, int n, int alds = 0, int nnz = 0)
 {
     const size_t N = (size_t)m + n, z = alds ? (size_t)nnz : 0;
-    return sizeof(double) * ((size_t)m * (2 * m + n) + 5 * N + 5 * (size_t)m + 6 * ((size_t)m + 1) +
+    return sizeof(double) * ((size_t)m * (2 * m + n) + 5 * N + 6 * (size_t)m + 6 * ((size_t)m + 1) +
                              (alds ? (size_t)m * n : 0) + 2 * z) +
-           sizeof(int) * (2 * (size_t)m + N + (z ? (size_t)m + n + 2 + 2 * z : 0)) + N + 2 * (size_t)n + 16;
+           sizeof(int) * (2 * (size_t)m + N + (z ? (size_t)m + n + 2 + 2 * z : 0)) + 2 * N + 2 * (size_t)n + 16;
 }
 
 constexpr size_t NODE_LDS_MAX = 64 * 1024;

@@ -89,6 +89,12 @@ struct SpTriHost {
     int nlev = 0;
     std::vector<int> lvptr, lvlong, iin, iout, eptr, eidx;   // lvlong[l]: first step of level l with > TRI_LONG entries
     std::vector<double> diag, eval;
+    // LDS segments (sp_plan_sweep): entries [eptr[s], emid[s]) read the
+    // sweep's vectors (external), [emid[s], eptr[s+1]) the outputs of steps
+    // of the same segment, by their index within it (internal); aord: the
+    // segment's steps (local indices) for its external pass, the ones of at
+    // most TRI_LONG external entries first
+    std::vector<int> emid, aord;
 };
 
 struct SpSolves {
@@ -96,19 +102,19 @@ struct SpSolves {
 };
 
 struct SpTriDevBufs {
-    SBuf<int> lvptr, lvlong, iin, iout, eptr, eidx;
+    SBuf<int> lvptr, lvlong, iin, iout, eptr, eidx, emid, aord;
     SBuf<double> diag, eval;
     void release()
     {
         lvptr.release(); lvlong.release(); iin.release(); iout.release(); eptr.release(); eidx.release(); diag.release();
-        eval.release();
+        eval.release(); emid.release(); aord.release();
     }
 };
 
 struct SpFactor {
     int m = -1;
     SpTriDevBufs fl, fu, bu, bl;
-    SBuf<double> Y, Minv, zq, tpart, bt, scr, scr2, hh, bz;
+    SBuf<double> Y, Minv, zq, tpart, bt, scr, scr2, hh, bz, sacc;   // sacc: an LDS segment's external sums (k_sp_seg_a)
     SBuf<int> P, hdr;                     // hdr: nlev of fl, fu, bu, bl; k (updates in the chain); Y column of the last update
     long long nnz_l = 0, nnz_u = 0;
     int levels[4] = {0, 0, 0, 0};
@@ -116,8 +122,13 @@ struct SpFactor {
     // steps) as grid launches (k_sp_level), the runs of narrow levels
     // between them in one workgroup (k_sp_sweep); wide[i] = 0: the whole
     // sweep in the fused one-workgroup kernels
+    // grid: 1 a wide level on the grid (k_sp_level), 0 a run of narrow
+    // levels in k_sp_sweep, 2 an LDS segment (k_sp_seg: steps sb .. sb+ns-1,
+    // nas of them short in the external pass; pre: that pass on the grid
+    // first, k_sp_seg_a with ablocks blocks)
     struct Seg {
         int grid, l0, l1, blocks;
+        int sb = 0, ns = 0, nas = 0, pre = 0, ablocks = 0;
     };
     std::vector<Seg> plan[4];
     int wide[4] = {0, 0, 0, 0};
@@ -128,7 +139,7 @@ struct SpFactor {
     {
         fl.release(); fu.release(); bu.release(); bl.release();
         Y.release(); Minv.release(); zq.release(); tpart.release(); bt.release(); scr.release(); scr2.release();
-        hh.release(); bz.release(); stamps.release();
+        hh.release(); bz.release(); stamps.release(); sacc.release();
         P.release();
         hdr.release();
     }
@@ -615,11 +626,150 @@ static void sp_build_solves(const SpLU &F, SpSolves &S)
 }
 
 // ---------------------------------------------------------------------------
+// LDS segments.  A run of narrow levels costs one barrier per level in the
+// single workgroup, and on the m = 100k late basis about 6 us of it is the
+// trip to the L2 for the entries the level gathers from the level before.
+// A segment of consecutive narrow levels (at most SP_SEG_MAX steps) is
+// solved in two passes instead: the external pass sums, for every step at
+// once, the entries that read values produced before the segment (one
+// parallel gather, on the grid when it is large); the internal pass then
+// walks the segment's levels with the segment's own outputs in LDS — a level
+// is LDS reads and a barrier, its metadata loaded a level ahead.
+// ---------------------------------------------------------------------------
+constexpr int SP_SEG_MAX = 8192;
+
+static bool sp_seg_on()
+{
+    static const bool on = [] {
+        const char *e = std::getenv("GK_SP_SEG");
+        return !e || atoi(e) != 0;
+    }();
+    return on;
+}
+
+// external entries from which a segment's external pass runs on the grid
+static int sp_ga_min()
+{
+    static const int g = [] {
+        const char *e = std::getenv("GK_SP_GA");
+        return e ? std::max(0, atoi(e)) : 8192;
+    }();
+    return g;
+}
+
+// the launch plan of one sweep, and the re-encoding of its LDS segments:
+// within a segment's levels the steps of at most TRI_LONG internal entries
+// first, every step's external entries before its internal ones (each class
+// in its original order), internal entries by the producing step's index in
+// the segment.  wide: 1 when the sweep runs by its plan (not the fused
+// one-workgroup kernels)
+static void sp_plan_sweep(SpTriHost &T, std::vector<SpFactor::Seg> &plan, int &wide)
+{
+    plan.clear();
+    wide = 0;
+    const int nlev = T.nlev, nst = nlev ? T.lvptr[nlev] : 0;
+    const bool seg = sp_seg_on();
+    int run = -1;                            // first level of the current narrow run
+    auto close_run = [&](int l1) {
+        if (run < 0) return;
+        if (!seg) plan.push_back({0, run, l1, 1});
+        else
+            for (int a = run; a < l1;) {     // greedy: levels while the steps fit
+                int b = a + 1;
+                while (b < l1 && T.lvptr[b + 1] - T.lvptr[a] <= SP_SEG_MAX) b++;
+                SpFactor::Seg g{2, a, b, 1};
+                g.sb = T.lvptr[a];
+                g.ns = T.lvptr[b] - T.lvptr[a];
+                plan.push_back(g);
+                a = b;
+            }
+        run = -1;
+    };
+    for (int l = 0; l < nlev; l++) {
+        const int nshort = T.lvlong[l] - T.lvptr[l], nlong = T.lvptr[l + 1] - T.lvlong[l];
+        if (nshort + nlong >= sp_wide_min()) {
+            close_run(l);
+            plan.push_back({1, l, l + 1, std::max(1, std::max((nshort + 255) / 256, std::min((nlong + 3) / 4, 1024)))});
+            wide = 1;
+        } else if (run < 0)
+            run = l;
+    }
+    close_run(nlev);
+    T.emid.assign(T.eptr.begin() + 1, T.eptr.end());
+    T.aord.assign(std::max(nst, 1), 0);
+    if (!seg) return;
+    wide = 1;
+    // producing step of every index the sweep writes; segment of every step
+    int M = 0;
+    for (int s = 0; s < nst; s++) M = std::max(M, T.iout[s] + 1);
+    for (int x : T.eidx) M = std::max(M, x + 1);
+    std::vector<int> prod(M, -1), segof(nst, -1), nint(nst, 0), next(nst, 0), order(nst), newpos(nst);
+    for (int s = 0; s < nst; s++) prod[T.iout[s]] = s;
+    for (size_t g = 0; g < plan.size(); g++)
+        if (plan[g].grid == 2)
+            for (int s = plan[g].sb; s < plan[g].sb + plan[g].ns; s++) segof[s] = (int)g;
+    auto internal = [&](int s, int e) {
+        const int p = prod[T.eidx[e]];
+        return segof[s] >= 0 && p >= 0 && segof[p] == segof[s];
+    };
+    for (int s = 0; s < nst; s++)
+        for (int e = T.eptr[s]; e < T.eptr[s + 1]; e++) {
+            if (internal(s, e)) nint[s]++;
+            else next[s]++;
+        }
+    for (int s = 0; s < nst; s++) order[s] = s;
+    for (const auto &g : plan)
+        if (g.grid == 2)
+            for (int l = g.l0; l < g.l1; l++) {
+                auto b = order.begin() + T.lvptr[l], e = order.begin() + T.lvptr[l + 1];
+                auto mid = std::stable_partition(b, e, [&](int k) { return nint[k] <= TRI_LONG; });
+                T.lvlong[l] = (int)(mid - order.begin());
+            }
+    for (int s = 0; s < nst; s++) newpos[order[s]] = s;
+    SpTriHost R;
+    R.iin.resize(nst); R.iout.resize(nst); R.diag.resize(nst); R.eptr.assign(nst + 1, 0); R.emid.assign(nst, 0);
+    R.eidx.resize(T.eidx.size()); R.eval.resize(T.eval.size());
+    int ne = 0;
+    for (int s = 0; s < nst; s++) {
+        const int k = order[s];
+        R.iin[s] = T.iin[k]; R.iout[s] = T.iout[k]; R.diag[s] = T.diag[k];
+        for (int pass = 0; pass < 2; pass++) {
+            for (int e = T.eptr[k]; e < T.eptr[k + 1]; e++) {
+                const bool in = internal(k, e);
+                if (in != (pass == 1)) continue;
+                R.eidx[ne] = in ? newpos[prod[T.eidx[e]]] - plan[segof[k]].sb : T.eidx[e];
+                R.eval[ne] = T.eval[e];
+                ne++;
+            }
+            if (pass == 0) R.emid[s] = ne;
+        }
+        R.eptr[s + 1] = ne;
+    }
+    T.iin.swap(R.iin); T.iout.swap(R.iout); T.diag.swap(R.diag); T.eptr.swap(R.eptr); T.emid.swap(R.emid);
+    T.eidx.swap(R.eidx); T.eval.swap(R.eval);
+    for (auto &g : plan) {
+        if (g.grid != 2) continue;
+        int nas = 0;
+        long long ext = 0;
+        for (int i = 0; i < g.ns; i++) {
+            const int s = g.sb + i, x = T.emid[s] - T.eptr[s];
+            ext += x;
+            if (x <= TRI_LONG) T.aord[g.sb + nas++] = i;
+        }
+        g.nas = nas;
+        for (int i = 0, t = nas; i < g.ns; i++)
+            if (T.emid[g.sb + i] - T.eptr[g.sb + i] > TRI_LONG) T.aord[g.sb + t++] = i;
+        g.pre = ext >= sp_ga_min();
+        g.ablocks = std::max(1, std::max((nas + 255) / 256, std::min((g.ns - nas + 3) / 4, 1024)));
+    }
+}
+
+// ---------------------------------------------------------------------------
 // device: level-scheduled sweeps (one workgroup; each level is one barrier,
 // the vectors stay in L2), two right-hand sides at once for the pivot FTRAN
 // ---------------------------------------------------------------------------
 struct TriDev {
-    const int *lvptr, *lvlong, *iin, *iout, *eptr, *eidx;
+    const int *lvptr, *lvlong, *iin, *iout, *eptr, *eidx, *emid, *aord;
     const double *diag, *eval;
     const int *nlev;                              // device word: levels of the current factor
     unsigned long long *stamps;                   // GK_SP_STAMPS: device clock after each level (null: off)
@@ -1027,6 +1177,229 @@ __global__ void __launch_bounds__(1024) k_sp_sweep(SpDev sp, TriDev t, const DSt
     }
 }
 
+// ---- LDS segments (sp_plan_sweep) ---------------------------------------
+// the external sum of a step of few external entries: its right-hand side
+// less them, in entry order, four gathers in flight per trip
+template <int NRHS>
+__device__ __forceinline__ void seg_ext_thread(const TriDev &t, const double *in0, const double *in1,
+                                               const double *out0, const double *out1, int s, double &a0, double &a1)
+{
+    const int ii = t.iin[s], ee = t.emid[s];
+    int e = t.eptr[s];
+    a0 = in0[ii];
+    a1 = (NRHS == 2) ? in1[ii] : 0.0;
+    for (; e + 4 <= ee; e += 4) {
+        int ix[4];
+        double v[4], x0[4], x1[4];
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            ix[u] = t.eidx[e + u];
+            v[u] = t.eval[e + u];
+        }
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            x0[u] = out0[ix[u]];
+            x1[u] = (NRHS == 2) ? out1[ix[u]] : 0.0;
+        }
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            a0 -= v[u] * x0[u];
+            if (NRHS == 2) a1 -= v[u] * x1[u];
+        }
+    }
+    for (; e < ee; e++) {
+        const int ix = t.eidx[e];
+        a0 -= t.eval[e] * out0[ix];
+        if (NRHS == 2) a1 -= t.eval[e] * out1[ix];
+    }
+}
+
+// the external sum of a step of many: one wave, lanes strided, fixed-order
+// reduction; every lane returns it
+template <int NRHS>
+__device__ __forceinline__ void seg_ext_wave(const TriDev &t, const double *in0, const double *in1,
+                                             const double *out0, const double *out1, int s, double &a0, double &a1)
+{
+    const int lane = threadIdx.x & 63, eb = t.eptr[s], ee = t.emid[s];
+    double p0 = 0.0, p1 = 0.0;
+    int e = eb + lane;
+    for (; e + 64 < ee; e += 128) {
+        const int i0 = t.eidx[e], i1 = t.eidx[e + 64];
+        const double v0 = t.eval[e], v1 = t.eval[e + 64];
+        const double x0 = out0[i0], x1 = out0[i1];
+        p0 += v0 * x0;
+        p0 += v1 * x1;
+        if (NRHS == 2) {
+            p1 += v0 * out1[i0];
+            p1 += v1 * out1[i1];
+        }
+    }
+    for (; e < ee; e += 64) {
+        const int ix = t.eidx[e];
+        p0 += t.eval[e] * out0[ix];
+        if (NRHS == 2) p1 += t.eval[e] * out1[ix];
+    }
+    p0 = wsum(p0);
+    if (NRHS == 2) p1 = wsum(p1);
+    const int ii = t.iin[s];
+    a0 = in0[ii] - p0;
+    a1 = (NRHS == 2) ? in1[ii] - p1 : 0.0;
+}
+
+// the external pass of a segment by nthr threads (thread g; the grid or one
+// workgroup, a multiple of 64): acc[local step] = the step's external sum
+template <int NRHS>
+__device__ void seg_ext(const TriDev &t, const double *in0, const double *in1, const double *out0, const double *out1,
+                        int sb, int ns, int nas, double *acc0, double *acc1, int g, int nthr)
+{
+    for (int i = g; i < nas; i += nthr) {
+        const int li = t.aord[sb + i];
+        double a0, a1;
+        seg_ext_thread<NRHS>(t, in0, in1, out0, out1, sb + li, a0, a1);
+        acc0[li] = a0;
+        if (NRHS == 2) acc1[li] = a1;
+    }
+    const int lane = g & 63;
+    for (int i = nas + (g >> 6); i < ns; i += nthr >> 6) {
+        const int li = t.aord[sb + i];
+        double a0, a1;
+        seg_ext_wave<NRHS>(t, in0, in1, out0, out1, sb + li, a0, a1);
+        if (lane == 0) {
+            acc0[li] = a0;
+            if (NRHS == 2) acc1[li] = a1;
+        }
+    }
+}
+
+// the external pass on the grid (a segment of many external entries): into
+// acc (2 x SP_SEG_MAX), which k_sp_seg then stages in LDS
+template <int NRHS>
+__global__ void __launch_bounds__(256) k_sp_seg_a(TriDev t, const DState *st, int gate, const double *in0,
+                                                  const double *in1, const double *out0, const double *out1, int sb,
+                                                  int ns, int nas, double *acc)
+{
+    if (sp_gated(st, gate)) return;
+    seg_ext<NRHS>(t, in0, in1, out0, out1, sb, ns, nas, acc, acc + SP_SEG_MAX, blockIdx.x * blockDim.x + threadIdx.x,
+                  gridDim.x * blockDim.x);
+}
+
+// a short step of the internal pass: metadata and its first internal entries
+// loaded a level ahead (none depends on the sweep's values)
+struct SegPre {
+    int s, io, eb, ee;
+    double dg;
+    int ix[4];
+    double v[4];
+};
+
+__device__ __forceinline__ void segpre_load(const TriDev &t, int s, int lim, SegPre &q)
+{
+    q.s = s;
+    if (s >= lim) return;
+    q.io = t.iout[s];
+    q.eb = t.emid[s];
+    q.ee = t.eptr[s + 1];
+    q.dg = t.diag[s];
+#pragma unroll
+    for (int u = 0; u < 4; u++) {
+        const bool ok = q.eb + u < q.ee;
+        q.ix[u] = ok ? t.eidx[q.eb + u] : 0;
+        q.v[u] = ok ? t.eval[q.eb + u] : 0.0;
+    }
+}
+
+template <int NRHS>
+__device__ __forceinline__ void segpre_run(const TriDev &t, const SegPre &q, int sb, double *L, double *out0,
+                                           double *out1)
+{
+    const int li = q.s - sb;
+    double a0 = L[li], a1 = (NRHS == 2) ? L[SP_SEG_MAX + li] : 0.0;
+#pragma unroll
+    for (int u = 0; u < 4; u++) {
+        if (q.eb + u < q.ee) {
+            a0 -= q.v[u] * L[q.ix[u]];
+            if (NRHS == 2) a1 -= q.v[u] * L[SP_SEG_MAX + q.ix[u]];
+        }
+    }
+    for (int e = q.eb + 4; e < q.ee; e++) {
+        const int ix = t.eidx[e];
+        a0 -= t.eval[e] * L[ix];
+        if (NRHS == 2) a1 -= t.eval[e] * L[SP_SEG_MAX + ix];
+    }
+    a0 /= q.dg;
+    L[li] = a0;
+    out0[q.io] = a0;
+    if (NRHS == 2) {
+        a1 /= q.dg;
+        L[SP_SEG_MAX + li] = a1;
+        out1[q.io] = a1;
+    }
+}
+
+// one LDS segment: levels l0 .. l1-1, steps sb .. sb+ns-1 (one workgroup);
+// pre: the external pass ran on the grid (acc); clr as k_sp_sweep
+template <int NRHS>
+__global__ void __launch_bounds__(1024) k_sp_seg(SpDev sp, TriDev t, const DState *st, int gate, const double *in0,
+                                                 const double *in1, double *out0, double *out1, int sb, int ns,
+                                                 int nas, int l0, int l1, int pre, const double *acc, int clr)
+{
+    if (sp_gated(st, gate)) return;
+    __shared__ double L[NRHS * SP_SEG_MAX];
+    const int T = blockDim.x, w = threadIdx.x >> 6, nw = blockDim.x >> 6, lane = threadIdx.x & 63;
+    int le = t.lvptr[l0 + 1], ls = t.lvlong[l0];
+    SegPre cur;
+    segpre_load(t, t.lvptr[l0] + (int)threadIdx.x, ls, cur);
+    if (pre)
+        for (int i = threadIdx.x; i < ns; i += T) {
+            L[i] = acc[i];
+            if (NRHS == 2) L[SP_SEG_MAX + i] = acc[SP_SEG_MAX + i];
+        }
+    else
+        seg_ext<NRHS>(t, in0, in1, out0, out1, sb, ns, nas, L, L + SP_SEG_MAX, threadIdx.x, T);
+    __syncthreads();
+    if (t.stamps && threadIdx.x == 0 && l0 < SP_STAMP_MAX) t.stamps[l0] = wall_clock64();
+    for (int l = l0; l < l1; l++) {
+        const int nb = le, ne = (l + 1 < l1) ? t.lvptr[l + 2] : le, nls = (l + 1 < l1) ? t.lvlong[l + 1] : le;
+        SegPre nxt;
+        segpre_load(t, nb + (int)threadIdx.x, nls, nxt);
+        if (cur.s < ls) segpre_run<NRHS>(t, cur, sb, L, out0, out1);
+        for (int s = cur.s + T; s < ls; s += T) {            // short steps beyond one per thread
+            SegPre q;
+            segpre_load(t, s, ls, q);
+            segpre_run<NRHS>(t, q, sb, L, out0, out1);
+        }
+        for (int s = ls + w; s < le; s += nw) {               // many internal entries: a wave each
+            const int eb = t.emid[s], ee = t.eptr[s + 1];
+            double p0 = 0.0, p1 = 0.0;
+            for (int e = eb + lane; e < ee; e += 64) {
+                const int ix = t.eidx[e];
+                p0 += t.eval[e] * L[ix];
+                if (NRHS == 2) p1 += t.eval[e] * L[SP_SEG_MAX + ix];
+            }
+            p0 = wsum(p0);
+            if (NRHS == 2) p1 = wsum(p1);
+            if (lane == 0) {
+                const int li = s - sb, io = t.iout[s];
+                const double dg = t.diag[s];
+                const double v0 = (L[li] - p0) / dg;
+                L[li] = v0;
+                out0[io] = v0;
+                if (NRHS == 2) {
+                    const double v1 = (L[SP_SEG_MAX + li] - p1) / dg;
+                    L[SP_SEG_MAX + li] = v1;
+                    out1[io] = v1;
+                }
+            }
+        }
+        __syncthreads();
+        if (t.stamps && threadIdx.x == 0 && l + 1 < SP_STAMP_MAX) t.stamps[l + 1] = wall_clock64();
+        cur = nxt;
+        le = ne;
+        ls = nls;
+    }
+    if (clr) bz_clear(sp, st->p - 1, *sp.w.k);
+}
+
 // the FTRAN's inv(M) z[P] (k_sp_ftran_lu's tail) as its own launch, after a
 // U sweep that ended on the grid or in a k_sp_sweep
 template <int NRHS>
@@ -1249,6 +1622,12 @@ static void up_tri(hipStream_t s, SpTriDevBufs &B, const SpTriHost &T, int *d_nl
     B.eidx.ensure(std::max<size_t>(T.eidx.size(), 1));
     B.diag.ensure(std::max<size_t>(T.diag.size(), 1));
     B.eval.ensure(std::max<size_t>(T.eval.size(), 1));
+    B.emid.ensure(std::max<size_t>(T.emid.size(), 1));
+    B.aord.ensure(std::max<size_t>(T.aord.size(), 1));
+    if (!T.emid.empty())
+        SPCHK(hipMemcpyAsync(B.emid.p, T.emid.data(), T.emid.size() * sizeof(int), hipMemcpyHostToDevice, s));
+    if (!T.aord.empty())
+        SPCHK(hipMemcpyAsync(B.aord.p, T.aord.data(), T.aord.size() * sizeof(int), hipMemcpyHostToDevice, s));
     SPCHK(hipMemcpyAsync(B.lvptr.p, T.lvptr.data(), T.lvptr.size() * sizeof(int), hipMemcpyHostToDevice, s));
     if (!T.lvlong.empty())
         SPCHK(hipMemcpyAsync(B.lvlong.p, T.lvlong.data(), T.lvlong.size() * sizeof(int), hipMemcpyHostToDevice, s));
@@ -1267,7 +1646,7 @@ static TriDev tri_dev(const SpTriDevBufs &B, const int *nlev, unsigned long long
 {
     TriDev t;
     t.lvptr = B.lvptr.p; t.lvlong = B.lvlong.p; t.iin = B.iin.p; t.iout = B.iout.p; t.eptr = B.eptr.p; t.eidx = B.eidx.p;
-    t.diag = B.diag.p; t.eval = B.eval.p; t.nlev = nlev; t.stamps = stamps;
+    t.diag = B.diag.p; t.eval = B.eval.p; t.nlev = nlev; t.stamps = stamps; t.emid = B.emid.p; t.aord = B.aord.p;
     return t;
 }
 
@@ -1367,25 +1746,8 @@ static int sp_factorize_cols(SpFactor &F, hipStream_t s, int m, const std::vecto
     F.nnz_l = (long long)lu.Lrow.size();
     F.nnz_u = (long long)lu.Ucol.size() + m;
     F.levels[0] = S.fl.nlev; F.levels[1] = S.fu.nlev; F.levels[2] = S.bu.nlev; F.levels[3] = S.bl.nlev;
-    const SpTriHost *T4[4] = {&S.fl, &S.fu, &S.bu, &S.bl};
-    for (int i = 0; i < 4; i++) {
-        const SpTriHost &T = *T4[i];
-        F.plan[i].clear();
-        F.wide[i] = 0;
-        int run = -1;                        // first level of the current narrow run
-        for (int l = 0; l < T.nlev; l++) {
-            const int nshort = T.lvlong[l] - T.lvptr[l], nlong = T.lvptr[l + 1] - T.lvlong[l];
-            if (nshort + nlong >= sp_wide_min()) {
-                if (run >= 0) F.plan[i].push_back({0, run, l, 1});
-                run = -1;
-                F.plan[i].push_back({1, l, l + 1, std::max(1, std::max((nshort + 255) / 256,
-                                                                       std::min((nlong + 3) / 4, 1024)))});
-                F.wide[i] = 1;
-            } else if (run < 0)
-                run = l;
-        }
-        if (run >= 0) F.plan[i].push_back({0, run, T.nlev, 1});
-    }
+    SpTriHost *T4[4] = {&S.fl, &S.fu, &S.bu, &S.bl};
+    for (int i = 0; i < 4; i++) sp_plan_sweep(*T4[i], F.plan[i], F.wide[i]);
     if (F.m != m) {
         F.m = m;
         F.Y.ensure((size_t)m * SP_KMAX);
@@ -1399,6 +1761,7 @@ static int sp_factorize_cols(SpFactor &F, hipStream_t s, int m, const std::vecto
     }
     F.P.ensure(SP_KMAX);
     F.hh.ensure((size_t)2 * SP_KMAX);
+    F.sacc.ensure((size_t)2 * SP_SEG_MAX);
     F.Minv.ensure((size_t)SP_KMAX * SP_KMAX);
     F.hdr.ensure(8);
     if (sp_stamps_path()) {
@@ -1433,7 +1796,14 @@ static void run_plan(const SpFactor &F, int which, const SpDev &d, hipStream_t s
     const auto &pl = F.plan[which];
     for (size_t q = 0; q < pl.size(); q++) {
         const int last = clr && q + 1 == pl.size();
-        if (pl[q].grid) {
+        if (pl[q].grid == 2) {
+            const auto &g = pl[q];
+            if (g.pre)
+                hipLaunchKernelGGL((k_sp_seg_a<NRHS>), dim3(g.ablocks), dim3(256), 0, s, t, st, gate, in0, in1,
+                                   (const double *)out0, (const double *)out1, g.sb, g.ns, g.nas, F.sacc.p);
+            hipLaunchKernelGGL((k_sp_seg<NRHS>), dim3(1), dim3(1024), 0, s, d, t, st, gate, in0, in1, out0, out1, g.sb,
+                               g.ns, g.nas, g.l0, g.l1, g.pre, (const double *)F.sacc.p, last);
+        } else if (pl[q].grid) {
             hipLaunchKernelGGL((k_sp_level<NRHS>), dim3(pl[q].blocks), dim3(256), 0, s, t, st, gate, in0, in1, out0,
                                out1, pl[q].l0);
             if (last)
@@ -1578,14 +1948,35 @@ void sp_stamps_dump(SpFactor &F, hipStream_t s, int wall_khz)
 // BTRAN U' / L'.  Lets the CPU tests pin the elimination and the level
 // schedules against numpy without a GPU.
 // ---------------------------------------------------------------------------
-static void host_sweep(const SpTriHost &t, const double *in, double *out)
+// a sweep by its plan (the LDS segments' two passes, as k_sp_seg runs them)
+static void host_sweep_plan(const SpTriHost &t, const std::vector<SpFactor::Seg> &plan, const double *in, double *out)
 {
-    for (int l = 0; l < t.nlev; l++)
-        for (int s = t.lvptr[l]; s < t.lvptr[l + 1]; s++) {
-            double a = in[t.iin[s]];
-            for (int e = t.eptr[s]; e < t.eptr[s + 1]; e++) a -= t.eval[e] * out[t.eidx[e]];
-            out[t.iout[s]] = a / t.diag[s];
+    std::vector<double> acc;
+    for (const auto &g : plan) {
+        if (g.grid != 2) {
+            for (int l = g.l0; l < g.l1; l++)
+                for (int s = t.lvptr[l]; s < t.lvptr[l + 1]; s++) {
+                    double a = in[t.iin[s]];
+                    for (int e = t.eptr[s]; e < t.eptr[s + 1]; e++) a -= t.eval[e] * out[t.eidx[e]];
+                    out[t.iout[s]] = a / t.diag[s];
+                }
+            continue;
         }
+        acc.assign(g.ns, 0.0);
+        for (int i = 0; i < g.ns; i++) {
+            const int li = t.aord[g.sb + i], s = g.sb + li;
+            double a = in[t.iin[s]];
+            for (int e = t.eptr[s]; e < t.emid[s]; e++) a -= t.eval[e] * out[t.eidx[e]];
+            acc[li] = a;
+        }
+        for (int l = g.l0; l < g.l1; l++)
+            for (int s = t.lvptr[l]; s < t.lvptr[l + 1]; s++) {
+                double a = acc[s - g.sb];
+                for (int e = t.emid[s]; e < t.eptr[s + 1]; e++) a -= t.eval[e] * acc[t.eidx[e]];
+                acc[s - g.sb] = a / t.diag[s];
+                out[t.iout[s]] = acc[s - g.sb];
+            }
+    }
 }
 
 }  // namespace gk
@@ -1617,10 +2008,16 @@ extern "C" int gk_sp_selftest(int m, const int *ptr, const int *ind, const doubl
         stats[1] = (long long)lu.Ucol.size() + m;
         stats[2] = S.fl.nlev; stats[3] = S.fu.nlev; stats[4] = S.bu.nlev; stats[5] = S.bl.nlev;
     }
+    // the sweeps as the device runs them: re-encoded for LDS segments
+    // (GK_SP_SEG, sp_plan_sweep) and solved by their plans
+    std::vector<SpFactor::Seg> pl[4];
+    int wd[4];
+    SpTriHost *T4[4] = {&S.fl, &S.fu, &S.bu, &S.bl};
+    for (int i = 0; i < 4; i++) sp_plan_sweep(*T4[i], pl[i], wd[i]);
     std::vector<double> z(b, b + m), w(m);
-    host_sweep(S.fl, z.data(), z.data());
-    host_sweep(S.fu, z.data(), x);
-    host_sweep(S.bu, e, w.data());
-    host_sweep(S.bl, w.data(), y);
+    host_sweep_plan(S.fl, pl[0], z.data(), z.data());
+    host_sweep_plan(S.fu, pl[1], z.data(), x);
+    host_sweep_plan(S.bu, pl[2], e, w.data());
+    host_sweep_plan(S.bl, pl[3], w.data(), y);
     return 0;
 }
