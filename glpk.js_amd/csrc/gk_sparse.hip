@@ -39,6 +39,7 @@
 #include <cstring>
 #include <stdexcept>
 #include <string>
+#include <thread>
 #include <vector>
 
 namespace gk {
@@ -213,7 +214,8 @@ struct SpLUWork {
     std::vector<std::vector<double>> rv;
     std::vector<double> rmax;
     std::vector<char> ract, cact;
-    std::vector<int> wpos, rows;
+    std::vector<int> wpos, rows, rsing;
+    std::vector<char> cdone;
     Buckets R, C;
     std::vector<int> lid;                  // long rows: their slot in lmap (-1: short)
     std::vector<std::vector<int>> lmap;    // per long row: column -> index in the row (-1: none)
@@ -239,14 +241,57 @@ static int sp_lu_factor(SpLU &F, SpLUWork &Wk, int m, const std::vector<int> &cp
     std::vector<std::vector<int>> &cr = Wk.cr;     // column j: rows
     if ((int)rc.size() < m) { rc.resize(m); rv.resize(m); cr.resize(m); }
     for (int i = 0; i < m; i++) { rc[i].clear(); rv[i].clear(); cr[i].clear(); }
-    for (int j = 0; j < m; j++)
-        for (int t = cptr[j]; t < cptr[j + 1]; t++) {
-            const int i = crow[t];
-            if (cval[t] == 0.0) continue;
-            rc[i].push_back(j);
-            rv[i].push_back(cval[t]);
-            cr[j].push_back(i);
-        }
+    // the column singletons of B (the slack columns of an LP basis, most of
+    // the columns of a late one) pivot first, each on its own row, before
+    // the active matrix exists: their rows go to U as they are, their L etas
+    // are empty, and the elimination below starts on the rest (the pivots
+    // the loop would take first anyway, without its pattern upkeep)
+    std::vector<int> &rsing = Wk.rsing;            // row -> its singleton pivot (-1: none)
+    rsing.assign(m, -1);
+    std::vector<char> &cdone = Wk.cdone;
+    cdone.assign(m, 0);
+    int k0 = 0;
+    for (int j = 0; j < m; j++) {
+        int nz = 0, ti = -1;
+        for (int t = cptr[j]; t < cptr[j + 1]; t++)
+            if (cval[t] != 0.0) { nz++; ti = t; }
+        if (nz != 1 || rsing[crow[ti]] >= 0) continue;
+        rsing[crow[ti]] = k0;
+        cdone[j] = 1;
+        F.pr[k0] = crow[ti];
+        F.pc[k0] = j;
+        F.Udiag[k0] = cval[ti];
+        k0++;
+    }
+    {
+        // U rows of the singleton pivots: the other entries of their rows
+        std::vector<int> &cnt = Wk.wpos;
+        cnt.assign(k0 + 1, 0);
+        for (int j = 0; j < m; j++)
+            if (!cdone[j])
+                for (int t = cptr[j]; t < cptr[j + 1]; t++)
+                    if (cval[t] != 0.0 && rsing[crow[t]] >= 0) cnt[rsing[crow[t]] + 1]++;
+        for (int q = 0; q < k0; q++) cnt[q + 1] += cnt[q];
+        F.Uptr.assign(cnt.begin(), cnt.end());
+        F.Ucol.assign(cnt[k0], 0);
+        F.Uval.assign(cnt[k0], 0.0);
+        for (int j = 0; j < m; j++)
+            if (!cdone[j])
+                for (int t = cptr[j]; t < cptr[j + 1]; t++) {
+                    const int i = crow[t];
+                    if (cval[t] == 0.0) continue;
+                    if (rsing[i] >= 0) {
+                        const int f = cnt[rsing[i]]++;
+                        F.Ucol[f] = j;
+                        F.Uval[f] = cval[t];
+                    } else {
+                        rc[i].push_back(j);
+                        rv[i].push_back(cval[t]);
+                        cr[j].push_back(i);
+                    }
+                }
+        F.Lptr.assign(k0 + 1, 0);
+    }
     Buckets &R = Wk.R, &C = Wk.C;
     R.init(m, m);
     C.init(m, m);
@@ -276,11 +321,17 @@ static int sp_lu_factor(SpLU &F, SpLUWork &Wk, int m, const std::vector<int> &cp
     };
     for (int i = 0; i < m; i++)
         if ((int)rc[i].size() > LU_LONG) make_long(i);
-    for (int i = 0; i < m; i++) R.add(i, (int)rc[i].size());
-    for (int j = 0; j < m; j++) C.add(j, (int)cr[j].size());
+    for (int i = 0; i < m; i++)
+        if (rsing[i] < 0) R.add(i, (int)rc[i].size());
+    for (int j = 0; j < m; j++)
+        if (!cdone[j]) C.add(j, (int)cr[j].size());
     std::vector<char> &ract = Wk.ract, &cact = Wk.cact;
     ract.assign(m, 1);
     cact.assign(m, 1);
+    for (int i = 0; i < m; i++)
+        if (rsing[i] >= 0) ract[i] = 0;
+    for (int j = 0; j < m; j++)
+        if (cdone[j]) cact[j] = 0;
     std::vector<double> &rmax = Wk.rmax;           // cached max |a_ij| of row i (< 0: stale)
     rmax.assign(m, -1.0);
     auto row_max = [&](int i) {
@@ -300,17 +351,25 @@ static int sp_lu_factor(SpLU &F, SpLUWork &Wk, int m, const std::vector<int> &cp
     };
     std::vector<int> &wpos = Wk.wpos;              // column -> index in the row being updated
     wpos.assign(m, -1);
+    static const bool tdiag = std::getenv("GK_SP_TIMES") != nullptr;
+    double t_search = 0.0, t_elim = 0.0, tt = 0.0;
+    long long n_cs = 0, n_rs = 0, n_mk = 0, n_rows = 0, n_upd = 0, n_cand = 0;
     int k;
-    for (k = 0; k < m; k++) {
+    n_cs = k0;
+    for (k = k0; k < m; k++) {
+        if (tdiag) tt = sp_now();
         int pi = -1, pj = -1;
         // column singleton, then row singleton
         if (C.head[1] >= 0) {
             pj = C.head[1];
             pi = cr[pj][0];
+            n_cs++;
         } else if (R.head[1] >= 0) {
             pi = R.head[1];
             pj = rc[pi][0];
+            n_rs++;
         } else {
+            n_mk++;
             long long best = -1;
             double bestv = 0.0;
             int ncand = 0;
@@ -354,6 +413,11 @@ static int sp_lu_factor(SpLU &F, SpLUWork &Wk, int m, const std::vector<int> &cp
             }
         }
         if (pi < 0 || pj < 0) break;
+        if (tdiag) {
+            const double t1 = sp_now();
+            t_search += t1 - tt;
+            tt = t1;
+        }
         // the pivot
         const int tp = find_in_row(pi, pj);
         const double vp = rv[pi][tp];
@@ -383,6 +447,8 @@ static int sp_lu_factor(SpLU &F, SpLUWork &Wk, int m, const std::vector<int> &cp
         C.del(pj);
         cact[pj] = 0;
         cr[pj].clear();
+        n_rows += (long long)rows.size();
+        n_upd += (long long)rows.size() * (long long)rc[pi].size();
         for (int i : rows) {
             const int ti = find_in_row(i, pj);
             const double f = rv[i][ti] / vp;
@@ -458,7 +524,13 @@ static int sp_lu_factor(SpLU &F, SpLUWork &Wk, int m, const std::vector<int> &cp
             for (int j : rc[pi]) lmap[lid[pi]][j] = -1;      // the slot goes back all -1
         rc[pi].clear();
         rv[pi].clear();
+        if (tdiag) t_elim += sp_now() - tt;
     }
+    if (tdiag)
+        fprintf(stderr, "[gk sp times] LU search %.2f ms, elimination %.2f ms; pivots: %lld column / %lld row singletons, "
+                "%lld Markowitz; %lld row updates, %lld update entries\n", 1e3 * t_search, 1e3 * t_elim, n_cs, n_rs, n_mk,
+                n_rows, n_upd);
+    (void)n_cand;
     *rank = k;
     // (singular: rows left active keep entries in their maps)
     for (int i = 0; i < m; i++)
@@ -593,36 +665,66 @@ static void sp_deps_direct(SpDeps &D, int m, const std::vector<int> &sptr, const
     }
 }
 
-static void sp_build_solves(const SpLU &F, SpSolves &S)
+static void sp_plan_sweep(SpTriHost &T, std::vector<SpFactor::Seg> &plan, int &wide);
+
+// the four sweeps and their launch plans, one host thread each
+static void sp_build_solves(const SpLU &F, SpSolves &S, std::vector<SpFactor::Seg> *plan, int *wide)
 {
     const int m = F.m;
-    thread_local std::vector<int> step_of_row, step_of_pos, in, out;
-    thread_local std::vector<double> ones;
-    thread_local SpDeps D;
-    step_of_row.resize(m);
-    step_of_pos.resize(m);
+    std::vector<int> step_of_row(m), step_of_pos(m);
     for (int k = 0; k < m; k++) { step_of_row[F.pr[k]] = k; step_of_pos[F.pc[k]] = k; }
-    ones.assign(m, 1.0);
-    in.resize(m);
-    out.resize(m);
-    // FTRAN L: deps of step k' = (z index r_t, l) for every eta t < k' holding row r_k'
-    sp_deps_transposed(D, m, F.Lptr, F.Lval, [&](int e) { return step_of_row[F.Lrow[e]]; },
-                       [&](int t) { return F.pr[t]; });
-    for (int k = 0; k < m; k++) in[k] = F.pr[k];
-    sp_build_tri(S.fl, m, in, in, ones, D, false, true);
-    // FTRAN U: deps of step k = (x index c_t, u) for the entries of U row k
-    sp_deps_direct(D, m, F.Uptr, F.Ucol, F.Uval, [](int c) { return c; }, [&](int c) { return step_of_pos[c]; });
-    for (int k = 0; k < m; k++) { in[k] = F.pr[k]; out[k] = F.pc[k]; }
-    sp_build_tri(S.fu, m, in, out, F.Udiag, D, true);
-    // BTRAN U': deps of step k = (w index t, u) for every U row t < k holding column c_k
-    sp_deps_transposed(D, m, F.Uptr, F.Uval, [&](int e) { return step_of_pos[F.Ucol[e]]; },
-                       [](int t) { return t; });
-    for (int k = 0; k < m; k++) { in[k] = F.pc[k]; out[k] = k; }
-    sp_build_tri(S.bu, m, in, out, F.Udiag, D, false);
-    // BTRAN L': deps of step k = (y index i, l) for the entries of eta k
-    sp_deps_direct(D, m, F.Lptr, F.Lrow, F.Lval, [](int i) { return i; }, [&](int i) { return step_of_row[i]; });
-    for (int k = 0; k < m; k++) { in[k] = k; out[k] = F.pr[k]; }
-    sp_build_tri(S.bl, m, in, out, ones, D, true);
+    auto sweep = [&](int which) {
+        thread_local std::vector<int> in, out;
+        thread_local std::vector<double> ones;
+        thread_local SpDeps D;
+        in.resize(m);
+        out.resize(m);
+        switch (which) {
+        case 0:
+            // FTRAN L: deps of step k' = (z index r_t, l) for every eta t < k' holding row r_k'
+            sp_deps_transposed(D, m, F.Lptr, F.Lval, [&](int e) { return step_of_row[F.Lrow[e]]; },
+                               [&](int t) { return F.pr[t]; });
+            for (int k = 0; k < m; k++) in[k] = F.pr[k];
+            ones.assign(m, 1.0);
+            sp_build_tri(S.fl, m, in, in, ones, D, false, true);
+            sp_plan_sweep(S.fl, plan[0], wide[0]);
+            break;
+        case 1:
+            // FTRAN U: deps of step k = (x index c_t, u) for the entries of U row k
+            sp_deps_direct(D, m, F.Uptr, F.Ucol, F.Uval, [](int c) { return c; },
+                           [&](int c) { return step_of_pos[c]; });
+            for (int k = 0; k < m; k++) { in[k] = F.pr[k]; out[k] = F.pc[k]; }
+            sp_build_tri(S.fu, m, in, out, F.Udiag, D, true);
+            sp_plan_sweep(S.fu, plan[1], wide[1]);
+            break;
+        case 2:
+            // BTRAN U': deps of step k = (w index t, u) for every U row t < k holding column c_k
+            sp_deps_transposed(D, m, F.Uptr, F.Uval, [&](int e) { return step_of_pos[F.Ucol[e]]; },
+                               [](int t) { return t; });
+            for (int k = 0; k < m; k++) { in[k] = F.pc[k]; out[k] = k; }
+            sp_build_tri(S.bu, m, in, out, F.Udiag, D, false);
+            sp_plan_sweep(S.bu, plan[2], wide[2]);
+            break;
+        default:
+            // BTRAN L': deps of step k = (y index i, l) for the entries of eta k
+            sp_deps_direct(D, m, F.Lptr, F.Lrow, F.Lval, [](int i) { return i; },
+                           [&](int i) { return step_of_row[i]; });
+            for (int k = 0; k < m; k++) { in[k] = k; out[k] = F.pr[k]; }
+            ones.assign(m, 1.0);
+            sp_build_tri(S.bl, m, in, out, ones, D, true);
+            sp_plan_sweep(S.bl, plan[3], wide[3]);
+            break;
+        }
+    };
+    static const bool lvlog = std::getenv("GK_SP_LEVELS") != nullptr;   // (its lines in sweep order)
+    if (m < 4096 || lvlog) {
+        for (int w = 0; w < 4; w++) sweep(w);
+        return;
+    }
+    std::thread th[3];
+    for (int w = 1; w < 4; w++) th[w - 1] = std::thread(sweep, w);
+    sweep(0);
+    for (auto &t : th) t.join();
 }
 
 // ---------------------------------------------------------------------------
@@ -1742,12 +1844,11 @@ static int sp_factorize_cols(SpFactor &F, hipStream_t s, int m, const std::vecto
     F.t_lu = sp_now() - t0;
     if (ret) return 1;
     thread_local SpSolves S;
-    sp_build_solves(lu, S);
+    sp_build_solves(lu, S, F.plan, F.wide);
     F.nnz_l = (long long)lu.Lrow.size();
     F.nnz_u = (long long)lu.Ucol.size() + m;
     F.levels[0] = S.fl.nlev; F.levels[1] = S.fu.nlev; F.levels[2] = S.bu.nlev; F.levels[3] = S.bl.nlev;
-    SpTriHost *T4[4] = {&S.fl, &S.fu, &S.bu, &S.bl};
-    for (int i = 0; i < 4; i++) sp_plan_sweep(*T4[i], F.plan[i], F.wide[i]);
+    const SpTriHost *T4[4] = {&S.fl, &S.fu, &S.bu, &S.bl};
     if (F.m != m) {
         F.m = m;
         F.Y.ensure((size_t)m * SP_KMAX);
@@ -2000,9 +2101,15 @@ extern "C" int gk_sp_selftest(int m, const int *ptr, const int *ind, const doubl
     SpLU lu;
     SpLUWork wk;
     int rank = 0;
+    if (std::getenv("GK_SP_TIMES")) sp_lu_factor(lu, wk, m, cptr, crow, cval, 0.1, 4, 1e-15, &rank);   // warm storage
+    const double t0 = sp_now();
     if (sp_lu_factor(lu, wk, m, cptr, crow, cval, 0.1, 4, 1e-15, &rank)) return 1;
+    const double t1 = sp_now();
     SpSolves S;
-    sp_build_solves(lu, S);
+    std::vector<SpFactor::Seg> pl[4];
+    int wd[4];
+    sp_build_solves(lu, S, pl, wd);
+    const double t2 = sp_now();
     if (stats) {
         stats[0] = (long long)lu.Lrow.size();
         stats[1] = (long long)lu.Ucol.size() + m;
@@ -2010,10 +2117,8 @@ extern "C" int gk_sp_selftest(int m, const int *ptr, const int *ind, const doubl
     }
     // the sweeps as the device runs them: re-encoded for LDS segments
     // (GK_SP_SEG, sp_plan_sweep) and solved by their plans
-    std::vector<SpFactor::Seg> pl[4];
-    int wd[4];
-    SpTriHost *T4[4] = {&S.fl, &S.fu, &S.bu, &S.bl};
-    for (int i = 0; i < 4; i++) sp_plan_sweep(*T4[i], pl[i], wd[i]);
+    if (std::getenv("GK_SP_TIMES"))
+        fprintf(stderr, "[gk sp times] LU %.2f ms, solves and plans %.2f ms\n", 1e3 * (t1 - t0), 1e3 * (t2 - t1));
     std::vector<double> z(b, b + m), w(m);
     host_sweep_plan(S.fl, pl[0], z.data(), z.data());
     host_sweep_plan(S.fu, pl[1], z.data(), x);

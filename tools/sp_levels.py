@@ -23,11 +23,12 @@ def main():
         basis = args[1]
         args = args[2:]
     if os.environ.get("GK_SP_LEVELS") is None:
-        env = dict(os.environ, GK_SP_LEVELS="1")
+        env = dict(os.environ, GK_SP_LEVELS="1", GK_SP_TIMES="1")
         r = subprocess.run([sys.executable, __file__, "--basis", basis] + args, env=env, capture_output=True, text=True)
         sys.stdout.write(r.stdout)
         names = ["FTRAN L", "FTRAN U", "BTRAN U'", "BTRAN L'"]
         lines = [ln for ln in r.stderr.splitlines() if ln.startswith("[gk sp levels]")]
+        print("\n".join(ln for ln in r.stderr.splitlines() if ln.startswith("[gk sp times]")))
         for name, ln in zip(names, lines[-4:]):
             body = ln.split("]", 1)[1].split("(")[0].split()
             lv = [tuple(int(x) for x in t.split("/")) for t in body]
@@ -61,7 +62,10 @@ def main():
     f = lambda a: a.ctypes.data_as(C.c_void_p)  # noqa: E731
     L = gk.load_library()
     L.gk_sp_selftest.restype = C.c_int
+    import time
+    t0 = time.perf_counter()
     ret = L.gk_sp_selftest(m, f(ptr), f(ind), f(val), f(b), f(e), f(x), f(y), f(st))
+    print(f"selftest (LU + solves build + plans + host sweeps) {1e3 * (time.perf_counter() - t0):.1f} ms")
     print("selftest ret", ret, "stats", st.tolist(), flush=True)
     # residuals of the two solves (the sweeps as the device runs them)
     import scipy.sparse as sps
