@@ -1151,11 +1151,39 @@ struct Spx {
         return ret == 0;
     }
     int fact_ret = 0;
-    // B0 = L U of the current basis on the host (gk_sparse.hip), uploaded
+    int sp_replayed = 0;                     // pivots the look-ahead's factor was given back (the chain's length)
+    // B0 = L U of the current basis on the host (gk_sparse.hip), uploaded;
+    // or, at a scheduled refactorization, the look-ahead's factor of an
+    // earlier basis of the chain with the later pivots replayed onto it
     int sparse_reinvert()
     {
         const double t0 = now_s();
         int ret;
+        sp_replayed = 0;
+        if (sp_ahead_mark(*f->sp) >= 0) {
+            if (f->valid && hs.upd_cnt >= hs.upd_lim) {
+                MatDev A = E->mat();
+                double tw = 0.0;
+                const int r = sp_ahead_install(*f->sp, s, -1, A.cptr, A.cind, A.cval, E->h.p, &tw);
+                if (r >= 0) {
+                    sp_replayed = r;
+                    f->fact_ver++;
+                    f->valid = 1;
+                    f->upd_cnt = r;
+                    f->ext_upd = 0;
+                    f->stats.reinversions++;
+                    f->stats.lu_ahead++;
+                    f->stats.seconds_lu += tw;             // the LU time the pivots did not hide
+                    f->stats.seconds_reinvert += now_s() - t0;
+                    static const bool slog = std::getenv("GK_SPARSE_LOG") != nullptr;
+                    if (slog)
+                        fprintf(stderr, "[gk sparse] it %d: look-ahead factor, %d pivots replayed, join waited %.2f ms, "
+                                "refactor %.2f ms\n", hs.it_cnt, r, 1e3 * tw, 1e3 * (now_s() - t0));
+                    return 0;
+                }
+            } else
+                sp_ahead_cancel(*f->sp);
+        }
         try {
             ret = sp_factorize(*f->sp, s, m, head.data(), E->hcptr.data(), E->hcind.data(), E->hcval.data(),
                                f->parm.piv_tol, f->parm.piv_lim, f->parm.eps_tol);
@@ -1192,6 +1220,25 @@ struct Spx {
     // basis and may be refined instead of rebuilt (gk_newton.hip)
     bool refine_next = false;
     int echk_seen = 0;
+
+    // the sparse factor's look-ahead (GK_SP_AHEAD: the fraction of the update
+    // limit at which the next LU starts on a host thread; 0 turns it off):
+    // the basis at that point of the chain is factorized while the device
+    // pivots on, and the pivots since are replayed at the refactorization
+    // (sp_ahead_install).  The start is a pivot count, not a time, so the
+    // path stays deterministic
+    void ahead_maybe()
+    {
+        static const double frac = [] {
+            const char *e = std::getenv("GK_SP_AHEAD");
+            return e ? std::atof(e) : 0.5;
+        }();
+        if (frac <= 0.0 || !f->valid || sp_ahead_mark(*f->sp) >= 0 || hs.npiv == 0 || hs.refact_pending) return;
+        if (hs.upd_lim < 32 || hs.upd_cnt >= hs.upd_lim || hs.upd_cnt < (int)(frac * hs.upd_lim)) return;
+        pull();
+        sp_ahead_start(*f->sp, m, head.data(), E->hcptr.data(), E->hcind.data(), E->hcval.data(), f->parm.piv_tol,
+                       f->parm.piv_lim, f->parm.eps_tol, sp_log_count(*f->sp, s));
+    }
 
     // ---- the reference's terminal output (display, glpspx01.js:1550-1589 /
     // glpspx02.js:1452-1497, and the xprintf lines of the main loops), as
@@ -2079,7 +2126,7 @@ int Spx::run_dual()
             det_log(f->stats.refinements != nref0 ? "reinv-newton" : "reinv");
             binv_st = 1;
             bbar_st = cbar_st = 0;
-            hs.upd_cnt = 0; hs.refact_pending = 0; hs.grow_bits = 0;
+            hs.upd_cnt = sp_replayed; hs.refact_pending = 0; hs.grow_bits = 0;
         }
         hs.binv_fresh = (binv_st == 1);
         if (cbar_st == 0) {
@@ -2216,6 +2263,7 @@ int Spx::run_dual()
         K = align_to_refactor(K, hs.upd_lim - hs.upd_cnt);
         K = align_to_display(K);
         int why = batch(K, rigorous);
+        if (f->sparse) ahead_maybe();
         det_log("batch", K, why);
         if (f->sparse) sp_stamps_dump(*f->sp, s, ctx->wall_khz);
         E->kbatch = next_batch(E->kbatch, why);
@@ -2301,7 +2349,7 @@ int Spx::run_primal()
             det_log(f->stats.refinements != nref0 ? "reinv-newton" : "reinv");
             binv_st = 1;
             bbar_st = cbar_st = 0;
-            hs.upd_cnt = 0; hs.refact_pending = 0; hs.grow_bits = 0;
+            hs.upd_cnt = sp_replayed; hs.refact_pending = 0; hs.grow_bits = 0;
         }
         hs.binv_fresh = (binv_st == 1);
         if (bbar_st == 0) {
@@ -2380,6 +2428,7 @@ int Spx::run_primal()
         K = align_to_refactor(K, hs.upd_lim - hs.upd_cnt);
         K = align_to_display(K);
         int why = batch(K, rigorous);
+        if (f->sparse) ahead_maybe();
         det_log("batch", K, why);
         E->kbatch = next_batch(E->kbatch, why);
         if (hs.npiv > 0) {

@@ -168,7 +168,18 @@ void sp_pivot_ftran(SpFactor &F, hipStream_t s, const DState *st, double *h, dou
                     int pse);
 void sp_pivot_update(SpFactor &F, hipStream_t s, DState *st);
 void sp_pivot_btran2(SpFactor &F, hipStream_t s, DState *st, const double *v, double *rho, double *u);
-void sp_stamps_dump(SpFactor &F, hipStream_t s, int wall_khz);   // GK_SP_STAMPS (diagnostics)
+void sp_stamps_dump(SpFactor &F, hipStream_t s, int wall_khz);
+// the look-ahead factorization (gk_sparse.hip): started on a host thread at
+// a basis of the chain (mark: the chain's pivot count there), installed at
+// the next refactorization with the later pivots replayed (returns their
+// count, or -1: factorize the current basis instead)
+void sp_ahead_start(SpFactor &F, int m, const int *head1, const int *Aptr, const int *Aind, const double *Aval,
+                    double piv_tol, int piv_lim, double eps_tol, int mark);
+void sp_ahead_cancel(SpFactor &F);
+int sp_ahead_mark(const SpFactor &F);
+int sp_log_count(SpFactor &F, hipStream_t s);
+int sp_ahead_install(SpFactor &F, hipStream_t s, int cnt, const int *Acptr, const int *Acind, const double *Acval,
+                     double *h, double *t_wait);   // GK_SP_STAMPS (diagnostics)
 
 struct SpxDev {
     int m, n;

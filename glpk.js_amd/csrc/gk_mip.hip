@@ -2500,7 +2500,11 @@ extern "C" int gk_ios_driver_sharded_inc(gk_ctx *ctx, gk_mip *mip, const gk_iocp
     // single GPU: two batches in flight — the host assembles and launches
     // batch k + 1 before it processes the results of batch k (more
     // speculative nodes, the GPU never waits for the host)
-    const int depth = (size == 1) ? 2 : 1;
+    static const int depth_env = [] {
+        const char *e = std::getenv("GK_BNB_DEPTH");           // (experiments) batches in flight, 1 or 2
+        return e ? std::atoi(e) : 2;
+    }();
+    const int depth = (size == 1) ? (depth_env == 1 ? 1 : 2) : 1;
     int inflight[2] = {0, 0}, cur = 0;
     bool fail_sync = false;
     long long moved = 0;
@@ -2784,6 +2788,11 @@ extern "C" int gk_ios_driver_sharded_inc(gk_ctx *ctx, gk_mip *mip, const gk_iocp
         return e ? std::atoi(e) : 8;
     }();
     const int pre_cap = pre_cap_env > 0 ? pre_cap_env : 1 << 30;
+    static const int post_cap_env = [] {
+        const char *e = std::getenv("GK_BNB_CAP");              // (experiments) batch width with an incumbent
+        return e ? std::atoi(e) : 0;
+    }();
+    const int post_cap = post_cap_env > 0 ? post_cap_env : 1 << 30;
     int since_sync = 0;
     // show_progress (glpios03.js:2-48) through the context's report hook, and
     // the relative gap of ios_relative_gap (glpios01.js:842): both need the
@@ -2921,7 +2930,7 @@ extern "C" int gk_ios_driver_sharded_inc(gk_ctx *ctx, gk_mip *mip, const gk_iocp
         // until the first incumbent prunes, a wide batch is mostly nodes a
         // sequential walk never solves (the reference dives for an incumbent
         // first): the batch widens to BMAX once one exists
-        const int cap = S.have ? S.BMAX : std::min(S.BMAX, pre_cap);
+        const int cap = S.have ? std::min(S.BMAX, post_cap) : std::min(S.BMAX, pre_cap);
         {
             size_t k = 0;
             for (; k < S.probeq.size() && (int)bf.ents.size() < cap; k++) bf.ents.push_back(S.probeq[k]);

@@ -112,6 +112,8 @@ struct SpTriDevBufs {
     }
 };
 
+struct SpHost;
+
 struct SpFactor {
     int m = -1;
     SpTriDevBufs fl, fu, bu, bl;
@@ -136,14 +138,16 @@ struct SpFactor {
     SBuf<unsigned long long> stamps;      // GK_SP_STAMPS: 4 x SP_STAMP_MAX level stamps of the last solves
     std::vector<int> lv_host[4];          // (with stamps) the level sizes, for the dump
     double t_lu = 0.0, t_total = 0.0;
-    ~SpFactor()
-    {
-        fl.release(); fu.release(); bu.release(); bl.release();
-        Y.release(); Minv.release(); zq.release(); tpart.release(); bt.release(); scr.release(); scr2.release();
-        hh.release(); bz.release(); stamps.release(); sacc.release();
-        P.release();
-        hdr.release();
-    }
+    // the pivots of the current chain, in order (p, entering variable), and
+    // the look-ahead: the LU of an earlier basis of the chain factorized on
+    // a host thread (sp_ahead_start), installed at the next refactorization
+    // with the chain's later pivots replayed onto it (sp_ahead_install)
+    SBuf<int> plog, prep;
+    SBuf<char> rst;                       // the replay's DState (p, kq, refact_pending)
+    struct SpHost *cur = nullptr, *nxt = nullptr;
+    std::thread ahead;
+    int ahead_mark = -1;
+    ~SpFactor();
 };
 
 constexpr int TRI_LONG = 32;   // sweep steps with more entries run on a whole wave
@@ -220,6 +224,32 @@ struct SpLUWork {
     std::vector<int> lid;                  // long rows: their slot in lmap (-1: short)
     std::vector<std::vector<int>> lmap;    // per long row: column -> index in the row (-1: none)
 };
+
+// the host products of one factorization (LU, the four sweeps, their
+// plans) before they go to the device; the working storage stays with it
+struct SpHost {
+    SpLU lu;
+    SpLUWork wk;
+    SpSolves S;
+    std::vector<SpFactor::Seg> plan[4];
+    int wide[4] = {0, 0, 0, 0};
+    int m = 0, ret = 1;
+    double t_lu = 0.0;
+    std::vector<int> cptr, crow;          // the look-ahead's copy of B's columns
+    std::vector<double> cval;
+};
+
+SpFactor::~SpFactor()
+{
+    if (ahead.joinable()) ahead.join();
+    delete cur;
+    delete nxt;
+    fl.release(); fu.release(); bu.release(); bl.release();
+    Y.release(); Minv.release(); zq.release(); tpart.release(); bt.release(); scr.release(); scr2.release();
+    hh.release(); bz.release(); stamps.release(); sacc.release(); plog.release(); prep.release(); rst.release();
+    P.release();
+    hdr.release();
+}
 
 // rows longer than this keep a dense position map (the linking rows of a
 // block-angular basis: every elimination that touches one would rescan it)
@@ -739,6 +769,7 @@ static void sp_build_solves(const SpLU &F, SpSolves &S, std::vector<SpFactor::Se
 // is LDS reads and a barrier, its metadata loaded a level ahead.
 // ---------------------------------------------------------------------------
 constexpr int SP_SEG_MAX = 8192;
+constexpr int SP_SEG_LEVELS = 256;                // levels per LDS segment
 
 static bool sp_seg_on()
 {
@@ -747,6 +778,17 @@ static bool sp_seg_on()
         return !e || atoi(e) != 0;
     }();
     return on;
+}
+
+// entries from which a level runs on the grid (with LDS segments; a level
+// of many steps, sp_wide_min, does in any case)
+static int sp_wide_entries()
+{
+    static const int w = [] {
+        const char *e = std::getenv("GK_SP_WIDE_E");
+        return e ? std::max(1, atoi(e)) : 8192;
+    }();
+    return w;
 }
 
 // external entries from which a segment's external pass runs on the grid
@@ -772,13 +814,24 @@ static void sp_plan_sweep(SpTriHost &T, std::vector<SpFactor::Seg> &plan, int &w
     const int nlev = T.nlev, nst = nlev ? T.lvptr[nlev] : 0;
     const bool seg = sp_seg_on();
     int run = -1;                            // first level of the current narrow run
+    // a tail level: a few long steps (the linking rows of a block-angular
+    // basis, one per level at the end of FTRAN L); a segment holds tail
+    // levels or none, so that a tail step's entries into the levels before
+    // the tail are external (the grid gathers them) and only the dense
+    // triangle among the tail steps stays internal
+    auto tail = [&](int l) {
+        const int ns = T.lvptr[l + 1] - T.lvptr[l];
+        return ns <= 16 && T.eptr[T.lvptr[l + 1]] - T.eptr[T.lvptr[l]] >= 64 * ns;
+    };
     auto close_run = [&](int l1) {
         if (run < 0) return;
         if (!seg) plan.push_back({0, run, l1, 1});
         else
             for (int a = run; a < l1;) {     // greedy: levels while the steps fit
                 int b = a + 1;
-                while (b < l1 && T.lvptr[b + 1] - T.lvptr[a] <= SP_SEG_MAX) b++;
+                while (b < l1 && b - a < SP_SEG_LEVELS && T.lvptr[b + 1] - T.lvptr[a] <= SP_SEG_MAX &&
+                       tail(b) == tail(a))
+                    b++;
                 SpFactor::Seg g{2, a, b, 1};
                 g.sb = T.lvptr[a];
                 g.ns = T.lvptr[b] - T.lvptr[a];
@@ -789,7 +842,8 @@ static void sp_plan_sweep(SpTriHost &T, std::vector<SpFactor::Seg> &plan, int &w
     };
     for (int l = 0; l < nlev; l++) {
         const int nshort = T.lvlong[l] - T.lvptr[l], nlong = T.lvptr[l + 1] - T.lvlong[l];
-        if (nshort + nlong >= sp_wide_min()) {
+        const int nent = T.eptr[T.lvptr[l + 1]] - T.eptr[T.lvptr[l]];
+        if (nshort + nlong >= sp_wide_min() || (seg && nent >= sp_wide_entries())) {
             close_run(l);
             plan.push_back({1, l, l + 1, std::max(1, std::max((nshort + 255) / 256, std::min((nlong + 3) / 4, 1024)))});
             wide = 1;
@@ -1113,6 +1167,7 @@ struct WoodDev {
     double *hh;                                   // inv(M) z[P] of the FTRAN (2 x SP_KMAX)
     int *ycol;                                    // device word: Y column the last update wrote (-1: none)
     double *bz;                                   // e_p of the pivot's BTRAN (m; zero between uses)
+    int *log, *nlog;                              // the chain's pivots (p, kq) and their count
 };
 
 struct SpDev {
@@ -1385,10 +1440,10 @@ __global__ void __launch_bounds__(256) k_sp_seg_a(TriDev t, const DState *st, in
                   gridDim.x * blockDim.x);
 }
 
-// a short step of the internal pass: metadata and its first internal entries
-// loaded a level ahead (none depends on the sweep's values)
+// a short step of the internal pass: its first internal entries and
+// diagonal, loaded a level ahead (none depends on the sweep's values)
 struct SegPre {
-    int s, io, eb, ee;
+    int s, eb, ee;
     double dg;
     int ix[4];
     double v[4];
@@ -1398,7 +1453,6 @@ __device__ __forceinline__ void segpre_load(const TriDev &t, int s, int lim, Seg
 {
     q.s = s;
     if (s >= lim) return;
-    q.io = t.iout[s];
     q.eb = t.emid[s];
     q.ee = t.eptr[s + 1];
     q.dg = t.diag[s];
@@ -1411,8 +1465,7 @@ __device__ __forceinline__ void segpre_load(const TriDev &t, int s, int lim, Seg
 }
 
 template <int NRHS>
-__device__ __forceinline__ void segpre_run(const TriDev &t, const SegPre &q, int sb, double *L, double *out0,
-                                           double *out1)
+__device__ __forceinline__ void segpre_run(const TriDev &t, const SegPre &q, int sb, double *L)
 {
     const int li = q.s - sb;
     double a0 = L[li], a1 = (NRHS == 2) ? L[SP_SEG_MAX + li] : 0.0;
@@ -1428,18 +1481,91 @@ __device__ __forceinline__ void segpre_run(const TriDev &t, const SegPre &q, int
         a0 -= t.eval[e] * L[ix];
         if (NRHS == 2) a1 -= t.eval[e] * L[SP_SEG_MAX + ix];
     }
-    a0 /= q.dg;
-    L[li] = a0;
-    out0[q.io] = a0;
-    if (NRHS == 2) {
-        a1 /= q.dg;
-        L[SP_SEG_MAX + li] = a1;
-        out1[q.io] = a1;
+    L[li] = a0 / q.dg;
+    if (NRHS == 2) L[SP_SEG_MAX + li] = a1 / q.dg;
+}
+
+// the barrier between two levels of the internal pass: the level's LDS
+// writes done, the next levels' metadata loads left in flight (a
+// __syncthreads() may wait for them); the clobber keeps the compiler's LDS
+// accesses on their side of it
+__device__ __forceinline__ void seg_barrier()
+{
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
+
+// one level of the internal pass: the short steps (the first one of this
+// thread prefetched in q), then the long ones — split over the waves when
+// there are at most a quarter as many as waves, else a wave each
+template <int NRHS>
+__device__ __forceinline__ void seg_level(const TriDev &t, const SegPre &q, int sb, int ls, int le, double *L,
+                                          double *red)
+{
+    const int T = blockDim.x, w = threadIdx.x >> 6, nw = blockDim.x >> 6, lane = threadIdx.x & 63;
+    if (q.s < ls) segpre_run<NRHS>(t, q, sb, L);
+    for (int s = q.s + T; s < ls; s += T) {              // short steps beyond one per thread
+        SegPre r;
+        segpre_load(t, s, ls, r);
+        segpre_run<NRHS>(t, r, sb, L);
+    }
+    const int nl = le - ls;
+    if (nl <= 0) return;
+    if (4 * nl <= nw) {
+        const int g = nw / nl, sidx = w / g, sub = w % g;
+        double p0 = 0.0, p1 = 0.0;
+        if (sidx < nl) {
+            const int st = ls + sidx, eb = t.emid[st], ee = t.eptr[st + 1];
+            for (int e = eb + sub * 64 + lane; e < ee; e += g * 64) {
+                const int ix = t.eidx[e];
+                p0 += t.eval[e] * L[ix];
+                if (NRHS == 2) p1 += t.eval[e] * L[SP_SEG_MAX + ix];
+            }
+        }
+        p0 = wsum(p0);
+        if (NRHS == 2) p1 = wsum(p1);
+        if (lane == 0) {
+            red[w] = p0;
+            red[16 + w] = p1;
+        }
+        seg_barrier();
+        if (sidx < nl && sub == 0 && lane == 0) {
+            double s0 = 0.0, s1 = 0.0;
+            for (int u = 0; u < g; u++) {
+                s0 += red[w + u];
+                s1 += red[16 + w + u];
+            }
+            const int st = ls + sidx, li = st - sb;
+            const double dg = t.diag[st];
+            L[li] = (L[li] - s0) / dg;
+            if (NRHS == 2) L[SP_SEG_MAX + li] = (L[SP_SEG_MAX + li] - s1) / dg;
+        }
+        return;
+    }
+    for (int st = ls + w; st < le; st += nw) {
+        const int eb = t.emid[st], ee = t.eptr[st + 1];
+        double p0 = 0.0, p1 = 0.0;
+        for (int e = eb + lane; e < ee; e += 64) {
+            const int ix = t.eidx[e];
+            p0 += t.eval[e] * L[ix];
+            if (NRHS == 2) p1 += t.eval[e] * L[SP_SEG_MAX + ix];
+        }
+        p0 = wsum(p0);
+        if (NRHS == 2) p1 = wsum(p1);
+        if (lane == 0) {
+            const int li = st - sb;
+            const double dg = t.diag[st];
+            L[li] = (L[li] - p0) / dg;
+            if (NRHS == 2) L[SP_SEG_MAX + li] = (L[SP_SEG_MAX + li] - p1) / dg;
+        }
     }
 }
 
-// one LDS segment: levels l0 .. l1-1, steps sb .. sb+ns-1 (one workgroup);
-// pre: the external pass ran on the grid (acc); clr as k_sp_sweep
+// one LDS segment: levels l0 .. l1-1 (at most SP_SEG_LEVELS), steps sb ..
+// sb+ns-1 (one workgroup); pre: the external pass ran on the grid (acc).
+// The levels' bounds are staged in LDS; each level's short-step metadata is
+// loaded while the level before runs (two register sets, no copies: the
+// loads stay in flight across the barrier); the outputs go to the sweep's
+// vector once, after the last level.  clr as k_sp_sweep
 template <int NRHS>
 __global__ void __launch_bounds__(1024) k_sp_seg(SpDev sp, TriDev t, const DState *st, int gate, const double *in0,
                                                  const double *in1, double *out0, double *out1, int sb, int ns,
@@ -1447,10 +1573,15 @@ __global__ void __launch_bounds__(1024) k_sp_seg(SpDev sp, TriDev t, const DStat
 {
     if (sp_gated(st, gate)) return;
     __shared__ double L[NRHS * SP_SEG_MAX];
-    const int T = blockDim.x, w = threadIdx.x >> 6, nw = blockDim.x >> 6, lane = threadIdx.x & 63;
-    int le = t.lvptr[l0 + 1], ls = t.lvlong[l0];
-    SegPre cur;
-    segpre_load(t, t.lvptr[l0] + (int)threadIdx.x, ls, cur);
+    __shared__ int lvb[SP_SEG_LEVELS + 1], lvl[SP_SEG_LEVELS];
+    __shared__ double red[32];
+    const int T = blockDim.x, nlv = l1 - l0;
+    for (int l = threadIdx.x; l <= nlv; l += T) {
+        lvb[l] = t.lvptr[l0 + l];
+        if (l < nlv) lvl[l] = t.lvlong[l0 + l];
+    }
+    SegPre A, B;
+    segpre_load(t, t.lvptr[l0] + (int)threadIdx.x, t.lvlong[l0], A);
     if (pre)
         for (int i = threadIdx.x; i < ns; i += T) {
             L[i] = acc[i];
@@ -1459,47 +1590,28 @@ __global__ void __launch_bounds__(1024) k_sp_seg(SpDev sp, TriDev t, const DStat
     else
         seg_ext<NRHS>(t, in0, in1, out0, out1, sb, ns, nas, L, L + SP_SEG_MAX, threadIdx.x, T);
     __syncthreads();
-    if (t.stamps && threadIdx.x == 0 && l0 < SP_STAMP_MAX) t.stamps[l0] = wall_clock64();
-    for (int l = l0; l < l1; l++) {
-        const int nb = le, ne = (l + 1 < l1) ? t.lvptr[l + 2] : le, nls = (l + 1 < l1) ? t.lvlong[l + 1] : le;
-        SegPre nxt;
-        segpre_load(t, nb + (int)threadIdx.x, nls, nxt);
-        if (cur.s < ls) segpre_run<NRHS>(t, cur, sb, L, out0, out1);
-        for (int s = cur.s + T; s < ls; s += T) {            // short steps beyond one per thread
-            SegPre q;
-            segpre_load(t, s, ls, q);
-            segpre_run<NRHS>(t, q, sb, L, out0, out1);
-        }
-        for (int s = ls + w; s < le; s += nw) {               // many internal entries: a wave each
-            const int eb = t.emid[s], ee = t.eptr[s + 1];
-            double p0 = 0.0, p1 = 0.0;
-            for (int e = eb + lane; e < ee; e += 64) {
-                const int ix = t.eidx[e];
-                p0 += t.eval[e] * L[ix];
-                if (NRHS == 2) p1 += t.eval[e] * L[SP_SEG_MAX + ix];
-            }
-            p0 = wsum(p0);
-            if (NRHS == 2) p1 = wsum(p1);
-            if (lane == 0) {
-                const int li = s - sb, io = t.iout[s];
-                const double dg = t.diag[s];
-                const double v0 = (L[li] - p0) / dg;
-                L[li] = v0;
-                out0[io] = v0;
-                if (NRHS == 2) {
-                    const double v1 = (L[SP_SEG_MAX + li] - p1) / dg;
-                    L[SP_SEG_MAX + li] = v1;
-                    out1[io] = v1;
-                }
-            }
-        }
-        __syncthreads();
-        if (t.stamps && threadIdx.x == 0 && l + 1 < SP_STAMP_MAX) t.stamps[l + 1] = wall_clock64();
-        cur = nxt;
-        le = ne;
-        ls = nls;
+    const bool stamp = t.stamps && threadIdx.x == 0;
+    if (stamp && l0 < SP_STAMP_MAX) t.stamps[l0] = wall_clock64();
+    for (int l = 0; l < nlv; l += 2) {
+        if (l + 1 < nlv) segpre_load(t, lvb[l + 1] + (int)threadIdx.x, lvl[l + 1], B);
+        seg_level<NRHS>(t, A, sb, lvl[l], lvb[l + 1], L, red);
+        seg_barrier();
+        if (stamp && l0 + l + 1 < SP_STAMP_MAX) t.stamps[l0 + l + 1] = wall_clock64();
+        if (l + 1 >= nlv) break;
+        if (l + 2 < nlv) segpre_load(t, lvb[l + 2] + (int)threadIdx.x, lvl[l + 2], A);
+        seg_level<NRHS>(t, B, sb, lvl[l + 1], lvb[l + 2], L, red);
+        seg_barrier();
+        if (stamp && l0 + l + 2 < SP_STAMP_MAX) t.stamps[l0 + l + 2] = wall_clock64();
     }
-    if (clr) bz_clear(sp, st->p - 1, *sp.w.k);
+    for (int i = threadIdx.x; i < ns; i += T) {
+        const int io = t.iout[sb + i];
+        out0[io] = L[i];
+        if (NRHS == 2) out1[io] = L[SP_SEG_MAX + i];
+    }
+    if (clr) {
+        __syncthreads();
+        bz_clear(sp, st->p - 1, *sp.w.k);
+    }
 }
 
 // the FTRAN's inv(M) z[P] (k_sp_ftran_lu's tail) as its own launch, after a
@@ -1618,6 +1730,13 @@ __global__ void __launch_bounds__(1024) k_sp_update(SpDev sp, DState *st)
     __shared__ double c[SP_KMAX], r[SP_KMAX], ac[SP_KMAX], ra[SP_KMAX], col_old[SP_KMAX];
     __shared__ double sch;
     if (threadIdx.x == 0) {
+        // the pivot log (the look-ahead's replay): every basis change of the chain
+        const int nl = *sp.w.nlog;
+        if (nl < SP_KMAX) {
+            sp.w.log[2 * nl] = p;
+            sp.w.log[2 * nl + 1] = st->kq;
+        }
+        *sp.w.nlog = nl + 1;
         slot = -1;
         *sp.w.ycol = -1;
     }
@@ -1769,6 +1888,7 @@ static SpDev sp_dev(SpFactor &F)
     d.bl = tri_dev(F.bl, F.hdr.p + 3, sb ? sb + 3 * SP_STAMP_MAX : nullptr);
     d.w.Y = F.Y.p; d.w.P = F.P.p; d.w.Minv = F.Minv.p; d.w.k = F.hdr.p + 4; d.w.zq = F.zq.p;
     d.w.tpart = F.tpart.p; d.w.bt = F.bt.p; d.w.scr2 = F.scr2.p; d.w.hh = F.hh.p; d.w.ycol = F.hdr.p + 5; d.w.bz = F.bz.p;
+    d.w.log = F.plog.p; d.w.nlog = F.hdr.p + 6;
     return d;
 }
 
@@ -1832,21 +1952,32 @@ int sp_factorize_csc(SpFactor &F, hipStream_t s, int m, const int *ptr, const in
     return sp_factorize_cols(F, s, m, cptr, crow, cval, piv_tol, piv_lim, eps_tol, t0);
 }
 
-static int sp_factorize_cols(SpFactor &F, hipStream_t s, int m, const std::vector<int> &cptr,
-                             const std::vector<int> &crow, const std::vector<double> &cval, double piv_tol,
-                             int piv_lim, double eps_tol, double t0)
+// the host part of a factorization (any thread)
+static void sp_prepare(SpHost &H, int m, const std::vector<int> &cptr, const std::vector<int> &crow,
+                       const std::vector<double> &cval, double piv_tol, int piv_lim, double eps_tol)
 {
-    thread_local SpLU lu;
-    thread_local SpLUWork wk;
+    const double t0 = sp_now();
     int rank = 0;
-    const int ret = sp_lu_factor(lu, wk, m, cptr, crow, cval, piv_tol > 0.0 ? piv_tol : 0.1, piv_lim > 0 ? piv_lim : 4,
-                                 eps_tol > 0.0 ? eps_tol : 1e-15, &rank);
-    F.t_lu = sp_now() - t0;
-    if (ret) return 1;
-    thread_local SpSolves S;
-    sp_build_solves(lu, S, F.plan, F.wide);
-    F.nnz_l = (long long)lu.Lrow.size();
-    F.nnz_u = (long long)lu.Ucol.size() + m;
+    H.m = m;
+    H.ret = sp_lu_factor(H.lu, H.wk, m, cptr, crow, cval, piv_tol > 0.0 ? piv_tol : 0.1, piv_lim > 0 ? piv_lim : 4,
+                         eps_tol > 0.0 ? eps_tol : 1e-15, &rank);
+    H.t_lu = sp_now() - t0;
+    if (H.ret) return;
+    sp_build_solves(H.lu, H.S, H.plan, H.wide);
+}
+
+// the device part: buffers, the sweeps' upload, an empty chain
+static void sp_install(SpFactor &F, hipStream_t s, SpHost &H, double t0)
+{
+    const int m = H.m;
+    const SpSolves &S = H.S;
+    for (int i = 0; i < 4; i++) {
+        F.plan[i] = H.plan[i];
+        F.wide[i] = H.wide[i];
+    }
+    F.t_lu = H.t_lu;
+    F.nnz_l = (long long)H.lu.Lrow.size();
+    F.nnz_u = (long long)H.lu.Ucol.size() + m;
     F.levels[0] = S.fl.nlev; F.levels[1] = S.fu.nlev; F.levels[2] = S.bu.nlev; F.levels[3] = S.bl.nlev;
     const SpTriHost *T4[4] = {&S.fl, &S.fu, &S.bu, &S.bl};
     if (F.m != m) {
@@ -1864,6 +1995,9 @@ static int sp_factorize_cols(SpFactor &F, hipStream_t s, int m, const std::vecto
     F.hh.ensure((size_t)2 * SP_KMAX);
     F.sacc.ensure((size_t)2 * SP_SEG_MAX);
     F.Minv.ensure((size_t)SP_KMAX * SP_KMAX);
+    F.plog.ensure((size_t)2 * SP_KMAX);
+    F.prep.ensure((size_t)2 * SP_KMAX);
+    F.rst.ensure(sizeof(DState));
     F.hdr.ensure(8);
     if (sp_stamps_path()) {
         F.stamps.ensure((size_t)4 * SP_STAMP_MAX);
@@ -1881,11 +2015,139 @@ static int sp_factorize_cols(SpFactor &F, hipStream_t s, int m, const std::vecto
     up_tri(s, F.fu, S.fu, F.hdr.p + 1);
     up_tri(s, F.bu, S.bu, F.hdr.p + 2);
     up_tri(s, F.bl, S.bl, F.hdr.p + 3);
-    const int zero = 0;
-    SPCHK(hipMemcpyAsync(F.hdr.p + 4, &zero, sizeof(int), hipMemcpyHostToDevice, s));
-    SPCHK(hipStreamSynchronize(s));          // the host vectors of S go out of scope
+    SPCHK(hipMemsetAsync(F.hdr.p + 4, 0, sizeof(int), s));          // k: no updates
+    SPCHK(hipMemsetAsync(F.hdr.p + 6, 0, sizeof(int), s));          // the pivot log: empty
+    SPCHK(hipStreamSynchronize(s));          // (pageable uploads of H's vectors)
     F.t_total = sp_now() - t0;
+}
+
+static int sp_factorize_cols(SpFactor &F, hipStream_t s, int m, const std::vector<int> &cptr,
+                             const std::vector<int> &crow, const std::vector<double> &cval, double piv_tol,
+                             int piv_lim, double eps_tol, double t0)
+{
+    sp_ahead_cancel(F);
+    if (!F.cur) F.cur = new SpHost;
+    sp_prepare(*F.cur, m, cptr, crow, cval, piv_tol, piv_lim, eps_tol);
+    F.t_lu = F.cur->t_lu;
+    if (F.cur->ret) return 1;
+    sp_install(F, s, *F.cur, t0);
     return 0;
+}
+
+template <int NRHS>
+static void ftran_lu(SpFactor &F, hipStream_t s, const SpDev &d, const DState *st, int gated, double *h0, double *h1);
+
+// ---- the look-ahead ------------------------------------------------------
+void sp_ahead_cancel(SpFactor &F)
+{
+    if (F.ahead.joinable()) F.ahead.join();
+    F.ahead_mark = -1;
+}
+
+int sp_ahead_mark(const SpFactor &F) { return F.ahead_mark; }
+
+// the pivots the current chain logged (synchronizes the stream)
+int sp_log_count(SpFactor &F, hipStream_t s)
+{
+    int c = 0;
+    if (!F.hdr.p) return 0;
+    SPCHK(hipMemcpyAsync(&c, F.hdr.p + 6, sizeof(int), hipMemcpyDeviceToHost, s));
+    SPCHK(hipStreamSynchronize(s));
+    return c;
+}
+
+// B of the basis header head1 (as sp_factorize) factorized on a host thread;
+// mark: the chain's pivot count at this basis
+void sp_ahead_start(SpFactor &F, int m, const int *head1, const int *Aptr, const int *Aind, const double *Aval,
+                    double piv_tol, int piv_lim, double eps_tol, int mark)
+{
+    sp_ahead_cancel(F);
+    if (!F.nxt) F.nxt = new SpHost;
+    SpHost *H = F.nxt;
+    H->cptr.assign(m + 1, 0);
+    H->crow.clear();
+    H->cval.clear();
+    for (int i = 1; i <= m; i++) {
+        const int k = head1[i];
+        if (k <= m) {
+            H->crow.push_back(k - 1);
+            H->cval.push_back(1.0);
+        } else
+            for (int t = Aptr[k - m - 1]; t < Aptr[k - m]; t++) {
+                H->crow.push_back(Aind[t]);
+                H->cval.push_back(-Aval[t]);
+            }
+        H->cptr[i] = (int)H->crow.size();
+    }
+    H->ret = 1;
+    F.ahead_mark = mark;
+    F.ahead = std::thread([H, m, piv_tol, piv_lim, eps_tol] {
+        sp_prepare(*H, m, H->cptr, H->crow, H->cval, piv_tol, piv_lim, eps_tol);
+    });
+}
+
+// h = -N_kq of the logged pivot j (the column the pivot brought in, as
+// build_hq forms it) and the replay's state (p, kq, no stop); h was zeroed
+__global__ void __launch_bounds__(256) k_sp_replay_col(double *h, int m, const int *cptr, const int *cind,
+                                                       const double *cval, const int *log, int j, DState *rst)
+{
+    const int p = log[2 * j], kq = log[2 * j + 1];
+    if (kq <= m) {
+        if (threadIdx.x == 0) h[kq - 1] = -1.0;
+    } else {
+        const int c = kq - m - 1;
+        for (int t = cptr[c] + threadIdx.x; t < cptr[c + 1]; t += blockDim.x) h[cind[t]] = cval[t];
+    }
+    if (threadIdx.x == 0) {
+        rst->stop = 0;
+        rst->p = p + 1;
+        rst->kq = kq;
+    }
+}
+
+// the look-ahead's factor installed in place of the current one, and the
+// chain's pivots from its mark to cnt (the current chain length) replayed
+// onto it: an FTRAN of each entering column and its Schur-complement update,
+// in the pivots' order.  Returns the replayed count, or -1 when there was
+// no look-ahead, its LU failed or a replayed update asked for a fresh
+// factorization (the caller factorizes the current basis then).  A (CSC,
+// the engine's device copy, 0-based) supplies the columns; h: m doubles of
+// scratch; *t_wait: the time the join waited for the thread
+int sp_ahead_install(SpFactor &F, hipStream_t s, int cnt, const int *Acptr, const int *Acind, const double *Acval,
+                     double *h, double *t_wait)
+{
+    const int mark = F.ahead_mark;
+    *t_wait = 0.0;
+    if (mark < 0 || !F.ahead.joinable()) return -1;
+    const double t0 = sp_now();
+    F.ahead.join();
+    F.ahead_mark = -1;
+    *t_wait = sp_now() - t0;
+    if (cnt < 0) cnt = sp_log_count(F, s);
+    if (F.nxt->ret || F.nxt->m != F.m || cnt < mark || cnt - mark > SP_KMAX) return -1;
+    const int nrep = cnt - mark;
+    if (nrep > 0)
+        SPCHK(hipMemcpyAsync(F.prep.p, F.plog.p + 2 * mark, (size_t)2 * nrep * sizeof(int), hipMemcpyDeviceToDevice, s));
+    std::swap(F.cur, F.nxt);
+    sp_install(F, s, *F.cur, t0);
+    const int m = F.m;
+    DState *rst = (DState *)F.rst.p;
+    SPCHK(hipMemsetAsync(rst, 0, sizeof(DState), s));
+    SpDev d = sp_dev(F);
+    for (int j = 0; j < nrep; j++) {
+        SPCHK(hipMemsetAsync(h, 0, (size_t)m * sizeof(double), s));
+        hipLaunchKernelGGL(k_sp_replay_col, dim3(1), dim3(256), 0, s, h, m, Acptr, Acind, Acval, (const int *)F.prep.p,
+                           j, rst);
+        ftran_lu<1>(F, s, d, nullptr, 0, h, nullptr);
+        hipLaunchKernelGGL((k_sp_ftran_wood<1>), dim3((m + 255) / 256), dim3(256), 0, s, d, (const DState *)nullptr,
+                           F.scr.p, (double *)nullptr, 0, 1);
+        hipLaunchKernelGGL(k_sp_update, dim3(1), dim3(1024), 0, s, d, rst);
+        hipLaunchKernelGGL(k_sp_ycol, dim3((m + 255) / 256), dim3(256), 0, s, d, (const DState *)rst);
+    }
+    int pend = 0;
+    SPCHK(hipMemcpyAsync(&pend, &rst->refact_pending, sizeof(int), hipMemcpyDeviceToHost, s));
+    SPCHK(hipStreamSynchronize(s));
+    return pend ? -1 : nrep;
 }
 
 // one sweep by its plan; clr: the last launch clears bz (BTRAN of e_p)
