@@ -1221,20 +1221,21 @@ struct Spx {
     bool refine_next = false;
     int echk_seen = 0;
 
-    // the sparse factor's look-ahead (GK_SP_AHEAD: the fraction of the update
-    // limit at which the next LU starts on a host thread; 0 turns it off):
-    // the basis at that point of the chain is factorized while the device
-    // pivots on, and the pivots since are replayed at the refactorization
-    // (sp_ahead_install).  The start is a pivot count, not a time, so the
-    // path stays deterministic
+    // the sparse factor's look-ahead (GK_SP_AHEAD: the pivots before the
+    // update limit at which the next LU starts on a host thread; 0 turns it
+    // off): the basis at that point of the chain is factorized while the
+    // device pivots on, and the pivots since are replayed at the
+    // refactorization (sp_ahead_install).  The start is a pivot count, not a
+    // time, so the path stays deterministic; the default covers a host LU of
+    // ~40 ms (m = 100k) at ~1,000 pivots/s and costs ~32 replayed FTRANs
     void ahead_maybe()
     {
-        static const double frac = [] {
+        static const int lead = [] {
             const char *e = std::getenv("GK_SP_AHEAD");
-            return e ? std::atof(e) : 0.5;
+            return e ? std::atoi(e) : 32;
         }();
-        if (frac <= 0.0 || !f->valid || sp_ahead_mark(*f->sp) >= 0 || hs.npiv == 0 || hs.refact_pending) return;
-        if (hs.upd_lim < 32 || hs.upd_cnt >= hs.upd_lim || hs.upd_cnt < (int)(frac * hs.upd_lim)) return;
+        if (lead <= 0 || !f->valid || sp_ahead_mark(*f->sp) >= 0 || hs.npiv == 0 || hs.refact_pending) return;
+        if (hs.upd_lim < 2 * lead || hs.upd_cnt >= hs.upd_lim || hs.upd_cnt < hs.upd_lim - lead) return;
         pull();
         sp_ahead_start(*f->sp, m, head.data(), E->hcptr.data(), E->hcind.data(), E->hcval.data(), f->parm.piv_tol,
                        f->parm.piv_lim, f->parm.eps_tol, sp_log_count(*f->sp, s));

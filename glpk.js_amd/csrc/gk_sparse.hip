@@ -96,6 +96,12 @@ struct SpTriHost {
     // segment's steps (local indices) for its external pass, the ones of at
     // most TRI_LONG external entries first
     std::vector<int> emid, aord;
+    // per step of an LDS segment, its first four internal entries as one
+    // record (srx: local indices two per int and the internal count; srv:
+    // the coefficients, zero-padded), so that the internal pass loads a
+    // level's metadata by step index alone
+    std::vector<int> srx;
+    std::vector<double> srv;
 };
 
 struct SpSolves {
@@ -103,12 +109,12 @@ struct SpSolves {
 };
 
 struct SpTriDevBufs {
-    SBuf<int> lvptr, lvlong, iin, iout, eptr, eidx, emid, aord;
-    SBuf<double> diag, eval;
+    SBuf<int> lvptr, lvlong, iin, iout, eptr, eidx, emid, aord, srx;
+    SBuf<double> diag, eval, srv;
     void release()
     {
         lvptr.release(); lvlong.release(); iin.release(); iout.release(); eptr.release(); eidx.release(); diag.release();
-        eval.release(); emid.release(); aord.release();
+        eval.release(); emid.release(); aord.release(); srx.release(); srv.release();
     }
 };
 
@@ -780,6 +786,17 @@ static bool sp_seg_on()
     return on;
 }
 
+// (experiments) k_sp_seg variants: bit 0 level stamps kept in LDS, bit 1
+// the level metadata loaded at the level instead of a level ahead
+static int sp_seg_xf()
+{
+    static const int x = [] {
+        const char *e = std::getenv("GK_SP_SEGX");
+        return e ? atoi(e) : 0;
+    }();
+    return x;
+}
+
 // entries from which a level runs on the grid (with LDS segments; a level
 // of many steps, sp_wide_min, does in any case)
 static int sp_wide_entries()
@@ -918,6 +935,22 @@ static void sp_plan_sweep(SpTriHost &T, std::vector<SpFactor::Seg> &plan, int &w
         g.pre = ext >= sp_ga_min();
         g.ablocks = std::max(1, std::max((nas + 255) / 256, std::min((g.ns - nas + 3) / 4, 1024)));
     }
+    T.srx.assign((size_t)4 * std::max(nst, 1), 0);
+    T.srv.assign((size_t)4 * std::max(nst, 1), 0.0);
+    for (const auto &g : plan) {
+        if (g.grid != 2) continue;
+        for (int st = g.sb; st < g.sb + g.ns; st++) {
+            const int eb = T.emid[st], n = T.eptr[st + 1] - eb;
+            int ix[4] = {0, 0, 0, 0};
+            for (int u = 0; u < 4 && u < n; u++) {
+                ix[u] = T.eidx[eb + u];
+                T.srv[(size_t)4 * st + u] = T.eval[eb + u];
+            }
+            T.srx[(size_t)4 * st + 0] = ix[0] | (ix[1] << 16);
+            T.srx[(size_t)4 * st + 1] = ix[2] | (ix[3] << 16);
+            T.srx[(size_t)4 * st + 2] = n;
+        }
+    }
 }
 
 // ---------------------------------------------------------------------------
@@ -929,8 +962,65 @@ struct TriDev {
     const double *diag, *eval;
     const int *nlev;                              // device word: levels of the current factor
     unsigned long long *stamps;                   // GK_SP_STAMPS: device clock after each level (null: off)
+    const int4 *srx;                              // LDS segments: step records (SpTriHost::srx / srv)
+    const double2 *srv;
 };
 constexpr int SP_STAMP_MAX = 2048;                // levels stamped per sweep
+
+// a -= sum over entries [eb, ee) of val[e] x[idx[e]], eight entries per
+// trip: the index / value loads of a group are issued together (clamped
+// into the range, so unconditional), then its gathers, then the products in
+// entry order (a dropped entry subtracts 0).  A loop of one entry per
+// iteration waited for each entry's own loads: one L2 round trip per entry
+template <int NRHS, typename Get>
+__device__ __forceinline__ void gather_sub8(const int *eidx, const double *eval, int eb, int ee, Get get, double &a0,
+                                            double &a1)
+{
+    for (int e = eb; e < ee; e += 8) {
+        int ix[8];
+        double v[8], x0[8], x1[8];
+#pragma unroll
+        for (int u = 0; u < 8; u++) {
+            const int ec = min(e + u, ee - 1);
+            ix[u] = eidx[ec];
+            const double w = eval[ec];
+            v[u] = (e + u < ee) ? w : 0.0;
+        }
+#pragma unroll
+        for (int u = 0; u < 8; u++) get(ix[u], x0[u], x1[u]);
+#pragma unroll
+        for (int u = 0; u < 8; u++) {
+            a0 -= v[u] * x0[u];
+            if (NRHS == 2) a1 -= v[u] * x1[u];
+        }
+    }
+}
+
+// a wave's partial sums of val[e] x[idx[e]] over [eb, ee): each lane takes
+// entries lane, lane + 64, ... four per trip (clamped, unconditional loads)
+template <int NRHS, typename Get>
+__device__ __forceinline__ void wave_dot4(const int *eidx, const double *eval, int eb, int ee, Get get, double &p0,
+                                          double &p1)
+{
+    for (int e = eb + (int)(threadIdx.x & 63); e < ee; e += 256) {
+        int ix[4];
+        double v[4], x0[4], x1[4];
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            const int ec = min(e + 64 * u, ee - 1);
+            ix[u] = eidx[ec];
+            const double w = eval[ec];
+            v[u] = (e + 64 * u < ee) ? w : 0.0;
+        }
+#pragma unroll
+        for (int u = 0; u < 4; u++) get(ix[u], x0[u], x1[u]);
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            p0 += v[u] * x0[u];
+            if (NRHS == 2) p1 += v[u] * x1[u];
+        }
+    }
+}
 
 // one step of a sweep: its metadata and right-hand side(s) do not depend on
 // the sweep's own output, so they are loaded one level ahead (before the
@@ -981,11 +1071,11 @@ __device__ __forceinline__ void step_run(const TriDev &t, const StepPre<NRHS> &q
         a0 -= q.v[u] * x0[u];
         if (NRHS == 2) a1 -= q.v[u] * x1[u];
     }
-    for (int e = q.eb + 4; e < q.ee; e++) {
-        const int ix = t.eidx[e];
-        a0 -= t.eval[e] * out0[ix];
-        if (NRHS == 2) a1 -= t.eval[e] * out1[ix];
-    }
+    if (q.ee > q.eb + 4)
+        gather_sub8<NRHS>(t.eidx, t.eval, q.eb + 4, q.ee, [&](int ix, double &x0, double &x1) {
+            x0 = out0[ix];
+            x1 = (NRHS == 2) ? out1[ix] : 0.0;
+        }, a0, a1);
     out0[q.iout] = a0 / q.dg;
     if (NRHS == 2) out1[q.iout] = a1 / q.dg;
 }
@@ -1001,23 +1091,11 @@ __device__ __forceinline__ void step_wave(const TriDev &t, const double *in0, co
     const double dg = t.diag[s];
     const double b0 = in0[ii], b1 = (NRHS == 2) ? in1[ii] : 0.0;
     double a0 = 0.0, a1 = 0.0;
-    int e = eb + lane;
-    for (; e + 64 < ee; e += 128) {
-        const int i0 = t.eidx[e], i1 = t.eidx[e + 64];
-        const double v0 = t.eval[e], v1 = t.eval[e + 64];
-        const double x0 = out0[i0], x1 = out0[i1];
-        a0 += v0 * x0;
-        a0 += v1 * x1;
-        if (NRHS == 2) {
-            a1 += v0 * out1[i0];
-            a1 += v1 * out1[i1];
-        }
-    }
-    for (; e < ee; e += 64) {
-        const int ix = t.eidx[e];
-        a0 += t.eval[e] * out0[ix];
-        if (NRHS == 2) a1 += t.eval[e] * out1[ix];
-    }
+    (void)lane;
+    wave_dot4<NRHS>(t.eidx, t.eval, eb, ee, [&](int ix, double &x0, double &x1) {
+        x0 = out0[ix];
+        x1 = (NRHS == 2) ? out1[ix] : 0.0;
+    }, a0, a1);
     a0 = wsum(a0);
     if (NRHS == 2) a1 = wsum(a1);
     if (lane == 0) {
@@ -1345,30 +1423,11 @@ __device__ __forceinline__ void seg_ext_thread(const TriDev &t, const double *in
     int e = t.eptr[s];
     a0 = in0[ii];
     a1 = (NRHS == 2) ? in1[ii] : 0.0;
-    for (; e + 4 <= ee; e += 4) {
-        int ix[4];
-        double v[4], x0[4], x1[4];
-#pragma unroll
-        for (int u = 0; u < 4; u++) {
-            ix[u] = t.eidx[e + u];
-            v[u] = t.eval[e + u];
-        }
-#pragma unroll
-        for (int u = 0; u < 4; u++) {
-            x0[u] = out0[ix[u]];
-            x1[u] = (NRHS == 2) ? out1[ix[u]] : 0.0;
-        }
-#pragma unroll
-        for (int u = 0; u < 4; u++) {
-            a0 -= v[u] * x0[u];
-            if (NRHS == 2) a1 -= v[u] * x1[u];
-        }
-    }
-    for (; e < ee; e++) {
-        const int ix = t.eidx[e];
-        a0 -= t.eval[e] * out0[ix];
-        if (NRHS == 2) a1 -= t.eval[e] * out1[ix];
-    }
+    if (ee > e)
+        gather_sub8<NRHS>(t.eidx, t.eval, e, ee, [&](int ix, double &x0, double &x1) {
+            x0 = out0[ix];
+            x1 = (NRHS == 2) ? out1[ix] : 0.0;
+        }, a0, a1);
 }
 
 // the external sum of a step of many: one wave, lanes strided, fixed-order
@@ -1377,25 +1436,12 @@ template <int NRHS>
 __device__ __forceinline__ void seg_ext_wave(const TriDev &t, const double *in0, const double *in1,
                                              const double *out0, const double *out1, int s, double &a0, double &a1)
 {
-    const int lane = threadIdx.x & 63, eb = t.eptr[s], ee = t.emid[s];
+    const int eb = t.eptr[s], ee = t.emid[s];
     double p0 = 0.0, p1 = 0.0;
-    int e = eb + lane;
-    for (; e + 64 < ee; e += 128) {
-        const int i0 = t.eidx[e], i1 = t.eidx[e + 64];
-        const double v0 = t.eval[e], v1 = t.eval[e + 64];
-        const double x0 = out0[i0], x1 = out0[i1];
-        p0 += v0 * x0;
-        p0 += v1 * x1;
-        if (NRHS == 2) {
-            p1 += v0 * out1[i0];
-            p1 += v1 * out1[i1];
-        }
-    }
-    for (; e < ee; e += 64) {
-        const int ix = t.eidx[e];
-        p0 += t.eval[e] * out0[ix];
-        if (NRHS == 2) p1 += t.eval[e] * out1[ix];
-    }
+    wave_dot4<NRHS>(t.eidx, t.eval, eb, ee, [&](int ix, double &x0, double &x1) {
+        x0 = out0[ix];
+        x1 = (NRHS == 2) ? out1[ix] : 0.0;
+    }, p0, p1);
     p0 = wsum(p0);
     if (NRHS == 2) p1 = wsum(p1);
     const int ii = t.iin[s];
@@ -1443,25 +1489,26 @@ __global__ void __launch_bounds__(256) k_sp_seg_a(TriDev t, const DState *st, in
 // a short step of the internal pass: its first internal entries and
 // diagonal, loaded a level ahead (none depends on the sweep's values)
 struct SegPre {
-    int s, eb, ee;
+    int s, n;
     double dg;
     int ix[4];
     double v[4];
 };
 
+// one record load per step, unconditional (an index past the level reads a
+// valid record and is dropped by n = 0): the compiler can count the loads in
+// flight and the prefetch stays in flight across the level's barrier
 __device__ __forceinline__ void segpre_load(const TriDev &t, int s, int lim, SegPre &q)
 {
+    const int sc = max(min(s, lim - 1), 0);
+    const int4 r = t.srx[sc];
+    const double2 a = t.srv[2 * sc], b = t.srv[2 * sc + 1];
+    q.dg = t.diag[sc];
     q.s = s;
-    if (s >= lim) return;
-    q.eb = t.emid[s];
-    q.ee = t.eptr[s + 1];
-    q.dg = t.diag[s];
-#pragma unroll
-    for (int u = 0; u < 4; u++) {
-        const bool ok = q.eb + u < q.ee;
-        q.ix[u] = ok ? t.eidx[q.eb + u] : 0;
-        q.v[u] = ok ? t.eval[q.eb + u] : 0.0;
-    }
+    q.n = (s < lim) ? r.z : 0;
+    q.ix[0] = r.x & 0xffff; q.ix[1] = (unsigned)r.x >> 16;
+    q.ix[2] = r.y & 0xffff; q.ix[3] = (unsigned)r.y >> 16;
+    q.v[0] = a.x; q.v[1] = a.y; q.v[2] = b.x; q.v[3] = b.y;
 }
 
 template <int NRHS>
@@ -1471,15 +1518,17 @@ __device__ __forceinline__ void segpre_run(const TriDev &t, const SegPre &q, int
     double a0 = L[li], a1 = (NRHS == 2) ? L[SP_SEG_MAX + li] : 0.0;
 #pragma unroll
     for (int u = 0; u < 4; u++) {
-        if (q.eb + u < q.ee) {
+        if (u < q.n) {
             a0 -= q.v[u] * L[q.ix[u]];
             if (NRHS == 2) a1 -= q.v[u] * L[SP_SEG_MAX + q.ix[u]];
         }
     }
-    for (int e = q.eb + 4; e < q.ee; e++) {
-        const int ix = t.eidx[e];
-        a0 -= t.eval[e] * L[ix];
-        if (NRHS == 2) a1 -= t.eval[e] * L[SP_SEG_MAX + ix];
+    if (q.n > 4) {
+        const int eb = t.emid[q.s];
+        gather_sub8<NRHS>(t.eidx, t.eval, eb + 4, eb + q.n, [&](int ix, double &x0, double &x1) {
+            x0 = L[ix];
+            x1 = (NRHS == 2) ? L[SP_SEG_MAX + ix] : 0.0;
+        }, a0, a1);
     }
     L[li] = a0 / q.dg;
     if (NRHS == 2) L[SP_SEG_MAX + li] = a1 / q.dg;
@@ -1514,12 +1563,13 @@ __device__ __forceinline__ void seg_level(const TriDev &t, const SegPre &q, int 
         const int g = nw / nl, sidx = w / g, sub = w % g;
         double p0 = 0.0, p1 = 0.0;
         if (sidx < nl) {
+            // the step's entries in chunks of 256, chunk c to wave sub + c g
             const int st = ls + sidx, eb = t.emid[st], ee = t.eptr[st + 1];
-            for (int e = eb + sub * 64 + lane; e < ee; e += g * 64) {
-                const int ix = t.eidx[e];
-                p0 += t.eval[e] * L[ix];
-                if (NRHS == 2) p1 += t.eval[e] * L[SP_SEG_MAX + ix];
-            }
+            for (int c = eb + 256 * sub; c < ee; c += 256 * g)
+                wave_dot4<NRHS>(t.eidx, t.eval, c, min(c + 256, ee), [&](int ix, double &x0, double &x1) {
+                    x0 = L[ix];
+                    x1 = (NRHS == 2) ? L[SP_SEG_MAX + ix] : 0.0;
+                }, p0, p1);
         }
         p0 = wsum(p0);
         if (NRHS == 2) p1 = wsum(p1);
@@ -1544,11 +1594,10 @@ __device__ __forceinline__ void seg_level(const TriDev &t, const SegPre &q, int 
     for (int st = ls + w; st < le; st += nw) {
         const int eb = t.emid[st], ee = t.eptr[st + 1];
         double p0 = 0.0, p1 = 0.0;
-        for (int e = eb + lane; e < ee; e += 64) {
-            const int ix = t.eidx[e];
-            p0 += t.eval[e] * L[ix];
-            if (NRHS == 2) p1 += t.eval[e] * L[SP_SEG_MAX + ix];
-        }
+        wave_dot4<NRHS>(t.eidx, t.eval, eb, ee, [&](int ix, double &x0, double &x1) {
+            x0 = L[ix];
+            x1 = (NRHS == 2) ? L[SP_SEG_MAX + ix] : 0.0;
+        }, p0, p1);
         p0 = wsum(p0);
         if (NRHS == 2) p1 = wsum(p1);
         if (lane == 0) {
@@ -1569,16 +1618,19 @@ __device__ __forceinline__ void seg_level(const TriDev &t, const SegPre &q, int 
 template <int NRHS>
 __global__ void __launch_bounds__(1024) k_sp_seg(SpDev sp, TriDev t, const DState *st, int gate, const double *in0,
                                                  const double *in1, double *out0, double *out1, int sb, int ns,
-                                                 int nas, int l0, int l1, int pre, const double *acc, int clr)
+                                                 int nas, int l0, int l1, int pre, const double *acc, int clr, int xf)
 {
     if (sp_gated(st, gate)) return;
     __shared__ double L[NRHS * SP_SEG_MAX];
-    __shared__ int lvb[SP_SEG_LEVELS + 1], lvl[SP_SEG_LEVELS];
+    __shared__ int lvb[SP_SEG_LEVELS + 2], lvl[SP_SEG_LEVELS + 2];
     __shared__ double red[32];
+    __shared__ unsigned long long stl[SP_SEG_LEVELS + 1];     // (xf bit 0: the level stamps kept in LDS)
     const int T = blockDim.x, nlv = l1 - l0;
-    for (int l = threadIdx.x; l <= nlv; l += T) {
-        lvb[l] = t.lvptr[l0 + l];
-        if (l < nlv) lvl[l] = t.lvlong[l0 + l];
+    // (two empty levels past the last: the prefetch runs unconditionally)
+    for (int l = threadIdx.x; l < nlv + 2; l += T) {
+        const int e = t.lvptr[l0 + min(l, nlv)];
+        lvb[l] = e;
+        lvl[l] = (l < nlv) ? t.lvlong[l0 + l] : e;
     }
     SegPre A, B;
     segpre_load(t, t.lvptr[l0] + (int)threadIdx.x, t.lvlong[l0], A);
@@ -1592,17 +1644,28 @@ __global__ void __launch_bounds__(1024) k_sp_seg(SpDev sp, TriDev t, const DStat
     __syncthreads();
     const bool stamp = t.stamps && threadIdx.x == 0;
     if (stamp && l0 < SP_STAMP_MAX) t.stamps[l0] = wall_clock64();
+    const bool sync_ld = xf & 2;
     for (int l = 0; l < nlv; l += 2) {
-        if (l + 1 < nlv) segpre_load(t, lvb[l + 1] + (int)threadIdx.x, lvl[l + 1], B);
+        if (!sync_ld) segpre_load(t, lvb[l + 1] + (int)threadIdx.x, lvl[l + 1], B);
         seg_level<NRHS>(t, A, sb, lvl[l], lvb[l + 1], L, red);
         seg_barrier();
-        if (stamp && l0 + l + 1 < SP_STAMP_MAX) t.stamps[l0 + l + 1] = wall_clock64();
+        if (stamp && l0 + l + 1 < SP_STAMP_MAX) {
+            if (xf & 1) stl[l + 1] = wall_clock64();
+            else t.stamps[l0 + l + 1] = wall_clock64();
+        }
         if (l + 1 >= nlv) break;
-        if (l + 2 < nlv) segpre_load(t, lvb[l + 2] + (int)threadIdx.x, lvl[l + 2], A);
+        if (sync_ld) segpre_load(t, lvb[l + 1] + (int)threadIdx.x, lvl[l + 1], B);
+        if (!sync_ld) segpre_load(t, lvb[l + 2] + (int)threadIdx.x, lvl[l + 2], A);
         seg_level<NRHS>(t, B, sb, lvl[l + 1], lvb[l + 2], L, red);
         seg_barrier();
-        if (stamp && l0 + l + 2 < SP_STAMP_MAX) t.stamps[l0 + l + 2] = wall_clock64();
+        if (stamp && l0 + l + 2 < SP_STAMP_MAX) {
+            if (xf & 1) stl[l + 2] = wall_clock64();
+            else t.stamps[l0 + l + 2] = wall_clock64();
+        }
+        if (sync_ld) segpre_load(t, lvb[l + 2] + (int)threadIdx.x, lvl[l + 2], A);
     }
+    if ((xf & 1) && stamp)
+        for (int l = 1; l <= nlv && l0 + l < SP_STAMP_MAX; l++) t.stamps[l0 + l] = stl[l];
     for (int i = threadIdx.x; i < ns; i += T) {
         const int io = t.iout[sb + i];
         out0[io] = L[i];
@@ -1845,6 +1908,12 @@ static void up_tri(hipStream_t s, SpTriDevBufs &B, const SpTriHost &T, int *d_nl
     B.eval.ensure(std::max<size_t>(T.eval.size(), 1));
     B.emid.ensure(std::max<size_t>(T.emid.size(), 1));
     B.aord.ensure(std::max<size_t>(T.aord.size(), 1));
+    B.srx.ensure(std::max<size_t>(T.srx.size(), 4));
+    B.srv.ensure(std::max<size_t>(T.srv.size(), 4));
+    if (!T.srx.empty()) {
+        SPCHK(hipMemcpyAsync(B.srx.p, T.srx.data(), T.srx.size() * sizeof(int), hipMemcpyHostToDevice, s));
+        SPCHK(hipMemcpyAsync(B.srv.p, T.srv.data(), T.srv.size() * sizeof(double), hipMemcpyHostToDevice, s));
+    }
     if (!T.emid.empty())
         SPCHK(hipMemcpyAsync(B.emid.p, T.emid.data(), T.emid.size() * sizeof(int), hipMemcpyHostToDevice, s));
     if (!T.aord.empty())
@@ -1868,6 +1937,7 @@ static TriDev tri_dev(const SpTriDevBufs &B, const int *nlev, unsigned long long
     TriDev t;
     t.lvptr = B.lvptr.p; t.lvlong = B.lvlong.p; t.iin = B.iin.p; t.iout = B.iout.p; t.eptr = B.eptr.p; t.eidx = B.eidx.p;
     t.diag = B.diag.p; t.eval = B.eval.p; t.nlev = nlev; t.stamps = stamps; t.emid = B.emid.p; t.aord = B.aord.p;
+    t.srx = (const int4 *)B.srx.p; t.srv = (const double2 *)B.srv.p;
     return t;
 }
 
@@ -2165,7 +2235,7 @@ static void run_plan(const SpFactor &F, int which, const SpDev &d, hipStream_t s
                 hipLaunchKernelGGL((k_sp_seg_a<NRHS>), dim3(g.ablocks), dim3(256), 0, s, t, st, gate, in0, in1,
                                    (const double *)out0, (const double *)out1, g.sb, g.ns, g.nas, F.sacc.p);
             hipLaunchKernelGGL((k_sp_seg<NRHS>), dim3(1), dim3(1024), 0, s, d, t, st, gate, in0, in1, out0, out1, g.sb,
-                               g.ns, g.nas, g.l0, g.l1, g.pre, (const double *)F.sacc.p, last);
+                               g.ns, g.nas, g.l0, g.l1, g.pre, (const double *)F.sacc.p, last, sp_seg_xf());
         } else if (pl[q].grid) {
             hipLaunchKernelGGL((k_sp_level<NRHS>), dim3(pl[q].blocks), dim3(256), 0, s, t, st, gate, in0, in1, out0,
                                out1, pl[q].l0);
@@ -2335,7 +2405,13 @@ static void host_sweep_plan(const SpTriHost &t, const std::vector<SpFactor::Seg>
         for (int l = g.l0; l < g.l1; l++)
             for (int s = t.lvptr[l]; s < t.lvptr[l + 1]; s++) {
                 double a = acc[s - g.sb];
-                for (int e = t.emid[s]; e < t.eptr[s + 1]; e++) a -= t.eval[e] * acc[t.eidx[e]];
+                const int n = t.srx[(size_t)4 * s + 2];
+                if (n != t.eptr[s + 1] - t.emid[s]) throw std::runtime_error("sparse factor: step record count");
+                for (int u = 0; u < 4 && u < n; u++) {          // the record, as k_sp_seg reads it
+                    const int w = t.srx[(size_t)4 * s + u / 2], ix = (u & 1) ? (int)((unsigned)w >> 16) : (w & 0xffff);
+                    a -= t.srv[(size_t)4 * s + u] * acc[ix];
+                }
+                for (int e = t.emid[s] + 4; e < t.eptr[s + 1]; e++) a -= t.eval[e] * acc[t.eidx[e]];
                 acc[s - g.sb] = a / t.diag[s];
                 out[t.iout[s]] = acc[s - g.sb];
             }
