@@ -96,12 +96,13 @@ struct SpTriHost {
     // segment's steps (local indices) for its external pass, the ones of at
     // most TRI_LONG external entries first
     std::vector<int> emid, aord;
-    // per step of an LDS segment, its first four internal entries as one
-    // record (srx: local indices two per int and the internal count; srv:
-    // the coefficients, zero-padded), so that the internal pass loads a
-    // level's metadata by step index alone
-    std::vector<int> srx;
-    std::vector<double> srv;
+    std::vector<int> lvch;                        // level of one step of at most 64 internal entries (a chain link)
+    // per step of an LDS segment, its first SP_RECN internal entries as one
+    // record (srx: local indices two per int; srn: the internal count; srv:
+    // the coefficients, zero-padded; srd: the reciprocal of the diagonal),
+    // so that the internal pass loads a level's metadata by step index alone
+    std::vector<int> srx, srn;                    // SP_RECN local indices (two per int) / the internal count
+    std::vector<double> srv, srd;                 // SP_RECN coefficients / 1 / diag
 };
 
 struct SpSolves {
@@ -109,12 +110,13 @@ struct SpSolves {
 };
 
 struct SpTriDevBufs {
-    SBuf<int> lvptr, lvlong, iin, iout, eptr, eidx, emid, aord, srx;
-    SBuf<double> diag, eval, srv;
+    SBuf<int> lvptr, lvlong, iin, iout, eptr, eidx, emid, aord, srx, srn, lvch;
+    SBuf<double> diag, eval, srv, srd;
     void release()
     {
         lvptr.release(); lvlong.release(); iin.release(); iout.release(); eptr.release(); eidx.release(); diag.release();
-        eval.release(); emid.release(); aord.release(); srx.release(); srv.release();
+        eval.release(); emid.release(); aord.release(); srx.release(); srv.release(); srn.release(); srd.release();
+        lvch.release();
     }
 };
 
@@ -776,6 +778,9 @@ static void sp_build_solves(const SpLU &F, SpSolves &S, std::vector<SpFactor::Se
 // ---------------------------------------------------------------------------
 constexpr int SP_SEG_MAX = 8192;
 constexpr int SP_SEG_LEVELS = 256;                // levels per LDS segment
+// internal entries per step record: 8 measured slower (k_sp_seg<2> spilled
+// at 128 VGPRs with two records in flight per thread)
+constexpr int SP_RECN = 4;
 
 static bool sp_seg_on()
 {
@@ -784,17 +789,6 @@ static bool sp_seg_on()
         return !e || atoi(e) != 0;
     }();
     return on;
-}
-
-// (experiments) k_sp_seg variants: bit 0 level stamps kept in LDS, bit 1
-// the level metadata loaded at the level instead of a level ahead
-static int sp_seg_xf()
-{
-    static const int x = [] {
-        const char *e = std::getenv("GK_SP_SEGX");
-        return e ? atoi(e) : 0;
-    }();
-    return x;
 }
 
 // entries from which a level runs on the grid (with LDS segments; a level
@@ -838,7 +832,7 @@ static void sp_plan_sweep(SpTriHost &T, std::vector<SpFactor::Seg> &plan, int &w
     // triangle among the tail steps stays internal
     auto tail = [&](int l) {
         const int ns = T.lvptr[l + 1] - T.lvptr[l];
-        return ns <= 16 && T.eptr[T.lvptr[l + 1]] - T.eptr[T.lvptr[l]] >= 64 * ns;
+        return ns <= 16 && T.eptr[T.lvptr[l + 1]] - T.eptr[T.lvptr[l]] >= 512 * ns;
     };
     auto close_run = [&](int l1) {
         if (run < 0) return;
@@ -860,7 +854,9 @@ static void sp_plan_sweep(SpTriHost &T, std::vector<SpFactor::Seg> &plan, int &w
     for (int l = 0; l < nlev; l++) {
         const int nshort = T.lvlong[l] - T.lvptr[l], nlong = T.lvptr[l + 1] - T.lvlong[l];
         const int nent = T.eptr[T.lvptr[l + 1]] - T.eptr[T.lvptr[l]];
-        if (nshort + nlong >= sp_wide_min() || (seg && nent >= sp_wide_entries())) {
+        // (a level of a few long steps stays narrow: its entries into the
+        // levels before go to its segment's external pass)
+        if (nshort + nlong >= sp_wide_min() || (seg && nent >= sp_wide_entries() && nshort + nlong >= 64)) {
             close_run(l);
             plan.push_back({1, l, l + 1, std::max(1, std::max((nshort + 255) / 256, std::min((nlong + 3) / 4, 1024)))});
             wide = 1;
@@ -935,20 +931,27 @@ static void sp_plan_sweep(SpTriHost &T, std::vector<SpFactor::Seg> &plan, int &w
         g.pre = ext >= sp_ga_min();
         g.ablocks = std::max(1, std::max((nas + 255) / 256, std::min((g.ns - nas + 3) / 4, 1024)));
     }
-    T.srx.assign((size_t)4 * std::max(nst, 1), 0);
-    T.srv.assign((size_t)4 * std::max(nst, 1), 0.0);
+    T.lvch.assign(std::max(nlev, 1), 0);
+    for (const auto &g : plan)
+        if (g.grid == 2)
+            for (int l = g.l0; l < g.l1; l++)
+                T.lvch[l] = T.lvptr[l + 1] - T.lvptr[l] == 1 && T.eptr[T.lvptr[l] + 1] - T.emid[T.lvptr[l]] <= 64;
+    T.srx.assign((size_t)(SP_RECN / 2) * std::max(nst, 1), 0);
+    T.srn.assign(std::max(nst, 1), 0);
+    T.srv.assign((size_t)SP_RECN * std::max(nst, 1), 0.0);
+    T.srd.assign(std::max(nst, 1), 1.0);
     for (const auto &g : plan) {
         if (g.grid != 2) continue;
         for (int st = g.sb; st < g.sb + g.ns; st++) {
             const int eb = T.emid[st], n = T.eptr[st + 1] - eb;
-            int ix[4] = {0, 0, 0, 0};
-            for (int u = 0; u < 4 && u < n; u++) {
+            int ix[SP_RECN] = {};
+            for (int u = 0; u < SP_RECN && u < n; u++) {
                 ix[u] = T.eidx[eb + u];
-                T.srv[(size_t)4 * st + u] = T.eval[eb + u];
+                T.srv[(size_t)SP_RECN * st + u] = T.eval[eb + u];
             }
-            T.srx[(size_t)4 * st + 0] = ix[0] | (ix[1] << 16);
-            T.srx[(size_t)4 * st + 1] = ix[2] | (ix[3] << 16);
-            T.srx[(size_t)4 * st + 2] = n;
+            for (int u = 0; u < SP_RECN / 2; u++) T.srx[(size_t)(SP_RECN / 2) * st + u] = ix[2 * u] | (ix[2 * u + 1] << 16);
+            T.srn[st] = n;
+            T.srd[st] = 1.0 / T.diag[st];
         }
     }
 }
@@ -962,8 +965,11 @@ struct TriDev {
     const double *diag, *eval;
     const int *nlev;                              // device word: levels of the current factor
     unsigned long long *stamps;                   // GK_SP_STAMPS: device clock after each level (null: off)
-    const int4 *srx;                              // LDS segments: step records (SpTriHost::srx / srv)
+    const int *lvch;                              // LDS segments: chain-link levels (SpTriHost::lvch)
+    const int2 *srx;                              // LDS segments: step records (SpTriHost::srx / srn / srv / srd)
+    const int *srn;
     const double2 *srv;
+    const double *srd;
 };
 constexpr int SP_STAMP_MAX = 2048;                // levels stamped per sweep
 
@@ -1490,9 +1496,9 @@ __global__ void __launch_bounds__(256) k_sp_seg_a(TriDev t, const DState *st, in
 // diagonal, loaded a level ahead (none depends on the sweep's values)
 struct SegPre {
     int s, n;
-    double dg;
-    int ix[4];
-    double v[4];
+    double rd;
+    int ix[SP_RECN];
+    double v[SP_RECN];
 };
 
 // one record load per step, unconditional (an index past the level reads a
@@ -1500,12 +1506,14 @@ struct SegPre {
 // flight and the prefetch stays in flight across the level's barrier
 __device__ __forceinline__ void segpre_load(const TriDev &t, int s, int lim, SegPre &q)
 {
+    static_assert(SP_RECN == 4, "segpre_load reads records of four entries");
     const int sc = max(min(s, lim - 1), 0);
-    const int4 r = t.srx[sc];
+    const int2 r = t.srx[sc];
     const double2 a = t.srv[2 * sc], b = t.srv[2 * sc + 1];
-    q.dg = t.diag[sc];
+    const int n = t.srn[sc];
+    q.rd = t.srd[sc];
     q.s = s;
-    q.n = (s < lim) ? r.z : 0;
+    q.n = (s < lim) ? n : 0;
     q.ix[0] = r.x & 0xffff; q.ix[1] = (unsigned)r.x >> 16;
     q.ix[2] = r.y & 0xffff; q.ix[3] = (unsigned)r.y >> 16;
     q.v[0] = a.x; q.v[1] = a.y; q.v[2] = b.x; q.v[3] = b.y;
@@ -1517,21 +1525,21 @@ __device__ __forceinline__ void segpre_run(const TriDev &t, const SegPre &q, int
     const int li = q.s - sb;
     double a0 = L[li], a1 = (NRHS == 2) ? L[SP_SEG_MAX + li] : 0.0;
 #pragma unroll
-    for (int u = 0; u < 4; u++) {
+    for (int u = 0; u < SP_RECN; u++) {
         if (u < q.n) {
             a0 -= q.v[u] * L[q.ix[u]];
             if (NRHS == 2) a1 -= q.v[u] * L[SP_SEG_MAX + q.ix[u]];
         }
     }
-    if (q.n > 4) {
+    if (q.n > SP_RECN) {
         const int eb = t.emid[q.s];
-        gather_sub8<NRHS>(t.eidx, t.eval, eb + 4, eb + q.n, [&](int ix, double &x0, double &x1) {
+        gather_sub8<NRHS>(t.eidx, t.eval, eb + SP_RECN, eb + q.n, [&](int ix, double &x0, double &x1) {
             x0 = L[ix];
             x1 = (NRHS == 2) ? L[SP_SEG_MAX + ix] : 0.0;
         }, a0, a1);
     }
-    L[li] = a0 / q.dg;
-    if (NRHS == 2) L[SP_SEG_MAX + li] = a1 / q.dg;
+    L[li] = a0 * q.rd;
+    if (NRHS == 2) L[SP_SEG_MAX + li] = a1 * q.rd;
 }
 
 // the barrier between two levels of the internal pass: the level's LDS
@@ -1610,29 +1618,37 @@ __device__ __forceinline__ void seg_level(const TriDev &t, const SegPre &q, int 
 }
 
 // one LDS segment: levels l0 .. l1-1 (at most SP_SEG_LEVELS), steps sb ..
-// sb+ns-1 (one workgroup); pre: the external pass ran on the grid (acc).
-// The levels' bounds are staged in LDS; each level's short-step metadata is
-// loaded while the level before runs (two register sets, no copies: the
-// loads stay in flight across the barrier); the outputs go to the sweep's
-// vector once, after the last level.  clr as k_sp_sweep
+// sb+ns-1 (one workgroup of 1024); pre: the external pass ran on the grid
+// (acc).  The levels' bounds are staged in LDS; a level's short-step
+// metadata is loaded while the level before runs; the outputs go to the
+// sweep's vector once, after the last level.  A chain — consecutive levels
+// of one step of at most 64 internal entries each, the dense triangle of a
+// block-angular basis's linking rows — runs in wave 0 alone, 16 links per
+// round, their entries staged in LDS by the whole workgroup first: a link
+// is then an LDS gather, a wave reduction and one store, with no barrier.
+// clr as k_sp_sweep
+constexpr int SP_CHAIN = 16;                      // chain links staged per round (64 entries each)
+
 template <int NRHS>
 __global__ void __launch_bounds__(1024) k_sp_seg(SpDev sp, TriDev t, const DState *st, int gate, const double *in0,
                                                  const double *in1, double *out0, double *out1, int sb, int ns,
-                                                 int nas, int l0, int l1, int pre, const double *acc, int clr, int xf)
+                                                 int nas, int l0, int l1, int pre, const double *acc, int clr)
 {
     if (sp_gated(st, gate)) return;
     __shared__ double L[NRHS * SP_SEG_MAX];
-    __shared__ int lvb[SP_SEG_LEVELS + 2], lvl[SP_SEG_LEVELS + 2];
+    __shared__ int lvb[SP_SEG_LEVELS + 2], lvl[SP_SEG_LEVELS + 2], lch[SP_SEG_LEVELS + 2];
     __shared__ double red[32];
-    __shared__ unsigned long long stl[SP_SEG_LEVELS + 1];     // (xf bit 0: the level stamps kept in LDS)
-    const int T = blockDim.x, nlv = l1 - l0;
+    __shared__ int chx[SP_CHAIN * 64], chn[SP_CHAIN];
+    __shared__ double chv[SP_CHAIN * 64], chd[SP_CHAIN];
+    const int T = blockDim.x, nlv = l1 - l0, lane = threadIdx.x & 63;
     // (two empty levels past the last: the prefetch runs unconditionally)
     for (int l = threadIdx.x; l < nlv + 2; l += T) {
         const int e = t.lvptr[l0 + min(l, nlv)];
         lvb[l] = e;
         lvl[l] = (l < nlv) ? t.lvlong[l0 + l] : e;
+        lch[l] = (l < nlv) ? t.lvch[l0 + l] : 0;
     }
-    SegPre A, B;
+    SegPre A;
     segpre_load(t, t.lvptr[l0] + (int)threadIdx.x, t.lvlong[l0], A);
     if (pre)
         for (int i = threadIdx.x; i < ns; i += T) {
@@ -1644,28 +1660,56 @@ __global__ void __launch_bounds__(1024) k_sp_seg(SpDev sp, TriDev t, const DStat
     __syncthreads();
     const bool stamp = t.stamps && threadIdx.x == 0;
     if (stamp && l0 < SP_STAMP_MAX) t.stamps[l0] = wall_clock64();
-    const bool sync_ld = xf & 2;
-    for (int l = 0; l < nlv; l += 2) {
-        if (!sync_ld) segpre_load(t, lvb[l + 1] + (int)threadIdx.x, lvl[l + 1], B);
+    for (int l = 0; l < nlv;) {
+        int c = 0;
+        while (c < SP_CHAIN && l + c < nlv && lch[l + c]) c++;
+        if (c >= 2) {
+            {
+                const int j = threadIdx.x >> 6;
+                if (j < c) {
+                    const int s0 = lvb[l + j], eb = t.emid[s0], n = t.eptr[s0 + 1] - eb;
+                    if (lane < n) {
+                        chx[64 * j + lane] = t.eidx[eb + lane];
+                        chv[64 * j + lane] = t.eval[eb + lane];
+                    }
+                    if (lane == 0) {
+                        chn[j] = n;
+                        chd[j] = t.srd[s0];
+                    }
+                }
+            }
+            __syncthreads();
+            if (threadIdx.x < 64)
+                for (int j = 0; j < c; j++) {
+                    const int li = lvb[l + j] - sb, n = chn[j];
+                    double p0 = 0.0, p1 = 0.0;
+                    if (lane < n) {
+                        const int ix = chx[64 * j + lane];
+                        const double v = chv[64 * j + lane];
+                        p0 = v * L[ix];
+                        if (NRHS == 2) p1 = v * L[SP_SEG_MAX + ix];
+                    }
+                    p0 = wsum(p0);
+                    if (NRHS == 2) p1 = wsum(p1);
+                    if (lane == 0) {
+                        L[li] = (L[li] - p0) * chd[j];
+                        if (NRHS == 2) L[SP_SEG_MAX + li] = (L[SP_SEG_MAX + li] - p1) * chd[j];
+                        if (stamp && l0 + l + j + 1 < SP_STAMP_MAX) t.stamps[l0 + l + j + 1] = wall_clock64();
+                    }
+                }
+            __syncthreads();
+            l += c;
+            segpre_load(t, lvb[l] + (int)threadIdx.x, lvl[l], A);
+            continue;
+        }
+        SegPre B;
+        segpre_load(t, lvb[l + 1] + (int)threadIdx.x, lvl[l + 1], B);
         seg_level<NRHS>(t, A, sb, lvl[l], lvb[l + 1], L, red);
         seg_barrier();
-        if (stamp && l0 + l + 1 < SP_STAMP_MAX) {
-            if (xf & 1) stl[l + 1] = wall_clock64();
-            else t.stamps[l0 + l + 1] = wall_clock64();
-        }
-        if (l + 1 >= nlv) break;
-        if (sync_ld) segpre_load(t, lvb[l + 1] + (int)threadIdx.x, lvl[l + 1], B);
-        if (!sync_ld) segpre_load(t, lvb[l + 2] + (int)threadIdx.x, lvl[l + 2], A);
-        seg_level<NRHS>(t, B, sb, lvl[l + 1], lvb[l + 2], L, red);
-        seg_barrier();
-        if (stamp && l0 + l + 2 < SP_STAMP_MAX) {
-            if (xf & 1) stl[l + 2] = wall_clock64();
-            else t.stamps[l0 + l + 2] = wall_clock64();
-        }
-        if (sync_ld) segpre_load(t, lvb[l + 2] + (int)threadIdx.x, lvl[l + 2], A);
+        if (stamp && l0 + l + 1 < SP_STAMP_MAX) t.stamps[l0 + l + 1] = wall_clock64();
+        A = B;
+        l++;
     }
-    if ((xf & 1) && stamp)
-        for (int l = 1; l <= nlv && l0 + l < SP_STAMP_MAX; l++) t.stamps[l0 + l] = stl[l];
     for (int i = threadIdx.x; i < ns; i += T) {
         const int io = t.iout[sb + i];
         out0[io] = L[i];
@@ -1908,11 +1952,18 @@ static void up_tri(hipStream_t s, SpTriDevBufs &B, const SpTriHost &T, int *d_nl
     B.eval.ensure(std::max<size_t>(T.eval.size(), 1));
     B.emid.ensure(std::max<size_t>(T.emid.size(), 1));
     B.aord.ensure(std::max<size_t>(T.aord.size(), 1));
-    B.srx.ensure(std::max<size_t>(T.srx.size(), 4));
-    B.srv.ensure(std::max<size_t>(T.srv.size(), 4));
+    B.lvch.ensure(std::max<size_t>(T.lvch.size(), 1));
+    if (!T.lvch.empty())
+        SPCHK(hipMemcpyAsync(B.lvch.p, T.lvch.data(), T.lvch.size() * sizeof(int), hipMemcpyHostToDevice, s));
+    B.srx.ensure(std::max<size_t>(T.srx.size(), SP_RECN / 2));
+    B.srn.ensure(std::max<size_t>(T.srn.size(), 1));
+    B.srv.ensure(std::max<size_t>(T.srv.size(), SP_RECN));
+    B.srd.ensure(std::max<size_t>(T.srd.size(), 1));
     if (!T.srx.empty()) {
         SPCHK(hipMemcpyAsync(B.srx.p, T.srx.data(), T.srx.size() * sizeof(int), hipMemcpyHostToDevice, s));
+        SPCHK(hipMemcpyAsync(B.srn.p, T.srn.data(), T.srn.size() * sizeof(int), hipMemcpyHostToDevice, s));
         SPCHK(hipMemcpyAsync(B.srv.p, T.srv.data(), T.srv.size() * sizeof(double), hipMemcpyHostToDevice, s));
+        SPCHK(hipMemcpyAsync(B.srd.p, T.srd.data(), T.srd.size() * sizeof(double), hipMemcpyHostToDevice, s));
     }
     if (!T.emid.empty())
         SPCHK(hipMemcpyAsync(B.emid.p, T.emid.data(), T.emid.size() * sizeof(int), hipMemcpyHostToDevice, s));
@@ -1937,7 +1988,8 @@ static TriDev tri_dev(const SpTriDevBufs &B, const int *nlev, unsigned long long
     TriDev t;
     t.lvptr = B.lvptr.p; t.lvlong = B.lvlong.p; t.iin = B.iin.p; t.iout = B.iout.p; t.eptr = B.eptr.p; t.eidx = B.eidx.p;
     t.diag = B.diag.p; t.eval = B.eval.p; t.nlev = nlev; t.stamps = stamps; t.emid = B.emid.p; t.aord = B.aord.p;
-    t.srx = (const int4 *)B.srx.p; t.srv = (const double2 *)B.srv.p;
+    t.lvch = B.lvch.p;
+    t.srx = (const int2 *)B.srx.p; t.srn = B.srn.p; t.srv = (const double2 *)B.srv.p; t.srd = B.srd.p;
     return t;
 }
 
@@ -2235,7 +2287,7 @@ static void run_plan(const SpFactor &F, int which, const SpDev &d, hipStream_t s
                 hipLaunchKernelGGL((k_sp_seg_a<NRHS>), dim3(g.ablocks), dim3(256), 0, s, t, st, gate, in0, in1,
                                    (const double *)out0, (const double *)out1, g.sb, g.ns, g.nas, F.sacc.p);
             hipLaunchKernelGGL((k_sp_seg<NRHS>), dim3(1), dim3(1024), 0, s, d, t, st, gate, in0, in1, out0, out1, g.sb,
-                               g.ns, g.nas, g.l0, g.l1, g.pre, (const double *)F.sacc.p, last, sp_seg_xf());
+                               g.ns, g.nas, g.l0, g.l1, g.pre, (const double *)F.sacc.p, last);
         } else if (pl[q].grid) {
             hipLaunchKernelGGL((k_sp_level<NRHS>), dim3(pl[q].blocks), dim3(256), 0, s, t, st, gate, in0, in1, out0,
                                out1, pl[q].l0);
@@ -2405,14 +2457,15 @@ static void host_sweep_plan(const SpTriHost &t, const std::vector<SpFactor::Seg>
         for (int l = g.l0; l < g.l1; l++)
             for (int s = t.lvptr[l]; s < t.lvptr[l + 1]; s++) {
                 double a = acc[s - g.sb];
-                const int n = t.srx[(size_t)4 * s + 2];
+                const int n = t.srn[s];
                 if (n != t.eptr[s + 1] - t.emid[s]) throw std::runtime_error("sparse factor: step record count");
-                for (int u = 0; u < 4 && u < n; u++) {          // the record, as k_sp_seg reads it
-                    const int w = t.srx[(size_t)4 * s + u / 2], ix = (u & 1) ? (int)((unsigned)w >> 16) : (w & 0xffff);
-                    a -= t.srv[(size_t)4 * s + u] * acc[ix];
+                for (int u = 0; u < SP_RECN && u < n; u++) {    // the record, as k_sp_seg reads it
+                    const int w = t.srx[(size_t)(SP_RECN / 2) * s + u / 2];
+                    const int ix = (u & 1) ? (int)((unsigned)w >> 16) : (w & 0xffff);
+                    a -= t.srv[(size_t)SP_RECN * s + u] * acc[ix];
                 }
-                for (int e = t.emid[s] + 4; e < t.eptr[s + 1]; e++) a -= t.eval[e] * acc[t.eidx[e]];
-                acc[s - g.sb] = a / t.diag[s];
+                for (int e = t.emid[s] + SP_RECN; e < t.eptr[s + 1]; e++) a -= t.eval[e] * acc[t.eidx[e]];
+                acc[s - g.sb] = (s < t.lvlong[l]) ? a * t.srd[s] : a / t.diag[s];
                 out[t.iout[s]] = acc[s - g.sb];
             }
     }
@@ -2457,6 +2510,29 @@ extern "C" int gk_sp_selftest(int m, const int *ptr, const int *ind, const doubl
     // (GK_SP_SEG, sp_plan_sweep) and solved by their plans
     if (std::getenv("GK_SP_TIMES"))
         fprintf(stderr, "[gk sp times] LU %.2f ms, solves and plans %.2f ms\n", 1e3 * (t1 - t0), 1e3 * (t2 - t1));
+    if (std::getenv("GK_SP_LEVELS")) {
+        const SpTriHost *T4[4] = {&S.fl, &S.fu, &S.bu, &S.bl};
+        for (int i = 0; i < 4; i++) {
+            std::string line = "[gk sp plan]";
+            for (const auto &g : pl[i]) {
+                char b[160];
+                if (g.grid == 2) {
+                    long long ext = 0, in = 0;
+                    int mx = 0;
+                    for (int st = g.sb; st < g.sb + g.ns; st++) {
+                        ext += T4[i]->emid[st] - T4[i]->eptr[st];
+                        in += T4[i]->eptr[st + 1] - T4[i]->emid[st];
+                        mx = std::max(mx, T4[i]->eptr[st + 1] - T4[i]->emid[st]);
+                    }
+                    snprintf(b, sizeof b, " seg[%d,%d) ns %d ext %lld%s int %lld max %d;", g.l0, g.l1, g.ns, ext,
+                             g.pre ? "(grid)" : "", in, mx);
+                } else
+                    snprintf(b, sizeof b, " %s[%d,%d);", g.grid ? "grid" : "run", g.l0, g.l1);
+                line += b;
+            }
+            fprintf(stderr, "%s\n", line.c_str());
+        }
+    }
     std::vector<double> z(b, b + m), w(m);
     host_sweep_plan(S.fl, pl[0], z.data(), z.data());
     host_sweep_plan(S.fu, pl[1], z.data(), x);

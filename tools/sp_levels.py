@@ -28,7 +28,7 @@ def main():
         sys.stdout.write(r.stdout)
         names = ["FTRAN L", "FTRAN U", "BTRAN U'", "BTRAN L'"]
         lines = [ln for ln in r.stderr.splitlines() if ln.startswith("[gk sp levels]")]
-        print("\n".join(ln for ln in r.stderr.splitlines() if ln.startswith("[gk sp times]")))
+        print("\n".join(ln for ln in r.stderr.splitlines() if ln.startswith("[gk sp times]") or ln.startswith("[gk sp plan]")))
         for name, ln in zip(names, lines[-4:]):
             body = ln.split("]", 1)[1].split("(")[0].split()
             lv = [tuple(int(x) for x in t.split("/")) for t in body]
