@@ -395,7 +395,8 @@ def main():
             try:
                 port = int(os.environ.get("MASTER_PORT", "29500")) + 7
                 comm = gk.Comm(ctx, rank, world, f"{os.environ.get('MASTER_ADDR', '127.0.0.1')}:{port}")
-                extra = run_bnb(gk, problems, ctx, names=("c5s_12x30",), comm=comm)
+                # the deep C5s instance (the reference: 287,161 node LPs, 3,170 s)
+                extra = run_bnb(gk, problems, ctx, names=("c5s_12x40",), comm=comm)
                 extra["bnb_comm_backend"] = {1: "tcp", 2: "rccl"}.get(comm.backend, comm.backend)
             except Exception as e:            # noqa: BLE001 (reported, the headline stands)
                 extra = {"error": f"multi-rank B&B leg: {type(e).__name__}: {e}"}
@@ -553,7 +554,7 @@ def run_mid(gk, problems, ctx, c3, start=100000, steps=10):
             "advance_seconds": round(t_adv, 1)}
 
 
-def run_bnb(gk, problems, ctx, names=("gap", "c5s_12x30"), comm=None):
+def run_bnb(gk, problems, ctx, names=("gap", "c5s_12x30", "c5s_12x40"), comm=None):
     """B&B configs (BASELINE.json configs[3], C5s surrogate of configs[4]):
     root glp_simplex + glp_intopt on the device; LP-relaxations/s = node LP
     solves (all ranks) / wall time of glp_intopt."""
