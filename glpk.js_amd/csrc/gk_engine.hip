@@ -1234,7 +1234,10 @@ struct Spx {
             const char *e = std::getenv("GK_SP_AHEAD");
             return e ? std::atoi(e) : 32;
         }();
-        if (lead <= 0 || !f->valid || sp_ahead_mark(*f->sp) >= 0 || hs.npiv == 0 || hs.refact_pending) return;
+        // (below m = 50,000 the host LU takes a few ms: replaying the lead's
+        // FTRANs would cost more than it hides)
+        if (lead <= 0 || m < 50000 || !f->valid || sp_ahead_mark(*f->sp) >= 0 || hs.npiv == 0 || hs.refact_pending)
+            return;
         if (hs.upd_lim < 2 * lead || hs.upd_cnt >= hs.upd_lim || hs.upd_cnt < hs.upd_lim - lead) return;
         pull();
         sp_ahead_start(*f->sp, m, head.data(), E->hcptr.data(), E->hcind.data(), E->hcval.data(), f->parm.piv_tol,

@@ -823,7 +823,12 @@ static void sp_plan_sweep(SpTriHost &T, std::vector<SpFactor::Seg> &plan, int &w
     plan.clear();
     wide = 0;
     const int nlev = T.nlev, nst = nlev ? T.lvptr[nlev] : 0;
-    const bool seg = sp_seg_on();
+    // LDS segments for the large factors: a sweep with a level of
+    // sp_wide_min steps or more, or of many steps in all; a small one keeps
+    // the fused one-workgroup kernels (one launch per sweep pair)
+    bool big = nst >= 16384;
+    for (int l = 0; l < nlev && !big; l++) big = T.lvptr[l + 1] - T.lvptr[l] >= sp_wide_min();
+    const bool seg = sp_seg_on() && big;
     int run = -1;                            // first level of the current narrow run
     // a tail level: a few long steps (the linking rows of a block-angular
     // basis, one per level at the end of FTRAN L); a segment holds tail
