@@ -116,10 +116,13 @@ int     gk_bfd_get_count(const gk_bfd *bfd);
 int     gk_bfd_valid(const gk_bfd *bfd);
 
 /* ---- simplex (glpspx01.js / glpspx02.js) --------------------------------- */
-/* Limits of the explicit-inverse factor: m <= 65535 rows (grid limits of
- * the pivot kernels), and inv(B) is dense: 8 m^2 bytes of HBM per factor
- * (34 GB at m = 65535; 128 MiB at m = 4096).  gk_spx_* return GK_EABI with
- * a message beyond that; the JS shim then keeps the reference's own solver. */
+/* The factor behind gk_spx_* and gk_bfd_factorize* is chosen by a cost
+ * model: the explicit inverse inv(B) (dense, 8 m^2 bytes of
+ * HBM, m <= 65535) for dense A and small or dense-column sparse bases; a
+ * sparse LU with Schur-complement updates (at most SP_KMAX = 256 updates
+ * per chain) for sparse A with m >= 2048 and 16 nnz(A)/n <= m, and always
+ * beyond m = 65535.  GK_SPARSE=1 / 0 forces either; gk_spx_stats.factor_sparse
+ * reports the choice. */
 typedef struct {                /* glp_smcp, SMCP (glpapi06.js:359-375)       */
     int    msg_lev, meth, pricing, r_test;
     double tol_bnd, tol_dj, tol_piv, obj_ll, obj_ul;
