@@ -1590,6 +1590,7 @@ struct Spx {
     }
     void init();
     void run_graph(const SpxDev &d, const DualPlan &pl, int K, int kind = 0);
+    void run_graph_part(const SpxDev &d, const DualPlan &pl, int K, int kind, int part);
     bool lists_stale = false;                   // rlist / rpos / nr to rebuild from the header
     void rebuild_lists();
     void prof_events(int K)
@@ -2056,12 +2057,33 @@ void Spx::rebuild_lists()
     lists_stale = false;
 }
 
+// A batch of K pivots is one captured graph — or, from K = 32 on, two: a
+// head of 8 pivots and the rest.  hipGraphLaunch submits a graph's kernels
+// from the host before the device runs the first of them (≈140 µs for the
+// ≈300 kernels of a 100-pivot batch, GK_CALL_LOG): the device starts on the
+// head after ≈12 µs and runs it while the host submits the tail.  The
+// kernel sequence is the same either way.
 void Spx::run_graph(const SpxDev &d, const DualPlan &pl, int K, int kind)
+{
+    static const int head = [] {
+        const char *e = std::getenv("GK_GRAPH_HEAD");
+        return e ? std::atoi(e) : 8;
+    }();
+    if (head > 0 && K >= 32 && K > head) {
+        run_graph_part(d, pl, head, kind, 1);
+        run_graph_part(d, pl, K - head, kind, 2);
+    } else
+        run_graph_part(d, pl, K, kind, 0);
+}
+
+// part 0: the whole batch; 1: its head (batch begin, no end); 2: its tail
+void Spx::run_graph_part(const SpxDev &d, const DualPlan &pl, int K, int kind, int part)
 {
     Engine &En = *E;
     GraphEntry *hit = nullptr;
+    const int key = kind | (part << 4);
     for (auto &g : En.graphs)
-        if (g.K == K && g.kind == kind && std::memcmp(&g.pl, &pl, sizeof(pl)) == 0 &&
+        if (g.K == K && g.kind == key && std::memcmp(&g.pl, &pl, sizeof(pl)) == 0 &&
             std::memcmp(&g.d, &d, sizeof(d)) == 0) {
             hit = &g;
             break;
@@ -2070,11 +2092,11 @@ void Spx::run_graph(const SpxDev &d, const DualPlan &pl, int K, int kind)
         hipGraph_t graph = nullptr;
         HIPCHK(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
         if (kind == 0) {
-            dual_batch_begin(s, d, pl);
+            if (part != 2) dual_batch_begin(s, d, pl);
             for (int t = 0; t < K; t++) dual_iteration2(s, d, pl);
-            dual_batch_end(s, d, pl);
+            if (part != 1) dual_batch_end(s, d, pl);
         } else {
-            primal_batch_begin(s, d);
+            if (part != 2) primal_batch_begin(s, d);
             for (int t = 0; t < K; t++) primal_iteration2(s, d, pl);
         }
         HIPCHK(hipStreamEndCapture(s, &graph));
@@ -2088,7 +2110,7 @@ void Spx::run_graph(const SpxDev &d, const DualPlan &pl, int K, int kind)
             En.graphs.erase(lru);
         }
         GraphEntry g;
-        g.d = d; g.pl = pl; g.K = K; g.kind = kind; g.exec = exec;
+        g.d = d; g.pl = pl; g.K = K; g.kind = key; g.exec = exec;
         En.graphs.push_back(g);
         hit = &En.graphs.back();
         f->stats.graphs_built++;
