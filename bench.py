@@ -28,7 +28,7 @@ import __graft_entry__  # noqa: E402
 HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 ROOF_KERNEL = "k_dual_update"
 ROW_KERNEL = "k_dual_row"
-ROUND = "r04"
+ROUND = "r05"
 # the C port (oracle/) against the reference itself, both on one core of the
 # build container on C3 from the slack basis: the port 285.8 pivots/s over a
 # 20 s window (6,874 pivots, init_csa included), the reference node 9.4
