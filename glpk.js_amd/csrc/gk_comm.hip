@@ -436,6 +436,35 @@ static int comm_allgather(gk_comm *c, const void *send, size_t bytes, void *recv
 
 extern "C" int gk_comm_rank(const gk_comm *c) { return c ? c->rank : -1; }
 
+namespace gk {
+int gk_comm_size_rank(const gk_comm *c, int *rank)
+{
+    if (rank) *rank = c ? c->rank : 0;
+    return c ? c->size : 1;
+}
+
+// the column-sharded pricing's exchange (gk_dual.hip lp_shard_trow): RCCL
+// on the engine's stream, ordered after the column pass and before the
+// pivot's next kernels with no host round trip; TCP (ranks sharing a GPU,
+// tests) through the host
+int gk_comm_allgather_dev(gk_comm *c, const void *dsend, size_t bytes, void *drecv, hipStream_t s, void *hsend,
+                          void *hrecv)
+{
+    if (!c || c->failed) return 1;
+    if (c->backend == GK_COMM_RCCL) {
+        if (hipSetDevice(c->device) != hipSuccess) return 1;
+        return c->rccl.allgather(dsend, drecv, bytes, ncclChar, c->nc, s) == ncclSuccess ? 0 : 1;
+    }
+    if (hipMemcpyAsync(hsend, dsend, bytes, hipMemcpyDeviceToHost, s) != hipSuccess) return 1;
+    if (hipStreamSynchronize(s) != hipSuccess) return 1;
+    if (comm_allgather(c, hsend, bytes, hrecv) != 0) {
+        c->failed = true;
+        return 1;
+    }
+    return hipMemcpyAsync(drecv, hrecv, bytes * (size_t)c->size, hipMemcpyHostToDevice, s) == hipSuccess ? 0 : 1;
+}
+}  // namespace gk
+
 extern "C" double gk_comm_incumbent(gk_comm *c, double mine)
 {
     if (!c || !c->inc) return mine;

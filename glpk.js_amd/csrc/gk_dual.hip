@@ -36,6 +36,7 @@
 #include <hip/hip_ext.h>
 #include <algorithm>
 #include <cstdlib>
+#include <stdexcept>
 
 namespace gk {
 
@@ -2715,6 +2716,71 @@ __global__ void __launch_bounds__(1024) k_dual_update(SpxDev d, int gn, int ncb,
 // ---------------------------------------------------------------------------
 // host side
 // ---------------------------------------------------------------------------
+// ---- column-sharded pricing (gk_bfd_set_comm) ---------------------------
+// this rank's slice of the pivot row and its max |trow| (as bits) into the
+// send block; then every rank's slice into trow and the largest max
+__global__ void __launch_bounds__(256) k_shard_pack(const double *trow, int lo, int cnt, int L,
+                                                    const unsigned long long *maxbits, double *send)
+{
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < L) send[i] = (i < cnt) ? trow[lo + i] : 0.0;
+    if (i == 0) send[L] = __longlong_as_double((long long)*maxbits);
+}
+
+__global__ void __launch_bounds__(256) k_shard_unpack(const double *recv, int size, int L, int n, double *trow,
+                                                      unsigned long long *maxbits)
+{
+    const int j = blockIdx.x * blockDim.x + threadIdx.x;
+    if (j < n) {
+        const int r = j / L, i = j - r * L;
+        trow[j] = recv[(size_t)r * (L + 1) + i];
+    }
+    if (j == 0) {
+        unsigned long long b = 0;
+        for (int r = 0; r < size; r++) {
+            const unsigned long long x = (unsigned long long)__double_as_longlong(recv[(size_t)r * (L + 1) + L]);
+            b = x > b ? x : b;
+        }
+        *maxbits = b;
+    }
+}
+
+LpShard::~LpShard()
+{
+    if (dsend) (void)hipFree(dsend);
+    if (drecv) (void)hipFree(drecv);
+}
+
+bool lp_force_colpass()
+{
+    static const bool on = [] {
+        const char *e = std::getenv("GK_FORCE_COLPASS");
+        return e && std::atoi(e) != 0;
+    }();
+    return on;
+}
+
+// launched after this rank's column pass: the slices are all-gathered, so
+// every rank holds the pivot row the single-GPU column pass forms — the same
+// values, bit for bit (a column's dot product does not depend on the
+// slicing), and with them the same pivot path
+void lp_shard_trow(hipStream_t s, const SpxDev &d)
+{
+    LpShard &sh = *d.shard;
+    const int n = d.n, L = sh.L;
+    const int lo = std::min(n, sh.rank * L), cnt = std::min(n, lo + L) - lo;
+    hipLaunchKernelGGL(k_shard_pack, dim3(cdiv(L, 256)), dim3(256), 0, s, (const double *)d.trow, lo, cnt, L,
+                       (const unsigned long long *)&d.st->trow_max_bits, sh.dsend);
+    const size_t bytes = (size_t)(L + 1) * sizeof(double);
+    if (gk_comm_allgather_dev(sh.comm, sh.dsend, bytes, sh.drecv, s, sh.hsend.data(), sh.hrecv.data()) != 0) {
+        sh.failed = true;
+        throw std::runtime_error("column-sharded pricing: the exchange failed");
+    }
+    hipLaunchKernelGGL(k_shard_unpack, dim3(cdiv(n, 256)), dim3(256), 0, s, (const double *)sh.drecv, sh.size, L, n,
+                       d.trow, &d.st->trow_max_bits);
+    sh.exchanges++;
+}
+
 DualPlan dual_plan(const SpxDev &d, int nr_max, int nwl_max, int pse, int rigorous)
 {
     const int m = d.m, n = d.n;
@@ -2731,7 +2797,9 @@ DualPlan dual_plan(const SpxDev &d, int nr_max, int nwl_max, int pse, int rigoro
         const char *e = std::getenv("GK_ROWPATH_FRAC");
         return e ? std::atof(e) : 0.5;
     }();
-    pl.rowpath = (d.A.dense && d.A.AT && !rigorous && ns_max <= row_frac * m) ? 1 : 0;
+    // (column-sharded pricing: the column pass, whose slices the ranks own)
+    const bool cp_only = d.shard || lp_force_colpass();
+    pl.rowpath = (d.A.dense && d.A.AT && !rigorous && ns_max <= row_frac * m && !cp_only) ? 1 : 0;
     pl.fused = (d.A.dense && !rigorous) ? 1 : 0;
     const int tiles_t = cdiv(n, 512), tiles_f = cdiv(m, 512);
     pl.tsplits = std::max(1, std::min(2048 / tiles_t, cdiv(ns_max, 8)));
@@ -2770,7 +2838,7 @@ DualPlan dual_plan(const SpxDev &d, int nr_max, int nwl_max, int pse, int rigoro
         pl.gm = rows_blocks;
     }
     pl.awone = (pse && d.A.dense && nwl_max <= 512) ? std::max(nwl_max, 1) : 0;
-    pl.panel = panel_wanted(d, pl);
+    pl.panel = cp_only ? 0 : panel_wanted(d, pl);
     pl.panel_age = pl.panel ? panel_age_max() : 0;
     return pl;
 }
@@ -2917,7 +2985,14 @@ void dual_iteration2(hipStream_t s, const SpxDev &d, const DualPlan &pl, hipEven
         if (ev0) (void)hipEventRecord(ev0, s);
         if (pl.panel)   // the row of p from the MFMA panel (gk_panel.hip)
             panel_trow(s, d, pl);
-        else
+        else if (d.shard) {
+            // this rank's slice of the non-basic positions, then the exchange
+            const LpShard &sh = *d.shard;
+            const int lo = std::min(n, sh.rank * sh.L), hi = std::min(n, lo + sh.L);
+            colpass_gated(s, d.A, CP_TROW, m + lo, hi - lo, d.head, d.stat + lo, d.coef, nullptr, d.rho, nullptr,
+                          d.trow + lo, nullptr, &d.st->trow_max_bits, d.st, 0);
+            lp_shard_trow(s, d);
+        } else
             colpass_gated(s, d.A, CP_TROW, m, n, d.head, d.stat, d.coef, nullptr, d.rho, nullptr, d.trow, nullptr,
                           &d.st->trow_max_bits, d.st, 0);
         if (ev1) (void)hipEventRecord(ev1, s);

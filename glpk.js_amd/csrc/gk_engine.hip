@@ -302,6 +302,7 @@ struct gk_bfd {
     gk_spx_stats stats{};
     gk_report_fn rpt = nullptr;                // progress / termination reports (gk_bfd_set_report)
     void *rpt_ud = nullptr;
+    LpShard *shard = nullptr;                  // column-sharded pricing (gk_bfd_set_comm), or nullptr
 };
 
 // updates the factor takes before it is rebuilt: nfs_max Forrest-Tomlin
@@ -760,6 +761,7 @@ struct Spx {
         // bytes) cost stores and a reduction on the critical path of every
         // pivot: they run only while a profiling mode is on (gk_bfd_profile)
         d.sp = f->sparse ? f->sp : nullptr;
+        d.shard = (f->shard && E->dense && !f->sparse && dual) ? f->shard : nullptr;
         d.tslots = E->prof ? E->tslots.p : nullptr;
         d.xslots = E->prof ? E->xslots.p : nullptr;
         d.trace = nullptr;
@@ -1945,7 +1947,8 @@ int Spx::batch(int K, int rigorous)
         // keeps the graphs and records only the per-block clock stamps
         const int evp = E->prof == 1 || E->prof == 2;
         if (evp) prof_events(K);
-        if (!rigorous && K >= 4 && !evp && !f->sparse) run_graph(d, pl, K);
+        // (sharded: every pivot's exchange sits between its launches — eager)
+        if (!rigorous && K >= 4 && !evp && !f->sparse && !d.shard) run_graph(d, pl, K);
         else {
             dual_batch_begin(s, d, pl);
             for (int t = 0; t < K; t++) dual_iteration2(s, d, pl, ev0(t), ev1(t), ev2(t), ev3(t));
@@ -2593,6 +2596,7 @@ void gk_bfd_destroy(gk_bfd *f)
     (void)hipSetDevice(f->ctx->device);
     if (f->ctx->stream) (void)hipStreamSynchronize(f->ctx->stream);
     delete f->eng;
+    delete f->shard;
     if (f->sp) sp_destroy(f->sp);
     f->Binv.release(); f->C.release(); f->X.release(); f->Y.release(); f->CinvR.release(); f->BS.release();
     f->G.release(); f->vecx.release(); f->vecy.release(); f->partial.release(); f->idx_i.release();
@@ -2950,6 +2954,20 @@ static int spx_entry(gk_ctx *ctx, gk_lp *lp, gk_bfd *f, const gk_smcp *parm, int
             if (sp && !f->sp) f->sp = sp_create();
             f->stats.factor_sparse = sp;
         }
+        if (f->shard && f->shard->n != f->eng->n) {
+            // the exchange's buffers for this n: slices of L = ceil(n / size)
+            LpShard &sh = *f->shard;
+            const int n = f->eng->n;
+            sh.L = (n + sh.size - 1) / sh.size;
+            if (sh.dsend) (void)hipFree(sh.dsend);
+            if (sh.drecv) (void)hipFree(sh.drecv);
+            sh.dsend = sh.drecv = nullptr;
+            HIPCHK(hipMalloc((void **)&sh.dsend, (size_t)(sh.L + 1) * sizeof(double)));
+            HIPCHK(hipMalloc((void **)&sh.drecv, (size_t)sh.size * (sh.L + 1) * sizeof(double)));
+            sh.hsend.assign((size_t)sh.L + 1, 0.0);
+            sh.hrecv.assign((size_t)sh.size * (sh.L + 1), 0.0);
+            sh.n = n;
+        }
         Spx S;
         S.ctx = ctx; S.f = f; S.E = f->eng; S.lp = lp; S.parm = parm; S.dual = dual;
         S.mark("entry");
@@ -2977,10 +2995,38 @@ static int spx_entry(gk_ctx *ctx, gk_lp *lp, gk_bfd *f, const gk_smcp *parm, int
     } catch (const AbiError &e) {
         g_err = e.msg;
         return GK_EABI;
+    } catch (const std::exception &e) {
+        g_err = e.what();
+        return GK_EABI;
     }
 }
 
 int gk_spx_primal(gk_ctx *ctx, gk_lp *lp, gk_bfd *bfd, const gk_smcp *parm) { return spx_entry(ctx, lp, bfd, parm, 0); }
+
+// column-sharded pricing: the dual on this factor forms each
+// pivot row from this rank's slice of the non-basic positions and gathers
+// the others' over comm; every rank of comm must make the same calls on the
+// same problem.  comm = NULL (or a communicator of one rank) turns it off
+int gk_bfd_set_comm(gk_bfd *f, gk_comm *comm)
+{
+    try {
+        ABI_REQUIRE(f, "gk_bfd_set_comm: null factor");
+        delete f->shard;
+        f->shard = nullptr;
+        if (!comm) return 0;
+        int rank = 0;
+        const int size = gk_comm_size_rank(comm, &rank);
+        if (size <= 1) return 0;
+        f->shard = new LpShard;
+        f->shard->comm = comm;
+        f->shard->rank = rank;
+        f->shard->size = size;
+        return 0;
+    } catch (const AbiError &e) {
+        g_err = e.msg;
+        return GK_EABI;
+    }
+}
 
 int gk_spx_dual(gk_ctx *ctx, gk_lp *lp, gk_bfd *bfd, const gk_smcp *parm) { return spx_entry(ctx, lp, bfd, parm, 1); }
 

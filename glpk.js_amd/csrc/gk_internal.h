@@ -16,6 +16,9 @@
 #include <hip/hip_runtime.h>
 #include <cstdint>
 #include <cstddef>
+#include <vector>
+
+struct gk_comm;                     // the library's collective (gk_comm.hip, include/glpk_mi355x.h)
 
 namespace gk {
 
@@ -216,7 +219,30 @@ struct SpxDev {
     int *pslot, *ppos;
     int ldp;
     SpFactor *sp;                            // host pointer: the sparse factor (nullptr: explicit inverse)
+    struct LpShard *shard;                   // host pointer: column-sharded pricing (gk_bfd_set_comm), or nullptr
 };
+
+// column-sharded pricing of one LP (gk_bfd_set_comm): every rank
+// holds the whole problem and factor and takes the same pivots; the pivot
+// row's column pass runs over this rank's slice of the non-basic positions
+// [rank L, rank L + L), L = ceil(n / size), and the slices (with each
+// slice's max |trow|) are all-gathered before the ratio test
+struct LpShard {
+    ::gk_comm *comm = nullptr;
+    int rank = 0, size = 1, L = 0, n = 0;
+    double *dsend = nullptr, *drecv = nullptr;  // device: L + 1 | size (L + 1) doubles
+    std::vector<double> hsend, hrecv;           // host staging (TCP transport)
+    long long exchanges = 0;
+    bool failed = false;
+    ~LpShard();
+};
+// the all-gather of device blocks on stream s: RCCL on the stream itself,
+// TCP through the host staging (synchronizes s); 0 on success
+int gk_comm_allgather_dev(::gk_comm *c, const void *dsend, size_t bytes, void *drecv, hipStream_t s,
+                          void *hsend, void *hrecv);
+int gk_comm_size_rank(const ::gk_comm *c, int *rank);
+void lp_shard_trow(hipStream_t s, const SpxDev &d);
+bool lp_force_colpass();                     // GK_FORCE_COLPASS: the sharded plan on one GPU (comparisons)
 constexpr int PANEL_MAX = 32;
 constexpr int TRACE_KERNELS = 8, TRACE_BLOCKS = 2048;   // trace[(kid * TRACE_BLOCKS + block) * 2 + {0, 1}]
 constexpr int TRACE_PHASES = 8;   // then phase stamps of wave 0: [TRACE_KERNELS * TRACE_BLOCKS * 2 + (kid * TRACE_BLOCKS + block) * 8 + ph]

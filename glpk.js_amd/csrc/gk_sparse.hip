@@ -863,7 +863,7 @@ static void sp_plan_sweep(SpTriHost &T, std::vector<SpFactor::Seg> &plan, int &w
         // levels before go to its segment's external pass)
         if (nshort + nlong >= sp_wide_min() || (seg && nent >= sp_wide_entries() && nshort + nlong >= 64)) {
             close_run(l);
-            plan.push_back({1, l, l + 1, std::max(1, std::max((nshort + 255) / 256, std::min((nlong + 3) / 4, 1024)))});
+            plan.push_back({1, l, l + 1, std::max(1, (nshort + 255) / 256 + nlong)});   // (k_sp_level: a long step a block)
             wide = 1;
         } else if (run < 0)
             run = l;
@@ -934,7 +934,7 @@ static void sp_plan_sweep(SpTriHost &T, std::vector<SpFactor::Seg> &plan, int &w
         for (int i = 0, t = nas; i < g.ns; i++)
             if (T.emid[g.sb + i] - T.eptr[g.sb + i] > TRI_LONG) T.aord[g.sb + t++] = i;
         g.pre = ext >= sp_ga_min();
-        g.ablocks = std::max(1, std::max((nas + 255) / 256, std::min((g.ns - nas + 3) / 4, 1024)));
+        g.ablocks = std::max(1, (nas + 255) / 256 + (g.ns - nas));      // (k_sp_seg_a: a long step a block)
     }
     T.lvch.assign(std::max(nlev, 1), 0);
     for (const auto &g : plan)
@@ -1031,6 +1031,45 @@ __device__ __forceinline__ void wave_dot4(const int *eidx, const double *eval, i
             if (NRHS == 2) p1 += v[u] * x1[u];
         }
     }
+}
+
+// a long step's sum of val[e] x[idx[e]] over [eb, ee) by a whole block of
+// 256 (four entries per thread per trip), reduced in a fixed order (wave
+// sums, then the four waves in order); thread 0 returns it
+template <int NRHS, typename Get>
+__device__ __forceinline__ void block_dot4(const int *eidx, const double *eval, int eb, int ee, Get get, double &s0,
+                                           double &s1)
+{
+    __shared__ double red[2][4];
+    double p0 = 0.0, p1 = 0.0;
+    for (int e = eb + (int)threadIdx.x; e < ee; e += 1024) {
+        int ix[4];
+        double v[4], x0[4], x1[4];
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            const int ec = min(e + 256 * u, ee - 1);
+            ix[u] = eidx[ec];
+            const double w = eval[ec];
+            v[u] = (e + 256 * u < ee) ? w : 0.0;
+        }
+#pragma unroll
+        for (int u = 0; u < 4; u++) get(ix[u], x0[u], x1[u]);
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            p0 += v[u] * x0[u];
+            if (NRHS == 2) p1 += v[u] * x1[u];
+        }
+    }
+    p0 = wsum(p0);
+    if (NRHS == 2) p1 = wsum(p1);
+    const int w = threadIdx.x >> 6;
+    if ((threadIdx.x & 63) == 0) {
+        red[0][w] = p0;
+        red[1][w] = p1;
+    }
+    __syncthreads();
+    s0 = ((red[0][0] + red[0][1]) + red[0][2]) + red[0][3];
+    s1 = ((red[1][0] + red[1][1]) + red[1][2]) + red[1][3];
 }
 
 // one step of a sweep: its metadata and right-hand side(s) do not depend on
@@ -1282,14 +1321,30 @@ __global__ void __launch_bounds__(256) k_sp_level(TriDev t, const DState *st, in
 {
     if (sp_gated(st, gate)) return;
     const int lb = t.lvptr[l], ls = t.lvlong[l], le = t.lvptr[l + 1];
-    const int g = blockIdx.x * blockDim.x + threadIdx.x;
-    if (lb + g < ls) {
-        StepPre<NRHS> q;
-        step_load<NRHS>(t, in0, in1, lb + g, ls, q);
-        step_run<NRHS>(t, q, out0, out1);
+    const int nsb = (ls - lb + 255) / 256;                 // blocks of the short steps
+    if ((int)blockIdx.x < nsb) {
+        const int g = blockIdx.x * blockDim.x + threadIdx.x;
+        if (lb + g < ls) {
+            StepPre<NRHS> q;
+            step_load<NRHS>(t, in0, in1, lb + g, ls, q);
+            step_run<NRHS>(t, q, out0, out1);
+        }
+        return;
     }
-    const int gw = g >> 6, nw = (gridDim.x * blockDim.x) >> 6;
-    for (int s = ls + gw; s < le; s += nw) step_wave<NRHS>(t, in0, in1, s, out0, out1);
+    // a long step a block (blockDim 256)
+    const int s = ls + (int)blockIdx.x - nsb;
+    if (s >= le) return;
+    double a0, a1;
+    block_dot4<NRHS>(t.eidx, t.eval, t.eptr[s], t.eptr[s + 1], [&](int ix, double &x0, double &x1) {
+        x0 = out0[ix];
+        x1 = (NRHS == 2) ? out1[ix] : 0.0;
+    }, a0, a1);
+    if (threadIdx.x == 0) {
+        const int ii = t.iin[s], io = t.iout[s];
+        const double dg = t.diag[s];
+        out0[io] = (in0[ii] - a0) / dg;
+        if (NRHS == 2) out1[io] = (in1[ii] - a1) / dg;
+    }
 }
 
 template <int NRHS>
@@ -1493,8 +1548,32 @@ __global__ void __launch_bounds__(256) k_sp_seg_a(TriDev t, const DState *st, in
                                                   int ns, int nas, double *acc)
 {
     if (sp_gated(st, gate)) return;
-    seg_ext<NRHS>(t, in0, in1, out0, out1, sb, ns, nas, acc, acc + SP_SEG_MAX, blockIdx.x * blockDim.x + threadIdx.x,
-                  gridDim.x * blockDim.x);
+    const int nsb = (nas + 255) / 256;                     // blocks of the short steps
+    if ((int)blockIdx.x < nsb) {
+        const int i = blockIdx.x * blockDim.x + threadIdx.x;
+        if (i < nas) {
+            const int li = t.aord[sb + i];
+            double a0, a1;
+            seg_ext_thread<NRHS>(t, in0, in1, out0, out1, sb + li, a0, a1);
+            acc[li] = a0;
+            if (NRHS == 2) acc[SP_SEG_MAX + li] = a1;
+        }
+        return;
+    }
+    // a step of many external entries a block (blockDim 256)
+    const int i = nas + (int)blockIdx.x - nsb;
+    if (i >= ns) return;
+    const int li = t.aord[sb + i], sx = sb + li;
+    double a0, a1;
+    block_dot4<NRHS>(t.eidx, t.eval, t.eptr[sx], t.emid[sx], [&](int ix, double &x0, double &x1) {
+        x0 = out0[ix];
+        x1 = (NRHS == 2) ? out1[ix] : 0.0;
+    }, a0, a1);
+    if (threadIdx.x == 0) {
+        const int ii = t.iin[sx];
+        acc[li] = in0[ii] - a0;
+        if (NRHS == 2) acc[SP_SEG_MAX + li] = in1[ii] - a1;
+    }
 }
 
 // a short step of the internal pass: its first internal entries and

@@ -118,7 +118,7 @@ EXPORTS = ["gk_abi_version", "gk_device_count", "gk_ctx_create", "gk_ctx_destroy
            "gk_ios_driver_comm", "gk_comm_set_option", "gk_npp_create", "gk_npp_destroy", "gk_npp_load",
            "gk_npp_simplex", "gk_npp_integer", "gk_npp_build_size", "gk_npp_build", "gk_npp_postprocess",
            "gk_npp_unload_sol", "gk_npp_unload_mip", "gk_sp_selftest", "gk_comm_incumbent",
-           "gk_comm_shared_incumbent"]
+           "gk_comm_shared_incumbent", "gk_bfd_set_comm"]
 
 # gk_report_fn (glpk_mi355x.h): one progress line or termination message of
 # a gk_spx_* call, in the order the reference prints them
@@ -148,6 +148,8 @@ def load_library(path: str = LIB_PATH):
     L.gk_bfd_set_parm.argtypes = [P, C.POINTER(Bfcp)]
     L.gk_bfd_set_parm.restype = C.c_int
     L.gk_bfd_reset_parm.argtypes = [P]
+    L.gk_bfd_set_comm.argtypes = [P, P]
+    L.gk_bfd_set_comm.restype = C.c_int
     L.gk_bfd_reset_parm.restype = C.c_int
     L.gk_bfd_factorize_csc.argtypes = [P, C.c_int, P, P, P]
     L.gk_bfd_factorize_csc.restype = C.c_int
@@ -376,6 +378,14 @@ class GkProblem:
         if self.L.gk_bfd_set_parm(self.bfd, C.byref(b)) != 0:
             raise GkError(_err(self.L))
         self.bfcp = b
+
+    def set_comm(self, comm):
+        """Column-sharded pricing of this LP's dual simplex over comm
+        (gk_bfd_set_comm): every rank makes the same calls on the
+        same problem; None turns it off."""
+        self._comm = comm
+        if self.L.gk_bfd_set_comm(self.bfd, comm.h if comm is not None else None) != 0:
+            raise GkError(_err(self.L))
 
     def touch_matrix(self):
         """Invalidate the device copy of A (the shim's version counter)."""

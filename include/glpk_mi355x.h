@@ -40,7 +40,7 @@
 extern "C" {
 #endif
 
-#define GK_ABI_VERSION 9
+#define GK_ABI_VERSION 10
 #include <stddef.h>
 #define GK_EABI (-1)          /* contract violation; see gk_last_error() */
 
@@ -402,6 +402,15 @@ int      gk_comm_set_option(gk_comm *comm, int opt, int value);
  * mip_stat GLP_OPT when the search finished on every rank.  With a
  * one-rank comm it is gk_ios_driver. */
 int gk_ios_driver_comm(gk_ctx *ctx, gk_mip *mip, const gk_iocp *parm, gk_comm *comm);
+
+/* column-sharded pricing of one LP: gk_spx_dual on this
+ * factor forms each pivot row from this rank's slice of the non-basic
+ * positions (a column pass over 1/size of A) and all-gathers the slices over
+ * comm — RCCL on the engine's stream between distinct GPUs, TCP otherwise —
+ * so every rank takes the pivots the single-GPU column pass takes.  Every
+ * rank of comm makes the same gk_spx_dual calls on the same problem.  Dense
+ * A, dual simplex; comm = NULL turns it off.  0 or GK_EABI. */
+int gk_bfd_set_comm(gk_bfd *bfd, gk_comm *comm);
 
 /* glp_scale_prob (glpscl.js:1-225) on the device: the
  * row and column scale factors of A (CSC: ptr[0..n] 0-based offsets, ind[]

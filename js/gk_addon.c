@@ -497,6 +497,19 @@ static napi_value js_comm_option(napi_env env, napi_callback_info info)
     return mk_int(env, gk_comm_set_option((gk_comm *)get_ext(env, argv[0]), opt, v));
 }
 
+/* bfdSetComm(bfd, comm | null): column-sharded pricing of the dual simplex
+ * on this factor (gk_bfd_set_comm) */
+static napi_value js_bfd_set_comm(napi_env env, napi_callback_info info)
+{
+    napi_value argv[2];
+    if (!get_args(env, info, 2, argv)) return NULL;
+    napi_valuetype t;
+    CHECK(napi_typeof(env, argv[1], &t));
+    gk_comm *comm = (t == napi_external) ? (gk_comm *)get_ext(env, argv[1]) : NULL;
+    if (gk_bfd_set_comm((gk_bfd *)get_ext(env, argv[0]), comm) != 0) return throw_gk(env, "gk_bfd_set_comm");
+    return mk_int(env, 0);
+}
+
 /* -------------------------------------------------------------- ios_driver */
 /* ios(ctx, L, iocp): L = the marshalled root problem (solved to optimality,
  * pbs_stat/dbs_stat/obj_val set) plus col_kind (Int8Array [1..n]) and the
@@ -881,6 +894,7 @@ static napi_value init(napi_env env, napi_value exports)
     napi_add_env_cleanup_hook(env, teardown_hook, NULL);
     napi_property_descriptor d[] = {
         FN("commCreate", js_comm_create), FN("commBackend", js_comm_backend), FN("commOption", js_comm_option),
+        FN("bfdSetComm", js_bfd_set_comm),
         FN("create", js_create), FN("deviceCount", js_device_count), FN("abiVersion", js_abi_version),
         FN("lastError", js_last_error), FN("bfdCreate", js_bfd_create), FN("bfdSetParm", js_bfd_set_parm), FN("bfdResetParm", js_bfd_reset_parm),
         FN("bfdFactorizeCsc", js_bfd_factorize_csc), FN("bfdFtran", js_bfd_ftran), FN("bfdBtran", js_bfd_btran),

@@ -1,0 +1,84 @@
+"""Column-sharded pricing of one LP (gk_bfd_set_comm; SURVEY
+§8(e)): every rank holds the problem and the factor, forms its slice of the
+non-basic positions of each pivot row with the column pass, and the slices
+are all-gathered before the ratio test (glpspx02.js:655-935 — eval_trow,
+sort_trow, chuzc — then run on the whole row on every rank).
+
+The column pass's value for a position does not depend on the slicing, so
+the sharded run takes the pivots of the single-GPU run with the same plan
+(GK_FORCE_COLPASS=1: column pass, no pricing panel): return code, pivot
+count and objective bits equal, on every rank, and the objective is the
+reference's 978.22910129338311 (1024 x 4096 generator, tolerance 1e-9
+relative).  Two and three ranks share the one GPU through the library's
+TCP transport (RCCL refuses two ranks on one device); three ranks do not
+divide n = 4096, so the last slice is the short one."""
+import json
+import multiprocessing as mp
+import os
+import subprocess
+import sys
+
+import pytest
+
+from test_comm import free_port
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+REF_OBJ = 978.22910129338311
+
+SINGLE = r"""
+import json, sys
+sys.path.insert(0, %r)
+import __graft_entry__
+__graft_entry__.load_package()
+from glpk_js_amd import gk, problems
+ctx = gk.Context(0)
+P = gk.GkProblem(ctx, problems.gen_dense(1024, 4096, seed=42))
+ret = gk.glp_simplex(P, gk.SMCP(meth=gk.GLP_DUAL, msg_lev=gk.GLP_MSG_ERR))
+print(json.dumps({"ret": ret, "it_cnt": P.it_cnt, "obj": float(P.obj_val).hex()}))
+"""
+
+
+def _worker(rank, size, port, q):
+    try:
+        sys.path.insert(0, ROOT)
+        import __graft_entry__
+        __graft_entry__.load_package()
+        from glpk_js_amd import gk, problems
+        ctx = gk.Context(0)
+        comm = gk.Comm(ctx, rank, size, f"127.0.0.1:{port}")
+        P = gk.GkProblem(ctx, problems.gen_dense(1024, 4096, seed=42))
+        P.set_comm(comm)
+        ret = gk.glp_simplex(P, gk.SMCP(meth=gk.GLP_DUAL, msg_lev=gk.GLP_MSG_ERR))
+        q.put((rank, comm.backend, ret, P.it_cnt, float(P.obj_val).hex()))
+        del P
+        comm.close()
+    except Exception as e:                       # noqa: BLE001 (reported to the parent)
+        q.put((rank, -1, repr(e), None, None))
+
+
+def _single():
+    env = dict(os.environ, GK_FORCE_COLPASS="1")
+    r = subprocess.run([sys.executable, "-c", SINGLE % ROOT], capture_output=True, text=True, env=env, timeout=240)
+    assert r.returncode == 0, r.stderr[-2000:]
+    return json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("size", [2, 3])
+def test_gpu_lp_column_sharded_same_pivots(size):
+    single = _single()
+    assert single["ret"] == 0
+    assert abs(float.fromhex(single["obj"]) - REF_OBJ) <= 1e-9 * REF_OBJ
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = free_port()
+    ps = [ctx.Process(target=_worker, args=(r, size, port, q)) for r in range(size)]
+    for p in ps:
+        p.start()
+    res = sorted([q.get(timeout=240) for _ in range(size)], key=lambda t: t[0])
+    for p in ps:
+        p.join(timeout=60)
+    for rank, backend, ret, it_cnt, obj in res:
+        assert backend != -1, ret
+        assert (ret, it_cnt, obj) == (single["ret"], single["it_cnt"], single["obj"]), (rank, res, single)
+    print("size", size, "pivots", single["it_cnt"], "obj", float.fromhex(single["obj"]))
