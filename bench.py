@@ -382,9 +382,11 @@ def main():
             # ends every rank should the collective hang
             import threading
 
+            held = {"extra": {}}
+
             def _expire():
                 if rank == 0:
-                    line["extra"] = {"error": f"multi-rank B&B leg exceeded {EXTRA_MULTI_S:.0f} s"}
+                    line["extra"] = dict(held["extra"], error=f"multi-rank extras exceeded {EXTRA_MULTI_S:.0f} s")
                     print(json.dumps(line), flush=True)
                 sys.stderr.flush()
                 os._exit(3)            # a hang is a failure: non-zero exit after the line
@@ -400,6 +402,15 @@ def main():
                 extra["bnb_comm_backend"] = {1: "tcp", 2: "rccl"}.get(comm.backend, comm.backend)
             except Exception as e:            # noqa: BLE001 (reported, the headline stands)
                 extra = {"error": f"multi-rank B&B leg: {type(e).__name__}: {e}"}
+            if "error" not in extra:
+                # column-sharded pricing of one LP over the same communicator
+                try:
+                    del P
+                    held["extra"] = extra                  # (what the watchdog prints should this leg hang)
+                    extra["c3_mid_solve_sharded"] = run_mid_sharded(
+                        gk, ctx, problems.gen_dense(args.m, args.n, seed=42), comm)   # one instance on every rank
+                except Exception as e:        # noqa: BLE001
+                    extra["c3_mid_solve_sharded"] = {"error": f"{type(e).__name__}: {e}"}
             dog.cancel()
 
     if rank == 0:
@@ -552,6 +563,41 @@ def run_mid(gk, problems, ctx, c3, start=100000, steps=10):
             "pivots_per_s": round(piv / dt, 1), "bytes_per_pivot": round(byts / max(piv, 1)),
             "algorithmic_GBps": round(gbps, 1), "frac_of_hbm_peak": round(gbps / HBM_PEAK_GBS, 4),
             "advance_seconds": round(t_adv, 1)}
+
+
+def run_mid_sharded(gk, ctx, c3, comm, start=100000, steps=10):
+    """C3 dual in the HBM-bound regime with column-sharded pricing
+    (gk_bfd_set_comm): every rank advances the same instance to
+    pivot `start` on its own (the same pivots on every rank), then the
+    window of `steps` it_lim=100 calls runs with each pivot row's column pass
+    split over the ranks and the slices all-gathered over comm; the time is
+    the max over ranks.  The single-GPU window with the pricing panel is
+    `c3_mid_solve` of the one-GPU run."""
+    import struct
+    P = gk.GkProblem(ctx, c3)
+    adv = gk.SMCP(meth=gk.GLP_DUAL, it_lim=2000, msg_lev=gk.GLP_MSG_ERR)
+    while P.it_cnt < start:
+        leg(f"c3_mid_sharded advance from it_cnt={P.it_cnt}")
+        if gk.glp_simplex(P, adv) != 8:
+            return {"error": "solve ended before the window"}
+    P.set_comm(comm)
+    parm = gk.SMCP(meth=gk.GLP_DUAL, it_lim=100, msg_lev=gk.GLP_MSG_ERR)
+    gk.glp_simplex(P, parm)
+    comm.allgather(b"x")
+    t0 = time.perf_counter()
+    piv = 0
+    for _ in range(steps):
+        it0 = P.it_cnt
+        leg(f"c3_mid_sharded window from it_cnt={it0}")
+        gk.glp_simplex(P, parm)
+        piv += P.it_cnt - it0
+    dt = time.perf_counter() - t0
+    dt = max(struct.unpack("d", blk)[0] for blk in comm.allgather(struct.pack("d", dt)))
+    its = {struct.unpack("q", blk)[0] for blk in comm.allgather(struct.pack("q", int(P.it_cnt)))}
+    P.set_comm(None)
+    return {"window": f"pivots {start + 100}-{start + 100 + piv}", "ranks": comm.size, "pivots": piv,
+            "seconds": round(dt, 4), "pivots_per_s": round(piv / dt, 1), "ranks_agree": len(its) == 1,
+            "backend": {1: "tcp", 2: "rccl"}.get(comm.backend, comm.backend)}
 
 
 def run_bnb(gk, problems, ctx, names=("gap", "c5s_12x30", "c5s_12x40"), comm=None):
