@@ -5,10 +5,16 @@
 #include <cfloat>
 
 namespace gk {
+// need_p == EPI_GATE: the end-of-call epilogue enqueued behind a batch runs
+// only when that batch used its whole budget (stop is ST_RUN or ST_BATCH)
 #define GATE(st, need_p)                                                   \
     if ((st) != nullptr) {                                                 \
-        if ((st)->stop) return;                                            \
-        if ((need_p) && (st)->p <= 0) return;                              \
+        if ((need_p) == EPI_GATE) {                                        \
+            if ((st)->stop > ST_BATCH) return;                             \
+        } else {                                                           \
+            if ((st)->stop) return;                                        \
+            if ((need_p) && (st)->p <= 0) return;                          \
+        }                                                                  \
     }
 
 constexpr int WG = 1024;       // single-workgroup control kernels

@@ -3045,19 +3045,28 @@ void dual_iteration2(hipStream_t s, const SpxDev &d, const DualPlan &pl, hipEven
 // ---------------------------------------------------------------------------
 // y[i] = sum_t inv(B)[i, rlist[t]] x[rlist[t]] + (head[i] <= m ? x[head[i] - 1] : 0);
 // 64 rows per block, its waves split the list, partials meet in wave order
+static __host__ __device__ __forceinline__ int binv_list_waves(int nr) { return nr <= 32 ? 4 : (nr <= 128 ? 8 : 16); }
+
 __global__ void __launch_bounds__(1024) k_binv_list(SpxDev d, int nr, const double *__restrict__ x,
-                                                    double *__restrict__ y)
+                                                    double *__restrict__ y, const DState *eg)
 {
     __shared__ double sp[16][64];
     const int m = d.m;
     const int lane = threadIdx.x & 63;
     const int w = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
-    const int nw = blockDim.x >> 6;
+    int nw = blockDim.x >> 6;
+    if (eg) {
+        // the epilogue's form: the list length of the finished batch, and the
+        // waves the host would have launched for it (the same partial sums)
+        if (eg->stop > ST_BATCH) return;
+        nr = eg->nr;
+        nw = binv_list_waves(nr);
+    }
     const int r = blockIdx.x * 64 + lane;
     const bool act = r < m;
     const size_t ldb = (size_t)d.ldb;
     double acc = 0.0;
-    int t = w;
+    int t = w < nw ? w : nr;
     for (; t + 3 * nw < nr; t += 4 * nw) {
         int c[4];
         double xv[4], bv[4];
@@ -3089,11 +3098,17 @@ __global__ void __launch_bounds__(1024) k_binv_list(SpxDev d, int nr, const doub
 // y[c] = inv(B)[:, c]' x: block t < nr — the dense column rlist[t]; the
 // other blocks — the unit columns of the basic slacks (y[head[i] - 1] = x[i])
 __global__ void __launch_bounds__(256) k_binvt_list(SpxDev d, int nr, const double *__restrict__ x,
-                                                    double *__restrict__ y)
+                                                    double *__restrict__ y, const DState *eg)
 {
     __shared__ double sh[4];
     const int m = d.m;
+    int nrd = nr;                    // (eg: nr bounds the finished batch's list length)
+    if (eg) {
+        if (eg->stop > ST_BATCH) return;
+        nrd = eg->nr;
+    }
     if ((int)blockIdx.x < nr) {
+        if ((int)blockIdx.x >= nrd) return;
         const int c = d.rlist[blockIdx.x];
         const double *col = d.Binv + (size_t)c * d.ldb;
         double acc = 0.0;
@@ -3117,10 +3132,10 @@ __global__ void __launch_bounds__(256) k_binvt_list(SpxDev d, int nr, const doub
     }
 }
 
-void binv_ftran_list(hipStream_t s, const SpxDev &d, int nr, const double *x, double *y)
+void binv_ftran_list(hipStream_t s, const SpxDev &d, int nr, const double *x, double *y, const DState *eg)
 {
-    const int nw = nr <= 32 ? 4 : (nr <= 128 ? 8 : 16);
-    hipLaunchKernelGGL(k_binv_list, dim3(cdiv(d.m, 64)), dim3(64 * nw), 0, s, d, nr, x, y);
+    const int nw = eg ? 16 : binv_list_waves(nr);
+    hipLaunchKernelGGL(k_binv_list, dim3(cdiv(d.m, 64)), dim3(64 * nw), 0, s, d, nr, x, y, eg);
 }
 
 // ---------------------------------------------------------------------------
@@ -3134,19 +3149,27 @@ void binv_ftran_list(hipStream_t s, const SpxDev &d, int nr, const double *x, do
 //   CP_CBAR:  out[j] = coef[k] - N_k' pi for the non-basic position j of k
 //   CP_RESID: out[i] = h[i]   - N_k' pi for the basic position i of k
 // ---------------------------------------------------------------------------
+static __host__ __device__ __forceinline__ int rowpass_waves(int cnt) { return cnt <= 64 ? 4 : (cnt <= 256 ? 8 : 16); }
+
 __global__ void __launch_bounds__(1024) k_rowpass_pi(SpxDev d, int mode, int nr, const double *__restrict__ pi,
                                                      const double *__restrict__ h, double *__restrict__ out,
-                                                     const int *__restrict__ extra, int nextra)
+                                                     const int *__restrict__ extra, int nextra, const DState *eg)
 {
     __shared__ double sp[16][64];
     const int m = d.m, n = d.n;
     const int lane = threadIdx.x & 63;
-    const int w = threadIdx.x >> 6, nw = blockDim.x >> 6;
+    const int w = threadIdx.x >> 6;
+    int nw = blockDim.x >> 6;
+    if (eg) {                        // (as k_binv_list)
+        if (eg->stop > ST_BATCH) return;
+        nr = eg->nr;
+        nw = rowpass_waves(nr + nextra);
+    }
     const int idx = blockIdx.x * 64 + lane;
     const double *__restrict__ col = d.A.AT + min(idx, n - 1);
     const size_t ldt = (size_t)d.A.ldt;
     double acc = 0.0;
-    int t = w;
+    int t = w < nw ? w : nr;
     for (; t + 3 * nw < nr; t += 4 * nw) {
         int c[4];
         double v[4], a[4];
@@ -3164,7 +3187,7 @@ __global__ void __launch_bounds__(1024) k_rowpass_pi(SpxDev d, int mode, int nr,
         const int c = d.rlist[t];
         acc += pi[c] * col[(size_t)c * ldt];
     }
-    for (t = w; t < nextra; t += nw) {        // basic slacks with a cost (primal phase I)
+    for (t = w < nw ? w : nextra; t < nextra; t += nw) {        // basic slacks with a cost (primal phase I)
         const int c = extra[t];
         acc += pi[c] * col[(size_t)c * ldt];
     }
@@ -3186,16 +3209,16 @@ __global__ void __launch_bounds__(1024) k_rowpass_pi(SpxDev d, int mode, int nr,
 }
 
 void rowpass_pi(hipStream_t s, const SpxDev &d, int mode, int nr, const double *pi, const double *h, double *out,
-                const int *extra, int nextra)
+                const int *extra, int nextra, const DState *eg)
 {
-    const int nw = nr + nextra <= 64 ? 4 : (nr + nextra <= 256 ? 8 : 16);
+    const int nw = eg ? 16 : rowpass_waves(nr + nextra);
     hipLaunchKernelGGL(k_rowpass_pi, dim3(cdiv(std::max(d.m, d.n), 64)), dim3(64 * nw), 0, s, d, mode, nr, pi, h,
-                       out, extra, nextra);
+                       out, extra, nextra, eg);
 }
 
-void binv_btran_list(hipStream_t s, const SpxDev &d, int nr, const double *x, double *y)
+void binv_btran_list(hipStream_t s, const SpxDev &d, int nr, const double *x, double *y, const DState *eg)
 {
-    hipLaunchKernelGGL(k_binvt_list, dim3(nr + cdiv(d.m, 256)), dim3(256), 0, s, d, nr, x, y);
+    hipLaunchKernelGGL(k_binvt_list, dim3(nr + cdiv(d.m, 256)), dim3(256), 0, s, d, nr, x, y, eg);
 }
 
 // AT[r*ldt + c] = A[c*lda + r], 64 x 64 tiles through LDS

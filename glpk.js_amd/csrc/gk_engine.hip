@@ -7,7 +7,7 @@
 // Problem data, the basis header and the explicit inverse stay resident in
 // HBM across calls; O(m+n) vectors cross PCIe only at phase switches,
 // refactorizations and store_sol.
-#include "gk_internal.h"
+#include "gk_device.h"
 #include "../../include/glpk_mi355x.h"
 
 #include <algorithm>
@@ -189,6 +189,7 @@ struct Engine {
         unsigned long long fact_ver = 0;
         std::vector<signed char> stat_var;    // the status by variable (1..m+n) it was evaluated with
     } next_aux;
+    hipEvent_t epi_ev = nullptr;              // the end-of-call epilogue's results are on the host (Spx::epi_arm)
     std::vector<GraphEntry> graphs;
     unsigned long long graph_clock = 0;
     int kbatch = 8;                           // batch length carried across calls
@@ -229,6 +230,14 @@ struct Engine {
         std::vector<double> lb, ub, coef, orig_lb, orig_ub, obj, bbar, cbar, gamma;
         std::vector<int> head, bind;
     } spare;
+    // the auxiliary types and bounds of set_aux_bnds (a function of orig_type
+    // alone), kept across calls with the same bounds version; Spx swaps them
+    // with its current arrays instead of rebuilding (Spx::set_aux_bnds)
+    struct AuxCache {
+        bool ok = false;
+        std::vector<signed char> type;
+        std::vector<double> lb, ub;
+    } auxc;
     MatDev mat() const
     {
         MatDev M{};
@@ -252,6 +261,7 @@ struct Engine {
         graphs.clear();
         for (auto e : ev) (void)hipEventDestroy(e);
         ev.clear();
+        if (epi_ev) (void)hipEventDestroy(epi_ev);
         A.release(); AT.release(); cptr.release(); cind.release(); rptr.release(); rcol.release(); cval.release(); rval.release();
         rlist.release(); rpos.release(); rho_idx.release(); rho_val.release();
         gpart.release(); awcnt.release(); tslots.release(); xslots.release(); trace.release(); wlist.release(); wpos.release(); cand.release();
@@ -663,8 +673,9 @@ static void engine_upload_matrix(gk_bfd *f, const gk_lp *lp)
 // status of every non-basic position from the sign of its reduced cost
 __global__ void k_aux_bnds(int m, int n, const signed char *__restrict__ orig_type, const int *__restrict__ head,
                            const double *__restrict__ cbar, double *__restrict__ lb, double *__restrict__ ub,
-                           signed char *__restrict__ stat)
+                           signed char *__restrict__ stat, const DState *st, int need_p)
 {
+    GATE(st, need_p);
     const int k = blockIdx.x * blockDim.x + threadIdx.x;       // variable k + 1
     if (k < m + n) {
         const int t = orig_type[k];
@@ -675,6 +686,66 @@ __global__ void k_aux_bnds(int m, int n, const signed char *__restrict__ orig_ty
         const int v = head[m + k] - 1;
         const int t = orig_type[v];
         stat[k] = (t != FR && t != LO && t != UP) ? NS : (cbar[k] >= 0.0 ? NL : NU);
+    }
+}
+
+// the types and bounds of set_aux_bnds (aux = 1) or set_orig_bnds (aux = 0)
+// written on the device from its own copy of the original ones, instead of
+// an upload of the host's arrays (the statuses are uploaded: they follow the
+// host's numbering of the non-basic positions)
+__global__ void k_set_bounds(int mn, int aux, const signed char *__restrict__ orig_type,
+                             const double *__restrict__ orig_lb, const double *__restrict__ orig_ub,
+                             signed char *__restrict__ type, double *__restrict__ lb, double *__restrict__ ub)
+{
+    const int k = blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= mn) return;
+    const int t = orig_type[k];
+    if (!aux) {
+        type[k] = (signed char)t;
+        lb[k] = orig_lb[k];
+        ub[k] = orig_ub[k];
+        return;
+    }
+    switch (t) {
+    case FR: type[k] = DB; lb[k] = -1e3; ub[k] = +1e3; break;
+    case LO: type[k] = DB; lb[k] = 0.0; ub[k] = +1.0; break;
+    case UP: type[k] = DB; lb[k] = -1.0; ub[k] = 0.0; break;
+    default: type[k] = FX; lb[k] = 0.0; ub[k] = 0.0; break;
+    }
+}
+
+// set_orig_bnds (glpspx02.js:1361-1408) on the device: the original types
+// and bounds back in place, the status of every non-basic position from its
+// type and the sign of its reduced cost (the epilogue's form of the host
+// routine Spx::set_orig_bnds, which repeats it on the mirrors)
+__global__ void k_orig_bnds(int m, int n, const signed char *__restrict__ orig_type, const double *__restrict__ orig_lb,
+                            const double *__restrict__ orig_ub, const int *__restrict__ head,
+                            const double *__restrict__ cbar, signed char *__restrict__ type, double *__restrict__ lb,
+                            double *__restrict__ ub, signed char *__restrict__ stat, const DState *st, int need_p)
+{
+    GATE(st, need_p);
+    const int k = blockIdx.x * blockDim.x + threadIdx.x;
+    if (k < m + n) {
+        type[k] = orig_type[k];
+        lb[k] = orig_lb[k];
+        ub[k] = orig_ub[k];
+    }
+    if (k < n) {
+        const int v = head[m + k] - 1;
+        const double d = cbar[k];
+        signed char sv;
+        switch (orig_type[v]) {
+        case FR: sv = NF; break;
+        case LO: sv = NL; break;
+        case UP: sv = NU; break;
+        case DB:
+            if (d >= +DBL_EPSILON) sv = NL;
+            else if (d <= -DBL_EPSILON) sv = NU;
+            else sv = (fabs(orig_lb[v]) <= fabs(orig_ub[v])) ? NL : NU;
+            break;
+        default: sv = NS; break;
+        }
+        stat[k] = sv;
     }
 }
 
@@ -734,6 +805,22 @@ struct Spx {
     // by pivots, re-inversion, list rebuilds, and cost / bound changes.
     bool cbar_ok = false, bbar_ok = false;
     int evals_skipped = 0;
+    // the end-of-call epilogue (epi_arm): the evaluations the host takes up
+    // after the batch that reaches the iteration limit, enqueued behind that
+    // batch and gated on its budget, with their results downloaded in the
+    // same wait.  eg / eg_nr: the gate and the bound of the list length that
+    // the eval routines' launches take while it is enqueued
+    const DState *eg = nullptr;
+    int eg_nr = 0;
+    struct Epi {
+        bool ready = false;                // the batch ran to its budget: the results below are current
+        bool has_cbar = false, has_bbar = false;
+        bool bounds_pending = false;       // phase I: set_orig_bnds ran on the device (bbar is under them)
+        bool aux = false;                  // next_aux's evaluation launched too
+        std::vector<double> cbar, bbar;
+        std::vector<signed char> stat;
+    } epi;
+    void epi_drop() { epi.ready = epi.has_cbar = epi.has_bbar = epi.bounds_pending = epi.aux = false; }
 
     SpxDev dev() const
     {
@@ -879,6 +966,13 @@ struct Spx {
     {
         if (!head_stale && !vec_stale) return;
         mark("pull");
+        pull_enqueue();
+        sync();
+        head_stale = vec_stale = false;
+        mark("pull done");
+    }
+    void pull_enqueue()
+    {
         // head | bind | stat | bbar | cbar (| coef) lie contiguous in the
         // arena (engine_alloc): one copy into the pinned staging buffer
         const char *lo = (const char *)E->head.p;
@@ -903,17 +997,6 @@ struct Spx {
             take(cbar.data() + 1, E->cbar.p, (size_t)n * sizeof(double));
             if (!dual) take(coef.data() + 1, E->coef.p, ((size_t)m + n) * sizeof(double));
         }
-        sync();
-        head_stale = vec_stale = false;
-        mark("pull done");
-    }
-    void push_bounds()
-    {
-        bbar_ok = false;
-        up(E->type, type, (size_t)m + n);
-        up(E->lb, lb, (size_t)m + n);
-        up(E->ub, ub, (size_t)m + n);
-        up(E->stat, stat, n);
     }
     void push_state()
     {
@@ -957,12 +1040,14 @@ struct Spx {
     bool lists_ok() const { return dual || !lists_stale; }
     void ftran_(const double *x, double *y)
     {
+        if (eg) { binv_ftran_list(s, dev(), eg_nr, x, y, eg); return; }      // (epi_arm: the list form holds)
         if (f->sparse) { sp_ftran(*f->sp, s, x, y); return; }
         if (lists_ok() && hs.nr <= LIST_FTRAN_MAX) binv_ftran_list(s, dev(), hs.nr, x, y);
         else gemv_n(s, f->Binv.p, m, m, f->ldb, x, E->partial.p, PARTIAL_CAP, y, 1.0, nullptr, 0.0);
     }
     void btran_(const double *x, double *y)
     {
+        if (eg) { binv_btran_list(s, dev(), eg_nr, x, y, eg); return; }
         if (f->sparse) { sp_btran(*f->sp, s, x, y); return; }
         if (lists_ok()) binv_btran_list(s, dev(), hs.nr, x, y);
         else gemv_t(s, f->Binv.p, m, m, f->ldb, x, y, 1.0);
@@ -971,13 +1056,30 @@ struct Spx {
     void eval_cbar()
     {
         if (cbar_ok) { evals_skipped++; return; }
+        if (epi.ready && epi.has_cbar) {
+            // the epilogue behind the last batch evaluated it (epi_arm)
+            cbar.swap(epi.cbar);
+            epi.has_cbar = false;
+            cbar_ok = true;
+            evals_skipped++;
+            return;
+        }
         mark("eval_cbar");
         const double t0 = now_s();
         struct T { gk_bfd *f; double t0; ~T() { f->stats.seconds_eval += now_s() - t0; } } tt{f, t0};
+        eval_cbar_dev();
+        down(cbar, E->cbar, n);
+        sync();
+        cbar_ok = true;
+        mark("eval_cbar done");
+    }
+    // the device part of eval_cbar: E->cbar
+    void eval_cbar_dev()
+    {
         SpxDev d = dev();
         MatDev A = E->mat();
         double *cB = E->r1.p, *pi = E->u.p, *r = E->r2.p, *dd = E->work.p;
-        cb_vector(s, m, E->head.p, E->coef.p, cB);
+        cb_vector(s, m, E->head.p, E->coef.p, cB, eg, eg ? EPI_GATE : 0);
         btran_(cB, pi);
         // dense A: pi = inv(B)' cB lives on the dense columns of inv(B) and
         // the basic slacks with a nonzero cost (the primal's phase-I costs;
@@ -988,25 +1090,21 @@ struct Spx {
             for (int i = 1; i <= m; i++)
                 if (head[i] <= m && coef[head[i]] != 0.0) extra.push_back(head[i] - 1);
         }
-        const bool rows = E->dense && A.AT && lists_ok() && hs.nr <= LIST_FTRAN_MAX &&
-                          2 * (hs.nr + (int)extra.size()) <= m;
+        const int nrb = eg ? eg_nr : hs.nr;    // (epi_arm: a bound of the finished batch's nr)
+        const bool rows = E->dense && A.AT && lists_ok() && nrb <= LIST_FTRAN_MAX && 2 * (nrb + (int)extra.size()) <= m;
+        ABI_REQUIRE(!eg || (rows && extra.empty()), "spx: epilogue eval_cbar off the list form");
         if (rows && !extra.empty()) {
             E->xlist.ensure(extra.size());
             HIPCHK(hipMemcpyAsync(E->xlist.p, extra.data(), extra.size() * sizeof(int), hipMemcpyHostToDevice, s));
             sync();
         }
         const int nx = rows ? (int)extra.size() : 0;
-        if (rows) rowpass_pi(s, d, CP_RESID, hs.nr, pi, cB, r, E->xlist.p, nx);
+        if (rows) rowpass_pi(s, d, CP_RESID, nrb, pi, cB, r, E->xlist.p, nx, eg);
         else colpass(s, A, CP_RESID, 0, m, E->head.p, E->stat.p, E->coef.p, cB, pi, nullptr, r, nullptr, nullptr);
         btran_(r, dd);
-        vec_axpy(s, pi, dd, 1.0, m);
-        if (rows) rowpass_pi(s, d, CP_CBAR, hs.nr, pi, nullptr, E->cbar.p, E->xlist.p, nx);
+        vec_axpy(s, pi, dd, 1.0, m, eg, eg ? EPI_GATE : 0);
+        if (rows) rowpass_pi(s, d, CP_CBAR, nrb, pi, nullptr, E->cbar.p, E->xlist.p, nx, eg);
         else colpass(s, A, CP_CBAR, m, n, E->head.p, E->stat.p, E->coef.p, nullptr, pi, nullptr, E->cbar.p, nullptr, nullptr);
-        (void)d;
-        down(cbar, E->cbar, n);
-        sync();
-        cbar_ok = true;
-        mark("eval_cbar done");
     }
 
     // eval_beta (glpspx01.js:473): h = -N xN; beta = inv(B) h, refined once
@@ -1014,16 +1112,29 @@ struct Spx {
     void eval_bbar()
     {
         if (bbar_ok) { evals_skipped++; return; }
+        if (epi.ready && epi.has_bbar && !epi.bounds_pending) {
+            bbar.swap(epi.bbar);
+            epi.has_bbar = false;
+            bbar_ok = true;
+            evals_skipped++;
+            return;
+        }
         mark("eval_bbar");
         const double t0 = now_s();
         struct T { gk_bfd *f; double t0; ~T() { f->stats.seconds_eval += now_s() - t0; } } tt{f, t0};
         if (next_aux_take()) {
             // evaluated at the end of the last call with exactly these bounds,
-            // statuses, basis and factor (the same kernels, so the same bits)
+            // statuses, basis and factor (the same kernels, so the same bits);
+            // the host mirror follows with the next pull (phase I reads it
+            // only after the first batch)
             HIPCHK(hipMemcpyAsync(E->bbar.p, E->bbar_n.p, (size_t)m * sizeof(double), hipMemcpyDeviceToDevice, s));
             evals_skipped++;
-        } else
-            eval_bbar_into(dev(), E->bbar.p);
+            vec_stale = true;
+            bbar_ok = true;
+            mark("eval_bbar done");
+            return;
+        }
+        eval_bbar_into(dev(), E->bbar.p);
         down(bbar, E->bbar, m);
         sync();
         bbar_ok = true;
@@ -1034,14 +1145,15 @@ struct Spx {
     {
         MatDev A = E->mat();
         double *ys = E->r1.p, *wc = E->wcol.p, *h = E->h.p, *t = E->r2.p, *dd = E->work.p;
-        split_pos(s, d, 0, nullptr, ys, wc);
-        aprod_neg(s, A, wc, ys, h, E->partial.p, PARTIAL_CAP);                  // h = ys - A wc
+        const int gm = eg ? EPI_GATE : 0;
+        split_pos(s, d, 0, nullptr, ys, wc, eg, gm);
+        aprod_neg_gated(s, A, wc, ys, h, E->partial.p, PARTIAL_CAP, eg, gm);    // h = ys - A wc
         ftran_(h, beta);
-        split_pos(s, d, 1, beta, ys, wc);
-        aprod_neg(s, A, wc, ys, t, E->partial.p, PARTIAL_CAP);                  // t = B beta
+        split_pos(s, d, 1, beta, ys, wc, eg, gm);
+        aprod_neg_gated(s, A, wc, ys, t, E->partial.p, PARTIAL_CAP, eg, gm);    // t = B beta
         rsub_into(t, h);                                                       // t = h - B beta
         ftran_(t, dd);
-        vec_axpy(s, beta, dd, 1.0, m);
+        vec_axpy(s, beta, dd, 1.0, m, eg, gm);
     }
     // A dual call that stops on its iteration / time limit in phase I leaves
     // its basis for the next call, which (the reference's spx_dual from the
@@ -1063,12 +1175,10 @@ struct Spx {
         if (ev && std::atoi(ev) == 0) return;
         if (!dual || phase != 1 || head_stale || vec_stale) return;
         const size_t mn = (size_t)m + n;
-        E->lb_n.ensure(mn); E->ub_n.ensure(mn); E->stat_n.ensure(n); E->bbar_n.ensure(m);
-        hipLaunchKernelGGL(k_aux_bnds, dim3((unsigned)((std::max<size_t>(mn, n) + 255) / 256)), dim3(256), 0, s, m, n,
-                           E->orig_type.p, E->head.p, E->cbar.p, E->lb_n.p, E->ub_n.p, E->stat_n.p);
-        SpxDev d = dev();
-        d.lb = E->lb_n.p; d.ub = E->ub_n.p; d.stat = E->stat_n.p;
-        eval_bbar_into(d, E->bbar_n.p);
+        if (epi.ready && epi.aux)
+            epi.aux = false;           // the epilogue launched it from the same cbar and header (epi_arm)
+        else
+            next_aux_dev();
         // the host record: the same rule on the host mirrors (cbar is the
         // fresh evaluation the device holds)
         X.stat_var.assign(mn + 1, 0);
@@ -1079,6 +1189,17 @@ struct Spx {
         }
         X.fact_ver = f->fact_ver;
         X.ok = true;
+    }
+    void next_aux_dev()
+    {
+        const size_t mn = (size_t)m + n;
+        E->lb_n.ensure(mn); E->ub_n.ensure(mn); E->stat_n.ensure(n); E->bbar_n.ensure(m);
+        hipLaunchKernelGGL(k_aux_bnds, dim3((unsigned)((std::max<size_t>(mn, n) + 255) / 256)), dim3(256), 0, s, m, n,
+                           E->orig_type.p, E->head.p, E->cbar.p, E->lb_n.p, E->ub_n.p, E->stat_n.p, eg,
+                           eg ? EPI_GATE : 0);
+        SpxDev d = dev();
+        d.lb = E->lb_n.p; d.ub = E->ub_n.p; d.stat = E->stat_n.p;
+        eval_bbar_into(d, E->bbar_n.p);
     }
     bool next_aux_take()
     {
@@ -1126,6 +1247,7 @@ struct Spx {
 
     bool reinvert()
     {
+        epi_drop();
         pull();
         reinv_calls++;
         cbar_ok = bbar_ok = false;
@@ -1313,15 +1435,32 @@ struct Spx {
         }
         return 0;
     }
+    // the host's type / lb / ub hold the auxiliary bounds (the original ones
+    // parked in E->auxc) — see set_aux_bnds
+    bool cur_aux = false;
     void set_aux_bnds()                                  // glpspx02.js:1317
     {
-        for (int k = 1; k <= m + n; k++) {
-            switch (orig_type[k]) {
-            case FR: type[k] = DB; lb[k] = -1e3; ub[k] = +1e3; break;
-            case LO: type[k] = DB; lb[k] = 0.0; ub[k] = +1.0; break;
-            case UP: type[k] = DB; lb[k] = -1.0; ub[k] = 0.0; break;
-            default: type[k] = FX; lb[k] = ub[k] = 0.0; break;
+        // the auxiliary arrays depend on orig_type alone: built once per
+        // bounds version into the cache, then swapped with the current
+        // (original) arrays, and swapped back by set_orig_bnds
+        Engine::AuxCache &C = E->auxc;
+        if (!cur_aux) {
+            const size_t mn = (size_t)m + n + 1;
+            if (!C.ok || C.type.size() != mn) {
+                C.type.resize(mn); C.lb.resize(mn); C.ub.resize(mn);
+                C.type[0] = 0; C.lb[0] = C.ub[0] = 0.0;
+                for (int k = 1; k <= m + n; k++) {
+                    switch (orig_type[k]) {
+                    case FR: C.type[k] = DB; C.lb[k] = -1e3; C.ub[k] = +1e3; break;
+                    case LO: C.type[k] = DB; C.lb[k] = 0.0; C.ub[k] = +1.0; break;
+                    case UP: C.type[k] = DB; C.lb[k] = -1.0; C.ub[k] = 0.0; break;
+                    default: C.type[k] = FX; C.lb[k] = C.ub[k] = 0.0; break;
+                    }
+                }
+                C.ok = true;
             }
+            type.swap(C.type); lb.swap(C.lb); ub.swap(C.ub);
+            cur_aux = true;
         }
         for (int j = 1; j <= n; j++) {
             int k = head[m + j];
@@ -1329,11 +1468,36 @@ struct Spx {
             else if (cbar[j] >= 0.0) stat[j] = NL;
             else stat[j] = NU;
         }
-        push_bounds();
+        push_bounds_dev(1);
+    }
+    // the original arrays back in the host's type / lb / ub
+    void restore_orig_arrays()
+    {
+        if (cur_aux) {
+            Engine::AuxCache &C = E->auxc;
+            type.swap(C.type); lb.swap(C.lb); ub.swap(C.ub);
+            cur_aux = false;
+        } else {
+            type = orig_type; lb = orig_lb; ub = orig_ub;
+        }
+    }
+    // push_bounds, with the types and bounds written by the device from its
+    // original arrays (k_set_bounds) and the statuses uploaded
+    void push_bounds_dev(int aux)
+    {
+        epi_drop();
+        bbar_ok = false;
+        const int mn = m + n;
+        hipLaunchKernelGGL(k_set_bounds, dim3((unsigned)((mn + 255) / 256)), dim3(256), 0, s, mn, aux, E->orig_type.p,
+                           E->orig_lb.p, E->orig_ub.p, E->type.p, E->lb.p, E->ub.p);
+        up(E->stat, stat, n);
     }
     void set_orig_bnds()                                 // glpspx02.js:1361
     {
-        type = orig_type; lb = orig_lb; ub = orig_ub;
+        // (k_orig_bnds ran behind the batch, on the reduced costs the host
+        // now holds)
+        const bool on_dev = epi.ready && epi.bounds_pending && !epi.has_cbar;
+        restore_orig_arrays();
         for (int j = 1; j <= n; j++) {
             int k = head[m + j];
             switch (type[k]) {
@@ -1349,7 +1513,14 @@ struct Spx {
             default: stat[j] = NS; break;
             }
         }
-        push_bounds();
+        if (on_dev) {
+            ABI_REQUIRE(epi.stat.size() == stat.size() && std::memcmp(epi.stat.data() + 1, stat.data() + 1, n) == 0,
+                        "spx: epilogue statuses differ from set_orig_bnds");
+            epi.bounds_pending = false;
+            bbar_ok = false;
+            return;
+        }
+        push_bounds_dev(0);
     }
     int dual_check_stab(double tol_dj)                   // glpspx02.js:1410
     {
@@ -1613,17 +1784,20 @@ struct Spx {
     int run_dual();
     int run_primal();
     int batch(int K, int rigorous);
+    bool epi_arm(int K);
+    void epi_wait();
 };
 
-__global__ void k_rsub_plain(double *y, const double *a, int n)
+__global__ void k_rsub_plain(double *y, const double *a, int n, const DState *st, int need_p)
 {
+    GATE(st, need_p);
     int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i < n) y[i] = a[i] - y[i];
 }
 
 void Spx::rsub_into(double *y, const double *a)
 {
-    hipLaunchKernelGGL(k_rsub_plain, dim3((m + 255) / 256), dim3(256), 0, s, y, a, m);
+    hipLaunchKernelGGL(k_rsub_plain, dim3((m + 255) / 256), dim3(256), 0, s, y, a, m, eg, eg ? EPI_GATE : 0);
 }
 
 __global__ void k_gather_csc_sel(int k, const int *colJ, const int *cptr, const int *crow, const double *cval,
@@ -1682,8 +1856,14 @@ bool Spx::resident_match() const
 // become the resident record of what the device holds
 void Spx::save_resident()
 {
+    // (the record keeps the original arrays: a return in phase I restored
+    // them already, through set_orig_bnds)
+    if (cur_aux) restore_orig_arrays();
     Engine::Resident &R = E->res;
-    R.ok = !head_stale && !vec_stale && !lists_stale && f->valid;
+    // (an epilogue result not taken up: the device holds values the mirrors
+    // do not)
+    R.ok = !head_stale && !vec_stale && !lists_stale && f->valid &&
+           !(epi.ready && (epi.has_cbar || epi.has_bbar || epi.bounds_pending));
     if (!R.ok) return;
     R.dual = dual; R.m = m; R.n = n; R.nr = hs.nr;
     R.a_version = lp->a_version;
@@ -1735,6 +1915,7 @@ void Spx::init()
         orig_lb.swap(R0.orig_lb); orig_ub.swap(R0.orig_ub); coef.swap(R0.coef); obj.swap(R0.obj);
         zeta = R0.zeta;
     } else {
+    E->auxc.ok = false;                 // the original types may have changed
     type.resize(mn); lb.resize(mn); ub.resize(mn); coef.resize(mn); obj.resize(n + 1);
     type[0] = 0; lb[0] = ub[0] = coef[0] = 0.0;
     // init_csa (glpspx01.js:42-145 / glpspx02.js:89-190)
@@ -1904,11 +2085,86 @@ void Spx::init()
     // the stream before everything the solve enqueues next
 }
 
+// The end-of-call epilogue.  A dual batch whose budget ends the call at the
+// iteration limit is followed, on the host, by a fixed sequence of device
+// evaluations (glpspx02.js:1614-1700 at it_lim: eval_cbar, check_stab,
+// check_feas, phase I's set_orig_bnds and eval_beta, store_sol; then the next
+// call's phase-I values, next_aux_launch) — each one a round of launches and
+// a wait after the batch.  Enqueued here, behind the batch and before the
+// host waits for it, they run on the device at once when the batch ends,
+// every kernel gated on the batch having used its whole budget
+// (GATE / EPI_GATE: an earlier stop leaves them no-ops and the device state
+// untouched) and the list kernels reading the batch's final list length on
+// the device.  The same kernels with the same inputs in the same order as the
+// host sequence, so the same bits; the host sequence then takes the results
+// up instead of launching (eval_cbar, set_orig_bnds, eval_bbar,
+// next_aux_launch).  The paths that leave the sequence (instability, phase
+// change with a re-inversion) rebuild every array the epilogue touched.
+// GK_EPILOGUE=0 turns it off.
+bool Spx::epi_arm(int K)
+{
+    static const bool on = [] {
+        const char *e = std::getenv("GK_EPILOGUE");
+        return !e || std::atoi(e) != 0;
+    }();
+    if (!on || !dual || !E->dense || f->sparse || E->prof || (phase != 1 && phase != 2)) return false;
+    if (parm->it_lim >= 0x7fffffff || hs.it_cnt - it_beg + K < parm->it_lim) return false;
+    MatDev A = E->mat();
+    const int nrmax = std::min(m, hs.nr + K);      // one dense column of inv(B) more or less per pivot
+    if (!A.AT || !lists_ok() || nrmax > LIST_FTRAN_MAX || 2 * nrmax > m) return false;
+    if (!E->epi_ev) HIPCHK(hipEventCreateWithFlags(&E->epi_ev, hipEventDisableTiming));
+    // the state and the mirrors as the batch leaves them (pull_state, pull)
+    HIPCHK(hipMemcpyAsync(E->st_host, E->st.p, sizeof(DState), hipMemcpyDeviceToHost, s));
+    pull_enqueue();
+    eg = E->st.p;
+    eg_nr = nrmax;
+    eval_cbar_dev();
+    if (phase == 1) {
+        const size_t mn = (size_t)m + n;
+        hipLaunchKernelGGL(k_orig_bnds, dim3((unsigned)((mn + 255) / 256)), dim3(256), 0, s, m, n, E->orig_type.p,
+                           E->orig_lb.p, E->orig_ub.p, E->head.p, E->cbar.p, E->type.p, E->lb.p, E->ub.p, E->stat.p, eg,
+                           EPI_GATE);
+    }
+    eval_bbar_into(dev(), E->bbar.p);
+    epi.cbar.resize((size_t)n + 1);
+    epi.bbar.resize((size_t)m + 1);
+    epi.stat.resize((size_t)n + 1);
+    epi.cbar[0] = epi.bbar[0] = 0.0;
+    epi.stat[0] = stat[0];
+    down(epi.cbar, E->cbar, n);
+    down(epi.bbar, E->bbar, m);
+    down(epi.stat, E->stat, n);
+    HIPCHK(hipEventRecord(E->epi_ev, s));
+    // the next call's phase-I values (next_aux_launch) behind the wait point
+    static const bool aux_on = [] {
+        const char *e = std::getenv("GK_NEXT_AUX");
+        return !e || std::atoi(e) != 0;
+    }();
+    epi.aux = (phase == 1 && aux_on);
+    if (epi.aux) next_aux_dev();
+    eg = nullptr;
+    epi.has_cbar = epi.has_bbar = true;
+    epi.bounds_pending = (phase == 1);
+    return true;
+}
+
+void Spx::epi_wait()
+{
+    HIPCHK(hipEventSynchronize(E->epi_ev));
+    f->stats.host_syncs++;
+    for (const Pending &q : pending) std::memcpy(q.dst, q.src, q.bytes);
+    pending.clear();
+    pin_off = 0;
+    hs = *E->st_host;
+}
+
 int Spx::batch(int K, int rigorous)
 {
     mark("batch");
     const double t0 = now_s();
     struct T { gk_bfd *f; double t0; ~T() { f->stats.seconds_batches += now_s() - t0; } } tt{f, t0};
+    epi_drop();
+    bool armed = false;
     hs.stop = ST_RUN;
     std::memset(hs.gate, 0, sizeof hs.gate);   // (0 between launches; a clean start whatever a failed run left)
     hs.iter_left = K;
@@ -1948,8 +2204,10 @@ int Spx::batch(int K, int rigorous)
         const int evp = E->prof == 1 || E->prof == 2;
         if (evp) prof_events(K);
         // (sharded: every pivot's exchange sits between its launches — eager)
-        if (!rigorous && K >= 4 && !evp && !f->sparse && !d.shard) run_graph(d, pl, K);
-        else {
+        if (!rigorous && K >= 4 && !evp && !f->sparse && !d.shard) {
+            run_graph(d, pl, K);
+            armed = epi_arm(K);
+        } else {
             dual_batch_begin(s, d, pl);
             for (int t = 0; t < K; t++) dual_iteration2(s, d, pl, ev0(t), ev1(t), ev2(t), ev3(t));
             dual_batch_end(s, d, pl);
@@ -1980,7 +2238,8 @@ int Spx::batch(int K, int rigorous)
         lists_stale = true;                   // the single-workgroup kernels do not maintain rlist
     }
     mark("batch launched");
-    pull_state();
+    if (armed) epi_wait();
+    else pull_state();
     mark("batch done");
     f->stats.batches++;
     f->stats.pivots += hs.npiv;
@@ -2018,10 +2277,18 @@ int Spx::batch(int K, int rigorous)
             }
         }
     }
+    // (armed: the mirrors were downloaded behind the batch, before the
+    // epilogue changed anything)
+    if (armed) head_stale = vec_stale = false;
     if (hs.npiv > 0) {
-        head_stale = vec_stale = true;
+        if (!armed) head_stale = vec_stale = true;
         cbar_ok = bbar_ok = false;
     }
+    if (armed && hs.stop <= ST_BATCH) {
+        ABI_REQUIRE(hs.nr <= eg_nr, "spx: list length %d beyond the epilogue's bound %d", hs.nr, eg_nr);
+        epi.ready = true;
+    } else
+        epi_drop();
     // a stop on the budget leaves the top kernel of the next iteration unrun
     return hs.stop == ST_RUN ? ST_BATCH : hs.stop;
 }
@@ -2165,13 +2432,19 @@ int Spx::run_dual()
             drift_adapt(cbar, n, P->tol_dj);
             cbar_st = 1;
             if (phase == 0) {
+                mark("phase sel");
                 if (dual_check_feas(0.90 * P->tol_dj) != 0) { phase = 1; set_aux_bnds(); }
                 else { phase = 2; set_orig_bnds(); }
-                ABI_REQUIRE(dual_check_stab(P->tol_dj) == 0, "spx_dual: check_stab after phase selection");
+                mark("bounds set");
                 hs.refct = 0;
                 bbar_st = 0;
             }
-            if (dual_check_stab(P->tol_dj) != 0) {
+            // (right after the phase selection the statuses follow the signs
+            // of the reduced costs, so this holds by construction; the
+            // reference checks it there too)
+            const int stab_fail = dual_check_stab(P->tol_dj);
+            mark("stab checked");
+            if (stab_fail != 0) {
                 static const bool dlog = std::getenv("GK_DRIFT_LOG") != nullptr;
                 if (dlog) {
                     double worst = 0.0;
@@ -2262,10 +2535,12 @@ int Spx::run_dual()
                     pull();
                     d_stat = 3;
                     set_orig_bnds();
+                    mark("orig bounds");
                     eval_bbar();
                 } else
                     d_stat = 2;
                 store_sol(3, d_stat, 0);
+                mark("stored");
                 if (ph == 1) {
                     phase = 1;                     // the phase the next call resumes in
                     mark("next_aux");

@@ -43,6 +43,9 @@ enum : int {
     ST_REFACT = 9,    // update limit reached: re-invert before the next pivot
     ST_REFSP = 10,    // PSE reference space must be reset (refct == 0)
 };
+// the gate mode of the end-of-call epilogue's kernels (GATE, gk_device.h)
+constexpr int EPI_GATE = 0x100;
+
 
 struct DState {
     int stop, p, q, p_stat;
@@ -143,6 +146,8 @@ void colpass(hipStream_t s, const MatDev &A, int mode, int off, int cnt, const i
 // glp_eval_tab_row for a batch (gk_tabrow.hip): out[t * (m + n) + k - 1]
 void tab_rows(hipStream_t s, const double *Binv, int ldb, const MatDev &A, int nk, const int *pos, double *G,
               const double *aux, const double *cs, const double *rs, double *out, int use_mfma);
+void aprod_neg_gated(hipStream_t s, const MatDev &A, const double *w, const double *base, double *y,
+                     double *partial, size_t cap, const DState *st, int need_p);
 void aprod_neg(hipStream_t s, const MatDev &A, const double *w, const double *base, double *y,
                double *partial, size_t partial_cap);
 
@@ -294,8 +299,10 @@ struct UpSeg {
 };
 void scatter_segments(hipStream_t s, const char *src, const UpSeg *segs, int nseg);
 // dual, dense A: CP_CBAR / CP_RESID of eval_cbar over the rows of AT in rlist
+// (eg: the epilogue's form — gated on eg, nr read from eg->nr, the argument
+// an upper bound of it; the same sums in the same order)
 void rowpass_pi(hipStream_t s, const SpxDev &d, int mode, int nr, const double *pi, const double *h, double *out,
-                const int *extra, int nextra);
+                const int *extra, int nextra, const DState *eg = nullptr);
 // MFMA panel pricing (gk_panel.hip), column-pass path on dense A: the chosen
 // row from the panel (refilled on a miss) in place of the column pass, and
 // the panel's update after the commit; panel_wanted: the plan's panel size
@@ -307,8 +314,8 @@ void panel_update(hipStream_t s, const SpxDev &d, const DualPlan &pl);
 double launch_trow_rows(hipStream_t s, const SpxDev &d, const DualPlan &pl, int ns);
 // y = inv(B) x and y = inv(B)' x over the nr dense columns of rlist and the
 // unit columns of the basic slacks (valid while rlist is maintained: dual path)
-void binv_ftran_list(hipStream_t s, const SpxDev &d, int nr, const double *x, double *y);
-void binv_btran_list(hipStream_t s, const SpxDev &d, int nr, const double *x, double *y);
+void binv_ftran_list(hipStream_t s, const SpxDev &d, int nr, const double *x, double *y, const DState *eg = nullptr);
+void binv_btran_list(hipStream_t s, const SpxDev &d, int nr, const double *x, double *y, const DState *eg = nullptr);
 
 void primal_iteration(hipStream_t s, const SpxDev &d, int pse, int rigorous);
 void launch_reset_refsp(hipStream_t s, const SpxDev &d, int dual);
@@ -361,12 +368,14 @@ const double *newton_refine(hipStream_t s, int k, const double *C, const double 
                             unsigned long long *rbits, NewtonInfo *info);
 
 // basic helpers
-void vec_axpy(hipStream_t s, double *y, const double *x, double a, int n);
+void vec_axpy(hipStream_t s, double *y, const double *x, double a, int n, const DState *st = nullptr, int need_p = 0);
 void vec_copy(hipStream_t s, double *y, const double *x, int n);
 void gather_row(hipStream_t s, const double *Binv, int ldb, int m, int p, double *rho);
-void cb_vector(hipStream_t s, int m, const int *head, const double *coef, double *cB);
+void cb_vector(hipStream_t s, int m, const int *head, const double *coef, double *cB, const DState *st = nullptr,
+               int need_p = 0);
 void neg_xn_weights(hipStream_t s, const SpxDev &d, double *w);
 // eval_beta's right-hand sides by variable: mode 0 -N xN, mode 1 B beta (see gk_kernels.hip)
-void split_pos(hipStream_t s, const SpxDev &d, int mode, const double *beta, double *ys, double *wc);
+void split_pos(hipStream_t s, const SpxDev &d, int mode, const double *beta, double *ys, double *wc,
+               const DState *st = nullptr, int need_p = 0);
 
 }  // namespace gk

@@ -481,10 +481,10 @@ __global__ void k_axpy(double *y, const double *x, double a, int n, const DState
     if (i < n) y[i] += a * x[i];
 }
 
-void vec_axpy(hipStream_t s, double *y, const double *x, double a, int n)
+void vec_axpy(hipStream_t s, double *y, const double *x, double a, int n, const DState *st, int need_p)
 {
     if (n <= 0) return;
-    hipLaunchKernelGGL(k_axpy, dim3((n + 255) / 256), dim3(256), 0, s, y, x, a, n, (const DState *)nullptr, 0);
+    hipLaunchKernelGGL(k_axpy, dim3((n + 255) / 256), dim3(256), 0, s, y, x, a, n, st, need_p);
 }
 
 __global__ void k_copy(double *y, const double *x, int n, const DState *st, int need_p)
@@ -511,15 +511,16 @@ void gather_row(hipStream_t s, const double *Binv, int ldb, int m, int p, double
     hipLaunchKernelGGL(k_gather_row, dim3((m + 255) / 256), dim3(256), 0, s, Binv, ldb, m, p, rho);
 }
 
-__global__ void k_cb(int m, const int *head, const double *coef, double *cB)
+__global__ void k_cb(int m, const int *head, const double *coef, double *cB, const DState *st, int need_p)
 {
+    GATE(st, need_p);
     int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i < m) cB[i] = coef[head[i] - 1];
 }
 
-void cb_vector(hipStream_t s, int m, const int *head, const double *coef, double *cB)
+void cb_vector(hipStream_t s, int m, const int *head, const double *coef, double *cB, const DState *st, int need_p)
 {
-    hipLaunchKernelGGL(k_cb, dim3((m + 255) / 256), dim3(256), 0, s, m, head, coef, cB);
+    hipLaunchKernelGGL(k_cb, dim3((m + 255) / 256), dim3(256), 0, s, m, head, coef, cB, st, need_p);
 }
 
 
@@ -541,8 +542,10 @@ __global__ void k_neg_xn(int m, int n, const int *head, const signed char *stat,
 //   mode 1 (B beta):      beta[pos - 1] when pos <= m, else 0
 __global__ void k_split_pos(int m, int n, int mode, const int *__restrict__ bind, const signed char *__restrict__ stat,
                             const double *__restrict__ lb, const double *__restrict__ ub,
-                            const double *__restrict__ beta, double *__restrict__ ys, double *__restrict__ wc)
+                            const double *__restrict__ beta, double *__restrict__ ys, double *__restrict__ wc,
+                            const DState *st, int need_p)
 {
+    GATE(st, need_p);
     const int k = blockIdx.x * blockDim.x + threadIdx.x;          // variable k + 1
     if (k >= m + n) return;
     const int pos = bind[k];
@@ -555,11 +558,12 @@ __global__ void k_split_pos(int m, int n, int mode, const int *__restrict__ bind
     else wc[k - m] = v;
 }
 
-void split_pos(hipStream_t s, const SpxDev &d, int mode, const double *beta, double *ys, double *wc)
+void split_pos(hipStream_t s, const SpxDev &d, int mode, const double *beta, double *ys, double *wc, const DState *st,
+               int need_p)
 {
     const int N = d.m + d.n;
     hipLaunchKernelGGL(k_split_pos, dim3((N + 255) / 256), dim3(256), 0, s, d.m, d.n, mode, d.bind, d.stat, d.lb, d.ub,
-                       beta, ys, wc);
+                       beta, ys, wc, st, need_p);
 }
 
 void neg_xn_weights(hipStream_t s, const SpxDev &d, double *w)
