@@ -2849,8 +2849,7 @@ void colpass_gated(hipStream_t s, const MatDev &A, int mode, int off, int cnt, c
                    const signed char *stat, const double *coef, const double *h, const double *x,
                    const double *y, double *out1, double *out2, unsigned long long *maxbits,
                    const DState *st, int need_p);
-void aprod_neg_gated(hipStream_t s, const MatDev &A, const double *w, const double *base, double *y,
-                     double *partial, size_t cap, const DState *st, int need_p);
+
 
 double launch_trow_rows(hipStream_t s, const SpxDev &d, const DualPlan &pl, int ns)
 {
@@ -3048,7 +3047,7 @@ void dual_iteration2(hipStream_t s, const SpxDev &d, const DualPlan &pl, hipEven
 static __host__ __device__ __forceinline__ int binv_list_waves(int nr) { return nr <= 32 ? 4 : (nr <= 128 ? 8 : 16); }
 
 __global__ void __launch_bounds__(1024) k_binv_list(SpxDev d, int nr, const double *__restrict__ x,
-                                                    double *__restrict__ y, const DState *eg)
+                                                    double *__restrict__ y, const DState *eg, int accum)
 {
     __shared__ double sp[16][64];
     const int m = d.m;
@@ -3092,7 +3091,7 @@ __global__ void __launch_bounds__(1024) k_binv_list(SpxDev d, int nr, const doub
     for (int k = 0; k < nw; ++k) v += sp[k][lane];
     const int kh = d.head[r];
     if (kh <= m) v += x[kh - 1];
-    y[r] = v;
+    y[r] = accum ? y[r] + v : v;
 }
 
 // y[c] = inv(B)[:, c]' x: block t < nr — the dense column rlist[t]; the
@@ -3132,10 +3131,10 @@ __global__ void __launch_bounds__(256) k_binvt_list(SpxDev d, int nr, const doub
     }
 }
 
-void binv_ftran_list(hipStream_t s, const SpxDev &d, int nr, const double *x, double *y, const DState *eg)
+void binv_ftran_list(hipStream_t s, const SpxDev &d, int nr, const double *x, double *y, const DState *eg, int acc)
 {
     const int nw = eg ? 16 : binv_list_waves(nr);
-    hipLaunchKernelGGL(k_binv_list, dim3(cdiv(d.m, 64)), dim3(64 * nw), 0, s, d, nr, x, y, eg);
+    hipLaunchKernelGGL(k_binv_list, dim3(cdiv(d.m, 64)), dim3(64 * nw), 0, s, d, nr, x, y, eg, acc);
 }
 
 // ---------------------------------------------------------------------------

@@ -1150,10 +1150,20 @@ struct Spx {
         aprod_neg_gated(s, A, wc, ys, h, E->partial.p, PARTIAL_CAP, eg, gm);    // h = ys - A wc
         ftran_(h, beta);
         split_pos(s, d, 1, beta, ys, wc, eg, gm);
-        aprod_neg_gated(s, A, wc, ys, t, E->partial.p, PARTIAL_CAP, eg, gm);    // t = B beta
-        rsub_into(t, h);                                                       // t = h - B beta
-        ftran_(t, dd);
-        vec_axpy(s, beta, dd, 1.0, m, eg, gm);
+        if (A.dense) {
+            // t = h - B beta in the product's reduction pass
+            aprod_neg_gated(s, A, wc, ys, t, E->partial.p, PARTIAL_CAP, eg, gm, h);
+        } else {
+            aprod_neg_gated(s, A, wc, ys, t, E->partial.p, PARTIAL_CAP, eg, gm);  // t = B beta
+            rsub_into(t, h);                                                       // t = h - B beta
+        }
+        if (eg || (!f->sparse && lists_ok() && hs.nr <= LIST_FTRAN_MAX)) {
+            // beta += inv(B) t in the list FTRAN's pass (ftran_'s list form)
+            binv_ftran_list(s, dev(), eg ? eg_nr : hs.nr, t, beta, eg, 1);
+        } else {
+            ftran_(t, dd);
+            vec_axpy(s, beta, dd, 1.0, m, eg, gm);
+        }
     }
     // A dual call that stops on its iteration / time limit in phase I leaves
     // its basis for the next call, which (the reference's spx_dual from the
@@ -2131,9 +2141,21 @@ bool Spx::epi_arm(int K)
     epi.stat.resize((size_t)n + 1);
     epi.cbar[0] = epi.bbar[0] = 0.0;
     epi.stat[0] = stat[0];
-    down(epi.cbar, E->cbar, n);
-    down(epi.bbar, E->bbar, m);
-    down(epi.stat, E->stat, n);
+    {
+        // stat | bbar | cbar lie contiguous in the arena (pull): one copy
+        const char *lo = (const char *)E->stat.p, *hi = (const char *)(E->cbar.p + n);
+        char *stage = pin_take((size_t)(hi - lo));
+        if (!stage) {
+            down(epi.cbar, E->cbar, n);
+            down(epi.bbar, E->bbar, m);
+            down(epi.stat, E->stat, n);
+        } else {
+            HIPCHK(hipMemcpyAsync(stage, lo, (size_t)(hi - lo), hipMemcpyDeviceToHost, s));
+            pending.push_back(Pending{epi.stat.data() + 1, stage, (size_t)n});
+            pending.push_back(Pending{epi.bbar.data() + 1, stage + ((const char *)E->bbar.p - lo), (size_t)m * sizeof(double)});
+            pending.push_back(Pending{epi.cbar.data() + 1, stage + ((const char *)E->cbar.p - lo), (size_t)n * sizeof(double)});
+        }
+    }
     HIPCHK(hipEventRecord(E->epi_ev, s));
     // the next call's phase-I values (next_aux_launch) behind the wait point
     static const bool aux_on = [] {

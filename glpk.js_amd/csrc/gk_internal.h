@@ -146,8 +146,9 @@ void colpass(hipStream_t s, const MatDev &A, int mode, int off, int cnt, const i
 // glp_eval_tab_row for a batch (gk_tabrow.hip): out[t * (m + n) + k - 1]
 void tab_rows(hipStream_t s, const double *Binv, int ldb, const MatDev &A, int nk, const int *pos, double *G,
               const double *aux, const double *cs, const double *rs, double *out, int use_mfma);
+// (from, dense A only: y = from - (base - A w), the residual of eval_beta's refinement in one pass)
 void aprod_neg_gated(hipStream_t s, const MatDev &A, const double *w, const double *base, double *y,
-                     double *partial, size_t cap, const DState *st, int need_p);
+                     double *partial, size_t cap, const DState *st, int need_p, const double *from = nullptr);
 void aprod_neg(hipStream_t s, const MatDev &A, const double *w, const double *base, double *y,
                double *partial, size_t partial_cap);
 
@@ -314,7 +315,9 @@ void panel_update(hipStream_t s, const SpxDev &d, const DualPlan &pl);
 double launch_trow_rows(hipStream_t s, const SpxDev &d, const DualPlan &pl, int ns);
 // y = inv(B) x and y = inv(B)' x over the nr dense columns of rlist and the
 // unit columns of the basic slacks (valid while rlist is maintained: dual path)
-void binv_ftran_list(hipStream_t s, const SpxDev &d, int nr, const double *x, double *y, const DState *eg = nullptr);
+// (acc: y += inv(B) x, the refinement step's update in the same pass)
+void binv_ftran_list(hipStream_t s, const SpxDev &d, int nr, const double *x, double *y, const DState *eg = nullptr,
+                     int acc = 0);
 void binv_btran_list(hipStream_t s, const SpxDev &d, int nr, const double *x, double *y, const DState *eg = nullptr);
 
 void primal_iteration(hipStream_t s, const SpxDev &d, int pse, int rigorous);

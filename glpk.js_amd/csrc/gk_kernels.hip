@@ -104,7 +104,7 @@ __global__ void __launch_bounds__(256) k_gemv_n_part(const double *__restrict__ 
 __global__ void __launch_bounds__(512) k_gemv_reduce(const double *__restrict__ part, int rows, int splits,
                                                        double *__restrict__ y, double alpha,
                                                        const double *__restrict__ base, double beta,
-                                                       const DState *st, int need_p)
+                                                       const DState *st, int need_p, const double *__restrict__ from)
 {
     GATE(st, need_p);
     __shared__ double sh[8][64];
@@ -123,13 +123,13 @@ __global__ void __launch_bounds__(512) k_gemv_reduce(const double *__restrict__ 
         for (int k = 1; k < 8; ++k) v += sh[k][lane];
         v *= alpha;
         if (base) v = beta * base[r] + v;
-        y[r] = v;
+        y[r] = from ? from[r] - v : v;       // (from: y = from - (base - A x), eval_beta's residual)
     }
 }
 
 static void gemv_n_gated(hipStream_t s, const double *M, int rows, int cols, int ld, const double *x,
                          double *partial, size_t cap, double *y, double alpha, const double *base, double beta,
-                         const DState *st, int need_p)
+                         const DState *st, int need_p, const double *from = nullptr)
 {
     if (rows <= 0) return;
     GemvPlan p = gemv_plan(rows, cols, ld);
@@ -145,7 +145,7 @@ static void gemv_n_gated(hipStream_t s, const double *M, int rows, int cols, int
         p.splits = 0;
     }
     hipLaunchKernelGGL(k_gemv_reduce, dim3((rows + 63) / 64), dim3(512), 0, s, partial, rows, p.splits, y, alpha,
-                       base, beta, st, need_p);
+                       base, beta, st, need_p, from);
 }
 
 void gemv_n(hipStream_t s, const double *M, int rows, int cols, int ld, const double *x, double *partial,
@@ -401,10 +401,10 @@ __global__ void __launch_bounds__(256) k_csr_neg(int m, const int *__restrict__ 
 }
 
 void aprod_neg_gated(hipStream_t s, const MatDev &A, const double *w, const double *base, double *y,
-                            double *partial, size_t cap, const DState *st, int need_p)
+                            double *partial, size_t cap, const DState *st, int need_p, const double *from)
 {
     if (A.dense)
-        gemv_n_gated(s, A.A, A.m, A.n, A.lda, w, partial, cap, y, -1.0, base, 1.0, st, need_p);
+        gemv_n_gated(s, A.A, A.m, A.n, A.lda, w, partial, cap, y, -1.0, base, 1.0, st, need_p, from);
     else
         hipLaunchKernelGGL(k_csr_neg, dim3((A.m + 255) / 256), dim3(256), 0, s, A.m, A.rptr, A.rcol, A.rval, w, base, y,
                            st, need_p);
