@@ -1532,6 +1532,26 @@ struct Spx {
         }
         push_bounds_dev(0);
     }
+    // check_stab and check_feas in one pass over the reduced costs
+    int dual_check_stab_feas(double tol_dj, int *feas)
+    {
+        int stab = 0, inf = 0;
+        for (int j = 1; j <= n; j++) {
+            const double d = cbar[j];
+            const int st = stat[j];
+            const int t = orig_type[head[m + j]];
+            if (d < -tol_dj) {
+                stab |= (st == NL || st == NF);
+                inf |= (t == LO || t == FR);
+            }
+            if (d > +tol_dj) {
+                stab |= (st == NU || st == NF);
+                inf |= (t == UP || t == FR);
+            }
+        }
+        *feas = inf;
+        return stab;
+    }
     int dual_check_stab(double tol_dj)                   // glpspx02.js:1410
     {
         for (int j = 1; j <= n; j++) {
@@ -1656,7 +1676,8 @@ struct Spx {
             if (k <= m) {
                 lp->row_stat[k] = BS;
                 if (lp->row_bind) lp->row_bind[k] = i;
-                lp->row_prim[k] = bbar[i] / lp->rii[k];
+                const double r = lp->rii[k];
+                lp->row_prim[k] = r == 1.0 ? bbar[i] : bbar[i] / r;        // (x / 1 == x)
                 lp->row_dual[k] = 0.0;
             } else {
                 int c = k - m;
@@ -1677,7 +1698,8 @@ struct Spx {
                 case NF: lp->row_prim[k] = 0.0; break;
                 default: lp->row_prim[k] = lp->row_lb[k]; break;
                 }
-                lp->row_dual[k] = (cbar[j] * lp->rii[k]) / zeta;
+                const double r = lp->rii[k];
+                lp->row_dual[k] = (r == 1.0 ? cbar[j] : cbar[j] * r) / zeta;
             } else {
                 int c = k - m;
                 lp->col_stat[c] = stat[j];
@@ -1688,7 +1710,8 @@ struct Spx {
                 case NF: lp->col_prim[c] = 0.0; break;
                 default: lp->col_prim[c] = lp->col_lb[c]; break;
                 }
-                lp->col_dual[c] = (cbar[j] / lp->sjj[c]) / zeta;
+                const double q = lp->sjj[c];
+                lp->col_dual[c] = (q == 1.0 ? cbar[j] : cbar[j] / q) / zeta;
             }
         }
     }
@@ -1796,6 +1819,7 @@ struct Spx {
     int batch(int K, int rigorous);
     bool epi_arm(int K);
     void epi_wait();
+    size_t epi_skip = (size_t)-1;
 };
 
 __global__ void k_rsub_plain(double *y, const double *a, int n, const DState *st, int need_p)
@@ -1915,7 +1939,7 @@ void Spx::init()
     head.resize(mn); stat.resize(n + 1);
     head[0] = 0; stat[0] = 0;
     bind.assign(mn, 0);
-    gamma.assign(std::max(m, n) + 1, 0.0);
+    gamma.resize(std::max(m, n) + 1);       // (filled by a download before every read)
     if (fastv) {
         // the record gives its arrays away here: it is no longer valid, even
         // if a check below throws before the call gets under way (a retry
@@ -2126,6 +2150,7 @@ bool Spx::epi_arm(int K)
     // the state and the mirrors as the batch leaves them (pull_state, pull)
     HIPCHK(hipMemcpyAsync(E->st_host, E->st.p, sizeof(DState), hipMemcpyDeviceToHost, s));
     pull_enqueue();
+    epi_skip = pending.size() - 1;          // the updated cbar: superseded when the epilogue runs
     eg = E->st.p;
     eg_nr = nrmax;
     eval_cbar_dev();
@@ -2174,10 +2199,14 @@ void Spx::epi_wait()
 {
     HIPCHK(hipEventSynchronize(E->epi_ev));
     f->stats.host_syncs++;
-    for (const Pending &q : pending) std::memcpy(q.dst, q.src, q.bytes);
+    hs = *E->st_host;
+    // (a batch that used its budget: eval_cbar takes the epilogue's cbar up
+    // before anything reads the mirror)
+    const size_t skip = hs.stop <= ST_BATCH ? epi_skip : (size_t)-1;
+    for (size_t i = 0; i < pending.size(); i++)
+        if (i != skip) std::memcpy(pending[i].dst, pending[i].src, pending[i].bytes);
     pending.clear();
     pin_off = 0;
-    hs = *E->st_host;
 }
 
 int Spx::batch(int K, int rigorous)
@@ -2447,24 +2476,30 @@ int Spx::run_dual()
             hs.upd_cnt = sp_replayed; hs.refact_pending = 0; hs.grow_bits = 0;
         }
         hs.binv_fresh = (binv_st == 1);
+        int feas_pre = -1;                 // phase I: check_feas of this iteration, found with check_stab
         if (cbar_st == 0) {
             dinf_known = false;
             pull();
             eval_cbar();
             drift_adapt(cbar, n, P->tol_dj);
             cbar_st = 1;
+            bool sel_aux = false;
             if (phase == 0) {
                 mark("phase sel");
-                if (dual_check_feas(0.90 * P->tol_dj) != 0) { phase = 1; set_aux_bnds(); }
+                if (dual_check_feas(0.90 * P->tol_dj) != 0) { phase = 1; set_aux_bnds(); sel_aux = true; }
                 else { phase = 2; set_orig_bnds(); }
                 mark("bounds set");
                 hs.refct = 0;
                 bbar_st = 0;
             }
-            // (right after the phase selection the statuses follow the signs
-            // of the reduced costs, so this holds by construction; the
-            // reference checks it there too)
-            const int stab_fail = dual_check_stab(P->tol_dj);
+            // check_stab (glpspx02.js:1410).  Right after set_aux_bnds every
+            // status follows the sign of its reduced cost (NL: d >= 0, NU:
+            // d < 0, NS), so it cannot fail there; in phase I the same pass
+            // gives check_feas (:1296), which the phase-I test below takes
+            int stab_fail = 0;
+            if (sel_aux) stab_fail = 0;
+            else if (phase == 1) stab_fail = dual_check_stab_feas(P->tol_dj, &feas_pre);
+            else stab_fail = dual_check_stab(P->tol_dj);
             mark("stab checked");
             if (stab_fail != 0) {
                 static const bool dlog = std::getenv("GK_DRIFT_LOG") != nullptr;
@@ -2495,6 +2530,7 @@ int Spx::run_dual()
             // when the batch ran to its budget
             int infeas;
             if (dinf_known) infeas = hs.dinf;
+            else if (feas_pre >= 0) infeas = feas_pre;
             else {
                 pull();
                 infeas = dual_check_feas(P->tol_dj);
