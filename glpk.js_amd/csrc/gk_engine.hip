@@ -689,61 +689,54 @@ __global__ void k_aux_bnds(int m, int n, const signed char *__restrict__ orig_ty
     }
 }
 
-// the types and bounds of set_aux_bnds (aux = 1) or set_orig_bnds (aux = 0)
-// written on the device from its own copy of the original ones, instead of
-// an upload of the host's arrays (the statuses are uploaded: they follow the
-// host's numbering of the non-basic positions)
-__global__ void k_set_bounds(int mn, int aux, const signed char *__restrict__ orig_type,
-                             const double *__restrict__ orig_lb, const double *__restrict__ orig_ub,
-                             signed char *__restrict__ type, double *__restrict__ lb, double *__restrict__ ub)
-{
-    const int k = blockIdx.x * blockDim.x + threadIdx.x;
-    if (k >= mn) return;
-    const int t = orig_type[k];
-    if (!aux) {
-        type[k] = (signed char)t;
-        lb[k] = orig_lb[k];
-        ub[k] = orig_ub[k];
-        return;
-    }
-    switch (t) {
-    case FR: type[k] = DB; lb[k] = -1e3; ub[k] = +1e3; break;
-    case LO: type[k] = DB; lb[k] = 0.0; ub[k] = +1.0; break;
-    case UP: type[k] = DB; lb[k] = -1.0; ub[k] = 0.0; break;
-    default: type[k] = FX; lb[k] = 0.0; ub[k] = 0.0; break;
-    }
-}
-
-// set_orig_bnds (glpspx02.js:1361-1408) on the device: the original types
-// and bounds back in place, the status of every non-basic position from its
-// type and the sign of its reduced cost (the epilogue's form of the host
-// routine Spx::set_orig_bnds, which repeats it on the mirrors)
-__global__ void k_orig_bnds(int m, int n, const signed char *__restrict__ orig_type, const double *__restrict__ orig_lb,
-                            const double *__restrict__ orig_ub, const int *__restrict__ head,
-                            const double *__restrict__ cbar, signed char *__restrict__ type, double *__restrict__ lb,
-                            double *__restrict__ ub, signed char *__restrict__ stat, const DState *st, int need_p)
+// set_aux_bnds (glpspx02.js:1317-1359, aux = 1) or set_orig_bnds (:1361-1408,
+// aux = 0) on the device, from its own copy of the original types and
+// bounds and its reduced costs: the types and bounds of every variable and
+// the status of every non-basic position (the host repeats the same rules on
+// its mirrors: Spx::set_aux_bnds / set_orig_bnds).  Gated for the end-of-call
+// epilogue (epi_arm).
+__global__ void k_bounds(int m, int n, int aux, const signed char *__restrict__ orig_type,
+                         const double *__restrict__ orig_lb, const double *__restrict__ orig_ub,
+                         const int *__restrict__ head, const double *__restrict__ cbar, signed char *__restrict__ type,
+                         double *__restrict__ lb, double *__restrict__ ub, signed char *__restrict__ stat,
+                         const DState *st, int need_p)
 {
     GATE(st, need_p);
     const int k = blockIdx.x * blockDim.x + threadIdx.x;
     if (k < m + n) {
-        type[k] = orig_type[k];
-        lb[k] = orig_lb[k];
-        ub[k] = orig_ub[k];
+        const int t = orig_type[k];
+        if (!aux) {
+            type[k] = (signed char)t;
+            lb[k] = orig_lb[k];
+            ub[k] = orig_ub[k];
+        } else {
+            switch (t) {
+            case FR: type[k] = DB; lb[k] = -1e3; ub[k] = +1e3; break;
+            case LO: type[k] = DB; lb[k] = 0.0; ub[k] = +1.0; break;
+            case UP: type[k] = DB; lb[k] = -1.0; ub[k] = 0.0; break;
+            default: type[k] = FX; lb[k] = 0.0; ub[k] = 0.0; break;
+            }
+        }
     }
     if (k < n) {
         const int v = head[m + k] - 1;
+        const int t = orig_type[v];
         const double d = cbar[k];
         signed char sv;
-        switch (orig_type[v]) {
-        case FR: sv = NF; break;
-        case LO: sv = NL; break;
-        case UP: sv = NU; break;
-        case DB:
-            if (d >= +DBL_EPSILON) sv = NL;
-            else if (d <= -DBL_EPSILON) sv = NU;
-            else sv = (fabs(orig_lb[v]) <= fabs(orig_ub[v])) ? NL : NU;
-            break;
-        default: sv = NS; break;
+        if (aux) {
+            sv = (t != FR && t != LO && t != UP) ? NS : (d >= 0.0 ? NL : NU);
+        } else {
+            switch (t) {
+            case FR: sv = NF; break;
+            case LO: sv = NL; break;
+            case UP: sv = NU; break;
+            case DB:
+                if (d >= +DBL_EPSILON) sv = NL;
+                else if (d <= -DBL_EPSILON) sv = NU;
+                else sv = (fabs(orig_lb[v]) <= fabs(orig_ub[v])) ? NL : NU;
+                break;
+            default: sv = NS; break;
+            }
         }
         stat[k] = sv;
     }
@@ -1491,20 +1484,21 @@ struct Spx {
             type = orig_type; lb = orig_lb; ub = orig_ub;
         }
     }
-    // push_bounds, with the types and bounds written by the device from its
-    // original arrays (k_set_bounds) and the statuses uploaded
+    // push_bounds, with the types, bounds and statuses written by the device
+    // from its original arrays and its reduced costs (k_bounds: the device's
+    // cbar is the host's here — every caller evaluated it just before)
     void push_bounds_dev(int aux)
     {
         epi_drop();
         bbar_ok = false;
         const int mn = m + n;
-        hipLaunchKernelGGL(k_set_bounds, dim3((unsigned)((mn + 255) / 256)), dim3(256), 0, s, mn, aux, E->orig_type.p,
-                           E->orig_lb.p, E->orig_ub.p, E->type.p, E->lb.p, E->ub.p);
-        up(E->stat, stat, n);
+        hipLaunchKernelGGL(k_bounds, dim3((unsigned)((mn + 255) / 256)), dim3(256), 0, s, m, n, aux, E->orig_type.p,
+                           E->orig_lb.p, E->orig_ub.p, E->head.p, E->cbar.p, E->type.p, E->lb.p, E->ub.p, E->stat.p,
+                           (const DState *)nullptr, 0);
     }
     void set_orig_bnds()                                 // glpspx02.js:1361
     {
-        // (k_orig_bnds ran behind the batch, on the reduced costs the host
+        // (k_bounds ran behind the batch, on the reduced costs the host
         // now holds)
         const bool on_dev = epi.ready && epi.bounds_pending && !epi.has_cbar;
         restore_orig_arrays();
@@ -1671,46 +1665,39 @@ struct Spx {
         lp->obj_val = eval_obj();
         lp->it_cnt = hs.it_cnt;
         lp->some = ray;
-        for (int i = 1; i <= m; i++) {
-            int k = head[i];
-            if (k <= m) {
+        // by variable (the lp arrays written in order, each variable's
+        // position from bind): the values of glpspx01.js:1591-1681
+        for (int k = 1; k <= m; k++) {
+            const int pos = bind[k];
+            const double r = lp->rii[k];
+            if (pos <= m) {
                 lp->row_stat[k] = BS;
-                if (lp->row_bind) lp->row_bind[k] = i;
-                const double r = lp->rii[k];
-                lp->row_prim[k] = r == 1.0 ? bbar[i] : bbar[i] / r;        // (x / 1 == x)
+                if (lp->row_bind) lp->row_bind[k] = pos;
+                lp->row_prim[k] = r == 1.0 ? bbar[pos] : bbar[pos] / r;        // (x / 1 == x)
                 lp->row_dual[k] = 0.0;
             } else {
-                int c = k - m;
-                lp->col_stat[c] = BS;
-                if (lp->col_bind) lp->col_bind[c] = i;
-                lp->col_prim[c] = bbar[i] * lp->sjj[c];
-                lp->col_dual[c] = 0.0;
+                const int j = pos - m;
+                const int st = stat[j];
+                lp->row_stat[k] = (signed char)st;
+                if (lp->row_bind) lp->row_bind[k] = 0;
+                lp->row_prim[k] = st == NU ? lp->row_ub[k] : (st == NF ? 0.0 : lp->row_lb[k]);
+                lp->row_dual[k] = (r == 1.0 ? cbar[j] : cbar[j] * r) / zeta;
             }
         }
-        for (int j = 1; j <= n; j++) {
-            int k = head[m + j];
-            if (k <= m) {
-                lp->row_stat[k] = stat[j];
-                if (lp->row_bind) lp->row_bind[k] = 0;
-                switch (stat[j]) {
-                case NL: lp->row_prim[k] = lp->row_lb[k]; break;
-                case NU: lp->row_prim[k] = lp->row_ub[k]; break;
-                case NF: lp->row_prim[k] = 0.0; break;
-                default: lp->row_prim[k] = lp->row_lb[k]; break;
-                }
-                const double r = lp->rii[k];
-                lp->row_dual[k] = (r == 1.0 ? cbar[j] : cbar[j] * r) / zeta;
+        for (int c = 1; c <= n; c++) {
+            const int pos = bind[m + c];
+            const double q = lp->sjj[c];
+            if (pos <= m) {
+                lp->col_stat[c] = BS;
+                if (lp->col_bind) lp->col_bind[c] = pos;
+                lp->col_prim[c] = bbar[pos] * q;
+                lp->col_dual[c] = 0.0;
             } else {
-                int c = k - m;
-                lp->col_stat[c] = stat[j];
+                const int j = pos - m;
+                const int st = stat[j];
+                lp->col_stat[c] = (signed char)st;
                 if (lp->col_bind) lp->col_bind[c] = 0;
-                switch (stat[j]) {
-                case NL: lp->col_prim[c] = lp->col_lb[c]; break;
-                case NU: lp->col_prim[c] = lp->col_ub[c]; break;
-                case NF: lp->col_prim[c] = 0.0; break;
-                default: lp->col_prim[c] = lp->col_lb[c]; break;
-                }
-                const double q = lp->sjj[c];
+                lp->col_prim[c] = st == NU ? lp->col_ub[c] : (st == NF ? 0.0 : lp->col_lb[c]);
                 lp->col_dual[c] = (q == 1.0 ? cbar[j] : cbar[j] / q) / zeta;
             }
         }
@@ -2022,9 +2009,12 @@ void Spx::init()
     } else {
         // the non-basic variables are numbered as init_csa numbers them
         // (rows, then columns); the resident reduced costs follow them
-        cbar.assign(n + 1, 0.0);
+        // (renumbering on the device in one workgroup, k_canon, was measured
+        // 65 us per call slower than these uploads)
+        cbar.resize(n + 1);
+        cbar[0] = 0.0;
         for (int j = 1; j <= n; j++) cbar[j] = R.cbar[R.bind[head[m + j]] - m];
-        bbar = R.bbar;
+        bbar.swap(R.bbar);
         up(E->cbar, cbar, n);
     }
     up(E->head, head, mn - 1); up(E->bind, bind, mn - 1); up(E->stat, stat, n);
@@ -2156,7 +2146,7 @@ bool Spx::epi_arm(int K)
     eval_cbar_dev();
     if (phase == 1) {
         const size_t mn = (size_t)m + n;
-        hipLaunchKernelGGL(k_orig_bnds, dim3((unsigned)((mn + 255) / 256)), dim3(256), 0, s, m, n, E->orig_type.p,
+        hipLaunchKernelGGL(k_bounds, dim3((unsigned)((mn + 255) / 256)), dim3(256), 0, s, m, n, 0, E->orig_type.p,
                            E->orig_lb.p, E->orig_ub.p, E->head.p, E->cbar.p, E->type.p, E->lb.p, E->ub.p, E->stat.p, eg,
                            EPI_GATE);
     }
