@@ -165,6 +165,8 @@ struct Engine {
     DBuf<int> head, bind;
     DBuf<double> bbar, cbar, gamma, tcol, trow, rho, rowp, u, s, h, wcol, ys, work, r1, r2, partial;
     DBuf<DState> st;
+    DBuf<DState> stm;                       // the epilogue's copy of st, in front of the pull region
+    DBuf<int> eflags;                       // the epilogue's phase-I check_stab / check_feas results
     DState *st_host = nullptr;              // pinned staging copy of st (hipHostMalloc)
     char *pin = nullptr;                     // pinned staging of the per-call host <-> device copies
     size_t pin_cap = 0;
@@ -521,7 +523,9 @@ static void engine_alloc(Engine &E, int m, int n, gk_ctx *ctx)
             place(E.type, mn); place(E.orig_type, mn); place(E.refsp, mn);
             place(E.lb, mn); place(E.ub, mn); place(E.orig_lb, mn); place(E.orig_ub, mn);
             place(E.obj, n);
-            // what pull() brings back, contiguous: one copy
+            // what pull() brings back, contiguous: one copy (the epilogue's
+            // download starts at its copy of the state and check flags)
+            place(E.stm, 1); place(E.eflags, 2 * (((size_t)n + 255) / 256) + 4);
             place(E.head, mn); place(E.bind, mn); place(E.stat, n); place(E.bbar, m); place(E.cbar, n);
             place(E.coef, mn);
             place(E.gamma, std::max(m, n));
@@ -742,6 +746,55 @@ __global__ void k_bounds(int m, int n, int aux, const signed char *__restrict__ 
     }
 }
 
+// the state into its slot in front of the pull region (the epilogue's one
+// download covers both); not gated: the host reads the state either way
+__global__ void k_st_copy(const DState *__restrict__ st, DState *__restrict__ dst)
+{
+    const unsigned *a = (const unsigned *)st;
+    unsigned *b = (unsigned *)dst;
+    for (int i = threadIdx.x; i < (int)(sizeof(DState) / 4); i += blockDim.x) b[i] = a[i];
+}
+
+// the epilogue's phase-I tests on the fresh reduced costs and the statuses
+// the batch left: check_stab (glpspx02.js:1410) and check_feas (:1296), as
+// Spx::dual_check_stab_feas; block b writes its two flags to flags[2 b],
+// flags[2 b + 1] (the host ORs them after the download)
+__global__ void __launch_bounds__(256) k_epi_checks(int m, int n, const double *__restrict__ cbar,
+                                                    const signed char *__restrict__ stat, const int *__restrict__ head,
+                                                    const signed char *__restrict__ orig_type, double tol_dj,
+                                                    int *flags, const DState *st, int need_p)
+{
+    GATE(st, need_p);
+    __shared__ int red[2][4];
+    const int j = blockIdx.x * blockDim.x + threadIdx.x;
+    int stab = 0, inf = 0;
+    if (j < n) {
+        const double d = cbar[j];
+        const int s_ = stat[j];
+        const int t = orig_type[head[m + j] - 1];
+        if (d < -tol_dj) {
+            stab = (s_ == NL || s_ == NF);
+            inf = (t == LO || t == FR);
+        }
+        if (d > +tol_dj) {
+            stab |= (s_ == NU || s_ == NF);
+            inf |= (t == UP || t == FR);
+        }
+    }
+    stab = __any(stab);
+    inf = __any(inf);
+    const int w = threadIdx.x >> 6;
+    if ((threadIdx.x & 63) == 0) {
+        red[0][w] = stab;
+        red[1][w] = inf;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        flags[2 * blockIdx.x] = red[0][0] | red[0][1] | red[0][2] | red[0][3];
+        flags[2 * blockIdx.x + 1] = red[1][0] | red[1][1] | red[1][2] | red[1][3];
+    }
+}
+
 static double bits_double(unsigned long long b)
 {
     double v;
@@ -810,10 +863,11 @@ struct Spx {
         bool has_cbar = false, has_bbar = false;
         bool bounds_pending = false;       // phase I: set_orig_bnds ran on the device (bbar is under them)
         bool aux = false;                  // next_aux's evaluation launched too
-        std::vector<double> cbar, bbar;
-        std::vector<signed char> stat;
+        bool checks = false;               // phase I: check_stab / check_feas evaluated on the device
+        int stab = 0, feas = 0;
+        std::vector<signed char> stat;     // the statuses the epilogue's set_orig_bnds gave
     } epi;
-    void epi_drop() { epi.ready = epi.has_cbar = epi.has_bbar = epi.bounds_pending = epi.aux = false; }
+    void epi_drop() { epi.ready = epi.has_cbar = epi.has_bbar = epi.bounds_pending = epi.aux = epi.checks = false; }
 
     SpxDev dev() const
     {
@@ -1050,8 +1104,8 @@ struct Spx {
     {
         if (cbar_ok) { evals_skipped++; return; }
         if (epi.ready && epi.has_cbar) {
-            // the epilogue behind the last batch evaluated it (epi_arm)
-            cbar.swap(epi.cbar);
+            // the epilogue behind the last batch evaluated it (epi_arm; the
+            // mirror holds it)
             epi.has_cbar = false;
             cbar_ok = true;
             evals_skipped++;
@@ -1106,7 +1160,6 @@ struct Spx {
     {
         if (bbar_ok) { evals_skipped++; return; }
         if (epi.ready && epi.has_bbar && !epi.bounds_pending) {
-            bbar.swap(epi.bbar);
             epi.has_bbar = false;
             bbar_ok = true;
             evals_skipped++;
@@ -1806,7 +1859,7 @@ struct Spx {
     int batch(int K, int rigorous);
     bool epi_arm(int K);
     void epi_wait();
-    size_t epi_skip = (size_t)-1;
+    const char *epi_stage = nullptr;      // the epilogue's download in the staging ring
 };
 
 __global__ void k_rsub_plain(double *y, const double *a, int n, const DState *st, int need_p)
@@ -2136,41 +2189,34 @@ bool Spx::epi_arm(int K)
     MatDev A = E->mat();
     const int nrmax = std::min(m, hs.nr + K);      // one dense column of inv(B) more or less per pivot
     if (!A.AT || !lists_ok() || nrmax > LIST_FTRAN_MAX || 2 * nrmax > m) return false;
+    // (a progress line at the limit reads the batch's updated values, which
+    // the epilogue replaces before the one download)
+    if (f->rpt && parm->msg_lev >= 2) return false;
+    const size_t region = (size_t)((const char *)(E->cbar.p + n) - (const char *)E->stm.p);
+    char *stage = pin_take(region);
+    if (!stage) return false;
     if (!E->epi_ev) HIPCHK(hipEventCreateWithFlags(&E->epi_ev, hipEventDisableTiming));
-    // the state and the mirrors as the batch leaves them (pull_state, pull)
-    HIPCHK(hipMemcpyAsync(E->st_host, E->st.p, sizeof(DState), hipMemcpyDeviceToHost, s));
-    pull_enqueue();
-    epi_skip = pending.size() - 1;          // the updated cbar: superseded when the epilogue runs
     eg = E->st.p;
     eg_nr = nrmax;
     eval_cbar_dev();
     if (phase == 1) {
+        // check_stab / check_feas on the fresh reduced costs and the batch's
+        // statuses, before set_orig_bnds replaces them
+        hipLaunchKernelGGL(k_epi_checks, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, m, n, E->cbar.p, E->stat.p,
+                           E->head.p, E->orig_type.p, parm->tol_dj, E->eflags.p, eg, EPI_GATE);
         const size_t mn = (size_t)m + n;
         hipLaunchKernelGGL(k_bounds, dim3((unsigned)((mn + 255) / 256)), dim3(256), 0, s, m, n, 0, E->orig_type.p,
                            E->orig_lb.p, E->orig_ub.p, E->head.p, E->cbar.p, E->type.p, E->lb.p, E->ub.p, E->stat.p, eg,
                            EPI_GATE);
     }
     eval_bbar_into(dev(), E->bbar.p);
-    epi.cbar.resize((size_t)n + 1);
-    epi.bbar.resize((size_t)m + 1);
-    epi.stat.resize((size_t)n + 1);
-    epi.cbar[0] = epi.bbar[0] = 0.0;
-    epi.stat[0] = stat[0];
-    {
-        // stat | bbar | cbar lie contiguous in the arena (pull): one copy
-        const char *lo = (const char *)E->stat.p, *hi = (const char *)(E->cbar.p + n);
-        char *stage = pin_take((size_t)(hi - lo));
-        if (!stage) {
-            down(epi.cbar, E->cbar, n);
-            down(epi.bbar, E->bbar, m);
-            down(epi.stat, E->stat, n);
-        } else {
-            HIPCHK(hipMemcpyAsync(stage, lo, (size_t)(hi - lo), hipMemcpyDeviceToHost, s));
-            pending.push_back(Pending{epi.stat.data() + 1, stage, (size_t)n});
-            pending.push_back(Pending{epi.bbar.data() + 1, stage + ((const char *)E->bbar.p - lo), (size_t)m * sizeof(double)});
-            pending.push_back(Pending{epi.cbar.data() + 1, stage + ((const char *)E->cbar.p - lo), (size_t)n * sizeof(double)});
-        }
-    }
+    // one download: the state, the check flags and head | bind | stat |
+    // bbar | cbar — the batch's values when it stopped early (the epilogue
+    // did nothing), the epilogue's otherwise (head and bind are the batch's
+    // either way); epi_wait sorts them out
+    hipLaunchKernelGGL(k_st_copy, dim3(1), dim3(64), 0, s, E->st.p, E->stm.p);
+    HIPCHK(hipMemcpyAsync(stage, E->stm.p, region, hipMemcpyDeviceToHost, s));
+    epi_stage = stage;
     HIPCHK(hipEventRecord(E->epi_ev, s));
     // the next call's phase-I values (next_aux_launch) behind the wait point
     static const bool aux_on = [] {
@@ -2182,6 +2228,7 @@ bool Spx::epi_arm(int K)
     eg = nullptr;
     epi.has_cbar = epi.has_bbar = true;
     epi.bounds_pending = (phase == 1);
+    epi.checks = (phase == 1);
     return true;
 }
 
@@ -2189,13 +2236,33 @@ void Spx::epi_wait()
 {
     HIPCHK(hipEventSynchronize(E->epi_ev));
     f->stats.host_syncs++;
-    hs = *E->st_host;
-    // (a batch that used its budget: eval_cbar takes the epilogue's cbar up
-    // before anything reads the mirror)
-    const size_t skip = hs.stop <= ST_BATCH ? epi_skip : (size_t)-1;
-    for (size_t i = 0; i < pending.size(); i++)
-        if (i != skip) std::memcpy(pending[i].dst, pending[i].src, pending[i].bytes);
+    for (const Pending &q : pending) std::memcpy(q.dst, q.src, q.bytes);
     pending.clear();
+    const char *lo = (const char *)E->stm.p;
+    auto at = [&](const void *dev) { return epi_stage + ((const char *)dev - lo); };
+    std::memcpy(&hs, epi_stage, sizeof(DState));
+    std::memcpy(head.data() + 1, at(E->head.p), ((size_t)m + n) * sizeof(int));
+    std::memcpy(bind.data() + 1, at(E->bind.p), ((size_t)m + n) * sizeof(int));
+    std::memcpy(stat.data() + 1, at(E->stat.p), (size_t)n);
+    std::memcpy(bbar.data() + 1, at(E->bbar.p), (size_t)m * sizeof(double));
+    std::memcpy(cbar.data() + 1, at(E->cbar.p), (size_t)n * sizeof(double));
+    if (hs.stop <= ST_BATCH) {
+        // the epilogue ran: the mirrors hold its values (eval_cbar, phase
+        // I's set_orig_bnds and eval_beta), which the host sequence takes up
+        // in its own order (eval_cbar, set_orig_bnds, eval_bbar); the checks
+        // on the batch's statuses came from the device (eflags)
+        epi.stat.assign(stat.begin(), stat.end());
+        if (epi.checks) {
+            const int *fl = (const int *)at(E->eflags.p);
+            int sf = 0, ff = 0;
+            for (int b = 0; b < (n + 255) / 256; b++) {
+                sf |= fl[2 * b];
+                ff |= fl[2 * b + 1];
+            }
+            epi.stab = sf;
+            epi.feas = ff;
+        }
+    }
     pin_off = 0;
 }
 
@@ -2488,7 +2555,13 @@ int Spx::run_dual()
             // gives check_feas (:1296), which the phase-I test below takes
             int stab_fail = 0;
             if (sel_aux) stab_fail = 0;
-            else if (phase == 1) stab_fail = dual_check_stab_feas(P->tol_dj, &feas_pre);
+            else if (phase == 1 && epi.ready && epi.checks && !epi.has_cbar) {
+                // (the epilogue's checks: the cbar just taken up and the
+                // statuses the batch left)
+                stab_fail = epi.stab;
+                feas_pre = epi.feas;
+                epi.checks = false;
+            } else if (phase == 1) stab_fail = dual_check_stab_feas(P->tol_dj, &feas_pre);
             else stab_fail = dual_check_stab(P->tol_dj);
             mark("stab checked");
             if (stab_fail != 0) {
