@@ -3152,8 +3152,12 @@ static __host__ __device__ __forceinline__ int rowpass_waves(int cnt) { return c
 
 __global__ void __launch_bounds__(1024) k_rowpass_pi(SpxDev d, int mode, int nr, const double *__restrict__ pi,
                                                      const double *__restrict__ h, double *__restrict__ out,
-                                                     const int *__restrict__ extra, int nextra, const DState *eg)
+                                                     const int *__restrict__ extra, int nextra, const DState *eg,
+                                                     const double *__restrict__ pi2)
 {
+    // (pi2: the multipliers are pi + pi2, eval_pi's refinement step taken
+    // here instead of by an axpy)
+    auto PI = [&](int c) { return pi2 ? pi[c] + pi2[c] : pi[c]; };
     __shared__ double sp[16][64];
     const int m = d.m, n = d.n;
     const int lane = threadIdx.x & 63;
@@ -3176,7 +3180,7 @@ __global__ void __launch_bounds__(1024) k_rowpass_pi(SpxDev d, int mode, int nr,
         for (int u = 0; u < 4; ++u) c[u] = d.rlist[t + u * nw];
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
-            v[u] = pi[c[u]];
+            v[u] = PI(c[u]);
             a[u] = col[(size_t)c[u] * ldt];
         }
 #pragma unroll
@@ -3184,11 +3188,11 @@ __global__ void __launch_bounds__(1024) k_rowpass_pi(SpxDev d, int mode, int nr,
     }
     for (; t < nr; t += nw) {
         const int c = d.rlist[t];
-        acc += pi[c] * col[(size_t)c * ldt];
+        acc += PI(c) * col[(size_t)c * ldt];
     }
     for (t = w < nw ? w : nextra; t < nextra; t += nw) {        // basic slacks with a cost (primal phase I)
         const int c = extra[t];
-        acc += pi[c] * col[(size_t)c * ldt];
+        acc += PI(c) * col[(size_t)c * ldt];
     }
     sp[w][lane] = acc;
     __syncthreads();
@@ -3202,17 +3206,17 @@ __global__ void __launch_bounds__(1024) k_rowpass_pi(SpxDev d, int mode, int nr,
     }
     if (idx < m) {
         const int pos = d.bind[idx];
-        if (mode == CP_CBAR && pos > m) out[pos - m - 1] = d.coef[idx] - pi[idx];
-        if (mode == CP_RESID && pos <= m) out[pos - 1] = h[pos - 1] - pi[idx];
+        if (mode == CP_CBAR && pos > m) out[pos - m - 1] = d.coef[idx] - PI(idx);
+        if (mode == CP_RESID && pos <= m) out[pos - 1] = h[pos - 1] - PI(idx);
     }
 }
 
 void rowpass_pi(hipStream_t s, const SpxDev &d, int mode, int nr, const double *pi, const double *h, double *out,
-                const int *extra, int nextra, const DState *eg)
+                const int *extra, int nextra, const DState *eg, const double *pi2)
 {
     const int nw = eg ? 16 : rowpass_waves(nr + nextra);
     hipLaunchKernelGGL(k_rowpass_pi, dim3(cdiv(std::max(d.m, d.n), 64)), dim3(64 * nw), 0, s, d, mode, nr, pi, h,
-                       out, extra, nextra, eg);
+                       out, extra, nextra, eg, pi2);
 }
 
 void binv_btran_list(hipStream_t s, const SpxDev &d, int nr, const double *x, double *y, const DState *eg)

@@ -525,7 +525,7 @@ static void engine_alloc(Engine &E, int m, int n, gk_ctx *ctx)
             place(E.obj, n);
             // what pull() brings back, contiguous: one copy (the epilogue's
             // download starts at its copy of the state and check flags)
-            place(E.stm, 1); place(E.eflags, 2 * (((size_t)n + 255) / 256) + 4);
+            place(E.stm, 1); place(E.eflags, 2 * ((mn + 255) / 256) + 4);
             place(E.head, mn); place(E.bind, mn); place(E.stat, n); place(E.bbar, m); place(E.cbar, n);
             place(E.coef, mn);
             place(E.gamma, std::max(m, n));
@@ -755,31 +755,62 @@ __global__ void k_st_copy(const DState *__restrict__ st, DState *__restrict__ ds
     for (int i = threadIdx.x; i < (int)(sizeof(DState) / 4); i += blockDim.x) b[i] = a[i];
 }
 
-// the epilogue's phase-I tests on the fresh reduced costs and the statuses
-// the batch left: check_stab (glpspx02.js:1410) and check_feas (:1296), as
-// Spx::dual_check_stab_feas; block b writes its two flags to flags[2 b],
-// flags[2 b + 1] (the host ORs them after the download)
-__global__ void __launch_bounds__(256) k_epi_checks(int m, int n, const double *__restrict__ cbar,
-                                                    const signed char *__restrict__ stat, const int *__restrict__ head,
-                                                    const signed char *__restrict__ orig_type, double tol_dj,
-                                                    int *flags, const DState *st, int need_p)
+// The phase-I epilogue's step between eval_cbar and eval_beta, one thread
+// per variable k: check_stab (glpspx02.js:1410) and check_feas (:1296) of the
+// fresh reduced cost at k's non-basic position against the status the batch
+// left (block b's two flags to flags[2 b], flags[2 b + 1], ORed by the host),
+// set_orig_bnds (:1361) for k (k_bounds' rules: type, bounds, status), and
+// eval_beta's right-hand side split (k_split_pos mode 0: ys / wc from the new
+// status and bounds) — three launches' work in one
+__global__ void __launch_bounds__(256) k_epi_orig(int m, int n, const signed char *__restrict__ orig_type,
+                                                  const double *__restrict__ orig_lb, const double *__restrict__ orig_ub,
+                                                  const int *__restrict__ bind, const double *__restrict__ cbar,
+                                                  signed char *__restrict__ type, double *__restrict__ lb,
+                                                  double *__restrict__ ub, signed char *__restrict__ stat,
+                                                  double *__restrict__ ys, double *__restrict__ wc, double tol_dj,
+                                                  int *flags, const DState *st, int need_p)
 {
     GATE(st, need_p);
     __shared__ int red[2][4];
-    const int j = blockIdx.x * blockDim.x + threadIdx.x;
+    const int k = blockIdx.x * blockDim.x + threadIdx.x;      // variable k + 1
     int stab = 0, inf = 0;
-    if (j < n) {
-        const double d = cbar[j];
-        const int s_ = stat[j];
-        const int t = orig_type[head[m + j] - 1];
-        if (d < -tol_dj) {
-            stab = (s_ == NL || s_ == NF);
-            inf = (t == LO || t == FR);
+    if (k < m + n) {
+        const int t = orig_type[k];
+        const double l = orig_lb[k], u = orig_ub[k];
+        type[k] = (signed char)t;
+        lb[k] = l;
+        ub[k] = u;
+        const int pos = bind[k];
+        double v = 0.0;
+        if (pos > m) {
+            const int j = pos - m - 1;
+            const double d = cbar[j];
+            const int s0 = stat[j];
+            if (d < -tol_dj) {
+                stab = (s0 == NL || s0 == NF);
+                inf = (t == LO || t == FR);
+            }
+            if (d > +tol_dj) {
+                stab |= (s0 == NU || s0 == NF);
+                inf |= (t == UP || t == FR);
+            }
+            int sv;
+            switch (t) {
+            case FR: sv = NF; break;
+            case LO: sv = NL; break;
+            case UP: sv = NU; break;
+            case DB:
+                if (d >= +DBL_EPSILON) sv = NL;
+                else if (d <= -DBL_EPSILON) sv = NU;
+                else sv = (fabs(l) <= fabs(u)) ? NL : NU;
+                break;
+            default: sv = NS; break;
+            }
+            stat[j] = (signed char)sv;
+            v = -(sv == NU ? u : (sv == NF ? 0.0 : l));         // -get_xN
         }
-        if (d > +tol_dj) {
-            stab |= (s_ == NU || s_ == NF);
-            inf |= (t == UP || t == FR);
-        }
+        if (k < m) ys[k] = v;
+        else wc[k - m] = v;
     }
     stab = __any(stab);
     inf = __any(inf);
@@ -1149,9 +1180,13 @@ struct Spx {
         if (rows) rowpass_pi(s, d, CP_RESID, nrb, pi, cB, r, E->xlist.p, nx, eg);
         else colpass(s, A, CP_RESID, 0, m, E->head.p, E->stat.p, E->coef.p, cB, pi, nullptr, r, nullptr, nullptr);
         btran_(r, dd);
-        vec_axpy(s, pi, dd, 1.0, m, eg, eg ? EPI_GATE : 0);
-        if (rows) rowpass_pi(s, d, CP_CBAR, nrb, pi, nullptr, E->cbar.p, E->xlist.p, nx, eg);
-        else colpass(s, A, CP_CBAR, m, n, E->head.p, E->stat.p, E->coef.p, nullptr, pi, nullptr, E->cbar.p, nullptr, nullptr);
+        if (rows) {
+            // pi += dd (the refinement) inside the pass
+            rowpass_pi(s, d, CP_CBAR, nrb, pi, nullptr, E->cbar.p, E->xlist.p, nx, eg, dd);
+        } else {
+            vec_axpy(s, pi, dd, 1.0, m, eg, eg ? EPI_GATE : 0);
+            colpass(s, A, CP_CBAR, m, n, E->head.p, E->stat.p, E->coef.p, nullptr, pi, nullptr, E->cbar.p, nullptr, nullptr);
+        }
     }
 
     // eval_beta (glpspx01.js:473): h = -N xN; beta = inv(B) h, refined once
@@ -1187,12 +1222,13 @@ struct Spx {
         mark("eval_bbar done");
     }
     // h = -N xN over the statuses and bounds of d; beta = inv(B) h, refined once
-    void eval_bbar_into(const SpxDev &d, double *beta)
+    // (split_done: ys / wc of the right-hand side are in place — k_epi_orig)
+    void eval_bbar_into(const SpxDev &d, double *beta, bool split_done = false)
     {
         MatDev A = E->mat();
         double *ys = E->r1.p, *wc = E->wcol.p, *h = E->h.p, *t = E->r2.p, *dd = E->work.p;
         const int gm = eg ? EPI_GATE : 0;
-        split_pos(s, d, 0, nullptr, ys, wc, eg, gm);
+        if (!split_done) split_pos(s, d, 0, nullptr, ys, wc, eg, gm);
         aprod_neg_gated(s, A, wc, ys, h, E->partial.p, PARTIAL_CAP, eg, gm);    // h = ys - A wc
         ftran_(h, beta);
         split_pos(s, d, 1, beta, ys, wc, eg, gm);
@@ -2201,15 +2237,13 @@ bool Spx::epi_arm(int K)
     eval_cbar_dev();
     if (phase == 1) {
         // check_stab / check_feas on the fresh reduced costs and the batch's
-        // statuses, before set_orig_bnds replaces them
-        hipLaunchKernelGGL(k_epi_checks, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, m, n, E->cbar.p, E->stat.p,
-                           E->head.p, E->orig_type.p, parm->tol_dj, E->eflags.p, eg, EPI_GATE);
+        // statuses, set_orig_bnds, and eval_beta's right-hand side split
         const size_t mn = (size_t)m + n;
-        hipLaunchKernelGGL(k_bounds, dim3((unsigned)((mn + 255) / 256)), dim3(256), 0, s, m, n, 0, E->orig_type.p,
-                           E->orig_lb.p, E->orig_ub.p, E->head.p, E->cbar.p, E->type.p, E->lb.p, E->ub.p, E->stat.p, eg,
-                           EPI_GATE);
+        hipLaunchKernelGGL(k_epi_orig, dim3((unsigned)((mn + 255) / 256)), dim3(256), 0, s, m, n, E->orig_type.p,
+                           E->orig_lb.p, E->orig_ub.p, E->bind.p, E->cbar.p, E->type.p, E->lb.p, E->ub.p, E->stat.p,
+                           E->r1.p, E->wcol.p, parm->tol_dj, E->eflags.p, eg, EPI_GATE);
     }
-    eval_bbar_into(dev(), E->bbar.p);
+    eval_bbar_into(dev(), E->bbar.p, phase == 1);
     // one download: the state, the check flags and head | bind | stat |
     // bbar | cbar — the batch's values when it stopped early (the epilogue
     // did nothing), the epilogue's otherwise (head and bind are the batch's
@@ -2255,7 +2289,7 @@ void Spx::epi_wait()
         if (epi.checks) {
             const int *fl = (const int *)at(E->eflags.p);
             int sf = 0, ff = 0;
-            for (int b = 0; b < (n + 255) / 256; b++) {
+            for (int b = 0; b < (m + n + 255) / 256; b++) {
                 sf |= fl[2 * b];
                 ff |= fl[2 * b + 1];
             }

@@ -303,7 +303,7 @@ void scatter_segments(hipStream_t s, const char *src, const UpSeg *segs, int nse
 // (eg: the epilogue's form — gated on eg, nr read from eg->nr, the argument
 // an upper bound of it; the same sums in the same order)
 void rowpass_pi(hipStream_t s, const SpxDev &d, int mode, int nr, const double *pi, const double *h, double *out,
-                const int *extra, int nextra, const DState *eg = nullptr);
+                const int *extra, int nextra, const DState *eg = nullptr, const double *pi2 = nullptr);
 // MFMA panel pricing (gk_panel.hip), column-pass path on dense A: the chosen
 // row from the panel (refilled on a miss) in place of the column pass, and
 // the panel's update after the commit; panel_wanted: the plan's panel size
