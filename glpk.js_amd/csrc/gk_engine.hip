@@ -1444,12 +1444,28 @@ struct Spx {
     // refactorization (sp_ahead_install).  The start is a pivot count, not a
     // time, so the path stays deterministic; the default covers a host LU of
     // ~40 ms (m = 100k) at ~1,000 pivots/s and costs ~32 replayed FTRANs
-    void ahead_maybe()
+    static int ahead_lead()
     {
         static const int lead = [] {
             const char *e = std::getenv("GK_SP_AHEAD");
             return e ? std::atoi(e) : 32;
         }();
+        return lead;
+    }
+    // a batch that would run past the look-ahead's starting point ends
+    // there, so that the host LU gets the whole lead (batches of up to 64
+    // pivots otherwise started it as few as 8 pivots before the limit)
+    int ahead_align(int K) const
+    {
+        const int lead = ahead_lead();
+        if (!f->sparse || lead <= 0 || m < 50000 || !f->valid || sp_ahead_mark(*f->sp) >= 0 || hs.upd_lim < 2 * lead)
+            return K;
+        const int left = hs.upd_lim - lead - hs.upd_cnt;
+        return (left > 0 && left < K) ? left : K;
+    }
+    void ahead_maybe()
+    {
+        const int lead = ahead_lead();
         // (below m = 50,000 the host LU takes a few ms: replaying the lead's
         // FTRANs would cost more than it hides)
         if (lead <= 0 || m < 50000 || !f->valid || sp_ahead_mark(*f->sp) >= 0 || hs.npiv == 0 || hs.refact_pending)
@@ -2720,6 +2736,7 @@ int Spx::run_dual()
             K = (!rigorous && K >= 64 && rem <= 128) ? rem : std::max(1, std::min(K, rem));
         }
         K = align_to_refactor(K, hs.upd_lim - hs.upd_cnt);
+        K = ahead_align(K);
         K = align_to_display(K);
         int why = batch(K, rigorous);
         if (f->sparse) ahead_maybe();
@@ -2885,6 +2902,7 @@ int Spx::run_primal()
             K = (!rigorous && K >= 64 && rem <= 128) ? rem : std::max(1, std::min(K, rem));
         }
         K = align_to_refactor(K, hs.upd_lim - hs.upd_cnt);
+        K = ahead_align(K);
         K = align_to_display(K);
         int why = batch(K, rigorous);
         if (f->sparse) ahead_maybe();
