@@ -1452,13 +1452,22 @@ struct Spx {
         }();
         return lead;
     }
+    static int ahead_min_m()                 // GK_SP_AHEAD_MIN_M: the smallest m the look-ahead runs at
+    {
+        static const int v = [] {
+            const char *e = std::getenv("GK_SP_AHEAD_MIN_M");
+            return e ? std::atoi(e) : 50000;
+        }();
+        return v;
+    }
     // a batch that would run past the look-ahead's starting point ends
     // there, so that the host LU gets the whole lead (batches of up to 64
     // pivots otherwise started it as few as 8 pivots before the limit)
     int ahead_align(int K) const
     {
         const int lead = ahead_lead();
-        if (!f->sparse || lead <= 0 || m < 50000 || !f->valid || sp_ahead_mark(*f->sp) >= 0 || hs.upd_lim < 2 * lead)
+        if (!f->sparse || lead <= 0 || m < ahead_min_m() || !f->valid || sp_ahead_mark(*f->sp) >= 0 ||
+            hs.upd_lim < 2 * lead)
             return K;
         const int left = hs.upd_lim - lead - hs.upd_cnt;
         return (left > 0 && left < K) ? left : K;
@@ -1468,7 +1477,8 @@ struct Spx {
         const int lead = ahead_lead();
         // (below m = 50,000 the host LU takes a few ms: replaying the lead's
         // FTRANs would cost more than it hides)
-        if (lead <= 0 || m < 50000 || !f->valid || sp_ahead_mark(*f->sp) >= 0 || hs.npiv == 0 || hs.refact_pending)
+        if (lead <= 0 || m < ahead_min_m() || !f->valid || sp_ahead_mark(*f->sp) >= 0 || hs.npiv == 0 ||
+            hs.refact_pending)
             return;
         if (hs.upd_lim < 2 * lead || hs.upd_cnt >= hs.upd_lim || hs.upd_cnt < hs.upd_lim - lead) return;
         pull();
