@@ -14,6 +14,7 @@ module pads them.
 from __future__ import annotations
 
 import ctypes as C
+import operator
 import os
 
 import numpy as np
@@ -406,24 +407,28 @@ class GkProblem:
                   "A_ptr", "A_ind", "A_val", "head", "row_stat", "col_stat", "row_bind", "col_bind",
                   "row_prim", "row_dual", "col_prim", "col_dual")
 
+    _LP_GET = operator.itemgetter(*_LP_ARRAYS)
+
     def _lp_struct(self) -> Lp:
-        # the array pointers are cached per array object (a numpy array's
-        # data never moves; an attribute rebound to another array is seen by
-        # the identity test): a fresh ctypes pointer per field and call cost
-        # ~0.1 ms per glp_simplex call, ~2.5 % of a C3 it_lim=100 step
+        # the struct and its array pointers are kept while every array
+        # attribute is the same object (a numpy array's data never moves; an
+        # attribute rebound to another array fails the identity test): a
+        # fresh ctypes pointer per field and call cost ~0.1 ms per
+        # glp_simplex call, ~2.5 % of a C3 it_lim=100 step
         cache = self.__dict__.setdefault("_ptr_cache", {})
-        lp = Lp()
+        arrs = GkProblem._LP_GET(self.__dict__)
+        lp = cache.get("lp")
+        if lp is None or not all(map(operator.is_, arrs, cache["arrs"])):
+            lp = Lp()
+            for name, arr in zip(self._LP_ARRAYS, arrs):
+                setattr(lp, name, arr.ctypes.data)
+            cache["lp"], cache["arrs"] = lp, arrs
         lp.m, lp.n, lp.nnz, lp.dir, lp.c0 = self.m, self.n, self.nnz, self.dir, self.c0
-        for name in self._LP_ARRAYS:
-            arr = self.__dict__[name]
-            ent = cache.get(name)
-            if ent is None or ent[0] is not arr:
-                ent = (arr, arr.ctypes.data)
-                cache[name] = ent
-            setattr(lp, name, ent[1])
         lp.a_version = self.a_version
         lp.b_version = self.b_version
         lp.it_cnt = self.it_cnt
+        lp.pbs_stat = lp.dbs_stat = lp.some = lp.valid = 0     # (outputs: as a fresh struct)
+        lp.obj_val = 0.0
         return lp
 
     def _take(self, lp: Lp):
