@@ -936,6 +936,13 @@ __global__ void __launch_bounds__(1024) k_dual_row(SpxDev d, int pse, int nr_cap
     for (int u = 0; u < NP; ++u) c0[u] = d.rlist[min(w + u * nw, m - 1)];
     int pos1 = d.bind[m + min(idx, n - 1)];
     int pos2 = d.bind[min(idx, m - 1)];
+    // the wave's rows of AT depend on the list alone: issued now, in flight
+    // while the chuzr choice below resolves (the rho entries wait for it)
+    const double *__restrict__ col = d.A.AT + min(idx, n - 1);
+    const size_t ldt = (size_t)d.A.ldt;
+    double a0[NP];
+#pragma unroll
+    for (int u = 0; u < NP; ++u) a0[u] = col[(size_t)min(max(c0[u], 0), m - 1) * ldt];
     Cand cc = no_cand(0.0);
 #pragma unroll
     for (int u = 0; u < 4; ++u)
@@ -1002,18 +1009,20 @@ __global__ void __launch_bounds__(1024) k_dual_row(SpxDev d, int pse, int nr_cap
     // ---- trip 2: rho entries of the wave and their rows of AT; slot operands
     const double *__restrict__ brow = d.Binv + (p - 1);
     const size_t ldb = (size_t)d.ldb;
-    const double *__restrict__ col = d.A.AT + min(idx, n - 1);
-    const size_t ldt = (size_t)d.A.ldt;
-    double v0[NP], a0[NP];
+    double v0[NP];
 #pragma unroll
     for (int u = 0; u < NP; ++u) {
         const int t = w + u * nw;
         int c = c0[u];
-        if (t == nr) c = kp - 1;             // the unit entry (only when kp <= m: t < ns)
+        double av = a0[u];
+        if (t == nr) {                       // the unit entry (only when kp <= m: t < ns)
+            c = kp - 1;
+            av = col[(size_t)min(max(c, 0), m - 1) * ldt];
+        }
         // list entries past nr are stale (or never written): clamp the
         // address, the value is not used
         const int ca = min(max(c, 0), m - 1);
-        const double bv = brow[(size_t)ca * ldb], av = col[(size_t)ca * ldt];
+        const double bv = brow[(size_t)ca * ldb];
         v0[u] = (t < nr) ? bv : 1.0;
         a0[u] = (t < ns) ? av : 0.0;
         c0[u] = c;
