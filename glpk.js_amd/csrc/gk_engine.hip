@@ -2242,10 +2242,8 @@ void Spx::init()
 // GK_EPILOGUE=0 turns it off.
 bool Spx::epi_arm(int K)
 {
-    static const bool on = [] {
-        const char *e = std::getenv("GK_EPILOGUE");
-        return !e || std::atoi(e) != 0;
-    }();
+    const char *ev = std::getenv("GK_EPILOGUE");          // (read per call: tests switch it)
+    const bool on = !ev || std::atoi(ev) != 0;
     if (!on || !dual || !E->dense || f->sparse || E->prof || (phase != 1 && phase != 2)) return false;
     if (parm->it_lim >= 0x7fffffff || hs.it_cnt - it_beg + K < parm->it_lim) return false;
     MatDev A = E->mat();
@@ -2279,10 +2277,8 @@ bool Spx::epi_arm(int K)
     epi_stage = stage;
     HIPCHK(hipEventRecord(E->epi_ev, s));
     // the next call's phase-I values (next_aux_launch) behind the wait point
-    static const bool aux_on = [] {
-        const char *e = std::getenv("GK_NEXT_AUX");
-        return !e || std::atoi(e) != 0;
-    }();
+    const char *ea = std::getenv("GK_NEXT_AUX");
+    const bool aux_on = !ea || std::atoi(ea) != 0;
     epi.aux = (phase == 1 && aux_on);
     if (epi.aux) next_aux_dev();
     eg = nullptr;

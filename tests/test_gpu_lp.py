@@ -298,3 +298,41 @@ def test_gpu_bounds_version_fast_init_bit_identical(gpu_ctx):
             trace.append((ret, P.it_cnt, P.obj_val, bytes(P.row_stat), bytes(P.col_stat)))
         outs.append(trace)
     assert outs[0] == outs[1]
+
+
+def test_gpu_end_of_call_epilogue_bit_identical(gpu_ctx, monkeypatch):
+    """The end-of-call epilogue (gk_engine.hip Spx::epi_arm, DESIGN §5): the
+    evaluations an it_lim call ends with, enqueued behind its last batch and
+    gated on the batch's budget, give bit for bit the states of the host
+    sequence (GK_EPILOGUE=0): a 1024 x 4096 chain through phase I with a bound
+    changed in the middle and re-inversions inside calls, and a 512 x 2048
+    chain to the optimum (batches that stop early leave the gated kernels
+    doing nothing)."""
+    def chain(prob, on, calls, change):
+        monkeypatch.setenv("GK_EPILOGUE", "1" if on else "0")
+        P = gk.GkProblem(gpu_ctx, prob)
+        out, ret = [], 8
+        for k in range(calls):
+            if k == change:
+                P.col_ub[7] = P.col_ub[7] + 0.5 if P.col_ub[7] < 1e30 else 10.0
+            ret = gk.glp_simplex(P, gk.SMCP(meth=gk.GLP_DUAL, it_lim=100, msg_lev=gk.GLP_MSG_ERR))
+            out.append((ret, P.it_cnt, float(P.obj_val).hex(), P.row_prim[1:].tobytes(), P.col_prim[1:].tobytes(),
+                        P.row_dual[1:].tobytes(), P.col_dual[1:].tobytes(), bytes(P.row_stat[1:]),
+                        bytes(P.col_stat[1:])))
+            if ret != 8:
+                break
+        return out, ret
+
+    big = problems.gen_dense(1024, 4096, seed=42)
+    on, _ = chain(big, True, 60, 30)
+    off, _ = chain(big, False, 60, 30)
+    assert len(on) == len(off) == 60
+    for k, (a, b) in enumerate(zip(on, off)):
+        assert a == b, f"1024 x 4096, call {k} differs"
+    small = problems.gen_dense(512, 2048, seed=7)          # 187 calls, 18,607 pivots to the optimum
+    on, ret_on = chain(small, True, 400, -1)
+    off, ret_off = chain(small, False, 400, -1)
+    assert ret_on == ret_off == 0
+    assert len(on) == len(off) > 100
+    for k, (a, b) in enumerate(zip(on, off)):
+        assert a == b, f"512 x 2048, call {k} differs"
