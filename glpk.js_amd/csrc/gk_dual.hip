@@ -2153,7 +2153,7 @@ __global__ void __launch_bounds__(256) k_dual_commit(SpxDev d, int pse, int nvb,
     if (r >= m) return;
     const bool two = (r + 1 < m);
     const double tr0 = d.tcol[r], tr1 = two ? d.tcol[r + 1] : 0.0;
-    constexpr int U = 4;
+    constexpr int U = 16;
     int cc[U];
     double rl[U];
 #pragma unroll
