@@ -210,24 +210,35 @@ __global__ void __launch_bounds__(256) k_panel_trow(SpxDev d)
 // the panel follow the rows of inv(B) (k_dual_commit's rank-1 update)
 __global__ void __launch_bounds__(256) k_panel_update(SpxDev d)
 {
+    // block (x, t): row t != pcur of the panel at the columns of block x —
+    // one read-modify-write per thread, every row at once (a thread walking
+    // the rows did one dependent memory round trip per row); row pcur, which
+    // the others read, is replaced by k_panel_update_cur after them
     const DState *st = d.st;
     if (st->stop || !st->pend) return;
-    const int pk = st->pk, cur = st->pcur;
+    const int pk = st->pk, cur = st->pcur, t = blockIdx.y;
     const double tp = st->pivot;
     const int n = d.n;
     const int j = blockIdx.x * 256 + threadIdx.x;
-    if (j == 0) d.st->page = st->page + 1;
-    if (j >= n) return;
+    if (t >= pk || t == cur || j >= n) return;
     const size_t ldp = (size_t)d.ldp;
     const double gp = d.pnl[(size_t)cur * ldp + j];
-    for (int t = 0; t < pk; ++t) {
-        double *g = d.pnl + (size_t)t * ldp + j;
-        if (t == cur) *g = -gp / tp;
-        else {
-            const double f = d.tcol[d.ppos[t] - 1] / tp;
-            if (f != 0.0) *g -= f * gp;
-        }
-    }
+    double *g = d.pnl + (size_t)t * ldp + j;
+    const double f = d.tcol[d.ppos[t] - 1] / tp;
+    if (f != 0.0) *g -= f * gp;
+}
+
+__global__ void __launch_bounds__(256) k_panel_update_cur(SpxDev d)
+{
+    const DState *st = d.st;
+    if (st->stop || !st->pend) return;
+    const int cur = st->pcur;
+    const double tp = st->pivot;
+    const int j = blockIdx.x * 256 + threadIdx.x;
+    if (j == 0) d.st->page = st->page + 1;
+    if (st->pk <= 0 || j >= d.n) return;
+    double *g = d.pnl + (size_t)cur * d.ldp + j;
+    *g = -*g / tp;
 }
 
 // the plan's panel size: the column-pass path on dense A outside rigorous
@@ -266,7 +277,8 @@ void panel_trow(hipStream_t s, const SpxDev &d, const DualPlan &pl)
 void panel_update(hipStream_t s, const SpxDev &d, const DualPlan &pl)
 {
     (void)pl;
-    hipLaunchKernelGGL(k_panel_update, dim3(cdiv(d.n, 256)), dim3(256), 0, s, d);
+    hipLaunchKernelGGL(k_panel_update, dim3(cdiv(d.n, 256), PANEL_MAX), dim3(256), 0, s, d);
+    hipLaunchKernelGGL(k_panel_update_cur, dim3(cdiv(d.n, 256)), dim3(256), 0, s, d);
 }
 
 }  // namespace gk
