@@ -791,6 +791,17 @@ static bool sp_seg_on()
     return on;
 }
 
+// GK_SP_LDS=0: the small factors' fused sweeps keep their outputs in global
+// memory (the round-5 layout before lds_sweep)
+static bool sp_lds_on()
+{
+    static const bool on = [] {
+        const char *e = std::getenv("GK_SP_LDS");
+        return !e || atoi(e) != 0;
+    }();
+    return on;
+}
+
 // entries from which a level runs on the grid (with LDS segments; a level
 // of many steps, sp_wide_min, does in any case)
 static int sp_wide_entries()
@@ -1353,16 +1364,48 @@ __device__ void ftran_hh(const SpDev &sp);
 // FTRAN part 1 (one workgroup): z = inv(B0) [h, work]; L in place, U into
 // the scratch; the z of h is kept (zq) for the update of this pivot.
 // parts: bit 0 the L sweep (from level l0l), bit 1 the U sweep (from l0u)
+// a small factor's sweep with its output vector in LDS (lds_sweep): the
+// output copied in (an in-place sweep reads the entries no step writes),
+// the levels' gathers from LDS instead of the L2, the vector copied back
+// after the last level.  The same arithmetic in the same order.
+extern __shared__ double sp_lds[];
+template <int NRHS>
+__device__ void lds_sweep(const TriDev &t, int m, const double *in0, const double *in1, double *out0, double *out1,
+                          double *s0, int l0)
+{
+    double *s1 = s0 + m;
+    for (int i = threadIdx.x; i < m; i += blockDim.x) {
+        s0[i] = out0[i];
+        if (NRHS == 2) s1[i] = out1[i];
+    }
+    __syncthreads();
+    tri_sweep<NRHS>(t, in0, in1, s0, NRHS == 2 ? s1 : nullptr, l0);
+    __syncthreads();
+    for (int i = threadIdx.x; i < m; i += blockDim.x) {
+        out0[i] = s0[i];
+        if (NRHS == 2) out1[i] = s1[i];
+    }
+    __syncthreads();
+}
+
+// the sweeps of factors up to this m keep their output vectors in LDS
+// (NRHS = 2 FTRAN: 16 m bytes; the BTRAN's two sweeps: 16 m bytes)
+constexpr int SP_LDS_M = 6144;
+
 template <int NRHS>
 __global__ void __launch_bounds__(1024) k_sp_ftran_lu(SpDev sp, const DState *st, double *h0, double *h1, int gated,
-                                                      int parts, int l0l, int l0u)
+                                                      int parts, int l0l, int l0u, int lds)
 {
     if (gated && st->stop) return;
     const int m = sp.m;
-    if (parts & 1) tri_sweep<NRHS>(sp.fl, h0, h1, h0, h1, l0l);      // in place: z[r] (row space)
+    if (parts & 1) {                                                   // in place: z[r] (row space)
+        if (lds) lds_sweep<NRHS>(sp.fl, m, h0, h1, h0, h1, sp_lds, l0l);
+        else tri_sweep<NRHS>(sp.fl, h0, h1, h0, h1, l0l);
+    }
     double *x0 = sp.w.bt, *x1 = sp.w.bt + m;
     if (!(parts & 2)) return;
-    tri_sweep<NRHS>(sp.fu, h0, h1, x0, x1, l0u);                      // positions
+    if (lds) lds_sweep<NRHS>(sp.fu, m, h0, h1, x0, x1, sp_lds, l0u);   // positions
+    else tri_sweep<NRHS>(sp.fu, h0, h1, x0, x1, l0u);
     ftran_hh<NRHS>(sp);
 }
 
@@ -1819,7 +1862,7 @@ __global__ void __launch_bounds__(1024) k_sp_hh(SpDev sp, const DState *st, int 
 template <int NRHS>
 __global__ void __launch_bounds__(1024) k_sp_btran(SpDev sp, DState *st, const double *e, double *y, int mode,
                                                    int nparts, const double *e1, double *y1, int parts, int l0u,
-                                                   int l0l)
+                                                   int l0l, int lds)
 {
     if (mode >= 1 && (st->stop || st->p <= 0)) return;
     const int m = sp.m, k = *sp.w.k;
@@ -1883,6 +1926,36 @@ __global__ void __launch_bounds__(1024) k_sp_btran(SpDev sp, DState *st, const d
         if (NRHS == 2) b1[sp.w.P[t]] -= sv[1][t];
     }
     __syncthreads();
+    if (lds && (parts & 6) == 6) {
+        // both sweeps with their outputs in LDS (the U' output, the L'
+        // sweep's input, stays there; the step space is written back too)
+        double *sa = sp_lds, *sb = sp_lds + NRHS * m;
+        double *sa1 = sa + m, *sb1 = sb + m;
+        for (int i = threadIdx.x; i < m; i += blockDim.x) {
+            sa[i] = w0[i];
+            sb[i] = y[i];
+            if (NRHS == 2) {
+                sa1[i] = w1[i];
+                sb1[i] = y1[i];
+            }
+        }
+        __syncthreads();
+        tri_sweep<NRHS>(sp.bu, b0, b1, sa, NRHS == 2 ? sa1 : nullptr, l0u);
+        __syncthreads();
+        tri_sweep<NRHS>(sp.bl, sa, NRHS == 2 ? sa1 : nullptr, sb, NRHS == 2 ? sb1 : nullptr, l0l);
+        __syncthreads();
+        for (int i = threadIdx.x; i < m; i += blockDim.x) {
+            w0[i] = sa[i];
+            y[i] = sb[i];
+            if (NRHS == 2) {
+                w1[i] = sa1[i];
+                y1[i] = sb1[i];
+            }
+        }
+        __syncthreads();
+        if (mode == 1) bz_clear(sp, p, k);
+        return;
+    }
     if (parts & 2) tri_sweep<NRHS>(sp.bu, b0, b1, w0, w1, l0u);
     if (parts & 4) {
         tri_sweep<NRHS>(sp.bl, w0, w1, y, y1, l0l);
@@ -2387,13 +2460,30 @@ static void run_plan(const SpFactor &F, int which, const SpDev &d, hipStream_t s
                            0, 1);
 }
 
+// the fused sweep kernels may take up to 2 * 8 * SP_LDS_M bytes of dynamic LDS
+static void sp_lds_attrs()
+{
+    static const bool done = [] {
+        const int bytes = 2 * 8 * SP_LDS_M;
+        (void)hipFuncSetAttribute((const void *)k_sp_ftran_lu<1>, hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
+        (void)hipFuncSetAttribute((const void *)k_sp_ftran_lu<2>, hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
+        (void)hipFuncSetAttribute((const void *)k_sp_btran<1>, hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
+        (void)hipFuncSetAttribute((const void *)k_sp_btran<2>, hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
+        return true;
+    }();
+    (void)done;
+}
+
 // z = inv(L U) [h0, h1] (L in place, U into bt) and inv(M) z[P]: one fused
 // workgroup launch, or with wide levels the plans of both sweeps
 template <int NRHS>
 static void ftran_lu(SpFactor &F, hipStream_t s, const SpDev &d, const DState *st, int gated, double *h0, double *h1)
 {
     if (!F.wide[0] && !F.wide[1]) {
-        hipLaunchKernelGGL((k_sp_ftran_lu<NRHS>), dim3(1), dim3(1024), 0, s, d, st, h0, h1, gated, 3, 0, 0);
+        sp_lds_attrs();
+        const int lds = sp_lds_on() && F.m <= SP_LDS_M;
+        hipLaunchKernelGGL((k_sp_ftran_lu<NRHS>), dim3(1), dim3(1024), lds ? (size_t)NRHS * F.m * sizeof(double) : 0, s,
+                           d, st, h0, h1, gated, 3, 0, 0, lds);
         return;
     }
     double *x0 = F.bt.p, *x1 = F.bt.p + F.m;
@@ -2409,12 +2499,15 @@ static void btran_seq(SpFactor &F, hipStream_t s, const SpDev &d, DState *st, co
                       int nparts, const double *e1, double *y1)
 {
     if (!F.wide[2] && !F.wide[3]) {
-        hipLaunchKernelGGL((k_sp_btran<NRHS>), dim3(1), dim3(1024), 0, s, d, st, e, y, mode, nparts, e1, y1, 7, 0, 0);
+        sp_lds_attrs();
+        const int lds = sp_lds_on() && F.m <= SP_LDS_M && (NRHS == 1 || F.m <= SP_LDS_M / 2);
+        hipLaunchKernelGGL((k_sp_btran<NRHS>), dim3(1), dim3(1024), lds ? (size_t)2 * NRHS * F.m * sizeof(double) : 0,
+                           s, d, st, e, y, mode, nparts, e1, y1, 7, 0, 0, lds);
         return;
     }
     const int gate = mode >= 1 ? 2 : 0, m = F.m;
     double *b0 = (mode == 1) ? F.bz.p : F.bt.p, *b1 = F.bt.p + m, *w0 = F.scr2.p, *w1 = F.scr2.p + m;
-    hipLaunchKernelGGL((k_sp_btran<NRHS>), dim3(1), dim3(1024), 0, s, d, st, e, y, mode, nparts, e1, y1, 1, 0, 0);
+    hipLaunchKernelGGL((k_sp_btran<NRHS>), dim3(1), dim3(1024), 0, s, d, st, e, y, mode, nparts, e1, y1, 1, 0, 0, 0);
     run_plan<NRHS>(F, 2, d, s, st, gate, b0, b1, w0, w1, 0);
     run_plan<NRHS>(F, 3, d, s, st, gate, w0, w1, y, y1, mode == 1);
 }
