@@ -1956,7 +1956,7 @@ __global__ void __launch_bounds__(1024) k_dual_ftran1(SpxDev d, int gn, int awsp
 // accounts the pivot's algorithmic bytes.
 // ---------------------------------------------------------------------------
 __global__ void __launch_bounds__(256) k_dual_commit(SpxDev d, int pse, int nvb, int tiles, int lpsu, int rowpath,
-                                                     double bytes_fixed)
+                                                     double bytes_fixed, int pfrom)
 {
     const TraceScope trace_(d, 4);
     const ExitStamp xs_(d.xslots, blockIdx.x);
@@ -2143,6 +2143,29 @@ __global__ void __launch_bounds__(256) k_dual_commit(SpxDev d, int pse, int nvb,
             st->bytes += rowb + 8.0 * (double)m * nwl0 + 8.0 * (double)m * (nr0 + 1) +
                          16.0 * (double)m * (nr0 + (kp <= m ? 1 : 0)) + bytes_fixed;
         }
+        return;
+    }
+    if (pfrom > 0 && (int)blockIdx.x >= pfrom) {
+        // the pricing panel's rows t != pcur follow the rank-1 update
+        // (k_panel_update's work, gk_panel.hip: G[t] -= (tcol[pos_t] / alpha)
+        // G[pcur], one read-modify-write per thread); row pcur, which these
+        // read, is replaced by k_panel_update_cur after this launch
+        const int nbx = (n + 255) / 256;
+        const int pb = blockIdx.x - pfrom, t = pb / nbx;
+        const int j = (pb % nbx) * 256 + threadIdx.x;
+        const int pk = st->pk, cur = st->pcur;
+        const int binv_fresh = st->binv_fresh, rig = st->rigorous;
+        const double piv1 = d.tcol[p - 1], piv2 = d.trow[q - 1];
+        if (stop || t >= pk || t == cur || j >= n) return;
+        const bool bad = fabs(piv1 - piv2) > 1e-8 * (1.0 + fabs(piv1)) ||
+                         !((piv1 > 0.0 && piv2 > 0.0) || (piv1 < 0.0 && piv2 < 0.0));
+        if (bad && (!binv_fresh || !rig)) return;
+        const double tp = bad ? piv2 : piv1;
+        const size_t ldp = (size_t)d.ldp;
+        const double gp = d.pnl[(size_t)cur * ldp + j];
+        double *g = d.pnl + (size_t)t * ldp + j;
+        const double f = d.tcol[d.ppos[t] - 1] / tp;
+        if (f != 0.0) *g -= f * gp;
         return;
     }
     // rank-1 update over the dense columns (the compact rho: ns entries)
@@ -2945,7 +2968,7 @@ void dual_iteration2(hipStream_t s, const SpxDev &d, const DualPlan &pl, hipEven
         hipLaunchKernelGGL(k_dual_pick, dim3(1), dim3(1024), 0, s, d, pl.pse, gn, ncb);
         sp_pivot_ftran(*d.sp, s, d.st, d.h, d.work, d.tcol, d.u, pl.pse);
         hipLaunchKernelGGL(k_dual_commit, dim3(gv), dim3(256), 0, s, d, pl.pse, gv, tiles_m, pl.lpsu, 0,
-                           bytes_fixed(d));
+                           bytes_fixed(d), 0);
         sp_pivot_update(*d.sp, s, d.st);
         return;
     }
@@ -2970,7 +2993,7 @@ void dual_iteration2(hipStream_t s, const SpxDev &d, const DualPlan &pl, hipEven
             hipLaunchKernelGGL((k_dual_ftran1<1, 1, 16>), dim3(cdiv(m, 16)), dim3(64 * pl.fwaves), 0, s, d, gn,
                                pl.awsplits, ncb, pl.nr_cap);
         hipLaunchKernelGGL(k_dual_commit, dim3(gv + tiles_m * pl.uchunks), dim3(256), 0, s, d, pl.pse, gv, tiles_m,
-                           pl.lpsu, 2, bytes_fixed(d));
+                           pl.lpsu, 2, bytes_fixed(d), 0);
         return;
     }
     if (pl.rowpath) {
@@ -3040,8 +3063,12 @@ void dual_iteration2(hipStream_t s, const SpxDev &d, const DualPlan &pl, hipEven
         if (pl.rigorous) refine_tcol_dev(s, d, 0);
     }
     const int nvb = gv;
-    hipLaunchKernelGGL(k_dual_commit, dim3(nvb + tiles_m * pl.uchunks), dim3(256), 0, s, d, pl.pse, nvb, tiles_m,
-                       pl.lpsu, pl.rowpath, bytes_fixed(d));
+    // (with the pricing panel: its rows t != pcur updated by extra blocks of
+    // the commit, row pcur by panel_update after it)
+    const int pfrom = pl.panel ? nvb + tiles_m * pl.uchunks : 0;
+    const int pblocks = pl.panel ? cdiv(n, 256) * PANEL_MAX : 0;
+    hipLaunchKernelGGL(k_dual_commit, dim3(nvb + tiles_m * pl.uchunks + pblocks), dim3(256), 0, s, d, pl.pse, nvb,
+                       tiles_m, pl.lpsu, pl.rowpath, bytes_fixed(d), pfrom);
     if (pl.panel) panel_update(s, d, pl);
 }
 

@@ -28,7 +28,8 @@
 //   * k_panel_trow:   trow of every non-basic position, as the column pass
 //                     CP_TROW writes it: the panel row of p at a structural,
 //                     -rho at an auxiliary, 0 at a fixed variable;
-//   * k_panel_update: after the commit, the update above (PK rows, n columns).
+//   * after the commit, the update above (PK rows, n columns): k_dual_commit's
+//     extra blocks for the rows t != pcur, then k_panel_update_cur.
 // Pick, gather and MFMA are in every pivot of the captured graph and gate
 // themselves on the device flags.  A tableau row is a property of the basis,
 // not of the factor, so the panel survives batch boundaries; it is emptied
@@ -206,28 +207,13 @@ __global__ void __launch_bounds__(256) k_panel_trow(SpxDev d)
     if (threadIdx.x == 0 && b > 0.0) atomicMax(&st->trow_max_bits, dbits(b));
 }
 
-// after a committed pivot (pend set by k_dual_commit, no stop): the rows of
-// the panel follow the rows of inv(B) (k_dual_commit's rank-1 update)
-__global__ void __launch_bounds__(256) k_panel_update(SpxDev d)
-{
-    // block (x, t): row t != pcur of the panel at the columns of block x —
-    // one read-modify-write per thread, every row at once (a thread walking
-    // the rows did one dependent memory round trip per row); row pcur, which
-    // the others read, is replaced by k_panel_update_cur after them
-    const DState *st = d.st;
-    if (st->stop || !st->pend) return;
-    const int pk = st->pk, cur = st->pcur, t = blockIdx.y;
-    const double tp = st->pivot;
-    const int n = d.n;
-    const int j = blockIdx.x * 256 + threadIdx.x;
-    if (t >= pk || t == cur || j >= n) return;
-    const size_t ldp = (size_t)d.ldp;
-    const double gp = d.pnl[(size_t)cur * ldp + j];
-    double *g = d.pnl + (size_t)t * ldp + j;
-    const double f = d.tcol[d.ppos[t] - 1] / tp;
-    if (f != 0.0) *g -= f * gp;
-}
-
+// after a committed pivot (pend set by k_dual_commit, no stop) the rows of
+// the panel follow the rows of inv(B) (k_dual_commit's rank-1 update):
+// row pcur of the panel (G[p] := -G[p] / alpha), after the commit launch
+// whose extra blocks updated the other rows from it (k_dual_commit): one
+// read-modify-write per thread on the rows at once — a thread walking the
+// 32 rows of its column took 22.7 us per pivot, one dependent memory round
+// trip per row
 __global__ void __launch_bounds__(256) k_panel_update_cur(SpxDev d)
 {
     const DState *st = d.st;
@@ -277,7 +263,8 @@ void panel_trow(hipStream_t s, const SpxDev &d, const DualPlan &pl)
 void panel_update(hipStream_t s, const SpxDev &d, const DualPlan &pl)
 {
     (void)pl;
-    hipLaunchKernelGGL(k_panel_update, dim3(cdiv(d.n, 256), PANEL_MAX), dim3(256), 0, s, d);
+    // (the rows t != pcur: extra blocks of the k_dual_commit launch before
+    // this, the same work as k_panel_update)
     hipLaunchKernelGGL(k_panel_update_cur, dim3(cdiv(d.n, 256)), dim3(256), 0, s, d);
 }
 
