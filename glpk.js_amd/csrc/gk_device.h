@@ -363,6 +363,60 @@ static __device__ void build_hq(const SpxDev &d, int q, bool zeroed = false)
 static inline int cdiv(int a, int b) { return (a + b - 1) / b; }
 __device__ __forceinline__ int gv_of(int m, int n) { return (max(m, n) + 255) / 256; }
 __device__ __forceinline__ Cand *cand_chuzr(const SpxDev &d) { return (Cand *)d.cand; }
+
+// the pricing panel's pick for the leaving row p (gk_panel.hip): a hit sets
+// pcur to p's slot; a miss (or a panel older than age_max updates) ranks the
+// chuzr candidates by better<0> and fills the panel's positions, p first.
+// Called by every thread of one 256-thread block (k_panel_pick, or block 0
+// of k_dual_top_grid with the chuzr choice in hand).
+__device__ __forceinline__ void panel_pick_dev(const SpxDev &d, int gm, int cap, int age_max, int p)
+{
+    __shared__ Cand cs[1024];
+    __shared__ int nval;
+    DState *st = d.st;
+    const int valid = st->pvalid, pk = st->pk, age = st->page;
+    const int sl = d.pslot[p - 1];
+    const bool hit = valid && age < age_max && sl >= 0 && sl < pk && d.ppos[sl] == p;
+    if (hit) {
+        if (threadIdx.x == 0) {
+            st->pcur = sl;
+            st->pmiss = 0;
+            st->phits += 1.0;
+        }
+        return;
+    }
+    if (threadIdx.x == 0) nval = 0;
+    for (int b = threadIdx.x; b < gm; b += blockDim.x) cs[b] = cand_chuzr(d)[b];
+    __syncthreads();
+    int mine = 0;
+    for (int b = threadIdx.x; b < gm; b += blockDim.x) {
+        const Cand c = cs[b];
+        if (c.idx == 0 || c.idx == p) continue;
+        mine++;
+        int r = 0;
+        for (int u = 0; u < gm; ++u) {
+            const Cand e = cs[u];
+            if (e.idx != 0 && e.idx != p && better<0>(e, c)) r++;
+        }
+        if (r < cap - 1) {
+            d.ppos[1 + r] = c.idx;
+            d.pslot[c.idx - 1] = 1 + r;
+        }
+    }
+    if (mine) atomicAdd(&nval, mine);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        d.ppos[0] = p;
+        d.pslot[p - 1] = 0;
+        st->pk = 1 + min(nval, cap - 1);
+        st->page = 0;
+        st->pcur = 0;
+        st->pmiss = 1;
+        st->pvalid = 1;
+        st->pmisses += 1.0;
+    }
+}
+
 __device__ __forceinline__ Cand no_cand(double k1)
 {
     Cand c; c.k1 = k1; c.k2 = 0.0; c.idx = 0; c.aux = 0;

@@ -609,7 +609,7 @@ __global__ void __launch_bounds__(TOP_WG) k_dual_top(SpxDev d, int rowpath, int 
 // i, else 1 at the leaving slack, else 0: the unit columns are exact), the
 // compact rho by list position; 256 rows / list entries per thread block.
 // ---------------------------------------------------------------------------
-__global__ void __launch_bounds__(256) k_dual_top_grid(SpxDev d)
+__global__ void __launch_bounds__(256) k_dual_top_grid(SpxDev d, int pcap, int page_max)
 {
     const TraceScope trace_(d, 0);
     DState *st = d.st;
@@ -689,6 +689,9 @@ __global__ void __launch_bounds__(256) k_dual_top_grid(SpxDev d)
         st->ns = ns;
         st->dinf = 0;
     }
+    // the pricing panel's pick for this p (pcap > 0: the plan has the panel;
+    // k_panel_pick's work, one launch fewer)
+    if (lead && pcap > 0) panel_pick_dev(d, gm, pcap, page_max, p);
 }
 
 // ---------------------------------------------------------------------------
@@ -3008,14 +3011,15 @@ void dual_iteration2(hipStream_t s, const SpxDev &d, const DualPlan &pl, hipEven
         else
             hipLaunchKernelGGL(k_dual_row<8>, dim3(ncb), dim3(64 * pl.twaves), 0, s, d, pl.pse, pl.nr_cap, pl.gm);
     } else {
-        if (!pl.rigorous && d.A.dense && m >= 1024)
-            hipLaunchKernelGGL(k_dual_top_grid, dim3(cdiv(m, 256)), dim3(256), 0, s, d);
+        const bool tgrid = !pl.rigorous && d.A.dense && m >= 1024;
+        if (tgrid)
+            hipLaunchKernelGGL(k_dual_top_grid, dim3(cdiv(m, 256)), dim3(256), 0, s, d, pl.panel, pl.panel_age);
         else
             hipLaunchKernelGGL(k_dual_top, dim3(1), dim3(TOP_WG), 0, s, d, pl.rowpath, pl.nr_cap);
         if (pl.rigorous) refine_rho_dev(s, d);
         if (ev0) (void)hipEventRecord(ev0, s);
         if (pl.panel)   // the row of p from the MFMA panel (gk_panel.hip)
-            panel_trow(s, d, pl);
+            panel_trow(s, d, pl, tgrid);
         else if (d.shard) {
             // this rank's slice of the non-basic positions, then the exchange
             const LpShard &sh = *d.shard;

@@ -309,7 +309,7 @@ void rowpass_pi(hipStream_t s, const SpxDev &d, int mode, int nr, const double *
 // the panel's update after the commit; panel_wanted: the plan's panel size
 int panel_wanted(const SpxDev &d, const DualPlan &pl);
 int panel_age_max();
-void panel_trow(hipStream_t s, const SpxDev &d, const DualPlan &pl);
+void panel_trow(hipStream_t s, const SpxDev &d, const DualPlan &pl, bool picked = false);
 void panel_update(hipStream_t s, const SpxDev &d, const DualPlan &pl);
 // timing hook: the row-path pivot-row kernel alone (returns algorithmic bytes)
 double launch_trow_rows(hipStream_t s, const SpxDev &d, const DualPlan &pl, int ns);

@@ -50,51 +50,9 @@ namespace gk {
 // default), so the drift of a served row stays that of a freshly formed one
 __global__ void __launch_bounds__(256) k_panel_pick(SpxDev d, int gm, int cap, int age_max)
 {
-    __shared__ Cand cs[1024];
-    __shared__ int nval;
-    DState *st = d.st;
-    const int stop = st->stop, p = st->p, valid = st->pvalid, pk = st->pk, age = st->page;
-    if (stop || p <= 0) return;
-    const int sl = d.pslot[p - 1];
-    const bool hit = valid && age < age_max && sl >= 0 && sl < pk && d.ppos[sl] == p;
-    if (hit) {
-        if (threadIdx.x == 0) {
-            st->pcur = sl;
-            st->pmiss = 0;
-            st->phits += 1.0;
-        }
-        return;
-    }
-    if (threadIdx.x == 0) nval = 0;
-    for (int b = threadIdx.x; b < gm; b += blockDim.x) cs[b] = cand_chuzr(d)[b];
-    __syncthreads();
-    int mine = 0;
-    for (int b = threadIdx.x; b < gm; b += blockDim.x) {
-        const Cand c = cs[b];
-        if (c.idx == 0 || c.idx == p) continue;
-        mine++;
-        int r = 0;
-        for (int u = 0; u < gm; ++u) {
-            const Cand e = cs[u];
-            if (e.idx != 0 && e.idx != p && better<0>(e, c)) r++;
-        }
-        if (r < cap - 1) {
-            d.ppos[1 + r] = c.idx;
-            d.pslot[c.idx - 1] = 1 + r;
-        }
-    }
-    if (mine) atomicAdd(&nval, mine);
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        d.ppos[0] = p;
-        d.pslot[p - 1] = 0;
-        st->pk = 1 + min(nval, cap - 1);
-        st->page = 0;
-        st->pcur = 0;
-        st->pmiss = 1;
-        st->pvalid = 1;
-        st->pmisses += 1.0;
-    }
+    const DState *st = d.st;
+    if (st->stop || st->p <= 0) return;
+    panel_pick_dev(d, gm, cap, age_max, st->p);
 }
 
 // pnl_src[t * m + i] = inv(B)[pos_t, i] for a dense column i of inv(B); for a
@@ -251,10 +209,12 @@ int panel_age_max()
     return e ? std::max(1, std::atoi(e)) : 100;
 }
 
-void panel_trow(hipStream_t s, const SpxDev &d, const DualPlan &pl)
+void panel_trow(hipStream_t s, const SpxDev &d, const DualPlan &pl, bool picked)
 {
     const int m = d.m, n = d.n;
-    hipLaunchKernelGGL(k_panel_pick, dim3(1), dim3(256), 0, s, d, 4 * cdiv(m, 256), pl.panel, pl.panel_age);
+    // (picked: k_dual_top_grid's block 0 made the pick with the chuzr choice)
+    if (!picked)
+        hipLaunchKernelGGL(k_panel_pick, dim3(1), dim3(256), 0, s, d, 4 * cdiv(m, 256), pl.panel, pl.panel_age);
     hipLaunchKernelGGL(k_panel_gather, dim3(cdiv(m, 256), pl.panel), dim3(256), 0, s, d);
     hipLaunchKernelGGL(k_panel_mfma, dim3(cdiv(n, 32)), dim3(256), 0, s, d);
     hipLaunchKernelGGL(k_panel_trow, dim3(cdiv(n, 256)), dim3(256), 0, s, d);
