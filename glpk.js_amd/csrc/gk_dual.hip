@@ -701,7 +701,10 @@ __global__ void __launch_bounds__(256) k_dual_top_grid(SpxDev d, int pcap, int p
 // of those trow^2 (gamma_p), and the block's Harris pass-1 candidate under the
 // block-local significance tolerance (k_dual_ratio re-checks it).
 // ---------------------------------------------------------------------------
-__global__ void __launch_bounds__(256) k_trow_finish(SpxDev d, int pse)
+// (panel: the pivot row read from the pricing panel here — k_panel_trow's
+// work: the panel row of p at a structural, -rho at an auxiliary, 0 at a
+// fixed variable, stored to trow with its maximum — one launch fewer)
+__global__ void __launch_bounds__(256) k_trow_finish(SpxDev d, int pse, int panel)
 {
     const TraceScope trace_(d, 5);
     DState *st = d.st;
@@ -722,13 +725,21 @@ __global__ void __launch_bounds__(256) k_trow_finish(SpxDev d, int pse)
     if (j1 >= 0) {
         s1 = d.stat[j1];
         cb1 = d.cbar[j1];
-        tv1 = d.trow[j1];
+        if (panel) {
+            tv1 = (s1 != NS) ? d.pnl[(size_t)st->pcur * d.ldp + idx] : 0.0;
+            d.trow[j1] = tv1;
+        } else
+            tv1 = d.trow[j1];
         if (pse) ref1 = d.refsp[m + idx] != 0;
     }
     if (j2 >= 0) {
         s2 = d.stat[j2];
         cb2 = d.cbar[j2];
-        tv2 = d.trow[j2];
+        if (panel) {
+            tv2 = (s2 != NS) ? -d.rho[idx] : 0.0;
+            d.trow[j2] = tv2;
+        } else
+            tv2 = d.trow[j2];
         if (pse) ref2 = d.refsp[idx] != 0;
     }
     double gsum = 0.0;
@@ -753,6 +764,7 @@ __global__ void __launch_bounds__(256) k_trow_finish(SpxDev d, int pse)
         if (pse) d.gpart[grp] = g;
         tmax_part(d)[grp] = bmax;
         cand_pass1(d)[grp] = b;
+        if (panel && bmax > 0.0) atomicMax(&st->trow_max_bits, dbits(bmax));
     }
 }
 
@@ -2965,7 +2977,7 @@ void dual_iteration2(hipStream_t s, const SpxDev &d, const DualPlan &pl, hipEven
         colpass_gated(s, d.A, CP_TROW, m, n, d.head, d.stat, d.coef, nullptr, d.rho, nullptr, d.trow, nullptr,
                       &d.st->trow_max_bits, d.st, 0);
         if (ev1) (void)hipEventRecord(ev1, s);
-        hipLaunchKernelGGL(k_trow_finish, dim3(gv), dim3(256), 0, s, d, pl.pse);
+        hipLaunchKernelGGL(k_trow_finish, dim3(gv), dim3(256), 0, s, d, pl.pse, 0);
         hipLaunchKernelGGL(k_dual_ratio, dim3(gn + (pl.pse ? cdiv(m, 256) + d.A.nlr : 0)), dim3(256), 0, s, d, gn,
                            tiles_m, 0, ncb, 0, 0);
         hipLaunchKernelGGL(k_dual_pick, dim3(1), dim3(1024), 0, s, d, pl.pse, gn, ncb);
@@ -3031,7 +3043,7 @@ void dual_iteration2(hipStream_t s, const SpxDev &d, const DualPlan &pl, hipEven
             colpass_gated(s, d.A, CP_TROW, m, n, d.head, d.stat, d.coef, nullptr, d.rho, nullptr, d.trow, nullptr,
                           &d.st->trow_max_bits, d.st, 0);
         if (ev1) (void)hipEventRecord(ev1, s);
-        hipLaunchKernelGGL(k_trow_finish, dim3(gv), dim3(256), 0, s, d, pl.pse);
+        hipLaunchKernelGGL(k_trow_finish, dim3(gv), dim3(256), 0, s, d, pl.pse, pl.panel ? 1 : 0);
     }
     const int aw = (pl.pse && d.A.dense) ? 1 : 0;
     const int awone = (aw && pl.fused) ? pl.awone : 0;

@@ -25,7 +25,7 @@
 //   * k_panel_mfma:   times A on v_mfma_f64_16x16x4_f64 — one pass over A for
 //                     up to 32 rows (the batch of candidate rows packed into a
 //                     dense panel, the MFMA operand);
-//   * k_panel_trow:   trow of every non-basic position, as the column pass
+//   * trow (k_trow_finish with panel = 1): every non-basic position, as the column pass
 //                     CP_TROW writes it: the panel row of p at a structural,
 //                     -rho at an auxiliary, 0 at a fixed variable;
 //   * after the commit, the update above (PK rows, n columns): k_dual_commit's
@@ -144,27 +144,6 @@ __global__ void __launch_bounds__(256) k_panel_mfma(SpxDev d)
     }
 }
 
-// the pivot row for every non-basic position j (CP_TROW's values): 0 when
-// x_N[j] is fixed, -rho[k] for an auxiliary k, the panel row of p for a
-// structural; max |trow| by one atomic per block
-__global__ void __launch_bounds__(256) k_panel_trow(SpxDev d)
-{
-    __shared__ double sh[16];
-    DState *st = d.st;
-    if (st->stop) return;
-    const int m = d.m, n = d.n;
-    const int slot = st->pcur;
-    const int j = blockIdx.x * 256 + threadIdx.x;
-    double v = 0.0;
-    if (j < n) {
-        const int k = d.head[m + j];
-        if (d.stat[j] != NS) v = (k <= m) ? -d.rho[k - 1] : d.pnl[(size_t)slot * d.ldp + (k - m - 1)];
-        d.trow[j] = v;
-    }
-    const double b = block_max(fabs(v), sh);
-    if (threadIdx.x == 0 && b > 0.0) atomicMax(&st->trow_max_bits, dbits(b));
-}
-
 // after a committed pivot (pend set by k_dual_commit, no stop) the rows of
 // the panel follow the rows of inv(B) (k_dual_commit's rank-1 update):
 // row pcur of the panel (G[p] := -G[p] / alpha), after the commit launch
@@ -217,7 +196,8 @@ void panel_trow(hipStream_t s, const SpxDev &d, const DualPlan &pl, bool picked)
         hipLaunchKernelGGL(k_panel_pick, dim3(1), dim3(256), 0, s, d, 4 * cdiv(m, 256), pl.panel, pl.panel_age);
     hipLaunchKernelGGL(k_panel_gather, dim3(cdiv(m, 256), pl.panel), dim3(256), 0, s, d);
     hipLaunchKernelGGL(k_panel_mfma, dim3(cdiv(n, 32)), dim3(256), 0, s, d);
-    hipLaunchKernelGGL(k_panel_trow, dim3(cdiv(n, 256)), dim3(256), 0, s, d);
+    // (trow itself: k_trow_finish reads the panel row of p, panel = 1)
+    (void)n;
 }
 
 void panel_update(hipStream_t s, const SpxDev &d, const DualPlan &pl)
