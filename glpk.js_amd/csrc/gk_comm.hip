@@ -21,6 +21,7 @@
 // as every rank has mapped it, so nothing outlives the processes); ranks on
 // different hosts fall back to the epoch exchange alone.
 #include "../../include/glpk_mi355x.h"
+#include "gk_internal.h"
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
@@ -44,6 +45,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <new>
+#include <stdexcept>
 #include <string>
 #include <thread>
 #include <vector>
@@ -64,6 +66,7 @@ struct Rccl {
     decltype(&ncclCommInitRank) init = nullptr;
     decltype(&ncclAllGather) allgather = nullptr;
     decltype(&ncclCommDestroy) destroy = nullptr;
+    decltype(&ncclCommAbort) abort = nullptr;   // optional
     bool load()
     {
         if (lib) return true;
@@ -76,6 +79,7 @@ struct Rccl {
         init = (decltype(init))dlsym(lib, "ncclCommInitRank");
         allgather = (decltype(allgather))dlsym(lib, "ncclAllGather");
         destroy = (decltype(destroy))dlsym(lib, "ncclCommDestroy");
+        abort = (decltype(abort))dlsym(lib, "ncclCommAbort");
         return get_id && init && allgather && destroy;
     }
 };
@@ -462,6 +466,40 @@ int gk_comm_allgather_dev(gk_comm *c, const void *dsend, size_t bytes, void *dre
         return 1;
     }
     return hipMemcpyAsync(drecv, hrecv, bytes * (size_t)c->size, hipMemcpyHostToDevice, s) == hipSuccess ? 0 : 1;
+}
+
+// a rank-local failure inside a collective sequence (the sharded LP): the
+// communicator is marked failed and its links are shut down, so that every
+// peer's next exchange returns an error instead of waiting for this rank
+// (their failure then shuts their own links: the abort reaches every rank)
+void gk_comm_abort(gk_comm *c)
+{
+    if (!c) return;
+    c->failed = true;
+    for (int fd : c->fds)
+        if (fd >= 0) (void)::shutdown(fd, SHUT_RDWR);
+    if (c->nc && c->rccl.abort) {
+        (void)c->rccl.abort(c->nc);
+        c->nc = nullptr;
+    }
+}
+bool shard_any(LpShard &sh, bool flag)
+{
+    const char mine = flag ? 1 : 0;
+    std::vector<char> all((size_t)sh.size, 0);
+    if (sh.failed || gk_comm_allgather(sh.comm, &mine, 1, all.data()) != 0) {
+        sh.failed = true;
+        throw std::runtime_error("column-sharded pricing: the stop decision's exchange failed");
+    }
+    for (char c : all)
+        if (c) return true;
+    return false;
+}
+
+void shard_abort(LpShard &sh)
+{
+    sh.failed = true;
+    gk_comm_abort(sh.comm);
 }
 }  // namespace gk
 

@@ -2696,6 +2696,10 @@ int Spx::run_dual()
         {
             bool it_hit = P->it_lim < 0x7fffffff && hs.it_cnt - it_beg >= P->it_lim;
             bool tm_hit = !it_hit && P->tm_lim < 0x7fffffff && 1000.0 * (now_s() - tm_beg) >= P->tm_lim;
+            // (column-sharded pricing: every rank must stop on the same pivot,
+            // so the wall-clock decision is taken collectively — any rank's)
+            if (!it_hit && P->tm_lim < 0x7fffffff && f->shard && E->dense && !f->sparse)
+                tm_hit = shard_any(*f->shard, tm_hit);
             if (it_hit || tm_hit) {
                 if ((phase == 2 && bbar_st != 1) || cbar_st != 1) {
                     if (phase == 2 && bbar_st != 1) bbar_st = 0;
@@ -3422,6 +3426,7 @@ static int spx_entry(gk_ctx *ctx, gk_lp *lp, gk_bfd *f, const gk_smcp *parm, int
             sh.hrecv.assign((size_t)sh.size * (sh.L + 1), 0.0);
             sh.n = n;
         }
+        const long long shard_ex0 = f->shard ? f->shard->exchanges : 0;
         Spx S;
         S.ctx = ctx; S.f = f; S.E = f->eng; S.lp = lp; S.parm = parm; S.dual = dual;
         S.mark("entry");
@@ -3432,6 +3437,7 @@ static int spx_entry(gk_ctx *ctx, gk_lp *lp, gk_bfd *f, const gk_smcp *parm, int
         S.mark("run done");
         f->upd_cnt = S.hs.upd_cnt;
         f->stats.evals_skipped = S.evals_skipped;
+        if (f->shard) f->stats.shard_exchanges = f->shard->exchanges - shard_ex0;
         if (ret == 0 || (ret >= 6 && ret <= 9)) S.save_resident();
         S.swap_spare();
         S.mark("exit");
@@ -3448,9 +3454,11 @@ static int spx_entry(gk_ctx *ctx, gk_lp *lp, gk_bfd *f, const gk_smcp *parm, int
         return ret;
     } catch (const AbiError &e) {
         g_err = e.msg;
+        if (f && f->shard) shard_abort(*f->shard);
         return GK_EABI;
     } catch (const std::exception &e) {
         g_err = e.what();
+        if (f && f->shard) shard_abort(*f->shard);
         return GK_EABI;
     }
 }
@@ -3470,7 +3478,11 @@ int gk_bfd_set_comm(gk_bfd *f, gk_comm *comm)
         if (!comm) return 0;
         int rank = 0;
         const int size = gk_comm_size_rank(comm, &rank);
-        if (size <= 1) return 0;
+        static const bool one_rank = [] {          // test knob: the exchange with one rank
+            const char *e = std::getenv("GK_SHARD_ONE_RANK");
+            return e && std::atoi(e) != 0;
+        }();
+        if (size < 1 || (size == 1 && !one_rank)) return 0;
         f->shard = new LpShard;
         f->shard->comm = comm;
         f->shard->rank = rank;

@@ -247,7 +247,14 @@ struct LpShard {
 int gk_comm_allgather_dev(::gk_comm *c, const void *dsend, size_t bytes, void *drecv, hipStream_t s,
                           void *hsend, void *hrecv);
 int gk_comm_size_rank(const ::gk_comm *c, int *rank);
+void gk_comm_abort(::gk_comm *c);
 void lp_shard_trow(hipStream_t s, const SpxDev &d);
+// a host decision every rank of the shard takes together: true when any
+// rank's flag is set (one all-gather of a byte); throws if the exchange fails
+bool shard_any(LpShard &sh, bool flag);
+// a rank-local failure of the sharded LP: the communicator is aborted so
+// that the peers' exchanges fail instead of waiting (gk_comm_abort)
+void shard_abort(LpShard &sh);
 bool lp_force_colpass();                     // GK_FORCE_COLPASS: the sharded plan on one GPU (comparisons)
 constexpr int PANEL_MAX = 32;
 constexpr int TRACE_KERNELS = 8, TRACE_BLOCKS = 2048;   // trace[(kid * TRACE_BLOCKS + block) * 2 + {0, 1}]

@@ -177,6 +177,9 @@ int panel_wanted(const SpxDev &d, const DualPlan &pl)
     const char *em = std::getenv("GK_PANEL_MIN_M");
     const int min_m = em ? std::atoi(em) : 1024;
     if (d.m < min_m || k < 2) return 0;
+    // (panel_pick_dev gathers the 4 cdiv(m, 256) chuzr candidates in an LDS
+    // array of 1024: m <= 65536, the explicit inverse's range)
+    if (4 * cdiv(d.m, 256) > 1024) return 0;
     return k;
 }
 

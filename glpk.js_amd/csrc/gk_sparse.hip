@@ -2361,7 +2361,14 @@ void sp_ahead_start(SpFactor &F, int m, const int *head1, const int *Aptr, const
     H->ret = 1;
     F.ahead_mark = mark;
     F.ahead = std::thread([H, m, piv_tol, piv_lim, eps_tol] {
-        sp_prepare(*H, m, H->cptr, H->crow, H->cval, piv_tol, piv_lim, eps_tol);
+        // (an exception must not leave the thread: std::terminate would end
+        // a process that holds the GPU; a failed look-ahead is ret != 0 and
+        // the caller factorizes synchronously)
+        try {
+            sp_prepare(*H, m, H->cptr, H->crow, H->cval, piv_tol, piv_lim, eps_tol);
+        } catch (...) {
+            H->ret = 1;
+        }
     });
 }
 
@@ -2403,7 +2410,9 @@ int sp_ahead_install(SpFactor &F, hipStream_t s, int cnt, const int *Acptr, cons
     F.ahead_mark = -1;
     *t_wait = sp_now() - t0;
     if (cnt < 0) cnt = sp_log_count(F, s);
-    if (F.nxt->ret || F.nxt->m != F.m || cnt < mark || cnt - mark > SP_KMAX) return -1;
+    // (cnt > SP_KMAX: k_sp_update logs only the first SP_KMAX pivots of a
+    // chain, so a longer one cannot be replayed from the log)
+    if (F.nxt->ret || F.nxt->m != F.m || cnt < mark || cnt > SP_KMAX || cnt - mark > SP_KMAX) return -1;
     const int nrep = cnt - mark;
     if (nrep > 0)
         SPCHK(hipMemcpyAsync(F.prep.p, F.plog.p + 2 * mark, (size_t)2 * nrep * sizeof(int), hipMemcpyDeviceToDevice, s));

@@ -104,7 +104,7 @@ class SpxStats(C.Structure):
                 ("panel_hits", C.c_longlong), ("panel_refills", C.c_longlong),
                 ("refine_tries", C.c_longlong), ("refinements", C.c_longlong), ("refine_steps", C.c_longlong),
                 ("refine_resid_max", C.c_double), ("factor_sparse", C.c_int), ("lu_ahead", C.c_int),
-                ("seconds_lu", C.c_double)]
+                ("seconds_lu", C.c_double), ("shard_exchanges", C.c_longlong)]
 
 
 _lib = None
@@ -119,7 +119,7 @@ EXPORTS = ["gk_abi_version", "gk_device_count", "gk_ctx_create", "gk_ctx_destroy
            "gk_ios_driver_comm", "gk_comm_set_option", "gk_npp_create", "gk_npp_destroy", "gk_npp_load",
            "gk_npp_simplex", "gk_npp_integer", "gk_npp_build_size", "gk_npp_build", "gk_npp_postprocess",
            "gk_npp_unload_sol", "gk_npp_unload_mip", "gk_sp_selftest", "gk_comm_incumbent",
-           "gk_comm_shared_incumbent", "gk_bfd_set_comm"]
+           "gk_comm_shared_incumbent", "gk_bfd_set_comm", "gk_build_stamp"]
 
 # gk_report_fn (glpk_mi355x.h): one progress line or termination message of
 # a gk_spx_* call, in the order the reference prints them
@@ -137,6 +137,14 @@ def load_library(path: str = LIB_PATH):
         raise GkError(f"{path} is missing: build it with __graft_entry__.build()")
     L = C.CDLL(path)
     P = C.c_void_p
+    L.gk_build_stamp.restype = C.c_char_p
+    if "GK_LIB_PATH" not in os.environ and os.path.isdir(os.path.join(HERE, "csrc")):
+        # the library must be the build of the sources beside it (stamp.py)
+        from . import stamp as _stamp
+        want, got = _stamp.source_stamp(), L.gk_build_stamp().decode()
+        if got != want:
+            raise GkError(f"{path} was built from other sources (stamp {got}, sources {want}): "
+                          "rebuild it with __graft_entry__.build()")
     L.gk_abi_version.restype = C.c_int
     L.gk_device_count.restype = C.c_int
     L.gk_ctx_create.restype = P

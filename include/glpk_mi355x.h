@@ -40,7 +40,7 @@
 extern "C" {
 #endif
 
-#define GK_ABI_VERSION 10
+#define GK_ABI_VERSION 11
 #include <stddef.h>
 #define GK_EABI (-1)          /* contract violation; see gk_last_error() */
 
@@ -234,6 +234,8 @@ typedef struct {
     int factor_sparse;          /* 1: the sparse LU (gk_sparse.hip), 0: the explicit inverse */
     int lu_ahead;               /* sparse refactorizations taken from the look-ahead thread */
     double seconds_lu;          /* host wall time of the Markowitz LU factorizations (all threads) */
+    /* ABI 11: column-sharded pricing (gk_bfd_set_comm) */
+    long long shard_exchanges;  /* pivot-row all-gathers of the call (0 when not sharded) */
 } gk_spx_stats;
 void gk_bfd_last_stats(const gk_bfd *bfd, gk_spx_stats *st);
 /* record HIP events around the pivot-row kernel of every dual pivot (benches) */
@@ -409,8 +411,18 @@ int gk_ios_driver_comm(gk_ctx *ctx, gk_mip *mip, const gk_iocp *parm, gk_comm *c
  * comm — RCCL on the engine's stream between distinct GPUs, TCP otherwise —
  * so every rank takes the pivots the single-GPU column pass takes.  Every
  * rank of comm makes the same gk_spx_dual calls on the same problem.  Dense
- * A, dual simplex; comm = NULL turns it off.  0 or GK_EABI. */
+ * A, dual simplex; comm = NULL turns it off (so does a one-rank comm, unless
+ * GK_SHARD_ONE_RANK=1 — a test knob that runs the exchange with one rank).
+ * Stops are collective: tm_lim is decided by all-gathering every rank's
+ * time-limit flag at each batch boundary (any rank's stops all); a failure
+ * on one rank (GK_EABI) aborts comm, so the peers' next exchange fails and
+ * they return GK_EABI too instead of waiting.  0 or GK_EABI. */
 int gk_bfd_set_comm(gk_bfd *bfd, gk_comm *comm);
+
+/* the source stamp the library was built from (16 hex digits of a hash of
+ * its HIP / C++ sources and headers, glpk.js_amd/stamp.py); the Python host
+ * refuses a library whose stamp is not its sources' */
+const char *gk_build_stamp(void);
 
 /* glp_scale_prob (glpscl.js:1-225) on the device: the
  * row and column scale factors of A (CSC: ptr[0..n] 0-based offsets, ind[]

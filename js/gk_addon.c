@@ -589,6 +589,7 @@ static napi_value js_stats(napi_env env, napi_callback_info info)
     set_num(env, o, "panel_refills", (double)st.panel_refills);
     set_num(env, o, "factor_sparse", (double)st.factor_sparse);
     set_num(env, o, "seconds_lu", st.seconds_lu);
+    set_num(env, o, "shard_exchanges", (double)st.shard_exchanges);
     return o;
 }
 

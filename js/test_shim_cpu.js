@@ -11,7 +11,7 @@ var names = ['create', 'deviceCount', 'abiVersion', 'lastError', 'bfdCreate', 'b
              'evalTabRows', 'nppCreate', 'nppLoad', 'nppSimplex', 'nppInteger', 'nppBuildSize', 'nppBuild',
              'nppPostprocess', 'nppUnloadSol', 'nppUnloadMip'];
 names.forEach(function (k) { assert.strictEqual(typeof core.addon[k], 'function', k); });
-assert.strictEqual(core.addon.abiVersion(), 10);
+assert.strictEqual(core.addon.abiVersion(), 11);
 
 var ref = process.env.GLPK_REF || '/root/reference';
 var fs = require('fs');

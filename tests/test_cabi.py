@@ -41,7 +41,7 @@ def test_library_exports_symbol(lib, name):
 
 def test_abi_version():
     L = gk.load_library()
-    assert L.gk_abi_version() == 10
+    assert L.gk_abi_version() == 11
 
 
 def test_no_cpu_fallback_without_device():

@@ -132,7 +132,7 @@ def _mip_worker(rank, size, port, name, ramp, q, iocp=None):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("name,ramp", [("gap", 0), ("gap", -1), ("c5s_12x30", 0), ("c5s_12x20", -1), ("c5s_12x40", 0)])
+@pytest.mark.parametrize("name,ramp", [("gap", 0), ("gap", -1), ("c5s_12x30", 0), ("c5s_12x20", -1), ("c5s_12x40", 0), ("c5s_12x42", 0)])
 def test_gpu_sharded_bnb_library_comm(name, ramp):
     d = load_golden(os.path.join(os.path.dirname(__file__), "golden", f"mip_{name}.json"))
     ref = d["mip"]

@@ -63,6 +63,55 @@ def _single():
     return json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
 
 
+def _rccl_worker(port, q):
+    """One rank, GK_COMM_RCCL, the exchange forced on (GK_SHARD_ONE_RANK):
+    every pivot row goes through ncclAllGather on the engine's stream."""
+    try:
+        os.environ["GK_SHARD_ONE_RANK"] = "1"
+        sys.path.insert(0, ROOT)
+        import torch
+        import torch.distributed as dist
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK="0", WORLD_SIZE="1")
+        torch.cuda.set_device(0)
+        dist.init_process_group("nccl", rank=0, world_size=1)
+        import __graft_entry__
+        __graft_entry__.load_package()
+        from glpk_js_amd import gk, problems
+        ctx = gk.Context(0)
+        comm = gk.Comm(ctx, 0, 1, f"127.0.0.1:{port + 1}", gk.GK_COMM_RCCL)
+        P = gk.GkProblem(ctx, problems.gen_dense(1024, 4096, seed=42))
+        P.set_comm(comm)
+        ret = gk.glp_simplex(P, gk.SMCP(meth=gk.GLP_DUAL, msg_lev=gk.GLP_MSG_ERR))
+        ex = int(P.stats().shard_exchanges)
+        q.put((0, comm.backend, ret, P.it_cnt, float(P.obj_val).hex(), ex))
+        del P
+        comm.close()
+        dist.destroy_process_group()
+    except Exception as e:                       # noqa: BLE001 (reported to the parent)
+        q.put((0, -1, repr(e), None, None, None))
+
+
+@pytest.mark.gpu
+def test_gpu_lp_column_sharded_rccl_one_rank():
+    """The RCCL branch of the sharded exchange (gk_comm_allgather_dev: the
+    all-gather on the engine's stream, no host round trip) on hardware: one
+    RCCL rank with the exchange forced on takes the single-GPU column-pass
+    pivots, bit for bit, and every dual pivot's row went through it."""
+    single = _single()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_rccl_worker, args=(free_port(), q))
+    p.start()
+    rank, backend, ret, it_cnt, obj, ex = q.get(timeout=240)
+    p.join(timeout=60)
+    assert backend != -1, ret
+    from glpk_js_amd import gk
+    assert backend == gk.GK_COMM_RCCL
+    assert (ret, it_cnt, obj) == (single["ret"], single["it_cnt"], single["obj"]), (ret, it_cnt, obj, single)
+    assert ex > 0, ex
+    print("rccl one rank: pivots", it_cnt, "exchanges", ex)
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("size", [2, 3])
 def test_gpu_lp_column_sharded_same_pivots(size):

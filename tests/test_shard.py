@@ -123,7 +123,7 @@ def _bnb_worker(rank, world, port, names, q, ramp=0):
 
 @pytest.mark.gpu
 def test_sharded_bnb_two_ranks_one_gpu():
-    names = ["c5s_12x20", "mixint8", "mixint11", "gap", "c5s_12x40"]
+    names = ["c5s_12x20", "mixint8", "mixint11", "gap", "c5s_12x40", "c5s_12x42"]
     res = _run_ranks(_bnb_worker, 2, (names,), 240)
     for name in names:
         ref = json.load(open(os.path.join(ROOT, "tests", "golden", f"mip_{name}.json")))["mip"]
