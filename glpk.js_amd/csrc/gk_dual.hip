@@ -2155,8 +2155,12 @@ __global__ void __launch_bounds__(256) k_dual_commit(SpxDev d, int pse, int nvb,
                 }
             }
             st->tk_end = 0;
-            st->bytes += rowb + 8.0 * (double)m * nwl0 + 8.0 * (double)m * (nr0 + 1) +
-                         16.0 * (double)m * (nr0 + (kp <= m ? 1 : 0)) + bytes_fixed;
+            // (rowpath 3, the sparse factor: bytes_fixed carries the whole
+            // pivot's chain-independent bytes, sp_pivot_bytes; the host adds
+            // the Schur correction's, which grow with the chain)
+            st->bytes += rowpath == 3 ? bytes_fixed
+                                      : rowb + 8.0 * (double)m * nwl0 + 8.0 * (double)m * (nr0 + 1) +
+                                            16.0 * (double)m * (nr0 + (kp <= m ? 1 : 0)) + bytes_fixed;
         }
         return;
     }
@@ -2908,6 +2912,23 @@ double launch_trow_rows(hipStream_t s, const SpxDev &d, const DualPlan &pl, int 
 
 static double bytes_fixed(const SpxDev &d) { return 96.0 * ((double)d.m + d.n); }
 
+// algorithmic bytes of a dual pivot on the sparse factor, the
+// part that does not depend on the Schur chain: 12 B per stored L / U entry
+// per sweep — the BTRAN's two sweeps once, the 2-RHS FTRAN's two sweeps once
+// (each entry read once, applied to both right-hand sides) —, the pivot
+// row's CSC column pass and update_gamma's A w over the CSR rows (12 nnz(A)
+// each), the new Y column written and the O(m + n) vectors.  The chain's
+// Y / inv(M) reads (16 m k + 8 k^2 at chain length k) are added by the host
+// per batch (sp_chain_bytes)
+double sp_pivot_bytes(const SpxDev &d)
+{
+    long long nnz_lu = 0;
+    int lv[4];
+    double tl = 0.0;
+    sp_info(d.sp, &nnz_lu, lv, &tl);
+    return 24.0 * (double)nnz_lu + 24.0 * (double)d.A.nnz + 8.0 * d.m + bytes_fixed(d);
+}
+
 void dual_batch_begin(hipStream_t s, const SpxDev &d, const DualPlan &pl)
 {
     hipLaunchKernelGGL(k_dual_prep, dim3(cdiv(std::max(d.m, d.n), 256)), dim3(256), 0, s, d,
@@ -2982,8 +3003,8 @@ void dual_iteration2(hipStream_t s, const SpxDev &d, const DualPlan &pl, hipEven
                            tiles_m, 0, ncb, 0, 0);
         hipLaunchKernelGGL(k_dual_pick, dim3(1), dim3(1024), 0, s, d, pl.pse, gn, ncb);
         sp_pivot_ftran(*d.sp, s, d.st, d.h, d.work, d.tcol, d.u, pl.pse);
-        hipLaunchKernelGGL(k_dual_commit, dim3(gv), dim3(256), 0, s, d, pl.pse, gv, tiles_m, pl.lpsu, 0,
-                           bytes_fixed(d), 0);
+        hipLaunchKernelGGL(k_dual_commit, dim3(gv), dim3(256), 0, s, d, pl.pse, gv, tiles_m, pl.lpsu, 3,
+                           sp_pivot_bytes(d), 0);
         sp_pivot_update(*d.sp, s, d.st);
         return;
     }

@@ -1922,6 +1922,10 @@ struct Spx {
     bool epi_arm(int K);
     void epi_wait();
     const char *epi_stage = nullptr;      // the epilogue's download in the staging ring
+    // the sparse factor's Schur-correction bytes of the call's dual pivots
+    // (16 m k + 8 k^2 at chain length k: Y read by the FTRAN's and the
+    // BTRAN's corrections, inv(M) once), added per batch
+    double sp_chain_bytes = 0.0;
 };
 
 __global__ void k_rsub_plain(double *y, const double *a, int n, const DState *st, int need_p)
@@ -2326,6 +2330,7 @@ int Spx::batch(int K, int rigorous)
 {
     mark("batch");
     const double t0 = now_s();
+    const int k_chain0 = hs.upd_cnt;
     struct T { gk_bfd *f; double t0; ~T() { f->stats.seconds_batches += now_s() - t0; } } tt{f, t0};
     epi_drop();
     bool armed = false;
@@ -2407,7 +2412,12 @@ int Spx::batch(int K, int rigorous)
     mark("batch done");
     f->stats.batches++;
     f->stats.pivots += hs.npiv;
-    f->stats.bytes_pivots = hs.bytes;
+    if (dual && f->sparse)
+        for (int i = 0; i < hs.npiv; i++) {
+            const double k = (double)(k_chain0 + i);
+            sp_chain_bytes += 16.0 * (double)m * k + 8.0 * k * k;
+        }
+    f->stats.bytes_pivots = hs.bytes + sp_chain_bytes;
     f->stats.trow_bytes = hs.bytes_trow;
     f->stats.trow_dev_ms = hs.trow_ticks / (double)ctx->wall_khz;
     f->stats.trow_dev_ms_b = hs.trow_ticks_b / (double)ctx->wall_khz;

@@ -164,6 +164,8 @@ struct SpFactor;
 SpFactor *sp_create();
 void sp_destroy(SpFactor *F);
 void sp_info(const SpFactor *F, long long *nnz_lu, int *levels, double *t_lu);
+// a sparse dual pivot's chain-independent algorithmic bytes (gk_dual.hip)
+double sp_pivot_bytes(const struct SpxDev &d);
 // 0, or 1 when B0 is singular; head1 1-based over (I | -A); A CSC, 0-based rows
 int sp_factorize(SpFactor &F, hipStream_t s, int m, const int *head1, const int *Aptr, const int *Aind,
                  const double *Aval, double piv_tol, int piv_lim, double eps_tol);

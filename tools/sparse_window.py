@@ -56,7 +56,10 @@ def main():
            "ret": ret, "pivots": P.it_cnt, "seconds": round(dt, 3), "pivots_per_s": round(P.it_cnt / dt, 1),
            "factor_sparse": st.factor_sparse, "refactorizations": int(st.reinversions),
            "refactor_seconds": round(st.seconds_reinvert, 3), "host_lu_seconds": round(st.seconds_lu, 3),
-           "host_lu_share": round(st.seconds_lu / dt, 4), "bytes_per_pivot": round(st.bytes_pivots / max(1, st.pivots))}
+           "host_lu_share": round(st.seconds_lu / dt, 4), "bytes_per_pivot": round(st.bytes_pivots / max(1, st.pivots)),
+           # (the sparse pivot's algorithmic bytes, DESIGN §2f, over the window's wall time)
+           "achieved_GBps": round(st.bytes_pivots / dt / 1e9, 1),
+           "frac_of_hbm_peak": round(st.bytes_pivots / dt / 1e9 / 8000.0, 4)}
     print(json.dumps(out), flush=True)
 
 
