@@ -1121,6 +1121,16 @@ size_t node_lp_lds(int m, int n, int alds = 0, int nnz = 0)
 }
 
 constexpr size_t NODE_LDS_MAX = 64 * 1024;
+// the node kernel's work area per node beyond which the node LPs go to the
+// engine (GK_BNB_ENGINE_BYTES, default 2 MiB: m (2m + n) doubles streamed by
+// one CU per pivot against the revised simplex on a factor); engine mode
+// solves ENGINE_BATCH nodes per search step
+static size_t engine_node_bytes()
+{
+    const char *e = std::getenv("GK_BNB_ENGINE_BYTES");        // (read per search: tests switch it)
+    return e ? (size_t)std::max(0LL, std::atoll(e)) : ((size_t)2 << 20);
+}
+constexpr int ENGINE_BATCH = 8;
 
 void launch_node_lp(hipStream_t s, const NodeProb &P, const NodeIO &io, int nb)
 {
@@ -1505,6 +1515,7 @@ namespace gk {
 // one glp_intopt search (ios_driver, glpios03.js:1) on one GPU
 // ---------------------------------------------------------------------------
 struct MipSolver {
+    bool engine = false;                      // engine mode: every node LP by the engine (gk_ios_driver)
     gk_ctx *ctx = nullptr;
     hipStream_t s = nullptr;
     gk_mip *mip = nullptr;
@@ -2338,13 +2349,16 @@ extern "C" int gk_ios_driver_sharded_inc(gk_ctx *ctx, gk_mip *mip, const gk_iocp
         return GK_EABI;
     }
     // node LPs up to 64 KiB keep their tableau in LDS; larger ones work in a
-    // per-node slice of HBM, batches sized to at most 8 GiB of work area
+    // per-node slice of HBM, batches sized to at most 8 GiB of work area.
+    // Past engine_node_bytes() of work area per node (the dense tableau
+    // T = inv(B)[I | -A] streamed by one workgroup per pivot no longer pays)
+    // every node LP is solved by the engine instead — ios_solve_node's
+    // glp_simplex (glpios01.js:866) on the revised simplex with its factor
+    // (the explicit inverse or the sparse LU), warm-started from the parent's
+    // final basis (MipSolver::fallback); the node kernel is not launched
     const size_t lds = node_lp_lds(m, n);
     const size_t SCRATCH_MAX = (size_t)8 << 30;
-    if (lds > SCRATCH_MAX) {
-        set_err("gk_ios_driver: node LP %d x %d needs %zu bytes of work area; at most %zu", m, n, lds, SCRATCH_MAX);
-        return GK_EABI;
-    }
+    const bool eng = lds > engine_node_bytes();
     if (hipSetDevice(gk_ctx_device(ctx)) != hipSuccess) { set_err("gk_ios_driver: hipSetDevice failed"); return GK_EABI; }
     hipStream_t s = gk_ctx_stream(ctx);
     const auto t0 = std::chrono::steady_clock::now();
@@ -2372,12 +2386,14 @@ extern "C" int gk_ios_driver_sharded_inc(gk_ctx *ctx, gk_mip *mip, const gk_iocp
     };
     for (int i = 0; i < m; i++) bnds(L.row_type[i + 1], L.row_lb[i + 1], L.row_ub[i + 1], S.rlb[i], S.rub[i]);
     for (int j = 0; j < n; j++) bnds(L.col_type[j + 1], L.col_lb[j + 1], L.col_ub[j + 1], S.clb[j], S.cub[j]);
-    S.A.assign((size_t)m * n, 0.0);
+    S.engine = eng;
+    // (engine mode: no dense copy of A — the engine reads the CSC arrays)
+    S.A.assign(eng ? 0 : (size_t)m * n, 0.0);
     for (int j = 1; j <= n; j++)
         for (int t = L.A_ptr[j]; t < L.A_ptr[j + 1]; t++) {
             const int i = L.A_ind[t];
             if (i < 1 || i > m) { set_err("gk_ios_driver: A_ind[%d] = %d; out of range", t, i); return GK_EABI; }
-            S.A[(size_t)(j - 1) * m + (i - 1)] += L.A_val[t];
+            if (!eng) S.A[(size_t)(j - 1) * m + (i - 1)] += L.A_val[t];
         }
     S.c.assign(S.N, 0.0);
     S.isint.assign(n, 0);
@@ -2399,9 +2415,14 @@ extern "C" int gk_ios_driver_sharded_inc(gk_ctx *ctx, gk_mip *mip, const gk_iocp
     }
     MipCache &Cc = *S.cache;
     Cc.dA.ensure(S.A.size()); Cc.dc.ensure(S.N); Cc.dint.ensure(n); Cc.drb.ensure(2 * (size_t)m);
-    const int BMAX = (lds <= NODE_LDS_MAX) ? 1024 : (int)std::max<size_t>(1, std::min<size_t>(1024, SCRATCH_MAX / lds));
+    // (engine mode: the batch is the order the node LPs are solved in, one
+    // after another; ENGINE_BATCH of them keeps the search order of the
+    // batched search's narrow batches)
+    const int BMAX = eng ? ENGINE_BATCH
+                         : (lds <= NODE_LDS_MAX ? 1024
+                                                : (int)std::max<size_t>(1, std::min<size_t>(1024, SCRATCH_MAX / lds)));
     S.stride = (lds + 255) / 256 * 32;                    // doubles, 256-byte aligned slices
-    if (lds > NODE_LDS_MAX) {
+    if (lds > NODE_LDS_MAX && !eng) {
         Cc.dscratch.ensure(S.stride * BMAX);
         if (!Cc.dscratch.p) { set_err("gk_ios_driver: out of memory (node work area)"); return GK_EABI; }
     }
@@ -2421,7 +2442,7 @@ extern "C" int gk_ios_driver_sharded_inc(gk_ctx *ctx, gk_mip *mip, const gk_iocp
     P.nnz = 0;
     P.rptr = P.rind = P.cptr = P.cind = nullptr;
     P.rval = P.cval = nullptr;
-    {
+    if (!eng) {
         size_t nz = 0;
         for (double v : S.A) nz += v != 0.0;
         if (nz > 0 && 2 * nz <= (size_t)m * n) {
@@ -2472,7 +2493,7 @@ extern "C" int gk_ios_driver_sharded_inc(gk_ctx *ctx, gk_mip *mip, const gk_iocp
     pool.reset(n, S.N);
     // warm start store (GK_BNB_WARM=0: every node inverts its basis;
     // GK_BNB_TAB_MB: its size limit)
-    const size_t tab_cap = [] {
+    const size_t tab_cap = eng ? (size_t)0 : [] {
         const char *w = std::getenv("GK_BNB_WARM");
         if (w && std::atoi(w) == 0) return (size_t)0;
         const char *e = std::getenv("GK_BNB_TAB_MB");
@@ -2504,7 +2525,7 @@ extern "C" int gk_ios_driver_sharded_inc(gk_ctx *ctx, gk_mip *mip, const gk_iocp
         const char *e = std::getenv("GK_BNB_DEPTH");           // (experiments) batches in flight, 1 or 2
         return e ? std::atoi(e) : 2;
     }();
-    const int depth = (size == 1) ? (depth_env == 1 ? 1 : 2) : 1;
+    const int depth = (size == 1 && !eng) ? (depth_env == 1 ? 1 : 2) : 1;
     int inflight[2] = {0, 0}, cur = 0;
     bool fail_sync = false;
     long long moved = 0;
@@ -2532,6 +2553,7 @@ extern "C" int gk_ios_driver_sharded_inc(gk_ctx *ctx, gk_mip *mip, const gk_iocp
         n_ents += (long long)bf.ents.size();
         const int nb = (int)bf.ents.size();
         bf.nb = nb;
+        if (eng) return;                                  // (engine mode: solved in process)
         const double ball = S.bestall();
         const double cut = ball < INF ? ball - parm->tol_obj * (1.0 + std::fabs(S.c0 + S.sign * ball)) : INF;
         const Layout Y(S.N, n, nb);
@@ -2619,6 +2641,35 @@ extern "C" int gk_ios_driver_sharded_inc(gk_ctx *ctx, gk_mip *mip, const gk_iocp
         t_launch += secs(tl0);
     };
     auto process = [&](BatchBuf &bf) {
+        if (eng) {
+            // engine mode: every node LP by the engine from its parent's
+            // basis, in entry order (the search's decisions as node_done
+            // takes them for a fallback node: host integrality scan and
+            // branching, no tableau, no probes)
+            const auto tp0 = std::chrono::steady_clock::now();
+            std::vector<double> fx;
+            std::vector<signed char> fso;
+            const std::vector<double> zeros(2 * (size_t)n, 0.0);
+            for (const Entry &e : bf.ents) {
+                const NodeRec &nd = e.nd;
+                if (!S.err) {
+                    S.lp_solves++;
+                    double z = 0.0;
+                    bool opt = false;
+                    const int ret = S.fallback(nd, pool.lb(nd.slot), pool.ub(nd.slot), fx, fso, z, opt);
+                    if (ret) S.err = ret;
+                    else if (opt)
+                        S.node_done(nd, z, fx.data(), fso.data(), pool.lb(nd.slot), pool.ub(nd.slot), zeros.data(), 0, 0,
+                                    false);
+                }
+                pool.release(nd.slot);
+            }
+            bf.ents.clear();
+            for (const NodeRec &c : S.next_dive) S.dive.push_back(c);
+            S.next_dive.clear();
+            t_proc += secs(tp0);
+            return;
+        }
         const auto tw0 = std::chrono::steady_clock::now();
         if (hipEventSynchronize(bf.done) != hipSuccess) { fail_sync = true; return; }
         t_wait += secs(tw0);

@@ -104,7 +104,7 @@ class SpxStats(C.Structure):
                 ("panel_hits", C.c_longlong), ("panel_refills", C.c_longlong),
                 ("refine_tries", C.c_longlong), ("refinements", C.c_longlong), ("refine_steps", C.c_longlong),
                 ("refine_resid_max", C.c_double), ("factor_sparse", C.c_int), ("lu_ahead", C.c_int),
-                ("seconds_lu", C.c_double), ("shard_exchanges", C.c_longlong)]
+                ("seconds_lu", C.c_double), ("shard_exchanges", C.c_longlong), ("ratio_redo", C.c_longlong)]
 
 
 _lib = None

@@ -221,15 +221,15 @@ function spx(lp, parm, dual, print) {
 var GLP_IV = 2, GLP_FEAS = 2, GLP_OPT = 5;
 
 // the requests the native driver serves: no callbacks (glpios03.js:533-897),
-// no cut generators / feasibility pump (they stay in JS),
-// and node LPs whose work area fits the node kernel's limit (gk_mip.hip:
-// tableau in LDS up to 64 KiB, in HBM slices beyond, at most 8 GiB per node)
+// no cut generators / feasibility pump (they stay in JS).  Any size: node LPs
+// whose tableau fits the node kernel's work area (gk_mip.hip: LDS up to
+// 64 KiB, HBM slices up to 2 MiB) run batched in it, larger ones on the
+// engine's revised simplex (gk_mip.hip engine mode)
 function nativeIos(T) {
-    var P = T.mip, parm = T.parm, m = P.m, n = P.n;
+    var parm = T.parm;
     if (parm.cb_func != null) return false;
     if (parm.gmi_cuts || parm.mir_cuts || parm.cov_cuts || parm.clq_cuts || parm.fp_heur) return false;
-    var work = 8 * (m * (2 * m + n) + 4 * (m + n) + m) + 4 * m + (m + n) + 16;
-    return work <= 8 * 1024 * 1024 * 1024;
+    return true;
 }
 
 // T = the tree of ios_create_tree: T.mip is the problem (its LP relaxation

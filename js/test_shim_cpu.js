@@ -31,10 +31,10 @@ assert.strictEqual(core.mipProgressLine(1, [3, 3, 529, 133, 284, 259, 10]), '+52
 assert.strictEqual(core.mipProgressLine(1, [3, 6, 652, 0, 261, 0, 331]), '+652: mip = 261 >= tree is empty   0.0% (0; 331)');
 assert.strictEqual(core.nativeIos({mip: {m: 2, n: 3}, parm: {cb_func: null, mip_gap: 0, gmi_cuts: 1}}), false);
 assert.strictEqual(core.nativeIos({mip: {m: 2, n: 3}, parm: {cb_func: null, mip_gap: 0}}), true);
-// node LPs beyond 64 KiB of LDS run natively too (HBM work area); only a
-// work area beyond 8 GiB per node stays with the reference's driver
+// node LPs beyond 64 KiB of LDS run natively too (HBM work area), and
+// beyond 2 MiB on the engine: no size goes back to the reference's driver
 assert.strictEqual(core.nativeIos({mip: {m: 80, n: 200}, parm: {cb_func: null, mip_gap: 0}}), true);
-assert.strictEqual(core.nativeIos({mip: {m: 30000, n: 40000}, parm: {cb_func: null, mip_gap: 0}}), false);
+assert.strictEqual(core.nativeIos({mip: {m: 30000, n: 40000}, parm: {cb_func: null, mip_gap: 0}}), true);
 glpk.glp_set_print_func(function () {});
 // the feasibility pump writes its working lp's objective and bounds
 // directly (glpios10.js:186-247): while it runs, every solve hands the

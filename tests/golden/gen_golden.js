@@ -586,6 +586,14 @@ readCase('err_norhs', ['Minimize', ' x', 'Subject To', ' x <= y', 'End', ''].joi
 [[50, 80, 0.15], [60, 90, 0.15], [70, 100, 0.1], [48, 90, 0.35]].forEach(function (s, k) {
     mipCase('mixbig' + (k + 1), function () { return genMix(300 + k, s[0], s[1], 0.15, s[2], true, true); }, null);
 });
+// node LPs past the node kernel's work-area regime (m (2m + n) doubles of
+// at least 2 MiB): glp_intopt's node LPs go to the engine (gk_mip.hip engine
+// mode); sparse, a third of the columns integer, boxed columns (--bigmip)
+if (process.argv.indexOf('--bigmip') >= 0) {
+    [[250, 400, 0.012, 0.3], [320, 480, 0.01, 0.25], [400, 600, 0.008, 0.2]].forEach(function (s, k) {
+        mipCase('sparsebig' + (k + 1), function () { return genMix(700 + k, s[0], s[1], s[2], s[3], true, true); }, null);
+    });
+}
 if (BIG) {
     lpCase('c2s', function () { return genC2s(821, 1571, 7, 42); }, {kind: 'c2s', m: 821, n: 1571, nzc: 7, seed: 42}, [3, 1], 0);
     lpCase('dense_512x2048', function () { return genDense(512, 2048, 42); }, {kind: 'dense', m: 512, n: 2048, seed: 42}, [1, 3], 0);
