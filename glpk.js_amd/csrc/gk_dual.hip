@@ -704,8 +704,11 @@ __global__ void __launch_bounds__(256) k_dual_top_grid(SpxDev d, int pcap, int p
 // (panel: the pivot row read from the pricing panel here — k_panel_trow's
 // work: the panel row of p at a structural, -rho at an auxiliary, 0 at a
 // fixed variable, stored to trow with its maximum — one launch fewer)
-__global__ void __launch_bounds__(256) k_trow_finish(SpxDev d, int pse, int panel)
+// flags: 1 — the row comes from the MFMA panel; 2 — column-sharded pricing:
+// work holds the exchanged A w, made work = ys - A w here
+__global__ void __launch_bounds__(256) k_trow_finish(SpxDev d, int pse, int flags)
 {
+    const int panel = flags & 1;
     const TraceScope trace_(d, 5);
     DState *st = d.st;
     if (st->stop) return;
@@ -747,6 +750,7 @@ __global__ void __launch_bounds__(256) k_trow_finish(SpxDev d, int pse, int pane
         const double w1 = ref1 ? tv1 : 0.0, w2 = ref2 ? tv2 : 0.0;
         if (idx < n) d.wcol[idx] = w1;
         if (idx < m) d.ys[idx] = w2;
+        if ((flags & 2) && idx < m) d.work[idx] = w2 - d.work[idx];
         gsum = w1 * w1 + w2 * w2;
     }
     // per 64-slot group (one wave): max |trow|, gamma_p partial, pass-1
@@ -3090,8 +3094,46 @@ __global__ void __launch_bounds__(1024) k_dual_update(SpxDev d, int gn, int ncb,
 // host side
 // ---------------------------------------------------------------------------
 // ---- column-sharded pricing (gk_bfd_set_comm) ---------------------------
+// The exchange block of a rank: its slice of the pivot row (L doubles), its
+// max |trow| (as bits), and with PSE its partial A w over the members of W
+// whose non-basic position is in its slice (m doubles): update_gamma's A w
+// (glpspx02.js:1103-1134) sharded like the pivot row, the partials summed in
+// rank order on every rank
+__host__ __device__ static inline int shard_blk(int L, int m, int pse) { return L + 1 + (pse ? m : 0); }
+
+// this rank's partial A w: k_dual_ratio's one-pass A w blocks (64 rows per
+// block, the 4 waves split wlist, partials in wave order) over the members
+// at positions [lo, hi) only — with one rank the sum is k_dual_ratio's, bit
+// for bit
+__global__ void __launch_bounds__(256) k_shard_aw(SpxDev d, int lo, int hi, double *out)
+{
+    __shared__ double sw[4][64];
+    const DState *st = d.st;
+    const int m = d.m, n = d.n;
+    const int lane = threadIdx.x & 63, w4 = threadIdx.x >> 6;
+    const int r = blockIdx.x * 64 + lane;
+    const int rc = min(r, m - 1);
+    const int cnt = st->nwl;
+    if (st->stop) return;
+    const double *__restrict__ A = d.A.A;
+    const size_t lda = (size_t)d.A.lda;
+    double acc = 0.0;
+    for (int t = w4; t < cnt; t += 4) {
+        const int c = d.wlist[t];
+        const int j = d.bind[m + c] - m - 1;              // its non-basic position
+        const double wv = (j >= lo && j < hi) ? d.trow[j] : 0.0;
+        acc += (r < m ? A[(size_t)c * lda + rc] : 0.0) * wv;
+    }
+    (void)n;
+    sw[w4][lane] = acc;
+    __syncthreads();
+    if (w4 == 0 && r < m) out[r] = ((sw[0][lane] + sw[1][lane]) + sw[2][lane]) + sw[3][lane];
+}
+
 // this rank's slice of the pivot row and its max |trow| (as bits) into the
-// send block; then every rank's slice into trow and the largest max
+// send block; then every rank's slice into trow and the largest max, and the
+// rank-ordered sum of the A w partials into work (k_trow_finish forms
+// work = ys - A w from it)
 __global__ void __launch_bounds__(256) k_shard_pack(const double *trow, int lo, int cnt, int L,
                                                     const unsigned long long *maxbits, double *send)
 {
@@ -3100,18 +3142,24 @@ __global__ void __launch_bounds__(256) k_shard_pack(const double *trow, int lo, 
     if (i == 0) send[L] = __longlong_as_double((long long)*maxbits);
 }
 
-__global__ void __launch_bounds__(256) k_shard_unpack(const double *recv, int size, int L, int n, double *trow,
-                                                      unsigned long long *maxbits)
+__global__ void __launch_bounds__(256) k_shard_unpack(const double *recv, int size, int L, int n, int m, int pse,
+                                                      double *trow, unsigned long long *maxbits, double *aw)
 {
     const int j = blockIdx.x * blockDim.x + threadIdx.x;
+    const int B = shard_blk(L, m, pse);
     if (j < n) {
         const int r = j / L, i = j - r * L;
-        trow[j] = recv[(size_t)r * (L + 1) + i];
+        trow[j] = recv[(size_t)r * B + i];
+    }
+    if (pse && j < m) {
+        double a = recv[(size_t)L + 1 + j];
+        for (int r = 1; r < size; r++) a += recv[(size_t)r * B + L + 1 + j];
+        aw[j] = a;
     }
     if (j == 0) {
         unsigned long long b = 0;
         for (int r = 0; r < size; r++) {
-            const unsigned long long x = (unsigned long long)__double_as_longlong(recv[(size_t)r * (L + 1) + L]);
+            const unsigned long long x = (unsigned long long)__double_as_longlong(recv[(size_t)r * B + L]);
             b = x > b ? x : b;
         }
         *maxbits = b;
@@ -3137,20 +3185,22 @@ bool lp_force_colpass()
 // every rank holds the pivot row the single-GPU column pass forms — the same
 // values, bit for bit (a column's dot product does not depend on the
 // slicing), and with them the same pivot path
-void lp_shard_trow(hipStream_t s, const SpxDev &d)
+void lp_shard_trow(hipStream_t s, const SpxDev &d, int pse)
 {
     LpShard &sh = *d.shard;
-    const int n = d.n, L = sh.L;
+    const int n = d.n, m = d.m, L = sh.L;
     const int lo = std::min(n, sh.rank * L), cnt = std::min(n, lo + L) - lo;
+    if (pse)
+        hipLaunchKernelGGL(k_shard_aw, dim3(cdiv(m, 64)), dim3(256), 0, s, d, lo, lo + cnt, sh.dsend + L + 1);
     hipLaunchKernelGGL(k_shard_pack, dim3(cdiv(L, 256)), dim3(256), 0, s, (const double *)d.trow, lo, cnt, L,
                        (const unsigned long long *)&d.st->trow_max_bits, sh.dsend);
-    const size_t bytes = (size_t)(L + 1) * sizeof(double);
+    const size_t bytes = (size_t)shard_blk(L, m, pse) * sizeof(double);
     if (gk_comm_allgather_dev(sh.comm, sh.dsend, bytes, sh.drecv, s, sh.hsend.data(), sh.hrecv.data()) != 0) {
         sh.failed = true;
         throw std::runtime_error("column-sharded pricing: the exchange failed");
     }
-    hipLaunchKernelGGL(k_shard_unpack, dim3(cdiv(n, 256)), dim3(256), 0, s, (const double *)sh.drecv, sh.size, L, n,
-                       d.trow, &d.st->trow_max_bits);
+    hipLaunchKernelGGL(k_shard_unpack, dim3(cdiv(std::max(n, m), 256)), dim3(256), 0, s, (const double *)sh.drecv,
+                       sh.size, L, n, m, pse, d.trow, &d.st->trow_max_bits, d.work);
     sh.exchanges++;
 }
 
@@ -3428,14 +3478,15 @@ void dual_iteration2(hipStream_t s, const SpxDev &d, const DualPlan &pl, hipEven
             const int lo = std::min(n, sh.rank * sh.L), hi = std::min(n, lo + sh.L);
             colpass_gated(s, d.A, CP_TROW, m + lo, hi - lo, d.head, d.stat + lo, d.coef, nullptr, d.rho, nullptr,
                           d.trow + lo, nullptr, &d.st->trow_max_bits, d.st, 0);
-            lp_shard_trow(s, d);
+            lp_shard_trow(s, d, pl.pse);
         } else
             colpass_gated(s, d.A, CP_TROW, m, n, d.head, d.stat, d.coef, nullptr, d.rho, nullptr, d.trow, nullptr,
                           &d.st->trow_max_bits, d.st, 0);
         if (ev1) (void)hipEventRecord(ev1, s);
-        hipLaunchKernelGGL(k_trow_finish, dim3(gv), dim3(256), 0, s, d, pl.pse, pl.panel ? 1 : 0);
+        hipLaunchKernelGGL(k_trow_finish, dim3(gv), dim3(256), 0, s, d, pl.pse, (pl.panel ? 1 : 0) | (d.shard ? 2 : 0));
     }
-    const int aw = (pl.pse && d.A.dense) ? 1 : 0;
+    // (sharded: A w came with the exchange; k_trow_finish formed work)
+    const int aw = (pl.pse && d.A.dense && !d.shard) ? 1 : 0;
     const int awone = (aw && pl.fused) ? pl.awone : 0;
     hipLaunchKernelGGL(k_dual_ratio, dim3(gn + (aw ? (awone ? cdiv(m, 64) : tiles_m * pl.awsplits) : 0)), dim3(256), 0,
                        s, d, gn, tiles_m, pl.rowpath, ncb, awone, prev_blocks(d, pl));

@@ -3452,19 +3452,22 @@ static int spx_entry(gk_ctx *ctx, gk_lp *lp, gk_bfd *f, const gk_smcp *parm, int
             if (sp && !f->sp) f->sp = sp_create();
             f->stats.factor_sparse = sp;
         }
-        if (f->shard && f->shard->n != f->eng->n) {
-            // the exchange's buffers for this n: slices of L = ceil(n / size)
+        if (f->shard && (f->shard->n != f->eng->n || f->shard->m != f->eng->m)) {
+            // the exchange's buffers for this n: slices of L = ceil(n / size),
+            // then max |trow| and the A w partial (m) — L + 1 + m doubles a rank
             LpShard &sh = *f->shard;
-            const int n = f->eng->n;
+            const int n = f->eng->n, m = f->eng->m;
             sh.L = (n + sh.size - 1) / sh.size;
+            const size_t blk = (size_t)sh.L + 1 + (size_t)m;
             if (sh.dsend) (void)hipFree(sh.dsend);
             if (sh.drecv) (void)hipFree(sh.drecv);
             sh.dsend = sh.drecv = nullptr;
-            HIPCHK(hipMalloc((void **)&sh.dsend, (size_t)(sh.L + 1) * sizeof(double)));
-            HIPCHK(hipMalloc((void **)&sh.drecv, (size_t)sh.size * (sh.L + 1) * sizeof(double)));
-            sh.hsend.assign((size_t)sh.L + 1, 0.0);
-            sh.hrecv.assign((size_t)sh.size * (sh.L + 1), 0.0);
+            HIPCHK(hipMalloc((void **)&sh.dsend, blk * sizeof(double)));
+            HIPCHK(hipMalloc((void **)&sh.drecv, (size_t)sh.size * blk * sizeof(double)));
+            sh.hsend.assign(blk, 0.0);
+            sh.hrecv.assign((size_t)sh.size * blk, 0.0);
             sh.n = n;
+            sh.m = m;
         }
         const long long shard_ex0 = f->shard ? f->shard->exchanges : 0;
         Spx S;

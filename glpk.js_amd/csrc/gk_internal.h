@@ -262,12 +262,14 @@ struct SpxDev {
 // column-sharded pricing of one LP (gk_bfd_set_comm): every rank
 // holds the whole problem and factor and takes the same pivots; the pivot
 // row's column pass runs over this rank's slice of the non-basic positions
-// [rank L, rank L + L), L = ceil(n / size), and the slices (with each
-// slice's max |trow|) are all-gathered before the ratio test
+// [rank L, rank L + L), L = ceil(n / size), and with PSE so does
+// update_gamma's A w (the members of W in the slice); the slices (with each
+// slice's max |trow|) and the A w partials are all-gathered before the ratio
+// test (L + 1 + m doubles per rank)
 struct LpShard {
     ::gk_comm *comm = nullptr;
-    int rank = 0, size = 1, L = 0, n = 0;
-    double *dsend = nullptr, *drecv = nullptr;  // device: L + 1 | size (L + 1) doubles
+    int rank = 0, size = 1, L = 0, n = 0, m = 0;
+    double *dsend = nullptr, *drecv = nullptr;  // device: L + 1 + m | size (L + 1 + m) doubles
     std::vector<double> hsend, hrecv;           // host staging (TCP transport)
     long long exchanges = 0;
     bool failed = false;
@@ -279,7 +281,7 @@ int gk_comm_allgather_dev(::gk_comm *c, const void *dsend, size_t bytes, void *d
                           void *hsend, void *hrecv);
 int gk_comm_size_rank(const ::gk_comm *c, int *rank);
 void gk_comm_abort(::gk_comm *c);
-void lp_shard_trow(hipStream_t s, const SpxDev &d);
+void lp_shard_trow(hipStream_t s, const SpxDev &d, int pse);
 // a host decision every rank of the shard takes together: true when any
 // rank's flag is set (one all-gather of a byte); throws if the exchange fails
 bool shard_any(LpShard &sh, bool flag);

@@ -4,14 +4,19 @@ non-basic positions of each pivot row with the column pass, and the slices
 are all-gathered before the ratio test (glpspx02.js:655-935 — eval_trow,
 sort_trow, chuzc — then run on the whole row on every rank).
 
-The column pass's value for a position does not depend on the slicing, so
-the sharded run takes the pivots of the single-GPU run with the same plan
-(GK_FORCE_COLPASS=1: column pass, no pricing panel): return code, pivot
-count and objective bits equal, on every rank, and the objective is the
-reference's 978.22910129338311 (1024 x 4096 generator, tolerance 1e-9
-relative).  Two and three ranks share the one GPU through the library's
-TCP transport (RCCL refuses two ranks on one device); three ranks do not
-divide n = 4096, so the last slice is the short one."""
+update_gamma's A w (glpspx02.js:1103-1134) is sharded the same way: each
+rank sums the members of the reference space in its slice, and the
+partials travel in the same exchange and are summed in rank order.  The
+pivot row's values do not depend on the slicing, A w's rounding does (the
+sum's association): every rank takes the same pivots (return code, pivot
+count and objective bits equal across ranks — the run is deterministic),
+and the objective is the reference's 978.22910129338311 (1024 x 4096
+generator, tolerance 1e-9 relative).  With one rank (the RCCL test) the
+sum is the single-GPU one and the run is the single-GPU column-pass run
+(GK_FORCE_COLPASS=1) bit for bit.  Two and three ranks share the one GPU
+through the library's TCP transport (RCCL refuses two ranks on one
+device); three ranks do not divide n = 4096, so the last slice is the
+short one."""
 import json
 import multiprocessing as mp
 import os
@@ -129,5 +134,9 @@ def test_gpu_lp_column_sharded_same_pivots(size):
         p.join(timeout=60)
     for rank, backend, ret, it_cnt, obj in res:
         assert backend != -1, ret
-        assert (ret, it_cnt, obj) == (single["ret"], single["it_cnt"], single["obj"]), (rank, res, single)
-    print("size", size, "pivots", single["it_cnt"], "obj", float.fromhex(single["obj"]))
+        assert (ret, it_cnt, obj) == res[0][2:], ("ranks disagree", res)
+    ret, it_cnt, obj = res[0][2:]
+    assert ret == 0
+    assert abs(float.fromhex(obj) - REF_OBJ) <= 1e-9 * REF_OBJ, (float.fromhex(obj), REF_OBJ)
+    print("size", size, "pivots", it_cnt, "obj", float.fromhex(obj), "single-GPU pivots", single["it_cnt"],
+          "bits equal to single", (ret, it_cnt, obj) == (single["ret"], single["it_cnt"], single["obj"]))
