@@ -1133,7 +1133,7 @@ __global__ void __launch_bounds__(1024) k_dual_row(SpxDev d, int pse, int nr_cap
     int pos2 = d.bind[min(idx, m - 1)];
     // the W position of structural idx (its pivot-row value goes to twW for
     // k_dual_update's T = inv(B) A_W)
-    const int wposi = pse ? d.wpos[min(idx, n - 1)] : -1;
+    const int wposi = (pse && fold) ? d.wpos[min(idx, n - 1)] : -1;
     // the wave's rows of AT depend on the list alone: issued now, in flight
     // while the chuzr choice below resolves (the rho entries wait for it)
     const double *__restrict__ col = d.A.AT + min(idx, n - 1);
@@ -2706,7 +2706,7 @@ __global__ void __launch_bounds__(1024) k_dual_update(SpxDev d, int gn, int ncb,
         rv[u] = d.rho_val[t];
     }
     // T = inv(B) A_W at the block's rows, and the pivot row over W (twm)
-    const int twv = (NRHS == 2 && twm) ? st->tw_valid : 0, nwl_e = (NRHS == 2 && twm) ? st->nwl : 0;
+    const int twv = (NRHS == 2 && FOLD) ? st->tw_valid : 0, nwl_e = (NRHS == 2 && FOLD) ? st->nwl : 0;
     // (twm 2) this thread's share of (T w)_r, subtracted from its share of u
     double uT = 0.0;
     if (NRHS == 2 && FOLD) {
@@ -2789,7 +2789,7 @@ __global__ void __launch_bounds__(1024) k_dual_update(SpxDev d, int gn, int ncb,
     const double ua_l = SP ? 0.0 : hcolv[kou];
     const double ub_l = (NRHS == 2) ? uv[kou] : 0.0;
     // W position of the entering variable (twm: T's column to drop)
-    const int wq_l = (NRHS == 2 && twm) ? d.wpos[min(max(kqc - m, 1), n) - 1] : -1;
+    const int wq_l = (NRHS == 2 && FOLD) ? d.wpos[min(max(kqc - m, 1), n) - 1] : -1;
     const int tkp = d.type[kp - 1];
     const bool refkp = NRHS == 2 && d.refsp[kp - 1] != 0;
     const int knew = (r == p - 1) ? kqc : kold;
@@ -2950,7 +2950,7 @@ __global__ void __launch_bounds__(1024) k_dual_update(SpxDev d, int gn, int ncb,
     // fits the positions the blocks' threads cover
     const bool wout_t = kq > m && wq_l >= 0, win_t = kp > m && refkp && tkp != FX;
     const int nw1_t = nwl_e - (wout_t ? 1 : 0), nwa_t = nw1_t + (win_t ? 1 : 0);
-    const bool tw_keep = NRHS == 2 && twm && (twv || nwl_e == 0) && nwa_t <= min(TW_CAP, GM * NSL);
+    const bool tw_keep = NRHS == 2 && FOLD && twm && (twv || nwl_e == 0) && nwa_t <= min(TW_CAP, GM * NSL);
     if (bk && w == wa && lane == 0) {
         gate_wait(st);
         books_store<NRHS>(d, sbk, kp, kq, tkp, refkp, nr, ns, rowpath, bytes_fixed, tw_keep ? 1 : 0);
@@ -3204,13 +3204,15 @@ void lp_shard_trow(hipStream_t s, const SpxDev &d, int pse)
     sh.exchanges++;
 }
 
-// GK_FOLD=0: the three-kernel pivot everywhere (k_dual_row, k_dual_ratio,
-// k_dual_update), T not kept (A / B comparisons)
+// GK_FOLD=1: the two-kernel pivot where the plan allows it (experiment,
+// off by default: measured slower on C3, DESIGN §4 — the last block's tail
+// costs what k_dual_ratio's launch did, and 8-row update blocks double the
+// chuzr candidates k_dual_row reduces)
 bool fold_enabled()
 {
     static const bool on = [] {
         const char *e = std::getenv("GK_FOLD");
-        return !e || std::atoi(e) != 0;
+        return e && std::atoi(e) != 0;
     }();
     return on;
 }

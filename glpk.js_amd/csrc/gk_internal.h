@@ -324,7 +324,7 @@ struct DualPlan {
 void dual_batch_begin(hipStream_t s, const SpxDev &d, const DualPlan &pl);
 void dual_batch_end(hipStream_t s, const SpxDev &d, const DualPlan &pl);
 DualPlan dual_plan(const SpxDev &d, int nr_max, int nwl_max, int pse, int rigorous);
-bool fold_enabled();                         // GK_FOLD (default on): the two-kernel pivot and T
+bool fold_enabled();                         // GK_FOLD=1 (default off): the two-kernel pivot and T
 // ev0/ev1, ev2/ev3 (optional, eager launches only): the start / stop events
 // of the pivot-row kernel and of the fused update kernel (hipExtLaunchKernelGGL:
 // the command processor's timestamps of the dispatch itself, as a profiler's)

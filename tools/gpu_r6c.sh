@@ -6,3 +6,4 @@ timeout -k 10 600 python3 -u -m pytest -x -v --timeout 240 --timeout-method thre
 echo "tests rc $?" >> $O/tests.log
 timeout -k 10 200 python3 -u bench.py --no-cpu --no-extra > $O/bench_fold.json 2> $O/bench_fold.err || exit 2
 GK_FOLD=0 timeout -k 10 200 python3 -u bench.py --no-cpu --no-extra > $O/bench_nofold.json 2> $O/bench_nofold.err || exit 3
+timeout -k 10 400 python3 -u -m pytest -x -v --timeout 300 --timeout-method thread tests/test_lp_shard.py -s > $O/shard.log 2>&1 || exit 4
