@@ -636,7 +636,7 @@ def run_mid_sharded(gk, ctx, c3, comm, start=100000, steps=10):
             "backend": {1: "tcp", 2: "rccl"}.get(comm.backend, comm.backend)}
 
 
-def run_bnb(gk, problems, ctx, names=("gap", "c5s_12x30", "c5s_12x40", "c5s_12x42"), comm=None):
+def run_bnb(gk, problems, ctx, names=("gap", "c5s_12x30", "c5s_12x40", "c5s_12x42", "sparsebig4"), comm=None):
     """B&B configs (BASELINE.json configs[3], C5s surrogate of configs[4]):
     root glp_simplex + glp_intopt on the device; LP-relaxations/s = node LP
     solves (all ranks) / wall time of glp_intopt."""

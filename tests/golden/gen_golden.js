@@ -590,7 +590,7 @@ readCase('err_norhs', ['Minimize', ' x', 'Subject To', ' x <= y', 'End', ''].joi
 // at least 2 MiB): glp_intopt's node LPs go to the engine (gk_mip.hip engine
 // mode); sparse, a third of the columns integer, boxed columns (--bigmip)
 if (process.argv.indexOf('--bigmip') >= 0) {
-    [[250, 400, 0.012, 0.3], [320, 480, 0.01, 0.25], [400, 600, 0.008, 0.2]].forEach(function (s, k) {
+    [[250, 400, 0.012, 0.1], [320, 480, 0.01, 0.08], [400, 600, 0.008, 0.06], [800, 1200, 0.004, 0.05]].forEach(function (s, k) {
         mipCase('sparsebig' + (k + 1), function () { return genMix(700 + k, s[0], s[1], s[2], s[3], true, true); }, null);
     });
 }
