@@ -1255,6 +1255,8 @@ struct NodeMeta {
     double up_lpobj = 0.0;        // the parent's LP objective (minimisation form)
     double up_bound = 0.0;        // the parent's local bound (best projection)
     double up_ii = 0.0;           // the parent's sum of integer infeasibilities
+    double lpz = 0.0;             // its own LP objective estimate (minimisation form): the parent's
+                                  // objective plus the branch's degradation (branch_on's node.lp_obj)
 };
 
 // an open node: its local bound, the selection keys of the backtracking
@@ -1609,12 +1611,29 @@ struct MipSolver {
             if (bestall() == DBL_MAX || !root_seen || root_ii <= 0.0) r.key = mt.up_ii;   // most_feas
             else r.key = mt.up_bound + (bestall() - root_bound) / root_ii * mt.up_ii;  // best_proj
             break;
-        default:                                                    // BLB: best local bound,
-            r.key = r.bound;                                        // then the parent's ii_sum
-            r.key2 = mt.up_ii;
-            break;
+        default:                                                    // BLB: best local bound, then
+            r.key = r.bound;                                        // (best_node, glpios12.js:49) the
+            r.key2 = sign > 0 ? mt.up_ii : mt.lpz;                  // parent's ii_sum (MIN) or the best
+            break;                                                  // lp_obj (MAX)
         }
     }
+    // best_node's window (glpios12.js:49-87): the subproblems whose local
+    // bound is within 0.001 (1 + |bound|) of the best are equally good, and
+    // among them the one with the least parent ii_sum (minimisation) or the
+    // best lp_obj (maximisation) is chosen, the earliest created on ties.
+    // Applied while the open list is short enough that the window's scan is
+    // cheap (GK_BNB_BLB_WINDOW: its size limit, 0 off; a deep tree's frontier
+    // keeps the plain bound order)
+    static int blb_window_max()
+    {
+        static const int v = [] {
+            const char *e = std::getenv("GK_BNB_BLB_WINDOW");
+            return e ? std::max(0, std::atoi(e)) : 4096;
+        }();
+        return v;
+    }
+    double window_eps(double key) const { return 0.001 * (1.0 + std::fabs(c0 + sign * key)); }
+    std::vector<NodeRec> win_buf;
     void push_open(NodeRec r)
     {
         const unsigned long long t0 = tsc_on ? tsc() : 0ull;
@@ -1623,12 +1642,28 @@ struct MipSolver {
         std::push_heap(open.begin(), open.end(), NodeWorse());
         if (tsc_on) tsc_heap += tsc() - t0;
     }
-    NodeRec pop_open()
+    NodeRec pop_heap1()
     {
         std::pop_heap(open.begin(), open.end(), NodeWorse());
         NodeRec r = open.back();
         open.pop_back();
         return r;
+    }
+    NodeRec pop_open()
+    {
+        const int wmax = blb_window_max();
+        if (parm->bt_tech != 3 || wmax == 0 || (int)open.size() > wmax || open.size() < 2) return pop_heap1();
+        NodeRec best = pop_heap1();
+        const double lim = best.key + window_eps(best.key);
+        win_buf.clear();
+        while (!open.empty() && open.front().key <= lim) win_buf.push_back(pop_heap1());
+        for (NodeRec &r : win_buf)
+            if (r.key2 < best.key2 || (r.key2 == best.key2 && r.seq < best.seq)) std::swap(best, r);
+        for (const NodeRec &r : win_buf) {
+            open.push_back(r);
+            std::push_heap(open.begin(), open.end(), NodeWorse());
+        }
+        return best;
     }
     // the best projection keys depend on the incumbent
     void rekey()
@@ -1814,6 +1849,7 @@ struct MipSolver {
             cm.up_lpobj = z;
             cm.up_bound = bound;
             cm.up_ii = ii;
+            cm.lpz = z + dz[kase];
             NodeRec c{cb, 0.0, 0.0, seq++, sl};
             set_keys(c);
             if (!dived) {
@@ -1896,6 +1932,7 @@ struct MipSolver {
             cm.up_lpobj = z;
             cm.up_bound = pl.bound;
             cm.up_ii = pl.ii;
+            cm.lpz = z + pl.dz[kase];
             NodeRec c{pl.cb[kase], 0.0, 0.0, seq++, sl};
             if (!dived) {
                 set_keys(c);
@@ -2058,6 +2095,21 @@ struct MipSolver {
     // GLP_EFAIL.
     int fallback(const NodeRec &nd, const double *bl, const double *bu, std::vector<double> &x,
                  std::vector<signed char> &so, double &z, bool &opt);
+    // engine mode: what the node kernel returns besides the solution, from
+    // the engine's factor of the node's optimal basis — the fractional
+    // columns, ios_eval_degrad's degradations of every one of them
+    // (glpios01.js:615, minimisation form, DBL_MAX: that branch is
+    // infeasible) and branch_drtom's choice (glpios09.js:84; 0 when its
+    // degradation is negligible: the host takes the most fractional)
+    struct Degrad {
+        std::vector<int> cand;
+        double ii = 0.0;
+        std::vector<double> dz;               // 2 n: down | up per column
+        int kjj = 0, knext = 0;
+        bool ok = false;
+    } dg;
+    void engine_degrad(gk_lp &L, const std::vector<double> &x, const std::vector<signed char> &so, const double *bl,
+                       const double *bu);
 };
 
 int gk_spx_node(gk_ctx *ctx, gk_lp *lp, gk_bfd *bfd, const gk_smcp *parm);
@@ -2133,9 +2185,106 @@ int MipSolver::fallback(const NodeRec &nd, const double *bl, const double *bu, s
         z = sign * (L.obj_val - c0);
         pivots += L.it_cnt;
         opt = true;
+        if (engine) engine_degrad(L, x, so, bl, bu);
         return 0;
     }
     return 5;                                         // GLP_EFAIL (ios_driver, glpios03.js:669-673)
+}
+
+void MipSolver::engine_degrad(gk_lp &L, const std::vector<double> &x, const std::vector<signed char> &so,
+                              const double *bl, const double *bu)
+{
+    Degrad &D = dg;
+    D.ok = false;
+    D.kjj = 0;
+    D.knext = 0;
+    (void)integrality(x.data(), so.data(), bl, bu, D.cand, D.ii);
+    D.dz.assign(2 * (size_t)n, 0.0);
+    const int nk = (int)D.cand.size();
+    if (nk == 0) { D.ok = true; return; }
+    // the tableau rows of the fractional basic columns (glp_eval_tab_row),
+    // one pass on the engine's factor of this node's final basis
+    std::vector<int> kk(nk);
+    for (int t = 0; t < nk; t++) kk[t] = m + D.cand[t] + 1;
+    const int N1 = m + n;
+    std::vector<double> alfa((size_t)nk * N1);
+    if (gk_bfd_eval_tab_rows(fb, &L, nk, kk.data(), alfa.data(), 0) != 0) return;
+    const double obj = (L.dir == 1) ? +1.0 : -1.0;   // GLP_MIN = 1
+    auto stat_of = [&](int k) { return k <= m ? L.row_stat[k] : L.col_stat[k - m]; };
+    auto dual_of = [&](int k) { return k <= m ? L.row_dual[k] : L.col_dual[k - m]; };
+    // glp_dual_rtest (glpapi12.js:687) over the row's non-zeros in variable order
+    auto rtest = [&](const double *row, int dir, double &alfa_k) {
+        int piv = 0;
+        double teta = DBL_MAX, big = 0.0;
+        for (int k = 1; k <= N1; k++) {
+            const double v = row[k - 1];
+            if (v == 0.0) continue;
+            const int st = stat_of(k);
+            if (st == BS) continue;
+            const double a = dir > 0 ? v : -v, cost = dual_of(k);
+            double temp;
+            if (st == NL) { if (a < 1e-9) continue; temp = (obj * cost) / a; }
+            else if (st == NU) { if (a > -1e-9) continue; temp = (obj * cost) / a; }
+            else if (st == NF) { if (-1e-9 < a && a < 1e-9) continue; temp = 0.0; }
+            else continue;                                    // NS
+            if (temp < 0.0) temp = 0.0;
+            if (teta > temp || (teta == temp && big < std::fabs(a))) {
+                piv = k;
+                teta = temp;
+                big = std::fabs(a);
+                alfa_k = v;
+            }
+        }
+        return piv;
+    };
+    // the reduced cost of x[k] with the sign correction of a degenerate basis
+    auto dk_of = [&](int k) {
+        const int st = stat_of(k);
+        double d = dual_of(k);
+        if (obj > 0) { if ((st == NL && d < 0.0) || (st == NU && d > 0.0) || st == NF) d = 0.0; }
+        else if ((st == NL && d > 0.0) || (st == NU && d < 0.0) || st == NF) d = 0.0;
+        return d;
+    };
+    int jj = -1, next = 0;
+    double degrad = -1.0;
+    const double objv = L.obj_val;
+    for (int t = 0; t < nk; t++) {
+        const int j = D.cand[t];
+        const double *row = alfa.data() + (size_t)t * N1;
+        const double beta = x[m + j];
+        double dz_e[2], dz_t[2];                               // eval_degrad / branch_drtom (Tomlin)
+        for (int c = 0; c < 2; c++) {
+            const int kase = c == 0 ? -1 : +1;
+            double a = 0.0;
+            const int k = rtest(row, kase, a);
+            if (k == 0) {
+                dz_e[c] = dz_t[c] = obj * DBL_MAX;
+                continue;
+            }
+            const double dj = (kase < 0 ? std::floor(beta) : std::ceil(beta)) - beta;
+            const double g = dk_of(k);
+            dz_e[c] = g * (dj / a);
+            double dkk = dj / a;
+            if (k > m && mip->col_kind[k - m] != 1) {       // Tomlin: an integer x[k] moves by at least one
+                if (std::fabs(dkk - std::floor(dkk + 0.5)) > 1e-3) dkk = dkk > 0.0 ? std::ceil(dkk) : std::floor(dkk);
+            }
+            dz_t[c] = g * dkk;
+        }
+        // minimisation-form degradations of the two branches (the bounds)
+        for (int c = 0; c < 2; c++)
+            D.dz[2 * (size_t)j + c] = (std::fabs(dz_e[c]) == DBL_MAX) ? DBL_MAX : std::max(0.0, obj * dz_e[c]);
+        if (degrad < std::fabs(dz_t[0]) || degrad < std::fabs(dz_t[1])) {
+            jj = j;
+            if (std::fabs(dz_t[0]) < std::fabs(dz_t[1])) { next = -1; degrad = std::fabs(dz_t[1]); }
+            else { next = +1; degrad = std::fabs(dz_t[0]); }
+            if (degrad == DBL_MAX) break;
+        }
+    }
+    if (jj >= 0 && !(degrad < 1e-6 * (1.0 + 0.001 * std::fabs(objv)))) {
+        D.kjj = jj + 1;
+        D.knext = next;
+    }
+    D.ok = true;
 }
 
 static void setup_rounding(MipSolver &S, const gk_mip *mip)
@@ -2647,7 +2796,7 @@ extern "C" int gk_ios_driver_sharded_inc(gk_ctx *ctx, gk_mip *mip, const gk_iocp
             // takes them for a fallback node: host integrality scan and
             // branching, no tableau, no probes)
             const auto tp0 = std::chrono::steady_clock::now();
-            std::vector<double> fx;
+            std::vector<double> fx, fb(2 * (size_t)n);
             std::vector<signed char> fso;
             const std::vector<double> zeros(2 * (size_t)n, 0.0);
             for (const Entry &e : bf.ents) {
@@ -2656,11 +2805,22 @@ extern "C" int gk_ios_driver_sharded_inc(gk_ctx *ctx, gk_mip *mip, const gk_iocp
                     S.lp_solves++;
                     double z = 0.0;
                     bool opt = false;
-                    const int ret = S.fallback(nd, pool.lb(nd.slot), pool.ub(nd.slot), fx, fso, z, opt);
+                    // (the node's bounds copied out: branching allocates pool
+                    // slots, which may move the pool's arrays)
+                    std::memcpy(fb.data(), pool.lb(nd.slot), n * sizeof(double));
+                    std::memcpy(fb.data() + n, pool.ub(nd.slot), n * sizeof(double));
+                    const int ret = S.fallback(nd, fb.data(), fb.data() + n, fx, fso, z, opt);
                     if (ret) S.err = ret;
-                    else if (opt)
-                        S.node_done(nd, z, fx.data(), fso.data(), pool.lb(nd.slot), pool.ub(nd.slot), zeros.data(), 0, 0,
-                                    false);
+                    else if (opt) {
+                        // the tableau's degradations and branch_drtom's choice
+                        // (engine_degrad) as the node kernel returns them;
+                        // pseudocost branching without probes
+                        const MipSolver::Degrad &D = S.dg;
+                        const bool tab = D.ok && parm->br_tech != 5;
+                        S.node_done(nd, z, fx.data(), fso.data(), fb.data(), fb.data() + n,
+                                    tab ? D.dz.data() : zeros.data(), tab ? D.kjj : 0, tab ? D.knext : 0, tab,
+                                    D.ok ? D.cand.data() : nullptr, D.ok ? (int)D.cand.size() : -1, D.ii);
+                    }
                 }
                 pool.release(nd.slot);
             }
@@ -2844,6 +3004,10 @@ extern "C" int gk_ios_driver_sharded_inc(gk_ctx *ctx, gk_mip *mip, const gk_iocp
         return e ? std::atoi(e) : 0;
     }();
     const int post_cap = post_cap_env > 0 ? post_cap_env : 1 << 30;
+    static const int winbatch_min = [] {
+        const char *e = std::getenv("GK_BNB_WINBATCH");        // 0: batches as wide as BMAX
+        return e ? std::max(0, std::atoi(e)) : 0;
+    }();
     int since_sync = 0;
     // show_progress (glpios03.js:2-48) through the context's report hook, and
     // the relative gap of ios_relative_gap (glpios01.js:842): both need the
@@ -2996,9 +3160,16 @@ extern "C" int gk_ios_driver_sharded_inc(gk_ctx *ctx, gk_mip *mip, const gk_iocp
             }
             S.dive.clear();
         }
+        // (with an incumbent, GK_BNB_WINBATCH: the open nodes of a batch are
+        // those within best_node's window of its first one — the nodes a
+        // sequential walk treats as equally good — and at least
+        // winbatch_min of them)
+        double wlim = DBL_MAX;
         while (!S.open.empty() && (int)bf.ents.size() < cap) {
+            if (S.have && winbatch_min > 0 && (int)bf.ents.size() >= winbatch_min && S.open.front().key > wlim) break;
             const NodeRec nd = S.pop_open();
             if (!S.hopeful(nd.bound)) { pool.release(nd.slot); continue; }
+            if (wlim == DBL_MAX && parm->bt_tech == 3) wlim = nd.key + S.window_eps(nd.key);
             bf.ents.push_back(Entry{0, nd, 0, 0, 0});
         }
         if (!bf.ents.empty()) {
