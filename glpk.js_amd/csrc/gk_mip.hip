@@ -1621,14 +1621,15 @@ struct MipSolver {
     // bound is within 0.001 (1 + |bound|) of the best are equally good, and
     // among them the one with the least parent ii_sum (minimisation) or the
     // best lp_obj (maximisation) is chosen, the earliest created on ties.
-    // Applied while the open list is short enough that the window's scan is
-    // cheap (GK_BNB_BLB_WINDOW: its size limit, 0 off; a deep tree's frontier
-    // keeps the plain bound order)
+    // Opt-in (GK_BNB_BLB_WINDOW: the open-list size up to which the window is
+    // scanned; default 0, off): with the batched search it changed no node
+    // count on gap or the C5s fixtures (profiles/r06_bnb_selection.txt) and
+    // its scans cost C5s 12x30 21 -> 128 ms
     static int blb_window_max()
     {
         static const int v = [] {
             const char *e = std::getenv("GK_BNB_BLB_WINDOW");
-            return e ? std::max(0, std::atoi(e)) : 4096;
+            return e ? std::max(0, std::atoi(e)) : 0;
         }();
         return v;
     }
