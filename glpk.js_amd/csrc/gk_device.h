@@ -429,59 +429,9 @@ __device__ __forceinline__ Cand no_cand(double k1)
 // 64-slot group of the pivot row), pass-2 candidates (one per wave of
 // k_dual_ratio).  gpart: gamma_p sums of the 64-slot groups [4 gv), then
 // their max |trow| [4 gv).
-// (the chuzr slots take 8 gv: k_dual_update with 8 rows per block writes
-// ceil(m / 8) of them)
-__device__ __forceinline__ Cand *cand_pass1(const SpxDev &d) { return (Cand *)d.cand + 8 * gv_of(d.m, d.n); }
-__device__ __forceinline__ Cand *cand_pass2(const SpxDev &d) { return (Cand *)d.cand + 12 * gv_of(d.m, d.n); }
+__device__ __forceinline__ Cand *cand_pass1(const SpxDev &d) { return (Cand *)d.cand + 4 * gv_of(d.m, d.n); }
+__device__ __forceinline__ Cand *cand_pass2(const SpxDev &d) { return (Cand *)d.cand + 8 * gv_of(d.m, d.n); }
 __device__ __forceinline__ double *tmax_part(const SpxDev &d) { return d.gpart + 4 * gv_of(d.m, d.n); }
-
-// Values one block of a launch publishes for the launch's last block
-// (gate_last, the two-kernel pivot): stored and loaded as agent-scope atomics
-// (write-through to the coherent level on every XCD, not left in one XCD's
-// L2), and ordered by gate_arrive_ret's s_waitcnt before the arrival count
-__device__ __forceinline__ void st_coh(double *p, double v)
-{
-    __hip_atomic_store((unsigned long long *)p, dbits(v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ void st_coh(int *p, int v)
-{
-    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ double ld_coh(const double *p)
-{
-    return __longlong_as_double((long long)__hip_atomic_load((unsigned long long *)p, __ATOMIC_RELAXED,
-                                                             __HIP_MEMORY_SCOPE_AGENT));
-}
-__device__ __forceinline__ int ld_coh(const int *p)
-{
-    return __hip_atomic_load((int *)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ void cand_st_coh(Cand *p, const Cand &c)
-{
-    unsigned long long *q = (unsigned long long *)p;
-    __hip_atomic_store(q, dbits(c.k1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __hip_atomic_store(q + 1, dbits(c.k2), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __hip_atomic_store(q + 2, (unsigned long long)(unsigned)c.idx | ((unsigned long long)(unsigned)c.aux << 32),
-                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ Cand cand_ld_coh(const Cand *p)
-{
-    unsigned long long *q = (unsigned long long *)p;
-    const unsigned long long a = __hip_atomic_load(q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const unsigned long long b = __hip_atomic_load(q + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const unsigned long long c = __hip_atomic_load(q + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    Cand e;
-    e.k1 = __longlong_as_double((long long)a);
-    e.k2 = __longlong_as_double((long long)b);
-    e.idx = (int)(unsigned)(c & 0xffffffffull);
-    e.aux = (int)(unsigned)(c >> 32);
-    return e;
-}
-// lanes below this one whose bit is set
-__device__ __forceinline__ int lanes_below(unsigned long long mask)
-{
-    return (int)__builtin_amdgcn_mbcnt_hi((unsigned)(mask >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)mask, 0u));
-}
 
 // the choice over cnt stored candidates, made by one wave (lane-strided scan,
 // then the butterfly): the same result in every wave that calls it

@@ -910,182 +910,6 @@ __global__ void __launch_bounds__(1024) k_trow_rows(SpxDev d, int pse)
 }
 
 // ---------------------------------------------------------------------------
-// fold_resolve (the two-kernel pivot, DualPlan.fold): k_dual_ratio's choice,
-// made by the last block of k_dual_row to finish, from what every block
-// published — its max |trow|, its pass-1 candidate (block-local tolerance)
-// and its pass-2 candidates with t <= t1_b (glpspx02.js:793-935, Harris's
-// two passes).  The global tolerance eps = tol_bnd (1 + 0.01 max |trow|),
-// teta1 = the least relaxed ratio, then pass 2 = max |alfa| over t <= teta1.
-// The cases k_dual_ratio settles by rescanning a block's positions (a
-// block's pass-1 candidate below eps; a block with more pass-2 candidates
-// than it stored, none of the stored ones qualifying for a reason other
-// than eps) stop the batch with ST_RATIO: the positions' values are other
-// blocks' stores of this launch, which this block does not read, and the
-// host runs that pivot with the three-kernel plan.  Then the state
-// k_dual_ratio's block 0 writes: the pending pivot's counters, the new
-// pivot (p, kp, delta, ns), max |trow|, and the choice for k_dual_update
-// (pass 1 in q1 / teta1 / kq1 / alfa1 / need2, pass 2 in cand_pass2[0]).
-// Every thread of the block calls it (block barriers inside); at most two
-// published blocks per thread (the host plans fold only then).
-// ---------------------------------------------------------------------------
-__device__ __forceinline__ void fold_resolve(const SpxDev &d, const FinishIn &fin, bool reset, int p, int kp, double delta,
-                                          int ns, RatioIn rin, int nprev)
-{
-    DState *st = d.st;
-    const int tid = threadIdx.x, nth = blockDim.x, lane = tid & 63, w = tid >> 6, nw = nth >> 6;
-    const int ncb = gridDim.x;
-    __shared__ double fr_big[16];
-    __shared__ Cand fr_c[16];
-    __shared__ int fr_f[16];
-    __shared__ unsigned long long fr_x[16];
-    // one trip: everything the blocks published (clamped index, selected after)
-    double tm[2];
-    Cand c1[2], sl[2][P2_K];
-    int cn[2];
-#pragma unroll
-    for (int u = 0; u < 2; ++u) {
-        const int b = min(tid + u * nth, ncb - 1);
-        tm[u] = ld_coh(&tmax_part(d)[b]);
-        c1[u] = cand_ld_coh(&cand_pass1(d)[b]);
-        cn[u] = ld_coh(&d.p2cnt[b]);
-#pragma unroll
-        for (int k = 0; k < P2_K; ++k) sl[u][k] = cand_ld_coh((const Cand *)d.p2slot + (size_t)b * P2_K + k);
-    }
-    // update_gamma's gamma_p sum (glpspx02.js:1103-1132) in k_dual_update's
-    // order: wave 0, lane-strided over the blocks, then the wave sum
-    double gpl = 0.0;
-    if (w == 0) {
-        for (int b = lane; b < ncb; b += 64) gpl += ld_coh(&d.gpart[b]);
-        gpl = wsum(gpl);
-    }
-    // (benches) the last block exit of the kernel before this one
-    unsigned long long xx = 0ull;
-    if (d.tslots)
-        for (int b = tid; b < nprev; b += nth) xx = max(xx, d.xslots[b]);
-    double v = 0.0;
-#pragma unroll
-    for (int u = 0; u < 2; ++u)
-        if (tid + u * nth < ncb) v = fmax(v, tm[u]);
-    v = wmax(v);
-    const unsigned long long xw = d.tslots ? wmax_u64(xx) : 0ull;
-    if (lane == 0) {
-        fr_big[w] = v;
-        fr_x[w] = xw;
-    }
-    __syncthreads();
-    double big = 0.0;
-    for (int k = 0; k < nw; ++k) big = fmax(big, fr_big[k]);
-    RatioIn ri = rin;
-    ri.delta = delta;
-    const RatioCtx x = ratio_ctx(ri, big);
-    // pass 1
-    Cand c = no_cand(DBL_MAX);
-    int fail = 0;
-#pragma unroll
-    for (int u = 0; u < 2; ++u)
-        if (tid + u * nth < ncb) {
-            if (c1[u].idx != 0 && c1[u].k2 < x.eps) fail = 1;
-            else if (better<1>(c1[u], c)) c = c1[u];
-        }
-    c = wave_best<1>(c);
-    fail = __any(fail) ? 1 : 0;
-    if (lane == 0) {
-        fr_c[w] = c;
-        fr_f[w] = fail;
-    }
-    __syncthreads();
-    Cand b1 = no_cand(DBL_MAX);
-    int f1 = 0;
-    for (int k = 0; k < nw; ++k) {
-        if (better<1>(fr_c[k], b1)) b1 = fr_c[k];
-        f1 |= fr_f[k];
-    }
-    const int q1 = b1.idx;
-    const double teta1 = q1 ? b1.k1 : DBL_MAX;
-    const int need2 = !(x.rtol == 0.0 || q1 == 0 || teta1 == 0.0);
-    // pass 2 over the stored candidates
-    Cand b2 = no_cand(0.0);
-    int f2 = 0;
-    if (need2 && !f1) {
-        Cand c2 = no_cand(0.0);
-        int bad = 0;
-#pragma unroll
-        for (int u = 0; u < 2; ++u)
-            if (tid + u * nth < ncb) {
-                const int cnt = cn[u];
-                bool hasq = false, epsall = true;
-#pragma unroll
-                for (int k = 0; k < P2_K; ++k)
-                    if (k < cnt) {
-                        const Cand &e = sl[u][k];
-                        const bool small = e.k2 < x.eps;
-                        const bool q = e.k1 <= teta1 && !small;
-                        hasq = hasq || q;
-                        epsall = epsall && small;
-                        if (q && better<2>(e, c2)) c2 = e;
-                    }
-                // (the unstored ones are worse than every stored one: if a
-                // stored one qualifies the block's best is among them; if all
-                // failed the tolerance, so do the unstored ones)
-                if (cnt > P2_K && !hasq && !epsall) bad = 1;
-            }
-        c2 = wave_best<2>(c2);
-        bad = __any(bad) ? 1 : 0;
-        __syncthreads();
-        if (lane == 0) {
-            fr_c[w] = c2;
-            fr_f[w] = bad;
-        }
-        __syncthreads();
-        for (int k = 0; k < nw; ++k) {
-            if (better<2>(fr_c[k], b2)) b2 = fr_c[k];
-            f2 |= fr_f[k];
-        }
-    }
-    if (tid == 0) {
-        finish_scalars(d, fin, reset);
-        st->p = p;
-        st->kp = kp;
-        st->delta = delta;
-        st->ns = ns;
-        st->dinf = 0;
-        st->trow_max_bits = dbits(big);
-        st->q1 = q1;
-        st->teta1 = teta1;
-        st->need2 = need2;
-        st->kq1 = b1.aux;
-        st->alfa1 = b1.k2;
-        // the entering choice itself (pick_choose's: pass 2 when needed,
-        // else pass 1), and gamma_p
-        Cand fc = b1;
-        if (need2) fc = b2;
-        else if (q1 == 0) fc = no_cand(DBL_MAX);
-        cand_pass2(d)[0] = fc;
-        st->fold_gp = gpl;
-        if (f1 | f2) {
-            st->stop = ST_RATIO;
-            st->ratio_redo += 1;
-        }
-        if (d.tslots) {
-            // the stamps k_dual_ratio's block 0 keeps: the end of the pivot-row
-            // kernel (here: this block's end), the last exit of the kernel
-            // before it, and the previous k_dual_update's span
-            unsigned long long xm = 0ull;
-            for (int k = 0; k < nw; ++k) xm = max(xm, fr_x[k]);
-            const unsigned long long now = wall_clock64(), u0 = st->tk_upd0;
-            st->tk_end = now;
-            st->tk_next = now;
-            st->tk_prev = xm;
-            if (u0 != 0ull && xm > u0 && xm - u0 < 20000ull) {
-                st->upd_ticks += (double)(xm - u0);
-                st->upd_n += 1.0;
-            }
-            st->tk_upd0 = 0ull;
-        }
-    }
-}
-
-// ---------------------------------------------------------------------------
 // k_dual_row (row path, dense A): k_dual_top and k_trow_rows in ONE kernel.
 // Every block makes the chuzr choice itself (wave reduction over the
 // commit's per-wave candidates, the leaving variable in aux), reads its rho
@@ -1102,7 +926,7 @@ __device__ __forceinline__ void fold_resolve(const SpxDev &d, const FinishIn &fi
 // 8 per wave: the entries past them are read by a loop whose every
 // iteration is two dependent trips)
 template <int NP>
-__global__ void __launch_bounds__(1024) k_dual_row(SpxDev d, int pse, int nr_cap, int gm, int fold, int nprev)
+__global__ void __launch_bounds__(1024) k_dual_row(SpxDev d, int pse, int nr_cap, int gm)
 {
     const TraceScope trace_(d, 1);
     __shared__ double sp[16][64];
@@ -1131,9 +955,6 @@ __global__ void __launch_bounds__(1024) k_dual_row(SpxDev d, int pse, int nr_cap
     for (int u = 0; u < NP; ++u) c0[u] = d.rlist[min(w + u * nw, m - 1)];
     int pos1 = d.bind[m + min(idx, n - 1)];
     int pos2 = d.bind[min(idx, m - 1)];
-    // the W position of structural idx (its pivot-row value goes to twW for
-    // k_dual_update's T = inv(B) A_W)
-    const int wposi = (pse && fold) ? d.wpos[min(idx, n - 1)] : -1;
     // the wave's rows of AT depend on the list alone: issued now, in flight
     // while the chuzr choice below resolves (the rho entries wait for it)
     const double *__restrict__ col = d.A.AT + min(idx, n - 1);
@@ -1298,10 +1119,7 @@ __global__ void __launch_bounds__(1024) k_dual_row(SpxDev d, int pse, int nr_cap
     sp[w][lane] = (idx < n) ? acc : 0.0;
     __syncthreads();
     TPH(1, 2);
-    // wave 0 only from here: no block barriers (fold: the other waves go on
-    // to the last-block test at the end)
-    if (w != 0 && !fold) return;
-    if (w == 0) {
+    if (w != 0) return;                      // wave 0 only from here: no block barriers
     // the waves' partial sums in wave order; the LDS loads issued together
     // (a loop over the runtime wave count waited for each load in turn)
     double tp16[16];
@@ -1322,10 +1140,6 @@ __global__ void __launch_bounds__(1024) k_dual_row(SpxDev d, int pse, int nr_cap
         const double w1 = ref1 ? tv1 : 0.0, w2 = ref2 ? tv2 : 0.0;
         if (idx < n) d.wcol[idx] = w1;
         if (idx < m) d.ys[idx] = w2;
-        // by W position (a member of W is a non-basic structural of the
-        // reference space: w1 is its pivot-row value); after a reset W is
-        // empty and nothing reads these
-        if (idx < n && wposi >= 0 && wposi < TW_CAP) d.twW[wposi] = w1;
         gsum = w1 * w1 + w2 * w2;
     }
     const double bmax = wmax(fmax(fabs(tv1), fabs(tv2)));
@@ -1340,58 +1154,16 @@ __global__ void __launch_bounds__(1024) k_dual_row(SpxDev d, int pse, int nr_cap
     if (j1 >= 0 && pass1_cand(x, tv1, cb1, s1, j1, m + idx + 1, e) && better<1>(e, c)) c = e;
     if (j2 >= 0 && pass1_cand(x, tv2, cb2, s2, j2, idx + 1, e) && better<1>(e, c)) c = e;
     const Cand b = wave_best<1>(c);
-    // (fold) the block's pass-2 candidates: those whose unrelaxed ratio is at
-    // most the block's own pass-1 ratio t1_b — the global teta1 <= t1_b for
-    // every block whose candidate passes the global tolerance, so no other
-    // position of the block can qualify.  Up to P2_K are stored as they are;
-    // beyond that the P2_K best by pass 2's order (max |alfa|, lowest index),
-    // and the count tells the last block that the rest are worse than those
-    int p2n = 0;
-    if (fold) {
-        Cand e1 = no_cand(0.0), e2 = no_cand(0.0);
-        bool h1 = false, h2 = false;
-        if (b.idx != 0) {
-            h1 = j1 >= 0 && pass2_cand(x, tv1, cb1, s1, j1, m + idx + 1, b.k1, e1);
-            h2 = j2 >= 0 && pass2_cand(x, tv2, cb2, s2, j2, idx + 1, b.k1, e2);
-        }
-        const unsigned long long m1 = __ballot(h1), m2 = __ballot(h2);
-        p2n = __popcll(m1) + __popcll(m2);
-        Cand *slot = (Cand *)d.p2slot + (size_t)blockIdx.x * P2_K;
-        if (p2n <= P2_K) {
-            if (h1) cand_st_coh(slot + lanes_below(m1), e1);
-            if (h2) cand_st_coh(slot + __popcll(m1) + lanes_below(m2), e2);
-        } else {
-            for (int k = 0; k < P2_K; ++k) {
-                Cand c2 = no_cand(0.0);
-                if (h1 && better<2>(e1, c2)) c2 = e1;
-                if (h2 && better<2>(e2, c2)) c2 = e2;
-                const Cand bb = wave_best<2>(c2);
-                if (lane == 0) cand_st_coh(slot + k, bb);
-                if (h1 && e1.idx == bb.idx) h1 = false;
-                if (h2 && e2.idx == bb.idx) h2 = false;
-            }
-        }
-    }
     TPH(1, 5);
     if (lane == 0) {
-        if (fold) {
-            // read by this launch's last block (write-through stores)
-            st_coh(&tmax_part(d)[blockIdx.x], bmax);
-            cand_st_coh(&cand_pass1(d)[blockIdx.x], b);
-            st_coh(&d.p2cnt[blockIdx.x], p2n);
-        } else {
-            tmax_part(d)[blockIdx.x] = bmax;
-            cand_pass1(d)[blockIdx.x] = b;
-        }
-        if (pse) {
-            if (fold) st_coh(&d.gpart[blockIdx.x], g);
-            else d.gpart[blockIdx.x] = g;
-        }
+        tmax_part(d)[blockIdx.x] = bmax;
+        if (pse) d.gpart[blockIdx.x] = g;
+        cand_pass1(d)[blockIdx.x] = b;
         if (d.tslots) d.tslots[blockIdx.x] = wall_clock64();
         // the choice goes to the outbox, which no block of this launch reads;
         // the scalar state every block read at entry (the pending pivot, the
         // counters, dinf) is rewritten by k_dual_ratio's block 0 from it
-        if (lead && !fold) {
+        if (lead) {
             st->ob_p = p;
             st->ob_kp = kp;
             st->ob_delta = best.k2;
@@ -1399,17 +1171,6 @@ __global__ void __launch_bounds__(1024) k_dual_row(SpxDev d, int pse, int nr_cap
             st->ob_reset = reset ? 1 : 0;
         }
     }
-    }   // wave 0
-    if (!fold) return;
-    // (fold) the last block of the launch to finish resolves the ratio test
-    // for every block: gate_arrive_ret's s_waitcnt orders this block's
-    // published values before its arrival
-    const int arr = gate_arrive_ret(st);
-    __shared__ int slast;
-    if (threadIdx.x == 0) slast = gate_last(st, arr) ? 1 : 0;
-    __syncthreads();
-    if (!slast) return;
-    fold_resolve(d, fin, reset, p, kp, best.k2, ns, rin, nprev);
 }
 
 // ---------------------------------------------------------------------------
@@ -2377,7 +2138,6 @@ __global__ void __launch_bounds__(256) k_dual_commit(SpxDev d, int pse, int nvb,
                 }
                 st->nwl = nwl;
             }
-            st->tw_valid = 0;                     // T = inv(B) A_W is not kept by this path
             // algorithmic HBM bytes of this pivot: the pivot row (rows of A in
             // the support of rho, or all of A), A w over the reference-space
             // columns, inv(B) once for both right-hand sides, read + write of
@@ -2586,7 +2346,7 @@ __device__ __forceinline__ void books_load(const SpxDev &d, Books &b, int nr, in
 
 template <int NRHS>
 __device__ __forceinline__ void books_store(const SpxDev &d, const Books &b, int kp, int kq, int tkp, bool refkp,
-                                            int nr, int ns, int rowpath, double bytes_fixed, int tw_after)
+                                            int nr, int ns, int rowpath, double bytes_fixed)
 {
     // straight-line code (selects and stores to a spare slot past the end of
     // each list instead of branches): this runs in one wave per pivot, and
@@ -2612,7 +2372,6 @@ __device__ __forceinline__ void books_store(const SpxDev &d, const Books &b, int
         d.wpos[win ? kp - m - 1 : dw] = nw1;
         st->nwl = nw1 + (win ? 1 : 0);
     }
-    st->tw_valid = tw_after;
     if (!d.tslots) return;
     // (benches) the pivot row, A w, and inv(B) read once and written once
     // over the support of rho; the device-clock spans of the pivot-row
@@ -2637,18 +2396,9 @@ __device__ __forceinline__ void books_store(const SpxDev &d, const Books &b, int
     st->bytes_upd = b.abu + (16.0 * (double)m * ns + 16.0 * (double)m + 48.0 * (double)m + 29.0 * (double)n);
 }
 
-// twm (DualPlan.twm): 0 — T = inv(B) A_W is not kept (the commit clears
-// tw_valid); 1 — kept: each block applies this pivot's product-form update to
-// its rows of T, as to inv(B), the leaving structural's column appended when
-// it joins W, the entering one's dropped (update_gamma's list changes,
-// glpspx02.js:1160-1188); 2 — kept, and update_gamma's u = inv(B) (ys - A w)
-// formed as inv(B) ys - T w (w: the pivot row over W, k_dual_row's twW) with
-// no A w pass: k_dual_ratio's A w blocks are not needed (the two-kernel pivot)
-// FOLD (the two-kernel pivot): the entering choice was made by k_dual_row's
-// last block (cand_pass2[0]), and with PSE twm is 2
-template <int NRHS, int SP, int GM, int RPB, int FOLD>
+template <int NRHS, int SP, int GM, int RPB>
 __global__ void __launch_bounds__(1024) k_dual_update(SpxDev d, int gn, int ncb, int nr_cap, int rowpath,
-                                                      double bytes_fixed, int twm)
+                                                      double bytes_fixed)
 {
     const TraceScope trace_(d, 3);
     const ExitStamp xs_(d.xslots, blockIdx.x);
@@ -2684,15 +2434,13 @@ __global__ void __launch_bounds__(1024) k_dual_update(SpxDev d, int gn, int ncb,
     PickIn pin;
     pin.need2 = st->need2; pin.q1 = st->q1; pin.kq1 = st->kq1; pin.rigorous = st->rigorous;
     pin.teta1 = st->teta1; pin.alfa1 = st->alfa1; pin.big = trow_big(st); pin.delta = st->delta;
-    const int np2 = FOLD ? 1 : 4 * gn;
-    constexpr int C2U = FOLD ? 1 : 4;
-    Cand c2l[C2U];
+    const int np2 = 4 * gn;
+    Cand c2l[4];
 #pragma unroll
-    for (int u = 0; u < C2U; ++u) c2l[u] = cand_pass2(d)[FOLD ? 0 : min(lane + 64 * u, np2 - 1)];
-    constexpr int GPU = FOLD ? 1 : 4;
-    double gp[GPU];
+    for (int u = 0; u < 4; ++u) c2l[u] = cand_pass2(d)[min(lane + 64 * u, np2 - 1)];
+    double gp[4];
 #pragma unroll
-    for (int u = 0; u < GPU; ++u) gp[u] = (NRHS == 2) ? (FOLD ? st->fold_gp : d.gpart[min(lane + 64 * u, ncb - 1)]) : 0.0;
+    for (int u = 0; u < 4; ++u) gp[u] = (NRHS == 2) ? d.gpart[min(lane + 64 * u, ncb - 1)] : 0.0;
     const int nr = st->nr, ns = st->ns, p = max(st->p, 1), kp = max(st->kp, 1);
     const double delta = st->delta;
     const int binv_fresh = st->binv_fresh, rig = st->rigorous, phase = st->phase, refct = st->refct;
@@ -2704,22 +2452,6 @@ __global__ void __launch_bounds__(1024) k_dual_update(SpxDev d, int gn, int ncb,
         const int t = min(gs + u * NSL, m);
         c0[u] = d.rho_idx[t];
         rv[u] = d.rho_val[t];
-    }
-    // T = inv(B) A_W at the block's rows, and the pivot row over W (twm)
-    const int twv = (NRHS == 2 && FOLD) ? st->tw_valid : 0, nwl_e = (NRHS == 2 && FOLD) ? st->nwl : 0;
-    // (twm 2) this thread's share of (T w)_r, subtracted from its share of u
-    double uT = 0.0;
-    if (NRHS == 2 && FOLD) {
-        double tva[GM], twa[GM];
-#pragma unroll
-        for (int u = 0; u < GM; ++u) {
-            const int sc = min(gs + u * NSL, TW_CAP - 1);
-            tva[u] = d.tw[(size_t)sc * d.ldw + min(r, m - 1)];
-            twa[u] = d.twW[sc];
-        }
-#pragma unroll
-        for (int u = 0; u < GM; ++u)
-            if (act && gs + u * NSL < nwl_e) uT += tva[u] * twa[u];
     }
     // the block's rows
     const int rc = min(r, m - 1);
@@ -2736,21 +2468,17 @@ __global__ void __launch_bounds__(1024) k_dual_update(SpxDev d, int gn, int ncb,
     int hkj = d.head[m + jc];
     // ---- the selections of trip 1
     pin.c = no_cand(0.0);
-    if (FOLD)
-        pin.c = c2l[0];                             // (the same in every lane)
-    else {
 #pragma unroll
-        for (int u = 0; u < C2U; ++u)
-            if (lane + 64 * u < np2 && better<2>(c2l[u], pin.c)) pin.c = c2l[u];
-        for (int b = lane + 256; b < np2; b += 64) {
-            const Cand e = cand_pass2(d)[b];
-            if (better<2>(e, pin.c)) pin.c = e;
-        }
+    for (int u = 0; u < 4; ++u)
+        if (lane + 64 * u < np2 && better<2>(c2l[u], pin.c)) pin.c = c2l[u];
+    for (int b = lane + 256; b < np2; b += 64) {
+        const Cand e = cand_pass2(d)[b];
+        if (better<2>(e, pin.c)) pin.c = e;
     }
     pin.g = 0.0;                                    // gamma_p in every block, fixed order
-    if (NRHS == 2 && w == 0 && !FOLD) {
+    if (NRHS == 2 && w == 0) {
 #pragma unroll
-        for (int u = 0; u < GPU; ++u)
+        for (int u = 0; u < 4; ++u)
             if (lane + 64 * u < ncb) pin.g += gp[u];
         for (int b = lane + 256; b < ncb; b += 64) pin.g += d.gpart[b];
     }
@@ -2761,35 +2489,26 @@ __global__ void __launch_bounds__(1024) k_dual_update(SpxDev d, int gn, int ncb,
     if (!rowlane) { bb = 0.0; g = 0.0; }
     if (!colth) { cb = 0.0; tri = 0.0; hkj = 1; }
     TPH(3, 0);
-    const double gsum = (NRHS == 2 && FOLD) ? gp[0] : ((NRHS == 2 && w == 0) ? wsum(pin.g) : 0.0);
-    // ---- the entering choice (every wave; FOLD: made by k_dual_row)
-    PickOut pk;
-    if (FOLD) {
-        pk.q = pin.c.idx; pk.kq = pin.c.aux; pk.teta = pin.c.k1; pk.alfa = pin.c.k2;
-    } else
-        pk = pick_choose(pin);
+    const double gsum = (NRHS == 2 && w == 0) ? wsum(pin.g) : 0.0;
+    // ---- the entering choice (every wave)
+    const PickOut pk = pick_choose(pin);
     const int q = pk.q, kq = pk.kq;
     const int qc = min(max(q, 1), n), kqc = min(max(kq, 1), m + n);
     // ---- trip 2: inv(B) entries, the multipliers, the choice's operands
     // (issued before the stop tests; addresses clamped)
     const bool hdense = !SP && kqc > m;
     const double *__restrict__ hcolv = d.A.A + (size_t)(hdense ? kqc - m - 1 : 0) * d.A.lda;
-    // update_gamma's right-hand side: ys - A w (k_dual_ratio's work), or ys
-    // with T w subtracted from the sums (twm 2)
-    const double *__restrict__ uv = (NRHS == 2 && FOLD) ? d.ys : d.work;
     double bv[GM], xa[GM], xb[GM];
 #pragma unroll
     for (int u = 0; u < GM; ++u) {
         const int ca = min(max(c0[u], 0), m - 1);
         bv[u] = Bv[(size_t)ca * ldb + rc];
         xa[u] = SP ? 0.0 : hcolv[ca];
-        xb[u] = (NRHS == 2) ? uv[ca] : 0.0;
+        xb[u] = (NRHS == 2) ? d.work[ca] : 0.0;
     }
     const int kou = min(max(kold - 1, 0), m - 1);          // a basic slack's row (kold <= m)
     const double ua_l = SP ? 0.0 : hcolv[kou];
-    const double ub_l = (NRHS == 2) ? uv[kou] : 0.0;
-    // W position of the entering variable (twm: T's column to drop)
-    const int wq_l = (NRHS == 2 && FOLD) ? d.wpos[min(max(kqc - m, 1), n) - 1] : -1;
+    const double ub_l = (NRHS == 2) ? d.work[kou] : 0.0;
     const int tkp = d.type[kp - 1];
     const bool refkp = NRHS == 2 && d.refsp[kp - 1] != 0;
     const int knew = (r == p - 1) ? kqc : kold;
@@ -2810,12 +2529,6 @@ __global__ void __launch_bounds__(1024) k_dual_update(SpxDev d, int gn, int ncb,
     }
     if (stop) return;
     const bool lead = bk && threadIdx.x == 0;
-    if (NRHS == 2 && FOLD && nwl_e > 0 && !twv) {
-        // T is not current (a pivot of another plan since W was last empty):
-        // this pivot goes back to the three-kernel plan
-        if (lead) { st->stop = ST_RATIO; st->ratio_redo += 1; }
-        return;
-    }
     if (q == 0) {
         if (lead) { st->q = 0; st->stop = ST_Q0; }
         return;
@@ -2842,7 +2555,6 @@ __global__ void __launch_bounds__(1024) k_dual_update(SpxDev d, int gn, int ncb,
         }
         if (NRHS == 2 && t < nr) b += bvu * xb[u];
     }
-    if (NRHS == 2) b -= uT;
     double ua = 0.0, ub = 0.0;                      // unit columns of a basic slack at this row
     if (rowlane && kold <= m) {
         if (!SP) ua = hsel(kold - 1, ua_l);
@@ -2946,14 +2658,9 @@ __global__ void __launch_bounds__(1024) k_dual_update(SpxDev d, int gn, int ncb,
     // Nothing later in this kernel reads what it writes (the other blocks
     // read the compact rho, not the lists); st->nr / st->nwl, which every
     // block reads in trip 1, only once all blocks have passed the gate
-    // T after this pivot: current when it was (or W was empty) and the new W
-    // fits the positions the blocks' threads cover
-    const bool wout_t = kq > m && wq_l >= 0, win_t = kp > m && refkp && tkp != FX;
-    const int nw1_t = nwl_e - (wout_t ? 1 : 0), nwa_t = nw1_t + (win_t ? 1 : 0);
-    const bool tw_keep = NRHS == 2 && FOLD && twm && (twv || nwl_e == 0) && nwa_t <= min(TW_CAP, GM * NSL);
     if (bk && w == wa && lane == 0) {
         gate_wait(st);
-        books_store<NRHS>(d, sbk, kp, kq, tkp, refkp, nr, ns, rowpath, bytes_fixed, tw_keep ? 1 : 0);
+        books_store<NRHS>(d, sbk, kp, kq, tkp, refkp, nr, ns, rowpath, bytes_fixed);
     }
     // ---- product-form update of the entries held in registers
     {
@@ -2969,35 +2676,6 @@ __global__ void __launch_bounds__(1024) k_dual_update(SpxDev d, int gn, int ncb,
             if (c == ce) v = z ? 1.0 : 0.0;
             else v = (z ? 0.0 : v) - f * rv[u];
             d.Binv[(size_t)c * ldb + r] = v;
-        }
-        // T's rows: the same update with row p of T = the pivot row over W
-        // (T[p, s] = rho' A_j = trow_j), then the list changes — position wq
-        // takes the last column, the leaving structural's column inv(B') A_kp
-        // = f (its column before the pivot was -e_p) goes to nw1.  The thread
-        // of position wq reads the last column, so it also writes nw1 when
-        // that is the last position (no other thread touches it)
-        if (tw_keep && act) {
-            const int last = nwl_e - 1;
-            double t2[GM], w2[GM];
-#pragma unroll
-            for (int u = 0; u < GM; ++u) {
-                const int sp_ = gs + u * NSL;
-                const int src = min(max((wout_t && sp_ == wq_l) ? last : sp_, 0), TW_CAP - 1);
-                t2[u] = d.tw[(size_t)src * d.ldw + r];
-                w2[u] = d.twW[src];
-            }
-#pragma unroll
-            for (int u = 0; u < GM; ++u) {
-                const int sp_ = gs + u * NSL;
-                if (sp_ >= nwa_t) continue;
-                if (win_t && sp_ == nw1_t) {
-                    if (wout_t && wq_l != nw1_t) continue;     // written by the thread of wq
-                    d.tw[(size_t)sp_ * d.ldw + r] = f;
-                    continue;
-                }
-                d.tw[(size_t)sp_ * d.ldw + r] = (z ? 0.0 : t2[u]) - f * w2[u];
-                if (win_t && wout_t && sp_ == wq_l) d.tw[(size_t)nw1_t * d.ldw + r] = f;
-            }
         }
     }
     TPH(3, 4);
@@ -3204,19 +2882,6 @@ void lp_shard_trow(hipStream_t s, const SpxDev &d, int pse)
     sh.exchanges++;
 }
 
-// GK_FOLD=1: the two-kernel pivot where the plan allows it (experiment,
-// off by default: measured slower on C3, DESIGN §4 — the last block's tail
-// costs what k_dual_ratio's launch did, and 8-row update blocks double the
-// chuzr candidates k_dual_row reduces)
-bool fold_enabled()
-{
-    static const bool on = [] {
-        const char *e = std::getenv("GK_FOLD");
-        return e && std::atoi(e) != 0;
-    }();
-    return on;
-}
-
 DualPlan dual_plan(const SpxDev &d, int nr_max, int nwl_max, int pse, int rigorous)
 {
     const int m = d.m, n = d.n;
@@ -3262,15 +2927,11 @@ DualPlan dual_plan(const SpxDev &d, int nr_max, int nwl_max, int pse, int rigoro
     }();
     pl.gm = 4 * cdiv(m, 256);
     const int need = ns_max + 1;
-    // (the two-kernel pivot's update holds T's entries beside inv(B)'s: 8 rows
-    // per block, 2 entries of each per thread, fits the registers of 1024
-    // threads without spilling; 16 rows and 4 entries spilled 12 VGPRs)
-    const bool fold_cap = fold_enabled() && pl.rowpath && d.A.dense && !rigorous && !d.shard;
-    const int rpb = fold_cap ? 8 : upd_rpb(), sl = 64 / rpb;
+    const int rpb = upd_rpb(), sl = 64 / rpb;
     const int rows_blocks = cdiv(m, rpb);
     if (upd_on && !rigorous && (pl.rowpath || pl.colpath) && (pl.fone || pl.colpath) && need <= 4 * 4 * 16 &&
         n <= rows_blocks * 1024) {
-        pl.ugm = rpb == 32 ? 8 : (rpb == 8 ? 2 : 4);
+        pl.ugm = rpb == 32 ? 8 : 4;
         pl.uwaves = std::min(16, std::max(1, cdiv(need, pl.ugm * sl)));
         // every thread of the block also covers a column slot of update_cbar
         while (pl.uwaves < 16 && cdiv(n, rows_blocks) > 64 * pl.uwaves) pl.uwaves++;
@@ -3280,21 +2941,6 @@ DualPlan dual_plan(const SpxDev &d, int nr_max, int nwl_max, int pse, int rigoro
     pl.awone = (pse && d.A.dense && nwl_max <= 512) ? std::max(nwl_max, 1) : 0;
     pl.panel = cp_only ? 0 : panel_wanted(d, pl);
     pl.panel_age = pl.panel ? panel_age_max() : 0;
-    // T = inv(B) A_W kept by k_dual_update on the dense row path (PSE), while
-    // W fits TW_CAP and the positions the update's threads cover (GM = 4 per
-    // thread, 4 row slices per wave: 16 per wave)
-    pl.twm = 0;
-    if (pl.fupd && pl.rowpath && pse && d.A.dense && d.tw && nwl_max <= TW_CAP && fold_enabled()) {
-        pl.uwaves = std::max(pl.uwaves, std::min(16, cdiv(std::max(nwl_max, 1), 16)));
-        if (nwl_max <= pl.uwaves * 16) pl.twm = 1;
-    }
-    // the two-kernel pivot: k_dual_row's last block resolves the ratio test
-    // (at most two of its published blocks per thread), update_gamma's u from
-    // T (PSE) — the engine enables it per batch (Spx::batch: T current or W
-    // empty, no shard)
-    pl.fold = 0;
-    if (pl.fupd && fold_cap && pl.ugm == 2 && cdiv(std::max(m, n), 64) <= 2 * 64 * pl.twaves && (!pse || pl.twm))
-        pl.fold = 1;
     return pl;
 }
 
@@ -3342,38 +2988,30 @@ void dual_batch_begin(hipStream_t s, const SpxDev &d, const DualPlan &pl)
 // blocks of the kernel that ends a pivot (their exit stamps: xslots)
 static int prev_blocks(const SpxDev &d, const DualPlan &pl)
 {
-    if (pl.fupd) return cdiv(d.m, pl.ugm * 4);
+    if (pl.fupd) return cdiv(d.m, pl.ugm == 8 ? 32 : 16);
     return cdiv(std::max(d.m, d.n), 256) + cdiv(d.m, 512) * pl.uchunks;
 }
 
-template <int NRHS, int SP, int FOLD = 0>
+template <int NRHS, int SP>
 static void launch_update(hipStream_t s, const SpxDev &d, const DualPlan &pl, int gn, int ncb, int rowpath,
                           hipEvent_t e0 = nullptr, hipEvent_t e1 = nullptr)
 {
-    const int twm = (NRHS == 2 && !SP) ? pl.twm : 0;
-    const dim3 grid(cdiv(d.m, pl.ugm * 4)), block(64 * pl.uwaves);
+    const dim3 grid(cdiv(d.m, pl.ugm == 8 ? 32 : 16)), block(64 * pl.uwaves);
     // (the extended launch only with events: graph capture takes the plain one)
-    if (pl.ugm == 2) {
+    if (pl.ugm == 8) {
         if (e0)
-            hipExtLaunchKernelGGL((k_dual_update<NRHS, SP, 2, 8, FOLD>), grid, block, 0, s, e0, e1, 0, d, gn, ncb,
-                                  pl.nr_cap, rowpath, bytes_fixed(d), twm);
+            hipExtLaunchKernelGGL((k_dual_update<NRHS, SP, 8, 32>), grid, block, 0, s, e0, e1, 0, d, gn, ncb,
+                                  pl.nr_cap, rowpath, bytes_fixed(d));
         else
-            hipLaunchKernelGGL((k_dual_update<NRHS, SP, 2, 8, FOLD>), grid, block, 0, s, d, gn, ncb, pl.nr_cap, rowpath,
-                               bytes_fixed(d), twm);
-    } else if (pl.ugm == 8) {
-        if (e0)
-            hipExtLaunchKernelGGL((k_dual_update<NRHS, SP, 8, 32, FOLD>), grid, block, 0, s, e0, e1, 0, d, gn, ncb,
-                                  pl.nr_cap, rowpath, bytes_fixed(d), twm);
-        else
-            hipLaunchKernelGGL((k_dual_update<NRHS, SP, 8, 32, FOLD>), grid, block, 0, s, d, gn, ncb, pl.nr_cap, rowpath,
-                               bytes_fixed(d), twm);
+            hipLaunchKernelGGL((k_dual_update<NRHS, SP, 8, 32>), grid, block, 0, s, d, gn, ncb, pl.nr_cap, rowpath,
+                               bytes_fixed(d));
     } else {
         if (e0)
-            hipExtLaunchKernelGGL((k_dual_update<NRHS, SP, 4, 16, FOLD>), grid, block, 0, s, e0, e1, 0, d, gn, ncb,
-                                  pl.nr_cap, rowpath, bytes_fixed(d), twm);
+            hipExtLaunchKernelGGL((k_dual_update<NRHS, SP, 4, 16>), grid, block, 0, s, e0, e1, 0, d, gn, ncb,
+                                  pl.nr_cap, rowpath, bytes_fixed(d));
         else
-            hipLaunchKernelGGL((k_dual_update<NRHS, SP, 4, 16, FOLD>), grid, block, 0, s, d, gn, ncb, pl.nr_cap, rowpath,
-                               bytes_fixed(d), twm);
+            hipLaunchKernelGGL((k_dual_update<NRHS, SP, 4, 16>), grid, block, 0, s, d, gn, ncb, pl.nr_cap, rowpath,
+                               bytes_fixed(d));
     }
 }
 
@@ -3450,20 +3088,11 @@ void dual_iteration2(hipStream_t s, const SpxDev &d, const DualPlan &pl, hipEven
         // (16 entries per wave in trips 1-2 measured slower on C3 — 11.6 against
         // 9.0 us of span, profiles/r04_trace_pivot_np16_reverted.txt — than 8
         // plus the dependent loop: k_dual_row<16> is kept for experiments)
-        const int nprev = prev_blocks(d, pl);
         if (ev0)
             hipExtLaunchKernelGGL(k_dual_row<8>, dim3(ncb), dim3(64 * pl.twaves), 0, s, ev0, ev1, 0, d, pl.pse,
-                                  pl.nr_cap, pl.gm, pl.fold, nprev);
+                                  pl.nr_cap, pl.gm);
         else
-            hipLaunchKernelGGL(k_dual_row<8>, dim3(ncb), dim3(64 * pl.twaves), 0, s, d, pl.pse, pl.nr_cap, pl.gm,
-                               pl.fold, nprev);
-        if (pl.fold) {
-            // two kernels per pivot: k_dual_row's last block made the choice
-            // (cand_pass2[0]: gn = 1), u from T (pl.twm 2)
-            if (pl.pse) launch_update<2, 0, 1>(s, d, pl, 1, ncb, 1, ev2, ev3);
-            else launch_update<1, 0, 1>(s, d, pl, 1, ncb, 1, ev2, ev3);
-            return;
-        }
+            hipLaunchKernelGGL(k_dual_row<8>, dim3(ncb), dim3(64 * pl.twaves), 0, s, d, pl.pse, pl.nr_cap, pl.gm);
     } else {
         const bool tgrid = !pl.rigorous && d.A.dense && m >= 1024;
         if (tgrid)

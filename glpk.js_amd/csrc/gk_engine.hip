@@ -172,10 +172,6 @@ struct Engine {
     size_t pin_cap = 0;
     DBuf<int> rlist, rpos, rho_idx, wlist, wpos, awcnt;
     DBuf<double> rho_val, gpart, cand, awpart;
-    DBuf<double> p2slot, twW, twf;               // the two-kernel pivot (DualPlan.fold)
-    DBuf<int> p2cnt;
-    DBuf<double> tw;                             // T = inv(B) A_W, 2 x TW_CAP columns of ldw (allocated on first use)
-    int tw_m = -1;
     DBuf<char> upstage;                         // device side of the coalesced uploads
     DBuf<int> xlist;                            // eval_cbar: basic slacks with a nonzero cost (primal phase I)
     DBuf<unsigned long long> tslots, xslots;
@@ -272,7 +268,6 @@ struct Engine {
         rlist.release(); rpos.release(); rho_idx.release(); rho_val.release();
         gpart.release(); awcnt.release(); tslots.release(); xslots.release(); trace.release(); wlist.release(); wpos.release(); cand.release();
         awpart.release();
-        p2slot.release(); twW.release(); twf.release(); p2cnt.release(); tw.release();
         pnl.release(); pnl_src.release(); pslot.release(); ppos.release();
         lb_n.release(); ub_n.release(); bbar_n.release(); stat_n.release();
         type.release(); orig_type.release(); stat.release(); refsp.release();
@@ -544,18 +539,13 @@ static void engine_alloc(Engine &E, int m, int n, gk_ctx *ctx)
             // gv each; primal: max |tcol|, d_q sums, gamma_q sums of the row
             // groups, 16 gv each
             place(E.gpart, 56 * gv);
-            // candidates (24-byte entries): chuzr (8 gv) | pass 1 | pass 2 (4 gv
-            // each), then the primal pass-1 candidates of the row groups, 16 gv
-            place(E.cand, 3 * 32 * gv);
+            // candidates (24-byte entries): chuzr | pass 1 | pass 2, 4 gv each,
+            // then the primal pass-1 candidates of the row groups, 16 gv
+            place(E.cand, 3 * 28 * gv);
             // dual: reference-space non-basic structurals (n); primal: basic
             // slacks in the reference space (m)
             place(E.wlist, (size_t)std::max(m, n) + 1); place(E.wpos, (size_t)std::max(m, n) + 1);
             place(E.awcnt, (size_t)(m + 511) / 512 + 1);
-            // two-kernel pivot: P2_K pass-2 candidates and a count per 64-slot
-            // block (4 gv blocks), the pivot-row values of W (two buffers) and
-            // the last pivot's multipliers
-            place(E.p2slot, 4 * gv * P2_K * 3); place(E.p2cnt, 4 * gv);
-            place(E.twW, 2 * (size_t)TW_CAP); place(E.twf, m);
             place(E.tslots, std::max((size_t)((n + 511) / 512) * 2048, 4 * gv) + 1);
             place(E.xslots, (size_t)(m + 15) / 16 + gv + (size_t)((m + 511) / 512) * 2048 + 1);
         };
@@ -928,9 +918,6 @@ struct Spx {
         d.gpart = E->gpart.p;
         d.wlist = E->wlist.p; d.wpos = E->wpos.p; d.cand = E->cand.p;
         d.awpart = E->awpart.p; d.awpart_cap = (size_t)AW_SPLITS * m; d.awcnt = E->awcnt.p;
-        d.p2slot = E->p2slot.p; d.p2cnt = E->p2cnt.p; d.twW = E->twW.p; d.twf = E->twf.p;
-        d.ldw = (m + 7) & ~7;
-        d.tw = (E->tw_m == m) ? E->tw.p : nullptr;
         if (E->pnl_m == m && E->pnl_n == n) {
             d.pnl = E->pnl.p; d.pnl_src = E->pnl_src.p; d.pslot = E->pslot.p; d.ppos = E->ppos.p;
             d.ldp = (n + 7) & ~7;
@@ -1935,9 +1922,6 @@ struct Spx {
     bool epi_arm(int K);
     void epi_wait();
     const char *epi_stage = nullptr;      // the epilogue's download in the staging ring
-    // a pivot the two-kernel plan handed back (ST_RATIO): the next batch
-    // runs it alone with the three-kernel plan
-    int fold_off = 0;
     // the sparse factor's Schur-correction bytes of the call's dual pivots
     // (16 m k + 8 k^2 at chain length k: Y read by the FTRAN's and the
     // BTRAN's corrections, inv(M) once), added per batch
@@ -2372,11 +2356,6 @@ int Spx::batch(int K, int rigorous)
         E->pnl_m = m;
         E->pnl_n = n;
     }
-    if (dual && E->dense && parm->pricing == PT_PSE && !f->sparse && fold_enabled() && E->tw_m != m) {
-        // T = inv(B) A_W of the two-kernel pivot (TW_CAP columns)
-        E->tw.ensure((size_t)TW_CAP * (size_t)((m + 7) & ~7));
-        E->tw_m = m;
-    }
     SpxDev d = dev();
     const int pse = (parm->pricing == PT_PSE);
     if (dual) {
@@ -2387,11 +2366,6 @@ int Spx::batch(int K, int rigorous)
         };
         DualPlan pl = dual_plan(d, bucket(hs.nr + K + 1, m), bucket(hs.nwl + K + 1, n), pse, rigorous);
         pl.sparse = f->sparse ? 1 : 0;
-        // the two-kernel pivot needs T current at the first pivot (or W empty
-        // there: the batch starts with a reset when refct is 0); a pivot it
-        // handed back (ST_RATIO) runs with the three-kernel plan first
-        if (pl.fold && (fold_off || (pse && !(hs.tw_valid || hs.nwl == 0 || hs.refct == 0)))) pl.fold = 0;
-        fold_off = 0;
         // profiling launches eagerly: event-record nodes inside captured
         // graphs are not timed by every HIP runtime this library may bind to
         // prof 1/2 launch eagerly (events around the pivot-row kernel); prof 3
@@ -2784,12 +2758,11 @@ int Spx::run_dual()
         K = align_to_refactor(K, hs.upd_lim - hs.upd_cnt);
         K = ahead_align(K);
         K = align_to_display(K);
-        if (fold_off) K = 1;                    // the pivot ST_RATIO handed back, alone
         int why = batch(K, rigorous);
         if (f->sparse) ahead_maybe();
         det_log("batch", K, why);
         if (f->sparse) sp_stamps_dump(*f->sp, s, ctx->wall_khz);
-        if (why != ST_RATIO) E->kbatch = next_batch(E->kbatch, why);
+        E->kbatch = next_batch(E->kbatch, why);
         dinf_known = (why == ST_BATCH && hs.npiv > 0);
         if (hs.npiv > 0) {
             bbar_st = 2;
@@ -2848,9 +2821,6 @@ int Spx::run_dual()
         case ST_PIVCHK:
             if (binv_st != 1) binv_st = 0;
             rigorous = 5;
-            break;
-        case ST_RATIO:
-            fold_off = 1;
             break;
         default:
             throw AbiError{"spx_dual: unexpected device stop code"};
@@ -3481,7 +3451,6 @@ static int spx_entry(gk_ctx *ctx, gk_lp *lp, gk_bfd *f, const gk_smcp *parm, int
         f->upd_cnt = S.hs.upd_cnt;
         f->stats.evals_skipped = S.evals_skipped;
         if (f->shard) f->stats.shard_exchanges = f->shard->exchanges - shard_ex0;
-        f->stats.ratio_redo = S.hs.ratio_redo;
         if (ret == 0 || (ret >= 6 && ret <= 9)) S.save_resident();
         S.swap_spare();
         S.mark("exit");

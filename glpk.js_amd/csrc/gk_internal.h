@@ -42,14 +42,7 @@ enum : int {
     ST_DCHK = 8,      // primal: cbar[q] disagrees with re-evaluated d_q
     ST_REFACT = 9,    // update limit reached: re-invert before the next pivot
     ST_REFSP = 10,    // PSE reference space must be reset (refct == 0)
-    ST_RATIO = 11,    // two-kernel pivot (DualPlan.fold): the ratio test needs the rescans of
-                      // k_dual_ratio — the host runs this pivot with the three-kernel plan
 };
-// the two-kernel pivot (DualPlan.fold): pass-2 candidates kept per
-// 64-slot block of k_dual_row, and the reference-space tableau columns
-// T = inv(B) A_W of update_gamma kept for at most TW_CAP members of W
-constexpr int P2_K = 4;
-constexpr int TW_CAP = 256;
 // the gate mode of the end-of-call epilogue's kernels (GATE, gk_device.h)
 constexpr int EPI_GATE = 0x100;
 
@@ -107,20 +100,6 @@ struct DState {
     // commit thread owning cbar[q] overwrites that entry while other blocks
     // still need the old value
     double dq_ratio;
-    // the reference-space tableau columns T = inv(B) A_W (two-kernel pivot,
-    // k_dual_update): tw_valid — T is current for the members of W (a commit
-    // that does not maintain it clears it; with W empty there is nothing to
-    // be current); tw_par — the buffer parity of the current pivot (T of the
-    // pivot in buffer tw_par, the pivot-row values of W in twW[tw_par]); the
-    // last committed pivot's update, applied lazily by the next k_dual_update
-    // (its position p, 1-based, and the W list changes: wq <- last when wout,
-    // nw1 <- the leaving variable's column when win); ratio_redo — pivots the
-    // two-kernel plan handed back (ST_RATIO)
-    int tw_valid, tw_par, tw_p, tw_wout;
-    int tw_wq, tw_last, tw_win, tw_nw1;
-    long long ratio_redo;
-    double fold_gp;                         // (two-kernel pivot) update_gamma's sum of the pivot row's squares over
-                                            // the reference space, formed by k_dual_row's last block
 };
 
 // ---- dense GEMV helpers ---------------------------------------------------
@@ -247,14 +226,6 @@ struct SpxDev {
     double *pnl, *pnl_src;
     int *pslot, *ppos;
     int ldp;
-    // the two-kernel pivot (DualPlan.fold): per 64-slot block of k_dual_row,
-    // P2_K pass-2 candidates (24-byte entries) and their count; T = inv(B) A_W
-    // in two buffers (tw[(b TW_CAP + s) ldw + r]), the pivot-row values of the
-    // members of W by W position (twW[b TW_CAP + s]), and the multipliers of
-    // the last committed pivot's product-form update (twf[r])
-    double *p2slot; int *p2cnt;
-    double *tw; int ldw;
-    double *twW, *twf;
     SpFactor *sp;                            // host pointer: the sparse factor (nullptr: explicit inverse)
     struct LpShard *shard;                   // host pointer: column-sharded pricing (gk_bfd_set_comm), or nullptr
 };
@@ -315,16 +286,10 @@ struct DualPlan {
     int panel;                    // rows of the MFMA pricing panel (0: the pivot row is a column pass over A)
     int panel_age;                // product-form updates a panel row may go through before a refill
     int sparse;                   // 1: sparse factor (gk_sparse.hip): BTRAN / FTRAN / update hooks
-    int fold;                     // 1: two kernels per pivot — k_dual_row resolves the ratio test in
-                                  // its last block, k_dual_update forms update_gamma's u from T (no
-                                  // k_dual_ratio, no A w pass)
-    int twm;                      // k_dual_update: 0 T not kept (commits clear tw_valid), 1 kept,
-                                  // 2 kept and used for u (fold with PSE)
 };
 void dual_batch_begin(hipStream_t s, const SpxDev &d, const DualPlan &pl);
 void dual_batch_end(hipStream_t s, const SpxDev &d, const DualPlan &pl);
 DualPlan dual_plan(const SpxDev &d, int nr_max, int nwl_max, int pse, int rigorous);
-bool fold_enabled();                         // GK_FOLD=1 (default off): the two-kernel pivot and T
 // ev0/ev1, ev2/ev3 (optional, eager launches only): the start / stop events
 // of the pivot-row kernel and of the fused update kernel (hipExtLaunchKernelGGL:
 // the command processor's timestamps of the dispatch itself, as a profiler's)

@@ -37,7 +37,7 @@ namespace gk {
 // primal-only candidate / partial regions beyond the dual's (engine_alloc):
 // per-row-group pass-1 candidates, then max |tcol|, d_q check sums and
 // gamma_q sums of the groups (16 gv each)
-__device__ __forceinline__ Cand *pcand1(const SpxDev &d) { return (Cand *)d.cand + 16 * gv_of(d.m, d.n); }
+__device__ __forceinline__ Cand *pcand1(const SpxDev &d) { return (Cand *)d.cand + 12 * gv_of(d.m, d.n); }
 __device__ __forceinline__ double *ptmax(const SpxDev &d) { return d.gpart + 8 * gv_of(d.m, d.n); }
 __device__ __forceinline__ double *pdsum(const SpxDev &d) { return d.gpart + 24 * gv_of(d.m, d.n); }
 __device__ __forceinline__ double *pvsum(const SpxDev &d) { return d.gpart + 40 * gv_of(d.m, d.n); }

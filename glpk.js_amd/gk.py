@@ -104,7 +104,7 @@ class SpxStats(C.Structure):
                 ("panel_hits", C.c_longlong), ("panel_refills", C.c_longlong),
                 ("refine_tries", C.c_longlong), ("refinements", C.c_longlong), ("refine_steps", C.c_longlong),
                 ("refine_resid_max", C.c_double), ("factor_sparse", C.c_int), ("lu_ahead", C.c_int),
-                ("seconds_lu", C.c_double), ("shard_exchanges", C.c_longlong), ("ratio_redo", C.c_longlong)]
+                ("seconds_lu", C.c_double), ("shard_exchanges", C.c_longlong)]
 
 
 _lib = None
@@ -137,7 +137,8 @@ def load_library(path: str = LIB_PATH):
         raise GkError(f"{path} is missing: build it with __graft_entry__.build()")
     L = C.CDLL(path)
     P = C.c_void_p
-    L.gk_build_stamp.restype = C.c_char_p
+    if hasattr(L, "gk_build_stamp"):
+        L.gk_build_stamp.restype = C.c_char_p
     if "GK_LIB_PATH" not in os.environ and os.path.isdir(os.path.join(HERE, "csrc")):
         # the library must be the build of the sources beside it (stamp.py)
         from . import stamp as _stamp

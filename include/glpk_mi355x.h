@@ -236,8 +236,6 @@ typedef struct {
     double seconds_lu;          /* host wall time of the Markowitz LU factorizations (all threads) */
     /* ABI 11: column-sharded pricing (gk_bfd_set_comm) */
     long long shard_exchanges;  /* pivot-row all-gathers of the call (0 when not sharded) */
-    /* ABI 11: the two-kernel dual pivot */
-    long long ratio_redo;       /* pivots it handed back to the three-kernel plan (ST_RATIO) */
 } gk_spx_stats;
 void gk_bfd_last_stats(const gk_bfd *bfd, gk_spx_stats *st);
 /* record HIP events around the pivot-row kernel of every dual pivot (benches) */

@@ -590,7 +590,6 @@ static napi_value js_stats(napi_env env, napi_callback_info info)
     set_num(env, o, "factor_sparse", (double)st.factor_sparse);
     set_num(env, o, "seconds_lu", st.seconds_lu);
     set_num(env, o, "shard_exchanges", (double)st.shard_exchanges);
-    set_num(env, o, "ratio_redo", (double)st.ratio_redo);
     return o;
 }
 
