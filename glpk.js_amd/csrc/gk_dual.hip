@@ -1524,11 +1524,16 @@ __global__ void __launch_bounds__(256) k_dual_ratio(SpxDev d, int gn, int tiles_
     int sj = d.stat[jc], kj = d.head[m + jc];
     const bool lead = (blockIdx.x == 0 && threadIdx.x < 64);
     constexpr int CPL = 8;                    // group candidates per lane held in registers
+    // more groups than a wave holds (large n: the sparse factor's problems):
+    // the block's 4 waves split them and meet in LDS, instead of every wave
+    // walking all of them one load per iteration
+    const bool bsplit = ncb > CPL * 64;
+    const int tb = bsplit ? (int)threadIdx.x : lane, tst = bsplit ? (int)blockDim.x : 64;
     Cand cl[CPL];
     double tv[CPL];
 #pragma unroll
     for (int u = 0; u < CPL; ++u) {
-        const int b = min(lane + u * 64, ncb - 1);
+        const int b = min(tb + u * tst, ncb - 1);
         cl[u] = cand_pass1(d)[b];
         tv[u] = tmax_part(d)[b];
     }
@@ -1554,12 +1559,20 @@ __global__ void __launch_bounds__(256) k_dual_ratio(SpxDev d, int gn, int tiles_
     double v = 0.0;
 #pragma unroll
     for (int u = 0; u < CPL; ++u) {
-        if (lane + u * 64 >= ncb) cl[u] = no_cand(DBL_MAX);
+        if (tb + u * tst >= ncb) cl[u] = no_cand(DBL_MAX);
         else v = fmax(v, tv[u]);
     }
-    for (int b = lane + CPL * 64; b < ncb; b += 64) v = fmax(v, tmax_part(d)[b]);
-    const double big = wmax(v);
+    for (int b = tb + CPL * tst; b < ncb; b += tst) v = fmax(v, tmax_part(d)[b]);
+    double big = wmax(v);
     if (stop) return;
+    __shared__ double rbig[4];
+    __shared__ Cand rc1[4];
+    __shared__ int rfl[4];
+    if (bsplit) {
+        if (lane == 0) rbig[threadIdx.x >> 6] = big;
+        __syncthreads();
+        big = fmax(fmax(rbig[0], rbig[1]), fmax(rbig[2], rbig[3]));
+    }
     if (rowpath == 1 && blockIdx.x == 0 && threadIdx.x == 0) {
         // k_dual_row's outbox: the pending pivot's counters (finish_apply's
         // scalar half, from the state every block of k_dual_row read), then
@@ -1603,10 +1616,34 @@ __global__ void __launch_bounds__(256) k_dual_ratio(SpxDev d, int gn, int tiles_
         if (cl[u].idx != 0 && cl[u].k2 < x.eps) fail = 1;
         else if (better<1>(cl[u], c)) c = cl[u];
     }
-    for (int b = lane + CPL * 64; b < ncb; b += 64) {
+    for (int b = tb + CPL * tst; b < ncb; b += tst) {
         const Cand f = cand_pass1(d)[b];
         if (f.idx != 0 && f.k2 < x.eps) fail = 1;
         else if (better<1>(f, c)) c = f;
+    }
+    if (bsplit) {
+        // the waves' choices combined (better<1> is a total order: the same
+        // choice as one wave's walk over every group); with a failing group
+        // anywhere, every wave walks them all as below
+        const Cand cw = wave_best<1>(c);
+        const int fw = __any(fail) ? 1 : 0;
+        if (lane == 0) {
+            rc1[threadIdx.x >> 6] = cw;
+            rfl[threadIdx.x >> 6] = fw;
+        }
+        __syncthreads();
+        fail = rfl[0] | rfl[1] | rfl[2] | rfl[3];
+        if (!fail) {
+            c = rc1[0];
+            for (int k = 1; k < 4; ++k)
+                if (better<1>(rc1[k], c)) c = rc1[k];
+        } else {
+            c = no_cand(DBL_MAX);
+            for (int b = lane; b < ncb; b += 64) {
+                const Cand f = cand_pass1(d)[b];
+                if (!(f.idx != 0 && f.k2 < x.eps) && better<1>(f, c)) c = f;
+            }
+        }
     }
     if (__any(fail)) {
         // rare: rescan the groups whose candidate is not significant (lane =
@@ -1730,12 +1767,50 @@ __device__ __forceinline__ int dual_pick(const SpxDev &d, int pse, int gn, int n
     return pick_resolve(d, pi, pse, kq_out);
 }
 
-// sparse A / rigorous mode: the pick and h = -N[q] in one workgroup
+// sparse A / rigorous mode: the pick and h = -N[q] in one workgroup.  The
+// pass-2 candidates and gamma_p's group sums are split over the block's
+// waves (thousands of them on the sparse factor's problems, where one wave's
+// walk cost one load round trip per 64) and combined in LDS in wave order
 __global__ void __launch_bounds__(1024) k_dual_pick(SpxDev d, int pse, int gn, int ncb)
 {
-    if (d.st->stop) return;
+    const DState *st = d.st;
+    if (st->stop) return;
+    __shared__ Cand pc[16];
+    __shared__ double pg[16];
+    const int tid = threadIdx.x, nt = blockDim.x, lane = tid & 63, w = tid >> 6, nw = nt >> 6;
+    PickIn pi;
+    pi.need2 = st->need2;
+    pi.q1 = st->q1;
+    pi.kq1 = st->kq1;
+    pi.rigorous = st->rigorous;
+    pi.teta1 = st->teta1;
+    pi.alfa1 = st->alfa1;
+    pi.big = trow_big(st);
+    pi.delta = st->delta;
+    Cand c = no_cand(0.0);
+    for (int b = tid; b < 4 * gn; b += nt) {
+        const Cand e = cand_pass2(d)[b];
+        if (better<2>(e, c)) c = e;
+    }
+    c = wave_best<2>(c);
+    double g = 0.0;
+    if (pse)
+        for (int b = tid; b < ncb; b += nt) g += d.gpart[b];
+    g = wsum(g);
+    if (lane == 0) {
+        pc[w] = c;
+        pg[w] = g;
+    }
+    __syncthreads();
+    pi.c = pc[0];
+    double gt = pg[0];
+    for (int k = 1; k < nw; ++k) {
+        if (better<2>(pc[k], pi.c)) pi.c = pc[k];
+        gt += pg[k];
+    }
+    pi.g = (lane == 0) ? gt : 0.0;         // (pick_resolve's wave sum of it is gt exactly)
     int kq = 0;
-    const int q = dual_pick(d, pse, gn, ncb, &kq);
+    const int q = pick_resolve(d, pi, pse, &kq);
     if (q) build_hq(d, q, d.sp != nullptr);
 }
 
