@@ -3120,8 +3120,10 @@ void dual_iteration2(hipStream_t s, const SpxDev &d, const DualPlan &pl, hipEven
         hipLaunchKernelGGL(k_dual_top, dim3(1), dim3(TOP_WG), 0, s, d, 3, 0);
         sp_pivot_btran(*d.sp, s, d.st, d.rho);
         if (ev0) (void)hipEventRecord(ev0, s);
+        // (no max |trow| from the pass: k_trow_finish's group maxima give it,
+        // and one atomic per block on a single word cost most of the pass)
         colpass_gated(s, d.A, CP_TROW, m, n, d.head, d.stat, d.coef, nullptr, d.rho, nullptr, d.trow, nullptr,
-                      &d.st->trow_max_bits, d.st, 0);
+                      nullptr, d.st, 0);
         if (ev1) (void)hipEventRecord(ev1, s);
         hipLaunchKernelGGL(k_trow_finish, dim3(gv), dim3(256), 0, s, d, pl.pse, 0);
         hipLaunchKernelGGL(k_dual_ratio, dim3(gn + (pl.pse ? cdiv(m, 256) + d.A.nlr : 0)), dim3(256), 0, s, d, gn,
@@ -3187,7 +3189,7 @@ void dual_iteration2(hipStream_t s, const SpxDev &d, const DualPlan &pl, hipEven
             lp_shard_trow(s, d, pl.pse);
         } else
             colpass_gated(s, d.A, CP_TROW, m, n, d.head, d.stat, d.coef, nullptr, d.rho, nullptr, d.trow, nullptr,
-                          &d.st->trow_max_bits, d.st, 0);
+                          nullptr, d.st, 0);
         if (ev1) (void)hipEventRecord(ev1, s);
         hipLaunchKernelGGL(k_trow_finish, dim3(gv), dim3(256), 0, s, d, pl.pse, (pl.panel ? 1 : 0) | (d.shard ? 2 : 0));
     }
