@@ -28,10 +28,10 @@ import __graft_entry__  # noqa: E402
 HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 # the two kernels that carry the headline pivot's time; the roofline is
 # priced on whichever of them has the larger event time in the timed region
-# (k_dual_row in round 5)
+# (k_dual_row in rounds 5 and 6)
 UPDATE_KERNEL = "k_dual_update"
 ROW_KERNEL = "k_dual_row"
-ROUND = "r05"
+ROUND = "r06"
 # the C port (oracle/) against the reference itself, both on one core of the
 # build container on C3 from the slack basis: the port 285.8 pivots/s over a
 # 20 s window (6,874 pivots, init_csa included), the reference node 9.4
