@@ -3026,6 +3026,29 @@ void colpass_gated(hipStream_t s, const MatDev &A, int mode, int off, int cnt, c
                    const double *y, double *out1, double *out2, unsigned long long *maxbits,
                    const DState *st, int need_p);
 
+// GK_SHARD_SIM: every simulated rank's column pass, A w partial and pack in
+// rank order, written into its receive block, then the unpack every rank of
+// a real run executes (the same blocks, so the same row, maximum and A w)
+void lp_shard_sim(hipStream_t s, const SpxDev &d, int pse)
+{
+    LpShard &sh = *d.shard;
+    const int n = d.n, m = d.m, L = sh.L, G = sh.vsize;
+    const size_t blk = (size_t)shard_blk(L, m, pse);
+    for (int v = 0; v < G; ++v) {
+        const int lo = std::min(n, v * L), cnt = std::min(n, lo + L) - lo;
+        double *out = sh.drecv + (size_t)v * blk;
+        colpass_gated(s, d.A, CP_TROW, m + lo, cnt, d.head, d.stat + lo, d.coef, nullptr, d.rho, nullptr, d.trow + lo,
+                      nullptr, &d.st->trow_max_bits, d.st, 0);
+        if (pse)
+            hipLaunchKernelGGL(k_shard_aw, dim3(cdiv(m, 64)), dim3(256), 0, s, d, lo, lo + cnt, out + L + 1);
+        hipLaunchKernelGGL(k_shard_pack, dim3(cdiv(L, 256)), dim3(256), 0, s, (const double *)d.trow, lo, cnt, L,
+                           (const unsigned long long *)&d.st->trow_max_bits, out);
+    }
+    hipLaunchKernelGGL(k_shard_unpack, dim3(cdiv(std::max(n, m), 256)), dim3(256), 0, s, (const double *)sh.drecv, G,
+                       L, n, m, pse, d.trow, &d.st->trow_max_bits, d.work);
+    sh.exchanges++;
+}
+
 
 double launch_trow_rows(hipStream_t s, const SpxDev &d, const DualPlan &pl, int ns)
 {
@@ -3180,6 +3203,8 @@ void dual_iteration2(hipStream_t s, const SpxDev &d, const DualPlan &pl, hipEven
         if (ev0) (void)hipEventRecord(ev0, s);
         if (pl.panel)   // the row of p from the MFMA panel (gk_panel.hip)
             panel_trow(s, d, pl, tgrid);
+        else if (d.shard && d.shard->vsize > 1)
+            lp_shard_sim(s, d, pl.pse);
         else if (d.shard) {
             // this rank's slice of the non-basic positions, then the exchange
             const LpShard &sh = *d.shard;

@@ -3427,13 +3427,14 @@ static int spx_entry(gk_ctx *ctx, gk_lp *lp, gk_bfd *f, const gk_smcp *parm, int
             // then max |trow| and the A w partial (m) — L + 1 + m doubles a rank
             LpShard &sh = *f->shard;
             const int n = f->eng->n, m = f->eng->m;
-            sh.L = (n + sh.size - 1) / sh.size;
+            const int parts = sh.vsize > 1 ? sh.vsize : sh.size;
+            sh.L = (n + parts - 1) / parts;
             const size_t blk = (size_t)sh.L + 1 + (size_t)m;
             if (sh.dsend) (void)hipFree(sh.dsend);
             if (sh.drecv) (void)hipFree(sh.drecv);
             sh.dsend = sh.drecv = nullptr;
             HIPCHK(hipMalloc((void **)&sh.dsend, blk * sizeof(double)));
-            HIPCHK(hipMalloc((void **)&sh.drecv, (size_t)sh.size * blk * sizeof(double)));
+            HIPCHK(hipMalloc((void **)&sh.drecv, (size_t)parts * blk * sizeof(double)));
             sh.hsend.assign(blk, 0.0);
             sh.hrecv.assign((size_t)sh.size * blk, 0.0);
             sh.n = n;
@@ -3500,6 +3501,10 @@ int gk_bfd_set_comm(gk_bfd *f, gk_comm *comm)
         f->shard->comm = comm;
         f->shard->rank = rank;
         f->shard->size = size;
+        if (size == 1) {                            // (read per call: measurements switch it)
+            const char *e = std::getenv("GK_SHARD_SIM");
+            f->shard->vsize = e ? std::max(0, std::min(std::atoi(e), 64)) : 0;
+        }
         return 0;
     } catch (const AbiError &e) {
         g_err = e.msg;

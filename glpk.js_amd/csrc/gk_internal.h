@@ -240,7 +240,12 @@ struct SpxDev {
 struct LpShard {
     ::gk_comm *comm = nullptr;
     int rank = 0, size = 1, L = 0, n = 0, m = 0;
-    double *dsend = nullptr, *drecv = nullptr;  // device: L + 1 + m | size (L + 1 + m) doubles
+    // GK_SHARD_SIM = G with one rank (GK_SHARD_ONE_RANK): the G ranks' slices
+    // formed one after another by this process, packed straight into the
+    // receive blocks (no exchange) — the G-rank run's results, and per-slice
+    // kernel times as one rank of G on its own GPU would see them
+    int vsize = 0;
+    double *dsend = nullptr, *drecv = nullptr;  // device: L + 1 + m | max(size, vsize) (L + 1 + m) doubles
     std::vector<double> hsend, hrecv;           // host staging (TCP transport)
     long long exchanges = 0;
     bool failed = false;
@@ -253,6 +258,7 @@ int gk_comm_allgather_dev(::gk_comm *c, const void *dsend, size_t bytes, void *d
 int gk_comm_size_rank(const ::gk_comm *c, int *rank);
 void gk_comm_abort(::gk_comm *c);
 void lp_shard_trow(hipStream_t s, const SpxDev &d, int pse);
+void lp_shard_sim(hipStream_t s, const SpxDev &d, int pse);     // the pivot row of vsize simulated ranks
 // a host decision every rank of the shard takes together: true when any
 // rank's flag is set (one all-gather of a byte); throws if the exchange fails
 bool shard_any(LpShard &sh, bool flag);

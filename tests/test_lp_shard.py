@@ -43,6 +43,31 @@ print(json.dumps({"ret": ret, "it_cnt": P.it_cnt, "obj": float(P.obj_val).hex()}
 """
 
 
+SIM = r"""
+import json, sys
+sys.path.insert(0, %r)
+import __graft_entry__
+__graft_entry__.load_package()
+from glpk_js_amd import gk, problems
+ctx = gk.Context(0)
+comm = gk.Comm(ctx, 0, 1, "127.0.0.1:%d")
+P = gk.GkProblem(ctx, problems.gen_dense(1024, 4096, seed=42))
+P.set_comm(comm)
+ret = gk.glp_simplex(P, gk.SMCP(meth=gk.GLP_DUAL, msg_lev=gk.GLP_MSG_ERR))
+print(json.dumps({"ret": ret, "it_cnt": P.it_cnt, "obj": float(P.obj_val).hex(),
+                  "ex": int(P.stats().shard_exchanges)}))
+"""
+
+
+def _sim(size):
+    """One process forming all `size` ranks' slices in turn (GK_SHARD_SIM)."""
+    env = dict(os.environ, GK_SHARD_ONE_RANK="1", GK_SHARD_SIM=str(size))
+    r = subprocess.run([sys.executable, "-c", SIM % (ROOT, free_port())], capture_output=True, text=True, env=env,
+                       timeout=240)
+    assert r.returncode == 0, r.stderr[-2000:]
+    return json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
+
+
 def _worker(rank, size, port, q):
     try:
         sys.path.insert(0, ROOT)
@@ -140,3 +165,7 @@ def test_gpu_lp_column_sharded_same_pivots(size):
     assert abs(float.fromhex(obj) - REF_OBJ) <= 1e-9 * REF_OBJ, (float.fromhex(obj), REF_OBJ)
     print("size", size, "pivots", it_cnt, "obj", float.fromhex(obj), "single-GPU pivots", single["it_cnt"],
           "bits equal to single", (ret, it_cnt, obj) == (single["ret"], single["it_cnt"], single["obj"]))
+    # the simulated ranks (tools/shard_sim_prof.py's mode) are the real ones
+    sim = _sim(size)
+    assert (sim["ret"], sim["it_cnt"], sim["obj"]) == (ret, it_cnt, obj), (sim, res[0])
+    assert sim["ex"] > 0
