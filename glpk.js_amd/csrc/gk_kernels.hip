@@ -253,18 +253,21 @@ __global__ void __launch_bounds__(256) k_colpass_dense(int mode, int m, int off,
             const double *col = A + (size_t)(k - m - 1) * lda;
             double a1 = 0.0, a2 = 0.0;
             int r = lane * 2;
-            // 4 segments of the column in flight per lane (the pass is bound
-            // by the bytes in flight); the same order of accumulation
-            for (; r + 3 * 128 + 1 < m; r += 4 * 128) {
-                double2 v[4], xv[4], yv[4];
+            // SEG segments of the column in flight per lane (the pass is bound
+            // by the bytes in flight: 8 for one right-hand side — a slice of
+            // a sharded pricing pass fills the chip with a quarter of the
+            // waves); the same order of accumulation for any SEG
+            constexpr int SEG = TWO ? 4 : 8;
+            for (; r + (SEG - 1) * 128 + 1 < m; r += SEG * 128) {
+                double2 v[SEG], xv[SEG], yv[SEG];
 #pragma unroll
-                for (int u = 0; u < 4; ++u) {
+                for (int u = 0; u < SEG; ++u) {
                     v[u] = *(const double2 *)(col + r + 128 * u);
                     xv[u] = *(const double2 *)(x + r + 128 * u);
                     if (TWO) yv[u] = *(const double2 *)(y + r + 128 * u);
                 }
 #pragma unroll
-                for (int u = 0; u < 4; ++u) {
+                for (int u = 0; u < SEG; ++u) {
                     a1 += v[u].x * xv[u].x;
                     a1 += v[u].y * xv[u].y;
                     if (TWO) { a2 += v[u].x * yv[u].x; a2 += v[u].y * yv[u].y; }

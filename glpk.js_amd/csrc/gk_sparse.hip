@@ -837,7 +837,11 @@ static void sp_plan_sweep(SpTriHost &T, std::vector<SpFactor::Seg> &plan, int &w
     // LDS segments for the large factors: a sweep with a level of
     // sp_wide_min steps or more, or of many steps in all; a small one keeps
     // the fused one-workgroup kernels (one launch per sweep pair)
-    bool big = nst >= 16384;
+    static const int seg_min = [] {                  // GK_SP_SEG_MIN: steps from which a sweep is segmented
+        const char *e = std::getenv("GK_SP_SEG_MIN");
+        return e ? std::max(1, atoi(e)) : 4096;    // (16384 before round 6: m = 20k FTRAN L +4 %)
+    }();
+    bool big = nst >= seg_min;
     for (int l = 0; l < nlev && !big; l++) big = T.lvptr[l + 1] - T.lvptr[l] >= sp_wide_min();
     const bool seg = sp_seg_on() && big;
     int run = -1;                            // first level of the current narrow run
