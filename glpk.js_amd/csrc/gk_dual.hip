@@ -609,6 +609,9 @@ __global__ void __launch_bounds__(TOP_WG) k_dual_top(SpxDev d, int rowpath, int 
 // i, else 1 at the leaving slack, else 0: the unit columns are exact), the
 // compact rho by list position; 256 rows / list entries per thread block.
 // ---------------------------------------------------------------------------
+// (PANEL = 0: no panel pick compiled in, so the plans without the panel do
+// not reserve its 24 KB candidate array in LDS — ADVICE r5)
+template <int PANEL>
 __global__ void __launch_bounds__(256) k_dual_top_grid(SpxDev d, int pcap, int page_max)
 {
     const TraceScope trace_(d, 0);
@@ -691,7 +694,7 @@ __global__ void __launch_bounds__(256) k_dual_top_grid(SpxDev d, int pcap, int p
     }
     // the pricing panel's pick for this p (pcap > 0: the plan has the panel;
     // k_panel_pick's work, one launch fewer)
-    if (lead && pcap > 0) panel_pick_dev(d, gm, pcap, page_max, p);
+    if (PANEL && lead && pcap > 0) panel_pick_dev(d, gm, pcap, page_max, p);
 }
 
 // ---------------------------------------------------------------------------
@@ -3195,8 +3198,10 @@ void dual_iteration2(hipStream_t s, const SpxDev &d, const DualPlan &pl, hipEven
             hipLaunchKernelGGL(k_dual_row<8>, dim3(ncb), dim3(64 * pl.twaves), 0, s, d, pl.pse, pl.nr_cap, pl.gm);
     } else {
         const bool tgrid = !pl.rigorous && d.A.dense && m >= 1024;
-        if (tgrid)
-            hipLaunchKernelGGL(k_dual_top_grid, dim3(cdiv(m, 256)), dim3(256), 0, s, d, pl.panel, pl.panel_age);
+        if (tgrid && pl.panel)
+            hipLaunchKernelGGL(k_dual_top_grid<1>, dim3(cdiv(m, 256)), dim3(256), 0, s, d, pl.panel, pl.panel_age);
+        else if (tgrid)
+            hipLaunchKernelGGL(k_dual_top_grid<0>, dim3(cdiv(m, 256)), dim3(256), 0, s, d, 0, pl.panel_age);
         else
             hipLaunchKernelGGL(k_dual_top, dim3(1), dim3(TOP_WG), 0, s, d, pl.rowpath, pl.nr_cap);
         if (pl.rigorous) refine_rho_dev(s, d);
