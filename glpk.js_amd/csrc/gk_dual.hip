@@ -2957,7 +2957,6 @@ void lp_shard_trow(hipStream_t s, const SpxDev &d, int pse)
     }
     hipLaunchKernelGGL(k_shard_unpack, dim3(cdiv(std::max(n, m), 256)), dim3(256), 0, s, (const double *)sh.drecv,
                        sh.size, L, n, m, pse, d.trow, &d.st->trow_max_bits, d.work);
-    sh.exchanges++;
 }
 
 DualPlan dual_plan(const SpxDev &d, int nr_max, int nwl_max, int pse, int rigorous)
@@ -3049,7 +3048,6 @@ void lp_shard_sim(hipStream_t s, const SpxDev &d, int pse)
     }
     hipLaunchKernelGGL(k_shard_unpack, dim3(cdiv(std::max(n, m), 256)), dim3(256), 0, s, (const double *)sh.drecv, G,
                        L, n, m, pse, d.trow, &d.st->trow_max_bits, d.work);
-    sh.exchanges++;
 }
 
 

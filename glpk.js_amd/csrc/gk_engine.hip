@@ -2372,8 +2372,12 @@ int Spx::batch(int K, int rigorous)
         // keeps the graphs and records only the per-block clock stamps
         const int evp = E->prof == 1 || E->prof == 2;
         if (evp) prof_events(K);
-        // (sharded: every pivot's exchange sits between its launches — eager)
-        if (!rigorous && K >= 4 && !evp && !f->sparse && !d.shard) {
+        // sharded: the RCCL exchange is a stream operation and is captured
+        // with the pivot's kernels (so are the simulated ranks'); the TCP
+        // exchange goes through the host and keeps the batch eager
+        const bool shard_eager = d.shard && d.shard->vsize <= 1 && gk_comm_backend(d.shard->comm) != GK_COMM_RCCL;
+        if (d.shard) d.shard->exchanges += K;    // (every launched pivot exchanges, a stopped one too)
+        if (!rigorous && K >= 4 && !evp && !f->sparse && !shard_eager) {
             run_graph(d, pl, K);
             armed = epi_arm(K);
         } else {

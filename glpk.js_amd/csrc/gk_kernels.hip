@@ -257,7 +257,7 @@ __global__ void __launch_bounds__(256) k_colpass_dense(int mode, int m, int off,
             // by the bytes in flight: 8 for one right-hand side — a slice of
             // a sharded pricing pass fills the chip with a quarter of the
             // waves); the same order of accumulation for any SEG
-            constexpr int SEG = TWO ? 4 : 8;
+            constexpr int SEG = TWO ? 4 : 16;
             for (; r + (SEG - 1) * 128 + 1 < m; r += SEG * 128) {
                 double2 v[SEG], xv[SEG], yv[SEG];
 #pragma unroll
