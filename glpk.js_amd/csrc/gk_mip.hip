@@ -1122,13 +1122,15 @@ size_t node_lp_lds(int m, int n, int alds = 0, int nnz = 0)
 
 constexpr size_t NODE_LDS_MAX = 64 * 1024;
 // the node kernel's work area per node beyond which the node LPs go to the
-// engine (GK_BNB_ENGINE_BYTES, default 2 MiB: m (2m + n) doubles streamed by
-// one CU per pivot against the revised simplex on a factor); engine mode
-// solves ENGINE_BATCH nodes per search step
+// engine (GK_BNB_ENGINE_BYTES, default 1 MiB: m (2m + n) doubles streamed by
+// one CU per pivot against the revised simplex on a factor; sparsebig1, 1.8
+// MB per node: 0.58 s and 4,818 node LPs in the node kernel, 0.53 s and 410
+// in engine mode — reference 297); engine mode solves ENGINE_BATCH nodes per
+// search step
 static size_t engine_node_bytes()
 {
     const char *e = std::getenv("GK_BNB_ENGINE_BYTES");        // (read per search: tests switch it)
-    return e ? (size_t)std::max(0LL, std::atoll(e)) : ((size_t)2 << 20);
+    return e ? (size_t)std::max(0LL, std::atoll(e)) : ((size_t)1 << 20);
 }
 constexpr int ENGINE_BATCH = 8;
 
