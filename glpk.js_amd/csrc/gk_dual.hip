@@ -493,10 +493,24 @@ __global__ void __launch_bounds__(TOP_WG) k_dual_top(SpxDev d, int rowpath, int 
     const int stop = st->stop;               // tested before the first store
     const int m = d.m, n = d.n;
     const int gm = 4 * ((m + 255) / 256);
+    // more candidates than 4 per lane (m > 16,384: the sparse factor's
+    // problems): the block's waves split them and meet in LDS (better<0> is
+    // a total order: the choice of one wave's walk over all of them)
+    const bool split = gm > 256;
+    const int lane = threadIdx.x & 63;
     Cand c = no_cand(0.0);
-    for (int b = (int)(threadIdx.x & 63); b < gm; b += 64) {
+    for (int b = split ? (int)threadIdx.x : lane; b < gm; b += split ? TOP_WG : 64) {
         const Cand e = cand_chuzr(d)[b];
         if (better<0>(e, c)) c = e;
+    }
+    if (split) {
+        __shared__ Cand scw[TOP_WG / 64];
+        const Cand cw = wave_best<0>(c);
+        if (lane == 0) scw[threadIdx.x >> 6] = cw;
+        __syncthreads();
+        c = scw[0];
+        for (int k = 1; k < TOP_WG / 64; ++k)
+            if (better<0>(scw[k], c)) c = scw[k];
     }
     constexpr int RPT = 16;                   // list entries prefetched per thread
     int cl[RPT];

@@ -2027,8 +2027,18 @@ __global__ void __launch_bounds__(1024) k_sp_update(SpDev sp, DState *st)
         __syncthreads();
         rows_dot(Mi, c, k, ac);                          // inv(M) c
         for (int t = threadIdx.x; t < k; t += blockDim.x) {
+            // r inv(M): the column's entries eight at a time, loaded before
+            // their products (the same order of accumulation as one by one)
             double b = 0.0;
-            for (int u = 0; u < k; u++) b += r[u] * Mi[(size_t)u * SP_KMAX + t];     // r inv(M)
+            int u = 0;
+            for (; u + 8 <= k; u += 8) {
+                double mv[8];
+#pragma unroll
+                for (int q = 0; q < 8; q++) mv[q] = Mi[(size_t)(u + q) * SP_KMAX + t];
+#pragma unroll
+                for (int q = 0; q < 8; q++) b += r[u + q] * mv[q];
+            }
+            for (; u < k; u++) b += r[u] * Mi[(size_t)u * SP_KMAX + t];
             ra[t] = b;
         }
         __syncthreads();
@@ -2039,8 +2049,9 @@ __global__ void __launch_bounds__(1024) k_sp_update(SpDev sp, DState *st)
         }
         __syncthreads();
         const double s = sch;
-        double dmax = 0.0;
-        for (int u = 0; u < k; u++) dmax = fmax(dmax, fabs(ac[u]));
+        double dmax = 0.0;                                // (a wave maximum: exact, any order)
+        for (int u = (int)(threadIdx.x & 63); u < k; u += 64) dmax = fmax(dmax, fabs(ac[u]));
+        dmax = wmax(dmax);
         if (!(fabs(s) > 1e-11 * (1.0 + dmax))) {
             if (threadIdx.x == 0) st->refact_pending = 1;
             return;
@@ -2073,7 +2084,8 @@ __global__ void __launch_bounds__(1024) k_sp_update(SpDev sp, DState *st)
     __syncthreads();
     const double den = 1.0 + ac[t0];
     double amax = 0.0;
-    for (int u = 0; u < k; u++) amax = fmax(amax, fabs(ac[u]));
+    for (int u = (int)(threadIdx.x & 63); u < k; u += 64) amax = fmax(amax, fabs(ac[u]));
+    amax = wmax(amax);
     if (!(fabs(den) > 1e-11 * (1.0 + amax))) {
         if (threadIdx.x == 0) st->refact_pending = 1;
         return;
