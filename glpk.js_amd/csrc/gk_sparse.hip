@@ -159,15 +159,20 @@ struct SpFactor {
 };
 
 constexpr int TRI_LONG = 32;   // sweep steps with more entries run on a whole wave
-// a level 0 of at least this many steps runs on the grid (k_sp_level0):
-// below it the extra launch costs more than the workgroup's trips
-static int sp_wide_min()
+// a level of at least this many steps runs on the grid (k_sp_level): below
+// it the extra launch costs more than the workgroup's trips.  By the factor's
+// order m (GK_SP_WIDE overrides): 2,048 for 16,384 <= m < 65,536 (the m =
+// 20,020 mid-solve window 2,217 -> 2,351 pivots/s against 4,096), 4,096
+// otherwise (m = 100,050: 878 against 818 pivots/s at 2,048; m = 4,005 keeps
+// its one-workgroup sweeps)
+static int sp_wide_min(int m)
 {
     static const int w = [] {
         const char *e = std::getenv("GK_SP_WIDE");
-        return e ? std::max(1, atoi(e)) : 4096;
+        return e ? std::max(1, atoi(e)) : 0;
     }();
-    return w;
+    if (w > 0) return w;
+    return (m >= 16384 && m < 65536) ? 2048 : 4096;
 }
 
 // ---------------------------------------------------------------------------
@@ -703,7 +708,7 @@ static void sp_deps_direct(SpDeps &D, int m, const std::vector<int> &sptr, const
     }
 }
 
-static void sp_plan_sweep(SpTriHost &T, std::vector<SpFactor::Seg> &plan, int &wide);
+static void sp_plan_sweep(SpTriHost &T, std::vector<SpFactor::Seg> &plan, int &wide, int m);
 
 // the four sweeps and their launch plans, one host thread each
 static void sp_build_solves(const SpLU &F, SpSolves &S, std::vector<SpFactor::Seg> *plan, int *wide)
@@ -725,7 +730,7 @@ static void sp_build_solves(const SpLU &F, SpSolves &S, std::vector<SpFactor::Se
             for (int k = 0; k < m; k++) in[k] = F.pr[k];
             ones.assign(m, 1.0);
             sp_build_tri(S.fl, m, in, in, ones, D, false, true);
-            sp_plan_sweep(S.fl, plan[0], wide[0]);
+            sp_plan_sweep(S.fl, plan[0], wide[0], m);
             break;
         case 1:
             // FTRAN U: deps of step k = (x index c_t, u) for the entries of U row k
@@ -733,7 +738,7 @@ static void sp_build_solves(const SpLU &F, SpSolves &S, std::vector<SpFactor::Se
                            [&](int c) { return step_of_pos[c]; });
             for (int k = 0; k < m; k++) { in[k] = F.pr[k]; out[k] = F.pc[k]; }
             sp_build_tri(S.fu, m, in, out, F.Udiag, D, true);
-            sp_plan_sweep(S.fu, plan[1], wide[1]);
+            sp_plan_sweep(S.fu, plan[1], wide[1], m);
             break;
         case 2:
             // BTRAN U': deps of step k = (w index t, u) for every U row t < k holding column c_k
@@ -741,7 +746,7 @@ static void sp_build_solves(const SpLU &F, SpSolves &S, std::vector<SpFactor::Se
                                [](int t) { return t; });
             for (int k = 0; k < m; k++) { in[k] = F.pc[k]; out[k] = k; }
             sp_build_tri(S.bu, m, in, out, F.Udiag, D, false);
-            sp_plan_sweep(S.bu, plan[2], wide[2]);
+            sp_plan_sweep(S.bu, plan[2], wide[2], m);
             break;
         default:
             // BTRAN L': deps of step k = (y index i, l) for the entries of eta k
@@ -750,7 +755,7 @@ static void sp_build_solves(const SpLU &F, SpSolves &S, std::vector<SpFactor::Se
             for (int k = 0; k < m; k++) { in[k] = k; out[k] = F.pr[k]; }
             ones.assign(m, 1.0);
             sp_build_tri(S.bl, m, in, out, ones, D, true);
-            sp_plan_sweep(S.bl, plan[3], wide[3]);
+            sp_plan_sweep(S.bl, plan[3], wide[3], m);
             break;
         }
     };
@@ -814,11 +819,12 @@ static int sp_wide_entries()
 }
 
 // external entries from which a segment's external pass runs on the grid
+// (2,048; 8,192 before round 6: m = 20,020 window +6 %, m = 100,050 +5 %)
 static int sp_ga_min()
 {
     static const int g = [] {
         const char *e = std::getenv("GK_SP_GA");
-        return e ? std::max(0, atoi(e)) : 8192;
+        return e ? std::max(0, atoi(e)) : 2048;
     }();
     return g;
 }
@@ -829,7 +835,7 @@ static int sp_ga_min()
 // in its original order), internal entries by the producing step's index in
 // the segment.  wide: 1 when the sweep runs by its plan (not the fused
 // one-workgroup kernels)
-static void sp_plan_sweep(SpTriHost &T, std::vector<SpFactor::Seg> &plan, int &wide)
+static void sp_plan_sweep(SpTriHost &T, std::vector<SpFactor::Seg> &plan, int &wide, int m)
 {
     plan.clear();
     wide = 0;
@@ -842,7 +848,7 @@ static void sp_plan_sweep(SpTriHost &T, std::vector<SpFactor::Seg> &plan, int &w
         return e ? std::max(1, atoi(e)) : 4096;    // (16384 before round 6: m = 20k FTRAN L +4 %)
     }();
     bool big = nst >= seg_min;
-    for (int l = 0; l < nlev && !big; l++) big = T.lvptr[l + 1] - T.lvptr[l] >= sp_wide_min();
+    for (int l = 0; l < nlev && !big; l++) big = T.lvptr[l + 1] - T.lvptr[l] >= sp_wide_min(m);
     const bool seg = sp_seg_on() && big;
     int run = -1;                            // first level of the current narrow run
     // a tail level: a few long steps (the linking rows of a block-angular
@@ -876,7 +882,7 @@ static void sp_plan_sweep(SpTriHost &T, std::vector<SpFactor::Seg> &plan, int &w
         const int nent = T.eptr[T.lvptr[l + 1]] - T.eptr[T.lvptr[l]];
         // (a level of a few long steps stays narrow: its entries into the
         // levels before go to its segment's external pass)
-        if (nshort + nlong >= sp_wide_min() || (seg && nent >= sp_wide_entries() && nshort + nlong >= 64)) {
+        if (nshort + nlong >= sp_wide_min(m) || (seg && nent >= sp_wide_entries() && nshort + nlong >= 64)) {
             close_run(l);
             plan.push_back({1, l, l + 1, std::max(1, (nshort + 255) / 256 + nlong)});   // (k_sp_level: a long step a block)
             wide = 1;

@@ -1,0 +1,9 @@
+# round 6: the new sparse plan defaults — tests, windows, full solves
+set -e
+O=gpurun_out/${1:-r6w}; mkdir -p $O
+timeout -k 10 600 python3 -u -m pytest -q --timeout 300 --timeout-method thread tests/test_gpu_sparse.py tests/test_sparse_factor.py -m gpu > $O/tests.log 2>&1
+timeout -k 10 120 python3 -u tools/sparse_window.py --it 1000 --basis profiles/r06_blocks20k_basis_it61912.npz 200 20 > $O/w20.json 2>/dev/null
+timeout -k 10 120 python3 -u tools/sparse_window.py --it 1000 > $O/w100.json 2>/dev/null
+timeout -k 10 200 python3 -u tools/sparse_big.py --sparse blocks 200 20 > $O/full20k.json 2> $O/full20k.err
+timeout -k 10 200 python3 -u tools/sparse_big.py blocks 40 5 > $O/blocks40.json 2> $O/blocks40.err
+echo ok
