@@ -126,6 +126,7 @@ struct SpFactor {
     int m = -1;
     SpTriDevBufs fl, fu, bu, bl;
     SBuf<double> Y, Minv, zq, tpart, bt, scr, scr2, hh, bz, sacc;   // sacc: an LDS segment's external sums (k_sp_seg_a)
+    SBuf<double> upd;                     // k_sp_update's rank-1 factors of inv(M), applied by k_sp_ycol
     SBuf<int> P, hdr;                     // hdr: nlev of fl, fu, bu, bl; k (updates in the chain); Y column of the last update
     long long nnz_l = 0, nnz_u = 0;
     int levels[4] = {0, 0, 0, 0};
@@ -1317,6 +1318,8 @@ struct WoodDev {
     int *ycol;                                    // device word: Y column the last update wrote (-1: none)
     double *bz;                                   // e_p of the pivot's BTRAN (m; zero between uses)
     int *log, *nlog;                              // the chain's pivots (p, kq) and their count
+    double *upd;                                  // inv(M)'s rank-1 update: a (SP_KMAX) | r (SP_KMAX) | divisor | sign
+    int *nupd;                                    // device word: its order (0: none this pivot)
 };
 
 struct SpDev {
@@ -1435,19 +1438,38 @@ __device__ void ftran_hh(const SpDev &sp)
         if (NRHS == 2) g[1][t] = x1[p];
     }
     __syncthreads();
-    const int lane = threadIdx.x & 63;
-    for (int t = threadIdx.x >> 6; t < k; t += blockDim.x >> 6) {
-        const double *mr = sp.w.Minv + (size_t)t * SP_KMAX;
-        double a0 = 0.0, a1 = 0.0;
-        for (int u = lane; u < k; u += 64) {
-            a0 += mr[u] * g[0][u];
-            if (NRHS == 2) a1 += mr[u] * g[1][u];
+    // a wave per row of inv(M), four rows in flight at once (each row's sum
+    // in the order of one row at a time)
+    const int lane = threadIdx.x & 63, nw = blockDim.x >> 6;
+    for (int t0 = threadIdx.x >> 6; t0 < k; t0 += 4 * nw) {
+        double mv[4][SP_KMAX / 64];
+#pragma unroll
+        for (int r = 0; r < 4; r++) {
+            const int t = min(t0 + r * nw, k - 1);
+#pragma unroll
+            for (int q = 0; q < SP_KMAX / 64; q++) {
+                const int u = lane + 64 * q;
+                mv[r][q] = (u < k) ? sp.w.Minv[(size_t)t * SP_KMAX + u] : 0.0;
+            }
         }
-        a0 = wsum(a0);
-        if (NRHS == 2) a1 = wsum(a1);
-        if (lane == 0) {
-            sp.w.hh[t] = a0;
-            if (NRHS == 2) sp.w.hh[SP_KMAX + t] = a1;
+#pragma unroll
+        for (int r = 0; r < 4; r++) {
+            double a0 = 0.0, a1 = 0.0;
+#pragma unroll
+            for (int q = 0; q < SP_KMAX / 64; q++) {
+                const int u = lane + 64 * q;
+                if (u < k) {
+                    a0 += mv[r][q] * g[0][u];
+                    if (NRHS == 2) a1 += mv[r][q] * g[1][u];
+                }
+            }
+            a0 = wsum(a0);
+            if (NRHS == 2) a1 = wsum(a1);
+            const int t = t0 + r * nw;
+            if (lane == 0 && t < k) {
+                sp.w.hh[t] = a0;
+                if (NRHS == 2) sp.w.hh[SP_KMAX + t] = a1;
+            }
         }
     }
 }
@@ -1984,13 +2006,32 @@ __global__ void __launch_bounds__(1024) k_sp_btran(SpDev sp, DState *st, const d
 // with a barrier
 __device__ __forceinline__ void rows_dot(const double *M, const double *c, int k, double *out)
 {
-    const int lane = threadIdx.x & 63;
-    for (int t = threadIdx.x >> 6; t < k; t += blockDim.x >> 6) {
-        const double *mr = M + (size_t)t * SP_KMAX;
-        double a = 0.0;
-        for (int u = lane; u < k; u += 64) a += mr[u] * c[u];
-        a = wsum(a);
-        if (lane == 0) out[t] = a;
+    // a wave per row, four rows of the wave in flight at once (the row sums
+    // in the same order as one row at a time: lane u, u + 64, ... then wsum)
+    const int lane = threadIdx.x & 63, nw = blockDim.x >> 6;
+    for (int t0 = threadIdx.x >> 6; t0 < k; t0 += 4 * nw) {
+        double mv[4][SP_KMAX / 64];
+#pragma unroll
+        for (int r = 0; r < 4; r++) {
+            const int t = min(t0 + r * nw, k - 1);
+#pragma unroll
+            for (int q = 0; q < SP_KMAX / 64; q++) {
+                const int u = lane + 64 * q;
+                mv[r][q] = (u < k) ? M[(size_t)t * SP_KMAX + u] : 0.0;
+            }
+        }
+#pragma unroll
+        for (int r = 0; r < 4; r++) {
+            double a = 0.0;
+#pragma unroll
+            for (int q = 0; q < SP_KMAX / 64; q++) {
+                const int u = lane + 64 * q;
+                if (u < k) a += mv[r][q] * c[u];
+            }
+            a = wsum(a);
+            const int t = t0 + r * nw;
+            if (lane == 0 && t < k) out[t] = a;
+        }
     }
     __syncthreads();
 }
@@ -2013,6 +2054,7 @@ __global__ void __launch_bounds__(1024) k_sp_update(SpDev sp, DState *st)
         *sp.w.nlog = nl + 1;
         slot = -1;
         *sp.w.ycol = -1;
+        *sp.w.nupd = 0;
     }
     __syncthreads();
     for (int t = threadIdx.x; t < k; t += blockDim.x)
@@ -2062,9 +2104,11 @@ __global__ void __launch_bounds__(1024) k_sp_update(SpDev sp, DState *st)
             if (threadIdx.x == 0) st->refact_pending = 1;
             return;
         }
-        for (int e = threadIdx.x; e < k * k; e += blockDim.x) {
-            const int t = e / k, u = e % k;
-            Mi[(size_t)t * SP_KMAX + u] += ac[t] * ra[u] / s;
+        // the k x k block's rank-1 update inv(M) += a r / s: by k_sp_ycol's
+        // grid (one workgroup streamed the k^2 entries through one CU)
+        for (int t = threadIdx.x; t < k; t += blockDim.x) {
+            sp.w.upd[t] = ac[t];
+            sp.w.upd[SP_KMAX + t] = ra[t];
         }
         for (int t = threadIdx.x; t < k; t += blockDim.x) {
             Mi[(size_t)t * SP_KMAX + k] = -ac[t] / s;
@@ -2075,6 +2119,9 @@ __global__ void __launch_bounds__(1024) k_sp_update(SpDev sp, DState *st)
             sp.w.P[k] = p;
             *sp.w.k = k + 1;
             *sp.w.ycol = k;                              // k_sp_ycol writes the column
+            sp.w.upd[2 * SP_KMAX] = s;
+            sp.w.upd[2 * SP_KMAX + 1] = +1.0;
+            *sp.w.nupd = k;
         }
         return;
     }
@@ -2097,11 +2144,17 @@ __global__ void __launch_bounds__(1024) k_sp_update(SpDev sp, DState *st)
         return;
     }
     __syncthreads();
-    for (int e = threadIdx.x; e < k * k; e += blockDim.x) {
-        const int t = e / k, u = e % k;
-        Mi[(size_t)t * SP_KMAX + u] -= ac[t] * ra[u] / den;
+    // inv(M) -= a r / den on k_sp_ycol's grid
+    for (int t = threadIdx.x; t < k; t += blockDim.x) {
+        sp.w.upd[t] = ac[t];
+        sp.w.upd[SP_KMAX + t] = ra[t];
     }
-    if (threadIdx.x == 0) *sp.w.ycol = t0;
+    if (threadIdx.x == 0) {
+        *sp.w.ycol = t0;
+        sp.w.upd[2 * SP_KMAX] = den;
+        sp.w.upd[2 * SP_KMAX + 1] = -1.0;
+        *sp.w.nupd = k;
+    }
 }
 
 // the column of Y the update of this pivot bordered or replaced (grid; the
@@ -2112,6 +2165,21 @@ __global__ void __launch_bounds__(256) k_sp_ycol(SpDev sp, const DState *st)
     if (st->stop || st->p <= 0) return;
     const int c = *sp.w.ycol;
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    // k_sp_update's rank-1 update of inv(M)'s k x k block, spread over the
+    // grid (the same expression per entry: m + (a_t r_u) / d, or minus)
+    const int kk = *sp.w.nupd;
+    if (kk > 0) {
+        const double *a = sp.w.upd, *r = sp.w.upd + SP_KMAX;
+        const double dv = sp.w.upd[2 * SP_KMAX];
+        const bool plus = sp.w.upd[2 * SP_KMAX + 1] > 0.0;
+        double *Mi = sp.w.Minv;
+        for (int e = i; e < kk * kk; e += gridDim.x * blockDim.x) {
+            const int t = e / kk, u = e % kk;
+            double &x = Mi[(size_t)t * SP_KMAX + u];
+            if (plus) x += a[t] * r[u] / dv;
+            else x -= a[t] * r[u] / dv;
+        }
+    }
     if (c < 0 || i >= sp.m) return;
     sp.w.Y[(size_t)i * SP_KMAX + c] = -sp.w.zq[i] - (i == st->p - 1 ? 1.0 : 0.0);
 }
@@ -2190,6 +2258,7 @@ static SpDev sp_dev(SpFactor &F)
     d.w.Y = F.Y.p; d.w.P = F.P.p; d.w.Minv = F.Minv.p; d.w.k = F.hdr.p + 4; d.w.zq = F.zq.p;
     d.w.tpart = F.tpart.p; d.w.bt = F.bt.p; d.w.scr2 = F.scr2.p; d.w.hh = F.hh.p; d.w.ycol = F.hdr.p + 5; d.w.bz = F.bz.p;
     d.w.log = F.plog.p; d.w.nlog = F.hdr.p + 6;
+    d.w.upd = F.upd.p; d.w.nupd = F.hdr.p + 7;
     return d;
 }
 
@@ -2294,6 +2363,7 @@ static void sp_install(SpFactor &F, hipStream_t s, SpHost &H, double t0)
     }
     F.P.ensure(SP_KMAX);
     F.hh.ensure((size_t)2 * SP_KMAX);
+    F.upd.ensure((size_t)2 * SP_KMAX + 2);
     F.sacc.ensure((size_t)2 * SP_SEG_MAX);
     F.Minv.ensure((size_t)SP_KMAX * SP_KMAX);
     F.plog.ensure((size_t)2 * SP_KMAX);
