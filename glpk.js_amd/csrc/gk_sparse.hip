@@ -1936,12 +1936,26 @@ __global__ void __launch_bounds__(1024) k_sp_btran(SpDev sp, DState *st, const d
         const int q = threadIdx.x >> 8, t = threadIdx.x & 255;
         const int ub = q * ((k + 3) / 4), ue = min(k, ub + (k + 3) / 4);
         double a = 0.0, a1 = 0.0;
-        if (t < k && q < 4)
-            for (int u = ub; u < ue; u++) {
-                const double mi = sp.w.Minv[(size_t)u * SP_KMAX + t];    // inv(M)'
+        if (t < k && q < 4) {
+            // (eight entries of the column loaded before their products: the
+            // same order of accumulation as one by one)
+            int u = ub;
+            for (; u + 8 <= ue; u += 8) {
+                double mv[8];
+#pragma unroll
+                for (int r = 0; r < 8; r++) mv[r] = sp.w.Minv[(size_t)(u + r) * SP_KMAX + t];    // inv(M)'
+#pragma unroll
+                for (int r = 0; r < 8; r++) {
+                    a += mv[r] * tv[0][u + r];
+                    if (NRHS == 2) a1 += mv[r] * tv[1][u + r];
+                }
+            }
+            for (; u < ue; u++) {
+                const double mi = sp.w.Minv[(size_t)u * SP_KMAX + t];
                 a += mi * tv[0][u];
                 if (NRHS == 2) a1 += mi * tv[1][u];
             }
+        }
         if (t < k && q < 4) {
             svp[q][0][t] = a;
             svp[q][1][t] = a1;
