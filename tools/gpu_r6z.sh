@@ -8,3 +8,6 @@ bash tools/prof_sparse_window.sh r6z_new --it 1000 --basis $B 200 20 > $O/pn.log
 GK_LIB_PATH=$GRAFT_REPO_ROOT/glpk.js_amd/ab_head.so bash tools/prof_sparse_window.sh r6z_old --it 1000 --basis $B 200 20 > $O/po.log 2>&1
 timeout -k 10 200 python3 -u tools/sparse_big.py --sparse blocks 200 20 > $O/full20k.json 2> $O/full20k.err
 echo ok
+# (the m = 100k window both ways)
+timeout -k 10 120 python3 -u tools/sparse_window.py --it 1000 > $O/w100_new.json 2>/dev/null
+GK_LIB_PATH=$GRAFT_REPO_ROOT/glpk.js_amd/ab_head.so timeout -k 10 120 python3 -u tools/sparse_window.py --it 1000 > $O/w100_old.json 2>/dev/null
