@@ -1556,6 +1556,13 @@ struct MipSolver {
     // engine fallback (ios_solve_node with glp_simplex, glpios01.js:866)
     gk_bfd *fb = nullptr;
     unsigned long long fb_version = 0;
+    // engine mode: one context (stream) and factor per concurrent node LP
+    struct EngW {
+        gk_ctx *ctx = nullptr;
+        gk_bfd *fb = nullptr;
+        unsigned long long ver = 0;
+    };
+    std::vector<EngW> engw;
     // ios_round_bound (glpios01.js:730): objective integrality
     bool round_ok = false;
     double round_s = 0.0, round_d = 1.0;
@@ -1563,6 +1570,10 @@ struct MipSolver {
     ~MipSolver()
     {
         if (fb) gk_bfd_destroy(fb);
+        for (EngW &w : engw) {
+            if (w.fb) gk_bfd_destroy(w.fb);
+            if (w.ctx) gk_ctx_destroy(w.ctx);
+        }
     }
 
     size_t in_bytes(int nb) const { return Layout(N, n, nb).in_end; }
@@ -2098,6 +2109,13 @@ struct MipSolver {
     // GLP_EFAIL.
     int fallback(const NodeRec &nd, const double *bl, const double *bu, std::vector<double> &x,
                  std::vector<signed char> &so, double &z, bool &opt);
+    // its solve on a given context / factor (no search state written: the
+    // engine-mode workers run it concurrently, one node LP each); the
+    // degradations into *D when given
+    struct Degrad;
+    int solve_node(gk_ctx *c, gk_bfd *f, unsigned long long ver, const NodeRec &nd, const double *bl,
+                   const double *bu, std::vector<double> &x, std::vector<signed char> &so, double &z, bool &opt,
+                   long long &piv, Degrad *D);
     // engine mode: what the node kernel returns besides the solution, from
     // the engine's factor of the node's optimal basis — the fractional
     // columns, ios_eval_degrad's degradations of every one of them
@@ -2111,24 +2129,42 @@ struct MipSolver {
         int kjj = 0, knext = 0;
         bool ok = false;
     } dg;
-    void engine_degrad(gk_lp &L, const std::vector<double> &x, const std::vector<signed char> &so, const double *bl,
-                       const double *bu);
+    void engine_degrad(gk_bfd *f, Degrad &D, gk_lp &L, const std::vector<double> &x,
+                       const std::vector<signed char> &so, const double *bl, const double *bu) const;
 };
 
 int gk_spx_node(gk_ctx *ctx, gk_lp *lp, gk_bfd *bfd, const gk_smcp *parm);
 
+static unsigned long long engine_a_version()
+{
+    static std::atomic<unsigned long long> ver{0};
+    return (1ull << 62) | ++ver;                    // A uploaded once per factor and search
+}
+
 int MipSolver::fallback(const NodeRec &nd, const double *bl, const double *bu, std::vector<double> &x,
                         std::vector<signed char> &so, double &z, bool &opt)
 {
-    const gk_lp &R = mip->lp;
     opt = false;
     fallbacks++;
     if (!fb) {
         fb = gk_bfd_create(ctx);
         if (!fb) return 5;
-        static unsigned long long ver = 0;
-        fb_version = (1ull << 62) | ++ver;        // A uploaded once per search
+        fb_version = engine_a_version();
     }
+    materialize(nd.slot);
+    long long piv = 0;
+    const int ret = solve_node(ctx, fb, fb_version, nd, bl, bu, x, so, z, opt, piv, engine ? &dg : nullptr);
+    pivots += piv;
+    return ret;
+}
+
+int MipSolver::solve_node(gk_ctx *c, gk_bfd *f, unsigned long long ver, const NodeRec &nd, const double *bl,
+                          const double *bu, std::vector<double> &x, std::vector<signed char> &so, double &z,
+                          bool &opt, long long &piv, Degrad *D)
+{
+    const gk_lp &R = mip->lp;
+    opt = false;
+    piv = 0;
     std::vector<signed char> ctype(n + 1), rstat(m + 1), cstat(n + 1);
     std::vector<double> clo(n + 1, 0.0), cup(n + 1, 0.0);
     std::vector<int> head(m + 1), rbind(m + 1), cbind(n + 1);
@@ -2148,7 +2184,6 @@ int MipSolver::fallback(const NodeRec &nd, const double *bl, const double *bu, s
         if (sign > 0) sp.obj_ul = mo; else sp.obj_ll = mo;
     }
     sp.it_lim = 0x7fffffff; sp.tm_lim = 0x7fffffff; sp.out_frq = 500; sp.out_dly = 0;
-    materialize(nd.slot);
     for (int attempt = 0; attempt < 2; attempt++) {
         const signed char *st0 = pool.stat(nd.slot);
         for (int i = 0; i < m; i++) rstat[i + 1] = attempt == 0 ? st0[i] : (signed char)BS;
@@ -2172,11 +2207,11 @@ int MipSolver::fallback(const NodeRec &nd, const double *bl, const double *bu, s
         L.m = m; L.n = n; L.nnz = R.nnz; L.dir = R.dir; L.c0 = R.c0;
         L.row_type = R.row_type; L.row_lb = R.row_lb; L.row_ub = R.row_ub; L.rii = R.rii;
         L.col_type = ctype.data(); L.col_lb = clo.data(); L.col_ub = cup.data(); L.col_coef = R.col_coef; L.sjj = R.sjj;
-        L.A_ptr = R.A_ptr; L.A_ind = R.A_ind; L.A_val = R.A_val; L.a_version = fb_version;
+        L.A_ptr = R.A_ptr; L.A_ind = R.A_ind; L.A_val = R.A_val; L.a_version = ver;
         L.head = head.data(); L.row_stat = rstat.data(); L.col_stat = cstat.data();
         L.row_bind = rbind.data(); L.col_bind = cbind.data();
         L.row_prim = rprim.data(); L.row_dual = rdual.data(); L.col_prim = cprim.data(); L.col_dual = cdual.data();
-        const int ret = gk_spx_node(ctx, &L, fb, &sp);
+        const int ret = gk_spx_node(c, &L, f, &sp);
         if (ret == 6 || ret == 7) return 0;           // GLP_EOBJLL / EOBJUL: no better than the incumbent
         if (ret != 0) continue;
         if (L.dbs_stat != 2) break;                   // no dual feasible solution: the reference fails here
@@ -2186,18 +2221,17 @@ int MipSolver::fallback(const NodeRec &nd, const double *bl, const double *bu, s
         for (int i = 0; i < m; i++) { x[i] = rprim[i + 1]; so[i] = rstat[i + 1]; }
         for (int j = 0; j < n; j++) { x[m + j] = cprim[j + 1]; so[m + j] = cstat[j + 1]; }
         z = sign * (L.obj_val - c0);
-        pivots += L.it_cnt;
+        piv = L.it_cnt;
         opt = true;
-        if (engine) engine_degrad(L, x, so, bl, bu);
+        if (D) engine_degrad(f, *D, L, x, so, bl, bu);
         return 0;
     }
     return 5;                                         // GLP_EFAIL (ios_driver, glpios03.js:669-673)
 }
 
-void MipSolver::engine_degrad(gk_lp &L, const std::vector<double> &x, const std::vector<signed char> &so,
-                              const double *bl, const double *bu)
+void MipSolver::engine_degrad(gk_bfd *f, Degrad &D, gk_lp &L, const std::vector<double> &x,
+                              const std::vector<signed char> &so, const double *bl, const double *bu) const
 {
-    Degrad &D = dg;
     D.ok = false;
     D.kjj = 0;
     D.knext = 0;
@@ -2211,7 +2245,7 @@ void MipSolver::engine_degrad(gk_lp &L, const std::vector<double> &x, const std:
     for (int t = 0; t < nk; t++) kk[t] = m + D.cand[t] + 1;
     const int N1 = m + n;
     std::vector<double> alfa((size_t)nk * N1);
-    if (gk_bfd_eval_tab_rows(fb, &L, nk, kk.data(), alfa.data(), 0) != 0) return;
+    if (gk_bfd_eval_tab_rows(f, &L, nk, kk.data(), alfa.data(), 0) != 0) return;
     const double obj = (L.dir == 1) ? +1.0 : -1.0;   // GLP_MIN = 1
     auto stat_of = [&](int k) { return k <= m ? L.row_stat[k] : L.col_stat[k - m]; };
     auto dual_of = [&](int k) { return k <= m ? L.row_dual[k] : L.col_dual[k - m]; };
@@ -2799,28 +2833,87 @@ extern "C" int gk_ios_driver_sharded_inc(gk_ctx *ctx, gk_mip *mip, const gk_iocp
             // takes them for a fallback node: host integrality scan and
             // branching, no tableau, no probes)
             const auto tp0 = std::chrono::steady_clock::now();
-            std::vector<double> fx, fb(2 * (size_t)n);
-            std::vector<signed char> fso;
             const std::vector<double> zeros(2 * (size_t)n, 0.0);
-            for (const Entry &e : bf.ents) {
-                const NodeRec &nd = e.nd;
+            // the batch's node LPs solved concurrently, one context and
+            // factor per worker (each LP's path is its own: the same solution
+            // as one at a time), then the search's decisions in entry order.
+            // Each LP's objective limit is the incumbent at the batch's
+            // start: an LP a newer incumbent would have cut off is solved to
+            // its optimum and pruned by node_done's hopeful test instead,
+            // the same decision; a failed one is re-solved in order with the
+            // current incumbent, as one at a time would have solved it
+            struct Res {
+                std::vector<double> bnd, x;
+                std::vector<signed char> so;
+                double z = 0.0;
+                bool opt = false;
+                int ret = 0;
+                long long piv = 0;
+                MipSolver::Degrad dg;
+            };
+            const int ne = (int)bf.ents.size();
+            std::vector<Res> res(ne);
+            for (int i = 0; i < ne; i++) {
+                // (the node's bounds copied out: branching allocates pool
+                // slots, which may move the pool's arrays)
+                const int sl = bf.ents[i].nd.slot;
+                S.materialize(sl);
+                res[i].bnd.resize(2 * (size_t)n);
+                std::memcpy(res[i].bnd.data(), pool.lb(sl), n * sizeof(double));
+                std::memcpy(res[i].bnd.data() + n, pool.ub(sl), n * sizeof(double));
+            }
+            const int W = S.err ? 0 : std::min(ne, ENGINE_BATCH);
+            int dev = 0;
+            (void)hipGetDevice(&dev);                     // (the search's device: its contexts' and the workers')
+            while ((int)S.engw.size() < W) {
+                MipSolver::EngW w;
+                w.ctx = gk_ctx_create(dev);
+                w.fb = w.ctx ? gk_bfd_create(w.ctx) : nullptr;
+                w.ver = engine_a_version();
+                S.engw.push_back(w);
+            }
+            bool wok = true;
+            for (int w = 0; w < W; w++) wok = wok && S.engw[w].fb;
+            auto work = [&](int w) {
+                (void)hipSetDevice(dev);
+                const MipSolver::EngW &ew = S.engw[w];
+                for (int i = w; i < ne; i += W) {
+                    Res &r = res[i];
+                    try {
+                        r.ret = S.solve_node(ew.ctx, ew.fb, ew.ver, bf.ents[i].nd, r.bnd.data(), r.bnd.data() + n,
+                                             r.x, r.so, r.z, r.opt, r.piv, &r.dg);
+                    } catch (...) {
+                        r.ret = 5;                        // (re-solved in order below)
+                    }
+                }
+            };
+            if (W > 0 && wok) {
+                std::vector<std::thread> th;
+                for (int w = 1; w < W; w++) th.emplace_back(work, w);
+                work(0);
+                for (auto &t : th) t.join();
+            }
+            for (int i = 0; i < ne; i++) {
+                const NodeRec &nd = bf.ents[i].nd;
+                Res &r = res[i];
                 if (!S.err) {
                     S.lp_solves++;
-                    double z = 0.0;
-                    bool opt = false;
-                    // (the node's bounds copied out: branching allocates pool
-                    // slots, which may move the pool's arrays)
-                    std::memcpy(fb.data(), pool.lb(nd.slot), n * sizeof(double));
-                    std::memcpy(fb.data() + n, pool.ub(nd.slot), n * sizeof(double));
-                    const int ret = S.fallback(nd, fb.data(), fb.data() + n, fx, fso, z, opt);
-                    if (ret) S.err = ret;
-                    else if (opt) {
+                    if (!(W > 0 && wok) || r.ret) {
+                        // (no workers, or a failure: solved here, in order)
+                        r.ret = S.fallback(nd, r.bnd.data(), r.bnd.data() + n, r.x, r.so, r.z, r.opt);
+                        r.dg = S.dg;
+                    } else {
+                        S.fallbacks++;
+                        S.pivots += r.piv;
+                    }
+                    if (r.ret) S.err = r.ret;
+                    else if (r.opt) {
                         // the tableau's degradations and branch_drtom's choice
                         // (engine_degrad) as the node kernel returns them;
                         // pseudocost branching without probes
-                        const MipSolver::Degrad &D = S.dg;
+                        const MipSolver::Degrad &D = r.dg;
                         const bool tab = D.ok && parm->br_tech != 5;
-                        S.node_done(nd, z, fx.data(), fso.data(), fb.data(), fb.data() + n,
+                        S.node_done(nd, r.z, r.x.data(), r.so.data(), r.bnd.data(), r.bnd.data() + n,
                                     tab ? D.dz.data() : zeros.data(), tab ? D.kjj : 0, tab ? D.knext : 0, tab,
                                     D.ok ? D.cand.data() : nullptr, D.ok ? (int)D.cand.size() : -1, D.ii);
                     }
