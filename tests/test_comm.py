@@ -155,6 +155,38 @@ def test_gpu_sharded_bnb_library_comm(name, ramp):
     assert xs[0] == xs[1], "ranks disagree on the incumbent"
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("name,env", [("sparsebig2", {}), ("gap", {"GK_BNB_ENGINE_BYTES": "0"})],
+                         ids=["sparsebig2", "gap-engine-forced"])
+def test_gpu_sharded_bnb_engine_mode(monkeypatch, name, env):
+    """The sharded search with every node LP on the engine (engine mode,
+    DESIGN §7: each rank's batch solved concurrently on its own worker
+    contexts): both ranks reach the reference's objective and agree on the
+    incumbent."""
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    d = load_golden(os.path.join(os.path.dirname(__file__), "golden", f"mip_{name}.json"))
+    ref = d["mip"]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = free_port()
+    ps = [ctx.Process(target=_mip_worker, args=(r, 2, port, name, 0, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    res = sorted([q.get(timeout=240) for _ in range(2)], key=lambda t: t[0])
+    for p in ps:
+        p.join(timeout=60)
+    xs = []
+    for rank, backend, ret, stat, obj, x, stats in res:
+        assert backend == gk.GK_COMM_TCP, ret
+        assert ret == ref["ret"] and stat == ref["mip_stat"], (rank, ret, stat)
+        assert abs(obj - ref["mip_obj"]) <= 1e-9 * max(1.0, abs(ref["mip_obj"])), (rank, obj)
+        assert stats["node_fallbacks"] == stats["lp_solves"], stats      # every node LP on the engine
+        xs.append(x)
+        print(name, "rank", rank, stats)
+    assert xs[0] == xs[1], "ranks disagree on the incumbent"
+
+
 def _two_mips_worker(rank, size, port, names, q):
     try:
         import sys
