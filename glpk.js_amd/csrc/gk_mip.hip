@@ -1125,14 +1125,21 @@ constexpr size_t NODE_LDS_MAX = 64 * 1024;
 // engine (GK_BNB_ENGINE_BYTES, default 1 MiB: m (2m + n) doubles streamed by
 // one CU per pivot against the revised simplex on a factor; sparsebig1, 1.8
 // MB per node: 0.58 s and 4,818 node LPs in the node kernel, 0.53 s and 410
-// in engine mode — reference 297); engine mode solves ENGINE_BATCH nodes per
+// in engine mode — reference 297); engine mode solves engine_batch() nodes per
 // search step
 static size_t engine_node_bytes()
 {
     const char *e = std::getenv("GK_BNB_ENGINE_BYTES");        // (read per search: tests switch it)
     return e ? (size_t)std::max(0LL, std::atoll(e)) : ((size_t)1 << 20);
 }
-constexpr int ENGINE_BATCH = 8;
+static int engine_batch()                             // GK_BNB_ENGINE_BATCH (experiments), default 8
+{
+    static const int b = [] {
+        const char *e = std::getenv("GK_BNB_ENGINE_BATCH");
+        return e ? std::max(1, std::min(std::atoi(e), 64)) : 8;
+    }();
+    return b;
+}
 
 void launch_node_lp(hipStream_t s, const NodeProb &P, const NodeIO &io, int nb)
 {
@@ -2602,9 +2609,9 @@ extern "C" int gk_ios_driver_sharded_inc(gk_ctx *ctx, gk_mip *mip, const gk_iocp
     MipCache &Cc = *S.cache;
     Cc.dA.ensure(S.A.size()); Cc.dc.ensure(S.N); Cc.dint.ensure(n); Cc.drb.ensure(2 * (size_t)m);
     // (engine mode: the batch is the order the node LPs are solved in, one
-    // after another; ENGINE_BATCH of them keeps the search order of the
+    // after another; engine_batch() of them keeps the search order of the
     // batched search's narrow batches)
-    const int BMAX = eng ? ENGINE_BATCH
+    const int BMAX = eng ? engine_batch()
                          : (lds <= NODE_LDS_MAX ? 1024
                                                 : (int)std::max<size_t>(1, std::min<size_t>(1024, SCRATCH_MAX / lds)));
     S.stride = (lds + 255) / 256 * 32;                    // doubles, 256-byte aligned slices
@@ -2862,7 +2869,7 @@ extern "C" int gk_ios_driver_sharded_inc(gk_ctx *ctx, gk_mip *mip, const gk_iocp
                 std::memcpy(res[i].bnd.data(), pool.lb(sl), n * sizeof(double));
                 std::memcpy(res[i].bnd.data() + n, pool.ub(sl), n * sizeof(double));
             }
-            const int W = S.err ? 0 : std::min(ne, ENGINE_BATCH);
+            const int W = S.err ? 0 : std::min(ne, engine_batch());
             int dev = 0;
             (void)hipGetDevice(&dev);                     // (the search's device: its contexts' and the workers')
             while ((int)S.engw.size() < W) {
