@@ -2153,6 +2153,15 @@ int MipSolver::fallback(const NodeRec &nd, const double *bl, const double *bu, s
 {
     opt = false;
     fallbacks++;
+    // GK_BNB_FRESH_FB=1 (diagnostics): a new factor handle for every node LP
+    static const bool fresh = [] {
+        const char *e = std::getenv("GK_BNB_FRESH_FB");
+        return e && std::atoi(e) != 0;
+    }();
+    if (fresh && fb) {
+        gk_bfd_destroy(fb);
+        fb = nullptr;
+    }
     if (!fb) {
         fb = gk_bfd_create(ctx);
         if (!fb) return 5;
@@ -2878,7 +2887,11 @@ extern "C" int gk_ios_driver_sharded_inc(gk_ctx *ctx, gk_mip *mip, const gk_iocp
                 const char *e = std::getenv("GK_BNB_ENGINE_CONCURRENT");
                 return e && std::atoi(e) != 0;
             }();
-            const int W = (S.err || !conc) ? 0 : std::min(ne, engine_batch());
+            static const int wmax = [] {                  // GK_BNB_ENGINE_WORKERS (diagnostics): at most this many
+                const char *e = std::getenv("GK_BNB_ENGINE_WORKERS");
+                return e ? std::max(1, std::atoi(e)) : 64;
+            }();
+            const int W = (S.err || !conc) ? 0 : std::min(std::min(ne, engine_batch()), wmax);
             int dev = 0;
             (void)hipGetDevice(&dev);                     // (the search's device: its contexts' and the workers')
             while ((int)S.engw.size() < W) {
