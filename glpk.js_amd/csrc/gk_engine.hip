@@ -2377,7 +2377,11 @@ int Spx::batch(int K, int rigorous)
         // exchange goes through the host and keeps the batch eager
         const bool shard_eager = d.shard && d.shard->vsize <= 1 && gk_comm_backend(d.shard->comm) != GK_COMM_RCCL;
         if (d.shard) d.shard->exchanges += K;    // (every launched pivot exchanges, a stopped one too)
-        if (!rigorous && K >= 4 && !evp && !f->sparse && !shard_eager) {
+        static const bool no_graph = [] {      // GK_NO_GRAPH=1 (diagnostics): every batch eager
+            const char *e = std::getenv("GK_NO_GRAPH");
+            return e && std::atoi(e) != 0;
+        }();
+        if (!rigorous && K >= 4 && !evp && !f->sparse && !shard_eager && !no_graph) {
             run_graph(d, pl, K);
             armed = epi_arm(K);
         } else {
